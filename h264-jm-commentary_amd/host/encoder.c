@@ -1,0 +1,141 @@
+/*
+ * encoder.c — sequence / picture driver, restating JM 8.6 lencod.c › main frame loop and
+ * image.c › encode_one_frame [J]: read (or synthesise) the picture, choose I/P, run the
+ * macroblock hot path through the backend (encode_one_macroblock for every MB), write the
+ * slice (CAVLC), deblock the reconstruction, make it the reference (UnifiedOneForthPix runs in
+ * the backend), write the recon, print JM's per-frame report line.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "jmhost.h"
+
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+int jm_lambda_rdo_off(int qp) {
+    static const int QP2QUANT[40] = {1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 4,
+                                     5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 23,
+                                     25, 29, 32, 36, 40, 45, 51, 57, 64, 72, 81, 91};
+    int i = qp - 12;
+    return QP2QUANT[i < 0 ? 0 : i];
+}
+
+static double psnr(const uint8_t *a, int sa, const uint8_t *b, int sb, int w, int h) {
+    double se = 0;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int d = a[y * sa + x] - b[y * sb + x];
+            se += d * d;
+        }
+    if (se == 0) return 99.0;
+    return 10.0 * log10(255.0 * 255.0 * w * h / se);
+}
+
+int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *log) {
+    memset(st, 0, sizeof(*st));
+    jmh_config cfg;
+    jm_fill_config(inp, &cfg);
+    int W = cfg.width, H = cfg.height;
+    jm_seq s;
+    memset(&s, 0, sizeof(s));
+    s.width = W; s.height = H; s.disp_w = inp->width; s.disp_h = inp->height;
+    s.mbw = W / 16; s.mbh = H / 16;
+    s.profile_idc = inp->profile_idc; s.level_idc = inp->level_idc;
+    s.num_ref_frames = inp->num_ref_frames;
+    s.log2_max_frame_num = 8; s.log2_max_poc_lsb = 8;
+    s.chroma_qp_offset = inp->chroma_qp_offset;
+    s.lf_params_flag = inp->lf_params_flag; s.lf_disable = inp->lf_disable;
+    s.lf_alpha = inp->lf_alpha; s.lf_beta = inp->lf_beta;
+    s.constrained_intra = inp->constrained_intra;
+
+    FILE *fin = NULL, *fout = NULL, *frec = NULL;
+    uint64_t seed = 0;
+    int synthetic = !strncmp(inp->infile, "synthetic:", 10);
+    if (synthetic) seed = strtoull(inp->infile + 10, NULL, 10);
+    else if (!(fin = fopen(inp->infile, "rb"))) { fprintf(stderr, "Input file %s does not exist\n", inp->infile); return JMH_E_INVALID_ARG; }
+    if (!(fout = fopen(inp->outfile, "wb"))) { fprintf(stderr, "Cannot open output file %s\n", inp->outfile); if (fin) fclose(fin); return JMH_E_INVALID_ARG; }
+    if (inp->reconfile[0] && !(frec = fopen(inp->reconfile, "wb"))) { fprintf(stderr, "Cannot open recon file %s\n", inp->reconfile); fclose(fout); if (fin) fclose(fin); return JMH_E_INVALID_ARG; }
+
+    jm_pic cur, rec;
+    if (jm_pic_alloc(&cur, W, H) || jm_pic_alloc(&rec, W, H)) return JMH_E_OOM;
+    int nmb = s.mbw * s.mbh;
+    const jmh_mb_result **res = (const jmh_mb_result **)malloc(sizeof(*res) * nmb);
+    jm_bits out, rbsp;
+    jm_bits_init(&out); jm_bits_init(&rbsp);
+    jm_write_sps(&rbsp, &s); jm_write_nal(&out, 3, 7, &rbsp); jm_bits_free(&rbsp);
+    jm_write_pps(&rbsp, &s); jm_write_nal(&out, 3, 8, &rbsp); jm_bits_free(&rbsp);
+    long header_bits = out.len * 8;
+    fwrite(out.buf, 1, out.len, fout);
+    st->bits += header_bits;
+    out.len = 0;
+    if (log) {
+        fprintf(log, "------------------------------- MI355X jm-hot-path lencod (%s) -------------------------------\n", be->name);
+        fprintf(log, " Frame  Bit/pic  QP   SnrY    SnrU    SnrV    Time(ms) MET(ms) Frm/Fld  I D\n");
+    }
+    double t_start = now_ms();
+    int st_ret = 0, frame_num = 0;
+    for (int f = 0; f < inp->frames; f++) {
+        int idx = inp->start_frame + f;
+        if (synthetic) jm_synth_frame(&cur, inp->width, inp->height, seed, idx);
+        else if (jm_read_yuv_frame(fin, &cur, inp->width, inp->height, idx)) { fprintf(stderr, "ReadOneFrame: cannot read frame %d\n", idx); st_ret = JMH_E_INVALID_ARG; break; }
+        int is_i = f == 0 || (inp->intra_period && f % inp->intra_period == 0);
+        jmh_frame_params fp;
+        memset(&fp, 0, sizeof(fp));
+        fp.slice_type = is_i ? JMH_I_SLICE : JMH_P_SLICE;
+        fp.qp = is_i ? inp->qp_i : inp->qp_p;
+        fp.lambda_mode = fp.lambda_motion = jm_lambda_rdo_off(fp.qp);
+        fp.chroma_qp_offset = inp->chroma_qp_offset;
+        double t0 = now_ms();
+        int r = be->encode_frame(be->ctx, &cur, &fp);
+        double t1 = now_ms();
+        if (r) { fprintf(stderr, "hot path backend '%s' failed: status %d\n", be->name, r); st_ret = r; break; }
+        st->me_tq_ms += t1 - t0;
+        for (int a = 0; a < nmb; a++) res[a] = be->mb_result(be->ctx, a);
+        jm_slice sl;
+        sl.idr = f == 0; sl.slice_type = fp.slice_type; sl.frame_num = frame_num;
+        sl.poc_lsb = 2 * f; sl.idr_pic_id = 0; sl.qp = fp.qp;
+        jm_bits_init(&rbsp);
+        jm_write_slice(&rbsp, &s, &sl, res);
+        jm_write_nal(&out, sl.idr ? 3 : 2, sl.idr ? 5 : 1, &rbsp);
+        jm_bits_free(&rbsp);
+        double t2 = now_ms();
+        st->entropy_ms += t2 - t1;
+        long pic_bits = out.len * 8;
+        fwrite(out.buf, 1, out.len, fout);
+        out.len = 0;
+        be->read_recon(be->ctx, &rec);
+        jm_deblock_picture(&rec, &s, res, fp.qp);
+        double t3 = now_ms();
+        st->deblock_ms += t3 - t2;
+        if ((r = be->set_reference(be->ctx, &rec))) { fprintf(stderr, "set_reference failed: %d\n", r); st_ret = r; break; }
+        if (frec) jm_write_yuv_frame(frec, &rec, inp->width, inp->height);
+        double py = psnr(cur.y, W, rec.y, W, inp->width, inp->height);
+        double pu = psnr(cur.u, W / 2, rec.u, W / 2, inp->width / 2, inp->height / 2);
+        double pv = psnr(cur.v, W / 2, rec.v, W / 2, inp->width / 2, inp->height / 2);
+        st->psnr_y += py; st->psnr_u += pu; st->psnr_v += pv;
+        st->bits += pic_bits;
+        st->frames++;
+        frame_num++;
+        if (log)
+            fprintf(log, "%4d(%s) %8ld   %2d %7.4f %7.4f %7.4f %9.1f %7.1f    FRM\n", f, is_i ? "IDR" : " P ",
+                    pic_bits, fp.qp, py, pu, pv, t3 - t0, t1 - t0);
+    }
+    st->total_ms = now_ms() - t_start;
+    if (st->frames) { st->psnr_y /= st->frames; st->psnr_u /= st->frames; st->psnr_v /= st->frames; }
+    if (log && st->frames)
+        fprintf(log, " Total encoding time for the seq.  : %.3f sec\n Total ME+TQ time (backend)        : %.3f sec\n"
+                     " SNR Y(dB) %.4f U %.4f V %.4f   bits %ld\n",
+                st->total_ms / 1e3, st->me_tq_ms / 1e3, st->psnr_y, st->psnr_u, st->psnr_v, st->bits);
+    jm_bits_free(&out);
+    free(res);
+    jm_pic_free(&cur); jm_pic_free(&rec);
+    if (fin) fclose(fin);
+    fclose(fout);
+    if (frec) fclose(frec);
+    return st_ret;
+}

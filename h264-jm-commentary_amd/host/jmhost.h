@@ -1,0 +1,147 @@
+/*
+ * jmhost.h — lencod-compatible host plumbing around the jmh_* hot path.
+ *
+ * Mirrors the JM 8.6 lencod structure [J] (no file:line exists: /root/reference holds only
+ * README.md:1-4): configfile.c (encoder.cfg, Map[], -d/-f/-p), lencod.c main + frame loop,
+ * image.c encode_one_frame, slice.c/header.c/parset.c/nalu.c (slice + parameter sets + NAL),
+ * vlc.c + macroblock.c writers (CAVLC), loopfilter.c (deblocking).  The macroblock hot path is
+ * a pluggable backend: the product binary binds it to libjmhip.so (MI355X); the test-only CPU
+ * reference binary (oracle/lencod_cpu) binds it to the oracle.
+ */
+#ifndef JMHOST_H
+#define JMHOST_H
+
+#include <stdint.h>
+#include <stdio.h>
+#include "../../include/jmhip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- encoder.cfg (JM 8.6 keys, with JM>=10 spellings accepted as aliases) -------------- */
+typedef struct jm_input {
+    char infile[512];          /* InputFile ("synthetic:<seed>" = built-in generator)         */
+    char outfile[512];         /* OutputFile (.264 Annex B)                                   */
+    char reconfile[512];       /* ReconFile ("" = none)                                       */
+    int  frames;               /* FramesToBeEncoded                                           */
+    int  start_frame;          /* StartFrame                                                  */
+    int  width, height;        /* SourceWidth / SourceHeight (displayed size)                 */
+    int  intra_period;         /* IntraPeriod (0: only the first picture is intra)           */
+    int  qp_i, qp_p;           /* QPFirstFrame (QPISlice) / QPRemainingFrame (QPPSlice)       */
+    int  search_range;         /* SearchRange                                                 */
+    int  search_mode;          /* SearchMode: -1 full, 0 fast full (UseFME=0 == 0)             */
+    int  use_hadamard;         /* UseHadamard                                                 */
+    int  num_ref_frames;       /* NumberReferenceFrames                                       */
+    int  restrict_search_range;/* RestrictSearchRange                                         */
+    int  inter_search[8];      /* InterSearch16x16 .. InterSearch4x4 ([1..7])                 */
+    int  rdopt;                /* RDOptimization (must be 0)                                  */
+    int  profile_idc;          /* ProfileIDC (66)                                             */
+    int  level_idc;            /* LevelIDC                                                    */
+    int  symbol_mode;          /* SymbolMode (0 = CAVLC)                                       */
+    int  lf_params_flag;       /* LoopFilterParametersFlag                                    */
+    int  lf_disable;           /* LoopFilterDisable                                           */
+    int  lf_alpha, lf_beta;    /* LoopFilterAlphaC0Offset / LoopFilterBetaOffset              */
+    int  chroma_qp_offset;     /* ChromaQPOffset                                              */
+    int  constrained_intra;    /* UseConstrainedIntraPred                                     */
+    int  frame_rate;           /* FrameRate (report only)                                     */
+    int  hip_device;           /* (this build) HIP device index                               */
+    int  verbose;
+} jm_input;
+
+void jm_input_defaults(jm_input *inp);
+/* JM Configure(): argv "-d file", "-f file", "-p Key=Value", "-h"; returns 0 or -1 (message
+ * printed).  Unknown keys are an error (as in JM ParameterNameToMapIndex). */
+int  jm_configure(jm_input *inp, int argc, char **argv, char *err, int errlen);
+int  jm_parse_content(jm_input *inp, const char *buf, char *err, int errlen);
+int  jm_set_param(jm_input *inp, const char *key, const char *val, char *err, int errlen);
+int  jm_patch_input(jm_input *inp, char *err, int errlen);   /* PatchInp() */
+
+/* ---- pictures ---------------------------------------------------------------------------- */
+typedef struct jm_pic {
+    int w, h;                  /* coded (multiple of 16) */
+    uint8_t *y, *u, *v;        /* contiguous planes, stride = w / w/2                            */
+} jm_pic;
+int  jm_pic_alloc(jm_pic *p, int w, int h);
+void jm_pic_free(jm_pic *p);
+
+/* deterministic synthetic 4:2:0 source: integer-only texture, global
+ * quarter-pel motion, moving rectangles, per-frame noise.  Writes the displayed w x h into the
+ * coded picture and pads to the coded size by edge replication (JM PaddAutoCropBorders). */
+void jm_synth_frame(jm_pic *p, int disp_w, int disp_h, uint64_t seed, int frame);
+/* read frame `index` of a planar I420 file (displayed size) into the coded picture */
+int  jm_read_yuv_frame(FILE *f, jm_pic *p, int disp_w, int disp_h, int index);
+int  jm_write_yuv_frame(FILE *f, const jm_pic *p, int disp_w, int disp_h);
+void jm_pad_picture(jm_pic *p, int disp_w, int disp_h);
+
+/* ---- bitstream writer ------------------------------------------------------------------ */
+typedef struct jm_bits {
+    uint8_t *buf;
+    long cap, len;             /* bytes */
+    uint64_t acc;
+    int nacc;
+} jm_bits;
+void jm_bits_init(jm_bits *b);
+void jm_bits_free(jm_bits *b);
+void jm_put(jm_bits *b, uint32_t val, int n);
+void jm_put_ue(jm_bits *b, uint32_t v);
+void jm_put_se(jm_bits *b, int32_t v);
+void jm_trailing_bits(jm_bits *b);
+void jm_bits_align_flush(jm_bits *b);
+
+typedef struct jm_seq {
+    int width, height;         /* coded */
+    int disp_w, disp_h;
+    int mbw, mbh;
+    int profile_idc, level_idc;
+    int num_ref_frames;
+    int log2_max_frame_num, log2_max_poc_lsb;
+    int chroma_qp_offset;
+    int lf_params_flag, lf_disable, lf_alpha, lf_beta;
+    int constrained_intra;
+} jm_seq;
+
+/* NAL unit (Annex B start code + emulation prevention) appended to out */
+void jm_write_nal(jm_bits *out, int nal_ref_idc, int nal_type, const jm_bits *rbsp);
+void jm_write_sps(jm_bits *rbsp, const jm_seq *s);
+void jm_write_pps(jm_bits *rbsp, const jm_seq *s);
+
+typedef struct jm_slice {
+    int idr, slice_type, frame_num, poc_lsb, idr_pic_id, qp;
+} jm_slice;
+/* slice header + CAVLC slice data for a whole picture (one slice); results in raster order */
+int  jm_write_slice(jm_bits *rbsp, const jm_seq *s, const jm_slice *sl,
+                    const jmh_mb_result *const *res);
+
+/* ---- deblocking (H.264 8.7), in place on the reconstructed picture ---------------------- */
+void jm_deblock_picture(jm_pic *p, const jm_seq *s, const jmh_mb_result *const *res, int qp);
+
+/* ---- hot-path backend ------------------------------------------------------------------ */
+typedef struct jm_backend {
+    const char *name;
+    void *ctx;
+    int (*set_reference)(void *ctx, const jm_pic *ref);
+    int (*encode_frame)(void *ctx, const jm_pic *cur, const jmh_frame_params *fp); /* sync */
+    const jmh_mb_result *(*mb_result)(void *ctx, int mb_addr);
+    int (*read_recon)(void *ctx, jm_pic *rec);
+    void (*destroy)(void *ctx);
+} jm_backend;
+
+typedef struct jm_stats {
+    int frames;
+    double me_tq_ms;           /* backend encode_frame wall time (ME + TQ + recon)            */
+    double total_ms;
+    double entropy_ms, deblock_ms;
+    long bits;
+    double psnr_y, psnr_u, psnr_v;   /* averages                                              */
+} jm_stats;
+
+void jm_fill_config(const jm_input *inp, jmh_config *cfg);
+int  jm_lambda_rdo_off(int qp);    /* QP2QUANT[max(0,qp-12)] */
+/* encode the whole sequence: returns 0 or a negative status */
+int  jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *log);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,41 @@
+/*
+ * lencod.c — product encoder binary: JM 8.6 lencod.c › main [J] with the macroblock hot path
+ * bound to the MI355X C ABI (libjmhip.so).  There is no CPU fallback: if no HIP device is
+ * usable the run fails with the jmh_* status, as JM's error() would.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include "jmhost.h"
+
+static int gpu_set_ref(void *ctx, const jm_pic *p) {
+    return jmh_set_reference((jmh_ctx *)ctx, 0, 0, p->y, p->u, p->v, p->w, p->w / 2);
+}
+static int gpu_encode(void *ctx, const jm_pic *cur, const jmh_frame_params *fp) {
+    int r = jmh_frame_submit((jmh_ctx *)ctx, cur->y, cur->u, cur->v, cur->w, cur->w / 2, fp);
+    return r ? r : jmh_frame_wait((jmh_ctx *)ctx);
+}
+static const jmh_mb_result *gpu_res(void *ctx, int a) { return jmh_get_mb_result((const jmh_ctx *)ctx, a); }
+static int gpu_recon(void *ctx, jm_pic *p) {
+    return jmh_read_recon((jmh_ctx *)ctx, p->y, p->u, p->v, p->w, p->w / 2);
+}
+static void gpu_destroy(void *ctx) { jmh_destroy((jmh_ctx *)ctx); }
+
+int main(int argc, char **argv) {
+    jm_input inp;
+    char err[1024];
+    jm_input_defaults(&inp);
+    if (jm_configure(&inp, argc, argv, err, sizeof(err))) { fprintf(stderr, "%s\n", err); return 1; }
+    jmh_config cfg;
+    jm_fill_config(&inp, &cfg);
+    jmh_ctx *ctx = NULL;
+    int r = jmh_create(&cfg, inp.hip_device, &ctx);
+    if (r) { fprintf(stderr, "jmh_create failed: %s\n", jmh_strerror(r)); return 2; }
+    jm_backend be = {"mi355x-hip", ctx, gpu_set_ref, gpu_encode, gpu_res, gpu_recon, gpu_destroy};
+    jm_stats st;
+    r = jm_encode_sequence(&inp, &be, &st, stdout);
+    double mp = (double)inp.width * inp.height * st.frames / 1e6;
+    if (!r && st.me_tq_ms > 0)
+        printf(" ME+TQ throughput (host-observed, incl. PCIe): %.2f MP/s\n", mp / (st.me_tq_ms / 1e3));
+    be.destroy(ctx);
+    return r ? 3 : 0;
+}

@@ -1,0 +1,176 @@
+/*
+ * jmhip.h — C ABI of the MI355X-native JM (lencod) hot path:
+ *           motion estimation + integer transform / quantisation / reconstruction.
+ *
+ * This is the drop-in boundary.  JM has no plugin/FFI API; its seams are the
+ * C functions of lencod.  Each entry point below replaces one of them:
+ *
+ *   JM 8.6 lencod seam [J]                                  replaced by
+ *   ----------------------------------------------------    -----------------------------------
+ *   image.c  › UnifiedOneForthPix(enc_frame_picture)        jmh_set_reference()
+ *   image.c  › code_a_picture → encode_one_slice →
+ *              per MB encode_one_macroblock()  (rdopt.c)    jmh_frame_submit() + jmh_frame_wait()
+ *              (+ mv-search.c › PartitionMotionSearch /         then, per MB, jmh_get_mb_result()
+ *               BlockMotionSearch / SetupFastFullPelSearch /
+ *               FastFullPelBlockMotionSearch / SubPelBlock-
+ *               MotionSearch, block.c › dct_luma / dct_chroma /
+ *               dct_luma_16x16, macroblock.c › LumaResidual-
+ *               Coding / ChromaResidualCoding)
+ *   enc_picture->imgY / imgUV (unfiltered reconstruction)   jmh_read_recon()
+ *   mv-search.c › SetupFastFullPelSearch (BlockSAD table)    jmh_ffs_sad_table()   (unit seam)
+ *   block.c › dct_luma (4x4 TQ + recon)                     jmh_tq4x4_batch()     (unit seam)
+ *
+ * Reference citations: the mounted reference (/root/reference) holds only README.md:1-4 (an
+ * annotated-JM commentary with no source), so no file:line into JM source exists; the JM
+ * function names above are the JM 8.6 names (tag [J]).  docs/JM_SEMANTICS.md
+ * pins every non-normative choice.
+ *
+ * Conventions: plain C types only; 0 = OK, negative JMH_E_* on error; nothing throws or aborts
+ * across this boundary.  One context = one HIP device + one HIP stream; a context is not
+ * thread-safe (JM is single threaded).  Multi-GPU = one process (and one context) per GPU.
+ */
+#ifndef JMHIP_H
+#define JMHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JMH_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define JMH_OK                 0
+#define JMH_E_INVALID_ARG     (-1)
+#define JMH_E_HIP             (-2)
+#define JMH_E_OOM             (-3)
+#define JMH_E_UNSUPPORTED_CFG (-4)
+#define JMH_E_STATE           (-5)
+#define JMH_E_NO_DEVICE       (-6)
+
+/* ---- slice types (H.264 slice_type % 5) ------------------------------------------------- */
+#define JMH_P_SLICE 0
+#define JMH_I_SLICE 2
+
+/* ---- macroblock types: JM 8.6 defines.h numbering [J] ------------------------------------ */
+#define JMH_PSKIP  0   /* P_Skip (P slice, 16x16, ref 0, skip MV, cbp 0)  */
+#define JMH_P16x16 1
+#define JMH_P16x8  2
+#define JMH_P8x16  3
+#define JMH_SMB8x8 4   /* sub-macroblock types 4..7 = 8x8, 8x4, 4x8, 4x4 (b8mode[] only) */
+#define JMH_SMB8x4 5
+#define JMH_SMB4x8 6
+#define JMH_SMB4x4 7
+#define JMH_P8x8   8
+#define JMH_I4MB   9
+#define JMH_I16MB  10
+#define JMH_IBLOCK 11  /* b8mode[] of an I4MB */
+
+/* ---- encoder configuration (encoder.cfg subset that the hot path reads) ----------------- */
+typedef struct jmh_config {
+    int32_t width;                  /* coded luma width  (multiple of 16)                        */
+    int32_t height;                 /* coded luma height (multiple of 16)                        */
+    int32_t search_range;           /* SearchRange (full-pel), 1..64                              */
+    int32_t search_mode;            /* 0 = fast full search (FFS, JM _FAST_FULL_ME_), -1 = full   */
+    int32_t use_hadamard;           /* UseHadamard                                                */
+    int32_t restrict_search_range;  /* RestrictSearchRange 0 / 1 / 2                              */
+    int32_t inter_search[8];        /* [1..7] = InterSearch16x16 .. InterSearch4x4 ([0] unused)   */
+    int32_t num_ref_frames;         /* NumberReferenceFrames (this build: 1)                      */
+    int32_t constrained_intra_pred; /* UseConstrainedIntraPred (this build: 0)                    */
+    int32_t num_frame_slots;        /* device-resident input frame slots (bench / pipelining)     */
+    int32_t reserved[7];
+} jmh_config;
+
+/* ---- per-picture parameters ------------------------------------------------------------- */
+typedef struct jmh_frame_params {
+    int32_t slice_type;        /* JMH_P_SLICE / JMH_I_SLICE                                      */
+    int32_t qp;                /* slice QP (0..51), constant over the picture (no rate control)  */
+    int32_t lambda_mode;       /* RDO off: QP2QUANT[max(0,qp-12)] (integer, computed on host)    */
+    int32_t lambda_motion;     /* RDO off: == lambda_mode                                        */
+    int32_t chroma_qp_offset;  /* chroma_qp_index_offset                                         */
+    int32_t reserved[7];
+} jmh_frame_params;
+
+/* ---- per-macroblock result (what encode_one_macroblock leaves behind) ------------------- */
+typedef struct jmh_mb_result {
+    int16_t mb_type;           /* JMH_PSKIP .. JMH_I16MB                                          */
+    int16_t cbp;               /* luma bits 0..3 (8x8 blocks), chroma (0/1/2) << 4                */
+    int32_t cbp_blk;           /* bit (4*by+bx): 4x4 luma block has non-zero levels (I16: AC)     */
+    int8_t  b8mode[4];         /* per 8x8: sub-mb type 4..7 for P8x8, mb_type otherwise           */
+    int8_t  ref_idx[4];        /* per 8x8, list 0; -1 for intra                                  */
+    int8_t  i16mode;           /* Intra16x16 prediction mode 0..3 (I16MB only)                   */
+    int8_t  c_ipred_mode;      /* intra chroma prediction mode 0..3 (intra MBs)                  */
+    int8_t  pad0[2];
+    int8_t  ipred[16];         /* Intra4x4 modes, 4x4 raster order (by*4+bx); 2 (DC) if not I4MB */
+    int16_t mv[16][2];         /* final list-0 MV per 4x4 block (raster), quarter-pel            */
+    int16_t luma[16][16];      /* per 4x4 block (raster): levels in frame zig-zag scan order;
+                                  I16MB: AC only, [k][0] = 0                                       */
+    int16_t luma_dc[16];       /* I16MB DC levels, zig-zag scan order                             */
+    int16_t chroma_dc[2][4];   /* [uv][k] 2x2 DC levels, raster c0..c3                            */
+    int16_t chroma_ac[2][4][16]; /* [uv][4x4 blk raster][scan]; [..][0] = 0                       */
+    int32_t min_cost;          /* diagnostic: cost of the chosen mode                             */
+    int32_t reserved;
+} jmh_mb_result;
+
+/* ---- kernel timing of the last submitted picture (HIP events on the context stream) ----- */
+typedef struct jmh_timing {
+    float interp_ms;           /* quarter-pel reference interpolation (last jmh_set_reference*) */
+    float mb_ms;               /* whole macroblock wavefront of the last picture               */
+    float total_ms;            /* first to last event of the last picture (incl. H2D if any)   */
+    int32_t mb_launches;       /* wavefront launches per picture                               */
+    int32_t reserved[4];
+} jmh_timing;
+
+typedef struct jmh_ctx jmh_ctx;
+
+/* ---- lifecycle -------------------------------------------------------------------------- */
+int  jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out);
+void jmh_destroy(jmh_ctx *ctx);
+const char *jmh_strerror(int status);
+int  jmh_abi_version(void);
+int  jmh_device_count(void);
+
+/* ---- reference picture (replaces UnifiedOneForthPix on the deblocked recon) --------------
+ * list must be 0 and ref_idx 0 in this build.  Planes are 8-bit, coded size, 4:2:0.        */
+int  jmh_set_reference(jmh_ctx *ctx, int list, int ref_idx,
+                       const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                       int stride_y, int stride_c);
+
+/* ---- one picture of encode_one_macroblock() calls ----------------------------------------
+ * The caller's planes must stay valid until jmh_frame_submit returns (copied to the device).
+ * Results and recon become host-visible after jmh_frame_wait; pointers returned by
+ * jmh_get_mb_result stay valid until the next submit.                                           */
+int  jmh_frame_submit(jmh_ctx *ctx, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                      int stride_y, int stride_c, const jmh_frame_params *fp);
+int  jmh_frame_wait(jmh_ctx *ctx);
+const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *ctx, int mb_addr);
+int  jmh_read_recon(jmh_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y, int stride_c);
+
+/* ---- device-resident variants (inputs already in HBM; used by bench.py) ------------------ */
+int  jmh_load_frame(jmh_ctx *ctx, int slot, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                    int stride_y, int stride_c);
+int  jmh_set_reference_slot(jmh_ctx *ctx, int slot);   /* slot = -1: the last picture's recon  */
+int  jmh_encode_slot(jmh_ctx *ctx, int slot, const jmh_frame_params *fp); /* async, no D2H    */
+int  jmh_sync(jmh_ctx *ctx);
+int  jmh_get_timing(jmh_ctx *ctx, jmh_timing *t);
+
+/* ---- unit seams (minimum slice; tests call these directly) ------------------------------
+ * jmh_ffs_sad_table: SetupFastFullPelSearch's 4x4 BlockSAD table for n_mb macroblocks of the
+ *   picture last given to jmh_frame_submit/jmh_load_frame(slot 0) against the current
+ *   reference.  mb_xy[2*i] = (mb_x, mb_y); centres[2*i] = absolute full-pel window centre
+ *   offset (cx, cy) relative to the MB.  out[i][blk(16)][(2R+1)^2] in window raster order
+ *   (dy outer, dx inner, dy,dx in [-R,R]).                                                  */
+int  jmh_ffs_sad_table(jmh_ctx *ctx, int n_mb, const int32_t *mb_xy, const int32_t *centres,
+                       uint16_t *out);
+/* jmh_tq4x4_batch: dct_luma on n independent 4x4 residual blocks.  resid[n][16] (raster),
+ *   pred[n][16] (raster), levels[n][16] (scan order), recon[n][16] (raster); nonzero[n].
+ *   intra selects the JM 8.6 intra rounding offset ((1<<q_bits)/3) vs inter (/6).          */
+int  jmh_tq4x4_batch(jmh_ctx *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp,
+                     int intra, int16_t *levels, uint8_t *recon, int32_t *coeff_cost,
+                     int32_t *nonzero);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JMHIP_H */

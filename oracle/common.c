@@ -1,0 +1,225 @@
+/*
+ * common.c — oracle tables and primitives (TEST INFRASTRUCTURE ONLY).
+ *
+ * Restates: JM 8.6 lencod/src/mv-search.c › Init_Motion_Search_Module (spiral tables, mvbits),
+ * SATD(); image.c › UnifiedOneForthPix (quarter-pel reference) per ITU-T H.264 8.4.2.2.1;
+ * block.c quant tables (quant_coef / dequant_coef, SNGL_SCAN); rdopt.c QP2QUANT;
+ * QP_SCALE_CR (H.264 Table 8-15).  [J] = JM 8.6 name, unverifiable here.
+ */
+#include <stdlib.h>
+#include "jmo_internal.h"
+
+/* quant_coef[qp%6] (H.264 encoder scaling; JM block.c [J]); classes a=(even,even) b=(odd,odd) */
+#define QROW(a, b, c) {a, c, a, c, c, b, c, b, a, c, a, c, c, b, c, b}
+const int jmo_quant_coef[6][16] = {
+    QROW(13107, 5243, 8066), QROW(11916, 4660, 7490), QROW(10082, 4194, 6554),
+    QROW(9362, 3647, 5825),  QROW(8192, 3355, 5243),  QROW(7282, 2893, 4559)};
+/* dequant_coef[qp%6] = normAdjust4x4 (H.264 8.5.9, flat scaling lists) */
+const int jmo_dequant_coef[6][16] = {
+    QROW(10, 16, 13), QROW(11, 18, 14), QROW(13, 20, 16),
+    QROW(14, 23, 18), QROW(16, 25, 20), QROW(18, 29, 23)};
+#undef QROW
+
+/* SNGL_SCAN (4x4 frame zig-zag, H.264 Table 8-13) as raster indices */
+const int jmo_scan4x4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+
+/* QP2QUANT [J]: lambda for RDO-off mode decision (rdopt.c) */
+const int jmo_qp2quant_tab[40] = {1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 4,
+                              5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 23,
+                              25, 29, 32, 36, 40, 45, 51, 57, 64, 72, 81, 91};
+
+/* QP_SCALE_CR: QPc as a function of qPI (H.264 Table 8-15) */
+const int jmo_qp_scale_cr_tab[52] = {
+    0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
+    18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 32, 33,
+    34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+
+/* COEFF_COST [J] (block.c): cost of a |level|==1 coefficient by preceding zero run */
+const int jmo_coeff_cost_tab[16] = {3, 2, 2, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+/* input->blc_size [J] (configfile.c): {width, height} for blocktype 0..7 */
+const int jmo_blc_size[8][2] = {{16, 16}, {16, 16}, {16, 8}, {8, 16},
+                                {8, 8},   {8, 4},   {4, 8},  {4, 4}};
+
+int jmo_qp2quant(int qp) { return jmo_qp2quant_tab[imax(0, qp - SHIFT_QP)]; }
+int jmo_qp_scale_cr(int qp) { return qp < 0 ? qp : jmo_qp_scale_cr_tab[iclip(0, 51, qp)]; }
+
+/* mvbits[v] [J] (Init_Motion_Search_Module): length of se(v) Exp-Golomb code, 9.1 */
+int jmo_mvbits(int v) {
+    if (v == 0) return 1;
+    unsigned a = (unsigned)iabs(v);
+    int lg = 31 - __builtin_clz(a);          /* floor(log2|v|) */
+    return 2 * lg + 3;
+}
+
+/* Init_Motion_Search_Module spiral [J]: entry 0 = (0,0); ring l: (i,-l),(i,l) for
+ * i in [-l+1,l-1], then (-l,i),(l,i) for i in [-l,l]. */
+void jmo_spiral(int range, int32_t *sx, int32_t *sy) {
+    int k = 1;
+    sx[0] = sy[0] = 0;
+    for (int l = 1; l <= range; l++) {
+        for (int i = -l + 1; i < l; i++) {
+            sx[k] = i; sy[k] = -l; k++;
+            sx[k] = i; sy[k] = l;  k++;
+        }
+        for (int i = -l; i <= l; i++) {
+            sx[k] = -l; sy[k] = i; k++;
+            sx[k] = l;  sy[k] = i; k++;
+        }
+    }
+}
+
+void jmo_init_spiral(jmo_ctx *c) {
+    int n = c->npos, side = 2 * c->sr + 1;
+    c->spiral_x = (int32_t *)malloc(sizeof(int32_t) * n);
+    c->spiral_y = (int32_t *)malloc(sizeof(int32_t) * n);
+    c->spiral_of = (int32_t *)malloc(sizeof(int32_t) * n);
+    jmo_spiral(c->sr, c->spiral_x, c->spiral_y);
+    for (int k = 0; k < n; k++)
+        c->spiral_of[(c->spiral_y[k] + c->sr) * side + (c->spiral_x[k] + c->sr)] = k;
+}
+
+/* ---- luma quarter-pel interpolation, H.264 8.4.2.2.1 (normative) ----------------------- */
+static inline int px(const uint8_t *p, int w, int h, int s, int x, int y) {
+    return p[iclip(0, h - 1, y) * s + iclip(0, w - 1, x)];
+}
+static inline int tap6(int a, int b, int c, int d, int e, int f) {
+    return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
+}
+/* b1: horizontal half-pel intermediate between (x,y) and (x+1,y) */
+static int hb1(const uint8_t *p, int w, int h, int s, int x, int y) {
+    return tap6(px(p, w, h, s, x - 2, y), px(p, w, h, s, x - 1, y), px(p, w, h, s, x, y),
+                px(p, w, h, s, x + 1, y), px(p, w, h, s, x + 2, y), px(p, w, h, s, x + 3, y));
+}
+/* h1: vertical half-pel intermediate between (x,y) and (x,y+1) */
+static int vh1(const uint8_t *p, int w, int h, int s, int x, int y) {
+    return tap6(px(p, w, h, s, x, y - 2), px(p, w, h, s, x, y - 1), px(p, w, h, s, x, y),
+                px(p, w, h, s, x, y + 1), px(p, w, h, s, x, y + 2), px(p, w, h, s, x, y + 3));
+}
+int jmo_luma_qpel_sample(const uint8_t *p, int w, int h, int s, int X, int Y) {
+    int x = X >> 2, y = Y >> 2, fx = X & 3, fy = Y & 3;
+    int G = px(p, w, h, s, x, y);
+    if (fx == 0 && fy == 0) return G;
+    int b = clip255((hb1(p, w, h, s, x, y) + 16) >> 5);
+    int hh = clip255((vh1(p, w, h, s, x, y) + 16) >> 5);
+    int jj = 0;
+    if ((fx == 2 && fy != 0) || (fy == 2 && fx != 0)) {
+        int j1 = tap6(vh1(p, w, h, s, x - 2, y), vh1(p, w, h, s, x - 1, y), vh1(p, w, h, s, x, y),
+                      vh1(p, w, h, s, x + 1, y), vh1(p, w, h, s, x + 2, y),
+                      vh1(p, w, h, s, x + 3, y));
+        jj = clip255((j1 + 512) >> 10);
+    }
+    int s_ = clip255((hb1(p, w, h, s, x, y + 1) + 16) >> 5);   /* b at row y+1   */
+    int m = clip255((vh1(p, w, h, s, x + 1, y) + 16) >> 5);    /* h at column x+1 */
+    int H_ = px(p, w, h, s, x + 1, y), M = px(p, w, h, s, x, y + 1);
+    switch (fy * 4 + fx) {
+    case 1: return (G + b + 1) >> 1;        /* a */
+    case 2: return b;                       /* b */
+    case 3: return (H_ + b + 1) >> 1;       /* c */
+    case 4: return (G + hh + 1) >> 1;       /* d */
+    case 5: return (b + hh + 1) >> 1;       /* e */
+    case 6: return (b + jj + 1) >> 1;       /* f */
+    case 7: return (b + m + 1) >> 1;        /* g */
+    case 8: return hh;                      /* h */
+    case 9: return (hh + jj + 1) >> 1;      /* i */
+    case 10: return jj;                     /* j */
+    case 11: return (jj + m + 1) >> 1;      /* k */
+    case 12: return (M + hh + 1) >> 1;      /* n */
+    case 13: return (hh + s_ + 1) >> 1;     /* p */
+    case 14: return (jj + s_ + 1) >> 1;     /* q */
+    case 15: return (m + s_ + 1) >> 1;      /* r */
+    }
+    return G;
+}
+
+/* UnifiedOneForthPix [J]: 16 phase planes of the reference, padded by JMO_PAD so that
+ * clamping the integer position into [-PAD, W-1+PAD] (keeping the phase) equals the
+ * spec's per-tap coordinate clamping (PAD >= 3). */
+void jmo_build_qpel(jmo_ctx *c) {
+    int P = JMO_PAD, qs = c->qstride, qh = c->H + 2 * P;
+    for (int ph = 0; ph < 16; ph++) {
+        int fx = ph & 3, fy = ph >> 2;
+        uint8_t *pl = c->qpel + (size_t)ph * c->qplane;
+        for (int y = 0; y < qh; y++)
+            for (int x = 0; x < qs; x++)
+                pl[y * qs + x] = (uint8_t)jmo_luma_qpel_sample(
+                    c->refY, c->W, c->H, c->W, 4 * (x - P) + fx, 4 * (y - P) + fy);
+    }
+}
+
+int jmo_qpel_at(const jmo_ctx *c, int X, int Y) {
+    int P = JMO_PAD;
+    int x = iclip(-P, c->W - 1 + P, X >> 2), y = iclip(-P, c->H - 1 + P, Y >> 2);
+    int ph = (Y & 3) * 4 + (X & 3);
+    return c->qpel[(size_t)ph * c->qplane + (size_t)(y + P) * c->qstride + (x + P)];
+}
+
+/* SATD() [J] (mv-search.c): 4x4 Hadamard, sum |.|, >>1  (the sum is always even, so this
+ * equals JM>=10's (sum+1)>>1);  plain SAD when use_hadamard == 0. d[] raster. */
+int jmo_satd_block(const int32_t d[16], int use_hadamard) {
+    int satd = 0;
+    if (!use_hadamard) {
+        for (int k = 0; k < 16; k++) satd += iabs(d[k]);
+        return satd;
+    }
+    int m[16], t[16];
+    for (int x = 0; x < 4; x++) {        /* vertical (columns) */
+        int a0 = d[x] + d[12 + x], a1 = d[4 + x] + d[8 + x];
+        int a2 = d[4 + x] - d[8 + x], a3 = d[x] - d[12 + x];
+        m[x] = a0 + a1; m[8 + x] = a0 - a1; m[4 + x] = a2 + a3; m[12 + x] = a3 - a2;
+    }
+    for (int y = 0; y < 4; y++) {        /* horizontal (rows) */
+        int *r = m + 4 * y;
+        int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
+        t[4 * y + 0] = a0 + a1; t[4 * y + 2] = a0 - a1;
+        t[4 * y + 1] = a2 + a3; t[4 * y + 3] = a3 - a2;
+    }
+    for (int k = 0; k < 16; k++) satd += iabs(t[k]);
+    return satd >> 1;
+}
+int jmo_satd4x4(const int32_t *diff, int use_hadamard) { return jmo_satd_block(diff, use_hadamard); }
+
+/* forward 4x4 core transform (encoder; block.c dct_luma [J]) raster in place */
+void jmo_fwd4x4(int32_t m[16]) {
+    for (int y = 0; y < 4; y++) {        /* horizontal */
+        int32_t *r = m + 4 * y;
+        int p0 = r[0] + r[3], p3 = r[0] - r[3], p1 = r[1] + r[2], p2 = r[1] - r[2];
+        r[0] = p0 + p1; r[2] = p0 - p1; r[1] = 2 * p3 + p2; r[3] = p3 - 2 * p2;
+    }
+    for (int x = 0; x < 4; x++) {        /* vertical */
+        int p0 = m[x] + m[12 + x], p3 = m[x] - m[12 + x];
+        int p1 = m[4 + x] + m[8 + x], p2 = m[4 + x] - m[8 + x];
+        m[x] = p0 + p1; m[8 + x] = p0 - p1; m[4 + x] = 2 * p3 + p2; m[12 + x] = p3 - 2 * p2;
+    }
+}
+void jmo_forward4x4(const int32_t *in, int32_t *out) {
+    memcpy(out, in, 16 * sizeof(int32_t));
+    jmo_fwd4x4(out);
+}
+
+/* inverse 4x4 (H.264 8.5.12.2): rows first, then columns; no final shift */
+static void inv4x4_core(const int32_t in[16], int32_t out[16]) {
+    int32_t t[16];
+    for (int y = 0; y < 4; y++) {
+        const int32_t *d = in + 4 * y;
+        int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
+        t[4 * y + 0] = e0 + e3; t[4 * y + 1] = e1 + e2; t[4 * y + 2] = e1 - e2; t[4 * y + 3] = e0 - e3;
+    }
+    for (int x = 0; x < 4; x++) {
+        int d0 = t[x], d1 = t[4 + x], d2 = t[8 + x], d3 = t[12 + x];
+        int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+        out[x] = e0 + e3; out[4 + x] = e1 + e2; out[8 + x] = e1 - e2; out[12 + x] = e0 - e3;
+    }
+}
+void jmo_inverse4x4(const int32_t *in, int32_t *out) { inv4x4_core(in, out); }
+
+/* inverse transform + reconstruction: clip((r + (pred<<6) + 32) >> 6) */
+void jmo_inv4x4_add(const int32_t m[16], const uint8_t *pred, int pstride, uint8_t *out,
+                    int ostride) {
+    int32_t r[16];
+    inv4x4_core(m, r);
+    for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++)
+            out[y * ostride + x] =
+                (uint8_t)clip255((r[4 * y + x] + (pred[y * pstride + x] << DQ_BITS) + DQ_ROUND) >> DQ_BITS);
+}

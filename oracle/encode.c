@@ -1,0 +1,990 @@
+/*
+ * encode.c — oracle restatement of JM 8.6 lencod's RDO-off macroblock hot path
+ * (TEST INFRASTRUCTURE ONLY; see jm_oracle.h for the parity status).
+ *
+ * Restated JM 8.6 functions [J] (no file:line exists: /root/reference holds README.md:1-4):
+ *   rdopt.c      › encode_one_macroblock (RDO off), Mode_Decision_for_Intra4x4Macroblock,
+ *                  Mode_Decision_for_8x8IntraBlocks, Mode_Decision_for_4x4IntraBlocks,
+ *                  SetModesAndRefframeForBlocks, SetCoeffAndReconstruction8x8
+ *   mv-search.c  › SetMotionVectorPredictor, FindSkipModeMotionVector, PartitionMotionSearch,
+ *                  BlockMotionSearch, SetupFastFullPelSearch, SetupLargerBlocks,
+ *                  FastFullPelBlockMotionSearch, FullPelBlockMotionSearch,
+ *                  SubPelBlockMotionSearch
+ *   block.c      › intrapred_luma, intrapred_luma_16x16, find_sad_16x16, dct_luma,
+ *                  dct_luma_16x16, dct_chroma
+ *   macroblock.c › LumaResidualCoding, LumaResidualCoding8x8, LumaPrediction4x4,
+ *                  ChromaResidualCoding, OneComponentChromaPrediction4x4,
+ *                  IntraChromaPrediction8x8
+ * Normative pieces follow ITU-T H.264: 8.3.1/8.3.3/8.3.4 (intra prediction), 8.4.1.3 (MVP),
+ * 8.4.1.1 (P_Skip MV), 8.4.2.2 (sample interpolation), 8.5.10-8.5.12 (inverse transforms).
+ * Non-normative choices are listed in docs/JM_SEMANTICS.md.
+ */
+#include <stdlib.h>
+#include "jmo_internal.h"
+
+typedef struct {
+    jmo_ctx *c;
+    int mbx, mby, pix_x, pix_y, mb_addr;
+    int lambda;                /* lambda_mode == lambda_motion (RDO off, integer)        */
+    int lf;                    /* LAMBDA_FACTOR(lambda) = 65536*lambda                     */
+    int slice_p;
+    uint8_t org[256];          /* imgY_org of the MB                                       */
+    uint8_t orgc[2][64];
+    /* FFS state (SetupFastFullPelSearch) */
+    int setup_done, scx, scy, pos_00;
+    int16_t all_mv[8][16][2];  /* img->all_mv[.][.][LIST_0][ref 0][blocktype]               */
+    int motion_cost[8][4];
+    int skip_mv[2];
+} mbs;
+
+/* ====================================================================================== */
+/*  neighbour access (getLuma4x4Neighbour / getNeighbour, H.264 6.4.11/6.4.12, single slice) */
+/* ====================================================================================== */
+static int nb4(const mbs *s, int xN, int yN, int *idx) {
+    const jmo_ctx *c = s->c;
+    int mx, my;
+    if (yN > 15) return 0;
+    if (xN < 0) { mx = s->mbx - 1; my = yN < 0 ? s->mby - 1 : s->mby; }
+    else if (xN <= 15) { mx = s->mbx; my = yN < 0 ? s->mby - 1 : s->mby; }
+    else { if (yN >= 0) return 0; mx = s->mbx + 1; my = s->mby - 1; }
+    if (mx < 0 || my < 0 || mx >= c->mbw) return 0;
+    *idx = ((s->pix_y + yN) >> 2) * (c->W >> 2) + ((s->pix_x + xN) >> 2);
+    return 1;
+}
+
+/* SetMotionVectorPredictor [J] / H.264 8.4.1.3 (list 0). block_x/y in 4x4 units. */
+static void set_mvp(const mbs *s, int pmv[2], int ref, int block_x, int block_y, int bsx, int bsy) {
+    const jmo_ctx *c = s->c;
+    int mb_x = 4 * block_x, mb_y = 4 * block_y;
+    int ia = 0, ib = 0, ic = 0, id = 0;
+    int av_a = nb4(s, mb_x - 1, mb_y, &ia);
+    int av_b = nb4(s, mb_x, mb_y - 1, &ib);
+    int av_c = nb4(s, mb_x + bsx, mb_y - 1, &ic);
+    int av_d = nb4(s, mb_x - 1, mb_y - 1, &id);
+    if (mb_y > 0) {                       /* C inside the MB but later in decoding order */
+        if (mb_x < 8) {
+            if (mb_y == 8) { if (bsx == 16) av_c = 0; }
+            else if (mb_x + bsx == 8) av_c = 0;
+        } else if (mb_x + bsx == 16) av_c = 0;
+    }
+    if (!av_c) { av_c = av_d; ic = id; }
+    int rL = av_a ? c->refidx[ia] : -1;
+    int rU = av_b ? c->refidx[ib] : -1;
+    int rUR = av_c ? c->refidx[ic] : -1;
+    enum { MEDIAN, PL, PU, PUR } type = MEDIAN;
+    if (rL == ref && rU != ref && rUR != ref) type = PL;
+    else if (rL != ref && rU == ref && rUR != ref) type = PU;
+    else if (rL != ref && rU != ref && rUR == ref) type = PUR;
+    if (bsx == 8 && bsy == 16) {
+        if (mb_x == 0) { if (rL == ref) type = PL; }
+        else if (rUR == ref) type = PUR;
+    } else if (bsx == 16 && bsy == 8) {
+        if (mb_y == 0) { if (rU == ref) type = PU; }
+        else if (rL == ref) type = PL;
+    }
+    for (int hv = 0; hv < 2; hv++) {
+        int a = av_a ? c->mv[2 * ia + hv] : 0;
+        int b = av_b ? c->mv[2 * ib + hv] : 0;
+        int cc = av_c ? c->mv[2 * ic + hv] : 0;
+        int p;
+        switch (type) {
+        case PL: p = a; break;
+        case PU: p = b; break;
+        case PUR: p = cc; break;
+        default:
+            if (!(av_b || av_c)) p = a;
+            else p = a + b + cc - imin(a, imin(b, cc)) - imax(a, imax(b, cc));
+        }
+        pmv[hv] = p;
+    }
+}
+
+/* unit-test entry: the same rules on explicit neighbours (single MB, no picture) */
+void jmo_mvp_median(int av_a, int rL, int ax, int ay, int av_b, int rU, int bx, int by,
+                    int av_c, int rUR, int cx, int cy, int ref, int bsx, int bsy, int blk_x,
+                    int blk_y, int32_t *pmv) {
+    (void)blk_y;
+    int type = 0;
+    if (!av_a) rL = -1;
+    if (!av_b) rU = -1;
+    if (!av_c) rUR = -1;
+    if (rL == ref && rU != ref && rUR != ref) type = 1;
+    else if (rL != ref && rU == ref && rUR != ref) type = 2;
+    else if (rL != ref && rU != ref && rUR == ref) type = 3;
+    if (bsx == 8 && bsy == 16) { if (blk_x == 0) { if (rL == ref) type = 1; } else if (rUR == ref) type = 3; }
+    else if (bsx == 16 && bsy == 8) { if (blk_y == 0) { if (rU == ref) type = 2; } else if (rL == ref) type = 1; }
+    int va[2] = {av_a ? ax : 0, av_a ? ay : 0}, vb[2] = {av_b ? bx : 0, av_b ? by : 0},
+        vc[2] = {av_c ? cx : 0, av_c ? cy : 0};
+    for (int hv = 0; hv < 2; hv++) {
+        int a = va[hv], b = vb[hv], cc = vc[hv];
+        if (type == 1) pmv[hv] = a;
+        else if (type == 2) pmv[hv] = b;
+        else if (type == 3) pmv[hv] = cc;
+        else if (!(av_b || av_c)) pmv[hv] = a;
+        else pmv[hv] = a + b + cc - imin(a, imin(b, cc)) - imax(a, imax(b, cc));
+    }
+}
+
+/* FindSkipModeMotionVector [J] / H.264 8.4.1.1 */
+static void find_skip_mv(mbs *s) {
+    const jmo_ctx *c = s->c;
+    int ia = 0, ib = 0;
+    int av_a = nb4(s, -1, 0, &ia), av_b = nb4(s, 0, -1, &ib);
+    int zl = !av_a ? 1 : (c->refidx[ia] == 0 && c->mv[2 * ia] == 0 && c->mv[2 * ia + 1] == 0);
+    int za = !av_b ? 1 : (c->refidx[ib] == 0 && c->mv[2 * ib] == 0 && c->mv[2 * ib + 1] == 0);
+    if (za || zl) { s->skip_mv[0] = s->skip_mv[1] = 0; }
+    else {
+        int pmv[2];
+        set_mvp(s, pmv, 0, 0, 0, 16, 16);
+        s->skip_mv[0] = pmv[0]; s->skip_mv[1] = pmv[1];
+    }
+}
+
+/* ====================================================================================== */
+/*  motion estimation                                                                        */
+/* ====================================================================================== */
+static inline int refpel(const jmo_ctx *c, int x, int y) {   /* UMV integer access (clamp) */
+    return c->refY[iclip(0, c->H - 1, y) * c->W + iclip(0, c->W - 1, x)];
+}
+static inline int mv_cost(const mbs *s, int shift, int cx, int cy, int px, int py) {
+    /* MV_COST(f,s,cx,cy,px,py) = (f*(mvbits[(cx<<s)-px]+mvbits[(cy<<s)-py])) >> 16 [J] */
+    return (s->lf * (jmo_mvbits((cx << shift) - px) + jmo_mvbits((cy << shift) - py))) >> 16;
+}
+
+static int block_range(const mbs *s, int blocktype) {
+    int sr = s->c->sr, rs = s->c->cfg.restrict_search_range;
+    /* PartitionMotionSearch [J]: ref 0 -> (min(ref,1)+1) == 1 */
+    if (rs == 2) return sr;
+    if (rs == 1) return sr;
+    return sr / imin(2, blocktype);
+}
+
+/* SetupFastFullPelSearch [J]: window centre = 16x16 MVP/4 (trunc), clamped to +-SR (RDO off);
+ * 16 4x4 SADs per search position (stored in window raster order). */
+static void ffs_setup(mbs *s) {
+    jmo_ctx *c = s->c;
+    int sr = c->sr, side = 2 * sr + 1, pmv[2];
+    set_mvp(s, pmv, 0, 0, 0, 16, 16);
+    s->scx = iclip(-sr, sr, pmv[0] / 4);
+    s->scy = iclip(-sr, sr, pmv[1] / 4);
+    s->pos_00 = c->spiral_of[(-s->scy + sr) * side + (-s->scx + sr)];
+    for (int dy = -sr; dy <= sr; dy++)
+        for (int dx = -sr; dx <= sr; dx++) {
+            int ax = s->pix_x + s->scx + dx, ay = s->pix_y + s->scy + dy;
+            int r = (dy + sr) * side + (dx + sr);
+            for (int b = 0; b < 16; b++) {
+                int ox = (b & 3) * 4, oy = (b >> 2) * 4, sad = 0;
+                for (int y = 0; y < 4; y++)
+                    for (int x = 0; x < 4; x++)
+                        sad += iabs(s->org[(oy + y) * 16 + ox + x] - refpel(c, ax + ox + x, ay + oy + y));
+                c->blocksad[(size_t)b * c->npos + r] = (uint16_t)sad;
+            }
+        }
+    s->setup_done = 1;
+}
+
+/* SetupLargerBlocks [J] equivalent: SAD of a bsx x bsy block at window raster index r */
+static inline int block_sad_at(const mbs *s, int bx4, int by4, int w4, int h4, int r) {
+    const jmo_ctx *c = s->c;
+    int sum = 0;
+    for (int y = 0; y < h4; y++)
+        for (int x = 0; x < w4; x++)
+            sum += c->blocksad[(size_t)((by4 + y) * 4 + bx4 + x) * c->npos + r];
+    return sum;
+}
+
+/* FastFullPelBlockMotionSearch [J] */
+static int ffs_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int pmvy, int range,
+                      int *mvx, int *mvy) {
+    jmo_ctx *c = s->c;
+    int sr = c->sr, side = 2 * sr + 1;
+    int w4 = jmo_blc_size[blocktype][0] >> 2, h4 = jmo_blc_size[blocktype][1] >> 2;
+    int max_pos = (2 * range + 1) * (2 * range + 1);
+    int min_mcost = BIGCOST, best_pos = 0;
+    if (!s->setup_done) ffs_setup(s);
+    {   /* cost for (0,0)-vector first (RDO off) */
+        int r = (-s->scy + sr) * side + (-s->scx + sr);
+        int mcost = block_sad_at(s, bx4, by4, w4, h4, r) + mv_cost(s, 2, 0, 0, pmvx, pmvy);
+        if (mcost < min_mcost) { min_mcost = mcost; best_pos = s->pos_00; }
+    }
+    for (int pos = 0; pos < max_pos; pos++) {
+        int dx = c->spiral_x[pos], dy = c->spiral_y[pos];
+        int sad = block_sad_at(s, bx4, by4, w4, h4, (dy + sr) * side + (dx + sr));
+        if (sad < min_mcost) {
+            int mcost = sad + mv_cost(s, 2, s->scx + dx, s->scy + dy, pmvx, pmvy);
+            if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+        }
+    }
+    *mvx = s->scx + c->spiral_x[best_pos];
+    *mvy = s->scy + c->spiral_y[best_pos];
+    return min_mcost;
+}
+
+/* FullPelBlockMotionSearch [J] (SearchMode -1): window centred on the block's own MVP */
+static int full_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int pmvy, int range,
+                       int *mvx, int *mvy) {
+    jmo_ctx *c = s->c;
+    int bsx = jmo_blc_size[blocktype][0], bsy = jmo_blc_size[blocktype][1];
+    int max_pos = (2 * range + 1) * (2 * range + 1);
+    int pic_x = s->pix_x + 4 * bx4, pic_y = s->pix_y + 4 * by4;
+    int cxa = pic_x + *mvx, cya = pic_y + *mvy;
+    int check_00 = (blocktype == 1 && s->slice_p);
+    int min_mcost = BIGCOST, best_pos = 0;
+    for (int pos = 0; pos < max_pos; pos++) {
+        int cx = cxa + c->spiral_x[pos], cy = cya + c->spiral_y[pos];
+        int mcost = mv_cost(s, 2, cx - pic_x, cy - pic_y, pmvx, pmvy);
+        if (check_00 && cx == pic_x && cy == pic_y) mcost -= (s->lf * 16) >> 16;
+        if (mcost >= min_mcost) continue;
+        for (int y = 0; y < bsy; y++)
+            for (int x = 0; x < bsx; x++)
+                mcost += iabs(s->org[(4 * by4 + y) * 16 + 4 * bx4 + x] - refpel(c, cx + x, cy + y));
+        if (mcost < min_mcost) { best_pos = pos; min_mcost = mcost; }
+    }
+    *mvx += c->spiral_x[best_pos];
+    *mvy += c->spiral_y[best_pos];
+    return min_mcost;
+}
+
+/* SATD of a block at a quarter-pel candidate (sum over its 4x4 sub-blocks) */
+static int subpel_satd(const mbs *s, int bx4, int by4, int w4, int h4, int cmx, int cmy) {
+    const jmo_ctx *c = s->c;
+    int total = 0;
+    for (int y4 = 0; y4 < h4; y4++)
+        for (int x4 = 0; x4 < w4; x4++) {
+            int32_t d[16];
+            int ox = 4 * (bx4 + x4), oy = 4 * (by4 + y4);
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++)
+                    d[4 * y + x] = s->org[(oy + y) * 16 + ox + x] -
+                                   jmo_qpel_at(c, 4 * (s->pix_x + ox + x) + cmx, 4 * (s->pix_y + oy + y) + cmy);
+            total += jmo_satd_block(d, c->cfg.use_hadamard);
+        }
+    return total;
+}
+
+/* SubPelBlockMotionSearch [J] with search_pos2 = search_pos4 = 9 */
+static int subpel_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int pmvy, int *mvx,
+                         int *mvy, int min_mcost) {
+    jmo_ctx *c = s->c;
+    int had = c->cfg.use_hadamard;
+    int w4 = jmo_blc_size[blocktype][0] >> 2, h4 = jmo_blc_size[blocktype][1] >> 2;
+    int check_position0 = (blocktype == 1 && *mvx == 0 && *mvy == 0 && had && s->slice_p);
+    int min_pos2 = had ? 0 : 1, max_pos2 = 9;
+    int mx = *mvx << 2, my = *mvy << 2, best_pos = 0;
+    for (int pos = min_pos2; pos < max_pos2; pos++) {          /* half-pel */
+        int cx = mx + (c->spiral_x[pos] << 1), cy = my + (c->spiral_y[pos] << 1);
+        int mcost = mv_cost(s, 0, cx, cy, pmvx, pmvy);
+        if (check_position0 && pos == 0) mcost -= (s->lf * 16) >> 16;
+        if (mcost >= min_mcost) continue;
+        mcost += subpel_satd(s, bx4, by4, w4, h4, cx, cy);
+        if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+    }
+    if (best_pos) { mx += c->spiral_x[best_pos] << 1; my += c->spiral_y[best_pos] << 1; }
+    best_pos = 0;
+    for (int pos = 1; pos < 9; pos++) {                         /* quarter-pel */
+        int cx = mx + c->spiral_x[pos], cy = my + c->spiral_y[pos];
+        int mcost = mv_cost(s, 0, cx, cy, pmvx, pmvy);
+        if (mcost >= min_mcost) continue;
+        mcost += subpel_satd(s, bx4, by4, w4, h4, cx, cy);
+        if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
+    }
+    if (best_pos) { mx += c->spiral_x[best_pos]; my += c->spiral_y[best_pos]; }
+    *mvx = mx; *mvy = my;
+    return min_mcost;
+}
+
+/* BlockMotionSearch [J] (list 0, ref 0) */
+static int block_motion_search(mbs *s, int blocktype, int bx4, int by4, int range) {
+    jmo_ctx *c = s->c;
+    int bsx = jmo_blc_size[blocktype][0], bsy = jmo_blc_size[blocktype][1];
+    int pmv[2];
+    set_mvp(s, pmv, 0, bx4, by4, bsx, bsy);
+    int mvx = iclip(-range, range, pmv[0] / 4), mvy = iclip(-range, range, pmv[1] / 4);
+    int min_mcost;
+    if (c->cfg.search_mode == 0) min_mcost = ffs_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
+    else min_mcost = full_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
+    if (c->cfg.use_hadamard) min_mcost = BIGCOST;
+    min_mcost = subpel_search(s, blocktype, bx4, by4, pmv[0], pmv[1], &mvx, &mvy, min_mcost);
+    for (int y = 0; y < (bsy >> 2); y++)
+        for (int x = 0; x < (bsx >> 2); x++) {
+            s->all_mv[blocktype][(by4 + y) * 4 + bx4 + x][0] = (int16_t)mvx;
+            s->all_mv[blocktype][(by4 + y) * 4 + bx4 + x][1] = (int16_t)mvy;
+        }
+    return min_mcost;
+}
+
+static void write_enc_mv(mbs *s, int bx4, int by4, int w4, int h4, const int16_t (*mv)[2]) {
+    jmo_ctx *c = s->c;
+    int W4 = c->W >> 2;
+    for (int y = 0; y < h4; y++)
+        for (int x = 0; x < w4; x++) {
+            int k = (by4 + y) * 4 + bx4 + x;
+            int a = ((s->pix_y >> 2) + by4 + y) * W4 + (s->pix_x >> 2) + bx4 + x;
+            c->mv[2 * a] = mv[k][0];
+            c->mv[2 * a + 1] = mv[k][1];
+            c->refidx[a] = 0;
+        }
+}
+
+/* PartitionMotionSearch [J] (list 0, single reference) */
+static void partition_motion_search(mbs *s, int blocktype, int block8x8) {
+    static const int bx0[5][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 2, 0, 0}, {0, 2, 0, 2}};
+    static const int by0[5][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 2, 0, 0}, {0, 0, 0, 0}, {0, 0, 2, 2}};
+    int parttype = blocktype < 4 ? blocktype : 4;
+    int step_h0 = jmo_blc_size[parttype][0] >> 2, step_v0 = jmo_blc_size[parttype][1] >> 2;
+    int step_h = jmo_blc_size[blocktype][0] >> 2, step_v = jmo_blc_size[blocktype][1] >> 2;
+    int range = block_range(s, blocktype);
+    s->motion_cost[blocktype][block8x8] = 0;
+    for (int v = by0[parttype][block8x8]; v < by0[parttype][block8x8] + step_v0; v += step_v)
+        for (int h = bx0[parttype][block8x8]; h < bx0[parttype][block8x8] + step_h0; h += step_h) {
+            s->motion_cost[blocktype][block8x8] += block_motion_search(s, blocktype, h, v, range);
+            write_enc_mv(s, h, v, step_h, step_v, s->all_mv[blocktype]);
+        }
+}
+
+/* ====================================================================================== */
+/*  transform / quantisation                                                               */
+/* ====================================================================================== */
+/* dct_luma [J]: 4x4 forward, quant (deadzone qp_const), scan, dequant, inverse, recon */
+static int dct_luma4x4(const int32_t resid[16], const uint8_t *pred, int ps, int qp, int intra_round,
+                       int16_t levels[16], int *coeff_cost, uint8_t *rec, int rs) {
+    int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS + qp_per;
+    int qp_const = intra_round ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+    int32_t m[16];
+    memcpy(m, resid, sizeof(m));
+    jmo_fwd4x4(m);
+    int run = -1, nonzero = 0;
+    for (int k = 0; k < 16; k++) {
+        int pos = jmo_scan4x4[k];
+        run++;
+        int level = (iabs(m[pos]) * jmo_quant_coef[qp_rem][pos] + qp_const) >> q_bits;
+        int ilev = 0;
+        if (level != 0) {
+            nonzero = 1;
+            *coeff_cost += level > 1 ? MAX_VALUE : jmo_coeff_cost_tab[run];
+            levels[k] = (int16_t)isign(level, m[pos]);
+            run = -1;
+            ilev = level * jmo_dequant_coef[qp_rem][pos] << qp_per;
+        } else levels[k] = 0;
+        m[pos] = isign(ilev, m[pos]);
+    }
+    jmo_inv4x4_add(m, pred, ps, rec, rs);
+    return nonzero;
+}
+
+int jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,
+                    int16_t *levels, uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
+    if (n < 0 || qp < 0 || qp > 51) return JMH_E_INVALID_ARG;
+    for (int i = 0; i < n; i++) {
+        int32_t r[16];
+        int cc = 0;
+        for (int k = 0; k < 16; k++) r[k] = resid[16 * i + k];
+        nonzero[i] = dct_luma4x4(r, pred + 16 * i, 4, qp, intra, levels + 16 * i, &cc, recon + 16 * i, 4);
+        coeff_cost[i] = cc;
+    }
+    return JMH_OK;
+}
+
+/* dct_chroma [J] for one component: 4 4x4 AC blocks + 2x2 DC; returns updated cr_cbp.
+ * resid/pred raster 8x8.  DC reconstruction follows H.264 8.5.11.2 exactly. */
+static int dct_chroma(const int32_t resid[64], const uint8_t pred[64], int qpc, int intra_round,
+                      int cr_cbp, int16_t dc_out[4], int16_t ac_out[4][16], uint8_t rec[64]) {
+    int qp_per = qpc / 6, qp_rem = qpc % 6, q_bits = Q_BITS + qp_per;
+    int qp_const = intra_round ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+    int32_t m[4][16];
+    for (int b = 0; b < 4; b++) {
+        int ox = (b & 1) * 4, oy = (b >> 1) * 4;
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++) m[b][4 * y + x] = resid[(oy + y) * 8 + ox + x];
+        jmo_fwd4x4(m[b]);
+    }
+    int m1[4] = {m[0][0] + m[1][0] + m[2][0] + m[3][0], m[0][0] - m[1][0] + m[2][0] - m[3][0],
+                 m[0][0] + m[1][0] - m[2][0] - m[3][0], m[0][0] - m[1][0] - m[2][0] + m[3][0]};
+    int dccoded = 0;
+    for (int k = 0; k < 4; k++) {
+        int level = (iabs(m1[k]) * jmo_quant_coef[qp_rem][0] + 2 * qp_const) >> (q_bits + 1);
+        if (level != 0) { cr_cbp = imax(1, cr_cbp); dccoded = 1; }
+        dc_out[k] = (int16_t)isign(level, m1[k]);
+    }
+    (void)dccoded;
+    /* inverse 2x2 Hadamard of the levels and scaling (8.5.11.2): dcC = ((f*16v) << per) >> 5 */
+    int c0 = dc_out[0], c1 = dc_out[1], c2 = dc_out[2], c3 = dc_out[3];
+    int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+    int v00 = jmo_dequant_coef[qp_rem][0];
+    int coeff_cost = 0, ac_any = 0;
+    for (int b = 0; b < 4; b++) {
+        int run = -1;
+        ac_out[b][0] = 0;
+        for (int k = 1; k < 16; k++) {
+            int pos = jmo_scan4x4[k];
+            run++;
+            int level = (iabs(m[b][pos]) * jmo_quant_coef[qp_rem][pos] + qp_const) >> q_bits;
+            int ilev = 0;
+            if (level != 0) {
+                coeff_cost += level > 1 ? MAX_VALUE : jmo_coeff_cost_tab[run];
+                ac_any = 1;
+                run = -1;
+                ilev = level * jmo_dequant_coef[qp_rem][pos] << qp_per;
+            }
+            ac_out[b][k] = (int16_t)isign(level, m[b][pos]);
+            m[b][pos] = isign(ilev, m[b][pos]);
+        }
+    }
+    if (coeff_cost < CHROMA_COEFF_COST) {                 /* reset chroma AC coeffs [J] */
+        ac_any = 0;
+        for (int b = 0; b < 4; b++)
+            for (int k = 1; k < 16; k++) { ac_out[b][k] = 0; m[b][jmo_scan4x4[k]] = 0; }
+    }
+    if (ac_any) cr_cbp = 2;
+    for (int b = 0; b < 4; b++) {
+        m[b][0] = ((f[b] * 16 * v00) << qp_per) >> 5;
+        int ox = (b & 1) * 4, oy = (b >> 1) * 4;
+        jmo_inv4x4_add(m[b], pred + oy * 8 + ox, 8, rec + oy * 8 + ox, 8);
+    }
+    return cr_cbp;
+}
+
+/* dct_luma_16x16 [J]: returns luma cbp (15 if any AC level, else 0) */
+static int dct_luma_16x16(const int32_t resid[256], const uint8_t pred[256], int qp,
+                          int16_t dc_out[16], int16_t ac_out[16][16], int *cbp_blk, uint8_t rec[256]) {
+    int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS + qp_per;
+    int qp_const = (1 << q_bits) / 3, qp_const2 = qp_const << 1;
+    int32_t m[16][16];                     /* [4x4 block raster][coef raster] */
+    for (int b = 0; b < 16; b++) {
+        int ox = (b & 3) * 4, oy = (b >> 2) * 4;
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++) m[b][4 * y + x] = resid[(oy + y) * 16 + ox + x];
+        jmo_fwd4x4(m[b]);
+    }
+    int32_t dc[16];                        /* DC matrix raster: [by*4+bx] */
+    for (int b = 0; b < 16; b++) dc[b] = m[b][0];
+    /* forward Hadamard, rows then columns with >>1 */
+    for (int y = 0; y < 4; y++) {
+        int32_t *r = dc + 4 * y;
+        int a0 = r[0] + r[3], a3 = r[0] - r[3], a1 = r[1] + r[2], a2 = r[1] - r[2];
+        r[0] = a0 + a1; r[2] = a0 - a1; r[1] = a3 + a2; r[3] = a3 - a2;
+    }
+    for (int x = 0; x < 4; x++) {
+        int a0 = dc[x] + dc[12 + x], a3 = dc[x] - dc[12 + x];
+        int a1 = dc[4 + x] + dc[8 + x], a2 = dc[4 + x] - dc[8 + x];
+        dc[x] = (a0 + a1) >> 1; dc[8 + x] = (a0 - a1) >> 1;
+        dc[4 + x] = (a3 + a2) >> 1; dc[12 + x] = (a3 - a2) >> 1;
+    }
+    int32_t lev[16];
+    for (int k = 0; k < 16; k++) {
+        int pos = jmo_scan4x4[k];
+        int level = (iabs(dc[pos]) * jmo_quant_coef[qp_rem][0] + qp_const2) >> (q_bits + 1);
+        dc_out[k] = (int16_t)isign(level, dc[pos]);
+        lev[pos] = dc_out[k];
+    }
+    /* inverse Hadamard (8.5.10) + scaling ((f*v << per) + 2) >> 2 */
+    int32_t t[16], f[16];
+    for (int y = 0; y < 4; y++) {
+        const int32_t *c = lev + 4 * y;
+        int e0 = c[0] + c[2], e1 = c[0] - c[2], e2 = c[1] - c[3], e3 = c[1] + c[3];
+        t[4 * y + 0] = e0 + e3; t[4 * y + 3] = e0 - e3; t[4 * y + 1] = e1 + e2; t[4 * y + 2] = e1 - e2;
+    }
+    for (int x = 0; x < 4; x++) {
+        int e0 = t[x] + t[8 + x], e1 = t[x] - t[8 + x], e2 = t[4 + x] - t[12 + x], e3 = t[4 + x] + t[12 + x];
+        f[x] = e0 + e3; f[12 + x] = e0 - e3; f[4 + x] = e1 + e2; f[8 + x] = e1 - e2;
+    }
+    int v00 = jmo_dequant_coef[qp_rem][0];
+    int ac = 0;
+    for (int b = 0; b < 16; b++) {
+        int run = -1, nz = 0;
+        (void)run;
+        ac_out[b][0] = 0;
+        for (int k = 1; k < 16; k++) {
+            int pos = jmo_scan4x4[k];
+            int level = (iabs(m[b][pos]) * jmo_quant_coef[qp_rem][pos] + qp_const) >> q_bits;
+            if (level) { ac = 15; nz = 1; }
+            ac_out[b][k] = (int16_t)isign(level, m[b][pos]);
+            m[b][pos] = isign(level * jmo_dequant_coef[qp_rem][pos] << qp_per, m[b][pos]);
+        }
+        if (nz) *cbp_blk |= 1 << b;
+        m[b][0] = ((f[b] * v00 << qp_per) + 2) >> 2;
+        int ox = (b & 3) * 4, oy = (b >> 2) * 4;
+        jmo_inv4x4_add(m[b], pred + oy * 16 + ox, 16, rec + oy * 16 + ox, 16);
+    }
+    return ac;
+}
+
+/* ====================================================================================== */
+/*  intra prediction (H.264 8.3)                                                            */
+/* ====================================================================================== */
+static int mb_avail(const mbs *s, int dmx, int dmy) {
+    int mx = s->mbx + dmx, my = s->mby + dmy;
+    return mx >= 0 && my >= 0 && mx < s->c->mbw && my < s->c->mbh &&
+           (my < s->mby || (my == s->mby && mx < s->mbx));
+}
+/* luma sample availability at MB-relative (x,y) for intra prediction */
+static int luma_avail(const mbs *s, int x, int y) {
+    if (y > 15) return 0;
+    if (x < 0) return mb_avail(s, -1, y < 0 ? -1 : 0);
+    if (x <= 15) return y < 0 ? mb_avail(s, 0, -1) : 1;
+    return y < 0 ? mb_avail(s, 1, -1) : 0;
+}
+
+/* intrapred_luma [J] / 8.3.1.2: the 9 Intra4x4 predictions of the 4x4 block at (bx,by)
+ * (pixels, MB relative); pred[9][16]; avail[9] */
+static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int avail[9]) {
+    const jmo_ctx *c = s->c;
+    const uint8_t *R = c->recY;
+    int W = c->W, ax = s->pix_x + bx, ay = s->pix_y + by;
+    int up = luma_avail(s, bx, by - 1), left = luma_avail(s, bx - 1, by);
+    int ul = luma_avail(s, bx - 1, by - 1);
+    int ur = luma_avail(s, bx + 4, by - 1) && !((bx == 4 || bx == 12) && (by == 4 || by == 12));
+    int T[9], L[4];                      /* T[0] = p[-1,-1], T[1+x] = p[x,-1] */
+    T[0] = ul ? R[(ay - 1) * W + ax - 1] : 0;
+    for (int x = 0; x < 4; x++) T[1 + x] = up ? R[(ay - 1) * W + ax + x] : 0;
+    for (int x = 4; x < 8; x++) T[1 + x] = up ? (ur ? R[(ay - 1) * W + ax + x] : T[4]) : 0;
+    for (int y = 0; y < 4; y++) L[y] = left ? R[(ay + y) * W + ax - 1] : 0;
+#define PT(x) T[1 + (x)]
+#define PL(y) ((y) < 0 ? T[0] : L[y])
+    int all = up && left && ul;
+    for (int m = 0; m < 9; m++) avail[m] = 0;
+    avail[2] = 1;
+    avail[0] = avail[3] = avail[7] = up;
+    avail[1] = avail[8] = left;
+    avail[4] = avail[5] = avail[6] = all;
+    for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++) {
+            int k = 4 * y + x;
+            pred[0][k] = (uint8_t)PT(x);
+            pred[1][k] = (uint8_t)L[y];
+            /* DDL */
+            pred[3][k] = (uint8_t)((x == 3 && y == 3) ? (PT(6) + 3 * PT(7) + 2) >> 2
+                                                      : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2);
+            /* DDR */
+            if (x > y) pred[4][k] = (uint8_t)((PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2);
+            else if (x < y) pred[4][k] = (uint8_t)((PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2);
+            else pred[4][k] = (uint8_t)((PT(0) + 2 * T[0] + PL(0) + 2) >> 2);
+            /* VR */
+            {
+                int z = 2 * x - y, v;
+                if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
+                else if (z == -1) v = (PL(0) + 2 * T[0] + PT(0) + 2) >> 2;
+                else v = (PL(y - 1) + 2 * PL(y - 2) + PL(y - 3) + 2) >> 2;
+                pred[5][k] = (uint8_t)v;
+            }
+            /* HD */
+            {
+                int z = 2 * y - x, v;
+                if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
+                else if (z == -1) v = (PL(0) + 2 * T[0] + PT(0) + 2) >> 2;
+                else v = (PT(x - 1) + 2 * PT(x - 2) + PT(x - 3) + 2) >> 2;
+                pred[6][k] = (uint8_t)v;
+            }
+            /* VL */
+            if (!(y & 1)) pred[7][k] = (uint8_t)((PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1);
+            else pred[7][k] = (uint8_t)((PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2);
+            /* HU */
+            {
+                int z = x + 2 * y, v;
+                if (z > 5) v = L[3];
+                else if (z == 5) v = (L[2] + 3 * L[3] + 2) >> 2;
+                else if (!(z & 1)) v = (L[y + (x >> 1)] + L[y + (x >> 1) + 1] + 1) >> 1;
+                else v = (L[y + (x >> 1)] + 2 * L[y + (x >> 1) + 1] + L[y + (x >> 1) + 2] + 2) >> 2;
+                pred[8][k] = (uint8_t)v;
+            }
+        }
+    /* DC */
+    int dcv;
+    if (up && left) dcv = (PT(0) + PT(1) + PT(2) + PT(3) + L[0] + L[1] + L[2] + L[3] + 4) >> 3;
+    else if (left) dcv = (L[0] + L[1] + L[2] + L[3] + 2) >> 2;
+    else if (up) dcv = (PT(0) + PT(1) + PT(2) + PT(3) + 2) >> 2;
+    else dcv = 128;
+    for (int k = 0; k < 16; k++) pred[2][k] = (uint8_t)dcv;
+#undef PT
+#undef PL
+}
+
+/* intrapred_luma_16x16 [J] / 8.3.3 */
+static void intra16_pred(const mbs *s, uint8_t pred[4][256], int avail[4]) {
+    const jmo_ctx *c = s->c;
+    const uint8_t *R = c->recY;
+    int W = c->W, ax = s->pix_x, ay = s->pix_y;
+    int up = mb_avail(s, 0, -1), left = mb_avail(s, -1, 0), ul = mb_avail(s, -1, -1);
+    int T[16], L[16], P = ul ? R[(ay - 1) * W + ax - 1] : 0;
+    for (int i = 0; i < 16; i++) {
+        T[i] = up ? R[(ay - 1) * W + ax + i] : 0;
+        L[i] = left ? R[(ay + i) * W + ax - 1] : 0;
+    }
+    avail[0] = up; avail[1] = left; avail[2] = 1; avail[3] = up && left && ul;
+    int st = 0, sl = 0;
+    for (int i = 0; i < 16; i++) { st += T[i]; sl += L[i]; }
+    int dcv = (up && left) ? (st + sl + 16) >> 5 : up ? (st + 8) >> 4 : left ? (sl + 8) >> 4 : 128;
+    int ih = 0, iv = 0;
+    for (int i = 1; i <= 8; i++) {
+        ih += i * (T[7 + i] - (7 - i >= 0 ? T[7 - i] : P));
+        iv += i * (L[7 + i] - (7 - i >= 0 ? L[7 - i] : P));
+    }
+    int ib = (5 * ih + 32) >> 6, ic = (5 * iv + 32) >> 6, iaa = 16 * (L[15] + T[15]);
+    for (int y = 0; y < 16; y++)
+        for (int x = 0; x < 16; x++) {
+            int k = 16 * y + x;
+            pred[0][k] = (uint8_t)T[x];
+            pred[1][k] = (uint8_t)L[y];
+            pred[2][k] = (uint8_t)dcv;
+            pred[3][k] = (uint8_t)clip255((iaa + (x - 7) * ib + (y - 7) * ic + 16) >> 5);
+        }
+}
+
+/* IntraChromaPrediction8x8 [J] / 8.3.4 for one component; pred[4][64] */
+static void intra_chroma_pred(const mbs *s, int uv, uint8_t pred[4][64], int avail[4]) {
+    const jmo_ctx *c = s->c;
+    const uint8_t *R = uv ? c->recV : c->recU;
+    int W = c->Wc, ax = s->pix_x >> 1, ay = s->pix_y >> 1;
+    int up = mb_avail(s, 0, -1), left = mb_avail(s, -1, 0), ul = mb_avail(s, -1, -1);
+    int T[8], L[8], P = ul ? R[(ay - 1) * W + ax - 1] : 0;
+    for (int i = 0; i < 8; i++) {
+        T[i] = up ? R[(ay - 1) * W + ax + i] : 0;
+        L[i] = left ? R[(ay + i) * W + ax - 1] : 0;
+    }
+    avail[0] = 1; avail[1] = left; avail[2] = up; avail[3] = up && left && ul;
+    for (int b = 0; b < 4; b++) {          /* DC per 4x4 chroma block (8.3.4.1-3) */
+        int xo = (b & 1) * 4, yo = (b >> 1) * 4;
+        int s0 = 0, s1 = 0, s2 = 0, s3 = 0, sv = 128;
+        for (int i = 0; i < 4; i++) { s0 += T[i]; s1 += T[4 + i]; s2 += L[i]; s3 += L[4 + i]; }
+        if (b == 0) sv = (up && left) ? (s0 + s2 + 4) >> 3 : up ? (s0 + 2) >> 2 : left ? (s2 + 2) >> 2 : 128;
+        else if (b == 1) sv = up ? (s1 + 2) >> 2 : left ? (s2 + 2) >> 2 : 128;
+        else if (b == 2) sv = left ? (s3 + 2) >> 2 : up ? (s0 + 2) >> 2 : 128;
+        else sv = (up && left) ? (s1 + s3 + 4) >> 3 : up ? (s1 + 2) >> 2 : left ? (s3 + 2) >> 2 : 128;
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++) pred[0][(yo + y) * 8 + xo + x] = (uint8_t)sv;
+    }
+    int ih = 0, iv = 0;
+    for (int i = 1; i <= 4; i++) {
+        ih += i * (T[3 + i] - (3 - i >= 0 ? T[3 - i] : P));
+        iv += i * (L[3 + i] - (3 - i >= 0 ? L[3 - i] : P));
+    }
+    int ib = (34 * ih + 32) >> 6, ic = (34 * iv + 32) >> 6, iaa = 16 * (L[7] + T[7]);
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+            pred[1][y * 8 + x] = (uint8_t)L[y];
+            pred[2][y * 8 + x] = (uint8_t)T[x];
+            pred[3][y * 8 + x] = (uint8_t)clip255((iaa + (x - 3) * ib + (y - 3) * ic + 16) >> 5);
+        }
+}
+
+/* find_sad_16x16 [J]: Hadamard cost of the 4 Intra16x16 predictions */
+static int find_sad_16x16(const mbs *s, uint8_t pred[4][256], const int avail[4], int *mode) {
+    int best = MAX_VALUE;
+    *mode = 2;
+    for (int k = 0; k < 4; k++) {
+        if (!avail[k]) continue;
+        int cost = 0, dc[16];
+        for (int b = 0; b < 16; b++) {
+            int ox = (b & 3) * 4, oy = (b >> 2) * 4;
+            int m[16], t[16];
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++)
+                    m[4 * y + x] = s->org[(oy + y) * 16 + ox + x] - pred[k][(oy + y) * 16 + ox + x];
+            for (int y = 0; y < 4; y++) {
+                int *r = m + 4 * y;
+                int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
+                t[4 * y + 0] = a0 + a1; t[4 * y + 2] = a0 - a1; t[4 * y + 1] = a2 + a3; t[4 * y + 3] = a3 - a2;
+            }
+            for (int x = 0; x < 4; x++) {
+                int a0 = t[x] + t[12 + x], a1 = t[4 + x] + t[8 + x], a2 = t[4 + x] - t[8 + x], a3 = t[x] - t[12 + x];
+                m[x] = a0 + a1; m[8 + x] = a0 - a1; m[4 + x] = a2 + a3; m[12 + x] = a3 - a2;
+            }
+            for (int q = 1; q < 16; q++) cost += iabs(m[q]);
+            dc[b] = m[0] / 4;
+        }
+        int t[16];
+        for (int y = 0; y < 4; y++) {
+            int *r = dc + 4 * y;
+            int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
+            t[4 * y + 0] = a0 + a1; t[4 * y + 2] = a0 - a1; t[4 * y + 1] = a2 + a3; t[4 * y + 3] = a3 - a2;
+        }
+        for (int x = 0; x < 4; x++) {
+            int a0 = t[x] + t[12 + x], a1 = t[4 + x] + t[8 + x], a2 = t[4 + x] - t[8 + x], a3 = t[x] - t[12 + x];
+            cost += iabs(a0 + a1) + iabs(a0 - a1) + iabs(a2 + a3) + iabs(a3 - a2);
+        }
+        if (cost < best) { best = cost; *mode = k; }
+    }
+    return best / 2;
+}
+
+/* ====================================================================================== */
+/*  motion compensation                                                                    */
+/* ====================================================================================== */
+static void luma_pred_4x4(const mbs *s, int bx4, int by4, int mvx, int mvy, uint8_t *out, int os) {
+    for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++)
+            out[y * os + x] = (uint8_t)jmo_qpel_at(s->c, 4 * (s->pix_x + 4 * bx4 + x) + mvx,
+                                                  4 * (s->pix_y + 4 * by4 + y) + mvy);
+}
+/* OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2: pixel (i,j) uses the MV of luma 4x4 block
+ * (i>>1, j>>1) */
+static void chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], uint8_t pred[64]) {
+    const jmo_ctx *c = s->c;
+    const uint8_t *R = uv ? c->refV : c->refU;
+    int Wc = c->Wc, Hc = c->Hc;
+    for (int j = 0; j < 8; j++)
+        for (int i = 0; i < 8; i++) {
+            const int16_t *v = mv[(j >> 1) * 4 + (i >> 1)];
+            int ii = ((s->pix_x >> 1) + i) * 8 + v[0], jj = ((s->pix_y >> 1) + j) * 8 + v[1];
+            int x0 = iclip(0, Wc - 1, ii >> 3), y0 = iclip(0, Hc - 1, jj >> 3);
+            int x1 = iclip(0, Wc - 1, (ii + 7) >> 3), y1 = iclip(0, Hc - 1, (jj + 7) >> 3);
+            int fx = ii & 7, fy = jj & 7;
+            pred[j * 8 + i] = (uint8_t)(((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] +
+                                         (8 - fx) * fy * R[y1 * Wc + x0] + fx * fy * R[y1 * Wc + x1] + 32) >> 6);
+        }
+}
+
+/* ====================================================================================== */
+/*  encode_one_macroblock (RDO off)                                                         */
+/* ====================================================================================== */
+static void store_rec_luma(jmo_ctx *c, const mbs *s, const uint8_t rec[256]) {
+    for (int y = 0; y < 16; y++) memcpy(c->recY + (s->pix_y + y) * c->W + s->pix_x, rec + 16 * y, 16);
+}
+
+void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
+    mbs S;
+    mbs *s = &S;
+    memset(s, 0, sizeof(*s));
+    s->c = c; s->mbx = mbx; s->mby = mby; s->pix_x = 16 * mbx; s->pix_y = 16 * mby;
+    s->mb_addr = mby * c->mbw + mbx;
+    s->lambda = c->fp.lambda_motion;
+    s->lf = 65536 * s->lambda;
+    s->slice_p = c->fp.slice_type == JMH_P_SLICE;
+    int qp = c->fp.qp, lambda = c->fp.lambda_mode;
+    int intra_round = !s->slice_p;                 /* JM 8.6: qp_const by slice type [J] */
+    int W = c->W, W4 = W >> 2;
+    for (int y = 0; y < 16; y++) memcpy(s->org + 16 * y, c->orgY + (s->pix_y + y) * W + s->pix_x, 16);
+    for (int y = 0; y < 8; y++) {
+        memcpy(s->orgc[0] + 8 * y, c->orgU + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), 8);
+        memcpy(s->orgc[1] + 8 * y, c->orgV + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), 8);
+    }
+    jmh_mb_result *res = &c->res[s->mb_addr];
+    memset(res, 0, sizeof(*res));
+    const int *isr = c->cfg.inter_search;
+    int valid[9] = {0};
+    int intra_only = !s->slice_p;
+    for (int m = 1; m <= 7; m++) valid[m] = !intra_only && isr[m];
+    valid[8] = valid[4] || valid[5] || valid[6] || valid[7];
+
+    int min_cost = BIGCOST, best_mode = 1;
+    int best8x8mode[4] = {0, 0, 0, 0};
+    int W4i = W4;
+    (void)W4i;
+    if (!intra_only) {
+        /* ===== 16x16, 16x8, 8x16 ===== */
+        for (int mode = 1; mode < 4; mode++) {
+            if (!valid[mode]) continue;
+            int cost = 0;
+            for (int block = 0; block < (mode == 1 ? 1 : 2); block++) {
+                partition_motion_search(s, mode, block);
+                cost += s->motion_cost[mode][block];   /* + (int)(2*lambda*min(ref,1)) == 0 */
+            }
+            if (cost < min_cost) { best_mode = mode; min_cost = cost; }
+        }
+        /* ===== P8x8 ===== */
+        if (valid[8]) {
+            int cost8x8 = 0;
+            for (int block = 0; block < 4; block++) {
+                int min_cost8x8 = BIGCOST;
+                for (int mode = 4; mode <= 7; mode++) {
+                    if (!valid[mode]) continue;
+                    partition_motion_search(s, mode, block);
+                    int cost = s->motion_cost[mode][block];
+                    if (cost < min_cost8x8) { min_cost8x8 = cost; best8x8mode[block] = mode; }
+                }
+                cost8x8 += min_cost8x8;
+                /* reset stored motion vectors of this 8x8 to its best sub-mode */
+                int mode = best8x8mode[block];
+                if (mode > 0) write_enc_mv(s, (block & 1) * 2, (block >> 1) * 2, 2, 2, s->all_mv[mode]);
+            }
+            if (cost8x8 < min_cost) { best_mode = JMH_P8x8; min_cost = cost8x8; }
+        }
+        find_skip_mv(s);
+    }
+
+    /* ===== Intra 4x4 decision (with TQ + recon of every 4x4 in coding order) ===== */
+    uint8_t i4rec[256];
+    int16_t i4lev[16][16];
+    int i4modes[16];
+    int i4cbp = 0, i4cbpblk = 0, i4cost = 0;
+    {
+        int W4l = c->W >> 2;
+        /* save the recon area: Mode_Decision_for_Intra4x4Macroblock writes enc_picture */
+        for (int b8 = 0; b8 < 4; b8++) {
+            int cost8 = 6 * lambda;                         /* (int)floor(6*lambda+0.4999) */
+            for (int b4 = 0; b4 < 4; b4++) {
+                int bx = 8 * (b8 & 1) + 4 * (b4 & 1), by = 8 * (b8 >> 1) + 4 * (b4 >> 1);
+                int blk = (by >> 2) * 4 + (bx >> 2);
+                int ia = 0, ib = 0;
+                int av_l = nb4(s, bx - 1, by, &ia), av_u = nb4(s, bx, by - 1, &ib);
+                int upMode = av_u ? c->ipred[ib] : -1, leftMode = av_l ? c->ipred[ia] : -1;
+                int mpm = (upMode < 0 || leftMode < 0) ? 2 : imin(upMode, leftMode);
+                uint8_t pred[9][16];
+                int avail[9];
+                intra4x4_pred(s, bx, by, pred, avail);
+                int best = 0, bcost = BIGCOST;
+                for (int m = 0; m < 9; m++) {
+                    if (!avail[m]) continue;
+                    int32_t d[16];
+                    for (int y = 0; y < 4; y++)
+                        for (int x = 0; x < 4; x++)
+                            d[4 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[m][4 * y + x];
+                    int cost = (m == mpm) ? 0 : 4 * lambda;      /* (int)floor(4*lambda) */
+                    cost += jmo_satd_block(d, c->cfg.use_hadamard);
+                    if (cost < bcost) { best = m; bcost = cost; }
+                }
+                c->ipred[((s->pix_y + by) >> 2) * W4l + ((s->pix_x + bx) >> 2)] = (int8_t)best;
+                i4modes[blk] = best;
+                int32_t r[16];
+                for (int y = 0; y < 4; y++)
+                    for (int x = 0; x < 4; x++)
+                        r[4 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[best][4 * y + x];
+                int dummy = 0;
+                uint8_t *dst = c->recY + (s->pix_y + by) * c->W + s->pix_x + bx;
+                if (dct_luma4x4(r, pred[best], 4, qp, intra_round, i4lev[blk], &dummy, dst, c->W)) {
+                    i4cbp |= 1 << b8;
+                    i4cbpblk |= 1 << blk;
+                }
+                cost8 += bcost;
+            }
+            i4cost += cost8;
+        }
+        for (int y = 0; y < 16; y++) memcpy(i4rec + 16 * y, c->recY + (s->pix_y + y) * c->W + s->pix_x, 16);
+    }
+    if (i4cost <= min_cost) { min_cost = i4cost; best_mode = JMH_I4MB; }
+    /* ===== Intra 16x16 ===== */
+    uint8_t i16pred[4][256];
+    int i16avail[4], i16mode = 2;
+    intra16_pred(s, i16pred, i16avail);
+    int i16cost = find_sad_16x16(s, i16pred, i16avail, &i16mode);
+    if (i16cost < min_cost) { min_cost = i16cost; best_mode = JMH_I16MB; }
+
+    /* ===== final macroblock parameters ===== */
+    int is_intra = best_mode == JMH_I4MB || best_mode == JMH_I16MB;
+    int16_t fmv[16][2];
+    memset(fmv, 0, sizeof(fmv));
+    int b8mode[4];
+    for (int b = 0; b < 4; b++) b8mode[b] = best_mode == JMH_P8x8 ? best8x8mode[b] : best_mode;
+    if (best_mode == JMH_I4MB) for (int b = 0; b < 4; b++) b8mode[b] = JMH_IBLOCK;
+    if (best_mode == JMH_I16MB) for (int b = 0; b < 4; b++) b8mode[b] = 0;
+    if (!is_intra)
+        for (int k = 0; k < 16; k++) {
+            int b8 = ((k >> 3) << 1) + ((k & 3) >> 1);
+            fmv[k][0] = s->all_mv[b8mode[b8]][k][0];
+            fmv[k][1] = s->all_mv[b8mode[b8]][k][1];
+        }
+    int cbp = 0, cbp_blk = 0;
+    uint8_t rec[256];
+    if (best_mode == JMH_I4MB) {
+        cbp = i4cbp; cbp_blk = i4cbpblk;
+        memcpy(rec, i4rec, 256);
+        for (int k = 0; k < 16; k++) { res->ipred[k] = (int8_t)i4modes[k]; memcpy(res->luma[k], i4lev[k], 32); }
+    } else if (best_mode == JMH_I16MB) {
+        int32_t r[256];
+        for (int k = 0; k < 256; k++) r[k] = s->org[k] - i16pred[i16mode][k];
+        cbp = dct_luma_16x16(r, i16pred[i16mode], qp, res->luma_dc, res->luma, &cbp_blk, rec);
+        res->i16mode = (int8_t)i16mode;
+    } else {
+        /* LumaResidualCoding / LumaResidualCoding8x8 (also SetCoeffAndReconstruction8x8) */
+        uint8_t pred[256];
+        int sum_cnt_nonz = 0;
+        for (int b8 = 0; b8 < 4; b8++) {
+            int coeff_cost = 0, cbp8 = 0, blk8 = 0;
+            for (int b4 = 0; b4 < 4; b4++) {
+                int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1);
+                int k = by4 * 4 + bx4;
+                luma_pred_4x4(s, bx4, by4, fmv[k][0], fmv[k][1], pred + 4 * by4 * 16 + 4 * bx4, 16);
+                int32_t r[16];
+                for (int y = 0; y < 4; y++)
+                    for (int x = 0; x < 4; x++)
+                        r[4 * y + x] = s->org[(4 * by4 + y) * 16 + 4 * bx4 + x] - pred[(4 * by4 + y) * 16 + 4 * bx4 + x];
+                if (dct_luma4x4(r, pred + 4 * by4 * 16 + 4 * bx4, 16, qp, intra_round, res->luma[k], &coeff_cost,
+                                rec + 4 * by4 * 16 + 4 * bx4, 16)) {
+                    blk8 |= 1 << k;
+                    cbp8 = 1;
+                }
+            }
+            if (coeff_cost <= LUMA_COEFF_COST) {          /* discard "expensive" single coeffs */
+                coeff_cost = 0;
+                cbp8 = 0; blk8 = 0;
+                for (int b4 = 0; b4 < 4; b4++) {
+                    int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1);
+                    memset(res->luma[by4 * 4 + bx4], 0, 32);
+                    for (int y = 0; y < 4; y++)
+                        memcpy(rec + (4 * by4 + y) * 16 + 4 * bx4, pred + (4 * by4 + y) * 16 + 4 * bx4, 4);
+                }
+            }
+            if (cbp8) cbp |= 1 << b8;
+            cbp_blk |= blk8;
+            sum_cnt_nonz += coeff_cost;
+        }
+        if (sum_cnt_nonz <= LUMA_MB_COEFF_COST) {
+            cbp = 0; cbp_blk = 0;
+            memset(res->luma, 0, sizeof(res->luma));
+            memcpy(rec, pred, 256);
+        }
+    }
+    store_rec_luma(c, s, rec);
+
+    /* ===== chroma: IntraChromaPrediction8x8 (intra MBs) + ChromaResidualCoding ===== */
+    int c_mode = 0;
+    uint8_t cpred[2][4][64];
+    if (is_intra) {
+        int cav[4];
+        intra_chroma_pred(s, 0, cpred[0], cav);
+        intra_chroma_pred(s, 1, cpred[1], cav);
+        int min_c = BIGCOST;
+        for (int m = 0; m < 4; m++) {                 /* DC, H, V, Plane */
+            if (!cav[m]) continue;
+            int cost = 0;
+            for (int uv = 0; uv < 2; uv++)
+                for (int b = 0; b < 4; b++) {
+                    int32_t d[16];
+                    int xo = (b & 1) * 4, yo = (b >> 1) * 4;
+                    for (int y = 0; y < 4; y++)
+                        for (int x = 0; x < 4; x++)
+                            d[4 * y + x] = s->orgc[uv][(yo + y) * 8 + xo + x] - cpred[uv][m][(yo + y) * 8 + xo + x];
+                    cost += jmo_satd_block(d, c->cfg.use_hadamard);
+                }
+            if (cost < min_c) { min_c = cost; c_mode = m; }
+        }
+    }
+    int qpc = jmo_qp_scale_cr(qp + c->fp.chroma_qp_offset);
+    int cr_cbp = 0;
+    for (int uv = 0; uv < 2; uv++) {
+        uint8_t pred[64], crec[64];
+        if (is_intra) memcpy(pred, cpred[uv][c_mode], 64);
+        else chroma_pred_mb(s, uv, fmv, pred);
+        int32_t r[64];
+        for (int k = 0; k < 64; k++) r[k] = s->orgc[uv][k] - pred[k];
+        cr_cbp = dct_chroma(r, pred, qpc, intra_round, cr_cbp, res->chroma_dc[uv], res->chroma_ac[uv], crec);
+        uint8_t *R = uv ? c->recV : c->recU;
+        for (int y = 0; y < 8; y++) memcpy(R + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), crec + 8 * y, 8);
+    }
+    cbp |= cr_cbp << 4;
+
+    /* ===== results, picture arrays, P_Skip detection ===== */
+    int mb_type = best_mode;
+    if (s->slice_p && best_mode == 1 && cbp == 0 && fmv[0][0] == s->skip_mv[0] && fmv[0][1] == s->skip_mv[1])
+        mb_type = JMH_PSKIP;
+    res->mb_type = (int16_t)mb_type;
+    res->cbp = (int16_t)cbp;
+    res->cbp_blk = cbp_blk;
+    res->c_ipred_mode = (int8_t)(is_intra ? c_mode : 0);
+    res->min_cost = min_cost;
+    for (int b = 0; b < 4; b++) {
+        res->b8mode[b] = (int8_t)(mb_type == JMH_PSKIP ? 0 : b8mode[b]);
+        res->ref_idx[b] = (int8_t)(is_intra ? -1 : 0);
+    }
+    memcpy(res->mv, fmv, sizeof(fmv));
+    for (int k = 0; k < 16; k++) {
+        int a = ((s->pix_y >> 2) + (k >> 2)) * W4 + (s->pix_x >> 2) + (k & 3);
+        c->mv[2 * a] = fmv[k][0];
+        c->mv[2 * a + 1] = fmv[k][1];
+        c->refidx[a] = (int8_t)(is_intra ? -1 : 0);
+        if (best_mode != JMH_I4MB) { c->ipred[a] = 2; res->ipred[k] = 2; }
+    }
+    c->mbintra[s->mb_addr] = (int8_t)is_intra;
+}

@@ -1,0 +1,152 @@
+/*
+ * frame.c — oracle picture driver (TEST INFRASTRUCTURE ONLY).
+ * Restates JM 8.6 image.c › code_a_picture / slice.c › encode_one_slice's macroblock loop
+ * (one slice, raster order) around encode_one_macroblock, and exposes the unit seams that
+ * tests compare the GPU path against.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include "jmo_internal.h"
+
+static int cfg_ok(const jmh_config *cfg) {
+    if (!cfg || cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 15) || (cfg->height & 15))
+        return JMH_E_INVALID_ARG;
+    if (cfg->search_range < 1 || cfg->search_range > JMO_MAX_SR) return JMH_E_INVALID_ARG;
+    if (cfg->search_mode != 0 && cfg->search_mode != -1) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred != 0) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
+    return JMH_OK;
+}
+
+int jmo_create(const jmh_config *cfg, jmo_ctx **out) {
+    int st = cfg_ok(cfg);
+    if (st) return st;
+    jmo_ctx *c = (jmo_ctx *)calloc(1, sizeof(jmo_ctx));
+    if (!c) return JMH_E_OOM;
+    c->cfg = *cfg;
+    c->W = cfg->width; c->H = cfg->height; c->Wc = c->W / 2; c->Hc = c->H / 2;
+    c->mbw = c->W / 16; c->mbh = c->H / 16;
+    c->sr = cfg->search_range;
+    c->npos = (2 * c->sr + 1) * (2 * c->sr + 1);
+    jmo_init_spiral(c);
+    size_t ls = (size_t)c->W * c->H, cs = (size_t)c->Wc * c->Hc, n4 = ls / 16;
+    c->orgY = malloc(ls); c->orgU = malloc(cs); c->orgV = malloc(cs);
+    c->refY = malloc(ls); c->refU = malloc(cs); c->refV = malloc(cs);
+    c->recY = calloc(ls, 1); c->recU = calloc(cs, 1); c->recV = calloc(cs, 1);
+    c->qstride = c->W + 2 * JMO_PAD;
+    c->qplane = c->qstride * (c->H + 2 * JMO_PAD);
+    c->qpel = malloc((size_t)16 * c->qplane);
+    c->mv = calloc(2 * n4, sizeof(int16_t));
+    c->refidx = calloc(n4, 1);
+    c->ipred = calloc(n4, 1);
+    c->mbintra = calloc((size_t)c->mbw * c->mbh, 1);
+    c->res = calloc((size_t)c->mbw * c->mbh, sizeof(jmh_mb_result));
+    c->blocksad = malloc(sizeof(uint16_t) * 16 * (size_t)c->npos);
+    if (!c->orgY || !c->qpel || !c->res || !c->blocksad) { jmo_destroy(c); return JMH_E_OOM; }
+    *out = c;
+    return JMH_OK;
+}
+
+void jmo_destroy(jmo_ctx *c) {
+    if (!c) return;
+    free(c->spiral_x); free(c->spiral_y); free(c->spiral_of);
+    free(c->orgY); free(c->orgU); free(c->orgV);
+    free(c->refY); free(c->refU); free(c->refV);
+    free(c->recY); free(c->recU); free(c->recV);
+    free(c->qpel); free(c->mv); free(c->refidx); free(c->ipred); free(c->mbintra);
+    free(c->res); free(c->blocksad);
+    free(c);
+}
+
+static void copy_plane(uint8_t *dst, int dw, int dh, const uint8_t *src, int stride) {
+    for (int y = 0; y < dh; y++) memcpy(dst + (size_t)y * dw, src + (size_t)y * stride, dw);
+}
+
+int jmo_set_reference(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                      int stride_y, int stride_c) {
+    if (!c || !y || !u || !v) return JMH_E_INVALID_ARG;
+    copy_plane(c->refY, c->W, c->H, y, stride_y);
+    copy_plane(c->refU, c->Wc, c->Hc, u, stride_c);
+    copy_plane(c->refV, c->Wc, c->Hc, v, stride_c);
+    jmo_build_qpel(c);
+    c->have_ref = 1;
+    return JMH_OK;
+}
+
+int jmo_load_current(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                     int stride_y, int stride_c) {
+    if (!c || !y || !u || !v) return JMH_E_INVALID_ARG;
+    copy_plane(c->orgY, c->W, c->H, y, stride_y);
+    copy_plane(c->orgU, c->Wc, c->Hc, u, stride_c);
+    copy_plane(c->orgV, c->Wc, c->Hc, v, stride_c);
+    return JMH_OK;
+}
+
+int jmo_encode_frame(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                     int stride_y, int stride_c, const jmh_frame_params *fp) {
+    if (!c || !y || !u || !v || !fp) return JMH_E_INVALID_ARG;
+    if (fp->slice_type != JMH_P_SLICE && fp->slice_type != JMH_I_SLICE) return JMH_E_UNSUPPORTED_CFG;
+    if (fp->slice_type == JMH_P_SLICE && !c->have_ref) return JMH_E_STATE;
+    if (fp->qp < 0 || fp->qp > 51) return JMH_E_INVALID_ARG;
+    c->fp = *fp;
+    copy_plane(c->orgY, c->W, c->H, y, stride_y);
+    copy_plane(c->orgU, c->Wc, c->Hc, u, stride_c);
+    copy_plane(c->orgV, c->Wc, c->Hc, v, stride_c);
+    size_t n4 = (size_t)c->W * c->H / 16;
+    memset(c->mv, 0, 2 * n4 * sizeof(int16_t));
+    memset(c->refidx, -1, n4);
+    memset(c->ipred, 2, n4);
+    for (int my = 0; my < c->mbh; my++)
+        for (int mx = 0; mx < c->mbw; mx++) jmo_encode_mb(c, mx, my);
+    return JMH_OK;
+}
+
+const jmh_mb_result *jmo_mb_result(const jmo_ctx *c, int mb_addr) {
+    if (!c || mb_addr < 0 || mb_addr >= c->mbw * c->mbh) return NULL;
+    return &c->res[mb_addr];
+}
+
+int jmo_read_recon(const jmo_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y, int stride_c) {
+    if (!c) return JMH_E_INVALID_ARG;
+    for (int r = 0; r < c->H; r++) memcpy(y + (size_t)r * stride_y, c->recY + (size_t)r * c->W, c->W);
+    for (int r = 0; r < c->Hc; r++) {
+        memcpy(u + (size_t)r * stride_c, c->recU + (size_t)r * c->Wc, c->Wc);
+        memcpy(v + (size_t)r * stride_c, c->recV + (size_t)r * c->Wc, c->Wc);
+    }
+    return JMH_OK;
+}
+
+int jmo_read_qpel(const jmo_ctx *c, uint8_t *out) {
+    if (!c || !c->have_ref) return JMH_E_STATE;
+    memcpy(out, c->qpel, (size_t)16 * c->qplane);
+    return JMH_OK;
+}
+
+/* SetupFastFullPelSearch's 4x4 SAD table for explicit window centres (unit seam) */
+int jmo_ffs_sad_table(jmo_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t *centres,
+                      uint16_t *out) {
+    if (!c || n_mb < 0) return JMH_E_INVALID_ARG;
+    int sr = c->sr, side = 2 * sr + 1;
+    for (int i = 0; i < n_mb; i++) {
+        int px = 16 * mb_xy[2 * i], py = 16 * mb_xy[2 * i + 1];
+        if (mb_xy[2 * i] < 0 || mb_xy[2 * i] >= c->mbw || mb_xy[2 * i + 1] < 0 || mb_xy[2 * i + 1] >= c->mbh)
+            return JMH_E_INVALID_ARG;
+        int cx = centres[2 * i], cy = centres[2 * i + 1];
+        uint16_t *o = out + (size_t)i * 16 * c->npos;
+        for (int dy = -sr; dy <= sr; dy++)
+            for (int dx = -sr; dx <= sr; dx++) {
+                int r = (dy + sr) * side + dx + sr;
+                for (int b = 0; b < 16; b++) {
+                    int ox = (b & 3) * 4, oy = (b >> 2) * 4, sad = 0;
+                    for (int y = 0; y < 4; y++)
+                        for (int x = 0; x < 4; x++) {
+                            int ax = iclip(0, c->W - 1, px + cx + dx + ox + x);
+                            int ay = iclip(0, c->H - 1, py + cy + dy + oy + y);
+                            sad += iabs(c->orgY[(py + oy + y) * c->W + px + ox + x] - c->refY[ay * c->W + ax]);
+                        }
+                    o[(size_t)b * c->npos + r] = (uint16_t)sad;
+                }
+            }
+    }
+    return JMH_OK;
+}

@@ -1,0 +1,81 @@
+/*
+ * jm_oracle.h — CPU restatement of the JM lencod hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * This directory is the oracle: plain C, written from the ITU-T H.264 normative clauses and
+ * from JM 8.6 lencod's non-normative encoder semantics (docs/JM_SEMANTICS.md).  It is used
+ * only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker and
+ * the CPU baseline.  The product (h264-jm-commentary_amd/) never links or calls it.
+ *
+ * PARITY STATUS: the mounted reference holds only README.md:1-4 (no JM source, no tests, no
+ * fixtures, no binary), so parity of this restatement with JM's own output is UNPINNED.
+ * What IS pinned: (1) the normative parts by spec known-answer tests and by the independent
+ * closed-loop decoder in oracle/decoder.c (decoder output == encoder recon, byte for byte);
+ * (2) the GPU path by bit-exact equality with this oracle.  Every JM function restated here is
+ * cited as "JM 8.6 <file> › <function> [J]"; no file:line exists.
+ */
+#ifndef JM_ORACLE_H
+#define JM_ORACLE_H
+
+#include <stdint.h>
+#include "../include/jmhip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JMO_PAD 4            /* qpel-plane padding (JM IMG_PAD_SIZE [J]); >= 3 makes UMV
+                                clamping identical to the spec's coordinate clamping       */
+#define JMO_MAX_SR 64
+
+typedef struct jmo_ctx jmo_ctx;
+
+/* ---- backend API (mirrors jmh_*) ----------------------------------------------------- */
+int  jmo_create(const jmh_config *cfg, jmo_ctx **out);
+void jmo_destroy(jmo_ctx *c);
+int  jmo_set_reference(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                       int stride_y, int stride_c);
+int  jmo_encode_frame(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                      int stride_y, int stride_c, const jmh_frame_params *fp);
+const jmh_mb_result *jmo_mb_result(const jmo_ctx *c, int mb_addr);
+int  jmo_read_recon(const jmo_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y,
+                    int stride_c);
+/* copy the 16 quarter-pel phase planes: out[16][(H+2P)][(W+2P)], phase = 4*yfrac + xfrac  */
+int  jmo_read_qpel(const jmo_ctx *c, uint8_t *out);
+/* load the current picture without encoding (for jmo_ffs_sad_table)                       */
+int  jmo_load_current(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                      int stride_y, int stride_c);
+
+/* ---- unit entry points (known-answer + GPU unit parity) ------------------------------ */
+int  jmo_ffs_sad_table(jmo_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t *centres,
+                       uint16_t *out);
+int  jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,
+                     int16_t *levels, uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero);
+/* spec luma sample at quarter-pel position (X,Y) of an integer plane (clamped coords)   */
+int  jmo_luma_qpel_sample(const uint8_t *p, int w, int h, int stride, int X, int Y);
+void jmo_spiral(int range, int32_t *sx, int32_t *sy);           /* (2R+1)^2 entries       */
+int  jmo_mvbits(int v);
+int  jmo_satd4x4(const int32_t *diff, int use_hadamard);
+void jmo_forward4x4(const int32_t *in, int32_t *out);             /* raster in/out         */
+void jmo_inverse4x4(const int32_t *in, int32_t *out);             /* no rounding shift     */
+int  jmo_qp2quant(int qp);
+int  jmo_qp_scale_cr(int qp);
+/* median MV predictor of the spec on explicit neighbours (unit tests)                     */
+void jmo_mvp_median(int avail_a, int ref_a, int mva_x, int mva_y,
+                    int avail_b, int ref_b, int mvb_x, int mvb_y,
+                    int avail_c, int ref_c, int mvc_x, int mvc_y,
+                    int ref, int bsx, int bsy, int blk_x, int blk_y, int32_t *pmv);
+
+/* ---- closed-loop decoder (Baseline CAVLC subset emitted by the host encoder) --------- */
+typedef struct jmo_dec jmo_dec;
+int  jmo_dec_create(jmo_dec **out);
+void jmo_dec_destroy(jmo_dec *d);
+/* decode a whole Annex-B stream; frames are appended to out (cropped 4:2:0 I420), returns
+ * number of frames decoded or a negative error.  out_cap in bytes.                        */
+int  jmo_decode_annexb(jmo_dec *d, const uint8_t *buf, long len, uint8_t *out, long out_cap,
+                       int *width, int *height);
+const char *jmo_dec_error(const jmo_dec *d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

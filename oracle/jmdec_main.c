@@ -1,0 +1,29 @@
+/* jmdec_main.c — closed-loop decoder CLI (TEST INFRASTRUCTURE ONLY): jmdec in.264 out.yuv */
+#include <stdio.h>
+#include <stdlib.h>
+#include "jm_oracle.h"
+
+int main(int argc, char **argv) {
+    if (argc < 3) { fprintf(stderr, "usage: jmdec in.264 out.yuv\n"); return 1; }
+    FILE *f = fopen(argv[1], "rb");
+    if (!f) { perror(argv[1]); return 1; }
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    unsigned char *buf = malloc(n);
+    if (fread(buf, 1, n, f) != (size_t)n) return 1;
+    fclose(f);
+    long cap = 64L * 1024 * 1024 * 16;
+    unsigned char *out = malloc(cap);
+    jmo_dec *d;
+    jmo_dec_create(&d);
+    int w = 0, h = 0;
+    int frames = jmo_decode_annexb(d, buf, n, out, cap, &w, &h);
+    if (frames < 0) { fprintf(stderr, "decode error: %s\n", jmo_dec_error(d)); return 2; }
+    FILE *o = fopen(argv[2], "wb");
+    fwrite(out, 1, (size_t)frames * w * h * 3 / 2, o);
+    fclose(o);
+    printf("decoded %d frames %dx%d\n", frames, w, h);
+    jmo_dec_destroy(d);
+    return 0;
+}

@@ -1,0 +1,74 @@
+/* jmo_internal.h — oracle internals (TEST INFRASTRUCTURE ONLY; see jm_oracle.h header). */
+#ifndef JMO_INTERNAL_H
+#define JMO_INTERNAL_H
+
+#include <stdint.h>
+#include <string.h>
+#include "jm_oracle.h"
+
+#define MAX_VALUE 999999          /* JM 8.6 defines.h MAX_VALUE [J]                       */
+#define Q_BITS 15                 /* JM 8.6 defines.h Q_BITS [J]                          */
+#define DQ_BITS 6
+#define DQ_ROUND 32
+#define LUMA_COEFF_COST 4         /* _LUMA_COEFF_COST_    (8x8 block, "<=") [J]            */
+#define LUMA_MB_COEFF_COST 5      /* sum_cnt_nonz "<= 5" in LumaResidualCoding [J]         */
+#define CHROMA_COEFF_COST 4       /* _CHROMA_COEFF_COST_  ("<") [J]                         */
+#define SHIFT_QP 12
+#define BIGCOST (1 << 20)         /* JM max_value / min_cost initialisers [J]              */
+
+extern const int jmo_quant_coef[6][16];    /* raster [y*4+x] */
+extern const int jmo_dequant_coef[6][16];
+extern const int jmo_scan4x4[16];          /* zig-zag frame scan -> raster index */
+extern const int jmo_qp2quant_tab[40];
+extern const int jmo_qp_scale_cr_tab[52];
+extern const int jmo_coeff_cost_tab[16];
+extern const int jmo_blc_size[8][2];       /* JM input->blc_size [J]: {w,h} per blocktype */
+
+static inline int iabs(int a) { return a < 0 ? -a : a; }
+static inline int imin(int a, int b) { return a < b ? a : b; }
+static inline int imax(int a, int b) { return a > b ? a : b; }
+static inline int iclip(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+static inline int clip255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+static inline int isign(int a, int b) { return b < 0 ? -iabs(a) : iabs(a); } /* JM sign(a,b) */
+
+/* ---- encoder state (replaces JM's img/enc_picture globals for the hot path) ------------ */
+struct jmo_ctx {
+    jmh_config cfg;
+    int W, H, Wc, Hc, mbw, mbh;
+    int sr;                          /* max search range                                       */
+    int npos;                        /* (2sr+1)^2                                              */
+    int32_t *spiral_x, *spiral_y;    /* JM spiral_search_x/y [J]                               */
+    int32_t *spiral_of;              /* window raster (dy+sr)*(2sr+1)+(dx+sr) -> spiral index   */
+    /* current picture (coded size) */
+    uint8_t *orgY, *orgU, *orgV;
+    /* reference: integer planes + 16 quarter-pel phase planes (padded by JMO_PAD) */
+    uint8_t *refY, *refU, *refV;
+    uint8_t *qpel;                   /* [16][H+2P][W+2P]                                        */
+    int qstride, qplane;
+    int have_ref;
+    /* unfiltered reconstruction (enc_picture->imgY / imgUV) */
+    uint8_t *recY, *recU, *recV;
+    /* per-4x4 picture arrays (enc_picture->mv / ref_idx, img->ipredmode) */
+    int16_t *mv;                     /* [(H/4)*(W/4)][2] */
+    int8_t *refidx;                  /* [(H/4)*(W/4)]    */
+    int8_t *ipred;                   /* [(H/4)*(W/4)]    */
+    int8_t *mbintra;                 /* per MB: 1 if intra                                      */
+    jmh_mb_result *res;
+    jmh_frame_params fp;
+    /* per-MB scratch */
+    uint16_t *blocksad;              /* [16][npos] 4x4 SADs (window raster order)               */
+};
+
+/* common.c */
+void jmo_init_spiral(jmo_ctx *c);
+void jmo_build_qpel(jmo_ctx *c);
+int  jmo_qpel_at(const jmo_ctx *c, int X, int Y);   /* from the phase planes (clamped)   */
+int  jmo_satd_block(const int32_t d[16], int use_hadamard);
+void jmo_fwd4x4(int32_t m[16]);                       /* in-place, raster                 */
+void jmo_inv4x4_add(const int32_t m[16], const uint8_t *pred, int pstride, uint8_t *out,
+                    int ostride);
+
+/* encode.c */
+void jmo_encode_mb(jmo_ctx *c, int mbx, int mby);
+
+#endif
