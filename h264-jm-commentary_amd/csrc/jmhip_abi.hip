@@ -1,0 +1,407 @@
+// jmhip_abi.hip — the extern "C" boundary (include/jmhip.h) over the gfx950 kernels.
+// One context = one HIP device + one HIP stream; device buffers are sized once at create.
+// Per picture: H2D of the source (pinned staging) -> 254 wavefront launches at 1080p (one per
+// diagonal mbx + 2*mby) -> D2H of the macroblock results and the unfiltered reconstruction.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include "jmh_device.h"
+
+hipError_t jmh_launch_interp(const uint8_t *ref, int W, int H, uint8_t *qpel, int qstride, int qplane, hipStream_t st);
+hipError_t jmh_launch_mb(const DevParams &p, int nblocks, hipStream_t st);
+hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
+                                const int32_t *centres, uint16_t *out, hipStream_t st);
+hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
+                            int32_t *cc, int32_t *nz, hipStream_t st);
+
+// ring of begin/end event pairs; completed pairs are folded into `sum` (ms)
+#define EV_RING 64
+struct EvRing {
+    hipEvent_t a[EV_RING], b[EV_RING];
+    int head, count, n;
+    float sum;
+};
+static int ring_init(EvRing &r) {
+    memset(&r, 0, sizeof(r));
+    for (int i = 0; i < EV_RING; i++)
+        if (hipEventCreate(&r.a[i]) != hipSuccess || hipEventCreate(&r.b[i]) != hipSuccess) return -1;
+    return 0;
+}
+static void ring_free(EvRing &r) {
+    for (int i = 0; i < EV_RING; i++) {
+        if (r.a[i]) (void)hipEventDestroy(r.a[i]);
+        if (r.b[i]) (void)hipEventDestroy(r.b[i]);
+    }
+}
+static void ring_fold_oldest(EvRing &r) {
+    int i = (r.head - r.count + EV_RING) % EV_RING;
+    float ms = 0;
+    if (hipEventSynchronize(r.b[i]) == hipSuccess && hipEventElapsedTime(&ms, r.a[i], r.b[i]) == hipSuccess) {
+        r.sum += ms;
+        r.n++;
+    }
+    r.count--;
+}
+static hipError_t ring_begin(EvRing &r, hipStream_t st) {
+    if (r.count == EV_RING) ring_fold_oldest(r);
+    return hipEventRecord(r.a[r.head], st);
+}
+static hipError_t ring_end(EvRing &r, hipStream_t st) {
+    hipError_t e = hipEventRecord(r.b[r.head], st);
+    r.head = (r.head + 1) % EV_RING;
+    r.count++;
+    return e;
+}
+static void ring_drain(EvRing &r, float &sum, int &n) {
+    while (r.count) ring_fold_oldest(r);
+    sum = r.sum; n = r.n;
+    r.sum = 0; r.n = 0;
+}
+
+struct jmh_ctx {
+    jmh_config cfg;
+    int dev;
+    hipStream_t st;
+    int W, H, Wc, Hc, mbw, mbh, sr, side, npos, qstride, qplane;
+    size_t fsize;                        // bytes of one 4:2:0 picture (Y then U then V)
+    uint8_t *d_cur, *d_ref, *d_qpel, *d_rec, *d_slots;
+    int nslots;
+    int16_t *d_mv;
+    int8_t *d_refidx, *d_ipred;
+    jmh_mb_result *d_res;
+    int16_t *d_spiral, *d_spiral_of;
+    jmh_mb_result *h_res;
+    uint8_t *h_rec, *h_stage_cur, *h_stage_ref;
+    int have_ref, pending, have_results;
+    hipEvent_t ev_t0, ev_t1;
+    EvRing ring_interp, ring_mb;
+    jmh_timing timing;
+    std::vector<int> dcount, dymin;
+};
+
+#define HCHK(x)                                                                  \
+    do {                                                                         \
+        hipError_t e_ = (x);                                                     \
+        if (e_ != hipSuccess) {                                                  \
+            fprintf(stderr, "jmhip: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return JMH_E_HIP;                                                    \
+        }                                                                        \
+    } while (0)
+
+extern "C" {
+
+int jmh_abi_version(void) { return JMH_ABI_VERSION; }
+
+const char *jmh_strerror(int s) {
+    switch (s) {
+    case JMH_OK: return "ok";
+    case JMH_E_INVALID_ARG: return "invalid argument";
+    case JMH_E_HIP: return "HIP runtime error";
+    case JMH_E_OOM: return "out of memory";
+    case JMH_E_UNSUPPORTED_CFG: return "unsupported configuration";
+    case JMH_E_STATE: return "invalid call order";
+    case JMH_E_NO_DEVICE: return "no HIP device";
+    }
+    return "unknown status";
+}
+
+int jmh_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static void spiral(int range, std::vector<int16_t> &xy) {   // Init_Motion_Search_Module [J]
+    xy.assign(2, 0);
+    for (int l = 1; l <= range; l++) {
+        for (int i = -l + 1; i < l; i++) { xy.push_back(i); xy.push_back(-l); xy.push_back(i); xy.push_back(l); }
+        for (int i = -l; i <= l; i++) { xy.push_back(-l); xy.push_back(i); xy.push_back(l); xy.push_back(i); }
+    }
+}
+
+void jmh_destroy(jmh_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->dev);
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    void *dev_bufs[] = {c->d_cur, c->d_ref, c->d_qpel, c->d_rec, c->d_slots, c->d_mv, c->d_refidx,
+                        c->d_ipred, c->d_res, c->d_spiral, c->d_spiral_of};
+    for (void *p : dev_bufs) if (p) (void)hipFree(p);
+    void *host_bufs[] = {c->h_res, c->h_rec, c->h_stage_cur, c->h_stage_ref};
+    for (void *p : host_bufs) if (p) (void)hipHostFree(p);
+    if (c->ev_t0) (void)hipEventDestroy(c->ev_t0);
+    if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
+    ring_free(c->ring_interp);
+    ring_free(c->ring_mb);
+    if (c->st) (void)hipStreamDestroy(c->st);
+    delete c;
+}
+
+int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
+    if (!cfg || !out) return JMH_E_INVALID_ARG;
+    *out = nullptr;
+    if (cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 15) || (cfg->height & 15)) return JMH_E_INVALID_ARG;
+    if (cfg->search_range < 1 || cfg->search_range > 64) return JMH_E_INVALID_ARG;
+    if (cfg->search_range > SRMAX) return JMH_E_UNSUPPORTED_CFG;            // LDS-resident window
+    if (cfg->search_mode != 0) return JMH_E_UNSUPPORTED_CFG;                // FFS (SearchMode 0)
+    if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
+    int ndev = jmh_device_count();
+    if (ndev <= 0) return JMH_E_NO_DEVICE;
+    if (hip_device < 0 || hip_device >= ndev) return JMH_E_INVALID_ARG;
+    jmh_ctx *c = new jmh_ctx();
+    memset((void *)&c->cfg, 0, sizeof(c->cfg));
+    c->cfg = *cfg;
+    c->dev = hip_device;
+    HCHK(hipSetDevice(hip_device));
+    c->W = cfg->width; c->H = cfg->height; c->Wc = c->W / 2; c->Hc = c->H / 2;
+    c->mbw = c->W / 16; c->mbh = c->H / 16;
+    c->sr = cfg->search_range; c->side = 2 * c->sr + 1; c->npos = c->side * c->side;
+    c->qstride = c->W + 2 * QPAD; c->qplane = c->qstride * (c->H + 2 * QPAD);
+    c->fsize = (size_t)c->W * c->H * 3 / 2;
+    c->nslots = cfg->num_frame_slots > 0 ? cfg->num_frame_slots : 1;
+    int st = JMH_OK;
+#define ALLOC(p, n) do { if (hipMalloc((void **)&(p), (n)) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
+#define HALLOC(p, n) do { if (hipHostMalloc((void **)&(p), (n), hipHostMallocDefault) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
+    {
+        if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        size_t n4 = (size_t)c->W * c->H / 16, nmb = (size_t)c->mbw * c->mbh;
+        ALLOC(c->d_cur, c->fsize); ALLOC(c->d_ref, c->fsize); ALLOC(c->d_rec, c->fsize);
+        ALLOC(c->d_qpel, (size_t)16 * c->qplane);
+        ALLOC(c->d_slots, c->fsize * c->nslots);
+        ALLOC(c->d_mv, n4 * 2 * sizeof(int16_t)); ALLOC(c->d_refidx, n4); ALLOC(c->d_ipred, n4);
+        ALLOC(c->d_res, nmb * sizeof(jmh_mb_result));
+        ALLOC(c->d_spiral, (size_t)c->npos * 2 * sizeof(int16_t));
+        ALLOC(c->d_spiral_of, (size_t)c->npos * sizeof(int16_t));
+        HALLOC(c->h_res, nmb * sizeof(jmh_mb_result)); HALLOC(c->h_rec, c->fsize);
+        HALLOC(c->h_stage_cur, c->fsize); HALLOC(c->h_stage_ref, c->fsize);
+        std::vector<int16_t> xy, of(c->npos);
+        spiral(c->sr, xy);
+        for (int k = 0; k < c->npos; k++) of[(xy[2 * k + 1] + c->sr) * c->side + xy[2 * k] + c->sr] = (int16_t)k;
+        if (hipMemcpy(c->d_spiral, xy.data(), xy.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(c->d_spiral_of, of.data(), of.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemset(c->d_rec, 0, c->fsize) != hipSuccess || hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        if (hipEventCreate(&c->ev_t0) != hipSuccess || hipEventCreate(&c->ev_t1) != hipSuccess ||
+            ring_init(c->ring_interp) || ring_init(c->ring_mb)) { st = JMH_E_HIP; goto fail; }
+        int nd = (c->mbw - 1) + 2 * (c->mbh - 1) + 1;
+        c->dcount.resize(nd); c->dymin.resize(nd);
+        for (int dg = 0; dg < nd; dg++) {
+            int ymin = dg - (c->mbw - 1) > 0 ? (dg - (c->mbw - 1) + 1) / 2 : 0;
+            int ymax = dg / 2 < c->mbh - 1 ? dg / 2 : c->mbh - 1;
+            c->dymin[dg] = ymin;
+            c->dcount[dg] = ymax >= ymin ? ymax - ymin + 1 : 0;
+        }
+    }
+#undef ALLOC
+#undef HALLOC
+    *out = c;
+    return JMH_OK;
+fail:
+    jmh_destroy(c);
+    return st;
+}
+
+static void pack_planes(uint8_t *dst, int W, int H, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
+    for (int r = 0; r < H; r++) memcpy(dst + (size_t)r * W, y + (size_t)r * sy, W);
+    uint8_t *du = dst + (size_t)W * H, *dv = du + (size_t)W * H / 4;
+    for (int r = 0; r < H / 2; r++) {
+        memcpy(du + (size_t)r * (W / 2), u + (size_t)r * sc, W / 2);
+        memcpy(dv + (size_t)r * (W / 2), v + (size_t)r * sc, W / 2);
+    }
+}
+
+static int run_interp(jmh_ctx *c, const uint8_t *d_refY) {
+    HCHK(ring_begin(c->ring_interp, c->st));
+    HCHK(jmh_launch_interp(d_refY, c->W, c->H, c->d_qpel, c->qstride, c->qplane, c->st));
+    HCHK(ring_end(c->ring_interp, c->st));
+    c->have_ref = 1;
+    return JMH_OK;
+}
+
+int jmh_set_reference(jmh_ctx *c, int list, int ref_idx, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
+    if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
+    if (list != 0 || ref_idx != 0) return JMH_E_UNSUPPORTED_CFG;
+    HCHK(hipSetDevice(c->dev));
+    HCHK(hipStreamSynchronize(c->st));   // staging buffer reuse
+    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc);
+    HCHK(hipMemcpyAsync(c->d_ref, c->h_stage_ref, c->fsize, hipMemcpyHostToDevice, c->st));
+    return run_interp(c, c->d_ref);
+}
+
+int jmh_set_reference_slot(jmh_ctx *c, int slot) {
+    if (!c || slot < -1 || slot >= c->nslots) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    const uint8_t *src = slot < 0 ? c->d_rec : c->d_slots + (size_t)slot * c->fsize;
+    HCHK(hipMemcpyAsync(c->d_ref, src, c->fsize, hipMemcpyDeviceToDevice, c->st));
+    return run_interp(c, c->d_ref);
+}
+
+static int enqueue_encode(jmh_ctx *c, const uint8_t *d_pic, const jmh_frame_params *fp) {
+    if (fp->slice_type != JMH_P_SLICE && fp->slice_type != JMH_I_SLICE) return JMH_E_UNSUPPORTED_CFG;
+    if (fp->qp < 0 || fp->qp > 51 || fp->lambda_mode < 0 || fp->lambda_motion < 0) return JMH_E_INVALID_ARG;
+    if (fp->slice_type == JMH_P_SLICE && !c->have_ref) return JMH_E_STATE;
+    DevParams p;
+    memset(&p, 0, sizeof(p));
+    p.W = c->W; p.H = c->H; p.Wc = c->Wc; p.Hc = c->Hc; p.mbw = c->mbw; p.mbh = c->mbh;
+    p.sr = c->sr; p.side = c->side; p.npos = c->npos;
+    p.search_mode = c->cfg.search_mode; p.use_hadamard = c->cfg.use_hadamard; p.restrict_sr = c->cfg.restrict_search_range;
+    for (int i = 0; i < 8; i++) p.inter_search[i] = c->cfg.inter_search[i];
+    p.qstride = c->qstride; p.qplane = c->qplane;
+    size_t ls = (size_t)c->W * c->H;
+    p.orgY = d_pic; p.orgU = d_pic + ls; p.orgV = d_pic + ls + ls / 4;
+    p.refY = c->d_ref; p.refU = c->d_ref + ls; p.refV = c->d_ref + ls + ls / 4;
+    p.qpel = c->d_qpel;
+    p.recY = c->d_rec; p.recU = c->d_rec + ls; p.recV = c->d_rec + ls + ls / 4;
+    p.mv = c->d_mv; p.refidx = c->d_refidx; p.ipred = c->d_ipred; p.res = c->d_res;
+    p.spiral = c->d_spiral; p.spiral_of = c->d_spiral_of;
+    p.slice_type = fp->slice_type; p.qp = fp->qp; p.lambda_mode = fp->lambda_mode; p.lambda_motion = fp->lambda_motion;
+    p.cqp_off = fp->chroma_qp_offset;
+    HCHK(ring_begin(c->ring_mb, c->st));
+    for (size_t dg = 0; dg < c->dcount.size(); dg++) {
+        if (!c->dcount[dg]) continue;
+        p.diag = (int)dg; p.y_min = c->dymin[dg];
+        HCHK(jmh_launch_mb(p, c->dcount[dg], c->st));
+    }
+    HCHK(ring_end(c->ring_mb, c->st));
+    int nl = 0;
+    for (int n : c->dcount) nl += n > 0;
+    c->timing.mb_launches = nl;
+    return JMH_OK;
+}
+
+int jmh_frame_submit(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc, const jmh_frame_params *fp) {
+    if (!c || !y || !u || !v || !fp || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    HCHK(hipStreamSynchronize(c->st));
+    pack_planes(c->h_stage_cur, c->W, c->H, y, u, v, sy, sc);
+    HCHK(hipEventRecord(c->ev_t0, c->st));
+    HCHK(hipMemcpyAsync(c->d_cur, c->h_stage_cur, c->fsize, hipMemcpyHostToDevice, c->st));
+    int r = enqueue_encode(c, c->d_cur, fp);
+    if (r) return r;
+    HCHK(hipMemcpyAsync(c->h_res, c->d_res, (size_t)c->mbw * c->mbh * sizeof(jmh_mb_result), hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(c->h_rec, c->d_rec, c->fsize, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipEventRecord(c->ev_t1, c->st));
+    c->pending = 1;
+    c->have_results = 0;
+    return JMH_OK;
+}
+
+int jmh_frame_wait(jmh_ctx *c) {
+    if (!c) return JMH_E_INVALID_ARG;
+    if (!c->pending) return JMH_E_STATE;
+    HCHK(hipSetDevice(c->dev));
+    HCHK(hipStreamSynchronize(c->st));
+    HCHK(hipGetLastError());
+    c->pending = 0;
+    c->have_results = 1;
+    return JMH_OK;
+}
+
+const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *c, int mb_addr) {
+    if (!c || !c->have_results || mb_addr < 0 || mb_addr >= c->mbw * c->mbh) return nullptr;
+    return &c->h_res[mb_addr];
+}
+
+int jmh_read_recon(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
+    if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
+    if (!c->have_results) return JMH_E_STATE;
+    size_t ls = (size_t)c->W * c->H;
+    for (int r = 0; r < c->H; r++) memcpy(y + (size_t)r * sy, c->h_rec + (size_t)r * c->W, c->W);
+    for (int r = 0; r < c->Hc; r++) {
+        memcpy(u + (size_t)r * sc, c->h_rec + ls + (size_t)r * c->Wc, c->Wc);
+        memcpy(v + (size_t)r * sc, c->h_rec + ls + ls / 4 + (size_t)r * c->Wc, c->Wc);
+    }
+    return JMH_OK;
+}
+
+int jmh_load_frame(jmh_ctx *c, int slot, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
+    if (!c || slot < 0 || slot >= c->nslots || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    HCHK(hipStreamSynchronize(c->st));
+    pack_planes(c->h_stage_cur, c->W, c->H, y, u, v, sy, sc);
+    HCHK(hipMemcpyAsync(c->d_slots + (size_t)slot * c->fsize, c->h_stage_cur, c->fsize, hipMemcpyHostToDevice, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    return JMH_OK;
+}
+
+int jmh_encode_slot(jmh_ctx *c, int slot, const jmh_frame_params *fp) {
+    if (!c || !fp || slot < 0 || slot >= c->nslots) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    return enqueue_encode(c, c->d_slots + (size_t)slot * c->fsize, fp);
+}
+
+int jmh_sync(jmh_ctx *c) {
+    if (!c) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    HCHK(hipStreamSynchronize(c->st));
+    HCHK(hipGetLastError());
+    return JMH_OK;
+}
+
+int jmh_get_timing(jmh_ctx *c, jmh_timing *t) {
+    if (!c || !t) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    HCHK(hipStreamSynchronize(c->st));
+    float ms = 0;
+    ring_drain(c->ring_interp, c->timing.interp_ms, c->timing.interps);
+    ring_drain(c->ring_mb, c->timing.mb_ms, c->timing.pictures);
+    if (hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1) == hipSuccess) c->timing.total_ms = ms;
+    *t = c->timing;
+    return JMH_OK;
+}
+
+int jmh_ffs_sad_table(jmh_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t *centres, uint16_t *out) {
+    if (!c || n_mb <= 0 || !mb_xy || !centres || !out) return JMH_E_INVALID_ARG;
+    for (int i = 0; i < n_mb; i++)
+        if (mb_xy[2 * i] < 0 || mb_xy[2 * i] >= c->mbw || mb_xy[2 * i + 1] < 0 || mb_xy[2 * i + 1] >= c->mbh) return JMH_E_INVALID_ARG;
+    if (!c->have_ref) return JMH_E_STATE;
+    HCHK(hipSetDevice(c->dev));
+    int32_t *d_xy = nullptr, *d_c = nullptr;
+    uint16_t *d_out = nullptr;
+    size_t on = (size_t)n_mb * 16 * c->npos;
+    HCHK(hipMalloc((void **)&d_xy, n_mb * 8));
+    HCHK(hipMalloc((void **)&d_c, n_mb * 8));
+    HCHK(hipMalloc((void **)&d_out, on * 2));
+    HCHK(hipMemcpyAsync(d_xy, mb_xy, n_mb * 8, hipMemcpyHostToDevice, c->st));
+    HCHK(hipMemcpyAsync(d_c, centres, n_mb * 8, hipMemcpyHostToDevice, c->st));
+    HCHK(jmh_launch_sad_table(c->d_slots, c->d_ref, c->W, c->H, c->sr, n_mb, d_xy, d_c, d_out, c->st));
+    HCHK(hipMemcpyAsync(out, d_out, on * 2, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    HCHK(hipFree(d_xy)); HCHK(hipFree(d_c)); HCHK(hipFree(d_out));
+    return JMH_OK;
+}
+
+int jmh_tq4x4_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels,
+                    uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
+    if (!c || n <= 0 || !resid || !pred || !levels || !recon || !coeff_cost || !nonzero || qp < 0 || qp > 51) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    int16_t *dr, *dl;
+    uint8_t *dp, *drec;
+    int32_t *dcc, *dnz;
+    HCHK(hipMalloc((void **)&dr, n * 32)); HCHK(hipMalloc((void **)&dl, n * 32));
+    HCHK(hipMalloc((void **)&dp, n * 16)); HCHK(hipMalloc((void **)&drec, n * 16));
+    HCHK(hipMalloc((void **)&dcc, n * 4)); HCHK(hipMalloc((void **)&dnz, n * 4));
+    HCHK(hipMemcpyAsync(dr, resid, n * 32, hipMemcpyHostToDevice, c->st));
+    HCHK(hipMemcpyAsync(dp, pred, n * 16, hipMemcpyHostToDevice, c->st));
+    HCHK(jmh_launch_tq4x4(n, dr, dp, qp, intra, dl, drec, dcc, dnz, c->st));
+    HCHK(hipMemcpyAsync(levels, dl, n * 32, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(recon, drec, n * 16, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(coeff_cost, dcc, n * 4, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(nonzero, dnz, n * 4, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    HCHK(hipFree(dr)); HCHK(hipFree(dl)); HCHK(hipFree(dp)); HCHK(hipFree(drec)); HCHK(hipFree(dcc)); HCHK(hipFree(dnz));
+    return JMH_OK;
+}
+
+/* test seam: quarter-pel planes of the current reference, [16][H+8][W+8] */
+int jmh_read_qpel(jmh_ctx *c, uint8_t *out) {
+    if (!c || !out) return JMH_E_INVALID_ARG;
+    if (!c->have_ref) return JMH_E_STATE;
+    HCHK(hipSetDevice(c->dev));
+    HCHK(hipMemcpyAsync(out, c->d_qpel, (size_t)16 * c->qplane, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    return JMH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,275 @@
+"""Python mirror of the jmh_* C ABI (include/jmhip.h) — the MI355X JM hot path.
+
+This module is the host-side interface tests and bench.py drive: it mirrors lencod's per-picture
+use of the hot path (JM 8.6 image.c › encode_one_frame → encode_one_macroblock per MB [J]) over
+ctypes.  It loads ``csrc/libjmhip.so`` (built in-tree) and fails loudly if it is missing: there is
+no CPU fallback in the product path.  ``libjmhost.so`` (host plumbing: synthetic source, CAVLC
+writer, deblocking) is loaded on demand for the synthetic input generator.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "csrc", "libjmhip.so")
+HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
+
+JMH_OK = 0
+JMH_P_SLICE, JMH_I_SLICE = 0, 2
+STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
+          -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
+# JM 8.6 rdopt.c QP2QUANT [J]: RDO-off lambda = QP2QUANT[max(0, qp-12)]
+QP2QUANT = [1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 4, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18,
+            20, 23, 25, 29, 32, 36, 40, 45, 51, 57, 64, 72, 81, 91]
+
+
+def lambda_rdo_off(qp):
+    return QP2QUANT[max(0, qp - 12)]
+
+
+class JmhConfig(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("search_range", ctypes.c_int32), ("search_mode", ctypes.c_int32),
+                ("use_hadamard", ctypes.c_int32), ("restrict_search_range", ctypes.c_int32),
+                ("inter_search", ctypes.c_int32 * 8), ("num_ref_frames", ctypes.c_int32),
+                ("constrained_intra_pred", ctypes.c_int32), ("num_frame_slots", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 7)]
+
+
+class JmhFrameParams(ctypes.Structure):
+    _fields_ = [("slice_type", ctypes.c_int32), ("qp", ctypes.c_int32),
+                ("lambda_mode", ctypes.c_int32), ("lambda_motion", ctypes.c_int32),
+                ("chroma_qp_offset", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+
+
+class JmhTiming(ctypes.Structure):
+    _fields_ = [("interp_ms", ctypes.c_float), ("mb_ms", ctypes.c_float),
+                ("total_ms", ctypes.c_float), ("mb_launches", ctypes.c_int32),
+                ("pictures", ctypes.c_int32), ("interps", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 2)]
+
+
+# jmh_mb_result, field for field (include/jmhip.h)
+MB_RESULT_DTYPE = np.dtype([
+    ("mb_type", "<i2"), ("cbp", "<i2"), ("cbp_blk", "<i4"), ("b8mode", "i1", 4),
+    ("ref_idx", "i1", 4), ("i16mode", "i1"), ("c_ipred_mode", "i1"), ("pad0", "i1", 2),
+    ("ipred", "i1", 16), ("mv", "<i2", (16, 2)), ("luma", "<i2", (16, 16)),
+    ("luma_dc", "<i2", 16), ("chroma_dc", "<i2", (2, 4)), ("chroma_ac", "<i2", (2, 4, 16)),
+    ("min_cost", "<i4"), ("reserved", "<i4")])
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_SIGS = {
+    "jmh_create": (_I, [ctypes.POINTER(JmhConfig), _I, ctypes.POINTER(_P)]),
+    "jmh_destroy": (None, [_P]),
+    "jmh_strerror": (ctypes.c_char_p, [_I]),
+    "jmh_abi_version": (_I, []),
+    "jmh_device_count": (_I, []),
+    "jmh_set_reference": (_I, [_P, _I, _I, _P, _P, _P, _I, _I]),
+    "jmh_frame_submit": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(JmhFrameParams)]),
+    "jmh_frame_wait": (_I, [_P]),
+    "jmh_get_mb_result": (_P, [_P, _I]),
+    "jmh_read_recon": (_I, [_P, _P, _P, _P, _I, _I]),
+    "jmh_load_frame": (_I, [_P, _I, _P, _P, _P, _I, _I]),
+    "jmh_set_reference_slot": (_I, [_P, _I]),
+    "jmh_encode_slot": (_I, [_P, _I, ctypes.POINTER(JmhFrameParams)]),
+    "jmh_sync": (_I, [_P]),
+    "jmh_get_timing": (_I, [_P, ctypes.POINTER(JmhTiming)]),
+    "jmh_ffs_sad_table": (_I, [_P, _I, _P, _P, _P]),
+    "jmh_tq4x4_batch": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "jmh_read_qpel": (_I, [_P, _P]),
+}
+EXPORTED = tuple(_SIGS)
+
+
+class JmhError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libjmhip.so (raises if it was not built — the product has no fallback)."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise JmhError(f"libjmhip.so not found at {path}: build it with __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def _check(st, what):
+    if st != JMH_OK:
+        raise JmhError(f"{what}: {STATUS.get(st, st)} ({st})")
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
+                restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2):
+    cfg = JmhConfig()
+    cfg.width, cfg.height = width, height
+    cfg.search_range, cfg.search_mode = search_range, search_mode
+    cfg.use_hadamard, cfg.restrict_search_range = use_hadamard, restrict_search_range
+    for i, v in enumerate(inter_search):
+        cfg.inter_search[i + 1] = v
+    cfg.num_ref_frames, cfg.constrained_intra_pred, cfg.num_frame_slots = 1, 0, slots
+    return cfg
+
+
+def frame_params(slice_type, qp, chroma_qp_offset=0):
+    fp = JmhFrameParams()
+    fp.slice_type, fp.qp = slice_type, qp
+    fp.lambda_mode = fp.lambda_motion = lambda_rdo_off(qp)
+    fp.chroma_qp_offset = chroma_qp_offset
+    return fp
+
+
+def split_yuv(frame, w, h):
+    """I420 buffer (w*h*3/2 bytes) -> contiguous (y, u, v) uint8 planes."""
+    f = np.ascontiguousarray(frame, dtype=np.uint8).reshape(-1)
+    y = f[: w * h].reshape(h, w)
+    u = f[w * h: w * h + w * h // 4].reshape(h // 2, w // 2)
+    v = f[w * h + w * h // 4:].reshape(h // 2, w // 2)
+    return np.ascontiguousarray(y), np.ascontiguousarray(u), np.ascontiguousarray(v)
+
+
+class Encoder:
+    """One jmh_ctx: the macroblock hot path of one video stream on one HIP device."""
+
+    def __init__(self, width, height, device=0, **kw):
+        self.lib = load()
+        self.w, self.h = width, height
+        self.mbw, self.mbh = width // 16, height // 16
+        self.cfg = make_config(width, height, **kw)
+        ctx = ctypes.c_void_p()
+        _check(self.lib.jmh_create(ctypes.byref(self.cfg), device, ctypes.byref(ctx)), "jmh_create")
+        self.ctx = ctx
+
+    def close(self):
+        if self.ctx:
+            self.lib.jmh_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_reference(self, y, u, v):
+        _check(self.lib.jmh_set_reference(self.ctx, 0, 0, _ptr(y), _ptr(u), _ptr(v),
+                                          self.w, self.w // 2), "jmh_set_reference")
+
+    def encode(self, y, u, v, slice_type, qp, chroma_qp_offset=0):
+        fp = frame_params(slice_type, qp, chroma_qp_offset)
+        _check(self.lib.jmh_frame_submit(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2,
+                                         ctypes.byref(fp)), "jmh_frame_submit")
+        _check(self.lib.jmh_frame_wait(self.ctx), "jmh_frame_wait")
+        return self.results(), self.recon()
+
+    def results(self):
+        n = self.mbw * self.mbh
+        p = self.lib.jmh_get_mb_result(self.ctx, 0)
+        if not p:
+            raise JmhError("no results")
+        buf = (ctypes.c_char * (n * MB_RESULT_DTYPE.itemsize)).from_address(p)
+        return np.frombuffer(bytes(buf), dtype=MB_RESULT_DTYPE).copy()
+
+    def recon(self):
+        y = np.empty((self.h, self.w), np.uint8)
+        u = np.empty((self.h // 2, self.w // 2), np.uint8)
+        v = np.empty_like(u)
+        _check(self.lib.jmh_read_recon(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2),
+               "jmh_read_recon")
+        return y, u, v
+
+    # ---- device-resident path (bench) ----
+    def load_frame(self, slot, y, u, v):
+        _check(self.lib.jmh_load_frame(self.ctx, slot, _ptr(y), _ptr(u), _ptr(v), self.w,
+                                       self.w // 2), "jmh_load_frame")
+
+    def set_reference_slot(self, slot):
+        _check(self.lib.jmh_set_reference_slot(self.ctx, slot), "jmh_set_reference_slot")
+
+    def encode_slot(self, slot, slice_type, qp):
+        fp = frame_params(slice_type, qp)
+        _check(self.lib.jmh_encode_slot(self.ctx, slot, ctypes.byref(fp)), "jmh_encode_slot")
+
+    def sync(self):
+        _check(self.lib.jmh_sync(self.ctx), "jmh_sync")
+
+    def timing(self):
+        t = JmhTiming()
+        _check(self.lib.jmh_get_timing(self.ctx, ctypes.byref(t)), "jmh_get_timing")
+        return t
+
+    # ---- unit seams ----
+    def sad_table(self, mb_xy, centres):
+        mb_xy = np.ascontiguousarray(mb_xy, np.int32)
+        centres = np.ascontiguousarray(centres, np.int32)
+        n = mb_xy.shape[0]
+        side = 2 * self.cfg.search_range + 1
+        out = np.empty((n, 16, side * side), np.uint16)
+        _check(self.lib.jmh_ffs_sad_table(self.ctx, n, _ptr(mb_xy), _ptr(centres), _ptr(out)),
+               "jmh_ffs_sad_table")
+        return out
+
+    def tq4x4(self, resid, pred, qp, intra):
+        resid = np.ascontiguousarray(resid, np.int16)
+        pred = np.ascontiguousarray(pred, np.uint8)
+        n = resid.shape[0]
+        lev = np.empty((n, 16), np.int16)
+        rec = np.empty((n, 16), np.uint8)
+        cc = np.empty(n, np.int32)
+        nz = np.empty(n, np.int32)
+        _check(self.lib.jmh_tq4x4_batch(self.ctx, n, _ptr(resid), _ptr(pred), qp, intra, _ptr(lev),
+                                        _ptr(rec), _ptr(cc), _ptr(nz)), "jmh_tq4x4_batch")
+        return lev, rec, cc, nz
+
+    def read_qpel(self):
+        out = np.empty((16, self.h + 8, self.w + 8), np.uint8)
+        _check(self.lib.jmh_read_qpel(self.ctx, _ptr(out)), "jmh_read_qpel")
+        return out
+
+
+# ---- synthetic source (product host plumbing, libjmhost.so) ------------------------------
+_host = None
+
+
+def load_host(path=HOST_LIB_PATH):
+    global _host
+    if _host is None:
+        if not os.path.exists(path):
+            raise JmhError(f"libjmhost.so not found at {path}: build it with __graft_entry__.build()")
+        _host = ctypes.CDLL(path)
+        _host.jm_synth_frame.restype = None
+        _host.jm_synth_frame.argtypes = [_P, _I, _I, ctypes.c_uint64, _I]
+    return _host
+
+
+class _JmPic(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_int), ("h", ctypes.c_int), ("y", _P), ("u", _P), ("v", _P)]
+
+
+def synth_frame(disp_w, disp_h, seed, index):
+    """Deterministic synthetic 4:2:0 picture (coded size = multiple of 16), as (y, u, v)."""
+    host = load_host()
+    cw, ch = (disp_w + 15) // 16 * 16, (disp_h + 15) // 16 * 16
+    y = np.zeros((ch, cw), np.uint8)
+    u = np.zeros((ch // 2, cw // 2), np.uint8)
+    v = np.zeros_like(u)
+    pic = _JmPic(cw, ch, y.ctypes.data, u.ctypes.data, v.ctypes.data)
+    host.jm_synth_frame(ctypes.byref(pic), disp_w, disp_h, seed, index)
+    return y, u, v

@@ -113,13 +113,16 @@ typedef struct jmh_mb_result {
     int32_t reserved;
 } jmh_mb_result;
 
-/* ---- kernel timing of the last submitted picture (HIP events on the context stream) ----- */
+/* ---- kernel timing (HIP events on the context stream), summed since the previous
+ *      jmh_get_timing call (which resets the sums) ------------------------------------------ */
 typedef struct jmh_timing {
-    float interp_ms;           /* quarter-pel reference interpolation (last jmh_set_reference*) */
-    float mb_ms;               /* whole macroblock wavefront of the last picture               */
-    float total_ms;            /* first to last event of the last picture (incl. H2D if any)   */
-    int32_t mb_launches;       /* wavefront launches per picture                               */
-    int32_t reserved[4];
+    float interp_ms;           /* sum of quarter-pel interpolations (jmh_set_reference*)       */
+    float mb_ms;               /* sum of whole macroblock wavefronts (first to last dispatch)  */
+    float total_ms;            /* last jmh_frame_submit: H2D + wavefront + D2H                 */
+    int32_t mb_launches;       /* wavefront launches (dispatches) per picture                  */
+    int32_t pictures;          /* pictures summed in mb_ms                                     */
+    int32_t interps;           /* interpolations summed in interp_ms                           */
+    int32_t reserved[2];
 } jmh_timing;
 
 typedef struct jmh_ctx jmh_ctx;
@@ -157,8 +160,7 @@ int  jmh_get_timing(jmh_ctx *ctx, jmh_timing *t);
 
 /* ---- unit seams (minimum slice; tests call these directly) ------------------------------
  * jmh_ffs_sad_table: SetupFastFullPelSearch's 4x4 BlockSAD table for n_mb macroblocks of the
- *   picture last given to jmh_frame_submit/jmh_load_frame(slot 0) against the current
- *   reference.  mb_xy[2*i] = (mb_x, mb_y); centres[2*i] = absolute full-pel window centre
+ *   picture in resident slot 0 (jmh_load_frame) against the current reference.  mb_xy[2*i] = (mb_x, mb_y); centres[2*i] = absolute full-pel window centre
  *   offset (cx, cy) relative to the MB.  out[i][blk(16)][(2R+1)^2] in window raster order
  *   (dy outer, dx inner, dy,dx in [-R,R]).                                                  */
 int  jmh_ffs_sad_table(jmh_ctx *ctx, int n_mb, const int32_t *mb_xy, const int32_t *centres,
@@ -169,6 +171,9 @@ int  jmh_ffs_sad_table(jmh_ctx *ctx, int n_mb, const int32_t *mb_xy, const int32
 int  jmh_tq4x4_batch(jmh_ctx *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp,
                      int intra, int16_t *levels, uint8_t *recon, int32_t *coeff_cost,
                      int32_t *nonzero);
+/* jmh_read_qpel: the 16 quarter-pel phase planes of the current reference (test seam for
+ *   UnifiedOneForthPix), out[16][H+8][W+8], phase = 4*yfrac + xfrac, 4-sample padding.      */
+int  jmh_read_qpel(jmh_ctx *ctx, uint8_t *out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,141 @@
+"""ctypes binding of the oracle (oracle/_build/liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Mirrors jmhip.Encoder so parity tests read the same on both sides.
+"""
+import ctypes
+
+import numpy as np
+
+from jmpaths import LIBORACLE, ensure_built, load_jmhip
+
+jmhip = load_jmhip()
+_P, _I = ctypes.c_void_p, ctypes.c_int
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        ensure_built()
+        L = ctypes.CDLL(LIBORACLE)
+        sig = {
+            "jmo_create": (_I, [ctypes.POINTER(jmhip.JmhConfig), ctypes.POINTER(_P)]),
+            "jmo_destroy": (None, [_P]),
+            "jmo_set_reference": (_I, [_P, _P, _P, _P, _I, _I]),
+            "jmo_encode_frame": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(jmhip.JmhFrameParams)]),
+            "jmo_mb_result": (_P, [_P, _I]),
+            "jmo_read_recon": (_I, [_P, _P, _P, _P, _I, _I]),
+            "jmo_read_qpel": (_I, [_P, _P]),
+            "jmo_load_current": (_I, [_P, _P, _P, _P, _I, _I]),
+            "jmo_ffs_sad_table": (_I, [_P, _I, _P, _P, _P]),
+            "jmo_tq4x4_batch": (_I, [_I, _P, _P, _I, _I, _P, _P, _P, _P]),
+            "jmo_luma_qpel_sample": (_I, [_P, _I, _I, _I, _I, _I]),
+            "jmo_spiral": (None, [_I, _P, _P]),
+            "jmo_mvbits": (_I, [_I]),
+            "jmo_satd4x4": (_I, [_P, _I]),
+            "jmo_forward4x4": (None, [_P, _P]),
+            "jmo_inverse4x4": (None, [_P, _P]),
+            "jmo_qp2quant": (_I, [_I]),
+            "jmo_qp_scale_cr": (_I, [_I]),
+            "jmo_mvp_median": (None, [_I] * 17 + [_P]),
+            "jmo_dec_create": (_I, [ctypes.POINTER(_P)]),
+            "jmo_dec_destroy": (None, [_P]),
+            "jmo_decode_annexb": (_I, [_P, _P, ctypes.c_long, _P, ctypes.c_long, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+            "jmo_dec_error": (ctypes.c_char_p, [_P]),
+        }
+        for n, (r, a) in sig.items():
+            f = getattr(L, n)
+            f.restype, f.argtypes = r, a
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleEncoder:
+    def __init__(self, width, height, **kw):
+        self.L = lib()
+        self.w, self.h = width, height
+        self.mbw, self.mbh = width // 16, height // 16
+        self.cfg = jmhip.make_config(width, height, **kw)
+        c = ctypes.c_void_p()
+        st = self.L.jmo_create(ctypes.byref(self.cfg), ctypes.byref(c))
+        if st:
+            raise RuntimeError(f"jmo_create: {st}")
+        self.ctx = c
+
+    def close(self):
+        if self.ctx:
+            self.L.jmo_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_reference(self, y, u, v):
+        assert self.L.jmo_set_reference(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2) == 0
+
+    def load_current(self, y, u, v):
+        assert self.L.jmo_load_current(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2) == 0
+
+    def encode(self, y, u, v, slice_type, qp, chroma_qp_offset=0):
+        fp = jmhip.frame_params(slice_type, qp, chroma_qp_offset)
+        st = self.L.jmo_encode_frame(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2, ctypes.byref(fp))
+        assert st == 0, st
+        n = self.mbw * self.mbh
+        p = self.L.jmo_mb_result(self.ctx, 0)
+        buf = (ctypes.c_char * (n * jmhip.MB_RESULT_DTYPE.itemsize)).from_address(p)
+        res = np.frombuffer(bytes(buf), dtype=jmhip.MB_RESULT_DTYPE).copy()
+        ry = np.empty((self.h, self.w), np.uint8)
+        ru = np.empty((self.h // 2, self.w // 2), np.uint8)
+        rv = np.empty_like(ru)
+        assert self.L.jmo_read_recon(self.ctx, _ptr(ry), _ptr(ru), _ptr(rv), self.w, self.w // 2) == 0
+        return res, (ry, ru, rv)
+
+    def read_qpel(self):
+        out = np.empty((16, self.h + 8, self.w + 8), np.uint8)
+        assert self.L.jmo_read_qpel(self.ctx, _ptr(out)) == 0
+        return out
+
+    def sad_table(self, mb_xy, centres):
+        mb_xy = np.ascontiguousarray(mb_xy, np.int32)
+        centres = np.ascontiguousarray(centres, np.int32)
+        side = 2 * self.cfg.search_range + 1
+        out = np.empty((mb_xy.shape[0], 16, side * side), np.uint16)
+        assert self.L.jmo_ffs_sad_table(self.ctx, mb_xy.shape[0], _ptr(mb_xy), _ptr(centres), _ptr(out)) == 0
+        return out
+
+
+def tq4x4(resid, pred, qp, intra):
+    L = lib()
+    resid = np.ascontiguousarray(resid, np.int16)
+    pred = np.ascontiguousarray(pred, np.uint8)
+    n = resid.shape[0]
+    lev = np.empty((n, 16), np.int16)
+    rec = np.empty((n, 16), np.uint8)
+    cc = np.empty(n, np.int32)
+    nz = np.empty(n, np.int32)
+    assert L.jmo_tq4x4_batch(n, _ptr(resid), _ptr(pred), qp, intra, _ptr(lev), _ptr(rec), _ptr(cc), _ptr(nz)) == 0
+    return lev, rec, cc, nz
+
+
+def decode_annexb(data, max_frames=64, max_w=1920, max_h=1088):
+    L = lib()
+    d = ctypes.c_void_p()
+    L.jmo_dec_create(ctypes.byref(d))
+    buf = np.frombuffer(data, np.uint8).copy()
+    cap = max_frames * max_w * max_h * 3 // 2
+    out = np.empty(cap, np.uint8)
+    w, h = ctypes.c_int(), ctypes.c_int()
+    n = L.jmo_decode_annexb(d, _ptr(buf), len(buf), _ptr(out), cap, ctypes.byref(w), ctypes.byref(h))
+    err = L.jmo_dec_error(d).decode()
+    L.jmo_dec_destroy(d)
+    if n < 0:
+        raise RuntimeError("decode failed: " + err)
+    fs = w.value * h.value * 3 // 2
+    return [out[i * fs:(i + 1) * fs] for i in range(n)], w.value, h.value
