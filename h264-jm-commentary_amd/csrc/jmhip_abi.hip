@@ -74,7 +74,7 @@ struct jmh_ctx {
     int16_t *d_spiral, *d_spiral_of;
     jmh_mb_result *h_res;
     uint8_t *h_rec, *h_stage_cur, *h_stage_ref;
-    int have_ref, pending, have_results;
+    int have_ref, pending, have_results, have_total;
     hipEvent_t ev_t0, ev_t1;
     EvRing ring_interp, ring_mb;
     jmh_timing timing;
@@ -283,6 +283,7 @@ int jmh_frame_submit(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8
     HCHK(hipMemcpyAsync(c->h_rec, c->d_rec, c->fsize, hipMemcpyDeviceToHost, c->st));
     HCHK(hipEventRecord(c->ev_t1, c->st));
     c->pending = 1;
+    c->have_total = 1;
     c->have_results = 0;
     return JMH_OK;
 }
@@ -292,7 +293,6 @@ int jmh_frame_wait(jmh_ctx *c) {
     if (!c->pending) return JMH_E_STATE;
     HCHK(hipSetDevice(c->dev));
     HCHK(hipStreamSynchronize(c->st));
-    HCHK(hipGetLastError());
     c->pending = 0;
     c->have_results = 1;
     return JMH_OK;
@@ -335,7 +335,7 @@ int jmh_sync(jmh_ctx *c) {
     if (!c) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
     HCHK(hipStreamSynchronize(c->st));
-    HCHK(hipGetLastError());
+
     return JMH_OK;
 }
 
@@ -346,7 +346,7 @@ int jmh_get_timing(jmh_ctx *c, jmh_timing *t) {
     float ms = 0;
     ring_drain(c->ring_interp, c->timing.interp_ms, c->timing.interps);
     ring_drain(c->ring_mb, c->timing.mb_ms, c->timing.pictures);
-    if (hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1) == hipSuccess) c->timing.total_ms = ms;
+    if (c->have_total && hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1) == hipSuccess) c->timing.total_ms = ms;
     *t = c->timing;
     return JMH_OK;
 }

@@ -103,9 +103,12 @@ def test_sad_table(sr):
 
 
 # ---------------- a3..a14: whole pictures ----------------
-def encode_pair(w, h, frames, slice_types, qp, **kw):
+def encode_pair(w, h, frames, slice_types, qp, first_ref=None, **kw):
     g = jmhip.Encoder(w, h, **kw)
     o = oracle_lib.OracleEncoder(w, h, **kw)
+    if first_ref is not None:
+        g.set_reference(*first_ref)
+        o.set_reference(*first_ref)
     for i, (pic, st) in enumerate(zip(frames, slice_types)):
         gres, grec = g.encode(*pic, st, qp)
         ores, orec = o.encode(*pic, st, qp)
@@ -148,12 +151,13 @@ def test_ipp_configs(kw, qp):
 def test_random_content_p_frames():
     rng = np.random.default_rng(11)
     pics = [rand_picture(rng, 64, 64) for _ in range(3)]
-    encode_pair(64, 64, pics, [jmhip.JMH_P_SLICE] * 3, 26, search_range=16)
+    ref = rand_picture(rng, 64, 64, smooth=False)
+    encode_pair(64, 64, pics, [jmhip.JMH_P_SLICE] * 3, 26, first_ref=ref, search_range=16)
 
 
 def test_flat_frames_ties():
     flat = (np.full((48, 64), 100, np.uint8), np.full((24, 32), 128, np.uint8), np.full((24, 32), 128, np.uint8))
-    encode_pair(64, 48, [flat, flat], [jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], 28, search_range=8)
+    encode_pair(64, 48, [flat, flat], [jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], 28, first_ref=flat, search_range=8)
 
 
 def test_saturated_frames():
