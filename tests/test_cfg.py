@@ -1,0 +1,45 @@
+"""encoder.cfg interface (JM configfile.c semantics): Key = Value, comments, -f/-p order,
+unknown keys and unsupported settings are errors."""
+import subprocess
+import tempfile
+
+from jmpaths import LENCOD_CPU, ensure_built
+
+
+def run(*args):
+    ensure_built()
+    return subprocess.run([LENCOD_CPU, *args], capture_output=True, text=True, timeout=120)
+
+
+def test_cfg_file_and_override_order():
+    with tempfile.TemporaryDirectory() as d:
+        cfg = f"{d}/encoder.cfg"
+        with open(cfg, "w") as f:
+            f.write("# JM-style config\nInputFile = \"synthetic:4\"   # quoted\nFramesToBeEncoded = 2\n"
+                    "SourceWidth = 64\nSourceHeight = 48\nSearchRange = 4\nQPFirstFrame = 30\n"
+                    f"OutputFile = {d}/o.264\n")
+        r = run("-d", cfg, "-p", "QPFirstFrame=31")
+        assert r.returncode == 0, r.stderr
+        assert " 31 " in r.stdout.splitlines()[2]          # override applied after the file
+
+
+def test_unknown_key_is_error():
+    r = run("-p", "NoSuchKey=1")
+    assert r.returncode != 0 and "not recognized" in r.stderr
+
+
+def test_range_checked():
+    r = run("-p", "SearchRange=999")
+    assert r.returncode != 0 and "out of range" in r.stderr
+
+
+def test_unsupported_rdo_reported():
+    r = run("-p", "RDOptimization=1")
+    assert r.returncode != 0 and "RDOptimization" in r.stderr
+
+
+def test_jm86_spellings_accepted():
+    with tempfile.TemporaryDirectory() as d:
+        r = run("-p", "UseFME=0", "-p", "QPRemainingFrame=30", "-p", "FramesToBeEncoded=1", "-p", "SourceWidth=32",
+                "-p", "SourceHeight=32", "-p", "SearchRange=2", "-p", f"OutputFile={d}/o.264")
+        assert r.returncode == 0, r.stderr

@@ -116,7 +116,7 @@ def test_tq_round_trip_error_bounded_by_step():
 
 def test_qp_tables():
     assert [L.jmo_qp2quant(q) for q in (0, 12, 28, 51)] == [1, 1, 6, 91]
-    assert [L.jmo_qp_scale_cr(q) for q in (0, 29, 30, 34, 39, 45, 51)] == [0, 29, 29, 32, 35, 37, 39]
+    assert [L.jmo_qp_scale_cr(q) for q in (0, 29, 30, 34, 39, 45, 51)] == [0, 29, 29, 32, 35, 38, 39]
 
 
 # ---- 8.4.2.2.1 luma interpolation ----------------------------------------------------------
