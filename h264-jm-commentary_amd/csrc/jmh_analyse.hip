@@ -1,0 +1,595 @@
+// jmh_analyse.hip — k_mb_analyse: the decision half of encode_one_macroblock [J] (RDO off) for
+// every macroblock of one wavefront diagonal, split over three 768-thread workgroups per MB
+// that run concurrently on different CUs:
+//
+//   role 2  P8x8 motion search: 4 x (8x8, 2x 8x4, 2x 4x8, 4x 4x4) = 36 BlockMotionSearch calls
+//   role 1  16x16, 16x8, 8x16 motion search (5 calls) + FindSkipModeMotionVector
+//   role 0  Intra4x4 decision with its reconstruction, Intra16x16 and chroma intra mode decisions
+//
+// JM runs the 41 searches of a P macroblock one after another. The only coupling between them is
+// the motion vector predictor, which reads MVs already stored inside the MB. Enumerating those
+// reads (getLuma4x4Neighbour + the C-availability rules of SetMotionVectorPredictor): a 16x16 /
+// 16x8 / 8x16 search reads only MB neighbours and the same partition type's earlier block; a
+// P8x8 sub-mode search in 8x8 block b8 reads MB neighbours, the final (best sub-mode) MVs of the
+// 8x8 blocks before b8 and the same sub-mode's earlier blocks in b8. So the 41 searches form 16
+// dependent stages, each a set of independent searches evaluated together, with results
+// identical to JM's sequential order. Per-mode MV arrays provide the exact neighbour view.
+//
+// Motion search data path per ME workgroup:
+//   * 88x88 reference window (+4 margin for the 6-tap filter) and its b, h, j half-pel planes in
+//     LDS, computed once per MB (SubPelBlockMotionSearch reads only LDS);
+//   * the 16 4x4 SADs of every integer position (SetupFastFullPelSearch) in REGISTERS: each
+//     thread owns a column strip of 6 positions, accumulates v_sad_u8 over 20 window rows and
+//     keeps 6 x 8 packed u16 pairs; a search of any partition reduces them with plain 32-bit adds
+//     of packed pairs (no carries: a half never exceeds 8 x 4080);
+//   * cost = SAD + lambda*(mvbits(x) + mvbits(y)) from two per-search LDS tables, key =
+//     cost << 13 | JM order (0 for the (0,0) pre-check, else spiral index + 1), DPP wave min.
+#include "jmh_common.h"
+
+#define NPK 6                                 // search positions per thread (a column strip)
+#define TEAM 192                              // threads per search team (3 waves); 4 teams
+#define PLS (WIN_DIM_MAX * WST + 32)          // stride between the G, b, h, j planes
+
+struct MeS {
+    uint8_t org[256];
+    Border bd;
+    int16_t all_mv[8][16][2];
+    int motion_cost[8][4];
+    uint16_t ctab[4][2][72];                  // per team: lambda*mvbits for x and y offsets
+    unsigned red[NTA / 64][4];                // per wave, per team: partial argmin keys
+    int ccost[2][4][9];                       // per sub-pel pass, team, candidate
+    uint8_t planes[4 * PLS];                  // G (the window), b, h, j
+    int16_t h1[WIN_DIM_MAX * WST];            // unclipped vertical 6-tap intermediates
+};
+struct IntraS {
+    uint8_t org[256];
+    uint8_t orgc[2][64];
+    uint8_t rec[256];
+    Border bd;
+    uint8_t rtop[24];                         // luma row y = -1, x = -1..19 -> [x + 1]
+    uint8_t rleft[16];
+    uint8_t ctop[2][12];                      // chroma rows y = -1, x = -1..7 -> [x + 1]
+    uint8_t cleft[2][8];
+    int i4P[16];
+    int8_t ipred_cur[16];
+};
+union AnalyseS {
+    MeS me;
+    IntraS in;
+};
+
+// neighbour view of a motion search of block type bt in 8x8 block b8 (see header comment)
+struct NbMe {
+    const MeS &s;
+    int bt, b8, best8x8;
+    __device__ bool operator()(int xN, int yN, int &ref, int &mx, int &my) const {
+        if (yN > 15 || (xN > 15 && yN >= 0)) return false;
+        if (xN < 0 || yN < 0) {
+            int c = border_cell(xN, yN);
+            if (c < 0 || s.bd.ref[c] == -2) return false;
+            ref = s.bd.ref[c]; mx = s.bd.mv[c][0]; my = s.bd.mv[c][1];
+            return true;
+        }
+        int k = (yN >> 2) * 4 + (xN >> 2), cb8 = ((yN >> 3) << 1) | (xN >> 3);
+        int m = (bt <= 3 || cb8 == b8) ? bt : (best8x8 >> (4 * cb8)) & 15;
+        ref = 0; mx = s.all_mv[m][k][0]; my = s.all_mv[m][k][1];
+        return true;
+    }
+};
+
+// SAD of partition (BT, BX, BY) from the 8 packed pair registers of one position
+// (register 2*by + bx/2 holds 4x4 blocks (bx, by) low and (bx+1, by) high, bx even)
+template <int BT, int BX, int BY>
+__device__ __forceinline__ unsigned psum(const uint32_t (&r)[8]) {
+    uint32_t v;
+    if constexpr (BT == 1) v = r[0] + r[1] + r[2] + r[3] + r[4] + r[5] + r[6] + r[7];
+    else if constexpr (BT == 2) v = r[2 * BY] + r[2 * BY + 1] + r[2 * BY + 2] + r[2 * BY + 3];
+    else if constexpr (BT == 3) v = r[BX / 2] + r[2 + BX / 2] + r[4 + BX / 2] + r[6 + BX / 2];
+    else if constexpr (BT == 4) v = r[2 * BY + BX / 2] + r[2 * BY + 2 + BX / 2];
+    else if constexpr (BT == 5) v = r[2 * BY + BX / 2];
+    else if constexpr (BT == 6) { v = r[2 * BY + BX / 2] + r[2 * BY + 2 + BX / 2]; return (BX & 1) ? v >> 16 : v & 0xFFFFu; }
+    else { v = r[2 * BY + BX / 2]; return (BX & 1) ? v >> 16 : v & 0xFFFFu; }
+    return (v & 0xFFFFu) + (v >> 16);
+}
+
+// this thread's best key over its positions for search (team J, partition BT/BX/BY)
+template <int J, int BT, int BX, int BY>
+__device__ __forceinline__ unsigned eval_search(const MeS &s, const uint32_t (&sadp)[NPK][8], const uint32_t (&pinfo)[NPK], int dx,
+                                                int dy0, unsigned range) {
+    const unsigned cxv = s.ctab[J][0][dx];
+    unsigned b = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < NPK; k++) {
+        unsigned cost = psum<BT, BX, BY>(sadp[k]) + cxv + s.ctab[J][1][dy0 + k];
+        unsigned key = (cost << 13) | (pinfo[k] & 0x1FFFu);
+        b = min(b, (pinfo[k] >> 16) <= range ? key : 0xFFFFFFFFu);
+    }
+    return b;
+}
+
+__device__ __forceinline__ unsigned search_range(const DevParams &d, int bt) { return d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr; }
+
+// stage head: the MVP of each active team's search (every team thread, uniform) and its
+// lambda*mvbits tables; ends with the barrier that publishes the tables.
+__device__ __forceinline__ void stage_head(const DevParams &d, MeS &s, bool act, int bt, int bx4, int by4, int b8, int best8x8, int scx,
+                                           int scy, int &pmvx, int &pmvy) {
+    const int team = threadIdx.x / TEAM, u = threadIdx.x % TEAM, side = d.side, sr = d.sr, lam = d.lambda_motion;
+    pmvx = pmvy = 0;
+    if (act) {
+        set_mvp(NbMe{s, bt, b8, best8x8}, bx4, by4, c_blc[bt][0], c_blc[bt][1], pmvx, pmvy);
+        if (u < side) s.ctab[team][0][u] = (uint16_t)(lam * mvbits(((scx + u - sr) << 2) - pmvx));
+        else if (u < 2 * side) s.ctab[team][1][u - side] = (uint16_t)(lam * mvbits(((scy + u - side - sr) << 2) - pmvy));
+    }
+    __syncthreads();
+}
+
+// publish the per-thread keys of the stage's searches (teams with bit set in mask)
+__device__ __forceinline__ void stage_reduce(MeS &s, unsigned mask, const unsigned (&bk)[4]) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if ((mask >> j) & 1) {
+            unsigned v = wave_min_u32(bk[j]);
+            if (lane == 0) s.red[wave][j] = v;
+        }
+    __syncthreads();
+}
+
+// stage tail: each active team resolves its full-pel winner, runs SubPelBlockMotionSearch
+// (half then quarter pel, 9 candidates x up to 16 4x4 sub-blocks in parallel) and stores the MV.
+__device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act, int bt, int bx4, int by4, int mcidx, int pmvx, int pmvy,
+                                           int scx, int scy) {
+    const int team = threadIdx.x / TEAM, u = threadIdx.x % TEAM;
+    const int sr = d.sr, lam = d.lambda_motion, had = d.use_hadamard;
+    int rx = 0, ry = 0, fmx = 0, fmy = 0, min_mcost = 0, qx = 0, qy = 0, w4 = 1, nsub = 1, check0 = 0;
+    if (act) {
+        unsigned best = s.red[0][team];
+#pragma unroll
+        for (int w = 1; w < NTA / 64; w++) best = min(best, s.red[w][team]);
+        const unsigned order = best & 8191u;
+        if (order == 0) { rx = -scx; ry = -scy; }
+        else spiral_pos((int)order - 1, rx, ry);
+        fmx = scx + rx; fmy = scy + ry;
+        min_mcost = (int)(best >> 13);
+        w4 = c_blc[bt][0] >> 2; nsub = w4 * (c_blc[bt][1] >> 2);
+        check0 = bt == 1 && fmx == 0 && fmy == 0 && had && d.slice_type == JMH_P_SLICE;
+        if (had) min_mcost = BIGCOST;
+    }
+    const int wx0 = WM + sr + rx + 4 * bx4, wy0 = WM + sr + ry + 4 * by4;   // window coords of block pixel (0,0)
+    for (int pass = 0; pass < 2; pass++) {
+        const int step = pass == 0 ? 2 : 1;
+        const int min_pos = pass == 0 ? (had ? 0 : 1) : 1;
+        if (act && u < 144) {
+            const int c = u >> 4, sub = u & 15;
+            int sat = 0;
+            if (c >= min_pos && sub < nsub) {
+                const int ox = qx + step * c_sp9[c][0], oy = qy + step * c_sp9[c][1];
+                const int off = c_qoff[(oy & 3) * 4 + (ox & 3)];
+                const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
+                const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
+                const int oB = ((xb & 1) + 2 * (yb & 1)) * PLS + (yb >> 1) * WST + (xb >> 1);
+                const int bxp = 4 * (sub % w4), byp = 4 * (sub / w4);
+                const uint8_t *pp = s.planes + (wy0 + byp + (oy >> 2)) * WST + wx0 + bxp + (ox >> 2);
+                const uint8_t *o = s.org + (4 * by4 + byp) * 16 + 4 * bx4 + bxp;
+                int df[16];
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+#pragma unroll
+                    for (int x = 0; x < 4; x++) df[4 * y + x] = o[16 * y + x] - ((pp[y * WST + x + oA] + pp[y * WST + x + oB] + 1) >> 1);
+                sat = satd4x4(df, had);
+            }
+            const int tot = row16_sum(sat);
+            if (sub == 0 && c >= min_pos) {
+                const int vx = 4 * fmx + qx + step * c_sp9[c][0], vy = 4 * fmy + qy + step * c_sp9[c][1];
+                int mc = lam * (mvbits(vx - pmvx) + mvbits(vy - pmvy));
+                if (pass == 0 && check0 && c == 0) mc -= 16 * lam;
+                s.ccost[pass][team][c] = mc + tot;
+            }
+        }
+        __syncthreads();
+        if (act) {   // JM order, strict '<' against the running minimum
+            int bpos = 0;
+            for (int c = min_pos; c < 9; c++) {
+                const int v = s.ccost[pass][team][c];
+                if (v < min_mcost) { min_mcost = v; bpos = c; }
+            }
+            qx += step * c_sp9[bpos][0];
+            qy += step * c_sp9[bpos][1];
+        }
+    }
+    if (act) {
+        const int cmx = 4 * fmx + qx, cmy = 4 * fmy + qy;
+        if (u < nsub) {
+            const int k = (by4 + u / w4) * 4 + bx4 + u % w4;
+            s.all_mv[bt][k][0] = (int16_t)cmx; s.all_mv[bt][k][1] = (int16_t)cmy;
+        }
+        if (u == 0) s.motion_cost[bt][mcidx] += min_mcost;
+    }
+    __syncthreads();
+}
+
+#define EVAL(J, BT, BX, BY) bk[J] = eval_search<J, BT, BX, BY>(s, sadp, pinfo, dx, dy0, search_range(d, BT))
+
+// one 8x8 block of P8x8: 4 stages (sub-modes 4..7 in parallel, then the 4x4 chain), then the
+// P8x8 sub-mode decision for the block and the reset of its stored MVs (via best8x8)
+template <int B8>
+__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, const uint32_t (&sadp)[NPK][8], const uint32_t (&pinfo)[NPK], int dx,
+                                           int dy0, int scx, int scy, int &best8x8, int &cost8x8) {
+    constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
+    const int team = threadIdx.x / TEAM;
+    unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
+    int pmvx, pmvy;
+    {   // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left
+        const int bt = 4 + team;
+        stage_head(d, s, true, bt, X, Y, B8, best8x8, scx, scy, pmvx, pmvy);
+        EVAL(0, 4, X, Y); EVAL(1, 5, X, Y); EVAL(2, 6, X, Y); EVAL(3, 7, X, Y);
+        stage_reduce(s, 0xF, bk);
+        stage_tail(d, s, true, bt, X, Y, B8, pmvx, pmvy, scx, scy);
+    }
+    {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right
+        const bool act = team >= 1;
+        const int bt = 4 + team, bx4 = team == 1 ? X : X + 1, by4 = team == 1 ? Y + 1 : Y;
+        stage_head(d, s, act, bt, bx4, by4, B8, best8x8, scx, scy, pmvx, pmvy);
+        EVAL(1, 5, X, Y + 1); EVAL(2, 6, X + 1, Y); EVAL(3, 7, X + 1, Y);
+        stage_reduce(s, 0xE, bk);
+        stage_tail(d, s, act, bt, bx4, by4, B8, pmvx, pmvy, scx, scy);
+    }
+    {   // stage 2: 4x4 bottom-left
+        const bool act = team == 3;
+        stage_head(d, s, act, 7, X, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
+        EVAL(3, 7, X, Y + 1);
+        stage_reduce(s, 0x8, bk);
+        stage_tail(d, s, act, 7, X, Y + 1, B8, pmvx, pmvy, scx, scy);
+    }
+    {   // stage 3: 4x4 bottom-right
+        const bool act = team == 3;
+        stage_head(d, s, act, 7, X + 1, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
+        EVAL(3, 7, X + 1, Y + 1);
+        stage_reduce(s, 0x8, bk);
+        stage_tail(d, s, act, 7, X + 1, Y + 1, B8, pmvx, pmvy, scx, scy);
+    }
+    int mc8 = BIGCOST, bm = 0;
+    for (int mode = 4; mode <= 7; mode++) {
+        if (!d.inter_search[mode]) continue;
+        const int c = s.motion_cost[mode][B8];
+        if (c < mc8) { mc8 = c; bm = mode; }
+    }
+    best8x8 |= bm << (4 * B8);
+    cost8x8 += mc8;
+}
+
+// motion-search roles (1: 16x16/16x8/8x16, 2: P8x8)
+template <int ROLE>
+__device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int mby) {
+    const int tid = threadIdx.x, team = tid / TEAM;
+    const int W = d.W, sr = d.sr, side = d.side;
+    const int pix_x = 16 * mbx, pix_y = 16 * mby;
+    const bool prof = prof_mb_here(d, mbx, mby);
+    const int pb = ROLE == 2 ? 0 : 8;
+    PSTAMP(pb);
+    if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    if (tid >= 256 && tid < 266) load_border(d, s.bd, tid - 256, mbx, mby);
+    if (tid >= 512 && tid < 544) s.motion_cost[(tid - 512) >> 2][tid & 3] = 0;
+    __syncthreads();
+    // SetupFastFullPelSearch: centre = 16x16 MVP / 4 (trunc), clamped to +-SR
+    int pcx, pcy;
+    set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
+    const int scx = iclip(-sr, sr, pcx / 4), scy = iclip(-sr, sr, pcy / 4);
+    uint8_t *G = s.planes;
+    const int wdim = 2 * sr + 16 + 2 * WM;
+    {
+        const int X0 = pix_x + scx - sr - WM, Y0 = pix_y + scy - sr - WM;
+        for (int i = tid; i < wdim * WST; i += NTA) {
+            int y = i / WST, x = i - y * WST;
+            G[i] = x < wdim ? d.refY[iclip(0, d.H - 1, Y0 + y) * W + iclip(0, W - 1, X0 + x)] : 0;
+        }
+        if (tid < 32) G[wdim * WST + tid] = 0;
+    }
+    __syncthreads();
+    PSTAMP(pb + 1);
+    // ---- 16 4x4 SADs for this thread's column strip of NPK positions (registers)
+    const int nstrips = (side + NPK - 1) / NPK;
+    const bool sact = tid < side * nstrips;
+    const int dx = sact ? tid % side : 0, dy0 = sact ? (tid / side) * NPK : 0;
+    uint32_t sadp[NPK][8];
+    {
+        const uint4 *og = reinterpret_cast<const uint4 *>(s.org);   // LDS broadcast, one MB row per read
+        uint32_t acc[NPK][4];
+#pragma unroll
+        for (int k = 0; k < NPK; k++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[k][b] = 0;
+        const int wx = dx + WM;
+        const uint32_t sel = wx & 3;
+        const uint8_t *wb = G + (dy0 + WM) * WST + (wx & ~3);
+#pragma unroll
+        for (int r = 0; r < 16 + NPK - 1; r++) {
+            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(wb + r * WST);
+            const uint32_t a0 = w32[0], a1 = w32[1], a2 = w32[2], a3 = w32[3], a4 = w32[4];
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sel), w1 = __builtin_amdgcn_alignbyte(a2, a1, sel);
+            const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sel), w3 = __builtin_amdgcn_alignbyte(a4, a3, sel);
+#pragma unroll
+            for (int k = 0; k < NPK; k++) {
+                const int mr = r - k;
+                if (mr < 0 || mr > 15) continue;
+                const uint4 o = og[mr];
+                acc[k][0] = __builtin_amdgcn_sad_u8(w0, o.x, acc[k][0]);
+                acc[k][1] = __builtin_amdgcn_sad_u8(w1, o.y, acc[k][1]);
+                acc[k][2] = __builtin_amdgcn_sad_u8(w2, o.z, acc[k][2]);
+                acc[k][3] = __builtin_amdgcn_sad_u8(w3, o.w, acc[k][3]);
+                if ((mr & 3) == 3) {
+                    sadp[k][2 * (mr >> 2)] = acc[k][0] | (acc[k][1] << 16);
+                    sadp[k][2 * (mr >> 2) + 1] = acc[k][2] | (acc[k][3] << 16);
+                    acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
+                }
+            }
+        }
+    }
+    uint32_t pinfo[NPK];   // JM order (13 bits) | Chebyshev radius << 16; invalid: radius 0xFFFF
+#pragma unroll
+    for (int k = 0; k < NPK; k++) {
+        const int dy = dy0 + k, rx = dx - sr, ry = dy - sr;
+        if (!sact || dy >= side) pinfo[k] = 0xFFFF1FFFu;
+        else if (rx == -scx && ry == -scy) pinfo[k] = 0;   // the (0,0) pre-check position: order 0, never range-limited
+        else pinfo[k] = (uint32_t)(spiral_index(rx, ry) + 1) | ((uint32_t)max(abs(rx), abs(ry)) << 16);
+    }
+    // ---- half-pel planes of the window: h1 (vertical intermediates), b, h; then j
+    {
+        const int lo = WM - 1, n = 2 * sr + 18, h1w = wdim - 1;
+        uint8_t *PB = s.planes + PLS, *PH = s.planes + 2 * PLS;
+        for (int i = tid; i < h1w * n; i += NTA) {
+            const int y = lo + i / h1w, x = 1 + i % h1w;
+            const uint8_t *g = G + (y - 2) * WST + x;
+            s.h1[y * WST + x] = (int16_t)tap6(g[0], g[WST], g[2 * WST], g[3 * WST], g[4 * WST], g[5 * WST]);
+        }
+        for (int i = tid; i < n * n; i += NTA) {
+            const int y = lo + i / n, x = lo + i % n;
+            const uint8_t *g = G + y * WST + x;
+            PB[y * WST + x] = (uint8_t)clip255((tap6(g[-2], g[-1], g[0], g[1], g[2], g[3]) + 16) >> 5);
+            PH[y * WST + x] = (uint8_t)clip255((tap6(g[-2 * WST], g[-WST], g[0], g[WST], g[2 * WST], g[3 * WST]) + 16) >> 5);
+        }
+        __syncthreads();
+        uint8_t *PJ = s.planes + 3 * PLS;
+        for (int i = tid; i < n * n; i += NTA) {
+            const int y = lo + i / n, x = lo + i % n;
+            const int16_t *h = s.h1 + y * WST + x;
+            PJ[y * WST + x] = (uint8_t)clip255((tap6(h[-2], h[-1], h[0], h[1], h[2], h[3]) + 512) >> 10);
+        }
+        // j is first read after the next stage's barriers
+    }
+    PSTAMP(pb + 2);
+    MbScratch *scr = d.scr + mby * d.mbw + mbx;
+    if constexpr (ROLE == 1) {
+        unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
+        int pmvx, pmvy;
+        {   // stage 0: 16x16, 16x8 upper, 8x16 left
+            const bool act = team < 3;
+            const int bt = 1 + team;
+            stage_head(d, s, act, bt, 0, 0, 0, 0, scx, scy, pmvx, pmvy);
+            EVAL(0, 1, 0, 0); EVAL(1, 2, 0, 0); EVAL(2, 3, 0, 0);
+            stage_reduce(s, 0x7, bk);
+            stage_tail(d, s, act, bt, 0, 0, 0, pmvx, pmvy, scx, scy);
+        }
+        {   // stage 1: 16x8 lower, 8x16 right
+            const bool act = team == 1 || team == 2;
+            const int bt = 1 + team, bx4 = team == 2 ? 2 : 0, by4 = team == 1 ? 2 : 0;
+            stage_head(d, s, act, bt, bx4, by4, 0, 0, scx, scy, pmvx, pmvy);
+            EVAL(1, 2, 0, 2); EVAL(2, 3, 2, 0);
+            stage_reduce(s, 0x6, bk);
+            stage_tail(d, s, act, bt, bx4, by4, 1, pmvx, pmvy, scx, scy);
+        }
+        // results: MVs of types 1..3, partition costs, FindSkipModeMotionVector
+        if (tid < 96) {
+            const int m = 1 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
+            scr->all_mv[m][k][c] = s.all_mv[m][k][c];
+        }
+        if (tid >= 128 && tid < 140) { const int m = 1 + (tid - 128) / 4, k = tid & 3; scr->motion_cost[m][k] = s.motion_cost[m][k]; }
+        if (tid == 192) {
+            NbBorder nb{s.bd};
+            int ra = -1, ax = 0, ay = 0, rb = -1, bx = 0, by = 0;
+            const bool aa = nb(-1, 0, ra, ax, ay), ab = nb(0, -1, rb, bx, by);
+            const bool zl = !aa || (ra == 0 && ax == 0 && ay == 0), za = !ab || (rb == 0 && bx == 0 && by == 0);
+            scr->skipx = (za || zl) ? 0 : pcx;
+            scr->skipy = (za || zl) ? 0 : pcy;
+        }
+        PSTAMP(pb + 3);
+    } else {
+        int best8x8 = 0, cost8x8 = 0;
+        p8x8_block<0>(d, s, sadp, pinfo, dx, dy0, scx, scy, best8x8, cost8x8);
+        PSTAMP(3);
+        p8x8_block<1>(d, s, sadp, pinfo, dx, dy0, scx, scy, best8x8, cost8x8);
+        PSTAMP(4);
+        p8x8_block<2>(d, s, sadp, pinfo, dx, dy0, scx, scy, best8x8, cost8x8);
+        PSTAMP(5);
+        p8x8_block<3>(d, s, sadp, pinfo, dx, dy0, scx, scy, best8x8, cost8x8);
+        if (tid < 128) {
+            const int m = 4 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
+            scr->all_mv[m][k][c] = s.all_mv[m][k][c];
+        }
+        if (tid >= 128 && tid < 144) { const int m = 4 + (tid - 128) / 4, k = tid & 3; scr->motion_cost[m][k] = s.motion_cost[m][k]; }
+        if (tid == 192) { scr->best8x8 = best8x8; scr->cost8x8 = cost8x8; }
+        PSTAMP(6);
+    }
+}
+
+// MB-relative luma reconstruction sample for intra prediction (border rows/columns from LDS)
+__device__ __forceinline__ int lpix(const IntraS &s, int x, int y) {
+    if (y < 0) return s.rtop[x + 1];
+    if (x < 0) return s.rleft[y];
+    return s.rec[16 * y + x];
+}
+
+// intra role: wave 0 Intra4x4 (wave-synchronous, no workgroup barriers), wave 1 Intra16x16,
+// wave 2 chroma intra mode. The three decisions are independent of each other.
+__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, Wc = d.Wc;
+    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
+    if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    else if (tid < 384) {
+        const int uv = (tid - 256) >> 6, k = tid & 63;
+        s.orgc[uv][k] = (uv ? d.orgV : d.orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
+    } else if (tid < 394) load_border(d, s.bd, tid - 384, mbx, mby);
+    else if (tid >= 400 && tid < 421) {            // luma row y = -1, x = -1..19
+        const int x = tid - 401;
+        const bool av = x < 0 ? avTL : x < 16 ? avT : avTR;
+        s.rtop[x + 1] = av ? d.recY[(pix_y - 1) * W + pix_x + x] : 0;
+    } else if (tid >= 448 && tid < 464) {
+        const int y = tid - 448;
+        s.rleft[y] = avL ? d.recY[(pix_y + y) * W + pix_x - 1] : 0;
+    } else if (tid >= 464 && tid < 482) {          // chroma rows y = -1, x = -1..7
+        const int i = tid - 464, uv = i / 9, x = i - 9 * uv - 1;
+        const bool av = x < 0 ? avTL : avT;
+        s.ctop[uv][x + 1] = av ? (uv ? d.recV : d.recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
+    } else if (tid >= 512 && tid < 528) {
+        const int i = tid - 512, uv = i >> 3, y = i & 7;
+        s.cleft[uv][y] = avL ? (uv ? d.recV : d.recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
+    }
+    __syncthreads();
+    MbScratch *scr = d.scr + mby * d.mbw + mbx;
+    const int lambda = d.lambda_mode, qp = d.qp, had = d.use_hadamard;
+    if (wave == 0) {
+        // ======== Mode_Decision_for_Intra4x4Macroblock: 16 blocks, 9 modes x 16 pixels per pass
+        const bool prof = prof_mb_here(d, mbx, mby, 0);
+        PSTAMP(12);
+        const int q_bits = 15 + qp / 6;
+        const int qpk = d.slice_type == JMH_P_SLICE ? (1 << q_bits) / 6 : (1 << q_bits) / 3;
+        const int l = lane & 15, g = lane >> 4;
+        int i4cost = 0, i4cbp = 0, i4blk = 0;
+        for (int b8 = 0; b8 < 4; b8++) {
+            int cost8 = 6 * lambda;                                  // (int)floor(6*lambda+0.4999)
+            for (int b4 = 0; b4 < 4; b4++) {
+                const int bx = 8 * (b8 & 1) + 4 * (b4 & 1), by = 8 * (b8 >> 1) + 4 * (b4 >> 1);
+                const int blk = (by >> 2) * 4 + (bx >> 2);
+                const bool up = by > 0 || avT, left = bx > 0 || avL;
+                const bool ul = (bx > 0 && by > 0) || (bx == 0 && by > 0 && avL) || (bx > 0 && by == 0 && avT) || (bx == 0 && by == 0 && avTL);
+                bool ur = by == 0 ? (bx + 4 <= 15 ? avT : avTR) : (bx + 4 <= 15);
+                if ((bx == 4 || bx == 12) && (by == 4 || by == 12)) ur = false;
+                if (lane < 13) {
+                    int v;
+                    if (lane == 0) v = ul ? lpix(s, bx - 1, by - 1) : 0;
+                    else if (lane <= 4) v = up ? lpix(s, bx + lane - 1, by - 1) : 0;
+                    else if (lane <= 8) v = up ? lpix(s, ur ? bx + lane - 1 : bx + 3, by - 1) : 0;
+                    else v = left ? lpix(s, bx - 1, by + lane - 9) : 0;
+                    s.i4P[lane] = v;
+                }
+                const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + (bx >> 2)];
+                const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + (by >> 2)];
+                const int mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
+                wave_lds_sync();
+                const int o = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];
+                int pv[3], cst[3];
+#pragma unroll
+                for (int it = 0; it < 3; it++) {
+                    const int m = 4 * it + g;
+                    pv[it] = 0; cst[it] = BIGCOST + 1;
+                    if (m < 9) {
+                        const bool avm = m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul);
+                        const int p = i4_pred_px(s.i4P, up, left, m, l & 3, l >> 2);
+                        const int sat = lane_satd(o - p, l, had);
+                        pv[it] = p;
+                        cst[it] = avm ? (m == mpm ? 0 : 4 * lambda) + sat : BIGCOST + 1;
+                    }
+                }
+                int best = 0, bc = BIGCOST;
+#pragma unroll
+                for (int m = 0; m < 9; m++) {
+                    const int c = __builtin_amdgcn_readlane(cst[m >> 2], 16 * (m & 3));
+                    if (c < bc) { bc = c; best = m; }
+                }
+                const int src = (best >> 2) == 0 ? pv[0] : (best >> 2) == 1 ? pv[1] : pv[2];
+                const int pp = __shfl(src, 16 * (best & 3) + l, 64);
+                unsigned nz = 0;
+                if (lane < 16) {                                       // dct_luma on the chosen prediction
+                    const int c = lane_fwd4x4(o - pp, l);
+                    int lev, dq, cc;
+                    nz = lane_quant(c, l, qp, qpk, false, lev, dq, cc);
+                    scr->i4lev[blk][l] = (int16_t)lev;
+                    s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (uint8_t)lane_inv4x4(dq, l, pp);
+                    if (l == 0) s.ipred_cur[blk] = (int8_t)best;
+                }
+                nz = __builtin_amdgcn_readlane(nz, 0);
+                cost8 += bc;
+                if (nz) { i4cbp |= 1 << b8; i4blk |= 1 << blk; }
+                wave_lds_sync();
+            }
+            i4cost += cost8;
+        }
+        if (lane == 0) { scr->i4cost = i4cost; scr->i4cbp = i4cbp; scr->i4blk = i4blk; }
+        if (lane < 16) scr->ipred[lane] = s.ipred_cur[lane];
+        reinterpret_cast<uint32_t *>(scr->i4rec)[lane] = reinterpret_cast<const uint32_t *>(s.rec)[lane];
+        PSTAMP(13);
+    } else if (wave == 1) {
+        // ======== intrapred_luma_16x16 + find_sad_16x16: 4 modes x 16 blocks = 64 lanes
+        const bool prof = prof_mb_here(d, mbx, mby, 1);
+        const int m = lane >> 4, b = lane & 15, ox = (b & 3) * 4, oy = (b >> 2) * 4;
+        const uint8_t *T = s.rtop + 1, *L = s.rleft;
+        const I16Par par = i16_params(T, L, avT, avL);
+        int mm[16], t[16];
+        for (int yy = 0; yy < 4; yy++)
+            for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = s.org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy);
+        for (int yy = 0; yy < 4; yy++) {
+            int *r = mm + 4 * yy;
+            int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
+            t[4 * yy] = a0 + a1; t[4 * yy + 2] = a0 - a1; t[4 * yy + 1] = a2 + a3; t[4 * yy + 3] = a3 - a2;
+        }
+        int acs = 0, dcc = 0;
+        for (int xx = 0; xx < 4; xx++) {
+            int a0 = t[xx] + t[12 + xx], a1 = t[4 + xx] + t[8 + xx], a2 = t[4 + xx] - t[8 + xx], a3 = t[xx] - t[12 + xx];
+            int o0 = a0 + a1, o2 = a0 - a1, o1 = a2 + a3, o3 = a3 - a2;
+            if (xx == 0) dcc = o0; else acs += abs(o0);
+            acs += abs(o1) + abs(o2) + abs(o3);
+        }
+        const int cost = row16_sum(acs) + lane_had_abs(dcc / 4, b);
+        const bool av16[4] = {avT, avL, true, avT && avL && avTL};
+        int best = MAX_VALUE, i16mode = 2;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int c = __builtin_amdgcn_readlane(cost, 16 * k);
+            if (av16[k] && c < best) { best = c; i16mode = k; }
+        }
+        if (lane == 0) { scr->i16cost = best / 2; scr->i16mode = i16mode; }
+        PSTAMP(14);
+    } else if (wave == 2) {
+        // ======== IntraChromaPrediction8x8 mode decision: 4 modes x 2 components x 4 blocks
+        const bool prof = prof_mb_here(d, mbx, mby, 2);
+        int sat = 0;
+        if (lane < 32) {
+            const int m = lane >> 3, uv = (lane >> 2) & 1, b = lane & 3, xo = (b & 1) * 4, yo = (b >> 1) * 4;
+            const uint8_t *T = s.ctop[uv] + 1, *L = s.cleft[uv];
+            int df[16];
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++)
+                    df[4 * y + x] = s.orgc[uv][(yo + y) * 8 + xo + x] - chroma_pred_px(T, L, s.ctop[uv][0], avT, avL, m, xo + x, yo + y);
+            sat = satd4x4(df, had);
+        }
+        const bool cav[4] = {true, avL, avT, avT && avL && avTL};
+        int minc = BIGCOST, c_mode = 0;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            int c = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) c += __builtin_amdgcn_readlane(sat, 8 * m + q);
+            if (cav[m] && c < minc) { minc = c; c_mode = m; }
+        }
+        if (lane == 0) scr->c_mode = c_mode;
+        PSTAMP(15);
+    }
+}
+
+__global__ __launch_bounds__(NTA) void k_mb_analyse(DevParams d) {
+    __shared__ AnalyseS s;
+    const int n = d.ndiag;
+    int role = 0, i = blockIdx.x;
+    if (d.slice_type == JMH_P_SLICE) { role = 2 - (int)blockIdx.x / n; i = blockIdx.x % n; }
+    const int mby = d.y_min + i, mbx = d.diag - 2 * mby;
+    if (role == 2) me_role<2>(d, s.me, mbx, mby);
+    else if (role == 1) me_role<1>(d, s.me, mbx, mby);
+    else intra_role(d, s.in, mbx, mby);
+}
+
+hipError_t jmh_launch_analyse(const DevParams &p, hipStream_t st) {
+    const int nblocks = p.slice_type == JMH_P_SLICE ? 3 * p.ndiag : p.ndiag;
+    hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, p);
+    return hipGetLastError();
+}

@@ -1,0 +1,351 @@
+// jmh_common.h — device helpers shared by the gfx950 kernels: JM tables, H.264 integer
+// arithmetic, 16-lane transform primitives (wave shuffles / DPP), SATD, MV prediction.
+// Every translation unit gets its own (static) copy of the constant tables.
+#pragma once
+#include "jmh_device.h"
+
+#define MAX_VALUE 999999
+#define WM 4                                  // window margin (6-tap support of sub-pel samples)
+#define WIN_DIM_MAX (2 * SRMAX + 16 + 2 * WM) // 88
+#define WST 92                                // window row stride (>= WIN_DIM_MAX + 3, mult of 4)
+
+// quantisation / dequantisation coefficients by class: (even,even), (odd,odd), mixed
+static __constant__ int c_q3[6][3] = {{13107, 5243, 8066}, {11916, 4660, 7490}, {10082, 4194, 6554},
+                                      {9362, 3647, 5825},  {8192, 3355, 5243},  {7282, 2893, 4559}};
+static __constant__ int c_dq3[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
+static __constant__ int c_qpc[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
+                                     18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 32, 33,
+                                     34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+static __constant__ int c_blc[8][2] = {{16, 16}, {16, 16}, {16, 8}, {8, 16}, {8, 8}, {8, 4}, {4, 8}, {4, 4}};
+// sub-pel candidate offsets = spiral entries 0..8 (Init_Motion_Search_Module [J])
+static __constant__ int c_sp9[9][2] = {{0, 0}, {0, -1}, {0, 1}, {-1, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {1, 1}};
+// quarter-pel sample = average of two half-pel-grid samples A, B per phase ((G+b+1)>>1 ...
+// (m+s+1)>>1, H.264 8.4.2.2.1; a full/half sample has A == B). Offsets in half-grid units
+// packed as nibbles dxA, dyA, dxB, dyB (high to low); phase = (qy & 3) * 4 + (qx & 3).
+static __constant__ uint16_t c_qoff[16] = {
+    0x0000, 0x0010, 0x1010, 0x2010,   // G, a, b, c
+    0x0001, 0x1001, 0x1011, 0x1021,   // d, e, f, g
+    0x0101, 0x0111, 0x1111, 0x1121,   // h, i, j, k
+    0x0201, 0x0112, 0x1112, 0x2112};  // n, p, q, r
+// 4x4 frame zig-zag (scan position -> raster), packed as nibbles
+#define SCAN_PACKED 0xFEB7ADC963258410ULL
+__device__ __forceinline__ int scan_of(int k) { return (int)((SCAN_PACKED >> (4 * k)) & 15); }
+
+__device__ __forceinline__ int iclip(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ int clip255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+__device__ __forceinline__ int isign(int a, int b) { return b < 0 ? -abs(a) : abs(a); }
+__device__ __forceinline__ int mvbits(int v) { return v == 0 ? 1 : 2 * (31 - __clz(abs(v))) + 3; }
+__device__ __forceinline__ int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
+// JM spiral index of relative position (x, y) (Init_Motion_Search_Module ordering)
+__device__ __forceinline__ int spiral_index(int x, int y) {
+    int ax = abs(x), ay = abs(y), l = max(ax, ay);
+    if (l == 0) return 0;
+    int base = (2 * l - 1) * (2 * l - 1);
+    if (ay == l && ax < l) return base + 2 * (x + l - 1) + (y > 0);
+    return base + 2 * (2 * l - 1) + 2 * (y + l) + (x > 0);
+}
+__device__ __forceinline__ void spiral_pos(int k, int &x, int &y) {
+    if (k == 0) { x = y = 0; return; }
+    int l = 1;
+    while ((2 * l + 1) * (2 * l + 1) <= k) l++;
+    int o = k - (2 * l - 1) * (2 * l - 1);
+    if (o < 2 * (2 * l - 1)) { x = (o >> 1) - l + 1; y = (o & 1) ? l : -l; }
+    else { o -= 2 * (2 * l - 1); y = (o >> 1) - l; x = (o & 1) ? l : -l; }
+}
+// COEFF_COST [J] of a |level| == 1 coefficient by preceding zero run
+__device__ __forceinline__ int coeff_cost_run(int run) { return run == 0 ? 3 : run <= 2 ? 2 : run <= 5 ? 1 : 0; }
+
+// ---- cross-lane helpers ----------------------------------------------------------------
+// DPP: quad_perm [1,0,3,2] (0xB1), [2,3,0,1] (0x4E), row_half_mirror (0x141), row_mirror (0x140)
+__device__ __forceinline__ int dpp_(int v, int ctrl) {
+    switch (ctrl) {
+    case 0xB1: return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);
+    case 0x4E: return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);
+    case 0x141: return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);
+    default: return __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false);
+    }
+}
+// sum over each aligned 16-lane row (all 16 lanes must be active); every lane gets the sum
+__device__ __forceinline__ int row16_sum(int v) {
+    v += dpp_(v, 0xB1);
+    v += dpp_(v, 0x4E);
+    v += dpp_(v, 0x141);
+    v += dpp_(v, 0x140);
+    return v;
+}
+// minimum over the whole (fully active) wave, wave-uniform result
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+    v = min(v, (unsigned)dpp_((int)v, 0xB1));
+    v = min(v, (unsigned)dpp_((int)v, 0x4E));
+    v = min(v, (unsigned)dpp_((int)v, 0x141));
+    v = min(v, (unsigned)dpp_((int)v, 0x140));
+    unsigned a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    unsigned c = __builtin_amdgcn_readlane(v, 32), e = __builtin_amdgcn_readlane(v, 48);
+    return min(min(a, b), min(c, e));
+}
+// compiler + hardware ordering of LDS traffic between lanes of one wave (wave-synchronous code)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ======================================================================================
+//  16-lane 4x4 transform primitives (lane l of a 16-lane group holds raster element l)
+// ======================================================================================
+__device__ __forceinline__ int g16(int v, int src) { return __shfl(v, (int)(threadIdx.x & 48) + src, 64); }
+
+// forward 4x4 core transform (dct_luma [J]): rows then columns
+__device__ __forceinline__ int lane_fwd4x4(int r, int l) {
+    int y = l >> 2, x = l & 3;
+    int v0 = g16(r, 4 * y), v1 = g16(r, 4 * y + 1), v2 = g16(r, 4 * y + 2), v3 = g16(r, 4 * y + 3);
+    int p0 = v0 + v3, p3 = v0 - v3, p1 = v1 + v2, p2 = v1 - v2;
+    int t = x == 0 ? p0 + p1 : x == 1 ? 2 * p3 + p2 : x == 2 ? p0 - p1 : p3 - 2 * p2;
+    int u0 = g16(t, x), u1 = g16(t, 4 + x), u2 = g16(t, 8 + x), u3 = g16(t, 12 + x);
+    p0 = u0 + u3; p3 = u0 - u3; p1 = u1 + u2; p2 = u1 - u2;
+    return y == 0 ? p0 + p1 : y == 1 ? 2 * p3 + p2 : y == 2 ? p0 - p1 : p3 - 2 * p2;
+}
+// inverse 4x4 (8.5.12.2, rows first) + reconstruction clip((x + (pred << 6) + 32) >> 6)
+__device__ __forceinline__ int lane_inv4x4(int dq, int l, int pred) {
+    int y = l >> 2, x = l & 3;
+    int d0 = g16(dq, 4 * y), d1 = g16(dq, 4 * y + 1), d2 = g16(dq, 4 * y + 2), d3 = g16(dq, 4 * y + 3);
+    int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+    int t = x == 0 ? e0 + e3 : x == 1 ? e1 + e2 : x == 2 ? e1 - e2 : e0 - e3;
+    int f0 = g16(t, x), f1 = g16(t, 4 + x), f2 = g16(t, 8 + x), f3 = g16(t, 12 + x);
+    e0 = f0 + f2; e1 = f0 - f2; e2 = (f1 >> 1) - f3; e3 = f1 + (f3 >> 1);
+    int o = y == 0 ? e0 + e3 : y == 1 ? e1 + e2 : y == 2 ? e1 - e2 : e0 - e3;
+    return clip255((o + (pred << 6) + 32) >> 6);
+}
+// quantisation (dct_luma / dct_chroma AC [J]) of coefficient c at raster l.
+//   lev_scan: signed level at SCAN position l; dq: dequantised coefficient at raster l;
+//   cost: COEFF_COST sum over the block (all 16 lanes); returns the scan-order non-zero mask.
+__device__ __forceinline__ unsigned lane_quant(int c, int l, int qp, int qp_const, bool ac_only, int &lev_scan, int &dq, int &cost) {
+    const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per;
+    const int x = l & 3, y = l >> 2;
+    const int cls = ((x | y) & 1) == 0 ? 0 : ((x & y) & 1) ? 1 : 2;
+    const int qc = cls == 0 ? c_q3[qp_rem][0] : cls == 1 ? c_q3[qp_rem][1] : c_q3[qp_rem][2];
+    const int dqc = cls == 0 ? c_dq3[qp_rem][0] : cls == 1 ? c_dq3[qp_rem][1] : c_dq3[qp_rem][2];
+    int level = (abs(c) * qc + qp_const) >> q_bits;
+    if (ac_only && l == 0) level = 0;
+    dq = level ? isign(level * dqc << qp_per, c) : 0;
+    const int sr = scan_of(l);
+    const int lvs = g16(level, sr), cs = g16(c, sr);
+    const unsigned long long bal = __ballot(lvs != 0);
+    const unsigned m = (unsigned)(bal >> (threadIdx.x & 48)) & 0xFFFFu;
+    int k = 0;
+    if (lvs) {
+        unsigned below = m & ((1u << l) - 1u);
+        int prev = below ? 31 - __clz(below) : (ac_only ? 0 : -1);
+        k = lvs > 1 ? MAX_VALUE : coeff_cost_run(l - prev - 1);
+    }
+    cost = row16_sum(k);
+    lev_scan = lvs ? isign(lvs, cs) : 0;
+    return m;
+}
+
+// single-thread SATD() [J]: 4x4 Hadamard sum >> 1, or SAD
+__device__ __forceinline__ int satd4x4(const int d[16], int had) {
+    int s = 0;
+    if (!had) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) s += abs(d[k]);
+        return s;
+    }
+    int m[16];
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+        int a0 = d[x] + d[12 + x], a1 = d[4 + x] + d[8 + x], a2 = d[4 + x] - d[8 + x], a3 = d[x] - d[12 + x];
+        m[x] = a0 + a1; m[8 + x] = a0 - a1; m[4 + x] = a2 + a3; m[12 + x] = a3 - a2;
+    }
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+        int *r = m + 4 * y;
+        int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
+        s += abs(a0 + a1) + abs(a0 - a1) + abs(a2 + a3) + abs(a3 - a2);
+    }
+    return s >> 1;
+}
+// 16-lane sum of |4x4 Hadamard| (no >>1); every lane of the (fully active) group gets the sum
+__device__ __forceinline__ int lane_had_abs(int dv, int l) {
+    int y = l >> 2, x = l & 3;
+    int v0 = g16(dv, 4 * y), v1 = g16(dv, 4 * y + 1), v2 = g16(dv, 4 * y + 2), v3 = g16(dv, 4 * y + 3);
+    int a0 = v0 + v3, a1 = v1 + v2, a2 = v1 - v2, a3 = v0 - v3;
+    int t = x == 0 ? a0 + a1 : x == 1 ? a0 - a1 : x == 2 ? a2 + a3 : a3 - a2;
+    int u0 = g16(t, x), u1 = g16(t, 4 + x), u2 = g16(t, 8 + x), u3 = g16(t, 12 + x);
+    a0 = u0 + u3; a1 = u1 + u2; a2 = u1 - u2; a3 = u0 - u3;
+    return row16_sum(abs(y == 0 ? a0 + a1 : y == 1 ? a0 - a1 : y == 2 ? a2 + a3 : a3 - a2));
+}
+// 16-lane SATD() [J]
+__device__ __forceinline__ int lane_satd(int dv, int l, int had) {
+    return had ? lane_had_abs(dv, l) >> 1 : row16_sum(abs(dv));
+}
+
+// SetMotionVectorPredictor [J] / H.264 8.4.1.3 (list 0, ref 0). NB(xN, yN, ref, mx, my)
+// returns the availability of the 4x4 neighbour covering MB-relative pixel (xN, yN).
+template <class NB>
+__device__ __forceinline__ void set_mvp(const NB &nb, int bx4, int by4, int bsx, int bsy, int &px, int &py) {
+    int mb_x = 4 * bx4, mb_y = 4 * by4;
+    int ra = -1, rb = -1, rc = -1, rd = -1, ax = 0, ay = 0, bxv = 0, byv = 0, cx = 0, cy = 0, dx = 0, dy = 0;
+    bool av_a = nb(mb_x - 1, mb_y, ra, ax, ay);
+    bool av_b = nb(mb_x, mb_y - 1, rb, bxv, byv);
+    bool av_c = nb(mb_x + bsx, mb_y - 1, rc, cx, cy);
+    bool av_d = nb(mb_x - 1, mb_y - 1, rd, dx, dy);
+    if (mb_y > 0) {
+        if (mb_x < 8) {
+            if (mb_y == 8) { if (bsx == 16) av_c = false; }
+            else if (mb_x + bsx == 8) av_c = false;
+        } else if (mb_x + bsx == 16) av_c = false;
+    }
+    if (!av_c) { av_c = av_d; rc = rd; cx = dx; cy = dy; }
+    int rL = av_a ? ra : -1, rU = av_b ? rb : -1, rUR = av_c ? rc : -1;
+    int type = 0;
+    if (rL == 0 && rU != 0 && rUR != 0) type = 1;
+    else if (rL != 0 && rU == 0 && rUR != 0) type = 2;
+    else if (rL != 0 && rU != 0 && rUR == 0) type = 3;
+    if (bsx == 8 && bsy == 16) { if (mb_x == 0) { if (rL == 0) type = 1; } else if (rUR == 0) type = 3; }
+    else if (bsx == 16 && bsy == 8) { if (mb_y == 0) { if (rU == 0) type = 2; } else if (rL == 0) type = 1; }
+    int A[2] = {av_a ? ax : 0, av_a ? ay : 0}, B[2] = {av_b ? bxv : 0, av_b ? byv : 0}, C[2] = {av_c ? cx : 0, av_c ? cy : 0};
+    int p[2];
+#pragma unroll
+    for (int hv = 0; hv < 2; hv++) {
+        int a = A[hv], b = B[hv], c = C[hv];
+        if (type == 1) p[hv] = a;
+        else if (type == 2) p[hv] = b;
+        else if (type == 3) p[hv] = c;
+        else if (!(av_b || av_c)) p[hv] = a;
+        else p[hv] = a + b + c - min(a, min(b, c)) - max(a, max(b, c));
+    }
+    px = p[0]; py = p[1];
+}
+
+// border neighbour cells of an MB: 0..5 = row y4 = -1 (x4 = -1..4), 6..9 = column x4 = -1 (y4 = 0..3)
+struct Border {
+    int16_t mv[10][2];
+    int8_t ref[10];                      // -2: not available, -1: intra, 0: ref 0
+    int8_t ipm[10];                      // Intra4x4PredMode, -1 unavailable
+};
+__device__ __forceinline__ int border_cell(int xN, int yN) {   // -1: inside the MB or unavailable
+    if (yN < 0) { int b = xN >> 2; return b > 4 ? -1 : b + 1; }
+    if (xN < 0) return yN > 15 ? -1 : 6 + (yN >> 2);
+    return -1;
+}
+// prefetch by threads t < 10 of the workgroup
+__device__ __forceinline__ void load_border(const DevParams &d, Border &b, int t, int mbx, int mby) {
+    const int W4 = d.W >> 2;
+    int by4 = t < 6 ? -1 : t - 6, bx4 = t < 6 ? t - 1 : -1;
+    bool av = by4 < 0 ? (bx4 < 0 ? (mbx > 0 && mby > 0) : bx4 > 3 ? (mby > 0 && mbx + 1 < d.mbw) : mby > 0) : mbx > 0;
+    int ref = -2, mx = 0, my = 0, ipm = -1;
+    if (av) {
+        int a = (4 * mby + by4) * W4 + 4 * mbx + bx4;
+        ref = d.refidx[a]; mx = d.mv[2 * a]; my = d.mv[2 * a + 1]; ipm = d.ipred[a];
+    }
+    b.ref[t] = (int8_t)ref; b.mv[t][0] = (int16_t)mx; b.mv[t][1] = (int16_t)my; b.ipm[t] = (int8_t)ipm;
+}
+// neighbour view with only border cells (16x16 MVP, skip MV)
+struct NbBorder {
+    const Border &b;
+    __device__ bool operator()(int xN, int yN, int &ref, int &mx, int &my) const {
+        if (yN > 15 || (xN > 15 && yN >= 0)) return false;
+        int c = border_cell(xN, yN);
+        if (c < 0 || b.ref[c] == -2) return false;
+        ref = b.ref[c]; mx = b.mv[c][0]; my = b.mv[c][1];
+        return true;
+    }
+};
+
+// Intra4x4 prediction sample (8.3.1.2) of mode m at pixel (x,y); P[0] = p[-1,-1],
+// P[1+i] = p[i,-1] (i = 0..7), P[9+j] = p[-1,j]
+__device__ __forceinline__ int i4_pred_px(const int *P, int up, int left, int m, int x, int y) {
+#define PT(i) P[1 + (i)]
+#define PL(j) ((j) < 0 ? P[0] : P[9 + (j)])
+    switch (m) {
+    case 0: return PT(x);
+    case 1: return PL(y);
+    case 2:
+        if (up && left) return (PT(0) + PT(1) + PT(2) + PT(3) + PL(0) + PL(1) + PL(2) + PL(3) + 4) >> 3;
+        if (left) return (PL(0) + PL(1) + PL(2) + PL(3) + 2) >> 2;
+        if (up) return (PT(0) + PT(1) + PT(2) + PT(3) + 2) >> 2;
+        return 128;
+    case 3: return (x == 3 && y == 3) ? (PT(6) + 3 * PT(7) + 2) >> 2 : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
+    case 4:
+        if (x > y) return (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
+        if (x < y) return (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
+        return (PT(0) + 2 * P[0] + PL(0) + 2) >> 2;
+    case 5: {
+        int z = 2 * x - y;
+        if (z >= 0 && !(z & 1)) return (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
+        if (z >= 0) return (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
+        if (z == -1) return (PL(0) + 2 * P[0] + PT(0) + 2) >> 2;
+        return (PL(y - 1) + 2 * PL(y - 2) + PL(y - 3) + 2) >> 2;
+    }
+    case 6: {
+        int z = 2 * y - x;
+        if (z >= 0 && !(z & 1)) return (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
+        if (z >= 0) return (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
+        if (z == -1) return (PL(0) + 2 * P[0] + PT(0) + 2) >> 2;
+        return (PT(x - 1) + 2 * PT(x - 2) + PT(x - 3) + 2) >> 2;
+    }
+    case 7:
+        return (y & 1) ? (PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2
+                       : (PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1;
+    default: {
+        int z = x + 2 * y;
+        if (z > 5) return PL(3);
+        if (z == 5) return (PL(2) + 3 * PL(3) + 2) >> 2;
+        if (!(z & 1)) return (PL(y + (x >> 1)) + PL(y + (x >> 1) + 1) + 1) >> 1;
+        return (PL(y + (x >> 1)) + 2 * PL(y + (x >> 1) + 1) + PL(y + (x >> 1) + 2) + 2) >> 2;
+    }
+    }
+#undef PT
+#undef PL
+}
+
+// chroma DC prediction of one 4x4 chroma block (8.3.4.1-3)
+__device__ __forceinline__ int chroma_dc(const uint8_t *T, const uint8_t *L, int up, int left, int b) {
+    int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    for (int i = 0; i < 4; i++) { s0 += T[i]; s1 += T[4 + i]; s2 += L[i]; s3 += L[4 + i]; }
+    if (b == 0) return (up && left) ? (s0 + s2 + 4) >> 3 : up ? (s0 + 2) >> 2 : left ? (s2 + 2) >> 2 : 128;
+    if (b == 1) return up ? (s1 + 2) >> 2 : left ? (s2 + 2) >> 2 : 128;
+    if (b == 2) return left ? (s3 + 2) >> 2 : up ? (s0 + 2) >> 2 : 128;
+    return (up && left) ? (s1 + s3 + 4) >> 3 : up ? (s1 + 2) >> 2 : left ? (s3 + 2) >> 2 : 128;
+}
+// chroma intra prediction (8.3.4) of mode m at pixel (x, y) of one component
+__device__ __forceinline__ int chroma_pred_px(const uint8_t *T, const uint8_t *L, int Pc, int up, int left, int m, int x, int y) {
+    if (m == 0) return chroma_dc(T, L, up, left, (y >> 2) * 2 + (x >> 2));
+    if (m == 1) return L[y];
+    if (m == 2) return T[x];
+    int ih = 0, iv = 0;
+    for (int i = 1; i <= 4; i++) {
+        ih += i * (T[3 + i] - (3 - i >= 0 ? T[3 - i] : Pc));
+        iv += i * (L[3 + i] - (3 - i >= 0 ? L[3 - i] : Pc));
+    }
+    int ib = (34 * ih + 32) >> 6, ic = (34 * iv + 32) >> 6, iaa = 16 * (L[7] + T[7]);
+    return clip255((iaa + (x - 3) * ib + (y - 3) * ic + 16) >> 5);
+}
+// Intra16x16 prediction (8.3.3): mode-independent parameters, then per-pixel samples.
+// T = row y = -1 (T[-1] is the corner p[-1,-1]), L = column x = -1.
+struct I16Par { int dcv, ib, ic, iaa; };
+__device__ __forceinline__ I16Par i16_params(const uint8_t *T, const uint8_t *L, int up, int left) {
+    int st = 0, sl = 0, ih = 0, iv = 0;
+    for (int i = 0; i < 16; i++) { st += T[i]; sl += L[i]; }
+    for (int i = 1; i <= 8; i++) {
+        ih += i * (T[7 + i] - T[7 - i]);
+        iv += i * (L[7 + i] - (7 - i >= 0 ? L[7 - i] : T[-1]));
+    }
+    I16Par p;
+    p.dcv = (up && left) ? (st + sl + 16) >> 5 : up ? (st + 8) >> 4 : left ? (sl + 8) >> 4 : 128;
+    p.ib = (5 * ih + 32) >> 6; p.ic = (5 * iv + 32) >> 6; p.iaa = 16 * (L[15] + T[15]);
+    return p;
+}
+__device__ __forceinline__ int i16_pred(const I16Par &p, const uint8_t *T, const uint8_t *L, int m, int x, int y) {
+    if (m == 0) return T[x];
+    if (m == 1) return L[y];
+    if (m == 2) return p.dcv;
+    return clip255((p.iaa + (x - 7) * p.ib + (y - 7) * p.ic + 16) >> 5);
+}
+
+// debug phase profiling of one macroblock (DevParams::prof): lane 0 of wave w of the matching group
+__device__ __forceinline__ bool prof_mb_here(const DevParams &d, int mbx, int mby, int w = 0) {
+    return d.prof && threadIdx.x == 64 * w && d.prof_mb == mby * d.mbw + mbx;
+}
+#define PSTAMP(k) do { if (prof) d.prof[k] = wall_clock64(); } while (0)

@@ -1,0 +1,302 @@
+// jmh_final.hip — k_mb_final: the second half of encode_one_macroblock [J] (RDO off) for every
+// macroblock of one wavefront diagonal, after k_mb_analyse: the mode decision over the analysis
+// costs, then the residual coding of the chosen mode with 16-lane transform groups
+// (LumaResidualCoding / dct_luma_16x16 / dct_chroma + reconstruction) and the outputs the next
+// diagonal depends on (reconstruction, MVs, reference indices, Intra4x4 modes).
+#include "jmh_common.h"
+
+struct FinS {
+    uint8_t org[256];
+    uint8_t orgc[2][64];
+    uint8_t rec[256];
+    uint8_t rtop[24];                    // luma row y = -1, x = -1..19 -> [x + 1]
+    uint8_t rleft[16];
+    uint8_t ctop[2][12];                 // chroma rows y = -1, x = -1..7 -> [x + 1]
+    uint8_t cleft[2][8];
+    int16_t fmv[16][2];
+    int16_t lev[16][16];
+    int bcost[16];
+    int bnz[16];
+    int dc[16];
+    int dcdq[16];
+    int16_t dclev[16];
+    int cdcin[2][4];
+    int cdcq[2][4];
+    int16_t cdc[2][4];
+    int16_t cac[2][4][16];
+    int cbcost[2][4];
+    int cbnz[2][4];
+    int creset[2];
+    int cdcnz[2];
+    uint8_t cfin[2][64];
+};
+
+__device__ __forceinline__ int qpel_at(const DevParams &d, int X, int Y) {
+    int x = iclip(-QPAD, d.W - 1 + QPAD, X >> 2), y = iclip(-QPAD, d.H - 1 + QPAD, Y >> 2);
+    int ph = (Y & 3) * 4 + (X & 3);
+    return d.qpel[(size_t)ph * d.qplane + (size_t)(y + QPAD) * d.qstride + (x + QPAD)];
+}
+
+__global__ __launch_bounds__(NT) void k_mb_final(DevParams d) {
+    __shared__ FinS s;
+    const int tid = threadIdx.x;
+    const int mby = d.y_min + blockIdx.x, mbx = d.diag - 2 * mby;
+    const int pix_x = 16 * mbx, pix_y = 16 * mby;
+    const int W = d.W, Wc = d.Wc, W4 = d.W >> 2;
+    const int slice_p = d.slice_type == JMH_P_SLICE;
+    const int qp = d.qp;
+    const int intra_round = !slice_p;
+    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0;
+    const bool prof = prof_mb_here(d, mbx, mby);
+    PSTAMP(16);
+    const MbScratch *sc = d.scr + mby * d.mbw + mbx;
+
+    // ---- inputs into LDS
+    s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    if (tid < 128) {
+        const int uv = tid >> 6, k = tid & 63;
+        s.orgc[uv][k] = (uv ? d.orgV : d.orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
+    } else if (tid >= 128 && tid < 149) {
+        const int x = tid - 129;
+        const bool av = x < 0 ? avTL : x < 16 ? avT : false;
+        s.rtop[x + 1] = av ? d.recY[(pix_y - 1) * W + pix_x + x] : 0;
+    } else if (tid >= 160 && tid < 176) {
+        const int y = tid - 160;
+        s.rleft[y] = avL ? d.recY[(pix_y + y) * W + pix_x - 1] : 0;
+    } else if (tid >= 192 && tid < 210) {
+        const int i = tid - 192, uv = i / 9, x = i - 9 * uv - 1;
+        const bool av = x < 0 ? avTL : avT;
+        s.ctop[uv][x + 1] = av ? (uv ? d.recV : d.recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
+    } else if (tid >= 224 && tid < 240) {
+        const int i = tid - 224, uv = i >> 3, y = i & 7;
+        s.cleft[uv][y] = avL ? (uv ? d.recV : d.recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
+    }
+
+    // ---- mode decision (encode_one_macroblock, RDO off): costs from k_mb_analyse
+    int min_cost = BIGCOST, best_mode = 1, best8x8 = 0;
+    if (slice_p) {
+        for (int mode = 1; mode < 4; mode++) {
+            if (!d.inter_search[mode]) continue;
+            const int cost = mode == 1 ? sc->motion_cost[1][0] : sc->motion_cost[mode][0] + sc->motion_cost[mode][1];
+            if (cost < min_cost) { best_mode = mode; min_cost = cost; }
+        }
+        if (d.inter_search[4] || d.inter_search[5] || d.inter_search[6] || d.inter_search[7]) {
+            best8x8 = sc->best8x8;
+            if (sc->cost8x8 < min_cost) { best_mode = JMH_P8x8; min_cost = sc->cost8x8; }
+        }
+    }
+    if (sc->i4cost <= min_cost) { min_cost = sc->i4cost; best_mode = JMH_I4MB; }
+    const int i16mode = sc->i16mode;
+    if (sc->i16cost < min_cost) { min_cost = sc->i16cost; best_mode = JMH_I16MB; }
+    const int is_intra = best_mode == JMH_I4MB || best_mode == JMH_I16MB;
+    int b8mode[4];
+    for (int b = 0; b < 4; b++)
+        b8mode[b] = best_mode == JMH_P8x8 ? (best8x8 >> (4 * b)) & 15 : best_mode == JMH_I4MB ? JMH_IBLOCK : best_mode == JMH_I16MB ? 0 : best_mode;
+    if (tid < 32) {
+        const int k = tid >> 1, c = tid & 1, b8 = ((k >> 3) << 1) + ((k & 3) >> 1);
+        const int bm = best_mode == JMH_P8x8 ? (best8x8 >> (4 * b8)) & 15 : best_mode;
+        s.fmv[k][c] = is_intra ? 0 : sc->all_mv[bm][k][c];
+    }
+    __syncthreads();
+
+    // ======== luma residual coding: 16 blocks x 16 lanes
+    int cbp = 0, cbp_blk = 0;
+    const int blk = tid >> 4, l = tid & 15, lx = l & 3, ly = l >> 2;
+    const int px4 = 4 * (blk & 3) + lx, py4 = 4 * (blk >> 2) + ly;   // MB pixel of this lane
+    if (best_mode == JMH_I4MB) {
+        cbp = sc->i4cbp; cbp_blk = sc->i4blk;
+        s.lev[blk][l] = sc->i4lev[blk][l];
+        s.rec[tid] = sc->i4rec[tid];
+    } else if (best_mode == JMH_I16MB) {
+        // dct_luma_16x16 [J]
+        const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per;
+        const int qp_const = (1 << q_bits) / 3, qp_const2 = qp_const << 1;
+        const uint8_t *T = s.rtop + 1, *L = s.rleft;
+        const I16Par par = i16_params(T, L, avT, avL);
+        const int p = i16_pred(par, T, L, i16mode, px4, py4);
+        const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
+        if (l == 0) s.dc[blk] = c;
+        __syncthreads();
+        if (tid == 0) {
+            int *dc = s.dc;
+            for (int yy = 0; yy < 4; yy++) {
+                int *r = dc + 4 * yy;
+                int a0 = r[0] + r[3], a3 = r[0] - r[3], a1 = r[1] + r[2], a2 = r[1] - r[2];
+                r[0] = a0 + a1; r[2] = a0 - a1; r[1] = a3 + a2; r[3] = a3 - a2;
+            }
+            for (int xx = 0; xx < 4; xx++) {
+                int a0 = dc[xx] + dc[12 + xx], a3 = dc[xx] - dc[12 + xx], a1 = dc[4 + xx] + dc[8 + xx], a2 = dc[4 + xx] - dc[8 + xx];
+                dc[xx] = (a0 + a1) >> 1; dc[8 + xx] = (a0 - a1) >> 1; dc[4 + xx] = (a3 + a2) >> 1; dc[12 + xx] = (a3 - a2) >> 1;
+            }
+            int lev[16];
+            for (int k = 0; k < 16; k++) {
+                int pos = scan_of(k);
+                int level = (abs(dc[pos]) * c_q3[qp_rem][0] + qp_const2) >> (q_bits + 1);
+                s.dclev[k] = (int16_t)isign(level, dc[pos]);
+                lev[pos] = s.dclev[k];
+            }
+            int t[16];
+            for (int yy = 0; yy < 4; yy++) {
+                const int *cc = lev + 4 * yy;
+                int e0 = cc[0] + cc[2], e1 = cc[0] - cc[2], e2 = cc[1] - cc[3], e3 = cc[1] + cc[3];
+                t[4 * yy] = e0 + e3; t[4 * yy + 3] = e0 - e3; t[4 * yy + 1] = e1 + e2; t[4 * yy + 2] = e1 - e2;
+            }
+            int v00 = c_dq3[qp_rem][0];
+            for (int xx = 0; xx < 4; xx++) {
+                int e0 = t[xx] + t[8 + xx], e1 = t[xx] - t[8 + xx], e2 = t[4 + xx] - t[12 + xx], e3 = t[4 + xx] + t[12 + xx];
+                int fv[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
+                for (int yy = 0; yy < 4; yy++) s.dcdq[4 * yy + xx] = ((fv[yy] * v00 << qp_per) + 2) >> 2;
+            }
+        }
+        __syncthreads();
+        int lev, dq, cc;
+        unsigned nz = lane_quant(c, l, qp, qp_const, true, lev, dq, cc);
+        s.lev[blk][l] = (int16_t)lev;
+        if (l == 0) { dq = s.dcdq[blk]; s.bnz[blk] = nz != 0; }
+        s.rec[py4 * 16 + px4] = (uint8_t)lane_inv4x4(dq, l, p);
+        __syncthreads();
+        for (int b = 0; b < 16; b++)
+            if (s.bnz[b]) { cbp = 15; cbp_blk |= 1 << b; }
+    } else {
+        // LumaResidualCoding / LumaResidualCoding8x8 (+ SetCoeffAndReconstruction8x8)
+        const int p = qpel_at(d, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1]);
+        const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
+        int lev, dq, cc;
+        const int q_bits = 15 + qp / 6;
+        unsigned nz = lane_quant(c, l, qp, intra_round ? (1 << q_bits) / 3 : (1 << q_bits) / 6, false, lev, dq, cc);
+        const int rv = lane_inv4x4(dq, l, p);
+        if (l == 0) { s.bcost[blk] = cc; s.bnz[blk] = nz != 0; }
+        __syncthreads();
+        int sum_cnt = 0, keep8 = 0;
+        for (int b8 = 0; b8 < 4; b8++) {
+            int base = (b8 >> 1) * 8 + (b8 & 1) * 2;
+            int c8 = s.bcost[base] + s.bcost[base + 1] + s.bcost[base + 4] + s.bcost[base + 5];
+            int nz8 = s.bnz[base] | s.bnz[base + 1] | s.bnz[base + 4] | s.bnz[base + 5];
+            if (c8 <= 4) c8 = 0;                                   // _LUMA_COEFF_COST_
+            else {
+                keep8 |= 1 << b8;
+                if (nz8) cbp |= 1 << b8;
+                for (int q = 0; q < 4; q++) {
+                    int k = base + (q & 1) + (q >> 1) * 4;
+                    if (s.bnz[k]) cbp_blk |= 1 << k;
+                }
+            }
+            sum_cnt += c8;
+        }
+        if (sum_cnt <= 5) { keep8 = 0; cbp = 0; cbp_blk = 0; }      // _LUMA_MB_COEFF_COST_
+        const int mb8 = ((blk >> 3) << 1) + ((blk & 3) >> 1);
+        const bool keep = (keep8 >> mb8) & 1;
+        s.lev[blk][l] = keep ? (int16_t)lev : 0;
+        s.rec[py4 * 16 + px4] = (uint8_t)(keep ? rv : p);
+    }
+    PSTAMP(17);
+
+    // ======== chroma: prediction (intra mode from k_mb_analyse, or MC) + dct_chroma [J]
+    const int c_mode = is_intra ? sc->c_mode : 0;
+    const int qpc = c_qpc[iclip(0, 51, qp + d.cqp_off)];
+    const int cq_bits = 15 + qpc / 6;
+    const int cqp_const = intra_round ? (1 << cq_bits) / 3 : (1 << cq_bits) / 6;
+    const int cuv = blk >> 2, cb = blk & 3;
+    const int cxo = (cb & 1) * 4 + lx, cyo = (cb >> 1) * 4 + ly;
+    int cdq = 0, cpredv = 0;
+    if (tid < 128) {
+        if (is_intra) {
+            cpredv = chroma_pred_px(s.ctop[cuv] + 1, s.cleft[cuv], s.ctop[cuv][0], avT, avL, c_mode, cxo, cyo);
+        } else {
+            // OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2
+            const uint8_t *R = cuv ? d.refV : d.refU;
+            const int vx = s.fmv[(cyo >> 1) * 4 + (cxo >> 1)][0], vy = s.fmv[(cyo >> 1) * 4 + (cxo >> 1)][1];
+            const int ii = ((pix_x >> 1) + cxo) * 8 + vx, jj = ((pix_y >> 1) + cyo) * 8 + vy;
+            const int x0 = iclip(0, Wc - 1, ii >> 3), y0 = iclip(0, d.Hc - 1, jj >> 3);
+            const int x1 = iclip(0, Wc - 1, (ii + 7) >> 3), y1 = iclip(0, d.Hc - 1, (jj + 7) >> 3);
+            const int fx = ii & 7, fy = jj & 7;
+            cpredv = ((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] + (8 - fx) * fy * R[y1 * Wc + x0] +
+                      fx * fy * R[y1 * Wc + x1] + 32) >> 6;
+        }
+        const int c = lane_fwd4x4(s.orgc[cuv][cyo * 8 + cxo] - cpredv, l);
+        if (l == 0) s.cdcin[cuv][cb] = c;
+        int lev, cc;
+        unsigned nz = lane_quant(c, l, qpc, cqp_const, true, lev, cdq, cc);
+        s.cac[cuv][cb][l] = (int16_t)lev;
+        if (l == 0) { s.cbcost[cuv][cb] = cc; s.cbnz[cuv][cb] = nz != 0; }
+    }
+    __syncthreads();
+    if (tid < 2) {
+        const int uv = tid, qp_per = qpc / 6, qp_rem = qpc % 6;
+        const int *m = s.cdcin[uv];
+        int m1[4] = {m[0] + m[1] + m[2] + m[3], m[0] - m[1] + m[2] - m[3], m[0] + m[1] - m[2] - m[3], m[0] - m[1] - m[2] + m[3]};
+        int dcnz = 0;
+        for (int k = 0; k < 4; k++) {
+            int level = (abs(m1[k]) * c_q3[qp_rem][0] + 2 * cqp_const) >> (cq_bits + 1);
+            if (level) dcnz = 1;
+            s.cdc[uv][k] = (int16_t)isign(level, m1[k]);
+        }
+        int c0 = s.cdc[uv][0], c1 = s.cdc[uv][1], c2 = s.cdc[uv][2], c3 = s.cdc[uv][3];
+        int fv[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+        int v00 = c_dq3[qp_rem][0];
+        for (int k = 0; k < 4; k++) s.cdcq[uv][k] = ((fv[k] * 16 * v00) << qp_per) >> 5;   // 8.5.11.2
+        int cost = s.cbcost[uv][0] + s.cbcost[uv][1] + s.cbcost[uv][2] + s.cbcost[uv][3];
+        int acany = s.cbnz[uv][0] | s.cbnz[uv][1] | s.cbnz[uv][2] | s.cbnz[uv][3];
+        s.creset[uv] = cost < 4;                                  // _CHROMA_COEFF_COST_
+        s.cdcnz[uv] = (dcnz ? 1 : 0) | (acany && cost >= 4 ? 2 : 0);
+    }
+    __syncthreads();
+    if (tid < 128) {
+        if (s.creset[cuv]) { cdq = 0; s.cac[cuv][cb][l] = 0; }
+        if (l == 0) cdq = s.cdcq[cuv][cb];
+        s.cfin[cuv][cyo * 8 + cxo] = (uint8_t)lane_inv4x4(cdq, l, cpredv);
+    }
+    __syncthreads();
+    PSTAMP(18);
+    int cr = 0;
+    for (int uv = 0; uv < 2; uv++) {
+        if (s.cdcnz[uv] & 1) cr = max(cr, 1);
+        if (s.cdcnz[uv] & 2) cr = 2;
+    }
+    cbp |= cr << 4;
+
+    // ======== outputs: jmh_mb_result, reconstruction, picture MV / ref / Intra4x4-mode arrays
+    jmh_mb_result *res = d.res + mby * d.mbw + mbx;
+    int mb_type = best_mode;
+    if (slice_p && best_mode == 1 && cbp == 0 && s.fmv[0][0] == sc->skipx && s.fmv[0][1] == sc->skipy) mb_type = JMH_PSKIP;
+    if (tid == 0) {
+        res->mb_type = (int16_t)mb_type;
+        res->cbp = (int16_t)cbp;
+        res->cbp_blk = cbp_blk;
+        for (int b = 0; b < 4; b++) {
+            res->b8mode[b] = (int8_t)(mb_type == JMH_PSKIP ? 0 : b8mode[b]);
+            res->ref_idx[b] = (int8_t)(is_intra ? -1 : 0);
+        }
+        res->i16mode = (int8_t)(best_mode == JMH_I16MB ? i16mode : 0);
+        res->c_ipred_mode = (int8_t)c_mode;
+        res->pad0[0] = res->pad0[1] = 0;
+        res->min_cost = min_cost;
+        res->reserved = 0;
+    }
+    res->luma[blk][l] = s.lev[blk][l];
+    if (tid < 16) {
+        const int k = tid;
+        const int ip = best_mode == JMH_I4MB ? sc->ipred[k] : 2;
+        res->ipred[k] = (int8_t)ip;
+        res->mv[k][0] = s.fmv[k][0]; res->mv[k][1] = s.fmv[k][1];
+        res->luma_dc[k] = best_mode == JMH_I16MB ? s.dclev[k] : 0;
+        const int a = ((pix_y >> 2) + (k >> 2)) * W4 + (pix_x >> 2) + (k & 3);
+        d.mv[2 * a] = s.fmv[k][0]; d.mv[2 * a + 1] = s.fmv[k][1];
+        d.refidx[a] = (int8_t)(is_intra ? -1 : 0);
+        d.ipred[a] = (int8_t)ip;
+    }
+    if (tid < 8) { const int uv = tid >> 2, k = tid & 3; res->chroma_dc[uv][k] = s.cdc[uv][k]; }
+    if (tid < 128) {
+        const int uv = tid >> 6, b = (tid >> 4) & 3, q = tid & 15;
+        res->chroma_ac[uv][b][q] = s.cac[uv][b][q];
+        const int k = tid & 63;
+        (uv ? d.recV : d.recU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)] = s.cfin[uv][k];
+    }
+    d.recY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)] = s.rec[tid];
+    PSTAMP(19);
+}
+
+hipError_t jmh_launch_final(const DevParams &p, hipStream_t st) {
+    hipLaunchKernelGGL(k_mb_final, dim3(p.ndiag), dim3(NT), 0, st, p);
+    return hipGetLastError();
+}

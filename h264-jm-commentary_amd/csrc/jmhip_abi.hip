@@ -10,7 +10,8 @@
 #include "jmh_device.h"
 
 hipError_t jmh_launch_interp(const uint8_t *ref, int W, int H, uint8_t *qpel, int qstride, int qplane, hipStream_t st);
-hipError_t jmh_launch_mb(const DevParams &p, int nblocks, hipStream_t st);
+hipError_t jmh_launch_analyse(const DevParams &p, hipStream_t st);
+hipError_t jmh_launch_final(const DevParams &p, hipStream_t st);
 hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
                                 const int32_t *centres, uint16_t *out, hipStream_t st);
 hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
@@ -71,7 +72,9 @@ struct jmh_ctx {
     int16_t *d_mv;
     int8_t *d_refidx, *d_ipred;
     jmh_mb_result *d_res;
-    int16_t *d_spiral, *d_spiral_of;
+    MbScratch *d_scr;
+    unsigned long long *d_prof;          // JMH_PHASE_PROF=<mb>: per-phase wall clock of one MB
+    int prof_mb;
     jmh_mb_result *h_res;
     uint8_t *h_rec, *h_stage_cur, *h_stage_ref;
     int have_ref, pending, have_results, have_total;
@@ -113,20 +116,12 @@ int jmh_device_count(void) {
     return n;
 }
 
-static void spiral(int range, std::vector<int16_t> &xy) {   // Init_Motion_Search_Module [J]
-    xy.assign(2, 0);
-    for (int l = 1; l <= range; l++) {
-        for (int i = -l + 1; i < l; i++) { xy.push_back(i); xy.push_back(-l); xy.push_back(i); xy.push_back(l); }
-        for (int i = -l; i <= l; i++) { xy.push_back(-l); xy.push_back(i); xy.push_back(l); xy.push_back(i); }
-    }
-}
-
 void jmh_destroy(jmh_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     void *dev_bufs[] = {c->d_cur, c->d_ref, c->d_qpel, c->d_rec, c->d_slots, c->d_mv, c->d_refidx,
-                        c->d_ipred, c->d_res, c->d_spiral, c->d_spiral_of};
+                        c->d_ipred, c->d_res, c->d_scr, c->d_prof};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     void *host_bufs[] = {c->h_res, c->h_rec, c->h_stage_cur, c->h_stage_ref};
     for (void *p : host_bufs) if (p) (void)hipHostFree(p);
@@ -172,16 +167,16 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         ALLOC(c->d_slots, c->fsize * c->nslots);
         ALLOC(c->d_mv, n4 * 2 * sizeof(int16_t)); ALLOC(c->d_refidx, n4); ALLOC(c->d_ipred, n4);
         ALLOC(c->d_res, nmb * sizeof(jmh_mb_result));
-        ALLOC(c->d_spiral, (size_t)c->npos * 2 * sizeof(int16_t));
-        ALLOC(c->d_spiral_of, (size_t)c->npos * sizeof(int16_t));
+        ALLOC(c->d_scr, nmb * sizeof(MbScratch));
+        c->prof_mb = -1;
+        if (const char *e = getenv("JMH_PHASE_PROF")) {
+            c->prof_mb = atoi(e);
+            ALLOC(c->d_prof, 64 * sizeof(unsigned long long));
+            if (hipMemset(c->d_prof, 0, 64 * sizeof(unsigned long long)) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        }
         HALLOC(c->h_res, nmb * sizeof(jmh_mb_result)); HALLOC(c->h_rec, c->fsize);
         HALLOC(c->h_stage_cur, c->fsize); HALLOC(c->h_stage_ref, c->fsize);
-        std::vector<int16_t> xy, of(c->npos);
-        spiral(c->sr, xy);
-        for (int k = 0; k < c->npos; k++) of[(xy[2 * k + 1] + c->sr) * c->side + xy[2 * k] + c->sr] = (int16_t)k;
-        if (hipMemcpy(c->d_spiral, xy.data(), xy.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(c->d_spiral_of, of.data(), of.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemset(c->d_rec, 0, c->fsize) != hipSuccess || hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        if (hipMemset(c->d_rec, 0, c->fsize) != hipSuccess || hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         if (hipEventCreate(&c->ev_t0) != hipSuccess || hipEventCreate(&c->ev_t1) != hipSuccess ||
             ring_init(c->ring_interp) || ring_init(c->ring_mb)) { st = JMH_E_HIP; goto fail; }
         int nd = (c->mbw - 1) + 2 * (c->mbh - 1) + 1;
@@ -253,19 +248,20 @@ static int enqueue_encode(jmh_ctx *c, const uint8_t *d_pic, const jmh_frame_para
     p.refY = c->d_ref; p.refU = c->d_ref + ls; p.refV = c->d_ref + ls + ls / 4;
     p.qpel = c->d_qpel;
     p.recY = c->d_rec; p.recU = c->d_rec + ls; p.recV = c->d_rec + ls + ls / 4;
-    p.mv = c->d_mv; p.refidx = c->d_refidx; p.ipred = c->d_ipred; p.res = c->d_res;
-    p.spiral = c->d_spiral; p.spiral_of = c->d_spiral_of;
+    p.mv = c->d_mv; p.refidx = c->d_refidx; p.ipred = c->d_ipred; p.res = c->d_res; p.scr = c->d_scr;
+    p.prof = c->d_prof; p.prof_mb = c->prof_mb;
     p.slice_type = fp->slice_type; p.qp = fp->qp; p.lambda_mode = fp->lambda_mode; p.lambda_motion = fp->lambda_motion;
     p.cqp_off = fp->chroma_qp_offset;
     HCHK(ring_begin(c->ring_mb, c->st));
     for (size_t dg = 0; dg < c->dcount.size(); dg++) {
         if (!c->dcount[dg]) continue;
-        p.diag = (int)dg; p.y_min = c->dymin[dg];
-        HCHK(jmh_launch_mb(p, c->dcount[dg], c->st));
+        p.diag = (int)dg; p.y_min = c->dymin[dg]; p.ndiag = c->dcount[dg];
+        HCHK(jmh_launch_analyse(p, c->st));
+        HCHK(jmh_launch_final(p, c->st));
     }
     HCHK(ring_end(c->ring_mb, c->st));
     int nl = 0;
-    for (int n : c->dcount) nl += n > 0;
+    for (int n : c->dcount) nl += 2 * (n > 0);
     c->timing.mb_launches = nl;
     return JMH_OK;
 }
@@ -335,7 +331,19 @@ int jmh_sync(jmh_ctx *c) {
     if (!c) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
     HCHK(hipStreamSynchronize(c->st));
-
+    if (c->d_prof) {   // debug: phase timestamps of MB prof_mb from the last picture
+        unsigned long long h[64];
+        int rate_khz = 0;
+        HCHK(hipMemcpy(h, c->d_prof, sizeof(h), hipMemcpyDeviceToHost));
+        HCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->dev));
+        double us = rate_khz > 0 ? 1e3 / rate_khz : 0.01;
+        unsigned long long t0 = ~0ull;
+        for (int k = 0; k < 20; k++) if (h[k] && h[k] < t0) t0 = h[k];
+        fprintf(stderr, "jmh_phase mb=%d us since first stamp:", c->prof_mb);
+        for (int k = 0; k < 20; k++) fprintf(stderr, " [%d]%.2f", k, h[k] ? (double)(h[k] - t0) * us : -1.0);
+        fprintf(stderr, "\n");
+        HCHK(hipMemset(c->d_prof, 0, sizeof(h)));
+    }
     return JMH_OK;
 }
 
