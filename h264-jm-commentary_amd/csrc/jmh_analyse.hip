@@ -3,8 +3,9 @@
 // that run concurrently on different CUs:
 //
 //   role 2  P8x8 motion search: 4 x (8x8, 2x 8x4, 2x 4x8, 4x 4x4) = 36 BlockMotionSearch calls
-//   role 1  16x16, 16x8, 8x16 motion search (5 calls) + FindSkipModeMotionVector
-//   role 0  Intra4x4 decision with its reconstruction, Intra16x16 and chroma intra mode decisions
+//   role 1  16x16, 16x8, 8x16 motion search (5 calls) + FindSkipModeMotionVector, then the
+//           Intra16x16 and chroma intra-mode decisions (I slices: only the latter)
+//   role 0  Intra4x4 decision with its reconstruction
 //
 // JM runs the 41 searches of a P macroblock one after another. The only coupling between them is
 // the motion vector predictor, which reads MVs already stored inside the MB. Enumerating those
@@ -14,50 +15,108 @@
 // 8x8 blocks before b8 and the same sub-mode's earlier blocks in b8. So the 41 searches form 16
 // dependent stages, each a set of independent searches evaluated together, with results
 // identical to JM's sequential order. Per-mode MV arrays provide the exact neighbour view.
+// Likewise the 16 Intra4x4 blocks only read blocks on earlier (x4 + 2*y4) diagonals, so they run
+// as 10 steps of up to two blocks (one wave each) with JM's results.
 //
 // Motion search data path per ME workgroup:
 //   * 88x88 reference window (+4 margin for the 6-tap filter) and its b, h, j half-pel planes in
 //     LDS, computed once per MB (SubPelBlockMotionSearch reads only LDS);
 //   * the 16 4x4 SADs of every integer position (SetupFastFullPelSearch) in REGISTERS: each
-//     thread owns a column strip of 6 positions, accumulates v_sad_u8 over 20 window rows and
+//     thread owns a column strip of 6 positions, accumulates v_sad_u8 over 21 window rows and
 //     keeps 6 x 8 packed u16 pairs; a search of any partition reduces them with plain 32-bit adds
 //     of packed pairs (no carries: a half never exceeds 8 x 4080);
 //   * cost = SAD + lambda*(mvbits(x) + mvbits(y)) from two per-search LDS tables, key =
-//     cost << 13 | JM order (0 for the (0,0) pre-check, else spiral index + 1), DPP wave min.
+//     cost << 13 | JM order (0 for the (0,0) pre-check, else spiral index + 1), DPP wave min;
+//   * sub-pel SATD: one 4x4 sub-block per 16-lane row, DPP Hadamard, LDS-atomic candidate sums.
 #include "jmh_common.h"
 
 #define NPK 6                                 // search positions per thread (a column strip)
 #define TEAM 192                              // threads per search team (3 waves); 4 teams
+#define NGRP (TEAM / 16)                      // 16-lane rows per team
 #define PLS (WIN_DIM_MAX * WST + 32)          // stride between the G, b, h, j planes
 
-struct MeS {
-    uint8_t org[256];
-    Border bd;
-    int16_t all_mv[8][16][2];
-    int motion_cost[8][4];
-    uint16_t ctab[4][2][72];                  // per team: lambda*mvbits for x and y offsets
-    unsigned red[NTA / 64][4];                // per wave, per team: partial argmin keys
-    int ccost[2][4][9];                       // per sub-pel pass, team, candidate
-    uint8_t planes[4 * PLS];                  // G (the window), b, h, j
-    int16_t h1[WIN_DIM_MAX * WST];            // unclipped vertical 6-tap intermediates
-};
-struct IntraS {
-    uint8_t org[256];
+// Intra4x4 prediction (8.3.1.2) of mode m at pixel l as a formula over P[0..12]
+// (P[0] = p[-1,-1], P[1+i] = p[i,-1], P[9+j] = p[-1,j]): type | a << 2 | b << 6 | c << 10,
+// type 1: (Pa + Pb + 1) >> 1, 2: (Pa + 2 Pb + Pc + 2) >> 2 (a copy when a == b == c), 3: DC.
+static __constant__ uint16_t c_i4tab[9][16] = {
+    {0x0446, 0x088A, 0x0CCE, 0x1112, 0x0446, 0x088A, 0x0CCE, 0x1112, 0x0446, 0x088A, 0x0CCE, 0x1112, 0x0446, 0x088A, 0x0CCE, 0x1112},
+    {0x2666, 0x2666, 0x2666, 0x2666, 0x2AAA, 0x2AAA, 0x2AAA, 0x2AAA, 0x2EEE, 0x2EEE, 0x2EEE, 0x2EEE, 0x3332, 0x3332, 0x3332, 0x3332},
+    {0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003},
+    {0x0C86, 0x10CA, 0x150E, 0x1952, 0x10CA, 0x150E, 0x1952, 0x1D96, 0x150E, 0x1952, 0x1D96, 0x21DA, 0x1952, 0x1D96, 0x21DA, 0x221E},
+    {0x2406, 0x0842, 0x0C86, 0x10CA, 0x2A42, 0x2406, 0x0842, 0x0C86, 0x2EA6, 0x2A42, 0x2406, 0x0842, 0x32EA, 0x2EA6, 0x2A42, 0x2406},
+    {0x0041, 0x0085, 0x00C9, 0x010D, 0x0426, 0x0842, 0x0C86, 0x10CA, 0x026A, 0x0041, 0x0085, 0x00C9, 0x26AE, 0x0426, 0x0842, 0x0C86},
+    {0x0241, 0x0426, 0x004A, 0x048E, 0x02A5, 0x2A42, 0x0241, 0x0426, 0x02E9, 0x2EA6, 0x02A5, 0x2A42, 0x032D, 0x32EA, 0x02E9, 0x2EA6},
+    {0x0085, 0x00C9, 0x010D, 0x0151, 0x0C86, 0x10CA, 0x150E, 0x1952, 0x00C9, 0x010D, 0x0151, 0x0195, 0x10CA, 0x150E, 0x1952, 0x1D96},
+    {0x02A5, 0x2EA6, 0x02E9, 0x32EA, 0x02E9, 0x32EA, 0x032D, 0x332E, 0x032D, 0x332E, 0x3332, 0x3332, 0x3332, 0x3332, 0x3332, 0x3332}};
+
+// intra neighbourhood of an MB in LDS (unfiltered reconstruction of the current picture)
+struct IntraNb {
     uint8_t orgc[2][64];
-    uint8_t rec[256];
-    Border bd;
     uint8_t rtop[24];                         // luma row y = -1, x = -1..19 -> [x + 1]
     uint8_t rleft[16];
     uint8_t ctop[2][12];                      // chroma rows y = -1, x = -1..7 -> [x + 1]
     uint8_t cleft[2][8];
-    int i4P[16];
+};
+struct MeS {
+    uint8_t org[256];
+    Border bd;
+    IntraNb nb;
+    int16_t all_mv[8][16][2];
+    int motion_cost[8][4];
+    uint16_t ctab[4][2][72];                  // per team: lambda*mvbits for x and y offsets
+    unsigned red[NTA / 64][4];                // per wave, per team: partial argmin keys
+    int ccost[2][4][9];                       // per sub-pel pass, team, candidate (LDS atomics)
+    uint8_t planes[4 * PLS];                  // G (the window), b, h, j
+    int16_t h1[WIN_DIM_MAX * WST];            // unclipped vertical 6-tap intermediates
+    unsigned long long *pst;                  // debug: per-stage stamps (thread 0), null when off
+    int pn;
+};
+struct IntraS {
+    uint8_t org[256];
+    uint8_t rec[256];
+    Border bd;
+    IntraNb nb;
+    int i4P[2][16];
     int8_t ipred_cur[16];
+    int part[2][4];                           // per I4 wave: cost, cbp, blk mask
 };
 union AnalyseS {
     MeS me;
     IntraS in;
 };
 
+__device__ __forceinline__ void sstamp(MeS &s) {
+    if (threadIdx.x == 0 && s.pst && s.pn < 44) s.pst[s.pn++] = wall_clock64();
+}
+
+// prefetch of the intra neighbourhood by threads t in [0, 96)
+__device__ __forceinline__ void load_intra_nb(const DevParams &d, IntraNb &nb, int t, int mbx, int mby) {
+    const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, Wc = d.Wc;
+    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
+    if (t < 21) {                                  // luma row y = -1, x = -1..19
+        const int x = t - 1;
+        const bool av = x < 0 ? avTL : x < 16 ? avT : avTR;
+        nb.rtop[x + 1] = av ? d.recY[(pix_y - 1) * W + pix_x + x] : 0;
+    } else if (t < 37) {
+        const int y = t - 21;
+        nb.rleft[y] = avL ? d.recY[(pix_y + y) * W + pix_x - 1] : 0;
+    } else if (t < 55) {                           // chroma rows y = -1, x = -1..7
+        const int i = t - 37, uv = i / 9, x = i - 9 * uv - 1;
+        const bool av = x < 0 ? avTL : avT;
+        nb.ctop[uv][x + 1] = av ? (uv ? d.recV : d.recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
+    } else if (t < 71) {
+        const int i = t - 55, uv = i >> 3, y = i & 7;
+        nb.cleft[uv][y] = avL ? (uv ? d.recV : d.recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
+    }
+}
+__device__ __forceinline__ void load_orgc(const DevParams &d, IntraNb &nb, int t, int mbx, int mby) {   // t in [0, 128)
+    const int uv = t >> 6, k = t & 63;
+    nb.orgc[uv][k] = (uv ? d.orgV : d.orgU)[((8 * mby) + (k >> 3)) * d.Wc + 8 * mbx + (k & 7)];
+}
+
+// ======================================================================================
+//  motion search
+// ======================================================================================
 // neighbour view of a motion search of block type bt in 8x8 block b8 (see header comment)
 struct NbMe {
     const MeS &s;
@@ -92,25 +151,41 @@ __device__ __forceinline__ unsigned psum(const uint32_t (&r)[8]) {
     return (v & 0xFFFFu) + (v >> 16);
 }
 
-// this thread's best key over its positions for search (team J, partition BT/BX/BY)
+// per-thread search state: SADs of the thread's NPK positions and their JM order keys
+struct PosState {
+    uint32_t sadp[NPK][8];
+    uint32_t ordk[NPK];      // JM order (0 = (0,0) pre-check); 0xFFFFFFFF for slots outside the table
+    int dx, dy0;
+};
+
+// this thread's best key for search (team J, partition BT/BX/BY); 'range' < sr only with
+// RestrictSearchRange 0 (positions outside are skipped, the (0,0) pre-check never is)
 template <int J, int BT, int BX, int BY>
-__device__ __forceinline__ unsigned eval_search(const MeS &s, const uint32_t (&sadp)[NPK][8], const uint32_t (&pinfo)[NPK], int dx,
-                                                int dy0, unsigned range) {
-    const unsigned cxv = s.ctab[J][0][dx];
+__device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps, int sr, int range) {
+    const unsigned cxv = s.ctab[J][0][ps.dx];
     unsigned b = 0xFFFFFFFFu;
+    if (range >= sr) {
 #pragma unroll
-    for (int k = 0; k < NPK; k++) {
-        unsigned cost = psum<BT, BX, BY>(sadp[k]) + cxv + s.ctab[J][1][dy0 + k];
-        unsigned key = (cost << 13) | (pinfo[k] & 0x1FFFu);
-        b = min(b, (pinfo[k] >> 16) <= range ? key : 0xFFFFFFFFu);
+        for (int k = 0; k < NPK; k++) {
+            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + s.ctab[J][1][ps.dy0 + k];
+            b = min(b, (cost << 13) | ps.ordk[k]);
+        }
+    } else {
+        const int rx = abs(ps.dx - sr);
+#pragma unroll
+        for (int k = 0; k < NPK; k++) {
+            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + s.ctab[J][1][ps.dy0 + k];
+            const bool in = max(rx, abs(ps.dy0 + k - sr)) <= range || ps.ordk[k] == 0;
+            b = min(b, in ? (cost << 13) | ps.ordk[k] : 0xFFFFFFFFu);
+        }
     }
     return b;
 }
 
-__device__ __forceinline__ unsigned search_range(const DevParams &d, int bt) { return d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr; }
+__device__ __forceinline__ int search_range(const DevParams &d, int bt) { return d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr; }
 
-// stage head: the MVP of each active team's search (every team thread, uniform) and its
-// lambda*mvbits tables; ends with the barrier that publishes the tables.
+// stage head: the MVP of each active team's search (every team thread, uniform), its
+// lambda*mvbits tables and zeroed candidate sums; ends with the barrier that publishes them.
 __device__ __forceinline__ void stage_head(const DevParams &d, MeS &s, bool act, int bt, int bx4, int by4, int b8, int best8x8, int scx,
                                            int scy, int &pmvx, int &pmvy) {
     const int team = threadIdx.x / TEAM, u = threadIdx.x % TEAM, side = d.side, sr = d.sr, lam = d.lambda_motion;
@@ -119,8 +194,10 @@ __device__ __forceinline__ void stage_head(const DevParams &d, MeS &s, bool act,
         set_mvp(NbMe{s, bt, b8, best8x8}, bx4, by4, c_blc[bt][0], c_blc[bt][1], pmvx, pmvy);
         if (u < side) s.ctab[team][0][u] = (uint16_t)(lam * mvbits(((scx + u - sr) << 2) - pmvx));
         else if (u < 2 * side) s.ctab[team][1][u - side] = (uint16_t)(lam * mvbits(((scy + u - side - sr) << 2) - pmvy));
+        else if (u < 2 * side + 18) s.ccost[(u - 2 * side) / 9][team][(u - 2 * side) % 9] = 0;
     }
     __syncthreads();
+    sstamp(s);
 }
 
 // publish the per-thread keys of the stage's searches (teams with bit set in mask)
@@ -133,15 +210,17 @@ __device__ __forceinline__ void stage_reduce(MeS &s, unsigned mask, const unsign
             if (lane == 0) s.red[wave][j] = v;
         }
     __syncthreads();
+    sstamp(s);
 }
 
 // stage tail: each active team resolves its full-pel winner, runs SubPelBlockMotionSearch
-// (half then quarter pel, 9 candidates x up to 16 4x4 sub-blocks in parallel) and stores the MV.
+// (half then quarter pel: 9 candidates x up to 16 4x4 sub-blocks, one per 16-lane row) and
+// stores the MV and the partition cost.
 __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act, int bt, int bx4, int by4, int mcidx, int pmvx, int pmvy,
                                            int scx, int scy) {
-    const int team = threadIdx.x / TEAM, u = threadIdx.x % TEAM;
+    const int team = threadIdx.x / TEAM, u = threadIdx.x % TEAM, g = u >> 4, l = u & 15;
     const int sr = d.sr, lam = d.lambda_motion, had = d.use_hadamard;
-    int rx = 0, ry = 0, fmx = 0, fmy = 0, min_mcost = 0, qx = 0, qy = 0, w4 = 1, nsub = 1, check0 = 0;
+    int rx = 0, ry = 0, fmx = 0, fmy = 0, min_mcost = 0, qx = 0, qy = 0, lw4 = 0, lns = 0, check0 = 0;
     if (act) {
         unsigned best = s.red[0][team];
 #pragma unroll
@@ -151,42 +230,44 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act,
         else spiral_pos((int)order - 1, rx, ry);
         fmx = scx + rx; fmy = scy + ry;
         min_mcost = (int)(best >> 13);
-        w4 = c_blc[bt][0] >> 2; nsub = w4 * (c_blc[bt][1] >> 2);
+        const int w4 = c_blc[bt][0] >> 2, h4 = c_blc[bt][1] >> 2;
+        lw4 = w4 >> 1;                         // log2 of w4 (1, 2, 4)
+        lns = lw4 + (h4 >> 1);                // log2 of the sub-block count
         check0 = bt == 1 && fmx == 0 && fmy == 0 && had && d.slice_type == JMH_P_SLICE;
         if (had) min_mcost = BIGCOST;
     }
-    const int wx0 = WM + sr + rx + 4 * bx4, wy0 = WM + sr + ry + 4 * by4;   // window coords of block pixel (0,0)
+    // window coords of this lane's pixel in block (0,0) at the full-pel MV, and its original sample
+    const int wx0 = WM + sr + rx + 4 * bx4 + (l & 3), wy0 = WM + sr + ry + 4 * by4 + (l >> 2);
+    const uint8_t *orow = s.org + (4 * by4 + (l >> 2)) * 16 + 4 * bx4 + (l & 3);
     for (int pass = 0; pass < 2; pass++) {
         const int step = pass == 0 ? 2 : 1;
         const int min_pos = pass == 0 ? (had ? 0 : 1) : 1;
-        if (act && u < 144) {
-            const int c = u >> 4, sub = u & 15;
-            int sat = 0;
-            if (c >= min_pos && sub < nsub) {
+        if (act) {
+            const int ntask = 9 << lns;
+            for (int t = g; t < ntask; t += NGRP) {   // uniform per 16-lane row
+                const int c = t >> lns, sub = t & ((1 << lns) - 1);
+                if (c < min_pos) continue;
                 const int ox = qx + step * c_sp9[c][0], oy = qy + step * c_sp9[c][1];
                 const int off = c_qoff[(oy & 3) * 4 + (ox & 3)];
                 const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
                 const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
                 const int oB = ((xb & 1) + 2 * (yb & 1)) * PLS + (yb >> 1) * WST + (xb >> 1);
-                const int bxp = 4 * (sub % w4), byp = 4 * (sub / w4);
+                const int bxp = 4 * (sub & ((1 << lw4) - 1)), byp = 4 * (sub >> lw4);
                 const uint8_t *pp = s.planes + (wy0 + byp + (oy >> 2)) * WST + wx0 + bxp + (ox >> 2);
-                const uint8_t *o = s.org + (4 * by4 + byp) * 16 + 4 * bx4 + bxp;
-                int df[16];
-#pragma unroll
-                for (int y = 0; y < 4; y++)
-#pragma unroll
-                    for (int x = 0; x < 4; x++) df[4 * y + x] = o[16 * y + x] - ((pp[y * WST + x + oA] + pp[y * WST + x + oB] + 1) >> 1);
-                sat = satd4x4(df, had);
-            }
-            const int tot = row16_sum(sat);
-            if (sub == 0 && c >= min_pos) {
-                const int vx = 4 * fmx + qx + step * c_sp9[c][0], vy = 4 * fmy + qy + step * c_sp9[c][1];
-                int mc = lam * (mvbits(vx - pmvx) + mvbits(vy - pmvy));
-                if (pass == 0 && check0 && c == 0) mc -= 16 * lam;
-                s.ccost[pass][team][c] = mc + tot;
+                const int dv = orow[16 * byp + bxp] - ((pp[oA] + pp[oB] + 1) >> 1);
+                int sat = had ? row16_sum(abs(row16_had(dv, l))) >> 1 : row16_sum(abs(dv));
+                if (l == 0) {
+                    if (sub == 0) {
+                        const int vx = 4 * fmx + ox, vy = 4 * fmy + oy;
+                        sat += lam * (mvbits(vx - pmvx) + mvbits(vy - pmvy));
+                        if (pass == 0 && check0 && c == 0) sat -= 16 * lam;
+                    }
+                    atomicAdd(&s.ccost[pass][team][c], sat);
+                }
             }
         }
         __syncthreads();
+        sstamp(s);
         if (act) {   // JM order, strict '<' against the running minimum
             int bpos = 0;
             for (int c = min_pos; c < 9; c++) {
@@ -199,24 +280,24 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act,
     }
     if (act) {
         const int cmx = 4 * fmx + qx, cmy = 4 * fmy + qy;
-        if (u < nsub) {
-            const int k = (by4 + u / w4) * 4 + bx4 + u % w4;
+        if (u < (1 << lns)) {
+            const int k = (by4 + (u >> lw4)) * 4 + bx4 + (u & ((1 << lw4) - 1));
             s.all_mv[bt][k][0] = (int16_t)cmx; s.all_mv[bt][k][1] = (int16_t)cmy;
         }
         if (u == 0) s.motion_cost[bt][mcidx] += min_mcost;
     }
     __syncthreads();
+    sstamp(s);
 }
 
-#define EVAL(J, BT, BX, BY) bk[J] = eval_search<J, BT, BX, BY>(s, sadp, pinfo, dx, dy0, search_range(d, BT))
+#define EVAL(J, BT, BX, BY) bk[J] = eval_search<J, BT, BX, BY>(s, ps, sr, search_range(d, BT))
 
 // one 8x8 block of P8x8: 4 stages (sub-modes 4..7 in parallel, then the 4x4 chain), then the
 // P8x8 sub-mode decision for the block and the reset of its stored MVs (via best8x8)
 template <int B8>
-__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, const uint32_t (&sadp)[NPK][8], const uint32_t (&pinfo)[NPK], int dx,
-                                           int dy0, int scx, int scy, int &best8x8, int &cost8x8) {
+__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, const PosState &ps, int scx, int scy, int &best8x8, int &cost8x8) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
-    const int team = threadIdx.x / TEAM;
+    const int team = threadIdx.x / TEAM, sr = d.sr;
     unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
     int pmvx, pmvy;
     {   // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left
@@ -258,330 +339,364 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, const uin
     cost8x8 += mc8;
 }
 
-// motion-search roles (1: 16x16/16x8/8x16, 2: P8x8)
+// ======================================================================================
+//  intra decisions
+// ======================================================================================
+// intrapred_luma_16x16 + find_sad_16x16 on one wave: 4 modes x 16 blocks = 64 lanes
+__device__ __forceinline__ void i16_decision(const DevParams &d, const uint8_t *org, const IntraNb &nb, MbScratch *scr, int lane, bool avL, bool avT,
+                                             bool avTL) {
+    const int m = lane >> 4, b = lane & 15, ox = (b & 3) * 4, oy = (b >> 2) * 4;
+    const uint8_t *T = nb.rtop + 1, *L = nb.rleft;
+    const I16Par par = i16_params(T, L, avT, avL);
+    int mm[16], t[16];
+    for (int yy = 0; yy < 4; yy++)
+        for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy);
+    for (int yy = 0; yy < 4; yy++) {
+        int *r = mm + 4 * yy;
+        int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
+        t[4 * yy] = a0 + a1; t[4 * yy + 2] = a0 - a1; t[4 * yy + 1] = a2 + a3; t[4 * yy + 3] = a3 - a2;
+    }
+    int acs = 0, dcc = 0;
+    for (int xx = 0; xx < 4; xx++) {
+        int a0 = t[xx] + t[12 + xx], a1 = t[4 + xx] + t[8 + xx], a2 = t[4 + xx] - t[8 + xx], a3 = t[xx] - t[12 + xx];
+        int o0 = a0 + a1, o2 = a0 - a1, o1 = a2 + a3, o3 = a3 - a2;
+        if (xx == 0) dcc = o0; else acs += abs(o0);
+        acs += abs(o1) + abs(o2) + abs(o3);
+    }
+    const int cost = row16_sum(acs) + lane_had_abs(dcc / 4, b);
+    const bool av16[4] = {avT, avL, true, avT && avL && avTL};
+    int best = MAX_VALUE, i16mode = 2;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int c = __builtin_amdgcn_readlane(cost, 16 * k);
+        if (av16[k] && c < best) { best = c; i16mode = k; }
+    }
+    if (lane == 0) { scr->i16cost = best / 2; scr->i16mode = i16mode; }
+}
+
+// IntraChromaPrediction8x8 mode decision on one wave: 4 modes x 2 components x 4 blocks
+__device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraNb &nb, MbScratch *scr, int lane, bool avL, bool avT, bool avTL) {
+    int sat = 0;
+    if (lane < 32) {
+        const int m = lane >> 3, uv = (lane >> 2) & 1, b = lane & 3, xo = (b & 1) * 4, yo = (b >> 1) * 4;
+        const uint8_t *T = nb.ctop[uv] + 1, *L = nb.cleft[uv];
+        int df[16];
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++)
+                df[4 * y + x] = nb.orgc[uv][(yo + y) * 8 + xo + x] - chroma_pred_px(T, L, nb.ctop[uv][0], avT, avL, m, xo + x, yo + y);
+        sat = satd4x4(df, d.use_hadamard);
+    }
+    const bool cav[4] = {true, avL, avT, avT && avL && avTL};
+    int minc = BIGCOST, c_mode = 0;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) c += __builtin_amdgcn_readlane(sat, 8 * m + q);
+        if (cav[m] && c < minc) { minc = c; c_mode = m; }
+    }
+    if (lane == 0) scr->c_mode = c_mode;
+}
+
+// ======================================================================================
+//  role 1 / role 2: motion search
+// ======================================================================================
 template <int ROLE>
 __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int mby) {
     const int tid = threadIdx.x, team = tid / TEAM;
     const int W = d.W, sr = d.sr, side = d.side;
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
+    const bool slice_p = d.slice_type == JMH_P_SLICE;
+    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0;
     const bool prof = prof_mb_here(d, mbx, mby);
     const int pb = ROLE == 2 ? 0 : 8;
     PSTAMP(pb);
+    MbScratch *scr = d.scr + mby * d.mbw + mbx;
+    if (tid == 0) { s.pst = (prof && ROLE == 2) ? d.prof + 20 : nullptr; s.pn = 0; }
     if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    if (tid >= 256 && tid < 266) load_border(d, s.bd, tid - 256, mbx, mby);
-    if (tid >= 512 && tid < 544) s.motion_cost[(tid - 512) >> 2][tid & 3] = 0;
-    __syncthreads();
-    // SetupFastFullPelSearch: centre = 16x16 MVP / 4 (trunc), clamped to +-SR
-    int pcx, pcy;
-    set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
-    const int scx = iclip(-sr, sr, pcx / 4), scy = iclip(-sr, sr, pcy / 4);
+    else if (tid < 266) load_border(d, s.bd, tid - 256, mbx, mby);
+    else if (tid >= 320 && tid < 352) s.motion_cost[(tid - 320) >> 2][tid & 3] = 0;
+    else if (ROLE == 1 && tid >= 384 && tid < 512) load_orgc(d, s.nb, tid - 384, mbx, mby);
+    else if (ROLE == 1 && tid >= 512 && tid < 608) load_intra_nb(d, s.nb, tid - 512, mbx, mby);
+    int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
     const int wdim = 2 * sr + 16 + 2 * WM;
-    {
+    if (slice_p) {
+        // SetupFastFullPelSearch: centre = 16x16 MVP / 4 (trunc), clamped to +-SR; the window
+        // load starts right away (its centre depends only on the border cells)
+        __syncthreads();
+        set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
+        scx = iclip(-sr, sr, pcx / 4); scy = iclip(-sr, sr, pcy / 4);
         const int X0 = pix_x + scx - sr - WM, Y0 = pix_y + scy - sr - WM;
-        for (int i = tid; i < wdim * WST; i += NTA) {
-            int y = i / WST, x = i - y * WST;
-            G[i] = x < wdim ? d.refY[iclip(0, d.H - 1, Y0 + y) * W + iclip(0, W - 1, X0 + x)] : 0;
-        }
+        constexpr int RPP = NTA / WST;                  // window rows per pass
+        const int yi = tid / WST, xi = tid - yi * WST;
+        const int xs = iclip(0, W - 1, X0 + xi);
+        if (yi < RPP)
+            for (int y = yi; y < wdim; y += RPP) G[y * WST + xi] = xi < wdim ? d.refY[iclip(0, d.H - 1, Y0 + y) * W + xs] : 0;
         if (tid < 32) G[wdim * WST + tid] = 0;
     }
     __syncthreads();
     PSTAMP(pb + 1);
-    // ---- 16 4x4 SADs for this thread's column strip of NPK positions (registers)
-    const int nstrips = (side + NPK - 1) / NPK;
-    const bool sact = tid < side * nstrips;
-    const int dx = sact ? tid % side : 0, dy0 = sact ? (tid / side) * NPK : 0;
-    uint32_t sadp[NPK][8];
-    {
-        const uint4 *og = reinterpret_cast<const uint4 *>(s.org);   // LDS broadcast, one MB row per read
-        uint32_t acc[NPK][4];
+    if (slice_p) {
+        // ---- 16 4x4 SADs for this thread's column strip of NPK positions (registers)
+        PosState ps;
+        const int nstrips = (side + NPK - 1) / NPK;
+        const bool sact = tid < side * nstrips;
+        ps.dx = sact ? tid % side : 0;
+        ps.dy0 = sact ? (tid / side) * NPK : 0;
+        {
+            const uint4 *og = reinterpret_cast<const uint4 *>(s.org);   // LDS broadcast, one MB row per read
+            uint32_t acc[NPK][4];
 #pragma unroll
-        for (int k = 0; k < NPK; k++)
+            for (int k = 0; k < NPK; k++)
 #pragma unroll
-            for (int b = 0; b < 4; b++) acc[k][b] = 0;
-        const int wx = dx + WM;
-        const uint32_t sel = wx & 3;
-        const uint8_t *wb = G + (dy0 + WM) * WST + (wx & ~3);
+                for (int b = 0; b < 4; b++) acc[k][b] = 0;
+            const int wx = ps.dx + WM;
+            const uint32_t sel = wx & 3;
+            const uint8_t *wb = G + (ps.dy0 + WM) * WST + (wx & ~3);
 #pragma unroll
-        for (int r = 0; r < 16 + NPK - 1; r++) {
-            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(wb + r * WST);
-            const uint32_t a0 = w32[0], a1 = w32[1], a2 = w32[2], a3 = w32[3], a4 = w32[4];
-            const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sel), w1 = __builtin_amdgcn_alignbyte(a2, a1, sel);
-            const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sel), w3 = __builtin_amdgcn_alignbyte(a4, a3, sel);
+            for (int r = 0; r < 16 + NPK - 1; r++) {
+                const uint32_t *w32 = reinterpret_cast<const uint32_t *>(wb + r * WST);
+                const uint32_t a0 = w32[0], a1 = w32[1], a2 = w32[2], a3 = w32[3], a4 = w32[4];
+                const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sel), w1 = __builtin_amdgcn_alignbyte(a2, a1, sel);
+                const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sel), w3 = __builtin_amdgcn_alignbyte(a4, a3, sel);
 #pragma unroll
-            for (int k = 0; k < NPK; k++) {
-                const int mr = r - k;
-                if (mr < 0 || mr > 15) continue;
-                const uint4 o = og[mr];
-                acc[k][0] = __builtin_amdgcn_sad_u8(w0, o.x, acc[k][0]);
-                acc[k][1] = __builtin_amdgcn_sad_u8(w1, o.y, acc[k][1]);
-                acc[k][2] = __builtin_amdgcn_sad_u8(w2, o.z, acc[k][2]);
-                acc[k][3] = __builtin_amdgcn_sad_u8(w3, o.w, acc[k][3]);
-                if ((mr & 3) == 3) {
-                    sadp[k][2 * (mr >> 2)] = acc[k][0] | (acc[k][1] << 16);
-                    sadp[k][2 * (mr >> 2) + 1] = acc[k][2] | (acc[k][3] << 16);
-                    acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
+                for (int k = 0; k < NPK; k++) {
+                    const int mr = r - k;
+                    if (mr < 0 || mr > 15) continue;
+                    const uint4 o = og[mr];
+                    acc[k][0] = __builtin_amdgcn_sad_u8(w0, o.x, acc[k][0]);
+                    acc[k][1] = __builtin_amdgcn_sad_u8(w1, o.y, acc[k][1]);
+                    acc[k][2] = __builtin_amdgcn_sad_u8(w2, o.z, acc[k][2]);
+                    acc[k][3] = __builtin_amdgcn_sad_u8(w3, o.w, acc[k][3]);
+                    if ((mr & 3) == 3) {
+                        ps.sadp[k][2 * (mr >> 2)] = acc[k][0] | (acc[k][1] << 16);
+                        ps.sadp[k][2 * (mr >> 2) + 1] = acc[k][2] | (acc[k][3] << 16);
+                        acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
+                    }
                 }
             }
         }
-    }
-    uint32_t pinfo[NPK];   // JM order (13 bits) | Chebyshev radius << 16; invalid: radius 0xFFFF
 #pragma unroll
-    for (int k = 0; k < NPK; k++) {
-        const int dy = dy0 + k, rx = dx - sr, ry = dy - sr;
-        if (!sact || dy >= side) pinfo[k] = 0xFFFF1FFFu;
-        else if (rx == -scx && ry == -scy) pinfo[k] = 0;   // the (0,0) pre-check position: order 0, never range-limited
-        else pinfo[k] = (uint32_t)(spiral_index(rx, ry) + 1) | ((uint32_t)max(abs(rx), abs(ry)) << 16);
+        for (int k = 0; k < NPK; k++) {
+            const int dy = ps.dy0 + k, rx = ps.dx - sr, ry = dy - sr;
+            if (!sact || dy >= side) ps.ordk[k] = 0xFFFFFFFFu;
+            else if (rx == -scx && ry == -scy) ps.ordk[k] = 0;   // the (0,0) pre-check position
+            else ps.ordk[k] = (uint32_t)(spiral_index(rx, ry) + 1);
+        }
+        // ---- half-pel planes over window coords [3, 2sr+20]^2: h1 and h = clip(h1) by column
+        //      runs (sliding 6-tap), b by rows; then j from h1
+        {
+            const int lo = WM - 1, n = 2 * sr + 18, h1w = wdim - 1;
+            uint8_t *PB = s.planes + PLS, *PH = s.planes + 2 * PLS, *PJ = s.planes + 3 * PLS;
+            const int cx = 1 + tid % 96, rb = tid / 96;                // 96 columns x 8 row runs
+            const int run = (n + 7) >> 3, y0 = lo + rb * run, y1 = min(lo + n, y0 + run);
+            if (cx <= h1w) {
+                const uint8_t *g = G + cx;
+                int t0 = g[(y0 - 2) * WST], t1 = g[(y0 - 1) * WST], t2 = g[y0 * WST], t3 = g[(y0 + 1) * WST], t4 = g[(y0 + 2) * WST];
+                const bool inb = cx >= lo && cx < lo + n;
+                for (int y = y0; y < y1; y++) {
+                    const int t5 = g[(y + 3) * WST];
+                    const int v = tap6(t0, t1, t2, t3, t4, t5);
+                    s.h1[y * WST + cx] = (int16_t)v;
+                    if (inb) {
+                        PH[y * WST + cx] = (uint8_t)clip255((v + 16) >> 5);
+                        const uint8_t *q = G + y * WST + cx;
+                        PB[y * WST + cx] = (uint8_t)clip255((tap6(q[-2], q[-1], q[0], q[1], q[2], q[3]) + 16) >> 5);
+                    }
+                    t0 = t1; t1 = t2; t2 = t3; t3 = t4; t4 = t5;
+                }
+            }
+            __syncthreads();
+            if (cx >= lo && cx < lo + n)
+                for (int y = y0; y < y1; y++) {
+                    const int16_t *h = s.h1 + y * WST + cx;
+                    PJ[y * WST + cx] = (uint8_t)clip255((tap6(h[-2], h[-1], h[0], h[1], h[2], h[3]) + 512) >> 10);
+                }
+            // j is first read after the next stage's barriers
+        }
+        PSTAMP(pb + 2);
+        if constexpr (ROLE == 1) {
+            unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
+            int pmvx, pmvy;
+            {   // stage 0: 16x16, 16x8 upper, 8x16 left
+                const bool act = team < 3;
+                const int bt = 1 + team;
+                stage_head(d, s, act, bt, 0, 0, 0, 0, scx, scy, pmvx, pmvy);
+                EVAL(0, 1, 0, 0); EVAL(1, 2, 0, 0); EVAL(2, 3, 0, 0);
+                stage_reduce(s, 0x7, bk);
+                stage_tail(d, s, act, bt, 0, 0, 0, pmvx, pmvy, scx, scy);
+            }
+            {   // stage 1: 16x8 lower, 8x16 right
+                const bool act = team == 1 || team == 2;
+                const int bt = 1 + team, bx4 = team == 2 ? 2 : 0, by4 = team == 1 ? 2 : 0;
+                stage_head(d, s, act, bt, bx4, by4, 0, 0, scx, scy, pmvx, pmvy);
+                EVAL(1, 2, 0, 2); EVAL(2, 3, 2, 0);
+                stage_reduce(s, 0x6, bk);
+                stage_tail(d, s, act, bt, bx4, by4, 1, pmvx, pmvy, scx, scy);
+            }
+            // results: MVs of types 1..3, partition costs, FindSkipModeMotionVector
+            if (tid < 96) {
+                const int m = 1 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
+                scr->all_mv[m][k][c] = s.all_mv[m][k][c];
+            } else if (tid >= 128 && tid < 140) {
+                const int m = 1 + (tid - 128) / 4, k = tid & 3;
+                scr->motion_cost[m][k] = s.motion_cost[m][k];
+            } else if (tid == 192) {
+                NbBorder nbv{s.bd};
+                int ra = -1, ax = 0, ay = 0, rb = -1, bx = 0, by = 0;
+                const bool aa = nbv(-1, 0, ra, ax, ay), ab = nbv(0, -1, rb, bx, by);
+                const bool zl = !aa || (ra == 0 && ax == 0 && ay == 0), za = !ab || (rb == 0 && bx == 0 && by == 0);
+                scr->skipx = (za || zl) ? 0 : pcx;
+                scr->skipy = (za || zl) ? 0 : pcy;
+            }
+        } else {
+            int best8x8 = 0, cost8x8 = 0;
+            p8x8_block<0>(d, s, ps, scx, scy, best8x8, cost8x8);
+            PSTAMP(3);
+            p8x8_block<1>(d, s, ps, scx, scy, best8x8, cost8x8);
+            PSTAMP(4);
+            p8x8_block<2>(d, s, ps, scx, scy, best8x8, cost8x8);
+            PSTAMP(5);
+            p8x8_block<3>(d, s, ps, scx, scy, best8x8, cost8x8);
+            if (tid < 128) {
+                const int m = 4 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
+                scr->all_mv[m][k][c] = s.all_mv[m][k][c];
+            } else if (tid < 144) {
+                const int m = 4 + (tid - 128) / 4, k = tid & 3;
+                scr->motion_cost[m][k] = s.motion_cost[m][k];
+            } else if (tid == 192) {
+                scr->best8x8 = best8x8; scr->cost8x8 = cost8x8;
+            }
+            PSTAMP(6);
+        }
     }
-    // ---- half-pel planes of the window: h1 (vertical intermediates), b, h; then j
-    {
-        const int lo = WM - 1, n = 2 * sr + 18, h1w = wdim - 1;
-        uint8_t *PB = s.planes + PLS, *PH = s.planes + 2 * PLS;
-        for (int i = tid; i < h1w * n; i += NTA) {
-            const int y = lo + i / h1w, x = 1 + i % h1w;
-            const uint8_t *g = G + (y - 2) * WST + x;
-            s.h1[y * WST + x] = (int16_t)tap6(g[0], g[WST], g[2 * WST], g[3 * WST], g[4 * WST], g[5 * WST]);
-        }
-        for (int i = tid; i < n * n; i += NTA) {
-            const int y = lo + i / n, x = lo + i % n;
-            const uint8_t *g = G + y * WST + x;
-            PB[y * WST + x] = (uint8_t)clip255((tap6(g[-2], g[-1], g[0], g[1], g[2], g[3]) + 16) >> 5);
-            PH[y * WST + x] = (uint8_t)clip255((tap6(g[-2 * WST], g[-WST], g[0], g[WST], g[2 * WST], g[3 * WST]) + 16) >> 5);
-        }
-        __syncthreads();
-        uint8_t *PJ = s.planes + 3 * PLS;
-        for (int i = tid; i < n * n; i += NTA) {
-            const int y = lo + i / n, x = lo + i % n;
-            const int16_t *h = s.h1 + y * WST + x;
-            PJ[y * WST + x] = (uint8_t)clip255((tap6(h[-2], h[-1], h[0], h[1], h[2], h[3]) + 512) >> 10);
-        }
-        // j is first read after the next stage's barriers
-    }
-    PSTAMP(pb + 2);
-    MbScratch *scr = d.scr + mby * d.mbw + mbx;
-    if constexpr (ROLE == 1) {
-        unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
-        int pmvx, pmvy;
-        {   // stage 0: 16x16, 16x8 upper, 8x16 left
-            const bool act = team < 3;
-            const int bt = 1 + team;
-            stage_head(d, s, act, bt, 0, 0, 0, 0, scx, scy, pmvx, pmvy);
-            EVAL(0, 1, 0, 0); EVAL(1, 2, 0, 0); EVAL(2, 3, 0, 0);
-            stage_reduce(s, 0x7, bk);
-            stage_tail(d, s, act, bt, 0, 0, 0, pmvx, pmvy, scx, scy);
-        }
-        {   // stage 1: 16x8 lower, 8x16 right
-            const bool act = team == 1 || team == 2;
-            const int bt = 1 + team, bx4 = team == 2 ? 2 : 0, by4 = team == 1 ? 2 : 0;
-            stage_head(d, s, act, bt, bx4, by4, 0, 0, scx, scy, pmvx, pmvy);
-            EVAL(1, 2, 0, 2); EVAL(2, 3, 2, 0);
-            stage_reduce(s, 0x6, bk);
-            stage_tail(d, s, act, bt, bx4, by4, 1, pmvx, pmvy, scx, scy);
-        }
-        // results: MVs of types 1..3, partition costs, FindSkipModeMotionVector
-        if (tid < 96) {
-            const int m = 1 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
-            scr->all_mv[m][k][c] = s.all_mv[m][k][c];
-        }
-        if (tid >= 128 && tid < 140) { const int m = 1 + (tid - 128) / 4, k = tid & 3; scr->motion_cost[m][k] = s.motion_cost[m][k]; }
-        if (tid == 192) {
-            NbBorder nb{s.bd};
-            int ra = -1, ax = 0, ay = 0, rb = -1, bx = 0, by = 0;
-            const bool aa = nb(-1, 0, ra, ax, ay), ab = nb(0, -1, rb, bx, by);
-            const bool zl = !aa || (ra == 0 && ax == 0 && ay == 0), za = !ab || (rb == 0 && bx == 0 && by == 0);
-            scr->skipx = (za || zl) ? 0 : pcx;
-            scr->skipy = (za || zl) ? 0 : pcy;
-        }
+    if constexpr (ROLE == 1) {   // Intra16x16 (wave 0) and chroma intra mode (wave 1) decisions
+        const int wave = tid >> 6, lane = tid & 63;
+        if (wave == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
+        else if (wave == 1) chroma_decision(d, s.nb, scr, lane, avL, avT, avTL);
         PSTAMP(pb + 3);
-    } else {
-        int best8x8 = 0, cost8x8 = 0;
-        p8x8_block<0>(d, s, sadp, pinfo, dx, dy0, scx, scy, best8x8, cost8x8);
-        PSTAMP(3);
-        p8x8_block<1>(d, s, sadp, pinfo, dx, dy0, scx, scy, best8x8, cost8x8);
-        PSTAMP(4);
-        p8x8_block<2>(d, s, sadp, pinfo, dx, dy0, scx, scy, best8x8, cost8x8);
-        PSTAMP(5);
-        p8x8_block<3>(d, s, sadp, pinfo, dx, dy0, scx, scy, best8x8, cost8x8);
-        if (tid < 128) {
-            const int m = 4 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
-            scr->all_mv[m][k][c] = s.all_mv[m][k][c];
-        }
-        if (tid >= 128 && tid < 144) { const int m = 4 + (tid - 128) / 4, k = tid & 3; scr->motion_cost[m][k] = s.motion_cost[m][k]; }
-        if (tid == 192) { scr->best8x8 = best8x8; scr->cost8x8 = cost8x8; }
-        PSTAMP(6);
     }
 }
 
-// MB-relative luma reconstruction sample for intra prediction (border rows/columns from LDS)
+// ======================================================================================
+//  role 0: Intra4x4 (Mode_Decision_for_Intra4x4Macroblock) in 10 diagonal steps
+// ======================================================================================
 __device__ __forceinline__ int lpix(const IntraS &s, int x, int y) {
-    if (y < 0) return s.rtop[x + 1];
-    if (x < 0) return s.rleft[y];
+    if (y < 0) return s.nb.rtop[x + 1];
+    if (x < 0) return s.nb.rleft[y];
     return s.rec[16 * y + x];
 }
 
-// intra role: wave 0 Intra4x4 (wave-synchronous, no workgroup barriers), wave 1 Intra16x16,
-// wave 2 chroma intra mode. The three decisions are independent of each other.
+// one 4x4 block on one wave: 9 modes x 16 pixels in 3 passes, DPP SATD, then dct_luma on
+// lanes 0..15 of the chosen prediction
+__device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratch *scr, int w, int bx4, int by4, const int (&tab)[3],
+                                         bool avL, bool avT, bool avTL, bool avTR, int qpk, int (&acc)[3]) {
+    const int lane = threadIdx.x & 63, l = lane & 15, g = lane >> 4;
+    const int bx = 4 * bx4, by = 4 * by4, blk = 4 * by4 + bx4;
+    const int lambda = d.lambda_mode, qp = d.qp, had = d.use_hadamard;
+    const bool up = by > 0 || avT, left = bx > 0 || avL;
+    const bool ul = (bx > 0 && by > 0) || (bx == 0 && by > 0 && avL) || (bx > 0 && by == 0 && avT) || (bx == 0 && by == 0 && avTL);
+    bool ur = by == 0 ? (bx + 4 <= 15 ? avT : avTR) : (bx + 4 <= 15);
+    if ((bx == 4 || bx == 12) && (by == 4 || by == 12)) ur = false;
+    int *P = s.i4P[w];
+    if (lane < 13) {
+        int v;
+        if (lane == 0) v = ul ? lpix(s, bx - 1, by - 1) : 0;
+        else if (lane <= 4) v = up ? lpix(s, bx + lane - 1, by - 1) : 0;
+        else if (lane <= 8) v = up ? lpix(s, ur ? bx + lane - 1 : bx + 3, by - 1) : 0;
+        else v = left ? lpix(s, bx - 1, by + lane - 9) : 0;
+        P[lane] = v;
+    }
+    const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + bx4];
+    const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + by4];
+    const int mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
+    wave_lds_sync();
+    const int org = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];
+    const int st = P[1] + P[2] + P[3] + P[4], sl = P[9] + P[10] + P[11] + P[12];
+    const int dc = (up && left) ? (st + sl + 4) >> 3 : left ? (sl + 2) >> 2 : up ? (st + 2) >> 2 : 128;
+    int pv[3], cst[3];
+#pragma unroll
+    for (int it = 0; it < 3; it++) {
+        const int m = 4 * it + g;
+        pv[it] = 0; cst[it] = BIGCOST + 1;
+        if (m < 9) {
+            const int e = tab[it], ty = e & 3;
+            const int a = P[(e >> 2) & 15], b = P[(e >> 6) & 15], c = P[(e >> 10) & 15];
+            const int p = ty == 1 ? (a + b + 1) >> 1 : ty == 2 ? (a + 2 * b + c + 2) >> 2 : dc;
+            const int sat = had ? row16_sum(abs(row16_had(org - p, l))) >> 1 : row16_sum(abs(org - p));
+            const bool avm = m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul);
+            pv[it] = p;
+            cst[it] = avm ? (m == mpm ? 0 : 4 * lambda) + sat : BIGCOST + 1;
+        }
+    }
+    int best = 0, bc = BIGCOST;
+#pragma unroll
+    for (int m = 0; m < 9; m++) {
+        const int c = __builtin_amdgcn_readlane(cst[m >> 2], 16 * (m & 3));
+        if (c < bc) { bc = c; best = m; }
+    }
+    const int src = (best >> 2) == 0 ? pv[0] : (best >> 2) == 1 ? pv[1] : pv[2];
+    const int pp = __shfl(src, 16 * (best & 3) + l, 64);
+    unsigned nz = 0;
+    if (lane < 16) {
+        const int c = lane_fwd4x4(org - pp, l);
+        int lev, dq, cc;
+        nz = lane_quant(c, l, qp, qpk, false, lev, dq, cc);
+        scr->i4lev[blk][l] = (int16_t)lev;
+        s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (uint8_t)lane_inv4x4(dq, l, pp);
+        if (l == 0) s.ipred_cur[blk] = (int8_t)best;
+    }
+    nz = __builtin_amdgcn_readlane(nz, 0);
+    acc[0] += bc;
+    if (nz) { acc[1] |= 1 << ((by4 >> 1) * 2 + (bx4 >> 1)); acc[2] |= 1 << blk; }
+}
+
 __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, Wc = d.Wc;
+    const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
+    const bool prof = prof_mb_here(d, mbx, mby);
+    PSTAMP(12);
     if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    else if (tid < 384) {
-        const int uv = (tid - 256) >> 6, k = tid & 63;
-        s.orgc[uv][k] = (uv ? d.orgV : d.orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
-    } else if (tid < 394) load_border(d, s.bd, tid - 384, mbx, mby);
-    else if (tid >= 400 && tid < 421) {            // luma row y = -1, x = -1..19
-        const int x = tid - 401;
-        const bool av = x < 0 ? avTL : x < 16 ? avT : avTR;
-        s.rtop[x + 1] = av ? d.recY[(pix_y - 1) * W + pix_x + x] : 0;
-    } else if (tid >= 448 && tid < 464) {
-        const int y = tid - 448;
-        s.rleft[y] = avL ? d.recY[(pix_y + y) * W + pix_x - 1] : 0;
-    } else if (tid >= 464 && tid < 482) {          // chroma rows y = -1, x = -1..7
-        const int i = tid - 464, uv = i / 9, x = i - 9 * uv - 1;
-        const bool av = x < 0 ? avTL : avT;
-        s.ctop[uv][x + 1] = av ? (uv ? d.recV : d.recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
-    } else if (tid >= 512 && tid < 528) {
-        const int i = tid - 512, uv = i >> 3, y = i & 7;
-        s.cleft[uv][y] = avL ? (uv ? d.recV : d.recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
-    }
-    __syncthreads();
+    else if (tid < 266) load_border(d, s.bd, tid - 256, mbx, mby);
+    else if (tid >= 320 && tid < 416) load_intra_nb(d, s.nb, tid - 320, mbx, mby);
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
-    const int lambda = d.lambda_mode, qp = d.qp, had = d.use_hadamard;
-    if (wave == 0) {
-        // ======== Mode_Decision_for_Intra4x4Macroblock: 16 blocks, 9 modes x 16 pixels per pass
-        const bool prof = prof_mb_here(d, mbx, mby, 0);
-        PSTAMP(12);
-        const int q_bits = 15 + qp / 6;
-        const int qpk = d.slice_type == JMH_P_SLICE ? (1 << q_bits) / 6 : (1 << q_bits) / 3;
-        const int l = lane & 15, g = lane >> 4;
-        int i4cost = 0, i4cbp = 0, i4blk = 0;
-        for (int b8 = 0; b8 < 4; b8++) {
-            int cost8 = 6 * lambda;                                  // (int)floor(6*lambda+0.4999)
-            for (int b4 = 0; b4 < 4; b4++) {
-                const int bx = 8 * (b8 & 1) + 4 * (b4 & 1), by = 8 * (b8 >> 1) + 4 * (b4 >> 1);
-                const int blk = (by >> 2) * 4 + (bx >> 2);
-                const bool up = by > 0 || avT, left = bx > 0 || avL;
-                const bool ul = (bx > 0 && by > 0) || (bx == 0 && by > 0 && avL) || (bx > 0 && by == 0 && avT) || (bx == 0 && by == 0 && avTL);
-                bool ur = by == 0 ? (bx + 4 <= 15 ? avT : avTR) : (bx + 4 <= 15);
-                if ((bx == 4 || bx == 12) && (by == 4 || by == 12)) ur = false;
-                if (lane < 13) {
-                    int v;
-                    if (lane == 0) v = ul ? lpix(s, bx - 1, by - 1) : 0;
-                    else if (lane <= 4) v = up ? lpix(s, bx + lane - 1, by - 1) : 0;
-                    else if (lane <= 8) v = up ? lpix(s, ur ? bx + lane - 1 : bx + 3, by - 1) : 0;
-                    else v = left ? lpix(s, bx - 1, by + lane - 9) : 0;
-                    s.i4P[lane] = v;
-                }
-                const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + (bx >> 2)];
-                const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + (by >> 2)];
-                const int mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
-                wave_lds_sync();
-                const int o = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];
-                int pv[3], cst[3];
+    const int q_bits = 15 + d.qp / 6;
+    const int qpk = d.slice_type == JMH_P_SLICE ? (1 << q_bits) / 6 : (1 << q_bits) / 3;
+    int tab[3];
 #pragma unroll
-                for (int it = 0; it < 3; it++) {
-                    const int m = 4 * it + g;
-                    pv[it] = 0; cst[it] = BIGCOST + 1;
-                    if (m < 9) {
-                        const bool avm = m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul);
-                        const int p = i4_pred_px(s.i4P, up, left, m, l & 3, l >> 2);
-                        const int sat = lane_satd(o - p, l, had);
-                        pv[it] = p;
-                        cst[it] = avm ? (m == mpm ? 0 : 4 * lambda) + sat : BIGCOST + 1;
-                    }
-                }
-                int best = 0, bc = BIGCOST;
-#pragma unroll
-                for (int m = 0; m < 9; m++) {
-                    const int c = __builtin_amdgcn_readlane(cst[m >> 2], 16 * (m & 3));
-                    if (c < bc) { bc = c; best = m; }
-                }
-                const int src = (best >> 2) == 0 ? pv[0] : (best >> 2) == 1 ? pv[1] : pv[2];
-                const int pp = __shfl(src, 16 * (best & 3) + l, 64);
-                unsigned nz = 0;
-                if (lane < 16) {                                       // dct_luma on the chosen prediction
-                    const int c = lane_fwd4x4(o - pp, l);
-                    int lev, dq, cc;
-                    nz = lane_quant(c, l, qp, qpk, false, lev, dq, cc);
-                    scr->i4lev[blk][l] = (int16_t)lev;
-                    s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (uint8_t)lane_inv4x4(dq, l, pp);
-                    if (l == 0) s.ipred_cur[blk] = (int8_t)best;
-                }
-                nz = __builtin_amdgcn_readlane(nz, 0);
-                cost8 += bc;
-                if (nz) { i4cbp |= 1 << b8; i4blk |= 1 << blk; }
-                wave_lds_sync();
-            }
-            i4cost += cost8;
-        }
-        if (lane == 0) { scr->i4cost = i4cost; scr->i4cbp = i4cbp; scr->i4blk = i4blk; }
-        if (lane < 16) scr->ipred[lane] = s.ipred_cur[lane];
-        reinterpret_cast<uint32_t *>(scr->i4rec)[lane] = reinterpret_cast<const uint32_t *>(s.rec)[lane];
-        PSTAMP(13);
-    } else if (wave == 1) {
-        // ======== intrapred_luma_16x16 + find_sad_16x16: 4 modes x 16 blocks = 64 lanes
-        const bool prof = prof_mb_here(d, mbx, mby, 1);
-        const int m = lane >> 4, b = lane & 15, ox = (b & 3) * 4, oy = (b >> 2) * 4;
-        const uint8_t *T = s.rtop + 1, *L = s.rleft;
-        const I16Par par = i16_params(T, L, avT, avL);
-        int mm[16], t[16];
-        for (int yy = 0; yy < 4; yy++)
-            for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = s.org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy);
-        for (int yy = 0; yy < 4; yy++) {
-            int *r = mm + 4 * yy;
-            int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
-            t[4 * yy] = a0 + a1; t[4 * yy + 2] = a0 - a1; t[4 * yy + 1] = a2 + a3; t[4 * yy + 3] = a3 - a2;
-        }
-        int acs = 0, dcc = 0;
-        for (int xx = 0; xx < 4; xx++) {
-            int a0 = t[xx] + t[12 + xx], a1 = t[4 + xx] + t[8 + xx], a2 = t[4 + xx] - t[8 + xx], a3 = t[xx] - t[12 + xx];
-            int o0 = a0 + a1, o2 = a0 - a1, o1 = a2 + a3, o3 = a3 - a2;
-            if (xx == 0) dcc = o0; else acs += abs(o0);
-            acs += abs(o1) + abs(o2) + abs(o3);
-        }
-        const int cost = row16_sum(acs) + lane_had_abs(dcc / 4, b);
-        const bool av16[4] = {avT, avL, true, avT && avL && avTL};
-        int best = MAX_VALUE, i16mode = 2;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int c = __builtin_amdgcn_readlane(cost, 16 * k);
-            if (av16[k] && c < best) { best = c; i16mode = k; }
-        }
-        if (lane == 0) { scr->i16cost = best / 2; scr->i16mode = i16mode; }
-        PSTAMP(14);
-    } else if (wave == 2) {
-        // ======== IntraChromaPrediction8x8 mode decision: 4 modes x 2 components x 4 blocks
-        const bool prof = prof_mb_here(d, mbx, mby, 2);
-        int sat = 0;
-        if (lane < 32) {
-            const int m = lane >> 3, uv = (lane >> 2) & 1, b = lane & 3, xo = (b & 1) * 4, yo = (b >> 1) * 4;
-            const uint8_t *T = s.ctop[uv] + 1, *L = s.cleft[uv];
-            int df[16];
-            for (int y = 0; y < 4; y++)
-                for (int x = 0; x < 4; x++)
-                    df[4 * y + x] = s.orgc[uv][(yo + y) * 8 + xo + x] - chroma_pred_px(T, L, s.ctop[uv][0], avT, avL, m, xo + x, yo + y);
-            sat = satd4x4(df, had);
-        }
-        const bool cav[4] = {true, avL, avT, avT && avL && avTL};
-        int minc = BIGCOST, c_mode = 0;
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            int c = 0;
-#pragma unroll
-            for (int q = 0; q < 8; q++) c += __builtin_amdgcn_readlane(sat, 8 * m + q);
-            if (cav[m] && c < minc) { minc = c; c_mode = m; }
-        }
-        if (lane == 0) scr->c_mode = c_mode;
-        PSTAMP(15);
+    for (int it = 0; it < 3; it++) {
+        const int m = 4 * it + ((lane >> 4) & 3);
+        tab[it] = m < 9 ? c_i4tab[m][lane & 15] : 0;
     }
+    int acc[3] = {0, 0, 0};                   // cost, cbp (per b8), block mask
+    __syncthreads();
+    for (int dg = 0; dg < 10; dg++) {         // blocks with bx4 + 2*by4 == dg, by4 ascending
+        const int by_lo = dg > 3 ? (dg - 2) >> 1 : 0;
+        const int by4 = by_lo + wave, bx4 = dg - 2 * by4;
+        if (wave < 2 && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+        __syncthreads();
+    }
+    if (wave < 2 && lane == 0) { s.part[wave][0] = acc[0]; s.part[wave][1] = acc[1]; s.part[wave][2] = acc[2]; }
+    __syncthreads();
+    if (tid == 0) {
+        scr->i4cost = 24 * d.lambda_mode + s.part[0][0] + s.part[1][0];   // 4 x (int)floor(6*lambda+0.4999)
+        scr->i4cbp = s.part[0][1] | s.part[1][1];
+        scr->i4blk = s.part[0][2] | s.part[1][2];
+    }
+    if (tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
+    if (tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
+    PSTAMP(13);
 }
 
 __global__ __launch_bounds__(NTA) void k_mb_analyse(DevParams d) {
     __shared__ AnalyseS s;
     const int n = d.ndiag;
-    int role = 0, i = blockIdx.x;
-    if (d.slice_type == JMH_P_SLICE) { role = 2 - (int)blockIdx.x / n; i = blockIdx.x % n; }
+    // P slices: [0,n) role 2 (longest, dispatched first), [n,2n) role 1, [2n,3n) role 0
+    // I slices: [0,n) role 0, [n,2n) role 1 (intra decisions only)
+    const int grp = blockIdx.x / n, i = blockIdx.x % n;
+    const int role = d.slice_type == JMH_P_SLICE ? 2 - grp : (grp == 0 ? 0 : 1);
     const int mby = d.y_min + i, mbx = d.diag - 2 * mby;
     if (role == 2) me_role<2>(d, s.me, mbx, mby);
     else if (role == 1) me_role<1>(d, s.me, mbx, mby);
@@ -589,7 +704,7 @@ __global__ __launch_bounds__(NTA) void k_mb_analyse(DevParams d) {
 }
 
 hipError_t jmh_launch_analyse(const DevParams &p, hipStream_t st) {
-    const int nblocks = p.slice_type == JMH_P_SLICE ? 3 * p.ndiag : p.ndiag;
+    const int nblocks = (p.slice_type == JMH_P_SLICE ? 3 : 2) * p.ndiag;
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, p);
     return hipGetLastError();
 }

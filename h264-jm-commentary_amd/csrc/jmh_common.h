@@ -46,8 +46,9 @@ __device__ __forceinline__ int spiral_index(int x, int y) {
 }
 __device__ __forceinline__ void spiral_pos(int k, int &x, int &y) {
     if (k == 0) { x = y = 0; return; }
-    int l = 1;
-    while ((2 * l + 1) * (2 * l + 1) <= k) l++;
+    int l = max(1, (int)((sqrtf((float)k) + 1.0f) * 0.5f));   // ring: (2l-1)^2 <= k < (2l+1)^2
+    if ((2 * l + 1) * (2 * l + 1) <= k) l++;
+    if ((2 * l - 1) * (2 * l - 1) > k) l--;
     int o = k - (2 * l - 1) * (2 * l - 1);
     if (o < 2 * (2 * l - 1)) { x = (o >> 1) - l + 1; y = (o & 1) ? l : -l; }
     else { o -= 2 * (2 * l - 1); y = (o >> 1) - l; x = (o & 1) ? l : -l; }
@@ -56,29 +57,38 @@ __device__ __forceinline__ void spiral_pos(int k, int &x, int &y) {
 __device__ __forceinline__ int coeff_cost_run(int run) { return run == 0 ? 3 : run <= 2 ? 2 : run <= 5 ? 1 : 0; }
 
 // ---- cross-lane helpers ----------------------------------------------------------------
-// DPP: quad_perm [1,0,3,2] (0xB1), [2,3,0,1] (0x4E), row_half_mirror (0x141), row_mirror (0x140)
-__device__ __forceinline__ int dpp_(int v, int ctrl) {
-    switch (ctrl) {
-    case 0xB1: return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);
-    case 0x4E: return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);
-    case 0x141: return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);
-    default: return __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false);
-    }
-}
+// DPP lane moves: quad_perm [1,0,3,2] (0xB1), [2,3,0,1] (0x4E), [3,2,1,0] (0x1B),
+// row_half_mirror (0x141), row_mirror (0x140), row_ror:8 (0x128) — all within a 16-lane row
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) { return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false); }
 // sum over each aligned 16-lane row (all 16 lanes must be active); every lane gets the sum
 __device__ __forceinline__ int row16_sum(int v) {
-    v += dpp_(v, 0xB1);
-    v += dpp_(v, 0x4E);
-    v += dpp_(v, 0x141);
-    v += dpp_(v, 0x140);
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return v;
+}
+// 4x4 Hadamard of a block held one sample per lane (l = 4y + x) of a 16-lane row: four
+// butterfly stages over lane ^1, ^2 (quad_perm), ^4 (half_mirror + quad reverse), ^8 (row_ror:8).
+// Outputs are the 16 Walsh coefficients in butterfly order (sums of |.| are order-free).
+__device__ __forceinline__ int row16_had(int v, int l) {
+    int p = dpp<0xB1>(v);
+    v = (l & 1) ? p - v : v + p;
+    p = dpp<0x4E>(v);
+    v = (l & 2) ? p - v : v + p;
+    p = dpp<0x1B>(dpp<0x141>(v));
+    v = (l & 4) ? p - v : v + p;
+    p = dpp<0x128>(v);
+    v = (l & 8) ? p - v : v + p;
     return v;
 }
 // minimum over the whole (fully active) wave, wave-uniform result
 __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
-    v = min(v, (unsigned)dpp_((int)v, 0xB1));
-    v = min(v, (unsigned)dpp_((int)v, 0x4E));
-    v = min(v, (unsigned)dpp_((int)v, 0x141));
-    v = min(v, (unsigned)dpp_((int)v, 0x140));
+    v = min(v, (unsigned)dpp<0xB1>((int)v));
+    v = min(v, (unsigned)dpp<0x4E>((int)v));
+    v = min(v, (unsigned)dpp<0x141>((int)v));
+    v = min(v, (unsigned)dpp<0x140>((int)v));
     unsigned a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
     unsigned c = __builtin_amdgcn_readlane(v, 32), e = __builtin_amdgcn_readlane(v, 48);
     return min(min(a, b), min(c, e));
@@ -165,16 +175,8 @@ __device__ __forceinline__ int satd4x4(const int d[16], int had) {
     }
     return s >> 1;
 }
-// 16-lane sum of |4x4 Hadamard| (no >>1); every lane of the (fully active) group gets the sum
-__device__ __forceinline__ int lane_had_abs(int dv, int l) {
-    int y = l >> 2, x = l & 3;
-    int v0 = g16(dv, 4 * y), v1 = g16(dv, 4 * y + 1), v2 = g16(dv, 4 * y + 2), v3 = g16(dv, 4 * y + 3);
-    int a0 = v0 + v3, a1 = v1 + v2, a2 = v1 - v2, a3 = v0 - v3;
-    int t = x == 0 ? a0 + a1 : x == 1 ? a0 - a1 : x == 2 ? a2 + a3 : a3 - a2;
-    int u0 = g16(t, x), u1 = g16(t, 4 + x), u2 = g16(t, 8 + x), u3 = g16(t, 12 + x);
-    a0 = u0 + u3; a1 = u1 + u2; a2 = u1 - u2; a3 = u0 - u3;
-    return row16_sum(abs(y == 0 ? a0 + a1 : y == 1 ? a0 - a1 : y == 2 ? a2 + a3 : a3 - a2));
-}
+// 16-lane sum of |4x4 Hadamard| (no >>1); every lane of the (fully active) row gets the sum
+__device__ __forceinline__ int lane_had_abs(int dv, int l) { return row16_sum(abs(row16_had(dv, l))); }
 // 16-lane SATD() [J]
 __device__ __forceinline__ int lane_satd(int dv, int l, int had) {
     return had ? lane_had_abs(dv, l) >> 1 : row16_sum(abs(dv));

@@ -340,7 +340,7 @@ int jmh_sync(jmh_ctx *c) {
         unsigned long long t0 = ~0ull;
         for (int k = 0; k < 20; k++) if (h[k] && h[k] < t0) t0 = h[k];
         fprintf(stderr, "jmh_phase mb=%d us since first stamp:", c->prof_mb);
-        for (int k = 0; k < 20; k++) fprintf(stderr, " [%d]%.2f", k, h[k] ? (double)(h[k] - t0) * us : -1.0);
+        for (int k = 0; k < 64; k++) if (h[k]) fprintf(stderr, " [%d]%.2f", k, (double)(h[k] - t0) * us);
         fprintf(stderr, "\n");
         HCHK(hipMemset(c->d_prof, 0, sizeof(h)));
     }
