@@ -158,6 +158,17 @@ struct PosState {
     int dx, dy0;
 };
 
+// optimisation fence on the register-resident search state, once per stage: keeps the compiler
+// from hoisting unpacked partition sums of later stages (doubling the live registers)
+__device__ __forceinline__ void fence_state(PosState &ps) {
+#pragma unroll
+    for (int k = 0; k < NPK; k++) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) asm volatile("" : "+v"(ps.sadp[k][q]));
+        asm volatile("" : "+v"(ps.ordk[k]));
+    }
+}
+
 // this thread's best key for search (team J, partition BT/BX/BY); 'range' < sr only with
 // RestrictSearchRange 0 (positions outside are skipped, the (0,0) pre-check never is)
 template <int J, int BT, int BX, int BY>
@@ -191,7 +202,7 @@ __device__ __forceinline__ void stage_head(const DevParams &d, MeS &s, bool act,
     const int team = threadIdx.x / TEAM, u = threadIdx.x % TEAM, side = d.side, sr = d.sr, lam = d.lambda_motion;
     pmvx = pmvy = 0;
     if (act) {
-        set_mvp(NbMe{s, bt, b8, best8x8}, bx4, by4, c_blc[bt][0], c_blc[bt][1], pmvx, pmvy);
+        set_mvp(NbMe{s, bt, b8, best8x8}, bx4, by4, 4 << lw4_of(bt), 4 << lh4_of(bt), pmvx, pmvy);
         if (u < side) s.ctab[team][0][u] = (uint16_t)(lam * mvbits(((scx + u - sr) << 2) - pmvx));
         else if (u < 2 * side) s.ctab[team][1][u - side] = (uint16_t)(lam * mvbits(((scy + u - side - sr) << 2) - pmvy));
         else if (u < 2 * side + 18) s.ccost[(u - 2 * side) / 9][team][(u - 2 * side) % 9] = 0;
@@ -230,7 +241,7 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act,
         else spiral_pos((int)order - 1, rx, ry);
         fmx = scx + rx; fmy = scy + ry;
         min_mcost = (int)(best >> 13);
-        const int w4 = c_blc[bt][0] >> 2, h4 = c_blc[bt][1] >> 2;
+        const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt);
         lw4 = w4 >> 1;                         // log2 of w4 (1, 2, 4)
         lns = lw4 + (h4 >> 1);                // log2 of the sub-block count
         check0 = bt == 1 && fmx == 0 && fmy == 0 && had && d.slice_type == JMH_P_SLICE;
@@ -247,8 +258,8 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act,
             for (int t = g; t < ntask; t += NGRP) {   // uniform per 16-lane row
                 const int c = t >> lns, sub = t & ((1 << lns) - 1);
                 if (c < min_pos) continue;
-                const int ox = qx + step * c_sp9[c][0], oy = qy + step * c_sp9[c][1];
-                const int off = c_qoff[(oy & 3) * 4 + (ox & 3)];
+                const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+                const int off = qoff((oy & 3) * 4 + (ox & 3));
                 const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
                 const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
                 const int oB = ((xb & 1) + 2 * (yb & 1)) * PLS + (yb >> 1) * WST + (xb >> 1);
@@ -274,8 +285,8 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act,
                 const int v = s.ccost[pass][team][c];
                 if (v < min_mcost) { min_mcost = v; bpos = c; }
             }
-            qx += step * c_sp9[bpos][0];
-            qy += step * c_sp9[bpos][1];
+            qx += step * sp9x(bpos);
+            qy += step * sp9y(bpos);
         }
     }
     if (act) {
@@ -295,13 +306,14 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act,
 // one 8x8 block of P8x8: 4 stages (sub-modes 4..7 in parallel, then the 4x4 chain), then the
 // P8x8 sub-mode decision for the block and the reset of its stored MVs (via best8x8)
 template <int B8>
-__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, const PosState &ps, int scx, int scy, int &best8x8, int &cost8x8) {
+__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int scx, int scy, int &best8x8, int &cost8x8) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
     const int team = threadIdx.x / TEAM, sr = d.sr;
     unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
     int pmvx, pmvy;
     {   // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left
         const int bt = 4 + team;
+        fence_state(ps);
         stage_head(d, s, true, bt, X, Y, B8, best8x8, scx, scy, pmvx, pmvy);
         EVAL(0, 4, X, Y); EVAL(1, 5, X, Y); EVAL(2, 6, X, Y); EVAL(3, 7, X, Y);
         stage_reduce(s, 0xF, bk);
@@ -310,6 +322,7 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, const Pos
     {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right
         const bool act = team >= 1;
         const int bt = 4 + team, bx4 = team == 1 ? X : X + 1, by4 = team == 1 ? Y + 1 : Y;
+        fence_state(ps);
         stage_head(d, s, act, bt, bx4, by4, B8, best8x8, scx, scy, pmvx, pmvy);
         EVAL(1, 5, X, Y + 1); EVAL(2, 6, X + 1, Y); EVAL(3, 7, X + 1, Y);
         stage_reduce(s, 0xE, bk);
@@ -317,6 +330,7 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, const Pos
     }
     {   // stage 2: 4x4 bottom-left
         const bool act = team == 3;
+        fence_state(ps);
         stage_head(d, s, act, 7, X, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
         EVAL(3, 7, X, Y + 1);
         stage_reduce(s, 0x8, bk);
@@ -324,6 +338,7 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, const Pos
     }
     {   // stage 3: 4x4 bottom-right
         const bool act = team == 3;
+        fence_state(ps);
         stage_head(d, s, act, 7, X + 1, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
         EVAL(3, 7, X + 1, Y + 1);
         stage_reduce(s, 0x8, bk);
@@ -522,7 +537,8 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
             {   // stage 0: 16x16, 16x8 upper, 8x16 left
                 const bool act = team < 3;
                 const int bt = 1 + team;
-                stage_head(d, s, act, bt, 0, 0, 0, 0, scx, scy, pmvx, pmvy);
+                fence_state(ps);
+            stage_head(d, s, act, bt, 0, 0, 0, 0, scx, scy, pmvx, pmvy);
                 EVAL(0, 1, 0, 0); EVAL(1, 2, 0, 0); EVAL(2, 3, 0, 0);
                 stage_reduce(s, 0x7, bk);
                 stage_tail(d, s, act, bt, 0, 0, 0, pmvx, pmvy, scx, scy);
@@ -530,7 +546,8 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
             {   // stage 1: 16x8 lower, 8x16 right
                 const bool act = team == 1 || team == 2;
                 const int bt = 1 + team, bx4 = team == 2 ? 2 : 0, by4 = team == 1 ? 2 : 0;
-                stage_head(d, s, act, bt, bx4, by4, 0, 0, scx, scy, pmvx, pmvy);
+                fence_state(ps);
+            stage_head(d, s, act, bt, bx4, by4, 0, 0, scx, scy, pmvx, pmvy);
                 EVAL(1, 2, 0, 2); EVAL(2, 3, 2, 0);
                 stage_reduce(s, 0x6, bk);
                 stage_tail(d, s, act, bt, bx4, by4, 1, pmvx, pmvy, scx, scy);

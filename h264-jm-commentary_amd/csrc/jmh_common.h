@@ -27,6 +27,17 @@ static __constant__ uint16_t c_qoff[16] = {
     0x0001, 0x1001, 0x1011, 0x1021,   // d, e, f, g
     0x0101, 0x0111, 0x1111, 0x1121,   // h, i, j, k
     0x0201, 0x0112, 0x1112, 0x2112};  // n, p, q, r
+// the same two tables as immediates (no memory access; index may vary across lanes)
+__device__ __forceinline__ int sp9x(int c) { return ((0x22215 >> (2 * c)) & 3) - 1; }
+__device__ __forceinline__ int sp9y(int c) { return ((0x29421 >> (2 * c)) & 3) - 1; }
+__device__ __forceinline__ int qoff(int ph) {
+    const uint64_t q = ph < 8 ? (ph < 4 ? 0x2010101000100000ULL : 0x1021101110010001ULL)
+                              : (ph < 12 ? 0x1121111101110101ULL : 0x2112111201120201ULL);
+    return (int)((q >> (16 * (ph & 3))) & 0xFFFF);
+}
+// block type (1..7 = 16x16, 16x8, 8x16, 8x8, 8x4, 4x8, 4x4) -> log2 of width / 4 and height / 4
+__device__ __forceinline__ int lw4_of(int bt) { return bt <= 2 ? 2 : (bt <= 5 ? 1 : 0); }
+__device__ __forceinline__ int lh4_of(int bt) { return (bt == 1 || bt == 3) ? 2 : (bt == 2 || bt == 4 || bt == 6) ? 1 : 0; }
 // 4x4 frame zig-zag (scan position -> raster), packed as nibbles
 #define SCAN_PACKED 0xFEB7ADC963258410ULL
 __device__ __forceinline__ int scan_of(int k) { return (int)((SCAN_PACKED >> (4 * k)) & 15); }
@@ -246,7 +257,7 @@ __device__ __forceinline__ void load_border(const DevParams &d, Border &b, int t
 // neighbour view with only border cells (16x16 MVP, skip MV)
 struct NbBorder {
     const Border &b;
-    __device__ bool operator()(int xN, int yN, int &ref, int &mx, int &my) const {
+    __device__ __forceinline__ bool operator()(int xN, int yN, int &ref, int &mx, int &my) const {
         if (yN > 15 || (xN > 15 && yN >= 0)) return false;
         int c = border_cell(xN, yN);
         if (c < 0 || b.ref[c] == -2) return false;
