@@ -2,12 +2,13 @@
 """bench.py — JM hot path on MI355X: ME + transform megapixels/s, 1080p FFS SR=32.
 
 One step = one P picture of the hot path with inputs resident in HBM: quarter-pel
-interpolation of the new reference (the previous picture's reconstruction) + the full
-macroblock wavefront (integer FFS SAD table + argmin, sub-pel SATD search, RDO-off mode
-decision incl. intra, luma/chroma TQ + reconstruction) for all 8160 macroblocks of a coded
-1920x1088 picture.  Entropy coding and deblocking are excluded, as JM's MET column is
-(BASELINE.md).  Multi-GPU: one independent stream per rank (seed = rank), no collective in the
-data path; a gloo barrier brackets the timed region and the max time over ranks is used.
+interpolation of the new reference (the previous picture's reconstruction) + the whole
+macroblock wavefront (k_mb_analyse: FFS SAD table + argmin, sub-pel SATD search, intra
+decisions; k_mb_final: RDO-off mode decision, luma/chroma TQ + reconstruction) over all 8160
+macroblocks of a coded 1920x1088 picture.  Entropy coding and deblocking are excluded, as JM's
+ME/transform time is.  Multi-GPU: one independent stream per rank (seed = rank),
+no collective in the data path; a gloo barrier brackets the timed region and the maximum time
+over ranks is used (h264-jm-commentary_amd/streams.py).
 
 Prints ONE JSON line (rank 0).
 """
@@ -26,20 +27,23 @@ DISP_W, DISP_H = 1920, 1080
 W, H = 1920, 1088
 SR, QP = 32, 28
 NMB = (W // 16) * (H // 16)
-# algorithmic work per coded picture
-AD_PER_FRAME = NMB * (2 * SR + 1) ** 2 * 256          # integer-search absolute differences
-BYTES_PER_PIXEL = 7.5                                    # cur 1.5 + ref 1.5 + recon 1.5 + levels 3.0
+# algorithmic HBM bytes per coded picture: current 1.5 B/px + reference 1.5 B/px
+# (each read once) + reconstruction 1.5 B/px written + levels (int16 per sample) 3.0 B/px, plus
+# per-MB side data (MVs, refs, modes, cbp) 80 B/MB
+BYTES_PER_PIXEL = 7.5
 SIDE_BYTES_PER_MB = 80
 BYTES_PER_FRAME = W * H * BYTES_PER_PIXEL + NMB * SIDE_BYTES_PER_MB
 HBM_PEAK_GBS = 8000.0                                    # MI355X_MICROARCH.md (spec)
-# v_sad_u8: 4 absolute differences per lane-op; 256 CU x 128 lanes/clk x 2.4 GHz (nominal)
-VALU_SAD_PEAK_TADS = 256 * 128 * 4 * 2.4e9 / 1e12
+# integer search absolute differences per picture (FFS SAD table) and the v_sad_u8 peak:
+# 4 absolute differences per lane-op, 256 CU x 64 lanes/clk x 2.4 GHz
+AD_PER_FRAME = NMB * (2 * SR + 1) ** 2 * 256
+VALU_SAD_PEAK_TADS = 256 * 64 * 4 * 2.4e9 / 1e12
 
 
-def load_pkg():
-    spec = importlib.util.spec_from_file_location("jmhip", os.path.join(PKG, "jmhip.py"))
+def load_module(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
     mod = importlib.util.module_from_spec(spec)
-    sys.modules["jmhip"] = mod
+    sys.modules[name] = mod
     spec.loader.exec_module(mod)
     return mod
 
@@ -63,12 +67,10 @@ def cpu_baseline(jm, frames):
 
 def read_pmc_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
     try:
         with open(p) as f:
             return json.load(f)
-    except Exception:
+    except (OSError, ValueError):
         return None
 
 
@@ -85,57 +87,30 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")
 
-    jm = load_pkg()
+    jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
+    streams = load_module("jmh_streams", os.path.join(PKG, "streams.py"))
     frames = [jm.synth_frame(DISP_W, DISP_H, rank, i) for i in range(3)]
-    enc = jm.Encoder(W, H, device=local, search_range=SR, slots=3)
-    for i, f in enumerate(frames):
-        enc.load_frame(i, *f)
-    enc.encode_slot(0, jm.JMH_I_SLICE, QP)                # IDR picture -> first reference
-    enc.sync()
-
-    def step(i):
-        enc.set_reference_slot(-1)                        # previous recon -> quarter-pel planes
-        enc.encode_slot(1 + (i % 2), jm.JMH_P_SLICE, QP)  # P picture: the whole MB wavefront
-
-    for i in range(args.warmup):
-        step(i)
-    enc.sync()
-    enc.timing()                                          # reset the event sums
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
-    enc.sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    enc.sync()
-    t1 = time.perf_counter()
-    barrier()
-    dt = t1 - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    tm = enc.timing()
+    enc = jm.Encoder(W, H, device=local, search_range=SR, slots=3, kernel_timing=True)
+    stream = streams.PStream(enc, frames, QP)
+    dt = streams.timed_run(stream, args.steps, args.warmup, dist, on_start=enc.timing)   # on_start resets the event sums
+    tm = enc.timing()                                     # event sums of the timed steps only
 
     if rank != 0:
         if dist is not None:
             dist.barrier()
+        enc.close()
         return
     value = world * args.steps * DISP_W * DISP_H / 1e6 / dt
-    ms_per_step = dt * 1e3 / args.steps
-    launches = max(1, tm.mb_launches)
-    mb_ms_pic = tm.mb_ms / max(1, tm.pictures)
-    avg_launch_ms = mb_ms_pic / launches
-    achieved_gbs = (BYTES_PER_FRAME / launches) / (avg_launch_ms * 1e-3) / 1e9
+    pictures = max(1, tm.pictures)
+    an_launch_ms = tm.analyse_ms / max(1, tm.analyse_launches)
+    an_per_pic = tm.mb_launches / 2                      # one k_mb_analyse + one k_mb_final per diagonal
+    bytes_per_launch = BYTES_PER_FRAME / max(1.0, an_per_pic)
+    achieved_gbs = bytes_per_launch / (an_launch_ms * 1e-3) / 1e9
+    mb_ms_pic = tm.mb_ms / pictures
     pmc = read_pmc_traffic()
     out = {
         "metric": METRIC,
@@ -144,7 +119,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
+        "ms_per_step": round(dt * 1e3 / args.steps, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -164,19 +139,21 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-            "kernel": "k_mb_encode",
-            "algorithmic_bytes_per_launch": round(BYTES_PER_FRAME / launches),
-            "avg_launch_ms": round(avg_launch_ms, 5),
-            "launches_per_picture": launches,
+            "kernel": "k_mb_analyse",
+            "algorithmic_bytes_per_launch": round(bytes_per_launch),
+            "avg_launch_ms": round(an_launch_ms, 5),
+            "launches_per_picture": round(an_per_pic, 2),
         },
         "valu_roofline": {
-            "note": "binding roofline: integer-search absolute differences on v_sad_u8",
+            "note": "integer-search absolute differences (v_sad_u8) over the wavefront time",
             "achieved": round(AD_PER_FRAME / (mb_ms_pic * 1e-3) / 1e12, 4),
             "peak": round(VALU_SAD_PEAK_TADS, 2),
             "unit": "T abs-diff/s",
             "frac": round(AD_PER_FRAME / (mb_ms_pic * 1e-3) / 1e12 / VALU_SAD_PEAK_TADS, 6),
         },
-        "kernel_ms_per_picture": {"k_mb_encode_wavefront": round(mb_ms_pic, 4),
+        "kernel_ms_per_picture": {"wavefront": round(mb_ms_pic, 4),
+                                  "k_mb_analyse": round(tm.analyse_ms / pictures, 4),
+                                  "k_mb_final": round(tm.final_ms / pictures, 4),
                                   "k_interp": round(tm.interp_ms / max(1, tm.interps), 4)},
         "cpu_baseline": None,
     }

@@ -1,5 +1,5 @@
 // jmh_analyse.hip — k_mb_analyse: the decision half of encode_one_macroblock [J] (RDO off) for
-// every macroblock of one wavefront diagonal, split over three 768-thread workgroups per MB
+// every macroblock of one wavefront diagonal, split over three 512-thread workgroups per MB
 // that run concurrently on different CUs:
 //
 //   role 2  P8x8 motion search: 4 x (8x8, 2x 8x4, 2x 4x8, 4x 4x4) = 36 BlockMotionSearch calls
@@ -22,17 +22,15 @@
 //   * 88x88 reference window (+4 margin for the 6-tap filter) and its b, h, j half-pel planes in
 //     LDS, computed once per MB (SubPelBlockMotionSearch reads only LDS);
 //   * the 16 4x4 SADs of every integer position (SetupFastFullPelSearch) in REGISTERS: each
-//     thread owns a column strip of 6 positions, accumulates v_sad_u8 over 21 window rows and
-//     keeps 6 x 8 packed u16 pairs; a search of any partition reduces them with plain 32-bit adds
+//     thread owns a column strip of 10 positions, accumulates v_sad_u8 over 4 bands of 13 window
+//     rows and keeps 10 x 8 packed u16 pairs; a search of any partition reduces them with plain 32-bit adds
 //     of packed pairs (no carries: a half never exceeds 8 x 4080);
 //   * cost = SAD + lambda*(mvbits(x) + mvbits(y)) from two per-search LDS tables, key =
 //     cost << 13 | JM order (0 for the (0,0) pre-check, else spiral index + 1), DPP wave min;
 //   * sub-pel SATD: one 4x4 sub-block per 16-lane row, DPP Hadamard, LDS-atomic candidate sums.
 #include "jmh_common.h"
 
-#define NPK 6                                 // search positions per thread (a column strip)
-#define TEAM 192                              // threads per search team (3 waves); 4 teams
-#define NGRP (TEAM / 16)                      // 16-lane rows per team
+#define NPK 10                                // search positions per thread (a column strip)
 #define PLS (WIN_DIM_MAX * WST + 32)          // stride between the G, b, h, j planes
 
 // Intra4x4 prediction (8.3.1.2) of mode m at pixel l as a formula over P[0..12]
@@ -195,17 +193,26 @@ __device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps
 
 __device__ __forceinline__ int search_range(const DevParams &d, int bt) { return d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr; }
 
+// the threads working on one search of a stage: search slot j (ctab / red / ccost index),
+// thread offset u within the team and team size (a multiple of 64); act: this thread has a search
+struct Team {
+    bool act;
+    int j, u, size;
+};
+
 // stage head: the MVP of each active team's search (every team thread, uniform), its
 // lambda*mvbits tables and zeroed candidate sums; ends with the barrier that publishes them.
-__device__ __forceinline__ void stage_head(const DevParams &d, MeS &s, bool act, int bt, int bx4, int by4, int b8, int best8x8, int scx,
-                                           int scy, int &pmvx, int &pmvy) {
-    const int team = threadIdx.x / TEAM, u = threadIdx.x % TEAM, side = d.side, sr = d.sr, lam = d.lambda_motion;
+__device__ __forceinline__ void stage_head(const DevParams &d, MeS &s, const Team &tm, int bt, int bx4, int by4, int b8, int best8x8,
+                                           int scx, int scy, int &pmvx, int &pmvy) {
+    const int team = tm.j, side = d.side, sr = d.sr, lam = d.lambda_motion;
     pmvx = pmvy = 0;
-    if (act) {
+    if (tm.act) {
         set_mvp(NbMe{s, bt, b8, best8x8}, bx4, by4, 4 << lw4_of(bt), 4 << lh4_of(bt), pmvx, pmvy);
-        if (u < side) s.ctab[team][0][u] = (uint16_t)(lam * mvbits(((scx + u - sr) << 2) - pmvx));
-        else if (u < 2 * side) s.ctab[team][1][u - side] = (uint16_t)(lam * mvbits(((scy + u - side - sr) << 2) - pmvy));
-        else if (u < 2 * side + 18) s.ccost[(u - 2 * side) / 9][team][(u - 2 * side) % 9] = 0;
+        for (int u = tm.u; u < 2 * side + 18; u += tm.size) {
+            if (u < side) s.ctab[team][0][u] = (uint16_t)(lam * mvbits(((scx + u - sr) << 2) - pmvx));
+            else if (u < 2 * side) s.ctab[team][1][u - side] = (uint16_t)(lam * mvbits(((scy + u - side - sr) << 2) - pmvy));
+            else s.ccost[(u - 2 * side) / 9][team][(u - 2 * side) % 9] = 0;
+        }
     }
     __syncthreads();
     sstamp(s);
@@ -227,9 +234,10 @@ __device__ __forceinline__ void stage_reduce(MeS &s, unsigned mask, const unsign
 // stage tail: each active team resolves its full-pel winner, runs SubPelBlockMotionSearch
 // (half then quarter pel: 9 candidates x up to 16 4x4 sub-blocks, one per 16-lane row) and
 // stores the MV and the partition cost.
-__device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act, int bt, int bx4, int by4, int mcidx, int pmvx, int pmvy,
-                                           int scx, int scy) {
-    const int team = threadIdx.x / TEAM, u = threadIdx.x % TEAM, g = u >> 4, l = u & 15;
+__device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, const Team &tm, int bt, int bx4, int by4, int mcidx, int pmvx,
+                                           int pmvy, int scx, int scy) {
+    const bool act = tm.act;
+    const int team = tm.j, u = tm.u, g = u >> 4, l = u & 15, ngrp = tm.size >> 4;
     const int sr = d.sr, lam = d.lambda_motion, had = d.use_hadamard;
     int rx = 0, ry = 0, fmx = 0, fmy = 0, min_mcost = 0, qx = 0, qy = 0, lw4 = 0, lns = 0, check0 = 0;
     if (act) {
@@ -255,7 +263,7 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act,
         const int min_pos = pass == 0 ? (had ? 0 : 1) : 1;
         if (act) {
             const int ntask = 9 << lns;
-            for (int t = g; t < ntask; t += NGRP) {   // uniform per 16-lane row
+            for (int t = g; t < ntask; t += ngrp) {   // uniform per 16-lane row
                 const int c = t >> lns, sub = t & ((1 << lns) - 1);
                 if (c < min_pos) continue;
                 const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
@@ -308,41 +316,41 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, bool act,
 template <int B8>
 __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int scx, int scy, int &best8x8, int &cost8x8) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
-    const int team = threadIdx.x / TEAM, sr = d.sr;
+    const int tid = threadIdx.x, sr = d.sr;
+    const Team t4{true, tid >> 7, tid & 127, 128};       // four searches: 128 threads each
+    const Team t1{true, 3, tid, NTA};                    // one search: the whole workgroup
     unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
     int pmvx, pmvy;
     {   // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left
-        const int bt = 4 + team;
+        const int bt = 4 + t4.j;
         fence_state(ps);
-        stage_head(d, s, true, bt, X, Y, B8, best8x8, scx, scy, pmvx, pmvy);
+        stage_head(d, s, t4, bt, X, Y, B8, best8x8, scx, scy, pmvx, pmvy);
         EVAL(0, 4, X, Y); EVAL(1, 5, X, Y); EVAL(2, 6, X, Y); EVAL(3, 7, X, Y);
         stage_reduce(s, 0xF, bk);
-        stage_tail(d, s, true, bt, X, Y, B8, pmvx, pmvy, scx, scy);
+        stage_tail(d, s, t4, bt, X, Y, B8, pmvx, pmvy, scx, scy);
     }
-    {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right
-        const bool act = team >= 1;
-        const int bt = 4 + team, bx4 = team == 1 ? X : X + 1, by4 = team == 1 ? Y + 1 : Y;
+    {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right (teams 1..3)
+        const Team tm{t4.j >= 1, t4.j, t4.u, 128};
+        const int bt = 4 + tm.j, bx4 = tm.j == 1 ? X : X + 1, by4 = tm.j == 1 ? Y + 1 : Y;
         fence_state(ps);
-        stage_head(d, s, act, bt, bx4, by4, B8, best8x8, scx, scy, pmvx, pmvy);
+        stage_head(d, s, tm, bt, bx4, by4, B8, best8x8, scx, scy, pmvx, pmvy);
         EVAL(1, 5, X, Y + 1); EVAL(2, 6, X + 1, Y); EVAL(3, 7, X + 1, Y);
         stage_reduce(s, 0xE, bk);
-        stage_tail(d, s, act, bt, bx4, by4, B8, pmvx, pmvy, scx, scy);
+        stage_tail(d, s, tm, bt, bx4, by4, B8, pmvx, pmvy, scx, scy);
     }
     {   // stage 2: 4x4 bottom-left
-        const bool act = team == 3;
         fence_state(ps);
-        stage_head(d, s, act, 7, X, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
+        stage_head(d, s, t1, 7, X, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
         EVAL(3, 7, X, Y + 1);
         stage_reduce(s, 0x8, bk);
-        stage_tail(d, s, act, 7, X, Y + 1, B8, pmvx, pmvy, scx, scy);
+        stage_tail(d, s, t1, 7, X, Y + 1, B8, pmvx, pmvy, scx, scy);
     }
     {   // stage 3: 4x4 bottom-right
-        const bool act = team == 3;
         fence_state(ps);
-        stage_head(d, s, act, 7, X + 1, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
+        stage_head(d, s, t1, 7, X + 1, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
         EVAL(3, 7, X + 1, Y + 1);
         stage_reduce(s, 0x8, bk);
-        stage_tail(d, s, act, 7, X + 1, Y + 1, B8, pmvx, pmvy, scx, scy);
+        stage_tail(d, s, t1, 7, X + 1, Y + 1, B8, pmvx, pmvy, scx, scy);
     }
     int mc8 = BIGCOST, bm = 0;
     for (int mode = 4; mode <= 7; mode++) {
@@ -418,7 +426,7 @@ __device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraN
 // ======================================================================================
 template <int ROLE>
 __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int mby) {
-    const int tid = threadIdx.x, team = tid / TEAM;
+    const int tid = threadIdx.x;
     const int W = d.W, sr = d.sr, side = d.side;
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
     const bool slice_p = d.slice_type == JMH_P_SLICE;
@@ -429,10 +437,10 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     if (tid == 0) { s.pst = (prof && ROLE == 2) ? d.prof + 20 : nullptr; s.pn = 0; }
     if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    else if (tid < 266) load_border(d, s.bd, tid - 256, mbx, mby);
-    else if (tid >= 320 && tid < 352) s.motion_cost[(tid - 320) >> 2][tid & 3] = 0;
-    else if (ROLE == 1 && tid >= 384 && tid < 512) load_orgc(d, s.nb, tid - 384, mbx, mby);
-    else if (ROLE == 1 && tid >= 512 && tid < 608) load_intra_nb(d, s.nb, tid - 512, mbx, mby);
+    else if (ROLE == 1 && tid < 384) load_orgc(d, s.nb, tid - 256, mbx, mby);
+    else if (tid >= 384 && tid < 394) load_border(d, s.bd, tid - 384, mbx, mby);
+    else if (ROLE == 1 && tid >= 400 && tid < 471) load_intra_nb(d, s.nb, tid - 400, mbx, mby);
+    else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
     const int wdim = 2 * sr + 16 + 2 * WM;
@@ -504,8 +512,9 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
         {
             const int lo = WM - 1, n = 2 * sr + 18, h1w = wdim - 1;
             uint8_t *PB = s.planes + PLS, *PH = s.planes + 2 * PLS, *PJ = s.planes + 3 * PLS;
-            const int cx = 1 + tid % 96, rb = tid / 96;                // 96 columns x 8 row runs
-            const int run = (n + 7) >> 3, y0 = lo + rb * run, y1 = min(lo + n, y0 + run);
+            constexpr int NRUN = NTA / 96;                            // 96 columns x NRUN row runs
+            const int cx = 1 + tid % 96, rb = tid / 96;
+            const int run = (n + NRUN - 1) / NRUN, y0 = lo + rb * run, y1 = rb < NRUN ? min(lo + n, y0 + run) : y0;
             if (cx <= h1w) {
                 const uint8_t *g = G + cx;
                 int t0 = g[(y0 - 2) * WST], t1 = g[(y0 - 1) * WST], t2 = g[y0 * WST], t3 = g[(y0 + 1) * WST], t4 = g[(y0 + 2) * WST];
@@ -534,23 +543,24 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
         if constexpr (ROLE == 1) {
             unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
             int pmvx, pmvy;
-            {   // stage 0: 16x16, 16x8 upper, 8x16 left
-                const bool act = team < 3;
-                const int bt = 1 + team;
+            {   // stage 0: 16x16 (256 threads: 144 sub-pel tasks), 16x8 upper, 8x16 left (128 each)
+                const int j = tid < 256 ? 0 : tid < 384 ? 1 : 2;
+                const Team tm{true, j, tid - (j == 0 ? 0 : j == 1 ? 256 : 384), j == 0 ? 256 : 128};
+                const int bt = 1 + j;
                 fence_state(ps);
-            stage_head(d, s, act, bt, 0, 0, 0, 0, scx, scy, pmvx, pmvy);
+                stage_head(d, s, tm, bt, 0, 0, 0, 0, scx, scy, pmvx, pmvy);
                 EVAL(0, 1, 0, 0); EVAL(1, 2, 0, 0); EVAL(2, 3, 0, 0);
                 stage_reduce(s, 0x7, bk);
-                stage_tail(d, s, act, bt, 0, 0, 0, pmvx, pmvy, scx, scy);
+                stage_tail(d, s, tm, bt, 0, 0, 0, pmvx, pmvy, scx, scy);
             }
-            {   // stage 1: 16x8 lower, 8x16 right
-                const bool act = team == 1 || team == 2;
-                const int bt = 1 + team, bx4 = team == 2 ? 2 : 0, by4 = team == 1 ? 2 : 0;
+            {   // stage 1: 16x8 lower, 8x16 right (256 threads each)
+                const Team tm{true, 1 + (tid >> 8), tid & 255, 256};
+                const int bt = 1 + tm.j, bx4 = tm.j == 2 ? 2 : 0, by4 = tm.j == 1 ? 2 : 0;
                 fence_state(ps);
-            stage_head(d, s, act, bt, bx4, by4, 0, 0, scx, scy, pmvx, pmvy);
+                stage_head(d, s, tm, bt, bx4, by4, 0, 0, scx, scy, pmvx, pmvy);
                 EVAL(1, 2, 0, 2); EVAL(2, 3, 2, 0);
                 stage_reduce(s, 0x6, bk);
-                stage_tail(d, s, act, bt, bx4, by4, 1, pmvx, pmvy, scx, scy);
+                stage_tail(d, s, tm, bt, bx4, by4, 1, pmvx, pmvy, scx, scy);
             }
             // results: MVs of types 1..3, partition costs, FindSkipModeMotionVector
             if (tid < 96) {

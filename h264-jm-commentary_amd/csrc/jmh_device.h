@@ -9,7 +9,7 @@
 #define NPOS_MAX (SIDE_MAX * SIDE_MAX)   // 4225 search positions
 #define QPAD 4                           // quarter-pel plane padding (== oracle JMO_PAD)
 #define NT 256                           // threads per finalize / unit workgroup
-#define NTA 768                          // threads per analysis workgroup (12 waves, 3 per SIMD)
+#define NTA 512                          // threads per analysis workgroup (8 waves, 2 per SIMD)
 #define BIGCOST (1 << 20)
 
 // Per-macroblock analysis results, written by k_mb_analyse (three roles on separate

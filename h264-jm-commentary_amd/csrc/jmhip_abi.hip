@@ -17,27 +17,31 @@ hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, i
 hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st);
 
+// JMH_FLAG_KERNEL_TIMING brackets every KT_STRIDE-th diagonal's two launches with events: the
+// averages are sampled uniformly over the picture while the event packets stay off most launches
+#define KT_STRIDE 8
 // ring of begin/end event pairs; completed pairs are folded into `sum` (ms)
-#define EV_RING 64
 struct EvRing {
-    hipEvent_t a[EV_RING], b[EV_RING];
-    int head, count, n;
-    float sum;
+    std::vector<hipEvent_t> a, b;
+    int cap = 0, head = 0, count = 0, n = 0;
+    float sum = 0;
 };
-static int ring_init(EvRing &r) {
-    memset(&r, 0, sizeof(r));
-    for (int i = 0; i < EV_RING; i++)
+static int ring_init(EvRing &r, int cap) {
+    r.cap = cap; r.head = r.count = r.n = 0; r.sum = 0;
+    r.a.assign(cap, nullptr); r.b.assign(cap, nullptr);
+    for (int i = 0; i < cap; i++)
         if (hipEventCreate(&r.a[i]) != hipSuccess || hipEventCreate(&r.b[i]) != hipSuccess) return -1;
     return 0;
 }
 static void ring_free(EvRing &r) {
-    for (int i = 0; i < EV_RING; i++) {
+    for (int i = 0; i < r.cap; i++) {
         if (r.a[i]) (void)hipEventDestroy(r.a[i]);
         if (r.b[i]) (void)hipEventDestroy(r.b[i]);
     }
+    r.cap = 0;
 }
 static void ring_fold_oldest(EvRing &r) {
-    int i = (r.head - r.count + EV_RING) % EV_RING;
+    int i = (r.head - r.count + r.cap) % r.cap;
     float ms = 0;
     if (hipEventSynchronize(r.b[i]) == hipSuccess && hipEventElapsedTime(&ms, r.a[i], r.b[i]) == hipSuccess) {
         r.sum += ms;
@@ -46,12 +50,12 @@ static void ring_fold_oldest(EvRing &r) {
     r.count--;
 }
 static hipError_t ring_begin(EvRing &r, hipStream_t st) {
-    if (r.count == EV_RING) ring_fold_oldest(r);
+    if (r.count == r.cap) ring_fold_oldest(r);
     return hipEventRecord(r.a[r.head], st);
 }
 static hipError_t ring_end(EvRing &r, hipStream_t st) {
     hipError_t e = hipEventRecord(r.b[r.head], st);
-    r.head = (r.head + 1) % EV_RING;
+    r.head = (r.head + 1) % r.cap;
     r.count++;
     return e;
 }
@@ -79,7 +83,7 @@ struct jmh_ctx {
     uint8_t *h_rec, *h_stage_cur, *h_stage_ref;
     int have_ref, pending, have_results, have_total;
     hipEvent_t ev_t0, ev_t1;
-    EvRing ring_interp, ring_mb;
+    EvRing ring_interp, ring_mb, ring_an, ring_fin;   // ring_an / ring_fin: JMH_FLAG_KERNEL_TIMING
     jmh_timing timing;
     std::vector<int> dcount, dymin;
 };
@@ -129,6 +133,8 @@ void jmh_destroy(jmh_ctx *c) {
     if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
     ring_free(c->ring_interp);
     ring_free(c->ring_mb);
+    ring_free(c->ring_an);
+    ring_free(c->ring_fin);
     if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
 }
@@ -178,7 +184,8 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         HALLOC(c->h_stage_cur, c->fsize); HALLOC(c->h_stage_ref, c->fsize);
         if (hipMemset(c->d_rec, 0, c->fsize) != hipSuccess || hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         if (hipEventCreate(&c->ev_t0) != hipSuccess || hipEventCreate(&c->ev_t1) != hipSuccess ||
-            ring_init(c->ring_interp) || ring_init(c->ring_mb)) { st = JMH_E_HIP; goto fail; }
+            ring_init(c->ring_interp, 64) || ring_init(c->ring_mb, 64) ||
+            ((cfg->flags & JMH_FLAG_KERNEL_TIMING) && (ring_init(c->ring_an, 2048) || ring_init(c->ring_fin, 2048)))) { st = JMH_E_HIP; goto fail; }
         int nd = (c->mbw - 1) + 2 * (c->mbh - 1) + 1;
         c->dcount.resize(nd); c->dymin.resize(nd);
         for (int dg = 0; dg < nd; dg++) {
@@ -256,8 +263,12 @@ static int enqueue_encode(jmh_ctx *c, const uint8_t *d_pic, const jmh_frame_para
     for (size_t dg = 0; dg < c->dcount.size(); dg++) {
         if (!c->dcount[dg]) continue;
         p.diag = (int)dg; p.y_min = c->dymin[dg]; p.ndiag = c->dcount[dg];
+        const bool kt = c->ring_an.cap > 0 && dg % KT_STRIDE == 0;   // sampled per-launch timing
+        if (kt) HCHK(ring_begin(c->ring_an, c->st));
         HCHK(jmh_launch_analyse(p, c->st));
+        if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
         HCHK(jmh_launch_final(p, c->st));
+        if (kt) HCHK(ring_end(c->ring_fin, c->st));
     }
     HCHK(ring_end(c->ring_mb, c->st));
     int nl = 0;
@@ -354,6 +365,10 @@ int jmh_get_timing(jmh_ctx *c, jmh_timing *t) {
     float ms = 0;
     ring_drain(c->ring_interp, c->timing.interp_ms, c->timing.interps);
     ring_drain(c->ring_mb, c->timing.mb_ms, c->timing.pictures);
+    if (c->ring_an.cap) {
+        ring_drain(c->ring_an, c->timing.analyse_ms, c->timing.analyse_launches);
+        ring_drain(c->ring_fin, c->timing.final_ms, c->timing.final_launches);
+    }
     if (c->have_total && hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1) == hipSuccess) c->timing.total_ms = ms;
     *t = c->timing;
     return JMH_OK;

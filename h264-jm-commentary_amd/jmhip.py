@@ -17,6 +17,8 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
+JMH_ABI_VERSION = 2
+JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
 # JM 8.6 rdopt.c QP2QUANT [J]: RDO-off lambda = QP2QUANT[max(0, qp-12)]
@@ -34,7 +36,7 @@ class JmhConfig(ctypes.Structure):
                 ("use_hadamard", ctypes.c_int32), ("restrict_search_range", ctypes.c_int32),
                 ("inter_search", ctypes.c_int32 * 8), ("num_ref_frames", ctypes.c_int32),
                 ("constrained_intra_pred", ctypes.c_int32), ("num_frame_slots", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 7)]
+                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
 
 
 class JmhFrameParams(ctypes.Structure):
@@ -47,7 +49,8 @@ class JmhTiming(ctypes.Structure):
     _fields_ = [("interp_ms", ctypes.c_float), ("mb_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("mb_launches", ctypes.c_int32),
                 ("pictures", ctypes.c_int32), ("interps", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 2)]
+                ("analyse_ms", ctypes.c_float), ("analyse_launches", ctypes.c_int32),
+                ("final_ms", ctypes.c_float), ("final_launches", ctypes.c_int32)]
 
 
 # jmh_mb_result, field for field (include/jmhip.h)
@@ -102,6 +105,8 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.jmh_abi_version() != JMH_ABI_VERSION:
+        raise JmhError(f"{path}: ABI version {lib.jmh_abi_version()} != {JMH_ABI_VERSION} (stale build?)")
     if path == LIB_PATH:
         _lib = lib
     return lib
@@ -117,7 +122,7 @@ def _ptr(a):
 
 
 def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
-                restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2):
+                restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False):
     cfg = JmhConfig()
     cfg.width, cfg.height = width, height
     cfg.search_range, cfg.search_mode = search_range, search_mode
@@ -125,6 +130,7 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     for i, v in enumerate(inter_search):
         cfg.inter_search[i + 1] = v
     cfg.num_ref_frames, cfg.constrained_intra_pred, cfg.num_frame_slots = 1, 0, slots
+    cfg.flags = JMH_FLAG_KERNEL_TIMING if kernel_timing else 0
     return cfg
 
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 1
+#define JMH_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define JMH_OK                 0
@@ -79,8 +79,12 @@ typedef struct jmh_config {
     int32_t num_ref_frames;         /* NumberReferenceFrames (this build: 1)                      */
     int32_t constrained_intra_pred; /* UseConstrainedIntraPred (this build: 0)                    */
     int32_t num_frame_slots;        /* device-resident input frame slots (bench / pipelining)     */
-    int32_t reserved[7];
+    int32_t flags;                  /* JMH_FLAG_* (0 for the defaults)                            */
+    int32_t reserved[6];
 } jmh_config;
+/* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
+ * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */
+#define JMH_FLAG_KERNEL_TIMING 1
 
 /* ---- per-picture parameters ------------------------------------------------------------- */
 typedef struct jmh_frame_params {
@@ -122,7 +126,10 @@ typedef struct jmh_timing {
     int32_t mb_launches;       /* wavefront launches (dispatches) per picture                  */
     int32_t pictures;          /* pictures summed in mb_ms                                     */
     int32_t interps;           /* interpolations summed in interp_ms                           */
-    int32_t reserved[2];
+    float analyse_ms;          /* JMH_FLAG_KERNEL_TIMING: sum of sampled k_mb_analyse launches   */
+    int32_t analyse_launches;  /*   ... and the number of launches summed                       */
+    float final_ms;            /* JMH_FLAG_KERNEL_TIMING: sum of k_mb_final launch durations    */
+    int32_t final_launches;
 } jmh_timing;
 
 typedef struct jmh_ctx jmh_ctx;

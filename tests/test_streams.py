@@ -1,0 +1,109 @@
+"""Multi-stream execution model on CPU: two gloo ranks, one independent P-picture
+stream each (seed = rank), timing reduced with MAX — no picture data crosses ranks.
+
+The stream harness (h264-jm-commentary_amd/streams.py) is the one bench.py drives on the GPUs;
+here its encoder is an oracle-backed stand-in with the same slot interface, so the test checks
+the harness (warmup / timed steps / barrier / max-reduce) and that every rank's reconstruction
+equals an undistributed run of the same seed.
+"""
+import hashlib
+import importlib.util
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_lib
+from jmpaths import PKG, ensure_built, load_jmhip
+
+W, H, SR, QP = 64, 48, 8, 28
+
+
+def load_streams():
+    spec = importlib.util.spec_from_file_location("jmh_streams", os.path.join(PKG, "streams.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+class OracleSlots:
+    """Slot interface of jmhip.Encoder (load_frame / encode_slot / set_reference_slot / sync)."""
+
+    def __init__(self):
+        self.o = oracle_lib.OracleEncoder(W, H, search_range=SR)
+        self.slots, self.rec, self.results = {}, None, []
+
+    def load_frame(self, slot, y, u, v):
+        self.slots[slot] = (y, u, v)
+
+    def encode_slot(self, slot, slice_type, qp):
+        res, self.rec = self.o.encode(*self.slots[slot], slice_type, qp)
+        self.results.append(res)
+
+    def set_reference_slot(self, slot):
+        assert slot == -1
+        self.o.set_reference(*self.rec)
+
+    def sync(self):
+        pass
+
+
+def run_stream(seed, steps, warmup, dist_mod=None):
+    jm, streams = load_jmhip(), load_streams()
+    frames = [jm.synth_frame(W, H, seed, i) for i in range(3)]
+    enc = OracleSlots()
+    dt = streams.timed_run(streams.PStream(enc, frames, QP), steps, warmup, dist_mod)
+    h = hashlib.sha256(b"".join(p.tobytes() for p in enc.rec) + b"".join(r.tobytes() for r in enc.results))
+    return dt, h.hexdigest()
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dt, digest = run_stream(rank, steps=2, warmup=1, dist_mod=dist)
+    q.put((rank, dt, digest))
+    dist.destroy_process_group()
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_streams_are_independent_replicas():
+    ensure_built()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    # the timed region is reduced with MAX: every rank reports the same time
+    assert out[0][1] == out[1][1] and out[0][1] > 0
+    # each rank's stream is exactly the undistributed stream of its seed, and seeds differ
+    for rank, _, digest in out:
+        assert digest == run_stream(rank, steps=2, warmup=1)[1]
+    assert out[0][2] != out[1][2]
+
+
+def test_single_process_harness_counts_steps():
+    ensure_built()
+    jm, streams = load_jmhip(), load_streams()
+    frames = [jm.synth_frame(W, H, 5, i) for i in range(3)]
+    enc = OracleSlots()
+    streams.timed_run(streams.PStream(enc, frames, QP), steps=3, warmup=2)
+    # one IDR picture + warmup + timed P pictures; the IDR picture is all intra (I4MB 9 /
+    # I16MB 10), the P pictures reference the previous reconstruction and use inter types
+    assert len(enc.results) == 1 + 2 + 3
+    assert np.all(enc.results[0]["mb_type"] >= 9)
+    assert all(np.any(r["mb_type"] < 9) for r in enc.results[1:])

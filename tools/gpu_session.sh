@@ -6,7 +6,7 @@ TAG=${1:-run}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests/test_gpu_parity.py -x -q -m gpu -p no:cacheprovider "$@" > gpurun_out/${TAG}_pytest.log 2>&1
+timeout -k 10 900 python -m pytest tests -x -q -m gpu -p no:cacheprovider "$@" > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -25 gpurun_out/${TAG}_pytest.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/${TAG}_bench.log 2>&1
