@@ -37,6 +37,8 @@ struct DevParams {
     const uint8_t *refY, *refU, *refV;
     const uint8_t *qpel;
     uint8_t *recY, *recU, *recV;
+    uint8_t *dbkY, *dbkU, *dbkV;   // deblocked reconstruction (null: no deblocking on the device)
+    int lf_disable, lf_offA, lf_offB;   // disable_deblocking_filter_idc, FilterOffsetA/B (= 2 x div2)
     int16_t *mv;
     int8_t *refidx;
     int8_t *ipred;

@@ -29,7 +29,67 @@ struct FinS {
     int creset[2];
     int cdcnz[2];
     uint8_t cfin[2][64];
+    // deblocking: the MB with 4 rows / columns of its (already filtered) top / left neighbours
+    uint8_t dy[20][20];                  // luma, rows / columns -4..15 -> [r + 4][c + 4]
+    uint8_t dc2[2][12][12];              // chroma, rows / columns -4..7
+    int8_t bs[2][4][4];                  // boundary strength [dir][edge][segment]
 };
+
+// 8.7.2.2 thresholds (index = clip3(0, 51, qp + filter offset)) and tc0 (bS 1..3)
+static __constant__ uint8_t c_alpha[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   4,   4,
+                                           5,  6,  7,  8,  9,  10, 12, 13, 15, 17, 20, 22, 25,  28,  32,  36,  40,  45,
+                                           50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
+static __constant__ uint8_t c_beta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  2,  2,
+                                          2,  3,  3,  3,  3,  4,  4,  4,  6,  6,  7,  7,  8,  8,  9,  9,  10, 10,
+                                          11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
+static __constant__ uint8_t c_tc0[52][3] = {
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1},
+    {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1},
+    {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 2, 3}, {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4},
+    {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11},
+    {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
+
+// one line of samples across an edge (8.7.2.3 / 8.7.2.4): q0 at q[0], p_k at q[-(k+1)*step]
+__device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int alpha, int beta, int tc0, bool chroma) {
+    const int p0 = q[-step], p1 = q[-2 * step], q0 = q[0], q1 = q[step];
+    if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
+    if (chroma) {
+        if (bS < 4) {
+            const int tc = tc0 + 1;
+            const int dl = iclip(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+            q[-step] = (uint8_t)clip255(p0 + dl);
+            q[0] = (uint8_t)clip255(q0 - dl);
+        } else {
+            q[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
+            q[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+        }
+        return;
+    }
+    const int p2 = q[-3 * step], q2 = q[2 * step];
+    const int ap = abs(p2 - p0), aq = abs(q2 - q0);
+    if (bS < 4) {
+        const int tc = tc0 + (ap < beta) + (aq < beta);
+        const int dl = iclip(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+        q[-step] = (uint8_t)clip255(p0 + dl);
+        q[0] = (uint8_t)clip255(q0 - dl);
+        if (ap < beta) q[-2 * step] = (uint8_t)(p1 + iclip(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
+        if (aq < beta) q[step] = (uint8_t)(q1 + iclip(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
+    } else {
+        const int p3 = q[-4 * step], q3 = q[3 * step];
+        const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
+        if (ap < beta && small) {
+            q[-step] = (uint8_t)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+            q[-2 * step] = (uint8_t)((p2 + p1 + p0 + q0 + 2) >> 2);
+            q[-3 * step] = (uint8_t)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+        } else q[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
+        if (aq < beta && small) {
+            q[0] = (uint8_t)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+            q[step] = (uint8_t)((p0 + q0 + q1 + q2 + 2) >> 2);
+            q[2 * step] = (uint8_t)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+        } else q[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+    }
+}
 
 __device__ __forceinline__ int qpel_at(const DevParams &d, int X, int Y) {
     int x = iclip(-QPAD, d.W - 1 + QPAD, X >> 2), y = iclip(-QPAD, d.H - 1 + QPAD, Y >> 2);
@@ -293,6 +353,100 @@ __global__ __launch_bounds__(NT) void k_mb_final(DevParams d) {
         (uv ? d.recV : d.recU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)] = s.cfin[uv][k];
     }
     d.recY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)] = s.rec[tid];
+
+    // ======== DeblockMb [J] / 8.7 into the reference picture (d.dbkY..): this MB's edges, in
+    // place on its already-filtered left / top neighbours. MBs of one diagonal touch disjoint
+    // samples and every neighbour they read lies on an earlier diagonal, so the result equals
+    // JM's raster-order DeblockFrame.
+    if (d.dbkY) {
+        const int Hc = d.Hc;
+        const bool filt = d.lf_disable != 1;
+        __syncthreads();                          // s.rec, s.cfin final
+        for (int i = tid; i < 400 + 288; i += NT) {
+            if (i < 400) {
+                const int r = i / 20 - 4, c = i % 20 - 4;
+                int v = 0;
+                if (r >= 0 && c >= 0) v = s.rec[16 * r + c];
+                else if ((r < 0 && c >= 0 && avT) || (c < 0 && r >= 0 && avL)) v = d.dbkY[(pix_y + r) * W + pix_x + c];
+                s.dy[r + 4][c + 4] = (uint8_t)v;
+            } else {
+                const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
+                int v = 0;
+                if (r >= 0 && c >= 0) v = s.cfin[pl][8 * r + c];
+                else if ((r < 0 && c >= 0 && avT) || (c < 0 && r >= 0 && avL))
+                    v = (pl ? d.dbkV : d.dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c];
+                s.dc2[pl][r + 4][c + 4] = (uint8_t)v;
+            }
+        }
+        if (tid < 32) {                           // boundary strength (8.7.2.1), frame MBs, one slice
+            const int dir = tid >> 4, e = (tid >> 2) & 3, i = tid & 3;
+            const bool mb_edge = e == 0;
+            int bS = 0;
+            if (filt && !(mb_edge && (dir == 0 ? !avL : !avT))) {
+                const int bq = dir == 0 ? i * 4 + e : e * 4 + i;
+                const int bp = dir == 0 ? (mb_edge ? i * 4 + 3 : bq - 1) : (mb_edge ? 12 + i : bq - 4);
+                bool intra_p = is_intra, pcoef;
+                int pref, pmx, pmy;
+                const int qref = is_intra ? -1 : 0, qmx = s.fmv[bq][0], qmy = s.fmv[bq][1];
+                const bool qcoef = (cbp_blk >> bq) & 1;
+                if (mb_edge) {
+                    const int nx = dir == 0 ? mbx - 1 : mbx, ny = dir == 0 ? mby : mby - 1;
+                    const jmh_mb_result *rp = d.res + ny * d.mbw + nx;
+                    intra_p = rp->mb_type == JMH_I4MB || rp->mb_type == JMH_I16MB;
+                    pcoef = (rp->cbp_blk >> bp) & 1;
+                    pref = intra_p ? -1 : 0;
+                    pmx = rp->mv[bp][0]; pmy = rp->mv[bp][1];
+                } else {
+                    pcoef = (cbp_blk >> bp) & 1;
+                    pref = qref; pmx = s.fmv[bp][0]; pmy = s.fmv[bp][1];
+                }
+                if (intra_p || is_intra) bS = mb_edge ? 4 : 3;
+                else if (pcoef || qcoef) bS = 2;
+                else if (pref != qref || abs(pmx - qmx) >= 4 || abs(pmy - qmy) >= 4) bS = 1;
+            }
+            s.bs[dir][e][i] = (int8_t)bS;
+        }
+        __syncthreads();
+        if (tid < 64 && filt) {                   // one wave: luma lines on lanes 0..15, chroma on 16..31
+            const int offA = d.lf_offA, offB = d.lf_offB;
+            const int iA = iclip(0, 51, qp + offA), iB = iclip(0, 51, qp + offB);
+            const int alpha = c_alpha[iA], beta = c_beta[iB];
+            const int t1 = c_tc0[iA][0], t2 = c_tc0[iA][1], t3 = c_tc0[iA][2];
+            const int cA = iclip(0, 51, qpc + offA), cB = iclip(0, 51, qpc + offB);
+            const int calpha = c_alpha[cA], cbeta = c_beta[cB];
+            const int u1 = c_tc0[cA][0], u2 = c_tc0[cA][1], u3 = c_tc0[cA][2];
+            for (int dir = 0; dir < 2; dir++)
+                for (int e = 0; e < 4; e++) {
+                    if (tid < 16) {
+                        const int k = tid, b = s.bs[dir][e][k >> 2];
+                        if (b) {
+                            uint8_t *q = dir == 0 ? &s.dy[k + 4][4 * e + 4] : &s.dy[4 * e + 4][k + 4];
+                            filter_line(q, dir == 0 ? 1 : 20, b, alpha, beta, b == 1 ? t1 : b == 2 ? t2 : t3, false);
+                        }
+                    } else if (tid < 32 && !(e & 1)) {
+                        const int pl = (tid - 16) >> 3, k = tid & 7, b = s.bs[dir][e][k >> 1];
+                        if (b) {
+                            uint8_t *q = dir == 0 ? &s.dc2[pl][k + 4][2 * e + 4] : &s.dc2[pl][2 * e + 4][k + 4];
+                            filter_line(q, dir == 0 ? 1 : 12, b, calpha, cbeta, b == 1 ? u1 : b == 2 ? u2 : u3, true);
+                        }
+                    }
+                    wave_lds_sync();
+                }
+        }
+        __syncthreads();
+        for (int i = tid; i < 400 + 288; i += NT) {
+            if (i < 400) {
+                const int r = i / 20 - 4, c = i % 20 - 4;
+                if ((r >= 0 && c >= 0) || (r >= -3 && r < 0 && c >= 0 && avT) || (c >= -3 && c < 0 && r >= 0 && avL))
+                    d.dbkY[(pix_y + r) * W + pix_x + c] = s.dy[r + 4][c + 4];
+            } else {
+                const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
+                if ((r >= 0 && c >= 0) || (r == -1 && c >= 0 && c < 8 && avT) || (c == -1 && r >= 0 && r < 8 && avL))
+                    if (r < 8 && c < 8) (pl ? d.dbkV : d.dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c] = s.dc2[pl][r + 4][c + 4];
+            }
+        }
+        (void)Hc;
+    }
     PSTAMP(19);
 }
 

@@ -72,6 +72,7 @@ struct jmh_ctx {
     int W, H, Wc, Hc, mbw, mbh, sr, side, npos, qstride, qplane;
     size_t fsize;                        // bytes of one 4:2:0 picture (Y then U then V)
     uint8_t *d_cur, *d_ref, *d_qpel, *d_rec, *d_slots;
+    uint8_t *d_dbk;                      // deblocked reconstruction (next reference); swapped with d_ref
     int nslots;
     int16_t *d_mv;
     int8_t *d_refidx, *d_ipred;
@@ -80,8 +81,9 @@ struct jmh_ctx {
     unsigned long long *d_prof;          // JMH_PHASE_PROF=<mb>: per-phase wall clock of one MB
     int prof_mb;
     jmh_mb_result *h_res;
-    uint8_t *h_rec, *h_stage_cur, *h_stage_ref;
+    uint8_t *h_rec, *h_dbk, *h_stage_cur, *h_stage_ref;
     int have_ref, pending, have_results, have_total;
+    int dbk_dev, dbk_host;               // d_dbk / h_dbk hold the last picture's deblocking
     hipEvent_t ev_t0, ev_t1;
     EvRing ring_interp, ring_mb, ring_an, ring_fin;   // ring_an / ring_fin: JMH_FLAG_KERNEL_TIMING
     jmh_timing timing;
@@ -124,10 +126,10 @@ void jmh_destroy(jmh_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    void *dev_bufs[] = {c->d_cur, c->d_ref, c->d_qpel, c->d_rec, c->d_slots, c->d_mv, c->d_refidx,
+    void *dev_bufs[] = {c->d_cur, c->d_ref, c->d_qpel, c->d_rec, c->d_dbk, c->d_slots, c->d_mv, c->d_refidx,
                         c->d_ipred, c->d_res, c->d_scr, c->d_prof};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
-    void *host_bufs[] = {c->h_res, c->h_rec, c->h_stage_cur, c->h_stage_ref};
+    void *host_bufs[] = {c->h_res, c->h_rec, c->h_dbk, c->h_stage_cur, c->h_stage_ref};
     for (void *p : host_bufs) if (p) (void)hipHostFree(p);
     if (c->ev_t0) (void)hipEventDestroy(c->ev_t0);
     if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
@@ -168,7 +170,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     {
         if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         size_t n4 = (size_t)c->W * c->H / 16, nmb = (size_t)c->mbw * c->mbh;
-        ALLOC(c->d_cur, c->fsize); ALLOC(c->d_ref, c->fsize); ALLOC(c->d_rec, c->fsize);
+        ALLOC(c->d_cur, c->fsize); ALLOC(c->d_ref, c->fsize); ALLOC(c->d_rec, c->fsize); ALLOC(c->d_dbk, c->fsize);
         ALLOC(c->d_qpel, (size_t)16 * c->qplane);
         ALLOC(c->d_slots, c->fsize * c->nslots);
         ALLOC(c->d_mv, n4 * 2 * sizeof(int16_t)); ALLOC(c->d_refidx, n4); ALLOC(c->d_ipred, n4);
@@ -180,7 +182,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
             ALLOC(c->d_prof, 64 * sizeof(unsigned long long));
             if (hipMemset(c->d_prof, 0, 64 * sizeof(unsigned long long)) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         }
-        HALLOC(c->h_res, nmb * sizeof(jmh_mb_result)); HALLOC(c->h_rec, c->fsize);
+        HALLOC(c->h_res, nmb * sizeof(jmh_mb_result)); HALLOC(c->h_rec, c->fsize); HALLOC(c->h_dbk, c->fsize);
         HALLOC(c->h_stage_cur, c->fsize); HALLOC(c->h_stage_ref, c->fsize);
         if (hipMemset(c->d_rec, 0, c->fsize) != hipSuccess || hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         if (hipEventCreate(&c->ev_t0) != hipSuccess || hipEventCreate(&c->ev_t1) != hipSuccess ||
@@ -232,8 +234,14 @@ int jmh_set_reference(jmh_ctx *c, int list, int ref_idx, const uint8_t *y, const
 }
 
 int jmh_set_reference_slot(jmh_ctx *c, int slot) {
-    if (!c || slot < -1 || slot >= c->nslots) return JMH_E_INVALID_ARG;
+    if (!c || slot < -2 || slot >= c->nslots) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
+    if (slot == -2) {   // the device deblocking becomes the reference: swap buffers, no copy
+        if (!c->dbk_dev) return JMH_E_STATE;
+        uint8_t *t = c->d_ref; c->d_ref = c->d_dbk; c->d_dbk = t;
+        c->dbk_dev = 0;
+        return run_interp(c, c->d_ref);
+    }
     const uint8_t *src = slot < 0 ? c->d_rec : c->d_slots + (size_t)slot * c->fsize;
     HCHK(hipMemcpyAsync(c->d_ref, src, c->fsize, hipMemcpyDeviceToDevice, c->st));
     return run_interp(c, c->d_ref);
@@ -259,6 +267,14 @@ static int enqueue_encode(jmh_ctx *c, const uint8_t *d_pic, const jmh_frame_para
     p.prof = c->d_prof; p.prof_mb = c->prof_mb;
     p.slice_type = fp->slice_type; p.qp = fp->qp; p.lambda_mode = fp->lambda_mode; p.lambda_motion = fp->lambda_motion;
     p.cqp_off = fp->chroma_qp_offset;
+    if (fp->deblock) {   // DeblockFrame fused into k_mb_final, into d_dbk (never aliases d_ref)
+        if (fp->lf_disable < 0 || fp->lf_disable > 2 || fp->lf_alpha_div2 < -6 || fp->lf_alpha_div2 > 6 ||
+            fp->lf_beta_div2 < -6 || fp->lf_beta_div2 > 6) return JMH_E_INVALID_ARG;
+        p.dbkY = c->d_dbk; p.dbkU = c->d_dbk + ls; p.dbkV = c->d_dbk + ls + ls / 4;
+        p.lf_disable = fp->lf_disable;   // idc 2 == 0 with one slice per picture
+        p.lf_offA = 2 * fp->lf_alpha_div2; p.lf_offB = 2 * fp->lf_beta_div2;
+    }
+    c->dbk_dev = fp->deblock != 0;
     HCHK(ring_begin(c->ring_mb, c->st));
     for (size_t dg = 0; dg < c->dcount.size(); dg++) {
         if (!c->dcount[dg]) continue;
@@ -288,6 +304,8 @@ int jmh_frame_submit(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8
     if (r) return r;
     HCHK(hipMemcpyAsync(c->h_res, c->d_res, (size_t)c->mbw * c->mbh * sizeof(jmh_mb_result), hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(c->h_rec, c->d_rec, c->fsize, hipMemcpyDeviceToHost, c->st));
+    if (c->dbk_dev) HCHK(hipMemcpyAsync(c->h_dbk, c->d_dbk, c->fsize, hipMemcpyDeviceToHost, c->st));
+    c->dbk_host = c->dbk_dev;
     HCHK(hipEventRecord(c->ev_t1, c->st));
     c->pending = 1;
     c->have_total = 1;
@@ -310,15 +328,26 @@ const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *c, int mb_addr) {
     return &c->h_res[mb_addr];
 }
 
+static void unpack_planes(const uint8_t *src, int W, int H, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
+    size_t ls = (size_t)W * H;
+    for (int r = 0; r < H; r++) memcpy(y + (size_t)r * sy, src + (size_t)r * W, W);
+    for (int r = 0; r < H / 2; r++) {
+        memcpy(u + (size_t)r * sc, src + ls + (size_t)r * (W / 2), W / 2);
+        memcpy(v + (size_t)r * sc, src + ls + ls / 4 + (size_t)r * (W / 2), W / 2);
+    }
+}
+
 int jmh_read_recon(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
     if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
     if (!c->have_results) return JMH_E_STATE;
-    size_t ls = (size_t)c->W * c->H;
-    for (int r = 0; r < c->H; r++) memcpy(y + (size_t)r * sy, c->h_rec + (size_t)r * c->W, c->W);
-    for (int r = 0; r < c->Hc; r++) {
-        memcpy(u + (size_t)r * sc, c->h_rec + ls + (size_t)r * c->Wc, c->Wc);
-        memcpy(v + (size_t)r * sc, c->h_rec + ls + ls / 4 + (size_t)r * c->Wc, c->Wc);
-    }
+    unpack_planes(c->h_rec, c->W, c->H, y, u, v, sy, sc);
+    return JMH_OK;
+}
+
+int jmh_read_deblocked(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
+    if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
+    if (!c->have_results || !c->dbk_host) return JMH_E_STATE;
+    unpack_planes(c->h_dbk, c->W, c->H, y, u, v, sy, sc);
     return JMH_OK;
 }
 

@@ -90,6 +90,13 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         fp.qp = is_i ? inp->qp_i : inp->qp_p;
         fp.lambda_mode = fp.lambda_motion = jm_lambda_rdo_off(fp.qp);
         fp.chroma_qp_offset = inp->chroma_qp_offset;
+        const int dev_dbk = be->read_deblocked && be->reference_deblocked;
+        if (dev_dbk) {   /* same parameters jm_deblock_picture derives from the slice header */
+            fp.deblock = 1;
+            fp.lf_disable = s.lf_params_flag ? s.lf_disable : 0;
+            fp.lf_alpha_div2 = s.lf_params_flag ? s.lf_alpha : 0;
+            fp.lf_beta_div2 = s.lf_params_flag ? s.lf_beta : 0;
+        }
         double t0 = now_ms();
         int r = be->encode_frame(be->ctx, &cur, &fp);
         double t1 = now_ms();
@@ -108,11 +115,17 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         long pic_bits = out.len * 8;
         fwrite(out.buf, 1, out.len, fout);
         out.len = 0;
-        be->read_recon(be->ctx, &rec);
-        jm_deblock_picture(&rec, &s, res, fp.qp);
+        if (dev_dbk) {
+            r = be->read_deblocked(be->ctx, &rec);
+            if (!r) r = be->reference_deblocked(be->ctx);
+        } else {
+            be->read_recon(be->ctx, &rec);
+            jm_deblock_picture(&rec, &s, res, fp.qp);
+            r = be->set_reference(be->ctx, &rec);
+        }
         double t3 = now_ms();
         st->deblock_ms += t3 - t2;
-        if ((r = be->set_reference(be->ctx, &rec))) { fprintf(stderr, "set_reference failed: %d\n", r); st_ret = r; break; }
+        if (r) { fprintf(stderr, "set_reference failed: %d\n", r); st_ret = r; break; }
         if (frec) jm_write_yuv_frame(frec, &rec, inp->width, inp->height);
         double py = psnr(cur.y, W, rec.y, W, inp->width, inp->height);
         double pu = psnr(cur.u, W / 2, rec.u, W / 2, inp->width / 2, inp->height / 2);

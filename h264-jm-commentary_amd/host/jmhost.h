@@ -125,6 +125,11 @@ typedef struct jm_backend {
     const jmh_mb_result *(*mb_result)(void *ctx, int mb_addr);
     int (*read_recon)(void *ctx, jm_pic *rec);
     void (*destroy)(void *ctx);
+    /* optional (NULL: DeblockFrame runs on the host, jm_deblock_picture): the backend deblocks
+       while encoding (jmh_frame_params.deblock), returns the filtered picture and makes it the
+       next reference without a host round trip */
+    int (*read_deblocked)(void *ctx, jm_pic *rec);
+    int (*reference_deblocked)(void *ctx);
 } jm_backend;
 
 typedef struct jm_stats {

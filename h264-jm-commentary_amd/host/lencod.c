@@ -19,6 +19,10 @@ static int gpu_recon(void *ctx, jm_pic *p) {
     return jmh_read_recon((jmh_ctx *)ctx, p->y, p->u, p->v, p->w, p->w / 2);
 }
 static void gpu_destroy(void *ctx) { jmh_destroy((jmh_ctx *)ctx); }
+static int gpu_deblocked(void *ctx, jm_pic *p) {
+    return jmh_read_deblocked((jmh_ctx *)ctx, p->y, p->u, p->v, p->w, p->w / 2);
+}
+static int gpu_ref_deblocked(void *ctx) { return jmh_set_reference_slot((jmh_ctx *)ctx, -2); }
 
 int main(int argc, char **argv) {
     jm_input inp;
@@ -30,7 +34,9 @@ int main(int argc, char **argv) {
     jmh_ctx *ctx = NULL;
     int r = jmh_create(&cfg, inp.hip_device, &ctx);
     if (r) { fprintf(stderr, "jmh_create failed: %s\n", jmh_strerror(r)); return 2; }
-    jm_backend be = {"mi355x-hip", ctx, gpu_set_ref, gpu_encode, gpu_res, gpu_recon, gpu_destroy};
+    jm_backend be = {"mi355x-hip", ctx, gpu_set_ref, gpu_encode, gpu_res, gpu_recon, gpu_destroy,
+                     gpu_deblocked, gpu_ref_deblocked};
+    if (getenv("JMH_HOST_DEBLOCK")) be.read_deblocked = NULL, be.reference_deblocked = NULL;
     jm_stats st;
     r = jm_encode_sequence(&inp, &be, &st, stdout);
     double mp = (double)inp.width * inp.height * st.frames / 1e6;

@@ -17,7 +17,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 2
+JMH_ABI_VERSION = 3
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -42,7 +42,9 @@ class JmhConfig(ctypes.Structure):
 class JmhFrameParams(ctypes.Structure):
     _fields_ = [("slice_type", ctypes.c_int32), ("qp", ctypes.c_int32),
                 ("lambda_mode", ctypes.c_int32), ("lambda_motion", ctypes.c_int32),
-                ("chroma_qp_offset", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+                ("chroma_qp_offset", ctypes.c_int32), ("deblock", ctypes.c_int32),
+                ("lf_disable", ctypes.c_int32), ("lf_alpha_div2", ctypes.c_int32),
+                ("lf_beta_div2", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
 
 
 class JmhTiming(ctypes.Structure):
@@ -74,6 +76,7 @@ _SIGS = {
     "jmh_frame_wait": (_I, [_P]),
     "jmh_get_mb_result": (_P, [_P, _I]),
     "jmh_read_recon": (_I, [_P, _P, _P, _P, _I, _I]),
+    "jmh_read_deblocked": (_I, [_P, _P, _P, _P, _I, _I]),
     "jmh_load_frame": (_I, [_P, _I, _P, _P, _P, _I, _I]),
     "jmh_set_reference_slot": (_I, [_P, _I]),
     "jmh_encode_slot": (_I, [_P, _I, ctypes.POINTER(JmhFrameParams)]),
@@ -134,11 +137,15 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     return cfg
 
 
-def frame_params(slice_type, qp, chroma_qp_offset=0):
+def frame_params(slice_type, qp, chroma_qp_offset=0, deblock=None):
+    """deblock: None (no device deblocking) or (disable_idc, alpha_div2, beta_div2)."""
     fp = JmhFrameParams()
     fp.slice_type, fp.qp = slice_type, qp
     fp.lambda_mode = fp.lambda_motion = lambda_rdo_off(qp)
     fp.chroma_qp_offset = chroma_qp_offset
+    if deblock is not None:
+        fp.deblock = 1
+        fp.lf_disable, fp.lf_alpha_div2, fp.lf_beta_div2 = deblock
     return fp
 
 
@@ -178,8 +185,8 @@ class Encoder:
         _check(self.lib.jmh_set_reference(self.ctx, 0, 0, _ptr(y), _ptr(u), _ptr(v),
                                           self.w, self.w // 2), "jmh_set_reference")
 
-    def encode(self, y, u, v, slice_type, qp, chroma_qp_offset=0):
-        fp = frame_params(slice_type, qp, chroma_qp_offset)
+    def encode(self, y, u, v, slice_type, qp, chroma_qp_offset=0, deblock=None):
+        fp = frame_params(slice_type, qp, chroma_qp_offset, deblock)
         _check(self.lib.jmh_frame_submit(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2,
                                          ctypes.byref(fp)), "jmh_frame_submit")
         _check(self.lib.jmh_frame_wait(self.ctx), "jmh_frame_wait")
@@ -193,13 +200,19 @@ class Encoder:
         buf = (ctypes.c_char * (n * MB_RESULT_DTYPE.itemsize)).from_address(p)
         return np.frombuffer(bytes(buf), dtype=MB_RESULT_DTYPE).copy()
 
-    def recon(self):
+    def _read(self, fn):
         y = np.empty((self.h, self.w), np.uint8)
         u = np.empty((self.h // 2, self.w // 2), np.uint8)
         v = np.empty_like(u)
-        _check(self.lib.jmh_read_recon(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2),
-               "jmh_read_recon")
+        _check(getattr(self.lib, fn)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2), fn)
         return y, u, v
+
+    def recon(self):
+        return self._read("jmh_read_recon")
+
+    def deblocked(self):
+        """DeblockFrame output of the last encode(..., deblock=...) (jmh_read_deblocked)."""
+        return self._read("jmh_read_deblocked")
 
     # ---- device-resident path (bench) ----
     def load_frame(self, slot, y, u, v):
@@ -209,8 +222,8 @@ class Encoder:
     def set_reference_slot(self, slot):
         _check(self.lib.jmh_set_reference_slot(self.ctx, slot), "jmh_set_reference_slot")
 
-    def encode_slot(self, slot, slice_type, qp):
-        fp = frame_params(slice_type, qp)
+    def encode_slot(self, slot, slice_type, qp, deblock=None):
+        fp = frame_params(slice_type, qp, deblock=deblock)
         _check(self.lib.jmh_encode_slot(self.ctx, slot, ctypes.byref(fp)), "jmh_encode_slot")
 
     def sync(self):

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 2
+#define JMH_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define JMH_OK                 0
@@ -93,7 +93,12 @@ typedef struct jmh_frame_params {
     int32_t lambda_mode;       /* RDO off: QP2QUANT[max(0,qp-12)] (integer, computed on host)    */
     int32_t lambda_motion;     /* RDO off: == lambda_mode                                        */
     int32_t chroma_qp_offset;  /* chroma_qp_index_offset                                         */
-    int32_t reserved[7];
+    int32_t deblock;           /* 1: also deblock (DeblockFrame, 8.7) on the device into the     */
+                               /*    next reference (jmh_read_deblocked, set_reference_slot(-2)) */
+    int32_t lf_disable;        /* disable_deblocking_filter_idc (1: copy, no filtering)          */
+    int32_t lf_alpha_div2;     /* slice_alpha_c0_offset_div2                                     */
+    int32_t lf_beta_div2;      /* slice_beta_offset_div2                                         */
+    int32_t reserved[3];
 } jmh_frame_params;
 
 /* ---- per-macroblock result (what encode_one_macroblock leaves behind) ------------------- */
@@ -156,11 +161,14 @@ int  jmh_frame_submit(jmh_ctx *ctx, const uint8_t *y, const uint8_t *u, const ui
 int  jmh_frame_wait(jmh_ctx *ctx);
 const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *ctx, int mb_addr);
 int  jmh_read_recon(jmh_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y, int stride_c);
+/* the deblocked picture of the last jmh_frame_submit with deblock = 1 (replaces DeblockFrame)  */
+int  jmh_read_deblocked(jmh_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y, int stride_c);
 
 /* ---- device-resident variants (inputs already in HBM; used by bench.py) ------------------ */
 int  jmh_load_frame(jmh_ctx *ctx, int slot, const uint8_t *y, const uint8_t *u, const uint8_t *v,
                     int stride_y, int stride_c);
-int  jmh_set_reference_slot(jmh_ctx *ctx, int slot);   /* slot = -1: the last picture's recon  */
+int  jmh_set_reference_slot(jmh_ctx *ctx, int slot);   /* slot -1: the last picture's recon,    */
+                                                         /* -2: its device deblocking (deblock=1) */
 int  jmh_encode_slot(jmh_ctx *ctx, int slot, const jmh_frame_params *fp); /* async, no D2H    */
 int  jmh_sync(jmh_ctx *ctx);
 int  jmh_get_timing(jmh_ctx *ctx, jmh_timing *t);

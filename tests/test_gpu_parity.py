@@ -169,6 +169,34 @@ def test_saturated_frames():
     encode_pair(64, 48, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE], 18, search_range=8)
 
 
+def test_device_resident_deblocked_reference():
+    """f2: the slot path (encode_slot with the fused loop filter, set_reference_slot(-2) swaps the
+    deblocked picture in as reference) == the host-copy path (encode, read_deblocked, set_reference)."""
+    w, h, qp, dbk = 96, 64, 30, (0, 1, -2)
+    pics = synth_seq(w, h, 4, 11)
+    a = jmhip.Encoder(w, h, search_range=8, slots=3)
+    b = jmhip.Encoder(w, h, search_range=8)
+    for i in range(3):
+        a.load_frame(i, *pics[i])
+    a.encode_slot(0, jmhip.JMH_I_SLICE, qp, deblock=dbk)
+    for i in (1, 2):
+        a.set_reference_slot(-2)
+        a.encode_slot(i, jmhip.JMH_P_SLICE, qp, deblock=dbk)
+    a.set_reference_slot(-2)
+    ares, arec = a.encode(*pics[3], jmhip.JMH_P_SLICE, qp, deblock=dbk)
+    adbk = a.deblocked()
+    for i in range(3):
+        b.encode(*pics[i], jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE, qp, deblock=dbk)
+        b.set_reference(*b.deblocked())
+    bres, brec = b.encode(*pics[3], jmhip.JMH_P_SLICE, qp, deblock=dbk)
+    assert_same(ares, arec, bres, brec, w // 16)
+    for x, y in zip(adbk, b.deblocked()):
+        assert np.array_equal(x, y)
+    with pytest.raises(jmhip.JmhError):   # the swap consumed the deblocked picture
+        a.set_reference_slot(-2)
+        a.set_reference_slot(-2)
+
+
 # ---------------- end to end: lencod bitstream + recon, closed loop ----------------
 def run_lencod(binary, out_dir, extra):
     args = [binary, "-p", f"OutputFile={out_dir}/a.264", "-p", f"ReconFile={out_dir}/rec.yuv"]
@@ -185,6 +213,11 @@ def run_lencod(binary, out_dir, extra):
      "IntraPeriod=3", "QPRemainingFrame=33"],
     ["InputFile=synthetic:3", "FramesToBeEncoded=3", "SourceWidth=200", "SourceHeight=120", "SearchRange=8",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=2", "LoopFilterBetaOffset=-1"],
+    ["InputFile=synthetic:4", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=8",
+     "LoopFilterParametersFlag=1", "LoopFilterDisable=1"],
+    ["InputFile=synthetic:5", "FramesToBeEncoded=4", "SourceWidth=320", "SourceHeight=240", "SearchRange=16",
+     "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=6", "LoopFilterBetaOffset=6", "QPFirstFrame=40",
+     "QPRemainingFrame=44"],
 ])
 def test_lencod_bitstream_identical(extra):
     with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:

@@ -55,7 +55,7 @@ def run_stream(seed, steps, warmup, dist_mod=None):
     jm, streams = load_jmhip(), load_streams()
     frames = [jm.synth_frame(W, H, seed, i) for i in range(3)]
     enc = OracleSlots()
-    dt = streams.timed_run(streams.PStream(enc, frames, QP), steps, warmup, dist_mod)
+    dt = streams.timed_run(streams.PStream(enc, frames, QP, deblock=None), steps, warmup, dist_mod)
     h = hashlib.sha256(b"".join(p.tobytes() for p in enc.rec) + b"".join(r.tobytes() for r in enc.results))
     return dt, h.hexdigest()
 
@@ -101,7 +101,7 @@ def test_single_process_harness_counts_steps():
     jm, streams = load_jmhip(), load_streams()
     frames = [jm.synth_frame(W, H, 5, i) for i in range(3)]
     enc = OracleSlots()
-    streams.timed_run(streams.PStream(enc, frames, QP), steps=3, warmup=2)
+    streams.timed_run(streams.PStream(enc, frames, QP, deblock=None), steps=3, warmup=2)
     # one IDR picture + warmup + timed P pictures; the IDR picture is all intra (I4MB 9 /
     # I16MB 10), the P pictures reference the previous reconstruction and use inter types
     assert len(enc.results) == 1 + 2 + 3
