@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """bench.py — JM hot path on MI355X: ME + transform megapixels/s, 1080p FFS SR=32.
 
-One step = one P picture of the hot path with inputs resident in HBM: quarter-pel
-interpolation of the new reference (the previous picture's reconstruction) + the whole
-macroblock wavefront (k_mb_analyse: FFS SAD table + argmin, sub-pel SATD search, intra
-decisions; k_mb_final: RDO-off mode decision, luma/chroma TQ + reconstruction) over all 8160
-macroblocks of a coded 1920x1088 picture.  Entropy coding and deblocking are excluded, as JM's
-ME/transform time is.  Multi-GPU: one independent stream per rank (seed = rank),
-no collective in the data path; a gloo barrier brackets the timed region and the maximum time
-over ranks is used (h264-jm-commentary_amd/streams.py).
+One step = one P picture of the hot path with inputs resident in HBM, referencing the previous
+picture's deblocked reconstruction: the whole macroblock wavefront (k_mb_analyse: FFS SAD table
++ argmin, sub-pel SATD search on the fly from the reference, intra decisions; k_mb_final: RDO-off
+mode decision, luma/chroma TQ + reconstruction, deblocking) over all 8160 macroblocks of a coded
+1920x1088 picture.  Pictures are pipelined: picture q runs diagonal d once picture q-1 has
+finished diagonal d + PIPE_LAG, so ~15 pictures share each launch; the timed region holds the
+pipeline fill and drain (sync on both sides).  Entropy coding is excluded, as in JM's
+ME/transform time.  Multi-GPU: one independent stream per rank (seed = rank), no
+collective in the data path; a gloo barrier brackets the timed region and the maximum time over
+ranks is used (h264-jm-commentary_amd/streams.py).
 
 Prints ONE JSON line (rank 0).
 """
@@ -28,9 +30,9 @@ W, H = 1920, 1088
 SR, QP = 32, 28
 NMB = (W // 16) * (H // 16)
 # algorithmic HBM bytes per coded picture: current 1.5 B/px + reference 1.5 B/px
-# (each read once) + reconstruction 1.5 B/px written + levels (int16 per sample) 3.0 B/px, plus
-# per-MB side data (MVs, refs, modes, cbp) 80 B/MB
-BYTES_PER_PIXEL = 7.5
+# (each read once) + reconstruction 1.5 B/px and deblocked reconstruction 1.5 B/px written +
+# levels (int16 per sample) 3.0 B/px, plus per-MB side data (MVs, refs, modes, cbp) 80 B/MB
+BYTES_PER_PIXEL = 9.0
 SIDE_BYTES_PER_MB = 80
 BYTES_PER_FRAME = W * H * BYTES_PER_PIXEL + NMB * SIDE_BYTES_PER_MB
 HBM_PEAK_GBS = 8000.0                                    # MI355X_MICROARCH.md (spec)
@@ -77,8 +79,8 @@ def read_pmc_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=120)
+    ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -107,8 +109,9 @@ def main():
     value = world * args.steps * DISP_W * DISP_H / 1e6 / dt
     pictures = max(1, tm.pictures)
     an_launch_ms = tm.analyse_ms / max(1, tm.analyse_launches)
-    an_per_pic = tm.mb_launches / 2                      # one k_mb_analyse + one k_mb_final per diagonal
-    bytes_per_launch = BYTES_PER_FRAME / max(1.0, an_per_pic)
+    an_per_pic = tm.ticks / pictures                     # one k_mb_analyse + one k_mb_final per tick
+    mbs_per_launch = tm.tick_mbs / max(1, tm.ticks)      # MBs of all pictures in flight, per tick
+    bytes_per_launch = BYTES_PER_FRAME / NMB * mbs_per_launch
     achieved_gbs = bytes_per_launch / (an_launch_ms * 1e-3) / 1e9
     mb_ms_pic = tm.mb_ms / pictures
     pmc = read_pmc_traffic()
@@ -131,6 +134,7 @@ def main():
                         "RDO off, QP 28, P pictures (one independent stream per GPU)",
             "global_batch": world,
             "parallelism": f"streams{world}",
+            "pipeline_depth": enc.depth,
         },
         "roofline": {
             "bound": "hbm",
@@ -143,6 +147,7 @@ def main():
             "algorithmic_bytes_per_launch": round(bytes_per_launch),
             "avg_launch_ms": round(an_launch_ms, 5),
             "launches_per_picture": round(an_per_pic, 2),
+            "mbs_per_launch": round(mbs_per_launch, 1),
         },
         "valu_roofline": {
             "note": "integer-search absolute differences (v_sad_u8) over the wavefront time",

@@ -717,21 +717,23 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     PSTAMP(13);
 }
 
-__global__ __launch_bounds__(NTA) void k_mb_analyse(DevParams d) {
+__global__ __launch_bounds__(NTA) void k_mb_analyse(const TickArgs t) {
     __shared__ AnalyseS s;
-    const int n = d.ndiag;
-    // P slices: [0,n) role 2 (longest, dispatched first), [n,2n) role 1, [2n,3n) role 0
-    // I slices: [0,n) role 0, [n,2n) role 1 (intra decisions only)
-    const int grp = blockIdx.x / n, i = blockIdx.x % n;
-    const int role = d.slice_type == JMH_P_SLICE ? 2 - grp : (grp == 0 ? 0 : 1);
-    const int mby = d.y_min + i, mbx = d.diag - 2 * mby;
+    // blocks: [0, nPm) role 2 of the P pictures' MBs (longest, dispatched first), then role 1 and
+    // role 0 over every picture's MBs (an I picture runs roles 0 and 1 only)
+    const int nPm = t.pre[t.nP], tot = t.pre[t.npic], b = blockIdx.x;
+    const int role = b < nPm ? 2 : (b < nPm + tot ? 1 : 0);
+    const int idx = role == 2 ? b : (role == 1 ? b - nPm : b - nPm - tot);
+    const int e = tick_entry(t, idx);
+    const DevParams d = tick_params(t, e);
+    const int mby = d.y_min + (idx - t.pre[e]), mbx = d.diag - 2 * mby;
     if (role == 2) me_role<2>(d, s.me, mbx, mby);
     else if (role == 1) me_role<1>(d, s.me, mbx, mby);
     else intra_role(d, s.in, mbx, mby);
 }
 
-hipError_t jmh_launch_analyse(const DevParams &p, hipStream_t st) {
-    const int nblocks = (p.slice_type == JMH_P_SLICE ? 3 : 2) * p.ndiag;
-    hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, p);
+hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
+    const int nblocks = t.pre[t.nP] + 2 * t.pre[t.npic];
+    hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }

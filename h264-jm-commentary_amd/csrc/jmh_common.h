@@ -48,6 +48,42 @@ __device__ __forceinline__ int isign(int a, int b) { return b < 0 ? -abs(a) : ab
 __device__ __forceinline__ int mvbits(int v) { return v == 0 ? 1 : 2 * (31 - __clz(abs(v))) + 3; }
 __device__ __forceinline__ int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
 // JM spiral index of relative position (x, y) (Init_Motion_Search_Module ordering)
+// ---- quarter-pel samples straight from the reference (H.264 8.4.2.2.1, spec clamping) ----
+__device__ __forceinline__ int rpx(const uint8_t *p, int w, int h, int x, int y) { return p[iclip(0, h - 1, y) * w + iclip(0, w - 1, x)]; }
+__device__ __forceinline__ int hb1(const uint8_t *p, int w, int h, int x, int y) {
+    return tap6(rpx(p, w, h, x - 2, y), rpx(p, w, h, x - 1, y), rpx(p, w, h, x, y), rpx(p, w, h, x + 1, y), rpx(p, w, h, x + 2, y),
+                rpx(p, w, h, x + 3, y));
+}
+__device__ __forceinline__ int vh1(const uint8_t *p, int w, int h, int x, int y) {
+    return tap6(rpx(p, w, h, x, y - 2), rpx(p, w, h, x, y - 1), rpx(p, w, h, x, y), rpx(p, w, h, x, y + 1), rpx(p, w, h, x, y + 2),
+                rpx(p, w, h, x, y + 3));
+}
+// one luma sample at quarter-pel position (X, Y) (units of 1/4 pel): only the half-pel samples
+// the phase needs (G, b, h, s, m, j of Figure 8-4), same values as k_interp's 16 planes
+__device__ __forceinline__ int qpel_direct(const uint8_t *ref, int W, int H, int X, int Y) {
+    const int x = X >> 2, y = Y >> 2, fx = X & 3, fy = Y & 3;
+    auto hb = [&](int xx, int yy) { return clip255((hb1(ref, W, H, xx, yy) + 16) >> 5); };
+    auto vb = [&](int xx, int yy) { return clip255((vh1(ref, W, H, xx, yy) + 16) >> 5); };
+    if (fy == 0) {
+        const int G = rpx(ref, W, H, x, y);
+        if (fx == 0) return G;
+        const int b = hb(x, y);
+        return fx == 2 ? b : ((fx == 1 ? G : rpx(ref, W, H, x + 1, y)) + b + 1) >> 1;
+    }
+    if (fx == 0) {
+        const int h = vb(x, y);
+        return fy == 2 ? h : ((fy == 1 ? rpx(ref, W, H, x, y) : rpx(ref, W, H, x, y + 1)) + h + 1) >> 1;
+    }
+    if ((fx & 1) && (fy & 1)) return (hb(x, fy == 1 ? y : y + 1) + vb(fx == 1 ? x : x + 1, y) + 1) >> 1;   // e g p r
+    int j1 = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) j1 += (k == 0 || k == 5 ? 1 : (k == 1 || k == 4 ? -5 : 20)) * vh1(ref, W, H, x - 2 + k, y);
+    const int j = clip255((j1 + 512) >> 10);
+    if (fx == 2 && fy == 2) return j;
+    const int o = fx == 2 ? hb(x, fy == 1 ? y : y + 1) : vb(fx == 1 ? x : x + 1, y);   // f q / i k
+    return (j + o + 1) >> 1;
+}
+
 __device__ __forceinline__ int spiral_index(int x, int y) {
     int ax = abs(x), ay = abs(y), l = max(ax, ay);
     if (l == 0) return 0;

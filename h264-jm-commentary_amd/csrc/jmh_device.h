@@ -11,6 +11,13 @@
 #define NT 256                           // threads per finalize / unit workgroup
 #define NTA 512                          // threads per analysis workgroup (8 waves, 2 per SIMD)
 #define BIGCOST (1 << 20)
+#define PMAX 20                          // pictures per wavefront tick (pipelined pictures in flight)
+// A picture's macroblock (x, y) reads its reference inside MB columns x-5..x+5 and rows y-5..y+5:
+// window centre |MVP/4| <= SR, positions +-SR around it, +-3/4 sub-pel and the 6-tap (|dx| <= 68
+// px for SR 32).  The reference MB (x', y') is final (deblocked) once the final kernel of its
+// bottom neighbour (diagonal x' + 2y' + 2) has run, so picture q may run diagonal d once picture
+// q-1 has completed diagonals <= d + 5 + 10 + 2: a lag of PIPE_LAG diagonals.
+#define PIPE_LAG 18
 
 // Per-macroblock analysis results, written by k_mb_analyse (three roles on separate
 // workgroups) and consumed by k_mb_final on the same wavefront diagonal.
@@ -32,10 +39,8 @@ struct DevParams {
     int sr, side, npos;
     int search_mode, use_hadamard, restrict_sr;
     int inter_search[8];
-    int qstride, qplane;
     const uint8_t *orgY, *orgU, *orgV;
     const uint8_t *refY, *refU, *refV;
-    const uint8_t *qpel;
     uint8_t *recY, *recU, *recV;
     uint8_t *dbkY, *dbkU, *dbkV;   // deblocked reconstruction (null: no deblocking on the device)
     int lf_disable, lf_offA, lf_offB;   // disable_deblocking_filter_idc, FilterOffsetA/B (= 2 x div2)
@@ -47,5 +52,54 @@ struct DevParams {
     unsigned long long *prof;   // debug phase timestamps (null: off)
     int prof_mb;
     int slice_type, qp, lambda_mode, lambda_motion, cqp_off;
-    int diag, y_min, ndiag;     // wavefront diagonal of this launch: mbx + 2*mby == diag, ndiag MBs
+    int diag, y_min;            // wavefront diagonal of this picture in the launch: mbx + 2*mby == diag
 };
+
+// One wavefront tick: the same diagonal step for up to PMAX pictures in flight, each on its own
+// diagonal (kernel argument, by value; ~2.4 KB).  Entries [0, nP) are P pictures.
+struct PicParams {
+    const uint8_t *org, *ref;            // 4:2:0 pictures, Y then U then V
+    uint8_t *rec, *dbk;                  // dbk null: no deblocking
+    int16_t *mv;
+    int8_t *refidx, *ipred;
+    jmh_mb_result *res;
+    MbScratch *scr;
+    int32_t slice_type, qp, lambda_mode, lambda_motion, cqp_off, lf_disable, lf_offA, lf_offB;
+    int32_t diag, y_min;
+};
+struct TickArgs {
+    int W, H, mbw, mbh, sr, search_mode, use_hadamard, restrict_sr;
+    int inter_search[8];
+    unsigned long long *prof;
+    int prof_mb;
+    int npic, nP;
+    int pre[PMAX + 1];                   // MB prefix sums over the entries
+    PicParams p[PMAX];
+};
+
+// entry of MB index idx (pre[e] <= idx < pre[e + 1]); uniform scalar loop
+__device__ __forceinline__ int tick_entry(const TickArgs &t, int idx) {
+    int e = 0;
+    while (e + 1 < t.npic && t.pre[e + 1] <= idx) e++;
+    return e;
+}
+__device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
+    DevParams d;
+    const PicParams &q = t.p[e];
+    d.W = t.W; d.H = t.H; d.Wc = t.W >> 1; d.Hc = t.H >> 1; d.mbw = t.mbw; d.mbh = t.mbh;
+    d.sr = t.sr; d.side = 2 * t.sr + 1; d.npos = d.side * d.side;
+    d.search_mode = t.search_mode; d.use_hadamard = t.use_hadamard; d.restrict_sr = t.restrict_sr;
+#pragma unroll
+    for (int i = 0; i < 8; i++) d.inter_search[i] = t.inter_search[i];
+    const int ls = t.W * t.H, lc = ls >> 2;
+    d.orgY = q.org; d.orgU = q.org + ls; d.orgV = q.org + ls + lc;
+    d.refY = q.ref; d.refU = q.ref + ls; d.refV = q.ref + ls + lc;
+    d.recY = q.rec; d.recU = q.rec + ls; d.recV = q.rec + ls + lc;
+    d.dbkY = q.dbk; d.dbkU = q.dbk ? q.dbk + ls : nullptr; d.dbkV = q.dbk ? q.dbk + ls + lc : nullptr;
+    d.lf_disable = q.lf_disable; d.lf_offA = q.lf_offA; d.lf_offB = q.lf_offB;
+    d.mv = q.mv; d.refidx = q.refidx; d.ipred = q.ipred; d.res = q.res; d.scr = q.scr;
+    d.prof = e == 0 ? t.prof : nullptr; d.prof_mb = t.prof_mb;
+    d.slice_type = q.slice_type; d.qp = q.qp; d.lambda_mode = q.lambda_mode; d.lambda_motion = q.lambda_motion;
+    d.cqp_off = q.cqp_off; d.diag = q.diag; d.y_min = q.y_min;
+    return d;
+}

@@ -91,16 +91,13 @@ __device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int al
     }
 }
 
-__device__ __forceinline__ int qpel_at(const DevParams &d, int X, int Y) {
-    int x = iclip(-QPAD, d.W - 1 + QPAD, X >> 2), y = iclip(-QPAD, d.H - 1 + QPAD, Y >> 2);
-    int ph = (Y & 3) * 4 + (X & 3);
-    return d.qpel[(size_t)ph * d.qplane + (size_t)(y + QPAD) * d.qstride + (x + QPAD)];
-}
 
-__global__ __launch_bounds__(NT) void k_mb_final(DevParams d) {
+__global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
     __shared__ FinS s;
     const int tid = threadIdx.x;
-    const int mby = d.y_min + blockIdx.x, mbx = d.diag - 2 * mby;
+    const int e = tick_entry(t, blockIdx.x);
+    const DevParams d = tick_params(t, e);
+    const int mby = d.y_min + (blockIdx.x - t.pre[e]), mbx = d.diag - 2 * mby;
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
     const int W = d.W, Wc = d.Wc, W4 = d.W >> 2;
     const int slice_p = d.slice_type == JMH_P_SLICE;
@@ -219,7 +216,7 @@ __global__ __launch_bounds__(NT) void k_mb_final(DevParams d) {
             if (s.bnz[b]) { cbp = 15; cbp_blk |= 1 << b; }
     } else {
         // LumaResidualCoding / LumaResidualCoding8x8 (+ SetCoeffAndReconstruction8x8)
-        const int p = qpel_at(d, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1]);
+        const int p = qpel_direct(d.refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1]);
         const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
         int lev, dq, cc;
         const int q_bits = 15 + qp / 6;
@@ -450,7 +447,7 @@ __global__ __launch_bounds__(NT) void k_mb_final(DevParams d) {
     PSTAMP(19);
 }
 
-hipError_t jmh_launch_final(const DevParams &p, hipStream_t st) {
-    hipLaunchKernelGGL(k_mb_final, dim3(p.ndiag), dim3(NT), 0, st, p);
+hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st) {
+    hipLaunchKernelGGL(k_mb_final, dim3(t.pre[t.npic]), dim3(NT), 0, st, t);
     return hipGetLastError();
 }

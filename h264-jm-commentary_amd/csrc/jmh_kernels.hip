@@ -2,7 +2,9 @@
 //
 //  k_interp      UnifiedOneForthPix [J] / H.264 8.4.2.2.1: 16 quarter-pel phase planes of the
 //                reference (HBM-bound; one thread per padded integer position, all 16 phases),
-//                read by the final luma motion compensation in k_mb_final.
+//                for the jmh_read_qpel seam (a1).  The macroblock kernels interpolate on the fly
+//                (LDS planes in k_mb_analyse, qpel_direct in k_mb_final), so a picture can be
+//                searched while its reference is still being reconstructed (pipelining).
 //  k_sad_table / k_tq4x4   unit seams (jmh_ffs_sad_table / jmh_tq4x4_batch); k_tq4x4 runs the
 //                same 16-lane TQ primitive the macroblock kernels use.
 //
@@ -12,15 +14,7 @@
 // ======================================================================================
 //  quarter-pel interpolation (H.264 8.4.2.2.1), spec coordinate clamping
 // ======================================================================================
-__device__ __forceinline__ int rpx(const uint8_t *p, int w, int h, int x, int y) { return p[iclip(0, h - 1, y) * w + iclip(0, w - 1, x)]; }
-__device__ __forceinline__ int hb1(const uint8_t *p, int w, int h, int x, int y) {
-    return tap6(rpx(p, w, h, x - 2, y), rpx(p, w, h, x - 1, y), rpx(p, w, h, x, y), rpx(p, w, h, x + 1, y), rpx(p, w, h, x + 2, y),
-                rpx(p, w, h, x + 3, y));
-}
-__device__ __forceinline__ int vh1(const uint8_t *p, int w, int h, int x, int y) {
-    return tap6(rpx(p, w, h, x, y - 2), rpx(p, w, h, x, y - 1), rpx(p, w, h, x, y), rpx(p, w, h, x, y + 1), rpx(p, w, h, x, y + 2),
-                rpx(p, w, h, x, y + 3));
-}
+// rpx / hb1 / vh1: jmh_common.h
 
 __global__ __launch_bounds__(256) void k_interp(const uint8_t *__restrict__ ref, int W, int H, uint8_t *__restrict__ qpel, int qstride,
                                                 int qplane) {

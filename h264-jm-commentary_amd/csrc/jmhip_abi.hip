@@ -1,24 +1,35 @@
 // jmhip_abi.hip — the extern "C" boundary (include/jmhip.h) over the gfx950 kernels.
 // One context = one HIP device + one HIP stream; device buffers are sized once at create.
-// Per picture: H2D of the source (pinned staging) -> 254 wavefront launches at 1080p (one per
-// diagonal mbx + 2*mby) -> D2H of the macroblock results and the unfiltered reconstruction.
+//
+// Pictures run as a pipeline of wavefront ticks.  A picture walks its 254 diagonals (1080p;
+// mbx + 2*mby == d); a tick launches k_mb_analyse + k_mb_final once for the next diagonal of
+// every picture in flight.  A picture that references the previous one starts once that one is
+// PIPE_LAG diagonals ahead, so in steady state ~254/PIPE_LAG pictures share each launch and the
+// chip sees hundreds of macroblocks per dispatch instead of <= 34.  Ticks are issued lazily
+// from the host (push issues until the new picture has started; pop / sync drain), all on one
+// stream, so stream order is the only synchronisation.
+//
+// Per-picture device state lives in a ring of nring = depth + 2 entries (source, recon,
+// deblocked recon, MV / ref_idx / ipred maps, results, MbScratch); an entry is reused only once
+// no picture in flight reads or writes it and its results were popped.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <deque>
 #include <vector>
 #include "jmh_device.h"
 
 hipError_t jmh_launch_interp(const uint8_t *ref, int W, int H, uint8_t *qpel, int qstride, int qplane, hipStream_t st);
-hipError_t jmh_launch_analyse(const DevParams &p, hipStream_t st);
-hipError_t jmh_launch_final(const DevParams &p, hipStream_t st);
+hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
                                 const int32_t *centres, uint16_t *out, hipStream_t st);
 hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st);
 
-// JMH_FLAG_KERNEL_TIMING brackets every KT_STRIDE-th diagonal's two launches with events: the
-// averages are sampled uniformly over the picture while the event packets stay off most launches
+// JMH_FLAG_KERNEL_TIMING brackets every KT_STRIDE-th tick's two launches with events: the
+// averages are sampled uniformly while the event packets stay off most launches
 #define KT_STRIDE 8
 // ring of begin/end event pairs; completed pairs are folded into `sum` (ms)
 struct EvRing {
@@ -65,28 +76,53 @@ static void ring_drain(EvRing &r, float &sum, int &n) {
     r.sum = 0; r.n = 0;
 }
 
+
+// one ring entry: everything one picture in flight owns
+struct PicBuf {
+    uint8_t *src, *rec, *dbk;            // device: source (jmh_frame_push), recon, deblocked recon
+    int16_t *mv;
+    int8_t *refidx, *ipred;
+    jmh_mb_result *res;
+    MbScratch *scr;
+    jmh_mb_result *h_res;                // pinned host copies (allocated on first readback use)
+    uint8_t *h_src, *h_rec, *h_dbk;
+    hipEvent_t ev_src, ev_t0, ev_done;   // staging reuse / push..done timing
+    int unpopped;                        // readback picture not yet popped
+    int deblocked;                       // the occupant was deblocked on the device (dbk valid)
+};
+
+// a picture in flight (not yet fully issued)
+struct Flight {
+    int id, entry, ref_entry;            // ref_entry: ring entry read as reference (-1: d_ref / none)
+    int pred_id;                         // picture it must trail by PIPE_LAG diagonals (-1: none)
+    int stage, started, readback;
+    PicParams pp;
+};
+
+enum { REF_NONE, REF_BUF, REF_REC, REF_DBK };
+
 struct jmh_ctx {
     jmh_config cfg;
     int dev;
     hipStream_t st;
-    int W, H, Wc, Hc, mbw, mbh, sr, side, npos, qstride, qplane;
-    size_t fsize;                        // bytes of one 4:2:0 picture (Y then U then V)
-    uint8_t *d_cur, *d_ref, *d_qpel, *d_rec, *d_slots;
-    uint8_t *d_dbk;                      // deblocked reconstruction (next reference); swapped with d_ref
+    int W, H, Wc, Hc, mbw, mbh, sr, side, npos, qstride, qplane, nd;
+    size_t fsize, n4, nmb;               // bytes of one 4:2:0 picture (Y then U then V)
+    uint8_t *d_ref, *d_qpel, *d_slots;   // explicit reference (set_reference), a1 seam, slots
     int nslots;
-    int16_t *d_mv;
-    int8_t *d_refidx, *d_ipred;
-    jmh_mb_result *d_res;
-    MbScratch *d_scr;
+    int depth, nring;
+    std::vector<PicBuf> ring;
+    std::deque<Flight> fl;               // issued-incompletely pictures, oldest first
+    std::deque<int> popq;                // readback pictures (ring entries) not yet popped
+    int next_id, next_entry;
+    int last_id, last_entry;             // the last pushed picture
+    int ref_kind, ref_entry;             // the reference of the next pushed picture
+    int cur_entry;                       // results visible through get_mb_result / read_*
     unsigned long long *d_prof;          // JMH_PHASE_PROF=<mb>: per-phase wall clock of one MB
     int prof_mb;
-    jmh_mb_result *h_res;
-    uint8_t *h_rec, *h_dbk, *h_stage_cur, *h_stage_ref;
-    int have_ref, pending, have_results, have_total;
-    int dbk_dev, dbk_host;               // d_dbk / h_dbk hold the last picture's deblocking
-    hipEvent_t ev_t0, ev_t1;
+    uint8_t *h_stage_ref;
     EvRing ring_interp, ring_mb, ring_an, ring_fin;   // ring_an / ring_fin: JMH_FLAG_KERNEL_TIMING
     jmh_timing timing;
+    int ticks_total;
     std::vector<int> dcount, dymin;
 };
 
@@ -122,17 +158,50 @@ int jmh_device_count(void) {
     return n;
 }
 
+}  // extern "C"
+
+static void free_entry(PicBuf &b) {
+    void *dev_bufs[] = {b.src, b.rec, b.dbk, b.mv, b.refidx, b.ipred, b.res, b.scr};
+    for (void *p : dev_bufs) if (p) (void)hipFree(p);
+    void *host_bufs[] = {b.h_res, b.h_src, b.h_rec, b.h_dbk};
+    for (void *p : host_bufs) if (p) (void)hipHostFree(p);
+    hipEvent_t evs[] = {b.ev_src, b.ev_t0, b.ev_done};
+    for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
+}
+
+static int alloc_entry(jmh_ctx *c, PicBuf &b) {
+    memset((void *)&b, 0, sizeof(b));
+#define ALLOC(p, n) do { if (hipMalloc((void **)&(p), (n)) != hipSuccess) return JMH_E_OOM; } while (0)
+    ALLOC(b.src, c->fsize); ALLOC(b.rec, c->fsize); ALLOC(b.dbk, c->fsize);
+    ALLOC(b.mv, c->n4 * 2 * sizeof(int16_t)); ALLOC(b.refidx, c->n4); ALLOC(b.ipred, c->n4);
+    ALLOC(b.res, c->nmb * sizeof(jmh_mb_result));
+    ALLOC(b.scr, c->nmb * sizeof(MbScratch));
+#undef ALLOC
+    if (hipMemset(b.rec, 0, c->fsize) != hipSuccess || hipMemset(b.dbk, 0, c->fsize) != hipSuccess) return JMH_E_HIP;
+    if (hipEventCreate(&b.ev_src) != hipSuccess || hipEventCreate(&b.ev_t0) != hipSuccess ||
+        hipEventCreate(&b.ev_done) != hipSuccess) return JMH_E_HIP;
+    return JMH_OK;
+}
+
+static int alloc_host(jmh_ctx *c, PicBuf &b) {   // pinned readback / staging, on first use
+    if (b.h_res) return JMH_OK;
+#define HALLOC(p, n) do { if (hipHostMalloc((void **)&(p), (n), hipHostMallocDefault) != hipSuccess) return JMH_E_OOM; } while (0)
+    HALLOC(b.h_res, c->nmb * sizeof(jmh_mb_result)); HALLOC(b.h_src, c->fsize);
+    HALLOC(b.h_rec, c->fsize); HALLOC(b.h_dbk, c->fsize);
+#undef HALLOC
+    return JMH_OK;
+}
+
+extern "C" {
+
 void jmh_destroy(jmh_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
-    void *dev_bufs[] = {c->d_cur, c->d_ref, c->d_qpel, c->d_rec, c->d_dbk, c->d_slots, c->d_mv, c->d_refidx,
-                        c->d_ipred, c->d_res, c->d_scr, c->d_prof};
+    for (PicBuf &b : c->ring) free_entry(b);
+    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
-    void *host_bufs[] = {c->h_res, c->h_rec, c->h_dbk, c->h_stage_cur, c->h_stage_ref};
-    for (void *p : host_bufs) if (p) (void)hipHostFree(p);
-    if (c->ev_t0) (void)hipEventDestroy(c->ev_t0);
-    if (c->ev_t1) (void)hipEventDestroy(c->ev_t1);
+    if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     ring_free(c->ring_interp);
     ring_free(c->ring_mb);
     ring_free(c->ring_an);
@@ -150,11 +219,11 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->search_mode != 0) return JMH_E_UNSUPPORTED_CFG;                // FFS (SearchMode 0)
     if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
+    if (cfg->pipeline_depth < 0 || cfg->pipeline_depth > PMAX) return JMH_E_INVALID_ARG;
     int ndev = jmh_device_count();
     if (ndev <= 0) return JMH_E_NO_DEVICE;
     if (hip_device < 0 || hip_device >= ndev) return JMH_E_INVALID_ARG;
     jmh_ctx *c = new jmh_ctx();
-    memset((void *)&c->cfg, 0, sizeof(c->cfg));
     c->cfg = *cfg;
     c->dev = hip_device;
     HCHK(hipSetDevice(hip_device));
@@ -163,34 +232,39 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     c->sr = cfg->search_range; c->side = 2 * c->sr + 1; c->npos = c->side * c->side;
     c->qstride = c->W + 2 * QPAD; c->qplane = c->qstride * (c->H + 2 * QPAD);
     c->fsize = (size_t)c->W * c->H * 3 / 2;
+    c->n4 = (size_t)c->W * c->H / 16; c->nmb = (size_t)c->mbw * c->mbh;
     c->nslots = cfg->num_frame_slots > 0 ? cfg->num_frame_slots : 1;
+    c->nd = (c->mbw - 1) + 2 * (c->mbh - 1) + 1;
+    // enough pictures to cover the wavefront: one starts every PIPE_LAG diagonals
+    int auto_depth = (c->nd + PIPE_LAG - 1) / PIPE_LAG + 1;
+    c->depth = cfg->pipeline_depth > 0 ? cfg->pipeline_depth : (auto_depth < PMAX ? auto_depth : PMAX);
+    c->nring = c->depth + 2;
+    c->next_id = 0; c->next_entry = 0; c->last_id = -1; c->last_entry = -1;
+    c->ref_kind = REF_NONE; c->ref_entry = -1; c->cur_entry = -1;
+    c->prof_mb = -1;
     int st = JMH_OK;
 #define ALLOC(p, n) do { if (hipMalloc((void **)&(p), (n)) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
-#define HALLOC(p, n) do { if (hipHostMalloc((void **)&(p), (n), hipHostMallocDefault) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
     {
         if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { st = JMH_E_HIP; goto fail; }
-        size_t n4 = (size_t)c->W * c->H / 16, nmb = (size_t)c->mbw * c->mbh;
-        ALLOC(c->d_cur, c->fsize); ALLOC(c->d_ref, c->fsize); ALLOC(c->d_rec, c->fsize); ALLOC(c->d_dbk, c->fsize);
+        ALLOC(c->d_ref, c->fsize);
         ALLOC(c->d_qpel, (size_t)16 * c->qplane);
         ALLOC(c->d_slots, c->fsize * c->nslots);
-        ALLOC(c->d_mv, n4 * 2 * sizeof(int16_t)); ALLOC(c->d_refidx, n4); ALLOC(c->d_ipred, n4);
-        ALLOC(c->d_res, nmb * sizeof(jmh_mb_result));
-        ALLOC(c->d_scr, nmb * sizeof(MbScratch));
-        c->prof_mb = -1;
+        c->ring.resize(c->nring);
+        for (PicBuf &b : c->ring) {
+            if ((st = alloc_entry(c, b))) goto fail;
+            if (hipEventRecord(b.ev_src, c->st) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        }
         if (const char *e = getenv("JMH_PHASE_PROF")) {
             c->prof_mb = atoi(e);
             ALLOC(c->d_prof, 64 * sizeof(unsigned long long));
             if (hipMemset(c->d_prof, 0, 64 * sizeof(unsigned long long)) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         }
-        HALLOC(c->h_res, nmb * sizeof(jmh_mb_result)); HALLOC(c->h_rec, c->fsize); HALLOC(c->h_dbk, c->fsize);
-        HALLOC(c->h_stage_cur, c->fsize); HALLOC(c->h_stage_ref, c->fsize);
-        if (hipMemset(c->d_rec, 0, c->fsize) != hipSuccess || hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
-        if (hipEventCreate(&c->ev_t0) != hipSuccess || hipEventCreate(&c->ev_t1) != hipSuccess ||
-            ring_init(c->ring_interp, 64) || ring_init(c->ring_mb, 64) ||
+        if (hipHostMalloc((void **)&c->h_stage_ref, c->fsize, hipHostMallocDefault) != hipSuccess) { st = JMH_E_OOM; goto fail; }
+        if (hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        if (ring_init(c->ring_interp, 64) || ring_init(c->ring_mb, 64) ||
             ((cfg->flags & JMH_FLAG_KERNEL_TIMING) && (ring_init(c->ring_an, 2048) || ring_init(c->ring_fin, 2048)))) { st = JMH_E_HIP; goto fail; }
-        int nd = (c->mbw - 1) + 2 * (c->mbh - 1) + 1;
-        c->dcount.resize(nd); c->dymin.resize(nd);
-        for (int dg = 0; dg < nd; dg++) {
+        c->dcount.resize(c->nd); c->dymin.resize(c->nd);
+        for (int dg = 0; dg < c->nd; dg++) {
             int ymin = dg - (c->mbw - 1) > 0 ? (dg - (c->mbw - 1) + 1) / 2 : 0;
             int ymax = dg / 2 < c->mbh - 1 ? dg / 2 : c->mbh - 1;
             c->dymin[dg] = ymin;
@@ -198,13 +272,16 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         }
     }
 #undef ALLOC
-#undef HALLOC
     *out = c;
     return JMH_OK;
 fail:
     jmh_destroy(c);
     return st;
 }
+
+int jmh_pipeline_depth(const jmh_ctx *c) { return c ? c->depth : JMH_E_INVALID_ARG; }
+
+}  // extern "C"
 
 static void pack_planes(uint8_t *dst, int W, int H, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
     for (int r = 0; r < H; r++) memcpy(dst + (size_t)r * W, y + (size_t)r * sy, W);
@@ -213,119 +290,6 @@ static void pack_planes(uint8_t *dst, int W, int H, const uint8_t *y, const uint
         memcpy(du + (size_t)r * (W / 2), u + (size_t)r * sc, W / 2);
         memcpy(dv + (size_t)r * (W / 2), v + (size_t)r * sc, W / 2);
     }
-}
-
-static int run_interp(jmh_ctx *c, const uint8_t *d_refY) {
-    HCHK(ring_begin(c->ring_interp, c->st));
-    HCHK(jmh_launch_interp(d_refY, c->W, c->H, c->d_qpel, c->qstride, c->qplane, c->st));
-    HCHK(ring_end(c->ring_interp, c->st));
-    c->have_ref = 1;
-    return JMH_OK;
-}
-
-int jmh_set_reference(jmh_ctx *c, int list, int ref_idx, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
-    if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
-    if (list != 0 || ref_idx != 0) return JMH_E_UNSUPPORTED_CFG;
-    HCHK(hipSetDevice(c->dev));
-    HCHK(hipStreamSynchronize(c->st));   // staging buffer reuse
-    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc);
-    HCHK(hipMemcpyAsync(c->d_ref, c->h_stage_ref, c->fsize, hipMemcpyHostToDevice, c->st));
-    return run_interp(c, c->d_ref);
-}
-
-int jmh_set_reference_slot(jmh_ctx *c, int slot) {
-    if (!c || slot < -2 || slot >= c->nslots) return JMH_E_INVALID_ARG;
-    HCHK(hipSetDevice(c->dev));
-    if (slot == -2) {   // the device deblocking becomes the reference: swap buffers, no copy
-        if (!c->dbk_dev) return JMH_E_STATE;
-        uint8_t *t = c->d_ref; c->d_ref = c->d_dbk; c->d_dbk = t;
-        c->dbk_dev = 0;
-        return run_interp(c, c->d_ref);
-    }
-    const uint8_t *src = slot < 0 ? c->d_rec : c->d_slots + (size_t)slot * c->fsize;
-    HCHK(hipMemcpyAsync(c->d_ref, src, c->fsize, hipMemcpyDeviceToDevice, c->st));
-    return run_interp(c, c->d_ref);
-}
-
-static int enqueue_encode(jmh_ctx *c, const uint8_t *d_pic, const jmh_frame_params *fp) {
-    if (fp->slice_type != JMH_P_SLICE && fp->slice_type != JMH_I_SLICE) return JMH_E_UNSUPPORTED_CFG;
-    if (fp->qp < 0 || fp->qp > 51 || fp->lambda_mode < 0 || fp->lambda_motion < 0) return JMH_E_INVALID_ARG;
-    if (fp->slice_type == JMH_P_SLICE && !c->have_ref) return JMH_E_STATE;
-    DevParams p;
-    memset(&p, 0, sizeof(p));
-    p.W = c->W; p.H = c->H; p.Wc = c->Wc; p.Hc = c->Hc; p.mbw = c->mbw; p.mbh = c->mbh;
-    p.sr = c->sr; p.side = c->side; p.npos = c->npos;
-    p.search_mode = c->cfg.search_mode; p.use_hadamard = c->cfg.use_hadamard; p.restrict_sr = c->cfg.restrict_search_range;
-    for (int i = 0; i < 8; i++) p.inter_search[i] = c->cfg.inter_search[i];
-    p.qstride = c->qstride; p.qplane = c->qplane;
-    size_t ls = (size_t)c->W * c->H;
-    p.orgY = d_pic; p.orgU = d_pic + ls; p.orgV = d_pic + ls + ls / 4;
-    p.refY = c->d_ref; p.refU = c->d_ref + ls; p.refV = c->d_ref + ls + ls / 4;
-    p.qpel = c->d_qpel;
-    p.recY = c->d_rec; p.recU = c->d_rec + ls; p.recV = c->d_rec + ls + ls / 4;
-    p.mv = c->d_mv; p.refidx = c->d_refidx; p.ipred = c->d_ipred; p.res = c->d_res; p.scr = c->d_scr;
-    p.prof = c->d_prof; p.prof_mb = c->prof_mb;
-    p.slice_type = fp->slice_type; p.qp = fp->qp; p.lambda_mode = fp->lambda_mode; p.lambda_motion = fp->lambda_motion;
-    p.cqp_off = fp->chroma_qp_offset;
-    if (fp->deblock) {   // DeblockFrame fused into k_mb_final, into d_dbk (never aliases d_ref)
-        if (fp->lf_disable < 0 || fp->lf_disable > 2 || fp->lf_alpha_div2 < -6 || fp->lf_alpha_div2 > 6 ||
-            fp->lf_beta_div2 < -6 || fp->lf_beta_div2 > 6) return JMH_E_INVALID_ARG;
-        p.dbkY = c->d_dbk; p.dbkU = c->d_dbk + ls; p.dbkV = c->d_dbk + ls + ls / 4;
-        p.lf_disable = fp->lf_disable;   // idc 2 == 0 with one slice per picture
-        p.lf_offA = 2 * fp->lf_alpha_div2; p.lf_offB = 2 * fp->lf_beta_div2;
-    }
-    c->dbk_dev = fp->deblock != 0;
-    HCHK(ring_begin(c->ring_mb, c->st));
-    for (size_t dg = 0; dg < c->dcount.size(); dg++) {
-        if (!c->dcount[dg]) continue;
-        p.diag = (int)dg; p.y_min = c->dymin[dg]; p.ndiag = c->dcount[dg];
-        const bool kt = c->ring_an.cap > 0 && dg % KT_STRIDE == 0;   // sampled per-launch timing
-        if (kt) HCHK(ring_begin(c->ring_an, c->st));
-        HCHK(jmh_launch_analyse(p, c->st));
-        if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
-        HCHK(jmh_launch_final(p, c->st));
-        if (kt) HCHK(ring_end(c->ring_fin, c->st));
-    }
-    HCHK(ring_end(c->ring_mb, c->st));
-    int nl = 0;
-    for (int n : c->dcount) nl += 2 * (n > 0);
-    c->timing.mb_launches = nl;
-    return JMH_OK;
-}
-
-int jmh_frame_submit(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc, const jmh_frame_params *fp) {
-    if (!c || !y || !u || !v || !fp || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
-    HCHK(hipSetDevice(c->dev));
-    HCHK(hipStreamSynchronize(c->st));
-    pack_planes(c->h_stage_cur, c->W, c->H, y, u, v, sy, sc);
-    HCHK(hipEventRecord(c->ev_t0, c->st));
-    HCHK(hipMemcpyAsync(c->d_cur, c->h_stage_cur, c->fsize, hipMemcpyHostToDevice, c->st));
-    int r = enqueue_encode(c, c->d_cur, fp);
-    if (r) return r;
-    HCHK(hipMemcpyAsync(c->h_res, c->d_res, (size_t)c->mbw * c->mbh * sizeof(jmh_mb_result), hipMemcpyDeviceToHost, c->st));
-    HCHK(hipMemcpyAsync(c->h_rec, c->d_rec, c->fsize, hipMemcpyDeviceToHost, c->st));
-    if (c->dbk_dev) HCHK(hipMemcpyAsync(c->h_dbk, c->d_dbk, c->fsize, hipMemcpyDeviceToHost, c->st));
-    c->dbk_host = c->dbk_dev;
-    HCHK(hipEventRecord(c->ev_t1, c->st));
-    c->pending = 1;
-    c->have_total = 1;
-    c->have_results = 0;
-    return JMH_OK;
-}
-
-int jmh_frame_wait(jmh_ctx *c) {
-    if (!c) return JMH_E_INVALID_ARG;
-    if (!c->pending) return JMH_E_STATE;
-    HCHK(hipSetDevice(c->dev));
-    HCHK(hipStreamSynchronize(c->st));
-    c->pending = 0;
-    c->have_results = 1;
-    return JMH_OK;
-}
-
-const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *c, int mb_addr) {
-    if (!c || !c->have_results || mb_addr < 0 || mb_addr >= c->mbw * c->mbh) return nullptr;
-    return &c->h_res[mb_addr];
 }
 
 static void unpack_planes(const uint8_t *src, int W, int H, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
@@ -337,41 +301,305 @@ static void unpack_planes(const uint8_t *src, int W, int H, uint8_t *y, uint8_t 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+//  the tick scheduler
+// ---------------------------------------------------------------------------------------------
+static int skip_empty(const jmh_ctx *c, int stage) {
+    while (stage < c->nd && c->dcount[stage] == 0) stage++;
+    return stage;
+}
+
+// after a picture's last tick: enqueue its readback, mark the done event
+static int finish_picture(jmh_ctx *c, const Flight &f) {
+    if (!f.readback) return JMH_OK;
+    PicBuf &b = c->ring[f.entry];
+    HCHK(hipMemcpyAsync(b.h_res, b.res, c->nmb * sizeof(jmh_mb_result), hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(b.h_rec, b.rec, c->fsize, hipMemcpyDeviceToHost, c->st));
+    if (f.pp.dbk) HCHK(hipMemcpyAsync(b.h_dbk, b.dbk, c->fsize, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipEventRecord(b.ev_done, c->st));
+    return JMH_OK;
+}
+
+// one tick: the next diagonal of every picture whose dependencies are met (oldest first)
+static int issue_tick(jmh_ctx *c) {
+    TickArgs t;
+    memset(&t, 0, sizeof(t));
+    t.W = c->W; t.H = c->H; t.mbw = c->mbw; t.mbh = c->mbh; t.sr = c->sr;
+    t.search_mode = c->cfg.search_mode; t.use_hadamard = c->cfg.use_hadamard; t.restrict_sr = c->cfg.restrict_search_range;
+    for (int i = 0; i < 8; i++) t.inter_search[i] = c->cfg.inter_search[i];
+    t.prof = c->d_prof; t.prof_mb = c->prof_mb;
+    int act[PMAX], nact = 0, nP = 0;
+    const int nf = (int)c->fl.size();
+    std::vector<int> before(nf);
+    for (int i = 0; i < nf; i++) before[i] = c->fl[i].stage = skip_empty(c, c->fl[i].stage);
+    for (int i = 0; i < nf && nact < PMAX; i++) {
+        const Flight &f = c->fl[i];
+        if (f.stage >= c->nd) continue;
+        if (f.pred_id >= 0 && i > 0 && c->fl[i - 1].id == f.pred_id &&
+            before[i - 1] < c->nd && before[i - 1] - f.stage < PIPE_LAG) continue;
+        act[nact++] = i;
+        nP += f.pp.slice_type == JMH_P_SLICE;
+    }
+    // entries: P pictures first (role 2 runs on those only)
+    int k = 0, mbs = 0;
+    for (int pass = 0; pass < 2; pass++)
+        for (int a = 0; a < nact; a++) {
+            Flight &f = c->fl[act[a]];
+            if ((f.pp.slice_type == JMH_P_SLICE) != (pass == 0)) continue;
+            t.p[k] = f.pp;
+            t.p[k].diag = f.stage;
+            t.p[k].y_min = c->dymin[f.stage];
+            t.pre[k] = mbs;
+            mbs += c->dcount[f.stage];
+            k++;
+        }
+    t.npic = k; t.nP = nP; t.pre[k] = mbs;
+    if (nact) {
+        const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
+        if (kt) HCHK(ring_begin(c->ring_an, c->st));
+        HCHK(jmh_launch_analyse(t, c->st));
+        if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
+        HCHK(jmh_launch_final(t, c->st));
+        if (kt) HCHK(ring_end(c->ring_fin, c->st));
+        c->ticks_total++;
+        c->timing.ticks++;
+        c->timing.tick_mbs += mbs;
+        c->timing.mb_launches += 2;
+    }
+    for (int a = 0; a < nact; a++) {
+        Flight &f = c->fl[act[a]];
+        f.started = 1;
+        f.stage = skip_empty(c, f.stage + 1);
+    }
+    while (!c->fl.empty() && skip_empty(c, c->fl.front().stage) >= c->nd) {
+        int r = finish_picture(c, c->fl.front());
+        c->fl.pop_front();
+        if (r) return r;
+    }
+    return JMH_OK;
+}
+
+static bool entry_busy(const jmh_ctx *c, int e) {
+    for (const Flight &f : c->fl)
+        if (f.entry == e || f.ref_entry == e) return true;
+    return false;
+}
+
+// issue ticks while cond() holds, bracketed by one mb-timing event pair
+template <class Cond>
+static int issue_while(jmh_ctx *c, Cond cond) {
+    if (!cond()) return JMH_OK;
+    HCHK(ring_begin(c->ring_mb, c->st));
+    int r = JMH_OK;
+    while (!r && cond()) {
+        if (c->fl.empty()) { r = JMH_E_STATE; break; }   // cannot progress (never expected)
+        r = issue_tick(c);
+    }
+    HCHK(ring_end(c->ring_mb, c->st));
+    return r;
+}
+
+static int drain(jmh_ctx *c) { return issue_while(c, [c] { return !c->fl.empty(); }); }
+
+static const uint8_t *ref_ptr(const jmh_ctx *c) {
+    if (c->ref_kind == REF_REC) return c->ring[c->ref_entry].rec;
+    if (c->ref_kind == REF_DBK) return c->ring[c->ref_entry].dbk;
+    return c->d_ref;
+}
+
+// queue one picture (src: device 4:2:0 picture that stays valid until it is fully issued)
+static int push_picture(jmh_ctx *c, const uint8_t *src, int entry, const jmh_frame_params *fp, bool readback) {
+    const bool p_slice = fp->slice_type == JMH_P_SLICE;
+    PicBuf &b = c->ring[entry];
+    Flight f;
+    memset(&f, 0, sizeof(f));
+    f.id = c->next_id++;
+    f.entry = entry;
+    f.ref_entry = p_slice && (c->ref_kind == REF_REC || c->ref_kind == REF_DBK) ? c->ref_entry : -1;
+    f.pred_id = -1;
+    if (f.ref_entry >= 0)
+        for (const Flight &g : c->fl)
+            if (g.entry == f.ref_entry) f.pred_id = g.id;
+    // the chained predecessor must be the picture right before this one in the flight list
+    if (f.pred_id >= 0 && (c->fl.empty() || c->fl.back().id != f.pred_id)) {
+        int r = drain(c);
+        if (r) return r;
+        f.pred_id = -1;
+    }
+    f.readback = readback;
+    PicParams &q = f.pp;
+    q.org = src; q.ref = ref_ptr(c);
+    q.rec = b.rec; q.dbk = fp->deblock ? b.dbk : nullptr;
+    q.mv = b.mv; q.refidx = b.refidx; q.ipred = b.ipred; q.res = b.res; q.scr = b.scr;
+    q.slice_type = fp->slice_type; q.qp = fp->qp; q.lambda_mode = fp->lambda_mode; q.lambda_motion = fp->lambda_motion;
+    q.cqp_off = fp->chroma_qp_offset;
+    q.lf_disable = fp->lf_disable; q.lf_offA = 2 * fp->lf_alpha_div2; q.lf_offB = 2 * fp->lf_beta_div2;
+    b.unpopped = readback;
+    b.deblocked = fp->deblock != 0;
+    c->fl.push_back(f);
+    c->last_id = f.id;
+    c->last_entry = entry;
+    c->timing.pictures++;
+    const int id = f.id;
+    // run until the new picture has started (older pictures advance up to PIPE_LAG diagonals)
+    return issue_while(c, [c, id] {
+        for (const Flight &g : c->fl)
+            if (g.id == id) return !g.started;
+        return false;
+    });
+}
+
+static int check_params(const jmh_ctx *c, const jmh_frame_params *fp) {
+    if (fp->slice_type != JMH_P_SLICE && fp->slice_type != JMH_I_SLICE) return JMH_E_UNSUPPORTED_CFG;
+    if (fp->qp < 0 || fp->qp > 51 || fp->lambda_mode < 0 || fp->lambda_motion < 0) return JMH_E_INVALID_ARG;
+    if (fp->deblock && (fp->lf_disable < 0 || fp->lf_disable > 2 || fp->lf_alpha_div2 < -6 || fp->lf_alpha_div2 > 6 ||
+                        fp->lf_beta_div2 < -6 || fp->lf_beta_div2 > 6)) return JMH_E_INVALID_ARG;
+    if (fp->slice_type == JMH_P_SLICE && c->ref_kind == REF_NONE) return JMH_E_STATE;
+    return JMH_OK;
+}
+
+// claim the next ring entry: nothing in flight may touch it, its results must have been popped,
+// and a reference that lives in it is copied out first
+static int claim_entry(jmh_ctx *c, int *out) {
+    const int e = c->next_entry;
+    if (c->ring[e].unpopped) return JMH_E_STATE;
+    int r = issue_while(c, [c, e] { return entry_busy(c, e); });
+    if (r) return r;
+    if ((c->ref_kind == REF_REC || c->ref_kind == REF_DBK) && c->ref_entry == e) {
+        if ((r = drain(c))) return r;   // pictures in flight may still read d_ref
+        HCHK(hipMemcpyAsync(c->d_ref, ref_ptr(c), c->fsize, hipMemcpyDeviceToDevice, c->st));
+        c->ref_kind = REF_BUF;
+        c->ref_entry = -1;
+    }
+    c->next_entry = (e + 1) % c->nring;
+    *out = e;
+    return JMH_OK;
+}
+
+extern "C" {
+
+int jmh_set_reference(jmh_ctx *c, int list, int ref_idx, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
+    if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
+    if (list != 0 || ref_idx != 0) return JMH_E_UNSUPPORTED_CFG;
+    HCHK(hipSetDevice(c->dev));
+    int r = drain(c);   // pictures in flight may read d_ref
+    if (r) return r;
+    HCHK(hipStreamSynchronize(c->st));   // staging buffer reuse
+    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc);
+    HCHK(hipMemcpyAsync(c->d_ref, c->h_stage_ref, c->fsize, hipMemcpyHostToDevice, c->st));
+    c->ref_kind = REF_BUF; c->ref_entry = -1;
+    return JMH_OK;
+}
+
+int jmh_set_reference_slot(jmh_ctx *c, int slot) {
+    if (!c || slot < -2 || slot >= c->nslots) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    if (slot < 0) {   // the last pushed picture (its recon, or its device deblocking): no copy
+        if (c->last_id < 0 || (slot == -2 && !c->ring[c->last_entry].deblocked)) return JMH_E_STATE;
+        c->ref_kind = slot == -1 ? REF_REC : REF_DBK;
+        c->ref_entry = c->last_entry;
+        return JMH_OK;
+    }
+    int r = drain(c);
+    if (r) return r;
+    HCHK(hipMemcpyAsync(c->d_ref, c->d_slots + (size_t)slot * c->fsize, c->fsize, hipMemcpyDeviceToDevice, c->st));
+    c->ref_kind = REF_BUF; c->ref_entry = -1;
+    return JMH_OK;
+}
+
+int jmh_frame_push(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc, const jmh_frame_params *fp) {
+    if (!c || !y || !u || !v || !fp || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
+    int r = check_params(c, fp);
+    if (r) return r;
+    if ((int)c->popq.size() >= c->depth) return JMH_E_STATE;
+    HCHK(hipSetDevice(c->dev));
+    int e;
+    if ((r = claim_entry(c, &e))) return r;
+    PicBuf &b = c->ring[e];
+    if ((r = alloc_host(c, b))) return r;
+    HCHK(hipEventSynchronize(b.ev_src));   // the previous H2D out of this staging buffer
+    pack_planes(b.h_src, c->W, c->H, y, u, v, sy, sc);
+    HCHK(hipEventRecord(b.ev_t0, c->st));
+    HCHK(hipMemcpyAsync(b.src, b.h_src, c->fsize, hipMemcpyHostToDevice, c->st));
+    HCHK(hipEventRecord(b.ev_src, c->st));
+    c->popq.push_back(e);
+    return push_picture(c, b.src, e, fp, true);
+}
+
+int jmh_frame_pop(jmh_ctx *c) {
+    if (!c) return JMH_E_INVALID_ARG;
+    if (c->popq.empty()) return JMH_E_STATE;
+    HCHK(hipSetDevice(c->dev));
+    const int e = c->popq.front();
+    int r = issue_while(c, [c, e] {
+        for (const Flight &f : c->fl)
+            if (f.entry == e) return true;
+        return false;
+    });
+    if (r) return r;
+    HCHK(hipEventSynchronize(c->ring[e].ev_done));
+    c->popq.pop_front();
+    c->ring[e].unpopped = 0;
+    c->cur_entry = e;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ring[e].ev_t0, c->ring[e].ev_done) == hipSuccess) c->timing.total_ms = ms;
+    return JMH_OK;
+}
+
+int jmh_frame_submit(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc, const jmh_frame_params *fp) {
+    return jmh_frame_push(c, y, u, v, sy, sc, fp);
+}
+
+int jmh_frame_wait(jmh_ctx *c) { return jmh_frame_pop(c); }
+
+const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *c, int mb_addr) {
+    if (!c || c->cur_entry < 0 || mb_addr < 0 || mb_addr >= c->mbw * c->mbh) return nullptr;
+    return &c->ring[c->cur_entry].h_res[mb_addr];
+}
+
 int jmh_read_recon(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
     if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
-    if (!c->have_results) return JMH_E_STATE;
-    unpack_planes(c->h_rec, c->W, c->H, y, u, v, sy, sc);
+    if (c->cur_entry < 0) return JMH_E_STATE;
+    unpack_planes(c->ring[c->cur_entry].h_rec, c->W, c->H, y, u, v, sy, sc);
     return JMH_OK;
 }
 
 int jmh_read_deblocked(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
     if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
-    if (!c->have_results || !c->dbk_host) return JMH_E_STATE;
-    unpack_planes(c->h_dbk, c->W, c->H, y, u, v, sy, sc);
+    if (c->cur_entry < 0 || !c->ring[c->cur_entry].deblocked) return JMH_E_STATE;
+    unpack_planes(c->ring[c->cur_entry].h_dbk, c->W, c->H, y, u, v, sy, sc);
     return JMH_OK;
 }
 
 int jmh_load_frame(jmh_ctx *c, int slot, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
     if (!c || slot < 0 || slot >= c->nslots || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
+    int r = drain(c);   // pictures in flight may read the slot
+    if (r) return r;
     HCHK(hipStreamSynchronize(c->st));
-    pack_planes(c->h_stage_cur, c->W, c->H, y, u, v, sy, sc);
-    HCHK(hipMemcpyAsync(c->d_slots + (size_t)slot * c->fsize, c->h_stage_cur, c->fsize, hipMemcpyHostToDevice, c->st));
+    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc);
+    HCHK(hipMemcpyAsync(c->d_slots + (size_t)slot * c->fsize, c->h_stage_ref, c->fsize, hipMemcpyHostToDevice, c->st));
     HCHK(hipStreamSynchronize(c->st));
     return JMH_OK;
 }
 
 int jmh_encode_slot(jmh_ctx *c, int slot, const jmh_frame_params *fp) {
     if (!c || !fp || slot < 0 || slot >= c->nslots) return JMH_E_INVALID_ARG;
+    int r = check_params(c, fp);
+    if (r) return r;
     HCHK(hipSetDevice(c->dev));
-    return enqueue_encode(c, c->d_slots + (size_t)slot * c->fsize, fp);
+    int e;
+    if ((r = claim_entry(c, &e))) return r;
+    return push_picture(c, c->d_slots + (size_t)slot * c->fsize, e, fp, false);
 }
 
 int jmh_sync(jmh_ctx *c) {
     if (!c) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
+    int r = drain(c);
+    if (r) return r;
     HCHK(hipStreamSynchronize(c->st));
-    if (c->d_prof) {   // debug: phase timestamps of MB prof_mb from the last picture
+    if (c->d_prof) {   // debug: phase timestamps of MB prof_mb (first picture of a tick)
         unsigned long long h[64];
         int rate_khz = 0;
         HCHK(hipMemcpy(h, c->d_prof, sizeof(h), hipMemcpyDeviceToHost));
@@ -390,16 +618,19 @@ int jmh_sync(jmh_ctx *c) {
 int jmh_get_timing(jmh_ctx *c, jmh_timing *t) {
     if (!c || !t) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
+    int r = drain(c);
+    if (r) return r;
     HCHK(hipStreamSynchronize(c->st));
-    float ms = 0;
+    int npic = 0;
     ring_drain(c->ring_interp, c->timing.interp_ms, c->timing.interps);
-    ring_drain(c->ring_mb, c->timing.mb_ms, c->timing.pictures);
+    ring_drain(c->ring_mb, c->timing.mb_ms, npic);
     if (c->ring_an.cap) {
         ring_drain(c->ring_an, c->timing.analyse_ms, c->timing.analyse_launches);
         ring_drain(c->ring_fin, c->timing.final_ms, c->timing.final_launches);
     }
-    if (c->have_total && hipEventElapsedTime(&ms, c->ev_t0, c->ev_t1) == hipSuccess) c->timing.total_ms = ms;
     *t = c->timing;
+    // counters restart (total_ms stays: the last popped picture)
+    c->timing.pictures = 0; c->timing.mb_launches = 0; c->timing.ticks = 0; c->timing.tick_mbs = 0;
     return JMH_OK;
 }
 
@@ -407,8 +638,10 @@ int jmh_ffs_sad_table(jmh_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t 
     if (!c || n_mb <= 0 || !mb_xy || !centres || !out) return JMH_E_INVALID_ARG;
     for (int i = 0; i < n_mb; i++)
         if (mb_xy[2 * i] < 0 || mb_xy[2 * i] >= c->mbw || mb_xy[2 * i + 1] < 0 || mb_xy[2 * i + 1] >= c->mbh) return JMH_E_INVALID_ARG;
-    if (!c->have_ref) return JMH_E_STATE;
+    if (c->ref_kind == REF_NONE) return JMH_E_STATE;
     HCHK(hipSetDevice(c->dev));
+    int r = drain(c);
+    if (r) return r;
     int32_t *d_xy = nullptr, *d_c = nullptr;
     uint16_t *d_out = nullptr;
     size_t on = (size_t)n_mb * 16 * c->npos;
@@ -417,7 +650,7 @@ int jmh_ffs_sad_table(jmh_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t 
     HCHK(hipMalloc((void **)&d_out, on * 2));
     HCHK(hipMemcpyAsync(d_xy, mb_xy, n_mb * 8, hipMemcpyHostToDevice, c->st));
     HCHK(hipMemcpyAsync(d_c, centres, n_mb * 8, hipMemcpyHostToDevice, c->st));
-    HCHK(jmh_launch_sad_table(c->d_slots, c->d_ref, c->W, c->H, c->sr, n_mb, d_xy, d_c, d_out, c->st));
+    HCHK(jmh_launch_sad_table(c->d_slots, ref_ptr(c), c->W, c->H, c->sr, n_mb, d_xy, d_c, d_out, c->st));
     HCHK(hipMemcpyAsync(out, d_out, on * 2, hipMemcpyDeviceToHost, c->st));
     HCHK(hipStreamSynchronize(c->st));
     HCHK(hipFree(d_xy)); HCHK(hipFree(d_c)); HCHK(hipFree(d_out));
@@ -446,11 +679,16 @@ int jmh_tq4x4_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     return JMH_OK;
 }
 
-/* test seam: quarter-pel planes of the current reference, [16][H+8][W+8] */
+/* test seam: quarter-pel planes of the current reference, [16][H+8][W+8] (UnifiedOneForthPix) */
 int jmh_read_qpel(jmh_ctx *c, uint8_t *out) {
     if (!c || !out) return JMH_E_INVALID_ARG;
-    if (!c->have_ref) return JMH_E_STATE;
+    if (c->ref_kind == REF_NONE) return JMH_E_STATE;
     HCHK(hipSetDevice(c->dev));
+    int r = drain(c);
+    if (r) return r;
+    HCHK(ring_begin(c->ring_interp, c->st));
+    HCHK(jmh_launch_interp(ref_ptr(c), c->W, c->H, c->d_qpel, c->qstride, c->qplane, c->st));
+    HCHK(ring_end(c->ring_interp, c->st));
     HCHK(hipMemcpyAsync(out, c->d_qpel, (size_t)16 * c->qplane, hipMemcpyDeviceToHost, c->st));
     HCHK(hipStreamSynchronize(c->st));
     return JMH_OK;

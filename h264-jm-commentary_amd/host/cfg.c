@@ -58,6 +58,7 @@ static const map_entry Map[] = {
     {"UseConstrainedIntraPred", 0, OFF(constrained_intra), 0, 1},
     {"FrameRate", 0, OFF(frame_rate), 1, 1000},
     {"HIPDevice", 0, OFF(hip_device), 0, 63},
+    {"PipelineDepth", 0, OFF(pipeline_depth), 0, 20},
     {NULL, 0, 0, 0, 0}};
 #undef OFF
 
@@ -198,4 +199,5 @@ void jm_fill_config(const jm_input *inp, jmh_config *cfg) {
     cfg->num_ref_frames = inp->num_ref_frames;
     cfg->constrained_intra_pred = inp->constrained_intra;
     cfg->num_frame_slots = 2;
+    cfg->pipeline_depth = inp->pipeline_depth;
 }

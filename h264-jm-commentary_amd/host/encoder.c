@@ -61,8 +61,17 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     if (!(fout = fopen(inp->outfile, "wb"))) { fprintf(stderr, "Cannot open output file %s\n", inp->outfile); if (fin) fclose(fin); return JMH_E_INVALID_ARG; }
     if (inp->reconfile[0] && !(frec = fopen(inp->reconfile, "wb"))) { fprintf(stderr, "Cannot open recon file %s\n", inp->reconfile); fclose(fout); if (fin) fclose(fin); return JMH_E_INVALID_ARG; }
 
-    jm_pic cur, rec;
-    if (jm_pic_alloc(&cur, W, H) || jm_pic_alloc(&rec, W, H)) return JMH_E_OOM;
+    /* pictures waiting for their results: depth > 1 when the backend pipelines (jmh_frame_push /
+       jmh_frame_pop, lencod.c); their sources stay here for the PSNR */
+    const int dev_dbk = be->read_deblocked && be->reference_deblocked;
+    const int pipelined = dev_dbk && be->push && be->pop && be->depth > 1;
+    const int depth = pipelined ? be->depth : 1;
+    typedef struct { jm_pic cur; jmh_frame_params fp; int f, is_i, frame_num; } pend_t;
+    pend_t *pend = (pend_t *)calloc(depth, sizeof(pend_t));
+    jm_pic rec;
+    int alloc_fail = !pend || jm_pic_alloc(&rec, W, H);
+    for (int k = 0; k < depth && !alloc_fail; k++) alloc_fail = jm_pic_alloc(&pend[k].cur, W, H);
+    if (alloc_fail) return JMH_E_OOM;
     int nmb = s.mbw * s.mbh;
     const jmh_mb_result **res = (const jmh_mb_result **)malloc(sizeof(*res) * nmb);
     jm_bits out, rbsp;
@@ -75,69 +84,103 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     out.len = 0;
     if (log) {
         fprintf(log, "------------------------------- MI355X jm-hot-path lencod (%s) -------------------------------\n", be->name);
+        if (pipelined) fprintf(log, " (%d pictures in flight)\n", depth);
         fprintf(log, " Frame  Bit/pic  QP   SnrY    SnrU    SnrV    Time(ms) MET(ms) Frm/Fld  I D\n");
     }
     double t_start = now_ms();
-    int st_ret = 0, frame_num = 0;
-    for (int f = 0; f < inp->frames; f++) {
+    int st_ret = 0, frame_num = 0, head = 0, count = 0;
+    /* the rest of encode_one_frame for a picture whose macroblock results are available:
+       slice (CAVLC), deblocking / next reference, recon file, PSNR, report line */
+    #define EMIT(P, MET_MS)                                                                          \
+    do {                                                                                           \
+        pend_t *p_ = (P);                                                                          \
+        double t1 = now_ms();                                                                      \
+        for (int a = 0; a < nmb; a++) res[a] = be->mb_result(be->ctx, a);                          \
+        jm_slice sl;                                                                               \
+        sl.idr = p_->f == 0; sl.slice_type = p_->fp.slice_type; sl.frame_num = p_->frame_num;      \
+        sl.poc_lsb = 2 * p_->f; sl.idr_pic_id = 0; sl.qp = p_->fp.qp;                              \
+        jm_bits_init(&rbsp);                                                                       \
+        jm_write_slice(&rbsp, &s, &sl, res);                                                       \
+        jm_write_nal(&out, sl.idr ? 3 : 2, sl.idr ? 5 : 1, &rbsp);                                 \
+        jm_bits_free(&rbsp);                                                                       \
+        double t2 = now_ms();                                                                      \
+        st->entropy_ms += t2 - t1;                                                                 \
+        long pic_bits = out.len * 8;                                                               \
+        fwrite(out.buf, 1, out.len, fout);                                                         \
+        out.len = 0;                                                                               \
+        int r_;                                                                                    \
+        if (dev_dbk) r_ = be->read_deblocked(be->ctx, &rec);                                       \
+        else {                                                                                     \
+            be->read_recon(be->ctx, &rec);                                                         \
+            jm_deblock_picture(&rec, &s, res, p_->fp.qp);                                          \
+            r_ = be->set_reference(be->ctx, &rec);                                                 \
+        }                                                                                          \
+        double t3 = now_ms();                                                                      \
+        st->deblock_ms += t3 - t2;                                                                 \
+        if (r_) { fprintf(stderr, "set_reference failed: %d\n", r_); st_ret = r_; break; }         \
+        if (frec) jm_write_yuv_frame(frec, &rec, inp->width, inp->height);                         \
+        double py = psnr(p_->cur.y, W, rec.y, W, inp->width, inp->height);                         \
+        double pu = psnr(p_->cur.u, W / 2, rec.u, W / 2, inp->width / 2, inp->height / 2);         \
+        double pv = psnr(p_->cur.v, W / 2, rec.v, W / 2, inp->width / 2, inp->height / 2);         \
+        st->psnr_y += py; st->psnr_u += pu; st->psnr_v += pv;                                      \
+        st->bits += pic_bits;                                                                      \
+        st->frames++;                                                                              \
+        if (log)                                                                                   \
+            fprintf(log, "%4d(%s) %8ld   %2d %7.4f %7.4f %7.4f %9.1f %7.1f    FRM\n", p_->f,          \
+                    p_->is_i ? "IDR" : " P ", pic_bits, p_->fp.qp, py, pu, pv, t3 - t1 + (MET_MS), (MET_MS)); \
+    } while (0)
+    for (int f = 0; f < inp->frames && !st_ret; f++) {
+        if (pipelined && count == depth) {   /* the oldest picture's results */
+            double t0 = now_ms();
+            int r = be->pop(be->ctx);
+            double met = now_ms() - t0;
+            if (r) { fprintf(stderr, "hot path backend '%s' failed: status %d\n", be->name, r); st_ret = r; break; }
+            st->me_tq_ms += met;
+            EMIT(&pend[head], met);
+            if (st_ret) break;
+            head = (head + 1) % depth;
+            count--;
+        }
+        pend_t *p = &pend[(head + count) % depth];
         int idx = inp->start_frame + f;
-        if (synthetic) jm_synth_frame(&cur, inp->width, inp->height, seed, idx);
-        else if (jm_read_yuv_frame(fin, &cur, inp->width, inp->height, idx)) { fprintf(stderr, "ReadOneFrame: cannot read frame %d\n", idx); st_ret = JMH_E_INVALID_ARG; break; }
-        int is_i = f == 0 || (inp->intra_period && f % inp->intra_period == 0);
-        jmh_frame_params fp;
-        memset(&fp, 0, sizeof(fp));
-        fp.slice_type = is_i ? JMH_I_SLICE : JMH_P_SLICE;
-        fp.qp = is_i ? inp->qp_i : inp->qp_p;
-        fp.lambda_mode = fp.lambda_motion = jm_lambda_rdo_off(fp.qp);
-        fp.chroma_qp_offset = inp->chroma_qp_offset;
-        const int dev_dbk = be->read_deblocked && be->reference_deblocked;
+        if (synthetic) jm_synth_frame(&p->cur, inp->width, inp->height, seed, idx);
+        else if (jm_read_yuv_frame(fin, &p->cur, inp->width, inp->height, idx)) { fprintf(stderr, "ReadOneFrame: cannot read frame %d\n", idx); st_ret = JMH_E_INVALID_ARG; break; }
+        p->f = f;
+        p->is_i = f == 0 || (inp->intra_period && f % inp->intra_period == 0);
+        p->frame_num = frame_num++;
+        jmh_frame_params *fp = &p->fp;
+        memset(fp, 0, sizeof(*fp));
+        fp->slice_type = p->is_i ? JMH_I_SLICE : JMH_P_SLICE;
+        fp->qp = p->is_i ? inp->qp_i : inp->qp_p;
+        fp->lambda_mode = fp->lambda_motion = jm_lambda_rdo_off(fp->qp);
+        fp->chroma_qp_offset = inp->chroma_qp_offset;
         if (dev_dbk) {   /* same parameters jm_deblock_picture derives from the slice header */
-            fp.deblock = 1;
-            fp.lf_disable = s.lf_params_flag ? s.lf_disable : 0;
-            fp.lf_alpha_div2 = s.lf_params_flag ? s.lf_alpha : 0;
-            fp.lf_beta_div2 = s.lf_params_flag ? s.lf_beta : 0;
+            fp->deblock = 1;
+            fp->lf_disable = s.lf_params_flag ? s.lf_disable : 0;
+            fp->lf_alpha_div2 = s.lf_params_flag ? s.lf_alpha : 0;
+            fp->lf_beta_div2 = s.lf_params_flag ? s.lf_beta : 0;
         }
         double t0 = now_ms();
-        int r = be->encode_frame(be->ctx, &cur, &fp);
-        double t1 = now_ms();
+        int r = 0;
+        if (dev_dbk && !p->is_i) r = be->reference_deblocked(be->ctx);   /* previous picture, on the device */
+        if (!r) r = pipelined ? be->push(be->ctx, &p->cur, fp) : be->encode_frame(be->ctx, &p->cur, fp);
+        double met = now_ms() - t0;
         if (r) { fprintf(stderr, "hot path backend '%s' failed: status %d\n", be->name, r); st_ret = r; break; }
-        st->me_tq_ms += t1 - t0;
-        for (int a = 0; a < nmb; a++) res[a] = be->mb_result(be->ctx, a);
-        jm_slice sl;
-        sl.idr = f == 0; sl.slice_type = fp.slice_type; sl.frame_num = frame_num;
-        sl.poc_lsb = 2 * f; sl.idr_pic_id = 0; sl.qp = fp.qp;
-        jm_bits_init(&rbsp);
-        jm_write_slice(&rbsp, &s, &sl, res);
-        jm_write_nal(&out, sl.idr ? 3 : 2, sl.idr ? 5 : 1, &rbsp);
-        jm_bits_free(&rbsp);
-        double t2 = now_ms();
-        st->entropy_ms += t2 - t1;
-        long pic_bits = out.len * 8;
-        fwrite(out.buf, 1, out.len, fout);
-        out.len = 0;
-        if (dev_dbk) {
-            r = be->read_deblocked(be->ctx, &rec);
-            if (!r) r = be->reference_deblocked(be->ctx);
-        } else {
-            be->read_recon(be->ctx, &rec);
-            jm_deblock_picture(&rec, &s, res, fp.qp);
-            r = be->set_reference(be->ctx, &rec);
-        }
-        double t3 = now_ms();
-        st->deblock_ms += t3 - t2;
-        if (r) { fprintf(stderr, "set_reference failed: %d\n", r); st_ret = r; break; }
-        if (frec) jm_write_yuv_frame(frec, &rec, inp->width, inp->height);
-        double py = psnr(cur.y, W, rec.y, W, inp->width, inp->height);
-        double pu = psnr(cur.u, W / 2, rec.u, W / 2, inp->width / 2, inp->height / 2);
-        double pv = psnr(cur.v, W / 2, rec.v, W / 2, inp->width / 2, inp->height / 2);
-        st->psnr_y += py; st->psnr_u += pu; st->psnr_v += pv;
-        st->bits += pic_bits;
-        st->frames++;
-        frame_num++;
-        if (log)
-            fprintf(log, "%4d(%s) %8ld   %2d %7.4f %7.4f %7.4f %9.1f %7.1f    FRM\n", f, is_i ? "IDR" : " P ",
-                    pic_bits, fp.qp, py, pu, pv, t3 - t0, t1 - t0);
+        st->me_tq_ms += met;
+        if (pipelined) count++;
+        else EMIT(p, met);
     }
+    while (pipelined && count && !st_ret) {
+        double t0 = now_ms();
+        int r = be->pop(be->ctx);
+        double met = now_ms() - t0;
+        if (r) { fprintf(stderr, "hot path backend '%s' failed: status %d\n", be->name, r); st_ret = r; break; }
+        st->me_tq_ms += met;
+        EMIT(&pend[head], met);
+        head = (head + 1) % depth;
+        count--;
+    }
+    #undef EMIT
     st->total_ms = now_ms() - t_start;
     if (st->frames) { st->psnr_y /= st->frames; st->psnr_u /= st->frames; st->psnr_v /= st->frames; }
     if (log && st->frames)
@@ -146,7 +189,9 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
                 st->total_ms / 1e3, st->me_tq_ms / 1e3, st->psnr_y, st->psnr_u, st->psnr_v, st->bits);
     jm_bits_free(&out);
     free(res);
-    jm_pic_free(&cur); jm_pic_free(&rec);
+    for (int k = 0; k < depth; k++) jm_pic_free(&pend[k].cur);
+    free(pend);
+    jm_pic_free(&rec);
     if (fin) fclose(fin);
     fclose(fout);
     if (frec) fclose(frec);

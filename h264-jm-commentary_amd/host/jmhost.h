@@ -46,6 +46,7 @@ typedef struct jm_input {
     int  constrained_intra;    /* UseConstrainedIntraPred                                     */
     int  frame_rate;           /* FrameRate (report only)                                     */
     int  hip_device;           /* (this build) HIP device index                               */
+    int  pipeline_depth;       /* (this build) pictures in flight on the device (0 = auto)   */
     int  verbose;
 } jm_input;
 
@@ -130,6 +131,11 @@ typedef struct jm_backend {
        next reference without a host round trip */
     int (*read_deblocked)(void *ctx, jm_pic *rec);
     int (*reference_deblocked)(void *ctx);
+    /* optional pipelining (NULL / depth <= 1: one picture at a time): push queues a picture,
+       pop waits for the oldest one and makes its results current; up to depth in flight */
+    int (*push)(void *ctx, const jm_pic *cur, const jmh_frame_params *fp);
+    int (*pop)(void *ctx);
+    int depth;
 } jm_backend;
 
 typedef struct jm_stats {

@@ -23,6 +23,10 @@ static int gpu_deblocked(void *ctx, jm_pic *p) {
     return jmh_read_deblocked((jmh_ctx *)ctx, p->y, p->u, p->v, p->w, p->w / 2);
 }
 static int gpu_ref_deblocked(void *ctx) { return jmh_set_reference_slot((jmh_ctx *)ctx, -2); }
+static int gpu_push(void *ctx, const jm_pic *cur, const jmh_frame_params *fp) {
+    return jmh_frame_push((jmh_ctx *)ctx, cur->y, cur->u, cur->v, cur->w, cur->w / 2, fp);
+}
+static int gpu_pop(void *ctx) { return jmh_frame_pop((jmh_ctx *)ctx); }
 
 int main(int argc, char **argv) {
     jm_input inp;
@@ -35,7 +39,7 @@ int main(int argc, char **argv) {
     int r = jmh_create(&cfg, inp.hip_device, &ctx);
     if (r) { fprintf(stderr, "jmh_create failed: %s\n", jmh_strerror(r)); return 2; }
     jm_backend be = {"mi355x-hip", ctx, gpu_set_ref, gpu_encode, gpu_res, gpu_recon, gpu_destroy,
-                     gpu_deblocked, gpu_ref_deblocked};
+                     gpu_deblocked, gpu_ref_deblocked, gpu_push, gpu_pop, jmh_pipeline_depth(ctx)};
     if (getenv("JMH_HOST_DEBLOCK")) be.read_deblocked = NULL, be.reference_deblocked = NULL;
     jm_stats st;
     r = jm_encode_sequence(&inp, &be, &st, stdout);

@@ -17,7 +17,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 3
+JMH_ABI_VERSION = 4
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -36,7 +36,8 @@ class JmhConfig(ctypes.Structure):
                 ("use_hadamard", ctypes.c_int32), ("restrict_search_range", ctypes.c_int32),
                 ("inter_search", ctypes.c_int32 * 8), ("num_ref_frames", ctypes.c_int32),
                 ("constrained_intra_pred", ctypes.c_int32), ("num_frame_slots", ctypes.c_int32),
-                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
+                ("flags", ctypes.c_int32), ("pipeline_depth", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 5)]
 
 
 class JmhFrameParams(ctypes.Structure):
@@ -52,7 +53,8 @@ class JmhTiming(ctypes.Structure):
                 ("total_ms", ctypes.c_float), ("mb_launches", ctypes.c_int32),
                 ("pictures", ctypes.c_int32), ("interps", ctypes.c_int32),
                 ("analyse_ms", ctypes.c_float), ("analyse_launches", ctypes.c_int32),
-                ("final_ms", ctypes.c_float), ("final_launches", ctypes.c_int32)]
+                ("final_ms", ctypes.c_float), ("final_launches", ctypes.c_int32),
+                ("ticks", ctypes.c_int32), ("tick_mbs", ctypes.c_int32)]
 
 
 # jmh_mb_result, field for field (include/jmhip.h)
@@ -74,6 +76,9 @@ _SIGS = {
     "jmh_set_reference": (_I, [_P, _I, _I, _P, _P, _P, _I, _I]),
     "jmh_frame_submit": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(JmhFrameParams)]),
     "jmh_frame_wait": (_I, [_P]),
+    "jmh_frame_push": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(JmhFrameParams)]),
+    "jmh_frame_pop": (_I, [_P]),
+    "jmh_pipeline_depth": (_I, [_P]),
     "jmh_get_mb_result": (_P, [_P, _I]),
     "jmh_read_recon": (_I, [_P, _P, _P, _P, _I, _I]),
     "jmh_read_deblocked": (_I, [_P, _P, _P, _P, _I, _I]),
@@ -125,7 +130,8 @@ def _ptr(a):
 
 
 def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
-                restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False):
+                restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False,
+                pipeline_depth=0):
     cfg = JmhConfig()
     cfg.width, cfg.height = width, height
     cfg.search_range, cfg.search_mode = search_range, search_mode
@@ -134,6 +140,7 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
         cfg.inter_search[i + 1] = v
     cfg.num_ref_frames, cfg.constrained_intra_pred, cfg.num_frame_slots = 1, 0, slots
     cfg.flags = JMH_FLAG_KERNEL_TIMING if kernel_timing else 0
+    cfg.pipeline_depth = pipeline_depth
     return cfg
 
 
@@ -191,6 +198,21 @@ class Encoder:
                                          ctypes.byref(fp)), "jmh_frame_submit")
         _check(self.lib.jmh_frame_wait(self.ctx), "jmh_frame_wait")
         return self.results(), self.recon()
+
+    # ---- pipelined pictures (jmh_frame_push / jmh_frame_pop) ----
+    def push(self, y, u, v, slice_type, qp, chroma_qp_offset=0, deblock=None):
+        fp = frame_params(slice_type, qp, chroma_qp_offset, deblock)
+        _check(self.lib.jmh_frame_push(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2,
+                                       ctypes.byref(fp)), "jmh_frame_push")
+
+    def pop(self):
+        """Wait for the oldest pushed picture; returns (results, recon)."""
+        _check(self.lib.jmh_frame_pop(self.ctx), "jmh_frame_pop")
+        return self.results(), self.recon()
+
+    @property
+    def depth(self):
+        return self.lib.jmh_pipeline_depth(self.ctx)
 
     def results(self):
         n = self.mbw * self.mbh

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 3
+#define JMH_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define JMH_OK                 0
@@ -80,7 +80,9 @@ typedef struct jmh_config {
     int32_t constrained_intra_pred; /* UseConstrainedIntraPred (this build: 0)                    */
     int32_t num_frame_slots;        /* device-resident input frame slots (bench / pipelining)     */
     int32_t flags;                  /* JMH_FLAG_* (0 for the defaults)                            */
-    int32_t reserved[6];
+    int32_t pipeline_depth;         /* pictures in flight at once (0: enough to fill the device,  */
+                                    /*   1: one picture at a time); see jmh_frame_push            */
+    int32_t reserved[5];
 } jmh_config;
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */
@@ -135,6 +137,9 @@ typedef struct jmh_timing {
     int32_t analyse_launches;  /*   ... and the number of launches summed                       */
     float final_ms;            /* JMH_FLAG_KERNEL_TIMING: sum of k_mb_final launch durations    */
     int32_t final_launches;
+    int32_t ticks;             /* wavefront ticks (one k_mb_analyse + one k_mb_final each; a tick
+                                  runs one diagonal of every picture in flight)                   */
+    int32_t tick_mbs;          /* macroblocks processed by those ticks                          */
 } jmh_timing;
 
 typedef struct jmh_ctx jmh_ctx;
@@ -155,10 +160,22 @@ int  jmh_set_reference(jmh_ctx *ctx, int list, int ref_idx,
 /* ---- one picture of encode_one_macroblock() calls ----------------------------------------
  * The caller's planes must stay valid until jmh_frame_submit returns (copied to the device).
  * Results and recon become host-visible after jmh_frame_wait; pointers returned by
- * jmh_get_mb_result stay valid until the next submit.                                           */
+ * jmh_get_mb_result stay valid until the next submit / pop.                                     */
 int  jmh_frame_submit(jmh_ctx *ctx, const uint8_t *y, const uint8_t *u, const uint8_t *v,
                       int stride_y, int stride_c, const jmh_frame_params *fp);
 int  jmh_frame_wait(jmh_ctx *ctx);
+/* ---- pipelined pictures (the frame loop of lencod.c › main with pictures in flight) --------
+ * jmh_frame_push queues a picture against the current reference and returns at once; a P
+ * picture whose reference is the previous picture (jmh_set_reference_slot -1 / -2) runs each
+ * wavefront diagonal d once that picture has finished diagonal d + PIPE_LAG (jmh_device.h), so
+ * up to jmh_pipeline_depth() pictures share every launch.  jmh_frame_pop waits for the oldest
+ * pushed picture; jmh_get_mb_result / jmh_read_recon / jmh_read_deblocked then return its
+ * results (submit == push, wait == pop).  Results are identical to one picture at a time.
+ * Push returns JMH_E_STATE when jmh_pipeline_depth() pictures are waiting to be popped.       */
+int  jmh_frame_push(jmh_ctx *ctx, const uint8_t *y, const uint8_t *u, const uint8_t *v,
+                    int stride_y, int stride_c, const jmh_frame_params *fp);
+int  jmh_frame_pop(jmh_ctx *ctx);
+int  jmh_pipeline_depth(const jmh_ctx *ctx);
 const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *ctx, int mb_addr);
 int  jmh_read_recon(jmh_ctx *ctx, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y, int stride_c);
 /* the deblocked picture of the last jmh_frame_submit with deblock = 1 (replaces DeblockFrame)  */
@@ -169,7 +186,7 @@ int  jmh_load_frame(jmh_ctx *ctx, int slot, const uint8_t *y, const uint8_t *u, 
                     int stride_y, int stride_c);
 int  jmh_set_reference_slot(jmh_ctx *ctx, int slot);   /* slot -1: the last picture's recon,    */
                                                          /* -2: its device deblocking (deblock=1) */
-int  jmh_encode_slot(jmh_ctx *ctx, int slot, const jmh_frame_params *fp); /* async, no D2H    */
+int  jmh_encode_slot(jmh_ctx *ctx, int slot, const jmh_frame_params *fp); /* pipelined, no D2H */
 int  jmh_sync(jmh_ctx *ctx);
 int  jmh_get_timing(jmh_ctx *ctx, jmh_timing *t);
 

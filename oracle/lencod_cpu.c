@@ -26,7 +26,7 @@ int main(int argc, char **argv) {
     jmo_ctx *ctx = NULL;
     int r = jmo_create(&cfg, &ctx);
     if (r) { fprintf(stderr, "jmo_create failed: %d\n", r); return 2; }
-    jm_backend be = {"cpu-oracle", ctx, o_set_ref, o_encode, o_res, o_recon, o_destroy, NULL, NULL};
+    jm_backend be = {"cpu-oracle", ctx, o_set_ref, o_encode, o_res, o_recon, o_destroy, NULL, NULL, NULL, NULL, 1};
     jm_stats st;
     r = jm_encode_sequence(&inp, &be, &st, stdout);
     double mp = (double)inp.width * inp.height * st.frames / 1e6;

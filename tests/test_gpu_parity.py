@@ -170,8 +170,9 @@ def test_saturated_frames():
 
 
 def test_device_resident_deblocked_reference():
-    """f2: the slot path (encode_slot with the fused loop filter, set_reference_slot(-2) swaps the
-    deblocked picture in as reference) == the host-copy path (encode, read_deblocked, set_reference)."""
+    """f2: the slot path (encode_slot with the fused loop filter, set_reference_slot(-2) makes the
+    deblocked picture the reference on the device) == the host-copy path (encode, read_deblocked,
+    set_reference)."""
     w, h, qp, dbk = 96, 64, 30, (0, 1, -2)
     pics = synth_seq(w, h, 4, 11)
     a = jmhip.Encoder(w, h, search_range=8, slots=3)
@@ -192,9 +193,87 @@ def test_device_resident_deblocked_reference():
     assert_same(ares, arec, bres, brec, w // 16)
     for x, y in zip(adbk, b.deblocked()):
         assert np.array_equal(x, y)
-    with pytest.raises(jmhip.JmhError):   # the swap consumed the deblocked picture
+    a.encode_slot(1, jmhip.JMH_P_SLICE, qp)   # no loop filter: no deblocked picture to reference
+    with pytest.raises(jmhip.JmhError):
         a.set_reference_slot(-2)
-        a.set_reference_slot(-2)
+
+
+# ---------------- pipelined pictures (several pictures per wavefront tick) ----------------
+def moving_seq(w, h, n, seed, step=(37, -29)):
+    """Smooth random texture under large global motion (MVs near the window edge) plus noise."""
+    rng = np.random.default_rng(seed)
+    big = rand_picture(rng, w + abs(step[0]) * n + 64, h + abs(step[1]) * n + 64)[0]
+    pics = []
+    for i in range(n):
+        x0 = 32 + (i * step[0] if step[0] >= 0 else (n - i) * -step[0])
+        y0 = 32 + (i * step[1] if step[1] >= 0 else (n - i) * -step[1])
+        y = big[y0:y0 + h, x0:x0 + w].copy()
+        y = np.clip(y.astype(np.int16) + rng.integers(-6, 7, y.shape), 0, 255).astype(np.uint8)
+        u = np.ascontiguousarray(y[::2, ::2] // 2 + 40)
+        v = np.ascontiguousarray(255 - y[1::2, 1::2])
+        pics.append((np.ascontiguousarray(y), u, v))
+    return pics
+
+
+def run_chain(enc, pics, qp, dbk, pipelined):
+    """IPPP chain, each P referencing the previous picture's device deblocking."""
+    out, pending = [], 0
+    for i, pic in enumerate(pics):
+        st = jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE
+        if i:
+            enc.set_reference_slot(-2)
+        if pipelined:
+            if pending == enc.depth:
+                out.append(enc.pop() + (enc.deblocked(),))
+                pending -= 1
+            enc.push(*pic, st, qp, deblock=dbk)
+            pending += 1
+        else:
+            out.append(enc.encode(*pic, st, qp, deblock=dbk) + (enc.deblocked(),))
+    for _ in range(pending):
+        out.append(enc.pop() + (enc.deblocked(),))
+    return out
+
+
+@pytest.mark.parametrize("w,h,sr,n", [(176, 144, 16, 9), (320, 240, 32, 8), (1920, 1088, 32, 20)])
+def test_pipelined_chain_equals_sequential(w, h, sr, n):
+    """Pictures in flight together (lag PIPE_LAG diagonals) == one picture at a time, bit for
+    bit, under motion that pushes MVs to the search-window edge."""
+    pics = moving_seq(w, h, n, seed=w + n)
+    dbk = (0, 0, 0)
+    a = jmhip.Encoder(w, h, search_range=sr)                       # auto depth
+    b = jmhip.Encoder(w, h, search_range=sr, pipeline_depth=1)
+    assert a.depth > 1 and b.depth == 1
+    ra = run_chain(a, pics, 30, dbk, True)
+    rb = run_chain(b, pics, 30, dbk, False)
+    assert len(ra) == len(rb) == n
+    for (gres, grec, gdbk), (ores, orec, odbk) in zip(ra, rb):
+        assert_same(gres, grec, ores, orec, w // 16)
+        for x, y in zip(gdbk, odbk):
+            assert np.array_equal(x, y)
+    assert any((r["mb_type"] != 0).any() for r, _, _ in ra[1:])
+
+
+def test_pipelined_slots_equal_sequential():
+    """bench.py's path: encode_slot chain (no readback) pipelined == depth 1 (checked through the
+    reference it leaves for a final read-back picture)."""
+    w, h = 352, 288
+    pics = moving_seq(w, h, 4, seed=5, step=(-21, 13))
+    res = []
+    for depth in (0, 1):
+        e = jmhip.Encoder(w, h, search_range=32, slots=3, pipeline_depth=depth)
+        for i in range(3):
+            e.load_frame(i, *pics[i])
+        e.encode_slot(0, jmhip.JMH_I_SLICE, 28, deblock=(0, 0, 0))
+        for k in range(11):
+            e.set_reference_slot(-2)
+            e.encode_slot(1 + k % 2, jmhip.JMH_P_SLICE, 28, deblock=(0, 0, 0))
+        e.set_reference_slot(-2)
+        res.append(e.encode(*pics[3], jmhip.JMH_P_SLICE, 28, deblock=(0, 0, 0)) + (e.deblocked(),))
+    (gres, grec, gd), (ores, orec, od) = res
+    assert_same(gres, grec, ores, orec, w // 16)
+    for x, y in zip(gd, od):
+        assert np.array_equal(x, y)
 
 
 # ---------------- end to end: lencod bitstream + recon, closed loop ----------------
@@ -215,6 +294,8 @@ def run_lencod(binary, out_dir, extra):
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=2", "LoopFilterBetaOffset=-1"],
     ["InputFile=synthetic:4", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=8",
      "LoopFilterParametersFlag=1", "LoopFilterDisable=1"],
+    ["InputFile=synthetic:6", "FramesToBeEncoded=5", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "PipelineDepth=1"],
     ["InputFile=synthetic:5", "FramesToBeEncoded=4", "SourceWidth=320", "SourceHeight=240", "SearchRange=16",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=6", "LoopFilterBetaOffset=6", "QPFirstFrame=40",
      "QPRemainingFrame=44"],
@@ -234,7 +315,7 @@ def test_lencod_bitstream_identical(extra):
 @pytest.mark.slow
 def test_1080p_closed_loop_gpu():
     """Full config-2 size: GPU bitstream decodes to exactly the GPU reconstruction."""
-    extra = ["InputFile=synthetic:0", "FramesToBeEncoded=3", "SourceWidth=1920", "SourceHeight=1080", "SearchRange=32"]
+    extra = ["InputFile=synthetic:0", "FramesToBeEncoded=6", "SourceWidth=1920", "SourceHeight=1080", "SearchRange=32"]
     with tempfile.TemporaryDirectory() as a:
         run_lencod(LENCOD, a, extra)
         r = subprocess.run([JMDEC, f"{a}/a.264", f"{a}/dec.yuv"], capture_output=True, text=True, timeout=600)

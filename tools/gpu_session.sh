@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 timeout -k 10 900 python -m pytest tests -x -q -m gpu -p no:cacheprovider "$@" > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -25 gpurun_out/${TAG}_pytest.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/${TAG}_bench.log 2>&1
+timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/${TAG}_bench.log
 [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
