@@ -21,10 +21,12 @@
 // Motion search data path per ME workgroup:
 //   * 88x88 reference window (+4 margin for the 6-tap filter) and its b, h, j half-pel planes in
 //     LDS, computed once per MB (SubPelBlockMotionSearch reads only LDS);
-//   * the 16 4x4 SADs of every integer position (SetupFastFullPelSearch) in REGISTERS: each
-//     thread owns a column strip of 10 positions, accumulates v_sad_u8 over 4 bands of 13 window
-//     rows and keeps 10 x 8 packed u16 pairs; a search of any partition reduces them with plain 32-bit adds
-//     of packed pairs (no carries: a half never exceeds 8 x 4080);
+//   * SetupFastFullPelSearch's SADs of every integer position in REGISTERS, only those the role's
+//     next searches read: each thread owns a column strip of NPK positions and keeps 2 packed u16
+//     pairs per position -- role 1 the four 8x8 SADs (16x16 / 16x8 / 8x16 are sums of them), role
+//     2 the four 4x4 SADs of the 8x8 block it is searching (recomputed per 8x8 block).  Any
+//     partition reduces with plain 32-bit adds of packed pairs (no carries: a half never exceeds
+//     2 x 16320).  The small table keeps the workgroup under 128 VGPRs (two per CU);
 //   * cost = SAD + lambda*(mvbits(x) + mvbits(y)) from two per-search LDS tables, key =
 //     cost << 13 | JM order (0 for the (0,0) pre-check, else spiral index + 1), DPP wave min;
 //   * sub-pel SATD: one 4x4 sub-block per 16-lane row, DPP Hadamard, LDS-atomic candidate sums.
@@ -134,24 +136,24 @@ struct NbMe {
     }
 };
 
-// SAD of partition (BT, BX, BY) from the 8 packed pair registers of one position
-// (register 2*by + bx/2 holds 4x4 blocks (bx, by) low and (bx+1, by) high, bx even)
+// SAD of partition (BT, BX, BY) from the 2 packed pair registers of one position.
+// Role 1: r[h] = 8x8 blocks (0, h) low, (1, h) high.  Role 2 (8x8 block at 4x4 coords X, Y even):
+// r[ly] = 4x4 blocks (X, Y + ly) low, (X + 1, Y + ly) high.
 template <int BT, int BX, int BY>
-__device__ __forceinline__ unsigned psum(const uint32_t (&r)[8]) {
+__device__ __forceinline__ unsigned psum(const uint32_t (&r)[2]) {
     uint32_t v;
-    if constexpr (BT == 1) v = r[0] + r[1] + r[2] + r[3] + r[4] + r[5] + r[6] + r[7];
-    else if constexpr (BT == 2) v = r[2 * BY] + r[2 * BY + 1] + r[2 * BY + 2] + r[2 * BY + 3];
-    else if constexpr (BT == 3) v = r[BX / 2] + r[2 + BX / 2] + r[4 + BX / 2] + r[6 + BX / 2];
-    else if constexpr (BT == 4) v = r[2 * BY + BX / 2] + r[2 * BY + 2 + BX / 2];
-    else if constexpr (BT == 5) v = r[2 * BY + BX / 2];
-    else if constexpr (BT == 6) { v = r[2 * BY + BX / 2] + r[2 * BY + 2 + BX / 2]; return (BX & 1) ? v >> 16 : v & 0xFFFFu; }
-    else { v = r[2 * BY + BX / 2]; return (BX & 1) ? v >> 16 : v & 0xFFFFu; }
+    if constexpr (BT == 1 || BT == 4) v = r[0] + r[1];
+    else if constexpr (BT == 2) v = r[BY >> 1];
+    else if constexpr (BT == 5) v = r[BY & 1];
+    else if constexpr (BT == 3) { v = r[0] + r[1]; return (BX >> 1) ? v >> 16 : v & 0xFFFFu; }
+    else if constexpr (BT == 6) { v = r[0] + r[1]; return (BX & 1) ? v >> 16 : v & 0xFFFFu; }
+    else { v = r[BY & 1]; return (BX & 1) ? v >> 16 : v & 0xFFFFu; }
     return (v & 0xFFFFu) + (v >> 16);
 }
 
 // per-thread search state: SADs of the thread's NPK positions and their JM order keys
 struct PosState {
-    uint32_t sadp[NPK][8];
+    uint32_t sadp[NPK][2];
     uint32_t ordk[NPK];      // JM order (0 = (0,0) pre-check); 0xFFFFFFFF for slots outside the table
     int dx, dy0;
 };
@@ -162,7 +164,7 @@ __device__ __forceinline__ void fence_state(PosState &ps) {
 #pragma unroll
     for (int k = 0; k < NPK; k++) {
 #pragma unroll
-        for (int q = 0; q < 8; q++) asm volatile("" : "+v"(ps.sadp[k][q]));
+        for (int q = 0; q < 2; q++) asm volatile("" : "+v"(ps.sadp[k][q]));
         asm volatile("" : "+v"(ps.ordk[k]));
     }
 }
@@ -311,12 +313,49 @@ __device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, const Tea
 
 #define EVAL(J, BT, BX, BY) bk[J] = eval_search<J, BT, BX, BY>(s, ps, sr, search_range(d, BT))
 
-// one 8x8 block of P8x8: 4 stages (sub-modes 4..7 in parallel, then the 4x4 chain), then the
-// P8x8 sub-mode decision for the block and the reset of its stored MVs (via best8x8)
+// SADs at this thread's NPK positions (column strip dx, rows dy0..dy0+NPK-1 of the window) of the
+// 8x8 org block at pixel (OX, OY).  EIGHT: the 8x8 SAD into half HI of ps.sadp[k][SLOT] (role 1);
+// else the four 4x4 SADs, rows 0..3 into ps.sadp[k][0] and 4..7 into [1] (role 2).  One 8-pixel
+// column at a time keeps the unrolled window rows (3 dwords each) within the register budget.
+template <bool EIGHT, int OX, int OY, int SLOT, int HI>
+__device__ __forceinline__ void sad_strip(const MeS &s, PosState &ps) {
+    const int wx = ps.dx + WM + OX;
+    const uint32_t sel = wx & 3;
+    const uint8_t *wb = s.planes + (ps.dy0 + WM + OY) * WST + (wx & ~3);
+    uint32_t acc[NPK][2];
+#pragma unroll
+    for (int k = 0; k < NPK; k++) acc[k][0] = acc[k][1] = 0;
+#pragma unroll
+    for (int r = 0; r < 8 + NPK - 1; r++) {
+        const uint32_t *w32 = reinterpret_cast<const uint32_t *>(wb + r * WST);
+        const uint32_t a0 = w32[0], a1 = w32[1], a2 = w32[2];
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sel), w1 = __builtin_amdgcn_alignbyte(a2, a1, sel);
+#pragma unroll
+        for (int k = 0; k < NPK; k++) {
+            const int mr = r - k;
+            if (mr < 0 || mr > 7) continue;
+            const uint2 o = *reinterpret_cast<const uint2 *>(s.org + (OY + mr) * 16 + OX);
+            if constexpr (EIGHT) {
+                acc[k][0] = __builtin_amdgcn_sad_u8(w1, o.y, __builtin_amdgcn_sad_u8(w0, o.x, acc[k][0]));
+                if (mr == 7) ps.sadp[k][SLOT] = HI ? (ps.sadp[k][SLOT] | (acc[k][0] << 16)) : acc[k][0];
+            } else {
+                acc[k][0] = __builtin_amdgcn_sad_u8(w0, o.x, acc[k][0]);
+                acc[k][1] = __builtin_amdgcn_sad_u8(w1, o.y, acc[k][1]);
+                if ((mr & 3) == 3) {
+                    ps.sadp[k][mr >> 2] = acc[k][0] | (acc[k][1] << 16);
+                    acc[k][0] = acc[k][1] = 0;
+                }
+            }
+        }
+    }
+}
+
 template <int B8>
 __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int scx, int scy, int &best8x8, int &cost8x8) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
     const int tid = threadIdx.x, sr = d.sr;
+    fence_state(ps);
+    sad_strip<false, 4 * X, 4 * Y, 0, 0>(s, ps);        // the four 4x4 SADs of this 8x8 block
     const Team t4{true, tid >> 7, tid & 127, 128};       // four searches: 128 threads each
     const Team t1{true, 3, tid, NTA};                    // one search: the whole workgroup
     unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
@@ -461,44 +500,20 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
     __syncthreads();
     PSTAMP(pb + 1);
     if (slice_p) {
-        // ---- 16 4x4 SADs for this thread's column strip of NPK positions (registers)
+        // ---- this thread's column strip of NPK positions: SADs (registers) and JM order keys
         PosState ps;
         const int nstrips = (side + NPK - 1) / NPK;
         const bool sact = tid < side * nstrips;
         ps.dx = sact ? tid % side : 0;
         ps.dy0 = sact ? (tid / side) * NPK : 0;
-        {
-            const uint4 *og = reinterpret_cast<const uint4 *>(s.org);   // LDS broadcast, one MB row per read
-            uint32_t acc[NPK][4];
-#pragma unroll
-            for (int k = 0; k < NPK; k++)
-#pragma unroll
-                for (int b = 0; b < 4; b++) acc[k][b] = 0;
-            const int wx = ps.dx + WM;
-            const uint32_t sel = wx & 3;
-            const uint8_t *wb = G + (ps.dy0 + WM) * WST + (wx & ~3);
-#pragma unroll
-            for (int r = 0; r < 16 + NPK - 1; r++) {
-                const uint32_t *w32 = reinterpret_cast<const uint32_t *>(wb + r * WST);
-                const uint32_t a0 = w32[0], a1 = w32[1], a2 = w32[2], a3 = w32[3], a4 = w32[4];
-                const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sel), w1 = __builtin_amdgcn_alignbyte(a2, a1, sel);
-                const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sel), w3 = __builtin_amdgcn_alignbyte(a4, a3, sel);
-#pragma unroll
-                for (int k = 0; k < NPK; k++) {
-                    const int mr = r - k;
-                    if (mr < 0 || mr > 15) continue;
-                    const uint4 o = og[mr];
-                    acc[k][0] = __builtin_amdgcn_sad_u8(w0, o.x, acc[k][0]);
-                    acc[k][1] = __builtin_amdgcn_sad_u8(w1, o.y, acc[k][1]);
-                    acc[k][2] = __builtin_amdgcn_sad_u8(w2, o.z, acc[k][2]);
-                    acc[k][3] = __builtin_amdgcn_sad_u8(w3, o.w, acc[k][3]);
-                    if ((mr & 3) == 3) {
-                        ps.sadp[k][2 * (mr >> 2)] = acc[k][0] | (acc[k][1] << 16);
-                        ps.sadp[k][2 * (mr >> 2) + 1] = acc[k][2] | (acc[k][3] << 16);
-                        acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
-                    }
-                }
-            }
+        if constexpr (ROLE == 1) {   // the four 8x8 SADs
+            sad_strip<true, 0, 0, 0, 0>(s, ps);
+            fence_state(ps);
+            sad_strip<true, 8, 0, 0, 1>(s, ps);
+            fence_state(ps);
+            sad_strip<true, 0, 8, 1, 0>(s, ps);
+            fence_state(ps);
+            sad_strip<true, 8, 8, 1, 1>(s, ps);
         }
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
@@ -717,7 +732,7 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     PSTAMP(13);
 }
 
-__global__ __launch_bounds__(NTA) void k_mb_analyse(const TickArgs t) {
+__global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     __shared__ AnalyseS s;
     // blocks: [0, nPm) role 2 of the P pictures' MBs (longest, dispatched first), then role 1 and
     // role 0 over every picture's MBs (an I picture runs roles 0 and 1 only)
@@ -727,9 +742,26 @@ __global__ __launch_bounds__(NTA) void k_mb_analyse(const TickArgs t) {
     const int e = tick_entry(t, idx);
     const DevParams d = tick_params(t, e);
     const int mby = d.y_min + (idx - t.pre[e]), mbx = d.diag - 2 * mby;
+    const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
+#ifndef ONLY_ROLE
     if (role == 2) me_role<2>(d, s.me, mbx, mby);
     else if (role == 1) me_role<1>(d, s.me, mbx, mby);
     else intra_role(d, s.in, mbx, mby);
+#elif ONLY_ROLE == 2
+    me_role<2>(d, s.me, mbx, mby);
+#elif ONLY_ROLE == 1
+    me_role<1>(d, s.me, mbx, mby);
+#else
+    intra_role(d, s.in, mbx, mby);
+#endif
+    if (t.bprof) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            t.bprof[3 * b] = t0;
+            t.bprof[3 * b + 1] = wall_clock64();
+            t.bprof[3 * b + 2] = role;
+        }
+    }
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {

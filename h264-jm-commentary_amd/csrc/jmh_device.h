@@ -72,6 +72,7 @@ struct TickArgs {
     int inter_search[8];
     unsigned long long *prof;
     int prof_mb;
+    unsigned long long *bprof;           // debug (JMH_BLOCK_PROF): per-block start / end / role
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
     PicParams p[PMAX];

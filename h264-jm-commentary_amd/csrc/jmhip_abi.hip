@@ -119,6 +119,8 @@ struct jmh_ctx {
     int cur_entry;                       // results visible through get_mb_result / read_*
     unsigned long long *d_prof;          // JMH_PHASE_PROF=<mb>: per-phase wall clock of one MB
     int prof_mb;
+    unsigned long long *d_bprof;         // JMH_BLOCK_PROF=<tick>: k_mb_analyse block start/end/role
+    int bprof_tick, bprof_blocks;
     uint8_t *h_stage_ref;
     EvRing ring_interp, ring_mb, ring_an, ring_fin;   // ring_an / ring_fin: JMH_FLAG_KERNEL_TIMING
     jmh_timing timing;
@@ -199,7 +201,7 @@ void jmh_destroy(jmh_ctx *c) {
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     for (PicBuf &b : c->ring) free_entry(b);
-    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof};
+    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     ring_free(c->ring_interp);
@@ -253,6 +255,11 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         for (PicBuf &b : c->ring) {
             if ((st = alloc_entry(c, b))) goto fail;
             if (hipEventRecord(b.ev_src, c->st) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        }
+        c->bprof_tick = -1;
+        if (const char *e = getenv("JMH_BLOCK_PROF")) {
+            c->bprof_tick = atoi(e);
+            ALLOC(c->d_bprof, (size_t)3 * 3 * PMAX * c->mbh * sizeof(unsigned long long));
         }
         if (const char *e = getenv("JMH_PHASE_PROF")) {
             c->prof_mb = atoi(e);
@@ -354,6 +361,10 @@ static int issue_tick(jmh_ctx *c) {
             k++;
         }
     t.npic = k; t.nP = nP; t.pre[k] = mbs;
+    if (c->d_bprof && c->ticks_total == c->bprof_tick) {
+        t.bprof = c->d_bprof;
+        c->bprof_blocks = t.pre[nP] + 2 * t.pre[k];
+    }
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
         if (kt) HCHK(ring_begin(c->ring_an, c->st));
@@ -599,6 +610,29 @@ int jmh_sync(jmh_ctx *c) {
     int r = drain(c);
     if (r) return r;
     HCHK(hipStreamSynchronize(c->st));
+    if (c->d_bprof && c->bprof_blocks) {   // debug: block durations of one tick, per role
+        std::vector<unsigned long long> h(3 * c->bprof_blocks);
+        HCHK(hipMemcpy(h.data(), c->d_bprof, h.size() * 8, hipMemcpyDeviceToHost));
+        int rate_khz = 0;
+        HCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->dev));
+        double us = rate_khz > 0 ? 1e3 / rate_khz : 0.01;
+        unsigned long long t0 = ~0ull, t1 = 0;
+        double sum[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
+        int n[3] = {0, 0, 0};
+        for (int i = 0; i < c->bprof_blocks; i++) {
+            unsigned long long a = h[3 * i], b = h[3 * i + 1];
+            int role = (int)h[3 * i + 2];
+            if (role < 0 || role > 2 || b < a) continue;
+            t0 = a < t0 ? a : t0; t1 = b > t1 ? b : t1;
+            double dur = (double)(b - a) * us;
+            sum[role] += dur; n[role]++; mx[role] = dur > mx[role] ? dur : mx[role];
+        }
+        fprintf(stderr, "jmh_blocks tick=%d blocks=%d span=%.1fus", c->bprof_tick, c->bprof_blocks, (double)(t1 - t0) * us);
+        for (int r = 0; r < 3; r++)
+            fprintf(stderr, " role%d: n=%d mean=%.1fus max=%.1fus", r, n[r], n[r] ? sum[r] / n[r] : 0.0, mx[r]);
+        fprintf(stderr, "\n");
+        c->bprof_blocks = 0;
+    }
     if (c->d_prof) {   // debug: phase timestamps of MB prof_mb (first picture of a tick)
         unsigned long long h[64];
         int rate_khz = 0;
