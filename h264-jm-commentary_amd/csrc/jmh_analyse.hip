@@ -5,7 +5,7 @@
 //   role 2  P8x8 motion search: 4 x (8x8, 2x 8x4, 2x 4x8, 4x 4x4) = 36 BlockMotionSearch calls
 //   role 1  16x16, 16x8, 8x16 motion search (5 calls) + FindSkipModeMotionVector, then the
 //           Intra16x16 and chroma intra-mode decisions (I slices: only the latter)
-//   role 0  Intra4x4 decision with its reconstruction
+//   role 0  Intra4x4 decision with its reconstruction: four MBs per workgroup, two waves each
 //
 // JM runs the 41 searches of a P macroblock one after another. The only coupling between them is
 // the motion vector predictor, which reads MVs already stored inside the MB. Enumerating those
@@ -82,7 +82,7 @@ struct IntraS {
 };
 union AnalyseS {
     MeS me;
-    IntraS in;
+    IntraS in[4];
 };
 
 __device__ __forceinline__ void sstamp(MeS &s) {
@@ -461,29 +461,23 @@ __device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraN
 }
 
 // ======================================================================================
-//  role 1 / role 2: motion search
+//  motion search of one P macroblock (all 41 searches)
 // ======================================================================================
-template <int ROLE>
-__device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int mby) {
+__device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int mby) {
     const int tid = threadIdx.x;
     const int W = d.W, sr = d.sr, side = d.side;
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
-    const bool slice_p = d.slice_type == JMH_P_SLICE;
-    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0;
     const bool prof = prof_mb_here(d, mbx, mby);
-    const int pb = ROLE == 2 ? 0 : 8;
-    PSTAMP(pb);
+    PSTAMP(0);
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
-    if (tid == 0) { s.pst = (prof && ROLE == 2) ? d.prof + 20 : nullptr; s.pn = 0; }
+    if (tid == 0) { s.pst = prof ? d.prof + 20 : nullptr; s.pn = 0; }
     if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    else if (ROLE == 1 && tid < 384) load_orgc(d, s.nb, tid - 256, mbx, mby);
     else if (tid >= 384 && tid < 394) load_border(d, s.bd, tid - 384, mbx, mby);
-    else if (ROLE == 1 && tid >= 400 && tid < 471) load_intra_nb(d, s.nb, tid - 400, mbx, mby);
     else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
     const int wdim = 2 * sr + 16 + 2 * WM;
-    if (slice_p) {
+    {
         // SetupFastFullPelSearch: centre = 16x16 MVP / 4 (trunc), clamped to +-SR; the window
         // load starts right away (its centre depends only on the border cells)
         __syncthreads();
@@ -498,23 +492,21 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
         if (tid < 32) G[wdim * WST + tid] = 0;
     }
     __syncthreads();
-    PSTAMP(pb + 1);
-    if (slice_p) {
+    PSTAMP(1);
+    {
         // ---- this thread's column strip of NPK positions: SADs (registers) and JM order keys
         PosState ps;
         const int nstrips = (side + NPK - 1) / NPK;
         const bool sact = tid < side * nstrips;
         ps.dx = sact ? tid % side : 0;
         ps.dy0 = sact ? (tid / side) * NPK : 0;
-        if constexpr (ROLE == 1) {   // the four 8x8 SADs
-            sad_strip<true, 0, 0, 0, 0>(s, ps);
-            fence_state(ps);
-            sad_strip<true, 8, 0, 0, 1>(s, ps);
-            fence_state(ps);
-            sad_strip<true, 0, 8, 1, 0>(s, ps);
-            fence_state(ps);
-            sad_strip<true, 8, 8, 1, 1>(s, ps);
-        }
+        sad_strip<true, 0, 0, 0, 0>(s, ps);   // the four 8x8 SADs (16x16 / 16x8 / 8x16 searches)
+        fence_state(ps);
+        sad_strip<true, 8, 0, 0, 1>(s, ps);
+        fence_state(ps);
+        sad_strip<true, 0, 8, 1, 0>(s, ps);
+        fence_state(ps);
+        sad_strip<true, 8, 8, 1, 1>(s, ps);
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
             const int dy = ps.dy0 + k, rx = ps.dx - sr, ry = dy - sr;
@@ -554,8 +546,8 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
                 }
             // j is first read after the next stage's barriers
         }
-        PSTAMP(pb + 2);
-        if constexpr (ROLE == 1) {
+        PSTAMP(2);
+        {   // ---- 16x16, 16x8, 8x16
             unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
             int pmvx, pmvy;
             {   // stage 0: 16x16 (256 threads: 144 sub-pel tasks), 16x8 upper, 8x16 left (128 each)
@@ -592,7 +584,9 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
                 scr->skipx = (za || zl) ? 0 : pcx;
                 scr->skipy = (za || zl) ? 0 : pcy;
             }
-        } else {
+        }
+        PSTAMP(7);
+        {   // ---- P8x8: 4 x 4 stages
             int best8x8 = 0, cost8x8 = 0;
             p8x8_block<0>(d, s, ps, scx, scy, best8x8, cost8x8);
             PSTAMP(3);
@@ -612,12 +606,6 @@ __device__ __forceinline__ void me_role(const DevParams &d, MeS &s, int mbx, int
             }
             PSTAMP(6);
         }
-    }
-    if constexpr (ROLE == 1) {   // Intra16x16 (wave 0) and chroma intra mode (wave 1) decisions
-        const int wave = tid >> 6, lane = tid & 63;
-        if (wave == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
-        else if (wave == 1) chroma_decision(d, s.nb, scr, lane, avL, avT, avTL);
-        PSTAMP(pb + 3);
     }
 }
 
@@ -694,15 +682,21 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratc
     if (nz) { acc[1] |= 1 << ((by4 >> 1) * 2 + (bx4 >> 1)); acc[2] |= 1 << blk; }
 }
 
-__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby) {
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+// one MB on 128 threads (tid = 0..127, waves 0 and 1 of the group); every thread of the
+// workgroup reaches the same barriers (act: the group has an MB)
+__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act) {
+    const int wave = tid >> 6, lane = tid & 63;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
-    const bool prof = prof_mb_here(d, mbx, mby);
+    const bool prof = act && prof_mb_here(d, mbx, mby);
     PSTAMP(12);
-    if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    else if (tid < 266) load_border(d, s.bd, tid - 256, mbx, mby);
-    else if (tid >= 320 && tid < 416) load_intra_nb(d, s.nb, tid - 320, mbx, mby);
+    if (act) {
+        s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+        s.org[tid + 128] = d.orgY[(pix_y + 8 + (tid >> 4)) * W + pix_x + (tid & 15)];
+        load_orgc(d, s.nb, tid, mbx, mby);
+        if (tid < 10) load_border(d, s.bd, tid, mbx, mby);
+        else if (tid >= 16 && tid < 16 + 71) load_intra_nb(d, s.nb, tid - 16, mbx, mby);
+    }
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const int q_bits = 15 + d.qp / 6;
     const int qpk = d.slice_type == JMH_P_SLICE ? (1 << q_bits) / 6 : (1 << q_bits) / 3;
@@ -717,11 +711,12 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     for (int dg = 0; dg < 10; dg++) {         // blocks with bx4 + 2*by4 == dg, by4 ascending
         const int by_lo = dg > 3 ? (dg - 2) >> 1 : 0;
         const int by4 = by_lo + wave, bx4 = dg - 2 * by4;
-        if (wave < 2 && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+        if (act && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
         __syncthreads();
     }
-    if (wave < 2 && lane == 0) { s.part[wave][0] = acc[0]; s.part[wave][1] = acc[1]; s.part[wave][2] = acc[2]; }
+    if (act && lane == 0) { s.part[wave][0] = acc[0]; s.part[wave][1] = acc[1]; s.part[wave][2] = acc[2]; }
     __syncthreads();
+    if (!act) return;
     if (tid == 0) {
         scr->i4cost = 24 * d.lambda_mode + s.part[0][0] + s.part[1][0];   // 4 x (int)floor(6*lambda+0.4999)
         scr->i4cbp = s.part[0][1] | s.part[1][1];
@@ -730,30 +725,32 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     if (tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
     if (tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
     PSTAMP(13);
+    // Intra16x16 (wave 0) and intra chroma mode (wave 1) decisions
+    if (wave == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
+    else chroma_decision(d, s.nb, scr, lane, avL, avT, avTL);
+    PSTAMP(14);
 }
 
 __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     __shared__ AnalyseS s;
-    // blocks: [0, nPm) role 2 of the P pictures' MBs (longest, dispatched first), then role 1 and
-    // role 0 over every picture's MBs (an I picture runs roles 0 and 1 only)
+    // blocks: [0, nPm) the motion search of each P picture MB (longest, dispatched first), then
+    // the intra decisions of every MB, four MBs (128 threads each) per workgroup
     const int nPm = t.pre[t.nP], tot = t.pre[t.npic], b = blockIdx.x;
-    const int role = b < nPm ? 2 : (b < nPm + tot ? 1 : 0);
-    const int idx = role == 2 ? b : (role == 1 ? b - nPm : b - nPm - tot);
-    const int e = tick_entry(t, idx);
-    const DevParams d = tick_params(t, e);
-    const int mby = d.y_min + (idx - t.pre[e]), mbx = d.diag - 2 * mby;
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
-#ifndef ONLY_ROLE
-    if (role == 2) me_role<2>(d, s.me, mbx, mby);
-    else if (role == 1) me_role<1>(d, s.me, mbx, mby);
-    else intra_role(d, s.in, mbx, mby);
-#elif ONLY_ROLE == 2
-    me_role<2>(d, s.me, mbx, mby);
-#elif ONLY_ROLE == 1
-    me_role<1>(d, s.me, mbx, mby);
-#else
-    intra_role(d, s.in, mbx, mby);
-#endif
+    const int role = b < nPm ? 2 : 0;
+    if (role == 2) {
+        const int e = tick_entry(t, b);
+        const DevParams d = tick_params(t, e);
+        const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
+        me_mb(d, s.me, mbx, mby);
+    } else {
+        const int q = __builtin_amdgcn_readfirstlane(4 * (b - nPm) + (int)(threadIdx.x >> 7));
+        const bool act = q < tot;
+        const int e = tick_entry(t, act ? q : 0);
+        const DevParams d = tick_params(t, e);
+        const int mby = d.y_min + ((act ? q : t.pre[e]) - t.pre[e]), mbx = d.diag - 2 * mby;
+        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act);
+    }
     if (t.bprof) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -765,7 +762,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
-    const int nblocks = t.pre[t.nP] + 2 * t.pre[t.npic];
+    const int nblocks = t.pre[t.nP] + (t.pre[t.npic] + 3) / 4;
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }

@@ -363,7 +363,7 @@ static int issue_tick(jmh_ctx *c) {
     t.npic = k; t.nP = nP; t.pre[k] = mbs;
     if (c->d_bprof && c->ticks_total == c->bprof_tick) {
         t.bprof = c->d_bprof;
-        c->bprof_blocks = t.pre[nP] + 2 * t.pre[k];
+        c->bprof_blocks = t.pre[nP] + (t.pre[k] + 3) / 4;
     }
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
