@@ -33,6 +33,8 @@
 #include "jmh_common.h"
 
 #define NPK 10                                // search positions per thread (a column strip)
+#define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
+#define MVB_LEN 1104
 #define PLS (WIN_DIM_MAX * WST + 32)          // stride between the G, b, h, j planes
 
 // Intra4x4 prediction (8.3.1.2) of mode m at pixel l as a formula over P[0..12]
@@ -63,9 +65,9 @@ struct MeS {
     IntraNb nb;
     int16_t all_mv[8][16][2];
     int motion_cost[8][4];
-    uint16_t ctab[4][2][72];                  // per team: lambda*mvbits for x and y offsets
-    unsigned red[NTA / 64][4];                // per wave, per team: partial argmin keys
-    int ccost[2][4][9];                       // per sub-pel pass, team, candidate (LDS atomics)
+    unsigned red[NTA / 64][4];                // per wave, per search of the stage: argmin keys
+    int pmv[4][2];                            // MVPs of the next stage's searches (forwarded)
+    uint8_t mvb[MVB_LEN];                     // mvbits(v) at [v + MVB_OFF] (|v| <= 4*2*SR + 259)
     uint8_t planes[4 * PLS];                  // G (the window), b, h, j
     int16_t h1[WIN_DIM_MAX * WST];            // unclipped vertical 6-tap intermediates
     unsigned long long *pst;                  // debug: per-stage stamps (thread 0), null when off
@@ -156,6 +158,7 @@ struct PosState {
     uint32_t sadp[NPK][2];
     uint32_t ordk[NPK];      // JM order (0 = (0,0) pre-check); 0xFFFFFFFF for slots outside the table
     int dx, dy0;
+    int scx, scy;            // window centre (full pel, relative to the MB)
 };
 
 // optimisation fence on the register-resident search state, once per stage: keeps the compiler
@@ -169,23 +172,26 @@ __device__ __forceinline__ void fence_state(PosState &ps) {
     }
 }
 
-// this thread's best key for search (team J, partition BT/BX/BY); 'range' < sr only with
+// this thread's best key for a search of partition (BT, BX, BY) with predictor (pmx, pmy):
+// cost = SAD + lambda*(mvbits(x) + mvbits(y)) from the LDS mvbits table; 'range' < sr only with
 // RestrictSearchRange 0 (positions outside are skipped, the (0,0) pre-check never is)
-template <int J, int BT, int BX, int BY>
-__device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps, int sr, int range) {
-    const unsigned cxv = s.ctab[J][0][ps.dx];
+template <int BT, int BX, int BY>
+__device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps, int sr, int range, int lam, int pmx, int pmy, int scx,
+                                                int scy) {
+    const unsigned cxv = lam * s.mvb[4 * (scx - sr + ps.dx) - pmx + MVB_OFF];
+    const uint8_t *cy = s.mvb + 4 * (scy - sr + ps.dy0) - pmy + MVB_OFF;
     unsigned b = 0xFFFFFFFFu;
     if (range >= sr) {
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
-            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + s.ctab[J][1][ps.dy0 + k];
+            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + lam * cy[4 * k];
             b = min(b, (cost << 13) | ps.ordk[k]);
         }
     } else {
         const int rx = abs(ps.dx - sr);
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
-            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + s.ctab[J][1][ps.dy0 + k];
+            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + lam * cy[4 * k];
             const bool in = max(rx, abs(ps.dy0 + k - sr)) <= range || ps.ordk[k] == 0;
             b = min(b, in ? (cost << 13) | ps.ordk[k] : 0xFFFFFFFFu);
         }
@@ -195,123 +201,179 @@ __device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps
 
 __device__ __forceinline__ int search_range(const DevParams &d, int bt) { return d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr; }
 
-// the threads working on one search of a stage: search slot j (ctab / red / ccost index),
-// thread offset u within the team and team size (a multiple of 64); act: this thread has a search
-struct Team {
-    bool act;
-    int j, u, size;
+// one search of a stage: block type, position (4x4 units), partition index of motion_cost, and
+// the next-stage search whose MVP depends only on this result and on final MVs (fbt 0: none),
+// which the sub-pel wave computes into pmv[fslot]
+struct SDesc {
+    int bt, bx4, by4, mc;
+    int fbt, fbx4, fby4, fslot;
 };
 
-// stage head: the MVP of each active team's search (every team thread, uniform), its
-// lambda*mvbits tables and zeroed candidate sums; ends with the barrier that publishes them.
-__device__ __forceinline__ void stage_head(const DevParams &d, MeS &s, const Team &tm, int bt, int bx4, int by4, int b8, int best8x8,
-                                           int scx, int scy, int &pmvx, int &pmvy) {
-    const int team = tm.j, side = d.side, sr = d.sr, lam = d.lambda_motion;
-    pmvx = pmvy = 0;
-    if (tm.act) {
-        set_mvp(NbMe{s, bt, b8, best8x8}, bx4, by4, 4 << lw4_of(bt), 4 << lh4_of(bt), pmvx, pmvy);
-        for (int u = tm.u; u < 2 * side + 18; u += tm.size) {
-            if (u < side) s.ctab[team][0][u] = (uint16_t)(lam * mvbits(((scx + u - sr) << 2) - pmvx));
-            else if (u < 2 * side) s.ctab[team][1][u - side] = (uint16_t)(lam * mvbits(((scy + u - side - sr) << 2) - pmvy));
-            else s.ccost[(u - 2 * side) / 9][team][(u - 2 * side) % 9] = 0;
-        }
-    }
-    __syncthreads();
-    sstamp(s);
+// SATD() [J] of one 4x4 sub-block against the sub-pel prediction at quarter-pel offset (ox, oy)
+// from the full-pel position; wbase = window offset of the sub-block's top-left sample there.
+// One lane does the whole block: rows of 4 samples as dwords (two aligned LDS reads +
+// v_alignbyte per plane), the rounding average of the two planes per byte.
+__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t *p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ s16x2 abs2(s16x2 v) { return __builtin_elementwise_max(v, (s16x2)(0) - v); }
 
-// publish the per-thread keys of the stage's searches (teams with bit set in mask)
-__device__ __forceinline__ void stage_reduce(MeS &s, unsigned mask, const unsigned (&bk)[4]) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__device__ __forceinline__ int subblock_satd(const MeS &s, int wbase, int obase, int ox, int oy, int had) {
+    const int off = qoff((oy & 3) * 4 + (ox & 3));
+    const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
+    const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
+    const int oB = ((xb & 1) + 2 * (yb & 1)) * PLS + (yb >> 1) * WST + (xb >> 1);
+    const uint8_t *r0 = s.planes + wbase + (oy >> 2) * WST + (ox >> 2);
+    uint32_t O[4], P[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-        if ((mask >> j) & 1) {
-            unsigned v = wave_min_u32(bk[j]);
-            if (lane == 0) s.red[wave][j] = v;
-        }
-    __syncthreads();
-    sstamp(s);
+    for (int yy = 0; yy < 4; yy++) {
+        const uint32_t A = lds_u32_at(r0 + yy * WST + oA), B = lds_u32_at(r0 + yy * WST + oB);
+        P[yy] = (A | B) - (((A ^ B) >> 1) & 0x7F7F7F7Fu);   // per byte (a + b + 1) >> 1
+        O[yy] = *reinterpret_cast<const uint32_t *>(s.org + obase + 16 * yy);
+    }
+    if (!had) {
+        uint32_t sad = 0;
+#pragma unroll
+        for (int yy = 0; yy < 4; yy++) sad = __builtin_amdgcn_sad_u8(O[yy], P[yy], sad);
+        return (int)sad;
+    }
+    // 4x4 Hadamard on packed int16 pairs (|coefficient| <= 16 * 255): r[y][h] = columns 2h, 2h+1
+    s16x2 r[4][2];
+#pragma unroll
+    for (int yy = 0; yy < 4; yy++) {
+        r[yy][0] = as_s2(__builtin_amdgcn_perm(0u, O[yy], 0x0c010c00u)) - as_s2(__builtin_amdgcn_perm(0u, P[yy], 0x0c010c00u));
+        r[yy][1] = as_s2(__builtin_amdgcn_perm(0u, O[yy], 0x0c030c02u)) - as_s2(__builtin_amdgcn_perm(0u, P[yy], 0x0c030c02u));
+    }
+    s16x2 m[4][2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {   // vertical
+        const s16x2 a0 = r[0][h] + r[3][h], a1 = r[1][h] + r[2][h], a2 = r[1][h] - r[2][h], a3 = r[0][h] - r[3][h];
+        m[0][h] = a0 + a1; m[2][h] = a0 - a1; m[1][h] = a2 + a3; m[3][h] = a3 - a2;
+    }
+    s16x2 acc = (s16x2)(0);
+#pragma unroll
+    for (int p = 0; p < 2; p++) {   // horizontal, rows 2p and 2p+1 packed together
+        const uint32_t u0 = as_u32(m[2 * p][0]), v0 = as_u32(m[2 * p + 1][0]);
+        const uint32_t u1 = as_u32(m[2 * p][1]), v1 = as_u32(m[2 * p + 1][1]);
+        const s16x2 x0 = as_s2(__builtin_amdgcn_perm(v0, u0, 0x05040100u)), x1 = as_s2(__builtin_amdgcn_perm(v0, u0, 0x07060302u));
+        const s16x2 x2 = as_s2(__builtin_amdgcn_perm(v1, u1, 0x05040100u)), x3 = as_s2(__builtin_amdgcn_perm(v1, u1, 0x07060302u));
+        const s16x2 a0 = x0 + x3, a1 = x1 + x2, a2 = x1 - x2, a3 = x0 - x3;
+        acc += abs2(a0 + a1) + abs2(a0 - a1) + abs2(a2 + a3) + abs2(a3 - a2);   // <= 8 * 4080 per half
+    }
+    const uint32_t t = as_u32(acc);
+    return (int)(((t & 0xFFFFu) + (t >> 16)) >> 1);
 }
 
-// stage tail: each active team resolves its full-pel winner, runs SubPelBlockMotionSearch
-// (half then quarter pel: 9 candidates x up to 16 4x4 sub-blocks, one per 16-lane row) and
-// stores the MV and the partition cost.
-__device__ __forceinline__ void stage_tail(const DevParams &d, MeS &s, const Team &tm, int bt, int bx4, int by4, int mcidx, int pmvx,
-                                           int pmvy, int scx, int scy) {
-    const bool act = tm.act;
-    const int team = tm.j, u = tm.u, g = u >> 4, l = u & 15, ngrp = tm.size >> 4;
+// SubPelBlockMotionSearch [J] of search j of the stage on ONE wave: full-pel winner from the
+// per-wave keys, then half-pel (9 candidates) and quarter-pel (8) passes.  Lane task = (candidate,
+// 4x4 sub-block), aligned groups of nsub lanes sum a candidate, the wave minimum of
+// (cost, candidate) keys is JM's strict '<' scan in candidate order.  No workgroup barrier.
+#define KOFF 4096
+__device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, const SDesc q, int pmvx, int pmvy, int scx, int scy, int b8,
+                                            int best8x8) {
+    const int lane = threadIdx.x & 63;
     const int sr = d.sr, lam = d.lambda_motion, had = d.use_hadamard;
-    int rx = 0, ry = 0, fmx = 0, fmy = 0, min_mcost = 0, qx = 0, qy = 0, lw4 = 0, lns = 0, check0 = 0;
-    if (act) {
-        unsigned best = s.red[0][team];
+    unsigned best = s.red[0][j];
 #pragma unroll
-        for (int w = 1; w < NTA / 64; w++) best = min(best, s.red[w][team]);
-        const unsigned order = best & 8191u;
-        if (order == 0) { rx = -scx; ry = -scy; }
-        else spiral_pos((int)order - 1, rx, ry);
-        fmx = scx + rx; fmy = scy + ry;
-        min_mcost = (int)(best >> 13);
-        const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt);
-        lw4 = w4 >> 1;                         // log2 of w4 (1, 2, 4)
-        lns = lw4 + (h4 >> 1);                // log2 of the sub-block count
-        check0 = bt == 1 && fmx == 0 && fmy == 0 && had && d.slice_type == JMH_P_SLICE;
-        if (had) min_mcost = BIGCOST;
-    }
-    // window coords of this lane's pixel in block (0,0) at the full-pel MV, and its original sample
-    const int wx0 = WM + sr + rx + 4 * bx4 + (l & 3), wy0 = WM + sr + ry + 4 * by4 + (l >> 2);
-    const uint8_t *orow = s.org + (4 * by4 + (l >> 2)) * 16 + 4 * bx4 + (l & 3);
+    for (int w = 1; w < NTA / 64; w++) best = min(best, s.red[w][j]);
+    const unsigned order = best & 8191u;
+    int rx, ry;
+    if (order == 0) { rx = -scx; ry = -scy; }
+    else spiral_pos((int)order - 1, rx, ry);
+    const int fmx = scx + rx, fmy = scy + ry;
+    int min_mcost = had ? BIGCOST : (int)(best >> 13);
+    const int lw4 = lw4_of(q.bt), lns = lw4 + lh4_of(q.bt), nsub = 1 << lns;
+    const bool check0 = q.bt == 1 && fmx == 0 && fmy == 0 && had && d.slice_type == JMH_P_SLICE;
+    const int wb0 = (WM + sr + ry) * WST + WM + sr + rx;   // window offset of MB pixel (0,0) at the full-pel MV
+    int qx = 0, qy = 0;
+#pragma unroll
     for (int pass = 0; pass < 2; pass++) {
         const int step = pass == 0 ? 2 : 1;
         const int min_pos = pass == 0 ? (had ? 0 : 1) : 1;
-        if (act) {
-            const int ntask = 9 << lns;
-            for (int t = g; t < ntask; t += ngrp) {   // uniform per 16-lane row
-                const int c = t >> lns, sub = t & ((1 << lns) - 1);
-                if (c < min_pos) continue;
-                const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
-                const int off = qoff((oy & 3) * 4 + (ox & 3));
-                const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
-                const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
-                const int oB = ((xb & 1) + 2 * (yb & 1)) * PLS + (yb >> 1) * WST + (xb >> 1);
-                const int bxp = 4 * (sub & ((1 << lw4) - 1)), byp = 4 * (sub >> lw4);
-                const uint8_t *pp = s.planes + (wy0 + byp + (oy >> 2)) * WST + wx0 + bxp + (ox >> 2);
-                const int dv = orow[16 * byp + bxp] - ((pp[oA] + pp[oB] + 1) >> 1);
-                int sat = had ? row16_sum(abs(row16_had(dv, l))) >> 1 : row16_sum(abs(dv));
-                if (l == 0) {
-                    if (sub == 0) {
-                        const int vx = 4 * fmx + ox, vy = 4 * fmy + oy;
-                        sat += lam * (mvbits(vx - pmvx) + mvbits(vy - pmvy));
-                        if (pass == 0 && check0 && c == 0) sat -= 16 * lam;
-                    }
-                    atomicAdd(&s.ccost[pass][team][c], sat);
-                }
+        unsigned kb = 0xFFFFFFFFu;
+        for (int t0 = 0; t0 < (9 << lns); t0 += 64) {
+            const int task = t0 + lane, c = task >> lns, sub = task & (nsub - 1);
+            const bool val = c < 9 && c >= min_pos;
+            const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+            int sat = 0;
+            if (val) {
+                const int bxs = q.bx4 + (sub & ((1 << lw4) - 1)), bys = q.by4 + (sub >> lw4);
+                sat = subblock_satd(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had);
+            }
+            for (int m = 1; m < nsub; m <<= 1) sat += __shfl_xor(sat, m, 64);
+            if (val && sub == 0) {
+                int cost = sat + lam * (mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
+                if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
+                kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
             }
         }
-        __syncthreads();
-        sstamp(s);
-        if (act) {   // JM order, strict '<' against the running minimum
-            int bpos = 0;
-            for (int c = min_pos; c < 9; c++) {
-                const int v = s.ccost[pass][team][c];
-                if (v < min_mcost) { min_mcost = v; bpos = c; }
-            }
-            qx += step * sp9x(bpos);
-            qy += step * sp9y(bpos);
+        kb = wave_min_u32(kb);
+        if (kb != 0xFFFFFFFFu && (int)(kb >> 4) - KOFF < min_mcost) {
+            const int c = kb & 15;
+            min_mcost = (int)(kb >> 4) - KOFF;
+            qx += step * sp9x(c);
+            qy += step * sp9y(c);
         }
     }
-    if (act) {
-        const int cmx = 4 * fmx + qx, cmy = 4 * fmy + qy;
-        if (u < (1 << lns)) {
-            const int k = (by4 + (u >> lw4)) * 4 + bx4 + (u & ((1 << lw4) - 1));
-            s.all_mv[bt][k][0] = (int16_t)cmx; s.all_mv[bt][k][1] = (int16_t)cmy;
-        }
-        if (u == 0) s.motion_cost[bt][mcidx] += min_mcost;
+    if (lane < nsub) {
+        const int k = (q.by4 + (lane >> lw4)) * 4 + q.bx4 + (lane & ((1 << lw4) - 1));
+        s.all_mv[q.bt][k][0] = (int16_t)(4 * fmx + qx);
+        s.all_mv[q.bt][k][1] = (int16_t)(4 * fmy + qy);
     }
+    if (lane == 0) s.motion_cost[q.bt][q.mc] += min_mcost;
+    if (q.fbt) {   // forwarded MVP of the next stage's search (reads the MVs just stored)
+        int mx, my;
+        set_mvp(NbMe{s, q.fbt, b8, best8x8}, q.fbx4, q.fby4, 4 << lw4_of(q.fbt), 4 << lh4_of(q.fbt), mx, my);
+        if (lane == 0) { s.pmv[q.fslot][0] = mx; s.pmv[q.fslot][1] = my; }
+    }
+}
+
+// one stage of NS independent searches: MVPs (FWD: forwarded by the previous stage's sub-pel
+// waves through LDS; else lane j of every wave computes search j's, then readlane), the full-pel
+// argmin over all positions by every thread (EV fills bk[] from pmx/pmy), per-wave minima -> LDS
+// -> barrier, sub-pel search j on wave j (+ forwarded MVPs), barrier.
+template <int NS, bool FWD, class EV>
+__device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &ps, const SDesc (&sd)[NS], int b8, int best8x8, EV ev) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    fence_state(ps);
+    int pmx[NS], pmy[NS];
+    unsigned bk[NS];
+    if constexpr (FWD) {
+#pragma unroll
+        for (int j = 0; j < NS; j++) { pmx[j] = s.pmv[j][0]; pmy[j] = s.pmv[j][1]; }
+    } else {
+        int mx = 0, my = 0;
+        if (lane < NS) {
+            SDesc q = sd[0];
+#pragma unroll
+            for (int j = 1; j < NS; j++)
+                if (lane == j) q = sd[j];
+            set_mvp(NbMe{s, q.bt, b8, best8x8}, q.bx4, q.by4, 4 << lw4_of(q.bt), 4 << lh4_of(q.bt), mx, my);
+        }
+#pragma unroll
+        for (int j = 0; j < NS; j++) { pmx[j] = __builtin_amdgcn_readlane(mx, j); pmy[j] = __builtin_amdgcn_readlane(my, j); }
+    }
+    ev(bk, pmx, pmy);
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+        const unsigned v = wave_min_u32(bk[j]);
+        if (lane == 0) s.red[wave][j] = v;
+    }
+    __syncthreads();
+    sstamp(s);
+#pragma unroll
+    for (int j = 0; j < NS; j++)
+        if (wave == j) subpel_wave(d, s, j, sd[j], pmx[j], pmy[j], ps.scx, ps.scy, b8, best8x8);
     __syncthreads();
     sstamp(s);
 }
 
-#define EVAL(J, BT, BX, BY) bk[J] = eval_search<J, BT, BX, BY>(s, ps, sr, search_range(d, BT))
+#define EV(J, BT, BX, BY) bk[J] = eval_search<BT, BX, BY>(s, ps, sr, search_range(d, BT), lam, pmx[J], pmy[J], ps.scx, ps.scy)
 
 // SADs at this thread's NPK positions (column strip dx, rows dy0..dy0+NPK-1 of the window) of the
 // 8x8 org block at pixel (OX, OY).  EIGHT: the 8x8 SAD into half HI of ps.sadp[k][SLOT] (role 1);
@@ -350,46 +412,36 @@ __device__ __forceinline__ void sad_strip(const MeS &s, PosState &ps) {
     }
 }
 
+// one 8x8 block of P8x8: its 4x4 SADs, 4 stages (sub-modes 4..7 in parallel, then the 4x4
+// chain), then the P8x8 sub-mode decision for the block (its MVs are read through best8x8)
 template <int B8>
-__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int scx, int scy, int &best8x8, int &cost8x8) {
+__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
-    const int tid = threadIdx.x, sr = d.sr;
+    const int sr = d.sr, lam = d.lambda_motion;
     fence_state(ps);
     sad_strip<false, 4 * X, 4 * Y, 0, 0>(s, ps);        // the four 4x4 SADs of this 8x8 block
-    const Team t4{true, tid >> 7, tid & 127, 128};       // four searches: 128 threads each
-    const Team t1{true, 3, tid, NTA};                    // one search: the whole workgroup
-    unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
-    int pmvx, pmvy;
     {   // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left
-        const int bt = 4 + t4.j;
-        fence_state(ps);
-        stage_head(d, s, t4, bt, X, Y, B8, best8x8, scx, scy, pmvx, pmvy);
-        EVAL(0, 4, X, Y); EVAL(1, 5, X, Y); EVAL(2, 6, X, Y); EVAL(3, 7, X, Y);
-        stage_reduce(s, 0xF, bk);
-        stage_tail(d, s, t4, bt, X, Y, B8, pmvx, pmvy, scx, scy);
+        const SDesc sd[4] = {{4, X, Y, B8, 0, 0, 0, 0},
+                             {5, X, Y, B8, 5, X, Y + 1, 0},
+                             {6, X, Y, B8, 6, X + 1, Y, 1},
+                             {7, X, Y, B8, 7, X + 1, Y, 2}};
+        me_stage<4, false>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[4], const int (&pmx)[4], const int (&pmy)[4]) {
+            EV(0, 4, X, Y); EV(1, 5, X, Y); EV(2, 6, X, Y); EV(3, 7, X, Y);
+        });
     }
-    {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right (teams 1..3)
-        const Team tm{t4.j >= 1, t4.j, t4.u, 128};
-        const int bt = 4 + tm.j, bx4 = tm.j == 1 ? X : X + 1, by4 = tm.j == 1 ? Y + 1 : Y;
-        fence_state(ps);
-        stage_head(d, s, tm, bt, bx4, by4, B8, best8x8, scx, scy, pmvx, pmvy);
-        EVAL(1, 5, X, Y + 1); EVAL(2, 6, X + 1, Y); EVAL(3, 7, X + 1, Y);
-        stage_reduce(s, 0xE, bk);
-        stage_tail(d, s, tm, bt, bx4, by4, B8, pmvx, pmvy, scx, scy);
+    {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right
+        const SDesc sd[3] = {{5, X, Y + 1, B8, 0, 0, 0, 0}, {6, X + 1, Y, B8, 0, 0, 0, 0}, {7, X + 1, Y, B8, 7, X, Y + 1, 0}};
+        me_stage<3, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
+            EV(0, 5, X, Y + 1); EV(1, 6, X + 1, Y); EV(2, 7, X + 1, Y);
+        });
     }
     {   // stage 2: 4x4 bottom-left
-        fence_state(ps);
-        stage_head(d, s, t1, 7, X, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
-        EVAL(3, 7, X, Y + 1);
-        stage_reduce(s, 0x8, bk);
-        stage_tail(d, s, t1, 7, X, Y + 1, B8, pmvx, pmvy, scx, scy);
+        const SDesc sd[1] = {{7, X, Y + 1, B8, 7, X + 1, Y + 1, 0}};
+        me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X, Y + 1); });
     }
     {   // stage 3: 4x4 bottom-right
-        fence_state(ps);
-        stage_head(d, s, t1, 7, X + 1, Y + 1, B8, best8x8, scx, scy, pmvx, pmvy);
-        EVAL(3, 7, X + 1, Y + 1);
-        stage_reduce(s, 0x8, bk);
-        stage_tail(d, s, t1, 7, X + 1, Y + 1, B8, pmvx, pmvy, scx, scy);
+        const SDesc sd[1] = {{7, X + 1, Y + 1, B8, 0, 0, 0, 0}};
+        me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X + 1, Y + 1); });
     }
     int mc8 = BIGCOST, bm = 0;
     for (int mode = 4; mode <= 7; mode++) {
@@ -474,21 +526,39 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     else if (tid >= 384 && tid < 394) load_border(d, s.bd, tid - 384, mbx, mby);
     else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
+    for (int i = tid; i < MVB_LEN; i += NTA) s.mvb[i] = (uint8_t)mvbits(i - MVB_OFF);
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
     const int wdim = 2 * sr + 16 + 2 * WM;
     {
         // SetupFastFullPelSearch: centre = 16x16 MVP / 4 (trunc), clamped to +-SR; the window
-        // load starts right away (its centre depends only on the border cells)
+        // load starts right away (its centre depends only on the border cells).  One LDS dword
+        // per task: two aligned global dwords + v_alignbyte inside the picture, clamped bytes
+        // at its edges; columns >= wdim are zero.
         __syncthreads();
         set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
         scx = iclip(-sr, sr, pcx / 4); scy = iclip(-sr, sr, pcy / 4);
         const int X0 = pix_x + scx - sr - WM, Y0 = pix_y + scy - sr - WM;
-        constexpr int RPP = NTA / WST;                  // window rows per pass
-        const int yi = tid / WST, xi = tid - yi * WST;
-        const int xs = iclip(0, W - 1, X0 + xi);
-        if (yi < RPP)
-            for (int y = yi; y < wdim; y += RPP) G[y * WST + xi] = xi < wdim ? d.refY[iclip(0, d.H - 1, Y0 + y) * W + xs] : 0;
+        constexpr int ND4 = WST / 4;
+#pragma unroll
+        for (int i = 0; i < (WIN_DIM_MAX * ND4 + NTA - 1) / NTA; i++) {
+            const int task = tid + i * NTA;
+            if (task >= wdim * ND4) break;
+            const int y = task / ND4, j = task - y * ND4;
+            const uint8_t *row = d.refY + iclip(0, d.H - 1, Y0 + y) * W;
+            const int x0 = X0 + 4 * j;
+            uint32_t v;
+            if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
+                const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
+                v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
+            } else {
+                v = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
+            }
+            *reinterpret_cast<uint32_t *>(G + y * WST + 4 * j) = v;
+        }
         if (tid < 32) G[wdim * WST + tid] = 0;
     }
     __syncthreads();
@@ -500,6 +570,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         const bool sact = tid < side * nstrips;
         ps.dx = sact ? tid % side : 0;
         ps.dy0 = sact ? (tid / side) * NPK : 0;
+        ps.scx = scx; ps.scy = scy;
         sad_strip<true, 0, 0, 0, 0>(s, ps);   // the four 8x8 SADs (16x16 / 16x8 / 8x16 searches)
         fence_state(ps);
         sad_strip<true, 8, 0, 0, 1>(s, ps);
@@ -507,6 +578,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         sad_strip<true, 0, 8, 1, 0>(s, ps);
         fence_state(ps);
         sad_strip<true, 8, 8, 1, 1>(s, ps);
+        PSTAMP(8);
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
             const int dy = ps.dy0 + k, rx = ps.dx - sr, ry = dy - sr;
@@ -514,6 +586,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
             else if (rx == -scx && ry == -scy) ps.ordk[k] = 0;   // the (0,0) pre-check position
             else ps.ordk[k] = (uint32_t)(spiral_index(rx, ry) + 1);
         }
+        PSTAMP(9);
         // ---- half-pel planes over window coords [3, 2sr+20]^2: h1 and h = clip(h1) by column
         //      runs (sliding 6-tap), b by rows; then j from h1
         {
@@ -539,6 +612,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
                 }
             }
             __syncthreads();
+            PSTAMP(10);
             if (cx >= lo && cx < lo + n)
                 for (int y = y0; y < y1; y++) {
                     const int16_t *h = s.h1 + y * WST + cx;
@@ -548,26 +622,18 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         }
         PSTAMP(2);
         {   // ---- 16x16, 16x8, 8x16
-            unsigned bk[4] = {~0u, ~0u, ~0u, ~0u};
-            int pmvx, pmvy;
-            {   // stage 0: 16x16 (256 threads: 144 sub-pel tasks), 16x8 upper, 8x16 left (128 each)
-                const int j = tid < 256 ? 0 : tid < 384 ? 1 : 2;
-                const Team tm{true, j, tid - (j == 0 ? 0 : j == 1 ? 256 : 384), j == 0 ? 256 : 128};
-                const int bt = 1 + j;
-                fence_state(ps);
-                stage_head(d, s, tm, bt, 0, 0, 0, 0, scx, scy, pmvx, pmvy);
-                EVAL(0, 1, 0, 0); EVAL(1, 2, 0, 0); EVAL(2, 3, 0, 0);
-                stage_reduce(s, 0x7, bk);
-                stage_tail(d, s, tm, bt, 0, 0, 0, pmvx, pmvy, scx, scy);
+            const int lam = d.lambda_motion;
+            {   // stage 0: 16x16, 16x8 upper, 8x16 left
+                const SDesc sd[3] = {{1, 0, 0, 0, 0, 0, 0, 0}, {2, 0, 0, 0, 2, 0, 2, 0}, {3, 0, 0, 0, 3, 2, 0, 1}};
+                me_stage<3, false>(d, s, ps, sd, 0, 0, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
+                    EV(0, 1, 0, 0); EV(1, 2, 0, 0); EV(2, 3, 0, 0);
+                });
             }
-            {   // stage 1: 16x8 lower, 8x16 right (256 threads each)
-                const Team tm{true, 1 + (tid >> 8), tid & 255, 256};
-                const int bt = 1 + tm.j, bx4 = tm.j == 2 ? 2 : 0, by4 = tm.j == 1 ? 2 : 0;
-                fence_state(ps);
-                stage_head(d, s, tm, bt, bx4, by4, 0, 0, scx, scy, pmvx, pmvy);
-                EVAL(1, 2, 0, 2); EVAL(2, 3, 2, 0);
-                stage_reduce(s, 0x6, bk);
-                stage_tail(d, s, tm, bt, bx4, by4, 1, pmvx, pmvy, scx, scy);
+            {   // stage 1: 16x8 lower, 8x16 right
+                const SDesc sd[2] = {{2, 0, 2, 1, 0, 0, 0, 0}, {3, 2, 0, 1, 0, 0, 0, 0}};
+                me_stage<2, true>(d, s, ps, sd, 0, 0, [&](unsigned (&bk)[2], const int (&pmx)[2], const int (&pmy)[2]) {
+                    EV(0, 2, 0, 2); EV(1, 3, 2, 0);
+                });
             }
             // results: MVs of types 1..3, partition costs, FindSkipModeMotionVector
             if (tid < 96) {
@@ -588,13 +654,13 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         PSTAMP(7);
         {   // ---- P8x8: 4 x 4 stages
             int best8x8 = 0, cost8x8 = 0;
-            p8x8_block<0>(d, s, ps, scx, scy, best8x8, cost8x8);
+            p8x8_block<0>(d, s, ps, best8x8, cost8x8);
             PSTAMP(3);
-            p8x8_block<1>(d, s, ps, scx, scy, best8x8, cost8x8);
+            p8x8_block<1>(d, s, ps, best8x8, cost8x8);
             PSTAMP(4);
-            p8x8_block<2>(d, s, ps, scx, scy, best8x8, cost8x8);
+            p8x8_block<2>(d, s, ps, best8x8, cost8x8);
             PSTAMP(5);
-            p8x8_block<3>(d, s, ps, scx, scy, best8x8, cost8x8);
+            p8x8_block<3>(d, s, ps, best8x8, cost8x8);
             if (tid < 128) {
                 const int m = 4 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
                 scr->all_mv[m][k][c] = s.all_mv[m][k][c];
