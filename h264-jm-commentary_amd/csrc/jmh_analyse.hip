@@ -222,6 +222,15 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s16x2 as_s2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ s16x2 abs2(s16x2 v) { return __builtin_elementwise_max(v, (s16x2)(0) - v); }
+__device__ __forceinline__ s16x2 lo16(uint32_t w) { return as_s2(__builtin_amdgcn_perm(0u, w, 0x0c010c00u)); }   // bytes 0, 1
+__device__ __forceinline__ s16x2 hi16(uint32_t w) { return as_s2(__builtin_amdgcn_perm(0u, w, 0x0c030c02u)); }   // bytes 2, 3
+__device__ __forceinline__ s16x2 tap6_2(s16x2 a, s16x2 b, s16x2 c, s16x2 d, s16x2 e, s16x2 f) {
+    return (a + f) + (s16x2)(20) * (c + d) - (s16x2)(5) * (b + e);
+}
+__device__ __forceinline__ s16x2 clip5(s16x2 v) {   // clip255((v + 16) >> 5)
+    return __builtin_elementwise_min(__builtin_elementwise_max((v + (s16x2)(16)) >> (s16x2)(5), (s16x2)(0)), (s16x2)(255));
+}
+__device__ __forceinline__ uint32_t pack4(s16x2 lo, s16x2 hi) { return __builtin_amdgcn_perm(as_u32(hi), as_u32(lo), 0x06040200u); }
 
 __device__ __forceinline__ int subblock_satd(const MeS &s, int wbase, int obase, int ox, int oy, int had) {
     const int off = qoff((oy & 3) * 4 + (ox & 3));
@@ -262,11 +271,42 @@ __device__ __forceinline__ int subblock_satd(const MeS &s, int wbase, int obase,
         const uint32_t u1 = as_u32(m[2 * p][1]), v1 = as_u32(m[2 * p + 1][1]);
         const s16x2 x0 = as_s2(__builtin_amdgcn_perm(v0, u0, 0x05040100u)), x1 = as_s2(__builtin_amdgcn_perm(v0, u0, 0x07060302u));
         const s16x2 x2 = as_s2(__builtin_amdgcn_perm(v1, u1, 0x05040100u)), x3 = as_s2(__builtin_amdgcn_perm(v1, u1, 0x07060302u));
+        // last butterfly: |a + b| + |a - b| = 2 max(|a|, |b|), so SATD = sum of the maxima
         const s16x2 a0 = x0 + x3, a1 = x1 + x2, a2 = x1 - x2, a3 = x0 - x3;
-        acc += abs2(a0 + a1) + abs2(a0 - a1) + abs2(a2 + a3) + abs2(a3 - a2);   // <= 8 * 4080 per half
+        acc += __builtin_elementwise_max(abs2(a0), abs2(a1)) + __builtin_elementwise_max(abs2(a2), abs2(a3));   // <= 4 * 4080 per half
     }
     const uint32_t t = as_u32(acc);
-    return (int)(((t & 0xFFFFu) + (t >> 16)) >> 1);
+    return (int)((t & 0xFFFFu) + (t >> 16));
+}
+
+// one row (row = lane & 3) of a 4x4 SATD on a quad of lanes: the vertical transform crosses the
+// quad by DPP, the result is this row's share (the quad sum is the block's SATD)
+__device__ __forceinline__ int quad_row_satd(const MeS &s, int wbase, int obase, int ox, int oy, int row, int had) {
+    const int off = qoff((oy & 3) * 4 + (ox & 3));
+    const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
+    const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
+    const int oB = ((xb & 1) + 2 * (yb & 1)) * PLS + (yb >> 1) * WST + (xb >> 1);
+    const uint8_t *rr = s.planes + wbase + (oy >> 2) * WST + (ox >> 2) + row * WST;
+    const uint32_t A = lds_u32_at(rr + oA), B = lds_u32_at(rr + oB);
+    const uint32_t P = (A | B) - (((A ^ B) >> 1) & 0x7F7F7F7Fu);
+    const uint32_t O = *reinterpret_cast<const uint32_t *>(s.org + obase + 16 * row);
+    if (!had) return (int)__builtin_amdgcn_sad_u8(O, P, 0u);
+    s16x2 p0 = as_s2(__builtin_amdgcn_perm(0u, O, 0x0c010c00u)) - as_s2(__builtin_amdgcn_perm(0u, P, 0x0c010c00u));
+    s16x2 p1 = as_s2(__builtin_amdgcn_perm(0u, O, 0x0c030c02u)) - as_s2(__builtin_amdgcn_perm(0u, P, 0x0c030c02u));
+    {   // rows (0,3), (1,2): sums on rows 0, 1, differences on rows 2, 3
+        const s16x2 q0 = as_s2((uint32_t)dpp<0x1B>((int)as_u32(p0))), q1 = as_s2((uint32_t)dpp<0x1B>((int)as_u32(p1)));
+        p0 = row < 2 ? p0 + q0 : q0 - p0;
+        p1 = row < 2 ? p1 + q1 : q1 - p1;
+    }
+    {   // rows (0,1), (2,3)
+        const s16x2 q0 = as_s2((uint32_t)dpp<0xB1>((int)as_u32(p0))), q1 = as_s2((uint32_t)dpp<0xB1>((int)as_u32(p1)));
+        p0 = (row & 1) == 0 ? p0 + q0 : q0 - p0;
+        p1 = (row & 1) == 0 ? p1 + q1 : q1 - p1;
+    }
+    // horizontal: (x0, x1) = p0, (x2, x3) = p1 -> (x0 + x3, x1 + x2), (x0 - x3, x1 - x2)
+    const s16x2 sw = as_s2(__builtin_amdgcn_alignbit(as_u32(p1), as_u32(p1), 16));
+    const uint32_t t = as_u32(abs2(p0 + sw)), u = as_u32(abs2(p0 - sw));
+    return (int)(max(t & 0xFFFFu, t >> 16) + max(u & 0xFFFFu, u >> 16));
 }
 
 // SubPelBlockMotionSearch [J] of search j of the stage on ONE wave: full-pel winner from the
@@ -296,20 +336,42 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
         const int step = pass == 0 ? 2 : 1;
         const int min_pos = pass == 0 ? (had ? 0 : 1) : 1;
         unsigned kb = 0xFFFFFFFFu;
-        for (int t0 = 0; t0 < (9 << lns); t0 += 64) {
-            const int task = t0 + lane, c = task >> lns, sub = task & (nsub - 1);
-            const bool val = c < 9 && c >= min_pos;
-            const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
-            int sat = 0;
-            if (val) {
-                const int bxs = q.bx4 + (sub & ((1 << lw4) - 1)), bys = q.by4 + (sub >> lw4);
-                sat = subblock_satd(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had);
+        if (lns <= 1) {   // 4x4 / 8x4 / 4x8: one row per lane, a quad per (candidate, 4x4 block)
+            const int row = lane & 3;
+            for (int t0 = 0; t0 < (9 << lns); t0 += 16) {
+                const int task = t0 + (lane >> 2), c = task >> lns, sub = task & (nsub - 1);
+                const bool val = c < 9 && c >= min_pos;
+                const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+                int sat = 0;
+                if (c < 9) {   // quad-uniform
+                    const int bxs = q.bx4 + (sub & ((1 << lw4) - 1)), bys = q.by4 + (sub >> lw4);
+                    sat = quad_row_satd(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, row, had);
+                }
+                sat += dpp<0xB1>(sat);
+                sat += dpp<0x4E>(sat);
+                if (lns) sat += __shfl_xor(sat, 4, 64);
+                if (val && sub == 0 && row == 0) {
+                    int cost = sat + lam * (mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
+                    if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
+                    kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
+                }
             }
-            for (int m = 1; m < nsub; m <<= 1) sat += __shfl_xor(sat, m, 64);
-            if (val && sub == 0) {
-                int cost = sat + lam * (mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
-                if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
-                kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
+        } else {   // one lane per (candidate, 4x4 block), nsub-lane groups sum a candidate
+            for (int t0 = 0; t0 < (9 << lns); t0 += 64) {
+                const int task = t0 + lane, c = task >> lns, sub = task & (nsub - 1);
+                const bool val = c < 9 && c >= min_pos;
+                const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+                int sat = 0;
+                if (val) {
+                    const int bxs = q.bx4 + (sub & ((1 << lw4) - 1)), bys = q.by4 + (sub >> lw4);
+                    sat = subblock_satd(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had);
+                }
+                for (int m = 1; m < nsub; m <<= 1) sat += __shfl_xor(sat, m, 64);
+                if (val && sub == 0) {
+                    int cost = sat + lam * (mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
+                    if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
+                    kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
+                }
             }
         }
         kb = wave_min_u32(kb);
@@ -587,37 +649,64 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
             else ps.ordk[k] = (uint32_t)(spiral_index(rx, ry) + 1);
         }
         PSTAMP(9);
-        // ---- half-pel planes over window coords [3, 2sr+20]^2: h1 and h = clip(h1) by column
-        //      runs (sliding 6-tap), b by rows; then j from h1
+        // ---- half-pel planes over window rows / columns [3, 2sr+21): four columns (one dword) per
+        //      thread: h1 (unclipped vertical taps, int16) and h by a sliding column run, b from
+        //      the row's dwords; then j from h1
         {
-            const int lo = WM - 1, n = 2 * sr + 18, h1w = wdim - 1;
+            const int lo = WM - 1, n = 2 * sr + 18;
             uint8_t *PB = s.planes + PLS, *PH = s.planes + 2 * PLS, *PJ = s.planes + 3 * PLS;
-            constexpr int NRUN = NTA / 96;                            // 96 columns x NRUN row runs
-            const int cx = 1 + tid % 96, rb = tid / 96;
-            const int run = (n + NRUN - 1) / NRUN, y0 = lo + rb * run, y1 = rb < NRUN ? min(lo + n, y0 + run) : y0;
-            if (cx <= h1w) {
-                const uint8_t *g = G + cx;
-                int t0 = g[(y0 - 2) * WST], t1 = g[(y0 - 1) * WST], t2 = g[y0 * WST], t3 = g[(y0 + 1) * WST], t4 = g[(y0 + 2) * WST];
-                const bool inb = cx >= lo && cx < lo + n;
+            constexpr int NG = WIN_DIM_MAX / 4, NR = NTA / NG;        // 22 column groups x 23 row runs
+            const int g = tid % NG, rb = tid / NG, c0 = 4 * g;
+            const int run = (n + NR - 1) / NR, y0 = lo + rb * run, y1 = rb < NR ? min(lo + n, y0 + run) : y0;
+            if (y0 < y1) {
+                const uint32_t *gc = reinterpret_cast<const uint32_t *>(G + c0);
+                constexpr int WS4 = WST / 4;
+                uint32_t w0 = gc[(y0 - 2) * WS4], w1 = gc[(y0 - 1) * WS4], w2 = gc[y0 * WS4], w3 = gc[(y0 + 1) * WS4], w4 = gc[(y0 + 2) * WS4];
                 for (int y = y0; y < y1; y++) {
-                    const int t5 = g[(y + 3) * WST];
-                    const int v = tap6(t0, t1, t2, t3, t4, t5);
-                    s.h1[y * WST + cx] = (int16_t)v;
-                    if (inb) {
-                        PH[y * WST + cx] = (uint8_t)clip255((v + 16) >> 5);
-                        const uint8_t *q = G + y * WST + cx;
-                        PB[y * WST + cx] = (uint8_t)clip255((tap6(q[-2], q[-1], q[0], q[1], q[2], q[3]) + 16) >> 5);
+                    const uint32_t w5 = gc[(y + 3) * WS4];
+                    const uint32_t L = gc[y * WS4 - 1], R = gc[y * WS4 + 1];
+                    int hv[4];
+                    uint32_t ph = 0, pb = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int sh = 8 * i;
+                        hv[i] = tap6((int)((w0 >> sh) & 255u), (int)((w1 >> sh) & 255u), (int)((w2 >> sh) & 255u), (int)((w3 >> sh) & 255u),
+                                     (int)((w4 >> sh) & 255u), (int)((w5 >> sh) & 255u));
+                        ph |= (uint32_t)clip255((hv[i] + 16) >> 5) << sh;
                     }
-                    t0 = t1; t1 = t2; t2 = t3; t3 = t4; t4 = t5;
+                    // b: bytes c0-2 .. c0+6 of row y (w2) from L | w2 | R
+                    const uint64_t mr = ((uint64_t)R << 32) | w2;
+                    int bx[9];
+                    bx[0] = (int)((L >> 16) & 255u); bx[1] = (int)(L >> 24);
+#pragma unroll
+                    for (int k = 0; k < 7; k++) bx[2 + k] = (int)((mr >> (8 * k)) & 255u);
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        pb |= (uint32_t)clip255((tap6(bx[i], bx[i + 1], bx[i + 2], bx[i + 3], bx[i + 4], bx[i + 5]) + 16) >> 5) << (8 * i);
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int cx = c0 + i;
+                        s.h1[y * WST + cx] = (int16_t)hv[i];
+                        { PH[y * WST + cx] = (uint8_t)(ph >> (8 * i)); PB[y * WST + cx] = (uint8_t)(pb >> (8 * i)); }
+                    }
+                    w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5;
                 }
             }
             __syncthreads();
             PSTAMP(10);
-            if (cx >= lo && cx < lo + n)
-                for (int y = y0; y < y1; y++) {
-                    const int16_t *h = s.h1 + y * WST + cx;
-                    PJ[y * WST + cx] = (uint8_t)clip255((tap6(h[-2], h[-1], h[0], h[1], h[2], h[3]) + 512) >> 10);
-                }
+            for (int y = y0; y < y1; y++) {   // j = clip((6-tap of h1 + 512) >> 10), 32-bit taps
+                const uint32_t *hr = reinterpret_cast<const uint32_t *>(s.h1 + y * WST + c0);
+                const uint32_t q0 = hr[-1], q1 = hr[0], q2 = hr[1], q3 = hr[2], q4 = hr[3];
+                const int x[9] = {(int)(int16_t)q0, (int)q0 >> 16, (int)(int16_t)q1, (int)q1 >> 16, (int)(int16_t)q2,
+                                  (int)q2 >> 16, (int)(int16_t)q3, (int)q3 >> 16, (int)(int16_t)q4};
+                uint32_t jv = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    jv |= (uint32_t)clip255((tap6(x[i], x[i + 1], x[i + 2], x[i + 3], x[i + 4], x[i + 5]) + 512) >> 10) << (8 * i);
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    PJ[y * WST + c0 + i] = (uint8_t)(jv >> (8 * i));
+            }
             // j is first read after the next stage's barriers
         }
         PSTAMP(2);
