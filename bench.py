@@ -68,11 +68,13 @@ def cpu_baseline(jm, frames):
 
 
 def read_pmc_traffic():
+    """HBM bytes per macroblock of k_mb_analyse measured by rocprofv3 PMC passes
+    (tools/pmc_traffic.sh -> profiles/pmc_traffic.json), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f)
-    except (OSError, ValueError):
+            return json.load(f)["kernels"]["k_mb_analyse"]["hbm_bytes_per_mb"]
+    except (OSError, ValueError, KeyError, TypeError):
         return None
 
 
@@ -142,7 +144,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
-            "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+            "traffic": round(pmc * mbs_per_launch) if pmc else None,
             "kernel": "k_mb_analyse",
             "algorithmic_bytes_per_launch": round(bytes_per_launch),
             "avg_launch_ms": round(an_launch_ms, 5),
