@@ -601,19 +601,28 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
         scx = iclip(-sr, sr, pcx / 4); scy = iclip(-sr, sr, pcy / 4);
         const int X0 = pix_x + scx - sr - WM, Y0 = pix_y + scy - sr - WM;
-        constexpr int ND4 = WST / 4;
+        constexpr int ND4 = WST / 4, NWT = (WIN_DIM_MAX * ND4 + NTA - 1) / NTA;
+        // all global loads first (interior dwords; edge tasks fall back to clamped bytes below)
+        uint32_t lo_[NWT], hi_[NWT];
+        bool fast[NWT];
 #pragma unroll
-        for (int i = 0; i < (WIN_DIM_MAX * ND4 + NTA - 1) / NTA; i++) {
+        for (int i = 0; i < NWT; i++) {
+            const int task = tid + i * NTA;
+            const int y = task / ND4, j = task - y * ND4, x0 = X0 + 4 * j;
+            fast[i] = task < wdim * ND4 && 4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W;
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(d.refY + iclip(0, d.H - 1, Y0 + y) * W + (fast[i] ? (x0 & ~3) : 0));
+            lo_[i] = p[0];
+            hi_[i] = (fast[i] && (x0 & 3)) ? p[1] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < NWT; i++) {
             const int task = tid + i * NTA;
             if (task >= wdim * ND4) break;
-            const int y = task / ND4, j = task - y * ND4;
-            const uint8_t *row = d.refY + iclip(0, d.H - 1, Y0 + y) * W;
-            const int x0 = X0 + 4 * j;
+            const int y = task / ND4, j = task - y * ND4, x0 = X0 + 4 * j;
             uint32_t v;
-            if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
-                const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
-                v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
-            } else {
+            if (fast[i]) v = __builtin_amdgcn_alignbyte(hi_[i], lo_[i], x0 & 3);
+            else {
+                const uint8_t *row = d.refY + iclip(0, d.H - 1, Y0 + y) * W;
                 v = 0;
 #pragma unroll
                 for (int q = 0; q < 4; q++)
@@ -890,7 +899,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     __shared__ AnalyseS s;
     // blocks: [0, nPm) the motion search of each P picture MB (longest, dispatched first), then
     // the intra decisions of every MB, four MBs (128 threads each) per workgroup
-    const int nPm = t.pre[t.nP], tot = t.pre[t.npic], b = blockIdx.x;
+    const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0, tot = t.pre[t.npic], b = blockIdx.x;
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
     const int role = b < nPm ? 2 : 0;
     if (role == 2) {
@@ -917,7 +926,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
-    const int nblocks = t.pre[t.nP] + (t.pre[t.npic] + 3) / 4;
+    const int nblocks = (t.me_in_analyse ? t.pre[t.nP] : 0) + (t.pre[t.npic] + 3) / 4;
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }

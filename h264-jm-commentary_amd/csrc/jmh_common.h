@@ -58,30 +58,38 @@ __device__ __forceinline__ int vh1(const uint8_t *p, int w, int h, int x, int y)
     return tap6(rpx(p, w, h, x, y - 2), rpx(p, w, h, x, y - 1), rpx(p, w, h, x, y), rpx(p, w, h, x, y + 1), rpx(p, w, h, x, y + 2),
                 rpx(p, w, h, x, y + 3));
 }
-// one luma sample at quarter-pel position (X, Y) (units of 1/4 pel): only the half-pel samples
-// the phase needs (G, b, h, s, m, j of Figure 8-4), same values as k_interp's 16 planes
-__device__ __forceinline__ int qpel_direct(const uint8_t *ref, int W, int H, int X, int Y) {
+// one luma sample at quarter-pel position (X, Y) (units of 1/4 pel) from integer samples px(x, y):
+// only the half-pel samples the phase needs (G, b, h, s, m, j of Figure 8-4), same values as
+// k_interp's 16 planes
+template <class PX>
+__device__ __forceinline__ int qpel_from(PX px, int X, int Y) {
     const int x = X >> 2, y = Y >> 2, fx = X & 3, fy = Y & 3;
-    auto hb = [&](int xx, int yy) { return clip255((hb1(ref, W, H, xx, yy) + 16) >> 5); };
-    auto vb = [&](int xx, int yy) { return clip255((vh1(ref, W, H, xx, yy) + 16) >> 5); };
+    auto hb1p = [&](int xx, int yy) { return tap6(px(xx - 2, yy), px(xx - 1, yy), px(xx, yy), px(xx + 1, yy), px(xx + 2, yy), px(xx + 3, yy)); };
+    auto vh1p = [&](int xx, int yy) { return tap6(px(xx, yy - 2), px(xx, yy - 1), px(xx, yy), px(xx, yy + 1), px(xx, yy + 2), px(xx, yy + 3)); };
+    auto hb = [&](int xx, int yy) { return clip255((hb1p(xx, yy) + 16) >> 5); };
+    auto vb = [&](int xx, int yy) { return clip255((vh1p(xx, yy) + 16) >> 5); };
     if (fy == 0) {
-        const int G = rpx(ref, W, H, x, y);
+        const int G = px(x, y);
         if (fx == 0) return G;
         const int b = hb(x, y);
-        return fx == 2 ? b : ((fx == 1 ? G : rpx(ref, W, H, x + 1, y)) + b + 1) >> 1;
+        return fx == 2 ? b : ((fx == 1 ? G : px(x + 1, y)) + b + 1) >> 1;
     }
     if (fx == 0) {
         const int h = vb(x, y);
-        return fy == 2 ? h : ((fy == 1 ? rpx(ref, W, H, x, y) : rpx(ref, W, H, x, y + 1)) + h + 1) >> 1;
+        return fy == 2 ? h : ((fy == 1 ? px(x, y) : px(x, y + 1)) + h + 1) >> 1;
     }
     if ((fx & 1) && (fy & 1)) return (hb(x, fy == 1 ? y : y + 1) + vb(fx == 1 ? x : x + 1, y) + 1) >> 1;   // e g p r
     int j1 = 0;
 #pragma unroll
-    for (int k = 0; k < 6; k++) j1 += (k == 0 || k == 5 ? 1 : (k == 1 || k == 4 ? -5 : 20)) * vh1(ref, W, H, x - 2 + k, y);
+    for (int k = 0; k < 6; k++) j1 += (k == 0 || k == 5 ? 1 : (k == 1 || k == 4 ? -5 : 20)) * vh1p(x - 2 + k, y);
     const int j = clip255((j1 + 512) >> 10);
     if (fx == 2 && fy == 2) return j;
     const int o = fx == 2 ? hb(x, fy == 1 ? y : y + 1) : vb(fx == 1 ? x : x + 1, y);   // f q / i k
     return (j + o + 1) >> 1;
+}
+// ... straight from the reference picture in HBM, spec coordinate clamping (k_mb_final MC)
+__device__ __forceinline__ int qpel_direct(const uint8_t *ref, int W, int H, int X, int Y) {
+    return qpel_from([&](int x, int y) { return rpx(ref, W, H, x, y); }, X, Y);
 }
 
 __device__ __forceinline__ int spiral_index(int x, int y) {

@@ -73,6 +73,7 @@ struct TickArgs {
     unsigned long long *prof;
     int prof_mb;
     unsigned long long *bprof;           // debug (JMH_BLOCK_PROF): per-block start / end / role
+    int me_in_analyse;                   // 1: k_mb_analyse runs the FFS searches; 0: k_mb_me_full did
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
     PicParams p[PMAX];

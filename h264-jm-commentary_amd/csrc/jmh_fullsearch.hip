@@ -1,0 +1,219 @@
+// jmh_fullsearch.hip — k_mb_me_full: the motion-search half of encode_one_macroblock [J] with
+// SearchMode = -1 (FullPelBlockMotionSearch), one 256-thread workgroup per P macroblock.
+//
+// Unlike FFS, every search centres its window on its OWN predictor (MVP/4 clamped to its range),
+// so there is no shared SAD table: each of the 41 searches computes the SAD of its block at all
+// (2*range+1)^2 positions straight from an LDS window that covers every block's reach (MB +-
+// (2*SR + 4): block offset <= range + |centre| <= 2*SR, sub-pel and 6-tap margin).  cost =
+// lambda*(mvbits(x) + mvbits(y)) - 16*lambda for the 16x16 zero vector + SAD, key = cost <<
+// 13 | spiral index, strict '<' (FullPelBlockMotionSearch [J]).  Sub-pel samples come from the
+// same window through the 6-tap on the fly (qpel_from), candidate SATD sums by LDS atomics.
+//
+// The searches run in JM's order (16x16, 16x8, 8x16, then per 8x8 block the sub-modes 4..7),
+// which is dependency-exact by construction.  The results land in MbScratch exactly like
+// k_mb_analyse's FFS search, so the intra workgroups and k_mb_final are shared.
+#include "jmh_common.h"
+
+#define NTF 256                               // threads per full-search workgroup
+#define FOFF_MAX (2 * SRMAX + 4)              // window margin around the MB
+#define FW_MAX (16 + 2 * FOFF_MAX)            // 152
+#define FST 156                               // window row stride (>= FW_MAX + 4, multiple of 4)
+#define FKOFF 4096                            // cost offset in keys (16x16 zero-vector bias)
+
+struct FullS {
+    uint8_t g[FW_MAX * FST + 16];
+    uint8_t org[256];
+    Border bd;
+    int16_t all_mv[8][16][2];
+    int motion_cost[8][4];
+    unsigned red[NTF / 64];
+    int ccost[9];
+};
+
+// neighbour view of a search of block type bt in 8x8 block b8 (as NbMe in jmh_analyse.hip)
+struct NbFull {
+    const FullS &s;
+    int bt, b8, best8x8;
+    __device__ __forceinline__ bool operator()(int xN, int yN, int &ref, int &mx, int &my) const {
+        if (yN > 15 || (xN > 15 && yN >= 0)) return false;
+        if (xN < 0 || yN < 0) {
+            int c = border_cell(xN, yN);
+            if (c < 0 || s.bd.ref[c] == -2) return false;
+            ref = s.bd.ref[c]; mx = s.bd.mv[c][0]; my = s.bd.mv[c][1];
+            return true;
+        }
+        int k = (yN >> 2) * 4 + (xN >> 2), cb8 = ((yN >> 3) << 1) | (xN >> 3);
+        int m = (bt <= 3 || cb8 == b8) ? bt : (best8x8 >> (4 * cb8)) & 15;
+        ref = 0; mx = s.all_mv[m][k][0]; my = s.all_mv[m][k][1];
+        return true;
+    }
+};
+
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t *p) {   // 4 bytes at any LDS address
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+// BlockMotionSearch [J] for one block: full-pel full search + SubPelBlockMotionSearch
+__device__ __attribute__((noinline)) void full_block_search(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int mc, int b8, int best8x8) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lam = d.lambda_motion, had = d.use_hadamard;
+    const bool slice_p = d.slice_type == JMH_P_SLICE;
+    const int range = d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr;
+    const int lw4 = lw4_of(bt), lh4 = lh4_of(bt), w4 = 1 << lw4, h4 = 1 << lh4, lns = lw4 + lh4, nsub = 1 << lns;
+    int pmx, pmy;
+    set_mvp(NbFull{s, bt, b8, best8x8}, bx4, by4, 4 * w4, 4 * h4, pmx, pmy);
+    const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
+    // ---- full pel: every thread a stride of positions, SADs by dword v_sad_u8
+    const int side = 2 * range + 1, npos = side * side;
+    unsigned kb = 0xFFFFFFFFu;
+    for (int p = tid; p < npos; p += NTF) {
+        const int dy = p / side - range, dx = p - (dy + range) * side - range;
+        const int cx = mvx0 + dx, cy = mvy0 + dy;
+        int cost = lam * (mvbits(4 * cx - pmx) + mvbits(4 * cy - pmy));
+        if (bt == 1 && slice_p && cx == 0 && cy == 0) cost -= 16 * lam;
+        const int wx = off + 4 * bx4 + cx, wy = off + 4 * by4 + cy;
+        uint32_t sad = 0;
+        for (int r = 0; r < 4 * h4; r++) {
+            const uint8_t *row = s.g + (wy + r) * FST + wx;
+            const uint32_t *org = reinterpret_cast<const uint32_t *>(s.org + (4 * by4 + r) * 16 + 4 * bx4);
+            for (int q = 0; q < w4; q++) sad = __builtin_amdgcn_sad_u8(lds_u32(row + 4 * q), org[q], sad);
+        }
+        cost += (int)sad;
+        kb = min(kb, ((unsigned)(cost + FKOFF) << 13) | (unsigned)spiral_index(dx, dy));
+    }
+    kb = wave_min_u32(kb);
+    if (lane == 0) s.red[wave] = kb;
+    __syncthreads();
+    unsigned best = s.red[0];
+#pragma unroll
+    for (int w = 1; w < NTF / 64; w++) best = min(best, s.red[w]);
+    int rx, ry;
+    spiral_pos((int)(best & 8191u), rx, ry);
+    const int fmx = mvx0 + rx, fmy = mvy0 + ry;
+    int min_mcost = had ? BIGCOST : (int)(best >> 13) - FKOFF;
+    // ---- sub pel (half then quarter), samples from the window through the 6-tap
+    const bool check0 = bt == 1 && fmx == 0 && fmy == 0 && had && slice_p;
+    auto px = [&](int x, int y) { return (int)s.g[y * FST + x]; };
+    int qx = 0, qy = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const int step = pass == 0 ? 2 : 1, min_pos = pass == 0 ? (had ? 0 : 1) : 1;
+        if (tid < 9) s.ccost[tid] = 0;
+        __syncthreads();
+        for (int task = tid; task < (9 << lns); task += NTF) {
+            const int c = task >> lns, sub = task & (nsub - 1);
+            if (c < min_pos) continue;
+            const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+            const int bxs = bx4 + (sub & (w4 - 1)), bys = by4 + (sub >> lw4);
+            int df[16];
+            for (int yy = 0; yy < 4; yy++)
+                for (int xx = 0; xx < 4; xx++)
+                    df[4 * yy + xx] = s.org[(4 * bys + yy) * 16 + 4 * bxs + xx] -
+                                      qpel_from(px, 4 * (off + 4 * bxs + xx + fmx) + ox, 4 * (off + 4 * bys + yy + fmy) + oy);
+            atomicAdd(&s.ccost[c], satd4x4(df, had));
+        }
+        __syncthreads();
+        int bpos = 0;
+        for (int c = min_pos; c < 9; c++) {   // JM order, strict '<'
+            const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+            int v = s.ccost[c] + lam * (mvbits(4 * fmx + ox - pmx) + mvbits(4 * fmy + oy - pmy));
+            if (pass == 0 && check0 && c == 0) v -= 16 * lam;
+            if (v < min_mcost) { min_mcost = v; bpos = c; }
+        }
+        qx += step * sp9x(bpos);
+        qy += step * sp9y(bpos);
+        __syncthreads();
+    }
+    if (tid < nsub) {
+        const int k = (by4 + (tid >> lw4)) * 4 + bx4 + (tid & (w4 - 1));
+        s.all_mv[bt][k][0] = (int16_t)(4 * fmx + qx);
+        s.all_mv[bt][k][1] = (int16_t)(4 * fmy + qy);
+    }
+    if (tid == 0) s.motion_cost[bt][mc] += min_mcost;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
+    __shared__ FullS s;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int e = tick_entry(t, b);
+    const DevParams d = tick_params(t, e);
+    const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
+    const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, sr = d.sr;
+    const int off = 2 * sr + 4, wdim = 16 + 2 * off;
+    MbScratch *scr = d.scr + mby * d.mbw + mbx;
+    s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    if (tid < 10) load_border(d, s.bd, tid, mbx, mby);
+    else if (tid >= 32 && tid < 64) s.motion_cost[(tid - 32) >> 2][tid & 3] = 0;
+    {   // window: MB pixel (0,0) at (off, off); per-coordinate clamping is the spec's UMV access
+        constexpr int ND4 = FST / 4;
+        const int X0 = pix_x - off, Y0 = pix_y - off;
+        for (int task = tid; task < wdim * ND4; task += NTF) {
+            const int y = task / ND4, j = task - y * ND4, x0 = X0 + 4 * j;
+            const uint8_t *row = d.refY + iclip(0, d.H - 1, Y0 + y) * W;
+            uint32_t v;
+            if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
+                const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
+                v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
+            } else {
+                v = 0;
+                for (int q = 0; q < 4; q++)
+                    if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
+            }
+            *reinterpret_cast<uint32_t *>(s.g + y * FST + 4 * j) = v;
+        }
+    }
+    __syncthreads();
+    // PartitionMotionSearch [J] order: 16x16, 16x8 (2), 8x16 (2)
+    full_block_search(d, s, off, 1, 0, 0, 0, 0, 0);
+    full_block_search(d, s, off, 2, 0, 0, 0, 0, 0);
+    full_block_search(d, s, off, 2, 0, 2, 1, 0, 0);
+    full_block_search(d, s, off, 3, 0, 0, 0, 0, 0);
+    full_block_search(d, s, off, 3, 2, 0, 1, 0, 0);
+    // P8x8: per 8x8 block the sub-modes 4..7, then its best sub-mode (read through best8x8)
+    int best8x8 = 0, cost8x8 = 0;
+    for (int b8 = 0; b8 < 4; b8++) {
+        const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
+        full_block_search(d, s, off, 4, X, Y, b8, b8, best8x8);
+        full_block_search(d, s, off, 5, X, Y, b8, b8, best8x8);
+        full_block_search(d, s, off, 5, X, Y + 1, b8, b8, best8x8);
+        full_block_search(d, s, off, 6, X, Y, b8, b8, best8x8);
+        full_block_search(d, s, off, 6, X + 1, Y, b8, b8, best8x8);
+        full_block_search(d, s, off, 7, X, Y, b8, b8, best8x8);
+        full_block_search(d, s, off, 7, X + 1, Y, b8, b8, best8x8);
+        full_block_search(d, s, off, 7, X, Y + 1, b8, b8, best8x8);
+        full_block_search(d, s, off, 7, X + 1, Y + 1, b8, b8, best8x8);
+        int mc8 = BIGCOST, bm = 0;
+        for (int mode = 4; mode <= 7; mode++) {
+            if (!d.inter_search[mode]) continue;
+            const int c = s.motion_cost[mode][b8];
+            if (c < mc8) { mc8 = c; bm = mode; }
+        }
+        best8x8 |= bm << (4 * b8);
+        cost8x8 += mc8;
+    }
+    // results: MVs and partition costs of types 1..7, P8x8 decision, FindSkipModeMotionVector
+    for (int i = tid; i < 7 * 32; i += NTF) {
+        const int m = 1 + i / 32, k = (i & 31) >> 1, c = i & 1;
+        scr->all_mv[m][k][c] = s.all_mv[m][k][c];
+    }
+    if (tid < 28) scr->motion_cost[1 + tid / 4][tid & 3] = s.motion_cost[1 + tid / 4][tid & 3];
+    else if (tid == 64) { scr->best8x8 = best8x8; scr->cost8x8 = cost8x8; }
+    else if (tid == 128) {
+        int pcx, pcy;
+        set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
+        NbBorder nbv{s.bd};
+        int ra = -1, ax = 0, ay = 0, rb = -1, bx = 0, by = 0;
+        const bool aa = nbv(-1, 0, ra, ax, ay), ab = nbv(0, -1, rb, bx, by);
+        const bool zl = !aa || (ra == 0 && ax == 0 && ay == 0), za = !ab || (rb == 0 && bx == 0 && by == 0);
+        scr->skipx = (za || zl) ? 0 : pcx;
+        scr->skipy = (za || zl) ? 0 : pcy;
+    }
+}
+
+hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st) {
+    if (t.pre[t.nP] == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mb_me_full, dim3(t.pre[t.nP]), dim3(NTF), 0, st, t);
+    return hipGetLastError();
+}

@@ -23,6 +23,7 @@
 hipError_t jmh_launch_interp(const uint8_t *ref, int W, int H, uint8_t *qpel, int qstride, int qplane, hipStream_t st);
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
                                 const int32_t *centres, uint16_t *out, hipStream_t st);
 hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
@@ -218,7 +219,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 15) || (cfg->height & 15)) return JMH_E_INVALID_ARG;
     if (cfg->search_range < 1 || cfg->search_range > 64) return JMH_E_INVALID_ARG;
     if (cfg->search_range > SRMAX) return JMH_E_UNSUPPORTED_CFG;            // LDS-resident window
-    if (cfg->search_mode != 0) return JMH_E_UNSUPPORTED_CFG;                // FFS (SearchMode 0)
+    if (cfg->search_mode != 0 && cfg->search_mode != -1) return JMH_E_UNSUPPORTED_CFG;   // FFS / full search
     if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
     if (cfg->pipeline_depth < 0 || cfg->pipeline_depth > PMAX) return JMH_E_INVALID_ARG;
@@ -335,6 +336,7 @@ static int issue_tick(jmh_ctx *c) {
     t.search_mode = c->cfg.search_mode; t.use_hadamard = c->cfg.use_hadamard; t.restrict_sr = c->cfg.restrict_search_range;
     for (int i = 0; i < 8; i++) t.inter_search[i] = c->cfg.inter_search[i];
     t.prof = c->d_prof; t.prof_mb = c->prof_mb;
+    t.me_in_analyse = c->cfg.search_mode == 0;
     int act[PMAX], nact = 0, nP = 0;
     const int nf = (int)c->fl.size();
     std::vector<int> before(nf);
@@ -368,6 +370,7 @@ static int issue_tick(jmh_ctx *c) {
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
         if (kt) HCHK(ring_begin(c->ring_an, c->st));
+        if (!t.me_in_analyse) HCHK(jmh_launch_me_full(t, c->st));   // SearchMode -1
         HCHK(jmh_launch_analyse(t, c->st));
         if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
         HCHK(jmh_launch_final(t, c->st));

@@ -142,6 +142,9 @@ def test_ippp_qcif_sr16():
     (dict(search_range=4), 0),
     (dict(search_range=4), 51),
     (dict(search_range=32), 28),
+    (dict(search_range=8, search_mode=-1), 28),                              # FullPelBlockMotionSearch
+    (dict(search_range=16, search_mode=-1, restrict_search_range=0), 30),
+    (dict(search_range=8, search_mode=-1, use_hadamard=0, inter_search=(1, 1, 0, 1, 1, 0, 1)), 36),
 ])
 def test_ipp_configs(kw, qp):
     pics = synth_seq(96, 64, 3, 7)
@@ -296,6 +299,11 @@ def run_lencod(binary, out_dir, extra):
      "LoopFilterParametersFlag=1", "LoopFilterDisable=1"],
     ["InputFile=synthetic:6", "FramesToBeEncoded=5", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
      "PipelineDepth=1"],
+    # config 1: SearchMode -1 (FullPelBlockMotionSearch), QCIF, SR 16
+    ["InputFile=synthetic:7", "FramesToBeEncoded=4", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "SearchMode=-1"],
+    ["InputFile=synthetic:8", "FramesToBeEncoded=3", "SourceWidth=320", "SourceHeight=240", "SearchRange=8",
+     "SearchMode=-1", "RestrictSearchRange=0", "UseHadamard=0"],
     ["InputFile=synthetic:5", "FramesToBeEncoded=4", "SourceWidth=320", "SourceHeight=240", "SearchRange=16",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=6", "LoopFilterBetaOffset=6", "QPFirstFrame=40",
      "QPRemainingFrame=44"],
