@@ -50,12 +50,12 @@ def load_module(name, path):
     return mod
 
 
-def cpu_baseline(jm, frames):
+def cpu_baseline(jm, frames, search_mode=0):
     """The oracle (JM restated in C, scalar -O2, 1 thread) on one full 1080p P picture."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
 
-    o = oracle_lib.OracleEncoder(W, H, search_range=SR)
+    o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode)
     _, rec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
     t0 = time.perf_counter()
     o.set_reference(*rec)                                 # UnifiedOneForthPix
@@ -63,7 +63,8 @@ def cpu_baseline(jm, frames):
     dt = time.perf_counter() - t0
     o.close()
     return {"value": round(DISP_W * DISP_H / 1e6 / dt, 4), "unit": "MP/s", "cores": 1, "kind": "port",
-            "sample": f"one 1920x1080 P picture (coded 1920x1088, 8160 MBs, FFS SR=32, QP {QP}) incl. "
+            "sample": f"one 1920x1080 P picture (coded 1920x1088, 8160 MBs, "
+                      f"{'FFS' if search_mode == 0 else 'full search'} SR=32, QP {QP}) incl. "
                       f"quarter-pel interpolation, oracle/liboracle.so -O2 scalar, {dt:.1f} s"}
 
 
@@ -81,9 +82,11 @@ def read_pmc_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=120)
+    ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--search-mode", type=int, default=0, choices=(0, -1),
+                    help="0: FFS (the BASELINE workload); -1: FullPelBlockMotionSearch variant")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -98,7 +101,7 @@ def main():
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
     streams = load_module("jmh_streams", os.path.join(PKG, "streams.py"))
     frames = [jm.synth_frame(DISP_W, DISP_H, rank, i) for i in range(3)]
-    enc = jm.Encoder(W, H, device=local, search_range=SR, slots=3, kernel_timing=True)
+    enc = jm.Encoder(W, H, device=local, search_range=SR, search_mode=args.search_mode, slots=3, kernel_timing=True)
     stream = streams.PStream(enc, frames, QP)
     dt = streams.timed_run(stream, args.steps, args.warmup, dist, on_start=enc.timing)   # on_start resets the event sums
     tm = enc.timing()                                     # event sums of the timed steps only
@@ -131,8 +134,9 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": "1080p synthetic YUV420 (coded 1920x1088), Baseline, FFS SearchMode=0 "
-                        "SearchRange=32, RestrictSearchRange=2, UseHadamard=1, 7 inter block sizes, "
+            "workload": "1080p synthetic YUV420 (coded 1920x1088), Baseline, "
+                        + ("FFS SearchMode=0" if args.search_mode == 0 else "full search SearchMode=-1")
+                        + " SearchRange=32, RestrictSearchRange=2, UseHadamard=1, 7 inter block sizes, "
                         "RDO off, QP 28, P pictures (one independent stream per GPU)",
             "global_batch": world,
             "parallelism": f"streams{world}",
@@ -166,7 +170,7 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(jm, frames)
+        out["cpu_baseline"] = cpu_baseline(jm, frames, args.search_mode)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -59,6 +59,15 @@ struct IntraNb {
     uint8_t ctop[2][12];                      // chroma rows y = -1, x = -1..7 -> [x + 1]
     uint8_t cleft[2][8];
 };
+struct IntraS {
+    uint8_t org[256];
+    uint8_t rec[256];
+    Border bd;
+    IntraNb nb;
+    int i4P[2][16];
+    int8_t ipred_cur[16];
+    int part[2][4];                           // per I4 wave: cost, cbp, blk mask
+};
 struct MeS {
     uint8_t org[256];
     Border bd;
@@ -72,15 +81,7 @@ struct MeS {
     int16_t h1[WIN_DIM_MAX * WST];            // unclipped vertical 6-tap intermediates
     unsigned long long *pst;                  // debug: per-stage stamps (thread 0), null when off
     int pn;
-};
-struct IntraS {
-    uint8_t org[256];
-    uint8_t rec[256];
-    Border bd;
-    IntraNb nb;
-    int i4P[2][16];
-    int8_t ipred_cur[16];
-    int part[2][4];                           // per I4 wave: cost, cbp, blk mask
+    IntraS in;                                // the MB's intra decisions, run by waves 6 and 7
 };
 union AnalyseS {
     MeS me;
@@ -399,8 +400,9 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
 // waves through LDS; else lane j of every wave computes search j's, then readlane), the full-pel
 // argmin over all positions by every thread (EV fills bk[] from pmx/pmy), per-wave minima -> LDS
 // -> barrier, sub-pel search j on wave j (+ forwarded MVPs), barrier.
-template <int NS, bool FWD, class EV>
-__device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &ps, const SDesc (&sd)[NS], int b8, int best8x8, EV ev) {
+template <int NS, bool FWD, class EV, class IDLE>
+__device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &ps, const SDesc (&sd)[NS], int b8, int best8x8, EV ev,
+                                         int islot, IDLE idle) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     fence_state(ps);
     int pmx[NS], pmy[NS];
@@ -431,6 +433,7 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
 #pragma unroll
     for (int j = 0; j < NS; j++)
         if (wave == j) subpel_wave(d, s, j, sd[j], pmx[j], pmy[j], ps.scx, ps.scy, b8, best8x8);
+    if (islot >= 0 && wave >= 6) idle(islot, wave - 6);   // the MB's Intra4x4 on otherwise idle waves
     __syncthreads();
     sstamp(s);
 }
@@ -476,8 +479,8 @@ __device__ __forceinline__ void sad_strip(const MeS &s, PosState &ps) {
 
 // one 8x8 block of P8x8: its 4x4 SADs, 4 stages (sub-modes 4..7 in parallel, then the 4x4
 // chain), then the P8x8 sub-mode decision for the block (its MVs are read through best8x8)
-template <int B8>
-__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8) {
+template <int B8, class IDLE>
+__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8, IDLE idle) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
     const int sr = d.sr, lam = d.lambda_motion;
     fence_state(ps);
@@ -489,21 +492,23 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
                              {7, X, Y, B8, 7, X + 1, Y, 2}};
         me_stage<4, false>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[4], const int (&pmx)[4], const int (&pmy)[4]) {
             EV(0, 4, X, Y); EV(1, 5, X, Y); EV(2, 6, X, Y); EV(3, 7, X, Y);
-        });
+        }, 2 + 2 * B8, idle);
     }
     {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right
         const SDesc sd[3] = {{5, X, Y + 1, B8, 0, 0, 0, 0}, {6, X + 1, Y, B8, 0, 0, 0, 0}, {7, X + 1, Y, B8, 7, X, Y + 1, 0}};
         me_stage<3, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
             EV(0, 5, X, Y + 1); EV(1, 6, X + 1, Y); EV(2, 7, X + 1, Y);
-        });
+        }, 3 + 2 * B8, idle);
     }
     {   // stage 2: 4x4 bottom-left
         const SDesc sd[1] = {{7, X, Y + 1, B8, 7, X + 1, Y + 1, 0}};
-        me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X, Y + 1); });
+        me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X, Y + 1); },
+                          B8 == 3 ? 10 : -1, idle);
     }
     {   // stage 3: 4x4 bottom-right
         const SDesc sd[1] = {{7, X + 1, Y + 1, B8, 0, 0, 0, 0}};
-        me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X + 1, Y + 1); });
+        me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X + 1, Y + 1); },
+                          -1, idle);
     }
     int mc8 = BIGCOST, bm = 0;
     for (int mode = 4; mode <= 7; mode++) {
@@ -577,6 +582,8 @@ __device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraN
 // ======================================================================================
 //  motion search of one P macroblock (all 41 searches)
 // ======================================================================================
+__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int (&acc)[3], int mbx, int mby);
+
 __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int mby) {
     const int tid = threadIdx.x;
     const int W = d.W, sr = d.sr, side = d.side;
@@ -585,9 +592,14 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     PSTAMP(0);
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     if (tid == 0) { s.pst = prof ? d.prof + 20 : nullptr; s.pn = 0; }
-    if (tid < 256) s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    else if (tid >= 384 && tid < 394) load_border(d, s.bd, tid - 384, mbx, mby);
+    if (tid < 256) s.in.org[tid] = s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    else if (tid >= 384 && tid < 394) { load_border(d, s.bd, tid - 384, mbx, mby); load_border(d, s.in.bd, tid - 384, mbx, mby); }
+    else if (tid >= 472 && tid < 475) s.in.part[0][tid - 472] = 0;
     else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
+    // the MB's Intra4x4 decision (10 diagonal steps, then the results) runs on waves 6 and 7
+    // while the motion search's sub-pel waves work: slots 0..10 (intra_slot)
+    int iacc[3] = {0, 0, 0};
+    auto idle = [&](int k, int w) { intra_slot(d, s.in, scr, k, w, iacc, mbx, mby); };
     for (int i = tid; i < MVB_LEN; i += NTA) s.mvb[i] = (uint8_t)mvbits(i - MVB_OFF);
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
@@ -631,6 +643,8 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
             *reinterpret_cast<uint32_t *>(G + y * WST + 4 * j) = v;
         }
         if (tid < 32) G[wdim * WST + tid] = 0;
+        // intra neighbourhood (first read in intra slot 0, after the next barriers)
+        if (tid >= 128 && tid < 199) load_intra_nb(d, s.in.nb, tid - 128, mbx, mby);
     }
     __syncthreads();
     PSTAMP(1);
@@ -725,13 +739,13 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
                 const SDesc sd[3] = {{1, 0, 0, 0, 0, 0, 0, 0}, {2, 0, 0, 0, 2, 0, 2, 0}, {3, 0, 0, 0, 3, 2, 0, 1}};
                 me_stage<3, false>(d, s, ps, sd, 0, 0, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
                     EV(0, 1, 0, 0); EV(1, 2, 0, 0); EV(2, 3, 0, 0);
-                });
+                }, 0, idle);
             }
             {   // stage 1: 16x8 lower, 8x16 right
                 const SDesc sd[2] = {{2, 0, 2, 1, 0, 0, 0, 0}, {3, 2, 0, 1, 0, 0, 0, 0}};
                 me_stage<2, true>(d, s, ps, sd, 0, 0, [&](unsigned (&bk)[2], const int (&pmx)[2], const int (&pmy)[2]) {
                     EV(0, 2, 0, 2); EV(1, 3, 2, 0);
-                });
+                }, 1, idle);
             }
             // results: MVs of types 1..3, partition costs, FindSkipModeMotionVector
             if (tid < 96) {
@@ -752,13 +766,13 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         PSTAMP(7);
         {   // ---- P8x8: 4 x 4 stages
             int best8x8 = 0, cost8x8 = 0;
-            p8x8_block<0>(d, s, ps, best8x8, cost8x8);
+            p8x8_block<0>(d, s, ps, best8x8, cost8x8, idle);
             PSTAMP(3);
-            p8x8_block<1>(d, s, ps, best8x8, cost8x8);
+            p8x8_block<1>(d, s, ps, best8x8, cost8x8, idle);
             PSTAMP(4);
-            p8x8_block<2>(d, s, ps, best8x8, cost8x8);
+            p8x8_block<2>(d, s, ps, best8x8, cost8x8, idle);
             PSTAMP(5);
-            p8x8_block<3>(d, s, ps, best8x8, cost8x8);
+            p8x8_block<3>(d, s, ps, best8x8, cost8x8, idle);
             if (tid < 128) {
                 const int m = 4 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
                 scr->all_mv[m][k][c] = s.all_mv[m][k][c];
@@ -848,7 +862,7 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratc
 
 // one MB on 128 threads (tid = 0..127, waves 0 and 1 of the group); every thread of the
 // workgroup reaches the same barriers (act: the group has an MB)
-__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act) {
+__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act, bool i4) {
     const int wave = tid >> 6, lane = tid & 63;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
@@ -875,19 +889,19 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     for (int dg = 0; dg < 10; dg++) {         // blocks with bx4 + 2*by4 == dg, by4 ascending
         const int by_lo = dg > 3 ? (dg - 2) >> 1 : 0;
         const int by4 = by_lo + wave, bx4 = dg - 2 * by4;
-        if (act && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+        if (act && i4 && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
         __syncthreads();
     }
     if (act && lane == 0) { s.part[wave][0] = acc[0]; s.part[wave][1] = acc[1]; s.part[wave][2] = acc[2]; }
     __syncthreads();
     if (!act) return;
-    if (tid == 0) {
+    if (i4 && tid == 0) {
         scr->i4cost = 24 * d.lambda_mode + s.part[0][0] + s.part[1][0];   // 4 x (int)floor(6*lambda+0.4999)
         scr->i4cbp = s.part[0][1] | s.part[1][1];
         scr->i4blk = s.part[0][2] | s.part[1][2];
     }
-    if (tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
-    if (tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
+    if (i4 && tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
+    if (i4 && tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
     PSTAMP(13);
     // Intra16x16 (wave 0) and intra chroma mode (wave 1) decisions
     if (wave == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
@@ -895,10 +909,42 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     PSTAMP(14);
 }
 
+// the Intra4x4 decision inside a motion-search workgroup, on its waves 6 and 7 (w = wave - 6)
+// while the sub-pel waves of a stage work; steps are separated by the stage barriers.  Slot
+// k = 0..9: diagonal k of the 4x4 grid; slot 10: the totals and results.
+__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int (&acc)[3], int mbx, int mby) {
+    const int lane = threadIdx.x & 63;
+    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
+    if (k < 10) {
+        const int q_bits = 15 + d.qp / 6;
+        const int qpk = d.slice_type == JMH_P_SLICE ? (1 << q_bits) / 6 : (1 << q_bits) / 3;
+        int tab[3];
+#pragma unroll
+        for (int it = 0; it < 3; it++) {
+            const int m = 4 * it + ((lane >> 4) & 3);
+            tab[it] = m < 9 ? c_i4tab[m][lane & 15] : 0;
+        }
+        const int by_lo = k > 3 ? (k - 2) >> 1 : 0;
+        const int by4 = by_lo + w, bx4 = k - 2 * by4;
+        if (by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, w, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+        if (k == 9 && lane == 0) { atomicAdd(&s.part[0][0], acc[0]); atomicOr(&s.part[0][1], acc[1]); atomicOr(&s.part[0][2], acc[2]); }
+    } else if (w == 0) {
+        if (lane == 0) {
+            scr->i4cost = 24 * d.lambda_mode + s.part[0][0];   // 4 x (int)floor(6*lambda+0.4999)
+            scr->i4cbp = s.part[0][1];
+            scr->i4blk = s.part[0][2];
+        }
+        if (lane < 16) scr->ipred[lane] = s.ipred_cur[lane];
+        reinterpret_cast<uint32_t *>(scr->i4rec)[lane] = reinterpret_cast<const uint32_t *>(s.rec)[lane];
+    }
+}
+
 __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     __shared__ AnalyseS s;
-    // blocks: [0, nPm) the motion search of each P picture MB (longest, dispatched first), then
-    // the intra decisions of every MB, four MBs (128 threads each) per workgroup
+    // blocks: [0, nPm) the motion search of each P picture MB with its Intra4x4 decision (longest,
+    // dispatched first), then intra workgroups over every MB, four MBs (128 threads each) per
+    // workgroup: Intra16x16 + chroma decisions, and Intra4x4 for MBs without a motion-search
+    // workgroup (I pictures; SearchMode -1, where k_mb_me_full searched)
     const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0, tot = t.pre[t.npic], b = blockIdx.x;
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
     const int role = b < nPm ? 2 : 0;
@@ -913,7 +959,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
         const int e = tick_entry(t, act ? q : 0);
         const DevParams d = tick_params(t, e);
         const int mby = d.y_min + ((act ? q : t.pre[e]) - t.pre[e]), mbx = d.diag - 2 * mby;
-        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act);
+        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act, q >= nPm);
     }
     if (t.bprof) {
         __syncthreads();

@@ -12,12 +12,14 @@
 #define NTA 512                          // threads per analysis workgroup (8 waves, 2 per SIMD)
 #define BIGCOST (1 << 20)
 #define PMAX 20                          // pictures per wavefront tick (pipelined pictures in flight)
-// A picture's macroblock (x, y) reads its reference inside MB columns x-5..x+5 and rows y-5..y+5:
-// window centre |MVP/4| <= SR, positions +-SR around it, +-3/4 sub-pel and the 6-tap (|dx| <= 68
-// px for SR 32).  The reference MB (x', y') is final (deblocked) once the final kernel of its
-// bottom neighbour (diagonal x' + 2y' + 2) has run, so picture q may run diagonal d once picture
-// q-1 has completed diagonals <= d + 5 + 10 + 2: a lag of PIPE_LAG diagonals.
-#define PIPE_LAG 18
+// A picture's macroblock (x, y) reads its reference (the previous picture, deblocked) at pixel
+// offsets -68..+83 from the MB origin: window centre |MVP/4| <= SR, positions +-SR around it,
+// +-3/4 sub-pel, the 6-tap support and the LDS window margin (SR 32).  The farthest samples, rows
+// and columns 0..3 of MB (x+5, y+5), are final once that MB's own final kernel (DeblockMb of its
+// left and top edges) has run; samples 13..15 of MBs x+4 / y+4 wait for the same MB.  So picture q
+// may run diagonal d once picture q-1 has completed diagonal (x+5) + 2(y+5) = d + 15: a lag of
+// PIPE_LAG diagonals (tests/test_gpu_parity.py checks pipelined == sequential at the window edge).
+#define PIPE_LAG 16
 
 // Per-macroblock analysis results, written by k_mb_analyse (three roles on separate
 // workgroups) and consumed by k_mb_final on the same wavefront diagonal.

@@ -365,7 +365,7 @@ static int issue_tick(jmh_ctx *c) {
     t.npic = k; t.nP = nP; t.pre[k] = mbs;
     if (c->d_bprof && c->ticks_total == c->bprof_tick) {
         t.bprof = c->d_bprof;
-        c->bprof_blocks = t.pre[nP] + (t.pre[k] + 3) / 4;
+        c->bprof_blocks = (t.me_in_analyse ? t.pre[nP] : 0) + (t.pre[k] + 3) / 4;
     }
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing

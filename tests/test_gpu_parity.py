@@ -238,11 +238,14 @@ def run_chain(enc, pics, qp, dbk, pipelined):
     return out
 
 
-@pytest.mark.parametrize("w,h,sr,n", [(176, 144, 16, 9), (320, 240, 32, 8), (1920, 1088, 32, 20)])
-def test_pipelined_chain_equals_sequential(w, h, sr, n):
+@pytest.mark.parametrize("w,h,sr,n,step", [(176, 144, 16, 9, (37, -29)), (320, 240, 32, 8, (37, -29)),
+                                           (1920, 1088, 32, 20, (37, -29)), (1920, 1088, 32, 12, (-62, -61)),
+                                           (640, 480, 32, 10, (63, 62))])
+def test_pipelined_chain_equals_sequential(w, h, sr, n, step):
     """Pictures in flight together (lag PIPE_LAG diagonals) == one picture at a time, bit for
-    bit, under motion that pushes MVs to the search-window edge."""
-    pics = moving_seq(w, h, n, seed=w + n)
+    bit, under motion that pushes MVs to the search-window edge (|MV| up to 63 px at SR 32: the
+    reference is read up to 67 px beyond the MB, the reach PIPE_LAG is derived from)."""
+    pics = moving_seq(w, h, n, seed=w + n, step=step)
     dbk = (0, 0, 0)
     a = jmhip.Encoder(w, h, search_range=sr)                       # auto depth
     b = jmhip.Encoder(w, h, search_range=sr, pipeline_depth=1)
