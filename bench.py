@@ -18,6 +18,7 @@ import argparse
 import importlib.util
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -50,22 +51,56 @@ def load_module(name, path):
     return mod
 
 
-def cpu_baseline(jm, frames, search_mode=0):
-    """The oracle (JM restated in C, scalar -O2, 1 thread) on one full 1080p P picture."""
+def cpu_one_picture(seed, search_mode):
+    """Seconds the oracle (JM restated in C, scalar -O2, one thread) takes for one 1080p P picture
+    of stream `seed` (UnifiedOneForthPix + encode_one_macroblock x 8160).  Runs in a child
+    process (bench.py --cpu-worker): no GPU is touched."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
-
+    jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
+    frames = [jm.synth_frame(DISP_W, DISP_H, seed, i) for i in range(2)]
     o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode)
     _, rec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
     t0 = time.perf_counter()
-    o.set_reference(*rec)                                 # UnifiedOneForthPix
-    o.encode(*frames[1], jm.JMH_P_SLICE, QP)              # encode_one_macroblock x 8160
+    o.set_reference(*rec)
+    o.encode(*frames[1], jm.JMH_P_SLICE, QP)
     dt = time.perf_counter() - t0
     o.close()
-    return {"value": round(DISP_W * DISP_H / 1e6 / dt, 4), "unit": "MP/s", "cores": 1, "kind": "port",
-            "sample": f"one 1920x1080 P picture (coded 1920x1088, 8160 MBs, "
-                      f"{'FFS' if search_mode == 0 else 'full search'} SR=32, QP {QP}) incl. "
-                      f"quarter-pel interpolation, oracle/liboracle.so -O2 scalar, {dt:.1f} s"}
+    return dt
+
+
+def cpu_workers(n, search_mode):
+    """n concurrent child processes (distinct seeds); their per-picture seconds."""
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(k), str(search_mode)],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True) for k in range(n)]
+    return [float(p.communicate()[0].split()[-1]) for p in procs]
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(search_mode=0):
+    """The CPU path timed on this node's host cores: one process on one core (JM is
+    single threaded; the reported baseline), and n processes on distinct streams at once
+    (aggregate, n = min(16, cores available to this process))."""
+    one = cpu_workers(1, search_mode)[0]
+    n = max(1, min(16, len(os.sched_getaffinity(0))))
+    many = cpu_workers(n, search_mode)
+    mode = "FFS" if search_mode == 0 else "full search"
+    return {"value": round(DISP_W * DISP_H / 1e6 / one, 4), "unit": "MP/s", "cores": 1, "kind": "port",
+            "sample": f"one 1920x1080 P picture (coded 1920x1088, 8160 MBs, {mode} SR=32, QP {QP}) incl. "
+                      f"quarter-pel interpolation, oracle/liboracle.so -O2 scalar, {one:.1f} s, on {cpu_model()}",
+            "all_cores": {"value": round(n * DISP_W * DISP_H / 1e6 / max(many), 4), "unit": "MP/s", "cores": n,
+                          "sample": f"{n} processes, one P picture each on distinct streams, concurrently, "
+                                    f"{max(many):.1f} s wall"}}
 
 
 def read_pmc_traffic():
@@ -80,6 +115,9 @@ def read_pmc_traffic():
 
 
 def main():
+    if len(sys.argv) == 4 and sys.argv[1] == "--cpu-worker":    # child of cpu_baseline()
+        print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[3])), flush=True)
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
@@ -170,7 +208,7 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(jm, frames, args.search_mode)
+        out["cpu_baseline"] = cpu_baseline(args.search_mode)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
