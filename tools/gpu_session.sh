@@ -13,7 +13,7 @@ timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/${TAG}_bench.log
 [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}" -o ${TAG} --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}" -o ${TAG} --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1
 rc=$?; echo "prof rc=$rc"
 find gpurun_out/prof_${TAG} -name "*kernel_stats*" -exec cat {} \;
 exit $rc
