@@ -157,7 +157,8 @@ __device__ __forceinline__ unsigned psum(const uint32_t (&r)[2]) {
 // per-thread search state: SADs of the thread's NPK positions and their JM order keys
 struct PosState {
     uint32_t sadp[NPK][2];
-    uint32_t ordk[NPK];      // JM order (0 = (0,0) pre-check); 0xFFFFFFFF for slots outside the table
+    uint32_t ordk2[NPK / 2]; // JM order of positions 2i (low half) and 2i+1 (high half): 0 = (0,0)
+                             // pre-check, else spiral index + 1; 0xFFFF for slots outside the table
     int dx, dy0;
     int scx, scy;            // window centre (full pel, relative to the MB)
 };
@@ -169,8 +170,16 @@ __device__ __forceinline__ void fence_state(PosState &ps) {
     for (int k = 0; k < NPK; k++) {
 #pragma unroll
         for (int q = 0; q < 2; q++) asm volatile("" : "+v"(ps.sadp[k][q]));
-        asm volatile("" : "+v"(ps.ordk[k]));
     }
+#pragma unroll
+    for (int k = 0; k < NPK / 2; k++) asm volatile("" : "+v"(ps.ordk2[k]));
+}
+
+// order key of position k, sign-extended: a slot outside the table gives 0xFFFFFFFF, which ORed
+// into any key loses every comparison
+__device__ __forceinline__ uint32_t ordk_of(const PosState &ps, int k) {
+    const uint32_t w = ps.ordk2[k >> 1];
+    return (k & 1) ? (uint32_t)((int)w >> 16) : (uint32_t)(int)(int16_t)(w & 0xFFFFu);
 }
 
 // this thread's best key for a search of partition (BT, BX, BY) with predictor (pmx, pmy):
@@ -186,15 +195,16 @@ __device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
             const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + lam * cy[4 * k];
-            b = min(b, (cost << 13) | ps.ordk[k]);
+            b = min(b, (cost << 13) | ordk_of(ps, k));
         }
     } else {
         const int rx = abs(ps.dx - sr);
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
             const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + lam * cy[4 * k];
-            const bool in = max(rx, abs(ps.dy0 + k - sr)) <= range || ps.ordk[k] == 0;
-            b = min(b, in ? (cost << 13) | ps.ordk[k] : 0xFFFFFFFFu);
+            const uint32_t o = ordk_of(ps, k);
+            const bool in = max(rx, abs(ps.dy0 + k - sr)) <= range || o == 0;
+            b = min(b, in ? (cost << 13) | o : 0xFFFFFFFFu);
         }
     }
     return b;
@@ -582,7 +592,7 @@ __device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraN
 // ======================================================================================
 //  motion search of one P macroblock (all 41 searches)
 // ======================================================================================
-__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int (&acc)[3], int mbx, int mby);
+__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int mbx, int mby);
 
 __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int mby) {
     const int tid = threadIdx.x;
@@ -594,12 +604,11 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     if (tid == 0) { s.pst = prof ? d.prof + 20 : nullptr; s.pn = 0; }
     if (tid < 256) s.in.org[tid] = s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     else if (tid >= 384 && tid < 394) { load_border(d, s.bd, tid - 384, mbx, mby); load_border(d, s.in.bd, tid - 384, mbx, mby); }
-    else if (tid >= 472 && tid < 475) s.in.part[0][tid - 472] = 0;
+    else if (tid >= 472 && tid < 478) s.in.part[(tid - 472) / 3][(tid - 472) % 3] = 0;
     else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
     // the MB's Intra4x4 decision (10 diagonal steps, then the results) runs on waves 6 and 7
     // while the motion search's sub-pel waves work: slots 0..10 (intra_slot)
-    int iacc[3] = {0, 0, 0};
-    auto idle = [&](int k, int w) { intra_slot(d, s.in, scr, k, w, iacc, mbx, mby); };
+    auto idle = [&](int k, int w) { intra_slot(d, s.in, scr, k, w, mbx, mby); };
     for (int i = tid; i < MVB_LEN; i += NTA) s.mvb[i] = (uint8_t)mvbits(i - MVB_OFF);
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
@@ -667,9 +676,12 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
             const int dy = ps.dy0 + k, rx = ps.dx - sr, ry = dy - sr;
-            if (!sact || dy >= side) ps.ordk[k] = 0xFFFFFFFFu;
-            else if (rx == -scx && ry == -scy) ps.ordk[k] = 0;   // the (0,0) pre-check position
-            else ps.ordk[k] = (uint32_t)(spiral_index(rx, ry) + 1);
+            uint32_t o;
+            if (!sact || dy >= side) o = 0xFFFFu;
+            else if (rx == -scx && ry == -scy) o = 0;   // the (0,0) pre-check position
+            else o = (uint32_t)(spiral_index(rx, ry) + 1);
+            if (k & 1) ps.ordk2[k >> 1] |= o << 16;
+            else ps.ordk2[k >> 1] = o;
         }
         PSTAMP(9);
         // ---- half-pel planes over window rows / columns [3, 2sr+21): four columns (one dword) per
@@ -912,7 +924,7 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
 // the Intra4x4 decision inside a motion-search workgroup, on its waves 6 and 7 (w = wave - 6)
 // while the sub-pel waves of a stage work; steps are separated by the stage barriers.  Slot
 // k = 0..9: diagonal k of the 4x4 grid; slot 10: the totals and results.
-__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int (&acc)[3], int mbx, int mby) {
+__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int mbx, int mby) {
     const int lane = threadIdx.x & 63;
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
     if (k < 10) {
@@ -926,13 +938,16 @@ __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScra
         }
         const int by_lo = k > 3 ? (k - 2) >> 1 : 0;
         const int by4 = by_lo + w, bx4 = k - 2 * by4;
-        if (by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, w, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
-        if (k == 9 && lane == 0) { atomicAdd(&s.part[0][0], acc[0]); atomicOr(&s.part[0][1], acc[1]); atomicOr(&s.part[0][2], acc[2]); }
+        if (by4 <= 3 && bx4 >= 0 && bx4 <= 3) {   // the wave's running cost / cbp / block mask live in LDS
+            int acc[3] = {s.part[w][0], s.part[w][1], s.part[w][2]};
+            i4_block(d, s, scr, w, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+            if (lane == 0) { s.part[w][0] = acc[0]; s.part[w][1] = acc[1]; s.part[w][2] = acc[2]; }
+        }
     } else if (w == 0) {
         if (lane == 0) {
-            scr->i4cost = 24 * d.lambda_mode + s.part[0][0];   // 4 x (int)floor(6*lambda+0.4999)
-            scr->i4cbp = s.part[0][1];
-            scr->i4blk = s.part[0][2];
+            scr->i4cost = 24 * d.lambda_mode + s.part[0][0] + s.part[1][0];   // 4 x (int)floor(6*lambda+0.4999)
+            scr->i4cbp = s.part[0][1] | s.part[1][1];
+            scr->i4blk = s.part[0][2] | s.part[1][2];
         }
         if (lane < 16) scr->ipred[lane] = s.ipred_cur[lane];
         reinterpret_cast<uint32_t *>(scr->i4rec)[lane] = reinterpret_cast<const uint32_t *>(s.rec)[lane];
