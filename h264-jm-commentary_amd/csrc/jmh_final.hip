@@ -326,7 +326,7 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
         }
         res->i16mode = (int8_t)(best_mode == JMH_I16MB ? i16mode : 0);
         res->c_ipred_mode = (int8_t)c_mode;
-        res->pad0[0] = res->pad0[1] = 0;
+        res->transform_8x8 = 0; res->pad0 = 0;
         res->min_cost = min_cost;
         res->reserved = 0;
     }

@@ -58,6 +58,13 @@ void jm_write_sps(jm_bits *b, const jm_seq *s) {
     jm_put(b, 0, 8);                         /* constraint_set0..3 = 0, reserved_zero_4bits */
     jm_put(b, s->level_idc, 8);
     jm_put_ue(b, 0);                         /* seq_parameter_set_id */
+    if (s->profile_idc >= 100) {             /* High: 4:2:0, 8 bit, no scaling matrices */
+        jm_put_ue(b, 1);                     /* chroma_format_idc */
+        jm_put_ue(b, 0);                     /* bit_depth_luma_minus8 */
+        jm_put_ue(b, 0);                     /* bit_depth_chroma_minus8 */
+        jm_put(b, 0, 1);                     /* qpprime_y_zero_transform_bypass_flag */
+        jm_put(b, 0, 1);                     /* seq_scaling_matrix_present_flag */
+    }
     jm_put_ue(b, s->log2_max_frame_num - 4);
     jm_put_ue(b, 0);                         /* pic_order_cnt_type */
     jm_put_ue(b, s->log2_max_poc_lsb - 4);
@@ -95,6 +102,11 @@ void jm_write_pps(jm_bits *b, const jm_seq *s) {
     jm_put(b, s->lf_params_flag, 1);         /* deblocking_filter_control_present_flag */
     jm_put(b, s->constrained_intra, 1);
     jm_put(b, 0, 1);                         /* redundant_pic_cnt_present_flag */
+    if (s->profile_idc >= 100) {             /* PPS range extension (High) */
+        jm_put(b, s->transform_8x8_mode ? 1 : 0, 1);   /* transform_8x8_mode_flag */
+        jm_put(b, 0, 1);                     /* pic_scaling_matrix_present_flag */
+        jm_put_se(b, s->chroma_qp_offset);   /* second_chroma_qp_index_offset */
+    }
     jm_trailing_bits(b);
 }
 
@@ -290,7 +302,8 @@ static int calc_nc(const wctx *w, int mx, int my, int comp, int x4, int y4, cons
 
 static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r, int slice_p) {
     int mbt = r->mb_type, cbp = r->cbp, W4 = w->s->mbw * 4;
-    int is_i4 = mbt == JMH_I4MB, is_i16 = mbt == JMH_I16MB, is_intra = is_i4 || is_i16;
+    int is_i8 = mbt == JMH_I8MB, is_i4 = mbt == JMH_I4MB || is_i8, is_i16 = mbt == JMH_I16MB;
+    int is_intra = is_i4 || is_i16, t8 = r->transform_8x8;   /* is_i4: I_NxN (4x4 or 8x8) */
     int cbpl = cbp & 15, cbpc = cbp >> 4;
     /* mark the MB's final motion / intra data (needed by its own MVP / MPM derivations) */
     for (int k = 0; k < 16; k++) {
@@ -311,7 +324,21 @@ static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r,
     jm_put_ue(b, ue_type);
     if (mbt == JMH_P8x8)
         for (int i = 0; i < 4; i++) jm_put_ue(b, r->b8mode[i] - 4);
-    if (is_i4) {
+    if (is_i4 && w->s->transform_8x8_mode) jm_put(b, is_i8, 1);   /* transform_size_8x8_flag */
+    if (is_i8) {
+        for (int b8 = 0; b8 < 4; b8++) {           /* prev_intra8x8_pred_mode / rem (8.3.2.1) */
+            int x4 = (b8 & 1) * 2, y4 = (b8 >> 1) * 2, ia = 0, ib = 0;
+            int aa = nb(w, mx, my, 4 * x4 - 1, 4 * y4, &ia, 1), ab = nb(w, mx, my, 4 * x4, 4 * y4 - 1, &ib, 1);
+            int pred = 2;
+            if (aa && ab) {
+                int ma = w->ipm[ia] < 0 ? 2 : w->ipm[ia], mb = w->ipm[ib] < 0 ? 2 : w->ipm[ib];
+                pred = ma < mb ? ma : mb;
+            }
+            int m = r->ipred[y4 * 4 + x4];
+            if (m == pred) jm_put(b, 1, 1);
+            else { jm_put(b, 0, 1); jm_put(b, m < pred ? m : m - 1, 3); }
+        }
+    } else if (is_i4) {
         for (int blk = 0; blk < 16; blk++) {
             int x4 = ((blk >> 2) & 1) * 2 + (blk & 1), y4 = (blk >> 3) * 2 + ((blk >> 1) & 1);
             int ia = 0, ib = 0;
@@ -342,6 +369,10 @@ static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r,
         }
     }
     if (!is_i16) jm_put_ue(b, is_i4 ? cbp_intra_code[cbp] : cbp_inter_code[cbp]);
+    /* transform_size_8x8_flag of inter MBs: luma coded, no sub-8x8 partitions (7.3.5) */
+    if (!is_intra && cbpl && w->s->transform_8x8_mode &&
+        (mbt != JMH_P8x8 || (r->b8mode[0] == 4 && r->b8mode[1] == 4 && r->b8mode[2] == 4 && r->b8mode[3] == 4)))
+        jm_put(b, t8, 1);
     uint8_t *tc = w->tc + (size_t)(my * w->s->mbw + mx) * 24;
     memset(tc, 0, 24);
     if (cbp > 0 || is_i16) {

@@ -48,6 +48,7 @@ static const map_entry Map[] = {
     {"InterSearch4x4", 0, OFF(inter_search[7]), 0, 1},
     {"RDOptimization", 0, OFF(rdopt), 0, 2},
     {"ProfileIDC", 0, OFF(profile_idc), 66, 144},
+    {"Transform8x8Mode", 0, OFF(transform_8x8_mode), 0, 2},
     {"LevelIDC", 0, OFF(level_idc), 9, 62},
     {"SymbolMode", 0, OFF(symbol_mode), 0, 1},
     {"LoopFilterParametersFlag", 0, OFF(lf_params_flag), 0, 1},
@@ -160,7 +161,9 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->search_mode != 0 && inp->search_mode != -1) { snprintf(err, errlen, "SearchMode=%d not supported (use -1 or 0)", inp->search_mode); return -1; }
     if (inp->num_ref_frames != 1) { snprintf(err, errlen, "NumberReferenceFrames=%d not supported (1)", inp->num_ref_frames); return -1; }
     if (inp->constrained_intra) { snprintf(err, errlen, "UseConstrainedIntraPred=1 not supported"); return -1; }
-    if (inp->profile_idc != 66) { snprintf(err, errlen, "ProfileIDC=%d not supported (66)", inp->profile_idc); return -1; }
+    if (inp->profile_idc != 66 && inp->profile_idc != 100) { snprintf(err, errlen, "ProfileIDC=%d not supported (66 or 100)", inp->profile_idc); return -1; }
+    if (inp->transform_8x8_mode == 2) { snprintf(err, errlen, "Transform8x8Mode=2 not supported (0 or 1)"); return -1; }
+    if (inp->transform_8x8_mode && inp->profile_idc < 100) { snprintf(err, errlen, "Transform8x8Mode=1 requires ProfileIDC=100 (High)"); return -1; }
     if ((inp->width & 1) || (inp->height & 1)) { snprintf(err, errlen, "Source size must be even"); return -1; }
     return 0;
 }
@@ -200,4 +203,5 @@ void jm_fill_config(const jm_input *inp, jmh_config *cfg) {
     cfg->constrained_intra_pred = inp->constrained_intra;
     cfg->num_frame_slots = 2;
     cfg->pipeline_depth = inp->pipeline_depth;
+    cfg->transform_8x8_mode = inp->transform_8x8_mode;
 }

@@ -28,7 +28,7 @@ static const uint8_t QPC[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 
 static inline int clip3(int lo, int hi, int v) { return v < lo ? lo : v > hi ? hi : v; }
 static inline int iabs_(int v) { return v < 0 ? -v : v; }
 
-static int is_intra(const jmh_mb_result *r) { return r->mb_type == JMH_I4MB || r->mb_type == JMH_I16MB; }
+static int is_intra(const jmh_mb_result *r) { return r->mb_type == JMH_I4MB || r->mb_type == JMH_I16MB || r->mb_type == JMH_I8MB; }
 static int has_coef(const jmh_mb_result *r, int blk) {   /* 4x4 luma block (raster) coded */
     if (r->mb_type == JMH_I16MB) return 1;              /* intra: bS >= 3 anyway            */
     return (r->cbp_blk >> blk) & 1;
@@ -95,6 +95,7 @@ void jm_deblock_picture(jm_pic *p, const jm_seq *s, const jmh_mb_result *const *
             for (int dir = 0; dir < 2; dir++) {       /* 0: vertical edges, 1: horizontal */
                 for (int e = 0; e < 4; e++) {
                     int mb_edge = e == 0;
+                    if ((e & 1) && rq->transform_8x8) continue;   /* 8x8 transform: no 4x4 luma edges */
                     const jmh_mb_result *rp = rq;
                     if (mb_edge) {
                         if (dir == 0 && mx == 0) continue;

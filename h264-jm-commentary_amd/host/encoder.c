@@ -52,6 +52,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     s.lf_params_flag = inp->lf_params_flag; s.lf_disable = inp->lf_disable;
     s.lf_alpha = inp->lf_alpha; s.lf_beta = inp->lf_beta;
     s.constrained_intra = inp->constrained_intra;
+    s.transform_8x8_mode = inp->transform_8x8_mode;
 
     FILE *fin = NULL, *fout = NULL, *frec = NULL;
     uint64_t seed = 0;

@@ -36,7 +36,8 @@ typedef struct jm_input {
     int  restrict_search_range;/* RestrictSearchRange                                         */
     int  inter_search[8];      /* InterSearch16x16 .. InterSearch4x4 ([1..7])                 */
     int  rdopt;                /* RDOptimization (must be 0)                                  */
-    int  profile_idc;          /* ProfileIDC (66)                                             */
+    int  profile_idc;          /* ProfileIDC (66 Baseline, 100 High)                          */
+    int  transform_8x8_mode;   /* Transform8x8Mode (0, 1; needs ProfileIDC 100)               */
     int  level_idc;            /* LevelIDC                                                    */
     int  symbol_mode;          /* SymbolMode (0 = CAVLC)                                       */
     int  lf_params_flag;       /* LoopFilterParametersFlag                                    */
@@ -100,6 +101,7 @@ typedef struct jm_seq {
     int chroma_qp_offset;
     int lf_params_flag, lf_disable, lf_alpha, lf_beta;
     int constrained_intra;
+    int transform_8x8_mode;    /* PPS transform_8x8_mode_flag (High profile)                   */
 } jm_seq;
 
 /* NAL unit (Annex B start code + emulation prevention) appended to out */

@@ -17,7 +17,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 4
+JMH_ABI_VERSION = 5
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -37,7 +37,7 @@ class JmhConfig(ctypes.Structure):
                 ("inter_search", ctypes.c_int32 * 8), ("num_ref_frames", ctypes.c_int32),
                 ("constrained_intra_pred", ctypes.c_int32), ("num_frame_slots", ctypes.c_int32),
                 ("flags", ctypes.c_int32), ("pipeline_depth", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 5)]
+                ("transform_8x8_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
 class JmhFrameParams(ctypes.Structure):
@@ -60,7 +60,7 @@ class JmhTiming(ctypes.Structure):
 # jmh_mb_result, field for field (include/jmhip.h)
 MB_RESULT_DTYPE = np.dtype([
     ("mb_type", "<i2"), ("cbp", "<i2"), ("cbp_blk", "<i4"), ("b8mode", "i1", 4),
-    ("ref_idx", "i1", 4), ("i16mode", "i1"), ("c_ipred_mode", "i1"), ("pad0", "i1", 2),
+    ("ref_idx", "i1", 4), ("i16mode", "i1"), ("c_ipred_mode", "i1"), ("transform_8x8", "i1"), ("pad0", "i1"),
     ("ipred", "i1", 16), ("mv", "<i2", (16, 2)), ("luma", "<i2", (16, 16)),
     ("luma_dc", "<i2", 16), ("chroma_dc", "<i2", (2, 4)), ("chroma_ac", "<i2", (2, 4, 16)),
     ("min_cost", "<i4"), ("reserved", "<i4")])
@@ -131,7 +131,7 @@ def _ptr(a):
 
 def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
                 restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False,
-                pipeline_depth=0):
+                pipeline_depth=0, transform_8x8_mode=0):
     cfg = JmhConfig()
     cfg.width, cfg.height = width, height
     cfg.search_range, cfg.search_mode = search_range, search_mode
@@ -141,6 +141,7 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     cfg.num_ref_frames, cfg.constrained_intra_pred, cfg.num_frame_slots = 1, 0, slots
     cfg.flags = JMH_FLAG_KERNEL_TIMING if kernel_timing else 0
     cfg.pipeline_depth = pipeline_depth
+    cfg.transform_8x8_mode = transform_8x8_mode
     return cfg
 
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 4
+#define JMH_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define JMH_OK                 0
@@ -66,6 +66,7 @@ extern "C" {
 #define JMH_I4MB   9
 #define JMH_I16MB  10
 #define JMH_IBLOCK 11  /* b8mode[] of an I4MB */
+#define JMH_I8MB   13  /* Intra8x8 (High profile, Transform8x8Mode; JM FRExt numbering [J])       */
 
 /* ---- encoder configuration (encoder.cfg subset that the hot path reads) ----------------- */
 typedef struct jmh_config {
@@ -82,7 +83,8 @@ typedef struct jmh_config {
     int32_t flags;                  /* JMH_FLAG_* (0 for the defaults)                            */
     int32_t pipeline_depth;         /* pictures in flight at once (0: enough to fill the device,  */
                                     /*   1: one picture at a time); see jmh_frame_push            */
-    int32_t reserved[5];
+    int32_t transform_8x8_mode;     /* Transform8x8Mode: 0 off, 1 adaptive 4x4 / 8x8 (High profile) */
+    int32_t reserved[4];
 } jmh_config;
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */
@@ -107,16 +109,22 @@ typedef struct jmh_frame_params {
 typedef struct jmh_mb_result {
     int16_t mb_type;           /* JMH_PSKIP .. JMH_I16MB                                          */
     int16_t cbp;               /* luma bits 0..3 (8x8 blocks), chroma (0/1/2) << 4                */
-    int32_t cbp_blk;           /* bit (4*by+bx): 4x4 luma block has non-zero levels (I16: AC)     */
+    int32_t cbp_blk;           /* bit (4*by+bx): 4x4 luma block has non-zero levels (I16: AC);
+                                  transform_8x8: all four bits of an 8x8 block with any level      */
     int8_t  b8mode[4];         /* per 8x8: sub-mb type 4..7 for P8x8, mb_type otherwise           */
     int8_t  ref_idx[4];        /* per 8x8, list 0; -1 for intra                                  */
     int8_t  i16mode;           /* Intra16x16 prediction mode 0..3 (I16MB only)                   */
     int8_t  c_ipred_mode;      /* intra chroma prediction mode 0..3 (intra MBs)                  */
-    int8_t  pad0[2];
-    int8_t  ipred[16];         /* Intra4x4 modes, 4x4 raster order (by*4+bx); 2 (DC) if not I4MB */
+    int8_t  transform_8x8;     /* transform_size_8x8_flag (0 unless the MB codes luma with 8x8)   */
+    int8_t  pad0;
+    int8_t  ipred[16];         /* Intra4x4 modes, 4x4 raster order (by*4+bx); I8MB: the Intra8x8
+                                  mode of the 8x8 block, repeated on its four 4x4; 2 (DC) otherwise */
     int16_t mv[16][2];         /* final list-0 MV per 4x4 block (raster), quarter-pel            */
     int16_t luma[16][16];      /* per 4x4 block (raster): levels in frame zig-zag scan order;
-                                  I16MB: AC only, [k][0] = 0                                       */
+                                  I16MB: AC only, [k][0] = 0.  transform_8x8: the 8x8 block's 64
+                                  levels in 8x8 zig-zag order, interleaved as CAVLC codes them
+                                  (7.3.5.3.2): luma[4x4 j of the 8x8][k] = level8x8[4k + j], j in
+                                  0 TL, 1 TR, 2 BL, 3 BR                                            */
     int16_t luma_dc[16];       /* I16MB DC levels, zig-zag scan order                             */
     int16_t chroma_dc[2][4];   /* [uv][k] 2x2 DC levels, raster c0..c3                            */
     int16_t chroma_ac[2][4][16]; /* [uv][4x4 blk raster][scan]; [..][0] = 0                       */

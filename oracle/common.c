@@ -223,3 +223,102 @@ void jmo_inv4x4_add(const int32_t m[16], const uint8_t *pred, int pstride, uint8
             out[y * ostride + x] =
                 (uint8_t)clip255((r[4 * y + x] + (pred[y * pstride + x] << DQ_BITS) + DQ_ROUND) >> DQ_BITS);
 }
+
+/* ======================================================================================== */
+/*  8x8 transform (High profile, Transform8x8Mode) — JM FRExt block.c › dct_luma8x8 [J]      */
+/* ======================================================================================== */
+/* normAdjust8x8 position class (H.264 8.5.9): 0 (i%4==0,j%4==0), 1 (odd,odd), 2 (2 mod 4 both),
+ * 3 (0 mod 4 / odd), 4 (0 mod 4 / 2 mod 4), 5 otherwise */
+int jmo_class8(int x, int y) {
+    if (!(x & 3) && !(y & 3)) return 0;
+    if ((x & 1) && (y & 1)) return 1;
+    if ((x & 3) == 2 && (y & 3) == 2) return 2;
+    if ((!(x & 3) && (y & 1)) || ((x & 1) && !(y & 3))) return 3;
+    if ((!(x & 3) && (y & 3) == 2) || ((x & 3) == 2 && !(y & 3))) return 4;
+    return 5;
+}
+/* dequant_coef8 = normAdjust8x8 v[m][class] (H.264 Table 8-16 / 8.5.9) */
+const int jmo_dequant8_cls[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26},
+                                    {26, 23, 42, 24, 33, 31}, {28, 25, 45, 26, 35, 33},
+                                    {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+/* quant_coef8 [J] by class: q * v == 2^18 * (4x4 class norm), rounded as in JM's table */
+const int jmo_quant8_cls[6][6] = {{13107, 11428, 20972, 12222, 16777, 15481},
+                                  {11916, 10826, 19174, 11058, 14980, 14290},
+                                  {10082, 8943, 15978, 9675, 12710, 11985},
+                                  {9362, 8228, 14913, 8931, 11984, 11259},
+                                  {8192, 7346, 13159, 7740, 10486, 9777},
+                                  {7282, 6428, 11570, 6830, 9118, 8640}};
+/* COEFF_COST8x8[0] [J]: cost of a |level|==1 coefficient by preceding zero run (64-scan) */
+int jmo_coeff_cost8(int run) { return run < 4 ? 3 : run < 12 ? 2 : run < 24 ? 1 : 0; }
+
+/* SNGL_SCAN8x8 (8x8 frame zig-zag, H.264 Table 8-13... same order as JPEG): raster index */
+void jmo_scan8x8(int scan[64]) {
+    int k = 0;
+    for (int s = 0; s < 15; s++) {
+        if (s & 1) for (int x = s < 8 ? s : 7; x >= 0 && s - x < 8; x--) scan[k++] = (s - x) * 8 + x;
+        else for (int x = s < 8 ? 0 : s - 7; x <= 7 && s - x >= 0; x++) scan[k++] = (s - x) * 8 + x;
+    }
+}
+
+/* one 8-point forward butterfly (JM forward8x8 [J]) */
+static void fwd8(const int32_t *in, int st, int32_t *out, int ost) {
+    int x0 = in[0], x1 = in[st], x2 = in[2 * st], x3 = in[3 * st], x4 = in[4 * st], x5 = in[5 * st],
+        x6 = in[6 * st], x7 = in[7 * st];
+    int a0 = x0 + x7, a1 = x1 + x6, a2 = x2 + x5, a3 = x3 + x4;
+    int b0 = a0 + a3, b1 = a1 + a2, b2 = a0 - a3, b3 = a1 - a2;
+    int a4 = x0 - x7, a5 = x1 - x6, a6 = x2 - x5, a7 = x3 - x4;
+    int b4 = a5 + a6 + ((a4 >> 1) + a4), b5 = a4 - a7 - ((a6 >> 1) + a6);
+    int b6 = a4 + a7 - ((a5 >> 1) + a5), b7 = a5 - a6 + ((a7 >> 1) + a7);
+    out[0] = b0 + b1; out[ost] = b4 + (b7 >> 2); out[2 * ost] = b2 + (b3 >> 1); out[3 * ost] = b5 + (b6 >> 2);
+    out[4 * ost] = b0 - b1; out[5 * ost] = b6 - (b5 >> 2); out[6 * ost] = (b2 >> 1) - b3; out[7 * ost] = (b4 >> 2) - b7;
+}
+void jmo_fwd8x8(int32_t m[64]) {          /* raster in place: rows, then columns */
+    int32_t t[64];
+    for (int y = 0; y < 8; y++) fwd8(m + 8 * y, 1, t + 8 * y, 1);
+    for (int x = 0; x < 8; x++) fwd8(t + x, 8, m + x, 8);
+}
+/* one 8-point inverse (H.264 8.5.13.2) */
+static void inv8(const int32_t *in, int st, int32_t *out, int ost) {
+    int d0 = in[0], d1 = in[st], d2 = in[2 * st], d3 = in[3 * st], d4 = in[4 * st], d5 = in[5 * st],
+        d6 = in[6 * st], d7 = in[7 * st];
+    int a0 = d0 + d4, a4 = d0 - d4, a2 = (d2 >> 1) - d6, a6 = d2 + (d6 >> 1);
+    int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+    int a1 = -d3 + d5 - d7 - (d7 >> 1), a3 = d1 + d7 - d3 - (d3 >> 1);
+    int a5 = -d1 + d7 + d5 + (d5 >> 1), a7 = d3 + d5 + d1 + (d1 >> 1);
+    int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+    out[0] = b0 + b7; out[ost] = b2 + b5; out[2 * ost] = b4 + b3; out[3 * ost] = b6 + b1;
+    out[4 * ost] = b6 - b1; out[5 * ost] = b4 - b3; out[6 * ost] = b2 - b5; out[7 * ost] = b0 - b7;
+}
+void jmo_inverse8x8(const int32_t *in, int32_t *out) {   /* rows first, then columns */
+    int32_t t[64];
+    for (int y = 0; y < 8; y++) inv8(in + 8 * y, 1, t + 8 * y, 1);
+    for (int x = 0; x < 8; x++) inv8(t + x, 8, out + x, 8);
+}
+void jmo_inv8x8_add(const int32_t m[64], const uint8_t *pred, int pstride, uint8_t *out, int ostride) {
+    int32_t r[64];
+    jmo_inverse8x8(m, r);
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++)
+            out[y * ostride + x] =
+                (uint8_t)clip255((r[8 * y + x] + (pred[y * pstride + x] << DQ_BITS) + DQ_ROUND) >> DQ_BITS);
+}
+/* HadamardSAD8x8 [J]: (sum |H8 D H8| + 2) >> 2; SAD when use_hadamard == 0.  d[] raster. */
+int jmo_satd8x8(const int32_t d[64], int use_hadamard) {
+    int sum = 0;
+    if (!use_hadamard) {
+        for (int k = 0; k < 64; k++) sum += iabs(d[k]);
+        return sum;
+    }
+    int32_t m[64];
+    memcpy(m, d, sizeof(m));
+    for (int pass = 0; pass < 2; pass++)
+        for (int i = 0; i < 8; i++) {
+            int st = pass ? 8 : 1;
+            int32_t *v = pass ? m + i : m + 8 * i;
+            for (int h = 1; h < 8; h <<= 1)
+                for (int k = 0; k < 8; k++)
+                    if (!(k & h)) { int a = v[k * st], b = v[(k + h) * st]; v[k * st] = a + b; v[(k + h) * st] = a - b; }
+        }
+    for (int k = 0; k < 64; k++) sum += iabs(m[k]);
+    return (sum + 2) >> 2;
+}

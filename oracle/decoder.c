@@ -1,9 +1,9 @@
 /*
  * decoder.c — minimal normative H.264 decoder for closed-loop checks (TEST INFRASTRUCTURE ONLY).
  *
- * Scope: the Baseline subset the host encoder emits — progressive frames, 4:2:0 8-bit, one
- * slice per picture, CAVLC, I and P slices, one reference picture, no FMO/ASO/redundant
- * slices, POC type 0.  Written from ITU-T H.264 clauses 7.3 (syntax), 8.3 (intra), 8.4
+ * Scope: the Baseline / High subset the host encoder emits — progressive frames, 4:2:0 8-bit,
+ * one slice per picture, CAVLC, I and P slices, one reference picture, no FMO/ASO/redundant
+ * slices, POC type 0; High: transform_size_8x8_flag (8x8 residual, Intra_8x8), flat scaling.  Written from ITU-T H.264 clauses 7.3 (syntax), 8.3 (intra), 8.4
  * (inter, MVP via "partition already decoded" tracking, independent of the encoder's JM
  * shape rules), 8.5 (scaling/inverse transforms), 8.7 (deblocking), 9.1/9.2 (Exp-Golomb,
  * CAVLC).  This is SURVEY.md §2 row 20: JM's ldecod closed-loop role — an encoder is correct
@@ -136,7 +136,8 @@ static int read_block(br_t *b, int nC, int maxn, int *coef) {
 
 /* ---- decoder state -------------------------------------------------------------------- */
 typedef struct {
-    int mbtype;           /* 0 P_L0 inter, 1 I4x4, 2 I16, 3 P_Skip */
+    int mbtype;           /* 0 P_L0 inter, 1 I4x4, 2 I16, 3 P_Skip, 4 I8x8 */
+    int t8;               /* transform_size_8x8_flag */
     int intra;
     int qp;
     uint8_t tc[24];       /* total_coeff: 16 luma (raster 4x4), 4 cb, 4 cr               */
@@ -149,7 +150,7 @@ struct jmo_dec {
     int have_sps, have_pps;
     int mbw, mbh, W, H, crop_l, crop_r, crop_t, crop_b;
     int log2_fn, poc_type, log2_poc;
-    int num_ref_l0, init_qp, cqp_off, dfc_present, cip;
+    int num_ref_l0, init_qp, cqp_off, dfc_present, cip, t8mode;
     uint8_t *cur[3], *ref[3];
     int have_ref;
     mbinfo *mi;
@@ -185,7 +186,12 @@ static int parse_sps(jmo_dec *d, br_t *b) {
     int profile = rbits(b, 8);
     rbits(b, 16);
     rue(b);
-    if (profile >= 100) { snprintf(d->err, sizeof d->err, "profile %d unsupported", profile); return -1; }
+    if (profile == 100) {                 /* High: only 4:2:0 8-bit with flat scaling lists */
+        if (rue(b) != 1 || rue(b) != 0 || rue(b) != 0 || rb(b) || rb(b)) {
+            snprintf(d->err, sizeof d->err, "High profile SPS options unsupported");
+            return -1;
+        }
+    } else if (profile >= 100) { snprintf(d->err, sizeof d->err, "profile %d unsupported", profile); return -1; }
     d->log2_fn = rue(b) + 4;
     d->poc_type = rue(b);
     if (d->poc_type != 0) { snprintf(d->err, sizeof d->err, "poc type"); return -1; }
@@ -217,6 +223,15 @@ static int parse_pps(jmo_dec *d, br_t *b) {
     d->dfc_present = rb(b);
     d->cip = rb(b);
     rb(b);
+    d->t8mode = 0;
+    /* more_rbsp_data(): anything before the rbsp_stop_one_bit */
+    long last = b->n * 8 - 1;
+    while (last >= 0 && !((b->p[last >> 3] >> (7 - (last & 7))) & 1)) last--;
+    if (b->pos < last) {
+        d->t8mode = rb(b);
+        if (rb(b)) { snprintf(d->err, sizeof d->err, "scaling matrices unsupported"); return -1; }
+        if (rse(b) != d->cqp_off) { snprintf(d->err, sizeof d->err, "second_chroma_qp_index_offset unsupported"); return -1; }
+    }
     d->have_pps = 1;
     return b->err ? -1 : 0;
 }
@@ -386,6 +401,105 @@ static void recon4x4(int32_t *c, const uint8_t *pred, int ps, uint8_t *out, int 
         for (int x = 0; x < 4; x++) out[y * os + x] = (uint8_t)clip255(pred[y * ps + x] + ((r[4 * y + x] + 32) >> 6));
 }
 
+/* ---- Intra_8x8 (8.3.2.2): the 25 reference samples as one edge e[0..24] running from
+ * p[-1,7] up to p[-1,0] (e[7-y]), the corner p[-1,-1] (e[8]) and along p[0..15,-1] (e[9+x]);
+ * the 8.3.2.2.1 filter is a [1 2 1] tap along the edge whose missing outer neighbour is
+ * replaced by the centre sample, and every directional mode reads that filtered edge. */
+static int pred8x8(const jmo_dec *d, int mx, int my, int b8, int mode, uint8_t *pr) {
+    const uint8_t *R = d->cur[0];
+    int W = d->W, bx = 8 * (b8 & 1), by = 8 * (b8 >> 1), X = 16 * mx + bx, Y = 16 * my + by;
+    int left = bx ? 1 : avail_mb(d, mx - 1, my, mx, my);
+    int up = by ? 1 : avail_mb(d, mx, my - 1, mx, my);
+    int ul = bx && by ? 1 : bx ? avail_mb(d, mx, my - 1, mx, my) : by ? avail_mb(d, mx - 1, my, mx, my) : avail_mb(d, mx - 1, my - 1, mx, my);
+    int ur = b8 == 0 ? avail_mb(d, mx, my - 1, mx, my) : b8 == 1 ? avail_mb(d, mx + 1, my - 1, mx, my) : b8 == 2;
+    int e[25], av[25], f[25];
+    for (int i = 0; i < 25; i++) { e[i] = 0; av[i] = 0; }
+    for (int y = 0; y < 8; y++) if (left) { e[7 - y] = R[(Y + y) * W + X - 1]; av[7 - y] = 1; }
+    if (ul) { e[8] = R[(Y - 1) * W + X - 1]; av[8] = 1; }
+    for (int x = 0; x < 16; x++)
+        if (up) { e[9 + x] = x < 8 || ur ? R[(Y - 1) * W + X + x] : R[(Y - 1) * W + X + 7]; av[9 + x] = 1; }
+    for (int i = 0; i < 25; i++) {
+        if (!av[i]) continue;
+        int l = i > 0 && av[i - 1] ? e[i - 1] : e[i], r = i < 24 && av[i + 1] ? e[i + 1] : e[i];
+        f[i] = (l + 2 * e[i] + r + 2) >> 2;
+    }
+#define TT(x) f[9 + (x)]
+#define LL(y) f[7 - (y)]
+#define TAP(c) ((f[(c) - 1] + 2 * f[c] + f[(c) + 1] + 2) >> 2)
+    if (((mode == 0 || mode == 3 || mode == 7) && !up) || ((mode == 1 || mode == 8) && !left) ||
+        ((mode == 4 || mode == 5 || mode == 6) && !(up && left && ul)))
+        return -1;
+    int dc = 128, st = 0, sl = 0;
+    for (int i = 0; i < 8; i++) { st += up ? TT(i) : 0; sl += left ? LL(i) : 0; }
+    if (up && left) dc = (st + sl + 8) >> 4;
+    else if (up) dc = (st + 4) >> 3;
+    else if (left) dc = (sl + 4) >> 3;
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+            int v = dc, z;
+            switch (mode) {
+            case 0: v = TT(x); break;
+            case 1: v = LL(y); break;
+            case 3: v = x + y < 14 ? TAP(10 + x + y) : (f[23] + 3 * f[24] + 2) >> 2; break;
+            case 4: v = TAP(8 + x - y); break;
+            case 5:
+                z = 2 * x - y;
+                if (z >= 0 && !(z & 1)) v = (f[8 + x - (y >> 1)] + f[9 + x - (y >> 1)] + 1) >> 1;
+                else if (z > 0) v = TAP(8 + x - (y >> 1));
+                else v = TAP(9 + z);
+                break;
+            case 6:
+                z = 2 * y - x;
+                if (z >= 0 && !(z & 1)) v = (f[8 - y + (x >> 1)] + f[7 - y + (x >> 1)] + 1) >> 1;
+                else if (z > 0) v = TAP(8 - y + (x >> 1));
+                else v = TAP(7 - z);
+                break;
+            case 7:
+                v = (y & 1) ? (TT(x + (y >> 1)) + 2 * TT(x + (y >> 1) + 1) + TT(x + (y >> 1) + 2) + 2) >> 2
+                            : (TT(x + (y >> 1)) + TT(x + (y >> 1) + 1) + 1) >> 1;
+                break;
+            case 8:
+                z = x + 2 * y;
+                if (z > 13) v = LL(7);
+                else if (z == 13) v = (LL(6) + 3 * LL(7) + 2) >> 2;
+                else if (!(z & 1)) v = (LL(y + (x >> 1)) + LL(y + (x >> 1) + 1) + 1) >> 1;
+                else v = (LL(y + (x >> 1)) + 2 * LL(y + (x >> 1) + 1) + LL(y + (x >> 1) + 2) + 2) >> 2;
+                break;
+            }
+            pr[8 * y + x] = (uint8_t)v;
+        }
+#undef TT
+#undef LL
+#undef TAP
+    return 0;
+}
+/* 8x8 frame zig-zag (Table 8-13, 8x8 field omitted) as (x, y) pairs */
+static const uint8_t zz8[64][2] = {
+    {0, 0}, {1, 0}, {0, 1}, {0, 2}, {1, 1}, {2, 0}, {3, 0}, {2, 1}, {1, 2}, {0, 3}, {0, 4}, {1, 3}, {2, 2},
+    {3, 1}, {4, 0}, {5, 0}, {4, 1}, {3, 2}, {2, 3}, {1, 4}, {0, 5}, {0, 6}, {1, 5}, {2, 4}, {3, 3}, {4, 2},
+    {5, 1}, {6, 0}, {7, 0}, {6, 1}, {5, 2}, {4, 3}, {3, 4}, {2, 5}, {1, 6}, {0, 7}, {1, 7}, {2, 6}, {3, 5},
+    {4, 4}, {5, 3}, {6, 2}, {7, 1}, {7, 2}, {6, 3}, {5, 4}, {4, 5}, {3, 6}, {2, 7}, {3, 7}, {4, 6}, {5, 5},
+    {6, 4}, {7, 3}, {7, 4}, {6, 5}, {5, 6}, {4, 7}, {5, 7}, {6, 6}, {7, 5}, {7, 6}, {6, 7}, {7, 7}};
+/* LevelScale8x8 = 16 * normAdjust8x8 (8.5.9, flat Default weights) and 8.5.13.1 scaling */
+static int lscale8(int qm, int i, int j) {
+    static const int v8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+                                 {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+    int k = (i % 4 == 0 && j % 4 == 0) ? 0 : (i % 2 == 1 && j % 2 == 1) ? 1 : (i % 4 == 2 && j % 4 == 2) ? 2
+          : ((i % 4 == 0 && j % 2 == 1) || (i % 2 == 1 && j % 4 == 0)) ? 3
+          : ((i % 4 == 0 && j % 4 == 2) || (i % 4 == 2 && j % 4 == 0)) ? 4 : 5;
+    return 16 * v8[qm][k];
+}
+static void recon8x8(const int *c64, int qp, const uint8_t *pred, int ps, uint8_t *out, int os) {
+    int32_t m[64], r[64];
+    for (int k = 0; k < 64; k++) {
+        int x = zz8[k][0], y = zz8[k][1], ls = lscale8(qp % 6, y, x), c = c64[k];
+        m[8 * y + x] = qp >= 36 ? c * ls * (1 << (qp / 6 - 6)) : (c * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+    }
+    jmo_inverse8x8(m, r);
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) out[y * os + x] = (uint8_t)clip255(pred[y * ps + x] + ((r[8 * y + x] + 32) >> 6));
+}
+
 /* ---- inter prediction (8.4.2.2) ------------------------------------------------------- */
 static void inter_pred(const jmo_dec *d, int mx, int my, const int16_t mv16[16][2], uint8_t *py, uint8_t *pu, uint8_t *pv) {
     for (int y = 0; y < 16; y++)
@@ -477,7 +591,8 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
     int16_t mv16[16][2];
     memset(mv16, 0, sizeof(mv16));
     uint8_t pred[256], predu[64], predv[64];
-    int i16mode = 0, cbp = 0, intra_type = -1;    /* intra_type: -1 inter, 0 I4, 1 I16 */
+    int i16mode = 0, cbp = 0, intra_type = -1;    /* intra_type: -1 inter, 0 I_NxN, 1 I16 */
+    int no_sub8x8 = 0;
     int ipm[16];
     if (skip) {
         mi->mbtype = 3;
@@ -502,17 +617,35 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
         if (intra_type >= 0) {
             mi->intra = 1;
             mi->mbtype = intra_type == 0 ? 1 : 2;
-            if (intra_type == 0) {
+            if (intra_type == 0 && d->t8mode) mi->t8 = rb(b);
+            if (mi->t8) {                               /* Intra_8x8: predIntra8x8PredMode (8.3.2.1) */
+                mi->mbtype = 4;
+                int m8[4];
+                for (int b8 = 0; b8 < 4; b8++) {
+                    int x4 = (b8 & 1) * 2, y4 = (b8 >> 1) * 2;
+                    int flag = rb(b), rem = flag ? 0 : (int)rbits(b, 3);
+                    int ma = -1, mb = -1, dcp = 0;
+                    if (x4 > 0) ma = m8[b8 - 1];
+                    else if (avail_mb(d, mx - 1, my, mx, my)) { const mbinfo *n = &d->mi[my * d->mbw + mx - 1]; ma = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[y4 * 4 + 3] : 2; }
+                    else dcp = 1;
+                    if (y4 > 0) mb = m8[b8 - 2];
+                    else if (avail_mb(d, mx, my - 1, mx, my)) { const mbinfo *n = &d->mi[(my - 1) * d->mbw + mx]; mb = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[12 + x4] : 2; }
+                    else dcp = 1;
+                    int pm = dcp ? 2 : imin(ma, mb);
+                    m8[b8] = flag ? pm : (rem < pm ? rem : rem + 1);
+                }
+                for (int k = 0; k < 16; k++) { ipm[k] = m8[((k >> 3) << 1) + ((k & 3) >> 1)]; mi->ipm[k] = (int8_t)ipm[k]; }
+            } else if (intra_type == 0) {
                 for (int blk = 0; blk < 16; blk++) {
                     int x4 = ((blk >> 2) & 1) * 2 + (blk & 1), y4 = (blk >> 3) * 2 + ((blk >> 1) & 1);
                     int flag = rb(b), rem = flag ? 0 : (int)rbits(b, 3);
                     /* predIntra4x4PredMode (8.3.1.1) */
                     int ma = -1, mb = -1, dcp = 0;
                     if (x4 > 0) ma = ipm[y4 * 4 + x4 - 1];
-                    else if (avail_mb(d, mx - 1, my, mx, my)) { const mbinfo *n = &d->mi[my * d->mbw + mx - 1]; ma = n->mbtype == 1 ? n->ipm[y4 * 4 + 3] : 2; }
+                    else if (avail_mb(d, mx - 1, my, mx, my)) { const mbinfo *n = &d->mi[my * d->mbw + mx - 1]; ma = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[y4 * 4 + 3] : 2; }
                     else dcp = 1;
                     if (y4 > 0) mb = ipm[(y4 - 1) * 4 + x4];
-                    else if (avail_mb(d, mx, my - 1, mx, my)) { const mbinfo *n = &d->mi[(my - 1) * d->mbw + mx]; mb = n->mbtype == 1 ? n->ipm[12 + x4] : 2; }
+                    else if (avail_mb(d, mx, my - 1, mx, my)) { const mbinfo *n = &d->mi[(my - 1) * d->mbw + mx]; mb = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[12 + x4] : 2; }
                     else dcp = 1;
                     int pm = dcp ? 2 : imin(ma, mb);
                     ipm[y4 * 4 + x4] = flag ? pm : (rem < pm ? rem : rem + 1);
@@ -527,9 +660,10 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
         } else {
             mi->mbtype = 0;
             if (t > 4) FAIL("bad P mb_type %d", t);
+            no_sub8x8 = 1;
             if (t == 3 || t == 4) {
                 int sub[4];
-                for (int i = 0; i < 4; i++) { sub[i] = rue(b); if (sub[i] > 3) FAIL("bad sub_mb_type"); }
+                for (int i = 0; i < 4; i++) { sub[i] = rue(b); if (sub[i] > 3) FAIL("bad sub_mb_type"); if (sub[i]) no_sub8x8 = 0; }
                 if (d->num_ref_l0 > 1) FAIL("multiple refs unsupported");
                 for (int i = 0; i < 4; i++) {
                     int ox = (i & 1) * 8, oy = (i >> 1) * 8;
@@ -557,6 +691,7 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
             int code = rue(b);
             if (code > 47) FAIL("bad cbp code");
             cbp = intra_type == 0 ? cbp_intra[code] : cbp_inter[code];
+            if (intra_type < 0 && (cbp & 15) && d->t8mode && no_sub8x8) mi->t8 = rb(b);
         }
         if (cbp > 0 || intra_type == 1) {
             int dq = rse(b);
@@ -591,7 +726,27 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
             }
         }
     }
-    for (int blk = 0; blk < 16; blk++) {
+    for (int b8 = 0; b8 < 4 && mi->t8; b8++) {       /* 8x8 transform: 4 interleaved CAVLC blocks */
+        int c64[64] = {0}, any = 0;
+        for (int i4 = 0; i4 < 4; i4++) {
+            int x4 = (b8 & 1) * 2 + (i4 & 1), y4 = (b8 >> 1) * 2 + (i4 >> 1), c[16] = {0}, tc = 0;
+            if (cbpl & (1 << b8)) {
+                tc = read_block(b, calc_nc(d, mx, my, 0, x4, y4, mi->tc), 16, c);
+                if (tc < 0) FAIL("luma 8x8 block %d at MB %d,%d", b8, mx, my);
+            }
+            mi->tc[y4 * 4 + x4] = (uint8_t)tc;
+            for (int k = 0; k < 16; k++) { c64[4 * k + i4] = c[k]; any |= c[k] != 0; }
+        }
+        int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+        if (any) mi->nzblk |= 0x33 << ((by >> 2) * 4 + (bx >> 2));
+        uint8_t *dst = RY + (16 * my + by) * W + 16 * mx + bx;
+        if (intra_type == 0) {
+            uint8_t p64[64];
+            if (pred8x8(d, mx, my, b8, ipm[(by >> 2) * 4 + (bx >> 2)], p64)) FAIL("I8 mode unavailable at MB %d,%d", mx, my);
+            recon8x8(c64, qp_, p64, 8, dst, W);
+        } else recon8x8(c64, qp_, pred + by * 16 + bx, 16, dst, W);
+    }
+    for (int blk = 0; blk < 16 && !mi->t8; blk++) {
         int b8 = blk >> 2;
         int x4 = (b8 & 1) * 2 + (blk & 1), y4 = (b8 >> 1) * 2 + ((blk >> 1) & 1);
         int c[16] = {0};
@@ -717,6 +872,7 @@ static void deblock(jmo_dec *d) {
             int qq = d->mi[my * d->mbw + mx].qp;
             for (int vert = 1; vert >= 0; vert--) {
                 for (int e = 0; e < 16; e += 4) {
+                    if ((e & 4) && d->mi[my * d->mbw + mx].t8) continue;   /* no 4x4 luma edges */
                     if (e == 0 && ((vert && mx == 0) || (!vert && my == 0))) continue;
                     int qp_ = d->mi[vert ? my * d->mbw + mx - (e == 0) : (my - (e == 0)) * d->mbw + mx].qp;
                     int qav = (qp_ + qq + 1) >> 1;

@@ -385,6 +385,65 @@ int jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, in
     return JMH_OK;
 }
 
+/* dct_luma8x8 [J] (JM FRExt block.c; forward8x8 + quant + dequant + inverse8x8): 8x8 core
+ * transform, level = (|c|*quant_coef8 + qp_const) >> (16 + qp/6) with qp_const by slice type as
+ * for 4x4 (docs/JM_SEMANTICS.md item 1), 8x8 frame zig-zag, COEFF_COST8x8 on the 64-scan runs,
+ * dequantisation by the normative 8.5.13.1 formula on the signed level (flat scaling lists),
+ * reconstruction clip((r + (pred<<6) + 32) >> 6).  levels[64] in scan order. */
+static int dct_luma8x8(const int32_t resid[64], const uint8_t *pred, int ps, int qp, int intra_round,
+                       int16_t levels[64], int *coeff_cost, uint8_t *rec, int rs) {
+    int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS_8 + qp_per;
+    int qp_const = intra_round ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+    int scan[64];
+    jmo_scan8x8(scan);
+    int32_t m[64];
+    memcpy(m, resid, sizeof(m));
+    jmo_fwd8x8(m);
+    int run = -1, nonzero = 0;
+    for (int k = 0; k < 64; k++) {
+        int pos = scan[k], cls = jmo_class8(pos & 7, pos >> 3);
+        run++;
+        int level = (iabs(m[pos]) * jmo_quant8_cls[qp_rem][cls] + qp_const) >> q_bits;
+        int c = isign(level, m[pos]), d = 0;
+        if (level != 0) {
+            nonzero = 1;
+            *coeff_cost += level > 1 ? MAX_VALUE : jmo_coeff_cost8(run);
+            run = -1;
+            int ls = 16 * jmo_dequant8_cls[qp_rem][cls];        /* LevelScale8x8, flat weights */
+            d = qp >= 36 ? c * ls * (1 << (qp_per - 6)) : (c * ls + (1 << (5 - qp_per))) >> (6 - qp_per);
+        }
+        levels[k] = (int16_t)c;
+        m[pos] = d;
+    }
+    jmo_inv8x8_add(m, pred, ps, rec, rs);
+    return nonzero;
+}
+
+int jmo_tq8x8_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,
+                    int16_t *levels, uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
+    if (n < 0 || qp < 0 || qp > 51) return JMH_E_INVALID_ARG;
+    for (int i = 0; i < n; i++) {
+        int32_t r[64];
+        int cc = 0;
+        for (int k = 0; k < 64; k++) r[k] = resid[64 * i + k];
+        nonzero[i] = dct_luma8x8(r, pred + 64 * i, 8, qp, intra, levels + 64 * i, &cc, recon + 64 * i, 8);
+        coeff_cost[i] = cc;
+    }
+    return JMH_OK;
+}
+void jmo_forward8x8(const int32_t *in, int32_t *out) {
+    memcpy(out, in, 64 * sizeof(int32_t));
+    jmo_fwd8x8(out);
+}
+
+/* store an 8x8 block's scan-order levels as CAVLC's four interleaved 4x4 blocks (7.3.5.3.2) */
+static void put_levels8(int16_t luma[16][16], int b8, const int16_t lev[64]) {
+    for (int j = 0; j < 4; j++) {
+        int blk = (2 * (b8 >> 1) + (j >> 1)) * 4 + 2 * (b8 & 1) + (j & 1);
+        for (int k = 0; k < 16; k++) luma[blk][k] = lev[4 * k + j];
+    }
+}
+
 /* dct_chroma [J] for one component: 4 4x4 AC blocks + 2x2 DC; returns updated cr_cbp.
  * resid/pred raster 8x8.  DC reconstruction follows H.264 8.5.11.2 exactly. */
 static int dct_chroma(const int32_t resid[64], const uint8_t pred[64], int qpc, int intra_round,
@@ -601,6 +660,82 @@ static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int
 #undef PL
 }
 
+/* Intra8x8 prediction (8.3.2.2, JM FRExt intrapred_luma8x8 [J]): reference sample filtering
+ * (8.3.2.2.1) then the nine modes.  See jm_oracle.h for nb[] / avail. */
+int jmo_intra8x8_pred(const int32_t nb[25], int avail, uint8_t pred[9][64]) {
+    int left = avail & 1, up = (avail >> 1) & 1, ur = (avail >> 2) & 1, ul = (avail >> 3) & 1;
+    int p[16], q[8], c = nb[0];                    /* raw top row (x = 0..15), left column, corner */
+    for (int x = 0; x < 16; x++) p[x] = x < 8 || ur ? nb[1 + x] : nb[8];   /* substitution p[7,-1] */
+    for (int y = 0; y < 8; y++) q[y] = nb[17 + y];
+    int T[16] = {0}, L[8] = {0}, Q = c;                /* filtered p'[x,-1], p'[-1,y], p'[-1,-1] */
+    if (up) {
+        T[0] = ul ? (c + 2 * p[0] + p[1] + 2) >> 2 : (3 * p[0] + p[1] + 2) >> 2;
+        for (int x = 1; x < 15; x++) T[x] = (p[x - 1] + 2 * p[x] + p[x + 1] + 2) >> 2;
+        T[15] = (p[14] + 3 * p[15] + 2) >> 2;
+    }
+    if (ul) {
+        if (up && left) Q = (p[0] + 2 * c + q[0] + 2) >> 2;
+        else if (up) Q = (3 * c + p[0] + 2) >> 2;
+        else if (left) Q = (3 * c + q[0] + 2) >> 2;
+    }
+    if (left) {
+        L[0] = ul ? (c + 2 * q[0] + q[1] + 2) >> 2 : (3 * q[0] + q[1] + 2) >> 2;
+        for (int y = 1; y < 7; y++) L[y] = (q[y - 1] + 2 * q[y] + q[y + 1] + 2) >> 2;
+        L[7] = (q[6] + 3 * q[7] + 2) >> 2;
+    }
+#define PT(i) ((i) < 0 ? Q : T[i])
+#define PL(j) ((j) < 0 ? Q : L[j])
+    int dcv = 128, st = 0, sl = 0;
+    for (int i = 0; i < 8; i++) { st += up ? T[i] : 0; sl += left ? L[i] : 0; }
+    if (up && left) dcv = (st + sl + 8) >> 4;
+    else if (up) dcv = (st + 4) >> 3;
+    else if (left) dcv = (sl + 4) >> 3;
+    int ok = (1 << 2) | (up ? (1 << 0) | (1 << 3) | (1 << 7) : 0) | (left ? (1 << 1) | (1 << 8) : 0) |
+             (up && left && ul ? (1 << 4) | (1 << 5) | (1 << 6) : 0);
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+            int k = 8 * y + x, v;
+            pred[2][k] = (uint8_t)dcv;
+            if (up) {
+                pred[0][k] = (uint8_t)T[x];
+                pred[3][k] = (uint8_t)(x == 7 && y == 7 ? (T[14] + 3 * T[15] + 2) >> 2
+                                                       : (T[x + y] + 2 * T[x + y + 1] + T[x + y + 2] + 2) >> 2);
+                pred[7][k] = (uint8_t)(!(y & 1) ? (T[x + (y >> 1)] + T[x + (y >> 1) + 1] + 1) >> 1
+                                                : (T[x + (y >> 1)] + 2 * T[x + (y >> 1) + 1] + T[x + (y >> 1) + 2] + 2) >> 2);
+            }
+            if (left) {
+                pred[1][k] = (uint8_t)L[y];
+                int z = x + 2 * y;
+                if (z > 13) v = L[7];
+                else if (z == 13) v = (L[6] + 3 * L[7] + 2) >> 2;
+                else if (!(z & 1)) v = (L[y + (x >> 1)] + L[y + (x >> 1) + 1] + 1) >> 1;
+                else v = (L[y + (x >> 1)] + 2 * L[y + (x >> 1) + 1] + L[y + (x >> 1) + 2] + 2) >> 2;
+                pred[8][k] = (uint8_t)v;
+            }
+            if (up && left && ul) {
+                if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
+                else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
+                else v = (PT(0) + 2 * Q + PL(0) + 2) >> 2;
+                pred[4][k] = (uint8_t)v;
+                int z = 2 * x - y;
+                if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
+                else if (z == -1) v = (PL(0) + 2 * Q + PT(0) + 2) >> 2;
+                else v = (PL(y - 2 * x - 1) + 2 * PL(y - 2 * x - 2) + PL(y - 2 * x - 3) + 2) >> 2;
+                pred[5][k] = (uint8_t)v;
+                z = 2 * y - x;
+                if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
+                else if (z == -1) v = (PL(0) + 2 * Q + PT(0) + 2) >> 2;
+                else v = (PT(x - 2 * y - 1) + 2 * PT(x - 2 * y - 2) + PT(x - 2 * y - 3) + 2) >> 2;
+                pred[6][k] = (uint8_t)v;
+            }
+        }
+#undef PT
+#undef PL
+    return ok;
+}
+
 /* intrapred_luma_16x16 [J] / 8.3.3 */
 static void intra16_pred(const mbs *s, uint8_t pred[4][256], int avail[4]) {
     const jmo_ctx *c = s->c;
@@ -737,6 +872,75 @@ static void chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], uint8_
 }
 
 /* ====================================================================================== */
+/*  Intra8x8 decision (High profile): JM FRExt rdopt.c › Mode_Decision_for_Intra8x8Macroblock /  */
+/*  Mode_Decision_for_new_8x8IntraBlocks, RDO off [J] (docs/JM_SEMANTICS.md items 26-28)      */
+/* ====================================================================================== */
+static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, uint8_t rec[256],
+                             int16_t lev[4][64], int modes[4], int *cbp) {
+    const jmo_ctx *c = s->c;
+    int cost = 6 * lambda;                                 /* (int)floor(6*lambda+0.4999), once */
+    *cbp = 0;
+    for (int b8 = 0; b8 < 4; b8++) {
+        int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+#define SMP(x, y) (((x) >= 0 && (x) < 16 && (y) >= 0 && (y) < 16) ? rec[(y) * 16 + (x)] \
+                   : c->recY[(s->pix_y + (y)) * c->W + s->pix_x + (x)])
+        int left = luma_avail(s, bx - 1, by), up = luma_avail(s, bx, by - 1);
+        int ul = luma_avail(s, bx - 1, by - 1), ur = luma_avail(s, bx + 8, by - 1);
+        int32_t nb[25] = {0};
+        if (ul) nb[0] = SMP(bx - 1, by - 1);
+        for (int x = 0; x < 16; x++) if (up && (x < 8 || ur)) nb[1 + x] = SMP(bx + x, by - 1);
+        for (int y = 0; y < 8; y++) if (left) nb[17 + y] = SMP(bx - 1, by + y);
+#undef SMP
+        uint8_t pred[9][64];
+        int ok = jmo_intra8x8_pred(nb, left | up << 1 | ur << 2 | ul << 3, pred);
+        /* predIntra8x8PredMode (8.3.2.1): neighbour 4x4 modes (I4: that block, I8: repeated, else 2) */
+        int ma = -1, mb = -1, ia = 0, ib = 0;
+        if (bx) ma = modes[b8 - 1];
+        else if (nb4(s, -1, by, &ia)) ma = c->ipred[ia];
+        if (by) mb = modes[b8 - 2];
+        else if (nb4(s, bx, -1, &ib)) mb = c->ipred[ib];
+        int mpm = (ma < 0 || mb < 0) ? 2 : imin(ma, mb);
+        int best = 2, bcost = BIGCOST;
+        for (int m = 0; m < 9; m++) {
+            if (!((ok >> m) & 1)) continue;
+            int32_t d[64];
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) d[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[m][8 * y + x];
+            int mc = (m == mpm ? 0 : 4 * lambda) + jmo_satd8x8(d, c->cfg.use_hadamard);
+            if (mc < bcost) { bcost = mc; best = m; }
+        }
+        modes[b8] = best;
+        int32_t r[64];
+        for (int y = 0; y < 8; y++)
+            for (int x = 0; x < 8; x++) r[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[best][8 * y + x];
+        int dummy = 0;
+        if (dct_luma8x8(r, pred[best], 8, qp, intra_round, lev[b8], &dummy, rec + by * 16 + bx, 16)) *cbp |= 1 << b8;
+        cost += bcost;
+    }
+    return cost;
+}
+
+/* TransformDecision [J] (RDO off): over the final prediction of the MB, sum of the 16 4x4 SATDs
+ * against the sum of the four 8x8 SATDs; 8x8 if strictly smaller (item 29) */
+static int transform_decision(const mbs *s, const uint8_t pred[256]) {
+    int had = s->c->cfg.use_hadamard, cost4 = 0, cost8 = 0;
+    for (int b8 = 0; b8 < 4; b8++) {
+        int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+        int32_t d[64];
+        for (int y = 0; y < 8; y++)
+            for (int x = 0; x < 8; x++) d[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[(by + y) * 16 + bx + x];
+        cost8 += jmo_satd8x8(d, had);
+        for (int q = 0; q < 4; q++) {
+            int32_t e[16];
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++) e[4 * y + x] = d[(4 * (q >> 1) + y) * 8 + 4 * (q & 1) + x];
+            cost4 += jmo_satd_block(e, had);
+        }
+    }
+    return cost8 < cost4;
+}
+
+/* ====================================================================================== */
 /*  encode_one_macroblock (RDO off)                                                         */
 /* ====================================================================================== */
 static void store_rec_luma(jmo_ctx *c, const mbs *s, const uint8_t rec[256]) {
@@ -804,6 +1008,15 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
         find_skip_mv(s);
     }
 
+    /* ===== Intra 8x8 decision (Transform8x8Mode; before Intra4x4, "<=") ===== */
+    const int t8 = c->cfg.transform_8x8_mode;
+    uint8_t i8rec[256];
+    int16_t i8lev[4][64];
+    int i8modes[4] = {2, 2, 2, 2}, i8cbp = 0;
+    if (t8) {
+        int i8cost = intra8x8_decision(s, qp, lambda, intra_round, i8rec, i8lev, i8modes, &i8cbp);
+        if (i8cost <= min_cost) { min_cost = i8cost; best_mode = JMH_I8MB; }
+    }
     /* ===== Intra 4x4 decision (with TQ + recon of every 4x4 in coding order) ===== */
     uint8_t i4rec[256];
     int16_t i4lev[16][16];
@@ -862,22 +1075,31 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     if (i16cost < min_cost) { min_cost = i16cost; best_mode = JMH_I16MB; }
 
     /* ===== final macroblock parameters ===== */
-    int is_intra = best_mode == JMH_I4MB || best_mode == JMH_I16MB;
+    int is_intra = best_mode == JMH_I4MB || best_mode == JMH_I16MB || best_mode == JMH_I8MB;
     int16_t fmv[16][2];
     memset(fmv, 0, sizeof(fmv));
     int b8mode[4];
     for (int b = 0; b < 4; b++) b8mode[b] = best_mode == JMH_P8x8 ? best8x8mode[b] : best_mode;
     if (best_mode == JMH_I4MB) for (int b = 0; b < 4; b++) b8mode[b] = JMH_IBLOCK;
     if (best_mode == JMH_I16MB) for (int b = 0; b < 4; b++) b8mode[b] = 0;
+    if (best_mode == JMH_I8MB) for (int b = 0; b < 4; b++) b8mode[b] = JMH_I8MB;
     if (!is_intra)
         for (int k = 0; k < 16; k++) {
             int b8 = ((k >> 3) << 1) + ((k & 3) >> 1);
             fmv[k][0] = s->all_mv[b8mode[b8]][k][0];
             fmv[k][1] = s->all_mv[b8mode[b8]][k][1];
         }
-    int cbp = 0, cbp_blk = 0;
+    int cbp = 0, cbp_blk = 0, tr8 = 0;
     uint8_t rec[256];
-    if (best_mode == JMH_I4MB) {
+    if (best_mode == JMH_I8MB) {
+        cbp = i8cbp; tr8 = 1;
+        memcpy(rec, i8rec, 256);
+        for (int b8 = 0; b8 < 4; b8++) {
+            put_levels8(res->luma, b8, i8lev[b8]);
+            if ((cbp >> b8) & 1) cbp_blk |= 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2);
+        }
+        for (int k = 0; k < 16; k++) res->ipred[k] = (int8_t)i8modes[((k >> 3) << 1) + ((k & 3) >> 1)];
+    } else if (best_mode == JMH_I4MB) {
         cbp = i4cbp; cbp_blk = i4cbpblk;
         memcpy(rec, i4rec, 256);
         for (int k = 0; k < 16; k++) { res->ipred[k] = (int8_t)i4modes[k]; memcpy(res->luma[k], i4lev[k], 32); }
@@ -890,12 +1112,26 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
         /* LumaResidualCoding / LumaResidualCoding8x8 (also SetCoeffAndReconstruction8x8) */
         uint8_t pred[256];
         int sum_cnt_nonz = 0;
+        for (int k = 0; k < 16; k++) luma_pred_4x4(s, k & 3, k >> 2, fmv[k][0], fmv[k][1], pred + 4 * (k >> 2) * 16 + 4 * (k & 3), 16);
+        if (t8 && (best_mode <= 3 || (b8mode[0] == 4 && b8mode[1] == 4 && b8mode[2] == 4 && b8mode[3] == 4)))
+            tr8 = transform_decision(s, pred);
         for (int b8 = 0; b8 < 4; b8++) {
             int coeff_cost = 0, cbp8 = 0, blk8 = 0;
-            for (int b4 = 0; b4 < 4; b4++) {
+            if (tr8) {                                    /* dct_luma8x8 path */
+                int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+                int32_t r[64];
+                int16_t lv[64];
+                for (int y = 0; y < 8; y++)
+                    for (int x = 0; x < 8; x++) r[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[(by + y) * 16 + bx + x];
+                if (dct_luma8x8(r, pred + by * 16 + bx, 16, qp, intra_round, lv, &coeff_cost, rec + by * 16 + bx, 16)) {
+                    cbp8 = 1;
+                    blk8 = 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2);
+                }
+                put_levels8(res->luma, b8, lv);
+            }
+            for (int b4 = 0; b4 < 4 && !tr8; b4++) {
                 int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1);
                 int k = by4 * 4 + bx4;
-                luma_pred_4x4(s, bx4, by4, fmv[k][0], fmv[k][1], pred + 4 * by4 * 16 + 4 * bx4, 16);
                 int32_t r[16];
                 for (int y = 0; y < 4; y++)
                     for (int x = 0; x < 4; x++)
@@ -970,6 +1206,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     if (s->slice_p && best_mode == 1 && cbp == 0 && fmv[0][0] == s->skip_mv[0] && fmv[0][1] == s->skip_mv[1])
         mb_type = JMH_PSKIP;
     res->mb_type = (int16_t)mb_type;
+    res->transform_8x8 = (int8_t)(tr8 && (best_mode == JMH_I8MB || (cbp & 15)));
     res->cbp = (int16_t)cbp;
     res->cbp_blk = cbp_blk;
     res->c_ipred_mode = (int8_t)(is_intra ? c_mode : 0);
@@ -984,7 +1221,8 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
         c->mv[2 * a] = fmv[k][0];
         c->mv[2 * a + 1] = fmv[k][1];
         c->refidx[a] = (int8_t)(is_intra ? -1 : 0);
-        if (best_mode != JMH_I4MB) { c->ipred[a] = 2; res->ipred[k] = 2; }
+        if (best_mode == JMH_I8MB) c->ipred[a] = res->ipred[k];
+        else if (best_mode != JMH_I4MB) { c->ipred[a] = 2; res->ipred[k] = 2; }
     }
     c->mbintra[s->mb_addr] = (int8_t)is_intra;
 }

@@ -15,6 +15,7 @@ static int cfg_ok(const jmh_config *cfg) {
     if (cfg->search_mode != 0 && cfg->search_mode != -1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred != 0) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
+    if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
     return JMH_OK;
 }
 

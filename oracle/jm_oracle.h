@@ -58,6 +58,16 @@ int  jmo_satd4x4(const int32_t *diff, int use_hadamard);
 void jmo_forward4x4(const int32_t *in, int32_t *out);             /* raster in/out         */
 void jmo_inverse4x4(const int32_t *in, int32_t *out);             /* no rounding shift     */
 int  jmo_qp2quant(int qp);
+/* 8x8 transform unit seams (known answers; GPU unit parity) */
+void jmo_forward8x8(const int32_t *in, int32_t *out);             /* raster in/out         */
+void jmo_inverse8x8(const int32_t *in, int32_t *out);             /* no rounding shift     */
+int  jmo_satd8x8(const int32_t d[64], int use_hadamard);
+int  jmo_tq8x8_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,
+                     int16_t *levels, uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero);
+/* Intra8x8 prediction (8.3.2.2) of one block from its 25 unfiltered neighbours
+ * nb[0] = p[-1,-1], nb[1..16] = p[0..15,-1], nb[17..24] = p[-1,0..7]; avail bits: 1 left,
+ * 2 top, 4 top-right, 8 top-left.  pred[9][64]; returns the bitmask of available modes.   */
+int  jmo_intra8x8_pred(const int32_t nb[25], int avail, uint8_t pred[9][64]);
 int  jmo_qp_scale_cr(int qp);
 /* median MV predictor of the spec on explicit neighbours (unit tests)                     */
 void jmo_mvp_median(int avail_a, int ref_a, int mva_x, int mva_y,

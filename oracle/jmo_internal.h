@@ -68,6 +68,18 @@ void jmo_fwd4x4(int32_t m[16]);                       /* in-place, raster       
 void jmo_inv4x4_add(const int32_t m[16], const uint8_t *pred, int pstride, uint8_t *out,
                     int ostride);
 
+/* 8x8 transform (High profile) */
+#define Q_BITS_8 16               /* JM FRExt Q_BITS_8 [J]                                 */
+extern const int jmo_quant8_cls[6][6];
+extern const int jmo_dequant8_cls[6][6];
+int  jmo_class8(int x, int y);
+int  jmo_coeff_cost8(int run);
+void jmo_scan8x8(int scan[64]);
+void jmo_fwd8x8(int32_t m[64]);
+void jmo_inverse8x8(const int32_t *in, int32_t *out);
+void jmo_inv8x8_add(const int32_t m[64], const uint8_t *pred, int pstride, uint8_t *out, int ostride);
+int  jmo_satd8x8(const int32_t d[64], int use_hadamard);
+
 /* encode.c */
 void jmo_encode_mb(jmo_ctx *c, int mbx, int mby);
 

@@ -29,6 +29,11 @@ def lib():
             "jmo_load_current": (_I, [_P, _P, _P, _P, _I, _I]),
             "jmo_ffs_sad_table": (_I, [_P, _I, _P, _P, _P]),
             "jmo_tq4x4_batch": (_I, [_I, _P, _P, _I, _I, _P, _P, _P, _P]),
+            "jmo_tq8x8_batch": (_I, [_I, _P, _P, _I, _I, _P, _P, _P, _P]),
+            "jmo_forward8x8": (None, [_P, _P]),
+            "jmo_inverse8x8": (None, [_P, _P]),
+            "jmo_satd8x8": (_I, [_P, _I]),
+            "jmo_intra8x8_pred": (_I, [_P, _I, _P]),
             "jmo_luma_qpel_sample": (_I, [_P, _I, _I, _I, _I, _I]),
             "jmo_spiral": (None, [_I, _P, _P]),
             "jmo_mvbits": (_I, [_I]),
@@ -121,6 +126,19 @@ def tq4x4(resid, pred, qp, intra):
     cc = np.empty(n, np.int32)
     nz = np.empty(n, np.int32)
     assert L.jmo_tq4x4_batch(n, _ptr(resid), _ptr(pred), qp, intra, _ptr(lev), _ptr(rec), _ptr(cc), _ptr(nz)) == 0
+    return lev, rec, cc, nz
+
+
+def tq8x8(resid, pred, qp, intra):
+    L = lib()
+    resid = np.ascontiguousarray(resid, np.int16)
+    pred = np.ascontiguousarray(pred, np.uint8)
+    n = resid.shape[0]
+    lev = np.empty((n, 64), np.int16)
+    rec = np.empty((n, 64), np.uint8)
+    cc = np.empty(n, np.int32)
+    nz = np.empty(n, np.int32)
+    assert L.jmo_tq8x8_batch(n, _ptr(resid), _ptr(pred), qp, intra, _ptr(lev), _ptr(rec), _ptr(cc), _ptr(nz)) == 0
     return lev, rec, cc, nz
 
 

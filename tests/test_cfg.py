@@ -43,3 +43,10 @@ def test_jm86_spellings_accepted():
         r = run("-p", "UseFME=0", "-p", "QPRemainingFrame=30", "-p", "FramesToBeEncoded=1", "-p", "SourceWidth=32",
                 "-p", "SourceHeight=32", "-p", "SearchRange=2", "-p", f"OutputFile={d}/o.264")
         assert r.returncode == 0, r.stderr
+
+
+def test_transform8x8_requires_high_profile():
+    r = run("-p", "Transform8x8Mode=1")
+    assert r.returncode != 0 and "ProfileIDC=100" in r.stderr
+    r = run("-p", "ProfileIDC=77")
+    assert r.returncode != 0 and "ProfileIDC" in r.stderr

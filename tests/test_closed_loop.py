@@ -24,6 +24,18 @@ CONFIGS = [
     ["InputFile=synthetic:11", "FramesToBeEncoded=3", "ChromaQPOffset=-5", "QPRemainingFrame=36"],
     ["InputFile=synthetic:12", "FramesToBeEncoded=2", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
      "QPRemainingFrame=40"],
+    # High profile with the 8x8 transform: Intra_8x8, transform_size_8x8_flag,
+    # interleaved CAVLC 8x8 residual, 8x8 deblocking edges
+    ["InputFile=synthetic:21", "FramesToBeEncoded=5", "SearchRange=16", "ProfileIDC=100", "Transform8x8Mode=1"],
+    ["InputFile=synthetic:22", "FramesToBeEncoded=4", "ProfileIDC=100", "Transform8x8Mode=1", "QPFirstFrame=40",
+     "QPRemainingFrame=40", "SearchRange=8"],
+    ["InputFile=synthetic:23", "FramesToBeEncoded=4", "ProfileIDC=100", "Transform8x8Mode=1", "QPFirstFrame=4",
+     "QPRemainingFrame=8", "SearchRange=8", "UseHadamard=0"],
+    ["InputFile=synthetic:24", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=1", "SourceWidth=200",
+     "SourceHeight=120", "InterSearch8x4=0", "InterSearch4x8=0", "InterSearch4x4=0", "IntraPeriod=2",
+     "QPFirstFrame=30", "QPRemainingFrame=33"],
+    ["InputFile=synthetic:25", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=0", "SearchRange=8",
+     "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=-2", "LoopFilterBetaOffset=3", "ChromaQPOffset=3"],
 ]
 
 

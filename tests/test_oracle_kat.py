@@ -222,3 +222,112 @@ def test_cavlc_tables_prefix_free(path):
     assert (C_[0][1][1], L_[0][1][1]) == (1, 2)          # "01"
     assert (C_[0][0][1], L_[0][0][1]) == (5, 6)          # "000101"
     assert (C_[0][3][3], L_[0][3][3]) == (3, 5)          # "00011"
+
+
+# ---- 8x8 transform (High profile) -------------------------------------------
+def hadamard8():
+    h = np.array([[1]])
+    while h.shape[0] < 8:
+        h = np.block([[h, h], [h, -h]])
+    return h
+
+
+def test_satd8x8_is_matrix_hadamard():
+    rng = np.random.default_rng(8)
+    H = hadamard8()
+    for _ in range(50):
+        d = rng.integers(-255, 256, (8, 8))
+        want = (int(np.abs(H @ d @ H.T).sum()) + 2) >> 2
+        assert L.jmo_satd8x8(ptr(arr(d.reshape(-1))), 1) == want
+        assert L.jmo_satd8x8(ptr(arr(d.reshape(-1))), 0) == int(np.abs(d).sum())
+
+
+def test_forward8x8_constant_block_is_dc_only():
+    for c in (-255, -1, 0, 9, 255):
+        out = np.zeros(64, np.int32)
+        L.jmo_forward8x8(ptr(arr([c] * 64)), ptr(out))
+        assert out[0] == 64 * c and not out[1:].any()
+
+
+def test_inverse8x8_dc_only_is_flat():
+    out = np.zeros(64, np.int32)
+    L.jmo_inverse8x8(ptr(arr([64 * 7] + [0] * 63)), ptr(out))
+    assert (out == 64 * 7).all()
+
+
+def inv8_py(v):
+    """8.5.13.2 one-dimensional inverse, written from the spec equations."""
+    d = list(v)
+    a = [0] * 8
+    b = [0] * 8
+    a[0] = d[0] + d[4]; a[4] = d[0] - d[4]; a[2] = (d[2] >> 1) - d[6]; a[6] = d[2] + (d[6] >> 1)
+    b[0] = a[0] + a[6]; b[2] = a[4] + a[2]; b[4] = a[4] - a[2]; b[6] = a[0] - a[6]
+    a[1] = -d[3] + d[5] - d[7] - (d[7] >> 1); a[3] = d[1] + d[7] - d[3] - (d[3] >> 1)
+    a[5] = -d[1] + d[7] + d[5] + (d[5] >> 1); a[7] = d[3] + d[5] + d[1] + (d[1] >> 1)
+    b[1] = a[1] + (a[7] >> 2); b[7] = a[7] - (a[1] >> 2); b[3] = a[3] + (a[5] >> 2); b[5] = (a[3] >> 2) - a[5]
+    return [b[0] + b[7], b[2] + b[5], b[4] + b[3], b[6] + b[1], b[6] - b[1], b[4] - b[3], b[2] - b[5], b[0] - b[7]]
+
+
+def test_inverse8x8_matches_spec_equations():
+    rng = np.random.default_rng(9)
+    for _ in range(30):
+        c = rng.integers(-4096, 4096, (8, 8))
+        t = np.array([inv8_py(r) for r in c])
+        want = np.array([inv8_py(col) for col in t.T]).T
+        out = np.zeros(64, np.int32)
+        L.jmo_inverse8x8(ptr(arr(c.reshape(-1))), ptr(out))
+        assert (out.reshape(8, 8) == want).all()
+
+
+def test_tq8x8_zero_residual_and_round_trip_bounded():
+    rng = np.random.default_rng(10)
+    pred = rng.integers(0, 256, (6, 64)).astype(np.uint8)
+    lev, rec, cc, nz = oracle_lib.tq8x8(np.zeros((6, 64), np.int16), pred, 28, 1)
+    assert not lev.any() and (rec == pred).all() and not nz.any() and not cc.any()
+    org = rng.integers(0, 256, (40, 64))
+    pred = rng.integers(0, 256, (40, 64)).astype(np.uint8)
+    for qp in (0, 6, 12):
+        lev, rec, cc, nz = oracle_lib.tq8x8((org - pred).astype(np.int16), pred, qp, 1)
+        # quantiser step 0.625 * 2^(qp/6); the 8x8 basis error stays within a few steps
+        assert np.abs(rec.astype(int) - org).max() <= 2 + (1 << (qp // 6)), qp
+
+
+def test_tq8x8_coeff_cost_counts_runs():
+    # a single +-1 level at scan position k costs COEFF_COST8x8[k] (3,3,3,3,2x8,1x12,0...)
+    want = [3] * 4 + [2] * 8 + [1] * 12 + [0] * 40
+    scan = []
+    for s in range(15):
+        xs = range(min(s, 7), -1, -1) if s & 1 else range(max(0, s - 7), min(s, 7) + 1)
+        scan += [(s - x) * 8 + x for x in xs if 0 <= s - x < 8]
+    assert len(scan) == 64 and len(set(scan)) == 64
+    lev, rec, cc, nz = oracle_lib.tq8x8(np.zeros((1, 64), np.int16), np.full((1, 64), 128, np.uint8), 0, 0)
+    assert cc[0] == 0
+    out = np.zeros(64, np.int32)
+    for k in (0, 3, 4, 11, 12, 23, 24, 63):
+        # craft a residual whose transform has (mostly) one coefficient: inverse of a unit level
+        c = np.zeros(64, np.int32)
+        c[scan[k]] = 64
+        L.jmo_inverse8x8(ptr(c), ptr(out))
+        r = ((out + 32) >> 6).astype(np.int16)
+        lev, _, cc, _ = oracle_lib.tq8x8(r.reshape(1, 64), np.full((1, 64), 128, np.uint8), 24, 0)
+        nzk = np.flatnonzero(lev[0])
+        if len(nzk) == 1 and abs(lev[0][nzk[0]]) == 1:
+            assert cc[0] == want[nzk[0]]
+
+
+def test_intra8x8_dc_and_vertical_known_answers():
+    nb = np.zeros(25, np.int32)
+    nb[0] = 100
+    nb[1:17] = np.arange(16) * 10        # top row p[0..15,-1]
+    nb[17:25] = 50                       # left column
+    pred = np.zeros((9, 64), np.uint8)
+    ok = L.jmo_intra8x8_pred(ptr(nb), 1 | 2 | 4 | 8, ptr(pred))
+    assert ok == 0x1FF
+    # filtered top row: p'[0] = (100 + 0 + 10 + 2) >> 2, p'[x] = 10x for a linear ramp inside
+    T = [(100 + 2 * 0 + 10 + 2) >> 2] + [10 * x for x in range(1, 8)]
+    assert list(pred[0][:8]) == T and all(list(pred[0][8 * y:8 * y + 8]) == T for y in range(8))
+    L_ = [(100 + 2 * 50 + 50 + 2) >> 2] + [50] * 7
+    assert (pred[2] == (sum(T) + sum(L_) + 8) >> 4).all()
+    assert all((pred[1][8 * y:8 * y + 8] == L_[y]).all() for y in range(8))
+    ok = L.jmo_intra8x8_pred(ptr(nb), 0, ptr(pred))
+    assert ok == 1 << 2 and (pred[2] == 128).all()
