@@ -401,6 +401,164 @@ __device__ __forceinline__ int i16_pred(const I16Par &p, const uint8_t *T, const
     return clip255((p.iaa + (x - 7) * p.ib + (y - 7) * p.ic + 16) >> 5);
 }
 
+// ======================================================================================
+//  64-lane 8x8 primitives (High profile, Transform8x8Mode): one wave per 8x8 block, lane
+//  l = 8y + x holds raster element l.  dct_luma8x8 / HadamardSAD8x8 / Intra8x8 [J]
+// ======================================================================================
+// normAdjust8x8 class (8.5.9) of raster position (x, y) and the per-class JM tables
+__device__ __forceinline__ int class8(int x, int y) {
+    if (!(x & 3) && !(y & 3)) return 0;
+    if ((x & 1) && (y & 1)) return 1;
+    if ((x & 3) == 2 && (y & 3) == 2) return 2;
+    if ((!(x & 3) && (y & 1)) || ((x & 1) && !(y & 3))) return 3;
+    if ((!(x & 3) && (y & 3) == 2) || ((x & 3) == 2 && !(y & 3))) return 4;
+    return 5;
+}
+static __constant__ int c_q8[6][6] = {{13107, 11428, 20972, 12222, 16777, 15481}, {11916, 10826, 19174, 11058, 14980, 14290},
+                                      {10082, 8943, 15978, 9675, 12710, 11985},   {9362, 8228, 14913, 8931, 11984, 11259},
+                                      {8192, 7346, 13159, 7740, 10486, 9777},     {7282, 6428, 11570, 6830, 9118, 8640}};
+static __constant__ int c_dq8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+                                       {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+// 8x8 frame zig-zag: scan index -> raster (8y + x)
+static __constant__ uint8_t c_scan8[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                           12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                           35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                           58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+// COEFF_COST8x8 [J] of a |level| == 1 coefficient by preceding zero run (64-scan)
+__device__ __forceinline__ int coeff_cost8_run(int run) { return run < 4 ? 3 : run < 12 ? 2 : run < 24 ? 1 : 0; }
+
+// sum over the whole (fully active) wave; every lane gets the sum
+__device__ __forceinline__ int wave_sum(int v) {
+    v = row16_sum(v);
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+__device__ __forceinline__ int w64(int v, int src) { return __shfl(v, src, 64); }
+
+// one 8-point butterfly of the forward 8x8 (JM forward8x8 [J]); returns output k
+__device__ __forceinline__ int fwd8_pick(int x0, int x1, int x2, int x3, int x4, int x5, int x6, int x7, int k) {
+    const int a0 = x0 + x7, a1 = x1 + x6, a2 = x2 + x5, a3 = x3 + x4;
+    const int b0 = a0 + a3, b1 = a1 + a2, b2 = a0 - a3, b3 = a1 - a2;
+    const int a4 = x0 - x7, a5 = x1 - x6, a6 = x2 - x5, a7 = x3 - x4;
+    const int b4 = a5 + a6 + ((a4 >> 1) + a4), b5 = a4 - a7 - ((a6 >> 1) + a6);
+    const int b6 = a4 + a7 - ((a5 >> 1) + a5), b7 = a5 - a6 + ((a7 >> 1) + a7);
+    switch (k) {
+    case 0: return b0 + b1;
+    case 1: return b4 + (b7 >> 2);
+    case 2: return b2 + (b3 >> 1);
+    case 3: return b5 + (b6 >> 2);
+    case 4: return b0 - b1;
+    case 5: return b6 - (b5 >> 2);
+    case 6: return (b2 >> 1) - b3;
+    default: return (b4 >> 2) - b7;
+    }
+}
+// one 8-point inverse (8.5.13.2); returns output k
+__device__ __forceinline__ int inv8_pick(int d0, int d1, int d2, int d3, int d4, int d5, int d6, int d7, int k) {
+    const int a0 = d0 + d4, a4 = d0 - d4, a2 = (d2 >> 1) - d6, a6 = d2 + (d6 >> 1);
+    const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+    const int a1 = -d3 + d5 - d7 - (d7 >> 1), a3 = d1 + d7 - d3 - (d3 >> 1);
+    const int a5 = -d1 + d7 + d5 + (d5 >> 1), a7 = d3 + d5 + d1 + (d1 >> 1);
+    const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+    switch (k) {
+    case 0: return b0 + b7;
+    case 1: return b2 + b5;
+    case 2: return b4 + b3;
+    case 3: return b6 + b1;
+    case 4: return b6 - b1;
+    case 5: return b4 - b3;
+    case 6: return b2 - b5;
+    default: return b0 - b7;
+    }
+}
+// forward 8x8 core transform: rows then columns (lanes exchange by ds_bpermute)
+__device__ __forceinline__ int wave_fwd8x8(int r, int l) {
+    const int x = l & 7, y = l >> 3, rb = 8 * y;
+    const int t = fwd8_pick(w64(r, rb), w64(r, rb + 1), w64(r, rb + 2), w64(r, rb + 3), w64(r, rb + 4), w64(r, rb + 5),
+                            w64(r, rb + 6), w64(r, rb + 7), x);
+    return fwd8_pick(w64(t, x), w64(t, 8 + x), w64(t, 16 + x), w64(t, 24 + x), w64(t, 32 + x), w64(t, 40 + x), w64(t, 48 + x),
+                     w64(t, 56 + x), y);
+}
+// inverse 8x8 (rows first) + reconstruction clip((x + (pred << 6) + 32) >> 6)
+__device__ __forceinline__ int wave_inv8x8(int dq, int l, int pred) {
+    const int x = l & 7, y = l >> 3, rb = 8 * y;
+    const int t = inv8_pick(w64(dq, rb), w64(dq, rb + 1), w64(dq, rb + 2), w64(dq, rb + 3), w64(dq, rb + 4), w64(dq, rb + 5),
+                            w64(dq, rb + 6), w64(dq, rb + 7), x);
+    const int o = inv8_pick(w64(t, x), w64(t, 8 + x), w64(t, 16 + x), w64(t, 24 + x), w64(t, 32 + x), w64(t, 40 + x), w64(t, 48 + x),
+                            w64(t, 56 + x), y);
+    return clip255((o + (pred << 6) + 32) >> 6);
+}
+// quantisation of coefficient c at raster l (dct_luma8x8 [J]): lev_scan = signed level at SCAN
+// position l, dq = normative 8.5.13.1 dequantisation of the signed level at raster l (flat
+// weights), cost = COEFF_COST8x8 sum (wave-uniform); returns the scan-order non-zero mask.
+__device__ __forceinline__ unsigned long long wave_quant8(int c, int l, int qp, int qp_const, int &lev_scan, int &dq, int &cost) {
+    const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 16 + qp_per;
+    const int cls = class8(l & 7, l >> 3);
+    const int level = (abs(c) * c_q8[qp_rem][cls] + qp_const) >> q_bits;
+    const int sl = c < 0 ? -level : level;
+    const int ls = 16 * c_dq8[qp_rem][cls];
+    dq = !level ? 0 : qp >= 36 ? sl * ls * (1 << (qp_per - 6)) : (sl * ls + (1 << (5 - qp_per))) >> (6 - qp_per);
+    const int lvs = w64(sl, c_scan8[l]);
+    const unsigned long long m = __ballot(lvs != 0);
+    int k = 0;
+    if (lvs) {
+        const unsigned long long below = m & ((1ull << l) - 1ull);
+        const int prev = below ? 63 - __clzll(below) : -1;
+        k = abs(lvs) > 1 ? MAX_VALUE : coeff_cost8_run(l - prev - 1);
+    }
+    cost = wave_sum(k);
+    lev_scan = lvs;
+    return m;
+}
+// sum over the wave of |Hadamard| of the 8x8 block (h = 1, 2, 4, 8, 16, 32) or, with quad4, of
+// the four 4x4 blocks (h = 1, 2, 8, 16); wave-uniform
+__device__ __forceinline__ int wave_had_abs(int v, int l, bool quad4) {
+#pragma unroll
+    for (int h = 1; h < 64; h <<= 1) {
+        if (quad4 && (h == 4 || h == 32)) continue;
+        const int p = __shfl_xor(v, h, 64);
+        v = (l & h) ? p - v : v + p;
+    }
+    return wave_sum(abs(v));
+}
+// SATD of an 8x8 block (HadamardSAD8x8 [J]: (sum + 2) >> 2) and the sum of its four 4x4 SATD()
+__device__ __forceinline__ int wave_satd8(int dv, int l, int had) { return had ? (wave_had_abs(dv, l, false) + 2) >> 2 : wave_sum(abs(dv)); }
+__device__ __forceinline__ int wave_satd4x4s(int dv, int l, int had) { return had ? wave_had_abs(dv, l, true) >> 1 : wave_sum(abs(dv)); }
+// scan index k of an 8x8 block b8 -> (raster 4x4 block of the CAVLC interleave, entry)
+__device__ __forceinline__ int il_blk(int b8, int k) { const int j = k & 3; return (2 * (b8 >> 1) + (j >> 1)) * 4 + 2 * (b8 & 1) + (j & 1); }
+
+// Intra8x8 prediction (8.3.2.2) of mode m at (x, y) from the filtered reference edge f[0..24]:
+// f[7 - y] = p'[-1, y], f[8] = p'[-1, -1], f[9 + x] = p'[x, -1]
+__device__ __forceinline__ int i8_pred_px(const int *f, int dcv, int m, int x, int y) {
+#define TAP(c) ((f[(c) - 1] + 2 * f[c] + f[(c) + 1] + 2) >> 2)
+    int z;
+    switch (m) {
+    case 0: return f[9 + x];
+    case 1: return f[7 - y];
+    case 2: return dcv;
+    case 3: return x + y < 14 ? TAP(10 + x + y) : (f[23] + 3 * f[24] + 2) >> 2;
+    case 4: return TAP(8 + x - y);
+    case 5:
+        z = 2 * x - y;
+        if (z >= 0 && !(z & 1)) return (f[8 + x - (y >> 1)] + f[9 + x - (y >> 1)] + 1) >> 1;
+        return z > 0 ? TAP(8 + x - (y >> 1)) : TAP(9 + z);
+    case 6:
+        z = 2 * y - x;
+        if (z >= 0 && !(z & 1)) return (f[8 - y + (x >> 1)] + f[7 - y + (x >> 1)] + 1) >> 1;
+        return z > 0 ? TAP(8 - y + (x >> 1)) : TAP(7 - z);
+    case 7:
+        return (y & 1) ? (f[9 + x + (y >> 1)] + 2 * f[10 + x + (y >> 1)] + f[11 + x + (y >> 1)] + 2) >> 2
+                       : (f[9 + x + (y >> 1)] + f[10 + x + (y >> 1)] + 1) >> 1;
+    default:
+        z = x + 2 * y;
+        if (z > 13) return f[0];
+        if (z == 13) return (f[1] + 3 * f[0] + 2) >> 2;
+        if (!(z & 1)) return (f[7 - y - (x >> 1)] + f[6 - y - (x >> 1)] + 1) >> 1;
+        return (f[7 - y - (x >> 1)] + 2 * f[6 - y - (x >> 1)] + f[5 - y - (x >> 1)] + 2) >> 2;
+    }
+#undef TAP
+}
+
 // debug phase profiling of one macroblock (DevParams::prof): lane 0 of wave w of the matching group
 __device__ __forceinline__ bool prof_mb_here(const DevParams &d, int mbx, int mby, int w = 0) {
     return d.prof && threadIdx.x == 64 * w && d.prof_mb == mby * d.mbw + mbx;

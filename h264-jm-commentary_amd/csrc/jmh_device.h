@@ -34,6 +34,10 @@ struct MbScratch {
     int8_t ipred[16];
     int16_t i4lev[16][16];               // Intra4x4 levels in scan order
     uint8_t i4rec[256];                  // Intra4x4 reconstruction of the MB
+    // Intra8x8 decision (k_mb_intra8, Transform8x8Mode only)
+    int32_t i8cost, i8cbp, i8modes;      // i8modes: 4 bits per 8x8 block
+    int16_t i8lev[16][16];               // levels in the CAVLC interleave (jmh_mb_result.luma)
+    uint8_t i8rec[256];
 };
 
 struct DevParams {
@@ -41,6 +45,7 @@ struct DevParams {
     int sr, side, npos;
     int search_mode, use_hadamard, restrict_sr;
     int inter_search[8];
+    int t8;                     // Transform8x8Mode (High profile)
     const uint8_t *orgY, *orgU, *orgV;
     const uint8_t *refY, *refU, *refV;
     uint8_t *recY, *recU, *recV;
@@ -76,6 +81,7 @@ struct TickArgs {
     int prof_mb;
     unsigned long long *bprof;           // debug (JMH_BLOCK_PROF): per-block start / end / role
     int me_in_analyse;                   // 1: k_mb_analyse runs the FFS searches; 0: k_mb_me_full did
+    int t8;                              // Transform8x8Mode: k_mb_intra8 ran, k_mb_final decides 4x4 / 8x8
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
     PicParams p[PMAX];
@@ -95,6 +101,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.search_mode = t.search_mode; d.use_hadamard = t.use_hadamard; d.restrict_sr = t.restrict_sr;
 #pragma unroll
     for (int i = 0; i < 8; i++) d.inter_search[i] = t.inter_search[i];
+    d.t8 = t.t8;
     const int ls = t.W * t.H, lc = ls >> 2;
     d.orgY = q.org; d.orgU = q.org + ls; d.orgV = q.org + ls + lc;
     d.refY = q.ref; d.refU = q.ref + ls; d.refV = q.ref + ls + lc;

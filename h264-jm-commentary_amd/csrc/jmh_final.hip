@@ -1,14 +1,17 @@
 // jmh_final.hip — k_mb_final: the second half of encode_one_macroblock [J] (RDO off) for every
-// macroblock of one wavefront diagonal, after k_mb_analyse: the mode decision over the analysis
-// costs, then the residual coding of the chosen mode with 16-lane transform groups
-// (LumaResidualCoding / dct_luma_16x16 / dct_chroma + reconstruction) and the outputs the next
-// diagonal depends on (reconstruction, MVs, reference indices, Intra4x4 modes).
+// macroblock of one wavefront diagonal, after k_mb_analyse (and k_mb_intra8 in the High profile):
+// the mode decision over the analysis costs, then the residual coding of the chosen mode with
+// 16-lane transform groups (LumaResidualCoding / dct_luma_16x16 / dct_chroma + reconstruction),
+// or, with Transform8x8Mode, TransformDecision and dct_luma8x8 on one wave per 8x8 block, and the
+// outputs the next diagonal depends on (reconstruction, MVs, reference indices, intra modes).
 #include "jmh_common.h"
 
 struct FinS {
     uint8_t org[256];
     uint8_t orgc[2][64];
     uint8_t rec[256];
+    uint8_t pred[256];                   // inter prediction (TransformDecision / 8x8 path)
+    int tdc[4][2];                       // per 8x8: sum of 4x4 SATDs, 8x8 SATD
     uint8_t rtop[24];                    // luma row y = -1, x = -1..19 -> [x + 1]
     uint8_t rleft[16];
     uint8_t ctop[2][12];                 // chroma rows y = -1, x = -1..7 -> [x + 1]
@@ -142,13 +145,15 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
             if (sc->cost8x8 < min_cost) { best_mode = JMH_P8x8; min_cost = sc->cost8x8; }
         }
     }
+    if (d.t8 && sc->i8cost <= min_cost) { min_cost = sc->i8cost; best_mode = JMH_I8MB; }   // item 27
     if (sc->i4cost <= min_cost) { min_cost = sc->i4cost; best_mode = JMH_I4MB; }
     const int i16mode = sc->i16mode;
     if (sc->i16cost < min_cost) { min_cost = sc->i16cost; best_mode = JMH_I16MB; }
-    const int is_intra = best_mode == JMH_I4MB || best_mode == JMH_I16MB;
+    const int is_intra = best_mode == JMH_I4MB || best_mode == JMH_I16MB || best_mode == JMH_I8MB;
     int b8mode[4];
     for (int b = 0; b < 4; b++)
-        b8mode[b] = best_mode == JMH_P8x8 ? (best8x8 >> (4 * b)) & 15 : best_mode == JMH_I4MB ? JMH_IBLOCK : best_mode == JMH_I16MB ? 0 : best_mode;
+        b8mode[b] = best_mode == JMH_P8x8 ? (best8x8 >> (4 * b)) & 15 : best_mode == JMH_I4MB ? JMH_IBLOCK : best_mode == JMH_I16MB ? 0
+                  : best_mode == JMH_I8MB ? JMH_I8MB : best_mode;
     if (tid < 32) {
         const int k = tid >> 1, c = tid & 1, b8 = ((k >> 3) << 1) + ((k & 3) >> 1);
         const int bm = best_mode == JMH_P8x8 ? (best8x8 >> (4 * b8)) & 15 : best_mode;
@@ -158,9 +163,18 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
 
     // ======== luma residual coding: 16 blocks x 16 lanes
     int cbp = 0, cbp_blk = 0;
+    bool tr8 = false;                                                 // 8x8 transform
     const int blk = tid >> 4, l = tid & 15, lx = l & 3, ly = l >> 2;
     const int px4 = 4 * (blk & 3) + lx, py4 = 4 * (blk >> 2) + ly;   // MB pixel of this lane
-    if (best_mode == JMH_I4MB) {
+    const int w8 = tid >> 6, l8 = tid & 63;                           // 8x8 layout: wave = 8x8 block
+    const int qx = 8 * (w8 & 1) + (l8 & 7), qy = 8 * (w8 >> 1) + (l8 >> 3);
+    if (best_mode == JMH_I8MB) {
+        cbp = sc->i8cbp; tr8 = true;
+        for (int b = 0; b < 4; b++)
+            if ((cbp >> b) & 1) cbp_blk |= 0x33 << ((b >> 1) * 8 + (b & 1) * 2);
+        s.lev[blk][l] = sc->i8lev[blk][l];
+        s.rec[tid] = sc->i8rec[tid];
+    } else if (best_mode == JMH_I4MB) {
         cbp = sc->i4cbp; cbp_blk = sc->i4blk;
         s.lev[blk][l] = sc->i4lev[blk][l];
         s.rec[tid] = sc->i4rec[tid];
@@ -217,6 +231,41 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
     } else {
         // LumaResidualCoding / LumaResidualCoding8x8 (+ SetCoeffAndReconstruction8x8)
         const int p = qpel_direct(d.refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1]);
+        if (d.t8 && (best_mode <= 3 || best8x8 == 0x4444)) {
+            // TransformDecision [J] (item 29): sum of 4x4 SATDs vs sum of 8x8 SATDs of the residual
+            s.pred[py4 * 16 + px4] = (uint8_t)p;
+            __syncthreads();
+            const int dv = s.org[qy * 16 + qx] - s.pred[qy * 16 + qx];
+            const int c4 = wave_satd4x4s(dv, l8, d.use_hadamard), c8 = wave_satd8(dv, l8, d.use_hadamard);
+            if (l8 == 0) { s.tdc[w8][0] = c4; s.tdc[w8][1] = c8; }
+            __syncthreads();
+            tr8 = s.tdc[0][1] + s.tdc[1][1] + s.tdc[2][1] + s.tdc[3][1] < s.tdc[0][0] + s.tdc[1][0] + s.tdc[2][0] + s.tdc[3][0];
+        }
+        if (tr8) {
+            // dct_luma8x8 [J] on one wave per 8x8 block, COEFF_COST8x8 thresholds as for 4x4
+            const int pv = s.pred[qy * 16 + qx];
+            const int q8 = 16 + qp / 6;
+            const int c = wave_fwd8x8(s.org[qy * 16 + qx] - pv, l8);
+            int lev, dq, cc;
+            const unsigned long long nz = wave_quant8(c, l8, qp, intra_round ? (1 << q8) / 3 : (1 << q8) / 6, lev, dq, cc);
+            const int rv = wave_inv8x8(dq, l8, pv);
+            if (l8 == 0) { s.bcost[w8] = cc; s.bnz[w8] = nz != 0; }
+            __syncthreads();
+            int sum_cnt = 0, keep8 = 0;
+            for (int b8 = 0; b8 < 4; b8++) {
+                int c8 = s.bcost[b8];
+                if (c8 <= 4) c8 = 0;                                   // _LUMA_COEFF_COST_
+                else {
+                    keep8 |= 1 << b8;
+                    if (s.bnz[b8]) { cbp |= 1 << b8; cbp_blk |= 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2); }
+                }
+                sum_cnt += c8;
+            }
+            if (sum_cnt <= 5) { keep8 = 0; cbp = 0; cbp_blk = 0; }      // _LUMA_MB_COEFF_COST_
+            const bool keep = (keep8 >> w8) & 1;
+            s.lev[il_blk(w8, l8)][l8 >> 2] = keep ? (int16_t)lev : 0;
+            s.rec[qy * 16 + qx] = (uint8_t)(keep ? rv : pv);
+        } else {
         const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
         int lev, dq, cc;
         const int q_bits = 15 + qp / 6;
@@ -245,7 +294,9 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
         const bool keep = (keep8 >> mb8) & 1;
         s.lev[blk][l] = keep ? (int16_t)lev : 0;
         s.rec[py4 * 16 + px4] = (uint8_t)(keep ? rv : p);
+        }
     }
+    const bool t8flag = tr8 && (best_mode == JMH_I8MB || (cbp & 15));   // transform_size_8x8_flag
     PSTAMP(17);
 
     // ======== chroma: prediction (intra mode from k_mb_analyse, or MC) + dct_chroma [J]
@@ -326,14 +377,15 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
         }
         res->i16mode = (int8_t)(best_mode == JMH_I16MB ? i16mode : 0);
         res->c_ipred_mode = (int8_t)c_mode;
-        res->transform_8x8 = 0; res->pad0 = 0;
+        res->transform_8x8 = (int8_t)t8flag; res->pad0 = 0;
         res->min_cost = min_cost;
         res->reserved = 0;
     }
     res->luma[blk][l] = s.lev[blk][l];
     if (tid < 16) {
         const int k = tid;
-        const int ip = best_mode == JMH_I4MB ? sc->ipred[k] : 2;
+        const int ip = best_mode == JMH_I4MB ? sc->ipred[k]
+                     : best_mode == JMH_I8MB ? (sc->i8modes >> (4 * (((k >> 3) << 1) + ((k & 3) >> 1)))) & 15 : 2;
         res->ipred[k] = (int8_t)ip;
         res->mv[k][0] = s.fmv[k][0]; res->mv[k][1] = s.fmv[k][1];
         res->luma_dc[k] = best_mode == JMH_I16MB ? s.dclev[k] : 0;
@@ -389,7 +441,7 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
                 if (mb_edge) {
                     const int nx = dir == 0 ? mbx - 1 : mbx, ny = dir == 0 ? mby : mby - 1;
                     const jmh_mb_result *rp = d.res + ny * d.mbw + nx;
-                    intra_p = rp->mb_type == JMH_I4MB || rp->mb_type == JMH_I16MB;
+                    intra_p = rp->mb_type == JMH_I4MB || rp->mb_type == JMH_I16MB || rp->mb_type == JMH_I8MB;
                     pcoef = (rp->cbp_blk >> bp) & 1;
                     pref = intra_p ? -1 : 0;
                     pmx = rp->mv[bp][0]; pmy = rp->mv[bp][1];
@@ -414,7 +466,7 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
             const int u1 = c_tc0[cA][0], u2 = c_tc0[cA][1], u3 = c_tc0[cA][2];
             for (int dir = 0; dir < 2; dir++)
                 for (int e = 0; e < 4; e++) {
-                    if (tid < 16) {
+                    if (tid < 16 && !((e & 1) && t8flag)) {             // 8x8 transform: no 4x4 luma edges
                         const int k = tid, b = s.bs[dir][e][k >> 2];
                         if (b) {
                             uint8_t *q = dir == 0 ? &s.dy[k + 4][4 * e + 4] : &s.dy[4 * e + 4][k + 4];

@@ -23,9 +23,12 @@
 hipError_t jmh_launch_interp(const uint8_t *ref, int W, int H, uint8_t *qpel, int qstride, int qplane, hipStream_t st);
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
                                 const int32_t *centres, uint16_t *out, hipStream_t st);
+hipError_t jmh_launch_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
+                            int32_t *cc, int32_t *nz, hipStream_t st);
 hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st);
 
@@ -223,6 +226,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
     if (cfg->pipeline_depth < 0 || cfg->pipeline_depth > PMAX) return JMH_E_INVALID_ARG;
+    if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
     int ndev = jmh_device_count();
     if (ndev <= 0) return JMH_E_NO_DEVICE;
     if (hip_device < 0 || hip_device >= ndev) return JMH_E_INVALID_ARG;
@@ -337,6 +341,7 @@ static int issue_tick(jmh_ctx *c) {
     for (int i = 0; i < 8; i++) t.inter_search[i] = c->cfg.inter_search[i];
     t.prof = c->d_prof; t.prof_mb = c->prof_mb;
     t.me_in_analyse = c->cfg.search_mode == 0;
+    t.t8 = c->cfg.transform_8x8_mode;
     int act[PMAX], nact = 0, nP = 0;
     const int nf = (int)c->fl.size();
     std::vector<int> before(nf);
@@ -372,6 +377,7 @@ static int issue_tick(jmh_ctx *c) {
         if (kt) HCHK(ring_begin(c->ring_an, c->st));
         if (!t.me_in_analyse) HCHK(jmh_launch_me_full(t, c->st));   // SearchMode -1
         HCHK(jmh_launch_analyse(t, c->st));
+        if (t.t8) HCHK(jmh_launch_intra8(t, c->st));   // Intra8x8 decision (High profile)
         if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
         HCHK(jmh_launch_final(t, c->st));
         if (kt) HCHK(ring_end(c->ring_fin, c->st));
@@ -709,6 +715,28 @@ int jmh_tq4x4_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     HCHK(jmh_launch_tq4x4(n, dr, dp, qp, intra, dl, drec, dcc, dnz, c->st));
     HCHK(hipMemcpyAsync(levels, dl, n * 32, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(recon, drec, n * 16, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(coeff_cost, dcc, n * 4, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(nonzero, dnz, n * 4, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    HCHK(hipFree(dr)); HCHK(hipFree(dl)); HCHK(hipFree(dp)); HCHK(hipFree(drec)); HCHK(hipFree(dcc)); HCHK(hipFree(dnz));
+    return JMH_OK;
+}
+
+int jmh_tq8x8_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels,
+                    uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
+    if (!c || n <= 0 || !resid || !pred || !levels || !recon || !coeff_cost || !nonzero || qp < 0 || qp > 51) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    int16_t *dr, *dl;
+    uint8_t *dp, *drec;
+    int32_t *dcc, *dnz;
+    HCHK(hipMalloc((void **)&dr, n * 128)); HCHK(hipMalloc((void **)&dl, n * 128));
+    HCHK(hipMalloc((void **)&dp, n * 64)); HCHK(hipMalloc((void **)&drec, n * 64));
+    HCHK(hipMalloc((void **)&dcc, n * 4)); HCHK(hipMalloc((void **)&dnz, n * 4));
+    HCHK(hipMemcpyAsync(dr, resid, n * 128, hipMemcpyHostToDevice, c->st));
+    HCHK(hipMemcpyAsync(dp, pred, n * 64, hipMemcpyHostToDevice, c->st));
+    HCHK(jmh_launch_tq8x8(n, dr, dp, qp, intra, dl, drec, dcc, dnz, c->st));
+    HCHK(hipMemcpyAsync(levels, dl, n * 128, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(recon, drec, n * 64, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(coeff_cost, dcc, n * 4, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(nonzero, dnz, n * 4, hipMemcpyDeviceToHost, c->st));
     HCHK(hipStreamSynchronize(c->st));

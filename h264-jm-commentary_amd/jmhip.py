@@ -89,6 +89,7 @@ _SIGS = {
     "jmh_get_timing": (_I, [_P, ctypes.POINTER(JmhTiming)]),
     "jmh_ffs_sad_table": (_I, [_P, _I, _P, _P, _P]),
     "jmh_tq4x4_batch": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "jmh_tq8x8_batch": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "jmh_read_qpel": (_I, [_P, _P]),
 }
 EXPORTED = tuple(_SIGS)
@@ -278,6 +279,18 @@ class Encoder:
         nz = np.empty(n, np.int32)
         _check(self.lib.jmh_tq4x4_batch(self.ctx, n, _ptr(resid), _ptr(pred), qp, intra, _ptr(lev),
                                         _ptr(rec), _ptr(cc), _ptr(nz)), "jmh_tq4x4_batch")
+        return lev, rec, cc, nz
+
+    def tq8x8(self, resid, pred, qp, intra):
+        resid = np.ascontiguousarray(resid, np.int16)
+        pred = np.ascontiguousarray(pred, np.uint8)
+        n = resid.shape[0]
+        lev = np.empty((n, 64), np.int16)
+        rec = np.empty((n, 64), np.uint8)
+        cc = np.empty(n, np.int32)
+        nz = np.empty(n, np.int32)
+        _check(self.lib.jmh_tq8x8_batch(self.ctx, n, _ptr(resid), _ptr(pred), qp, intra, _ptr(lev),
+                                        _ptr(rec), _ptr(cc), _ptr(nz)), "jmh_tq8x8_batch")
         return lev, rec, cc, nz
 
     def read_qpel(self):

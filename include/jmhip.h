@@ -19,6 +19,7 @@
  *   enc_picture->imgY / imgUV (unfiltered reconstruction)   jmh_read_recon()
  *   mv-search.c › SetupFastFullPelSearch (BlockSAD table)    jmh_ffs_sad_table()   (unit seam)
  *   block.c › dct_luma (4x4 TQ + recon)                     jmh_tq4x4_batch()     (unit seam)
+ *   block.c › dct_luma8x8 (JM FRExt, High profile)          jmh_tq8x8_batch()     (unit seam)
  *
  * Reference citations: the mounted reference (/root/reference) holds only README.md:1-4 (an
  * annotated-JM commentary with no source), so no file:line into JM source exists; the JM
@@ -209,6 +210,13 @@ int  jmh_ffs_sad_table(jmh_ctx *ctx, int n_mb, const int32_t *mb_xy, const int32
  *   pred[n][16] (raster), levels[n][16] (scan order), recon[n][16] (raster); nonzero[n].
  *   intra selects the JM 8.6 intra rounding offset ((1<<q_bits)/3) vs inter (/6).          */
 int  jmh_tq4x4_batch(jmh_ctx *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp,
+                     int intra, int16_t *levels, uint8_t *recon, int32_t *coeff_cost,
+                     int32_t *nonzero);
+/* jmh_tq8x8_batch: dct_luma8x8 (High profile, a12) on n independent 8x8 blocks, the same
+ *   one-wave-per-block primitive as the macroblock kernels.  resid[n][64] (raster), pred[n][64]
+ *   (raster), levels[n][64] (8x8 zig-zag scan order), recon[n][64] (raster); coeff_cost[n]
+ *   (COEFF_COST8x8), nonzero[n].  intra selects the (1<<q_bits)/3 rounding offset vs /6.   */
+int  jmh_tq8x8_batch(jmh_ctx *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp,
                      int intra, int16_t *levels, uint8_t *recon, int32_t *coeff_cost,
                      int32_t *nonzero);
 /* jmh_read_qpel: the 16 quarter-pel phase planes of the current reference (test seam for

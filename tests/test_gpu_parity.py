@@ -85,6 +85,25 @@ def test_tq4x4_all_qp(intra):
             assert np.array_equal(x, y), f"qp {qp}"
 
 
+# ---------------- a12: 8x8 TQ + recon (High profile) ----------------
+@pytest.mark.parametrize("intra", [0, 1])
+def test_tq8x8_all_qp(intra):
+    rng = np.random.default_rng(12)
+    g = jmhip.Encoder(32, 32, search_range=4)
+    n = 1024
+    resid = rng.integers(-255, 256, (n, 64)).astype(np.int16)
+    resid[:16] = 255          # max-magnitude residuals
+    resid[16:32] = -255
+    resid[32:48] = 0
+    resid[48:64] = rng.integers(-2, 3, (16, 64))    # sparse levels: COEFF_COST8x8 runs
+    pred = rng.integers(0, 256, (n, 64)).astype(np.uint8)
+    for qp in range(52):
+        a = g.tq8x8(resid, pred, qp, intra)
+        b = oracle_lib.tq8x8(resid, pred, qp, intra)
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y), f"qp {qp}"
+
+
 # ---------------- a2: FFS SAD table ----------------
 @pytest.mark.parametrize("sr", [4, 16, 32])
 def test_sad_table(sr):
@@ -149,6 +168,29 @@ def test_ippp_qcif_sr16():
 def test_ipp_configs(kw, qp):
     pics = synth_seq(96, 64, 3, 7)
     encode_pair(96, 64, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], qp, **kw)
+
+
+@pytest.mark.parametrize("kw,qp", [
+    (dict(search_range=16), 28),
+    (dict(search_range=8), 40),                                    # mostly Intra8x8 I pictures
+    (dict(search_range=8, use_hadamard=0), 8),
+    (dict(search_range=8), 0),
+    (dict(search_range=8), 51),
+    (dict(search_range=8, inter_search=(1, 1, 1, 1, 0, 0, 0)), 24),   # P8x8 with 8x8 sub-blocks only
+    (dict(search_range=8, search_mode=-1, restrict_search_range=0), 33),
+])
+def test_high_profile_transform8x8(kw, qp):
+    """a12 + Intra8x8 (Transform8x8Mode = 1): k_mb_intra8, TransformDecision, dct_luma8x8."""
+    pics = synth_seq(96, 64, 3, 17)
+    encode_pair(96, 64, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], qp,
+                transform_8x8_mode=1, **kw)
+
+
+def test_high_profile_qcif_ippp():
+    pics = synth_seq(176, 144, 4, 21)
+    for qp in (20, 30, 38):
+        encode_pair(176, 144, pics, [jmhip.JMH_I_SLICE] + [jmhip.JMH_P_SLICE] * 3, qp, search_range=16,
+                    transform_8x8_mode=1)
 
 
 def test_random_content_p_frames():
@@ -310,6 +352,12 @@ def run_lencod(binary, out_dir, extra):
     ["InputFile=synthetic:5", "FramesToBeEncoded=4", "SourceWidth=320", "SourceHeight=240", "SearchRange=16",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=6", "LoopFilterBetaOffset=6", "QPFirstFrame=40",
      "QPRemainingFrame=44"],
+    # High profile, 8x8 transform (a12): pipelined, device deblocking without 4x4 luma edges
+    ["InputFile=synthetic:21", "FramesToBeEncoded=8", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
+     "ProfileIDC=100", "Transform8x8Mode=1"],
+    ["InputFile=synthetic:22", "FramesToBeEncoded=4", "SourceWidth=200", "SourceHeight=120", "SearchRange=8",
+     "ProfileIDC=100", "Transform8x8Mode=1", "QPFirstFrame=38", "QPRemainingFrame=40", "IntraPeriod=2",
+     "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=-3", "LoopFilterBetaOffset=2"],
 ])
 def test_lencod_bitstream_identical(extra):
     with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:
