@@ -275,6 +275,23 @@ __device__ __forceinline__ void set_mvp(const NB &nb, int bx4, int by4, int bsx,
     px = p[0]; py = p[1];
 }
 
+// neighbour k (0 A, 1 B, 2 C, or D when C is not available, as in set_mvp) of a block
+template <class NB>
+__device__ __forceinline__ bool mvp_nbr(const NB &nb, int bx4, int by4, int bsx, int k, int &ref, int &mx, int &my) {
+    const int mb_x = 4 * bx4, mb_y = 4 * by4;
+    if (k == 0) return nb(mb_x - 1, mb_y, ref, mx, my);
+    if (k == 1) return nb(mb_x, mb_y - 1, ref, mx, my);
+    bool av_c = nb(mb_x + bsx, mb_y - 1, ref, mx, my);
+    if (mb_y > 0) {
+        if (mb_x < 8) {
+            if (mb_y == 8) { if (bsx == 16) av_c = false; }
+            else if (mb_x + bsx == 8) av_c = false;
+        } else if (mb_x + bsx == 16) av_c = false;
+    }
+    if (!av_c) av_c = nb(mb_x - 1, mb_y - 1, ref, mx, my);
+    return av_c;
+}
+
 // border neighbour cells of an MB: 0..5 = row y4 = -1 (x4 = -1..4), 6..9 = column x4 = -1 (y4 = 0..3)
 struct Border {
     int16_t mv[10][2];

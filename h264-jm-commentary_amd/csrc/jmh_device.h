@@ -54,6 +54,8 @@ struct DevParams {
     int16_t *mv;
     int8_t *refidx;
     int8_t *ipred;
+    const int16_t *tmv;         // EPZS temporal predictors: the previous picture's MVs / ref_idx
+    const int8_t *tref;         //   (null: no previous picture)
     jmh_mb_result *res;
     MbScratch *scr;
     unsigned long long *prof;   // debug phase timestamps (null: off)
@@ -69,6 +71,8 @@ struct PicParams {
     uint8_t *rec, *dbk;                  // dbk null: no deblocking
     int16_t *mv;
     int8_t *refidx, *ipred;
+    const int16_t *tmv;                  // previous picture's motion field (EPZS temporal predictors)
+    const int8_t *tref;
     jmh_mb_result *res;
     MbScratch *scr;
     int32_t slice_type, qp, lambda_mode, lambda_motion, cqp_off, lf_disable, lf_offA, lf_offB;
@@ -81,6 +85,7 @@ struct TickArgs {
     int prof_mb;
     unsigned long long *bprof;           // debug (JMH_BLOCK_PROF): per-block start / end / role
     int me_in_analyse;                   // 1: k_mb_analyse runs the FFS searches; 0: k_mb_me_full did
+                                         //   (full search, SearchMode -1, or EPZS, SearchMode 3)
     int t8;                              // Transform8x8Mode: k_mb_intra8 ran, k_mb_final decides 4x4 / 8x8
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
@@ -109,6 +114,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.dbkY = q.dbk; d.dbkU = q.dbk ? q.dbk + ls : nullptr; d.dbkV = q.dbk ? q.dbk + ls + lc : nullptr;
     d.lf_disable = q.lf_disable; d.lf_offA = q.lf_offA; d.lf_offB = q.lf_offB;
     d.mv = q.mv; d.refidx = q.refidx; d.ipred = q.ipred; d.res = q.res; d.scr = q.scr;
+    d.tmv = q.tmv; d.tref = q.tref;
     d.prof = e == 0 ? t.prof : nullptr; d.prof_mb = t.prof_mb;
     d.slice_type = q.slice_type; d.qp = q.qp; d.lambda_mode = q.lambda_mode; d.lambda_motion = q.lambda_motion;
     d.cqp_off = q.cqp_off; d.diag = q.diag; d.y_min = q.y_min;

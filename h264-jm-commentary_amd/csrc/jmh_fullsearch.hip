@@ -1,5 +1,6 @@
 // jmh_fullsearch.hip — k_mb_me_full: the motion-search half of encode_one_macroblock [J] with
-// SearchMode = -1 (FullPelBlockMotionSearch), one 256-thread workgroup per P macroblock.
+// SearchMode = -1 (FullPelBlockMotionSearch) or SearchMode = 3 (EPZSPelBlockMotionSearch, see
+// epzs_fullpel below), one 256-thread workgroup per P macroblock.
 //
 // Unlike FFS, every search centres its window on its OWN predictor (MVP/4 clamped to its range),
 // so there is no shared SAD table: each of the 41 searches computes the SAD of its block at all
@@ -20,14 +21,18 @@
 #define FST 156                               // window row stride (>= FW_MAX + 4, multiple of 4)
 #define FKOFF 4096                            // cost offset in keys (16x16 zero-vector bias)
 
+#define NPRED 41                              // EPZS predictor slots (oracle epzs_predictors)
+
 struct FullS {
     uint8_t g[FW_MAX * FST + 16];
     uint8_t org[256];
     Border bd;
     int16_t all_mv[8][16][2];
     int motion_cost[8][4];
-    unsigned red[NTF / 64];
+    unsigned red[2][NTF / 64];
     int ccost[9];
+    int16_t cand[NPRED][2];                    // EPZS predictors (full pel); invalid: INT16_MIN
+    int cost0;
 };
 
 // neighbour view of a search of block type bt in 8x8 block b8 (as NbMe in jmh_analyse.hip)
@@ -55,9 +60,131 @@ __device__ __forceinline__ uint32_t lds_u32(const uint8_t *p) {   // 4 bytes at 
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 
+// SAD of the block (bx4, by4, 4 w4 x 4 h4) at full-pel displacement (mx, my) from the LDS window
+// on a 16-lane group: lane r sums row r (rows >= 4 h4 contribute 0); all 16 lanes get the sum
+__device__ __forceinline__ int group_sad(const FullS &s, int off, int bx4, int by4, int w4, int h4, int mx, int my, int r) {
+    uint32_t sad = 0;
+    if (r < 4 * h4) {
+        const uint8_t *row = s.g + (off + 4 * by4 + r + my) * FST + off + 4 * bx4 + mx;
+        const uint32_t *org = reinterpret_cast<const uint32_t *>(s.org + (4 * by4 + r) * 16 + 4 * bx4);
+        for (int q = 0; q < w4; q++) sad = __builtin_amdgcn_sad_u8(lds_u32(row + 4 * q), org[q], sad);
+    }
+    return row16_sum((int)sad);
+}
+// workgroup minimum of per-thread keys (double-buffered slot: consecutive calls need no second
+// barrier); every thread returns the minimum
+__device__ __forceinline__ unsigned wg_min(FullS &s, unsigned k, int &slot) {
+    k = wave_min_u32(k);
+    if ((threadIdx.x & 63) == 0) s.red[slot][threadIdx.x >> 6] = k;
+    __syncthreads();
+    unsigned m = s.red[slot][0];
+#pragma unroll
+    for (int w = 1; w < NTF / 64; w++) m = min(m, s.red[slot][w]);
+    slot ^= 1;
+    return m;
+}
+
+// EPZSPelBlockMotionSearch [J] as restated in oracle/encode.c epzs_search (JM_SEMANTICS items
+// 33-40): the centre, then 40 ordered predictors (zero, spatial A/B/C, three window rings,
+// temporal co-located + 4, spatial memory, earlier block types), strict '<' in list order (the
+// key's low bits), thresholds medthres = block pixels, then small- or extended-diamond
+// refinement around the best until it stops moving.  16 lanes per candidate SAD.
+__device__ void epzs_fullpel(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int b8, int best8x8, int range,
+                             int mvx0, int mvy0, int pmx, int pmy, int X0, int Y0, int left, int &fmx, int &fmy, int &fcost) {
+    const int tid = threadIdx.x, g = tid >> 4, r = tid & 15;
+    const int lam = d.lambda_motion;
+    const int lw4 = lw4_of(bt), lh4 = lh4_of(bt), w4 = 1 << lw4, h4 = 1 << lh4;
+    const int med = 16 * w4 * h4;
+    const int k0 = by4 * 4 + bx4;
+    auto rnd = [](int v) { return (v + 2) >> 2; };
+    // ---- predictor list (thread i builds slot i)
+    if (tid < NPRED) {
+        const int i = tid;
+        int v = 1, x = 0, y = 0;
+        if (i == 0) { x = mvx0; y = mvy0; }
+        else if (i == 1) { x = 0; y = 0; }
+        else if (i <= 4) {
+            int ref = -1, ax = 0, ay = 0;
+            v = mvp_nbr(NbFull{s, bt, b8, best8x8}, bx4, by4, 4 * w4, i - 2, ref, ax, ay) && ref == 0;
+            x = rnd(ax); y = rnd(ay);
+        } else if (i <= 28) {
+            const int ring = (i - 5) >> 3, k = (i - 5) & 7, rr = range >> (2 - ring);
+            const int wx = k == 1 || k == 4 || k == 6 ? -1 : k == 2 || k == 5 || k == 7 ? 1 : 0;
+            const int wy = k == 0 || k == 4 || k == 5 ? -1 : k == 3 || k == 6 || k == 7 ? 1 : 0;
+            v = rr > 0; x = mvx0 + rr * wx; y = mvy0 + rr * wy;
+        } else if (i <= 33) {
+            const int W4 = d.W >> 2, H4 = d.H >> 2, k = i - 29;   // co-located, left, right, up, down
+            const int px = X0 + bx4 + (k == 1 ? -1 : k == 2 ? w4 : 0);
+            const int py = Y0 + by4 + (k == 3 ? -1 : k == 4 ? h4 : 0);
+            v = d.tref && px >= 0 && px < W4 && py >= 0 && py < H4;
+            const int a = v ? py * W4 + px : 0;
+            v = v && d.tref[a] == 0;
+            if (v) { x = rnd(d.tmv[2 * a]); y = rnd(d.tmv[2 * a + 1]); }
+        } else if (i == 34) {
+            v = left >= 0 && d.inter_search[bt];               // left MB's search (spatial memory)
+            if (v) { x = rnd(d.scr[left].all_mv[bt][k0][0]); y = rnd(d.scr[left].all_mv[bt][k0][1]); }
+        } else {
+            const int t = i - 34;                              // block types 1..6 below bt
+            v = t < bt && d.inter_search[t];
+            if (v) { x = rnd(s.all_mv[t][k0][0]); y = rnd(s.all_mv[t][k0][1]); }
+        }
+        if (v && (abs(x - mvx0) > range || abs(y - mvy0) > range)) v = 0;   // outside the window
+        s.cand[i][0] = (int16_t)(v ? x : -32768);
+        s.cand[i][1] = (int16_t)y;
+    }
+    __syncthreads();
+    int slot = 0;
+    unsigned kb = 0xFFFFFFFFu;
+    for (int i = g; i < NPRED; i += 16) {
+        const bool v = s.cand[i][0] != -32768;
+        const int x = v ? s.cand[i][0] : mvx0, y = v ? s.cand[i][1] : mvy0;
+        const int c = group_sad(s, off, bx4, by4, w4, h4, x, y, r) + lam * (mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+        if (i == 0 && r == 0) s.cost0 = c;
+        if (v) kb = min(kb, ((unsigned)c << 6) | (unsigned)i);
+    }
+    unsigned best = wg_min(s, kb, slot);
+    int bx = mvx0, by = mvy0, min_mcost = s.cost0;
+    if (min_mcost >= med) {                                   // else: stop at the centre
+        min_mcost = (int)(best >> 6);
+        bx = s.cand[best & 63][0]; by = s.cand[best & 63][1];
+        if (min_mcost >= med) {                               // pattern refinement
+            const bool sd = min_mcost < med + ((3 * med) >> 1);
+            const int np = sd ? 4 : 12;
+            for (int it = 0; it < 4 * NPOS_MAX; it++) {
+                unsigned k = 0xFFFFFFFFu;
+                if (g < np) {
+                    int px, py;
+                    if (sd) { px = g == 1 ? -1 : g == 2 ? 1 : 0; py = g == 0 ? -1 : g == 3 ? 1 : 0; }
+                    else {
+                        const int e = g;   // (0,-2) (-1,-1) (1,-1) (-2,0) (2,0) (-1,1) (1,1) (0,2) then the small diamond
+                        px = e < 8 ? (e == 1 || e == 5 ? -1 : e == 2 || e == 6 ? 1 : e == 3 ? -2 : e == 4 ? 2 : 0)
+                                   : (e == 9 ? -1 : e == 10 ? 1 : 0);
+                        py = e < 8 ? (e == 0 ? -2 : e <= 2 ? -1 : e <= 4 ? 0 : e <= 6 ? 1 : 2) : (e == 8 ? -1 : e == 11 ? 1 : 0);
+                    }
+                    const int x = bx + px, y = by + py;
+                    const bool v = abs(x - mvx0) <= range && abs(y - mvy0) <= range;
+                    const int c = group_sad(s, off, bx4, by4, w4, h4, v ? x : bx, v ? y : by, r) + lam * (mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+                    if (v) k = ((unsigned)c << 6) | (unsigned)g;
+                }
+                const unsigned m = wg_min(s, k, slot);
+                if (m == 0xFFFFFFFFu || (int)(m >> 6) >= min_mcost) break;
+                min_mcost = (int)(m >> 6);
+                const int e = (int)(m & 63);
+                if (sd) { bx += e == 1 ? -1 : e == 2 ? 1 : 0; by += e == 0 ? -1 : e == 3 ? 1 : 0; }
+                else {
+                    bx += e < 8 ? (e == 1 || e == 5 ? -1 : e == 2 || e == 6 ? 1 : e == 3 ? -2 : e == 4 ? 2 : 0) : (e == 9 ? -1 : e == 10 ? 1 : 0);
+                    by += e < 8 ? (e == 0 ? -2 : e <= 2 ? -1 : e <= 4 ? 0 : e <= 6 ? 1 : 2) : (e == 8 ? -1 : e == 11 ? 1 : 0);
+                }
+            }
+        }
+    }
+    fmx = bx; fmy = by; fcost = min_mcost;
+}
+
 // BlockMotionSearch [J] for one block: full-pel full search + SubPelBlockMotionSearch
-__device__ __attribute__((noinline)) void full_block_search(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int mc, int b8, int best8x8) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+__device__ __attribute__((noinline)) void full_block_search(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int mc, int b8,
+                                                           int best8x8, int X0, int Y0, int left) {
+    const int tid = threadIdx.x;
     const int lam = d.lambda_motion, had = d.use_hadamard;
     const bool slice_p = d.slice_type == JMH_P_SLICE;
     const int range = d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr;
@@ -65,6 +192,11 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
     int pmx, pmy;
     set_mvp(NbFull{s, bt, b8, best8x8}, bx4, by4, 4 * w4, 4 * h4, pmx, pmy);
     const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
+    int fmx, fmy, min_mcost;
+    if (d.search_mode == 3) {
+        epzs_fullpel(d, s, off, bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, pmx, pmy, X0, Y0, left, fmx, fmy, min_mcost);
+        if (had) min_mcost = BIGCOST;
+    } else {
     // ---- full pel: every thread a stride of positions, SADs by dword v_sad_u8
     const int side = 2 * range + 1, npos = side * side;
     unsigned kb = 0xFFFFFFFFu;
@@ -83,16 +215,13 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
         cost += (int)sad;
         kb = min(kb, ((unsigned)(cost + FKOFF) << 13) | (unsigned)spiral_index(dx, dy));
     }
-    kb = wave_min_u32(kb);
-    if (lane == 0) s.red[wave] = kb;
-    __syncthreads();
-    unsigned best = s.red[0];
-#pragma unroll
-    for (int w = 1; w < NTF / 64; w++) best = min(best, s.red[w]);
+    int slot = 0;
+    const unsigned best = wg_min(s, kb, slot);
     int rx, ry;
     spiral_pos((int)(best & 8191u), rx, ry);
-    const int fmx = mvx0 + rx, fmy = mvy0 + ry;
-    int min_mcost = had ? BIGCOST : (int)(best >> 13) - FKOFF;
+    fmx = mvx0 + rx; fmy = mvy0 + ry;
+    min_mcost = had ? BIGCOST : (int)(best >> 13) - FKOFF;
+    }
     // ---- sub pel (half then quarter), samples from the window through the 6-tap
     const bool check0 = bt == 1 && fmx == 0 && fmy == 0 && had && slice_p;
     auto px = [&](int x, int y) { return (int)s.g[y * FST + x]; };
@@ -143,6 +272,7 @@ __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, sr = d.sr;
     const int off = 2 * sr + 4, wdim = 16 + 2 * off;
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
+    const int X0 = 4 * mbx, Y0 = 4 * mby, left = mbx > 0 ? mby * d.mbw + mbx - 1 : -1;   // EPZS
     s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     if (tid < 10) load_border(d, s.bd, tid, mbx, mby);
     else if (tid >= 32 && tid < 64) s.motion_cost[(tid - 32) >> 2][tid & 3] = 0;
@@ -166,24 +296,24 @@ __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
     }
     __syncthreads();
     // PartitionMotionSearch [J] order: 16x16, 16x8 (2), 8x16 (2)
-    full_block_search(d, s, off, 1, 0, 0, 0, 0, 0);
-    full_block_search(d, s, off, 2, 0, 0, 0, 0, 0);
-    full_block_search(d, s, off, 2, 0, 2, 1, 0, 0);
-    full_block_search(d, s, off, 3, 0, 0, 0, 0, 0);
-    full_block_search(d, s, off, 3, 2, 0, 1, 0, 0);
+    full_block_search(d, s, off, 1, 0, 0, 0, 0, 0, X0, Y0, left);
+    full_block_search(d, s, off, 2, 0, 0, 0, 0, 0, X0, Y0, left);
+    full_block_search(d, s, off, 2, 0, 2, 1, 0, 0, X0, Y0, left);
+    full_block_search(d, s, off, 3, 0, 0, 0, 0, 0, X0, Y0, left);
+    full_block_search(d, s, off, 3, 2, 0, 1, 0, 0, X0, Y0, left);
     // P8x8: per 8x8 block the sub-modes 4..7, then its best sub-mode (read through best8x8)
     int best8x8 = 0, cost8x8 = 0;
     for (int b8 = 0; b8 < 4; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        full_block_search(d, s, off, 4, X, Y, b8, b8, best8x8);
-        full_block_search(d, s, off, 5, X, Y, b8, b8, best8x8);
-        full_block_search(d, s, off, 5, X, Y + 1, b8, b8, best8x8);
-        full_block_search(d, s, off, 6, X, Y, b8, b8, best8x8);
-        full_block_search(d, s, off, 6, X + 1, Y, b8, b8, best8x8);
-        full_block_search(d, s, off, 7, X, Y, b8, b8, best8x8);
-        full_block_search(d, s, off, 7, X + 1, Y, b8, b8, best8x8);
-        full_block_search(d, s, off, 7, X, Y + 1, b8, b8, best8x8);
-        full_block_search(d, s, off, 7, X + 1, Y + 1, b8, b8, best8x8);
+        full_block_search(d, s, off, 4, X, Y, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 5, X, Y, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 5, X, Y + 1, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 6, X, Y, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 6, X + 1, Y, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 7, X, Y, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 7, X + 1, Y, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 7, X, Y + 1, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 7, X + 1, Y + 1, b8, b8, best8x8, X0, Y0, left);
         int mc8 = BIGCOST, bm = 0;
         for (int mode = 4; mode <= 7; mode++) {
             if (!d.inter_search[mode]) continue;

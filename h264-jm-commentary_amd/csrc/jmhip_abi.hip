@@ -98,6 +98,7 @@ struct PicBuf {
 // a picture in flight (not yet fully issued)
 struct Flight {
     int id, entry, ref_entry;            // ref_entry: ring entry read as reference (-1: d_ref / none)
+    int tmv_entry;                       // ring entry whose motion field EPZS reads (-1: none)
     int pred_id;                         // picture it must trail by PIPE_LAG diagonals (-1: none)
     int stage, started, readback;
     PicParams pp;
@@ -222,7 +223,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 15) || (cfg->height & 15)) return JMH_E_INVALID_ARG;
     if (cfg->search_range < 1 || cfg->search_range > 64) return JMH_E_INVALID_ARG;
     if (cfg->search_range > SRMAX) return JMH_E_UNSUPPORTED_CFG;            // LDS-resident window
-    if (cfg->search_mode != 0 && cfg->search_mode != -1) return JMH_E_UNSUPPORTED_CFG;   // FFS / full search
+    if (cfg->search_mode != 0 && cfg->search_mode != -1 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;   // FFS / full / EPZS
     if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
     if (cfg->pipeline_depth < 0 || cfg->pipeline_depth > PMAX) return JMH_E_INVALID_ARG;
@@ -401,7 +402,7 @@ static int issue_tick(jmh_ctx *c) {
 
 static bool entry_busy(const jmh_ctx *c, int e) {
     for (const Flight &f : c->fl)
-        if (f.entry == e || f.ref_entry == e) return true;
+        if (f.entry == e || f.ref_entry == e || f.tmv_entry == e) return true;
     return false;
 }
 
@@ -437,6 +438,9 @@ static int push_picture(jmh_ctx *c, const uint8_t *src, int entry, const jmh_fra
     f.entry = entry;
     f.ref_entry = p_slice && (c->ref_kind == REF_REC || c->ref_kind == REF_DBK) ? c->ref_entry : -1;
     f.pred_id = -1;
+    // EPZS temporal predictors read the motion field of the picture pushed last (the reference
+    // itself when it is the previous picture on the device; otherwise a completed picture)
+    f.tmv_entry = p_slice && c->cfg.search_mode == 3 && c->last_id >= 0 ? c->last_entry : -1;
     if (f.ref_entry >= 0)
         for (const Flight &g : c->fl)
             if (g.entry == f.ref_entry) f.pred_id = g.id;
@@ -451,6 +455,8 @@ static int push_picture(jmh_ctx *c, const uint8_t *src, int entry, const jmh_fra
     q.org = src; q.ref = ref_ptr(c);
     q.rec = b.rec; q.dbk = fp->deblock ? b.dbk : nullptr;
     q.mv = b.mv; q.refidx = b.refidx; q.ipred = b.ipred; q.res = b.res; q.scr = b.scr;
+    q.tmv = f.tmv_entry >= 0 ? c->ring[f.tmv_entry].mv : nullptr;
+    q.tref = f.tmv_entry >= 0 ? c->ring[f.tmv_entry].refidx : nullptr;
     q.slice_type = fp->slice_type; q.qp = fp->qp; q.lambda_mode = fp->lambda_mode; q.lambda_motion = fp->lambda_motion;
     q.cqp_off = fp->chroma_qp_offset;
     q.lf_disable = fp->lf_disable; q.lf_offA = 2 * fp->lf_alpha_div2; q.lf_offB = 2 * fp->lf_beta_div2;

@@ -158,7 +158,7 @@ static int parse_file(jm_input *inp, const char *fn, char *err, int errlen) {
 int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->rdopt != 0) { snprintf(err, errlen, "RDOptimization=%d not supported (RDO-off path only)", inp->rdopt); return -1; }
     if (inp->symbol_mode != 0) { snprintf(err, errlen, "SymbolMode=1 (CABAC) not supported in this build"); return -1; }
-    if (inp->search_mode != 0 && inp->search_mode != -1) { snprintf(err, errlen, "SearchMode=%d not supported (use -1 or 0)", inp->search_mode); return -1; }
+    if (inp->search_mode != 0 && inp->search_mode != -1 && inp->search_mode != 3) { snprintf(err, errlen, "SearchMode=%d not supported (use -1, 0 or 3)", inp->search_mode); return -1; }
     if (inp->num_ref_frames != 1) { snprintf(err, errlen, "NumberReferenceFrames=%d not supported (1)", inp->num_ref_frames); return -1; }
     if (inp->constrained_intra) { snprintf(err, errlen, "UseConstrainedIntraPred=1 not supported"); return -1; }
     if (inp->profile_idc != 66 && inp->profile_idc != 100) { snprintf(err, errlen, "ProfileIDC=%d not supported (66 or 100)", inp->profile_idc); return -1; }

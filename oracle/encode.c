@@ -52,22 +52,31 @@ static int nb4(const mbs *s, int xN, int yN, int *idx) {
     return 1;
 }
 
-/* SetMotionVectorPredictor [J] / H.264 8.4.1.3 (list 0). block_x/y in 4x4 units. */
-static void set_mvp(const mbs *s, int pmv[2], int ref, int block_x, int block_y, int bsx, int bsy) {
-    const jmo_ctx *c = s->c;
-    int mb_x = 4 * block_x, mb_y = 4 * block_y;
-    int ia = 0, ib = 0, ic = 0, id = 0;
-    int av_a = nb4(s, mb_x - 1, mb_y, &ia);
-    int av_b = nb4(s, mb_x, mb_y - 1, &ib);
-    int av_c = nb4(s, mb_x + bsx, mb_y - 1, &ic);
+/* the A, B, C neighbours of SetMotionVectorPredictor [J] / 8.4.1.3 (C replaced by D when not
+ * available, including C inside the MB but later in decoding order); 4x4 picture indices */
+static void mvp_neighbours(const mbs *s, int block_x, int block_y, int bsx, int bsy, int *av_a, int *av_b,
+                           int *av_c, int *ia, int *ib, int *ic) {
+    int mb_x = 4 * block_x, mb_y = 4 * block_y, id = 0;
+    (void)bsy;
+    *av_a = nb4(s, mb_x - 1, mb_y, ia);
+    *av_b = nb4(s, mb_x, mb_y - 1, ib);
+    *av_c = nb4(s, mb_x + bsx, mb_y - 1, ic);
     int av_d = nb4(s, mb_x - 1, mb_y - 1, &id);
     if (mb_y > 0) {                       /* C inside the MB but later in decoding order */
         if (mb_x < 8) {
-            if (mb_y == 8) { if (bsx == 16) av_c = 0; }
-            else if (mb_x + bsx == 8) av_c = 0;
-        } else if (mb_x + bsx == 16) av_c = 0;
+            if (mb_y == 8) { if (bsx == 16) *av_c = 0; }
+            else if (mb_x + bsx == 8) *av_c = 0;
+        } else if (mb_x + bsx == 16) *av_c = 0;
     }
-    if (!av_c) { av_c = av_d; ic = id; }
+    if (!*av_c) { *av_c = av_d; *ic = id; }
+}
+
+/* SetMotionVectorPredictor [J] / H.264 8.4.1.3 (list 0). block_x/y in 4x4 units. */
+static void set_mvp(const mbs *s, int pmv[2], int ref, int block_x, int block_y, int bsx, int bsy) {
+    const jmo_ctx *c = s->c;
+    int ia = 0, ib = 0, ic = 0, av_a, av_b, av_c;
+    mvp_neighbours(s, block_x, block_y, bsx, bsy, &av_a, &av_b, &av_c, &ia, &ib, &ic);
+    int mb_x = 4 * block_x, mb_y = 4 * block_y;
     int rL = av_a ? c->refidx[ia] : -1;
     int rU = av_b ? c->refidx[ib] : -1;
     int rUR = av_c ? c->refidx[ic] : -1;
@@ -245,6 +254,97 @@ static int full_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int pm
     return min_mcost;
 }
 
+/* ====================================================================================== */
+/*  EPZS (SearchMode 3): me_epzs.c › EPZSPelBlockMotionSearch [J] as restated in             */
+/*  docs/JM_SEMANTICS.md items 33-40 (JM parity unpinned: no JM source exists here)          */
+/* ====================================================================================== */
+static const int epzs_ed[12][2] = {{0, -2}, {-1, -1}, {1, -1}, {-2, 0}, {2, 0}, {-1, 1},   /* extended diamond */
+                                   {1, 1},  {0, 2},   {0, -1}, {-1, 0}, {1, 0}, {0, 1}};
+static const int epzs_sd[4][2] = {{0, -1}, {-1, 0}, {1, 0}, {0, 1}};                       /* small diamond   */
+static const int epzs_win[8][2] = {{0, -1}, {-1, 0}, {1, 0}, {0, 1}, {-1, -1}, {1, -1}, {-1, 1}, {1, 1}};
+static inline int rnd_fp(int v) { return (v + 2) >> 2; }          /* rshift_rnd_sf(mv, 2) [J] */
+
+/* SAD of the block at full-pel displacement (mx, my) + MV_COST */
+static int epzs_cost(const mbs *s, int bt, int bx4, int by4, int mx, int my, int pmvx, int pmvy) {
+    const jmo_ctx *c = s->c;
+    int bsx = jmo_blc_size[bt][0], bsy = jmo_blc_size[bt][1];
+    int px = s->pix_x + 4 * bx4, py = s->pix_y + 4 * by4, sad = 0;
+    for (int y = 0; y < bsy; y++)
+        for (int x = 0; x < bsx; x++)
+            sad += iabs(s->org[(4 * by4 + y) * 16 + 4 * bx4 + x] - refpel(c, px + mx + x, py + my + y));
+    return sad + mv_cost(s, 2, mx, my, pmvx, pmvy);
+}
+
+/* the ordered EPZS predictor list of one search; returns its length (invalid entries flagged) */
+static int epzs_predictors(const mbs *s, int bt, int bx4, int by4, int range, int c0x, int c0y,
+                           int cand[41][2], int ok[41]) {
+    const jmo_ctx *c = s->c;
+    int n = 0, w4 = jmo_blc_size[bt][0] >> 2, h4 = jmo_blc_size[bt][1] >> 2;
+#define ADD(v, x, y) do { ok[n] = (v); cand[n][0] = (x); cand[n][1] = (y); n++; } while (0)
+    ADD(1, c0x, c0y);                                       /* 0: the search centre (median)   */
+    ADD(1, 0, 0);                                           /* 1: zero vector                  */
+    int av[3], ix[3];                                       /* 2-4: spatial A, B, C (or D)     */
+    mvp_neighbours(s, bx4, by4, 4 * w4, 4 * h4, &av[0], &av[1], &av[2], &ix[0], &ix[1], &ix[2]);
+    for (int k = 0; k < 3; k++) {
+        int v = av[k] && c->refidx[ix[k]] == 0;
+        ADD(v, v ? rnd_fp(c->mv[2 * ix[k]]) : 0, v ? rnd_fp(c->mv[2 * ix[k] + 1]) : 0);
+    }
+    for (int ring = 0; ring < 3; ring++) {                  /* 5-28: window rings R/4, R/2, R  */
+        int r = range >> (2 - ring);
+        for (int k = 0; k < 8; k++) ADD(r > 0, c0x + r * epzs_win[k][0], c0y + r * epzs_win[k][1]);
+    }
+    int W4 = c->W >> 2, H4 = c->H >> 2, X = (s->pix_x >> 2) + bx4, Y = (s->pix_y >> 2) + by4;
+    const int tx[5] = {X, X - 1, X + w4, X, X}, ty[5] = {Y, Y, Y, Y - 1, Y + h4};
+    for (int k = 0; k < 5; k++) {                           /* 29-33: temporal (co-located +4) */
+        int in = tx[k] >= 0 && tx[k] < W4 && ty[k] >= 0 && ty[k] < H4;
+        int i = in ? ty[k] * W4 + tx[k] : 0, v = in && c->tref[i] == 0;
+        ADD(v, v ? rnd_fp(c->tmv[2 * i]) : 0, v ? rnd_fp(c->tmv[2 * i + 1]) : 0);
+    }
+    int k0 = by4 * 4 + bx4;                                 /* 34: spatial memory (left MB)    */
+    int vm = s->mbx > 0 && c->cfg.inter_search[bt];
+    ADD(vm, vm ? rnd_fp(c->mem_mv[bt][k0][0]) : 0, vm ? rnd_fp(c->mem_mv[bt][k0][1]) : 0);
+    static const int types[6] = {1, 2, 3, 4, 5, 6};         /* 35-40: earlier block types      */
+    for (int k = 0; k < 6; k++) {
+        int t = types[k], v = t < bt && c->cfg.inter_search[t];
+        ADD(v, v ? rnd_fp(s->all_mv[t][k0][0]) : 0, v ? rnd_fp(s->all_mv[t][k0][1]) : 0);
+    }
+#undef ADD
+    return n;
+}
+
+static int epzs_search(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, int range, int *mvx, int *mvy) {
+    int c0x = *mvx, c0y = *mvy;
+    int med = jmo_blc_size[bt][0] * jmo_blc_size[bt][1];  /* medthres: EPZSMedThresScale 1 */
+    int cand[41][2], ok[41];
+    int n = epzs_predictors(s, bt, bx4, by4, range, c0x, c0y, cand, ok);
+    int min_mcost = epzs_cost(s, bt, bx4, by4, c0x, c0y, pmvx, pmvy), bx = c0x, by = c0y;
+    if (min_mcost >= med) {
+        for (int i = 1; i < n; i++) {                       /* predictors in order, strict '<' */
+            if (!ok[i] || iabs(cand[i][0] - c0x) > range || iabs(cand[i][1] - c0y) > range) continue;
+            int mc = epzs_cost(s, bt, bx4, by4, cand[i][0], cand[i][1], pmvx, pmvy);
+            if (mc < min_mcost) { min_mcost = mc; bx = cand[i][0]; by = cand[i][1]; }
+        }
+        if (min_mcost >= med) {                             /* pattern refinement          */
+            int sd = min_mcost < med + ((3 * med) >> 1);
+            const int (*pat)[2] = sd ? epzs_sd : epzs_ed;
+            int np = sd ? 4 : 12;
+            for (;;) {
+                int bi = -1, nbx = bx, nby = by;
+                for (int i = 0; i < np; i++) {
+                    int mx = bx + pat[i][0], my = by + pat[i][1];
+                    if (iabs(mx - c0x) > range || iabs(my - c0y) > range) continue;
+                    int mc = epzs_cost(s, bt, bx4, by4, mx, my, pmvx, pmvy);
+                    if (mc < min_mcost) { min_mcost = mc; bi = i; nbx = mx; nby = my; }
+                }
+                if (bi < 0) break;
+                bx = nbx; by = nby;
+            }
+        }
+    }
+    *mvx = bx; *mvy = by;
+    return min_mcost;
+}
+
 /* SATD of a block at a quarter-pel candidate (sum over its 4x4 sub-blocks) */
 static int subpel_satd(const mbs *s, int bx4, int by4, int w4, int h4, int cmx, int cmy) {
     const jmo_ctx *c = s->c;
@@ -302,6 +402,7 @@ static int block_motion_search(mbs *s, int blocktype, int bx4, int by4, int rang
     int mvx = iclip(-range, range, pmv[0] / 4), mvy = iclip(-range, range, pmv[1] / 4);
     int min_mcost;
     if (c->cfg.search_mode == 0) min_mcost = ffs_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
+    else if (c->cfg.search_mode == 3) min_mcost = epzs_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
     else min_mcost = full_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
     if (c->cfg.use_hadamard) min_mcost = BIGCOST;
     min_mcost = subpel_search(s, blocktype, bx4, by4, pmv[0], pmv[1], &mvx, &mvy, min_mcost);
@@ -1006,6 +1107,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
             if (cost8x8 < min_cost) { best_mode = JMH_P8x8; min_cost = cost8x8; }
         }
         find_skip_mv(s);
+        memcpy(c->mem_mv, s->all_mv, sizeof(c->mem_mv));   /* EPZS spatial memory of the next MB */
     }
 
     /* ===== Intra 8x8 decision (Transform8x8Mode; before Intra4x4, "<=") ===== */

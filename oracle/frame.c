@@ -12,7 +12,7 @@ static int cfg_ok(const jmh_config *cfg) {
     if (!cfg || cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 15) || (cfg->height & 15))
         return JMH_E_INVALID_ARG;
     if (cfg->search_range < 1 || cfg->search_range > JMO_MAX_SR) return JMH_E_INVALID_ARG;
-    if (cfg->search_mode != 0 && cfg->search_mode != -1) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->search_mode != 0 && cfg->search_mode != -1 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred != 0) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
     if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
@@ -40,10 +40,13 @@ int jmo_create(const jmh_config *cfg, jmo_ctx **out) {
     c->mv = calloc(2 * n4, sizeof(int16_t));
     c->refidx = calloc(n4, 1);
     c->ipred = calloc(n4, 1);
+    c->tmv = calloc(2 * n4, sizeof(int16_t));
+    c->tref = malloc(n4);
     c->mbintra = calloc((size_t)c->mbw * c->mbh, 1);
     c->res = calloc((size_t)c->mbw * c->mbh, sizeof(jmh_mb_result));
     c->blocksad = malloc(sizeof(uint16_t) * 16 * (size_t)c->npos);
-    if (!c->orgY || !c->qpel || !c->res || !c->blocksad) { jmo_destroy(c); return JMH_E_OOM; }
+    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref) { jmo_destroy(c); return JMH_E_OOM; }
+    memset(c->refidx, -1, n4);                             /* no previous picture: no motion */
     *out = c;
     return JMH_OK;
 }
@@ -55,7 +58,7 @@ void jmo_destroy(jmo_ctx *c) {
     free(c->refY); free(c->refU); free(c->refV);
     free(c->recY); free(c->recU); free(c->recV);
     free(c->qpel); free(c->mv); free(c->refidx); free(c->ipred); free(c->mbintra);
-    free(c->res); free(c->blocksad);
+    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref);
     free(c);
 }
 
@@ -94,6 +97,8 @@ int jmo_encode_frame(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8
     copy_plane(c->orgU, c->Wc, c->Hc, u, stride_c);
     copy_plane(c->orgV, c->Wc, c->Hc, v, stride_c);
     size_t n4 = (size_t)c->W * c->H / 16;
+    memcpy(c->tmv, c->mv, 2 * n4 * sizeof(int16_t));     /* EPZS temporal predictors: the last */
+    memcpy(c->tref, c->refidx, n4);                       /* encoded picture's motion field     */
     memset(c->mv, 0, 2 * n4 * sizeof(int16_t));
     memset(c->refidx, -1, n4);
     memset(c->ipred, 2, n4);

@@ -57,6 +57,11 @@ struct jmo_ctx {
     jmh_frame_params fp;
     /* per-MB scratch */
     uint16_t *blocksad;              /* [16][npos] 4x4 SADs (window raster order)               */
+    /* EPZS (SearchMode 3): the previous picture's motion field (temporal predictors) and the
+       left macroblock's per-blocktype search results (spatial memory predictors) */
+    int16_t *tmv;                    /* [(H/4)*(W/4)][2], snapshot of mv at picture start        */
+    int8_t *tref;                    /* [(H/4)*(W/4)], -1: intra / no previous picture          */
+    int16_t mem_mv[8][16][2];        /* all_mv of the MB to the left (valid when mbx > 0)       */
 };
 
 /* common.c */

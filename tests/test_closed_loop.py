@@ -34,6 +34,10 @@ CONFIGS = [
     ["InputFile=synthetic:24", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=1", "SourceWidth=200",
      "SourceHeight=120", "InterSearch8x4=0", "InterSearch4x8=0", "InterSearch4x4=0", "IntraPeriod=2",
      "QPFirstFrame=30", "QPRemainingFrame=33"],
+    # EPZS (SearchMode 3), Baseline and config-3 shape (High + 8x8)
+    ["InputFile=synthetic:26", "FramesToBeEncoded=5", "SearchMode=3", "SearchRange=32"],
+    ["InputFile=synthetic:27", "FramesToBeEncoded=4", "SearchMode=3", "SearchRange=16", "ProfileIDC=100",
+     "Transform8x8Mode=1", "SourceWidth=352", "SourceHeight=288", "QPRemainingFrame=31"],
     ["InputFile=synthetic:25", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=0", "SearchRange=8",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=-2", "LoopFilterBetaOffset=3", "ChromaQPOffset=3"],
 ]

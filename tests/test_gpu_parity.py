@@ -164,6 +164,11 @@ def test_ippp_qcif_sr16():
     (dict(search_range=8, search_mode=-1), 28),                              # FullPelBlockMotionSearch
     (dict(search_range=16, search_mode=-1, restrict_search_range=0), 30),
     (dict(search_range=8, search_mode=-1, use_hadamard=0, inter_search=(1, 1, 0, 1, 1, 0, 1)), 36),
+    # EPZS (SearchMode 3, a15): predictors, thresholds, diamond refinement, temporal predictors
+    (dict(search_range=16, search_mode=3), 28),
+    (dict(search_range=32, search_mode=3, restrict_search_range=0), 20),
+    (dict(search_range=8, search_mode=3, use_hadamard=0, inter_search=(1, 0, 1, 1, 0, 1, 1)), 36),
+    (dict(search_range=4, search_mode=3, inter_search=(0, 1, 1, 1, 1, 1, 1)), 44),
 ])
 def test_ipp_configs(kw, qp):
     pics = synth_seq(96, 64, 3, 7)
@@ -191,6 +196,15 @@ def test_high_profile_qcif_ippp():
     for qp in (20, 30, 38):
         encode_pair(176, 144, pics, [jmhip.JMH_I_SLICE] + [jmhip.JMH_P_SLICE] * 3, qp, search_range=16,
                     transform_8x8_mode=1)
+
+
+@pytest.mark.parametrize("qp", [16, 30])
+def test_epzs_moving_sequence(qp):
+    """a15: EPZS on large motion (window rings, temporal predictors from the previous picture's
+    motion field, spatial memory), High profile on top; GPU == oracle bit for bit."""
+    pics = moving_seq(176, 144, 5, seed=9, step=(13, -7))
+    encode_pair(176, 144, pics, [jmhip.JMH_I_SLICE] + [jmhip.JMH_P_SLICE] * 4, qp, search_range=32, search_mode=3,
+                transform_8x8_mode=1)
 
 
 def test_random_content_p_frames():
@@ -280,17 +294,19 @@ def run_chain(enc, pics, qp, dbk, pipelined):
     return out
 
 
-@pytest.mark.parametrize("w,h,sr,n,step", [(176, 144, 16, 9, (37, -29)), (320, 240, 32, 8, (37, -29)),
-                                           (1920, 1088, 32, 20, (37, -29)), (1920, 1088, 32, 12, (-62, -61)),
-                                           (640, 480, 32, 10, (63, 62))])
-def test_pipelined_chain_equals_sequential(w, h, sr, n, step):
+@pytest.mark.parametrize("w,h,sr,n,step,kw", [(176, 144, 16, 9, (37, -29), {}), (320, 240, 32, 8, (37, -29), {}),
+                                              (1920, 1088, 32, 20, (37, -29), {}), (1920, 1088, 32, 12, (-62, -61), {}),
+                                              (640, 480, 32, 10, (63, 62), {}),
+                                              (640, 480, 32, 10, (37, -29), dict(search_mode=3, transform_8x8_mode=1)),
+                                              (1920, 1088, 32, 20, (-62, -61), dict(search_mode=3, transform_8x8_mode=1))])
+def test_pipelined_chain_equals_sequential(w, h, sr, n, step, kw):
     """Pictures in flight together (lag PIPE_LAG diagonals) == one picture at a time, bit for
     bit, under motion that pushes MVs to the search-window edge (|MV| up to 63 px at SR 32: the
     reference is read up to 67 px beyond the MB, the reach PIPE_LAG is derived from)."""
     pics = moving_seq(w, h, n, seed=w + n, step=step)
     dbk = (0, 0, 0)
-    a = jmhip.Encoder(w, h, search_range=sr)                       # auto depth
-    b = jmhip.Encoder(w, h, search_range=sr, pipeline_depth=1)
+    a = jmhip.Encoder(w, h, search_range=sr, **kw)                 # auto depth
+    b = jmhip.Encoder(w, h, search_range=sr, pipeline_depth=1, **kw)
     assert a.depth > 1 and b.depth == 1
     ra = run_chain(a, pics, 30, dbk, True)
     rb = run_chain(b, pics, 30, dbk, False)
@@ -352,6 +368,11 @@ def run_lencod(binary, out_dir, extra):
     ["InputFile=synthetic:5", "FramesToBeEncoded=4", "SourceWidth=320", "SourceHeight=240", "SearchRange=16",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=6", "LoopFilterBetaOffset=6", "QPFirstFrame=40",
      "QPRemainingFrame=44"],
+    # config 3 shape at CIF: High profile, 8x8 transform (a12) + EPZS (a15), pipelined
+    ["InputFile=synthetic:23", "FramesToBeEncoded=8", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3"],
+    ["InputFile=synthetic:24", "FramesToBeEncoded=5", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "SearchMode=3", "RestrictSearchRange=0", "QPRemainingFrame=34"],
     # High profile, 8x8 transform (a12): pipelined, device deblocking without 4x4 luma edges
     ["InputFile=synthetic:21", "FramesToBeEncoded=8", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
      "ProfileIDC=100", "Transform8x8Mode=1"],
