@@ -12,6 +12,9 @@ ME/transform time.  Multi-GPU: one independent stream per rank (se
 collective in the data path; a gloo barrier brackets the timed region and the maximum time over
 ranks is used (h264-jm-commentary_amd/streams.py).
 
+--config 3 runs BASELINE.json's config 3 instead (a variant line, not the headline metric):
+2160p synthetic, High profile, EPZS (SearchMode 3) + adaptive 8x8 transform (Transform8x8Mode 1).
+
 Prints ONE JSON line (rank 0).
 """
 import argparse
@@ -26,6 +29,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "h264-jm-commentary_amd")
 
 METRIC = "ME+transform megapixels/sec @1080p FullSearch SR=32; bit-exact bitstream vs JM"
+# BASELINE.json configs measured here: 2 (the headline) and 3 (variant)
+CONFIGS = {
+    2: dict(metric=METRIC, disp=(1920, 1080), coded=(1920, 1088), search_mode=0, t8=0,
+            workload="1080p synthetic YUV420 (coded 1920x1088), Baseline, {sm} SearchRange=32, RestrictSearchRange=2, "
+                     "UseHadamard=1, 7 inter block sizes, RDO off, QP 28, P pictures (one independent stream per GPU)"),
+    3: dict(metric="ME+transform megapixels/sec @2160p High EPZS SR=32 + 8x8 transform (config 3)", disp=(3840, 2160),
+            coded=(3840, 2160), search_mode=3, t8=1,
+            workload="2160p synthetic YUV420, High profile (ProfileIDC 100), EPZS SearchMode=3 SearchRange=32, "
+                     "Transform8x8Mode=1 (Intra8x8 + TransformDecision), UseHadamard=1, 7 inter block sizes, RDO off, "
+                     "QP 28, P pictures (one independent stream per GPU)"),
+}
 DISP_W, DISP_H = 1920, 1080
 W, H = 1920, 1088
 SR, QP = 32, 28
@@ -51,15 +65,26 @@ def load_module(name, path):
     return mod
 
 
-def cpu_one_picture(seed, search_mode):
-    """Seconds the oracle (JM restated in C, scalar -O2, one thread) takes for one 1080p P picture
-    of stream `seed` (UnifiedOneForthPix + encode_one_macroblock x 8160).  Runs in a child
+def use_config(k):
+    """switch the module-level workload constants to BASELINE.json config k"""
+    global DISP_W, DISP_H, W, H, NMB, BYTES_PER_FRAME, AD_PER_FRAME
+    c = CONFIGS[k]
+    (DISP_W, DISP_H), (W, H) = c["disp"], c["coded"]
+    NMB = (W // 16) * (H // 16)
+    BYTES_PER_FRAME = W * H * BYTES_PER_PIXEL + NMB * SIDE_BYTES_PER_MB
+    AD_PER_FRAME = NMB * (2 * SR + 1) ** 2 * 256
+    return c
+
+
+def cpu_one_picture(seed, search_mode, t8=0):
+    """Seconds the oracle (JM restated in C, scalar -O2, one thread) takes for one P picture of the
+    configured size on stream `seed` (UnifiedOneForthPix + encode_one_macroblock per MB).  Runs in a child
     process (bench.py --cpu-worker): no GPU is touched."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
     frames = [jm.synth_frame(DISP_W, DISP_H, seed, i) for i in range(2)]
-    o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode)
+    o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8)
     _, rec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
     t0 = time.perf_counter()
     o.set_reference(*rec)
@@ -69,9 +94,9 @@ def cpu_one_picture(seed, search_mode):
     return dt
 
 
-def cpu_workers(n, search_mode):
+def cpu_workers(n, config, search_mode):
     """n concurrent child processes (distinct seeds); their per-picture seconds."""
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(k), str(search_mode)],
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(k), str(config), str(search_mode)],
                               stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True) for k in range(n)]
     return [float(p.communicate()[0].split()[-1]) for p in procs]
 
@@ -87,16 +112,16 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(search_mode=0):
+def cpu_baseline(config=2, search_mode=0):
     """The CPU path timed on this node's host cores: one process on one core (JM is
     single threaded; the reported baseline), and n processes on distinct streams at once
     (aggregate, n = min(16, cores available to this process))."""
-    one = cpu_workers(1, search_mode)[0]
+    one = cpu_workers(1, config, search_mode)[0]
     n = max(1, min(16, len(os.sched_getaffinity(0))))
-    many = cpu_workers(n, search_mode)
-    mode = "FFS" if search_mode == 0 else "full search"
+    many = cpu_workers(n, config, search_mode)
+    mode = {0: "FFS", -1: "full search", 3: "EPZS"}[search_mode] + (" + 8x8 transform" if CONFIGS[config]["t8"] else "")
     return {"value": round(DISP_W * DISP_H / 1e6 / one, 4), "unit": "MP/s", "cores": 1, "kind": "port",
-            "sample": f"one 1920x1080 P picture (coded 1920x1088, 8160 MBs, {mode} SR=32, QP {QP}) incl. "
+            "sample": f"one {DISP_W}x{DISP_H} P picture (coded {W}x{H}, {NMB} MBs, {mode} SR=32, QP {QP}) incl. "
                       f"quarter-pel interpolation, oracle/liboracle.so -O2 scalar, {one:.1f} s, on {cpu_model()}",
             "all_cores": {"value": round(n * DISP_W * DISP_H / 1e6 / max(many), 4), "unit": "MP/s", "cores": n,
                           "sample": f"{n} processes, one P picture each on distinct streams, concurrently, "
@@ -115,17 +140,22 @@ def read_pmc_traffic():
 
 
 def main():
-    if len(sys.argv) == 4 and sys.argv[1] == "--cpu-worker":    # child of cpu_baseline()
-        print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[3])), flush=True)
+    if len(sys.argv) == 5 and sys.argv[1] == "--cpu-worker":    # child of cpu_baseline()
+        c = use_config(int(sys.argv[3]))
+        print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[4]), c["t8"]), flush=True)
         return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--search-mode", type=int, default=0, choices=(0, -1),
-                    help="0: FFS (the BASELINE workload); -1: FullPelBlockMotionSearch variant")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+                    help="BASELINE.json config: 2 = 1080p Baseline FFS (the headline), 3 = 2160p High EPZS + 8x8")
+    ap.add_argument("--search-mode", type=int, default=None, choices=(0, -1, 3),
+                    help="override the config's SearchMode (config 2 variants: -1 full search, 3 EPZS)")
     args = ap.parse_args()
+    cfg = use_config(args.config)
+    search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -139,7 +169,8 @@ def main():
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
     streams = load_module("jmh_streams", os.path.join(PKG, "streams.py"))
     frames = [jm.synth_frame(DISP_W, DISP_H, rank, i) for i in range(3)]
-    enc = jm.Encoder(W, H, device=local, search_range=SR, search_mode=args.search_mode, slots=3, kernel_timing=True)
+    enc = jm.Encoder(W, H, device=local, search_range=SR, search_mode=search_mode, slots=3, kernel_timing=True,
+                     transform_8x8_mode=cfg["t8"])
     stream = streams.PStream(enc, frames, QP)
     dt = streams.timed_run(stream, args.steps, args.warmup, dist, on_start=enc.timing)   # on_start resets the event sums
     tm = enc.timing()                                     # event sums of the timed steps only
@@ -157,9 +188,10 @@ def main():
     bytes_per_launch = BYTES_PER_FRAME / NMB * mbs_per_launch
     achieved_gbs = bytes_per_launch / (an_launch_ms * 1e-3) / 1e9
     mb_ms_pic = tm.mb_ms / pictures
-    pmc = read_pmc_traffic()
+    pmc = read_pmc_traffic() if args.config == 2 and search_mode == 0 else None   # PMC pass is for config 2
+    sm_name = {0: "FFS SearchMode=0", -1: "full search SearchMode=-1", 3: "EPZS SearchMode=3"}[search_mode]
     out = {
-        "metric": METRIC,
+        "metric": cfg["metric"],
         "value": round(value, 3),
         "unit": "MP/s",
         "n_gpus": world,
@@ -172,10 +204,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": "1080p synthetic YUV420 (coded 1920x1088), Baseline, "
-                        + ("FFS SearchMode=0" if args.search_mode == 0 else "full search SearchMode=-1")
-                        + " SearchRange=32, RestrictSearchRange=2, UseHadamard=1, 7 inter block sizes, "
-                        "RDO off, QP 28, P pictures (one independent stream per GPU)",
+            "workload": cfg["workload"].replace("{sm}", sm_name),
             "global_batch": world,
             "parallelism": f"streams{world}",
             "pipeline_depth": enc.depth,
@@ -187,13 +216,14 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
             "traffic": round(pmc * mbs_per_launch) if pmc else None,
-            "kernel": "k_mb_analyse",
+            "kernel": "k_mb_analyse" if search_mode == 0 else
+                      "k_mb_me_full + k_mb_analyse" + (" + k_mb_intra8" if cfg["t8"] else "") + " (the tick's analysis launches)",
             "algorithmic_bytes_per_launch": round(bytes_per_launch),
             "avg_launch_ms": round(an_launch_ms, 5),
             "launches_per_picture": round(an_per_pic, 2),
             "mbs_per_launch": round(mbs_per_launch, 1),
         },
-        "valu_roofline": {
+        "valu_roofline": None if search_mode != 0 else {
             "note": "integer-search absolute differences (v_sad_u8) over the wavefront time",
             "achieved": round(AD_PER_FRAME / (mb_ms_pic * 1e-3) / 1e12, 4),
             "peak": round(VALU_SAD_PEAK_TADS, 2),
@@ -208,7 +238,7 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.search_mode)
+        out["cpu_baseline"] = cpu_baseline(args.config, search_mode)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -33,7 +33,16 @@ struct FullS {
     int ccost[9];
     int16_t cand[NPRED][2];                    // EPZS predictors (full pel); invalid: INT16_MIN
     int cost0;
+    uint8_t hp[3][18][20];                     // half-pel b / h / j around the block at its full-pel MV
 };
+
+// half-grid sample (hx, hy) relative to the block origin at its full-pel MV (window (gx0, gy0)):
+// even / even = integer sample, odd x = b, odd y = h, both odd = j (8.4.2.2.1)
+__device__ __forceinline__ int hg_at(const FullS &s, int gx0, int gy0, int hx, int hy) {
+    if (!((hx | hy) & 1)) return s.g[(gy0 + (hy >> 1)) * FST + gx0 + (hx >> 1)];
+    const int pl = (hx & hy & 1) ? 2 : (hx & 1) ? 0 : 1;
+    return s.hp[pl][(hy >> 1) + 1][(hx >> 1) + 1];
+}
 
 // neighbour view of a search of block type bt in 8x8 block b8 (as NbMe in jmh_analyse.hip)
 struct NbFull {
@@ -183,8 +192,9 @@ __device__ void epzs_fullpel(const DevParams &d, FullS &s, int off, int bt, int 
 
 // BlockMotionSearch [J] for one block: full-pel full search + SubPelBlockMotionSearch
 __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int mc, int b8,
-                                                           int best8x8, int X0, int Y0, int left) {
+                                                           int best8x8, int X0, int Y0, int left, int pslot) {
     const int tid = threadIdx.x;
+    const bool prof = pslot >= 0 && pslot < 28 && d.prof && tid == 0 && d.prof_mb == (Y0 >> 2) * d.mbw + (X0 >> 2);
     const int lam = d.lambda_motion, had = d.use_hadamard;
     const bool slice_p = d.slice_type == JMH_P_SLICE;
     const int range = d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr;
@@ -196,6 +206,7 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
     if (d.search_mode == 3) {
         epzs_fullpel(d, s, off, bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, pmx, pmy, X0, Y0, left, fmx, fmy, min_mcost);
         if (had) min_mcost = BIGCOST;
+        if (prof) d.prof[34 + pslot] = wall_clock64();
     } else {
     // ---- full pel: every thread a stride of positions, SADs by dword v_sad_u8
     const int side = 2 * range + 1, npos = side * side;
@@ -222,25 +233,45 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
     fmx = mvx0 + rx; fmy = mvy0 + ry;
     min_mcost = had ? BIGCOST : (int)(best >> 13) - FKOFF;
     }
-    // ---- sub pel (half then quarter), samples from the window through the 6-tap
+    // ---- sub pel (half then quarter): half-pel b / h / j planes of the block's neighbourhood
+    // (x, y in [-1, w] x [-1, h] around its full-pel position) built once, then every quarter
+    // sample is the average of two half-grid samples; one 16-lane group per (candidate, 4x4)
     const bool check0 = bt == 1 && fmx == 0 && fmy == 0 && had && slice_p;
     auto px = [&](int x, int y) { return (int)s.g[y * FST + x]; };
+    const int gx0 = off + 4 * bx4 + fmx, gy0 = off + 4 * by4 + fmy;
+    {
+        const int PW = 4 * w4 + 2, PH = 4 * h4 + 2;
+        for (int i = tid; i < PW * PH; i += NTF) {
+            const int y = i / PW, x = i - y * PW, gx = gx0 + x - 1, gy = gy0 + y - 1;
+            s.hp[0][y][x] = (uint8_t)clip255((tap6(px(gx - 2, gy), px(gx - 1, gy), px(gx, gy), px(gx + 1, gy), px(gx + 2, gy), px(gx + 3, gy)) + 16) >> 5);
+            s.hp[1][y][x] = (uint8_t)clip255((tap6(px(gx, gy - 2), px(gx, gy - 1), px(gx, gy), px(gx, gy + 1), px(gx, gy + 2), px(gx, gy + 3)) + 16) >> 5);
+            int v[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const int xx = gx - 2 + k;
+                v[k] = tap6(px(xx, gy - 2), px(xx, gy - 1), px(xx, gy), px(xx, gy + 1), px(xx, gy + 2), px(xx, gy + 3));
+            }
+            s.hp[2][y][x] = (uint8_t)clip255((tap6(v[0], v[1], v[2], v[3], v[4], v[5]) + 512) >> 10);
+        }
+    }
+    const int grp = tid >> 4, l = tid & 15;
     int qx = 0, qy = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int step = pass == 0 ? 2 : 1, min_pos = pass == 0 ? (had ? 0 : 1) : 1;
         if (tid < 9) s.ccost[tid] = 0;
         __syncthreads();
-        for (int task = tid; task < (9 << lns); task += NTF) {
+        for (int task = grp; task < (9 << lns); task += NTF / 16) {   // group-uniform
             const int c = task >> lns, sub = task & (nsub - 1);
             if (c < min_pos) continue;
             const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
-            const int bxs = bx4 + (sub & (w4 - 1)), bys = by4 + (sub >> lw4);
-            int df[16];
-            for (int yy = 0; yy < 4; yy++)
-                for (int xx = 0; xx < 4; xx++)
-                    df[4 * yy + xx] = s.org[(4 * bys + yy) * 16 + 4 * bxs + xx] -
-                                      qpel_from(px, 4 * (off + 4 * bxs + xx + fmx) + ox, 4 * (off + 4 * bys + yy + fmy) + oy);
-            atomicAdd(&s.ccost[c], satd4x4(df, had));
+            const int pxl = 4 * (sub & (w4 - 1)) + (l & 3), pyl = 4 * (sub >> lw4) + (l >> 2);
+            const int Qx = 4 * pxl + ox, Qy = 4 * pyl + oy, xi = Qx >> 2, yi = Qy >> 2;
+            const int q = qoff(((Qy & 3) << 2) | (Qx & 3));
+            const int a = hg_at(s, gx0, gy0, 2 * xi + ((q >> 12) & 15), 2 * yi + ((q >> 8) & 15));
+            const int b = hg_at(s, gx0, gy0, 2 * xi + ((q >> 4) & 15), 2 * yi + (q & 15));
+            const int dv = s.org[(4 * by4 + pyl) * 16 + 4 * bx4 + pxl] - ((a + b + 1) >> 1);
+            const int sat = lane_satd(dv, l, had);
+            if (l == 0) atomicAdd(&s.ccost[c], sat);
         }
         __syncthreads();
         int bpos = 0;
@@ -261,6 +292,7 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
     }
     if (tid == 0) s.motion_cost[bt][mc] += min_mcost;
     __syncthreads();
+    if (prof) d.prof[35 + pslot] = wall_clock64();
 }
 
 __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
@@ -273,6 +305,7 @@ __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
     const int off = 2 * sr + 4, wdim = 16 + 2 * off;
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const int X0 = 4 * mbx, Y0 = 4 * mby, left = mbx > 0 ? mby * d.mbw + mbx - 1 : -1;   // EPZS
+    if (d.prof && tid == 0 && d.prof_mb == mby * d.mbw + mbx) d.prof[32] = wall_clock64();
     s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     if (tid < 10) load_border(d, s.bd, tid, mbx, mby);
     else if (tid >= 32 && tid < 64) s.motion_cost[(tid - 32) >> 2][tid & 3] = 0;
@@ -295,25 +328,26 @@ __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
         }
     }
     __syncthreads();
+    if (d.prof && tid == 0 && d.prof_mb == mby * d.mbw + mbx) d.prof[33] = wall_clock64();
     // PartitionMotionSearch [J] order: 16x16, 16x8 (2), 8x16 (2)
-    full_block_search(d, s, off, 1, 0, 0, 0, 0, 0, X0, Y0, left);
-    full_block_search(d, s, off, 2, 0, 0, 0, 0, 0, X0, Y0, left);
-    full_block_search(d, s, off, 2, 0, 2, 1, 0, 0, X0, Y0, left);
-    full_block_search(d, s, off, 3, 0, 0, 0, 0, 0, X0, Y0, left);
-    full_block_search(d, s, off, 3, 2, 0, 1, 0, 0, X0, Y0, left);
+    full_block_search(d, s, off, 1, 0, 0, 0, 0, 0, X0, Y0, left, 0);
+    full_block_search(d, s, off, 2, 0, 0, 0, 0, 0, X0, Y0, left, 2);
+    full_block_search(d, s, off, 2, 0, 2, 1, 0, 0, X0, Y0, left, 4);
+    full_block_search(d, s, off, 3, 0, 0, 0, 0, 0, X0, Y0, left, 6);
+    full_block_search(d, s, off, 3, 2, 0, 1, 0, 0, X0, Y0, left, 8);
     // P8x8: per 8x8 block the sub-modes 4..7, then its best sub-mode (read through best8x8)
     int best8x8 = 0, cost8x8 = 0;
     for (int b8 = 0; b8 < 4; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        full_block_search(d, s, off, 4, X, Y, b8, b8, best8x8, X0, Y0, left);
-        full_block_search(d, s, off, 5, X, Y, b8, b8, best8x8, X0, Y0, left);
-        full_block_search(d, s, off, 5, X, Y + 1, b8, b8, best8x8, X0, Y0, left);
-        full_block_search(d, s, off, 6, X, Y, b8, b8, best8x8, X0, Y0, left);
-        full_block_search(d, s, off, 6, X + 1, Y, b8, b8, best8x8, X0, Y0, left);
-        full_block_search(d, s, off, 7, X, Y, b8, b8, best8x8, X0, Y0, left);
-        full_block_search(d, s, off, 7, X + 1, Y, b8, b8, best8x8, X0, Y0, left);
-        full_block_search(d, s, off, 7, X, Y + 1, b8, b8, best8x8, X0, Y0, left);
-        full_block_search(d, s, off, 7, X + 1, Y + 1, b8, b8, best8x8, X0, Y0, left);
+        full_block_search(d, s, off, 4, X, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
+        full_block_search(d, s, off, 5, X, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
+        full_block_search(d, s, off, 5, X, Y + 1, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
+        full_block_search(d, s, off, 6, X, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
+        full_block_search(d, s, off, 6, X + 1, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
+        full_block_search(d, s, off, 7, X, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
+        full_block_search(d, s, off, 7, X + 1, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
+        full_block_search(d, s, off, 7, X, Y + 1, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
+        full_block_search(d, s, off, 7, X + 1, Y + 1, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
         int mc8 = BIGCOST, bm = 0;
         for (int mode = 4; mode <= 7; mode++) {
             if (!d.inter_search[mode]) continue;

@@ -15,8 +15,9 @@ spec = importlib.util.spec_from_file_location("jmhip", os.path.join(ROOT, "h264-
 jm = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(jm)
 
+sm, t8 = int(os.environ.get("SEARCH_MODE", "0")), int(os.environ.get("T8", "0"))
 frames = [jm.synth_frame(1920, 1080, 0, i) for i in range(2)]
-enc = jm.Encoder(1920, 1088, search_range=32, slots=2)
+enc = jm.Encoder(1920, 1088, search_range=32, slots=2, search_mode=sm, transform_8x8_mode=t8)
 for i, f in enumerate(frames):
     enc.load_frame(i, *f)
 enc.encode_slot(0, jm.JMH_I_SLICE, 28)
