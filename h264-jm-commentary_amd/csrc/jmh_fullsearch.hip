@@ -30,9 +30,12 @@ struct FullS {
     int16_t all_mv[8][16][2];
     int motion_cost[8][4];
     unsigned red[2][NTF / 64];
-    int ccost[9];
-    int16_t cand[NPRED][2];                    // EPZS predictors (full pel); invalid: INT16_MIN
+    int ccost[2][9];
     int cost0;
+    int16_t tmv[6][6][2];                      // EPZS temporal: previous picture's MVs around the MB
+    int8_t tref[6][6];                         //   (4x4 units, MB origin at [1][1]; -1: none)
+    int16_t mem[8][16][2];                     // EPZS spatial memory: the left MB's searches
+    int memok;
     uint8_t hp[3][18][20];                     // half-pel b / h / j around the block at its full-pel MV
 };
 
@@ -93,69 +96,76 @@ __device__ __forceinline__ unsigned wg_min(FullS &s, unsigned k, int &slot) {
     return m;
 }
 
+// EPZS predictor i of a search (oracle/encode.c epzs_predictors order): 0 centre, 1 zero, 2-4
+// spatial A / B / C, 5-28 window rings R/4, R/2, R, 29-33 temporal (co-located, left, right, up,
+// down), 34 spatial memory (left MB), 35-40 earlier block types.  Returns false if not valid or
+// outside the window around the centre.  Temporal and memory data come from LDS (prefetched).
+__device__ __forceinline__ bool epzs_cand(const DevParams &d, const FullS &s, int i, int bt, int bx4, int by4, int b8, int best8x8,
+                                          int range, int mvx0, int mvy0, int &x, int &y) {
+    const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt), k0 = by4 * 4 + bx4;
+    auto rnd = [](int v) { return (v + 2) >> 2; };
+    bool v = true;
+    x = 0; y = 0;
+    if (i == 0) { x = mvx0; y = mvy0; }
+    else if (i == 1) { }
+    else if (i <= 4) {
+        int ref = -1, ax = 0, ay = 0;
+        v = mvp_nbr(NbFull{s, bt, b8, best8x8}, bx4, by4, 4 * w4, i - 2, ref, ax, ay) && ref == 0;
+        x = rnd(ax); y = rnd(ay);
+    } else if (i <= 28) {
+        const int ring = (i - 5) >> 3, k = (i - 5) & 7, rr = range >> (2 - ring);
+        const int wx = k == 1 || k == 4 || k == 6 ? -1 : k == 2 || k == 5 || k == 7 ? 1 : 0;
+        const int wy = k == 0 || k == 4 || k == 5 ? -1 : k == 3 || k == 6 || k == 7 ? 1 : 0;
+        v = rr > 0; x = mvx0 + rr * wx; y = mvy0 + rr * wy;
+    } else if (i <= 33) {
+        const int k = i - 29;                                  // co-located, left, right, up, down
+        const int tx = 1 + bx4 + (k == 1 ? -1 : k == 2 ? w4 : 0), ty = 1 + by4 + (k == 3 ? -1 : k == 4 ? h4 : 0);
+        v = s.tref[ty][tx] == 0;
+        x = rnd(s.tmv[ty][tx][0]); y = rnd(s.tmv[ty][tx][1]);
+    } else if (i == 34) {
+        v = s.memok && d.inter_search[bt];                     // left MB's search (spatial memory)
+        x = rnd(s.mem[bt][k0][0]); y = rnd(s.mem[bt][k0][1]);
+    } else if (i < NPRED) {
+        const int t = i - 34;                                  // block types 1..6 below bt
+        v = t < bt && d.inter_search[t];
+        x = rnd(s.all_mv[t][k0][0]); y = rnd(s.all_mv[t][k0][1]);
+    } else v = false;
+    return v && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
+}
+
+// refinement pattern point e: small diamond (0,-1) (-1,0) (1,0) (0,1); extended diamond (0,-2)
+// (-1,-1) (1,-1) (-2,0) (2,0) (-1,1) (1,1) (0,2) then the small diamond
+__device__ __forceinline__ void epzs_pat(bool sd, int e, int &px, int &py) {
+    if (sd) { px = e == 1 ? -1 : e == 2 ? 1 : 0; py = e == 0 ? -1 : e == 3 ? 1 : 0; return; }
+    px = e < 8 ? (e == 1 || e == 5 ? -1 : e == 2 || e == 6 ? 1 : e == 3 ? -2 : e == 4 ? 2 : 0) : (e == 9 ? -1 : e == 10 ? 1 : 0);
+    py = e < 8 ? (e == 0 ? -2 : e <= 2 ? -1 : e <= 4 ? 0 : e <= 6 ? 1 : 2) : (e == 8 ? -1 : e == 11 ? 1 : 0);
+}
+
 // EPZSPelBlockMotionSearch [J] as restated in oracle/encode.c epzs_search (JM_SEMANTICS items
-// 33-40): the centre, then 40 ordered predictors (zero, spatial A/B/C, three window rings,
-// temporal co-located + 4, spatial memory, earlier block types), strict '<' in list order (the
-// key's low bits), thresholds medthres = block pixels, then small- or extended-diamond
-// refinement around the best until it stops moving.  16 lanes per candidate SAD.
+// 33-40): the centre, then 40 ordered predictors, strict '<' in list order (the key's low bits),
+// medthres = block pixels, then small- or extended-diamond refinement around the best until it
+// stops moving.  One 16-lane group per candidate SAD; one barrier per candidate round.
 __device__ void epzs_fullpel(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int b8, int best8x8, int range,
-                             int mvx0, int mvy0, int pmx, int pmy, int X0, int Y0, int left, int &fmx, int &fmy, int &fcost) {
+                             int mvx0, int mvy0, int pmx, int pmy, int &fmx, int &fmy, int &fcost) {
     const int tid = threadIdx.x, g = tid >> 4, r = tid & 15;
     const int lam = d.lambda_motion;
-    const int lw4 = lw4_of(bt), lh4 = lh4_of(bt), w4 = 1 << lw4, h4 = 1 << lh4;
+    const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt);
     const int med = 16 * w4 * h4;
-    const int k0 = by4 * 4 + bx4;
-    auto rnd = [](int v) { return (v + 2) >> 2; };
-    // ---- predictor list (thread i builds slot i)
-    if (tid < NPRED) {
-        const int i = tid;
-        int v = 1, x = 0, y = 0;
-        if (i == 0) { x = mvx0; y = mvy0; }
-        else if (i == 1) { x = 0; y = 0; }
-        else if (i <= 4) {
-            int ref = -1, ax = 0, ay = 0;
-            v = mvp_nbr(NbFull{s, bt, b8, best8x8}, bx4, by4, 4 * w4, i - 2, ref, ax, ay) && ref == 0;
-            x = rnd(ax); y = rnd(ay);
-        } else if (i <= 28) {
-            const int ring = (i - 5) >> 3, k = (i - 5) & 7, rr = range >> (2 - ring);
-            const int wx = k == 1 || k == 4 || k == 6 ? -1 : k == 2 || k == 5 || k == 7 ? 1 : 0;
-            const int wy = k == 0 || k == 4 || k == 5 ? -1 : k == 3 || k == 6 || k == 7 ? 1 : 0;
-            v = rr > 0; x = mvx0 + rr * wx; y = mvy0 + rr * wy;
-        } else if (i <= 33) {
-            const int W4 = d.W >> 2, H4 = d.H >> 2, k = i - 29;   // co-located, left, right, up, down
-            const int px = X0 + bx4 + (k == 1 ? -1 : k == 2 ? w4 : 0);
-            const int py = Y0 + by4 + (k == 3 ? -1 : k == 4 ? h4 : 0);
-            v = d.tref && px >= 0 && px < W4 && py >= 0 && py < H4;
-            const int a = v ? py * W4 + px : 0;
-            v = v && d.tref[a] == 0;
-            if (v) { x = rnd(d.tmv[2 * a]); y = rnd(d.tmv[2 * a + 1]); }
-        } else if (i == 34) {
-            v = left >= 0 && d.inter_search[bt];               // left MB's search (spatial memory)
-            if (v) { x = rnd(d.scr[left].all_mv[bt][k0][0]); y = rnd(d.scr[left].all_mv[bt][k0][1]); }
-        } else {
-            const int t = i - 34;                              // block types 1..6 below bt
-            v = t < bt && d.inter_search[t];
-            if (v) { x = rnd(s.all_mv[t][k0][0]); y = rnd(s.all_mv[t][k0][1]); }
-        }
-        if (v && (abs(x - mvx0) > range || abs(y - mvy0) > range)) v = 0;   // outside the window
-        s.cand[i][0] = (int16_t)(v ? x : -32768);
-        s.cand[i][1] = (int16_t)y;
-    }
-    __syncthreads();
     int slot = 0;
     unsigned kb = 0xFFFFFFFFu;
     for (int i = g; i < NPRED; i += 16) {
-        const bool v = s.cand[i][0] != -32768;
-        const int x = v ? s.cand[i][0] : mvx0, y = v ? s.cand[i][1] : mvy0;
+        int x, y;
+        const bool v = epzs_cand(d, s, i, bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, x, y);
+        if (!v) { x = mvx0; y = mvy0; }
         const int c = group_sad(s, off, bx4, by4, w4, h4, x, y, r) + lam * (mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
         if (i == 0 && r == 0) s.cost0 = c;
         if (v) kb = min(kb, ((unsigned)c << 6) | (unsigned)i);
     }
-    unsigned best = wg_min(s, kb, slot);
+    const unsigned best = wg_min(s, kb, slot);
     int bx = mvx0, by = mvy0, min_mcost = s.cost0;
     if (min_mcost >= med) {                                   // else: stop at the centre
         min_mcost = (int)(best >> 6);
-        bx = s.cand[best & 63][0]; by = s.cand[best & 63][1];
+        epzs_cand(d, s, (int)(best & 63), bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, bx, by);
         if (min_mcost >= med) {                               // pattern refinement
             const bool sd = min_mcost < med + ((3 * med) >> 1);
             const int np = sd ? 4 : 12;
@@ -163,13 +173,7 @@ __device__ void epzs_fullpel(const DevParams &d, FullS &s, int off, int bt, int 
                 unsigned k = 0xFFFFFFFFu;
                 if (g < np) {
                     int px, py;
-                    if (sd) { px = g == 1 ? -1 : g == 2 ? 1 : 0; py = g == 0 ? -1 : g == 3 ? 1 : 0; }
-                    else {
-                        const int e = g;   // (0,-2) (-1,-1) (1,-1) (-2,0) (2,0) (-1,1) (1,1) (0,2) then the small diamond
-                        px = e < 8 ? (e == 1 || e == 5 ? -1 : e == 2 || e == 6 ? 1 : e == 3 ? -2 : e == 4 ? 2 : 0)
-                                   : (e == 9 ? -1 : e == 10 ? 1 : 0);
-                        py = e < 8 ? (e == 0 ? -2 : e <= 2 ? -1 : e <= 4 ? 0 : e <= 6 ? 1 : 2) : (e == 8 ? -1 : e == 11 ? 1 : 0);
-                    }
+                    epzs_pat(sd, g, px, py);
                     const int x = bx + px, y = by + py;
                     const bool v = abs(x - mvx0) <= range && abs(y - mvy0) <= range;
                     const int c = group_sad(s, off, bx4, by4, w4, h4, v ? x : bx, v ? y : by, r) + lam * (mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
@@ -178,12 +182,9 @@ __device__ void epzs_fullpel(const DevParams &d, FullS &s, int off, int bt, int 
                 const unsigned m = wg_min(s, k, slot);
                 if (m == 0xFFFFFFFFu || (int)(m >> 6) >= min_mcost) break;
                 min_mcost = (int)(m >> 6);
-                const int e = (int)(m & 63);
-                if (sd) { bx += e == 1 ? -1 : e == 2 ? 1 : 0; by += e == 0 ? -1 : e == 3 ? 1 : 0; }
-                else {
-                    bx += e < 8 ? (e == 1 || e == 5 ? -1 : e == 2 || e == 6 ? 1 : e == 3 ? -2 : e == 4 ? 2 : 0) : (e == 9 ? -1 : e == 10 ? 1 : 0);
-                    by += e < 8 ? (e == 0 ? -2 : e <= 2 ? -1 : e <= 4 ? 0 : e <= 6 ? 1 : 2) : (e == 8 ? -1 : e == 11 ? 1 : 0);
-                }
+                int px, py;
+                epzs_pat(sd, (int)(m & 63), px, py);
+                bx += px; by += py;
             }
         }
     }
@@ -204,7 +205,7 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
     const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
     int fmx, fmy, min_mcost;
     if (d.search_mode == 3) {
-        epzs_fullpel(d, s, off, bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, pmx, pmy, X0, Y0, left, fmx, fmy, min_mcost);
+        epzs_fullpel(d, s, off, bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, pmx, pmy, fmx, fmy, min_mcost);
         if (had) min_mcost = BIGCOST;
         if (prof) d.prof[34 + pslot] = wall_clock64();
     } else {
@@ -255,11 +256,11 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
         }
     }
     const int grp = tid >> 4, l = tid & 15;
+    if (tid < 18) s.ccost[tid / 9][tid % 9] = 0;
+    __syncthreads();
     int qx = 0, qy = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int step = pass == 0 ? 2 : 1, min_pos = pass == 0 ? (had ? 0 : 1) : 1;
-        if (tid < 9) s.ccost[tid] = 0;
-        __syncthreads();
         for (int task = grp; task < (9 << lns); task += NTF / 16) {   // group-uniform
             const int c = task >> lns, sub = task & (nsub - 1);
             if (c < min_pos) continue;
@@ -271,19 +272,18 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
             const int b = hg_at(s, gx0, gy0, 2 * xi + ((q >> 4) & 15), 2 * yi + (q & 15));
             const int dv = s.org[(4 * by4 + pyl) * 16 + 4 * bx4 + pxl] - ((a + b + 1) >> 1);
             const int sat = lane_satd(dv, l, had);
-            if (l == 0) atomicAdd(&s.ccost[c], sat);
+            if (l == 0) atomicAdd(&s.ccost[pass][c], sat);
         }
         __syncthreads();
         int bpos = 0;
         for (int c = min_pos; c < 9; c++) {   // JM order, strict '<'
             const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
-            int v = s.ccost[c] + lam * (mvbits(4 * fmx + ox - pmx) + mvbits(4 * fmy + oy - pmy));
+            int v = s.ccost[pass][c] + lam * (mvbits(4 * fmx + ox - pmx) + mvbits(4 * fmy + oy - pmy));
             if (pass == 0 && check0 && c == 0) v -= 16 * lam;
             if (v < min_mcost) { min_mcost = v; bpos = c; }
         }
         qx += step * sp9x(bpos);
         qy += step * sp9y(bpos);
-        __syncthreads();
     }
     if (tid < nsub) {
         const int k = (by4 + (tid >> lw4)) * 4 + bx4 + (tid & (w4 - 1));
@@ -309,6 +309,22 @@ __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
     s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     if (tid < 10) load_border(d, s.bd, tid, mbx, mby);
     else if (tid >= 32 && tid < 64) s.motion_cost[(tid - 32) >> 2][tid & 3] = 0;
+    if (d.search_mode == 3) {   // EPZS: temporal neighbourhood and the left MB's searches into LDS
+        if (tid >= 128 && tid < 164) {
+            const int i = tid - 128, ty = i / 6, tx = i - 6 * ty, px = X0 - 1 + tx, py = Y0 - 1 + ty;
+            int ref = -1, mx = 0, my = 0;
+            if (d.tref && px >= 0 && px < (W >> 2) && py >= 0 && py < (d.H >> 2)) {
+                const int a = py * (W >> 2) + px;
+                ref = d.tref[a]; mx = d.tmv[2 * a]; my = d.tmv[2 * a + 1];
+            }
+            s.tref[ty][tx] = (int8_t)ref; s.tmv[ty][tx][0] = (int16_t)mx; s.tmv[ty][tx][1] = (int16_t)my;
+        }
+        for (int i = tid; i < 7 * 32; i += NTF) {
+            const int m = 1 + i / 32, k = (i & 31) >> 1, c = i & 1;
+            s.mem[m][k][c] = left >= 0 ? d.scr[left].all_mv[m][k][c] : 0;
+        }
+        if (tid == 0) s.memok = left >= 0;
+    }
     {   // window: MB pixel (0,0) at (off, off); per-coordinate clamping is the spec's UMV access
         constexpr int ND4 = FST / 4;
         const int X0 = pix_x - off, Y0 = pix_y - off;
