@@ -960,16 +960,18 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     // dispatched first), then intra workgroups over every MB, four MBs (128 threads each) per
     // workgroup: Intra16x16 + chroma decisions, and Intra4x4 for MBs without a motion-search
     // workgroup (I pictures; SearchMode -1, where k_mb_me_full searched)
-    const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0, tot = t.pre[t.npic], b = blockIdx.x;
+    const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0, nPg = xcd_grid(nPm), tot = t.pre[t.npic], b = blockIdx.x;
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
-    const int role = b < nPm ? 2 : 0;
+    const int role = b < nPg ? 2 : 0;
     if (role == 2) {
-        const int e = tick_entry(t, b);
+        const int m = xcd_block(b, nPm);                      // XCD-aware: neighbouring MBs share an L2
+        if (m >= nPm) return;                                 // padding block (whole workgroup)
+        const int e = tick_entry(t, m);
         const DevParams d = tick_params(t, e);
-        const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
+        const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
         me_mb(d, s.me, mbx, mby);
     } else {
-        const int q = __builtin_amdgcn_readfirstlane(4 * (b - nPm) + (int)(threadIdx.x >> 7));
+        const int q = __builtin_amdgcn_readfirstlane(4 * (b - nPg) + (int)(threadIdx.x >> 7));
         const bool act = q < tot;
         const int e = tick_entry(t, act ? q : 0);
         const DevParams d = tick_params(t, e);
@@ -987,7 +989,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
-    const int nblocks = (t.me_in_analyse ? t.pre[t.nP] : 0) + (t.pre[t.npic] + 3) / 4;
+    const int nblocks = xcd_grid(t.me_in_analyse ? t.pre[t.nP] : 0) + (t.pre[t.npic] + 3) / 4;
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }

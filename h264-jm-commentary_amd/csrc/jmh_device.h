@@ -92,6 +92,15 @@ struct TickArgs {
     PicParams p[PMAX];
 };
 
+// XCD-aware block order.  Workgroups are dispatched round-robin over the 8 XCDs (hardware block b
+// runs on XCD b % 8), each with its own L2.  A launch of n logical blocks uses 8 * ceil(n / 8)
+// hardware blocks and gives every XCD one contiguous run of the logical list, whose consecutive
+// entries are neighbouring MBs of one picture's diagonal (search windows and MC reads overlap), so
+// they share that XCD's L2.  Returns the logical block (>= n: idle).
+#define NXCD 8
+__device__ __forceinline__ int xcd_block(int b, int n) { return (b % NXCD) * ((n + NXCD - 1) / NXCD) + b / NXCD; }
+__host__ __device__ __forceinline__ int xcd_grid(int n) { return NXCD * ((n + NXCD - 1) / NXCD); }
+
 // entry of MB index idx (pre[e] <= idx < pre[e + 1]); uniform scalar loop
 __device__ __forceinline__ int tick_entry(const TickArgs &t, int idx) {
     int e = 0;

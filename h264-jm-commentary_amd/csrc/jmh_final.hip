@@ -98,9 +98,11 @@ __device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int al
 __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
     __shared__ FinS s;
     const int tid = threadIdx.x;
-    const int e = tick_entry(t, blockIdx.x);
+    const int m = xcd_block(blockIdx.x, t.pre[t.npic]);       // XCD-aware (jmh_device.h)
+    if (m >= t.pre[t.npic]) return;                           // padding block (whole workgroup)
+    const int e = tick_entry(t, m);
     const DevParams d = tick_params(t, e);
-    const int mby = d.y_min + (blockIdx.x - t.pre[e]), mbx = d.diag - 2 * mby;
+    const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
     const int W = d.W, Wc = d.Wc, W4 = d.W >> 2;
     const int slice_p = d.slice_type == JMH_P_SLICE;
@@ -500,6 +502,6 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
 }
 
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st) {
-    hipLaunchKernelGGL(k_mb_final, dim3(t.pre[t.npic]), dim3(NT), 0, st, t);
+    hipLaunchKernelGGL(k_mb_final, dim3(xcd_grid(t.pre[t.npic])), dim3(NT), 0, st, t);
     return hipGetLastError();
 }

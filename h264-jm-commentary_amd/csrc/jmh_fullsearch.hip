@@ -297,7 +297,8 @@ __device__ __attribute__((noinline)) void full_block_search(const DevParams &d, 
 
 __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
     __shared__ FullS s;
-    const int b = blockIdx.x, tid = threadIdx.x;
+    const int b = xcd_block(blockIdx.x, t.pre[t.nP]), tid = threadIdx.x;   // XCD-aware (jmh_device.h)
+    if (b >= t.pre[t.nP]) return;
     const int e = tick_entry(t, b);
     const DevParams d = tick_params(t, e);
     const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
@@ -394,6 +395,6 @@ __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
 
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st) {
     if (t.pre[t.nP] == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mb_me_full, dim3(t.pre[t.nP]), dim3(NTF), 0, st, t);
+    hipLaunchKernelGGL(k_mb_me_full, dim3(xcd_grid(t.pre[t.nP])), dim3(NTF), 0, st, t);
     return hipGetLastError();
 }

@@ -23,9 +23,11 @@ struct I8S {
 __global__ __launch_bounds__(NT) void k_mb_intra8(const TickArgs t) {
     __shared__ I8S s;
     const int tid = threadIdx.x;
-    const int e = tick_entry(t, blockIdx.x);
+    const int mi = xcd_block(blockIdx.x, t.pre[t.npic]);      // XCD-aware (jmh_device.h)
+    if (mi >= t.pre[t.npic]) return;
+    const int e = tick_entry(t, mi);
     const DevParams d = tick_params(t, e);
-    const int mby = d.y_min + (blockIdx.x - t.pre[e]), mbx = d.diag - 2 * mby;
+    const int mby = d.y_min + (mi - t.pre[e]), mbx = d.diag - 2 * mby;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, W4 = d.W >> 2;
     const bool avL = mbx > 0, avT = mby > 0, avTL = avL && avT, avTR = avT && mbx + 1 < d.mbw;
     const int lambda = d.lambda_mode, qp = d.qp, had = d.use_hadamard;
@@ -103,6 +105,6 @@ __global__ __launch_bounds__(NT) void k_mb_intra8(const TickArgs t) {
 }
 
 hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st) {
-    hipLaunchKernelGGL(k_mb_intra8, dim3(t.pre[t.npic]), dim3(NT), 0, st, t);
+    hipLaunchKernelGGL(k_mb_intra8, dim3(xcd_grid(t.pre[t.npic])), dim3(NT), 0, st, t);
     return hipGetLastError();
 }

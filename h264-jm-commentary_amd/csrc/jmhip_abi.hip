@@ -265,7 +265,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         c->bprof_tick = -1;
         if (const char *e = getenv("JMH_BLOCK_PROF")) {
             c->bprof_tick = atoi(e);
-            ALLOC(c->d_bprof, (size_t)3 * 3 * PMAX * c->mbh * sizeof(unsigned long long));
+            ALLOC(c->d_bprof, ((size_t)3 * 3 * PMAX * c->mbh + 64) * sizeof(unsigned long long));
         }
         if (const char *e = getenv("JMH_PHASE_PROF")) {
             c->prof_mb = atoi(e);
@@ -371,7 +371,7 @@ static int issue_tick(jmh_ctx *c) {
     t.npic = k; t.nP = nP; t.pre[k] = mbs;
     if (c->d_bprof && c->ticks_total == c->bprof_tick) {
         t.bprof = c->d_bprof;
-        c->bprof_blocks = (t.me_in_analyse ? t.pre[nP] : 0) + (t.pre[k] + 3) / 4;
+        c->bprof_blocks = xcd_grid(t.me_in_analyse ? t.pre[nP] : 0) + (t.pre[k] + 3) / 4;
     }
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
