@@ -522,7 +522,7 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
     }
     int mc8 = BIGCOST, bm = 0;
     for (int mode = 4; mode <= 7; mode++) {
-        if (!d.inter_search[mode]) continue;
+        if (!inter_on(d.isr, mode)) continue;
         const int c = s.motion_cost[mode][B8];
         if (c < mc8) { mc8 = c; bm = mode; }
     }

@@ -44,7 +44,8 @@ struct DevParams {
     int W, H, Wc, Hc, mbw, mbh;
     int sr, side, npos;
     int search_mode, use_hadamard, restrict_sr;
-    int inter_search[8];
+    int isr;                    // InterSearch16x16..4x4 as bits 1..7 (a mask: a per-thread array
+                                // indexed at run time would put the whole DevParams in scratch)
     int t8;                     // Transform8x8Mode (High profile)
     const uint8_t *orgY, *orgU, *orgV;
     const uint8_t *refY, *refU, *refV;
@@ -107,14 +108,16 @@ __device__ __forceinline__ int tick_entry(const TickArgs &t, int idx) {
     while (e + 1 < t.npic && t.pre[e + 1] <= idx) e++;
     return e;
 }
+__device__ __forceinline__ bool inter_on(int isr, int mode) { return (isr >> mode) & 1; }
 __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     DevParams d;
     const PicParams &q = t.p[e];
     d.W = t.W; d.H = t.H; d.Wc = t.W >> 1; d.Hc = t.H >> 1; d.mbw = t.mbw; d.mbh = t.mbh;
     d.sr = t.sr; d.side = 2 * t.sr + 1; d.npos = d.side * d.side;
     d.search_mode = t.search_mode; d.use_hadamard = t.use_hadamard; d.restrict_sr = t.restrict_sr;
+    d.isr = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) d.inter_search[i] = t.inter_search[i];
+    for (int i = 1; i < 8; i++) d.isr |= (t.inter_search[i] != 0) << i;
     d.t8 = t.t8;
     const int ls = t.W * t.H, lc = ls >> 2;
     d.orgY = q.org; d.orgU = q.org + ls; d.orgV = q.org + ls + lc;

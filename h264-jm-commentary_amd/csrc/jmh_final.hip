@@ -138,11 +138,11 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
     int min_cost = BIGCOST, best_mode = 1, best8x8 = 0;
     if (slice_p) {
         for (int mode = 1; mode < 4; mode++) {
-            if (!d.inter_search[mode]) continue;
+            if (!inter_on(d.isr, mode)) continue;
             const int cost = mode == 1 ? sc->motion_cost[1][0] : sc->motion_cost[mode][0] + sc->motion_cost[mode][1];
             if (cost < min_cost) { best_mode = mode; min_cost = cost; }
         }
-        if (d.inter_search[4] || d.inter_search[5] || d.inter_search[6] || d.inter_search[7]) {
+        if (inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7)) {
             best8x8 = sc->best8x8;
             if (sc->cost8x8 < min_cost) { best_mode = JMH_P8x8; min_cost = sc->cost8x8; }
         }

@@ -123,11 +123,11 @@ __device__ __forceinline__ bool epzs_cand(const DevParams &d, const FullS &s, in
         v = s.tref[ty][tx] == 0;
         x = rnd(s.tmv[ty][tx][0]); y = rnd(s.tmv[ty][tx][1]);
     } else if (i == 34) {
-        v = s.memok && d.inter_search[bt];                     // left MB's search (spatial memory)
+        v = s.memok && inter_on(d.isr, bt);                     // left MB's search (spatial memory)
         x = rnd(s.mem[bt][k0][0]); y = rnd(s.mem[bt][k0][1]);
     } else if (i < NPRED) {
         const int t = i - 34;                                  // block types 1..6 below bt
-        v = t < bt && d.inter_search[t];
+        v = t < bt && inter_on(d.isr, t);
         x = rnd(s.all_mv[t][k0][0]); y = rnd(s.all_mv[t][k0][1]);
     } else v = false;
     return v && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
@@ -192,7 +192,7 @@ __device__ void epzs_fullpel(const DevParams &d, FullS &s, int off, int bt, int 
 }
 
 // BlockMotionSearch [J] for one block: full-pel full search + SubPelBlockMotionSearch
-__device__ __attribute__((noinline)) void full_block_search(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int mc, int b8,
+__device__ __forceinline__ void full_block_search(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int mc, int b8,
                                                            int best8x8, int X0, int Y0, int left, int pslot) {
     const int tid = threadIdx.x;
     const bool prof = pslot >= 0 && pslot < 28 && d.prof && tid == 0 && d.prof_mb == (Y0 >> 2) * d.mbw + (X0 >> 2);
@@ -346,33 +346,34 @@ __global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
     }
     __syncthreads();
     if (d.prof && tid == 0 && d.prof_mb == mby * d.mbw + mbx) d.prof[33] = wall_clock64();
-    // PartitionMotionSearch [J] order: 16x16, 16x8 (2), 8x16 (2)
-    full_block_search(d, s, off, 1, 0, 0, 0, 0, 0, X0, Y0, left, 0);
-    full_block_search(d, s, off, 2, 0, 0, 0, 0, 0, X0, Y0, left, 2);
-    full_block_search(d, s, off, 2, 0, 2, 1, 0, 0, X0, Y0, left, 4);
-    full_block_search(d, s, off, 3, 0, 0, 0, 0, 0, X0, Y0, left, 6);
-    full_block_search(d, s, off, 3, 2, 0, 1, 0, 0, X0, Y0, left, 8);
-    // P8x8: per 8x8 block the sub-modes 4..7, then its best sub-mode (read through best8x8)
+    // PartitionMotionSearch [J] order: 16x16, 16x8 (2), 8x16 (2), then per 8x8 block the sub-modes
+    // 4..7 and its best sub-mode (read through best8x8).  One call site (a loop over the 41
+    // searches) so the search inlines once: no call frames / register spills to scratch.
     int best8x8 = 0, cost8x8 = 0;
-    for (int b8 = 0; b8 < 4; b8++) {
-        const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        full_block_search(d, s, off, 4, X, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        full_block_search(d, s, off, 5, X, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        full_block_search(d, s, off, 5, X, Y + 1, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        full_block_search(d, s, off, 6, X, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        full_block_search(d, s, off, 6, X + 1, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        full_block_search(d, s, off, 7, X, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        full_block_search(d, s, off, 7, X + 1, Y, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        full_block_search(d, s, off, 7, X, Y + 1, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        full_block_search(d, s, off, 7, X + 1, Y + 1, b8, b8, best8x8, X0, Y0, left, b8 == 0 ? 10 + 2 * __COUNTER__ : -1);
-        int mc8 = BIGCOST, bm = 0;
-        for (int mode = 4; mode <= 7; mode++) {
-            if (!d.inter_search[mode]) continue;
-            const int c = s.motion_cost[mode][b8];
-            if (c < mc8) { mc8 = c; bm = mode; }
+#pragma unroll 1
+    for (int i = 0; i < 41; i++) {
+        int bt, bx4, by4, mc, b8;
+        if (i < 5) {   // 16x16; 16x8 upper, lower; 8x16 left, right
+            bt = i == 0 ? 1 : i <= 2 ? 2 : 3;
+            bx4 = i == 4 ? 2 : 0; by4 = i == 2 ? 2 : 0; mc = (i == 2 || i == 4) ? 1 : 0; b8 = 0;
+        } else {       // 8x8; 8x4 x2; 4x8 x2; 4x4 x4 of 8x8 block b8
+            const int j = (i - 5) % 9;
+            b8 = (i - 5) / 9; mc = b8;
+            bt = j == 0 ? 4 : j <= 2 ? 5 : j <= 4 ? 6 : 7;
+            const int sx = j == 4 || j == 6 || j == 8 ? 1 : 0, sy = j == 2 || j == 7 || j == 8 ? 1 : 0;
+            bx4 = 2 * (b8 & 1) + sx; by4 = 2 * (b8 >> 1) + sy;
         }
-        best8x8 |= bm << (4 * b8);
-        cost8x8 += mc8;
+        full_block_search(d, s, off, bt, bx4, by4, mc, b8, i < 5 ? 0 : best8x8, X0, Y0, left, i < 14 ? 2 * i : -1);
+        if (i >= 5 && (i - 5) % 9 == 8) {
+            int mc8 = BIGCOST, bm = 0;
+            for (int mode = 4; mode <= 7; mode++) {
+                if (!inter_on(d.isr, mode)) continue;
+                const int c = s.motion_cost[mode][b8];
+                if (c < mc8) { mc8 = c; bm = mode; }
+            }
+            best8x8 |= bm << (4 * b8);
+            cost8x8 += mc8;
+        }
     }
     // results: MVs and partition costs of types 1..7, P8x8 decision, FindSkipModeMotionVector
     for (int i = tid; i < 7 * 32; i += NTF) {
