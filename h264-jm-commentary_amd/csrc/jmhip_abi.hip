@@ -655,9 +655,11 @@ int jmh_sync(jmh_ctx *c) {
         HCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->dev));
         double us = rate_khz > 0 ? 1e3 / rate_khz : 0.01;
         unsigned long long t0 = ~0ull;
-        for (int k = 0; k < 64; k++) if (h[k] && h[k] < t0) t0 = h[k];
+        for (int k = 0; k < 64; k++) if (k != 31 && h[k] && h[k] < t0) t0 = h[k];   // [31]: a count
         fprintf(stderr, "jmh_phase mb=%d us since first stamp:", c->prof_mb);
-        for (int k = 0; k < 64; k++) if (h[k]) fprintf(stderr, " [%d]%.2f", k, (double)(h[k] - t0) * us);
+        for (int k = 0; k < 64; k++)
+            if (k == 31 && h[k]) fprintf(stderr, " [31]#%llu", h[k]);
+            else if (h[k]) fprintf(stderr, " [%d]%.2f", k, (double)(h[k] - t0) * us);
         fprintf(stderr, "\n");
         HCHK(hipMemset(c->d_prof, 0, sizeof(h)));
     }
