@@ -85,6 +85,7 @@ struct TickArgs {
     unsigned long long *prof;
     int prof_mb;
     unsigned long long *bprof;           // debug (JMH_BLOCK_PROF): per-block start / end / role
+    unsigned long long *bprof_fin;       //   ... of k_mb_final (role 3)
     int me_in_analyse;                   // 1: k_mb_analyse runs the FFS searches; 0: k_mb_me_full did
                                          //   (full search, SearchMode -1, or EPZS, SearchMode 3)
     int t8;                              // Transform8x8Mode: k_mb_intra8 ran, k_mb_final decides 4x4 / 8x8

@@ -98,6 +98,7 @@ __device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int al
 __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
     __shared__ FinS s;
     const int tid = threadIdx.x;
+    const unsigned long long bt0 = t.bprof_fin ? wall_clock64() : 0;
     const int m = xcd_block(blockIdx.x, t.pre[t.npic]);       // XCD-aware (jmh_device.h)
     if (m >= t.pre[t.npic]) return;                           // padding block (whole workgroup)
     const int e = tick_entry(t, m);
@@ -499,6 +500,11 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
         (void)Hc;
     }
     PSTAMP(19);
+    if (t.bprof_fin && tid == 0) {
+        t.bprof_fin[3 * blockIdx.x] = bt0;
+        t.bprof_fin[3 * blockIdx.x + 1] = wall_clock64();
+        t.bprof_fin[3 * blockIdx.x + 2] = 3;
+    }
 }
 
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st) {

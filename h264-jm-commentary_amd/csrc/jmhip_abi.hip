@@ -371,7 +371,10 @@ static int issue_tick(jmh_ctx *c) {
     t.npic = k; t.nP = nP; t.pre[k] = mbs;
     if (c->d_bprof && c->ticks_total == c->bprof_tick) {
         t.bprof = c->d_bprof;
-        c->bprof_blocks = xcd_grid(t.me_in_analyse ? t.pre[nP] : 0) + (t.pre[k] + 3) / 4;
+        const int na = xcd_grid(t.me_in_analyse ? t.pre[nP] : 0) + (t.pre[k] + 3) / 4;
+        t.bprof_fin = c->d_bprof + 3 * na;
+        HCHK(hipMemsetAsync(c->d_bprof, 0, ((size_t)3 * 3 * PMAX * c->mbh + 64) * sizeof(unsigned long long), c->st));
+        c->bprof_blocks = na + xcd_grid(t.pre[k]);
     }
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
@@ -632,19 +635,22 @@ int jmh_sync(jmh_ctx *c) {
         HCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->dev));
         double us = rate_khz > 0 ? 1e3 / rate_khz : 0.01;
         unsigned long long t0 = ~0ull, t1 = 0;
-        double sum[3] = {0, 0, 0}, mx[3] = {0, 0, 0};
-        int n[3] = {0, 0, 0};
+        double sum[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0};
+        int n[4] = {0, 0, 0, 0};
+        unsigned long long f0 = ~0ull, f1 = 0;
         for (int i = 0; i < c->bprof_blocks; i++) {
             unsigned long long a = h[3 * i], b = h[3 * i + 1];
             int role = (int)h[3 * i + 2];
-            if (role < 0 || role > 2 || b < a) continue;
+            if (!a || role < 0 || role > 3 || b < a) continue;   // 0: padding block, not written
+            if (role == 3) { f0 = a < f0 ? a : f0; f1 = b > f1 ? b : f1; }
             t0 = a < t0 ? a : t0; t1 = b > t1 ? b : t1;
             double dur = (double)(b - a) * us;
             sum[role] += dur; n[role]++; mx[role] = dur > mx[role] ? dur : mx[role];
         }
         fprintf(stderr, "jmh_blocks tick=%d blocks=%d span=%.1fus", c->bprof_tick, c->bprof_blocks, (double)(t1 - t0) * us);
-        for (int r = 0; r < 3; r++)
+        for (int r = 0; r < 4; r++)
             fprintf(stderr, " role%d: n=%d mean=%.1fus max=%.1fus", r, n[r], n[r] ? sum[r] / n[r] : 0.0, mx[r]);
+        if (f1) fprintf(stderr, " final: first start %.1fus after the analysis' first, span %.1fus", (double)(f0 - t0) * us, (double)(f1 - f0) * us);
         fprintf(stderr, "\n");
         c->bprof_blocks = 0;
     }
