@@ -11,7 +11,7 @@
 #define NT 256                           // threads per finalize / unit workgroup
 #define NTA 512                          // threads per analysis workgroup (8 waves, 2 per SIMD)
 #define BIGCOST (1 << 20)
-#define PMAX 20                          // pictures per wavefront tick (pipelined pictures in flight)
+#define PMAX 34                          // pictures per wavefront tick (pipelined pictures in flight)
 // A picture's macroblock (x, y) reads its reference (the previous picture, deblocked) at pixel
 // offsets -68..+83 from the MB origin: window centre |MVP/4| <= SR, positions +-SR around it,
 // +-3/4 sub-pel, the 6-tap support and the LDS window margin (SR 32).  The farthest samples, rows
@@ -76,8 +76,9 @@ struct PicParams {
     const int8_t *tref;
     jmh_mb_result *res;
     MbScratch *scr;
-    int32_t slice_type, qp, lambda_mode, lambda_motion, cqp_off, lf_disable, lf_offA, lf_offB;
-    int32_t diag, y_min;
+    int32_t lambda_mode, lambda_motion;
+    int16_t diag, y_min;
+    int8_t slice_type, qp, cqp_off, lf_disable, lf_offA, lf_offB;   // packed: PMAX entries fit 4 KB
 };
 struct TickArgs {
     int W, H, mbw, mbh, sr, search_mode, use_hadamard, restrict_sr;
@@ -93,6 +94,7 @@ struct TickArgs {
     int pre[PMAX + 1];                   // MB prefix sums over the entries
     PicParams p[PMAX];
 };
+static_assert(sizeof(TickArgs) <= 4096, "TickArgs is passed by value in the kernel argument segment");
 
 // XCD-aware block order.  Workgroups are dispatched round-robin over the 8 XCDs (hardware block b
 // runs on XCD b % 8), each with its own L2.  A launch of n logical blocks uses 8 * ceil(n / 8)

@@ -298,7 +298,10 @@ def run_chain(enc, pics, qp, dbk, pipelined):
                                               (1920, 1088, 32, 20, (37, -29), {}), (1920, 1088, 32, 12, (-62, -61), {}),
                                               (640, 480, 32, 10, (63, 62), {}),
                                               (640, 480, 32, 10, (37, -29), dict(search_mode=3, transform_8x8_mode=1)),
-                                              (1920, 1088, 32, 20, (-62, -61), dict(search_mode=3, transform_8x8_mode=1))])
+                                              (1920, 1088, 32, 20, (-62, -61), dict(search_mode=3, transform_8x8_mode=1)),
+                                              # tall: 526 diagonals, ~33 pictures in flight (PMAX entries per tick)
+                                              (256, 4096, 32, 40, (37, -29), {}),
+                                              (256, 4096, 32, 40, (-62, -61), dict(search_mode=3, transform_8x8_mode=1))])
 def test_pipelined_chain_equals_sequential(w, h, sr, n, step, kw):
     """Pictures in flight together (lag PIPE_LAG diagonals) == one picture at a time, bit for
     bit, under motion that pushes MVs to the search-window edge (|MV| up to 63 px at SR 32: the
