@@ -513,7 +513,7 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
     {   // stage 2: 4x4 bottom-left
         const SDesc sd[1] = {{7, X, Y + 1, B8, 7, X + 1, Y + 1, 0}};
         me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X, Y + 1); },
-                          B8 == 3 ? 10 : B8 == 0 ? 11 : -1, idle);
+                          B8 == 3 ? 10 : -1, idle);
     }
     {   // stage 3: 4x4 bottom-right
         const SDesc sd[1] = {{7, X + 1, Y + 1, B8, 0, 0, 0, 0}};
@@ -603,7 +603,6 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     if (tid == 0) { s.pst = prof ? d.prof + 20 : nullptr; s.pn = 0; }
     if (tid < 256) s.in.org[tid] = s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    else if (tid < 384) load_orgc(d, s.in.nb, tid - 256, mbx, mby);
     else if (tid >= 384 && tid < 394) { load_border(d, s.bd, tid - 384, mbx, mby); load_border(d, s.in.bd, tid - 384, mbx, mby); }
     else if (tid >= 472 && tid < 478) s.in.part[(tid - 472) / 3][(tid - 472) % 3] = 0;
     else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
@@ -875,7 +874,7 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratc
 
 // one MB on 128 threads (tid = 0..127, waves 0 and 1 of the group); every thread of the
 // workgroup reaches the same barriers (act: the group has an MB)
-__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act) {
+__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act, bool i4) {
     const int wave = tid >> 6, lane = tid & 63;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
@@ -902,19 +901,19 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     for (int dg = 0; dg < 10; dg++) {         // blocks with bx4 + 2*by4 == dg, by4 ascending
         const int by_lo = dg > 3 ? (dg - 2) >> 1 : 0;
         const int by4 = by_lo + wave, bx4 = dg - 2 * by4;
-        if (act && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+        if (act && i4 && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
         __syncthreads();
     }
     if (act && lane == 0) { s.part[wave][0] = acc[0]; s.part[wave][1] = acc[1]; s.part[wave][2] = acc[2]; }
     __syncthreads();
     if (!act) return;
-    if (tid == 0) {
+    if (i4 && tid == 0) {
         scr->i4cost = 24 * d.lambda_mode + s.part[0][0] + s.part[1][0];   // 4 x (int)floor(6*lambda+0.4999)
         scr->i4cbp = s.part[0][1] | s.part[1][1];
         scr->i4blk = s.part[0][2] | s.part[1][2];
     }
-    if (tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
-    if (tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
+    if (i4 && tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
+    if (i4 && tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
     PSTAMP(13);
     // Intra16x16 (wave 0) and intra chroma mode (wave 1) decisions
     if (wave == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
@@ -928,10 +927,7 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
 __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int mbx, int mby) {
     const int lane = threadIdx.x & 63;
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
-    if (k == 11) {   // the Intra16x16 (w 0) and intra chroma mode (w 1) decisions
-        if (w == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
-        else chroma_decision(d, s.nb, scr, lane, avL, avT, avTL);
-    } else if (k < 10) {
+    if (k < 10) {
         const int q_bits = 15 + d.qp / 6;
         const int qpk = d.slice_type == JMH_P_SLICE ? (1 << q_bits) / 6 : (1 << q_bits) / 3;
         int tab[3];
@@ -975,12 +971,12 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
         const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
         me_mb(d, s.me, mbx, mby);
     } else {
-        const int q = __builtin_amdgcn_readfirstlane(nPm + 4 * (b - nPg) + (int)(threadIdx.x >> 7));
+        const int q = __builtin_amdgcn_readfirstlane(4 * (b - nPg) + (int)(threadIdx.x >> 7));
         const bool act = q < tot;
         const int e = tick_entry(t, act ? q : 0);
         const DevParams d = tick_params(t, e);
         const int mby = d.y_min + ((act ? q : t.pre[e]) - t.pre[e]), mbx = d.diag - 2 * mby;
-        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act);
+        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act, q >= nPm);
     }
     if (t.bprof) {
         __syncthreads();
@@ -993,8 +989,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
-    const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0;
-    const int nblocks = xcd_grid(nPm) + (t.pre[t.npic] - nPm + 3) / 4;
+    const int nblocks = xcd_grid(t.me_in_analyse ? t.pre[t.nP] : 0) + (t.pre[t.npic] + 3) / 4;
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }
