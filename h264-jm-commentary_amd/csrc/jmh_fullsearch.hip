@@ -295,7 +295,7 @@ __device__ __forceinline__ void full_block_search(const DevParams &d, FullS &s, 
     if (prof) d.prof[35 + pslot] = wall_clock64();
 }
 
-__global__ __launch_bounds__(NTF, 2) void k_mb_me_full(const TickArgs t) {
+__global__ __launch_bounds__(NTF, 6) void k_mb_me_full(const TickArgs t) {
     __shared__ FullS s;
     const int b = xcd_block(blockIdx.x, t.pre[t.nP]), tid = threadIdx.x;   // XCD-aware (jmh_device.h)
     if (b >= t.pre[t.nP]) return;
