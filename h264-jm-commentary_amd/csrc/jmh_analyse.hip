@@ -51,6 +51,14 @@ static __constant__ uint16_t c_i4tab[9][16] = {
     {0x0085, 0x00C9, 0x010D, 0x0151, 0x0C86, 0x10CA, 0x150E, 0x1952, 0x00C9, 0x010D, 0x0151, 0x0195, 0x10CA, 0x150E, 0x1952, 0x1D96},
     {0x02A5, 0x2EA6, 0x02E9, 0x32EA, 0x02E9, 0x32EA, 0x032D, 0x332E, 0x032D, 0x332E, 0x3332, 0x3332, 0x3332, 0x3332, 0x3332, 0x3332}};
 
+// intra neighbourhood of an MB in LDS (unfiltered reconstruction of the current picture)
+struct IntraNb {
+    uint8_t orgc[2][64];
+    uint8_t rtop[24];                         // luma row y = -1, x = -1..19 -> [x + 1]
+    uint8_t rleft[16];
+    uint8_t ctop[2][12];                      // chroma rows y = -1, x = -1..7 -> [x + 1]
+    uint8_t cleft[2][8];
+};
 struct IntraS {
     uint8_t org[256];
     uint8_t rec[256];
@@ -525,6 +533,62 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
 // ======================================================================================
 //  intra decisions
 // ======================================================================================
+// intrapred_luma_16x16 + find_sad_16x16 on one wave: 4 modes x 16 blocks = 64 lanes
+__device__ __forceinline__ void i16_decision(const DevParams &d, const uint8_t *org, const IntraNb &nb, MbScratch *scr, int lane, bool avL, bool avT,
+                                             bool avTL) {
+    const int m = lane >> 4, b = lane & 15, ox = (b & 3) * 4, oy = (b >> 2) * 4;
+    const uint8_t *T = nb.rtop + 1, *L = nb.rleft;
+    const I16Par par = i16_params(T, L, avT, avL);
+    int mm[16], t[16];
+    for (int yy = 0; yy < 4; yy++)
+        for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy);
+    for (int yy = 0; yy < 4; yy++) {
+        int *r = mm + 4 * yy;
+        int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
+        t[4 * yy] = a0 + a1; t[4 * yy + 2] = a0 - a1; t[4 * yy + 1] = a2 + a3; t[4 * yy + 3] = a3 - a2;
+    }
+    int acs = 0, dcc = 0;
+    for (int xx = 0; xx < 4; xx++) {
+        int a0 = t[xx] + t[12 + xx], a1 = t[4 + xx] + t[8 + xx], a2 = t[4 + xx] - t[8 + xx], a3 = t[xx] - t[12 + xx];
+        int o0 = a0 + a1, o2 = a0 - a1, o1 = a2 + a3, o3 = a3 - a2;
+        if (xx == 0) dcc = o0; else acs += abs(o0);
+        acs += abs(o1) + abs(o2) + abs(o3);
+    }
+    const int cost = row16_sum(acs) + lane_had_abs(dcc / 4, b);
+    const bool av16[4] = {avT, avL, true, avT && avL && avTL};
+    int best = MAX_VALUE, i16mode = 2;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int c = __builtin_amdgcn_readlane(cost, 16 * k);
+        if (av16[k] && c < best) { best = c; i16mode = k; }
+    }
+    if (lane == 0) { scr->i16cost = best / 2; scr->i16mode = i16mode; }
+}
+
+// IntraChromaPrediction8x8 mode decision on one wave: 4 modes x 2 components x 4 blocks
+__device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraNb &nb, MbScratch *scr, int lane, bool avL, bool avT, bool avTL) {
+    int sat = 0;
+    if (lane < 32) {
+        const int m = lane >> 3, uv = (lane >> 2) & 1, b = lane & 3, xo = (b & 1) * 4, yo = (b >> 1) * 4;
+        const uint8_t *T = nb.ctop[uv] + 1, *L = nb.cleft[uv];
+        int df[16];
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++)
+                df[4 * y + x] = nb.orgc[uv][(yo + y) * 8 + xo + x] - chroma_pred_px(T, L, nb.ctop[uv][0], avT, avL, m, xo + x, yo + y);
+        sat = satd4x4(df, d.use_hadamard);
+    }
+    const bool cav[4] = {true, avL, avT, avT && avL && avTL};
+    int minc = BIGCOST, c_mode = 0;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) c += __builtin_amdgcn_readlane(sat, 8 * m + q);
+        if (cav[m] && c < minc) { minc = c; c_mode = m; }
+    }
+    if (lane == 0) scr->c_mode = c_mode;
+}
+
 // ======================================================================================
 //  motion search of one P macroblock (all 41 searches)
 // ======================================================================================
@@ -810,7 +874,7 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratc
 
 // one MB on 128 threads (tid = 0..127, waves 0 and 1 of the group); every thread of the
 // workgroup reaches the same barriers (act: the group has an MB)
-__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act) {
+__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act, bool i4) {
     const int wave = tid >> 6, lane = tid & 63;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
@@ -837,19 +901,19 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     for (int dg = 0; dg < 10; dg++) {         // blocks with bx4 + 2*by4 == dg, by4 ascending
         const int by_lo = dg > 3 ? (dg - 2) >> 1 : 0;
         const int by4 = by_lo + wave, bx4 = dg - 2 * by4;
-        if (act && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+        if (act && i4 && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
         __syncthreads();
     }
     if (act && lane == 0) { s.part[wave][0] = acc[0]; s.part[wave][1] = acc[1]; s.part[wave][2] = acc[2]; }
     __syncthreads();
     if (!act) return;
-    if (tid == 0) {
+    if (i4 && tid == 0) {
         scr->i4cost = 24 * d.lambda_mode + s.part[0][0] + s.part[1][0];   // 4 x (int)floor(6*lambda+0.4999)
         scr->i4cbp = s.part[0][1] | s.part[1][1];
         scr->i4blk = s.part[0][2] | s.part[1][2];
     }
-    if (tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
-    if (tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
+    if (i4 && tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
+    if (i4 && tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
     PSTAMP(13);
     // Intra16x16 (wave 0) and intra chroma mode (wave 1) decisions
     if (wave == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
@@ -893,11 +957,9 @@ __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScra
 __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     __shared__ AnalyseS s;
     // blocks: [0, nPm) the motion search of each P picture MB with its Intra4x4 decision (longest,
-    // dispatched first), then intra workgroups (Intra4x4, Intra16x16, chroma) over the MBs without
-    // a motion-search workgroup (I pictures; SearchMode -1 / 3, where k_mb_me_full searched), four
-    // MBs (128 threads each) per workgroup.  The Intra16x16 and chroma decisions of the P MBs run
-    // at the start of k_mb_final: as workgroups here they would wait for free slots behind the
-    // motion search (two 512-thread workgroups fill a CU) and end the launch late.
+    // dispatched first), then intra workgroups over every MB, four MBs (128 threads each) per
+    // workgroup: Intra16x16 + chroma decisions, and Intra4x4 for MBs without a motion-search
+    // workgroup (I pictures; SearchMode -1, where k_mb_me_full searched)
     const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0, nPg = xcd_grid(nPm), tot = t.pre[t.npic], b = blockIdx.x;
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
     const int role = b < nPg ? 2 : 0;
@@ -909,12 +971,12 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
         const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
         me_mb(d, s.me, mbx, mby);
     } else {
-        const int q = __builtin_amdgcn_readfirstlane(nPm + 4 * (b - nPg) + (int)(threadIdx.x >> 7));
+        const int q = __builtin_amdgcn_readfirstlane(4 * (b - nPg) + (int)(threadIdx.x >> 7));
         const bool act = q < tot;
         const int e = tick_entry(t, act ? q : 0);
         const DevParams d = tick_params(t, e);
         const int mby = d.y_min + ((act ? q : t.pre[e]) - t.pre[e]), mbx = d.diag - 2 * mby;
-        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act);
+        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act, q >= nPm);
     }
     if (t.bprof) {
         __syncthreads();
@@ -927,8 +989,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
-    const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0;
-    const int nblocks = xcd_grid(nPm) + (t.pre[t.npic] - nPm + 3) / 4;
+    const int nblocks = xcd_grid(t.me_in_analyse ? t.pre[t.nP] : 0) + (t.pre[t.npic] + 3) / 4;
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }

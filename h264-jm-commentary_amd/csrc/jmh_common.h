@@ -576,75 +576,6 @@ __device__ __forceinline__ int i8_pred_px(const int *f, int dcv, int m, int x, i
 #undef TAP
 }
 
-// ======================================================================================
-//  Intra16x16 and intra chroma mode decisions (k_mb_analyse intra workgroups; k_mb_final for
-//  P macroblocks of a motion-search workgroup)
-// ======================================================================================
-// intra neighbourhood of an MB in LDS (unfiltered reconstruction of the current picture)
-struct IntraNb {
-    uint8_t orgc[2][64];
-    uint8_t rtop[24];                         // luma row y = -1, x = -1..19 -> [x + 1]
-    uint8_t rleft[16];
-    uint8_t ctop[2][12];                      // chroma rows y = -1, x = -1..7 -> [x + 1]
-    uint8_t cleft[2][8];
-};
-
-// intrapred_luma_16x16 + find_sad_16x16 on one wave: 4 modes x 16 blocks = 64 lanes
-__device__ __forceinline__ void i16_decision(const DevParams &d, const uint8_t *org, const IntraNb &nb, MbScratch *scr, int lane, bool avL, bool avT,
-                                             bool avTL) {
-    const int m = lane >> 4, b = lane & 15, ox = (b & 3) * 4, oy = (b >> 2) * 4;
-    const uint8_t *T = nb.rtop + 1, *L = nb.rleft;
-    const I16Par par = i16_params(T, L, avT, avL);
-    int mm[16], t[16];
-    for (int yy = 0; yy < 4; yy++)
-        for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy);
-    for (int yy = 0; yy < 4; yy++) {
-        int *r = mm + 4 * yy;
-        int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
-        t[4 * yy] = a0 + a1; t[4 * yy + 2] = a0 - a1; t[4 * yy + 1] = a2 + a3; t[4 * yy + 3] = a3 - a2;
-    }
-    int acs = 0, dcc = 0;
-    for (int xx = 0; xx < 4; xx++) {
-        int a0 = t[xx] + t[12 + xx], a1 = t[4 + xx] + t[8 + xx], a2 = t[4 + xx] - t[8 + xx], a3 = t[xx] - t[12 + xx];
-        int o0 = a0 + a1, o2 = a0 - a1, o1 = a2 + a3, o3 = a3 - a2;
-        if (xx == 0) dcc = o0; else acs += abs(o0);
-        acs += abs(o1) + abs(o2) + abs(o3);
-    }
-    const int cost = row16_sum(acs) + lane_had_abs(dcc / 4, b);
-    const bool av16[4] = {avT, avL, true, avT && avL && avTL};
-    int best = MAX_VALUE, i16mode = 2;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int c = __builtin_amdgcn_readlane(cost, 16 * k);
-        if (av16[k] && c < best) { best = c; i16mode = k; }
-    }
-    if (lane == 0) { scr->i16cost = best / 2; scr->i16mode = i16mode; }
-}
-
-// IntraChromaPrediction8x8 mode decision on one wave: 4 modes x 2 components x 4 blocks
-__device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraNb &nb, MbScratch *scr, int lane, bool avL, bool avT, bool avTL) {
-    int sat = 0;
-    if (lane < 32) {
-        const int m = lane >> 3, uv = (lane >> 2) & 1, b = lane & 3, xo = (b & 1) * 4, yo = (b >> 1) * 4;
-        const uint8_t *T = nb.ctop[uv] + 1, *L = nb.cleft[uv];
-        int df[16];
-        for (int y = 0; y < 4; y++)
-            for (int x = 0; x < 4; x++)
-                df[4 * y + x] = nb.orgc[uv][(yo + y) * 8 + xo + x] - chroma_pred_px(T, L, nb.ctop[uv][0], avT, avL, m, xo + x, yo + y);
-        sat = satd4x4(df, d.use_hadamard);
-    }
-    const bool cav[4] = {true, avL, avT, avT && avL && avTL};
-    int minc = BIGCOST, c_mode = 0;
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-        int c = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) c += __builtin_amdgcn_readlane(sat, 8 * m + q);
-        if (cav[m] && c < minc) { minc = c; c_mode = m; }
-    }
-    if (lane == 0) scr->c_mode = c_mode;
-}
-
 // debug phase profiling of one macroblock (DevParams::prof): lane 0 of wave w of the matching group
 __device__ __forceinline__ bool prof_mb_here(const DevParams &d, int mbx, int mby, int w = 0) {
     return d.prof && threadIdx.x == 64 * w && d.prof_mb == mby * d.mbw + mbx;

@@ -8,10 +8,14 @@
 
 struct FinS {
     uint8_t org[256];
+    uint8_t orgc[2][64];
     uint8_t rec[256];
     uint8_t pred[256];                   // inter prediction (TransformDecision / 8x8 path)
     int tdc[4][2];                       // per 8x8: sum of 4x4 SATDs, 8x8 SATD
-    IntraNb nb;                          // chroma source + unfiltered neighbour samples
+    uint8_t rtop[24];                    // luma row y = -1, x = -1..19 -> [x + 1]
+    uint8_t rleft[16];
+    uint8_t ctop[2][12];                 // chroma rows y = -1, x = -1..7 -> [x + 1]
+    uint8_t cleft[2][8];
     int16_t fmv[16][2];
     int16_t lev[16][16];
     int bcost[16];
@@ -114,28 +118,21 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
     s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     if (tid < 128) {
         const int uv = tid >> 6, k = tid & 63;
-        s.nb.orgc[uv][k] = (uv ? d.orgV : d.orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
+        s.orgc[uv][k] = (uv ? d.orgV : d.orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
     } else if (tid >= 128 && tid < 149) {
         const int x = tid - 129;
         const bool av = x < 0 ? avTL : x < 16 ? avT : false;
-        s.nb.rtop[x + 1] = av ? d.recY[(pix_y - 1) * W + pix_x + x] : 0;
+        s.rtop[x + 1] = av ? d.recY[(pix_y - 1) * W + pix_x + x] : 0;
     } else if (tid >= 160 && tid < 176) {
         const int y = tid - 160;
-        s.nb.rleft[y] = avL ? d.recY[(pix_y + y) * W + pix_x - 1] : 0;
+        s.rleft[y] = avL ? d.recY[(pix_y + y) * W + pix_x - 1] : 0;
     } else if (tid >= 192 && tid < 210) {
         const int i = tid - 192, uv = i / 9, x = i - 9 * uv - 1;
         const bool av = x < 0 ? avTL : avT;
-        s.nb.ctop[uv][x + 1] = av ? (uv ? d.recV : d.recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
+        s.ctop[uv][x + 1] = av ? (uv ? d.recV : d.recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
     } else if (tid >= 224 && tid < 240) {
         const int i = tid - 224, uv = i >> 3, y = i & 7;
-        s.nb.cleft[uv][y] = avL ? (uv ? d.recV : d.recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
-    }
-
-    if (t.me_in_analyse && slice_p) {   // Intra16x16 (wave 0) and chroma (wave 1) decisions of a P MB
-        __syncthreads();                  // s.org, s.nb
-        if (tid < 64) i16_decision(d, s.org, s.nb, d.scr + mby * d.mbw + mbx, tid, avL, avT, avTL);
-        else if (tid < 128) chroma_decision(d, s.nb, d.scr + mby * d.mbw + mbx, tid - 64, avL, avT, avTL);
-        __syncthreads();                  // sc->i16cost / i16mode / c_mode
+        s.cleft[uv][y] = avL ? (uv ? d.recV : d.recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
     }
 
     // ---- mode decision (encode_one_macroblock, RDO off): costs from k_mb_analyse
@@ -188,7 +185,7 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
         // dct_luma_16x16 [J]
         const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per;
         const int qp_const = (1 << q_bits) / 3, qp_const2 = qp_const << 1;
-        const uint8_t *T = s.nb.rtop + 1, *L = s.nb.rleft;
+        const uint8_t *T = s.rtop + 1, *L = s.rleft;
         const I16Par par = i16_params(T, L, avT, avL);
         const int p = i16_pred(par, T, L, i16mode, px4, py4);
         const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
@@ -315,7 +312,7 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
     int cdq = 0, cpredv = 0;
     if (tid < 128) {
         if (is_intra) {
-            cpredv = chroma_pred_px(s.nb.ctop[cuv] + 1, s.nb.cleft[cuv], s.nb.ctop[cuv][0], avT, avL, c_mode, cxo, cyo);
+            cpredv = chroma_pred_px(s.ctop[cuv] + 1, s.cleft[cuv], s.ctop[cuv][0], avT, avL, c_mode, cxo, cyo);
         } else {
             // OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2
             const uint8_t *R = cuv ? d.refV : d.refU;
@@ -327,7 +324,7 @@ __global__ __launch_bounds__(NT) void k_mb_final(const TickArgs t) {
             cpredv = ((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] + (8 - fx) * fy * R[y1 * Wc + x0] +
                       fx * fy * R[y1 * Wc + x1] + 32) >> 6;
         }
-        const int c = lane_fwd4x4(s.nb.orgc[cuv][cyo * 8 + cxo] - cpredv, l);
+        const int c = lane_fwd4x4(s.orgc[cuv][cyo * 8 + cxo] - cpredv, l);
         if (l == 0) s.cdcin[cuv][cb] = c;
         int lev, cc;
         unsigned nz = lane_quant(c, l, qpc, cqp_const, true, lev, cdq, cc);

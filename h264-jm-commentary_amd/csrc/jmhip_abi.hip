@@ -371,8 +371,7 @@ static int issue_tick(jmh_ctx *c) {
     t.npic = k; t.nP = nP; t.pre[k] = mbs;
     if (c->d_bprof && c->ticks_total == c->bprof_tick) {
         t.bprof = c->d_bprof;
-        const int nPm = t.me_in_analyse ? t.pre[nP] : 0;
-        const int na = xcd_grid(nPm) + (t.pre[k] - nPm + 3) / 4;
+        const int na = xcd_grid(t.me_in_analyse ? t.pre[nP] : 0) + (t.pre[k] + 3) / 4;
         t.bprof_fin = c->d_bprof + 3 * na;
         HCHK(hipMemsetAsync(c->d_bprof, 0, ((size_t)3 * 3 * PMAX * c->mbh + 64) * sizeof(unsigned long long), c->st));
         c->bprof_blocks = na + xcd_grid(t.pre[k]);
