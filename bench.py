@@ -5,12 +5,25 @@ One step = one P picture of the hot path with inputs resident in HBM, referencin
 picture's deblocked reconstruction: the whole macroblock wavefront (k_mb_analyse: FFS SAD table
 + argmin, sub-pel SATD search on the fly from the reference, intra decisions; k_mb_final: RDO-off
 mode decision, luma/chroma TQ + reconstruction, deblocking) over all 8160 macroblocks of a coded
-1920x1088 picture.  Pictures are pipelined: picture q runs diagonal d once picture q-1 has
-finished diagonal d + PIPE_LAG, so ~15 pictures share each launch; the timed region holds the
-pipeline fill and drain (sync on both sides).  Entropy coding is excluded, as in JM's
-ME/transform time.  Multi-GPU: one independent stream per rank (seed = rank), no
-collective in the data path; a gloo barrier brackets the timed region and the maximum time over
-ranks is used (h264-jm-commentary_amd/streams.py).
+1920x1088 picture.  The source is SURVEY.md §8d's synthetic sequence (an IDR picture + --frames P
+pictures, resident in HBM, cycled).  Pictures are pipelined: picture q runs diagonal d once
+picture q-1 has finished diagonal d + PIPE_LAG, so ~16 pictures share each launch.  The timed
+region is steady state: the warmup (at least the pipeline depth) fills the pipeline, a barrier +
+wait for every issued launch brackets exactly --steps steps on both sides, and exactly --steps
+pictures complete inside it (checked: `pictures_completed`), so the value does not depend on
+--steps (h264-jm-commentary_amd/streams.py).  Entropy coding is excluded, as in JM's ME/transform
+time (BASELINE.md).
+
+Also reported (never `value`): the PCIe-inclusive rate of the host-buffer path (jmh_frame_push /
+jmh_frame_pop: source H2D, results + reconstruction D2H; SURVEY §8d's submit-to-host-visible
+timer), the single-picture latency (push -> results host-visible on an empty pipeline), and a
+correctness check — the CPU baseline's I + P pictures encoded on the GPU and compared with the
+oracle's results of the same run (`verified`).
+
+Multi-GPU (config 4): one independent stream per rank (seed = rank), no collective in the data
+path; a gloo barrier brackets the timed region and the maximum time over ranks is used.
+`--gpus N` without a launcher spawns N ranks itself (one process per GPU, rank k on device
+k mod the device count); under torchrun WORLD_SIZE must equal --gpus.
 
 --config 3 runs BASELINE.json's config 3 instead (a variant line, not the headline metric):
 2160p synthetic, High profile, EPZS (SearchMode 3) + adaptive 8x8 transform (Transform8x8Mode 1).
@@ -21,24 +34,27 @@ import argparse
 import importlib.util
 import json
 import os
+import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "h264-jm-commentary_amd")
 
-METRIC = "ME+transform megapixels/sec @1080p FullSearch SR=32; bit-exact bitstream vs JM"
+METRIC = "ME+transform megapixels/sec @1080p FullSearch SR=32; bit-exact vs the in-repo JM restatement (oracle)"
 # BASELINE.json configs measured here: 2 (the headline) and 3 (variant)
 CONFIGS = {
     2: dict(metric=METRIC, disp=(1920, 1080), coded=(1920, 1088), search_mode=0, t8=0,
             workload="1080p synthetic YUV420 (coded 1920x1088), Baseline, {sm} SearchRange=32, RestrictSearchRange=2, "
-                     "UseHadamard=1, 7 inter block sizes, RDO off, QP 28, P pictures (one independent stream per GPU)"),
+                     "UseHadamard=1, 7 inter block sizes, RDO off, QP 28, IDR + {nf}-picture P sequence cycled "
+                     "(one independent stream per GPU)"),
     3: dict(metric="ME+transform megapixels/sec @2160p High EPZS SR=32 + 8x8 transform (config 3)", disp=(3840, 2160),
             coded=(3840, 2160), search_mode=3, t8=1,
             workload="2160p synthetic YUV420, High profile (ProfileIDC 100), EPZS SearchMode=3 SearchRange=32, "
                      "Transform8x8Mode=1 (Intra8x8 + TransformDecision), UseHadamard=1, 7 inter block sizes, RDO off, "
-                     "QP 28, P pictures (one independent stream per GPU)"),
+                     "QP 28, IDR + {nf}-picture P sequence cycled (one independent stream per GPU)"),
 }
 DISP_W, DISP_H = 1920, 1080
 W, H = 1920, 1088
@@ -51,10 +67,11 @@ BYTES_PER_PIXEL = 9.0
 SIDE_BYTES_PER_MB = 80
 BYTES_PER_FRAME = W * H * BYTES_PER_PIXEL + NMB * SIDE_BYTES_PER_MB
 HBM_PEAK_GBS = 8000.0                                    # MI355X_MICROARCH.md (spec)
-# integer search absolute differences per picture (FFS SAD table) and the v_sad_u8 peak:
-# 4 absolute differences per lane-op, 256 CU x 64 lanes/clk x 2.4 GHz
+# integer-search absolute differences per picture (the FFS SAD table)
 AD_PER_FRAME = NMB * (2 * SR + 1) ** 2 * 256
-VALU_SAD_PEAK_TADS = 256 * 64 * 4 * 2.4e9 / 1e12
+# v_sad_u8 peak: measured by tools/sad_peak.hip on MI355X (profiles/r2_sad_peak.json), else the
+# nominal figure 256 CU x 128 lanes/clk (4 SIMD-32) x 2.4 GHz x 4 AD per lane-op
+VALU_SAD_NOMINAL_TADS = 256 * 128 * 4 * 2.4e9 / 1e12
 
 
 def load_module(name, path):
@@ -65,40 +82,71 @@ def load_module(name, path):
     return mod
 
 
-def use_config(k):
-    """switch the module-level workload constants to BASELINE.json config k"""
+def use_config(k, size=None):
+    """switch the module-level workload constants to BASELINE.json config k (size: test override)"""
     global DISP_W, DISP_H, W, H, NMB, BYTES_PER_FRAME, AD_PER_FRAME
     c = CONFIGS[k]
     (DISP_W, DISP_H), (W, H) = c["disp"], c["coded"]
+    if size:
+        DISP_W, DISP_H = size
+        W, H = (DISP_W + 15) // 16 * 16, (DISP_H + 15) // 16 * 16
     NMB = (W // 16) * (H // 16)
     BYTES_PER_FRAME = W * H * BYTES_PER_PIXEL + NMB * SIDE_BYTES_PER_MB
     AD_PER_FRAME = NMB * (2 * SR + 1) ** 2 * 256
     return c
 
 
-def cpu_one_picture(seed, search_mode, t8=0):
-    """Seconds the oracle (JM restated in C, scalar -O2, one thread) takes for one P picture of the
-    configured size on stream `seed` (UnifiedOneForthPix + encode_one_macroblock per MB).  Runs in a child
-    process (bench.py --cpu-worker): no GPU is touched."""
+def sad_peak():
+    """(T AD/s, source) of v_sad_u8 on this chip: profiles/r2_sad_peak.json (tools/sad_peak.hip,
+    measured on MI355X, at 2.4 GHz) or the nominal figure."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r2_sad_peak.json")) as f:
+            d = json.load(f)["ops"]["v_sad_u8"]
+        return d["ad_per_s_at_2p4ghz"] / 1e12, "measured (tools/sad_peak.hip, profiles/r2_sad_peak.json, at 2.4 GHz)"
+    except (OSError, ValueError, KeyError, TypeError):
+        return VALU_SAD_NOMINAL_TADS, "nominal (256 CU x 128 lanes x 2.4 GHz x 4 AD)"
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baseline (the oracle: JM restated in C, scalar -O2, one thread per process)
+# ------------------------------------------------------------------------------------------
+def cpu_one_picture(seed, search_mode, t8=0, dump=None):
+    """Seconds the oracle takes for one P picture of the configured size on stream `seed`
+    (UnifiedOneForthPix + encode_one_macroblock per MB).  Runs in a child process (bench.py
+    --cpu-worker): no GPU is touched.  dump: npz path for the I + P results (the GPU check)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
     import oracle_lib
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
     frames = [jm.synth_frame(DISP_W, DISP_H, seed, i) for i in range(2)]
     o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8)
-    _, rec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
+    ires, irec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
     t0 = time.perf_counter()
-    o.set_reference(*rec)
-    o.encode(*frames[1], jm.JMH_P_SLICE, QP)
+    o.set_reference(*irec)
+    pres, prec = o.encode(*frames[1], jm.JMH_P_SLICE, QP)
     dt = time.perf_counter() - t0
     o.close()
+    if dump:
+        np.savez(dump, ires=ires, iy=irec[0], iu=irec[1], iv=irec[2], pres=pres, py=prec[0], pu=prec[1], pv=prec[2])
     return dt
 
 
-def cpu_workers(n, config, search_mode):
+def cpu_workers(n, config, search_mode, size, dump_dir=None):
     """n concurrent child processes (distinct seeds); their per-picture seconds."""
-    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(k), str(config), str(search_mode)],
-                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True) for k in range(n)]
-    return [float(p.communicate()[0].split()[-1]) for p in procs]
+    procs = []
+    for k in range(n):
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", str(k), str(config), str(search_mode),
+               f"{size[0]}x{size[1]}"]
+        if dump_dir and k == 0:
+            cmd.append(os.path.join(dump_dir, "oracle_seed0.npz"))
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True))
+    out = []
+    for p in procs:
+        s = p.communicate()[0]
+        if p.returncode != 0 or not s.split():
+            raise RuntimeError(f"cpu worker failed (rc {p.returncode})")
+        out.append(float(s.split()[-1]))
+    return out
 
 
 def cpu_model():
@@ -112,13 +160,14 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(config=2, search_mode=0):
+def cpu_baseline(config, search_mode, dump_dir):
     """The CPU path timed on this node's host cores: one process on one core (JM is
     single threaded; the reported baseline), and n processes on distinct streams at once
-    (aggregate, n = min(16, cores available to this process))."""
-    one = cpu_workers(1, config, search_mode)[0]
+    (aggregate, n = min(16, cores available to this process)).  Worker 0 of the one-core run
+    dumps its I + P results for the GPU check."""
+    one = cpu_workers(1, config, search_mode, (DISP_W, DISP_H), dump_dir)[0]
     n = max(1, min(16, len(os.sched_getaffinity(0))))
-    many = cpu_workers(n, config, search_mode)
+    many = cpu_workers(n, config, search_mode, (DISP_W, DISP_H))
     mode = {0: "FFS", -1: "full search", 3: "EPZS"}[search_mode] + (" + 8x8 transform" if CONFIGS[config]["t8"] else "")
     return {"value": round(DISP_W * DISP_H / 1e6 / one, 4), "unit": "MP/s", "cores": 1, "kind": "port",
             "sample": f"one {DISP_W}x{DISP_H} P picture (coded {W}x{H}, {NMB} MBs, {mode} SR=32, QP {QP}) incl. "
@@ -126,6 +175,26 @@ def cpu_baseline(config=2, search_mode=0):
             "all_cores": {"value": round(n * DISP_W * DISP_H / 1e6 / max(many), 4), "unit": "MP/s", "cores": n,
                           "sample": f"{n} processes, one P picture each on distinct streams, concurrently, "
                                     f"{max(many):.1f} s wall"}}
+
+
+def verify_against_oracle(jm, dump, search_mode, t8, device):
+    """Encode the CPU baseline's I + P pictures (stream 0) on the GPU and compare every MB result
+    and the reconstructions with the oracle's (the dump of the cpu_baseline leg)."""
+    import numpy as np
+    d = np.load(dump)
+    frames = [jm.synth_frame(DISP_W, DISP_H, 0, i) for i in range(2)]
+    g = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
+                   pipeline_depth=1)
+    try:
+        ires, irec = g.encode(*frames[0], jm.JMH_I_SLICE, QP)
+        g.set_reference(*irec)
+        pres, prec = g.encode(*frames[1], jm.JMH_P_SLICE, QP)
+    finally:
+        g.close()
+    ok = ires.tobytes() == d["ires"].tobytes() and pres.tobytes() == d["pres"].tobytes()
+    for a, k in zip(irec + prec, ("iy", "iu", "iv", "py", "pu", "pv")):
+        ok = ok and np.array_equal(a, d[k])
+    return bool(ok)
 
 
 def read_pmc_traffic():
@@ -139,47 +208,135 @@ def read_pmc_traffic():
         return None
 
 
+# ------------------------------------------------------------------------------------------
+# the host-buffer path: PCIe-inclusive rate and single-picture latency (reported, not `value`)
+# ------------------------------------------------------------------------------------------
+def pcie_inclusive(jm, enc, frames, pictures):
+    """jmh_frame_push / jmh_frame_pop on host pictures (source H2D, results + recon + deblocked
+    D2H), steady state: `depth` pictures pushed untimed, then `pictures` push + pop pairs timed.
+    Returns (MP/s, single-picture latency ms on an empty pipeline)."""
+    enc.sync()
+    seq = frames[1:]
+    dbk = (0, 0, 0)
+    enc.set_reference_slot(-2)
+    enc.push(*seq[0], jm.JMH_P_SLICE, QP, deblock=dbk)   # latency: one picture, empty pipeline
+    enc.pop()
+    latency_ms = enc.timing().total_ms
+    pending = 0
+    for i in range(enc.depth):
+        enc.set_reference_slot(-2)
+        enc.push(*seq[(1 + i) % len(seq)], jm.JMH_P_SLICE, QP, deblock=dbk)
+        pending += 1
+    t0 = time.perf_counter()
+    for i in range(pictures):
+        enc.pop()
+        enc.set_reference_slot(-2)
+        enc.push(*seq[(1 + enc.depth + i) % len(seq)], jm.JMH_P_SLICE, QP, deblock=dbk)
+    enc.pop()
+    dt = time.perf_counter() - t0
+    pending -= 1
+    for _ in range(pending):
+        enc.pop()
+    return pictures * DISP_W * DISP_H / 1e6 / dt, latency_ms
+
+
+# ------------------------------------------------------------------------------------------
+# launcher: --gpus N without torchrun -> N ranks, one process per GPU
+# ------------------------------------------------------------------------------------------
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n):
+    """Spawn n ranks of this script (before anything touches the GPU) and return the worst exit
+    code.  Rank 0 prints the JSON line."""
+    port = str(free_port())
+    procs = []
+    for k in range(n):
+        env = dict(os.environ, RANK=str(k), LOCAL_RANK=str(k), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
 def main():
-    if len(sys.argv) == 5 and sys.argv[1] == "--cpu-worker":    # child of cpu_baseline()
-        c = use_config(int(sys.argv[3]))
-        print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[4]), c["t8"]), flush=True)
-        return
+    if len(sys.argv) in (6, 7) and sys.argv[1] == "--cpu-worker":    # child of cpu_baseline()
+        w, h = (int(v) for v in sys.argv[5].split("x"))
+        c = use_config(int(sys.argv[3]), (w, h))
+        print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[4]), c["t8"], sys.argv[6] if len(sys.argv) == 7 else None),
+              flush=True)
+        return 0
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--frames", type=int, default=60, help="P pictures of the resident source sequence")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive / latency measurement")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3),
                     help="BASELINE.json config: 2 = 1080p Baseline FFS (the headline), 3 = 2160p High EPZS + 8x8")
     ap.add_argument("--search-mode", type=int, default=None, choices=(0, -1, 3),
                     help="override the config's SearchMode (config 2 variants: -1 full search, 3 EPZS)")
+    # test knobs (tests/test_multistream_gpu.py): a smaller picture, a final read-back picture
+    ap.add_argument("--size", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--dump", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--no-deblock", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
-    cfg = use_config(args.config)
-    search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0 and args.gpus > 1:
+        return launch(args.gpus)
+    world = max(world, 1)
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    size = tuple(int(v) for v in args.size.split("x")) if args.size else None
+    cfg = use_config(args.config, size)
+    search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
     dist = None
     if world > 1:
         import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")
 
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
     streams = load_module("jmh_streams", os.path.join(PKG, "streams.py"))
-    frames = [jm.synth_frame(DISP_W, DISP_H, rank, i) for i in range(3)]
-    enc = jm.Encoder(W, H, device=local, search_range=SR, search_mode=search_mode, slots=3, kernel_timing=True,
-                     transform_8x8_mode=cfg["t8"])
-    stream = streams.PStream(enc, frames, QP)
+    ndev = jm.load().jmh_device_count()
+    if ndev <= 0:
+        raise SystemExit("bench.py: no HIP device")
+    device = local % ndev
+    frames = [jm.synth_frame(DISP_W, DISP_H, rank, i) for i in range(args.frames + 1)]
+    enc = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, slots=len(frames),
+                     kernel_timing=True, transform_8x8_mode=cfg["t8"])
+    stream = streams.PStream(enc, frames, QP, deblock=None if args.no_deblock else (0, 0, 0))
     dt = streams.timed_run(stream, args.steps, args.warmup, dist, on_start=enc.timing)   # on_start resets the event sums
     tm = enc.timing()                                     # event sums of the timed steps only
 
+    host = None
+    if not args.no_host_path and size is None and not args.no_deblock:
+        host = pcie_inclusive(jm, enc, frames, min(args.steps, 3 * enc.depth))
+    if args.dump:                                         # test: one read-back picture after the chain
+        import numpy as np
+        enc.set_reference_slot(stream.ref_slot)
+        res, rec = enc.encode(*frames[1], jm.JMH_P_SLICE, QP, deblock=stream.deblock)
+        np.savez(os.path.join(args.dump, f"rank{rank}.npz"), res=res, y=rec[0], u=rec[1], v=rec[2],
+                 slots=np.array(stream.slots_used), device=device, warmup=stream.warmup_steps)
+    mine = {"rank": rank, "device": device, "dt": dt, "pictures_completed": tm.pictures_done}
+    everyone = [mine]
+    if dist is not None:
+        everyone = [None] * world
+        dist.all_gather_object(everyone, mine)
     if rank != 0:
         if dist is not None:
             dist.barrier()
+        enc.sync()                                        # complete the pictures still in flight
         enc.close()
-        return
+        return 0
+
     value = world * args.steps * DISP_W * DISP_H / 1e6 / dt
     pictures = max(1, tm.pictures)
     an_launch_ms = tm.analyse_ms / max(1, tm.analyse_launches)
@@ -187,9 +344,36 @@ def main():
     mbs_per_launch = tm.tick_mbs / max(1, tm.ticks)      # MBs of all pictures in flight, per tick
     bytes_per_launch = BYTES_PER_FRAME / NMB * mbs_per_launch
     achieved_gbs = bytes_per_launch / (an_launch_ms * 1e-3) / 1e9
+    ad_per_launch = AD_PER_FRAME / NMB * mbs_per_launch
+    achieved_tads = ad_per_launch / (an_launch_ms * 1e-3) / 1e12
+    peak_tads, peak_src = sad_peak()
     mb_ms_pic = tm.mb_ms / pictures
     pmc = read_pmc_traffic() if args.config == 2 and search_mode == 0 else None   # PMC pass is for config 2
     sm_name = {0: "FFS SearchMode=0", -1: "full search SearchMode=-1", 3: "EPZS SearchMode=3"}[search_mode]
+    ffs = search_mode == 0
+    hbm = {
+        "bound": "hbm",
+        "achieved": round(achieved_gbs, 3),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
+        "traffic": round(pmc * mbs_per_launch) if pmc else None,
+        "algorithmic_bytes_per_launch": round(bytes_per_launch),
+    }
+    launch_info = {
+        "kernel": "k_mb_analyse" if ffs else
+                  "k_mb_me_full + k_mb_analyse" + (" + k_mb_intra8" if cfg["t8"] else "") + " (the tick's analysis launches)",
+        "avg_launch_ms": round(an_launch_ms, 5),
+        "launches_per_picture": round(an_per_pic, 2),
+        "mbs_per_launch": round(mbs_per_launch, 1),
+    }
+    if ffs:   # config 2: the FFS SAD table binds -> VALU roofline; HBM beside it
+        roofline = dict(bound="valu", achieved=round(achieved_tads, 4), peak=round(peak_tads, 2),
+                        unit="T abs-diff/s", frac=round(achieved_tads / peak_tads, 5),
+                        traffic=hbm["traffic"], peak_source=peak_src,
+                        algorithmic_ad_per_launch=round(ad_per_launch), **launch_info, hbm=hbm)
+    else:     # EPZS: latency-bound; HBM is the roofline the north star names
+        roofline = dict(hbm, **launch_info)
     out = {
         "metric": cfg["metric"],
         "value": round(value, 3),
@@ -204,46 +388,48 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": cfg["workload"].replace("{sm}", sm_name),
+            "workload": cfg["workload"].replace("{sm}", sm_name).replace("{nf}", str(args.frames)),
             "global_batch": world,
             "parallelism": f"streams{world}",
             "pipeline_depth": enc.depth,
+            "devices": [e["device"] for e in everyone],
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved_gbs, 3),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
-            "traffic": round(pmc * mbs_per_launch) if pmc else None,
-            "kernel": "k_mb_analyse" if search_mode == 0 else
-                      "k_mb_me_full + k_mb_analyse" + (" + k_mb_intra8" if cfg["t8"] else "") + " (the tick's analysis launches)",
-            "algorithmic_bytes_per_launch": round(bytes_per_launch),
-            "avg_launch_ms": round(an_launch_ms, 5),
-            "launches_per_picture": round(an_per_pic, 2),
-            "mbs_per_launch": round(mbs_per_launch, 1),
+        "timed_region": {
+            "warmup_steps_run": stream.warmup_steps,
+            "pictures_completed": [e["pictures_completed"] for e in everyone],
+            "per_rank_s": [round(e["dt"], 5) for e in everyone],
+            "note": "steady state: the pipeline is full at both ends (barrier + wait for the issued launches, "
+                    "pictures in flight are not drained); exactly `steps` pictures complete inside",
         },
-        "valu_roofline": None if search_mode != 0 else {
-            "note": "integer-search absolute differences (v_sad_u8) over the wavefront time",
-            "achieved": round(AD_PER_FRAME / (mb_ms_pic * 1e-3) / 1e12, 4),
-            "peak": round(VALU_SAD_PEAK_TADS, 2),
-            "unit": "T abs-diff/s",
-            "frac": round(AD_PER_FRAME / (mb_ms_pic * 1e-3) / 1e12 / VALU_SAD_PEAK_TADS, 6),
-        },
+        "roofline": roofline,
         # per-launch averages (sampled every 8th diagonal) x launches per picture
         "kernel_ms_per_picture": {"wavefront": round(mb_ms_pic, 4),
                                   "k_mb_analyse": round(an_launch_ms * an_per_pic, 4),
-                                  "k_mb_final": round(tm.final_ms / max(1, tm.final_launches) * an_per_pic, 4),
-                                  "k_interp": round(tm.interp_ms / max(1, tm.interps), 4)},
+                                  "k_mb_final": round(tm.final_ms / max(1, tm.final_launches) * an_per_pic, 4)},
+        "host_path": None if host is None else {
+            "pcie_inclusive_mp_s": round(host[0], 3),
+            "single_picture_latency_ms": round(host[1], 3),
+            "note": "jmh_frame_push/pop with host pictures: source H2D + results/recon/deblocked D2H, "
+                    "steady state; latency = one picture on an empty pipeline (fill + drain)",
+        },
+        "verified": None,
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.config, search_mode)
+        with tempfile.TemporaryDirectory() as tmp:
+            out["cpu_baseline"] = cpu_baseline(args.config, search_mode, tmp)
+            out["verified"] = verify_against_oracle(jm, os.path.join(tmp, "oracle_seed0.npz"), search_mode, cfg["t8"],
+                                                    device)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
+    enc.sync()                                            # complete the pictures still in flight
     enc.close()
+    if out["verified"] is False:
+        print("bench.py: GPU results differ from the oracle", file=sys.stderr)
+        return 3
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -190,14 +190,34 @@ static int alloc_entry(jmh_ctx *c, PicBuf &b) {
     return JMH_OK;
 }
 
-static int alloc_host(jmh_ctx *c, PicBuf &b) {   // pinned readback / staging, on first use
-    if (b.h_res) return JMH_OK;
-#define HALLOC(p, n) do { if (hipHostMalloc((void **)&(p), (n), hipHostMallocDefault) != hipSuccess) return JMH_E_OOM; } while (0)
-    HALLOC(b.h_res, c->nmb * sizeof(jmh_mb_result)); HALLOC(b.h_src, c->fsize);
-    HALLOC(b.h_rec, c->fsize); HALLOC(b.h_dbk, c->fsize);
-#undef HALLOC
+// pinned readback / staging, on first use: all four buffers or none (a partial allocation is
+// released, so a later call retries instead of seeing a half-initialised entry)
+static int alloc_host(jmh_ctx *c, PicBuf &b) {
+    if (b.h_res && b.h_src && b.h_rec && b.h_dbk) return JMH_OK;
+    void **bufs[4] = {(void **)&b.h_res, (void **)&b.h_src, (void **)&b.h_rec, (void **)&b.h_dbk};
+    const size_t sizes[4] = {c->nmb * sizeof(jmh_mb_result), c->fsize, c->fsize, c->fsize};
+    for (int i = 0; i < 4; i++)
+        if (!*bufs[i] && hipHostMalloc(bufs[i], sizes[i], hipHostMallocDefault) != hipSuccess) {
+            *bufs[i] = nullptr;
+            for (int k = 0; k < 4; k++)
+                if (*bufs[k]) { (void)hipHostFree(*bufs[k]); *bufs[k] = nullptr; }
+            return JMH_E_OOM;
+        }
     return JMH_OK;
 }
+
+// device temporaries of the unit seams: freed on every return path
+struct DevTemps {
+    std::vector<void *> p;
+    ~DevTemps() { for (void *q : p) if (q) (void)hipFree(q); }
+    template <class T> hipError_t alloc(T **out, size_t n) {
+        void *q = nullptr;
+        hipError_t e = hipMalloc(&q, n);
+        if (e == hipSuccess) p.push_back(q);
+        *out = (T *)q;
+        return e;
+    }
+};
 
 extern "C" {
 
@@ -324,6 +344,7 @@ static int skip_empty(const jmh_ctx *c, int stage) {
 
 // after a picture's last tick: enqueue its readback, mark the done event
 static int finish_picture(jmh_ctx *c, const Flight &f) {
+    c->timing.pictures_done++;
     if (!f.readback) return JMH_OK;
     PicBuf &b = c->ring[f.entry];
     HCHK(hipMemcpyAsync(b.h_res, b.res, c->nmb * sizeof(jmh_mb_result), hipMemcpyDeviceToHost, c->st));
@@ -672,12 +693,17 @@ int jmh_sync(jmh_ctx *c) {
     return JMH_OK;
 }
 
+int jmh_wait_issued(jmh_ctx *c) {
+    if (!c) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    HCHK(hipStreamSynchronize(c->st));
+    return JMH_OK;
+}
+
 int jmh_get_timing(jmh_ctx *c, jmh_timing *t) {
     if (!c || !t) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
-    int r = drain(c);
-    if (r) return r;
-    HCHK(hipStreamSynchronize(c->st));
+    HCHK(hipStreamSynchronize(c->st));   // the issued launches only: pictures in flight stay
     int npic = 0;
     ring_drain(c->ring_interp, c->timing.interp_ms, c->timing.interps);
     ring_drain(c->ring_mb, c->timing.mb_ms, npic);
@@ -688,6 +714,7 @@ int jmh_get_timing(jmh_ctx *c, jmh_timing *t) {
     *t = c->timing;
     // counters restart (total_ms stays: the last popped picture)
     c->timing.pictures = 0; c->timing.mb_launches = 0; c->timing.ticks = 0; c->timing.tick_mbs = 0;
+    c->timing.pictures_done = 0;
     return JMH_OK;
 }
 
@@ -702,15 +729,15 @@ int jmh_ffs_sad_table(jmh_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t 
     int32_t *d_xy = nullptr, *d_c = nullptr;
     uint16_t *d_out = nullptr;
     size_t on = (size_t)n_mb * 16 * c->npos;
-    HCHK(hipMalloc((void **)&d_xy, n_mb * 8));
-    HCHK(hipMalloc((void **)&d_c, n_mb * 8));
-    HCHK(hipMalloc((void **)&d_out, on * 2));
+    DevTemps tmp;
+    HCHK(tmp.alloc(&d_xy, n_mb * 8));
+    HCHK(tmp.alloc(&d_c, n_mb * 8));
+    HCHK(tmp.alloc(&d_out, on * 2));
     HCHK(hipMemcpyAsync(d_xy, mb_xy, n_mb * 8, hipMemcpyHostToDevice, c->st));
     HCHK(hipMemcpyAsync(d_c, centres, n_mb * 8, hipMemcpyHostToDevice, c->st));
     HCHK(jmh_launch_sad_table(c->d_slots, ref_ptr(c), c->W, c->H, c->sr, n_mb, d_xy, d_c, d_out, c->st));
     HCHK(hipMemcpyAsync(out, d_out, on * 2, hipMemcpyDeviceToHost, c->st));
     HCHK(hipStreamSynchronize(c->st));
-    HCHK(hipFree(d_xy)); HCHK(hipFree(d_c)); HCHK(hipFree(d_out));
     return JMH_OK;
 }
 
@@ -721,9 +748,10 @@ int jmh_tq4x4_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     int16_t *dr, *dl;
     uint8_t *dp, *drec;
     int32_t *dcc, *dnz;
-    HCHK(hipMalloc((void **)&dr, n * 32)); HCHK(hipMalloc((void **)&dl, n * 32));
-    HCHK(hipMalloc((void **)&dp, n * 16)); HCHK(hipMalloc((void **)&drec, n * 16));
-    HCHK(hipMalloc((void **)&dcc, n * 4)); HCHK(hipMalloc((void **)&dnz, n * 4));
+    DevTemps tmp;
+    HCHK(tmp.alloc(&dr, (size_t)n * 32)); HCHK(tmp.alloc(&dl, (size_t)n * 32));
+    HCHK(tmp.alloc(&dp, (size_t)n * 16)); HCHK(tmp.alloc(&drec, (size_t)n * 16));
+    HCHK(tmp.alloc(&dcc, (size_t)n * 4)); HCHK(tmp.alloc(&dnz, (size_t)n * 4));
     HCHK(hipMemcpyAsync(dr, resid, n * 32, hipMemcpyHostToDevice, c->st));
     HCHK(hipMemcpyAsync(dp, pred, n * 16, hipMemcpyHostToDevice, c->st));
     HCHK(jmh_launch_tq4x4(n, dr, dp, qp, intra, dl, drec, dcc, dnz, c->st));
@@ -732,7 +760,6 @@ int jmh_tq4x4_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     HCHK(hipMemcpyAsync(coeff_cost, dcc, n * 4, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(nonzero, dnz, n * 4, hipMemcpyDeviceToHost, c->st));
     HCHK(hipStreamSynchronize(c->st));
-    HCHK(hipFree(dr)); HCHK(hipFree(dl)); HCHK(hipFree(dp)); HCHK(hipFree(drec)); HCHK(hipFree(dcc)); HCHK(hipFree(dnz));
     return JMH_OK;
 }
 
@@ -743,9 +770,10 @@ int jmh_tq8x8_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     int16_t *dr, *dl;
     uint8_t *dp, *drec;
     int32_t *dcc, *dnz;
-    HCHK(hipMalloc((void **)&dr, n * 128)); HCHK(hipMalloc((void **)&dl, n * 128));
-    HCHK(hipMalloc((void **)&dp, n * 64)); HCHK(hipMalloc((void **)&drec, n * 64));
-    HCHK(hipMalloc((void **)&dcc, n * 4)); HCHK(hipMalloc((void **)&dnz, n * 4));
+    DevTemps tmp;
+    HCHK(tmp.alloc(&dr, (size_t)n * 128)); HCHK(tmp.alloc(&dl, (size_t)n * 128));
+    HCHK(tmp.alloc(&dp, (size_t)n * 64)); HCHK(tmp.alloc(&drec, (size_t)n * 64));
+    HCHK(tmp.alloc(&dcc, (size_t)n * 4)); HCHK(tmp.alloc(&dnz, (size_t)n * 4));
     HCHK(hipMemcpyAsync(dr, resid, n * 128, hipMemcpyHostToDevice, c->st));
     HCHK(hipMemcpyAsync(dp, pred, n * 64, hipMemcpyHostToDevice, c->st));
     HCHK(jmh_launch_tq8x8(n, dr, dp, qp, intra, dl, drec, dcc, dnz, c->st));
@@ -754,7 +782,6 @@ int jmh_tq8x8_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     HCHK(hipMemcpyAsync(coeff_cost, dcc, n * 4, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(nonzero, dnz, n * 4, hipMemcpyDeviceToHost, c->st));
     HCHK(hipStreamSynchronize(c->st));
-    HCHK(hipFree(dr)); HCHK(hipFree(dl)); HCHK(hipFree(dp)); HCHK(hipFree(drec)); HCHK(hipFree(dcc)); HCHK(hipFree(dnz));
     return JMH_OK;
 }
 

@@ -17,7 +17,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 5
+JMH_ABI_VERSION = 6
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -54,7 +54,8 @@ class JmhTiming(ctypes.Structure):
                 ("pictures", ctypes.c_int32), ("interps", ctypes.c_int32),
                 ("analyse_ms", ctypes.c_float), ("analyse_launches", ctypes.c_int32),
                 ("final_ms", ctypes.c_float), ("final_launches", ctypes.c_int32),
-                ("ticks", ctypes.c_int32), ("tick_mbs", ctypes.c_int32)]
+                ("ticks", ctypes.c_int32), ("tick_mbs", ctypes.c_int32),
+                ("pictures_done", ctypes.c_int32)]
 
 
 # jmh_mb_result, field for field (include/jmhip.h)
@@ -86,6 +87,7 @@ _SIGS = {
     "jmh_set_reference_slot": (_I, [_P, _I]),
     "jmh_encode_slot": (_I, [_P, _I, ctypes.POINTER(JmhFrameParams)]),
     "jmh_sync": (_I, [_P]),
+    "jmh_wait_issued": (_I, [_P]),
     "jmh_get_timing": (_I, [_P, ctypes.POINTER(JmhTiming)]),
     "jmh_ffs_sad_table": (_I, [_P, _I, _P, _P, _P]),
     "jmh_tq4x4_batch": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
@@ -251,9 +253,15 @@ class Encoder:
         _check(self.lib.jmh_encode_slot(self.ctx, slot, ctypes.byref(fp)), "jmh_encode_slot")
 
     def sync(self):
+        """Drain: every picture in flight runs to completion (jmh_sync)."""
         _check(self.lib.jmh_sync(self.ctx), "jmh_sync")
 
+    def wait_issued(self):
+        """Wait for the launches issued so far; pictures in flight stay in flight (jmh_wait_issued)."""
+        _check(self.lib.jmh_wait_issued(self.ctx), "jmh_wait_issued")
+
     def timing(self):
+        """Event sums since the previous call (waits for the issued launches, does not drain)."""
         t = JmhTiming()
         _check(self.lib.jmh_get_timing(self.ctx, ctypes.byref(t)), "jmh_get_timing")
         return t

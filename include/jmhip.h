@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 5
+#define JMH_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define JMH_OK                 0
@@ -73,7 +73,8 @@ extern "C" {
 typedef struct jmh_config {
     int32_t width;                  /* coded luma width  (multiple of 16)                        */
     int32_t height;                 /* coded luma height (multiple of 16)                        */
-    int32_t search_range;           /* SearchRange (full-pel), 1..64                              */
+    int32_t search_range;           /* SearchRange (full-pel), 1..32 (LDS-resident window; larger
+                                       values return JMH_E_UNSUPPORTED_CFG)                       */
     int32_t search_mode;            /* 0 = fast full search (FFS, JM _FAST_FULL_ME_), -1 = full   */
     int32_t use_hadamard;           /* UseHadamard                                                */
     int32_t restrict_search_range;  /* RestrictSearchRange 0 / 1 / 2                              */
@@ -134,7 +135,8 @@ typedef struct jmh_mb_result {
 } jmh_mb_result;
 
 /* ---- kernel timing (HIP events on the context stream), summed since the previous
- *      jmh_get_timing call (which resets the sums) ------------------------------------------ */
+ *      jmh_get_timing call (which resets the sums).  jmh_get_timing waits for the launches
+ *      issued so far and does NOT drain pictures in flight (the pipeline stays primed).  ---- */
 typedef struct jmh_timing {
     float interp_ms;           /* sum of quarter-pel interpolations (jmh_set_reference*)       */
     float mb_ms;               /* sum of whole macroblock wavefronts (first to last dispatch)  */
@@ -149,6 +151,8 @@ typedef struct jmh_timing {
     int32_t ticks;             /* wavefront ticks (one k_mb_analyse + one k_mb_final each; a tick
                                   runs one diagonal of every picture in flight)                   */
     int32_t tick_mbs;          /* macroblocks processed by those ticks                          */
+    int32_t pictures_done;     /* pictures whose last tick was issued (completed once the
+                                  issued work has drained: jmh_wait_issued)                      */
 } jmh_timing;
 
 typedef struct jmh_ctx jmh_ctx;
@@ -196,7 +200,10 @@ int  jmh_load_frame(jmh_ctx *ctx, int slot, const uint8_t *y, const uint8_t *u, 
 int  jmh_set_reference_slot(jmh_ctx *ctx, int slot);   /* slot -1: the last picture's recon,    */
                                                          /* -2: its device deblocking (deblock=1) */
 int  jmh_encode_slot(jmh_ctx *ctx, int slot, const jmh_frame_params *fp); /* pipelined, no D2H */
-int  jmh_sync(jmh_ctx *ctx);
+int  jmh_sync(jmh_ctx *ctx);           /* drain: every picture in flight runs to completion  */
+/* wait for the launches issued so far WITHOUT issuing more: pictures in flight stay in flight
+ * (partially encoded), so a timed region can start and end with the pipeline full            */
+int  jmh_wait_issued(jmh_ctx *ctx);
 int  jmh_get_timing(jmh_ctx *ctx, jmh_timing *t);
 
 /* ---- unit seams (minimum slice; tests call these directly) ------------------------------

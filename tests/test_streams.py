@@ -30,7 +30,9 @@ def load_streams():
 
 
 class OracleSlots:
-    """Slot interface of jmhip.Encoder (load_frame / encode_slot / set_reference_slot / sync)."""
+    """Slot interface of jmhip.Encoder (load_frame / encode_slot / set_reference_slot / wait_issued /
+    sync / depth): one picture at a time (depth 1), so the warmup is exactly `warmup` steps."""
+    depth = 1
 
     def __init__(self):
         self.o = oracle_lib.OracleEncoder(W, H, search_range=SR)
@@ -48,6 +50,9 @@ class OracleSlots:
         self.o.set_reference(*self.rec)
 
     def sync(self):
+        pass
+
+    def wait_issued(self):
         pass
 
 
@@ -105,5 +110,24 @@ def test_single_process_harness_counts_steps():
     # one IDR picture + warmup + timed P pictures; the IDR picture is all intra (I4MB 9 /
     # I16MB 10), the P pictures reference the previous reconstruction and use inter types
     assert len(enc.results) == 1 + 2 + 3
+    assert enc.depth == 1
     assert np.all(enc.results[0]["mb_type"] >= 9)
     assert all(np.any(r["mb_type"] < 9) for r in enc.results[1:])
+
+
+class DeepStandIn(OracleSlots):
+    """A stand-in that reports a pipeline depth: the warmup must cover the fill."""
+    depth = 4
+
+
+def test_warmup_covers_pipeline_depth():
+    ensure_built()
+    jm, streams = load_jmhip(), load_streams()
+    frames = [jm.synth_frame(W, H, 6, i) for i in range(4)]
+    enc = DeepStandIn()
+    st = streams.PStream(enc, frames, QP, deblock=None)
+    streams.timed_run(st, steps=2, warmup=1)
+    assert st.warmup_steps == 4
+    assert len(enc.results) == 1 + 4 + 2
+    # the P pictures cycle over the resident sequence (slots 1..3)
+    assert st.slots_used == [1, 2, 3, 1, 2, 3]

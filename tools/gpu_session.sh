@@ -1,19 +1,57 @@
 #!/bin/bash
-# One GPU session: parity suite (incl. 1080p), bench (with CPU baseline), rocprofv3 kernel trace.
-#   bash tools/gpu_session.sh TAG [pytest-args...]
-# Outputs: gpurun_out/TAG_pytest.log, TAG_bench.log, prof_TAG/ (kernel stats csv)
-TAG=${1:-run}; shift
+# One GPU session on the gpurun box, as a list of named steps (each under its own time limit;
+# the first failing step ends the session):
+#   bash tools/gpu_session.sh TAG step [step ...]
+# steps:
+#   build   make the product + oracle in-tree (normally done here on the CPU beforehand)
+#   peak    tools/sad_peak_bin                       -> gpurun_out/TAG_sad_peak.json
+#   tests   pytest -m gpu (all)                      -> gpurun_out/TAG_pytest.log
+#   fast    pytest -m "gpu and not slow"             -> gpurun_out/TAG_pytest.log
+#   smoke   __graft_entry__.smoke()                  -> gpurun_out/TAG_smoke.log
+#   bench   bench.py (defaults, with CPU baseline)   -> gpurun_out/TAG_bench.json
+#   bench20 bench.py --steps 20 --warmup 5 (the driver's invocation, no CPU baseline)
+#   c3      bench.py --config 3 (with CPU baseline)  -> gpurun_out/TAG_c3_bench.json
+#   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
+#   profc3  the same for config 3
+#   pmc     tools/pmc_traffic.sh (HBM bytes + SQ counters, separate passes)
+TAG=${1:?tag}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -x -q -m gpu -p no:cacheprovider "$@" > gpurun_out/${TAG}_pytest.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -25 gpurun_out/${TAG}_pytest.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/${TAG}_bench.log
-[ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}" -o ${TAG} --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1
-rc=$?; echo "prof rc=$rc"
-find gpurun_out/prof_${TAG} -name "*kernel_stats*" -exec cat {} \;
-exit $rc
+run() {   # name limit cmd...
+    local name=$1 lim=$2; shift 2
+    echo "== $name: $*"
+    timeout -k 10 "$lim" "$@"
+    local rc=$?
+    echo "== $name rc=$rc"
+    return $rc
+}
+for s in "$@"; do
+  case $s in
+    build)  run build 600 make -s -j16 all || exit $? ;;
+    peak)   run peak 120 tools/sad_peak_bin > gpurun_out/${TAG}_sad_peak.json || exit $?
+            cat gpurun_out/${TAG}_sad_peak.json ;;
+    tests)  run tests 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread \
+                > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc ;;
+    fast)   run fast 600 python -u -m pytest tests -x -v -m "gpu and not slow" -p no:cacheprovider --timeout 120 \
+                --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_pytest.log
+            [ $rc -eq 0 ] || exit $rc ;;
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit $?
+            cat gpurun_out/${TAG}_smoke.log ;;
+    bench)  run bench 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
+            cat gpurun_out/${TAG}_bench.json ;;
+    bench20) run bench20 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_bench20.json || exit $?
+            cat gpurun_out/${TAG}_bench20.json ;;
+    c3)     run c3 900 python bench.py --config 3 > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3_bench.err || exit $?
+            cat gpurun_out/${TAG}_c3_bench.json ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}" -o ${TAG} --output-format csv -- \
+                python3 "$R/bench.py" --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
+            find gpurun_out/prof_${TAG} -name "*kernel_stats*" -exec cat {} \; ;;
+    profc3) run profc3 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c3" -o ${TAG}_c3 --output-format csv -- \
+                python3 "$R/bench.py" --config 3 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc3.log 2>&1 || exit $?
+            find gpurun_out/prof_${TAG}_c3 -name "*kernel_stats*" -exec cat {} \; ;;
+    pmc)    run pmc 900 bash tools/pmc_traffic.sh "$TAG" || exit $? ;;
+    *)      echo "unknown step $s"; exit 2 ;;
+  esac
+done

@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
-steps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 30       # P pictures encoded in total (warmup + timed)
 root = os.path.join(os.environ.get("GRAFT_REPO_ROOT", os.getcwd()), "gpurun_out")
 NMB = 120 * 68
 
