@@ -29,6 +29,8 @@ hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, i
                                 const int32_t *centres, uint16_t *out, hipStream_t st);
 hipError_t jmh_launch_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st);
+hipError_t jmh_launch_block_search(int n, const jmh_block_search *reqs, jmh_block_result *out, const uint8_t *cur, const uint8_t *ref, int W,
+                                   int H, int had, hipStream_t st);
 hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st);
 
@@ -113,6 +115,7 @@ struct jmh_ctx {
     int W, H, Wc, Hc, mbw, mbh, sr, side, npos, qstride, qplane, nd;
     size_t fsize, n4, nmb;               // bytes of one 4:2:0 picture (Y then U then V)
     uint8_t *d_ref, *d_qpel, *d_slots;   // explicit reference (set_reference), a1 seam, slots
+    uint8_t *d_scur, *d_sref;            // luma pictures of the per-block searches (jmh_search_pictures)
     int nslots;
     int depth, nring;
     std::vector<PicBuf> ring;
@@ -226,7 +229,7 @@ void jmh_destroy(jmh_ctx *c) {
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     for (PicBuf &b : c->ring) free_entry(b);
-    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof};
+    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     ring_free(c->ring_interp);
@@ -781,6 +784,47 @@ int jmh_tq8x8_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     HCHK(hipMemcpyAsync(recon, drec, n * 64, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(coeff_cost, dcc, n * 4, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(nonzero, dnz, n * 4, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    return JMH_OK;
+}
+
+int jmh_search_pictures(jmh_ctx *c, const uint8_t *cur_y, const uint8_t *ref_y, int sy) {
+    if (!c || !cur_y || !ref_y || sy < c->W) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    const size_t ls = (size_t)c->W * c->H;
+    if (!c->d_scur) {
+        if (hipMalloc((void **)&c->d_scur, ls) != hipSuccess) return JMH_E_OOM;
+        if (hipMalloc((void **)&c->d_sref, ls) != hipSuccess) { (void)hipFree(c->d_scur); c->d_scur = nullptr; return JMH_E_OOM; }
+    }
+    HCHK(hipStreamSynchronize(c->st));   // an earlier search may still read the buffers
+    HCHK(hipMemcpy2DAsync(c->d_scur, c->W, cur_y, sy, c->W, c->H, hipMemcpyHostToDevice, c->st));
+    HCHK(hipMemcpy2DAsync(c->d_sref, c->W, ref_y, sy, c->W, c->H, hipMemcpyHostToDevice, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    return JMH_OK;
+}
+
+int jmh_block_motion_search(jmh_ctx *c, int n, const jmh_block_search *req, jmh_block_result *res) {
+    if (!c || n <= 0 || !req || !res) return JMH_E_INVALID_ARG;
+    if (!c->d_scur) return JMH_E_STATE;
+    for (int i = 0; i < n; i++) {   // the kernel's block and window assumptions, checked on the host
+        const jmh_block_search &q = req[i];
+        if (q.blocktype < 1 || q.blocktype > 7 || q.mb_x < 0 || q.mb_x >= c->mbw || q.mb_y < 0 || q.mb_y >= c->mbh) return JMH_E_INVALID_ARG;
+        static const int bw4[8] = {4, 4, 4, 2, 2, 2, 1, 1}, bh4[8] = {4, 4, 2, 4, 2, 1, 2, 1};
+        if (q.block_x < 0 || q.block_y < 0 || q.block_x + bw4[q.blocktype] > 4 || q.block_y + bh4[q.blocktype] > 4) return JMH_E_INVALID_ARG;
+        if (q.search_range < 0 || q.search_range > c->sr) return JMH_E_INVALID_ARG;
+        if (q.lambda_factor < 0 || q.lambda_factor > (1 << 24)) return JMH_E_INVALID_ARG;
+        if (q.search_mode != 0 && q.search_mode != -1) return JMH_E_UNSUPPORTED_CFG;
+        if (abs(q.centre[0]) > 2048 || abs(q.centre[1]) > 2048 || abs(q.pred_mv[0]) > 8192 || abs(q.pred_mv[1]) > 8192) return JMH_E_INVALID_ARG;
+    }
+    HCHK(hipSetDevice(c->dev));
+    DevTemps tmp;
+    jmh_block_search *d_req;
+    jmh_block_result *d_res;
+    HCHK(tmp.alloc(&d_req, (size_t)n * sizeof(jmh_block_search)));
+    HCHK(tmp.alloc(&d_res, (size_t)n * sizeof(jmh_block_result)));
+    HCHK(hipMemcpyAsync(d_req, req, (size_t)n * sizeof(jmh_block_search), hipMemcpyHostToDevice, c->st));
+    HCHK(jmh_launch_block_search(n, d_req, d_res, c->d_scur, c->d_sref, c->W, c->H, c->cfg.use_hadamard, c->st));
+    HCHK(hipMemcpyAsync(res, d_res, (size_t)n * sizeof(jmh_block_result), hipMemcpyDeviceToHost, c->st));
     HCHK(hipStreamSynchronize(c->st));
     return JMH_OK;
 }

@@ -401,7 +401,18 @@ static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r,
     return 0;
 }
 
-int jm_write_slice(jm_bits *b, const jm_seq *s, const jm_slice *sl, const jmh_mb_result *const *res) {
+/* the slice writer, one macroblock at a time (JM 8.6 slice.c › encode_one_slice calls
+ * macroblock.c › write_one_macroblock after encode_one_macroblock for every MB [J]) */
+struct jm_slice_writer {
+    jm_bits *b;
+    wctx w;
+    int skip_run, slice_p;
+    int open;                  /* header written and buffers allocated */
+};
+
+jm_slice_writer *jm_slice_begin(jm_bits *b, const jm_seq *s, const jm_slice *sl) {
+    jm_slice_writer *sw = calloc(1, sizeof(*sw));
+    if (!sw) return NULL;
     /* slice_header (7.3.3) */
     jm_put_ue(b, 0);                                  /* first_mb_in_slice */
     jm_put_ue(b, sl->slice_type);                     /* 0 = P, 2 = I            */
@@ -423,35 +434,55 @@ int jm_write_slice(jm_bits *b, const jm_seq *s, const jm_slice *sl, const jmh_mb
     }
     /* slice_data (7.3.4) */
     int nmb = s->mbw * s->mbh, W4 = s->mbw * 4, H4 = s->mbh * 4;
-    wctx w;
-    w.s = s;
-    w.mv = calloc((size_t)W4 * H4 * 2, sizeof(int16_t));
-    w.ref = malloc((size_t)W4 * H4);
-    w.ipm = malloc((size_t)W4 * H4);
-    w.written = calloc(nmb, 1);
-    w.tc = calloc((size_t)nmb * 24, 1);
-    memset(w.ref, -1, (size_t)W4 * H4);
-    memset(w.ipm, -1, (size_t)W4 * H4);
-    int skip_run = 0, slice_p = sl->slice_type == JMH_P_SLICE;
-    for (int a = 0; a < nmb; a++) {
-        int mx = a % s->mbw, my = a / s->mbw;
-        const jmh_mb_result *r = res[a];
-        if (slice_p && r->mb_type == JMH_PSKIP) {
-            for (int k = 0; k < 16; k++) {
-                int i = (my * 4 + (k >> 2)) * W4 + mx * 4 + (k & 3);
-                w.mv[2 * i] = r->mv[k][0]; w.mv[2 * i + 1] = r->mv[k][1];
-                w.ref[i] = 0; w.ipm[i] = -1;
-            }
-            w.written[a] = 1;
-            memset(w.tc + (size_t)a * 24, 0, 24);
-            skip_run++;
-            continue;
+    wctx *w = &sw->w;
+    sw->b = b;
+    w->s = s;
+    w->mv = calloc((size_t)W4 * H4 * 2, sizeof(int16_t));
+    w->ref = malloc((size_t)W4 * H4);
+    w->ipm = malloc((size_t)W4 * H4);
+    w->written = calloc(nmb, 1);
+    w->tc = calloc((size_t)nmb * 24, 1);
+    if (!w->mv || !w->ref || !w->ipm || !w->written || !w->tc) { jm_slice_end(sw); return NULL; }
+    memset(w->ref, -1, (size_t)W4 * H4);
+    memset(w->ipm, -1, (size_t)W4 * H4);
+    sw->slice_p = sl->slice_type == JMH_P_SLICE;
+    sw->open = 1;
+    return sw;
+}
+
+void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
+    wctx *w = &sw->w;
+    const jm_seq *s = w->s;
+    int mx = a % s->mbw, my = a / s->mbw, W4 = s->mbw * 4;
+    if (sw->slice_p && r->mb_type == JMH_PSKIP) {
+        for (int k = 0; k < 16; k++) {
+            int i = (my * 4 + (k >> 2)) * W4 + mx * 4 + (k & 3);
+            w->mv[2 * i] = r->mv[k][0]; w->mv[2 * i + 1] = r->mv[k][1];
+            w->ref[i] = 0; w->ipm[i] = -1;
         }
-        if (slice_p) { jm_put_ue(b, skip_run); skip_run = 0; }
-        write_mb(b, &w, mx, my, r, slice_p);
+        w->written[a] = 1;
+        memset(w->tc + (size_t)a * 24, 0, 24);
+        sw->skip_run++;
+        return;
     }
-    if (slice_p && skip_run) jm_put_ue(b, skip_run);
-    jm_trailing_bits(b);
-    free(w.mv); free(w.ref); free(w.ipm); free(w.written); free(w.tc);
+    if (sw->slice_p) { jm_put_ue(sw->b, sw->skip_run); sw->skip_run = 0; }
+    write_mb(sw->b, w, mx, my, r, sw->slice_p);
+}
+
+void jm_slice_end(jm_slice_writer *sw) {
+    if (!sw) return;
+    if (sw->open) {   /* close the slice data */
+        if (sw->slice_p && sw->skip_run) jm_put_ue(sw->b, sw->skip_run);
+        jm_trailing_bits(sw->b);
+    }
+    free(sw->w.mv); free(sw->w.ref); free(sw->w.ipm); free(sw->w.written); free(sw->w.tc);
+    free(sw);
+}
+
+int jm_write_slice(jm_bits *b, const jm_seq *s, const jm_slice *sl, const jmh_mb_result *const *res) {
+    jm_slice_writer *sw = jm_slice_begin(b, s, sl);
+    if (!sw) return JMH_E_OOM;
+    for (int a = 0; a < s->mbw * s->mbh; a++) jm_slice_write_mb(sw, a, res[a]);
+    jm_slice_end(sw);
     return 0;
 }

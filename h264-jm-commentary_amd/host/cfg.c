@@ -60,6 +60,7 @@ static const map_entry Map[] = {
     {"FrameRate", 0, OFF(frame_rate), 1, 1000},
     {"HIPDevice", 0, OFF(hip_device), 0, 63},
     {"PipelineDepth", 0, OFF(pipeline_depth), 0, 20},
+    {"JMCallSurface", 0, OFF(jm_call_surface), 0, 1},
     {NULL, 0, 0, 0, 0}};
 #undef OFF
 

@@ -36,6 +36,24 @@ static double psnr(const uint8_t *a, int sa, const uint8_t *b, int sb, int w, in
     return 10.0 * log10(255.0 * 255.0 * w * h / se);
 }
 
+/* slice.c › encode_one_slice [J]: the macroblock loop of one picture (one slice) through the JM
+ * 8.6 call surface (host/jm86.c): start_macroblock, encode_one_macroblock, write_one_macroblock */
+static int encode_one_slice(jm86_img *im, const jm_seq *s, const jm_slice *sl, const jmh_frame_params *fp, const jm_pic *cur,
+                            const jm_pic *ref, jm_bits *rbsp) {
+    jm_slice_writer *w = jm_slice_begin(rbsp, s, sl);
+    if (!w) return JMH_E_OOM;
+    int r = jm86_start_picture(im, fp, cur, ref, w);
+    if (r) { jm_slice_end(w); return r; }
+    for (int a = 0; a < s->mbw * s->mbh; a++) {
+        img->current_mb_nr = a;
+        start_macroblock();
+        encode_one_macroblock();
+        write_one_macroblock();
+    }
+    jm_slice_end(w);
+    return JMH_OK;
+}
+
 int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *log) {
     memset(st, 0, sizeof(*st));
     jmh_config cfg;
@@ -75,6 +93,8 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     if (alloc_fail) return JMH_E_OOM;
     int nmb = s.mbw * s.mbh;
     const jmh_mb_result **res = (const jmh_mb_result **)malloc(sizeof(*res) * nmb);
+    jm86_img im;
+    if (!res || jm86_init(&im, inp, be, W, H)) return JMH_E_OOM;
     jm_bits out, rbsp;
     jm_bits_init(&out); jm_bits_init(&rbsp);
     jm_write_sps(&rbsp, &s); jm_write_nal(&out, 3, 7, &rbsp); jm_bits_free(&rbsp);
@@ -101,7 +121,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         sl.idr = p_->f == 0; sl.slice_type = p_->fp.slice_type; sl.frame_num = p_->frame_num;      \
         sl.poc_lsb = 2 * p_->f; sl.idr_pic_id = 0; sl.qp = p_->fp.qp;                              \
         jm_bits_init(&rbsp);                                                                       \
-        jm_write_slice(&rbsp, &s, &sl, res);                                                       \
+        if (encode_one_slice(&im, &s, &sl, &p_->fp, &p_->cur, &rec, &rbsp)) { st_ret = JMH_E_OOM; break; } \
         jm_write_nal(&out, sl.idr ? 3 : 2, sl.idr ? 5 : 1, &rbsp);                                 \
         jm_bits_free(&rbsp);                                                                       \
         double t2 = now_ms();                                                                      \
@@ -183,6 +203,15 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     }
     #undef EMIT
     st->total_ms = now_ms() - t_start;
+    st->surface_checked = im.surface_checked;
+    st->surface_searches = im.surface_searches;
+    st->surface_mismatches = im.surface_mismatches;
+    if (log && inp->jm_call_surface)
+        fprintf(log, " JM call surface: %d P macroblocks through PartitionMotionSearch / BlockMotionSearch (%d backend "
+                     "searches), %d inconsistent with the wavefront decision\n",
+                im.surface_checked, im.surface_searches, im.surface_mismatches);
+    if (!st_ret && im.surface_mismatches) st_ret = JMH_E_STATE;
+    jm86_free(&im);
     if (st->frames) { st->psnr_y /= st->frames; st->psnr_u /= st->frames; st->psnr_v /= st->frames; }
     if (log && st->frames)
         fprintf(log, " Total encoding time for the seq.  : %.3f sec\n Total ME+TQ time (backend)        : %.3f sec\n"

@@ -48,6 +48,10 @@ typedef struct jm_input {
     int  frame_rate;           /* FrameRate (report only)                                     */
     int  hip_device;           /* (this build) HIP device index                               */
     int  pipeline_depth;       /* (this build) pictures in flight on the device (0 = auto)   */
+    int  jm_call_surface;      /* (this build) 1: every P macroblock also runs JM 8.6's inter
+                                  searches through PartitionMotionSearch / BlockMotionSearch
+                                  (the per-block device seam), checked against the wavefront
+                                  decision (host/jm86.c)                                      */
     int  verbose;
 } jm_input;
 
@@ -115,6 +119,11 @@ typedef struct jm_slice {
 /* slice header + CAVLC slice data for a whole picture (one slice); results in raster order */
 int  jm_write_slice(jm_bits *rbsp, const jm_seq *s, const jm_slice *sl,
                     const jmh_mb_result *const *res);
+/* the same, one macroblock at a time (write_one_macroblock), macroblocks in raster order */
+typedef struct jm_slice_writer jm_slice_writer;
+jm_slice_writer *jm_slice_begin(jm_bits *rbsp, const jm_seq *s, const jm_slice *sl);
+void jm_slice_write_mb(jm_slice_writer *w, int mb_addr, const jmh_mb_result *r);
+void jm_slice_end(jm_slice_writer *w);
 
 /* ---- deblocking (H.264 8.7), in place on the reconstructed picture ---------------------- */
 void jm_deblock_picture(jm_pic *p, const jm_seq *s, const jmh_mb_result *const *res, int qp);
@@ -138,6 +147,12 @@ typedef struct jm_backend {
     int (*push)(void *ctx, const jm_pic *cur, const jmh_frame_params *fp);
     int (*pop)(void *ctx);
     int depth;
+    /* optional per-call seams of the JM 8.6 call surface (host/jm86.c): BlockMotionSearch on
+       the luma pictures given to search_pictures, dct_luma on explicit residual blocks */
+    int (*search_pictures)(void *ctx, const jm_pic *cur, const jm_pic *ref);
+    int (*block_search)(void *ctx, int n, const jmh_block_search *req, jmh_block_result *res);
+    int (*tq4x4)(void *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,
+                 int16_t *levels, uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero);
 } jm_backend;
 
 typedef struct jm_stats {
@@ -147,7 +162,62 @@ typedef struct jm_stats {
     double entropy_ms, deblock_ms;
     long bits;
     double psnr_y, psnr_u, psnr_v;   /* averages                                              */
+    int surface_checked, surface_searches, surface_mismatches;   /* JMCallSurface (jm86.c)      */
 } jm_stats;
+
+/* ---- the JM 8.6 call surface (host/jm86.c) ------------------------------------------------
+ * JM 8.6 lencod keeps its state in globals (global.h: img, input, enc_picture) and calls, per
+ * macroblock of a slice, start_macroblock → encode_one_macroblock → write_one_macroblock
+ * (slice.c › encode_one_slice); encode_one_macroblock (rdopt.c) calls PartitionMotionSearch →
+ * BlockMotionSearch (mv-search.c) and, through the residual coding, dct_luma (block.c) [J].
+ * Those functions exist here with JM 8.6 signatures over the subset of that state the hot path
+ * reads and writes (jm86_img):
+ *   encode_one_macroblock()  the decision of macroblock img->current_mb_nr: the backend's result
+ *                            (the device computed the whole picture's encode_one_macroblock
+ *                            calls in one wavefront); with JMCallSurface = 1 a P macroblock
+ *                            also runs JM's RDO-off inter searches through
+ *                            PartitionMotionSearch / BlockMotionSearch (one device search per
+ *                            call) and checks the decision's inter mode, cost and MVs against
+ *                            them (jm86_img.surface_mismatches)
+ *   PartitionMotionSearch / BlockMotionSearch  one device search per block (jmh_block_motion_
+ *                            search), MVP from enc_picture's MVs (SetMotionVectorPredictor)
+ *   dct_luma                 the 4x4 TQ + reconstruction of img->m7 / img->mpr (jmh_tq4x4_batch)
+ */
+typedef struct jm86_img {
+    int current_mb_nr, mb_x, mb_y, pix_x, pix_y;
+    int width, height, mbw, mbh;
+    int type;                         /* slice type of the picture (JMH_P_SLICE / JMH_I_SLICE) */
+    int qp, lambda_mode, lambda_motion;
+    jmh_mb_result *mb_data;           /* img->mb_data (+ cofAC / cofDC / mv) per macroblock     */
+    int16_t all_mv[8][16][2];         /* img->all_mv[.][.][LIST_0][ref 0][blocktype] (this MB)  */
+    int motion_cost[8][4];            /* motion_cost[blocktype][LIST_0][ref 0][block]           */
+    int search_centre[2];             /* SetupFastFullPelSearch's window centre (this MB)      */
+    int setup_done;
+    int m7[16][16];                   /* img->m7: residual of the block dct_luma codes          */
+    uint8_t mpr[16][16];              /* img->mpr: its prediction                               */
+    int16_t *enc_mv;                  /* enc_picture->mv[LIST_0], per 4x4 of the picture [2]    */
+    int8_t *enc_ref;                  /*   and ->ref_idx (-1: intra / not coded yet)            */
+    uint8_t *enc_imgY;                /* enc_picture->imgY (dct_luma's reconstruction)          */
+    int surface_searches;             /* BlockMotionSearch calls made (statistics)              */
+    int surface_checked, surface_mismatches;   /* P MBs checked / found inconsistent            */
+    const jm_input *input;
+    jm_backend *be;
+    jm_slice_writer *writer;
+} jm86_img;
+extern jm86_img *img;
+
+int  jm86_init(jm86_img *im, const jm_input *inp, jm_backend *be, int width, int height);
+void jm86_free(jm86_img *im);
+/* start a picture: its slice type, QP, lambdas; with the call surface on, the luma pictures
+   of the per-block searches (cur, and ref for a P picture) */
+int  jm86_start_picture(jm86_img *im, const jmh_frame_params *fp, const jm_pic *cur, const jm_pic *ref,
+                        jm_slice_writer *writer);
+void start_macroblock(void);
+void encode_one_macroblock(void);
+void write_one_macroblock(void);
+int  BlockMotionSearch(int ref, int list, int mb_x, int mb_y, int blocktype, int search_range, double lambda);
+void PartitionMotionSearch(int blocktype, int block8x8, double lambda);
+int  dct_luma(int block_x, int block_y, int *coeff_cost, int old_intra_mode);
 
 void jm_fill_config(const jm_input *inp, jmh_config *cfg);
 int  jm_lambda_rdo_off(int qp);    /* QP2QUANT[max(0,qp-12)] */

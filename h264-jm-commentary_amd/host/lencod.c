@@ -27,6 +27,16 @@ static int gpu_push(void *ctx, const jm_pic *cur, const jmh_frame_params *fp) {
     return jmh_frame_push((jmh_ctx *)ctx, cur->y, cur->u, cur->v, cur->w, cur->w / 2, fp);
 }
 static int gpu_pop(void *ctx) { return jmh_frame_pop((jmh_ctx *)ctx); }
+static int gpu_search_pictures(void *ctx, const jm_pic *cur, const jm_pic *ref) {
+    return jmh_search_pictures((jmh_ctx *)ctx, cur->y, ref->y, cur->w);
+}
+static int gpu_block_search(void *ctx, int n, const jmh_block_search *q, jmh_block_result *r) {
+    return jmh_block_motion_search((jmh_ctx *)ctx, n, q, r);
+}
+static int gpu_tq4x4(void *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *lev, uint8_t *rec,
+                     int32_t *cc, int32_t *nz) {
+    return jmh_tq4x4_batch((jmh_ctx *)ctx, n, resid, pred, qp, intra, lev, rec, cc, nz);
+}
 
 int main(int argc, char **argv) {
     jm_input inp;
@@ -39,7 +49,8 @@ int main(int argc, char **argv) {
     int r = jmh_create(&cfg, inp.hip_device, &ctx);
     if (r) { fprintf(stderr, "jmh_create failed: %s\n", jmh_strerror(r)); return 2; }
     jm_backend be = {"mi355x-hip", ctx, gpu_set_ref, gpu_encode, gpu_res, gpu_recon, gpu_destroy,
-                     gpu_deblocked, gpu_ref_deblocked, gpu_push, gpu_pop, jmh_pipeline_depth(ctx)};
+                     gpu_deblocked, gpu_ref_deblocked, gpu_push, gpu_pop, jmh_pipeline_depth(ctx),
+                     gpu_search_pictures, gpu_block_search, gpu_tq4x4};
     if (getenv("JMH_HOST_DEBLOCK")) be.read_deblocked = NULL, be.reference_deblocked = NULL;
     jm_stats st;
     r = jm_encode_sequence(&inp, &be, &st, stdout);

@@ -58,6 +58,18 @@ class JmhTiming(ctypes.Structure):
                 ("pictures_done", ctypes.c_int32)]
 
 
+class JmhBlockSearch(ctypes.Structure):
+    _fields_ = [("mb_x", ctypes.c_int32), ("mb_y", ctypes.c_int32), ("blocktype", ctypes.c_int32),
+                ("block_x", ctypes.c_int32), ("block_y", ctypes.c_int32), ("pred_mv", ctypes.c_int32 * 2),
+                ("centre", ctypes.c_int32 * 2), ("search_range", ctypes.c_int32), ("lambda_factor", ctypes.c_int32),
+                ("search_mode", ctypes.c_int32), ("slice_p", ctypes.c_int32)]
+
+
+class JmhBlockResult(ctypes.Structure):
+    _fields_ = [("mv", ctypes.c_int32 * 2), ("min_mcost", ctypes.c_int32), ("fullpel_mv", ctypes.c_int32 * 2),
+                ("fullpel_cost", ctypes.c_int32)]
+
+
 # jmh_mb_result, field for field (include/jmhip.h)
 MB_RESULT_DTYPE = np.dtype([
     ("mb_type", "<i2"), ("cbp", "<i2"), ("cbp_blk", "<i4"), ("b8mode", "i1", 4),
@@ -93,6 +105,8 @@ _SIGS = {
     "jmh_tq4x4_batch": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "jmh_tq8x8_batch": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "jmh_read_qpel": (_I, [_P, _P]),
+    "jmh_search_pictures": (_I, [_P, _P, _P, _I]),
+    "jmh_block_motion_search": (_I, [_P, _I, _P, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -304,6 +318,17 @@ class Encoder:
     def read_qpel(self):
         out = np.empty((16, self.h + 8, self.w + 8), np.uint8)
         _check(self.lib.jmh_read_qpel(self.ctx, _ptr(out)), "jmh_read_qpel")
+        return out
+
+    def search_pictures(self, cur_y, ref_y):
+        cur_y, ref_y = np.ascontiguousarray(cur_y, np.uint8), np.ascontiguousarray(ref_y, np.uint8)
+        _check(self.lib.jmh_search_pictures(self.ctx, _ptr(cur_y), _ptr(ref_y), self.w), "jmh_search_pictures")
+
+    def block_motion_search(self, reqs):
+        """reqs: a ctypes array of JmhBlockSearch; returns the JmhBlockResult array."""
+        out = (JmhBlockResult * len(reqs))()
+        _check(self.lib.jmh_block_motion_search(self.ctx, len(reqs), ctypes.cast(reqs, _P), ctypes.cast(out, _P)),
+               "jmh_block_motion_search")
         return out
 
 

@@ -20,6 +20,10 @@
  *   mv-search.c › SetupFastFullPelSearch (BlockSAD table)    jmh_ffs_sad_table()   (unit seam)
  *   block.c › dct_luma (4x4 TQ + recon)                     jmh_tq4x4_batch()     (unit seam)
  *   block.c › dct_luma8x8 (JM FRExt, High profile)          jmh_tq8x8_batch()     (unit seam)
+ *   mv-search.c › BlockMotionSearch (one block, caller's MVP,   jmh_search_pictures() +
+ *               centre, range and lambda: the per-call seam    jmh_block_motion_search()
+ *               of host/jm86.c BlockMotionSearch /
+ *               PartitionMotionSearch and of an RDO-on loop)
  *
  * Reference citations: the mounted reference (/root/reference) holds only README.md:1-4 (an
  * annotated-JM commentary with no source), so no file:line into JM source exists; the JM
@@ -226,6 +230,36 @@ int  jmh_tq4x4_batch(jmh_ctx *ctx, int n, const int16_t *resid, const uint8_t *p
 int  jmh_tq8x8_batch(jmh_ctx *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp,
                      int intra, int16_t *levels, uint8_t *recon, int32_t *coeff_cost,
                      int32_t *nonzero);
+/* ---- per-block motion search: JM 8.6 mv-search.c › BlockMotionSearch [J] for one block per
+ * request, from the arguments BlockMotionSearch works from (the caller derives the MVP with
+ * SetMotionVectorPredictor, the centre with SetupFastFullPelSearch / the MVP, the range with
+ * RestrictSearchRange): full pel (FFS: (0,0) pre-check then the spiral around the MB's window
+ * centre; full search: the spiral around the block's own centre with the 16x16 zero-vector
+ * bias) and SubPelBlockMotionSearch (half then quarter pel, SATD with UseHadamard of the
+ * context's configuration).  Searches the luma pictures given to jmh_search_pictures.        */
+typedef struct jmh_block_search {
+    int32_t mb_x, mb_y;         /* macroblock, in MBs                                              */
+    int32_t blocktype;          /* 1..7: 16x16, 16x8, 8x16, 8x8, 8x4, 4x8, 4x4                      */
+    int32_t block_x, block_y;   /* block position inside the MB, 4x4 units                        */
+    int32_t pred_mv[2];         /* the block's MVP, quarter pel                                   */
+    int32_t centre[2];          /* full-pel search centre (an MV): FFS the MB's window centre,    */
+                                /*   full search pred_mv / 4 clamped to +-search_range            */
+    int32_t search_range;       /* 0..SearchRange: the spiral's first (2R+1)^2 positions          */
+    int32_t lambda_factor;      /* LAMBDA_FACTOR(lambda_motion) = (int)(65536 * lambda + 0.5)     */
+    int32_t search_mode;        /* 0 fast full search, -1 full search                             */
+    int32_t slice_p;            /* 1: P slice (the 16x16 zero-vector biases apply)                */
+} jmh_block_search;
+typedef struct jmh_block_result {
+    int32_t mv[2];              /* quarter pel (what BlockMotionSearch stores in all_mv)          */
+    int32_t min_mcost;          /* BlockMotionSearch's return value                               */
+    int32_t fullpel_mv[2];      /* the full-pel winner                                            */
+    int32_t fullpel_cost;
+} jmh_block_result;
+/* current and reference luma pictures (coded size) of the per-block searches (copied)         */
+int  jmh_search_pictures(jmh_ctx *ctx, const uint8_t *cur_y, const uint8_t *ref_y, int stride_y);
+/* n independent requests in one launch (n = 1 for a JM-shaped call); res[n]                   */
+int  jmh_block_motion_search(jmh_ctx *ctx, int n, const jmh_block_search *req, jmh_block_result *res);
+
 /* jmh_read_qpel: the 16 quarter-pel phase planes of the current reference (test seam for
  *   UnifiedOneForthPix), out[16][H+8][W+8], phase = 4*yfrac + xfrac, 4-sample padding.      */
 int  jmh_read_qpel(jmh_ctx *ctx, uint8_t *out);

@@ -170,12 +170,11 @@ static int block_range(const mbs *s, int blocktype) {
 
 /* SetupFastFullPelSearch [J]: window centre = 16x16 MVP/4 (trunc), clamped to +-SR (RDO off);
  * 16 4x4 SADs per search position (stored in window raster order). */
-static void ffs_setup(mbs *s) {
+static void ffs_setup_at(mbs *s, int scx, int scy) {
     jmo_ctx *c = s->c;
-    int sr = c->sr, side = 2 * sr + 1, pmv[2];
-    set_mvp(s, pmv, 0, 0, 0, 16, 16);
-    s->scx = iclip(-sr, sr, pmv[0] / 4);
-    s->scy = iclip(-sr, sr, pmv[1] / 4);
+    int sr = c->sr, side = 2 * sr + 1;
+    s->scx = scx;
+    s->scy = scy;
     s->pos_00 = c->spiral_of[(-s->scy + sr) * side + (-s->scx + sr)];
     for (int dy = -sr; dy <= sr; dy++)
         for (int dx = -sr; dx <= sr; dx++) {
@@ -190,6 +189,11 @@ static void ffs_setup(mbs *s) {
             }
         }
     s->setup_done = 1;
+}
+static void ffs_setup(mbs *s) {
+    int sr = s->c->sr, pmv[2];
+    set_mvp(s, pmv, 0, 0, 0, 16, 16);
+    ffs_setup_at(s, iclip(-sr, sr, pmv[0] / 4), iclip(-sr, sr, pmv[1] / 4));
 }
 
 /* SetupLargerBlocks [J] equivalent: SAD of a bsx x bsy block at window raster index r */
@@ -412,6 +416,46 @@ static int block_motion_search(mbs *s, int blocktype, int bx4, int by4, int rang
             s->all_mv[blocktype][(by4 + y) * 4 + bx4 + x][1] = (int16_t)mvy;
         }
     return min_mcost;
+}
+
+/* the per-block seam (jmh_block_motion_search's oracle): BlockMotionSearch from explicit
+ * arguments (MVP, centre, range, lambda_factor) on the pictures of jmo_search_pictures */
+int jmo_search_pictures(jmo_ctx *c, const uint8_t *cur_y, const uint8_t *ref_y, int stride) {
+    if (!c || !cur_y || !ref_y || stride < c->W) return JMH_E_INVALID_ARG;
+    for (int y = 0; y < c->H; y++) {
+        memcpy(c->orgY + (size_t)y * c->W, cur_y + (size_t)y * stride, c->W);
+        memcpy(c->refY + (size_t)y * c->W, ref_y + (size_t)y * stride, c->W);
+    }
+    jmo_build_qpel(c);
+    c->have_ref = 1;
+    return JMH_OK;
+}
+
+int jmo_block_motion_search(jmo_ctx *c, int n, const jmh_block_search *req, jmh_block_result *res) {
+    if (!c || n <= 0 || !req || !res) return JMH_E_INVALID_ARG;
+    for (int i = 0; i < n; i++) {
+        const jmh_block_search *q = &req[i];
+        if (q->blocktype < 1 || q->blocktype > 7 || q->search_range < 0 || q->search_range > c->sr) return JMH_E_INVALID_ARG;
+        if (q->search_mode != 0 && q->search_mode != -1) return JMH_E_UNSUPPORTED_CFG;
+        mbs S;
+        mbs *s = &S;
+        memset(s, 0, sizeof(*s));
+        s->c = c; s->mbx = q->mb_x; s->mby = q->mb_y; s->pix_x = 16 * q->mb_x; s->pix_y = 16 * q->mb_y;
+        s->lf = q->lambda_factor;
+        s->slice_p = q->slice_p != 0;
+        for (int y = 0; y < 16; y++) memcpy(s->org + 16 * y, c->orgY + (s->pix_y + y) * c->W + s->pix_x, 16);
+        int mvx = q->centre[0], mvy = q->centre[1], min_mcost;
+        if (q->search_mode == 0) {
+            ffs_setup_at(s, q->centre[0], q->centre[1]);
+            min_mcost = ffs_search(s, q->blocktype, q->block_x, q->block_y, q->pred_mv[0], q->pred_mv[1], q->search_range, &mvx, &mvy);
+        } else
+            min_mcost = full_search(s, q->blocktype, q->block_x, q->block_y, q->pred_mv[0], q->pred_mv[1], q->search_range, &mvx, &mvy);
+        res[i].fullpel_mv[0] = mvx; res[i].fullpel_mv[1] = mvy; res[i].fullpel_cost = min_mcost;
+        if (c->cfg.use_hadamard) min_mcost = BIGCOST;
+        min_mcost = subpel_search(s, q->blocktype, q->block_x, q->block_y, q->pred_mv[0], q->pred_mv[1], &mvx, &mvy, min_mcost);
+        res[i].mv[0] = mvx; res[i].mv[1] = mvy; res[i].min_mcost = min_mcost;
+    }
+    return JMH_OK;
 }
 
 static void write_enc_mv(mbs *s, int bx4, int by4, int w4, int h4, const int16_t (*mv)[2]) {

@@ -46,6 +46,10 @@ int  jmo_load_current(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint
                       int stride_y, int stride_c);
 
 /* ---- unit entry points (known-answer + GPU unit parity) ------------------------------ */
+/* per-block BlockMotionSearch seam (the oracle of jmh_block_motion_search); jmo_search_pictures
+ * replaces the context's current and reference luma                                        */
+int  jmo_search_pictures(jmo_ctx *c, const uint8_t *cur_y, const uint8_t *ref_y, int stride);
+int  jmo_block_motion_search(jmo_ctx *c, int n, const jmh_block_search *req, jmh_block_result *res);
 int  jmo_ffs_sad_table(jmo_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t *centres,
                        uint16_t *out);
 int  jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,

@@ -13,6 +13,7 @@ LENCOD = os.path.join(PKG, "host", "build", "lencod")
 LIBORACLE = os.path.join(ORACLE, "_build", "liboracle.so")
 LENCOD_CPU = os.path.join(ORACLE, "_build", "lencod_cpu")
 JMDEC = os.path.join(ORACLE, "_build", "jmdec")
+JM86_CHECK = os.path.join(ORACLE, "_build", "jm86_check")
 HEADER = os.path.join(ROOT, "include", "jmhip.h")
 
 

@@ -43,6 +43,8 @@ def lib():
             "jmo_qp2quant": (_I, [_I]),
             "jmo_qp_scale_cr": (_I, [_I]),
             "jmo_mvp_median": (None, [_I] * 17 + [_P]),
+            "jmo_search_pictures": (_I, [_P, _P, _P, _I]),
+            "jmo_block_motion_search": (_I, [_P, _I, _P, _P]),
             "jmo_dec_create": (_I, [ctypes.POINTER(_P)]),
             "jmo_dec_destroy": (None, [_P]),
             "jmo_decode_annexb": (_I, [_P, _P, ctypes.c_long, _P, ctypes.c_long, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
@@ -105,6 +107,16 @@ class OracleEncoder:
     def read_qpel(self):
         out = np.empty((16, self.h + 8, self.w + 8), np.uint8)
         assert self.L.jmo_read_qpel(self.ctx, _ptr(out)) == 0
+        return out
+
+    def search_pictures(self, cur_y, ref_y):
+        cur_y, ref_y = np.ascontiguousarray(cur_y, np.uint8), np.ascontiguousarray(ref_y, np.uint8)
+        assert self.L.jmo_search_pictures(self.ctx, _ptr(cur_y), _ptr(ref_y), self.w) == 0
+
+    def block_motion_search(self, reqs):
+        out = (jmhip.JmhBlockResult * len(reqs))()
+        st = self.L.jmo_block_motion_search(self.ctx, len(reqs), ctypes.cast(reqs, _P), ctypes.cast(out, _P))
+        assert st == 0, st
         return out
 
     def sad_table(self, mb_xy, centres):

@@ -19,7 +19,7 @@ def test_library_exports_every_declared_symbol():
     ensure_built()
     lib = ctypes.CDLL(LIBJMHIP)
     names = declared()
-    assert len(names) == 24
+    assert len(names) == 26
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(jmhip.EXPORTED)
