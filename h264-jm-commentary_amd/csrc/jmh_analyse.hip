@@ -32,7 +32,6 @@
 //   * sub-pel SATD: one 4x4 sub-block per 16-lane row, DPP Hadamard, LDS-atomic candidate sums.
 #include "jmh_common.h"
 
-#define NPK 10                                // search positions per thread (a column strip)
 #define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
 #define MVB_LEN 1104
 #define PLS (WIN_DIM_MAX * WST + 32)          // stride between the G, b, h, j planes
@@ -76,7 +75,7 @@ struct MeS {
     int motion_cost[8][4];
     unsigned red[NTA / 64][4];                // per wave, per search of the stage: argmin keys
     int pmv[4][2];                            // MVPs of the next stage's searches (forwarded)
-    uint8_t mvb[MVB_LEN];                     // mvbits(v) at [v + MVB_OFF] (|v| <= 4*2*SR + 259)
+    uint16_t mvc[MVB_LEN];                    // lambda * mvbits(v) at [v + MVB_OFF] (|v| <= 4*2*SR + 259)
     uint8_t planes[4 * PLS];                  // G (the window), b, h, j
     int16_t h1[WIN_DIM_MAX * WST];            // unclipped vertical 6-tap intermediates
     unsigned long long *pst;                  // debug: per-stage stamps (thread 0), null when off
@@ -88,8 +87,8 @@ union AnalyseS {
     IntraS in[4];
 };
 
-__device__ __forceinline__ void sstamp(MeS &s) {
-    if (threadIdx.x == 0 && s.pst && s.pn < 44) s.pst[s.pn++] = wall_clock64();
+__device__ __forceinline__ void sstamp(MeS &s, int wave) {
+    if (wave == 0 && __lane_id() == 0 && s.pst && s.pn < 44) s.pst[s.pn++] = wall_clock64();
 }
 
 // prefetch of the intra neighbourhood by threads t in [0, 96)
@@ -188,20 +187,20 @@ __device__ __forceinline__ uint32_t ordk_of(const PosState &ps, int k) {
 template <int BT, int BX, int BY>
 __device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps, int sr, int range, int lam, int pmx, int pmy, int scx,
                                                 int scy) {
-    const unsigned cxv = lam * s.mvb[4 * (scx - sr + ps.dx) - pmx + MVB_OFF];
-    const uint8_t *cy = s.mvb + 4 * (scy - sr + ps.dy0) - pmy + MVB_OFF;
+    const unsigned cxv = s.mvc[4 * (scx - sr + ps.dx) - pmx + MVB_OFF];
+    const uint16_t *cy = s.mvc + 4 * (scy - sr + ps.dy0) - pmy + MVB_OFF;
     unsigned b = 0xFFFFFFFFu;
     if (range >= sr) {
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
-            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + lam * cy[4 * k];
+            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + cy[4 * k];
             b = min(b, (cost << 13) | ordk_of(ps, k));
         }
     } else {
         const int rx = abs(ps.dx - sr);
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
-            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + lam * cy[4 * k];
+            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + cy[4 * k];
             const uint32_t o = ordk_of(ps, k);
             const bool in = max(rx, abs(ps.dy0 + k - sr)) <= range || o == 0;
             b = min(b, in ? (cost << 13) | o : 0xFFFFFFFFu);
@@ -327,7 +326,7 @@ __device__ __forceinline__ int quad_row_satd(const MeS &s, int wbase, int obase,
 #define KOFF 4096
 __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, const SDesc q, int pmvx, int pmvy, int scx, int scy, int b8,
                                             int best8x8) {
-    const int lane = threadIdx.x & 63;
+    const int lane = __lane_id();
     const int sr = d.sr, lam = d.lambda_motion, had = d.use_hadamard;
     unsigned best = s.red[0][j];
 #pragma unroll
@@ -362,7 +361,7 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
                 sat += dpp<0x4E>(sat);
                 if (lns) sat += __shfl_xor(sat, 4, 64);
                 if (val && sub == 0 && row == 0) {
-                    int cost = sat + lam * (mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
+                    int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
                     if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
                     kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
                 }
@@ -379,7 +378,7 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
                 }
                 for (int m = 1; m < nsub; m <<= 1) sat += __shfl_xor(sat, m, 64);
                 if (val && sub == 0) {
-                    int cost = sat + lam * (mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
+                    int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
                     if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
                     kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
                 }
@@ -412,8 +411,8 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
 // -> barrier, sub-pel search j on wave j (+ forwarded MVPs), barrier.
 template <int NS, bool FWD, class EV, class IDLE>
 __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &ps, const SDesc (&sd)[NS], int b8, int best8x8, EV ev,
-                                         int islot, IDLE idle) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                         int islot, IDLE idle, int wave) {
+    const int lane = __lane_id();
     fence_state(ps);
     int pmx[NS], pmy[NS];
     unsigned bk[NS];
@@ -439,13 +438,13 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
         if (lane == 0) s.red[wave][j] = v;
     }
     __syncthreads();
-    sstamp(s);
+    sstamp(s, wave);
 #pragma unroll
     for (int j = 0; j < NS; j++)
         if (wave == j) subpel_wave(d, s, j, sd[j], pmx[j], pmy[j], ps.scx, ps.scy, b8, best8x8);
     if (islot >= 0 && wave >= 6) idle(islot, wave - 6);   // the MB's Intra4x4 on otherwise idle waves
     __syncthreads();
-    sstamp(s);
+    sstamp(s, wave);
 }
 
 #define EV(J, BT, BX, BY) bk[J] = eval_search<BT, BX, BY>(s, ps, sr, search_range(d, BT), lam, pmx[J], pmy[J], ps.scx, ps.scy)
@@ -490,7 +489,7 @@ __device__ __forceinline__ void sad_strip(const MeS &s, PosState &ps) {
 // one 8x8 block of P8x8: its 4x4 SADs, 4 stages (sub-modes 4..7 in parallel, then the 4x4
 // chain), then the P8x8 sub-mode decision for the block (its MVs are read through best8x8)
 template <int B8, class IDLE>
-__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8, IDLE idle) {
+__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8, IDLE idle, int wave) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
     const int sr = d.sr, lam = d.lambda_motion;
     fence_state(ps);
@@ -502,23 +501,23 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
                              {7, X, Y, B8, 7, X + 1, Y, 2}};
         me_stage<4, false>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[4], const int (&pmx)[4], const int (&pmy)[4]) {
             EV(0, 4, X, Y); EV(1, 5, X, Y); EV(2, 6, X, Y); EV(3, 7, X, Y);
-        }, 2 + 2 * B8, idle);
+        }, 2 + 2 * B8, idle, wave);
     }
     {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right
         const SDesc sd[3] = {{5, X, Y + 1, B8, 0, 0, 0, 0}, {6, X + 1, Y, B8, 0, 0, 0, 0}, {7, X + 1, Y, B8, 7, X, Y + 1, 0}};
         me_stage<3, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
             EV(0, 5, X, Y + 1); EV(1, 6, X + 1, Y); EV(2, 7, X + 1, Y);
-        }, 3 + 2 * B8, idle);
+        }, 3 + 2 * B8, idle, wave);
     }
     {   // stage 2: 4x4 bottom-left
         const SDesc sd[1] = {{7, X, Y + 1, B8, 7, X + 1, Y + 1, 0}};
         me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X, Y + 1); },
-                          B8 == 3 ? 10 : -1, idle);
+                          B8 == 3 ? 10 : -1, idle, wave);
     }
     {   // stage 3: 4x4 bottom-right
         const SDesc sd[1] = {{7, X + 1, Y + 1, B8, 0, 0, 0, 0}};
         me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X + 1, Y + 1); },
-                          -1, idle);
+                          -1, idle, wave);
     }
     int mc8 = BIGCOST, bm = 0;
     for (int mode = 4; mode <= 7; mode++) {
@@ -596,6 +595,7 @@ __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScra
 
 __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int mby) {
     const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // an SGPR: tid itself dies after the setup
     const int W = d.W, sr = d.sr, side = d.side;
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
     const bool prof = prof_mb_here(d, mbx, mby);
@@ -609,7 +609,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     // the MB's Intra4x4 decision (10 diagonal steps, then the results) runs on waves 6 and 7
     // while the motion search's sub-pel waves work: slots 0..10 (intra_slot)
     auto idle = [&](int k, int w) { intra_slot(d, s.in, scr, k, w, mbx, mby); };
-    for (int i = tid; i < MVB_LEN; i += NTA) s.mvb[i] = (uint8_t)mvbits(i - MVB_OFF);
+    for (int i = tid; i < MVB_LEN; i += NTA) s.mvc[i] = (uint16_t)__umul24(d.lambda_motion, mvbits(i - MVB_OFF));
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
     const int wdim = 2 * sr + 16 + 2 * WM;
@@ -673,15 +673,17 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         fence_state(ps);
         sad_strip<true, 8, 8, 1, 1>(s, ps);
         PSTAMP(8);
+        // JM order keys of the strip from the per-context table (first read in the first stage, so
+        // the loads overlap the half-pel planes); the (0,0) pre-check position, order 0, depends on
+        // the MB's window centre
 #pragma unroll
-        for (int k = 0; k < NPK; k++) {
-            const int dy = ps.dy0 + k, rx = ps.dx - sr, ry = dy - sr;
-            uint32_t o;
-            if (!sact || dy >= side) o = 0xFFFFu;
-            else if (rx == -scx && ry == -scy) o = 0;   // the (0,0) pre-check position
-            else o = (uint32_t)(spiral_index(rx, ry) + 1);
-            if (k & 1) ps.ordk2[k >> 1] |= o << 16;
-            else ps.ordk2[k >> 1] = o;
+        for (int k2 = 0; k2 < NPK / 2; k2++) ps.ordk2[k2] = d.ordtab[k2 * NTA + tid];
+        {
+            const int k0 = sr - scy - ps.dy0;   // strip slot of the pre-check position
+            const bool mine = sact && ps.dx == sr - scx;
+#pragma unroll
+            for (int k2 = 0; k2 < NPK / 2; k2++)
+                if (mine && (k0 >> 1) == k2) ps.ordk2[k2] &= (k0 & 1) ? 0x0000FFFFu : 0xFFFF0000u;
         }
         PSTAMP(9);
         // ---- half-pel planes over window rows / columns [3, 2sr+21): four columns (one dword) per
@@ -751,15 +753,16 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
                 const SDesc sd[3] = {{1, 0, 0, 0, 0, 0, 0, 0}, {2, 0, 0, 0, 2, 0, 2, 0}, {3, 0, 0, 0, 3, 2, 0, 1}};
                 me_stage<3, false>(d, s, ps, sd, 0, 0, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
                     EV(0, 1, 0, 0); EV(1, 2, 0, 0); EV(2, 3, 0, 0);
-                }, 0, idle);
+                }, 0, idle, wave);
             }
             {   // stage 1: 16x8 lower, 8x16 right
                 const SDesc sd[2] = {{2, 0, 2, 1, 0, 0, 0, 0}, {3, 2, 0, 1, 0, 0, 0, 0}};
                 me_stage<2, true>(d, s, ps, sd, 0, 0, [&](unsigned (&bk)[2], const int (&pmx)[2], const int (&pmy)[2]) {
                     EV(0, 2, 0, 2); EV(1, 3, 2, 0);
-                }, 1, idle);
+                }, 1, idle, wave);
             }
             // results: MVs of types 1..3, partition costs, FindSkipModeMotionVector
+            const int tid = 64 * wave + __lane_id();
             if (tid < 96) {
                 const int m = 1 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
                 scr->all_mv[m][k][c] = s.all_mv[m][k][c];
@@ -778,13 +781,14 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         PSTAMP(7);
         {   // ---- P8x8: 4 x 4 stages
             int best8x8 = 0, cost8x8 = 0;
-            p8x8_block<0>(d, s, ps, best8x8, cost8x8, idle);
+            p8x8_block<0>(d, s, ps, best8x8, cost8x8, idle, wave);
             PSTAMP(3);
-            p8x8_block<1>(d, s, ps, best8x8, cost8x8, idle);
+            p8x8_block<1>(d, s, ps, best8x8, cost8x8, idle, wave);
             PSTAMP(4);
-            p8x8_block<2>(d, s, ps, best8x8, cost8x8, idle);
+            p8x8_block<2>(d, s, ps, best8x8, cost8x8, idle, wave);
             PSTAMP(5);
-            p8x8_block<3>(d, s, ps, best8x8, cost8x8, idle);
+            p8x8_block<3>(d, s, ps, best8x8, cost8x8, idle, wave);
+            const int tid = 64 * wave + __lane_id();
             if (tid < 128) {
                 const int m = 4 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
                 scr->all_mv[m][k][c] = s.all_mv[m][k][c];
@@ -962,6 +966,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     // workgroup (I pictures; SearchMode -1, where k_mb_me_full searched)
     const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0, nPg = xcd_grid(nPm), tot = t.pre[t.npic], b = blockIdx.x;
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
+    const bool first_thread = threadIdx.x == 0;   // a lane mask: threadIdx itself dies early
     const int role = b < nPg ? 2 : 0;
     if (role == 2) {
         const int m = xcd_block(b, nPm);                      // XCD-aware: neighbouring MBs share an L2
@@ -980,7 +985,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     }
     if (t.bprof) {
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (first_thread) {
             t.bprof[3 * b] = t0;
             t.bprof[3 * b + 1] = wall_clock64();
             t.bprof[3 * b + 2] = role;

@@ -10,6 +10,7 @@
 #define QPAD 4                           // quarter-pel plane padding (== oracle JMO_PAD)
 #define NT 256                           // threads per finalize / unit workgroup
 #define NTA 512                          // threads per analysis workgroup (8 waves, 2 per SIMD)
+#define NPK 10                           // FFS search positions per analysis thread (a column strip)
 #define BIGCOST (1 << 20)
 #define PMAX 34                          // pictures per wavefront tick (pipelined pictures in flight)
 // A picture's macroblock (x, y) reads its reference (the previous picture, deblocked) at pixel
@@ -57,6 +58,7 @@ struct DevParams {
     int8_t *ipred;
     const int16_t *tmv;         // EPZS temporal predictors: the previous picture's MVs / ref_idx
     const int8_t *tref;         //   (null: no previous picture)
+    const uint32_t *ordtab;     // FFS: JM order keys of every thread's positions (ordtab_fill)
     jmh_mb_result *res;
     MbScratch *scr;
     unsigned long long *prof;   // debug phase timestamps (null: off)
@@ -90,6 +92,7 @@ struct TickArgs {
     int me_in_analyse;                   // 1: k_mb_analyse runs the FFS searches; 0: k_mb_me_full did
                                          //   (full search, SearchMode -1, or EPZS, SearchMode 3)
     int t8;                              // Transform8x8Mode: k_mb_intra8 ran, k_mb_final decides 4x4 / 8x8
+    const uint32_t *ordtab;              // FFS order keys, [NPK / 2][NTA] packed pairs (jmh_create)
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
     PicParams p[PMAX];
@@ -129,7 +132,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.dbkY = q.dbk; d.dbkU = q.dbk ? q.dbk + ls : nullptr; d.dbkV = q.dbk ? q.dbk + ls + lc : nullptr;
     d.lf_disable = q.lf_disable; d.lf_offA = q.lf_offA; d.lf_offB = q.lf_offB;
     d.mv = q.mv; d.refidx = q.refidx; d.ipred = q.ipred; d.res = q.res; d.scr = q.scr;
-    d.tmv = q.tmv; d.tref = q.tref;
+    d.tmv = q.tmv; d.tref = q.tref; d.ordtab = t.ordtab;
     d.prof = e == 0 ? t.prof : nullptr; d.prof_mb = t.prof_mb;
     d.slice_type = q.slice_type; d.qp = q.qp; d.lambda_mode = q.lambda_mode; d.lambda_motion = q.lambda_motion;
     d.cqp_off = q.cqp_off; d.diag = q.diag; d.y_min = q.y_min;

@@ -116,6 +116,7 @@ struct jmh_ctx {
     size_t fsize, n4, nmb;               // bytes of one 4:2:0 picture (Y then U then V)
     uint8_t *d_ref, *d_qpel, *d_slots;   // explicit reference (set_reference), a1 seam, slots
     uint8_t *d_scur, *d_sref;            // luma pictures of the per-block searches (jmh_search_pictures)
+    uint32_t *d_ordtab;                  // FFS order keys of the analysis threads' strips (ordtab_fill)
     int nslots;
     int depth, nring;
     std::vector<PicBuf> ring;
@@ -222,6 +223,8 @@ struct DevTemps {
     }
 };
 
+static void ordtab_fill(std::vector<uint32_t> &tab, int sr);
+
 extern "C" {
 
 void jmh_destroy(jmh_ctx *c) {
@@ -229,7 +232,7 @@ void jmh_destroy(jmh_ctx *c) {
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     for (PicBuf &b : c->ring) free_entry(b);
-    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref};
+    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     ring_free(c->ring_interp);
@@ -280,6 +283,12 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         ALLOC(c->d_ref, c->fsize);
         ALLOC(c->d_qpel, (size_t)16 * c->qplane);
         ALLOC(c->d_slots, c->fsize * c->nslots);
+        {
+            std::vector<uint32_t> ot;
+            ordtab_fill(ot, c->sr);
+            ALLOC(c->d_ordtab, ot.size() * sizeof(uint32_t));
+            if (hipMemcpy(c->d_ordtab, ot.data(), ot.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        }
         c->ring.resize(c->nring);
         for (PicBuf &b : c->ring) {
             if ((st = alloc_entry(c, b))) goto fail;
@@ -318,6 +327,32 @@ fail:
 int jmh_pipeline_depth(const jmh_ctx *c) { return c ? c->depth : JMH_E_INVALID_ARG; }
 
 }  // extern "C"
+
+// JM spiral order (Init_Motion_Search_Module [J]) of relative position (x, y)
+static int host_spiral_index(int x, int y) {
+    const int ax = x < 0 ? -x : x, ay = y < 0 ? -y : y, l = ax > ay ? ax : ay;
+    if (l == 0) return 0;
+    const int base = (2 * l - 1) * (2 * l - 1);
+    if (ay == l && ax < l) return base + 2 * (x + l - 1) + (y > 0);
+    return base + 2 * (2 * l - 1) + 2 * (y + l) + (x > 0);
+}
+
+// order keys of the FFS analysis threads (k_mb_analyse): thread t owns window column t % side,
+// rows (t / side) * NPK .. + NPK - 1; key = spiral index + 1 (0 is the (0,0) pre-check, set per
+// MB in the kernel), 0xFFFF outside the window.  [NPK / 2][NTA] packed pairs (low = even slot).
+static void ordtab_fill(std::vector<uint32_t> &tab, int sr) {
+    const int side = 2 * sr + 1, nstrips = (side + NPK - 1) / NPK;
+    tab.assign((size_t)(NPK / 2) * NTA, 0);
+    for (int t = 0; t < NTA; t++) {
+        const bool sact = t < side * nstrips;
+        const int dx = sact ? t % side : 0, dy0 = sact ? (t / side) * NPK : 0;
+        for (int k = 0; k < NPK; k++) {
+            const int dy = dy0 + k;
+            const uint32_t o = (!sact || dy >= side) ? 0xFFFFu : (uint32_t)(host_spiral_index(dx - sr, dy - sr) + 1);
+            tab[(size_t)(k >> 1) * NTA + t] |= o << (16 * (k & 1));
+        }
+    }
+}
 
 static void pack_planes(uint8_t *dst, int W, int H, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
     for (int r = 0; r < H; r++) memcpy(dst + (size_t)r * W, y + (size_t)r * sy, W);
@@ -367,6 +402,7 @@ static int issue_tick(jmh_ctx *c) {
     t.prof = c->d_prof; t.prof_mb = c->prof_mb;
     t.me_in_analyse = c->cfg.search_mode == 0;
     t.t8 = c->cfg.transform_8x8_mode;
+    t.ordtab = c->d_ordtab;
     int act[PMAX], nact = 0, nP = 0;
     const int nf = (int)c->fl.size();
     std::vector<int> before(nf);
@@ -504,7 +540,8 @@ static int push_picture(jmh_ctx *c, const uint8_t *src, int entry, const jmh_fra
 
 static int check_params(const jmh_ctx *c, const jmh_frame_params *fp) {
     if (fp->slice_type != JMH_P_SLICE && fp->slice_type != JMH_I_SLICE) return JMH_E_UNSUPPORTED_CFG;
-    if (fp->qp < 0 || fp->qp > 51 || fp->lambda_mode < 0 || fp->lambda_motion < 0) return JMH_E_INVALID_ARG;
+    if (fp->qp < 0 || fp->qp > 51 || fp->lambda_mode < 0 || fp->lambda_motion < 0 || fp->lambda_mode > JMH_LAMBDA_MAX ||
+        fp->lambda_motion > JMH_LAMBDA_MAX) return JMH_E_INVALID_ARG;
     if (fp->deblock && (fp->lf_disable < 0 || fp->lf_disable > 2 || fp->lf_alpha_div2 < -6 || fp->lf_alpha_div2 > 6 ||
                         fp->lf_beta_div2 < -6 || fp->lf_beta_div2 > 6)) return JMH_E_INVALID_ARG;
     if (fp->slice_type == JMH_P_SLICE && c->ref_kind == REF_NONE) return JMH_E_STATE;

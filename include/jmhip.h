@@ -44,6 +44,7 @@ extern "C" {
 #endif
 
 #define JMH_ABI_VERSION 6
+#define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define JMH_OK                 0
@@ -100,8 +101,8 @@ typedef struct jmh_config {
 typedef struct jmh_frame_params {
     int32_t slice_type;        /* JMH_P_SLICE / JMH_I_SLICE                                      */
     int32_t qp;                /* slice QP (0..51), constant over the picture (no rate control)  */
-    int32_t lambda_mode;       /* RDO off: QP2QUANT[max(0,qp-12)] (integer, computed on host)    */
-    int32_t lambda_motion;     /* RDO off: == lambda_mode                                        */
+    int32_t lambda_mode;       /* RDO off: QP2QUANT[max(0,qp-12)] (integer, computed on host);   */
+    int32_t lambda_motion;     /* RDO off: == lambda_mode.  Both 0..JMH_LAMBDA_MAX (JM: <= 91)   */
     int32_t chroma_qp_offset;  /* chroma_qp_index_offset                                         */
     int32_t deblock;           /* 1: also deblock (DeblockFrame, 8.7) on the device into the     */
                                /*    next reference (jmh_read_deblocked, set_reference_slot(-2)) */
