@@ -242,6 +242,8 @@ __device__ __forceinline__ s16x2 clip5(s16x2 v) {   // clip255((v + 16) >> 5)
 }
 __device__ __forceinline__ uint32_t pack4(s16x2 lo, s16x2 hi) { return __builtin_amdgcn_perm(as_u32(hi), as_u32(lo), 0x06040200u); }
 
+// HALF: a half-pel (or full-pel) position, whose sample is one plane's (A == B): B is not read
+template <bool HALF>
 __device__ __forceinline__ int subblock_satd(const MeS &s, int wbase, int obase, int ox, int oy, int had) {
     const int off = qoff((oy & 3) * 4 + (ox & 3));
     const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
@@ -251,8 +253,12 @@ __device__ __forceinline__ int subblock_satd(const MeS &s, int wbase, int obase,
     uint32_t O[4], P[4];
 #pragma unroll
     for (int yy = 0; yy < 4; yy++) {
-        const uint32_t A = lds_u32_at(r0 + yy * WST + oA), B = lds_u32_at(r0 + yy * WST + oB);
-        P[yy] = (A | B) - (((A ^ B) >> 1) & 0x7F7F7F7Fu);   // per byte (a + b + 1) >> 1
+        const uint32_t A = lds_u32_at(r0 + yy * WST + oA);
+        if constexpr (HALF) P[yy] = A;
+        else {
+            const uint32_t B = lds_u32_at(r0 + yy * WST + oB);
+            P[yy] = (A | B) - (((A ^ B) >> 1) & 0x7F7F7F7Fu);   // per byte (a + b + 1) >> 1
+        }
         O[yy] = *reinterpret_cast<const uint32_t *>(s.org + obase + 16 * yy);
     }
     if (!had) {
@@ -291,14 +297,19 @@ __device__ __forceinline__ int subblock_satd(const MeS &s, int wbase, int obase,
 
 // one row (row = lane & 3) of a 4x4 SATD on a quad of lanes: the vertical transform crosses the
 // quad by DPP, the result is this row's share (the quad sum is the block's SATD)
+template <bool HALF>
 __device__ __forceinline__ int quad_row_satd(const MeS &s, int wbase, int obase, int ox, int oy, int row, int had) {
     const int off = qoff((oy & 3) * 4 + (ox & 3));
     const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
     const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
     const int oB = ((xb & 1) + 2 * (yb & 1)) * PLS + (yb >> 1) * WST + (xb >> 1);
     const uint8_t *rr = s.planes + wbase + (oy >> 2) * WST + (ox >> 2) + row * WST;
-    const uint32_t A = lds_u32_at(rr + oA), B = lds_u32_at(rr + oB);
-    const uint32_t P = (A | B) - (((A ^ B) >> 1) & 0x7F7F7F7Fu);
+    const uint32_t A = lds_u32_at(rr + oA);
+    uint32_t P = A;
+    if constexpr (!HALF) {
+        const uint32_t B = lds_u32_at(rr + oB);
+        P = (A | B) - (((A ^ B) >> 1) & 0x7F7F7F7Fu);
+    }
     const uint32_t O = *reinterpret_cast<const uint32_t *>(s.org + obase + 16 * row);
     if (!had) return (int)__builtin_amdgcn_sad_u8(O, P, 0u);
     s16x2 p0 = as_s2(__builtin_amdgcn_perm(0u, O, 0x0c010c00u)) - as_s2(__builtin_amdgcn_perm(0u, P, 0x0c010c00u));
@@ -355,11 +366,12 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
                 int sat = 0;
                 if (c < 9) {   // quad-uniform
                     const int bxs = q.bx4 + (sub & ((1 << lw4) - 1)), bys = q.by4 + (sub >> lw4);
-                    sat = quad_row_satd(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, row, had);
+                    sat = pass == 0 ? quad_row_satd<true>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, row, had)
+                                    : quad_row_satd<false>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, row, had);
                 }
-                sat += dpp<0xB1>(sat);
+                sat += dpp<0xB1>(sat);   // quad (the 4x4 block's rows), then the 8-lane pair of blocks
                 sat += dpp<0x4E>(sat);
-                if (lns) sat += __shfl_xor(sat, 4, 64);
+                if (lns) sat += dpp<0x141>(sat);
                 if (val && sub == 0 && row == 0) {
                     int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
                     if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
@@ -374,9 +386,15 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
                 int sat = 0;
                 if (val) {
                     const int bxs = q.bx4 + (sub & ((1 << lw4) - 1)), bys = q.by4 + (sub >> lw4);
-                    sat = subblock_satd(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had);
+                    sat = pass == 0 ? subblock_satd<true>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had)
+                                    : subblock_satd<false>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had);
                 }
-                for (int m = 1; m < nsub; m <<= 1) sat += __shfl_xor(sat, m, 64);
+                // sum over the aligned nsub-lane group (4, 8 or 16) by DPP: lane ^ 1, ^ 2 (quad
+                // permutes), then mirror within 8 and within 16 lanes (each pairs the group's halves)
+                sat += dpp<0xB1>(sat);
+                sat += dpp<0x4E>(sat);
+                if (nsub >= 8) sat += dpp<0x141>(sat);
+                if (nsub >= 16) sat += dpp<0x140>(sat);
                 if (val && sub == 0) {
                     int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
                     if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
