@@ -438,16 +438,17 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
 #pragma unroll
         for (int j = 0; j < NS; j++) { pmx[j] = s.pmv[j][0]; pmy[j] = s.pmv[j][1]; }
     } else {
-        int mx = 0, my = 0;
-        if (lane < NS) {
-            SDesc q = sd[0];
+        // wave j computes search j's MVP (wave-uniform code for a constant block), then LDS
 #pragma unroll
-            for (int j = 1; j < NS; j++)
-                if (lane == j) q = sd[j];
-            set_mvp(NbMe{s, q.bt, b8, best8x8}, q.bx4, q.by4, 4 << lw4_of(q.bt), 4 << lh4_of(q.bt), mx, my);
-        }
+        for (int j = 0; j < NS; j++)
+            if (wave == j) {
+                int mx, my;
+                set_mvp(NbMe{s, sd[j].bt, b8, best8x8}, sd[j].bx4, sd[j].by4, 4 << lw4_of(sd[j].bt), 4 << lh4_of(sd[j].bt), mx, my);
+                if (lane == 0) { s.pmv[j][0] = mx; s.pmv[j][1] = my; }
+            }
+        __syncthreads();
 #pragma unroll
-        for (int j = 0; j < NS; j++) { pmx[j] = __builtin_amdgcn_readlane(mx, j); pmy[j] = __builtin_amdgcn_readlane(my, j); }
+        for (int j = 0; j < NS; j++) { pmx[j] = s.pmv[j][0]; pmy[j] = s.pmv[j][1]; }
     }
     ev(bk, pmx, pmy);
 #pragma unroll
