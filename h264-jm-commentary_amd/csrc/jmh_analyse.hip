@@ -35,6 +35,7 @@
 #define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
 #define MVB_LEN 1104
 #define PLS (WIN_DIM_MAX * WST + 32)          // stride between the G, b, h, j planes
+#define MAXNS 7                               // searches per stage (block 0 stage 0: 3 + 4)
 
 // Intra4x4 prediction (8.3.1.2) of mode m at pixel l as a formula over P[0..12]
 // (P[0] = p[-1,-1], P[1+i] = p[i,-1], P[9+j] = p[-1,j]): type | a << 2 | b << 6 | c << 10,
@@ -73,11 +74,14 @@ struct MeS {
     IntraNb nb;
     int16_t all_mv[8][16][2];
     int motion_cost[8][4];
-    unsigned red[NTA / 64][4];                // per wave, per search of the stage: argmin keys
-    int pmv[4][2];                            // MVPs of the next stage's searches (forwarded)
+    unsigned red[NTA / 64][MAXNS];            // per wave, per search of the stage: argmin keys
+    int pmv[MAXNS][2];                        // MVPs of the next stage's searches (forwarded)
     uint16_t mvc[MVB_LEN];                    // lambda * mvbits(v) at [v + MVB_OFF] (|v| <= 4*2*SR + 259)
     uint8_t planes[4 * PLS];                  // G (the window), b, h, j
-    int16_t h1[WIN_DIM_MAX * WST];            // unclipped vertical 6-tap intermediates
+    union {
+        int16_t h1[WIN_DIM_MAX * WST];        // unclipped vertical 6-tap intermediates (planes only)
+        uint2 sad8[NPK * NTA];                // then: the 8x8 SADs of every thread's positions,
+    } hs;                                     //   [k][thread] (16x16 / 16x8 / 8x16 searches)
     unsigned long long *pst;                  // debug: per-stage stamps (thread 0), null when off
     int pn;
     IntraS in;                                // the MB's intra decisions, run by waves 6 and 7
@@ -172,6 +176,7 @@ __device__ __forceinline__ void fence_state(PosState &ps) {
     }
 #pragma unroll
     for (int k = 0; k < NPK / 2; k++) asm volatile("" : "+v"(ps.ordk2[k]));
+    asm volatile("" : "+v"(ps.dx), "+v"(ps.dy0));   // nor position arithmetic (RestrictSearchRange 0)
 }
 
 // order key of position k, sign-extended: a slot outside the table gives 0xFFFFFFFF, which ORed
@@ -185,22 +190,22 @@ __device__ __forceinline__ uint32_t ordk_of(const PosState &ps, int k) {
 // cost = SAD + lambda*(mvbits(x) + mvbits(y)) from the LDS mvbits table; 'range' < sr only with
 // RestrictSearchRange 0 (positions outside are skipped, the (0,0) pre-check never is)
 template <int BT, int BX, int BY>
-__device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps, int sr, int range, int lam, int pmx, int pmy, int scx,
-                                                int scy) {
+__device__ __forceinline__ unsigned eval_search(const MeS &s, const PosState &ps, const uint32_t (&sp)[NPK][2], int sr, int range, int pmx,
+                                                int pmy, int scx, int scy) {
     const unsigned cxv = s.mvc[4 * (scx - sr + ps.dx) - pmx + MVB_OFF];
     const uint16_t *cy = s.mvc + 4 * (scy - sr + ps.dy0) - pmy + MVB_OFF;
     unsigned b = 0xFFFFFFFFu;
     if (range >= sr) {
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
-            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + cy[4 * k];
+            const unsigned cost = psum<BT, BX, BY>(sp[k]) + cxv + cy[4 * k];
             b = min(b, (cost << 13) | ordk_of(ps, k));
         }
     } else {
         const int rx = abs(ps.dx - sr);
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
-            const unsigned cost = psum<BT, BX, BY>(ps.sadp[k]) + cxv + cy[4 * k];
+            const unsigned cost = psum<BT, BX, BY>(sp[k]) + cxv + cy[4 * k];
             const uint32_t o = ordk_of(ps, k);
             const bool in = max(rx, abs(ps.dy0 + k - sr)) <= range || o == 0;
             b = min(b, in ? (cost << 13) | o : 0xFFFFFFFFu);
@@ -436,7 +441,10 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
     unsigned bk[NS];
     if constexpr (FWD) {
 #pragma unroll
-        for (int j = 0; j < NS; j++) { pmx[j] = s.pmv[j][0]; pmy[j] = s.pmv[j][1]; }
+        for (int j = 0; j < NS; j++) {   // uniform: SGPRs
+            pmx[j] = __builtin_amdgcn_readfirstlane(s.pmv[j][0]);
+            pmy[j] = __builtin_amdgcn_readfirstlane(s.pmv[j][1]);
+        }
     } else {
         // wave j computes search j's MVP (wave-uniform code for a constant block), then LDS
 #pragma unroll
@@ -448,7 +456,10 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
             }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < NS; j++) { pmx[j] = s.pmv[j][0]; pmy[j] = s.pmv[j][1]; }
+        for (int j = 0; j < NS; j++) {   // uniform: SGPRs
+            pmx[j] = __builtin_amdgcn_readfirstlane(s.pmv[j][0]);
+            pmy[j] = __builtin_amdgcn_readfirstlane(s.pmv[j][1]);
+        }
     }
     ev(bk, pmx, pmy);
 #pragma unroll
@@ -466,7 +477,48 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
     sstamp(s, wave);
 }
 
-#define EV(J, BT, BX, BY) bk[J] = eval_search<BT, BX, BY>(s, ps, sr, search_range(d, BT), lam, pmx[J], pmy[J], ps.scx, ps.scy)
+#define EV(J, BT, BX, BY) bk[J] = eval_search<BT, BX, BY>(s, ps, ps.sadp, sr, search_range(d, BT), pmx[J], pmy[J], ps.scx, ps.scy)
+
+// up to three searches on the 8x8 SADs kept in LDS (16x16 / 16x8 / 8x16): one LDS read per
+// position shared by the searches, so only two SAD registers are live at a time.  Search j is
+// (BT[j], BX[j], BY[j]); keys as eval_search.
+template <int N, int BT0, int BX0, int BY0, int BT1, int BX1, int BY1, int BT2 = 0, int BX2 = 0, int BY2 = 0>
+__device__ __forceinline__ void eval_sad8(const MeS &s, const PosState &ps, int tid, int sr, const int (&range)[N], const int *pmx,
+                                          const int *pmy, unsigned *out) {
+    unsigned cxv[N];
+    const uint16_t *cy[N];
+    bool full = true;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        cxv[j] = s.mvc[4 * (ps.scx - sr + ps.dx) - pmx[j] + MVB_OFF];
+        cy[j] = s.mvc + 4 * (ps.scy - sr + ps.dy0) - pmy[j] + MVB_OFF;
+        out[j] = 0xFFFFFFFFu;
+        full = full && range[j] >= sr;
+    }
+    auto loop = [&](auto restricted) {
+        const int rx = abs(ps.dx - sr);
+#pragma unroll
+        for (int k = 0; k < NPK; k++) {
+            const uint2 v = s.hs.sad8[k * NTA + tid];
+            const uint32_t r[2] = {v.x, v.y};
+            const uint32_t o = ordk_of(ps, k);
+            unsigned c[3];
+            c[0] = psum<BT0, BX0, BY0>(r);
+            c[1] = psum<BT1, BX1, BY1>(r);
+            if constexpr (N > 2) c[2] = psum<BT2, BX2, BY2>(r);
+#pragma unroll
+            for (int j = 0; j < N; j++) {
+                const unsigned key = ((c[j] + cxv[j] + cy[j][4 * k]) << 13) | o;
+                if constexpr (decltype(restricted)::value)
+                    out[j] = min(out[j], (max(rx, abs(ps.dy0 + k - sr)) <= range[j] || o == 0) ? key : 0xFFFFFFFFu);
+                else
+                    out[j] = min(out[j], key);
+            }
+        }
+    };
+    if (full) loop(std::false_type{});
+    else loop(std::true_type{});   // RestrictSearchRange 0: positions outside a type's range
+}
 
 // SADs at this thread's NPK positions (column strip dx, rows dy0..dy0+NPK-1 of the window) of the
 // 8x8 org block at pixel (OX, OY).  EIGHT: the 8x8 SAD into half HI of ps.sadp[k][SLOT] (role 1);
@@ -506,37 +558,66 @@ __device__ __forceinline__ void sad_strip(const MeS &s, PosState &ps) {
 }
 
 // one 8x8 block of P8x8: its 4x4 SADs, 4 stages (sub-modes 4..7 in parallel, then the 4x4
-// chain), then the P8x8 sub-mode decision for the block (its MVs are read through best8x8)
+// chain), then the P8x8 sub-mode decision for the block (its MVs are read through best8x8).
+// Block 0 also runs the 16x16 / 16x8 / 8x16 searches, which are independent of P8x8: the first
+// blocks of each type in its stage 0, the second ones in its stage 1 (on the 8x8 SADs in LDS).
+// Intra4x4 slots (waves 6, 7): stage 0 of block 0 has no free waves.
 template <int B8, class IDLE>
-__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8, IDLE idle, int wave) {
+__device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8, IDLE idle, int wave, int tid) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
-    const int sr = d.sr, lam = d.lambda_motion;
+    constexpr int IS0 = B8 == 0 ? -1 : 2 * B8 + 1, IS1 = B8 == 0 ? 0 : 2 * B8 + 2;
+    constexpr int IS2 = B8 == 0 ? 1 : B8 == 3 ? 9 : -1, IS3 = B8 == 0 ? 2 : B8 == 3 ? 10 : -1;
+    const int sr = d.sr;
     fence_state(ps);
     sad_strip<false, 4 * X, 4 * Y, 0, 0>(s, ps);        // the four 4x4 SADs of this 8x8 block
-    {   // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left
-        const SDesc sd[4] = {{4, X, Y, B8, 0, 0, 0, 0},
+    if constexpr (B8 == 0) {
+        // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left + 16x16, 16x8 upper, 8x16 left
+        const SDesc sd[7] = {{4, X, Y, B8, 0, 0, 0, 0},
                              {5, X, Y, B8, 5, X, Y + 1, 0},
                              {6, X, Y, B8, 6, X + 1, Y, 1},
-                             {7, X, Y, B8, 7, X + 1, Y, 2}};
-        me_stage<4, false>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[4], const int (&pmx)[4], const int (&pmy)[4]) {
+                             {7, X, Y, B8, 7, X + 1, Y, 2},
+                             {1, 0, 0, 0, 0, 0, 0, 0},
+                             {2, 0, 0, 0, 2, 0, 2, 3},
+                             {3, 0, 0, 0, 3, 2, 0, 4}};
+        me_stage<7, false>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[7], const int (&pmx)[7], const int (&pmy)[7]) {
             EV(0, 4, X, Y); EV(1, 5, X, Y); EV(2, 6, X, Y); EV(3, 7, X, Y);
-        }, 2 + 2 * B8, idle, wave);
-    }
-    {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right
-        const SDesc sd[3] = {{5, X, Y + 1, B8, 0, 0, 0, 0}, {6, X + 1, Y, B8, 0, 0, 0, 0}, {7, X + 1, Y, B8, 7, X, Y + 1, 0}};
-        me_stage<3, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
+            const int rg[3] = {search_range(d, 1), search_range(d, 2), search_range(d, 3)};
+            eval_sad8<3, 1, 0, 0, 2, 0, 0, 3, 0, 0>(s, ps, tid, sr, rg, pmx + 4, pmy + 4, bk + 4);
+        }, IS0, idle, wave);
+        // stage 1: 8x4 lower, 4x8 right, 4x4 top-right + 16x8 lower, 8x16 right
+        const SDesc sd1[5] = {{5, X, Y + 1, B8, 0, 0, 0, 0}, {6, X + 1, Y, B8, 0, 0, 0, 0}, {7, X + 1, Y, B8, 7, X, Y + 1, 0},
+                              {2, 0, 2, 1, 0, 0, 0, 0}, {3, 2, 0, 1, 0, 0, 0, 0}};
+        me_stage<5, true>(d, s, ps, sd1, B8, best8x8, [&](unsigned (&bk)[5], const int (&pmx)[5], const int (&pmy)[5]) {
             EV(0, 5, X, Y + 1); EV(1, 6, X + 1, Y); EV(2, 7, X + 1, Y);
-        }, 3 + 2 * B8, idle, wave);
+            const int rg[2] = {search_range(d, 2), search_range(d, 3)};
+            eval_sad8<2, 2, 0, 2, 3, 2, 0>(s, ps, tid, sr, rg, pmx + 3, pmy + 3, bk + 3);
+        }, IS1, idle, wave);
+    } else {
+        {   // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left
+            const SDesc sd[4] = {{4, X, Y, B8, 0, 0, 0, 0},
+                                 {5, X, Y, B8, 5, X, Y + 1, 0},
+                                 {6, X, Y, B8, 6, X + 1, Y, 1},
+                                 {7, X, Y, B8, 7, X + 1, Y, 2}};
+            me_stage<4, false>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[4], const int (&pmx)[4], const int (&pmy)[4]) {
+                EV(0, 4, X, Y); EV(1, 5, X, Y); EV(2, 6, X, Y); EV(3, 7, X, Y);
+            }, IS0, idle, wave);
+        }
+        {   // stage 1: 8x4 lower, 4x8 right, 4x4 top-right
+            const SDesc sd[3] = {{5, X, Y + 1, B8, 0, 0, 0, 0}, {6, X + 1, Y, B8, 0, 0, 0, 0}, {7, X + 1, Y, B8, 7, X, Y + 1, 0}};
+            me_stage<3, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
+                EV(0, 5, X, Y + 1); EV(1, 6, X + 1, Y); EV(2, 7, X + 1, Y);
+            }, IS1, idle, wave);
+        }
     }
     {   // stage 2: 4x4 bottom-left
         const SDesc sd[1] = {{7, X, Y + 1, B8, 7, X + 1, Y + 1, 0}};
         me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X, Y + 1); },
-                          B8 == 3 ? 10 : -1, idle, wave);
+                          IS2, idle, wave);
     }
     {   // stage 3: 4x4 bottom-right
         const SDesc sd[1] = {{7, X + 1, Y + 1, B8, 0, 0, 0, 0}};
         me_stage<1, true>(d, s, ps, sd, B8, best8x8, [&](unsigned (&bk)[1], const int (&pmx)[1], const int (&pmy)[1]) { EV(0, 7, X + 1, Y + 1); },
-                          -1, idle, wave);
+                          IS3, idle, wave);
     }
     int mc8 = BIGCOST, bm = 0;
     for (int mode = 4; mode <= 7; mode++) {
@@ -742,7 +823,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         const int cx = c0 + i;
-                        s.h1[y * WST + cx] = (int16_t)hv[i];
+                        s.hs.h1[y * WST + cx] = (int16_t)hv[i];
                         { PH[y * WST + cx] = (uint8_t)(ph >> (8 * i)); PB[y * WST + cx] = (uint8_t)(pb >> (8 * i)); }
                     }
                     w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5;
@@ -751,7 +832,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
             __syncthreads();
             PSTAMP(10);
             for (int y = y0; y < y1; y++) {   // j = clip((6-tap of h1 + 512) >> 10), 32-bit taps
-                const uint32_t *hr = reinterpret_cast<const uint32_t *>(s.h1 + y * WST + c0);
+                const uint32_t *hr = reinterpret_cast<const uint32_t *>(s.hs.h1 + y * WST + c0);
                 const uint32_t q0 = hr[-1], q1 = hr[0], q2 = hr[1], q3 = hr[2], q4 = hr[3];
                 const int x[9] = {(int)(int16_t)q0, (int)q0 >> 16, (int)(int16_t)q1, (int)q1 >> 16, (int)(int16_t)q2,
                                   (int)q2 >> 16, (int)(int16_t)q3, (int)q3 >> 16, (int)(int16_t)q4};
@@ -763,59 +844,36 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
                 for (int i = 0; i < 4; i++)
                     PJ[y * WST + c0 + i] = (uint8_t)(jv >> (8 * i));
             }
-            // j is first read after the next stage's barriers
         }
+        __syncthreads();   // h1 is dead: its LDS holds the 8x8 SADs from here on
         PSTAMP(2);
-        {   // ---- 16x16, 16x8, 8x16
-            const int lam = d.lambda_motion;
-            {   // stage 0: 16x16, 16x8 upper, 8x16 left
-                const SDesc sd[3] = {{1, 0, 0, 0, 0, 0, 0, 0}, {2, 0, 0, 0, 2, 0, 2, 0}, {3, 0, 0, 0, 3, 2, 0, 1}};
-                me_stage<3, false>(d, s, ps, sd, 0, 0, [&](unsigned (&bk)[3], const int (&pmx)[3], const int (&pmy)[3]) {
-                    EV(0, 1, 0, 0); EV(1, 2, 0, 0); EV(2, 3, 0, 0);
-                }, 0, idle, wave);
-            }
-            {   // stage 1: 16x8 lower, 8x16 right
-                const SDesc sd[2] = {{2, 0, 2, 1, 0, 0, 0, 0}, {3, 2, 0, 1, 0, 0, 0, 0}};
-                me_stage<2, true>(d, s, ps, sd, 0, 0, [&](unsigned (&bk)[2], const int (&pmx)[2], const int (&pmy)[2]) {
-                    EV(0, 2, 0, 2); EV(1, 3, 2, 0);
-                }, 1, idle, wave);
-            }
-            // results: MVs of types 1..3, partition costs, FindSkipModeMotionVector
-            const int tid = 64 * wave + __lane_id();
-            if (tid < 96) {
+#pragma unroll
+        for (int k = 0; k < NPK; k++) s.hs.sad8[k * NTA + tid] = make_uint2(ps.sadp[k][0], ps.sadp[k][1]);
+        {   // ---- P8x8 (4 x 4 stages), the 16x16 / 16x8 / 8x16 searches inside block 0's stages 0, 1
+            int best8x8 = 0, cost8x8 = 0;
+            p8x8_block<0>(d, s, ps, best8x8, cost8x8, idle, wave, tid);
+            PSTAMP(3);
+            p8x8_block<1>(d, s, ps, best8x8, cost8x8, idle, wave, tid);
+            PSTAMP(4);
+            p8x8_block<2>(d, s, ps, best8x8, cost8x8, idle, wave, tid);
+            PSTAMP(5);
+            p8x8_block<3>(d, s, ps, best8x8, cost8x8, idle, wave, tid);
+            // results: MVs of types 1..7, partition costs, P8x8 modes, FindSkipModeMotionVector
+            if (tid < 224) {
                 const int m = 1 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
                 scr->all_mv[m][k][c] = s.all_mv[m][k][c];
-            } else if (tid >= 128 && tid < 140) {
-                const int m = 1 + (tid - 128) / 4, k = tid & 3;
+            } else if (tid < 252) {
+                const int m = 1 + (tid - 224) / 4, k = tid & 3;
                 scr->motion_cost[m][k] = s.motion_cost[m][k];
-            } else if (tid == 192) {
+            } else if (tid == 256) {
+                scr->best8x8 = best8x8; scr->cost8x8 = cost8x8;
+            } else if (tid == 320) {
                 NbBorder nbv{s.bd};
                 int ra = -1, ax = 0, ay = 0, rb = -1, bx = 0, by = 0;
                 const bool aa = nbv(-1, 0, ra, ax, ay), ab = nbv(0, -1, rb, bx, by);
                 const bool zl = !aa || (ra == 0 && ax == 0 && ay == 0), za = !ab || (rb == 0 && bx == 0 && by == 0);
                 scr->skipx = (za || zl) ? 0 : pcx;
                 scr->skipy = (za || zl) ? 0 : pcy;
-            }
-        }
-        PSTAMP(7);
-        {   // ---- P8x8: 4 x 4 stages
-            int best8x8 = 0, cost8x8 = 0;
-            p8x8_block<0>(d, s, ps, best8x8, cost8x8, idle, wave);
-            PSTAMP(3);
-            p8x8_block<1>(d, s, ps, best8x8, cost8x8, idle, wave);
-            PSTAMP(4);
-            p8x8_block<2>(d, s, ps, best8x8, cost8x8, idle, wave);
-            PSTAMP(5);
-            p8x8_block<3>(d, s, ps, best8x8, cost8x8, idle, wave);
-            const int tid = 64 * wave + __lane_id();
-            if (tid < 128) {
-                const int m = 4 + tid / 32, k = (tid & 31) >> 1, c = tid & 1;
-                scr->all_mv[m][k][c] = s.all_mv[m][k][c];
-            } else if (tid < 144) {
-                const int m = 4 + (tid - 128) / 4, k = tid & 3;
-                scr->motion_cost[m][k] = s.motion_cost[m][k];
-            } else if (tid == 192) {
-                scr->best8x8 = best8x8; scr->cost8x8 = cost8x8;
             }
             PSTAMP(6);
         }
