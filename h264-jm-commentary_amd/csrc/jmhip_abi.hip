@@ -93,6 +93,8 @@ struct PicBuf {
     jmh_mb_result *h_res;                // pinned host copies (allocated on first readback use)
     uint8_t *h_src, *h_rec, *h_dbk;
     hipEvent_t ev_src, ev_t0, ev_done;   // staging reuse / push..done timing
+    hipEvent_t ev_fin;                   // the picture's last tick (the copy stream's readback waits)
+    int recon_read;                      // h_rec holds the occupant's reconstruction
     int unpopped;                        // readback picture not yet popped
     int deblocked;                       // the occupant was deblocked on the device (dbk valid)
 };
@@ -111,7 +113,8 @@ enum { REF_NONE, REF_BUF, REF_REC, REF_DBK };
 struct jmh_ctx {
     jmh_config cfg;
     int dev;
-    hipStream_t st;
+    hipStream_t st;                      // the wavefront ticks (and source uploads)
+    hipStream_t cst;                     // readback of finished pictures, overlapping later ticks
     int W, H, Wc, Hc, mbw, mbh, sr, side, npos, qstride, qplane, nd;
     size_t fsize, n4, nmb;               // bytes of one 4:2:0 picture (Y then U then V)
     uint8_t *d_ref, *d_qpel, *d_slots;   // explicit reference (set_reference), a1 seam, slots
@@ -176,7 +179,7 @@ static void free_entry(PicBuf &b) {
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     void *host_bufs[] = {b.h_res, b.h_src, b.h_rec, b.h_dbk};
     for (void *p : host_bufs) if (p) (void)hipHostFree(p);
-    hipEvent_t evs[] = {b.ev_src, b.ev_t0, b.ev_done};
+    hipEvent_t evs[] = {b.ev_src, b.ev_t0, b.ev_done, b.ev_fin};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
 }
 
@@ -190,7 +193,8 @@ static int alloc_entry(jmh_ctx *c, PicBuf &b) {
 #undef ALLOC
     if (hipMemset(b.rec, 0, c->fsize) != hipSuccess || hipMemset(b.dbk, 0, c->fsize) != hipSuccess) return JMH_E_HIP;
     if (hipEventCreate(&b.ev_src) != hipSuccess || hipEventCreate(&b.ev_t0) != hipSuccess ||
-        hipEventCreate(&b.ev_done) != hipSuccess) return JMH_E_HIP;
+        hipEventCreate(&b.ev_done) != hipSuccess || hipEventCreateWithFlags(&b.ev_fin, hipEventDisableTiming) != hipSuccess)
+        return JMH_E_HIP;
     return JMH_OK;
 }
 
@@ -231,6 +235,7 @@ void jmh_destroy(jmh_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
+    if (c->cst) (void)hipStreamSynchronize(c->cst);
     for (PicBuf &b : c->ring) free_entry(b);
     void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
@@ -240,6 +245,7 @@ void jmh_destroy(jmh_ctx *c) {
     ring_free(c->ring_an);
     ring_free(c->ring_fin);
     if (c->st) (void)hipStreamDestroy(c->st);
+    if (c->cst) (void)hipStreamDestroy(c->cst);
     delete c;
 }
 
@@ -279,7 +285,8 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     int st = JMH_OK;
 #define ALLOC(p, n) do { if (hipMalloc((void **)&(p), (n)) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
     {
-        if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         ALLOC(c->d_ref, c->fsize);
         ALLOC(c->d_qpel, (size_t)16 * c->qplane);
         ALLOC(c->d_slots, c->fsize * c->nslots);
@@ -380,15 +387,20 @@ static int skip_empty(const jmh_ctx *c, int stage) {
     return stage;
 }
 
-// after a picture's last tick: enqueue its readback, mark the done event
+// after a picture's last tick: its readback on the copy stream (the D2H overlaps the ticks of
+// the pictures still in flight; the entry's device buffers are not written again before the host
+// has popped the picture, which waits for ev_done), then the done event
 static int finish_picture(jmh_ctx *c, const Flight &f) {
     c->timing.pictures_done++;
     if (!f.readback) return JMH_OK;
     PicBuf &b = c->ring[f.entry];
-    HCHK(hipMemcpyAsync(b.h_res, b.res, c->nmb * sizeof(jmh_mb_result), hipMemcpyDeviceToHost, c->st));
-    HCHK(hipMemcpyAsync(b.h_rec, b.rec, c->fsize, hipMemcpyDeviceToHost, c->st));
-    if (f.pp.dbk) HCHK(hipMemcpyAsync(b.h_dbk, b.dbk, c->fsize, hipMemcpyDeviceToHost, c->st));
-    HCHK(hipEventRecord(b.ev_done, c->st));
+    HCHK(hipEventRecord(b.ev_fin, c->st));
+    HCHK(hipStreamWaitEvent(c->cst, b.ev_fin, 0));
+    HCHK(hipMemcpyAsync(b.h_res, b.res, c->nmb * sizeof(jmh_mb_result), hipMemcpyDeviceToHost, c->cst));
+    b.recon_read = !(f.pp.dbk && (c->cfg.flags & JMH_FLAG_NO_RECON_READBACK));
+    if (b.recon_read) HCHK(hipMemcpyAsync(b.h_rec, b.rec, c->fsize, hipMemcpyDeviceToHost, c->cst));
+    if (f.pp.dbk) HCHK(hipMemcpyAsync(b.h_dbk, b.dbk, c->fsize, hipMemcpyDeviceToHost, c->cst));
+    HCHK(hipEventRecord(b.ev_done, c->cst));
     return JMH_OK;
 }
 
@@ -649,7 +661,7 @@ const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *c, int mb_addr) {
 
 int jmh_read_recon(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
     if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
-    if (c->cur_entry < 0) return JMH_E_STATE;
+    if (c->cur_entry < 0 || !c->ring[c->cur_entry].recon_read) return JMH_E_STATE;
     unpack_planes(c->ring[c->cur_entry].h_rec, c->W, c->H, y, u, v, sy, sc);
     return JMH_OK;
 }

@@ -61,6 +61,7 @@ static const map_entry Map[] = {
     {"HIPDevice", 0, OFF(hip_device), 0, 63},
     {"PipelineDepth", 0, OFF(pipeline_depth), 0, 20},
     {"JMCallSurface", 0, OFF(jm_call_surface), 0, 1},
+    {"WriterThreads", 0, OFF(writer_threads), 0, 64},
     {NULL, 0, 0, 0, 0}};
 #undef OFF
 
@@ -81,6 +82,7 @@ void jm_input_defaults(jm_input *inp) {
     inp->profile_idc = 66;
     inp->level_idc = 40;
     inp->frame_rate = 30;
+    inp->writer_threads = 4;
 }
 
 int jm_set_param(jm_input *inp, const char *key, const char *val, char *err, int errlen) {

@@ -6,6 +6,7 @@
  * the backend), write the recon, print JM's per-frame report line.
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -25,15 +26,21 @@ int jm_lambda_rdo_off(int qp) {
     return QP2QUANT[i < 0 ? 0 : i];
 }
 
+/* squared error summed in integers (per row in 32 bits: 65025 * w < 2^32 for w < 66051), so
+   the value equals JM's double accumulation of integer squares exactly */
 static double psnr(const uint8_t *a, int sa, const uint8_t *b, int sb, int w, int h) {
-    double se = 0;
-    for (int y = 0; y < h; y++)
+    uint64_t se = 0;
+    for (int y = 0; y < h; y++) {
+        const uint8_t *pa = a + (size_t)y * sa, *pb = b + (size_t)y * sb;
+        uint32_t r = 0;
         for (int x = 0; x < w; x++) {
-            int d = a[y * sa + x] - b[y * sb + x];
-            se += d * d;
+            const int d = pa[x] - pb[x];
+            r += (uint32_t)(d * d);
         }
+        se += r;
+    }
     if (se == 0) return 99.0;
-    return 10.0 * log10(255.0 * 255.0 * w * h / se);
+    return 10.0 * log10(255.0 * 255.0 * w * h / (double)se);
 }
 
 /* slice.c › encode_one_slice [J]: the macroblock loop of one picture (one slice) through the JM
@@ -52,6 +59,92 @@ static int encode_one_slice(jm86_img *im, const jm_seq *s, const jm_slice *sl, c
     }
     jm_slice_end(w);
     return JMH_OK;
+}
+
+/* ---- parallel slice writing (WriterThreads > 0, pipelined device backend) -------------------
+ * The slices of different pictures are independent once their macroblock results exist (one
+ * slice per picture, device deblocking), so popped pictures are written by a pool of threads,
+ * each with its own JM state (img is thread-local), and emitted in picture order.  The main
+ * thread keeps the device busy: pop, copy the results and the deblocked picture into a job,
+ * push the next picture. */
+typedef struct wjob {
+    jm86_img im;                 /* the job's JM state; im.mb_data holds the picture's results   */
+    jm_pic rec;                  /* its deblocked reconstruction                                 */
+    const jm_pic *cur;           /* its source (pend slot, not refilled before the job is flushed) */
+    jmh_frame_params fp;
+    jm_slice sl;
+    int f, is_i;
+    double met;                  /* backend time charged to the picture (report line)           */
+    jm_bits out;                 /* NAL unit                                                     */
+    long pic_bits;
+    double py, pu, pv, write_ms;
+    int status, state;           /* state: 0 idle, 1 queued, 2 running, 3 done                   */
+} wjob_t;
+
+typedef struct wpool {
+    pthread_mutex_t mu;
+    pthread_cond_t cv_work, cv_done;
+    wjob_t *jobs;
+    int nj, stop;
+    int *queue, qh, qt;          /* job indices, FIFO */
+    const jm_seq *s;
+    const jm_input *inp;
+    pthread_t *th;
+    int nth;
+} wpool_t;
+
+static int encode_one_slice(jm86_img *im, const jm_seq *s, const jm_slice *sl, const jmh_frame_params *fp, const jm_pic *cur,
+                            const jm_pic *ref, jm_bits *rbsp);
+
+static void job_run(wpool_t *P, wjob_t *j) {
+    const jm_seq *s = P->s;
+    const jm_input *inp = P->inp;
+    const int W = s->width;
+    double t0 = now_ms();
+    jm_bits rbsp;
+    jm_bits_init(&rbsp);
+    j->status = encode_one_slice(&j->im, s, &j->sl, &j->fp, j->cur, &j->rec, &rbsp);
+    j->out.len = 0;
+    if (!j->status) jm_write_nal(&j->out, j->sl.idr ? 3 : 2, j->sl.idr ? 5 : 1, &rbsp);
+    jm_bits_free(&rbsp);
+    j->pic_bits = j->out.len * 8;
+    j->py = psnr(j->cur->y, W, j->rec.y, W, inp->width, inp->height);
+    j->pu = psnr(j->cur->u, W / 2, j->rec.u, W / 2, inp->width / 2, inp->height / 2);
+    j->pv = psnr(j->cur->v, W / 2, j->rec.v, W / 2, inp->width / 2, inp->height / 2);
+    j->write_ms = now_ms() - t0;
+}
+
+static void *writer_main(void *arg) {
+    wpool_t *P = (wpool_t *)arg;
+    for (;;) {
+        pthread_mutex_lock(&P->mu);
+        while (!P->stop && P->qh == P->qt) pthread_cond_wait(&P->cv_work, &P->mu);
+        if (P->qh == P->qt) { pthread_mutex_unlock(&P->mu); return NULL; }   /* stop, queue drained */
+        wjob_t *j = &P->jobs[P->queue[P->qh % P->nj]];
+        P->qh++;
+        j->state = 2;
+        pthread_mutex_unlock(&P->mu);
+        job_run(P, j);
+        pthread_mutex_lock(&P->mu);
+        j->state = 3;
+        pthread_cond_broadcast(&P->cv_done);
+        pthread_mutex_unlock(&P->mu);
+    }
+}
+
+static void pool_submit(wpool_t *P, int k) {
+    pthread_mutex_lock(&P->mu);
+    P->jobs[k].state = 1;
+    P->queue[P->qt % P->nj] = k;
+    P->qt++;
+    pthread_cond_signal(&P->cv_work);
+    pthread_mutex_unlock(&P->mu);
+}
+
+static void pool_wait(wpool_t *P, int k) {
+    pthread_mutex_lock(&P->mu);
+    while (P->jobs[k].state != 3) pthread_cond_wait(&P->cv_done, &P->mu);
+    pthread_mutex_unlock(&P->mu);
 }
 
 int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *log) {
@@ -85,16 +178,43 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     const int dev_dbk = be->read_deblocked && be->reference_deblocked;
     const int pipelined = dev_dbk && be->push && be->pop && be->depth > 1;
     const int depth = pipelined ? be->depth : 1;
+    /* parallel slice writing: pipelined device backend, not with the call surface's per-MB
+       device searches (those share the context with the frame loop) */
+    const int nwr = (pipelined && !inp->jm_call_surface) ? inp->writer_threads : 0;
+    const int nj = nwr ? 2 * nwr : 0;                  /* jobs in flight: queued + running + done */
+    const int plen = depth + nj + 1;                   /* source slots: a job's source stays put */
     typedef struct { jm_pic cur; jmh_frame_params fp; int f, is_i, frame_num; } pend_t;
-    pend_t *pend = (pend_t *)calloc(depth, sizeof(pend_t));
+    pend_t *pend = (pend_t *)calloc(plen, sizeof(pend_t));
     jm_pic rec;
     int alloc_fail = !pend || jm_pic_alloc(&rec, W, H);
-    for (int k = 0; k < depth && !alloc_fail; k++) alloc_fail = jm_pic_alloc(&pend[k].cur, W, H);
+    for (int k = 0; k < plen && !alloc_fail; k++) alloc_fail = jm_pic_alloc(&pend[k].cur, W, H);
     if (alloc_fail) return JMH_E_OOM;
     int nmb = s.mbw * s.mbh;
     const jmh_mb_result **res = (const jmh_mb_result **)malloc(sizeof(*res) * nmb);
     jm86_img im;
     if (!res || jm86_init(&im, inp, be, W, H)) return JMH_E_OOM;
+    wpool_t pool;
+    memset(&pool, 0, sizeof(pool));
+    if (nwr) {
+        pool.nj = nj; pool.s = &s; pool.inp = inp; pool.nth = nwr;
+        pool.jobs = (wjob_t *)calloc(nj, sizeof(wjob_t));
+        pool.queue = (int *)calloc(nj, sizeof(int));
+        pool.th = (pthread_t *)calloc(nwr, sizeof(pthread_t));
+        if (!pool.jobs || !pool.queue || !pool.th) return JMH_E_OOM;
+        for (int k = 0; k < nj; k++) {
+            if (jm86_init(&pool.jobs[k].im, inp, be, W, H) || jm_pic_alloc(&pool.jobs[k].rec, W, H)) return JMH_E_OOM;
+            pool.jobs[k].im.res = pool.jobs[k].im.mb_data;   /* results copied in at pop */
+            jm_bits_init(&pool.jobs[k].out);
+        }
+        img = &im;   /* jm86_init of the jobs set this thread's img */
+        pthread_mutex_init(&pool.mu, NULL);
+        pthread_cond_init(&pool.cv_work, NULL);
+        pthread_cond_init(&pool.cv_done, NULL);
+        for (int k = 0; k < nwr; k++)
+            if (pthread_create(&pool.th[k], NULL, writer_main, &pool)) return JMH_E_OOM;
+    }
+    long jseq = 0, jflushed = 0;   /* jobs submitted / emitted (picture order) */
+    double copy_ms = 0, write_ms = 0;
     jm_bits out, rbsp;
     jm_bits_init(&out); jm_bits_init(&rbsp);
     jm_write_sps(&rbsp, &s); jm_write_nal(&out, 3, 7, &rbsp); jm_bits_free(&rbsp);
@@ -105,15 +225,57 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     out.len = 0;
     if (log) {
         fprintf(log, "------------------------------- MI355X jm-hot-path lencod (%s) -------------------------------\n", be->name);
-        if (pipelined) fprintf(log, " (%d pictures in flight)\n", depth);
+        if (pipelined) fprintf(log, " (%d pictures in flight%s)\n", depth, nwr ? ", parallel slice writing" : "");
+        if (nwr) fprintf(log, " (%d slice-writer threads)\n", nwr);
         fprintf(log, " Frame  Bit/pic  QP   SnrY    SnrU    SnrV    Time(ms) MET(ms) Frm/Fld  I D\n");
     }
     double t_start = now_ms();
     int st_ret = 0, frame_num = 0, head = 0, count = 0;
     /* the rest of encode_one_frame for a picture whose macroblock results are available:
        slice (CAVLC), deblocking / next reference, recon file, PSNR, report line */
+    /* emit a finished job: NAL unit, recon, statistics, report line (picture order) */
+    #define FLUSH_JOB(J)                                                                           \
+    do {                                                                                           \
+        wjob_t *fj_ = (J);                                                                          \
+        pool_wait(&pool, (int)(fj_ - pool.jobs));                                                   \
+        if (fj_->status) { st_ret = fj_->status; break; }                                           \
+        fwrite(fj_->out.buf, 1, fj_->out.len, fout);                                                 \
+        if (frec) jm_write_yuv_frame(frec, &fj_->rec, inp->width, inp->height);                     \
+        st->psnr_y += fj_->py; st->psnr_u += fj_->pu; st->psnr_v += fj_->pv;                          \
+        st->bits += fj_->pic_bits;                                                                  \
+        st->frames++;                                                                              \
+        st->entropy_ms += fj_->write_ms;                                                            \
+        write_ms += fj_->write_ms;                                                                  \
+        if (log)                                                                                   \
+            fprintf(log, "%4d(%s) %8ld   %2d %7.4f %7.4f %7.4f %9.1f %7.1f    FRM\n", fj_->f,          \
+                    fj_->is_i ? "IDR" : " P ", fj_->pic_bits, fj_->fp.qp, fj_->py, fj_->pu, fj_->pv,       \
+                    fj_->write_ms + fj_->met, fj_->met);                                              \
+        fj_->state = 0;                                                                             \
+        jflushed++;                                                                                \
+    } while (0)
+    /* hand a popped picture to the writer pool: its results and deblocked picture into a job */
+    #define SUBMIT(P, MET_MS)                                                                      \
+    do {                                                                                           \
+        pend_t *p_ = (P);                                                                          \
+        wjob_t *j_ = &pool.jobs[jseq % nj];                                                       \
+        if (j_->state) { FLUSH_JOB(j_); if (st_ret) break; }                                       \
+        double t1 = now_ms();                                                                      \
+        const jmh_mb_result *r0_ = be->mb_result(be->ctx, 0);                                      \
+        if (nmb > 1 && be->mb_result(be->ctx, nmb - 1) != r0_ + (nmb - 1)) { st_ret = JMH_E_STATE; break; } \
+        memcpy(j_->im.mb_data, r0_, (size_t)nmb * sizeof(jmh_mb_result));                         \
+        int r_ = be->read_deblocked(be->ctx, &j_->rec);                                            \
+        if (r_) { fprintf(stderr, "read_deblocked failed: %d\n", r_); st_ret = r_; break; }       \
+        copy_ms += now_ms() - t1;                                                                  \
+        st->deblock_ms += now_ms() - t1;                                                           \
+        j_->cur = &p_->cur; j_->fp = p_->fp; j_->f = p_->f; j_->is_i = p_->is_i; j_->met = (MET_MS); \
+        j_->sl.idr = p_->f == 0; j_->sl.slice_type = p_->fp.slice_type; j_->sl.frame_num = p_->frame_num; \
+        j_->sl.poc_lsb = 2 * p_->f; j_->sl.idr_pic_id = 0; j_->sl.qp = p_->fp.qp;                  \
+        pool_submit(&pool, (int)(j_ - pool.jobs));                                                 \
+        jseq++;                                                                                    \
+    } while (0)
     #define EMIT(P, MET_MS)                                                                          \
     do {                                                                                           \
+        if (nwr) { SUBMIT(P, MET_MS); break; }                                                     \
         pend_t *p_ = (P);                                                                          \
         double t1 = now_ms();                                                                      \
         for (int a = 0; a < nmb; a++) res[a] = be->mb_result(be->ctx, a);                          \
@@ -159,10 +321,10 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
             st->me_tq_ms += met;
             EMIT(&pend[head], met);
             if (st_ret) break;
-            head = (head + 1) % depth;
+            head = (head + 1) % plen;
             count--;
         }
-        pend_t *p = &pend[(head + count) % depth];
+        pend_t *p = &pend[(head + count) % plen];
         int idx = inp->start_frame + f;
         if (synthetic) jm_synth_frame(&p->cur, inp->width, inp->height, seed, idx);
         else if (jm_read_yuv_frame(fin, &p->cur, inp->width, inp->height, idx)) { fprintf(stderr, "ReadOneFrame: cannot read frame %d\n", idx); st_ret = JMH_E_INVALID_ARG; break; }
@@ -198,10 +360,26 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         if (r) { fprintf(stderr, "hot path backend '%s' failed: status %d\n", be->name, r); st_ret = r; break; }
         st->me_tq_ms += met;
         EMIT(&pend[head], met);
-        head = (head + 1) % depth;
+        head = (head + 1) % plen;
         count--;
     }
+    while (nwr && jflushed < jseq && !st_ret) FLUSH_JOB(&pool.jobs[jflushed % nj]);
     #undef EMIT
+    #undef SUBMIT
+    #undef FLUSH_JOB
+    if (nwr) {
+        pthread_mutex_lock(&pool.mu);
+        pool.stop = 1;
+        pthread_cond_broadcast(&pool.cv_work);
+        pthread_mutex_unlock(&pool.mu);
+        for (int k = 0; k < nwr; k++) pthread_join(pool.th[k], NULL);
+        for (int k = 0; k < nj; k++) { jm86_free(&pool.jobs[k].im); jm_pic_free(&pool.jobs[k].rec); jm_bits_free(&pool.jobs[k].out); }
+        pthread_mutex_destroy(&pool.mu);
+        pthread_cond_destroy(&pool.cv_work);
+        pthread_cond_destroy(&pool.cv_done);
+        free(pool.jobs); free(pool.queue); free(pool.th);
+        img = &im;
+    }
     st->total_ms = now_ms() - t_start;
     st->surface_checked = im.surface_checked;
     st->surface_searches = im.surface_searches;
@@ -217,9 +395,13 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         fprintf(log, " Total encoding time for the seq.  : %.3f sec\n Total ME+TQ time (backend)        : %.3f sec\n"
                      " SNR Y(dB) %.4f U %.4f V %.4f   bits %ld\n",
                 st->total_ms / 1e3, st->me_tq_ms / 1e3, st->psnr_y, st->psnr_u, st->psnr_v, st->bits);
+    if (log && st->frames)
+        fprintf(log, " Host per picture: slice writing + PSNR %.2f ms (%s), results + readback (+ host deblocking) %.2f ms, wall %.2f ms\n",
+                st->entropy_ms / st->frames, nwr ? "writer threads" : "main thread", st->deblock_ms / st->frames,
+                st->total_ms / st->frames);
     jm_bits_free(&out);
     free(res);
-    for (int k = 0; k < depth; k++) jm_pic_free(&pend[k].cur);
+    for (int k = 0; k < plen; k++) jm_pic_free(&pend[k].cur);
     free(pend);
     jm_pic_free(&rec);
     if (fin) fclose(fin);

@@ -20,7 +20,7 @@
 #include <string.h>
 #include "jmhost.h"
 
-jm86_img *img = NULL;
+__thread jm86_img *img = NULL;
 
 static const int blc_size[8][2] = {{16, 16}, {16, 16}, {16, 8}, {8, 16}, {8, 8}, {8, 4}, {4, 8}, {4, 4}};
 
@@ -254,7 +254,7 @@ static int check_decision(const jmh_mb_result *r, int best_mode, int best_cost, 
 /* rdopt.c › encode_one_macroblock [J] (RDO off) for img->current_mb_nr */
 void encode_one_macroblock(void) {
     const int a = img->current_mb_nr;
-    const jmh_mb_result *r = img->be->mb_result(img->be->ctx, a);
+    const jmh_mb_result *r = img->res ? &img->res[a] : img->be->mb_result(img->be->ctx, a);
     if (surface_on(img)) {
         int best_cost = 0, best8x8[4] = {0, 0, 0, 0};
         const int best_mode = inter_searches(&best_cost, best8x8);
@@ -265,7 +265,7 @@ void encode_one_macroblock(void) {
                             "inter searches (mode %d, cost %d)\n", a, r->mb_type, r->min_cost, best_mode, best_cost);
         }
     }
-    img->mb_data[a] = *r;
+    if (r != &img->mb_data[a]) img->mb_data[a] = *r;
     /* the final MVs become enc_picture's (intra: ref_idx -1) */
     const int intra = r->mb_type == JMH_I4MB || r->mb_type == JMH_I16MB || r->mb_type == JMH_I8MB;
     set_enc_mv(0, 0, 4, 4, intra ? NULL : (const int16_t (*)[2])r->mv, intra ? -1 : 0);

@@ -48,6 +48,8 @@ typedef struct jm_input {
     int  frame_rate;           /* FrameRate (report only)                                     */
     int  hip_device;           /* (this build) HIP device index                               */
     int  pipeline_depth;       /* (this build) pictures in flight on the device (0 = auto)   */
+    int  writer_threads;       /* (this build) slice-writer threads (0: the frame loop writes;
+                                  used with a pipelined device backend)                       */
     int  jm_call_surface;      /* (this build) 1: every P macroblock also runs JM 8.6's inter
                                   searches through PartitionMotionSearch / BlockMotionSearch
                                   (the per-block device seam), checked against the wavefront
@@ -203,8 +205,9 @@ typedef struct jm86_img {
     const jm_input *input;
     jm_backend *be;
     jm_slice_writer *writer;
+    const jmh_mb_result *res;         /* the picture's results (NULL: the backend's current ones) */
 } jm86_img;
-extern jm86_img *img;
+extern __thread jm86_img *img;       /* JM's global img, one per slice-writing thread */
 
 int  jm86_init(jm86_img *im, const jm_input *inp, jm_backend *be, int width, int height);
 void jm86_free(jm86_img *im);

@@ -45,6 +45,9 @@ int main(int argc, char **argv) {
     if (jm_configure(&inp, argc, argv, err, sizeof(err))) { fprintf(stderr, "%s\n", err); return 1; }
     jmh_config cfg;
     jm_fill_config(&inp, &cfg);
+    /* device deblocking: only the deblocked picture comes back (the recon file, PSNR and the
+       next reference are the filtered picture, as in JM) */
+    if (!getenv("JMH_HOST_DEBLOCK")) cfg.flags |= JMH_FLAG_NO_RECON_READBACK;
     jmh_ctx *ctx = NULL;
     int r = jmh_create(&cfg, inp.hip_device, &ctx);
     if (r) { fprintf(stderr, "jmh_create failed: %s\n", jmh_strerror(r)); return 2; }

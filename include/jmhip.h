@@ -96,6 +96,10 @@ typedef struct jmh_config {
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */
 #define JMH_FLAG_KERNEL_TIMING 1
+/* pictures deblocked on the device (jmh_frame_params.deblock) skip the readback of the
+   reconstruction before deblocking: jmh_read_recon returns JMH_E_STATE for them (lencod with
+   device deblocking reads only jmh_read_deblocked) */
+#define JMH_FLAG_NO_RECON_READBACK 2
 
 /* ---- per-picture parameters ------------------------------------------------------------- */
 typedef struct jmh_frame_params {

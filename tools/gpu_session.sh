@@ -14,9 +14,9 @@
 #   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
 #   profc3  the same for config 3
 #   pmc     tools/pmc_traffic.sh (HBM bytes + SQ counters, separate passes)
-#   lencod  the product lencod end to end, 1080p, 60 pictures (FFS SR 32), per-frame report
-#           -> gpurun_out/TAG_lencod1080.log
-#   lencodc3 the same for the config-3 shape (2160p High, EPZS + 8x8), 30 pictures
+#   lencod  the product lencod end to end on an I420 file (tools/make_yuv.py), 1080p, 60 pictures
+#           (FFS SR 32), WriterThreads 0 / 4 / 8 -> gpurun_out/TAG_lencod1080_w*.log
+#   lencodc3 the same for the config-3 shape (2160p High, EPZS + 8x8), 30 pictures, 8 writers
 TAG=${1:?tag}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
@@ -54,14 +54,19 @@ for s in "$@"; do
     profc3) run profc3 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c3" -o ${TAG}_c3 --output-format csv -- \
                 python3 "$R/bench.py" --config 3 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc3.log 2>&1 || exit $?
             find gpurun_out/prof_${TAG}_c3 -name "*kernel_stats*" -exec cat {} \; ;;
-    lencod) run lencod 600 h264-jm-commentary_amd/host/build/lencod -p InputFile=synthetic:0 -p FramesToBeEncoded=60 \
-                -p SourceWidth=1920 -p SourceHeight=1080 -p SearchRange=32 -p OutputFile=/tmp/l1080.264 \
-                > gpurun_out/${TAG}_lencod1080.log 2>&1 || exit $?
-            tail -8 gpurun_out/${TAG}_lencod1080.log ;;
-    lencodc3) run lencodc3 900 h264-jm-commentary_amd/host/build/lencod -p InputFile=synthetic:0 -p FramesToBeEncoded=30 \
+    lencod) run mkyuv 300 python tools/make_yuv.py /tmp/s1080.yuv 1920 1080 60 || exit $?
+            for wt in 0 4 8; do
+              run lencod_w$wt 600 h264-jm-commentary_amd/host/build/lencod -p InputFile=/tmp/s1080.yuv -p FramesToBeEncoded=60 \
+                -p SourceWidth=1920 -p SourceHeight=1080 -p SearchRange=32 -p WriterThreads=$wt -p OutputFile=/tmp/l1080_$wt.264 \
+                > gpurun_out/${TAG}_lencod1080_w$wt.log 2>&1 || exit $?
+              tail -5 gpurun_out/${TAG}_lencod1080_w$wt.log
+            done
+            cmp /tmp/l1080_0.264 /tmp/l1080_4.264 && cmp /tmp/l1080_0.264 /tmp/l1080_8.264 && echo "bitstreams identical" || exit 1 ;;
+    lencodc3) run mkyuv 300 python tools/make_yuv.py /tmp/s2160.yuv 3840 2160 30 || exit $?
+            run lencodc3 900 h264-jm-commentary_amd/host/build/lencod -p InputFile=/tmp/s2160.yuv -p FramesToBeEncoded=30 \
                 -p SourceWidth=3840 -p SourceHeight=2160 -p SearchRange=32 -p ProfileIDC=100 -p Transform8x8Mode=1 \
-                -p SearchMode=3 -p OutputFile=/tmp/l2160.264 > gpurun_out/${TAG}_lencod2160.log 2>&1 || exit $?
-            tail -8 gpurun_out/${TAG}_lencod2160.log ;;
+                -p SearchMode=3 -p WriterThreads=8 -p OutputFile=/tmp/l2160.264 > gpurun_out/${TAG}_lencod2160.log 2>&1 || exit $?
+            tail -5 gpurun_out/${TAG}_lencod2160.log ;;
     pmc)    run pmc 900 bash tools/pmc_traffic.sh "$TAG" || exit $? ;;
     *)      echo "unknown step $s"; exit 2 ;;
   esac
