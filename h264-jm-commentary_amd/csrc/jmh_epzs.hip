@@ -1,0 +1,430 @@
+// jmh_epzs.hip — k_mb_epzs: the motion-search half of encode_one_macroblock [J] with SearchMode 3
+// (EPZSPelBlockMotionSearch as restated in oracle/encode.c epzs_search, docs/JM_SEMANTICS.md
+// items 33-40), ONE WAVE per P macroblock.
+//
+// EPZS evaluates few positions per search (41 ordered predictors, then a handful of diamond
+// rounds) but its 41 searches are strictly sequential (MVP, spatial memory and earlier-type
+// predictors read the searches before).  So the search is latency-bound, and one wave per MB with
+// wave-synchronous LDS (no workgroup barrier anywhere) beats a workgroup of waves meeting at
+// barriers:
+//   * full pel: lane i evaluates predictor i (i < 41) — the whole block SAD per lane from the
+//     LDS window by aligned dwords + v_alignbyte + v_sad_u8 — one wave minimum of
+//     (cost << 6 | i) keys is JM's strict '<' scan in list order; a refinement round is one
+//     pattern point per lane (4 or 12 lanes) and one wave minimum;
+//   * sub pel: the block's b / h / j neighbourhood at its full-pel MV in three small planes (b
+//     and j from unclipped horizontal taps, so j is one vertical 6-tap per sample; G is the window),
+//     lane task = (candidate, 4x4 sub-block) with a packed int16 Hadamard, DPP sums over the
+//     candidate's lanes, one wave minimum per pass.
+// LDS: the window MB +- (2 SR + 4) (every block's reach when each search centres on its own
+// MVP, as k_mb_me_full) + ~3.5 KB state = 26 KB, six macroblocks per CU.  Results land in
+// MbScratch exactly like the other search kernels (the intra workgroups and k_mb_final are shared).
+#include "jmh_common.h"
+
+#define NTE 64                                // one wave per macroblock
+#define EOFF_MAX (2 * SRMAX + 4)              // window margin around the MB
+#define EW_MAX (16 + 2 * EOFF_MAX)            // 152
+#define EST EW_MAX                            // window row stride (the second dword of an
+                                              // unaligned read may touch the next row: harmless)
+#define NPRED 41                              // EPZS predictor slots (oracle epzs_predictors)
+#define HPS 20                                // sub-pel plane stride (>= 18 + 2 alignment slack)
+#define HPR 18                                // sub-pel plane rows (block + 1 on each side)
+#define HPL (HPR * HPS + 8)                   // sub-pel plane size (b, h, j)
+#define EKOFF 4096                            // sub-pel cost offset in keys (16x16 zero-vector bias)
+
+struct EpzS {
+    uint8_t g[EW_MAX * EST];                  // (a dword read past the last row lands in org: harmless)
+    uint8_t org[256];
+    Border bd;
+    int16_t all_mv[8][16][2];
+    int motion_cost[8][4];
+    int16_t tmv[6][6][2];                     // previous picture's MVs around the MB (4x4 units,
+    int8_t tref[6][6];                        //   MB origin at [1][1]; -1: none)
+    int16_t mem[7][16][2];                    // spatial memory: the left MB's searches (types 1..7)
+    int memok;
+    uint8_t hp[3][HPL];                       // b, h, j of the block's [-1, w] x [-1, h] at its MV
+    int16_t b1[HPR + 5][HPR];                 // unclipped horizontal taps, rows -3 .. h + 1
+};
+
+// neighbour view of a search of block type bt in 8x8 block b8 (as NbMe in jmh_analyse.hip)
+struct NbEpz {
+    const EpzS &s;
+    int bt, b8, best8x8;
+    __device__ __forceinline__ bool operator()(int xN, int yN, int &ref, int &mx, int &my) const {
+        if (yN > 15 || (xN > 15 && yN >= 0)) return false;
+        if (xN < 0 || yN < 0) {
+            int c = border_cell(xN, yN);
+            if (c < 0 || s.bd.ref[c] == -2) return false;
+            ref = s.bd.ref[c]; mx = s.bd.mv[c][0]; my = s.bd.mv[c][1];
+            return true;
+        }
+        int k = (yN >> 2) * 4 + (xN >> 2), cb8 = ((yN >> 3) << 1) | (xN >> 3);
+        int m = (bt <= 3 || cb8 == b8) ? bt : (best8x8 >> (4 * cb8)) & 15;
+        ref = 0; mx = s.all_mv[m][k][0]; my = s.all_mv[m][k][1];
+        return true;
+    }
+};
+
+__device__ __forceinline__ uint32_t eld_u32(const uint8_t *p) {   // 4 bytes at any LDS address
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+// EPZS predictor i of a search (oracle/encode.c epzs_predictors order): 0 centre, 1 zero, 2-4
+// spatial A / B / C (or D), 5-28 window rings R/4, R/2, R, 29-33 temporal (co-located, left,
+// right, up, down), 34 spatial memory (left MB), 35-40 earlier block types.  False if not valid
+// or outside the window around the centre.
+__device__ __forceinline__ bool epzs_cand(const DevParams &d, const EpzS &s, int i, int bt, int bx4, int by4, int b8, int best8x8,
+                                          int range, int mvx0, int mvy0, int &x, int &y) {
+    const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt), k0 = by4 * 4 + bx4;
+    auto rnd = [](int v) { return (v + 2) >> 2; };
+    bool v = true;
+    x = 0; y = 0;
+    if (i == 0) { x = mvx0; y = mvy0; }
+    else if (i == 1) { }
+    else if (i <= 4) {
+        int ref = -1, ax = 0, ay = 0;
+        v = mvp_nbr(NbEpz{s, bt, b8, best8x8}, bx4, by4, 4 * w4, i - 2, ref, ax, ay) && ref == 0;
+        x = rnd(ax); y = rnd(ay);
+    } else if (i <= 28) {
+        const int ring = (i - 5) >> 3, k = (i - 5) & 7, rr = range >> (2 - ring);
+        const int wx = k == 1 || k == 4 || k == 6 ? -1 : k == 2 || k == 5 || k == 7 ? 1 : 0;
+        const int wy = k == 0 || k == 4 || k == 5 ? -1 : k == 3 || k == 6 || k == 7 ? 1 : 0;
+        v = rr > 0; x = mvx0 + rr * wx; y = mvy0 + rr * wy;
+    } else if (i <= 33) {
+        const int k = i - 29;
+        const int tx = 1 + bx4 + (k == 1 ? -1 : k == 2 ? w4 : 0), ty = 1 + by4 + (k == 3 ? -1 : k == 4 ? h4 : 0);
+        v = s.tref[ty][tx] == 0;
+        x = rnd(s.tmv[ty][tx][0]); y = rnd(s.tmv[ty][tx][1]);
+    } else if (i == 34) {
+        v = s.memok && inter_on(d.isr, bt);
+        x = rnd(s.mem[bt - 1][k0][0]); y = rnd(s.mem[bt - 1][k0][1]);
+    } else if (i < NPRED) {
+        const int t = i - 34;
+        v = t < bt && inter_on(d.isr, t);
+        x = rnd(s.all_mv[t][k0][0]); y = rnd(s.all_mv[t][k0][1]);
+    } else v = false;
+    return v && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
+}
+
+// refinement pattern point e: small diamond (0,-1) (-1,0) (1,0) (0,1); extended diamond (0,-2)
+// (-1,-1) (1,-1) (-2,0) (2,0) (-1,1) (1,1) (0,2) then the small diamond
+__device__ __forceinline__ void epzs_pat(bool sd, int e, int &px, int &py) {
+    if (sd) { px = e == 1 ? -1 : e == 2 ? 1 : 0; py = e == 0 ? -1 : e == 3 ? 1 : 0; return; }
+    px = e < 8 ? (e == 1 || e == 5 ? -1 : e == 2 || e == 6 ? 1 : e == 3 ? -2 : e == 4 ? 2 : 0) : (e == 9 ? -1 : e == 10 ? 1 : 0);
+    py = e < 8 ? (e == 0 ? -2 : e <= 2 ? -1 : e <= 4 ? 0 : e <= 6 ? 1 : 2) : (e == 8 ? -1 : e == 11 ? 1 : 0);
+}
+
+// SAD of the whole block (4 w4 x 4 h4 at 4x4 position bx4, by4) at full-pel displacement (x, y)
+// on this lane: per row w4 + 1 aligned dwords, v_alignbyte, v_sad_u8
+template <int LW4, int LH4>
+__device__ __forceinline__ unsigned lane_block_sad(const EpzS &s, int off, int bx4, int by4, int x, int y) {
+    constexpr int W4 = 1 << LW4, H = 4 << LH4;
+    const int a = (off + 4 * by4 + y) * EST + off + 4 * bx4 + x;
+    const uint32_t sel = (uint32_t)(a & 3);
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~3));
+    const uint32_t *org = reinterpret_cast<const uint32_t *>(s.org + (4 * by4) * 16 + 4 * bx4);
+    uint32_t sad = 0;
+#pragma unroll
+    for (int r = 0; r < H; r++) {
+        uint32_t w[W4 + 1];
+#pragma unroll
+        for (int q = 0; q <= W4; q++) w[q] = base[r * (EST / 4) + q];
+#pragma unroll
+        for (int q = 0; q < W4; q++) sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), org[r * 4 + q], sad);
+    }
+    return sad;
+}
+
+typedef short e16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ e16x2 e_s2(uint32_t v) { return __builtin_bit_cast(e16x2, v); }
+__device__ __forceinline__ uint32_t e_u32(e16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ e16x2 e_abs2(e16x2 v) { return __builtin_elementwise_max(v, (e16x2)(0) - v); }
+
+// row pointer and stride of half-grid plane pl (0 G = the window, 1 b, 2 h, 3 j) at block-
+// relative integer position (rx, ry) (b / h / j sample [y][x] = position (x - 1, y - 1))
+__device__ __forceinline__ const uint8_t *hp_row(const EpzS &s, int pl, int gx0, int gy0, int rx, int ry, int &stride) {
+    if (pl == 0) { stride = EST; return s.g + (gy0 + ry) * EST + gx0 + rx; }
+    stride = HPS;
+    return s.hp[pl - 1] + (ry + 1) * HPS + rx + 1;
+}
+
+// SATD() [J] of one 4x4 sub-block at quarter-pel offset (ox, oy) in [-3, 3] from the full-pel
+// MV (window position gx0, gy0 of the block origin): block-relative sub-block origin (sx, sy);
+// rows as dwords from the phase's two half-grid planes, their rounding average per byte, packed
+// int16 Hadamard (as subblock_satd)
+__device__ __forceinline__ int hp_satd(const EpzS &s, int gx0, int gy0, int sx, int sy, int obase, int ox, int oy, int had) {
+    const int off = qoff((oy & 3) * 4 + (ox & 3));
+    const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
+    const int rx = sx + (ox >> 2), ry = sy + (oy >> 2);
+    int sa, sb;
+    const uint8_t *pA = hp_row(s, (xa & 1) + 2 * (ya & 1), gx0, gy0, rx + (xa >> 1), ry + (ya >> 1), sa);
+    const uint8_t *pB = hp_row(s, (xb & 1) + 2 * (yb & 1), gx0, gy0, rx + (xb >> 1), ry + (yb >> 1), sb);
+    uint32_t O[4], P[4];
+#pragma unroll
+    for (int yy = 0; yy < 4; yy++) {
+        const uint32_t A = eld_u32(pA + yy * sa), B = eld_u32(pB + yy * sb);
+        P[yy] = (A | B) - (((A ^ B) >> 1) & 0x7F7F7F7Fu);   // per byte (a + b + 1) >> 1
+        O[yy] = *reinterpret_cast<const uint32_t *>(s.org + obase + 16 * yy);
+    }
+    if (!had) {
+        uint32_t sad = 0;
+#pragma unroll
+        for (int yy = 0; yy < 4; yy++) sad = __builtin_amdgcn_sad_u8(O[yy], P[yy], sad);
+        return (int)sad;
+    }
+    e16x2 r[4][2];
+#pragma unroll
+    for (int yy = 0; yy < 4; yy++) {
+        r[yy][0] = e_s2(__builtin_amdgcn_perm(0u, O[yy], 0x0c010c00u)) - e_s2(__builtin_amdgcn_perm(0u, P[yy], 0x0c010c00u));
+        r[yy][1] = e_s2(__builtin_amdgcn_perm(0u, O[yy], 0x0c030c02u)) - e_s2(__builtin_amdgcn_perm(0u, P[yy], 0x0c030c02u));
+    }
+    e16x2 m[4][2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const e16x2 a0 = r[0][h] + r[3][h], a1 = r[1][h] + r[2][h], a2 = r[1][h] - r[2][h], a3 = r[0][h] - r[3][h];
+        m[0][h] = a0 + a1; m[2][h] = a0 - a1; m[1][h] = a2 + a3; m[3][h] = a3 - a2;
+    }
+    e16x2 acc = (e16x2)(0);
+#pragma unroll
+    for (int p = 0; p < 2; p++) {
+        const uint32_t u0 = e_u32(m[2 * p][0]), v0 = e_u32(m[2 * p + 1][0]);
+        const uint32_t u1 = e_u32(m[2 * p][1]), v1 = e_u32(m[2 * p + 1][1]);
+        const e16x2 x0 = e_s2(__builtin_amdgcn_perm(v0, u0, 0x05040100u)), x1 = e_s2(__builtin_amdgcn_perm(v0, u0, 0x07060302u));
+        const e16x2 x2 = e_s2(__builtin_amdgcn_perm(v1, u1, 0x05040100u)), x3 = e_s2(__builtin_amdgcn_perm(v1, u1, 0x07060302u));
+        const e16x2 a0 = x0 + x3, a1 = x1 + x2, a2 = x1 - x2, a3 = x0 - x3;
+        acc += __builtin_elementwise_max(e_abs2(a0), e_abs2(a1)) + __builtin_elementwise_max(e_abs2(a2), e_abs2(a3));
+    }
+    const uint32_t t = e_u32(acc);
+    return (int)((t & 0xFFFFu) + (t >> 16));
+}
+
+// BlockMotionSearch [J] of one block on the wave: EPZS full pel + SubPelBlockMotionSearch
+template <int BT>
+__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off, int bx4, int by4, int mc, int b8, int best8x8) {
+    constexpr int LW4 = BT <= 2 ? 2 : (BT <= 5 ? 1 : 0), LH4 = (BT == 1 || BT == 3) ? 2 : (BT == 2 || BT == 4 || BT == 6) ? 1 : 0;
+    constexpr int W4 = 1 << LW4, H4 = 1 << LH4, LNS = LW4 + LH4, NSUB = 1 << LNS;
+    const int lane = threadIdx.x;
+    const int lam = d.lambda_motion, had = d.use_hadamard;
+    const bool slice_p = d.slice_type == JMH_P_SLICE;
+    const int range = d.restrict_sr == 0 ? d.sr / min(2, BT) : d.sr;
+    int pmx, pmy;
+    set_mvp(NbEpz{s, BT, b8, best8x8}, bx4, by4, 4 * W4, 4 * H4, pmx, pmy);
+    pmx = __builtin_amdgcn_readfirstlane(pmx);
+    pmy = __builtin_amdgcn_readfirstlane(pmy);
+    const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
+    const int med = 16 * W4 * H4;
+    // ---- full pel: predictor `lane`, then pattern rounds
+    int cx, cy;
+    const bool cv = epzs_cand(d, s, lane, BT, bx4, by4, b8, best8x8, range, mvx0, mvy0, cx, cy);
+    if (!cv) { cx = mvx0; cy = mvy0; }   // any valid position for the SAD (key discarded)
+    const int c0 = (int)lane_block_sad<LW4, LH4>(s, off, bx4, by4, cx, cy) +
+                   (int)__umul24(lam, mvbits(4 * cx - pmx) + mvbits(4 * cy - pmy));
+    const int cost0 = __builtin_amdgcn_readfirstlane(c0);   // predictor 0: the centre, always valid
+    int bx = mvx0, by = mvy0, min_mcost = cost0;
+    if (cost0 >= med) {                                    // else: stop at the centre
+        const unsigned m0 = wave_min_u32(cv ? ((unsigned)c0 << 6) | (unsigned)lane : 0xFFFFFFFFu);
+        min_mcost = (int)(m0 >> 6);
+        bx = __builtin_amdgcn_readlane(cx, m0 & 63);
+        by = __builtin_amdgcn_readlane(cy, m0 & 63);
+        if (min_mcost >= med) {                            // pattern refinement until it stops
+            const bool sd = min_mcost < med + ((3 * med) >> 1);
+            const int np = sd ? 4 : 12;
+            int px = 0, py = 0;
+            epzs_pat(sd, lane, px, py);
+            for (int it = 0; it < 4 * NPOS_MAX; it++) {
+                const int x = bx + px, y = by + py;
+                const bool v = lane < np && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
+                unsigned k = 0xFFFFFFFFu;
+                if (v) {
+                    const int c = (int)lane_block_sad<LW4, LH4>(s, off, bx4, by4, x, y) +
+                                  (int)__umul24(lam, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+                    k = ((unsigned)c << 6) | (unsigned)lane;
+                }
+                const unsigned m = wave_min_u32(k);
+                if (m == 0xFFFFFFFFu || (int)(m >> 6) >= min_mcost) break;
+                min_mcost = (int)(m >> 6);
+                bx = __builtin_amdgcn_readlane(x, m & 63);
+                by = __builtin_amdgcn_readlane(y, m & 63);
+            }
+        }
+    }
+    const int fmx = bx, fmy = by;
+    if (had) min_mcost = BIGCOST;
+    // ---- sub-pel neighbourhood of the block at (fmx, fmy): b, h, j planes, sample [y][x] =
+    //      block-relative (x - 1, y - 1); b1 = unclipped horizontal taps, row rr <-> y = rr - 2
+    constexpr int PW = 4 * W4 + 2, PH = 4 * H4 + 2;
+    const int gx0 = off + 4 * bx4 + fmx, gy0 = off + 4 * by4 + fmy;   // window position of (0, 0)
+    auto G = [&](int x, int y) { return (int)s.g[y * EST + x]; };
+    for (int i = lane; i < PW * (PH + 5); i += NTE) {
+        const int rr = i / PW, x = i - rr * PW, gx = gx0 + x - 1, gy = gy0 + rr - 3;
+        const int h1 = tap6(G(gx - 2, gy), G(gx - 1, gy), G(gx, gy), G(gx + 1, gy), G(gx + 2, gy), G(gx + 3, gy));
+        s.b1[rr][x] = (int16_t)h1;
+        if (rr >= 2 && rr < PH + 2) {
+            s.hp[0][(rr - 2) * HPS + x] = (uint8_t)clip255((h1 + 16) >> 5);
+            s.hp[1][(rr - 2) * HPS + x] =
+                (uint8_t)clip255((tap6(G(gx, gy - 2), G(gx, gy - 1), G(gx, gy), G(gx, gy + 1), G(gx, gy + 2), G(gx, gy + 3)) + 16) >> 5);
+        }
+    }
+    wave_lds_sync();
+    for (int i = lane; i < PW * PH; i += NTE) {
+        const int y = i / PW, x = i - y * PW;
+        s.hp[2][y * HPS + x] =
+            (uint8_t)clip255((tap6(s.b1[y][x], s.b1[y + 1][x], s.b1[y + 2][x], s.b1[y + 3][x], s.b1[y + 4][x], s.b1[y + 5][x]) + 512) >> 10);
+    }
+    wave_lds_sync();
+    // ---- half then quarter pel: lane task = (candidate, 4x4 sub-block), JM order, strict '<'
+    const bool check0 = BT == 1 && fmx == 0 && fmy == 0 && had && slice_p;
+    int qx = 0, qy = 0;
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++) {
+        const int step = pass == 0 ? 2 : 1, min_pos = pass == 0 ? (had ? 0 : 1) : 1;
+        unsigned kb = 0xFFFFFFFFu;
+#pragma unroll
+        for (int t0 = 0; t0 < (9 << LNS); t0 += NTE) {
+            const int task = t0 + lane, c = task >> LNS, sub = task & (NSUB - 1);
+            const bool val = c < 9 && c >= min_pos;
+            const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+            int sat = 0;
+            if (val) {
+                const int sx = 4 * (sub & (W4 - 1)), sy = 4 * (sub >> LW4);
+                sat = hp_satd(s, gx0, gy0, sx, sy, 64 * by4 + 4 * bx4 + 16 * sy + sx, ox, oy, had);
+            }
+            if constexpr (NSUB >= 2) sat += dpp<0xB1>(sat);
+            if constexpr (NSUB >= 4) sat += dpp<0x4E>(sat);
+            if constexpr (NSUB >= 8) sat += dpp<0x141>(sat);
+            if constexpr (NSUB >= 16) sat += dpp<0x140>(sat);
+            if (val && sub == 0) {
+                int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmx) + mvbits(4 * fmy + oy - pmy));
+                if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
+                kb = min(kb, ((unsigned)(cost + EKOFF) << 4) | (unsigned)c);
+            }
+        }
+        kb = wave_min_u32(kb);
+        if (kb != 0xFFFFFFFFu && (int)(kb >> 4) - EKOFF < min_mcost) {
+            const int c = kb & 15;
+            min_mcost = (int)(kb >> 4) - EKOFF;
+            qx += step * sp9x(c);
+            qy += step * sp9y(c);
+        }
+    }
+    if (lane < NSUB) {
+        const int k = (by4 + (lane >> LW4)) * 4 + bx4 + (lane & (W4 - 1));
+        s.all_mv[BT][k][0] = (int16_t)(4 * fmx + qx);
+        s.all_mv[BT][k][1] = (int16_t)(4 * fmy + qy);
+    }
+    if (lane == 0) s.motion_cost[BT][mc] += min_mcost;
+    wave_lds_sync();
+}
+
+__global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
+    __shared__ EpzS s;
+    const int b = xcd_block(blockIdx.x, t.pre[t.nP]), lane = threadIdx.x;   // XCD-aware (jmh_device.h)
+    if (b >= t.pre[t.nP]) return;
+    const int e = tick_entry(t, b);
+    const DevParams d = tick_params(t, e);
+    const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
+    const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, sr = d.sr;
+    const int off = 2 * sr + 4, wdim = 16 + 2 * off;
+    MbScratch *scr = d.scr + mby * d.mbw + mbx;
+    const int X0 = 4 * mbx, Y0 = 4 * mby, left = mbx > 0 ? mby * d.mbw + mbx - 1 : -1;
+    const bool prof = d.prof && lane == 0 && d.prof_mb == mby * d.mbw + mbx;
+    if (prof) d.prof[32] = wall_clock64();
+    // ---- inputs: the MB (one dword per lane), border cells, the temporal neighbourhood, the left
+    //      MB's searches, the window (dword per task: two aligned global dwords + v_alignbyte
+    //      inside the picture, clamped bytes at its edges: the spec's UMV access)
+    reinterpret_cast<uint32_t *>(s.org)[lane] =
+        *reinterpret_cast<const uint32_t *>(d.orgY + (pix_y + (lane >> 2)) * W + pix_x + 4 * (lane & 3));
+    if (lane < 10) load_border(d, s.bd, lane, mbx, mby);
+    if (lane < 32) s.motion_cost[lane >> 2][lane & 3] = 0;
+    if (lane < 36) {
+        const int ty = lane / 6, tx = lane - 6 * ty, px = X0 - 1 + tx, py = Y0 - 1 + ty;
+        int ref = -1, mx = 0, my = 0;
+        if (d.tref && px >= 0 && px < (W >> 2) && py >= 0 && py < (d.H >> 2)) {
+            const int a = py * (W >> 2) + px;
+            ref = d.tref[a]; mx = d.tmv[2 * a]; my = d.tmv[2 * a + 1];
+        }
+        s.tref[ty][tx] = (int8_t)ref; s.tmv[ty][tx][0] = (int16_t)mx; s.tmv[ty][tx][1] = (int16_t)my;
+    }
+    for (int i = lane; i < 7 * 32; i += NTE) {
+        const int m = 1 + i / 32, k = (i & 31) >> 1, c = i & 1;
+        s.mem[m - 1][k][c] = left >= 0 ? d.scr[left].all_mv[m][k][c] : 0;
+    }
+    if (lane == 0) s.memok = left >= 0;
+    {
+        constexpr int ND4 = EST / 4;
+        const int WX0 = pix_x - off, WY0 = pix_y - off;
+        for (int task = lane; task < wdim * ND4; task += NTE) {
+            const int y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
+            const uint8_t *row = d.refY + iclip(0, d.H - 1, WY0 + y) * W;
+            uint32_t v;
+            if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
+                const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
+                v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
+            } else {
+                v = 0;
+                for (int q = 0; q < 4; q++)
+                    if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
+            }
+            *reinterpret_cast<uint32_t *>(s.g + y * EST + 4 * j) = v;
+        }
+    }
+    wave_lds_sync();
+    if (prof) d.prof[33] = wall_clock64();
+    // PartitionMotionSearch [J] order: 16x16, 16x8 (2), 8x16 (2), then per 8x8 block the sub-modes
+    // 4..7 and its best sub-mode (read through best8x8)
+    int best8x8 = 0, cost8x8 = 0;
+    epzs_block<1>(d, s, off, 0, 0, 0, 0, 0);
+    if (prof) d.prof[34] = wall_clock64();
+    epzs_block<2>(d, s, off, 0, 0, 0, 0, 0);
+    epzs_block<2>(d, s, off, 0, 2, 1, 0, 0);
+    epzs_block<3>(d, s, off, 0, 0, 0, 0, 0);
+    epzs_block<3>(d, s, off, 2, 0, 1, 0, 0);
+    if (prof) d.prof[35] = wall_clock64();
+#pragma unroll 1
+    for (int b8 = 0; b8 < 4; b8++) {
+        const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
+        epzs_block<4>(d, s, off, X, Y, b8, b8, best8x8);
+        epzs_block<5>(d, s, off, X, Y, b8, b8, best8x8);
+        epzs_block<5>(d, s, off, X, Y + 1, b8, b8, best8x8);
+        epzs_block<6>(d, s, off, X, Y, b8, b8, best8x8);
+        epzs_block<6>(d, s, off, X + 1, Y, b8, b8, best8x8);
+        epzs_block<7>(d, s, off, X, Y, b8, b8, best8x8);
+        epzs_block<7>(d, s, off, X + 1, Y, b8, b8, best8x8);
+        epzs_block<7>(d, s, off, X, Y + 1, b8, b8, best8x8);
+        epzs_block<7>(d, s, off, X + 1, Y + 1, b8, b8, best8x8);
+        int mc8 = BIGCOST, bm = 0;
+        for (int mode = 4; mode <= 7; mode++) {
+            if (!inter_on(d.isr, mode)) continue;
+            const int c = s.motion_cost[mode][b8];
+            if (c < mc8) { mc8 = c; bm = mode; }
+        }
+        best8x8 |= bm << (4 * b8);
+        cost8x8 += mc8;
+        if (prof) d.prof[36 + b8] = wall_clock64();
+    }
+    // results: MVs and partition costs of types 1..7, P8x8 decision, FindSkipModeMotionVector
+    for (int i = lane; i < 7 * 32; i += NTE) {
+        const int m = 1 + i / 32, k = (i & 31) >> 1, c = i & 1;
+        scr->all_mv[m][k][c] = s.all_mv[m][k][c];
+    }
+    if (lane < 28) scr->motion_cost[1 + lane / 4][lane & 3] = s.motion_cost[1 + lane / 4][lane & 3];
+    else if (lane == 32) { scr->best8x8 = best8x8; scr->cost8x8 = cost8x8; }
+    else if (lane == 48) {
+        int pcx, pcy;
+        set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
+        NbBorder nbv{s.bd};
+        int ra = -1, ax = 0, ay = 0, rb = -1, bx = 0, by = 0;
+        const bool aa = nbv(-1, 0, ra, ax, ay), ab = nbv(0, -1, rb, bx, by);
+        const bool zl = !aa || (ra == 0 && ax == 0 && ay == 0), za = !ab || (rb == 0 && bx == 0 && by == 0);
+        scr->skipx = (za || zl) ? 0 : pcx;
+        scr->skipy = (za || zl) ? 0 : pcy;
+    }
+    if (prof) d.prof[40] = wall_clock64();
+}
+
+hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st) {
+    if (t.pre[t.nP] == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mb_epzs, dim3(xcd_grid(t.pre[t.nP])), dim3(NTE), 0, st, t);
+    return hipGetLastError();
+}

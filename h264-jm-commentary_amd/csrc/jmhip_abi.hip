@@ -25,6 +25,7 @@ hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
                                 const int32_t *centres, uint16_t *out, hipStream_t st);
 hipError_t jmh_launch_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
@@ -451,7 +452,8 @@ static int issue_tick(jmh_ctx *c) {
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
         if (kt) HCHK(ring_begin(c->ring_an, c->st));
-        if (!t.me_in_analyse) HCHK(jmh_launch_me_full(t, c->st));   // SearchMode -1
+        if (t.search_mode == 3) HCHK(jmh_launch_epzs(t, c->st));               // EPZS: one wave per MB
+        else if (!t.me_in_analyse) HCHK(jmh_launch_me_full(t, c->st));     // SearchMode -1
         HCHK(jmh_launch_analyse(t, c->st));
         if (t.t8) HCHK(jmh_launch_intra8(t, c->st));   // Intra8x8 decision (High profile)
         if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }

@@ -207,6 +207,16 @@ def test_epzs_moving_sequence(qp):
                 transform_8x8_mode=1)
 
 
+def test_config3_width_3840_epzs():
+    """Config 3 at its real width (3840, as 3840x2160 in the bench): High profile, EPZS + 8x8
+    transform, SR 32, an I picture and two P pictures under large motion and with the temporal
+    predictors of the previous P picture; GPU == oracle on every macroblock."""
+    w, h = 3840, 256
+    pics = moving_seq(w, h, 3, seed=38, step=(37, -29))
+    encode_pair(w, h, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], 28, search_range=32, search_mode=3,
+                transform_8x8_mode=1)
+
+
 def test_random_content_p_frames():
     rng = np.random.default_rng(11)
     pics = [rand_picture(rng, 64, 64) for _ in range(3)]
