@@ -70,11 +70,55 @@ __device__ __forceinline__ uint32_t eld_u32(const uint8_t *p) {   // 4 bytes at 
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 
+// the spatial neighbours A, B, C (or D) of a block as SetMotionVectorPredictor reads them (H.264
+// 8.4.1.3), and the MVP from them (set_mvp's rules): EPZS predictors 2-4 are the same reads
+struct MvpNb {   // scalar fields: a lane-indexed array would live in scratch
+    int va, ra, xa, ya, vb, rb, xb, yb, vc, rc, xc, yc;
+};
+template <class NB>
+__device__ __forceinline__ void set_mvp_nb(const NB &nb, int bx4, int bby4, int bsx, int bsy, int &px, int &py, MvpNb &n) {
+    int ra = -1, rb = -1, rc = -1, rd = -1, ax = 0, ay = 0, bxv = 0, byv = 0, cx = 0, cy = 0, dx = 0, dy = 0;
+    const int mb_x = 4 * bx4, mb_y = 4 * bby4;
+    const bool av_a = nb(mb_x - 1, mb_y, ra, ax, ay);
+    const bool av_b = nb(mb_x, mb_y - 1, rb, bxv, byv);
+    bool av_c = nb(mb_x + bsx, mb_y - 1, rc, cx, cy);
+    const bool av_d = nb(mb_x - 1, mb_y - 1, rd, dx, dy);
+    if (mb_y > 0) {
+        if (mb_x < 8) {
+            if (mb_y == 8) { if (bsx == 16) av_c = false; }
+            else if (mb_x + bsx == 8) av_c = false;
+        } else if (mb_x + bsx == 16) av_c = false;
+    }
+    if (!av_c) { av_c = av_d; rc = rd; cx = dx; cy = dy; }
+    n.va = av_a; n.ra = ra; n.xa = ax; n.ya = ay;
+    n.vb = av_b; n.rb = rb; n.xb = bxv; n.yb = byv;
+    n.vc = av_c; n.rc = rc; n.xc = cx; n.yc = cy;
+    const int rL = av_a ? ra : -1, rU = av_b ? rb : -1, rUR = av_c ? rc : -1;
+    int type = 0;
+    if (rL == 0 && rU != 0 && rUR != 0) type = 1;
+    else if (rL != 0 && rU == 0 && rUR != 0) type = 2;
+    else if (rL != 0 && rU != 0 && rUR == 0) type = 3;
+    if (bsx == 8 && bsy == 16) { if (mb_x == 0) { if (rL == 0) type = 1; } else if (rUR == 0) type = 3; }
+    else if (bsx == 16 && bsy == 8) { if (mb_y == 0) { if (rU == 0) type = 2; } else if (rL == 0) type = 1; }
+    const int A[2] = {av_a ? ax : 0, av_a ? ay : 0}, B[2] = {av_b ? bxv : 0, av_b ? byv : 0}, C[2] = {av_c ? cx : 0, av_c ? cy : 0};
+    int p[2];
+#pragma unroll
+    for (int hv = 0; hv < 2; hv++) {
+        const int a = A[hv], b = B[hv], c = C[hv];
+        if (type == 1) p[hv] = a;
+        else if (type == 2) p[hv] = b;
+        else if (type == 3) p[hv] = c;
+        else if (!(av_b || av_c)) p[hv] = a;
+        else p[hv] = a + b + c - min(a, min(b, c)) - max(a, max(b, c));
+    }
+    px = p[0]; py = p[1];
+}
+
 // EPZS predictor i of a search (oracle/encode.c epzs_predictors order): 0 centre, 1 zero, 2-4
-// spatial A / B / C (or D), 5-28 window rings R/4, R/2, R, 29-33 temporal (co-located, left,
-// right, up, down), 34 spatial memory (left MB), 35-40 earlier block types.  False if not valid
-// or outside the window around the centre.
-__device__ __forceinline__ bool epzs_cand(const DevParams &d, const EpzS &s, int i, int bt, int bx4, int by4, int b8, int best8x8,
+// spatial A / B / C (or D) (nb: the MVP's neighbour reads), 5-28 window rings R/4, R/2, R,
+// 29-33 temporal (co-located, left, right, up, down), 34 spatial memory (left MB), 35-40 earlier
+// block types.  False if not valid or outside the window around the centre.
+__device__ __forceinline__ bool epzs_cand(const DevParams &d, const EpzS &s, int i, int bt, int bx4, int by4, const MvpNb &nb,
                                           int range, int mvx0, int mvy0, int &x, int &y) {
     const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt), k0 = by4 * 4 + bx4;
     auto rnd = [](int v) { return (v + 2) >> 2; };
@@ -83,9 +127,13 @@ __device__ __forceinline__ bool epzs_cand(const DevParams &d, const EpzS &s, int
     if (i == 0) { x = mvx0; y = mvy0; }
     else if (i == 1) { }
     else if (i <= 4) {
-        int ref = -1, ax = 0, ay = 0;
-        v = mvp_nbr(NbEpz{s, bt, b8, best8x8}, bx4, by4, 4 * w4, i - 2, ref, ax, ay) && ref == 0;
-        x = rnd(ax); y = rnd(ay);
+        const int k = i - 2;
+        // bit masks, not selects: a select of struct fields becomes an indexed scratch load
+        const int m0 = -(k == 0), m1 = -(k == 1), m2 = -(k == 2);
+        const int av = (nb.va & m0) | (nb.vb & m1) | (nb.vc & m2), ref = (nb.ra & m0) | (nb.rb & m1) | (nb.rc & m2);
+        v = av && ref == 0;
+        x = rnd((nb.xa & m0) | (nb.xb & m1) | (nb.xc & m2));
+        y = rnd((nb.ya & m0) | (nb.yb & m1) | (nb.yc & m2));
     } else if (i <= 28) {
         const int ring = (i - 5) >> 3, k = (i - 5) & 7, rr = range >> (2 - ring);
         const int wx = k == 1 || k == 4 || k == 6 ? -1 : k == 2 || k == 5 || k == 7 ? 1 : 0;
@@ -106,6 +154,10 @@ __device__ __forceinline__ bool epzs_cand(const DevParams &d, const EpzS &s, int
     } else v = false;
     return v && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
 }
+
+// offsets (dx + 4) | (dy + 4) << 4 of the 41 positions with |dx| + |dy| <= 4 (refinement batches)
+static __constant__ uint8_t c_dia41[41] = {4,  19, 20, 21, 34, 35, 36, 37, 38, 49, 50, 51, 52, 53, 54, 55, 64, 65, 66, 67, 68,
+                                           69, 70, 71, 72, 81, 82, 83, 84, 85, 86, 87, 98, 99, 100, 101, 102, 115, 116, 117, 132};
 
 // refinement pattern point e: small diamond (0,-1) (-1,0) (1,0) (0,1); extended diamond (0,-2)
 // (-1,-1) (1,-1) (-2,0) (2,0) (-1,1) (1,1) (0,2) then the small diamond
@@ -201,7 +253,11 @@ __device__ __forceinline__ int hp_satd(const EpzS &s, int gx0, int gy0, int sx, 
 
 // BlockMotionSearch [J] of one block on the wave: EPZS full pel + SubPelBlockMotionSearch
 template <int BT>
-__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off, int bx4, int by4, int mc, int b8, int best8x8) {
+__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off, int bx4, int by4, int mc, int b8, int best8x8, bool prof) {
+    // debug (JMH_PHASE_PROF): steps of the MB's first 4x4 search into prof[41..46]
+    const bool sp = prof && BT == 7 && bx4 == 0 && by4 == 0;
+#define SSTAMP(k) do { if (sp) d.prof[41 + (k)] = wall_clock64(); } while (0)
+    SSTAMP(0);
     constexpr int LW4 = BT <= 2 ? 2 : (BT <= 5 ? 1 : 0), LH4 = (BT == 1 || BT == 3) ? 2 : (BT == 2 || BT == 4 || BT == 6) ? 1 : 0;
     constexpr int W4 = 1 << LW4, H4 = 1 << LH4, LNS = LW4 + LH4, NSUB = 1 << LNS;
     const int lane = threadIdx.x;
@@ -209,18 +265,21 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
     const bool slice_p = d.slice_type == JMH_P_SLICE;
     const int range = d.restrict_sr == 0 ? d.sr / min(2, BT) : d.sr;
     int pmx, pmy;
-    set_mvp(NbEpz{s, BT, b8, best8x8}, bx4, by4, 4 * W4, 4 * H4, pmx, pmy);
+    MvpNb nb;
+    set_mvp_nb(NbEpz{s, BT, b8, best8x8}, bx4, by4, 4 * W4, 4 * H4, pmx, pmy, nb);
     pmx = __builtin_amdgcn_readfirstlane(pmx);
     pmy = __builtin_amdgcn_readfirstlane(pmy);
     const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
     const int med = 16 * W4 * H4;
+    SSTAMP(1);
     // ---- full pel: predictor `lane`, then pattern rounds
     int cx, cy;
-    const bool cv = epzs_cand(d, s, lane, BT, bx4, by4, b8, best8x8, range, mvx0, mvy0, cx, cy);
+    const bool cv = epzs_cand(d, s, lane, BT, bx4, by4, nb, range, mvx0, mvy0, cx, cy);
     if (!cv) { cx = mvx0; cy = mvy0; }   // any valid position for the SAD (key discarded)
     const int c0 = (int)lane_block_sad<LW4, LH4>(s, off, bx4, by4, cx, cy) +
                    (int)__umul24(lam, mvbits(4 * cx - pmx) + mvbits(4 * cy - pmy));
     const int cost0 = __builtin_amdgcn_readfirstlane(c0);   // predictor 0: the centre, always valid
+    SSTAMP(2);
     int bx = mvx0, by = mvy0, min_mcost = cost0;
     if (cost0 >= med) {                                    // else: stop at the centre
         const unsigned m0 = wave_min_u32(cv ? ((unsigned)c0 << 6) | (unsigned)lane : 0xFFFFFFFFu);
@@ -228,29 +287,40 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
         bx = __builtin_amdgcn_readlane(cx, m0 & 63);
         by = __builtin_amdgcn_readlane(cy, m0 & 63);
         if (min_mcost >= med) {                            // pattern refinement until it stops
+            // Rounds are resolved in batches: the cost of every position within |dx| + |dy| <= 4
+            // of the batch centre (one per lane, 41 lanes), then up to 2 extended-diamond rounds
+            // (each moves <= 2) or 4 small-diamond rounds (<= 1) on those costs, exactly as JM
+            // scans them (pattern order, strict '<', window check); then a new batch.
             const bool sd = min_mcost < med + ((3 * med) >> 1);
-            const int np = sd ? 4 : 12;
-            int px = 0, py = 0;
-            epzs_pat(sd, lane, px, py);
-            for (int it = 0; it < 4 * NPOS_MAX; it++) {
-                const int x = bx + px, y = by + py;
-                const bool v = lane < np && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
-                unsigned k = 0xFFFFFFFFu;
-                if (v) {
-                    const int c = (int)lane_block_sad<LW4, LH4>(s, off, bx4, by4, x, y) +
-                                  (int)__umul24(lam, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
-                    k = ((unsigned)c << 6) | (unsigned)lane;
+            const int steps = sd ? 4 : 2;
+            const int dia = lane < 41 ? (int)c_dia41[lane] : 0x44;
+            const int ddx = (dia & 15) - 4, ddy = (dia >> 4) - 4;
+            for (bool done = false; !done;) {
+                const int x = bx + ddx, y = by + ddy;
+                const bool inw = lane < 41 && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
+                int c = 0;
+                if (inw) c = (int)lane_block_sad<LW4, LH4>(s, off, bx4, by4, x, y) + (int)__umul24(lam, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+                for (int k = 0; k < steps; k++) {
+                    const int rx = x - bx, ry = y - by;   // this lane's position relative to the current best
+                    int e = 15;
+                    if (sd) { if (abs(rx) <= 1 && abs(ry) <= 1) e = (int)((0xf3f2f1f0full >> (4 * ((ry + 1) * 3 + rx + 1))) & 15); }
+                    else if (abs(rx) <= 2 && abs(ry) <= 2) {
+                        const int i = (ry + 2) * 5 + rx + 2;
+                        e = (int)((i < 16 ? 0xf4af93f281fff0ffull >> (4 * i) : 0xff7fff6b5ull >> (4 * (i - 16))) & 15);
+                    }
+                    const unsigned m = wave_min_u32(inw && e != 15 ? ((unsigned)c << 6) | (unsigned)e : 0xFFFFFFFFu);
+                    if (m == 0xFFFFFFFFu || (int)(m >> 6) >= min_mcost) { done = true; break; }
+                    min_mcost = (int)(m >> 6);
+                    int px, py;
+                    epzs_pat(sd, (int)(m & 63), px, py);
+                    bx += px; by += py;
                 }
-                const unsigned m = wave_min_u32(k);
-                if (m == 0xFFFFFFFFu || (int)(m >> 6) >= min_mcost) break;
-                min_mcost = (int)(m >> 6);
-                bx = __builtin_amdgcn_readlane(x, m & 63);
-                by = __builtin_amdgcn_readlane(y, m & 63);
             }
         }
     }
     const int fmx = bx, fmy = by;
     if (had) min_mcost = BIGCOST;
+    SSTAMP(3);
     // ---- sub-pel neighbourhood of the block at (fmx, fmy): b, h, j planes, sample [y][x] =
     //      block-relative (x - 1, y - 1); b1 = unclipped horizontal taps, row rr <-> y = rr - 2
     constexpr int PW = 4 * W4 + 2, PH = 4 * H4 + 2;
@@ -273,39 +343,93 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
             (uint8_t)clip255((tap6(s.b1[y][x], s.b1[y + 1][x], s.b1[y + 2][x], s.b1[y + 3][x], s.b1[y + 4][x], s.b1[y + 5][x]) + 512) >> 10);
     }
     wave_lds_sync();
-    // ---- half then quarter pel: lane task = (candidate, 4x4 sub-block), JM order, strict '<'
+    SSTAMP(4);
+    // ---- half then quarter pel, JM order, strict '<'
     const bool check0 = BT == 1 && fmx == 0 && fmy == 0 && had && slice_p;
     int qx = 0, qy = 0;
+    if constexpr (NSUB <= 4) {
+        // blocks of up to four 4x4: the SATD of every position of the 7x7 quarter-pel grid around
+        // the full-pel MV in one batch (lane task = (position, 4x4 sub-block)), then the half-pel
+        // pass over the 9 even positions and the quarter-pel pass around its winner on the costs
+        constexpr int NIT = (49 * NSUB + NTE - 1) / NTE;
+        int cst[NIT];
 #pragma unroll
-    for (int pass = 0; pass < 2; pass++) {
-        const int step = pass == 0 ? 2 : 1, min_pos = pass == 0 ? (had ? 0 : 1) : 1;
-        unsigned kb = 0xFFFFFFFFu;
-#pragma unroll
-        for (int t0 = 0; t0 < (9 << LNS); t0 += NTE) {
-            const int task = t0 + lane, c = task >> LNS, sub = task & (NSUB - 1);
-            const bool val = c < 9 && c >= min_pos;
-            const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+        for (int it = 0; it < NIT; it++) {
+            const int task = it * NTE + lane, p = task >> LNS, sub = task & (NSUB - 1);
+            const int ox = p % 7 - 3, oy = p / 7 - 3;
             int sat = 0;
-            if (val) {
+            if (p < 49) {
                 const int sx = 4 * (sub & (W4 - 1)), sy = 4 * (sub >> LW4);
                 sat = hp_satd(s, gx0, gy0, sx, sy, 64 * by4 + 4 * bx4 + 16 * sy + sx, ox, oy, had);
             }
             if constexpr (NSUB >= 2) sat += dpp<0xB1>(sat);
             if constexpr (NSUB >= 4) sat += dpp<0x4E>(sat);
-            if constexpr (NSUB >= 8) sat += dpp<0x141>(sat);
-            if constexpr (NSUB >= 16) sat += dpp<0x140>(sat);
-            if (val && sub == 0) {
-                int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmx) + mvbits(4 * fmy + oy - pmy));
-                if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
-                kb = min(kb, ((unsigned)(cost + EKOFF) << 4) | (unsigned)c);
+            cst[it] = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmx) + mvbits(4 * fmy + oy - pmy));
+        }
+        // candidate index of offset (dx, dy) in {-1,0,1}^2 (spiral entries 0..8)
+        auto c9 = [](int dx, int dy) { return (int)((0x827605413ull >> (4 * ((dy + 1) * 3 + dx + 1))) & 15); };
+        const int min_pos = had ? 0 : 1;
+        unsigned kb = 0xFFFFFFFFu;
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int task = it * NTE + lane, p = task >> LNS, sub = task & (NSUB - 1);
+            const int ox = p % 7 - 3, oy = p / 7 - 3;
+            if (p < 49 && sub == 0 && !(ox & 1) && !(oy & 1) && abs(ox) <= 2 && abs(oy) <= 2) {
+                const int c = c9(ox >> 1, oy >> 1);
+                if (c >= min_pos) kb = min(kb, ((unsigned)(cst[it] - ((check0 && c == 0) ? 16 * lam : 0) + EKOFF) << 4) | (unsigned)c);
             }
         }
         kb = wave_min_u32(kb);
         if (kb != 0xFFFFFFFFu && (int)(kb >> 4) - EKOFF < min_mcost) {
-            const int c = kb & 15;
             min_mcost = (int)(kb >> 4) - EKOFF;
-            qx += step * sp9x(c);
-            qy += step * sp9y(c);
+            qx = 2 * sp9x(kb & 15); qy = 2 * sp9y(kb & 15);
+        }
+        kb = 0xFFFFFFFFu;
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int task = it * NTE + lane, p = task >> LNS, sub = task & (NSUB - 1);
+            const int ox = p % 7 - 3, oy = p / 7 - 3;
+            if (p < 49 && sub == 0 && abs(ox - qx) <= 1 && abs(oy - qy) <= 1 && (ox != qx || oy != qy))
+                kb = min(kb, ((unsigned)(cst[it] + EKOFF) << 4) | (unsigned)c9(ox - qx, oy - qy));
+        }
+        kb = wave_min_u32(kb);
+        if (kb != 0xFFFFFFFFu && (int)(kb >> 4) - EKOFF < min_mcost) {
+            min_mcost = (int)(kb >> 4) - EKOFF;
+            qx += sp9x(kb & 15); qy += sp9y(kb & 15);
+        }
+    } else {
+        // larger blocks: half pass, then the quarter pass around its winner (9 x NSUB tasks each)
+#pragma unroll
+        for (int pass = 0; pass < 2; pass++) {
+            const int step = pass == 0 ? 2 : 1, min_pos = pass == 0 ? (had ? 0 : 1) : 1;
+            unsigned kb = 0xFFFFFFFFu;
+#pragma unroll
+            for (int t0 = 0; t0 < (9 << LNS); t0 += NTE) {
+                const int task = t0 + lane, c = task >> LNS, sub = task & (NSUB - 1);
+                const bool val = c < 9 && c >= min_pos;
+                const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+                int sat = 0;
+                if (val) {
+                    const int sx = 4 * (sub & (W4 - 1)), sy = 4 * (sub >> LW4);
+                    sat = hp_satd(s, gx0, gy0, sx, sy, 64 * by4 + 4 * bx4 + 16 * sy + sx, ox, oy, had);
+                }
+                sat += dpp<0xB1>(sat);
+                sat += dpp<0x4E>(sat);
+                sat += dpp<0x141>(sat);
+                if constexpr (NSUB >= 16) sat += dpp<0x140>(sat);
+                if (val && sub == 0) {
+                    int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmx) + mvbits(4 * fmy + oy - pmy));
+                    if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
+                    kb = min(kb, ((unsigned)(cost + EKOFF) << 4) | (unsigned)c);
+                }
+            }
+            kb = wave_min_u32(kb);
+            if (kb != 0xFFFFFFFFu && (int)(kb >> 4) - EKOFF < min_mcost) {
+                const int c = kb & 15;
+                min_mcost = (int)(kb >> 4) - EKOFF;
+                qx += step * sp9x(c);
+                qy += step * sp9y(c);
+            }
         }
     }
     if (lane < NSUB) {
@@ -315,6 +439,8 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
     }
     if (lane == 0) s.motion_cost[BT][mc] += min_mcost;
     wave_lds_sync();
+    SSTAMP(5);
+#undef SSTAMP
 }
 
 __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
@@ -352,21 +478,47 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     }
     if (lane == 0) s.memok = left >= 0;
     {
-        constexpr int ND4 = EST / 4;
-        const int WX0 = pix_x - off, WY0 = pix_y - off;
-        for (int task = lane; task < wdim * ND4; task += NTE) {
-            const int y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
-            const uint8_t *row = d.refY + iclip(0, d.H - 1, WY0 + y) * W;
-            uint32_t v;
-            if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
-                const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
-                v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
-            } else {
-                v = 0;
-                for (int q = 0; q < 4; q++)
-                    if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
+        // with SearchRange even the window's dwords are aligned in the picture (pix_x % 16 == 0,
+        // off % 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an
+        // outside dword is the replicated edge sample.  Batches of 8 loads per lane in flight.
+        constexpr int ND4 = EST / 4, NB = 8;
+        const int WX0 = pix_x - off, WY0 = pix_y - off, ntask = wdim * ND4;
+        if ((off & 3) == 0) {
+            for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
+                uint32_t v[NB];
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const int task = t0 + u * NTE + lane, y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
+                    const uint8_t *row = d.refY + iclip(0, d.H - 1, WY0 + y) * W;
+                    const int xs = x0 < 0 ? 0 : x0 >= W ? W - 4 : x0;
+                    v[u] = task < ntask ? *reinterpret_cast<const uint32_t *>(row + xs) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const int task = t0 + u * NTE + lane, y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
+                    if (task >= ntask) continue;
+                    uint32_t w = v[u];
+                    if (x0 < 0) w = (w & 0xFFu) * 0x01010101u;              // left of the picture
+                    else if (x0 >= W) w = (w >> 24) * 0x01010101u;          // right of it
+                    if (4 * j >= wdim) w = 0;
+                    *reinterpret_cast<uint32_t *>(s.g + y * EST + 4 * j) = w;
+                }
             }
-            *reinterpret_cast<uint32_t *>(s.g + y * EST + 4 * j) = v;
+        } else {   // odd SearchRange: two aligned global dwords + v_alignbyte, clamped bytes at the edges
+            for (int task = lane; task < ntask; task += NTE) {
+                const int y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
+                const uint8_t *row = d.refY + iclip(0, d.H - 1, WY0 + y) * W;
+                uint32_t v;
+                if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
+                    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
+                    v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
+                } else {
+                    v = 0;
+                    for (int q = 0; q < 4; q++)
+                        if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
+                }
+                *reinterpret_cast<uint32_t *>(s.g + y * EST + 4 * j) = v;
+            }
         }
     }
     wave_lds_sync();
@@ -374,25 +526,25 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     // PartitionMotionSearch [J] order: 16x16, 16x8 (2), 8x16 (2), then per 8x8 block the sub-modes
     // 4..7 and its best sub-mode (read through best8x8)
     int best8x8 = 0, cost8x8 = 0;
-    epzs_block<1>(d, s, off, 0, 0, 0, 0, 0);
+    epzs_block<1>(d, s, off, 0, 0, 0, 0, 0, prof);
     if (prof) d.prof[34] = wall_clock64();
-    epzs_block<2>(d, s, off, 0, 0, 0, 0, 0);
-    epzs_block<2>(d, s, off, 0, 2, 1, 0, 0);
-    epzs_block<3>(d, s, off, 0, 0, 0, 0, 0);
-    epzs_block<3>(d, s, off, 2, 0, 1, 0, 0);
+    epzs_block<2>(d, s, off, 0, 0, 0, 0, 0, prof);
+    epzs_block<2>(d, s, off, 0, 2, 1, 0, 0, prof);
+    epzs_block<3>(d, s, off, 0, 0, 0, 0, 0, prof);
+    epzs_block<3>(d, s, off, 2, 0, 1, 0, 0, prof);
     if (prof) d.prof[35] = wall_clock64();
 #pragma unroll 1
     for (int b8 = 0; b8 < 4; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        epzs_block<4>(d, s, off, X, Y, b8, b8, best8x8);
-        epzs_block<5>(d, s, off, X, Y, b8, b8, best8x8);
-        epzs_block<5>(d, s, off, X, Y + 1, b8, b8, best8x8);
-        epzs_block<6>(d, s, off, X, Y, b8, b8, best8x8);
-        epzs_block<6>(d, s, off, X + 1, Y, b8, b8, best8x8);
-        epzs_block<7>(d, s, off, X, Y, b8, b8, best8x8);
-        epzs_block<7>(d, s, off, X + 1, Y, b8, b8, best8x8);
-        epzs_block<7>(d, s, off, X, Y + 1, b8, b8, best8x8);
-        epzs_block<7>(d, s, off, X + 1, Y + 1, b8, b8, best8x8);
+        epzs_block<4>(d, s, off, X, Y, b8, b8, best8x8, prof);
+        epzs_block<5>(d, s, off, X, Y, b8, b8, best8x8, prof);
+        epzs_block<5>(d, s, off, X, Y + 1, b8, b8, best8x8, prof);
+        epzs_block<6>(d, s, off, X, Y, b8, b8, best8x8, prof);
+        epzs_block<6>(d, s, off, X + 1, Y, b8, b8, best8x8, prof);
+        epzs_block<7>(d, s, off, X, Y, b8, b8, best8x8, prof);
+        epzs_block<7>(d, s, off, X + 1, Y, b8, b8, best8x8, prof);
+        epzs_block<7>(d, s, off, X, Y + 1, b8, b8, best8x8, prof);
+        epzs_block<7>(d, s, off, X + 1, Y + 1, b8, b8, best8x8, prof);
         int mc8 = BIGCOST, bm = 0;
         for (int mode = 4; mode <= 7; mode++) {
             if (!inter_on(d.isr, mode)) continue;

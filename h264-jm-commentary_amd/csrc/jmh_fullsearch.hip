@@ -1,6 +1,6 @@
 // jmh_fullsearch.hip — k_mb_me_full: the motion-search half of encode_one_macroblock [J] with
-// SearchMode = -1 (FullPelBlockMotionSearch) or SearchMode = 3 (EPZSPelBlockMotionSearch, see
-// epzs_fullpel below), one 256-thread workgroup per P macroblock.
+// SearchMode = -1 (FullPelBlockMotionSearch), one 256-thread workgroup per P macroblock (EPZS,
+// SearchMode 3, has its own one-wave kernel: jmh_epzs.hip).
 //
 // Unlike FFS, every search centres its window on its OWN predictor (MVP/4 clamped to its range),
 // so there is no shared SAD table: each of the 41 searches computes the SAD of its block at all
@@ -21,7 +21,6 @@
 #define FST 156                               // window row stride (>= FW_MAX + 4, multiple of 4)
 #define FKOFF 4096                            // cost offset in keys (16x16 zero-vector bias)
 
-#define NPRED 41                              // EPZS predictor slots (oracle epzs_predictors)
 
 struct FullS {
     uint8_t g[FW_MAX * FST + 16];
@@ -32,10 +31,6 @@ struct FullS {
     unsigned red[2][NTF / 64];
     int ccost[2][9];
     int cost0;
-    int16_t tmv[6][6][2];                      // EPZS temporal: previous picture's MVs around the MB
-    int8_t tref[6][6];                         //   (4x4 units, MB origin at [1][1]; -1: none)
-    int16_t mem[8][16][2];                     // EPZS spatial memory: the left MB's searches
-    int memok;
     uint8_t hp[3][18][20];                     // half-pel b / h / j around the block at its full-pel MV
 };
 
@@ -72,17 +67,6 @@ __device__ __forceinline__ uint32_t lds_u32(const uint8_t *p) {   // 4 bytes at 
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 
-// SAD of the block (bx4, by4, 4 w4 x 4 h4) at full-pel displacement (mx, my) from the LDS window
-// on a 16-lane group: lane r sums row r (rows >= 4 h4 contribute 0); all 16 lanes get the sum
-__device__ __forceinline__ int group_sad(const FullS &s, int off, int bx4, int by4, int w4, int h4, int mx, int my, int r) {
-    uint32_t sad = 0;
-    if (r < 4 * h4) {
-        const uint8_t *row = s.g + (off + 4 * by4 + r + my) * FST + off + 4 * bx4 + mx;
-        const uint32_t *org = reinterpret_cast<const uint32_t *>(s.org + (4 * by4 + r) * 16 + 4 * bx4);
-        for (int q = 0; q < w4; q++) sad = __builtin_amdgcn_sad_u8(lds_u32(row + 4 * q), org[q], sad);
-    }
-    return row16_sum((int)sad);
-}
 // workgroup minimum of per-thread keys (double-buffered slot: consecutive calls need no second
 // barrier); every thread returns the minimum
 __device__ __forceinline__ unsigned wg_min(FullS &s, unsigned k, int &slot) {
@@ -96,104 +80,9 @@ __device__ __forceinline__ unsigned wg_min(FullS &s, unsigned k, int &slot) {
     return m;
 }
 
-// EPZS predictor i of a search (oracle/encode.c epzs_predictors order): 0 centre, 1 zero, 2-4
-// spatial A / B / C, 5-28 window rings R/4, R/2, R, 29-33 temporal (co-located, left, right, up,
-// down), 34 spatial memory (left MB), 35-40 earlier block types.  Returns false if not valid or
-// outside the window around the centre.  Temporal and memory data come from LDS (prefetched).
-__device__ __forceinline__ bool epzs_cand(const DevParams &d, const FullS &s, int i, int bt, int bx4, int by4, int b8, int best8x8,
-                                          int range, int mvx0, int mvy0, int &x, int &y) {
-    const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt), k0 = by4 * 4 + bx4;
-    auto rnd = [](int v) { return (v + 2) >> 2; };
-    bool v = true;
-    x = 0; y = 0;
-    if (i == 0) { x = mvx0; y = mvy0; }
-    else if (i == 1) { }
-    else if (i <= 4) {
-        int ref = -1, ax = 0, ay = 0;
-        v = mvp_nbr(NbFull{s, bt, b8, best8x8}, bx4, by4, 4 * w4, i - 2, ref, ax, ay) && ref == 0;
-        x = rnd(ax); y = rnd(ay);
-    } else if (i <= 28) {
-        const int ring = (i - 5) >> 3, k = (i - 5) & 7, rr = range >> (2 - ring);
-        const int wx = k == 1 || k == 4 || k == 6 ? -1 : k == 2 || k == 5 || k == 7 ? 1 : 0;
-        const int wy = k == 0 || k == 4 || k == 5 ? -1 : k == 3 || k == 6 || k == 7 ? 1 : 0;
-        v = rr > 0; x = mvx0 + rr * wx; y = mvy0 + rr * wy;
-    } else if (i <= 33) {
-        const int k = i - 29;                                  // co-located, left, right, up, down
-        const int tx = 1 + bx4 + (k == 1 ? -1 : k == 2 ? w4 : 0), ty = 1 + by4 + (k == 3 ? -1 : k == 4 ? h4 : 0);
-        v = s.tref[ty][tx] == 0;
-        x = rnd(s.tmv[ty][tx][0]); y = rnd(s.tmv[ty][tx][1]);
-    } else if (i == 34) {
-        v = s.memok && inter_on(d.isr, bt);                     // left MB's search (spatial memory)
-        x = rnd(s.mem[bt][k0][0]); y = rnd(s.mem[bt][k0][1]);
-    } else if (i < NPRED) {
-        const int t = i - 34;                                  // block types 1..6 below bt
-        v = t < bt && inter_on(d.isr, t);
-        x = rnd(s.all_mv[t][k0][0]); y = rnd(s.all_mv[t][k0][1]);
-    } else v = false;
-    return v && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
-}
-
-// refinement pattern point e: small diamond (0,-1) (-1,0) (1,0) (0,1); extended diamond (0,-2)
-// (-1,-1) (1,-1) (-2,0) (2,0) (-1,1) (1,1) (0,2) then the small diamond
-__device__ __forceinline__ void epzs_pat(bool sd, int e, int &px, int &py) {
-    if (sd) { px = e == 1 ? -1 : e == 2 ? 1 : 0; py = e == 0 ? -1 : e == 3 ? 1 : 0; return; }
-    px = e < 8 ? (e == 1 || e == 5 ? -1 : e == 2 || e == 6 ? 1 : e == 3 ? -2 : e == 4 ? 2 : 0) : (e == 9 ? -1 : e == 10 ? 1 : 0);
-    py = e < 8 ? (e == 0 ? -2 : e <= 2 ? -1 : e <= 4 ? 0 : e <= 6 ? 1 : 2) : (e == 8 ? -1 : e == 11 ? 1 : 0);
-}
-
-// EPZSPelBlockMotionSearch [J] as restated in oracle/encode.c epzs_search (JM_SEMANTICS items
-// 33-40): the centre, then 40 ordered predictors, strict '<' in list order (the key's low bits),
-// medthres = block pixels, then small- or extended-diamond refinement around the best until it
-// stops moving.  One 16-lane group per candidate SAD; one barrier per candidate round.
-__device__ void epzs_fullpel(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int b8, int best8x8, int range,
-                             int mvx0, int mvy0, int pmx, int pmy, int &fmx, int &fmy, int &fcost) {
-    const int tid = threadIdx.x, g = tid >> 4, r = tid & 15;
-    const int lam = d.lambda_motion;
-    const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt);
-    const int med = 16 * w4 * h4;
-    int slot = 0;
-    unsigned kb = 0xFFFFFFFFu;
-    for (int i = g; i < NPRED; i += 16) {
-        int x, y;
-        const bool v = epzs_cand(d, s, i, bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, x, y);
-        if (!v) { x = mvx0; y = mvy0; }
-        const int c = group_sad(s, off, bx4, by4, w4, h4, x, y, r) + lam * (mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
-        if (i == 0 && r == 0) s.cost0 = c;
-        if (v) kb = min(kb, ((unsigned)c << 6) | (unsigned)i);
-    }
-    const unsigned best = wg_min(s, kb, slot);
-    int bx = mvx0, by = mvy0, min_mcost = s.cost0;
-    if (min_mcost >= med) {                                   // else: stop at the centre
-        min_mcost = (int)(best >> 6);
-        epzs_cand(d, s, (int)(best & 63), bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, bx, by);
-        if (min_mcost >= med) {                               // pattern refinement
-            const bool sd = min_mcost < med + ((3 * med) >> 1);
-            const int np = sd ? 4 : 12;
-            for (int it = 0; it < 4 * NPOS_MAX; it++) {
-                unsigned k = 0xFFFFFFFFu;
-                if (g < np) {
-                    int px, py;
-                    epzs_pat(sd, g, px, py);
-                    const int x = bx + px, y = by + py;
-                    const bool v = abs(x - mvx0) <= range && abs(y - mvy0) <= range;
-                    const int c = group_sad(s, off, bx4, by4, w4, h4, v ? x : bx, v ? y : by, r) + lam * (mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
-                    if (v) k = ((unsigned)c << 6) | (unsigned)g;
-                }
-                const unsigned m = wg_min(s, k, slot);
-                if (m == 0xFFFFFFFFu || (int)(m >> 6) >= min_mcost) break;
-                min_mcost = (int)(m >> 6);
-                int px, py;
-                epzs_pat(sd, (int)(m & 63), px, py);
-                bx += px; by += py;
-            }
-        }
-    }
-    fmx = bx; fmy = by; fcost = min_mcost;
-}
-
 // BlockMotionSearch [J] for one block: full-pel full search + SubPelBlockMotionSearch
 __device__ __forceinline__ void full_block_search(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int mc, int b8,
-                                                           int best8x8, int X0, int Y0, int left, int pslot) {
+                                                           int best8x8, int X0, int Y0, int pslot) {
     const int tid = threadIdx.x;
     const bool prof = pslot >= 0 && pslot < 28 && d.prof && tid == 0 && d.prof_mb == (Y0 >> 2) * d.mbw + (X0 >> 2);
     const int lam = d.lambda_motion, had = d.use_hadamard;
@@ -204,11 +93,7 @@ __device__ __forceinline__ void full_block_search(const DevParams &d, FullS &s, 
     set_mvp(NbFull{s, bt, b8, best8x8}, bx4, by4, 4 * w4, 4 * h4, pmx, pmy);
     const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
     int fmx, fmy, min_mcost;
-    if (d.search_mode == 3) {
-        epzs_fullpel(d, s, off, bt, bx4, by4, b8, best8x8, range, mvx0, mvy0, pmx, pmy, fmx, fmy, min_mcost);
-        if (had) min_mcost = BIGCOST;
-        if (prof) d.prof[34 + pslot] = wall_clock64();
-    } else {
+    {
     // ---- full pel: every thread a stride of positions, SADs by dword v_sad_u8
     const int side = 2 * range + 1, npos = side * side;
     unsigned kb = 0xFFFFFFFFu;
@@ -305,27 +190,11 @@ __global__ __launch_bounds__(NTF, 6) void k_mb_me_full(const TickArgs t) {
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, sr = d.sr;
     const int off = 2 * sr + 4, wdim = 16 + 2 * off;
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
-    const int X0 = 4 * mbx, Y0 = 4 * mby, left = mbx > 0 ? mby * d.mbw + mbx - 1 : -1;   // EPZS
+    const int X0 = 4 * mbx, Y0 = 4 * mby;
     if (d.prof && tid == 0 && d.prof_mb == mby * d.mbw + mbx) d.prof[32] = wall_clock64();
     s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     if (tid < 10) load_border(d, s.bd, tid, mbx, mby);
     else if (tid >= 32 && tid < 64) s.motion_cost[(tid - 32) >> 2][tid & 3] = 0;
-    if (d.search_mode == 3) {   // EPZS: temporal neighbourhood and the left MB's searches into LDS
-        if (tid >= 128 && tid < 164) {
-            const int i = tid - 128, ty = i / 6, tx = i - 6 * ty, px = X0 - 1 + tx, py = Y0 - 1 + ty;
-            int ref = -1, mx = 0, my = 0;
-            if (d.tref && px >= 0 && px < (W >> 2) && py >= 0 && py < (d.H >> 2)) {
-                const int a = py * (W >> 2) + px;
-                ref = d.tref[a]; mx = d.tmv[2 * a]; my = d.tmv[2 * a + 1];
-            }
-            s.tref[ty][tx] = (int8_t)ref; s.tmv[ty][tx][0] = (int16_t)mx; s.tmv[ty][tx][1] = (int16_t)my;
-        }
-        for (int i = tid; i < 7 * 32; i += NTF) {
-            const int m = 1 + i / 32, k = (i & 31) >> 1, c = i & 1;
-            s.mem[m][k][c] = left >= 0 ? d.scr[left].all_mv[m][k][c] : 0;
-        }
-        if (tid == 0) s.memok = left >= 0;
-    }
     {   // window: MB pixel (0,0) at (off, off); per-coordinate clamping is the spec's UMV access
         constexpr int ND4 = FST / 4;
         const int X0 = pix_x - off, Y0 = pix_y - off;
@@ -363,7 +232,7 @@ __global__ __launch_bounds__(NTF, 6) void k_mb_me_full(const TickArgs t) {
             const int sx = j == 4 || j == 6 || j == 8 ? 1 : 0, sy = j == 2 || j == 7 || j == 8 ? 1 : 0;
             bx4 = 2 * (b8 & 1) + sx; by4 = 2 * (b8 >> 1) + sy;
         }
-        full_block_search(d, s, off, bt, bx4, by4, mc, b8, i < 5 ? 0 : best8x8, X0, Y0, left, i < 14 ? 2 * i : -1);
+        full_block_search(d, s, off, bt, bx4, by4, mc, b8, i < 5 ? 0 : best8x8, X0, Y0, i < 14 ? 2 * i : -1);
         if (i >= 5 && (i - 5) % 9 == 8) {
             int mc8 = BIGCOST, bm = 0;
             for (int mode = 4; mode <= 7; mode++) {
