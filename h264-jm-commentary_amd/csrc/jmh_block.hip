@@ -22,9 +22,12 @@ __device__ __forceinline__ int mv_cost_lf(int lf, int shift, int cx, int cy, int
     return (lf * (mvbits((cx << shift) - px) + mvbits((cy << shift) - py))) >> 16;   // MV_COST [J]
 }
 
-__global__ __launch_bounds__(256) void k_block_search(const jmh_block_search *reqs, jmh_block_result *out, const uint8_t *cur,
-                                                      const uint8_t *ref, int W, int H, int had) {
-    __shared__ uint8_t org[256];
+// T: uint8_t (8-bit) or uint16_t (High 10 seam, jmh_block_motion_search_u16: maxv = 2^bd - 1, the
+// quarter-pel samples clipped to it; a 16x16 cost needs 19 bits, the key's 13-bit order still fits)
+template <class T>
+__global__ __launch_bounds__(256) void k_block_search(const jmh_block_search *reqs, jmh_block_result *out, const T *cur, const T *ref,
+                                                      int W, int H, int had, int maxv) {
+    __shared__ T org[256];
     __shared__ unsigned red[4];
     __shared__ int csum[9];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -78,7 +81,7 @@ __global__ __launch_bounds__(256) void k_block_search(const jmh_block_search *re
             for (int y = 0; y < 4; y++)
 #pragma unroll
                 for (int x = 0; x < 4; x++)
-                    d[4 * y + x] = (int)org[(oy + y) * bw + ox + x] - qpel_direct(ref, W, H, 4 * (px0 + ox + x) + cx, 4 * (py0 + oy + y) + cy);
+                    d[4 * y + x] = (int)org[(oy + y) * bw + ox + x] - qpel_direct(ref, W, H, 4 * (px0 + ox + x) + cx, 4 * (py0 + oy + y) + cy, maxv);
             atomicAdd(&csum[c], satd4x4(d, had));
         }
         __syncthreads();
@@ -112,6 +115,11 @@ __global__ __launch_bounds__(256) void k_block_search(const jmh_block_search *re
 
 hipError_t jmh_launch_block_search(int n, const jmh_block_search *reqs, jmh_block_result *out, const uint8_t *cur, const uint8_t *ref, int W,
                                    int H, int had, hipStream_t st) {
-    hipLaunchKernelGGL(k_block_search, dim3(n), dim3(256), 0, st, reqs, out, cur, ref, W, H, had);
+    hipLaunchKernelGGL(k_block_search<uint8_t>, dim3(n), dim3(256), 0, st, reqs, out, cur, ref, W, H, had, 255);
+    return hipGetLastError();
+}
+hipError_t jmh_launch_block_search_u16(int n, const jmh_block_search *reqs, jmh_block_result *out, const uint16_t *cur, const uint16_t *ref,
+                                       int W, int H, int had, int bit_depth, hipStream_t st) {
+    hipLaunchKernelGGL(k_block_search<uint16_t>, dim3(n), dim3(256), 0, st, reqs, out, cur, ref, W, H, had, (1 << bit_depth) - 1);
     return hipGetLastError();
 }

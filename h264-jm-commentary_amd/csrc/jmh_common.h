@@ -49,7 +49,8 @@ __device__ __forceinline__ int mvbits(int v) { return v == 0 ? 1 : 2 * (31 - __c
 __device__ __forceinline__ int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
 // JM spiral index of relative position (x, y) (Init_Motion_Search_Module ordering)
 // ---- quarter-pel samples straight from the reference (H.264 8.4.2.2.1, spec clamping) ----
-__device__ __forceinline__ int rpx(const uint8_t *p, int w, int h, int x, int y) { return p[iclip(0, h - 1, y) * w + iclip(0, w - 1, x)]; }
+template <class T>
+__device__ __forceinline__ int rpx(const T *p, int w, int h, int x, int y) { return p[iclip(0, h - 1, y) * w + iclip(0, w - 1, x)]; }
 __device__ __forceinline__ int hb1(const uint8_t *p, int w, int h, int x, int y) {
     return tap6(rpx(p, w, h, x - 2, y), rpx(p, w, h, x - 1, y), rpx(p, w, h, x, y), rpx(p, w, h, x + 1, y), rpx(p, w, h, x + 2, y),
                 rpx(p, w, h, x + 3, y));
@@ -60,14 +61,14 @@ __device__ __forceinline__ int vh1(const uint8_t *p, int w, int h, int x, int y)
 }
 // one luma sample at quarter-pel position (X, Y) (units of 1/4 pel) from integer samples px(x, y):
 // only the half-pel samples the phase needs (G, b, h, s, m, j of Figure 8-4), same values as
-// k_interp's 16 planes
+// k_interp's 16 planes; maxv = (1 << BitDepthY) - 1 (Clip1Y)
 template <class PX>
-__device__ __forceinline__ int qpel_from(PX px, int X, int Y) {
+__device__ __forceinline__ int qpel_from(PX px, int X, int Y, int maxv = 255) {
     const int x = X >> 2, y = Y >> 2, fx = X & 3, fy = Y & 3;
     auto hb1p = [&](int xx, int yy) { return tap6(px(xx - 2, yy), px(xx - 1, yy), px(xx, yy), px(xx + 1, yy), px(xx + 2, yy), px(xx + 3, yy)); };
     auto vh1p = [&](int xx, int yy) { return tap6(px(xx, yy - 2), px(xx, yy - 1), px(xx, yy), px(xx, yy + 1), px(xx, yy + 2), px(xx, yy + 3)); };
-    auto hb = [&](int xx, int yy) { return clip255((hb1p(xx, yy) + 16) >> 5); };
-    auto vb = [&](int xx, int yy) { return clip255((vh1p(xx, yy) + 16) >> 5); };
+    auto hb = [&](int xx, int yy) { return iclip(0, maxv, (hb1p(xx, yy) + 16) >> 5); };
+    auto vb = [&](int xx, int yy) { return iclip(0, maxv, (vh1p(xx, yy) + 16) >> 5); };
     if (fy == 0) {
         const int G = px(x, y);
         if (fx == 0) return G;
@@ -82,14 +83,15 @@ __device__ __forceinline__ int qpel_from(PX px, int X, int Y) {
     int j1 = 0;
 #pragma unroll
     for (int k = 0; k < 6; k++) j1 += (k == 0 || k == 5 ? 1 : (k == 1 || k == 4 ? -5 : 20)) * vh1p(x - 2 + k, y);
-    const int j = clip255((j1 + 512) >> 10);
+    const int j = iclip(0, maxv, (j1 + 512) >> 10);
     if (fx == 2 && fy == 2) return j;
     const int o = fx == 2 ? hb(x, fy == 1 ? y : y + 1) : vb(fx == 1 ? x : x + 1, y);   // f q / i k
     return (j + o + 1) >> 1;
 }
 // ... straight from the reference picture in HBM, spec coordinate clamping (k_mb_final MC)
-__device__ __forceinline__ int qpel_direct(const uint8_t *ref, int W, int H, int X, int Y) {
-    return qpel_from([&](int x, int y) { return rpx(ref, W, H, x, y); }, X, Y);
+template <class T>
+__device__ __forceinline__ int qpel_direct(const T *ref, int W, int H, int X, int Y, int maxv = 255) {
+    return qpel_from([&](int x, int y) { return rpx(ref, W, H, x, y); }, X, Y, maxv);
 }
 
 __device__ __forceinline__ int spiral_index(int x, int y) {
@@ -170,8 +172,8 @@ __device__ __forceinline__ int lane_fwd4x4(int r, int l) {
     p0 = u0 + u3; p3 = u0 - u3; p1 = u1 + u2; p2 = u1 - u2;
     return y == 0 ? p0 + p1 : y == 1 ? 2 * p3 + p2 : y == 2 ? p0 - p1 : p3 - 2 * p2;
 }
-// inverse 4x4 (8.5.12.2, rows first) + reconstruction clip((x + (pred << 6) + 32) >> 6)
-__device__ __forceinline__ int lane_inv4x4(int dq, int l, int pred) {
+// inverse 4x4 (8.5.12.2, rows first) + reconstruction clip((x + (pred << 6) + 32) >> 6) to maxv
+__device__ __forceinline__ int lane_inv4x4(int dq, int l, int pred, int maxv = 255) {
     int y = l >> 2, x = l & 3;
     int d0 = g16(dq, 4 * y), d1 = g16(dq, 4 * y + 1), d2 = g16(dq, 4 * y + 2), d3 = g16(dq, 4 * y + 3);
     int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
@@ -179,7 +181,7 @@ __device__ __forceinline__ int lane_inv4x4(int dq, int l, int pred) {
     int f0 = g16(t, x), f1 = g16(t, 4 + x), f2 = g16(t, 8 + x), f3 = g16(t, 12 + x);
     e0 = f0 + f2; e1 = f0 - f2; e2 = (f1 >> 1) - f3; e3 = f1 + (f3 >> 1);
     int o = y == 0 ? e0 + e3 : y == 1 ? e1 + e2 : y == 2 ? e1 - e2 : e0 - e3;
-    return clip255((o + (pred << 6) + 32) >> 6);
+    return iclip(0, maxv, (o + (pred << 6) + 32) >> 6);
 }
 // quantisation (dct_luma / dct_chroma AC [J]) of coefficient c at raster l.
 //   lev_scan: signed level at SCAN position l; dq: dequantised coefficient at raster l;
@@ -496,14 +498,14 @@ __device__ __forceinline__ int wave_fwd8x8(int r, int l) {
     return fwd8_pick(w64(t, x), w64(t, 8 + x), w64(t, 16 + x), w64(t, 24 + x), w64(t, 32 + x), w64(t, 40 + x), w64(t, 48 + x),
                      w64(t, 56 + x), y);
 }
-// inverse 8x8 (rows first) + reconstruction clip((x + (pred << 6) + 32) >> 6)
-__device__ __forceinline__ int wave_inv8x8(int dq, int l, int pred) {
+// inverse 8x8 (rows first) + reconstruction clip((x + (pred << 6) + 32) >> 6) to maxv
+__device__ __forceinline__ int wave_inv8x8(int dq, int l, int pred, int maxv = 255) {
     const int x = l & 7, y = l >> 3, rb = 8 * y;
     const int t = inv8_pick(w64(dq, rb), w64(dq, rb + 1), w64(dq, rb + 2), w64(dq, rb + 3), w64(dq, rb + 4), w64(dq, rb + 5),
                             w64(dq, rb + 6), w64(dq, rb + 7), x);
     const int o = inv8_pick(w64(t, x), w64(t, 8 + x), w64(t, 16 + x), w64(t, 24 + x), w64(t, 32 + x), w64(t, 40 + x), w64(t, 48 + x),
                             w64(t, 56 + x), y);
-    return clip255((o + (pred << 6) + 32) >> 6);
+    return iclip(0, maxv, (o + (pred << 6) + 32) >> 6);
 }
 // quantisation of coefficient c at raster l (dct_luma8x8 [J]): lev_scan = signed level at SCAN
 // position l, dq = normative 8.5.13.1 dequantisation of the signed level at raster l (flat

@@ -26,6 +26,14 @@ hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_block_search_u16(int n, const jmh_block_search *reqs, jmh_block_result *out, const uint16_t *cur, const uint16_t *ref,
+                                       int W, int H, int had, int bit_depth, hipStream_t st);
+hipError_t jmh_launch_sad_table_u16(const uint16_t *org, const uint16_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
+                                    const int32_t *centres, uint16_t *out, hipStream_t st);
+hipError_t jmh_launch_tq4x4_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+                                uint16_t *recon, int32_t *cc, int32_t *nz, hipStream_t st);
+hipError_t jmh_launch_tq8x8_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+                                uint16_t *recon, int32_t *cc, int32_t *nz, hipStream_t st);
 hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
                                 const int32_t *centres, uint16_t *out, hipStream_t st);
 hipError_t jmh_launch_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
@@ -121,6 +129,8 @@ struct jmh_ctx {
     uint8_t *d_ref, *d_qpel, *d_slots;   // explicit reference (set_reference), a1 seam, slots
     uint8_t *d_scur, *d_sref;            // luma pictures of the per-block searches (jmh_search_pictures)
     uint32_t *d_ordtab;                  // FFS order keys of the analysis threads' strips (ordtab_fill)
+    uint16_t *d_scur16, *d_sref16;       // 16-bit luma pictures of the High 10 seams (jmh_search_pictures_u16)
+    int hbd_bits;                        //   and their bit depth
     int nslots;
     int depth, nring;
     std::vector<PicBuf> ring;
@@ -238,7 +248,8 @@ void jmh_destroy(jmh_ctx *c) {
     if (c->st) (void)hipStreamSynchronize(c->st);
     if (c->cst) (void)hipStreamSynchronize(c->cst);
     for (PicBuf &b : c->ring) free_entry(b);
-    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab};
+    void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab, c->d_scur16,
+                        c->d_sref16};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     ring_free(c->ring_interp);
@@ -854,9 +865,7 @@ int jmh_search_pictures(jmh_ctx *c, const uint8_t *cur_y, const uint8_t *ref_y, 
     return JMH_OK;
 }
 
-int jmh_block_motion_search(jmh_ctx *c, int n, const jmh_block_search *req, jmh_block_result *res) {
-    if (!c || n <= 0 || !req || !res) return JMH_E_INVALID_ARG;
-    if (!c->d_scur) return JMH_E_STATE;
+static int check_block_requests(const jmh_ctx *c, int n, const jmh_block_search *req) {
     for (int i = 0; i < n; i++) {   // the kernel's block and window assumptions, checked on the host
         const jmh_block_search &q = req[i];
         if (q.blocktype < 1 || q.blocktype > 7 || q.mb_x < 0 || q.mb_x >= c->mbw || q.mb_y < 0 || q.mb_y >= c->mbh) return JMH_E_INVALID_ARG;
@@ -867,6 +876,13 @@ int jmh_block_motion_search(jmh_ctx *c, int n, const jmh_block_search *req, jmh_
         if (q.search_mode != 0 && q.search_mode != -1) return JMH_E_UNSUPPORTED_CFG;
         if (abs(q.centre[0]) > 2048 || abs(q.centre[1]) > 2048 || abs(q.pred_mv[0]) > 8192 || abs(q.pred_mv[1]) > 8192) return JMH_E_INVALID_ARG;
     }
+    return JMH_OK;
+}
+int jmh_block_motion_search(jmh_ctx *c, int n, const jmh_block_search *req, jmh_block_result *res) {
+    if (!c || n <= 0 || !req || !res) return JMH_E_INVALID_ARG;
+    if (!c->d_scur) return JMH_E_STATE;
+    int r = check_block_requests(c, n, req);
+    if (r) return r;
     HCHK(hipSetDevice(c->dev));
     DevTemps tmp;
     jmh_block_search *d_req;
@@ -878,6 +894,103 @@ int jmh_block_motion_search(jmh_ctx *c, int n, const jmh_block_search *req, jmh_
     HCHK(hipMemcpyAsync(res, d_res, (size_t)n * sizeof(jmh_block_result), hipMemcpyDeviceToHost, c->st));
     HCHK(hipStreamSynchronize(c->st));
     return JMH_OK;
+}
+
+// ---- High 10 seams (16-bit samples) ----------------------------------------------------------
+int jmh_search_pictures_u16(jmh_ctx *c, const uint16_t *cur_y, const uint16_t *ref_y, int sy, int bit_depth) {
+    if (!c || !cur_y || !ref_y || sy < c->W || bit_depth < 8 || bit_depth > 10) return JMH_E_INVALID_ARG;
+    const int maxv = (1 << bit_depth) - 1;
+    for (int y = 0; y < c->H; y++)   // out-of-range samples would break the 19-bit cost keys
+        for (int x = 0; x < c->W; x++)
+            if (cur_y[(size_t)y * sy + x] > maxv || ref_y[(size_t)y * sy + x] > maxv) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    const size_t ls = (size_t)c->W * c->H * 2;
+    if (!c->d_scur16) {
+        if (hipMalloc((void **)&c->d_scur16, ls) != hipSuccess) return JMH_E_OOM;
+        if (hipMalloc((void **)&c->d_sref16, ls) != hipSuccess) { (void)hipFree(c->d_scur16); c->d_scur16 = nullptr; return JMH_E_OOM; }
+    }
+    HCHK(hipStreamSynchronize(c->st));   // an earlier search may still read the buffers
+    HCHK(hipMemcpy2DAsync(c->d_scur16, (size_t)c->W * 2, cur_y, (size_t)sy * 2, (size_t)c->W * 2, c->H, hipMemcpyHostToDevice, c->st));
+    HCHK(hipMemcpy2DAsync(c->d_sref16, (size_t)c->W * 2, ref_y, (size_t)sy * 2, (size_t)c->W * 2, c->H, hipMemcpyHostToDevice, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    c->hbd_bits = bit_depth;
+    return JMH_OK;
+}
+int jmh_block_motion_search_u16(jmh_ctx *c, int n, const jmh_block_search *req, jmh_block_result *res) {
+    if (!c || n <= 0 || !req || !res) return JMH_E_INVALID_ARG;
+    if (!c->d_scur16) return JMH_E_STATE;
+    int r = check_block_requests(c, n, req);
+    if (r) return r;
+    HCHK(hipSetDevice(c->dev));
+    DevTemps tmp;
+    jmh_block_search *d_req;
+    jmh_block_result *d_res;
+    HCHK(tmp.alloc(&d_req, (size_t)n * sizeof(jmh_block_search)));
+    HCHK(tmp.alloc(&d_res, (size_t)n * sizeof(jmh_block_result)));
+    HCHK(hipMemcpyAsync(d_req, req, (size_t)n * sizeof(jmh_block_search), hipMemcpyHostToDevice, c->st));
+    HCHK(jmh_launch_block_search_u16(n, d_req, d_res, c->d_scur16, c->d_sref16, c->W, c->H, c->cfg.use_hadamard, c->hbd_bits, c->st));
+    HCHK(hipMemcpyAsync(res, d_res, (size_t)n * sizeof(jmh_block_result), hipMemcpyDeviceToHost, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    return JMH_OK;
+}
+int jmh_ffs_sad_table_u16(jmh_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t *centres, uint16_t *out) {
+    if (!c || n_mb <= 0 || !mb_xy || !centres || !out) return JMH_E_INVALID_ARG;
+    for (int i = 0; i < n_mb; i++)
+        if (mb_xy[2 * i] < 0 || mb_xy[2 * i] >= c->mbw || mb_xy[2 * i + 1] < 0 || mb_xy[2 * i + 1] >= c->mbh ||
+            abs(centres[2 * i]) > c->sr || abs(centres[2 * i + 1]) > c->sr) return JMH_E_INVALID_ARG;
+    if (!c->d_scur16) return JMH_E_STATE;
+    HCHK(hipSetDevice(c->dev));
+    int32_t *d_xy = nullptr, *d_c = nullptr;
+    uint16_t *d_out = nullptr;
+    const size_t on = (size_t)n_mb * 16 * c->npos;
+    DevTemps tmp;
+    HCHK(tmp.alloc(&d_xy, n_mb * 8));
+    HCHK(tmp.alloc(&d_c, n_mb * 8));
+    HCHK(tmp.alloc(&d_out, on * 2));
+    HCHK(hipMemcpyAsync(d_xy, mb_xy, n_mb * 8, hipMemcpyHostToDevice, c->st));
+    HCHK(hipMemcpyAsync(d_c, centres, n_mb * 8, hipMemcpyHostToDevice, c->st));
+    HCHK(jmh_launch_sad_table_u16(c->d_scur16, c->d_sref16, c->W, c->H, c->sr, n_mb, d_xy, d_c, d_out, c->st));
+    HCHK(hipMemcpyAsync(out, d_out, on * 2, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    return JMH_OK;
+}
+}  // extern "C"
+// dct_luma / dct_luma8x8 at bit_depth (EL = 16 or 64 samples per block)
+template <int EL>
+static int tq_batch_u16(jmh_ctx *c, int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+                        uint16_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
+    if (!c || n <= 0 || !resid || !pred || !levels || !recon || !coeff_cost || !nonzero || qp < 0 || qp > 51 || bit_depth < 8 ||
+        bit_depth > 10) return JMH_E_INVALID_ARG;
+    const int maxv = (1 << bit_depth) - 1;
+    for (size_t k = 0; k < (size_t)n * EL; k++)   // the int32 headroom of the quantiser assumes these ranges
+        if (pred[k] > maxv || resid[k] > maxv || resid[k] < -maxv) return JMH_E_INVALID_ARG;
+    HCHK(hipSetDevice(c->dev));
+    int16_t *dr, *dl;
+    uint16_t *dp, *drec;
+    int32_t *dcc, *dnz;
+    DevTemps tmp;
+    HCHK(tmp.alloc(&dr, (size_t)n * EL * 2)); HCHK(tmp.alloc(&dl, (size_t)n * EL * 2));
+    HCHK(tmp.alloc(&dp, (size_t)n * EL * 2)); HCHK(tmp.alloc(&drec, (size_t)n * EL * 2));
+    HCHK(tmp.alloc(&dcc, (size_t)n * 4)); HCHK(tmp.alloc(&dnz, (size_t)n * 4));
+    HCHK(hipMemcpyAsync(dr, resid, (size_t)n * EL * 2, hipMemcpyHostToDevice, c->st));
+    HCHK(hipMemcpyAsync(dp, pred, (size_t)n * EL * 2, hipMemcpyHostToDevice, c->st));
+    if (EL == 16) HCHK(jmh_launch_tq4x4_u16(n, dr, dp, qp, intra, bit_depth, dl, drec, dcc, dnz, c->st));
+    else HCHK(jmh_launch_tq8x8_u16(n, dr, dp, qp, intra, bit_depth, dl, drec, dcc, dnz, c->st));
+    HCHK(hipMemcpyAsync(levels, dl, (size_t)n * EL * 2, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(recon, drec, (size_t)n * EL * 2, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(coeff_cost, dcc, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipMemcpyAsync(nonzero, dnz, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
+    HCHK(hipStreamSynchronize(c->st));
+    return JMH_OK;
+}
+extern "C" {
+int jmh_tq4x4_batch_u16(jmh_ctx *c, int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+                        uint16_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
+    return tq_batch_u16<16>(c, n, resid, pred, qp, intra, bit_depth, levels, recon, coeff_cost, nonzero);
+}
+int jmh_tq8x8_batch_u16(jmh_ctx *c, int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+                        uint16_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
+    return tq_batch_u16<64>(c, n, resid, pred, qp, intra, bit_depth, levels, recon, coeff_cost, nonzero);
 }
 
 /* test seam: quarter-pel planes of the current reference, [16][H+8][W+8] (UnifiedOneForthPix) */

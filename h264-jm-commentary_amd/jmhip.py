@@ -17,7 +17,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 6
+JMH_ABI_VERSION = 7
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -107,6 +107,11 @@ _SIGS = {
     "jmh_read_qpel": (_I, [_P, _P]),
     "jmh_search_pictures": (_I, [_P, _P, _P, _I]),
     "jmh_block_motion_search": (_I, [_P, _I, _P, _P]),
+    "jmh_search_pictures_u16": (_I, [_P, _P, _P, _I, _I]),
+    "jmh_block_motion_search_u16": (_I, [_P, _I, _P, _P]),
+    "jmh_ffs_sad_table_u16": (_I, [_P, _I, _P, _P, _P]),
+    "jmh_tq4x4_batch_u16": (_I, [_P, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
+    "jmh_tq8x8_batch_u16": (_I, [_P, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -330,6 +335,41 @@ class Encoder:
         _check(self.lib.jmh_block_motion_search(self.ctx, len(reqs), ctypes.cast(reqs, _P), ctypes.cast(out, _P)),
                "jmh_block_motion_search")
         return out
+
+    # ---- High 10 seams (16-bit samples, bit_depth 8..10) ----
+    def search_pictures_u16(self, cur_y, ref_y, bit_depth):
+        cur_y, ref_y = np.ascontiguousarray(cur_y, np.uint16), np.ascontiguousarray(ref_y, np.uint16)
+        _check(self.lib.jmh_search_pictures_u16(self.ctx, _ptr(cur_y), _ptr(ref_y), self.w, bit_depth),
+               "jmh_search_pictures_u16")
+
+    def block_motion_search_u16(self, reqs):
+        out = (JmhBlockResult * len(reqs))()
+        _check(self.lib.jmh_block_motion_search_u16(self.ctx, len(reqs), ctypes.cast(reqs, _P), ctypes.cast(out, _P)),
+               "jmh_block_motion_search_u16")
+        return out
+
+    def sad_table_u16(self, mb_xy, centres):
+        mb_xy = np.ascontiguousarray(mb_xy, np.int32)
+        centres = np.ascontiguousarray(centres, np.int32)
+        n = mb_xy.shape[0]
+        side = 2 * self.cfg.search_range + 1
+        out = np.empty((n, 16, side * side), np.uint16)
+        _check(self.lib.jmh_ffs_sad_table_u16(self.ctx, n, _ptr(mb_xy), _ptr(centres), _ptr(out)), "jmh_ffs_sad_table_u16")
+        return out
+
+    def tq_u16(self, resid, pred, qp, intra, bit_depth):
+        """dct_luma (resid[n][16]) or dct_luma8x8 (resid[n][64]) on 16-bit samples."""
+        resid = np.ascontiguousarray(resid, np.int16)
+        pred = np.ascontiguousarray(pred, np.uint16)
+        n, el = resid.shape
+        lev = np.empty((n, el), np.int16)
+        rec = np.empty((n, el), np.uint16)
+        cc = np.empty(n, np.int32)
+        nz = np.empty(n, np.int32)
+        fn = self.lib.jmh_tq4x4_batch_u16 if el == 16 else self.lib.jmh_tq8x8_batch_u16
+        _check(fn(self.ctx, n, _ptr(resid), _ptr(pred), qp, intra, bit_depth, _ptr(lev), _ptr(rec), _ptr(cc), _ptr(nz)),
+               "jmh_tq%s_batch_u16" % ("4x4" if el == 16 else "8x8"))
+        return lev, rec, cc, nz
 
 
 # ---- synthetic source (product host plumbing, libjmhost.so) ------------------------------

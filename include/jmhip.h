@@ -24,6 +24,7 @@
  *               centre, range and lambda: the per-call seam    jmh_block_motion_search()
  *               of host/jm86.c BlockMotionSearch /
  *               PartitionMotionSearch and of an RDO-on loop)
+ *   the same seams at 9 / 10 bits (JM >= 10 imgpel = u16)   jmh_*_u16()
  *
  * Reference citations: the mounted reference (/root/reference) holds only README.md:1-4 (an
  * annotated-JM commentary with no source), so no file:line into JM source exists; the JM
@@ -43,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 6
+#define JMH_ABI_VERSION 7
 #define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
 
 /* ---- status codes ---------------------------------------------------------------------- */
@@ -264,6 +265,32 @@ typedef struct jmh_block_result {
 int  jmh_search_pictures(jmh_ctx *ctx, const uint8_t *cur_y, const uint8_t *ref_y, int stride_y);
 /* n independent requests in one launch (n = 1 for a JM-shaped call); res[n]                   */
 int  jmh_block_motion_search(jmh_ctx *ctx, int n, const jmh_block_search *req, jmh_block_result *res);
+
+/* ---- High 10 (config 5, BitDepthLuma 9 / 10) sample path: the same seams on 16-bit samples
+ * 0 .. (1 << bit_depth) - 1, bit_depth 8..10 (8 gives exactly the 8-bit seams' results).
+ * JM >= 10 FRExt [J] (imgpel = unsigned short): SAD / SATD on the wider samples, quarter-pel
+ * interpolation clipped to (1 << bit_depth) - 1 (H.264 8.4.2.2.1 Clip1Y), quantisation at
+ * qp + QpBdOffsetY (6 * (bit_depth - 8), qp_per / qp_rem / q_bits of block.c › dct_luma /
+ * dct_luma8x8), reconstruction clipped to (1 << bit_depth) - 1.  The whole-picture wavefront
+ * stays 8-bit (docs/JM_SEMANTICS.md items 41-44).                        */
+/* luma pictures (coded size, 16-bit samples) of the 10-bit per-block searches (copied)        */
+int  jmh_search_pictures_u16(jmh_ctx *ctx, const uint16_t *cur_y, const uint16_t *ref_y, int stride_y,
+                             int bit_depth);
+/* jmh_block_motion_search on the pictures of jmh_search_pictures_u16 (costs need 19 bits:
+   a 16x16 SAD reaches 256 * 1023)                                                            */
+int  jmh_block_motion_search_u16(jmh_ctx *ctx, int n, const jmh_block_search *req, jmh_block_result *res);
+/* SetupFastFullPelSearch's 4x4 BlockSAD table (as jmh_ffs_sad_table, a 4x4 SAD <= 16 * 1023
+   fits 16 bits) on the pictures of jmh_search_pictures_u16, by v_sad_u16 on sample pairs       */
+int  jmh_ffs_sad_table_u16(jmh_ctx *ctx, int n_mb, const int32_t *mb_xy, const int32_t *centres,
+                           uint16_t *out);
+/* dct_luma / dct_luma8x8 on 16-bit predictions and reconstructions; qp 0..51 is the slice QP
+   (QpBdOffsetY is added from bit_depth); resid within +-((1 << bit_depth) - 1)                */
+int  jmh_tq4x4_batch_u16(jmh_ctx *ctx, int n, const int16_t *resid, const uint16_t *pred, int qp,
+                         int intra, int bit_depth, int16_t *levels, uint16_t *recon,
+                         int32_t *coeff_cost, int32_t *nonzero);
+int  jmh_tq8x8_batch_u16(jmh_ctx *ctx, int n, const int16_t *resid, const uint16_t *pred, int qp,
+                         int intra, int bit_depth, int16_t *levels, uint16_t *recon,
+                         int32_t *coeff_cost, int32_t *nonzero);
 
 /* jmh_read_qpel: the 16 quarter-pel phase planes of the current reference (test seam for
  *   UnifiedOneForthPix), out[16][H+8][W+8], phase = 4*yfrac + xfrac, 4-sample padding.      */

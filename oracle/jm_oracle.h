@@ -79,6 +79,20 @@ void jmo_mvp_median(int avail_a, int ref_a, int mva_x, int mva_y,
                     int avail_c, int ref_c, int mvc_x, int mvc_y,
                     int ref, int bsx, int bsy, int blk_x, int blk_y, int32_t *pmv);
 
+/* ---- High 10 per-block seams (hbd.c): the oracles of jmh_*_u16 -------------------------- */
+typedef struct jmo_hbd jmo_hbd;
+int  jmo_hbd_create(int W, int H, int sr, jmo_hbd **out);
+void jmo_hbd_destroy(jmo_hbd *h);
+int  jmo_hbd_pictures(jmo_hbd *h, const uint16_t *cur, const uint16_t *ref, int stride, int bit_depth);
+int  jmo_hbd_qpel(const jmo_hbd *h, int X, int Y);
+int  jmo_hbd_block_motion_search(const jmo_hbd *h, int use_hadamard, int n, const jmh_block_search *req,
+                                 jmh_block_result *res);
+int  jmo_hbd_sad_table(const jmo_hbd *h, int n_mb, const int32_t *mb_xy, const int32_t *centres, uint16_t *out);
+int  jmo_hbd_tq4x4_batch(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth,
+                         int16_t *levels, uint16_t *recon, int32_t *coeff_cost, int32_t *nonzero);
+int  jmo_hbd_tq8x8_batch(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth,
+                         int16_t *levels, uint16_t *recon, int32_t *coeff_cost, int32_t *nonzero);
+
 /* ---- closed-loop decoder (Baseline CAVLC subset emitted by the host encoder) --------- */
 typedef struct jmo_dec jmo_dec;
 int  jmo_dec_create(jmo_dec **out);

@@ -45,6 +45,14 @@ def lib():
             "jmo_mvp_median": (None, [_I] * 17 + [_P]),
             "jmo_search_pictures": (_I, [_P, _P, _P, _I]),
             "jmo_block_motion_search": (_I, [_P, _I, _P, _P]),
+            "jmo_hbd_create": (_I, [_I, _I, _I, ctypes.POINTER(_P)]),
+            "jmo_hbd_destroy": (None, [_P]),
+            "jmo_hbd_pictures": (_I, [_P, _P, _P, _I, _I]),
+            "jmo_hbd_qpel": (_I, [_P, _I, _I]),
+            "jmo_hbd_block_motion_search": (_I, [_P, _I, _I, _P, _P]),
+            "jmo_hbd_sad_table": (_I, [_P, _I, _P, _P, _P]),
+            "jmo_hbd_tq4x4_batch": (_I, [_I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
+            "jmo_hbd_tq8x8_batch": (_I, [_I, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
             "jmo_dec_create": (_I, [ctypes.POINTER(_P)]),
             "jmo_dec_destroy": (None, [_P]),
             "jmo_decode_annexb": (_I, [_P, _P, ctypes.c_long, _P, ctypes.c_long, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
@@ -169,3 +177,61 @@ def decode_annexb(data, max_frames=64, max_w=1920, max_h=1088):
         raise RuntimeError("decode failed: " + err)
     fs = w.value * h.value * 3 // 2
     return [out[i * fs:(i + 1) * fs] for i in range(n)], w.value, h.value
+
+
+class OracleHbd:
+    """The High 10 per-block seams of the oracle (oracle/hbd.c): the checker of jmh_*_u16."""
+
+    def __init__(self, width, height, search_range, use_hadamard=1):
+        self.L = lib()
+        self.w, self.h, self.sr, self.had = width, height, search_range, use_hadamard
+        h = _P()
+        assert self.L.jmo_hbd_create(width, height, search_range, ctypes.byref(h)) == 0
+        self.h_ = h
+
+    def close(self):
+        if self.h_:
+            self.L.jmo_hbd_destroy(self.h_)
+            self.h_ = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def pictures(self, cur_y, ref_y, bit_depth):
+        cur_y, ref_y = np.ascontiguousarray(cur_y, np.uint16), np.ascontiguousarray(ref_y, np.uint16)
+        assert self.L.jmo_hbd_pictures(self.h_, _ptr(cur_y), _ptr(ref_y), self.w, bit_depth) == 0
+
+    def qpel(self, X, Y):
+        return self.L.jmo_hbd_qpel(self.h_, X, Y)
+
+    def block_motion_search(self, reqs):
+        out = (jmhip.JmhBlockResult * len(reqs))()
+        st = self.L.jmo_hbd_block_motion_search(self.h_, self.had, len(reqs), ctypes.cast(reqs, _P), ctypes.cast(out, _P))
+        assert st == 0, st
+        return out
+
+    def sad_table(self, mb_xy, centres):
+        mb_xy = np.ascontiguousarray(mb_xy, np.int32)
+        centres = np.ascontiguousarray(centres, np.int32)
+        side = 2 * self.sr + 1
+        out = np.empty((mb_xy.shape[0], 16, side * side), np.uint16)
+        assert self.L.jmo_hbd_sad_table(self.h_, mb_xy.shape[0], _ptr(mb_xy), _ptr(centres), _ptr(out)) == 0
+        return out
+
+
+def tq_u16(resid, pred, qp, intra, bit_depth):
+    """jmo_hbd_tq4x4_batch (resid[n][16]) / jmo_hbd_tq8x8_batch (resid[n][64])."""
+    L = lib()
+    resid = np.ascontiguousarray(resid, np.int16)
+    pred = np.ascontiguousarray(pred, np.uint16)
+    n, el = resid.shape
+    lev = np.empty((n, el), np.int16)
+    rec = np.empty((n, el), np.uint16)
+    cc = np.empty(n, np.int32)
+    nz = np.empty(n, np.int32)
+    fn = L.jmo_hbd_tq4x4_batch if el == 16 else L.jmo_hbd_tq8x8_batch
+    assert fn(n, _ptr(resid), _ptr(pred), qp, intra, bit_depth, _ptr(lev), _ptr(rec), _ptr(cc), _ptr(nz)) == 0
+    return lev, rec, cc, nz
