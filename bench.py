@@ -69,9 +69,6 @@ BYTES_PER_FRAME = W * H * BYTES_PER_PIXEL + NMB * SIDE_BYTES_PER_MB
 HBM_PEAK_GBS = 8000.0                                    # MI355X_MICROARCH.md (spec)
 # integer-search absolute differences per picture (the FFS SAD table)
 AD_PER_FRAME = NMB * (2 * SR + 1) ** 2 * 256
-# v_sad_u8 peak: measured by tools/sad_peak.hip on MI355X (profiles/r2_sad_peak.json), else the
-# nominal figure 256 CU x 128 lanes/clk (4 SIMD-32) x 2.4 GHz x 4 AD per lane-op
-VALU_SAD_NOMINAL_TADS = 256 * 128 * 4 * 2.4e9 / 1e12
 
 
 def load_module(name, path):
@@ -96,15 +93,15 @@ def use_config(k, size=None):
     return c
 
 
+# v_sad_u8 issue rate measured on MI355X by tools/sad_peak.hip (profiles/r2_sad_peak.json: 62.2
+# lane-ops per CU per clock x 256 CUs x 4 absolute differences, scaled to 2.4 GHz); profiles/ does
+# not travel to the GPU box, so the figure is kept here
+VALU_SAD_MEASURED_TADS = 152.90
+
+
 def sad_peak():
-    """(T AD/s, source) of v_sad_u8 on this chip: profiles/r2_sad_peak.json (tools/sad_peak.hip,
-    measured on MI355X, at 2.4 GHz) or the nominal figure."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "r2_sad_peak.json")) as f:
-            d = json.load(f)["ops"]["v_sad_u8"]
-        return d["ad_per_s_at_2p4ghz"] / 1e12, "measured (tools/sad_peak.hip, profiles/r2_sad_peak.json, at 2.4 GHz)"
-    except (OSError, ValueError, KeyError, TypeError):
-        return VALU_SAD_NOMINAL_TADS, "nominal (256 CU x 128 lanes x 2.4 GHz x 4 AD)"
+    """(T AD/s, source) of v_sad_u8 on this chip (measured, tools/sad_peak.hip)."""
+    return VALU_SAD_MEASURED_TADS, "measured: v_sad_u8 62.2 lane-ops/CU/clk (tools/sad_peak.hip, profiles/r2_sad_peak.json), at 2.4 GHz"
 
 
 # ------------------------------------------------------------------------------------------

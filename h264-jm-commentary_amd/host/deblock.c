@@ -50,7 +50,7 @@ static void filter_line(uint8_t *q0p, int step, int bS, int alpha, int beta, int
     if (chroma) {
         if (bS < 4) {
             int tc = tc0 + 1;
-            int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+            int d = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
             q0p[-step] = (uint8_t)clip3(0, 255, p0 + d);
             q0p[0] = (uint8_t)clip3(0, 255, q0 - d);
         } else {
@@ -63,7 +63,7 @@ static void filter_line(uint8_t *q0p, int step, int bS, int alpha, int beta, int
     int ap = iabs_(p2 - p0), aq = iabs_(q2 - q0);
     if (bS < 4) {
         int tc = tc0 + (ap < beta) + (aq < beta);
-        int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+        int d = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
         q0p[-step] = (uint8_t)clip3(0, 255, p0 + d);
         q0p[0] = (uint8_t)clip3(0, 255, q0 - d);
         if (ap < beta) q0p[-2 * step] = (uint8_t)(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));

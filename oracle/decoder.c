@@ -390,7 +390,7 @@ static int lscale(int qm, int pos) {       /* LevelScale4x4 = 16 * normAdjust (f
 static void scale4x4(int32_t *c, int qp, int skip_dc) {
     for (int k = skip_dc; k < 16; k++) {
         int ls = lscale(qp % 6, k);
-        if (qp >= 24) c[k] = (c[k] * ls) << (qp / 6 - 4);
+        if (qp >= 24) c[k] = c[k] * ls * (1 << (qp / 6 - 4));
         else c[k] = (c[k] * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
     }
 }
@@ -721,7 +721,7 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
             int f[4] = {a0 + a1 + a2 + a3, a0 + a1 - a2 - a3, a0 - a1 - a2 + a3, a0 - a1 + a2 - a3};
             for (int y = 0; y < 4; y++) {
                 int ls = lscale(qp_ % 6, 0);
-                int v = qp_ >= 36 ? (f[y] * ls) << (qp_ / 6 - 6) : (f[y] * ls + (1 << (5 - qp_ / 6))) >> (6 - qp_ / 6);
+                int v = qp_ >= 36 ? f[y] * ls * (1 << (qp_ / 6 - 6)) : (f[y] * ls + (1 << (5 - qp_ / 6))) >> (6 - qp_ / 6);
                 dcY[4 * y + x] = v;
             }
         }
@@ -781,7 +781,7 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
             int c[4];
             if (read_block(b, -1, 4, c) < 0) FAIL("chroma DC");
             int f[4] = {c[0] + c[1] + c[2] + c[3], c[0] - c[1] + c[2] - c[3], c[0] + c[1] - c[2] - c[3], c[0] - c[1] - c[2] + c[3]};
-            for (int k = 0; k < 4; k++) dcc[comp][k] = ((f[k] * lscale(qpc % 6, 0)) << (qpc / 6)) >> 5;
+            for (int k = 0; k < 4; k++) dcc[comp][k] = (f[k] * lscale(qpc % 6, 0) * (1 << (qpc / 6))) >> 5;
         }
     }
     for (int comp = 0; comp < 2; comp++) {

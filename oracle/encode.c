@@ -157,7 +157,7 @@ static inline int refpel(const jmo_ctx *c, int x, int y) {   /* UMV integer acce
 }
 static inline int mv_cost(const mbs *s, int shift, int cx, int cy, int px, int py) {
     /* MV_COST(f,s,cx,cy,px,py) = (f*(mvbits[(cx<<s)-px]+mvbits[(cy<<s)-py])) >> 16 [J] */
-    return (s->lf * (jmo_mvbits((cx << shift) - px) + jmo_mvbits((cy << shift) - py))) >> 16;
+    return (s->lf * (jmo_mvbits(cx * (1 << shift) - px) + jmo_mvbits(cy * (1 << shift) - py))) >> 16;
 }
 
 static int block_range(const mbs *s, int blocktype) {
@@ -374,16 +374,16 @@ static int subpel_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int 
     int w4 = jmo_blc_size[blocktype][0] >> 2, h4 = jmo_blc_size[blocktype][1] >> 2;
     int check_position0 = (blocktype == 1 && *mvx == 0 && *mvy == 0 && had && s->slice_p);
     int min_pos2 = had ? 0 : 1, max_pos2 = 9;
-    int mx = *mvx << 2, my = *mvy << 2, best_pos = 0;
+    int mx = *mvx * 4, my = *mvy * 4, best_pos = 0;
     for (int pos = min_pos2; pos < max_pos2; pos++) {          /* half-pel */
-        int cx = mx + (c->spiral_x[pos] << 1), cy = my + (c->spiral_y[pos] << 1);
+        int cx = mx + c->spiral_x[pos] * 2, cy = my + c->spiral_y[pos] * 2;
         int mcost = mv_cost(s, 0, cx, cy, pmvx, pmvy);
         if (check_position0 && pos == 0) mcost -= (s->lf * 16) >> 16;
         if (mcost >= min_mcost) continue;
         mcost += subpel_satd(s, bx4, by4, w4, h4, cx, cy);
         if (mcost < min_mcost) { min_mcost = mcost; best_pos = pos; }
     }
-    if (best_pos) { mx += c->spiral_x[best_pos] << 1; my += c->spiral_y[best_pos] << 1; }
+    if (best_pos) { mx += c->spiral_x[best_pos] * 2; my += c->spiral_y[best_pos] * 2; }
     best_pos = 0;
     for (int pos = 1; pos < 9; pos++) {                         /* quarter-pel */
         int cx = mx + c->spiral_x[pos], cy = my + c->spiral_y[pos];
@@ -641,7 +641,7 @@ static int dct_chroma(const int32_t resid[64], const uint8_t pred[64], int qpc, 
     }
     if (ac_any) cr_cbp = 2;
     for (int b = 0; b < 4; b++) {
-        m[b][0] = ((f[b] * 16 * v00) << qp_per) >> 5;
+        m[b][0] = (f[b] * 16 * v00 * (1 << qp_per)) >> 5;   /* (x << per) of the spec: x * 2^per (x may be < 0) */
         int ox = (b & 1) * 4, oy = (b >> 1) * 4;
         jmo_inv4x4_add(m[b], pred + oy * 8 + ox, 8, rec + oy * 8 + ox, 8);
     }
@@ -706,7 +706,7 @@ static int dct_luma_16x16(const int32_t resid[256], const uint8_t pred[256], int
             m[b][pos] = isign(level * jmo_dequant_coef[qp_rem][pos] << qp_per, m[b][pos]);
         }
         if (nz) *cbp_blk |= 1 << b;
-        m[b][0] = ((f[b] * v00 << qp_per) + 2) >> 2;
+        m[b][0] = (f[b] * v00 * (1 << qp_per) + 2) >> 2;
         int ox = (b & 3) * 4, oy = (b >> 2) * 4;
         jmo_inv4x4_add(m[b], pred + oy * 16 + ox, 16, rec + oy * 16 + ox, 16);
     }

@@ -90,7 +90,7 @@ int jmo_hbd_qpel(const jmo_hbd *h, int X, int Y) {
 }
 
 static int mvc(int lf, int shift, int cx, int cy, int px, int py) {   /* MV_COST [J] */
-    return (lf * (jmo_mvbits((cx << shift) - px) + jmo_mvbits((cy << shift) - py))) >> 16;
+    return (lf * (jmo_mvbits(cx * (1 << shift) - px) + jmo_mvbits(cy * (1 << shift) - py))) >> 16;
 }
 
 /* SAD of the w x h block at picture position (px0, py0) displaced by (mx, my) (UMV clamping) */

@@ -10,20 +10,23 @@ int main(int argc, char **argv) {
     fseek(f, 0, SEEK_END);
     long n = ftell(f);
     fseek(f, 0, SEEK_SET);
-    unsigned char *buf = malloc(n);
-    if (fread(buf, 1, n, f) != (size_t)n) return 1;
+    unsigned char *buf = malloc(n > 0 ? n : 1);
+    if (!buf || fread(buf, 1, n, f) != (size_t)n) { free(buf); fclose(f); return 1; }
     fclose(f);
     long cap = 64L * 1024 * 1024 * 16;
     unsigned char *out = malloc(cap);
-    jmo_dec *d;
-    jmo_dec_create(&d);
+    jmo_dec *d = NULL;
+    if (!out || jmo_dec_create(&d)) { free(buf); free(out); return 1; }
     int w = 0, h = 0;
     int frames = jmo_decode_annexb(d, buf, n, out, cap, &w, &h);
-    if (frames < 0) { fprintf(stderr, "decode error: %s\n", jmo_dec_error(d)); return 2; }
+    free(buf);
+    if (frames < 0) { fprintf(stderr, "decode error: %s\n", jmo_dec_error(d)); jmo_dec_destroy(d); free(out); return 2; }
     FILE *o = fopen(argv[2], "wb");
+    if (!o) { perror(argv[2]); jmo_dec_destroy(d); free(out); return 1; }
     fwrite(out, 1, (size_t)frames * w * h * 3 / 2, o);
     fclose(o);
     printf("decoded %d frames %dx%d\n", frames, w, h);
     jmo_dec_destroy(d);
+    free(out);
     return 0;
 }
