@@ -970,7 +970,7 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     }
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const int q_bits = 15 + d.qp / 6;
-    const int qpk = d.slice_type == JMH_P_SLICE ? (1 << q_bits) / 6 : (1 << q_bits) / 3;
+    const int qpk = q_round(d.qsel, q_bits);
     int tab[3];
 #pragma unroll
     for (int it = 0; it < 3; it++) {
@@ -1010,7 +1010,7 @@ __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScra
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
     if (k < 10) {
         const int q_bits = 15 + d.qp / 6;
-        const int qpk = d.slice_type == JMH_P_SLICE ? (1 << q_bits) / 6 : (1 << q_bits) / 3;
+        const int qpk = q_round(d.qsel, q_bits);
         int tab[3];
 #pragma unroll
         for (int it = 0; it < 3; it++) {

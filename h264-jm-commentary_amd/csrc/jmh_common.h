@@ -183,6 +183,14 @@ __device__ __forceinline__ int lane_inv4x4(int dq, int l, int pred, int maxv = 2
     int o = y == 0 ? e0 + e3 : y == 1 ? e1 + e2 : y == 2 ? e1 - e2 : e0 - e3;
     return iclip(0, maxv, (o + (pred << 6) + 32) >> 6);
 }
+// quantisation rounding offset at q_bits (docs/JM_SEMANTICS.md items 1 and 45; oracle jmo_qround):
+//   sel 0 / 1 = JM 8.6 (1 << q_bits) / 6 (P slice) / 3 (I slice, and Intra16x16 always);
+//   sel 2 + o = JM >= 10 flat OffsetMatrix entry o at OffsetBits 11: o << (q_bits - 11)
+__device__ __forceinline__ int q_round(int sel, int q_bits) {
+    return sel >= 2 ? (sel - 2) << (q_bits - 11) : sel ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+}
+// the Intra16x16 selector: JM 8.6 always rounds dct_luma_16x16 with / 3
+__device__ __forceinline__ int q_sel16(int sel) { return sel >= 2 ? sel : 1; }
 // quantisation (dct_luma / dct_chroma AC [J]) of coefficient c at raster l.
 //   lev_scan: signed level at SCAN position l; dq: dequantised coefficient at raster l;
 //   cost: COEFF_COST sum over the block (all 16 lanes); returns the scan-order non-zero mask.

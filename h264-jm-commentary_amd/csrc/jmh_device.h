@@ -64,6 +64,7 @@ struct DevParams {
     unsigned long long *prof;   // debug phase timestamps (null: off)
     int prof_mb;
     int slice_type, qp, lambda_mode, lambda_motion, cqp_off;
+    int qsel;                   // quantisation rounding selector of this slice (q_round, jmh_common.h)
     int diag, y_min;            // wavefront diagonal of this picture in the launch: mbx + 2*mby == diag
 };
 
@@ -80,6 +81,7 @@ struct PicParams {
     MbScratch *scr;
     int32_t lambda_mode, lambda_motion;
     int16_t diag, y_min;
+    int16_t qsel;                        // q_round selector (JM 8.6 !P / JM >= 10 2 + quant_offset)
     int8_t slice_type, qp, cqp_off, lf_disable, lf_offA, lf_offB;   // packed: PMAX entries fit 4 KB
 };
 struct TickArgs {
@@ -135,6 +137,6 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.tmv = q.tmv; d.tref = q.tref; d.ordtab = t.ordtab;
     d.prof = e == 0 ? t.prof : nullptr; d.prof_mb = t.prof_mb;
     d.slice_type = q.slice_type; d.qp = q.qp; d.lambda_mode = q.lambda_mode; d.lambda_motion = q.lambda_motion;
-    d.cqp_off = q.cqp_off; d.diag = q.diag; d.y_min = q.y_min;
+    d.cqp_off = q.cqp_off; d.qsel = q.qsel; d.diag = q.diag; d.y_min = q.y_min;
     return d;
 }

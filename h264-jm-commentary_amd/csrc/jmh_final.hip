@@ -108,7 +108,6 @@ __global__ __launch_bounds__(NT, 7) void k_mb_final(const TickArgs t) {
     const int W = d.W, Wc = d.Wc, W4 = d.W >> 2;
     const int slice_p = d.slice_type == JMH_P_SLICE;
     const int qp = d.qp;
-    const int intra_round = !slice_p;
     const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0;
     const bool prof = prof_mb_here(d, mbx, mby);
     PSTAMP(16);
@@ -184,7 +183,7 @@ __global__ __launch_bounds__(NT, 7) void k_mb_final(const TickArgs t) {
     } else if (best_mode == JMH_I16MB) {
         // dct_luma_16x16 [J]
         const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per;
-        const int qp_const = (1 << q_bits) / 3, qp_const2 = qp_const << 1;
+        const int qp_const = q_round(q_sel16(d.qsel), q_bits), qp_const2 = qp_const << 1;
         const uint8_t *T = s.rtop + 1, *L = s.rleft;
         const I16Par par = i16_params(T, L, avT, avL);
         const int p = i16_pred(par, T, L, i16mode, px4, py4);
@@ -250,7 +249,7 @@ __global__ __launch_bounds__(NT, 7) void k_mb_final(const TickArgs t) {
             const int q8 = 16 + qp / 6;
             const int c = wave_fwd8x8(s.org[qy * 16 + qx] - pv, l8);
             int lev, dq, cc;
-            const unsigned long long nz = wave_quant8(c, l8, qp, intra_round ? (1 << q8) / 3 : (1 << q8) / 6, lev, dq, cc);
+            const unsigned long long nz = wave_quant8(c, l8, qp, q_round(d.qsel, q8), lev, dq, cc);
             const int rv = wave_inv8x8(dq, l8, pv);
             if (l8 == 0) { s.bcost[w8] = cc; s.bnz[w8] = nz != 0; }
             __syncthreads();
@@ -272,7 +271,7 @@ __global__ __launch_bounds__(NT, 7) void k_mb_final(const TickArgs t) {
         const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
         int lev, dq, cc;
         const int q_bits = 15 + qp / 6;
-        unsigned nz = lane_quant(c, l, qp, intra_round ? (1 << q_bits) / 3 : (1 << q_bits) / 6, false, lev, dq, cc);
+        unsigned nz = lane_quant(c, l, qp, q_round(d.qsel, q_bits), false, lev, dq, cc);
         const int rv = lane_inv4x4(dq, l, p);
         if (l == 0) { s.bcost[blk] = cc; s.bnz[blk] = nz != 0; }
         __syncthreads();
@@ -306,7 +305,7 @@ __global__ __launch_bounds__(NT, 7) void k_mb_final(const TickArgs t) {
     const int c_mode = is_intra ? sc->c_mode : 0;
     const int qpc = c_qpc[iclip(0, 51, qp + d.cqp_off)];
     const int cq_bits = 15 + qpc / 6;
-    const int cqp_const = intra_round ? (1 << cq_bits) / 3 : (1 << cq_bits) / 6;
+    const int cqp_const = q_round(d.qsel, cq_bits);
     const int cuv = blk >> 2, cb = blk & 3;
     const int cxo = (cb & 1) * 4 + lx, cyo = (cb >> 1) * 4 + ly;
     int cdq = 0, cpredv = 0;

@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void k_sad_table_u16(const uint16_t *__restric
     }
 }
 
-__global__ __launch_bounds__(256) void k_tq4x4_u16(int n, const int16_t *resid, const uint16_t *pred, int qpb, int intra, int maxv,
+__global__ __launch_bounds__(256) void k_tq4x4_u16(int n, const int16_t *resid, const uint16_t *pred, int qpb, int qsel, int maxv,
                                                    int16_t *levels, uint16_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
     const int blk = blockIdx.x * 16 + (threadIdx.x >> 4), l = threadIdx.x & 15;
     const bool act = blk < n;
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_tq4x4_u16(int n, const int16_t *resid, 
     const int c = lane_fwd4x4(resid[16 * bi + l], l);
     int lev, dq, cc;
     const int q_bits = 15 + qpb / 6;
-    const unsigned nz = lane_quant(c, l, qpb, intra ? (1 << q_bits) / 3 : (1 << q_bits) / 6, false, lev, dq, cc);
+    const unsigned nz = lane_quant(c, l, qpb, q_round(qsel, q_bits), false, lev, dq, cc);
     const int rv = lane_inv4x4(dq, l, pred[16 * bi + l], maxv);
     if (act) {
         levels[16 * blk + l] = (int16_t)lev;
@@ -57,14 +57,14 @@ __global__ __launch_bounds__(256) void k_tq4x4_u16(int n, const int16_t *resid, 
     }
 }
 
-__global__ __launch_bounds__(256) void k_tq8x8_u16(int n, const int16_t *resid, const uint16_t *pred, int qpb, int intra, int maxv,
+__global__ __launch_bounds__(256) void k_tq8x8_u16(int n, const int16_t *resid, const uint16_t *pred, int qpb, int qsel, int maxv,
                                                    int16_t *levels, uint16_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
     const int blk = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
     if (blk >= n) return;                        // whole waves only: no workgroup barrier below
     const int q_bits = 16 + qpb / 6;
     const int c = wave_fwd8x8(resid[64 * blk + l], l);
     int lev, dq, cc;
-    const unsigned long long nz = wave_quant8(c, l, qpb, intra ? (1 << q_bits) / 3 : (1 << q_bits) / 6, lev, dq, cc);
+    const unsigned long long nz = wave_quant8(c, l, qpb, q_round(qsel, q_bits), lev, dq, cc);
     recon[64 * blk + l] = (uint16_t)wave_inv8x8(dq, l, pred[64 * blk + l], maxv);
     levels[64 * blk + l] = (int16_t)lev;
     if (l == 0) { coeff_cost[blk] = cc; nonzero[blk] = nz != 0; }
@@ -76,15 +76,15 @@ hipError_t jmh_launch_sad_table_u16(const uint16_t *org, const uint16_t *ref, in
     hipLaunchKernelGGL(k_sad_table_u16, dim3((npos + 255) / 256, n_mb), dim3(256), 0, st, org, ref, W, H, sr, mb_xy, centres, out);
     return hipGetLastError();
 }
-hipError_t jmh_launch_tq4x4_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+hipError_t jmh_launch_tq4x4_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int qsel, int bit_depth, int16_t *levels,
                                 uint16_t *recon, int32_t *cc, int32_t *nz, hipStream_t st) {
-    hipLaunchKernelGGL(k_tq4x4_u16, dim3((n + 15) / 16), dim3(256), 0, st, n, resid, pred, qp + 6 * (bit_depth - 8), intra,
+    hipLaunchKernelGGL(k_tq4x4_u16, dim3((n + 15) / 16), dim3(256), 0, st, n, resid, pred, qp + 6 * (bit_depth - 8), qsel,
                        (1 << bit_depth) - 1, levels, recon, cc, nz);
     return hipGetLastError();
 }
-hipError_t jmh_launch_tq8x8_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+hipError_t jmh_launch_tq8x8_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int qsel, int bit_depth, int16_t *levels,
                                 uint16_t *recon, int32_t *cc, int32_t *nz, hipStream_t st) {
-    hipLaunchKernelGGL(k_tq8x8_u16, dim3((n + 3) / 4), dim3(256), 0, st, n, resid, pred, qp + 6 * (bit_depth - 8), intra,
+    hipLaunchKernelGGL(k_tq8x8_u16, dim3((n + 3) / 4), dim3(256), 0, st, n, resid, pred, qp + 6 * (bit_depth - 8), qsel,
                        (1 << bit_depth) - 1, levels, recon, cc, nz);
     return hipGetLastError();
 }

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(NT, 6) void k_mb_intra8(const TickArgs t) {
     const bool avL = mbx > 0, avT = mby > 0, avTL = avL && avT, avTR = avT && mbx + 1 < d.mbw;
     const int lambda = d.lambda_mode, qp = d.qp, had = d.use_hadamard;
     const int q_bits = 16 + qp / 6;
-    const int qp_const = d.slice_type != JMH_P_SLICE ? (1 << q_bits) / 3 : (1 << q_bits) / 6;   // item 1
+    const int qp_const = q_round(d.qsel, q_bits);   // items 1, 45
     const int wv = tid >> 6, l = tid & 63, x = l & 7, y = l >> 3;
     MbScratch *sc = d.scr + mby * d.mbw + mbx;
 

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_sad_table(const uint8_t *__restrict__ o
 }
 
 // the macroblock kernel's 16-lane dct_luma on independent blocks (16 lanes per block)
-__global__ __launch_bounds__(256) void k_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels,
+__global__ __launch_bounds__(256) void k_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int qsel, int16_t *levels,
                                                uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
     const int blk = blockIdx.x * 16 + (threadIdx.x >> 4), l = threadIdx.x & 15;
     const bool act = blk < n;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_tq4x4(int n, const int16_t *resid, cons
     const int c = lane_fwd4x4(resid[16 * bi + l], l);
     int lev, dq, cc;
     const int q_bits = 15 + qp / 6;
-    unsigned nz = lane_quant(c, l, qp, intra ? (1 << q_bits) / 3 : (1 << q_bits) / 6, false, lev, dq, cc);
+    unsigned nz = lane_quant(c, l, qp, q_round(qsel, q_bits), false, lev, dq, cc);
     const int rv = lane_inv4x4(dq, l, pred[16 * bi + l]);
     if (act) {
         levels[16 * blk + l] = (int16_t)lev;
@@ -79,14 +79,14 @@ __global__ __launch_bounds__(256) void k_tq4x4(int n, const int16_t *resid, cons
 }
 
 // the macroblock kernels' one-wave dct_luma8x8 on independent blocks (4 blocks per workgroup)
-__global__ __launch_bounds__(256) void k_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels,
+__global__ __launch_bounds__(256) void k_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int qsel, int16_t *levels,
                                                uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
     const int blk = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
     if (blk >= n) return;                        // whole waves only: no workgroup barrier below
     const int q_bits = 16 + qp / 6;
     const int c = wave_fwd8x8(resid[64 * blk + l], l);
     int lev, dq, cc;
-    const unsigned long long nz = wave_quant8(c, l, qp, intra ? (1 << q_bits) / 3 : (1 << q_bits) / 6, lev, dq, cc);
+    const unsigned long long nz = wave_quant8(c, l, qp, q_round(qsel, q_bits), lev, dq, cc);
     recon[64 * blk + l] = (uint8_t)wave_inv8x8(dq, l, pred[64 * blk + l]);
     levels[64 * blk + l] = (int16_t)lev;
     if (l == 0) { coeff_cost[blk] = cc; nonzero[blk] = nz != 0; }
@@ -104,13 +104,13 @@ hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, i
     hipLaunchKernelGGL(k_sad_table, dim3((npos + 255) / 256, n_mb), dim3(256), 0, st, org, ref, W, H, sr, mb_xy, centres, out);
     return hipGetLastError();
 }
-hipError_t jmh_launch_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
+hipError_t jmh_launch_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int qsel, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st) {
-    hipLaunchKernelGGL(k_tq8x8, dim3((n + 3) / 4), dim3(256), 0, st, n, resid, pred, qp, intra, levels, recon, cc, nz);
+    hipLaunchKernelGGL(k_tq8x8, dim3((n + 3) / 4), dim3(256), 0, st, n, resid, pred, qp, qsel, levels, recon, cc, nz);
     return hipGetLastError();
 }
-hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
+hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int qsel, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st) {
-    hipLaunchKernelGGL(k_tq4x4, dim3((n + 15) / 16), dim3(256), 0, st, n, resid, pred, qp, intra, levels, recon, cc, nz);
+    hipLaunchKernelGGL(k_tq4x4, dim3((n + 15) / 16), dim3(256), 0, st, n, resid, pred, qp, qsel, levels, recon, cc, nz);
     return hipGetLastError();
 }

@@ -30,18 +30,24 @@ hipError_t jmh_launch_block_search_u16(int n, const jmh_block_search *reqs, jmh_
                                        int W, int H, int had, int bit_depth, hipStream_t st);
 hipError_t jmh_launch_sad_table_u16(const uint16_t *org, const uint16_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
                                     const int32_t *centres, uint16_t *out, hipStream_t st);
-hipError_t jmh_launch_tq4x4_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+hipError_t jmh_launch_tq4x4_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int qsel, int bit_depth, int16_t *levels,
                                 uint16_t *recon, int32_t *cc, int32_t *nz, hipStream_t st);
-hipError_t jmh_launch_tq8x8_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bit_depth, int16_t *levels,
+hipError_t jmh_launch_tq8x8_u16(int n, const int16_t *resid, const uint16_t *pred, int qp, int qsel, int bit_depth, int16_t *levels,
                                 uint16_t *recon, int32_t *cc, int32_t *nz, hipStream_t st);
 hipError_t jmh_launch_sad_table(const uint8_t *org, const uint8_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
                                 const int32_t *centres, uint16_t *out, hipStream_t st);
-hipError_t jmh_launch_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
+hipError_t jmh_launch_tq8x8(int n, const int16_t *resid, const uint8_t *pred, int qp, int qsel, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st);
 hipError_t jmh_launch_block_search(int n, const jmh_block_search *reqs, jmh_block_result *out, const uint8_t *cur, const uint8_t *ref, int W,
                                    int H, int had, hipStream_t st);
-hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra, int16_t *levels, uint8_t *recon,
+hipError_t jmh_launch_tq4x4(int n, const int16_t *resid, const uint8_t *pred, int qp, int qsel, int16_t *levels, uint8_t *recon,
                             int32_t *cc, int32_t *nz, hipStream_t st);
+
+// quantisation rounding selector of a slice (q_round, jmh_common.h; docs/JM_SEMANTICS.md items 1
+// and 45): JM 8.6 = 1 in I slices, 0 in P slices; JMVersion >= 10 = 2 + the slice's OffsetMatrix entry
+static int q_selector(const jmh_config &cfg, bool i_slice) {
+    return cfg.jm_version >= 10 ? 2 + cfg.quant_offset[i_slice ? 0 : 1] : i_slice ? 1 : 0;
+}
 
 // JMH_FLAG_KERNEL_TIMING brackets every KT_STRIDE-th tick's two launches with events: the
 // averages are sampled uniformly while the event packets stay off most launches
@@ -272,6 +278,9 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
     if (cfg->pipeline_depth < 0 || cfg->pipeline_depth > PMAX) return JMH_E_INVALID_ARG;
     if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->jm_version < 0 || cfg->jm_version == 9 || cfg->jm_version > 99) return JMH_E_UNSUPPORTED_CFG;   // 0 / 8: JM 8.6, 10..: JM >= 10
+    if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
+                                  cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     int ndev = jmh_device_count();
     if (ndev <= 0) return JMH_E_NO_DEVICE;
     if (hip_device < 0 || hip_device >= ndev) return JMH_E_INVALID_ARG;
@@ -547,6 +556,7 @@ static int push_picture(jmh_ctx *c, const uint8_t *src, int entry, const jmh_fra
     q.tref = f.tmv_entry >= 0 ? c->ring[f.tmv_entry].refidx : nullptr;
     q.slice_type = fp->slice_type; q.qp = fp->qp; q.lambda_mode = fp->lambda_mode; q.lambda_motion = fp->lambda_motion;
     q.cqp_off = fp->chroma_qp_offset;
+    q.qsel = (int16_t)q_selector(c->cfg, fp->slice_type != JMH_P_SLICE);
     q.lf_disable = fp->lf_disable; q.lf_offA = 2 * fp->lf_alpha_div2; q.lf_offB = 2 * fp->lf_beta_div2;
     b.unpopped = readback;
     b.deblocked = fp->deblock != 0;
@@ -819,7 +829,7 @@ int jmh_tq4x4_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     HCHK(tmp.alloc(&dcc, (size_t)n * 4)); HCHK(tmp.alloc(&dnz, (size_t)n * 4));
     HCHK(hipMemcpyAsync(dr, resid, n * 32, hipMemcpyHostToDevice, c->st));
     HCHK(hipMemcpyAsync(dp, pred, n * 16, hipMemcpyHostToDevice, c->st));
-    HCHK(jmh_launch_tq4x4(n, dr, dp, qp, intra, dl, drec, dcc, dnz, c->st));
+    HCHK(jmh_launch_tq4x4(n, dr, dp, qp, q_selector(c->cfg, intra != 0), dl, drec, dcc, dnz, c->st));
     HCHK(hipMemcpyAsync(levels, dl, n * 32, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(recon, drec, n * 16, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(coeff_cost, dcc, n * 4, hipMemcpyDeviceToHost, c->st));
@@ -841,7 +851,7 @@ int jmh_tq8x8_batch(jmh_ctx *c, int n, const int16_t *resid, const uint8_t *pred
     HCHK(tmp.alloc(&dcc, (size_t)n * 4)); HCHK(tmp.alloc(&dnz, (size_t)n * 4));
     HCHK(hipMemcpyAsync(dr, resid, n * 128, hipMemcpyHostToDevice, c->st));
     HCHK(hipMemcpyAsync(dp, pred, n * 64, hipMemcpyHostToDevice, c->st));
-    HCHK(jmh_launch_tq8x8(n, dr, dp, qp, intra, dl, drec, dcc, dnz, c->st));
+    HCHK(jmh_launch_tq8x8(n, dr, dp, qp, q_selector(c->cfg, intra != 0), dl, drec, dcc, dnz, c->st));
     HCHK(hipMemcpyAsync(levels, dl, n * 128, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(recon, drec, n * 64, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(coeff_cost, dcc, n * 4, hipMemcpyDeviceToHost, c->st));
@@ -974,8 +984,8 @@ static int tq_batch_u16(jmh_ctx *c, int n, const int16_t *resid, const uint16_t 
     HCHK(tmp.alloc(&dcc, (size_t)n * 4)); HCHK(tmp.alloc(&dnz, (size_t)n * 4));
     HCHK(hipMemcpyAsync(dr, resid, (size_t)n * EL * 2, hipMemcpyHostToDevice, c->st));
     HCHK(hipMemcpyAsync(dp, pred, (size_t)n * EL * 2, hipMemcpyHostToDevice, c->st));
-    if (EL == 16) HCHK(jmh_launch_tq4x4_u16(n, dr, dp, qp, intra, bit_depth, dl, drec, dcc, dnz, c->st));
-    else HCHK(jmh_launch_tq8x8_u16(n, dr, dp, qp, intra, bit_depth, dl, drec, dcc, dnz, c->st));
+    if (EL == 16) HCHK(jmh_launch_tq4x4_u16(n, dr, dp, qp, q_selector(c->cfg, intra != 0), bit_depth, dl, drec, dcc, dnz, c->st));
+    else HCHK(jmh_launch_tq8x8_u16(n, dr, dp, qp, q_selector(c->cfg, intra != 0), bit_depth, dl, drec, dcc, dnz, c->st));
     HCHK(hipMemcpyAsync(levels, dl, (size_t)n * EL * 2, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(recon, drec, (size_t)n * EL * 2, hipMemcpyDeviceToHost, c->st));
     HCHK(hipMemcpyAsync(coeff_cost, dcc, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));

@@ -62,6 +62,11 @@ static const map_entry Map[] = {
     {"PipelineDepth", 0, OFF(pipeline_depth), 0, 20},
     {"JMCallSurface", 0, OFF(jm_call_surface), 0, 1},
     {"WriterThreads", 0, OFF(writer_threads), 0, 64},
+    {"JMVersion", 0, OFF(jm_version), 8, 99},
+    {"QOffsetIntra", 0, OFF(qoff_intra), -1, JMH_QOFFSET_MAX},
+    {"QOffsetInter", 0, OFF(qoff_inter), -1, JMH_QOFFSET_MAX},
+    {"AdaptiveRounding", 0, OFF(adaptive_rounding), 0, 1},
+    {"OffsetMatrixPresentFlag", 0, OFF(offset_matrix_present), 0, 1},
     {NULL, 0, 0, 0, 0}};
 #undef OFF
 
@@ -83,6 +88,8 @@ void jm_input_defaults(jm_input *inp) {
     inp->level_idc = 40;
     inp->frame_rate = 30;
     inp->writer_threads = 4;
+    inp->jm_version = 8;
+    inp->qoff_intra = inp->qoff_inter = -1;
 }
 
 int jm_set_param(jm_input *inp, const char *key, const char *val, char *err, int errlen) {
@@ -168,6 +175,14 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->transform_8x8_mode == 2) { snprintf(err, errlen, "Transform8x8Mode=2 not supported (0 or 1)"); return -1; }
     if (inp->transform_8x8_mode && inp->profile_idc < 100) { snprintf(err, errlen, "Transform8x8Mode=1 requires ProfileIDC=100 (High)"); return -1; }
     if ((inp->width & 1) || (inp->height & 1)) { snprintf(err, errlen, "Source size must be even"); return -1; }
+    if (inp->jm_version == 9) { snprintf(err, errlen, "JMVersion=9 not supported (8 or >= 10)"); return -1; }
+    if (inp->adaptive_rounding) { snprintf(err, errlen, "AdaptiveRounding=1 not supported (0)"); return -1; }
+    if (inp->offset_matrix_present) { snprintf(err, errlen, "OffsetMatrixPresentFlag=1 not supported (flat lists: QOffsetIntra / QOffsetInter)"); return -1; }
+    if (inp->jm_version < 10 && (inp->qoff_intra >= 0 || inp->qoff_inter >= 0)) { snprintf(err, errlen, "QOffsetIntra / QOffsetInter need JMVersion >= 10"); return -1; }
+    if (inp->jm_version >= 10) {               /* q_offsets.c defaults (OffsetMatrixPresentFlag 0) [J] */
+        if (inp->qoff_intra < 0) inp->qoff_intra = 682;
+        if (inp->qoff_inter < 0) inp->qoff_inter = 342;
+    }
     return 0;
 }
 
@@ -207,4 +222,6 @@ void jm_fill_config(const jm_input *inp, jmh_config *cfg) {
     cfg->num_frame_slots = 2;
     cfg->pipeline_depth = inp->pipeline_depth;
     cfg->transform_8x8_mode = inp->transform_8x8_mode;
+    cfg->jm_version = inp->jm_version;
+    if (inp->jm_version >= 10) { cfg->quant_offset[0] = inp->qoff_intra; cfg->quant_offset[1] = inp->qoff_inter; }
 }

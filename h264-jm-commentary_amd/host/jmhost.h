@@ -38,6 +38,12 @@ typedef struct jm_input {
     int  rdopt;                /* RDOptimization (must be 0)                                  */
     int  profile_idc;          /* ProfileIDC (66 Baseline, 100 High)                          */
     int  transform_8x8_mode;   /* Transform8x8Mode (0, 1; needs ProfileIDC 100)               */
+    int  jm_version;           /* JMVersion: 8 (JM 8.6 rules, default) or >= 10 (JM >= 10
+                                  quantisation offsets, docs/JM_SEMANTICS.md item 45)          */
+    int  qoff_intra, qoff_inter;/* QOffsetIntra / QOffsetInter: flat OffsetMatrix entries at
+                                  OffsetBits 11 (JMVersion >= 10; -1 = JM defaults 682 / 342) */
+    int  adaptive_rounding;    /* AdaptiveRounding (must be 0)                                */
+    int  offset_matrix_present;/* OffsetMatrixPresentFlag (must be 0: flat lists only)         */
     int  level_idc;            /* LevelIDC                                                    */
     int  symbol_mode;          /* SymbolMode (0 = CAVLC)                                       */
     int  lf_params_flag;       /* LoopFilterParametersFlag                                    */

@@ -17,7 +17,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 7
+JMH_ABI_VERSION = 8
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -37,7 +37,8 @@ class JmhConfig(ctypes.Structure):
                 ("inter_search", ctypes.c_int32 * 8), ("num_ref_frames", ctypes.c_int32),
                 ("constrained_intra_pred", ctypes.c_int32), ("num_frame_slots", ctypes.c_int32),
                 ("flags", ctypes.c_int32), ("pipeline_depth", ctypes.c_int32),
-                ("transform_8x8_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+                ("transform_8x8_mode", ctypes.c_int32), ("jm_version", ctypes.c_int32),
+                ("quant_offset", ctypes.c_int32 * 2), ("reserved", ctypes.c_int32 * 1)]
 
 
 class JmhFrameParams(ctypes.Structure):
@@ -153,7 +154,9 @@ def _ptr(a):
 
 def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
                 restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False,
-                pipeline_depth=0, transform_8x8_mode=0):
+                pipeline_depth=0, transform_8x8_mode=0, jm_version=8, quant_offset=(682, 342)):
+    """jm_version >= 10 selects the JM >= 10 quantisation rounding with the flat OffsetMatrix
+    entries quant_offset = (I slices, P slices) at OffsetBits 11 (docs/JM_SEMANTICS.md item 45)."""
     cfg = JmhConfig()
     cfg.width, cfg.height = width, height
     cfg.search_range, cfg.search_mode = search_range, search_mode
@@ -164,6 +167,9 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     cfg.flags = JMH_FLAG_KERNEL_TIMING if kernel_timing else 0
     cfg.pipeline_depth = pipeline_depth
     cfg.transform_8x8_mode = transform_8x8_mode
+    cfg.jm_version = jm_version
+    if jm_version >= 10:
+        cfg.quant_offset[0], cfg.quant_offset[1] = quant_offset
     return cfg
 
 

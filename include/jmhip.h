@@ -44,8 +44,9 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 7
+#define JMH_ABI_VERSION 8
 #define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
+#define JMH_QOFFSET_MAX 2047  /* jmh_config.quant_offset: OffsetBits 11 (1 << 11 = a whole step)    */
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define JMH_OK                 0
@@ -92,7 +93,15 @@ typedef struct jmh_config {
     int32_t pipeline_depth;         /* pictures in flight at once (0: enough to fill the device,  */
                                     /*   1: one picture at a time); see jmh_frame_push            */
     int32_t transform_8x8_mode;     /* Transform8x8Mode: 0 off, 1 adaptive 4x4 / 8x8 (High profile) */
-    int32_t reserved[4];
+    int32_t jm_version;             /* JMVersion: 0 or 8 = JM 8.6 quantisation rounding ((1 << q_bits)
+                                       / 3 in I slices, / 6 in P slices, Intra16x16 always / 3);
+                                       >= 10 = JM >= 10 q_offsets.c: every block of a slice rounds
+                                       with quant_offset[slice] << (q_bits - 11) (docs/JM_SEMANTICS.md
+                                       items 1, 45; AdaptiveRounding off)                           */
+    int32_t quant_offset[2];        /* JMVersion >= 10: flat OffsetMatrix entries at OffsetBits 11 for
+                                       [0] I slices, [1] P slices, 0..JMH_QOFFSET_MAX (JM defaults
+                                       682, 342: Offset_intra_default_intra / _inter) [J]          */
+    int32_t reserved[1];
 } jmh_config;
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */
@@ -225,14 +234,15 @@ int  jmh_ffs_sad_table(jmh_ctx *ctx, int n_mb, const int32_t *mb_xy, const int32
                        uint16_t *out);
 /* jmh_tq4x4_batch: dct_luma on n independent 4x4 residual blocks.  resid[n][16] (raster),
  *   pred[n][16] (raster), levels[n][16] (scan order), recon[n][16] (raster); nonzero[n].
- *   intra selects the JM 8.6 intra rounding offset ((1<<q_bits)/3) vs inter (/6).          */
+ *   intra selects the I-slice rounding offset vs the P-slice one: JM 8.6 (1<<q_bits)/3 vs /6,
+ *   or with jm_version >= 10 the context's quant_offset[0] vs [1] << (q_bits - 11).          */
 int  jmh_tq4x4_batch(jmh_ctx *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp,
                      int intra, int16_t *levels, uint8_t *recon, int32_t *coeff_cost,
                      int32_t *nonzero);
 /* jmh_tq8x8_batch: dct_luma8x8 (High profile, a12) on n independent 8x8 blocks, the same
  *   one-wave-per-block primitive as the macroblock kernels.  resid[n][64] (raster), pred[n][64]
  *   (raster), levels[n][64] (8x8 zig-zag scan order), recon[n][64] (raster); coeff_cost[n]
- *   (COEFF_COST8x8), nonzero[n].  intra selects the (1<<q_bits)/3 rounding offset vs /6.   */
+ *   (COEFF_COST8x8), nonzero[n].  intra selects the rounding offset as for jmh_tq4x4_batch. */
 int  jmh_tq8x8_batch(jmh_ctx *ctx, int n, const int16_t *resid, const uint8_t *pred, int qp,
                      int intra, int16_t *levels, uint8_t *recon, int32_t *coeff_cost,
                      int32_t *nonzero);

@@ -494,7 +494,7 @@ static void partition_motion_search(mbs *s, int blocktype, int block8x8) {
 static int dct_luma4x4(const int32_t resid[16], const uint8_t *pred, int ps, int qp, int intra_round,
                        int16_t levels[16], int *coeff_cost, uint8_t *rec, int rs) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS + qp_per;
-    int qp_const = intra_round ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+    int qp_const = jmo_qround(intra_round, q_bits);
     int32_t m[16];
     memcpy(m, resid, sizeof(m));
     jmo_fwd4x4(m);
@@ -519,7 +519,7 @@ static int dct_luma4x4(const int32_t resid[16], const uint8_t *pred, int ps, int
 
 int jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,
                     int16_t *levels, uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
-    if (n < 0 || qp < 0 || qp > 51) return JMH_E_INVALID_ARG;
+    if (n < 0 || qp < 0 || qp > 51 || intra < 0 || intra > JMO_RND_OFF(JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     for (int i = 0; i < n; i++) {
         int32_t r[16];
         int cc = 0;
@@ -538,7 +538,7 @@ int jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, in
 static int dct_luma8x8(const int32_t resid[64], const uint8_t *pred, int ps, int qp, int intra_round,
                        int16_t levels[64], int *coeff_cost, uint8_t *rec, int rs) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS_8 + qp_per;
-    int qp_const = intra_round ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+    int qp_const = jmo_qround(intra_round, q_bits);
     int scan[64];
     jmo_scan8x8(scan);
     int32_t m[64];
@@ -566,7 +566,7 @@ static int dct_luma8x8(const int32_t resid[64], const uint8_t *pred, int ps, int
 
 int jmo_tq8x8_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,
                     int16_t *levels, uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero) {
-    if (n < 0 || qp < 0 || qp > 51) return JMH_E_INVALID_ARG;
+    if (n < 0 || qp < 0 || qp > 51 || intra < 0 || intra > JMO_RND_OFF(JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     for (int i = 0; i < n; i++) {
         int32_t r[64];
         int cc = 0;
@@ -594,7 +594,7 @@ static void put_levels8(int16_t luma[16][16], int b8, const int16_t lev[64]) {
 static int dct_chroma(const int32_t resid[64], const uint8_t pred[64], int qpc, int intra_round,
                       int cr_cbp, int16_t dc_out[4], int16_t ac_out[4][16], uint8_t rec[64]) {
     int qp_per = qpc / 6, qp_rem = qpc % 6, q_bits = Q_BITS + qp_per;
-    int qp_const = intra_round ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+    int qp_const = jmo_qround(intra_round, q_bits);
     int32_t m[4][16];
     for (int b = 0; b < 4; b++) {
         int ox = (b & 1) * 4, oy = (b >> 1) * 4;
@@ -649,10 +649,10 @@ static int dct_chroma(const int32_t resid[64], const uint8_t pred[64], int qpc, 
 }
 
 /* dct_luma_16x16 [J]: returns luma cbp (15 if any AC level, else 0) */
-static int dct_luma_16x16(const int32_t resid[256], const uint8_t pred[256], int qp,
+static int dct_luma_16x16(const int32_t resid[256], const uint8_t pred[256], int qp, int rnd,
                           int16_t dc_out[16], int16_t ac_out[16][16], int *cbp_blk, uint8_t rec[256]) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS + qp_per;
-    int qp_const = (1 << q_bits) / 3, qp_const2 = qp_const << 1;
+    int qp_const = jmo_qround(rnd, q_bits), qp_const2 = qp_const << 1;   /* JM 8.6: always / 3 */
     int32_t m[16][16];                     /* [4x4 block raster][coef raster] */
     for (int b = 0; b < 16; b++) {
         int ox = (b & 3) * 4, oy = (b >> 2) * 4;
@@ -1102,7 +1102,11 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     s->lf = 65536 * s->lambda;
     s->slice_p = c->fp.slice_type == JMH_P_SLICE;
     int qp = c->fp.qp, lambda = c->fp.lambda_mode;
-    int intra_round = !s->slice_p;                 /* JM 8.6: qp_const by slice type [J] */
+    /* JM 8.6: qp_const by slice type, Intra16x16 always / 3 [J]; JM >= 10: the slice's flat
+     * OffsetMatrix entry for every block (items 1, 45) */
+    const int jm10 = c->cfg.jm_version >= 10;
+    int intra_round = jm10 ? JMO_RND_OFF(c->cfg.quant_offset[s->slice_p]) : !s->slice_p;
+    int i16_round = jm10 ? intra_round : JMO_RND_I;
     int W = c->W, W4 = W >> 2;
     for (int y = 0; y < 16; y++) memcpy(s->org + 16 * y, c->orgY + (s->pix_y + y) * W + s->pix_x, 16);
     for (int y = 0; y < 8; y++) {
@@ -1252,7 +1256,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     } else if (best_mode == JMH_I16MB) {
         int32_t r[256];
         for (int k = 0; k < 256; k++) r[k] = s->org[k] - i16pred[i16mode][k];
-        cbp = dct_luma_16x16(r, i16pred[i16mode], qp, res->luma_dc, res->luma, &cbp_blk, rec);
+        cbp = dct_luma_16x16(r, i16pred[i16mode], qp, i16_round, res->luma_dc, res->luma, &cbp_blk, rec);
         res->i16mode = (int8_t)i16mode;
     } else {
         /* LumaResidualCoding / LumaResidualCoding8x8 (also SetCoeffAndReconstruction8x8) */

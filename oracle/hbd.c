@@ -185,10 +185,10 @@ int jmo_hbd_sad_table(const jmo_hbd *h, int n_mb, const int32_t *mb_xy, const in
 /* dct_luma [J] at qp + QpBdOffsetY: levels (scan order), recon clipped to (1 << bd) - 1 */
 int jmo_hbd_tq4x4_batch(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bd, int16_t *levels, uint16_t *recon,
                         int32_t *coeff_cost, int32_t *nonzero) {
-    if (n < 0 || qp < 0 || qp > 51 || bd < 8 || bd > 10) return JMH_E_INVALID_ARG;
+    if (n < 0 || qp < 0 || qp > 51 || bd < 8 || bd > 10 || intra < 0 || intra > JMO_RND_OFF(JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     const int qpb = qp + 6 * (bd - 8), maxv = (1 << bd) - 1;
     const int qp_per = qpb / 6, qp_rem = qpb % 6, q_bits = Q_BITS + qp_per;
-    const int qp_const = intra ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+    const int qp_const = jmo_qround(intra, q_bits);
     for (int i = 0; i < n; i++) {
         int32_t m[16], rr[16];
         for (int k = 0; k < 16; k++) m[k] = resid[16 * i + k];
@@ -221,10 +221,10 @@ int jmo_hbd_tq4x4_batch(int n, const int16_t *resid, const uint16_t *pred, int q
 /* dct_luma8x8 [J] at qp + QpBdOffsetY: normative 8.5.13.1 dequantisation, recon clipped */
 int jmo_hbd_tq8x8_batch(int n, const int16_t *resid, const uint16_t *pred, int qp, int intra, int bd, int16_t *levels, uint16_t *recon,
                         int32_t *coeff_cost, int32_t *nonzero) {
-    if (n < 0 || qp < 0 || qp > 51 || bd < 8 || bd > 10) return JMH_E_INVALID_ARG;
+    if (n < 0 || qp < 0 || qp > 51 || bd < 8 || bd > 10 || intra < 0 || intra > JMO_RND_OFF(JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     const int qpb = qp + 6 * (bd - 8), maxv = (1 << bd) - 1;
     const int qp_per = qpb / 6, qp_rem = qpb % 6, q_bits = Q_BITS_8 + qp_per;
-    const int qp_const = intra ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+    const int qp_const = jmo_qround(intra, q_bits);
     int scan[64];
     jmo_scan8x8(scan);
     for (int i = 0; i < n; i++) {

@@ -52,6 +52,9 @@ int  jmo_search_pictures(jmo_ctx *c, const uint8_t *cur_y, const uint8_t *ref_y,
 int  jmo_block_motion_search(jmo_ctx *c, int n, const jmh_block_search *req, jmh_block_result *res);
 int  jmo_ffs_sad_table(jmo_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t *centres,
                        uint16_t *out);
+/* TQ seams: `intra` is the rounding selector of jmo_internal.h (0: JM 8.6 P-slice / 6, 1: I-slice
+ * / 3, 2 + o: JM >= 10 flat OffsetMatrix entry o at OffsetBits 11), here and in jmo_tq8x8_batch /
+ * jmo_hbd_tq*_batch                                                                         */
 int  jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, int intra,
                      int16_t *levels, uint8_t *recon, int32_t *coeff_cost, int32_t *nonzero);
 /* spec luma sample at quarter-pel position (X,Y) of an integer plane (clamped coords)   */

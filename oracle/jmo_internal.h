@@ -75,6 +75,18 @@ void jmo_inv4x4_add(const int32_t m[16], const uint8_t *pred, int pstride, uint8
 
 /* 8x8 transform (High profile) */
 #define Q_BITS_8 16               /* JM FRExt Q_BITS_8 [J]                                 */
+
+/* Quantisation rounding selector (docs/JM_SEMANTICS.md items 1 and 45), the `intra_round` argument
+ * of the dct_* functions and the oracle's TQ seams: JMO_RND_P / JMO_RND_I are JM 8.6's
+ * (1 << q_bits) / 6 and / 3; JMO_RND_OFF(o) is a JM >= 10 flat OffsetMatrix entry o at OffsetBits 11
+ * (q_offsets.c CalculateOffsetParam: LevelOffset = OffsetList << (q_bits - OffsetBits)) [J] */
+#define JMO_RND_P 0
+#define JMO_RND_I 1
+#define JMO_RND_OFF(o) (2 + (o))
+#define OFFSET_BITS 11
+static inline int jmo_qround(int rnd, int q_bits) {
+    return rnd >= 2 ? (rnd - 2) << (q_bits - OFFSET_BITS) : rnd ? (1 << q_bits) / 3 : (1 << q_bits) / 6;
+}
 extern const int jmo_quant8_cls[6][6];
 extern const int jmo_dequant8_cls[6][6];
 int  jmo_class8(int x, int y);

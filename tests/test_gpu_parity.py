@@ -392,6 +392,11 @@ def run_lencod(binary, out_dir, extra):
     ["InputFile=synthetic:22", "FramesToBeEncoded=4", "SourceWidth=200", "SourceHeight=120", "SearchRange=8",
      "ProfileIDC=100", "Transform8x8Mode=1", "QPFirstFrame=38", "QPRemainingFrame=40", "IntraPeriod=2",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=-3", "LoopFilterBetaOffset=2"],
+    # JMVersion 10 (docs/JM_SEMANTICS.md item 45): q_offsets.c flat offsets 682 / 342, Intra16x16 in P
+    ["InputFile=synthetic:25", "FramesToBeEncoded=4", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "JMVersion=10", "QPRemainingFrame=30"],
+    ["InputFile=synthetic:26", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "JMVersion=10"],
 ])
 def test_lencod_bitstream_identical(extra):
     with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:

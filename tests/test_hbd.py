@@ -65,12 +65,13 @@ COST = [3, 2, 2, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0]
 
 
 def np_dct_luma(resid, pred, qp, intra, bd):
-    """dct_luma [J] at qp + 6 (bd - 8) (8.5.12 inverse, JM 8.6 rounding offsets)."""
+    """dct_luma [J] at qp + 6 (bd - 8) (8.5.12 inverse; JM 8.6 or JM >= 10 rounding offsets)."""
     C = np.array([[1, 1, 1, 1], [2, 1, -1, -2], [1, -1, -1, 1], [1, -2, 2, -1]], np.int64)
     m = C @ resid.reshape(4, 4).astype(np.int64) @ C.T
     qpb = qp + 6 * (bd - 8)
     per, rem, qb = qpb // 6, qpb % 6, 15 + qpb // 6
-    const = (1 << qb) // 3 if intra else (1 << qb) // 6
+    # intra: the rounding selector (0 / 1 JM 8.6 / 6 and / 3; 2 + o JM >= 10 offset o at OffsetBits 11)
+    const = (intra - 2) << (qb - 11) if intra >= 2 else (1 << qb) // 3 if intra else (1 << qb) // 6
     lev = np.zeros(16, np.int64)
     dq = np.zeros((4, 4), np.int64)
     cost, run = 0, -1

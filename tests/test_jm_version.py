@@ -1,0 +1,157 @@
+"""JMVersion (docs/JM_SEMANTICS.md item 45): the JM 8.6 quantisation rounding ((1 << q_bits) / 3
+in I slices, / 6 in P slices, Intra16x16 always / 3) against JM >= 10's q_offsets.c rounding (flat
+OffsetMatrix entries at OffsetBits 11, defaults 682 / 342, applied to every block of the slice,
+AdaptiveRounding off).  CPU: the oracle's selector against a numpy restatement, the encoder.cfg
+knobs, the closed loop under JMVersion 10 and that the knob changes the bitstream.  GPU: the unit
+seams and whole pictures under jm_version 10 against the oracle."""
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from jmpaths import JMDEC, LENCOD_CPU, ensure_built, load_jmhip
+from test_hbd import np_dct_luma
+
+jmhip = load_jmhip()
+SEL = lambda o: 2 + o   # the oracle's JMO_RND_OFF(o)
+
+
+# ---------------- CPU ----------------
+@pytest.mark.parametrize("bd", [8, 10])
+def test_oracle_offsets_match_numpy(bd):
+    rng = np.random.default_rng(70 + bd)
+    mx = (1 << bd) - 1
+    resid = rng.integers(-mx, mx + 1, (48, 16)).astype(np.int16)
+    resid[:4] = np.where(rng.random((4, 16)) < 0.5, mx, -mx)
+    pred = rng.integers(0, mx + 1, (48, 16)).astype(np.uint16)
+    for qp in (0, 5, 18, 28, 40, 51):
+        for sel in (SEL(682), SEL(342), SEL(0), SEL(2047), SEL(1024)):
+            lev, rec, cc, nz = oracle_lib.tq_u16(resid, pred, qp, sel, bd)
+            if bd == 8:   # the 8-bit seam takes the same selector
+                l8, r8, c8, n8 = oracle_lib.tq4x4(resid, pred.astype(np.uint8), qp, sel)
+                assert np.array_equal(l8, lev) and np.array_equal(r8, rec) and np.array_equal(c8, cc)
+            for i in range(0, 48, 5):
+                l2, r2, c2 = np_dct_luma(resid[i], pred[i], qp, sel, bd)
+                assert np.array_equal(lev[i], l2) and np.array_equal(rec[i], r2) and cc[i] == c2, (qp, sel, i)
+
+
+def test_offsets_differ_from_jm86_rounding():
+    """682 << (q_bits - 11) = 10912 << per is below (1 << q_bits) / 3 = 10922 << per: some levels
+    round differently; 342 << 4 = 5472 is above 5461."""
+    assert 682 << 4 < (1 << 15) // 3 and 342 << 4 > (1 << 15) // 6
+    rng = np.random.default_rng(3)
+    resid = rng.integers(-60, 61, (4096, 16)).astype(np.int16)
+    pred = np.full((4096, 16), 128, np.uint8)
+    a = oracle_lib.tq4x4(resid, pred, 28, 1)[0]
+    b = oracle_lib.tq4x4(resid, pred, 28, SEL(682))[0]
+    assert not np.array_equal(a, b)
+
+
+def test_selector_range_checked():
+    resid = np.zeros((1, 16), np.int16)
+    pred = np.zeros((1, 16), np.uint8)
+    L = oracle_lib.lib()
+    lev, rec = np.empty((1, 16), np.int16), np.empty((1, 16), np.uint8)
+    cc, nz = np.empty(1, np.int32), np.empty(1, np.int32)
+    P = oracle_lib._ptr
+    assert L.jmo_tq4x4_batch(1, P(resid), P(pred), 28, SEL(2048), P(lev), P(rec), P(cc), P(nz)) != 0
+    assert L.jmo_tq4x4_batch(1, P(resid), P(pred), 28, -1, P(lev), P(rec), P(cc), P(nz)) != 0
+
+
+def run(*args):
+    ensure_built()
+    return subprocess.run([LENCOD_CPU, *args], capture_output=True, text=True, timeout=300)
+
+
+def test_cfg_knobs():
+    assert "JMVersion=9" in run("-p", "JMVersion=9").stderr
+    r = run("-p", "QOffsetIntra=600")
+    assert r.returncode != 0 and "JMVersion" in r.stderr
+    r = run("-p", "JMVersion=10", "-p", "AdaptiveRounding=1")
+    assert r.returncode != 0 and "AdaptiveRounding" in r.stderr
+    r = run("-p", "JMVersion=10", "-p", "OffsetMatrixPresentFlag=1")
+    assert r.returncode != 0 and "OffsetMatrixPresentFlag" in r.stderr
+    r = run("-p", "JMVersion=10", "-p", "QOffsetInter=2048")
+    assert r.returncode != 0 and "out of range" in r.stderr
+
+
+JM10_CASES = [
+    ["InputFile=synthetic:31", "FramesToBeEncoded=4", "SearchRange=16", "JMVersion=10"],
+    ["InputFile=synthetic:32", "FramesToBeEncoded=4", "SearchRange=16", "JMVersion=10", "QPRemainingFrame=36",
+     "IntraPeriod=2"],
+    ["InputFile=synthetic:33", "FramesToBeEncoded=4", "SearchMode=3", "SearchRange=16", "ProfileIDC=100",
+     "Transform8x8Mode=1", "SourceWidth=352", "SourceHeight=288", "JMVersion=10"],
+    ["InputFile=synthetic:34", "FramesToBeEncoded=3", "SearchRange=8", "JMVersion=10", "QOffsetIntra=1024",
+     "QOffsetInter=0", "ProfileIDC=100", "Transform8x8Mode=1"],
+    ["InputFile=synthetic:35", "FramesToBeEncoded=3", "SearchRange=8", "JMVersion=10", "QOffsetIntra=2047",
+     "QOffsetInter=2047", "QPFirstFrame=20", "QPRemainingFrame=24"],
+]
+
+
+def encode(d, extra, name="a"):
+    args = ["-p", f"OutputFile={d}/{name}.264", "-p", f"ReconFile={d}/{name}.yuv"]
+    for e in extra:
+        args += ["-p", e]
+    r = run(*args)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return open(f"{d}/{name}.264", "rb").read()
+
+
+@pytest.mark.parametrize("extra", JM10_CASES, ids=[c[0].split(":")[1] for c in JM10_CASES])
+def test_closed_loop_jm10(extra):
+    with tempfile.TemporaryDirectory() as d:
+        bs10 = encode(d, extra)
+        r = subprocess.run([JMDEC, f"{d}/a.264", f"{d}/dec.yuv"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/a.yuv", "rb").read()
+        # the default offsets move few levels (10912 vs 10922, 5472 vs 5461 per 2^per), so a short
+        # sequence may come out identical; the QCIF default case and the explicit offsets do not
+        if extra in (JM10_CASES[0], JM10_CASES[3], JM10_CASES[4]):
+            plain = [e for e in extra if not e.startswith(("JMVersion", "QOffset"))]
+            assert encode(d, plain, "b") != bs10, "JMVersion 10 rounding did not change the bitstream"
+
+
+# ---------------- GPU ----------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("offs", [(682, 342), (2047, 0), (1024, 1)])
+def test_gpu_tq_seams_jm10(offs):
+    rng = np.random.default_rng(sum(offs))
+    g = jmhip.Encoder(32, 32, search_range=4, jm_version=10, quant_offset=offs)
+    for el, gf, of in ((16, g.tq4x4, oracle_lib.tq4x4), (64, g.tq8x8, oracle_lib.tq8x8)):
+        resid = rng.integers(-255, 256, (512, el)).astype(np.int16)
+        resid[:16] = np.where(rng.random((16, el)) < 0.5, 255, -255)
+        pred = rng.integers(0, 256, (512, el)).astype(np.uint8)
+        for qp in range(52):
+            for intra in (0, 1):
+                a = gf(resid, pred, qp, intra)
+                b = of(resid, pred, qp, SEL(offs[0] if intra else offs[1]))
+                for x, y in zip(a, b):
+                    assert np.array_equal(x, y), (el, qp, intra)
+    for bd in (10, 9):
+        mx = (1 << bd) - 1
+        for el in (16, 64):
+            resid = rng.integers(-mx, mx + 1, (128, el)).astype(np.int16)
+            resid[:16] = np.where(rng.random((16, el)) < 0.5, mx, -mx)
+            pred = rng.integers(0, mx + 1, (128, el)).astype(np.uint16)
+            for qp in range(0, 52, 3):
+                for intra in (0, 1):
+                    a = g.tq_u16(resid, pred, qp, intra, bd)
+                    b = oracle_lib.tq_u16(resid, pred, qp, SEL(offs[0] if intra else offs[1]), bd)
+                    for x, y in zip(a, b):
+                        assert np.array_equal(x, y), (bd, el, qp, intra)
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw,qp", [
+    (dict(search_range=16), 28),
+    (dict(search_range=8, quant_offset=(2047, 0)), 24),
+    (dict(search_range=16, search_mode=3, transform_8x8_mode=1), 30),
+    (dict(search_range=8, search_mode=-1, transform_8x8_mode=1, quant_offset=(1024, 1024)), 36),
+])
+def test_gpu_pictures_jm10(kw, qp):
+    from test_gpu_parity import encode_pair, synth_seq
+    pics = synth_seq(176, 144, 3, 41)
+    encode_pair(176, 144, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], qp, jm_version=10, **kw)
