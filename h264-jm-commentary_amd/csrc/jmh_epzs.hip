@@ -15,24 +15,33 @@
 //     and j from unclipped horizontal taps, so j is one vertical 6-tap per sample; G is the window),
 //     lane task = (candidate, 4x4 sub-block) with a packed int16 Hadamard, DPP sums over the
 //     candidate's lanes, one wave minimum per pass.
-// LDS: the window MB +- (2 SR + 4) (every block's reach when each search centres on its own
-// MVP, as k_mb_me_full) + ~3.5 KB state = 26 KB, six macroblocks per CU.  Results land in
-// MbScratch exactly like the other search kernels (the intra workgroups and k_mb_final are shared).
+// LDS: a 120x120 window (+ ~4.5 KB state = 18.6 KB: eight macroblocks per CU, so a 2160p tick's
+// ~2,000 P macroblocks run in one round).  A block's reach is MB +- (2 SR + 4) when each search
+// centres on its own MVP; the window covers MB +- 52 around the MB's 16x16 MVP / 4 (the centre
+// of most searches), i.e. everything when 2 SR + 4 <= 52, and a sample outside it is read from
+// the reference picture in global memory instead (UMV-clamped, as the window load clamps): per
+// lane in the full-pel SADs, per search (into a small neighbourhood plane) for the sub-pel planes.
+// Results land in MbScratch exactly like the other search kernels (the intra workgroups and
+// k_mb_final are shared).
 #include "jmh_common.h"
 
 #define NTE 64                                // one wave per macroblock
-#define EOFF_MAX (2 * SRMAX + 4)              // window margin around the MB
-#define EW_MAX (16 + 2 * EOFF_MAX)            // 152
-#define EST EW_MAX                            // window row stride (the second dword of an
-                                              // unaligned read may touch the next row: harmless)
+#define EOFF_L 52                             // LDS window margin around the MB (or 2 SR + 4 if less)
+#define EW_MAX (16 + 2 * EOFF_L)              // 120
+#define EST EW_MAX                            // window row stride
 #define NPRED 41                              // EPZS predictor slots (oracle epzs_predictors)
 #define HPS 20                                // sub-pel plane stride (>= 18 + 2 alignment slack)
 #define HPR 18                                // sub-pel plane rows (block + 1 on each side)
 #define HPL (HPR * HPS + 8)                   // sub-pel plane size (b, h, j)
 #define EKOFF 4096                            // sub-pel cost offset in keys (16x16 zero-vector bias)
+#define GNX 8                                 // sub-pel neighbourhood plane (a search whose reach leaves
+#define GNY 5                                 //   the window): block-relative x in [-GNX, 4 w4 + 2 + GNX),
+#define GNS 36                                //   y in [-GNY, 4 h4 + 2 + GNY), stride GNS
+#define GNR (18 + 2 * GNY)
 
 struct EpzS {
-    uint8_t g[EW_MAX * EST];                  // (a dword read past the last row lands in org: harmless)
+    uint8_t g[EW_MAX * EST];                  // the window
+    uint8_t gn[GNR * GNS + 8];                // a search's integer-sample neighbourhood read from global
     uint8_t org[256];
     Border bd;
     int16_t all_mv[8][16][2];
@@ -68,6 +77,17 @@ __device__ __forceinline__ uint32_t eld_u32(const uint8_t *p) {   // 4 bytes at 
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+// the LDS window: picture position of its sample (0, 0) and window position of the MB origin
+struct EWin {
+    const uint8_t *ref;
+    int W, H;
+    int wx0, wy0, mx, my;
+};
+// reference sample at picture position (x, y), UMV-clamped (8.4.2.2.1), from global memory
+__device__ __forceinline__ uint32_t gref(const EWin &w, int x, int y) {
+    return w.ref[iclip(0, w.H - 1, y) * w.W + iclip(0, w.W - 1, x)];
 }
 
 // the spatial neighbours A, B, C (or D) of a block as SetMotionVectorPredictor reads them (H.264
@@ -170,20 +190,35 @@ __device__ __forceinline__ void epzs_pat(bool sd, int e, int &px, int &py) {
 // SAD of the whole block (4 w4 x 4 h4 at 4x4 position bx4, by4) at full-pel displacement (x, y)
 // on this lane: per row w4 + 1 aligned dwords, v_alignbyte, v_sad_u8
 template <int LW4, int LH4>
-__device__ __forceinline__ unsigned lane_block_sad(const EpzS &s, int off, int bx4, int by4, int x, int y) {
+__device__ __forceinline__ unsigned lane_block_sad(const EpzS &s, const EWin &wn, int bx4, int by4, int x, int y) {
     constexpr int W4 = 1 << LW4, H = 4 << LH4;
-    const int a = (off + 4 * by4 + y) * EST + off + 4 * bx4 + x;
-    const uint32_t sel = (uint32_t)(a & 3);
-    const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~3));
+    const int gx = wn.mx + 4 * bx4 + x, gy = wn.my + 4 * by4 + y;
     const uint32_t *org = reinterpret_cast<const uint32_t *>(s.org + (4 * by4) * 16 + 4 * bx4);
     uint32_t sad = 0;
+    if (gx >= 0 && gx + 4 * W4 + 4 <= EST && gy >= 0 && gy + H <= EW_MAX) {   // inside the window
+        const int a = gy * EST + gx;
+        const uint32_t sel = (uint32_t)(a & 3);
+        const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~3));
 #pragma unroll
-    for (int r = 0; r < H; r++) {
-        uint32_t w[W4 + 1];
+        for (int r = 0; r < H; r++) {
+            uint32_t w[W4 + 1];
 #pragma unroll
-        for (int q = 0; q <= W4; q++) w[q] = base[r * (EST / 4) + q];
+            for (int q = 0; q <= W4; q++) w[q] = base[r * (EST / 4) + q];
 #pragma unroll
-        for (int q = 0; q < W4; q++) sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), org[r * 4 + q], sad);
+            for (int q = 0; q < W4; q++) sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), org[r * 4 + q], sad);
+        }
+    } else {   // outside: the reference picture in global memory, clamped (rare: far predictors)
+        const int px = wn.wx0 + gx, py = wn.wy0 + gy;
+#pragma unroll 1
+        for (int r = 0; r < H; r++) {
+#pragma unroll
+            for (int q = 0; q < W4; q++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) v |= gref(wn, px + 4 * q + b, py + r) << (8 * b);
+                sad = __builtin_amdgcn_sad_u8(v, org[r * 4 + q], sad);
+            }
+        }
     }
     return sad;
 }
@@ -195,8 +230,8 @@ __device__ __forceinline__ e16x2 e_abs2(e16x2 v) { return __builtin_elementwise_
 
 // row pointer and stride of half-grid plane pl (0 G = the window, 1 b, 2 h, 3 j) at block-
 // relative integer position (rx, ry) (b / h / j sample [y][x] = position (x - 1, y - 1))
-__device__ __forceinline__ const uint8_t *hp_row(const EpzS &s, int pl, int gx0, int gy0, int rx, int ry, int &stride) {
-    if (pl == 0) { stride = EST; return s.g + (gy0 + ry) * EST + gx0 + rx; }
+__device__ __forceinline__ const uint8_t *hp_row(const EpzS &s, int pl, const uint8_t *gb, int gs, int rx, int ry, int &stride) {
+    if (pl == 0) { stride = gs; return gb + ry * gs + rx; }
     stride = HPS;
     return s.hp[pl - 1] + (ry + 1) * HPS + rx + 1;
 }
@@ -205,13 +240,13 @@ __device__ __forceinline__ const uint8_t *hp_row(const EpzS &s, int pl, int gx0,
 // MV (window position gx0, gy0 of the block origin): block-relative sub-block origin (sx, sy);
 // rows as dwords from the phase's two half-grid planes, their rounding average per byte, packed
 // int16 Hadamard (as subblock_satd)
-__device__ __forceinline__ int hp_satd(const EpzS &s, int gx0, int gy0, int sx, int sy, int obase, int ox, int oy, int had) {
+__device__ __forceinline__ int hp_satd(const EpzS &s, const uint8_t *gb, int gs, int sx, int sy, int obase, int ox, int oy, int had) {
     const int off = qoff((oy & 3) * 4 + (ox & 3));
     const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
     const int rx = sx + (ox >> 2), ry = sy + (oy >> 2);
     int sa, sb;
-    const uint8_t *pA = hp_row(s, (xa & 1) + 2 * (ya & 1), gx0, gy0, rx + (xa >> 1), ry + (ya >> 1), sa);
-    const uint8_t *pB = hp_row(s, (xb & 1) + 2 * (yb & 1), gx0, gy0, rx + (xb >> 1), ry + (yb >> 1), sb);
+    const uint8_t *pA = hp_row(s, (xa & 1) + 2 * (ya & 1), gb, gs, rx + (xa >> 1), ry + (ya >> 1), sa);
+    const uint8_t *pB = hp_row(s, (xb & 1) + 2 * (yb & 1), gb, gs, rx + (xb >> 1), ry + (yb >> 1), sb);
     uint32_t O[4], P[4];
 #pragma unroll
     for (int yy = 0; yy < 4; yy++) {
@@ -253,7 +288,7 @@ __device__ __forceinline__ int hp_satd(const EpzS &s, int gx0, int gy0, int sx, 
 
 // BlockMotionSearch [J] of one block on the wave: EPZS full pel + SubPelBlockMotionSearch
 template <int BT>
-__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off, int bx4, int by4, int mc, int b8, int best8x8, bool prof) {
+__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, const EWin &wn, int bx4, int by4, int mc, int b8, int best8x8, bool prof) {
     // debug (JMH_PHASE_PROF): steps of the MB's first 4x4 search into prof[41..46]
     const bool sp = prof && BT == 7 && bx4 == 0 && by4 == 0;
 #define SSTAMP(k) do { if (sp) d.prof[41 + (k)] = wall_clock64(); } while (0)
@@ -276,7 +311,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
     int cx, cy;
     const bool cv = epzs_cand(d, s, lane, BT, bx4, by4, nb, range, mvx0, mvy0, cx, cy);
     if (!cv) { cx = mvx0; cy = mvy0; }   // any valid position for the SAD (key discarded)
-    const int c0 = (int)lane_block_sad<LW4, LH4>(s, off, bx4, by4, cx, cy) +
+    const int c0 = (int)lane_block_sad<LW4, LH4>(s, wn, bx4, by4, cx, cy) +
                    (int)__umul24(lam, mvbits(4 * cx - pmx) + mvbits(4 * cy - pmy));
     const int cost0 = __builtin_amdgcn_readfirstlane(c0);   // predictor 0: the centre, always valid
     SSTAMP(2);
@@ -299,7 +334,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
                 const int x = bx + ddx, y = by + ddy;
                 const bool inw = lane < 41 && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
                 int c = 0;
-                if (inw) c = (int)lane_block_sad<LW4, LH4>(s, off, bx4, by4, x, y) + (int)__umul24(lam, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+                if (inw) c = (int)lane_block_sad<LW4, LH4>(s, wn, bx4, by4, x, y) + (int)__umul24(lam, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
                 for (int k = 0; k < steps; k++) {
                     const int rx = x - bx, ry = y - by;   // this lane's position relative to the current best
                     int e = 15;
@@ -324,10 +359,24 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
     // ---- sub-pel neighbourhood of the block at (fmx, fmy): b, h, j planes, sample [y][x] =
     //      block-relative (x - 1, y - 1); b1 = unclipped horizontal taps, row rr <-> y = rr - 2
     constexpr int PW = 4 * W4 + 2, PH = 4 * H4 + 2;
-    const int gx0 = off + 4 * bx4 + fmx, gy0 = off + 4 * by4 + fmy;   // window position of (0, 0)
-    auto G = [&](int x, int y) { return (int)s.g[y * EST + x]; };
+    const int gx0 = wn.mx + 4 * bx4 + fmx, gy0 = wn.my + 4 * by4 + fmy;   // window position of (0, 0)
+    // integer samples around the block at its full-pel MV: the window, or when the reach
+    // [-GNX, PW + GNX) x [-GNY, PH + GNY) leaves it, the neighbourhood plane read from global
+    const uint8_t *gb;
+    int gs;
+    if (gx0 - GNX >= 0 && gx0 + PW + GNX <= EST && gy0 - GNY >= 0 && gy0 + PH + GNY <= EW_MAX) {   // wave-uniform
+        gb = s.g + gy0 * EST + gx0; gs = EST;
+    } else {
+        for (int i = lane; i < (PH + 2 * GNY) * GNS; i += NTE) {
+            const int y = i / GNS, x = i - y * GNS;
+            s.gn[i] = (uint8_t)gref(wn, wn.wx0 + gx0 + x - GNX, wn.wy0 + gy0 + y - GNY);
+        }
+        wave_lds_sync();
+        gb = s.gn + GNY * GNS + GNX; gs = GNS;
+    }
+    auto G = [&](int x, int y) { return (int)gb[y * gs + x]; };
     for (int i = lane; i < PW * (PH + 5); i += NTE) {
-        const int rr = i / PW, x = i - rr * PW, gx = gx0 + x - 1, gy = gy0 + rr - 3;
+        const int rr = i / PW, x = i - rr * PW, gx = x - 1, gy = rr - 3;
         const int h1 = tap6(G(gx - 2, gy), G(gx - 1, gy), G(gx, gy), G(gx + 1, gy), G(gx + 2, gy), G(gx + 3, gy));
         s.b1[rr][x] = (int16_t)h1;
         if (rr >= 2 && rr < PH + 2) {
@@ -360,7 +409,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
             int sat = 0;
             if (p < 49) {
                 const int sx = 4 * (sub & (W4 - 1)), sy = 4 * (sub >> LW4);
-                sat = hp_satd(s, gx0, gy0, sx, sy, 64 * by4 + 4 * bx4 + 16 * sy + sx, ox, oy, had);
+                sat = hp_satd(s, gb, gs, sx, sy, 64 * by4 + 4 * bx4 + 16 * sy + sx, ox, oy, had);
             }
             if constexpr (NSUB >= 2) sat += dpp<0xB1>(sat);
             if constexpr (NSUB >= 4) sat += dpp<0x4E>(sat);
@@ -411,7 +460,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, int off,
                 int sat = 0;
                 if (val) {
                     const int sx = 4 * (sub & (W4 - 1)), sy = 4 * (sub >> LW4);
-                    sat = hp_satd(s, gx0, gy0, sx, sy, 64 * by4 + 4 * bx4 + 16 * sy + sx, ox, oy, had);
+                    sat = hp_satd(s, gb, gs, sx, sy, 64 * by4 + 4 * bx4 + 16 * sy + sx, ox, oy, had);
                 }
                 sat += dpp<0xB1>(sat);
                 sat += dpp<0x4E>(sat);
@@ -451,7 +500,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     const DevParams d = tick_params(t, e);
     const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, sr = d.sr;
-    const int off = 2 * sr + 4, wdim = 16 + 2 * off;
+    const int off = min(2 * sr + 4, EOFF_L), wdim = 16 + 2 * off;
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const int X0 = 4 * mbx, Y0 = 4 * mby, left = mbx > 0 ? mby * d.mbw + mbx - 1 : -1;
     const bool prof = d.prof && lane == 0 && d.prof_mb == mby * d.mbw + mbx;
@@ -477,12 +526,23 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
         s.mem[m - 1][k][c] = left >= 0 ? d.scr[left].all_mv[m][k][c] : 0;
     }
     if (lane == 0) s.memok = left >= 0;
+    // the window: MB +- off, shifted to the MB's 16x16 MVP / 4 (clamped to +-SR; horizontally a
+    // multiple of 4) when off < 2 SR + 4 -- the centre most searches search around
+    int wcx = 0, wcy = 0;
+    if (off < 2 * sr + 4) {
+        wave_lds_sync();   // the border cells
+        int pcx, pcy;
+        set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
+        wcx = __builtin_amdgcn_readfirstlane(iclip(-sr, sr, pcx / 4) & ~3);
+        wcy = __builtin_amdgcn_readfirstlane(iclip(-sr, sr, pcy / 4));
+    }
+    const EWin wn{d.refY, W, d.H, pix_x + wcx - off, pix_y + wcy - off, off - wcx, off - wcy};
     {
-        // with SearchRange even the window's dwords are aligned in the picture (pix_x % 16 == 0,
-        // off % 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an
-        // outside dword is the replicated edge sample.  Batches of 8 loads per lane in flight.
+        // with off % 4 == 0 the window's dwords are aligned in the picture (pix_x % 16 == 0, wcx %
+        // 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an outside
+        // dword is the replicated edge sample.  Batches of 8 loads per lane in flight.
         constexpr int ND4 = EST / 4, NB = 8;
-        const int WX0 = pix_x - off, WY0 = pix_y - off, ntask = wdim * ND4;
+        const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND4;
         if ((off & 3) == 0) {
             for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
                 uint32_t v[NB];
@@ -526,25 +586,25 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     // PartitionMotionSearch [J] order: 16x16, 16x8 (2), 8x16 (2), then per 8x8 block the sub-modes
     // 4..7 and its best sub-mode (read through best8x8)
     int best8x8 = 0, cost8x8 = 0;
-    epzs_block<1>(d, s, off, 0, 0, 0, 0, 0, prof);
+    epzs_block<1>(d, s, wn, 0, 0, 0, 0, 0, prof);
     if (prof) d.prof[34] = wall_clock64();
-    epzs_block<2>(d, s, off, 0, 0, 0, 0, 0, prof);
-    epzs_block<2>(d, s, off, 0, 2, 1, 0, 0, prof);
-    epzs_block<3>(d, s, off, 0, 0, 0, 0, 0, prof);
-    epzs_block<3>(d, s, off, 2, 0, 1, 0, 0, prof);
+    epzs_block<2>(d, s, wn, 0, 0, 0, 0, 0, prof);
+    epzs_block<2>(d, s, wn, 0, 2, 1, 0, 0, prof);
+    epzs_block<3>(d, s, wn, 0, 0, 0, 0, 0, prof);
+    epzs_block<3>(d, s, wn, 2, 0, 1, 0, 0, prof);
     if (prof) d.prof[35] = wall_clock64();
 #pragma unroll 1
     for (int b8 = 0; b8 < 4; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        epzs_block<4>(d, s, off, X, Y, b8, b8, best8x8, prof);
-        epzs_block<5>(d, s, off, X, Y, b8, b8, best8x8, prof);
-        epzs_block<5>(d, s, off, X, Y + 1, b8, b8, best8x8, prof);
-        epzs_block<6>(d, s, off, X, Y, b8, b8, best8x8, prof);
-        epzs_block<6>(d, s, off, X + 1, Y, b8, b8, best8x8, prof);
-        epzs_block<7>(d, s, off, X, Y, b8, b8, best8x8, prof);
-        epzs_block<7>(d, s, off, X + 1, Y, b8, b8, best8x8, prof);
-        epzs_block<7>(d, s, off, X, Y + 1, b8, b8, best8x8, prof);
-        epzs_block<7>(d, s, off, X + 1, Y + 1, b8, b8, best8x8, prof);
+        epzs_block<4>(d, s, wn, X, Y, b8, b8, best8x8, prof);
+        epzs_block<5>(d, s, wn, X, Y, b8, b8, best8x8, prof);
+        epzs_block<5>(d, s, wn, X, Y + 1, b8, b8, best8x8, prof);
+        epzs_block<6>(d, s, wn, X, Y, b8, b8, best8x8, prof);
+        epzs_block<6>(d, s, wn, X + 1, Y, b8, b8, best8x8, prof);
+        epzs_block<7>(d, s, wn, X, Y, b8, b8, best8x8, prof);
+        epzs_block<7>(d, s, wn, X + 1, Y, b8, b8, best8x8, prof);
+        epzs_block<7>(d, s, wn, X, Y + 1, b8, b8, best8x8, prof);
+        epzs_block<7>(d, s, wn, X + 1, Y + 1, b8, b8, best8x8, prof);
         int mc8 = BIGCOST, bm = 0;
         for (int mode = 4; mode <= 7; mode++) {
             if (!inter_on(d.isr, mode)) continue;
