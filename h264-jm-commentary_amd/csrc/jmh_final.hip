@@ -95,7 +95,7 @@ __device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int al
 }
 
 
-__global__ __launch_bounds__(NT, 7) void k_mb_final(const TickArgs t) {
+__global__ __launch_bounds__(NT, 8) void k_mb_final(const TickArgs t) {
     __shared__ FinS s;
     const int tid = threadIdx.x;
     const unsigned long long bt0 = t.bprof_fin ? wall_clock64() : 0;

@@ -20,7 +20,7 @@ struct I8S {
     int nz[4];
 };
 
-__global__ __launch_bounds__(NT, 6) void k_mb_intra8(const TickArgs t) {
+__global__ __launch_bounds__(NT, 8) void k_mb_intra8(const TickArgs t) {
     __shared__ I8S s;
     const int tid = threadIdx.x;
     const int mi = xcd_block(blockIdx.x, t.pre[t.npic]);      // XCD-aware (jmh_device.h)
