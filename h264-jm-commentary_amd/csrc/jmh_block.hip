@@ -19,7 +19,7 @@
 #define BKOFF 8192                       // cost offset: the zero-vector bias can make a cost negative
 
 __device__ __forceinline__ int mv_cost_lf(int lf, int shift, int cx, int cy, int px, int py) {
-    return (lf * (mvbits((cx << shift) - px) + mvbits((cy << shift) - py))) >> 16;   // MV_COST [J]
+    return (lf * (mvbits(cx * (1 << shift) - px) + mvbits(cy * (1 << shift) - py))) >> 16;   // MV_COST [J]
 }
 
 // T: uint8_t (8-bit) or uint16_t (High 10 seam, jmh_block_motion_search_u16: maxv = 2^bd - 1, the

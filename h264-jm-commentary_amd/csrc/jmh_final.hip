@@ -60,7 +60,7 @@ __device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int al
     if (chroma) {
         if (bS < 4) {
             const int tc = tc0 + 1;
-            const int dl = iclip(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+            const int dl = iclip(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
             q[-step] = (uint8_t)clip255(p0 + dl);
             q[0] = (uint8_t)clip255(q0 - dl);
         } else {
@@ -73,7 +73,7 @@ __device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int al
     const int ap = abs(p2 - p0), aq = abs(q2 - q0);
     if (bS < 4) {
         const int tc = tc0 + (ap < beta) + (aq < beta);
-        const int dl = iclip(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+        const int dl = iclip(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
         q[-step] = (uint8_t)clip255(p0 + dl);
         q[0] = (uint8_t)clip255(q0 - dl);
         if (ap < beta) q[-2 * step] = (uint8_t)(p1 + iclip(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(NT, 8) void k_mb_final(const TickArgs t) {
             for (int xx = 0; xx < 4; xx++) {
                 int e0 = t[xx] + t[8 + xx], e1 = t[xx] - t[8 + xx], e2 = t[4 + xx] - t[12 + xx], e3 = t[4 + xx] + t[12 + xx];
                 int fv[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
-                for (int yy = 0; yy < 4; yy++) s.dcdq[4 * yy + xx] = ((fv[yy] * v00 << qp_per) + 2) >> 2;
+                for (int yy = 0; yy < 4; yy++) s.dcdq[4 * yy + xx] = (fv[yy] * v00 * (1 << qp_per) + 2) >> 2;
             }
         }
         __syncthreads();
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(NT, 8) void k_mb_final(const TickArgs t) {
         int c0 = s.cdc[uv][0], c1 = s.cdc[uv][1], c2 = s.cdc[uv][2], c3 = s.cdc[uv][3];
         int fv[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
         int v00 = c_dq3[qp_rem][0];
-        for (int k = 0; k < 4; k++) s.cdcq[uv][k] = ((fv[k] * 16 * v00) << qp_per) >> 5;   // 8.5.11.2
+        for (int k = 0; k < 4; k++) s.cdcq[uv][k] = (fv[k] * 16 * v00 * (1 << qp_per)) >> 5;   // 8.5.11.2
         int cost = s.cbcost[uv][0] + s.cbcost[uv][1] + s.cbcost[uv][2] + s.cbcost[uv][3];
         int acany = s.cbnz[uv][0] | s.cbnz[uv][1] | s.cbnz[uv][2] | s.cbnz[uv][3];
         s.creset[uv] = cost < 4;                                  // _CHROMA_COEFF_COST_
