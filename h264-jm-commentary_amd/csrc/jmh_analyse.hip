@@ -31,6 +31,7 @@
 //     cost << 13 | JM order (0 for the (0,0) pre-check, else spiral index + 1), DPP wave min;
 //   * sub-pel SATD: one 4x4 sub-block per 16-lane row, DPP Hadamard, LDS-atomic candidate sums.
 #include "jmh_common.h"
+#include "jmh_intra8.h"
 
 #define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
 #define MVB_LEN 1104
@@ -1068,6 +1069,41 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
             t.bprof[3 * b + 2] = role;
         }
     }
+}
+
+// The intra analysis of a tick whose motion search has its own kernel (SearchMode -1: k_mb_me_full,
+// 3: k_mb_epzs): every MB's Intra4x4 + Intra16x16 + chroma decisions (intra_role, two MBs per
+// 256-thread workgroup) and, in the High profile, its Intra8x8 decision (intra8_mb, one MB per
+// workgroup) in ONE launch of small workgroups -- instead of k_mb_analyse's 512-thread, 78 KB LDS
+// workgroups followed by k_mb_intra8 -- so the two independent decisions share the CUs (eight
+// workgroups per CU): blocks [0, nRg) the intra roles (longest, first), then the Intra8x8 blocks.
+__global__ __launch_bounds__(NT, 8) void k_mb_intra(const TickArgs t) {
+    __shared__ union {
+        IntraS in[2];
+        I8S i8;
+    } s;
+    const int tot = t.pre[t.npic], nR = (tot + 1) / 2, nRg = xcd_grid(nR), b = blockIdx.x;
+    if (b < nRg) {
+        const int r = xcd_block(b, nR);
+        if (r >= nR) return;                                   // padding block (whole workgroup)
+        const int q = __builtin_amdgcn_readfirstlane(2 * r + (int)(threadIdx.x >> 7));
+        const bool act = q < tot;
+        const int e = tick_entry(t, act ? q : 0);
+        const DevParams d = tick_params(t, e);
+        const int mby = d.y_min + ((act ? q : t.pre[e]) - t.pre[e]), mbx = d.diag - 2 * mby;
+        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act, true);
+    } else {
+        const int mi = xcd_block(b - nRg, tot);
+        if (mi >= tot) return;
+        intra8_mb(t, s.i8, mi);
+    }
+}
+
+hipError_t jmh_launch_intra(const TickArgs &t, hipStream_t st) {
+    const int tot = t.pre[t.npic];
+    const int nblocks = xcd_grid((tot + 1) / 2) + (t.t8 ? xcd_grid(tot) : 0);
+    hipLaunchKernelGGL(k_mb_intra, dim3(nblocks), dim3(NT), 0, st, t);
+    return hipGetLastError();
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {

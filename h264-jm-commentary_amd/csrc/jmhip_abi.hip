@@ -22,6 +22,7 @@
 
 hipError_t jmh_launch_interp(const uint8_t *ref, int W, int H, uint8_t *qpel, int qstride, int qplane, hipStream_t st);
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_intra(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st);
@@ -472,10 +473,14 @@ static int issue_tick(jmh_ctx *c) {
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
         if (kt) HCHK(ring_begin(c->ring_an, c->st));
-        if (t.search_mode == 3) HCHK(jmh_launch_epzs(t, c->st));               // EPZS: one wave per MB
-        else if (!t.me_in_analyse) HCHK(jmh_launch_me_full(t, c->st));     // SearchMode -1
-        HCHK(jmh_launch_analyse(t, c->st));
-        if (t.t8) HCHK(jmh_launch_intra8(t, c->st));   // Intra8x8 decision (High profile)
+        if (t.me_in_analyse) {                          // FFS: motion search + intra in k_mb_analyse
+            HCHK(jmh_launch_analyse(t, c->st));
+            if (t.t8) HCHK(jmh_launch_intra8(t, c->st));   // Intra8x8 decision (High profile)
+        } else {                                        // EPZS (one wave per MB) / SearchMode -1
+            if (t.search_mode == 3) HCHK(jmh_launch_epzs(t, c->st));
+            else HCHK(jmh_launch_me_full(t, c->st));
+            HCHK(jmh_launch_intra(t, c->st));           // all intra decisions incl. Intra8x8
+        }
         if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
         HCHK(jmh_launch_final(t, c->st));
         if (kt) HCHK(ring_end(c->ring_fin, c->st));
