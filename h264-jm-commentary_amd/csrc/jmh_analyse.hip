@@ -363,26 +363,26 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
         const int step = pass == 0 ? 2 : 1;
         const int min_pos = pass == 0 ? (had ? 0 : 1) : 1;
         unsigned kb = 0xFFFFFFFFu;
-        if (lns <= 1) {   // 4x4 / 8x4 / 4x8: one row per lane, a quad per (candidate, 4x4 block)
-            const int row = lane & 3;
-            for (int t0 = 0; t0 < (9 << lns); t0 += 16) {
-                const int task = t0 + (lane >> 2), c = task >> lns, sub = task & (nsub - 1);
-                const bool val = c < 9 && c >= min_pos;
-                const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
-                int sat = 0;
-                if (c < 9) {   // quad-uniform
-                    const int bxs = q.bx4 + (sub & ((1 << lw4) - 1)), bys = q.by4 + (sub >> lw4);
-                    sat = pass == 0 ? quad_row_satd<true>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, row, had)
-                                    : quad_row_satd<false>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, row, had);
-                }
-                sat += dpp<0xB1>(sat);   // quad (the 4x4 block's rows), then the 8-lane pair of blocks
-                sat += dpp<0x4E>(sat);
-                if (lns) sat += dpp<0x141>(sat);
-                if (val && sub == 0 && row == 0) {
-                    int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
-                    if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
-                    kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
-                }
+        if (lns <= 1) {   // 4x4 / 8x4 / 4x8: a quad per candidate, one row per lane -- of both 4x4
+                          // sub-blocks for 8x4 / 4x8, so the nine candidates take one pass of the wave
+            const int row = lane & 3, c = lane >> 2;
+            const bool val = c < 9 && c >= min_pos;
+            const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+            int sat = 0;
+            if (c < 9) {   // quad-uniform
+                const int bxs1 = q.bx4 + lw4, bys1 = q.by4 + (lns - lw4);   // the second sub-block
+                sat = pass == 0 ? quad_row_satd<true>(s, wb0 + 4 * q.by4 * WST + 4 * q.bx4, 64 * q.by4 + 4 * q.bx4, ox, oy, row, had)
+                                : quad_row_satd<false>(s, wb0 + 4 * q.by4 * WST + 4 * q.bx4, 64 * q.by4 + 4 * q.bx4, ox, oy, row, had);
+                if (lns)
+                    sat += pass == 0 ? quad_row_satd<true>(s, wb0 + 4 * bys1 * WST + 4 * bxs1, 64 * bys1 + 4 * bxs1, ox, oy, row, had)
+                                     : quad_row_satd<false>(s, wb0 + 4 * bys1 * WST + 4 * bxs1, 64 * bys1 + 4 * bxs1, ox, oy, row, had);
+            }
+            sat += dpp<0xB1>(sat);   // the quad's rows
+            sat += dpp<0x4E>(sat);
+            if (val && row == 0) {
+                int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
+                if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
+                kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
             }
         } else {   // one lane per (candidate, 4x4 block), nsub-lane groups sum a candidate
             for (int t0 = 0; t0 < (9 << lns); t0 += 64) {

@@ -504,6 +504,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const int X0 = 4 * mbx, Y0 = 4 * mby, left = mbx > 0 ? mby * d.mbw + mbx - 1 : -1;
     const bool prof = d.prof && lane == 0 && d.prof_mb == mby * d.mbw + mbx;
+    const unsigned long long bt0 = t.bprof ? wall_clock64() : 0;   // debug (JMH_BLOCK_PROF): role 4
     if (prof) d.prof[32] = wall_clock64();
     // ---- inputs: the MB (one dword per lane), border cells, the temporal neighbourhood, the left
     //      MB's searches, the window (dword per task: two aligned global dwords + v_alignbyte
@@ -633,6 +634,11 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
         scr->skipy = (za || zl) ? 0 : pcy;
     }
     if (prof) d.prof[40] = wall_clock64();
+    if (t.bprof && lane == 0) {
+        t.bprof[3 * blockIdx.x] = bt0;
+        t.bprof[3 * blockIdx.x + 1] = wall_clock64();
+        t.bprof[3 * blockIdx.x + 2] = 4;
+    }
 }
 
 hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st) {

@@ -18,6 +18,7 @@
 #include <string.h>
 #include <deque>
 #include <vector>
+#include <algorithm>
 #include "jmh_device.h"
 
 hipError_t jmh_launch_interp(const uint8_t *ref, int W, int H, uint8_t *qpel, int qstride, int qplane, hipStream_t st);
@@ -465,7 +466,8 @@ static int issue_tick(jmh_ctx *c) {
     t.npic = k; t.nP = nP; t.pre[k] = mbs;
     if (c->d_bprof && c->ticks_total == c->bprof_tick) {
         t.bprof = c->d_bprof;
-        const int na = xcd_grid(t.me_in_analyse ? t.pre[nP] : 0) + (t.pre[k] + 3) / 4;
+        // the analysis blocks: k_mb_analyse's (roles 0 / 2), or the separate search kernel's (role 4)
+        const int na = t.me_in_analyse ? xcd_grid(t.pre[nP]) + (t.pre[k] + 3) / 4 : xcd_grid(t.pre[nP]);
         t.bprof_fin = c->d_bprof + 3 * na;
         HCHK(hipMemsetAsync(c->d_bprof, 0, ((size_t)3 * 3 * PMAX * c->mbh + 64) * sizeof(unsigned long long), c->st));
         c->bprof_blocks = na + xcd_grid(t.pre[k]);
@@ -736,21 +738,27 @@ int jmh_sync(jmh_ctx *c) {
         HCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->dev));
         double us = rate_khz > 0 ? 1e3 / rate_khz : 0.01;
         unsigned long long t0 = ~0ull, t1 = 0;
-        double sum[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0};
-        int n[4] = {0, 0, 0, 0};
+        double sum[5] = {0, 0, 0, 0, 0}, mx[5] = {0, 0, 0, 0, 0};
+        std::vector<double> durs[5];
+        int n[5] = {0, 0, 0, 0, 0};
         unsigned long long f0 = ~0ull, f1 = 0;
         for (int i = 0; i < c->bprof_blocks; i++) {
             unsigned long long a = h[3 * i], b = h[3 * i + 1];
             int role = (int)h[3 * i + 2];
-            if (!a || role < 0 || role > 3 || b < a) continue;   // 0: padding block, not written
+            if (!a || role < 0 || role > 4 || b < a) continue;   // 0: padding block, not written
             if (role == 3) { f0 = a < f0 ? a : f0; f1 = b > f1 ? b : f1; }
             t0 = a < t0 ? a : t0; t1 = b > t1 ? b : t1;
             double dur = (double)(b - a) * us;
             sum[role] += dur; n[role]++; mx[role] = dur > mx[role] ? dur : mx[role];
+            durs[role].push_back(dur);
         }
         fprintf(stderr, "jmh_blocks tick=%d blocks=%d span=%.1fus", c->bprof_tick, c->bprof_blocks, (double)(t1 - t0) * us);
-        for (int r = 0; r < 4; r++)
-            fprintf(stderr, " role%d: n=%d mean=%.1fus max=%.1fus", r, n[r], n[r] ? sum[r] / n[r] : 0.0, mx[r]);
+        for (int r = 0; r < 5; r++)
+            if (n[r]) {
+                std::sort(durs[r].begin(), durs[r].end());
+                fprintf(stderr, " role%d: n=%d mean=%.1fus p50=%.1f p90=%.1f max=%.1fus", r, n[r], sum[r] / n[r], durs[r][n[r] / 2],
+                        durs[r][(9 * n[r]) / 10], mx[r]);
+            }
         if (f1) fprintf(stderr, " final: first start %.1fus after the analysis' first, span %.1fus", (double)(f0 - t0) * us, (double)(f1 - f0) * us);
         fprintf(stderr, "\n");
         c->bprof_blocks = 0;
