@@ -384,28 +384,28 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
                 if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
                 kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
             }
-        } else {   // one lane per (candidate, 4x4 block), nsub-lane groups sum a candidate
-            for (int t0 = 0; t0 < (9 << lns); t0 += 64) {
-                const int task = t0 + lane, c = task >> lns, sub = task & (nsub - 1);
-                const bool val = c < 9 && c >= min_pos;
-                const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
-                int sat = 0;
-                if (val) {
+        } else {   // 8x8 and larger: a quad per candidate, lane g of it takes the 4x4 sub-blocks
+                   // g * spl .. g * spl + spl - 1 (spl = nsub / 4), so one pass of the wave
+            const int g = lane & 3, c = lane >> 2, lspl = lns - 2;
+            const bool val = c < 9 && c >= min_pos;
+            const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
+            int sat = 0;
+            if (val) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (k >= (1 << lspl)) break;
+                    const int sub = (g << lspl) + k;
                     const int bxs = q.bx4 + (sub & ((1 << lw4) - 1)), bys = q.by4 + (sub >> lw4);
-                    sat = pass == 0 ? subblock_satd<true>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had)
-                                    : subblock_satd<false>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had);
+                    sat += pass == 0 ? subblock_satd<true>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had)
+                                     : subblock_satd<false>(s, wb0 + 4 * bys * WST + 4 * bxs, 64 * bys + 4 * bxs, ox, oy, had);
                 }
-                // sum over the aligned nsub-lane group (4, 8 or 16) by DPP: lane ^ 1, ^ 2 (quad
-                // permutes), then mirror within 8 and within 16 lanes (each pairs the group's halves)
-                sat += dpp<0xB1>(sat);
-                sat += dpp<0x4E>(sat);
-                if (nsub >= 8) sat += dpp<0x141>(sat);
-                if (nsub >= 16) sat += dpp<0x140>(sat);
-                if (val && sub == 0) {
-                    int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
-                    if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
-                    kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
-                }
+            }
+            sat += dpp<0xB1>(sat);   // the quad
+            sat += dpp<0x4E>(sat);
+            if (val && g == 0) {
+                int cost = sat + (int)__umul24(lam, mvbits(4 * fmx + ox - pmvx) + mvbits(4 * fmy + oy - pmvy));
+                if (pass == 0 && check0 && c == 0) cost -= 16 * lam;
+                kb = min(kb, ((unsigned)(cost + KOFF) << 4) | (unsigned)c);
             }
         }
         kb = wave_min_u32(kb);
