@@ -215,6 +215,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     }
     long jseq = 0, jflushed = 0;   /* jobs submitted / emitted (picture order) */
     double copy_ms = 0, write_ms = 0;
+    double read_ms = 0, push_ms = 0, pop_ms = 0, flush_ms = 0;   /* main thread, for the summary */
     jm_bits out, rbsp;
     jm_bits_init(&out); jm_bits_init(&rbsp);
     jm_write_sps(&rbsp, &s); jm_write_nal(&out, 3, 7, &rbsp); jm_bits_free(&rbsp);
@@ -237,6 +238,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     #define FLUSH_JOB(J)                                                                           \
     do {                                                                                           \
         wjob_t *fj_ = (J);                                                                          \
+        double tf_ = now_ms();                                                                      \
         pool_wait(&pool, (int)(fj_ - pool.jobs));                                                   \
         if (fj_->status) { st_ret = fj_->status; break; }                                           \
         fwrite(fj_->out.buf, 1, fj_->out.len, fout);                                                 \
@@ -252,6 +254,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
                     fj_->write_ms + fj_->met, fj_->met);                                              \
         fj_->state = 0;                                                                             \
         jflushed++;                                                                                \
+        flush_ms += now_ms() - tf_;                                                                 \
     } while (0)
     /* hand a popped picture to the writer pool: its results and deblocked picture into a job */
     #define SUBMIT(P, MET_MS)                                                                      \
@@ -319,6 +322,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
             double met = now_ms() - t0;
             if (r) { fprintf(stderr, "hot path backend '%s' failed: status %d\n", be->name, r); st_ret = r; break; }
             st->me_tq_ms += met;
+            pop_ms += met;
             EMIT(&pend[head], met);
             if (st_ret) break;
             head = (head + 1) % plen;
@@ -326,8 +330,10 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         }
         pend_t *p = &pend[(head + count) % plen];
         int idx = inp->start_frame + f;
+        double tr = now_ms();
         if (synthetic) jm_synth_frame(&p->cur, inp->width, inp->height, seed, idx);
         else if (jm_read_yuv_frame(fin, &p->cur, inp->width, inp->height, idx)) { fprintf(stderr, "ReadOneFrame: cannot read frame %d\n", idx); st_ret = JMH_E_INVALID_ARG; break; }
+        read_ms += now_ms() - tr;
         p->f = f;
         p->is_i = f == 0 || (inp->intra_period && f % inp->intra_period == 0);
         p->frame_num = frame_num++;
@@ -350,6 +356,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         double met = now_ms() - t0;
         if (r) { fprintf(stderr, "hot path backend '%s' failed: status %d\n", be->name, r); st_ret = r; break; }
         st->me_tq_ms += met;
+        push_ms += met;
         if (pipelined) count++;
         else EMIT(p, met);
     }
@@ -399,6 +406,9 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         fprintf(log, " Host per picture: slice writing + PSNR %.2f ms (%s), results + readback (+ host deblocking) %.2f ms, wall %.2f ms\n",
                 st->entropy_ms / st->frames, nwr ? "writer threads" : "main thread", st->deblock_ms / st->frames,
                 st->total_ms / st->frames);
+    if (log && st->frames)
+        fprintf(log, " Main thread per picture: read %.2f ms, push %.2f, pop (wait) %.2f, results to writer %.2f, flush %.2f\n",
+                read_ms / st->frames, push_ms / st->frames, pop_ms / st->frames, copy_ms / st->frames, flush_ms / st->frames);
     jm_bits_free(&out);
     free(res);
     for (int k = 0; k < plen; k++) jm_pic_free(&pend[k].cur);

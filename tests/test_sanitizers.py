@@ -5,6 +5,7 @@ encoder loop with its writer threads, the JM 8.6 call surface) and the spec deco
 the closed-loop configurations.  Any report aborts the process, so a clean exit plus the
 closed-loop equality (decoder output == encoder reconstruction) is the check.  GPU-side ASan is
 not available on this pool; the device code is covered by the parity tests instead."""
+import fcntl
 import os
 import subprocess
 import tempfile
@@ -31,7 +32,10 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=86
 
 @pytest.fixture(scope="module")
 def sanitized():
-    r = subprocess.run(["make", "-s", "-C", ORACLE, "sanitize"], capture_output=True, text=True)
+    # one build at a time (pytest-xdist workers each run this fixture)
+    with open(os.path.join(ORACLE, ".sanitize.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", ORACLE, "sanitize"], capture_output=True, text=True)
     if r.returncode != 0:
         pytest.fail("sanitizer build failed:\n" + r.stdout + r.stderr)
     return LENCOD_ASAN, JMDEC_ASAN
