@@ -41,12 +41,18 @@ void jm_pad_picture(jm_pic *p, int dw, int dh) {
 int jm_read_yuv_frame(FILE *f, jm_pic *p, int dw, int dh, int index) {
     long fs = (long)dw * dh * 3 / 2;
     if (fseek(f, fs * index, SEEK_SET)) return -1;
-    for (int y = 0; y < dh; y++)
-        if (fread(p->y + (size_t)y * p->w, 1, dw, f) != (size_t)dw) return -1;
-    for (int y = 0; y < dh / 2; y++)
-        if (fread(p->u + (size_t)y * (p->w / 2), 1, dw / 2, f) != (size_t)(dw / 2)) return -1;
-    for (int y = 0; y < dh / 2; y++)
-        if (fread(p->v + (size_t)y * (p->w / 2), 1, dw / 2, f) != (size_t)(dw / 2)) return -1;
+    if (p->w == dw) {   /* rows contiguous in the planes: one read per plane (no stdio buffering) */
+        if (fread(p->y, 1, (size_t)dw * dh, f) != (size_t)dw * dh) return -1;
+        if (fread(p->u, 1, (size_t)(dw / 2) * (dh / 2), f) != (size_t)(dw / 2) * (dh / 2)) return -1;
+        if (fread(p->v, 1, (size_t)(dw / 2) * (dh / 2), f) != (size_t)(dw / 2) * (dh / 2)) return -1;
+    } else {
+        for (int y = 0; y < dh; y++)
+            if (fread(p->y + (size_t)y * p->w, 1, dw, f) != (size_t)dw) return -1;
+        for (int y = 0; y < dh / 2; y++)
+            if (fread(p->u + (size_t)y * (p->w / 2), 1, dw / 2, f) != (size_t)(dw / 2)) return -1;
+        for (int y = 0; y < dh / 2; y++)
+            if (fread(p->v + (size_t)y * (p->w / 2), 1, dw / 2, f) != (size_t)(dw / 2)) return -1;
+    }
     jm_pad_picture(p, dw, dh);
     return 0;
 }
