@@ -1,11 +1,15 @@
 // jmh_analyse.hip — k_mb_analyse: the decision half of encode_one_macroblock [J] (RDO off) for
-// every macroblock of one wavefront diagonal, split over three 512-thread workgroups per MB
-// that run concurrently on different CUs:
+// every macroblock of one wavefront tick (SearchMode 0, fast full search), on 512-thread
+// workgroups of two kinds:
 //
-//   role 2  P8x8 motion search: 4 x (8x8, 2x 8x4, 2x 4x8, 4x 4x4) = 36 BlockMotionSearch calls
-//   role 1  16x16, 16x8, 8x16 motion search (5 calls) + FindSkipModeMotionVector, then the
-//           Intra16x16 and chroma intra-mode decisions (I slices: only the latter)
-//   role 0  Intra4x4 decision with its reconstruction: four MBs per workgroup, two waves each
+//   motion search (one per P macroblock): all 41 BlockMotionSearch calls -- 16x16, 16x8, 8x16 and
+//           the P8x8 sub-modes of the four 8x8 blocks -- plus FindSkipModeMotionVector, with the
+//           MB's Intra4x4 decision on waves 6 and 7 between the search stages (intra_slot)
+//   intra (four MBs per workgroup, 128 threads each): Intra16x16 and chroma intra-mode decisions,
+//           and Intra4x4 for MBs without a motion-search workgroup (I pictures)
+//
+// k_mb_intra (end of file) runs the intra decisions for ticks whose search has its own kernel
+// (SearchMode -1: k_mb_me_full, 3: k_mb_epzs).
 //
 // JM runs the 41 searches of a P macroblock one after another. The only coupling between them is
 // the motion vector predictor, which reads MVs already stored inside the MB. Enumerating those
@@ -13,23 +17,24 @@
 // 16x8 / 8x16 search reads only MB neighbours and the same partition type's earlier block; a
 // P8x8 sub-mode search in 8x8 block b8 reads MB neighbours, the final (best sub-mode) MVs of the
 // 8x8 blocks before b8 and the same sub-mode's earlier blocks in b8. So the 41 searches form 16
-// dependent stages, each a set of independent searches evaluated together, with results
-// identical to JM's sequential order. Per-mode MV arrays provide the exact neighbour view.
-// Likewise the 16 Intra4x4 blocks only read blocks on earlier (x4 + 2*y4) diagonals, so they run
-// as 10 steps of up to two blocks (one wave each) with JM's results.
+// dependent stages (the 16x16-type searches inside block 0's first two), each a set of
+// independent searches evaluated together, with results identical to JM's sequential order.
+// Per-mode MV arrays provide the exact neighbour view. Likewise the 16 Intra4x4 blocks only read
+// blocks on earlier (x4 + 2*y4) diagonals, so they run as 10 steps of up to two blocks.
 //
-// Motion search data path per ME workgroup:
+// Motion search data path per workgroup:
 //   * 88x88 reference window (+4 margin for the 6-tap filter) and its b, h, j half-pel planes in
 //     LDS, computed once per MB (SubPelBlockMotionSearch reads only LDS);
-//   * SetupFastFullPelSearch's SADs of every integer position in REGISTERS, only those the role's
-//     next searches read: each thread owns a column strip of NPK positions and keeps 2 packed u16
-//     pairs per position -- role 1 the four 8x8 SADs (16x16 / 16x8 / 8x16 are sums of them), role
-//     2 the four 4x4 SADs of the 8x8 block it is searching (recomputed per 8x8 block).  Any
+//   * SetupFastFullPelSearch's SADs of every integer position in REGISTERS, only those the next
+//     searches read: each thread owns a column strip of NPK positions and keeps 2 packed u16 pairs
+//     per position -- first the four 8x8 SADs (16x16 / 16x8 / 8x16 are sums of them; kept in LDS
+//     for block 0's stages), then per 8x8 block its four 4x4 SADs (recomputed per block).  Any
 //     partition reduces with plain 32-bit adds of packed pairs (no carries: a half never exceeds
-//     2 x 16320).  The small table keeps the workgroup under 128 VGPRs (two per CU);
-//   * cost = SAD + lambda*(mvbits(x) + mvbits(y)) from two per-search LDS tables, key =
+//     2 x 16320).  The small table keeps the workgroup at 128 VGPRs (two per CU);
+//   * cost = SAD + (lambda * mvbits)(x) + (lambda * mvbits)(y) from one u16 LDS table, key =
 //     cost << 13 | JM order (0 for the (0,0) pre-check, else spiral index + 1), DPP wave min;
-//   * sub-pel SATD: one 4x4 sub-block per 16-lane row, DPP Hadamard, LDS-atomic candidate sums.
+//   * sub-pel on one wave per search: a quad of lanes per candidate, DPP butterflies / packed
+//     int16 Hadamard, one wave minimum per half / quarter pass.
 #include "jmh_common.h"
 #include "jmh_intra8.h"
 

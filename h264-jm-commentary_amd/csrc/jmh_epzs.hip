@@ -541,7 +541,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     {
         // with off % 4 == 0 the window's dwords are aligned in the picture (pix_x % 16 == 0, wcx %
         // 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an outside
-        // dword is the replicated edge sample.  Batches of 8 loads per lane in flight.
+        // dword is the replicated edge sample.  Two batches of 32 loads per lane in flight.
         constexpr int ND4 = EST / 4, NB = 32;
         const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND4;
         if ((off & 3) == 0) {
