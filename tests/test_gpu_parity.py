@@ -207,6 +207,32 @@ def test_epzs_moving_sequence(qp):
                 transform_8x8_mode=1)
 
 
+def shear_seq(w, h, n, seed):
+    """Vertical bands moving in opposite directions (+30 / -30 px horizontally, +-20 vertically):
+    sub-block MVPs at the band edges differ from the macroblock's 16x16 MVP by ~60 px, so EPZS
+    candidates and sub-pel neighbourhoods leave k_mb_epzs's LDS window (the global-memory path)."""
+    rng = np.random.default_rng(seed)
+    big = rand_picture(rng, w + 64 * n + 128, h + 48 * n + 128)[0]
+    pics = []
+    for i in range(n):
+        y = np.empty((h, w), np.uint8)
+        for b0 in range(0, w, 24):
+            sgn = 1 if (b0 // 24) % 2 == 0 else -1
+            x0, y0 = 64 + 32 * n + sgn * 30 * i + b0, 64 + 24 * n + sgn * 20 * i
+            y[:, b0:b0 + 24] = big[y0:y0 + h, x0:x0 + min(24, w - b0)]
+        y = np.clip(y.astype(np.int16) + rng.integers(-4, 5, y.shape), 0, 255).astype(np.uint8)
+        pics.append((np.ascontiguousarray(y), np.ascontiguousarray(y[::2, ::2] // 2 + 40), np.ascontiguousarray(255 - y[1::2, 1::2])))
+    return pics
+
+
+@pytest.mark.parametrize("t8", [0, 1])
+def test_epzs_window_misses(t8):
+    """EPZS with motion that leaves the 120x120 LDS window (opposite shears): GPU == oracle."""
+    pics = shear_seq(176, 144, 4, seed=51)
+    encode_pair(176, 144, pics, [jmhip.JMH_I_SLICE] + [jmhip.JMH_P_SLICE] * 3, 26, search_range=32, search_mode=3,
+                transform_8x8_mode=t8)
+
+
 def test_config3_width_3840_epzs():
     """Config 3 at its real width (3840, as 3840x2160 in the bench): High profile, EPZS + 8x8
     transform, SR 32, an I picture and two P pictures under large motion and with the temporal
