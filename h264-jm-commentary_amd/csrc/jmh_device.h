@@ -48,6 +48,7 @@ struct DevParams {
     int isr;                    // InterSearch16x16..4x4 as bits 1..7 (a mask: a per-thread array
                                 // indexed at run time would put the whole DevParams in scratch)
     int t8;                     // Transform8x8Mode (High profile)
+    int epzs_dual;              // EPZSDualRefinement (SearchMode 3)
     const uint8_t *orgY, *orgU, *orgV;
     const uint8_t *refY, *refU, *refV;
     uint8_t *recY, *recU, *recV;
@@ -94,6 +95,7 @@ struct TickArgs {
     int me_in_analyse;                   // 1: k_mb_analyse runs the FFS searches; 0: k_mb_me_full did
                                          //   (full search, SearchMode -1, or EPZS, SearchMode 3)
     int t8;                              // Transform8x8Mode: k_mb_intra8 ran, k_mb_final decides 4x4 / 8x8
+    int epzs_dual;                       // EPZSDualRefinement (k_mb_epzs)
     const uint32_t *ordtab;              // FFS order keys, [NPK / 2][NTA] packed pairs (jmh_create)
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
@@ -127,6 +129,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
 #pragma unroll
     for (int i = 1; i < 8; i++) d.isr |= (t.inter_search[i] != 0) << i;
     d.t8 = t.t8;
+    d.epzs_dual = t.epzs_dual;
     const int ls = t.W * t.H, lc = ls >> 2;
     d.orgY = q.org; d.orgU = q.org + ls; d.orgV = q.org + ls + lc;
     d.refY = q.ref; d.refU = q.ref + ls; d.refV = q.ref + ls + lc;

@@ -330,25 +330,41 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, const EW
             const int steps = sd ? 4 : 2;
             const int dia = lane < 41 ? (int)c_dia41[lane] : 0x44;
             const int ddx = (dia & 15) - 4, ddy = (dia >> 4) - 4;
-            for (bool done = false; !done;) {
-                const int x = bx + ddx, y = by + ddy;
-                const bool inw = lane < 41 && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
-                int c = 0;
-                if (inw) c = (int)lane_block_sad<LW4, LH4>(s, wn, bx4, by4, x, y) + (int)__umul24(lam, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
-                for (int k = 0; k < steps; k++) {
-                    const int rx = x - bx, ry = y - by;   // this lane's position relative to the current best
-                    int e = 15;
-                    if (sd) { if (abs(rx) <= 1 && abs(ry) <= 1) e = (int)((0xf3f2f1f0full >> (4 * ((ry + 1) * 3 + rx + 1))) & 15); }
-                    else if (abs(rx) <= 2 && abs(ry) <= 2) {
-                        const int i = (ry + 2) * 5 + rx + 2;
-                        e = (int)((i < 16 ? 0xf4af93f281fff0ffull >> (4 * i) : 0xff7fff6b5ull >> (4 * (i - 16))) & 15);
+            auto refine = [&](int &rbx, int &rby, int &rcost) {
+                for (bool done = false; !done;) {
+                    const int x = rbx + ddx, y = rby + ddy;
+                    const bool inw = lane < 41 && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
+                    int c = 0;
+                    if (inw) c = (int)lane_block_sad<LW4, LH4>(s, wn, bx4, by4, x, y) + (int)__umul24(lam, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+                    for (int k = 0; k < steps; k++) {
+                        const int rx = x - rbx, ry = y - rby;   // this lane's position relative to the current best
+                        int e = 15;
+                        if (sd) { if (abs(rx) <= 1 && abs(ry) <= 1) e = (int)((0xf3f2f1f0full >> (4 * ((ry + 1) * 3 + rx + 1))) & 15); }
+                        else if (abs(rx) <= 2 && abs(ry) <= 2) {
+                            const int i = (ry + 2) * 5 + rx + 2;
+                            e = (int)((i < 16 ? 0xf4af93f281fff0ffull >> (4 * i) : 0xff7fff6b5ull >> (4 * (i - 16))) & 15);
+                        }
+                        const unsigned m = wave_min_u32(inw && e != 15 ? ((unsigned)c << 6) | (unsigned)e : 0xFFFFFFFFu);
+                        if (m == 0xFFFFFFFFu || (int)(m >> 6) >= rcost) { done = true; break; }
+                        rcost = (int)(m >> 6);
+                        int px, py;
+                        epzs_pat(sd, (int)(m & 63), px, py);
+                        rbx += px; rby += py;
                     }
-                    const unsigned m = wave_min_u32(inw && e != 15 ? ((unsigned)c << 6) | (unsigned)e : 0xFFFFFFFFu);
-                    if (m == 0xFFFFFFFFu || (int)(m >> 6) >= min_mcost) { done = true; break; }
-                    min_mcost = (int)(m >> 6);
-                    int px, py;
-                    epzs_pat(sd, (int)(m & 63), px, py);
-                    bx += px; by += py;
+                }
+            };
+            const int pbx = bx, pby = by;                  // the best predictor
+            refine(bx, by, min_mcost);
+            if (d.epzs_dual) {
+                // EPZSDualRefinement (item 46): the runner-up predictor -- the cheapest other lane,
+                // lowest index on ties -- refined the same way; it wins only if strictly cheaper
+                const unsigned m1 = wave_min_u32(cv && (unsigned)lane != (m0 & 63) ? ((unsigned)c0 << 6) | (unsigned)lane : 0xFFFFFFFFu);
+                if (m1 != 0xFFFFFFFFu) {
+                    int x2 = __builtin_amdgcn_readlane(cx, m1 & 63), y2 = __builtin_amdgcn_readlane(cy, m1 & 63), c2 = (int)(m1 >> 6);
+                    if (x2 != pbx || y2 != pby) {
+                        refine(x2, y2, c2);
+                        if (c2 < min_mcost) { min_mcost = c2; bx = x2; by = y2; }
+                    }
                 }
             }
         }

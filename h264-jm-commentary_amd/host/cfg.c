@@ -67,6 +67,8 @@ static const map_entry Map[] = {
     {"QOffsetInter", 0, OFF(qoff_inter), -1, JMH_QOFFSET_MAX},
     {"AdaptiveRounding", 0, OFF(adaptive_rounding), 0, 1},
     {"OffsetMatrixPresentFlag", 0, OFF(offset_matrix_present), 0, 1},
+    {"EPZSDualRefinement", 0, OFF(epzs_dual), 0, 4},
+    {"EPZSSubPelME", 0, OFF(epzs_subpel), 0, 1},
     {NULL, 0, 0, 0, 0}};
 #undef OFF
 
@@ -176,6 +178,8 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->transform_8x8_mode && inp->profile_idc < 100) { snprintf(err, errlen, "Transform8x8Mode=1 requires ProfileIDC=100 (High)"); return -1; }
     if ((inp->width & 1) || (inp->height & 1)) { snprintf(err, errlen, "Source size must be even"); return -1; }
     if (inp->jm_version == 9) { snprintf(err, errlen, "JMVersion=9 not supported (8 or >= 10)"); return -1; }
+    if (inp->epzs_dual > 1) { snprintf(err, errlen, "EPZSDualRefinement=%d not supported (0 or 1)", inp->epzs_dual); return -1; }
+    if (inp->epzs_subpel) { snprintf(err, errlen, "EPZSSubPelME=1 not supported (0: SubPelBlockMotionSearch)"); return -1; }
     if (inp->adaptive_rounding) { snprintf(err, errlen, "AdaptiveRounding=1 not supported (0)"); return -1; }
     if (inp->offset_matrix_present) { snprintf(err, errlen, "OffsetMatrixPresentFlag=1 not supported (flat lists: QOffsetIntra / QOffsetInter)"); return -1; }
     if (inp->jm_version < 10 && (inp->qoff_intra >= 0 || inp->qoff_inter >= 0)) { snprintf(err, errlen, "QOffsetIntra / QOffsetInter need JMVersion >= 10"); return -1; }
@@ -223,5 +227,6 @@ void jm_fill_config(const jm_input *inp, jmh_config *cfg) {
     cfg->pipeline_depth = inp->pipeline_depth;
     cfg->transform_8x8_mode = inp->transform_8x8_mode;
     cfg->jm_version = inp->jm_version;
+    cfg->epzs_dual_refinement = inp->epzs_dual;
     if (inp->jm_version >= 10) { cfg->quant_offset[0] = inp->qoff_intra; cfg->quant_offset[1] = inp->qoff_inter; }
 }

@@ -43,6 +43,8 @@ typedef struct jm_input {
     int  qoff_intra, qoff_inter;/* QOffsetIntra / QOffsetInter: flat OffsetMatrix entries at
                                   OffsetBits 11 (JMVersion >= 10; -1 = JM defaults 682 / 342) */
     int  adaptive_rounding;    /* AdaptiveRounding (must be 0)                                */
+    int  epzs_dual;            /* EPZSDualRefinement (0, 1; SearchMode 3)                      */
+    int  epzs_subpel;          /* EPZSSubPelME (must be 0)                                     */
     int  offset_matrix_present;/* OffsetMatrixPresentFlag (must be 0: flat lists only)         */
     int  level_idc;            /* LevelIDC                                                    */
     int  symbol_mode;          /* SymbolMode (0 = CAVLC)                                       */

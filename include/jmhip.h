@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 8
+#define JMH_ABI_VERSION 9
 #define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
 #define JMH_QOFFSET_MAX 2047  /* jmh_config.quant_offset: OffsetBits 11 (1 << 11 = a whole step)    */
 
@@ -101,7 +101,8 @@ typedef struct jmh_config {
     int32_t quant_offset[2];        /* JMVersion >= 10: flat OffsetMatrix entries at OffsetBits 11 for
                                        [0] I slices, [1] P slices, 0..JMH_QOFFSET_MAX (JM defaults
                                        682, 342: Offset_intra_default_intra / _inter) [J]          */
-    int32_t reserved[1];
+    int32_t epzs_dual_refinement;   /* EPZSDualRefinement (SearchMode 3): 0 off, 1 refine the runner-up
+                                       predictor too (docs/JM_SEMANTICS.md item 46)                 */
 } jmh_config;
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */

@@ -316,32 +316,48 @@ static int epzs_predictors(const mbs *s, int bt, int bx4, int by4, int range, in
     return n;
 }
 
+/* pattern refinement (item 37/38) from (bx, by) at cost *mc: small or extended diamond around the
+ * current best, strict '<' in pattern order, move and repeat until no point improves */
+static void epzs_refine(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, int range, int c0x, int c0y, int sd,
+                        int *bx, int *by, int *mc) {
+    const int (*pat)[2] = sd ? epzs_sd : epzs_ed;
+    int np = sd ? 4 : 12;
+    for (;;) {
+        int bi = -1, nbx = *bx, nby = *by;
+        for (int i = 0; i < np; i++) {
+            int mx = *bx + pat[i][0], my = *by + pat[i][1];
+            if (iabs(mx - c0x) > range || iabs(my - c0y) > range) continue;
+            int m = epzs_cost(s, bt, bx4, by4, mx, my, pmvx, pmvy);
+            if (m < *mc) { *mc = m; bi = i; nbx = mx; nby = my; }
+        }
+        if (bi < 0) break;
+        *bx = nbx; *by = nby;
+    }
+}
+
 static int epzs_search(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, int range, int *mvx, int *mvy) {
     int c0x = *mvx, c0y = *mvy;
     int med = jmo_blc_size[bt][0] * jmo_blc_size[bt][1];  /* medthres: EPZSMedThresScale 1 */
     int cand[41][2], ok[41];
     int n = epzs_predictors(s, bt, bx4, by4, range, c0x, c0y, cand, ok);
     int min_mcost = epzs_cost(s, bt, bx4, by4, c0x, c0y, pmvx, pmvy), bx = c0x, by = c0y;
+    /* the runner-up predictor (EPZSDualRefinement, item 46): the cheapest of the others,
+     * earliest first on ties -- what a scan keeping best and second best ends with */
+    int m2 = 0x7FFFFFFF, x2 = 0, y2 = 0;
     if (min_mcost >= med) {
         for (int i = 1; i < n; i++) {                       /* predictors in order, strict '<' */
             if (!ok[i] || iabs(cand[i][0] - c0x) > range || iabs(cand[i][1] - c0y) > range) continue;
             int mc = epzs_cost(s, bt, bx4, by4, cand[i][0], cand[i][1], pmvx, pmvy);
-            if (mc < min_mcost) { min_mcost = mc; bx = cand[i][0]; by = cand[i][1]; }
+            if (mc < min_mcost) { m2 = min_mcost; x2 = bx; y2 = by; min_mcost = mc; bx = cand[i][0]; by = cand[i][1]; }
+            else if (mc < m2) { m2 = mc; x2 = cand[i][0]; y2 = cand[i][1]; }
         }
         if (min_mcost >= med) {                             /* pattern refinement          */
             int sd = min_mcost < med + ((3 * med) >> 1);
-            const int (*pat)[2] = sd ? epzs_sd : epzs_ed;
-            int np = sd ? 4 : 12;
-            for (;;) {
-                int bi = -1, nbx = bx, nby = by;
-                for (int i = 0; i < np; i++) {
-                    int mx = bx + pat[i][0], my = by + pat[i][1];
-                    if (iabs(mx - c0x) > range || iabs(my - c0y) > range) continue;
-                    int mc = epzs_cost(s, bt, bx4, by4, mx, my, pmvx, pmvy);
-                    if (mc < min_mcost) { min_mcost = mc; bi = i; nbx = mx; nby = my; }
-                }
-                if (bi < 0) break;
-                bx = nbx; by = nby;
+            int pbx = bx, pby = by;
+            epzs_refine(s, bt, bx4, by4, pmvx, pmvy, range, c0x, c0y, sd, &bx, &by, &min_mcost);
+            if (s->c->cfg.epzs_dual_refinement && m2 != 0x7FFFFFFF && (x2 != pbx || y2 != pby)) {
+                epzs_refine(s, bt, bx4, by4, pmvx, pmvy, range, c0x, c0y, sd, &x2, &y2, &m2);
+                if (m2 < min_mcost) { min_mcost = m2; bx = x2; by = y2; }
             }
         }
     }

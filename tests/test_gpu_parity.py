@@ -423,6 +423,8 @@ def run_lencod(binary, out_dir, extra):
      "JMVersion=10", "QPRemainingFrame=30"],
     ["InputFile=synthetic:26", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
      "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "JMVersion=10"],
+    ["InputFile=synthetic:27", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "JMVersion=10", "EPZSDualRefinement=1"],
 ])
 def test_lencod_bitstream_identical(extra):
     with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:

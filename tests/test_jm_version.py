@@ -155,3 +155,42 @@ def test_gpu_pictures_jm10(kw, qp):
     from test_gpu_parity import encode_pair, synth_seq
     pics = synth_seq(176, 144, 3, 41)
     encode_pair(176, 144, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], qp, jm_version=10, **kw)
+
+
+# ---------------- EPZSDualRefinement (item 46) ----------------
+DUAL_CASES = [
+    ["InputFile=synthetic:36", "FramesToBeEncoded=4", "SearchMode=3", "SearchRange=32", "EPZSDualRefinement=1"],
+    ["InputFile=synthetic:37", "FramesToBeEncoded=4", "SearchMode=3", "SearchRange=16", "ProfileIDC=100",
+     "Transform8x8Mode=1", "JMVersion=10", "EPZSDualRefinement=1", "QPRemainingFrame=34"],
+]
+
+
+@pytest.mark.parametrize("extra", DUAL_CASES, ids=["baseline", "high-jm10"])
+def test_closed_loop_epzs_dual(extra):
+    with tempfile.TemporaryDirectory() as d:
+        bs = encode(d, extra)
+        r = subprocess.run([JMDEC, f"{d}/a.264", f"{d}/dec.yuv"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/a.yuv", "rb").read()
+        plain = [e for e in extra if not e.startswith("EPZSDual")]
+        assert encode(d, plain, "b") != bs, "EPZSDualRefinement=1 did not change the bitstream"
+
+
+def test_epzs_knob_ranges():
+    r = run("-p", "SearchMode=3", "-p", "EPZSDualRefinement=2")
+    assert r.returncode != 0 and "EPZSDualRefinement" in r.stderr
+    r = run("-p", "SearchMode=3", "-p", "EPZSSubPelME=1")
+    assert r.returncode != 0 and "EPZSSubPelME" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw,qp", [
+    (dict(search_range=32), 28),
+    (dict(search_range=16, transform_8x8_mode=1, jm_version=10), 33),
+    (dict(search_range=32, restrict_search_range=0, use_hadamard=0), 24),
+])
+def test_gpu_epzs_dual(kw, qp):
+    from test_gpu_parity import encode_pair, moving_seq, shear_seq
+    for pics in (moving_seq(176, 144, 4, seed=61, step=(13, -7)), shear_seq(176, 144, 4, seed=62)):
+        encode_pair(176, 144, pics, [jmhip.JMH_I_SLICE] + [jmhip.JMH_P_SLICE] * 3, qp, search_mode=3, epzs_dual_refinement=1,
+                    **kw)
