@@ -671,10 +671,10 @@ int jmh_frame_pop(jmh_ctx *c) {
         return false;
     });
     if (r) return r;
-    // look-ahead: half a lag of ticks more before waiting, so the device keeps working while the
+    // look-ahead: a lag of ticks more before waiting, so the device keeps working while the
     // caller writes the popped picture and reads the next one (the next push then needs that many
     // fewer ticks to start its picture; results are unchanged: ticks only advance legal diagonals)
-    int ahead = PIPE_LAG / 2;
+    int ahead = PIPE_LAG;
     if ((r = issue_while(c, [c, &ahead] { return ahead-- > 0 && !c->fl.empty(); }))) return r;
     HCHK(hipEventSynchronize(c->ring[e].ev_done));
     c->popq.pop_front();
