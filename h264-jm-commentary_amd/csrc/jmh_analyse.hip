@@ -36,6 +36,9 @@
 //   * sub-pel on one wave per search: a quad of lanes per candidate, DPP butterflies / packed
 //     int16 Hadamard, one wave minimum per half / quarter pass.
 #include "jmh_common.h"
+#ifndef JMH_EXP
+#define JMH_EXP 0                             // tools/valu_split.sh builds variants without parts
+#endif
 #include "jmh_intra8.h"
 
 #define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
@@ -256,6 +259,9 @@ __device__ __forceinline__ uint32_t pack4(s16x2 lo, s16x2 hi) { return __builtin
 // HALF: a half-pel (or full-pel) position, whose sample is one plane's (A == B): B is not read
 template <bool HALF>
 __device__ __forceinline__ int subblock_satd(const MeS &s, int wbase, int obase, int ox, int oy, int had) {
+#if JMH_EXP & 1   // instruction-count experiment (tools/valu_split.sh): no sub-pel SATD
+    return 0;
+#endif
     const int off = qoff((oy & 3) * 4 + (ox & 3));
     const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
     const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
@@ -310,6 +316,9 @@ __device__ __forceinline__ int subblock_satd(const MeS &s, int wbase, int obase,
 // quad by DPP, the result is this row's share (the quad sum is the block's SATD)
 template <bool HALF>
 __device__ __forceinline__ int quad_row_satd(const MeS &s, int wbase, int obase, int ox, int oy, int row, int had) {
+#if JMH_EXP & 1
+    return 0;
+#endif
     const int off = qoff((oy & 3) * 4 + (ox & 3));
     const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
     const int oA = ((xa & 1) + 2 * (ya & 1)) * PLS + (ya >> 1) * WST + (xa >> 1);
@@ -532,6 +541,9 @@ __device__ __forceinline__ void eval_sad8(const MeS &s, const PosState &ps, int 
 // column at a time keeps the unrolled window rows (3 dwords each) within the register budget.
 template <bool EIGHT, int OX, int OY, int SLOT, int HI>
 __device__ __forceinline__ void sad_strip(const MeS &s, PosState &ps) {
+#if JMH_EXP & 4   // instruction-count experiment: no SAD strips
+    return;
+#endif
     const int wx = ps.dx + WM + OX;
     const uint32_t sel = wx & 3;
     const uint8_t *wb = s.planes + (ps.dy0 + WM + OY) * WST + (wx & ~3);
@@ -714,7 +726,11 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
     // the MB's Intra4x4 decision (10 diagonal steps, then the results) runs on waves 6 and 7
     // while the motion search's sub-pel waves work: slots 0..10 (intra_slot)
+#if JMH_EXP & 2   // instruction-count experiment: no Intra4x4 in the search workgroup
+    auto idle = [&](int, int) {};
+#else
     auto idle = [&](int k, int w) { intra_slot(d, s.in, scr, k, w, mbx, mby); };
+#endif
     for (int i = tid; i < MVB_LEN; i += NTA) s.mvc[i] = (uint16_t)__umul24(d.lambda_motion, mvbits(i - MVB_OFF));
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
