@@ -589,6 +589,13 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
     fence_state(ps);
     sad_strip<false, 4 * X, 4 * Y, 0, 0>(s, ps);        // the four 4x4 SADs of this 8x8 block
     if constexpr (B8 == 0) {
+        // block 0's 8x8 SAD = the sum of its 4x4 SADs, into the low half of the 8x8 table's first
+        // word (each thread reads only its own entries: no barrier)
+#pragma unroll
+        for (int k = 0; k < NPK; k++) {
+            const uint32_t a = ps.sadp[k][0], b = ps.sadp[k][1];
+            reinterpret_cast<uint16_t *>(&s.hs.sad8[k * NTA + tid])[0] = (uint16_t)((a & 0xFFFFu) + (a >> 16) + (b & 0xFFFFu) + (b >> 16));
+        }
         // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left + 16x16, 16x8 upper, 8x16 left
         const SDesc sd[7] = {{4, X, Y, B8, 0, 0, 0, 0},
                              {5, X, Y, B8, 5, X, Y + 1, 0},
@@ -787,8 +794,10 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         ps.dx = sact ? tid % side : 0;
         ps.dy0 = sact ? (tid / side) * NPK : 0;
         ps.scx = scx; ps.scy = scy;
-        sad_strip<true, 0, 0, 0, 0>(s, ps);   // the four 8x8 SADs (16x16 / 16x8 / 8x16 searches)
-        fence_state(ps);
+        // the 8x8 SADs of blocks 1..3 (16x16 / 16x8 / 8x16 searches); block 0's comes from its
+        // four 4x4 SADs at the start of p8x8_block<0> (one strip fewer)
+#pragma unroll
+        for (int k = 0; k < NPK; k++) ps.sadp[k][0] = 0;
         sad_strip<true, 8, 0, 0, 1>(s, ps);
         fence_state(ps);
         sad_strip<true, 0, 8, 1, 0>(s, ps);
