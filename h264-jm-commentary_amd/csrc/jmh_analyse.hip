@@ -577,25 +577,26 @@ __device__ __forceinline__ void sad_strip(const MeS &s, PosState &ps) {
 
 // one 8x8 block of P8x8: its 4x4 SADs, 4 stages (sub-modes 4..7 in parallel, then the 4x4
 // chain), then the P8x8 sub-mode decision for the block (its MVs are read through best8x8).
-// Block 0 also runs the 16x16 / 16x8 / 8x16 searches, which are independent of P8x8: the first
-// blocks of each type in its stage 0, the second ones in its stage 1 (on the 8x8 SADs in LDS).
-// Intra4x4 slots (waves 6, 7): stage 0 of block 0 has no free waves.
+// Every block leaves its 8x8 SAD (the sum of its 4x4 SADs) in the LDS 8x8 table, so block 3 also
+// runs the 16x16 / 16x8 / 8x16 searches, which are independent of P8x8: the first blocks of each
+// type in its stage 0, the second ones in its stage 1.  Intra4x4 slots 0..10 (waves 6, 7) run in
+// the stages of blocks 0..2 (block 3's stage 0 has no free waves).
 template <int B8, class IDLE>
 __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8, IDLE idle, int wave, int tid) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
-    constexpr int IS0 = B8 == 0 ? -1 : 2 * B8 + 1, IS1 = B8 == 0 ? 0 : 2 * B8 + 2;
-    constexpr int IS2 = B8 == 0 ? 1 : B8 == 3 ? 9 : -1, IS3 = B8 == 0 ? 2 : B8 == 3 ? 10 : -1;
+    constexpr int IS0 = B8 == 3 ? -1 : 4 * B8, IS1 = B8 == 3 ? -1 : 4 * B8 + 1;
+    constexpr int IS2 = B8 == 3 ? -1 : 4 * B8 + 2, IS3 = B8 >= 2 ? -1 : 4 * B8 + 3;
     const int sr = d.sr;
     fence_state(ps);
     sad_strip<false, 4 * X, 4 * Y, 0, 0>(s, ps);        // the four 4x4 SADs of this 8x8 block
-    if constexpr (B8 == 0) {
-        // block 0's 8x8 SAD = the sum of its 4x4 SADs, into the low half of the 8x8 table's first
-        // word (each thread reads only its own entries: no barrier)
+    // this block's 8x8 SAD into its 16-bit half of the 8x8 table entry (each thread reads only its
+    // own entries: no barrier)
 #pragma unroll
-        for (int k = 0; k < NPK; k++) {
-            const uint32_t a = ps.sadp[k][0], b = ps.sadp[k][1];
-            reinterpret_cast<uint16_t *>(&s.hs.sad8[k * NTA + tid])[0] = (uint16_t)((a & 0xFFFFu) + (a >> 16) + (b & 0xFFFFu) + (b >> 16));
-        }
+    for (int k = 0; k < NPK; k++) {
+        const uint32_t a = ps.sadp[k][0], b = ps.sadp[k][1];
+        reinterpret_cast<uint16_t *>(&s.hs.sad8[k * NTA + tid])[B8] = (uint16_t)((a & 0xFFFFu) + (a >> 16) + (b & 0xFFFFu) + (b >> 16));
+    }
+    if constexpr (B8 == 3) {
         // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left + 16x16, 16x8 upper, 8x16 left
         const SDesc sd[7] = {{4, X, Y, B8, 0, 0, 0, 0},
                              {5, X, Y, B8, 5, X, Y + 1, 0},
@@ -794,15 +795,8 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         ps.dx = sact ? tid % side : 0;
         ps.dy0 = sact ? (tid / side) * NPK : 0;
         ps.scx = scx; ps.scy = scy;
-        // the 8x8 SADs of blocks 1..3 (16x16 / 16x8 / 8x16 searches); block 0's comes from its
-        // four 4x4 SADs at the start of p8x8_block<0> (one strip fewer)
-#pragma unroll
-        for (int k = 0; k < NPK; k++) ps.sadp[k][0] = 0;
-        sad_strip<true, 8, 0, 0, 1>(s, ps);
-        fence_state(ps);
-        sad_strip<true, 0, 8, 1, 0>(s, ps);
-        fence_state(ps);
-        sad_strip<true, 8, 8, 1, 1>(s, ps);
+        // (the 8x8 SADs of the 16x16 / 16x8 / 8x16 searches come from each 8x8 block's 4x4 SADs,
+        // p8x8_block)
         PSTAMP(8);
         // JM order keys of the strip from the per-context table (first read in the first stage, so
         // the loads overlap the half-pel planes); the (0,0) pre-check position, order 0, depends on
@@ -878,9 +872,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         }
         __syncthreads();   // h1 is dead: its LDS holds the 8x8 SADs from here on
         PSTAMP(2);
-#pragma unroll
-        for (int k = 0; k < NPK; k++) s.hs.sad8[k * NTA + tid] = make_uint2(ps.sadp[k][0], ps.sadp[k][1]);
-        {   // ---- P8x8 (4 x 4 stages), the 16x16 / 16x8 / 8x16 searches inside block 0's stages 0, 1
+        {   // ---- P8x8 (4 x 4 stages), the 16x16 / 16x8 / 8x16 searches inside block 3's stages 0, 1
             int best8x8 = 0, cost8x8 = 0;
             p8x8_block<0>(d, s, ps, best8x8, cost8x8, idle, wave, tid);
             PSTAMP(3);
