@@ -651,8 +651,8 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
         const int c = s.motion_cost[mode][B8];
         if (c < mc8) { mc8 = c; bm = mode; }
     }
-    best8x8 |= bm << (4 * B8);
-    cost8x8 += mc8;
+    best8x8 = __builtin_amdgcn_readfirstlane(best8x8 | bm << (4 * B8));   // uniform: SGPRs
+    cost8x8 = __builtin_amdgcn_readfirstlane(cost8x8 + mc8);
 }
 
 // ======================================================================================
