@@ -5,6 +5,7 @@
 // or, with Transform8x8Mode, TransformDecision and dct_luma8x8 on one wave per 8x8 block, and the
 // outputs the next diagonal depends on (reconstruction, MVs, reference indices, intra modes).
 #include "jmh_common.h"
+#include <cstdlib>
 
 struct FinS {
     uint8_t org[256];
@@ -95,7 +96,10 @@ __device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int al
 }
 
 
-__global__ __launch_bounds__(NT, 8) void k_mb_final(const TickArgs t) {
+// OCC workgroups per CU: 8 (64 VGPRs, a few spilled) for ticks of more than 5 x 256 MBs (2160p,
+// one dispatch round), 5 (no spills, a shorter per-MB chain) for smaller ticks
+template <int OCC>
+__global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     __shared__ FinS s;
     const int tid = threadIdx.x;
     const unsigned long long bt0 = t.bprof_fin ? wall_clock64() : 0;
@@ -507,6 +511,9 @@ __global__ __launch_bounds__(NT, 8) void k_mb_final(const TickArgs t) {
 }
 
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st) {
-    hipLaunchKernelGGL(k_mb_final, dim3(xcd_grid(t.pre[t.npic])), dim3(NT), 0, st, t);
+    static const bool occ8 = getenv("JMH_FINAL_OCC8") != nullptr;   // A/B: the 8-per-CU build always
+    const int n = t.pre[t.npic];
+    if (occ8 || n > 5 * 256) hipLaunchKernelGGL(k_mb_final<8>, dim3(xcd_grid(n)), dim3(NT), 0, st, t);
+    else hipLaunchKernelGGL(k_mb_final<5>, dim3(xcd_grid(n)), dim3(NT), 0, st, t);
     return hipGetLastError();
 }

@@ -10,6 +10,7 @@
 #   smoke   __graft_entry__.smoke()                  -> gpurun_out/TAG_smoke.log
 #   bench   bench.py (defaults, with CPU baseline)   -> gpurun_out/TAG_bench.json
 #   bench20 bench.py --steps 20 --warmup 5 (the driver's invocation, no CPU baseline)
+#   benchf8 bench20 with JMH_FINAL_OCC8=1 (k_mb_final's 8-per-CU build for every tick: A/B)
 #   c3      bench.py --config 3 (with CPU baseline)  -> gpurun_out/TAG_c3_bench.json
 #   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
 #   profc3  the same for config 3
@@ -46,6 +47,8 @@ for s in "$@"; do
             cat gpurun_out/${TAG}_bench.json ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_bench20.json || exit $?
             cat gpurun_out/${TAG}_bench20.json ;;
+    benchf8) JMH_FINAL_OCC8=1 run benchf8 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_benchf8.json || exit $?
+            cat gpurun_out/${TAG}_benchf8.json ;;
     c3)     run c3 900 python bench.py --config 3 > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3_bench.err || exit $?
             cat gpurun_out/${TAG}_c3_bench.json ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}" -o ${TAG} --output-format csv -- \
