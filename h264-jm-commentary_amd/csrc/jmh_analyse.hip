@@ -107,7 +107,8 @@ __device__ __forceinline__ void sstamp(MeS &s, int wave) {
 // prefetch of the intra neighbourhood by threads t in [0, 96)
 __device__ __forceinline__ void load_intra_nb(const DevParams &d, IntraNb &nb, int t, int mbx, int mby) {
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, Wc = d.Wc;
-    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
+    const MbAvail mav = mb_avail(d, mbx, mby);
+    const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     if (t < 21) {                                  // luma row y = -1, x = -1..19
         const int x = t - 1;
         const bool av = x < 0 ? avTL : x < 16 ? avT : avTR;
@@ -981,7 +982,8 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratc
 __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act, bool i4) {
     const int wave = tid >> 6, lane = tid & 63;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
-    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
+    const MbAvail mav = mb_avail(d, mbx, mby);
+    const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     const bool prof = act && prof_mb_here(d, mbx, mby);
     PSTAMP(12);
     if (act) {
@@ -1030,7 +1032,8 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
 // k = 0..9: diagonal k of the 4x4 grid; slot 10: the totals and results.
 __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int mbx, int mby) {
     const int lane = threadIdx.x & 63;
-    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0, avTR = mby > 0 && mbx + 1 < d.mbw;
+    const MbAvail mav = mb_avail(d, mbx, mby);
+    const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     if (k < 10) {
         const int q_bits = 15 + d.qp / 6;
         const int qpk = q_round(d.qsel, q_bits);

@@ -317,7 +317,8 @@ __device__ __forceinline__ int border_cell(int xN, int yN) {   // -1: inside the
 __device__ __forceinline__ void load_border(const DevParams &d, Border &b, int t, int mbx, int mby) {
     const int W4 = d.W >> 2;
     int by4 = t < 6 ? -1 : t - 6, bx4 = t < 6 ? t - 1 : -1;
-    bool av = by4 < 0 ? (bx4 < 0 ? (mbx > 0 && mby > 0) : bx4 > 3 ? (mby > 0 && mbx + 1 < d.mbw) : mby > 0) : mbx > 0;
+    const MbAvail m = mb_avail(d, mbx, mby);
+    bool av = by4 < 0 ? (bx4 < 0 ? m.TL : bx4 > 3 ? m.TR : m.T) : m.L;
     int ref = -2, mx = 0, my = 0, ipm = -1;
     if (av) {
         int a = (4 * mby + by4) * W4 + 4 * mbx + bx4;

@@ -49,6 +49,7 @@ struct DevParams {
                                 // indexed at run time would put the whole DevParams in scratch)
     int t8;                     // Transform8x8Mode (High profile)
     int epzs_dual;              // EPZSDualRefinement (SearchMode 3)
+    int slice_mbs;              // SliceMode 1: MBs per slice (the whole picture for one slice)
     const uint8_t *orgY, *orgU, *orgV;
     const uint8_t *refY, *refU, *refV;
     uint8_t *recY, *recU, *recV;
@@ -68,6 +69,20 @@ struct DevParams {
     int qsel;                   // quantisation rounding selector of this slice (q_round, jmh_common.h)
     int diag, y_min;            // wavefront diagonal of this picture in the launch: mbx + 2*mby == diag
 };
+
+// Neighbour MB availability (6.4.8 / JM getNeighbour): inside the picture and in the current
+// slice.  Slices are runs of slice_mbs MBs in raster order and every neighbour precedes the MB,
+// so "same slice" is "address >= the slice's first MB".  One slice: the picture-edge rules.
+struct MbAvail { bool L, T, TL, TR; };
+__device__ __forceinline__ MbAvail mb_avail(const DevParams &d, int mbx, int mby) {
+    const int a = mby * d.mbw + mbx, first = a - a % d.slice_mbs;
+    MbAvail v;
+    v.L = mbx > 0 && a - 1 >= first;
+    v.T = mby > 0 && a - d.mbw >= first;
+    v.TL = mbx > 0 && mby > 0 && a - d.mbw - 1 >= first;
+    v.TR = mby > 0 && mbx + 1 < d.mbw && a - d.mbw + 1 >= first;
+    return v;
+}
 
 // One wavefront tick: the same diagonal step for up to PMAX pictures in flight, each on its own
 // diagonal (kernel argument, by value; ~2.4 KB).  Entries [0, nP) are P pictures.
@@ -96,6 +111,7 @@ struct TickArgs {
                                          //   (full search, SearchMode -1, or EPZS, SearchMode 3)
     int t8;                              // Transform8x8Mode: k_mb_intra8 ran, k_mb_final decides 4x4 / 8x8
     int epzs_dual;                       // EPZSDualRefinement (k_mb_epzs)
+    int slice_mbs;                       // SliceMode 1: MBs per slice (>= 1; mbw * mbh for one slice)
     const uint32_t *ordtab;              // FFS order keys, [NPK / 2][NTA] packed pairs (jmh_create)
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
@@ -130,6 +146,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     for (int i = 1; i < 8; i++) d.isr |= (t.inter_search[i] != 0) << i;
     d.t8 = t.t8;
     d.epzs_dual = t.epzs_dual;
+    d.slice_mbs = t.slice_mbs;
     const int ls = t.W * t.H, lc = ls >> 2;
     d.orgY = q.org; d.orgU = q.org + ls; d.orgV = q.org + ls + lc;
     d.refY = q.ref; d.refU = q.ref + ls; d.refV = q.ref + ls + lc;

@@ -518,7 +518,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, sr = d.sr;
     const int off = min(2 * sr + 4, EOFF_L), wdim = 16 + 2 * off;
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
-    const int X0 = 4 * mbx, Y0 = 4 * mby, left = mbx > 0 ? mby * d.mbw + mbx - 1 : -1;
+    const int X0 = 4 * mbx, Y0 = 4 * mby, left = mb_avail(d, mbx, mby).L ? mby * d.mbw + mbx - 1 : -1;
     const bool prof = d.prof && lane == 0 && d.prof_mb == mby * d.mbw + mbx;
     const unsigned long long bt0 = t.bprof ? wall_clock64() : 0;   // debug (JMH_BLOCK_PROF): role 4
     if (prof) d.prof[32] = wall_clock64();

@@ -112,7 +112,8 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     const int W = d.W, Wc = d.Wc, W4 = d.W >> 2;
     const int slice_p = d.slice_type == JMH_P_SLICE;
     const int qp = d.qp;
-    const bool avL = mbx > 0, avT = mby > 0, avTL = mbx > 0 && mby > 0;
+    const MbAvail mav = mb_avail(d, mbx, mby);
+    const bool avL = mav.L, avT = mav.T, avTL = mav.TL;
     const bool prof = prof_mb_here(d, mbx, mby);
     PSTAMP(16);
     const MbScratch *sc = d.scr + mby * d.mbw + mbx;

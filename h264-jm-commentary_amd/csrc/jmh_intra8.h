@@ -19,7 +19,8 @@ __device__ __forceinline__ void intra8_mb(const TickArgs &t, I8S &s, int mi) {
     const DevParams d = tick_params(t, e);
     const int mby = d.y_min + (mi - t.pre[e]), mbx = d.diag - 2 * mby;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, W4 = d.W >> 2;
-    const bool avL = mbx > 0, avT = mby > 0, avTL = avL && avT, avTR = avT && mbx + 1 < d.mbw;
+    const MbAvail mav = mb_avail(d, mbx, mby);
+    const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     const int lambda = d.lambda_mode, qp = d.qp, had = d.use_hadamard;
     const int q_bits = 16 + qp / 6;
     const int qp_const = q_round(d.qsel, q_bits);   // items 1, 45

@@ -282,6 +282,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version < 0 || cfg->jm_version == 9 || cfg->jm_version > 99) return JMH_E_UNSUPPORTED_CFG;   // 0 / 8: JM 8.6, 10..: JM >= 10
     if (cfg->epzs_dual_refinement != 0 && cfg->epzs_dual_refinement != 1) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->slice_mbs < 0) return JMH_E_INVALID_ARG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     int ndev = jmh_device_count();
@@ -439,6 +440,7 @@ static int issue_tick(jmh_ctx *c) {
     t.me_in_analyse = c->cfg.search_mode == 0;
     t.t8 = c->cfg.transform_8x8_mode;
     t.epzs_dual = c->cfg.epzs_dual_refinement;
+    t.slice_mbs = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : c->mbw * c->mbh;
     t.ordtab = c->d_ordtab;
     int act[PMAX], nact = 0, nP = 0;
     const int nf = (int)c->fl.size();

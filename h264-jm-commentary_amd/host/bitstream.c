@@ -414,7 +414,7 @@ jm_slice_writer *jm_slice_begin(jm_bits *b, const jm_seq *s, const jm_slice *sl)
     jm_slice_writer *sw = calloc(1, sizeof(*sw));
     if (!sw) return NULL;
     /* slice_header (7.3.3) */
-    jm_put_ue(b, 0);                                  /* first_mb_in_slice */
+    jm_put_ue(b, sl->first_mb);                       /* first_mb_in_slice */
     jm_put_ue(b, sl->slice_type);                     /* 0 = P, 2 = I            */
     jm_put_ue(b, 0);                                  /* pic_parameter_set_id    */
     jm_put(b, sl->frame_num & ((1 << s->log2_max_frame_num) - 1), s->log2_max_frame_num);

@@ -68,6 +68,8 @@ static const map_entry Map[] = {
     {"AdaptiveRounding", 0, OFF(adaptive_rounding), 0, 1},
     {"OffsetMatrixPresentFlag", 0, OFF(offset_matrix_present), 0, 1},
     {"EPZSDualRefinement", 0, OFF(epzs_dual), 0, 4},
+    {"SliceMode", 0, OFF(slice_mode), 0, 3},
+    {"SliceArgument", 0, OFF(slice_arg), 1, 1 << 20},
     {"EPZSSubPelME", 0, OFF(epzs_subpel), 0, 1},
     {NULL, 0, 0, 0, 0}};
 #undef OFF
@@ -92,6 +94,7 @@ void jm_input_defaults(jm_input *inp) {
     inp->writer_threads = 4;
     inp->jm_version = 8;
     inp->qoff_intra = inp->qoff_inter = -1;
+    inp->slice_arg = 50;                       /* encoder.cfg SliceArgument default [J] */
 }
 
 int jm_set_param(jm_input *inp, const char *key, const char *val, char *err, int errlen) {
@@ -179,6 +182,7 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if ((inp->width & 1) || (inp->height & 1)) { snprintf(err, errlen, "Source size must be even"); return -1; }
     if (inp->jm_version == 9) { snprintf(err, errlen, "JMVersion=9 not supported (8 or >= 10)"); return -1; }
     if (inp->epzs_dual > 1) { snprintf(err, errlen, "EPZSDualRefinement=%d not supported (0 or 1)", inp->epzs_dual); return -1; }
+    if (inp->slice_mode > 1) { snprintf(err, errlen, "SliceMode=%d not supported (0 or 1: SliceArgument macroblocks per slice)", inp->slice_mode); return -1; }
     if (inp->epzs_subpel) { snprintf(err, errlen, "EPZSSubPelME=1 not supported (0: SubPelBlockMotionSearch)"); return -1; }
     if (inp->adaptive_rounding) { snprintf(err, errlen, "AdaptiveRounding=1 not supported (0)"); return -1; }
     if (inp->offset_matrix_present) { snprintf(err, errlen, "OffsetMatrixPresentFlag=1 not supported (flat lists: QOffsetIntra / QOffsetInter)"); return -1; }
@@ -228,5 +232,6 @@ void jm_fill_config(const jm_input *inp, jmh_config *cfg) {
     cfg->transform_8x8_mode = inp->transform_8x8_mode;
     cfg->jm_version = inp->jm_version;
     cfg->epzs_dual_refinement = inp->epzs_dual;
+    cfg->slice_mbs = inp->slice_mode == 1 ? inp->slice_arg : 0;
     if (inp->jm_version >= 10) { cfg->quant_offset[0] = inp->qoff_intra; cfg->quant_offset[1] = inp->qoff_inter; }
 }

@@ -43,21 +43,40 @@ static double psnr(const uint8_t *a, int sa, const uint8_t *b, int sb, int w, in
     return 10.0 * log10(255.0 * 255.0 * w * h / (double)se);
 }
 
-/* slice.c › encode_one_slice [J]: the macroblock loop of one picture (one slice) through the JM
- * 8.6 call surface (host/jm86.c): start_macroblock, encode_one_macroblock, write_one_macroblock */
-static int encode_one_slice(jm86_img *im, const jm_seq *s, const jm_slice *sl, const jmh_frame_params *fp, const jm_pic *cur,
-                            const jm_pic *ref, jm_bits *rbsp) {
-    jm_slice_writer *w = jm_slice_begin(rbsp, s, sl);
-    if (!w) return JMH_E_OOM;
-    int r = jm86_start_picture(im, fp, cur, ref, w);
-    if (r) { jm_slice_end(w); return r; }
-    for (int a = 0; a < s->mbw * s->mbh; a++) {
+/* slice.c › encode_one_slice [J]: the macroblock loop of one slice through the JM 8.6 call
+ * surface (host/jm86.c): start_macroblock, encode_one_macroblock, write_one_macroblock.
+ * image.c › code_a_picture [J] calls it for every slice of the picture (SliceMode 1:
+ * SliceArgument MBs each, raster order); each slice is its own NAL unit, appended to out. */
+static int encode_one_slice(jm86_img *im, const jm_seq *s, const jm_slice *sl, jm_bits *out) {
+    const int nmb = s->mbw * s->mbh, end = s->slice_mbs > 0 && sl->first_mb + s->slice_mbs < nmb ? sl->first_mb + s->slice_mbs : nmb;
+    jm_bits rbsp;
+    jm_bits_init(&rbsp);
+    jm_slice_writer *w = jm_slice_begin(&rbsp, s, sl);
+    if (!w) { jm_bits_free(&rbsp); return JMH_E_OOM; }
+    im->writer = w;
+    im->slice_first = sl->first_mb;
+    for (int a = sl->first_mb; a < end; a++) {
         img->current_mb_nr = a;
         start_macroblock();
         encode_one_macroblock();
         write_one_macroblock();
     }
     jm_slice_end(w);
+    im->writer = NULL;
+    jm_write_nal(out, sl->idr ? 3 : 2, sl->idr ? 5 : 1, &rbsp);
+    jm_bits_free(&rbsp);
+    return JMH_OK;
+}
+static int encode_picture_slices(jm86_img *im, const jm_seq *s, const jm_slice *sl0, const jmh_frame_params *fp,
+                                 const jm_pic *cur, const jm_pic *ref, jm_bits *out) {
+    int r = jm86_start_picture(im, fp, cur, ref, NULL);
+    if (r) return r;
+    const int nmb = s->mbw * s->mbh, step = s->slice_mbs > 0 ? s->slice_mbs : nmb;
+    for (int first = 0; first < nmb; first += step) {
+        jm_slice sl = *sl0;
+        sl.first_mb = first;
+        if ((r = encode_one_slice(im, s, &sl, out))) return r;
+    }
     return JMH_OK;
 }
 
@@ -93,20 +112,16 @@ typedef struct wpool {
     int nth;
 } wpool_t;
 
-static int encode_one_slice(jm86_img *im, const jm_seq *s, const jm_slice *sl, const jmh_frame_params *fp, const jm_pic *cur,
-                            const jm_pic *ref, jm_bits *rbsp);
+static int encode_picture_slices(jm86_img *im, const jm_seq *s, const jm_slice *sl0, const jmh_frame_params *fp,
+                                 const jm_pic *cur, const jm_pic *ref, jm_bits *out);
 
 static void job_run(wpool_t *P, wjob_t *j) {
     const jm_seq *s = P->s;
     const jm_input *inp = P->inp;
     const int W = s->width;
     double t0 = now_ms();
-    jm_bits rbsp;
-    jm_bits_init(&rbsp);
-    j->status = encode_one_slice(&j->im, s, &j->sl, &j->fp, j->cur, &j->rec, &rbsp);
     j->out.len = 0;
-    if (!j->status) jm_write_nal(&j->out, j->sl.idr ? 3 : 2, j->sl.idr ? 5 : 1, &rbsp);
-    jm_bits_free(&rbsp);
+    j->status = encode_picture_slices(&j->im, s, &j->sl, &j->fp, j->cur, &j->rec, &j->out);
     j->pic_bits = j->out.len * 8;
     j->py = psnr(j->cur->y, W, j->rec.y, W, inp->width, inp->height);
     j->pu = psnr(j->cur->u, W / 2, j->rec.u, W / 2, inp->width / 2, inp->height / 2);
@@ -161,6 +176,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     s.log2_max_frame_num = 8; s.log2_max_poc_lsb = 8;
     s.chroma_qp_offset = inp->chroma_qp_offset;
     s.lf_params_flag = inp->lf_params_flag; s.lf_disable = inp->lf_disable;
+    s.slice_mbs = inp->slice_mode == 1 ? inp->slice_arg : 0;
     s.lf_alpha = inp->lf_alpha; s.lf_beta = inp->lf_beta;
     s.constrained_intra = inp->constrained_intra;
     s.transform_8x8_mode = inp->transform_8x8_mode;
@@ -272,7 +288,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         st->deblock_ms += now_ms() - t1;                                                           \
         j_->cur = &p_->cur; j_->fp = p_->fp; j_->f = p_->f; j_->is_i = p_->is_i; j_->met = (MET_MS); \
         j_->sl.idr = p_->f == 0; j_->sl.slice_type = p_->fp.slice_type; j_->sl.frame_num = p_->frame_num; \
-        j_->sl.poc_lsb = 2 * p_->f; j_->sl.idr_pic_id = 0; j_->sl.qp = p_->fp.qp;                  \
+        j_->sl.poc_lsb = 2 * p_->f; j_->sl.idr_pic_id = 0; j_->sl.qp = p_->fp.qp; j_->sl.first_mb = 0; \
         pool_submit(&pool, (int)(j_ - pool.jobs));                                                 \
         jseq++;                                                                                    \
     } while (0)
@@ -285,10 +301,8 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         jm_slice sl;                                                                               \
         sl.idr = p_->f == 0; sl.slice_type = p_->fp.slice_type; sl.frame_num = p_->frame_num;      \
         sl.poc_lsb = 2 * p_->f; sl.idr_pic_id = 0; sl.qp = p_->fp.qp;                              \
-        jm_bits_init(&rbsp);                                                                       \
-        if (encode_one_slice(&im, &s, &sl, &p_->fp, &p_->cur, &rec, &rbsp)) { st_ret = JMH_E_OOM; break; } \
-        jm_write_nal(&out, sl.idr ? 3 : 2, sl.idr ? 5 : 1, &rbsp);                                 \
-        jm_bits_free(&rbsp);                                                                       \
+        sl.first_mb = 0;                                                                           \
+        if (encode_picture_slices(&im, &s, &sl, &p_->fp, &p_->cur, &rec, &out)) { st_ret = JMH_E_OOM; break; } \
         double t2 = now_ms();                                                                      \
         st->entropy_ms += t2 - t1;                                                                 \
         long pic_bits = out.len * 8;                                                               \

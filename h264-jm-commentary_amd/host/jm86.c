@@ -59,6 +59,7 @@ int jm86_start_picture(jm86_img *im, const jmh_frame_params *fp, const jm_pic *c
     im->lambda_mode = fp->lambda_mode;
     im->lambda_motion = fp->lambda_motion;
     im->writer = writer;
+    im->slice_first = 0;
     memset(im->enc_mv, 0, (size_t)im->width * im->height / 16 * 2 * sizeof(int16_t));
     memset(im->enc_ref, -1, (size_t)im->width * im->height / 16);
     if (surface_on(im)) return im->be->search_pictures(im->be->ctx, cur, ref);
@@ -84,7 +85,8 @@ static int nb4(int xN, int yN, int *idx) {
     if (xN < 0) { mx = img->mb_x - 1; my = yN < 0 ? img->mb_y - 1 : img->mb_y; }
     else if (xN <= 15) { mx = img->mb_x; my = yN < 0 ? img->mb_y - 1 : img->mb_y; }
     else { if (yN >= 0) return 0; mx = img->mb_x + 1; my = img->mb_y - 1; }
-    if (mx < 0 || my < 0 || mx >= img->mbw) return 0;   /* one slice, raster order: the rest is coded */
+    /* raster order: the rest is coded; outside the current slice is unavailable (6.4.8) */
+    if (mx < 0 || my < 0 || mx >= img->mbw || my * img->mbw + mx < img->slice_first) return 0;
     *idx = ((img->pix_y + yN) >> 2) * (img->width >> 2) + ((img->pix_x + xN) >> 2);
     return 1;
 }

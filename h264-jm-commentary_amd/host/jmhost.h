@@ -44,6 +44,8 @@ typedef struct jm_input {
                                   OffsetBits 11 (JMVersion >= 10; -1 = JM defaults 682 / 342) */
     int  adaptive_rounding;    /* AdaptiveRounding (must be 0)                                */
     int  epzs_dual;            /* EPZSDualRefinement (0, 1; SearchMode 3)                      */
+    int  slice_mode;           /* SliceMode (0: one slice per picture, 1: SliceArgument MBs)   */
+    int  slice_arg;            /* SliceArgument (MBs per slice with SliceMode 1)               */
     int  epzs_subpel;          /* EPZSSubPelME (must be 0)                                     */
     int  offset_matrix_present;/* OffsetMatrixPresentFlag (must be 0: flat lists only)         */
     int  level_idc;            /* LevelIDC                                                    */
@@ -116,6 +118,7 @@ typedef struct jm_seq {
     int lf_params_flag, lf_disable, lf_alpha, lf_beta;
     int constrained_intra;
     int transform_8x8_mode;    /* PPS transform_8x8_mode_flag (High profile)                   */
+    int slice_mbs;             /* MBs per slice, raster order (SliceMode 1); 0: one slice      */
 } jm_seq;
 
 /* NAL unit (Annex B start code + emulation prevention) appended to out */
@@ -125,6 +128,7 @@ void jm_write_pps(jm_bits *rbsp, const jm_seq *s);
 
 typedef struct jm_slice {
     int idr, slice_type, frame_num, poc_lsb, idr_pic_id, qp;
+    int first_mb;              /* first_mb_in_slice                                             */
 } jm_slice;
 /* slice header + CAVLC slice data for a whole picture (one slice); results in raster order */
 int  jm_write_slice(jm_bits *rbsp, const jm_seq *s, const jm_slice *sl,
@@ -213,6 +217,7 @@ typedef struct jm86_img {
     const jm_input *input;
     jm_backend *be;
     jm_slice_writer *writer;
+    int slice_first;                  /* first MB of the current slice (neighbour availability) */
     const jmh_mb_result *res;         /* the picture's results (NULL: the backend's current ones) */
 } jm86_img;
 extern __thread jm86_img *img;       /* JM's global img, one per slice-writing thread */

@@ -17,7 +17,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 9
+JMH_ABI_VERSION = 10
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -38,7 +38,8 @@ class JmhConfig(ctypes.Structure):
                 ("constrained_intra_pred", ctypes.c_int32), ("num_frame_slots", ctypes.c_int32),
                 ("flags", ctypes.c_int32), ("pipeline_depth", ctypes.c_int32),
                 ("transform_8x8_mode", ctypes.c_int32), ("jm_version", ctypes.c_int32),
-                ("quant_offset", ctypes.c_int32 * 2), ("epzs_dual_refinement", ctypes.c_int32)]
+                ("quant_offset", ctypes.c_int32 * 2), ("epzs_dual_refinement", ctypes.c_int32),
+                ("slice_mbs", ctypes.c_int32)]
 
 
 class JmhFrameParams(ctypes.Structure):
@@ -154,7 +155,7 @@ def _ptr(a):
 
 def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
                 restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False,
-                pipeline_depth=0, transform_8x8_mode=0, jm_version=8, quant_offset=(682, 342), epzs_dual_refinement=0):
+                pipeline_depth=0, transform_8x8_mode=0, jm_version=8, quant_offset=(682, 342), epzs_dual_refinement=0, slice_mbs=0):
     """jm_version >= 10 selects the JM >= 10 quantisation rounding with the flat OffsetMatrix
     entries quant_offset = (I slices, P slices) at OffsetBits 11 (docs/JM_SEMANTICS.md item 45)."""
     cfg = JmhConfig()
@@ -169,6 +170,7 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     cfg.transform_8x8_mode = transform_8x8_mode
     cfg.jm_version = jm_version
     cfg.epzs_dual_refinement = epzs_dual_refinement
+    cfg.slice_mbs = slice_mbs
     if jm_version >= 10:
         cfg.quant_offset[0], cfg.quant_offset[1] = quant_offset
     return cfg

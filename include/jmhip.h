@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 9
+#define JMH_ABI_VERSION 10
 #define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
 #define JMH_QOFFSET_MAX 2047  /* jmh_config.quant_offset: OffsetBits 11 (1 << 11 = a whole step)    */
 
@@ -103,6 +103,11 @@ typedef struct jmh_config {
                                        682, 342: Offset_intra_default_intra / _inter) [J]          */
     int32_t epzs_dual_refinement;   /* EPZSDualRefinement (SearchMode 3): 0 off, 1 refine the runner-up
                                        predictor too (docs/JM_SEMANTICS.md item 46)                 */
+    int32_t slice_mbs;              /* SliceMode 1 / SliceArgument: macroblocks per slice in raster
+                                       order (0: one slice per picture).  Intra prediction, MV
+                                       prediction and the EPZS spatial memory see only neighbours of
+                                       the same slice (H.264 6.4.8, docs/JM_SEMANTICS.md item 47);
+                                       deblocking still crosses slice edges (idc 0)                 */
 } jmh_config;
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */

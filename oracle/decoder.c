@@ -2,7 +2,7 @@
  * decoder.c — minimal normative H.264 decoder for closed-loop checks (TEST INFRASTRUCTURE ONLY).
  *
  * Scope: the Baseline / High subset the host encoder emits — progressive frames, 4:2:0 8-bit,
- * one slice per picture, CAVLC, I and P slices, one reference picture, no FMO/ASO/redundant
+ * one or more slices per picture (raster order, no ASO), CAVLC, I and P slices, one reference picture, no FMO/ASO/redundant
  * slices, POC type 0; High: transform_size_8x8_flag (8x8 residual, Intra_8x8), flat scaling.  Written from ITU-T H.264 clauses 7.3 (syntax), 8.3 (intra), 8.4
  * (inter, MVP via "partition already decoded" tracking, independent of the encoder's JM
  * shape rules), 8.5 (scaling/inverse transforms), 8.7 (deblocking), 9.1/9.2 (Exp-Golomb,
@@ -158,6 +158,8 @@ struct jmo_dec {
     int8_t *refi;         /* per 4x4 */
     int8_t *dec4;         /* per 4x4: decoded in the current picture */
     int dis_dbf, offA, offB;
+    int slice_first;      /* first MB of the current slice: MBs before it are unavailable (6.4.8) */
+    int mbs_done;         /* MBs of the current picture decoded so far (a picture may have many slices) */
 };
 
 int jmo_dec_create(jmo_dec **out) { *out = (jmo_dec *)calloc(1, sizeof(jmo_dec)); return *out ? 0 : JMH_E_OOM; }
@@ -238,7 +240,7 @@ static int parse_pps(jmo_dec *d, br_t *b) {
 
 /* ---- intra prediction (8.3) ------------------------------------------------------------ */
 static int avail_mb(const jmo_dec *d, int mx, int my, int cmx, int cmy) {
-    if (mx < 0 || my < 0 || mx >= d->mbw || my >= d->mbh) return 0;
+    if (mx < 0 || my < 0 || mx >= d->mbw || my >= d->mbh || my * d->mbw + mx < d->slice_first) return 0;
     return my < cmy || (my == cmy && mx < cmx);
 }
 /* availability of luma sample at MB-relative (x,y) for intra 4x4 block at (bx,by) */
@@ -527,7 +529,7 @@ static int nb4(const jmo_dec *d, int mx, int my, int xN, int yN, int *idx) {
     if (xN < 0) { tx = mx - 1; ty = yN < 0 ? my - 1 : my; }
     else if (xN <= 15) { tx = mx; ty = yN < 0 ? my - 1 : my; }
     else { if (yN >= 0) return 0; tx = mx + 1; ty = my - 1; }
-    if (tx < 0 || ty < 0 || tx >= d->mbw) return 0;
+    if (tx < 0 || ty < 0 || tx >= d->mbw || ty * d->mbw + tx < d->slice_first) return 0;
     int W4 = d->W / 4;
     int i = ((16 * my + yN) >> 2) * W4 + ((16 * mx + xN) >> 2);
     if (tx == mx && ty == my && !d->dec4[i]) return 0;   /* not yet decoded partition */
@@ -897,8 +899,23 @@ static void deblock(jmo_dec *d) {
  * 4x4 edge segment k/2); the loop above filters chroma line k/2 when visiting luma line k (even)
  * using the bS of luma line k, which lies in the same 4-sample segment as 2*(k/2). */
 
-static int decode_slice(jmo_dec *d, br_t *b, int nal_type, int nal_ref_idc) {
-    rue(b);                                   /* first_mb_in_slice (single slice) */
+/* more_rbsp_data() (7.2): bits remain before the rbsp_stop_one_bit */
+static int more_rbsp_data(const br_t *b) {
+    long n = b->n;
+    while (n > 0 && b->p[n - 1] == 0) n--;
+    if (n == 0) return 0;
+    int v = b->p[n - 1], k = 0;
+    while (!(v & 1)) { v >>= 1; k++; }
+    return b->pos < n * 8 - 1 - k;
+}
+
+/* one slice (7.3.3 / 7.3.4).  *pic_done = 1 when it completes the picture (then deblocked). */
+static int decode_slice(jmo_dec *d, br_t *b, int nal_type, int nal_ref_idc, int *pic_done) {
+    int nmb = d->mbw * d->mbh;
+    int first = rue(b);                       /* first_mb_in_slice */
+    if (first >= nmb) FAIL("first_mb_in_slice %d", first);
+    if (first == 0) d->mbs_done = 0;
+    else if (first != d->mbs_done) FAIL("slice starts at MB %d, expected %d", first, d->mbs_done);
     int st = rue(b) % 5;
     if (st != 0 && st != 2) FAIL("slice type %d unsupported", st);
     rue(b);
@@ -917,23 +934,29 @@ static int decode_slice(jmo_dec *d, br_t *b, int nal_type, int nal_ref_idc) {
         if (d->dis_dbf != 1) { d->offA = 2 * rse(b); d->offB = 2 * rse(b); }
     }
     if (st == 0 && !d->have_ref) FAIL("P slice without reference");
-    memset(d->dec4, 0, (size_t)d->W * d->H / 16);
-    int nmb = d->mbw * d->mbh;
-    for (int a = 0; a < nmb;) {
+    if (first == 0) memset(d->dec4, 0, (size_t)d->W * d->H / 16);
+    d->slice_first = first;
+    int a = first, more = 1;
+    while (more && a < nmb) {
         if (st == 0) {
             int run = rue(b);
             if (b->err) FAIL("skip run");
             for (int i = 0; i < run && a < nmb; i++, a++) {
                 if (decode_mb(d, b, a % d->mbw, a / d->mbw, 1, 0, 1, &qp)) return -1;
             }
-            if (a >= nmb) break;
+            if (run > 0) more = more_rbsp_data(b);
         }
-        int t = rue(b);
-        if (b->err) FAIL("mb_type at MB %d", a);
-        if (decode_mb(d, b, a % d->mbw, a / d->mbw, st == 0, t, 0, &qp)) return -1;
-        a++;
+        if (more && a < nmb) {
+            int t = rue(b);
+            if (b->err) FAIL("mb_type at MB %d", a);
+            if (decode_mb(d, b, a % d->mbw, a / d->mbw, st == 0, t, 0, &qp)) return -1;
+            a++;
+            more = more_rbsp_data(b);
+        }
     }
-    deblock(d);
+    d->mbs_done = a;
+    *pic_done = a >= nmb;
+    if (*pic_done) deblock(d);
     return 0;
 }
 
@@ -960,8 +983,9 @@ int jmo_decode_annexb(jmo_dec *d, const uint8_t *buf, long len, uint8_t *out, lo
         else if (nal_type == 8) r = parse_pps(d, &b);
         else if (nal_type == 1 || nal_type == 5) {
             if (!d->have_sps || !d->have_pps) { snprintf(d->err, sizeof d->err, "slice before SPS/PPS"); r = -1; }
-            else r = decode_slice(d, &b, nal_type, nal_ref);
-            if (!r) {
+            int pic_done = 0;
+            if (!r) r = decode_slice(d, &b, nal_type, nal_ref, &pic_done);
+            if (!r && pic_done) {
                 int cw = d->W - 2 * (d->crop_l + d->crop_r), ch = d->H - 2 * (d->crop_t + d->crop_b);
                 long fs = (long)cw * ch * 3 / 2;
                 if ((nframes + 1) * fs > out_cap) { snprintf(d->err, sizeof d->err, "output buffer too small"); r = -1; }

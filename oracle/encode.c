@@ -38,7 +38,8 @@ typedef struct {
 } mbs;
 
 /* ====================================================================================== */
-/*  neighbour access (getLuma4x4Neighbour / getNeighbour, H.264 6.4.11/6.4.12, single slice) */
+/*  neighbour access (getLuma4x4Neighbour / getNeighbour, H.264 6.4.11/6.4.12; neighbours
+ *  outside the current slice are unavailable, 6.4.8 / JM_SEMANTICS item 47) */
 /* ====================================================================================== */
 static int nb4(const mbs *s, int xN, int yN, int *idx) {
     const jmo_ctx *c = s->c;
@@ -47,7 +48,7 @@ static int nb4(const mbs *s, int xN, int yN, int *idx) {
     if (xN < 0) { mx = s->mbx - 1; my = yN < 0 ? s->mby - 1 : s->mby; }
     else if (xN <= 15) { mx = s->mbx; my = yN < 0 ? s->mby - 1 : s->mby; }
     else { if (yN >= 0) return 0; mx = s->mbx + 1; my = s->mby - 1; }
-    if (mx < 0 || my < 0 || mx >= c->mbw) return 0;
+    if (mx < 0 || my < 0 || mx >= c->mbw || !jmo_same_slice(c, s->mby * c->mbw + s->mbx, my * c->mbw + mx)) return 0;
     *idx = ((s->pix_y + yN) >> 2) * (c->W >> 2) + ((s->pix_x + xN) >> 2);
     return 1;
 }
@@ -305,7 +306,7 @@ static int epzs_predictors(const mbs *s, int bt, int bx4, int by4, int range, in
         ADD(v, v ? rnd_fp(c->tmv[2 * i]) : 0, v ? rnd_fp(c->tmv[2 * i + 1]) : 0);
     }
     int k0 = by4 * 4 + bx4;                                 /* 34: spatial memory (left MB)    */
-    int vm = s->mbx > 0 && c->cfg.inter_search[bt];
+    int vm = s->mbx > 0 && jmo_same_slice(c, s->mby * c->mbw + s->mbx, s->mby * c->mbw + s->mbx - 1) && c->cfg.inter_search[bt];
     ADD(vm, vm ? rnd_fp(c->mem_mv[bt][k0][0]) : 0, vm ? rnd_fp(c->mem_mv[bt][k0][1]) : 0);
     static const int types[6] = {1, 2, 3, 4, 5, 6};         /* 35-40: earlier block types      */
     for (int k = 0; k < 6; k++) {
@@ -735,7 +736,8 @@ static int dct_luma_16x16(const int32_t resid[256], const uint8_t pred[256], int
 static int mb_avail(const mbs *s, int dmx, int dmy) {
     int mx = s->mbx + dmx, my = s->mby + dmy;
     return mx >= 0 && my >= 0 && mx < s->c->mbw && my < s->c->mbh &&
-           (my < s->mby || (my == s->mby && mx < s->mbx));
+           (my < s->mby || (my == s->mby && mx < s->mbx)) &&
+           jmo_same_slice(s->c, s->mby * s->c->mbw + s->mbx, my * s->c->mbw + mx);
 }
 /* luma sample availability at MB-relative (x,y) for intra prediction */
 static int luma_avail(const mbs *s, int x, int y) {

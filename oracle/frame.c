@@ -18,6 +18,7 @@ static int cfg_ok(const jmh_config *cfg) {
     if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version < 0 || cfg->jm_version == 9 || cfg->jm_version > 99) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->epzs_dual_refinement != 0 && cfg->epzs_dual_refinement != 1) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->slice_mbs < 0) return JMH_E_INVALID_ARG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     return JMH_OK;

@@ -64,6 +64,13 @@ struct jmo_ctx {
     int16_t mem_mv[8][16][2];        /* all_mv of the MB to the left (valid when mbx > 0)       */
 };
 
+/* SliceMode 1 (SliceArgument MBs per slice, raster order): MB addresses a and n lie in one slice.
+ * Neighbours precede the current MB, so this is "n >= the slice's first MB" (6.4.8).          */
+static inline int jmo_same_slice(const jmo_ctx *c, int a, int n) {
+    int k = c->cfg.slice_mbs;
+    return k <= 0 || n >= a - a % k;
+}
+
 /* common.c */
 void jmo_init_spiral(jmo_ctx *c);
 void jmo_build_qpel(jmo_ctx *c);

@@ -40,6 +40,18 @@ CONFIGS = [
      "Transform8x8Mode=1", "SourceWidth=352", "SourceHeight=288", "QPRemainingFrame=31"],
     ["InputFile=synthetic:25", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=0", "SearchRange=8",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=-2", "LoopFilterBetaOffset=3", "ChromaQPOffset=3"],
+    # SliceMode 1 (row f4's slice structure): neighbours across slice edges are unavailable for
+    # intra / MV prediction, CAVLC nC and the skip run; deblocking still crosses them
+    ["InputFile=synthetic:31", "FramesToBeEncoded=4", "SliceMode=1", "SliceArgument=11", "SearchRange=16"],
+    ["InputFile=synthetic:32", "FramesToBeEncoded=4", "SliceMode=1", "SliceArgument=7", "SearchRange=8",
+     "IntraPeriod=2"],
+    ["InputFile=synthetic:33", "FramesToBeEncoded=3", "SliceMode=1", "SliceArgument=1", "SearchRange=4"],
+    ["InputFile=synthetic:34", "FramesToBeEncoded=3", "SliceMode=1", "SliceArgument=30", "SearchMode=-1",
+     "SearchRange=8", "SourceWidth=200", "SourceHeight=120"],
+    ["InputFile=synthetic:35", "FramesToBeEncoded=4", "SliceMode=1", "SliceArgument=22", "SearchMode=3",
+     "SearchRange=16", "ProfileIDC=100", "Transform8x8Mode=1", "SourceWidth=352", "SourceHeight=288"],
+    ["InputFile=synthetic:36", "FramesToBeEncoded=3", "SliceMode=1", "SliceArgument=13", "ProfileIDC=100",
+     "Transform8x8Mode=1", "SearchMode=3", "EPZSDualRefinement=1", "QPRemainingFrame=36"],
 ]
 
 
@@ -68,3 +80,40 @@ def test_deterministic_bitstream():
         encode(a, CONFIGS[0])
         encode(b, CONFIGS[0])
         assert open(f"{a}/a.264", "rb").read() == open(f"{b}/a.264", "rb").read()
+
+
+def nal_types(buf):
+    """NAL unit types of an Annex B byte stream"""
+    out, i = [], 0
+    while i + 3 < len(buf):
+        if buf[i] == 0 and buf[i + 1] == 0 and buf[i + 2] == 1:
+            out.append(buf[i + 3] & 31)
+            i += 3
+        else:
+            i += 1
+    return out
+
+
+@pytest.mark.parametrize("arg,nslices", [(11, 9), (7, 15), (99, 1), (500, 1)])
+def test_slice_count(arg, nslices):
+    """SliceMode 1: ceil(99 / SliceArgument) slice NAL units per QCIF picture, first_mb_in_slice
+    advancing by SliceArgument; the decoder reassembles each picture from its slices."""
+    ensure_built()
+    with tempfile.TemporaryDirectory() as d:
+        encode(d, ["InputFile=synthetic:37", "FramesToBeEncoded=3", "SliceMode=1", f"SliceArgument={arg}",
+                   "SearchRange=8"])
+        t = nal_types(open(f"{d}/a.264", "rb").read())
+        assert t.count(5) == nslices and t.count(1) == 2 * nslices
+        r = subprocess.run([JMDEC, f"{d}/a.264", f"{d}/dec.yuv"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/rec.yuv", "rb").read()
+
+
+def test_slices_change_the_decisions():
+    """Slice edges remove neighbours: one MB per slice differs from one slice per picture."""
+    ensure_built()
+    with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:
+        base = ["InputFile=synthetic:38", "FramesToBeEncoded=2", "SearchRange=8"]
+        encode(a, base)
+        encode(b, base + ["SliceMode=1", "SliceArgument=1"])
+        assert open(f"{a}/rec.yuv", "rb").read() != open(f"{b}/rec.yuv", "rb").read()

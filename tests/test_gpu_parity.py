@@ -169,6 +169,13 @@ def test_ippp_qcif_sr16():
     (dict(search_range=32, search_mode=3, restrict_search_range=0), 20),
     (dict(search_range=8, search_mode=3, use_hadamard=0, inter_search=(1, 0, 1, 1, 0, 1, 1)), 36),
     (dict(search_range=4, search_mode=3, inter_search=(0, 1, 1, 1, 1, 1, 1)), 44),
+    # SliceMode 1 (f4's slice structure): one MB row, ragged runs, one MB per slice
+    (dict(search_range=8, slice_mbs=6), 28),
+    (dict(search_range=8, slice_mbs=5), 24),
+    (dict(search_range=4, slice_mbs=1), 30),
+    (dict(search_range=8, search_mode=-1, slice_mbs=7), 28),
+    (dict(search_range=16, search_mode=3, slice_mbs=6), 28),
+    (dict(search_range=16, search_mode=3, slice_mbs=1, epzs_dual_refinement=1), 32),
 ])
 def test_ipp_configs(kw, qp):
     pics = synth_seq(96, 64, 3, 7)
@@ -183,6 +190,8 @@ def test_ipp_configs(kw, qp):
     (dict(search_range=8), 51),
     (dict(search_range=8, inter_search=(1, 1, 1, 1, 0, 0, 0)), 24),   # P8x8 with 8x8 sub-blocks only
     (dict(search_range=8, search_mode=-1, restrict_search_range=0), 33),
+    (dict(search_range=8, slice_mbs=5), 28),                       # Intra8x8 neighbours across slice edges
+    (dict(search_range=16, search_mode=3, slice_mbs=6), 30),
 ])
 def test_high_profile_transform8x8(kw, qp):
     """a12 + Intra8x8 (Transform8x8Mode = 1): k_mb_intra8, TransformDecision, dct_luma8x8."""
@@ -241,6 +250,18 @@ def test_config3_width_3840_epzs():
     pics = moving_seq(w, h, 3, seed=38, step=(37, -29))
     encode_pair(w, h, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], 28, search_range=32, search_mode=3,
                 transform_8x8_mode=1)
+
+
+@pytest.mark.parametrize("slice_mbs", [240, 173])
+def test_config5_slices_width_3840(slice_mbs):
+    """Config 5's slice structure at its real width: SliceArgument 240 = one 3840-wide MB row per
+    slice (and a ragged 173), High profile, EPZS + 8x8 transform, under large motion; GPU ==
+    oracle on every macroblock (8-bit samples: the 10-bit wavefront and CABAC / RDO are not
+    built)."""
+    w, h = 3840, 128
+    pics = moving_seq(w, h, 3, seed=40, step=(29, -23))
+    encode_pair(w, h, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE, jmhip.JMH_P_SLICE], 28, search_range=32, search_mode=3,
+                transform_8x8_mode=1, slice_mbs=slice_mbs)
 
 
 def test_random_content_p_frames():
@@ -337,7 +358,9 @@ def run_chain(enc, pics, qp, dbk, pipelined):
                                               (1920, 1088, 32, 20, (-62, -61), dict(search_mode=3, transform_8x8_mode=1)),
                                               # tall: 526 diagonals, ~33 pictures in flight (PMAX entries per tick)
                                               (256, 4096, 32, 40, (37, -29), {}),
-                                              (256, 4096, 32, 40, (-62, -61), dict(search_mode=3, transform_8x8_mode=1))])
+                                              (256, 4096, 32, 40, (-62, -61), dict(search_mode=3, transform_8x8_mode=1)),
+                                              (1920, 1088, 32, 12, (37, -29), dict(slice_mbs=120)),
+                                              (640, 480, 32, 10, (-62, -61), dict(search_mode=3, transform_8x8_mode=1, slice_mbs=57))])
 def test_pipelined_chain_equals_sequential(w, h, sr, n, step, kw):
     """Pictures in flight together (lag PIPE_LAG diagonals) == one picture at a time, bit for
     bit, under motion that pushes MVs to the search-window edge (|MV| up to 63 px at SR 32: the
@@ -425,6 +448,15 @@ def run_lencod(binary, out_dir, extra):
      "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "JMVersion=10"],
     ["InputFile=synthetic:27", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
      "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "JMVersion=10", "EPZSDualRefinement=1"],
+    # SliceMode 1: one NAL unit per slice, neighbours limited to the slice (pipelined, writer threads)
+    ["InputFile=synthetic:28", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "SliceMode=1", "SliceArgument=22"],
+    ["InputFile=synthetic:29", "FramesToBeEncoded=4", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "SliceMode=1", "SliceArgument=7", "IntraPeriod=2", "WriterThreads=0"],
+    ["InputFile=synthetic:30", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "SliceMode=1", "SliceArgument=40"],
+    ["InputFile=synthetic:31", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=8",
+     "SearchMode=-1", "SliceMode=1", "SliceArgument=1"],
 ])
 def test_lencod_bitstream_identical(extra):
     with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:

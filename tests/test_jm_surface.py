@@ -25,6 +25,9 @@ CASES = [
      "SearchMode=-1", "RestrictSearchRange=0"],
     ["InputFile=synthetic:9", "FramesToBeEncoded=2", "SourceWidth=208", "SourceHeight=112", "SearchRange=12",
      "RestrictSearchRange=1", "UseHadamard=0", "QPRemainingFrame=36", "InterSearch8x4=0"],
+    # SliceMode 1: SetMotionVectorPredictor sees only the current slice (img->slice_first)
+    ["InputFile=synthetic:11", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=8",
+     "SliceMode=1", "SliceArgument=8"],
 ]
 
 

@@ -24,7 +24,9 @@ JMDEC_ASAN = os.path.join(ASAN, "jmdec")
 SAN_CASES = [CONFIGS[0], CONFIGS[1], CONFIGS[4], CONFIGS[6], CONFIGS[7], CONFIGS[12], CONFIGS[15], CONFIGS[16],
              CONFIGS[0] + ["WriterThreads=4"],
              CONFIGS[6] + ["JMCallSurface=1"],
-             CONFIGS[12] + ["WriterThreads=0", "JMCallSurface=1"]]
+             CONFIGS[12] + ["WriterThreads=0", "JMCallSurface=1"],
+             CONFIGS[19] + ["WriterThreads=4"],                # SliceMode 1 (several NAL units per picture)
+             CONFIGS[20] + ["JMCallSurface=1"]]
 
 ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=86",
            UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=87")
