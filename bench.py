@@ -58,6 +58,7 @@ CONFIGS = {
 }
 DISP_W, DISP_H = 1920, 1080
 W, H = 1920, 1088
+SLICE_MBS = 0        # --slice-mbs: SliceMode 1 / SliceArgument (0: one slice per picture)
 SR, QP = 32, 28
 NMB = (W // 16) * (H // 16)
 # algorithmic HBM bytes per coded picture: current 1.5 B/px + reference 1.5 B/px
@@ -116,7 +117,8 @@ def cpu_one_picture(seed, search_mode, t8=0, dump=None):
     import oracle_lib
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
     frames = [jm.synth_frame(DISP_W, DISP_H, seed, i) for i in range(2)]
-    o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8)
+    o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
+                                 slice_mbs=SLICE_MBS)
     ires, irec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
     t0 = time.perf_counter()
     o.set_reference(*irec)
@@ -136,7 +138,8 @@ def cpu_workers(n, config, search_mode, size, dump_dir=None):
                f"{size[0]}x{size[1]}"]
         if dump_dir and k == 0:
             cmd.append(os.path.join(dump_dir, "oracle_seed0.npz"))
-        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True))
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                                      env=dict(os.environ, JMH_BENCH_SLICE_MBS=str(SLICE_MBS))))
     out = []
     for p in procs:
         s = p.communicate()[0]
@@ -181,7 +184,7 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
     d = np.load(dump)
     frames = [jm.synth_frame(DISP_W, DISP_H, 0, i) for i in range(2)]
     g = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
-                   pipeline_depth=1)
+                   pipeline_depth=1, slice_mbs=SLICE_MBS)
     try:
         ires, irec = g.encode(*frames[0], jm.JMH_I_SLICE, QP)
         g.set_reference(*irec)
@@ -260,7 +263,9 @@ def launch(n):
 
 
 def main():
+    global SLICE_MBS
     if len(sys.argv) in (6, 7) and sys.argv[1] == "--cpu-worker":    # child of cpu_baseline()
+        SLICE_MBS = int(os.environ.get("JMH_BENCH_SLICE_MBS", "0"))
         w, h = (int(v) for v in sys.argv[5].split("x"))
         c = use_config(int(sys.argv[3]), (w, h))
         print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[4]), c["t8"], sys.argv[6] if len(sys.argv) == 7 else None),
@@ -277,6 +282,8 @@ def main():
                     help="BASELINE.json config: 2 = 1080p Baseline FFS (the headline), 3 = 2160p High EPZS + 8x8")
     ap.add_argument("--search-mode", type=int, default=None, choices=(0, -1, 3),
                     help="override the config's SearchMode (config 2 variants: -1 full search, 3 EPZS)")
+    ap.add_argument("--slice-mbs", type=int, default=0,
+                    help="SliceMode 1 with SliceArgument N macroblocks per slice (a variant line; 0: one slice)")
     # test knobs (tests/test_multistream_gpu.py): a smaller picture, a final read-back picture
     ap.add_argument("--size", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--dump", default=None, help=argparse.SUPPRESS)
@@ -294,6 +301,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     size = tuple(int(v) for v in args.size.split("x")) if args.size else None
     cfg = use_config(args.config, size)
+    SLICE_MBS = max(0, args.slice_mbs)
     search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
     dist = None
     if world > 1:
@@ -308,7 +316,7 @@ def main():
     device = local % ndev
     frames = [jm.synth_frame(DISP_W, DISP_H, rank, i) for i in range(args.frames + 1)]
     enc = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, slots=len(frames),
-                     kernel_timing=True, transform_8x8_mode=cfg["t8"])
+                     kernel_timing=True, transform_8x8_mode=cfg["t8"], slice_mbs=SLICE_MBS)
     stream = streams.PStream(enc, frames, QP, deblock=None if args.no_deblock else (0, 0, 0))
     dt = streams.timed_run(stream, args.steps, args.warmup, dist, on_start=enc.timing)   # on_start resets the event sums
     tm = enc.timing()                                     # event sums of the timed steps only
@@ -385,7 +393,9 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": cfg["workload"].replace("{sm}", sm_name).replace("{nf}", str(args.frames)),
+            "workload": cfg["workload"].replace("{sm}", sm_name).replace("{nf}", str(args.frames))
+                        + (f", SliceMode=1 SliceArgument={SLICE_MBS} ({-(-NMB // SLICE_MBS)} slices per picture)"
+                           if SLICE_MBS else ""),
             "global_batch": world,
             "parallelism": f"streams{world}",
             "pipeline_depth": enc.depth,

@@ -12,6 +12,7 @@
 #   bench20 bench.py --steps 20 --warmup 5 (the driver's invocation, no CPU baseline)
 #   benchf8 bench20 with JMH_FINAL_OCC8=1 (k_mb_final's 8-per-CU build for every tick: A/B)
 #   c3      bench.py --config 3 (with CPU baseline)  -> gpurun_out/TAG_c3_bench.json
+#   c3s     config 3 with SliceMode 1, SliceArgument 240 (config 5's one-row slices, 8-bit, CAVLC)
 #   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
 #   profc3  the same for config 3
 #   pmc     tools/pmc_traffic.sh (HBM bytes + SQ counters, separate passes)
@@ -51,6 +52,8 @@ for s in "$@"; do
             cat gpurun_out/${TAG}_benchf8.json ;;
     c3)     run c3 900 python bench.py --config 3 > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3_bench.err || exit $?
             cat gpurun_out/${TAG}_c3_bench.json ;;
+    c3s)    run c3s 900 python bench.py --config 3 --slice-mbs 240 > gpurun_out/${TAG}_c3s_bench.json 2> gpurun_out/${TAG}_c3s_bench.err || exit $?
+            cat gpurun_out/${TAG}_c3s_bench.json ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}" -o ${TAG} --output-format csv -- \
                 python3 "$R/bench.py" --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
             find gpurun_out/prof_${TAG} -name "*kernel_stats*" -exec cat {} \; ;;
