@@ -227,12 +227,14 @@ typedef struct {
     int16_t *mv;        /* per 4x4 [2] of the picture, final values (written MBs) */
     int8_t *ref;        /* per 4x4, -1 intra / not yet written                      */
     int8_t *ipm;        /* per 4x4 Intra4x4PredMode, -1: MB not I4x4               */
-    int8_t *written;    /* per MB                                                   */
+    uint32_t *written;  /* per MB: the stamp of the slice that wrote it             */
+    uint32_t stamp;     /* the current slice's stamp (neighbours of other slices are not
+                           available, 6.4.8; the buffers serve every slice of a picture) */
     uint8_t *tc;        /* per MB: 16 luma + 4 Cb + 4 Cr total_coeff               */
 } wctx;
 
 static int mb_ok(const wctx *w, int mx, int my) {
-    return mx >= 0 && my >= 0 && mx < w->s->mbw && my < w->s->mbh && w->written[my * w->s->mbw + mx];
+    return mx >= 0 && my >= 0 && mx < w->s->mbw && my < w->s->mbh && w->written[my * w->s->mbw + mx] == w->stamp;
 }
 /* neighbour 4x4 in luma pixels relative to MB (mx,my): returns availability + 4x4 index */
 static int nb(const wctx *w, int mx, int my, int xN, int yN, int *idx, int cur_ok) {
@@ -313,7 +315,7 @@ static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r,
         w->ref[a] = is_intra ? -1 : 0;
         w->ipm[a] = is_i4 ? r->ipred[k] : -1;
     }
-    w->written[my * w->s->mbw + mx] = 1;
+    w->written[my * w->s->mbw + mx] = w->stamp;
     int ue_type;
     if (is_i16) {
         int t = 1 + r->i16mode + 4 * cbpc + (cbpl ? 12 : 0);
@@ -410,10 +412,8 @@ struct jm_slice_writer {
     int open;                  /* header written and buffers allocated */
 };
 
-jm_slice_writer *jm_slice_begin(jm_bits *b, const jm_seq *s, const jm_slice *sl) {
-    jm_slice_writer *sw = calloc(1, sizeof(*sw));
-    if (!sw) return NULL;
-    /* slice_header (7.3.3) */
+/* slice_header (7.3.3) */
+static void write_slice_header(jm_bits *b, const jm_seq *s, const jm_slice *sl) {
     jm_put_ue(b, sl->first_mb);                       /* first_mb_in_slice */
     jm_put_ue(b, sl->slice_type);                     /* 0 = P, 2 = I            */
     jm_put_ue(b, 0);                                  /* pic_parameter_set_id    */
@@ -432,22 +432,42 @@ jm_slice_writer *jm_slice_begin(jm_bits *b, const jm_seq *s, const jm_slice *sl)
         /* LoopFilterAlphaC0Offset / LoopFilterBetaOffset are the div2 values [J] */
         if (s->lf_disable != 1) { jm_put_se(b, s->lf_alpha); jm_put_se(b, s->lf_beta); }
     }
-    /* slice_data (7.3.4) */
+}
+
+jm_slice_writer *jm_slice_begin(jm_bits *b, const jm_seq *s, const jm_slice *sl) {
+    jm_slice_writer *sw = calloc(1, sizeof(*sw));
+    if (!sw) return NULL;
+    write_slice_header(b, s, sl);
+    /* slice_data (7.3.4); neighbour state of the picture (entries are read only for MBs that
+       carry the current slice's stamp, so no clearing between slices) */
     int nmb = s->mbw * s->mbh, W4 = s->mbw * 4, H4 = s->mbh * 4;
     wctx *w = &sw->w;
     sw->b = b;
     w->s = s;
-    w->mv = calloc((size_t)W4 * H4 * 2, sizeof(int16_t));
+    w->mv = malloc((size_t)W4 * H4 * 2 * sizeof(int16_t));
     w->ref = malloc((size_t)W4 * H4);
     w->ipm = malloc((size_t)W4 * H4);
-    w->written = calloc(nmb, 1);
-    w->tc = calloc((size_t)nmb * 24, 1);
+    w->written = calloc(nmb, sizeof(uint32_t));
+    w->tc = malloc((size_t)nmb * 24);
     if (!w->mv || !w->ref || !w->ipm || !w->written || !w->tc) { jm_slice_end(sw); return NULL; }
-    memset(w->ref, -1, (size_t)W4 * H4);
-    memset(w->ipm, -1, (size_t)W4 * H4);
+    w->stamp = 1;
     sw->slice_p = sl->slice_type == JMH_P_SLICE;
     sw->open = 1;
     return sw;
+}
+
+static void close_slice_data(jm_slice_writer *sw) {
+    if (sw->slice_p && sw->skip_run) jm_put_ue(sw->b, sw->skip_run);
+    sw->skip_run = 0;
+    jm_trailing_bits(sw->b);
+}
+
+void jm_slice_restart(jm_slice_writer *sw, jm_bits *b, const jm_slice *sl) {
+    close_slice_data(sw);
+    write_slice_header(b, sw->w.s, sl);
+    sw->b = b;
+    sw->w.stamp++;
+    sw->slice_p = sl->slice_type == JMH_P_SLICE;
 }
 
 void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
@@ -460,7 +480,7 @@ void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
             w->mv[2 * i] = r->mv[k][0]; w->mv[2 * i + 1] = r->mv[k][1];
             w->ref[i] = 0; w->ipm[i] = -1;
         }
-        w->written[a] = 1;
+        w->written[a] = w->stamp;
         memset(w->tc + (size_t)a * 24, 0, 24);
         sw->skip_run++;
         return;
@@ -471,10 +491,7 @@ void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
 
 void jm_slice_end(jm_slice_writer *sw) {
     if (!sw) return;
-    if (sw->open) {   /* close the slice data */
-        if (sw->slice_p && sw->skip_run) jm_put_ue(sw->b, sw->skip_run);
-        jm_trailing_bits(sw->b);
-    }
+    if (sw->open) close_slice_data(sw);
     free(sw->w.mv); free(sw->w.ref); free(sw->w.ipm); free(sw->w.written); free(sw->w.tc);
     free(sw);
 }

@@ -45,38 +45,45 @@ static double psnr(const uint8_t *a, int sa, const uint8_t *b, int sb, int w, in
 
 /* slice.c › encode_one_slice [J]: the macroblock loop of one slice through the JM 8.6 call
  * surface (host/jm86.c): start_macroblock, encode_one_macroblock, write_one_macroblock.
- * image.c › code_a_picture [J] calls it for every slice of the picture (SliceMode 1:
- * SliceArgument MBs each, raster order); each slice is its own NAL unit, appended to out. */
-static int encode_one_slice(jm86_img *im, const jm_seq *s, const jm_slice *sl, jm_bits *out) {
-    const int nmb = s->mbw * s->mbh, end = s->slice_mbs > 0 && sl->first_mb + s->slice_mbs < nmb ? sl->first_mb + s->slice_mbs : nmb;
-    jm_bits rbsp;
-    jm_bits_init(&rbsp);
-    jm_slice_writer *w = jm_slice_begin(&rbsp, s, sl);
-    if (!w) { jm_bits_free(&rbsp); return JMH_E_OOM; }
-    im->writer = w;
-    im->slice_first = sl->first_mb;
-    for (int a = sl->first_mb; a < end; a++) {
+ * image.c › code_a_picture [J] runs it for every slice of the picture (SliceMode 1: SliceArgument
+ * MBs each, raster order); each slice is its own NAL unit, appended to out.  One slice writer
+ * serves the picture (jm_slice_restart between slices). */
+static void encode_one_slice(const jm_seq *s, int first) {
+    const int nmb = s->mbw * s->mbh, end = s->slice_mbs > 0 && first + s->slice_mbs < nmb ? first + s->slice_mbs : nmb;
+    img->slice_first = first;
+    for (int a = first; a < end; a++) {
         img->current_mb_nr = a;
         start_macroblock();
         encode_one_macroblock();
         write_one_macroblock();
     }
-    jm_slice_end(w);
-    im->writer = NULL;
-    jm_write_nal(out, sl->idr ? 3 : 2, sl->idr ? 5 : 1, &rbsp);
-    jm_bits_free(&rbsp);
-    return JMH_OK;
 }
 static int encode_picture_slices(jm86_img *im, const jm_seq *s, const jm_slice *sl0, const jmh_frame_params *fp,
                                  const jm_pic *cur, const jm_pic *ref, jm_bits *out) {
-    int r = jm86_start_picture(im, fp, cur, ref, NULL);
-    if (r) return r;
     const int nmb = s->mbw * s->mbh, step = s->slice_mbs > 0 ? s->slice_mbs : nmb;
+    jm_slice sl = *sl0;
+    sl.first_mb = 0;
+    jm_bits rbsp[2];             /* the slice being written and the next one (alternating) */
+    int k = 0;
+    jm_bits_init(&rbsp[0]);
+    jm_slice_writer *w = jm_slice_begin(&rbsp[0], s, &sl);
+    if (!w) { jm_bits_free(&rbsp[0]); return JMH_E_OOM; }
+    int r = jm86_start_picture(im, fp, cur, ref, w);
+    if (r) { jm_slice_end(w); jm_bits_free(&rbsp[0]); return r; }
     for (int first = 0; first < nmb; first += step) {
-        jm_slice sl = *sl0;
-        sl.first_mb = first;
-        if ((r = encode_one_slice(im, s, &sl, out))) return r;
+        encode_one_slice(s, first);
+        if (first + step >= nmb) {
+            jm_slice_end(w);
+        } else {
+            jm_bits_init(&rbsp[k ^ 1]);
+            sl.first_mb = first + step;
+            jm_slice_restart(w, &rbsp[k ^ 1], &sl);
+        }
+        jm_write_nal(out, sl0->idr ? 3 : 2, sl0->idr ? 5 : 1, &rbsp[k]);
+        jm_bits_free(&rbsp[k]);
+        k ^= 1;
     }
+    im->writer = NULL;
     return JMH_OK;
 }
 

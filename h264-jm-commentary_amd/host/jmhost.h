@@ -138,6 +138,9 @@ typedef struct jm_slice_writer jm_slice_writer;
 jm_slice_writer *jm_slice_begin(jm_bits *rbsp, const jm_seq *s, const jm_slice *sl);
 void jm_slice_write_mb(jm_slice_writer *w, int mb_addr, const jmh_mb_result *r);
 void jm_slice_end(jm_slice_writer *w);
+/* close the current slice's data in its rbsp and start the next slice (header into rbsp), keeping
+   the picture's neighbour buffers (SliceMode 1: one writer per picture, one rbsp per slice) */
+void jm_slice_restart(jm_slice_writer *w, jm_bits *rbsp, const jm_slice *sl);
 
 /* ---- deblocking (H.264 8.7), in place on the reconstructed picture ---------------------- */
 void jm_deblock_picture(jm_pic *p, const jm_seq *s, const jmh_mb_result *const *res, int qp);
