@@ -117,3 +117,24 @@ def test_slices_change_the_decisions():
         encode(a, base)
         encode(b, base + ["SliceMode=1", "SliceArgument=1"])
         assert open(f"{a}/rec.yuv", "rb").read() != open(f"{b}/rec.yuv", "rb").read()
+
+
+@pytest.mark.parametrize("arg", [1, 5, 99])
+def test_slices_of_skipped_macroblocks(arg):
+    """A still picture repeated: P slices that are (almost) all P_Skip, so slices end on a trailing
+    mb_skip_run (or consist of one); the decoder's more_rbsp_data() must end each slice there."""
+    ensure_built()
+    import numpy as np
+    rng = np.random.default_rng(arg)
+    y = rng.integers(0, 256, (144, 176), dtype=np.uint8)
+    y = ((y.astype(np.uint16) + np.roll(y, 1, 0) + np.roll(y, 1, 1)) // 3).astype(np.uint8)
+    frame = y.tobytes() + y[::2, ::2].tobytes() + y[1::2, 1::2].tobytes()
+    with tempfile.TemporaryDirectory() as d:
+        with open(f"{d}/in.yuv", "wb") as f:
+            f.write(frame * 3)
+        encode(d, [f"InputFile={d}/in.yuv", "FramesToBeEncoded=3", "SliceMode=1", f"SliceArgument={arg}",
+                   "SearchRange=8", "QPFirstFrame=20", "QPRemainingFrame=30"])
+        r = subprocess.run([JMDEC, f"{d}/a.264", f"{d}/dec.yuv"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/rec.yuv", "rb").read()
+        assert len(nal_types(open(f"{d}/a.264", "rb").read())) == 2 + 3 * -(-99 // arg)
