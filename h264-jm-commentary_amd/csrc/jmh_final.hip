@@ -114,6 +114,8 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     const int qp = d.qp;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL;
+    // deblocking filters across slice edges (disable_deblocking_filter_idc 0): picture edges only
+    const bool dbL = mbx > 0, dbT = mby > 0;
     const bool prof = prof_mb_here(d, mbx, mby);
     PSTAMP(16);
     const MbScratch *sc = d.scr + mby * d.mbw + mbx;
@@ -423,13 +425,13 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
                 const int r = i / 20 - 4, c = i % 20 - 4;
                 int v = 0;
                 if (r >= 0 && c >= 0) v = s.rec[16 * r + c];
-                else if ((r < 0 && c >= 0 && avT) || (c < 0 && r >= 0 && avL)) v = d.dbkY[(pix_y + r) * W + pix_x + c];
+                else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL)) v = d.dbkY[(pix_y + r) * W + pix_x + c];
                 s.dy[r + 4][c + 4] = (uint8_t)v;
             } else {
                 const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
                 int v = 0;
                 if (r >= 0 && c >= 0) v = s.cfin[pl][8 * r + c];
-                else if ((r < 0 && c >= 0 && avT) || (c < 0 && r >= 0 && avL))
+                else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL))
                     v = (pl ? d.dbkV : d.dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c];
                 s.dc2[pl][r + 4][c + 4] = (uint8_t)v;
             }
@@ -438,7 +440,7 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
             const int dir = tid >> 4, e = (tid >> 2) & 3, i = tid & 3;
             const bool mb_edge = e == 0;
             int bS = 0;
-            if (filt && !(mb_edge && (dir == 0 ? !avL : !avT))) {
+            if (filt && !(mb_edge && (dir == 0 ? !dbL : !dbT))) {
                 const int bq = dir == 0 ? i * 4 + e : e * 4 + i;
                 const int bp = dir == 0 ? (mb_edge ? i * 4 + 3 : bq - 1) : (mb_edge ? 12 + i : bq - 4);
                 bool intra_p = is_intra, pcoef;
@@ -493,11 +495,11 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
         for (int i = tid; i < 400 + 288; i += NT) {
             if (i < 400) {
                 const int r = i / 20 - 4, c = i % 20 - 4;
-                if ((r >= 0 && c >= 0) || (r >= -3 && r < 0 && c >= 0 && avT) || (c >= -3 && c < 0 && r >= 0 && avL))
+                if ((r >= 0 && c >= 0) || (r >= -3 && r < 0 && c >= 0 && dbT) || (c >= -3 && c < 0 && r >= 0 && dbL))
                     d.dbkY[(pix_y + r) * W + pix_x + c] = s.dy[r + 4][c + 4];
             } else {
                 const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
-                if ((r >= 0 && c >= 0) || (r == -1 && c >= 0 && c < 8 && avT) || (c == -1 && r >= 0 && r < 8 && avL))
+                if ((r >= 0 && c >= 0) || (r == -1 && c >= 0 && c < 8 && dbT) || (c == -1 && r >= 0 && r < 8 && dbL))
                     if (r < 8 && c < 8) (pl ? d.dbkV : d.dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c] = s.dc2[pl][r + 4][c + 4];
             }
         }
