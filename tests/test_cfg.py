@@ -50,3 +50,16 @@ def test_transform8x8_requires_high_profile():
     assert r.returncode != 0 and "ProfileIDC=100" in r.stderr
     r = run("-p", "ProfileIDC=77")
     assert r.returncode != 0 and "ProfileIDC" in r.stderr
+
+
+def test_slice_mode_keys():
+    """SliceMode 1 / SliceArgument accepted; byte-count slices (2) and slice groups (3) rejected,
+    SliceArgument range-checked."""
+    r = run("-p", "SliceMode=2")
+    assert r.returncode != 0 and "SliceMode=2" in r.stderr
+    r = run("-p", "SliceMode=1", "-p", "SliceArgument=0")
+    assert r.returncode != 0 and "out of range" in r.stderr
+    with tempfile.TemporaryDirectory() as d:
+        r = run("-p", "SliceMode=1", "-p", "SliceArgument=3", "-p", "FramesToBeEncoded=1", "-p", "SourceWidth=64",
+                "-p", "SourceHeight=48", "-p", "SearchRange=2", "-p", f"OutputFile={d}/o.264")
+        assert r.returncode == 0, r.stderr
