@@ -199,11 +199,12 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
 
 def read_pmc_traffic():
     """HBM bytes per macroblock of k_mb_analyse measured by rocprofv3 PMC passes
-    (tools/pmc_traffic.sh -> profiles/pmc_traffic.json), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    (tools/pmc_traffic.sh; the figure of the latest pass is kept in tools/pmc_traffic.json, which
+    travels to the GPU box, unlike profiles/), or None."""
+    p = os.path.join(ROOT, "tools", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f)["kernels"]["k_mb_analyse"]["hbm_bytes_per_mb"]
+            return json.load(f)["hbm_bytes_per_mb"]
     except (OSError, ValueError, KeyError, TypeError):
         return None
 
