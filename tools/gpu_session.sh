@@ -13,6 +13,7 @@
 #   benchf8 bench20 with JMH_FINAL_OCC8=1 (k_mb_final's 8-per-CU build for every tick: A/B)
 #   c3      bench.py --config 3 (with CPU baseline)  -> gpurun_out/TAG_c3_bench.json
 #   c3s     config 3 with SliceMode 1, SliceArgument 240 (config 5's one-row slices, 8-bit, CAVLC)
+#   lencodc5 lencodc3 with one slice and with SliceArgument 240 (135 one-row slices per picture)
 #   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
 #   profc3  the same for config 3
 #   pmc     tools/pmc_traffic.sh (HBM bytes + SQ counters, separate passes)
@@ -73,6 +74,14 @@ for s in "$@"; do
                 -p SourceWidth=3840 -p SourceHeight=2160 -p SearchRange=32 -p ProfileIDC=100 -p Transform8x8Mode=1 \
                 -p SearchMode=3 -p WriterThreads=8 -p OutputFile=/tmp/l2160.264 > gpurun_out/${TAG}_lencod2160.log 2>&1 || exit $?
             tail -5 gpurun_out/${TAG}_lencod2160.log ;;
+    lencodc5) run mkyuv 300 python tools/make_yuv.py /tmp/s2160.yuv 3840 2160 30 || exit $?
+            for sl in 0 240; do
+              run lencodc5_$sl 900 h264-jm-commentary_amd/host/build/lencod -p InputFile=/tmp/s2160.yuv -p FramesToBeEncoded=30 \
+                -p SourceWidth=3840 -p SourceHeight=2160 -p SearchRange=32 -p ProfileIDC=100 -p Transform8x8Mode=1 \
+                -p SearchMode=3 -p WriterThreads=8 -p SliceMode=$((sl > 0)) -p SliceArgument=$((sl > 0 ? sl : 50)) \
+                -p OutputFile=/tmp/l2160_$sl.264 > gpurun_out/${TAG}_lencod2160_slices$sl.log 2>&1 || exit $?
+              tail -3 gpurun_out/${TAG}_lencod2160_slices$sl.log
+            done ;;
     pmc)    run pmc 900 bash tools/pmc_traffic.sh "$TAG" || exit $? ;;
     *)      echo "unknown step $s"; exit 2 ;;
   esac
