@@ -4,8 +4,8 @@
   python tools/make_golden.py          # rewrite tests/golden/*
 
 Fixtures (all data; no reference source text):
-  manifest.json   sha256 of lencod_cpu bitstreams + reconstructions for three encoder.cfg
-                  configurations (the same ones the GPU bitstream test runs), and of the
+  manifest.json   sha256 of lencod_cpu bitstreams + reconstructions for four encoder.cfg
+                  configurations (the first three as in the GPU bitstream test; one with slices), and of the
                   per-picture jmh_mb_result arrays + reconstructions of a 64x48 I-P-P sequence
   tq4x4.npz       dct_luma vectors: residual/prediction inputs and levels/recon/cost/nonzero
                   outputs at QP 0, 12, 28, 51, intra and inter rounding
@@ -37,6 +37,9 @@ LENCOD_CONFIGS = [
      "IntraPeriod=3", "QPRemainingFrame=33"],
     ["InputFile=synthetic:3", "FramesToBeEncoded=3", "SourceWidth=200", "SourceHeight=120", "SearchRange=8",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=2", "LoopFilterBetaOffset=-1"],
+    # SliceMode 1 (docs/JM_SEMANTICS.md item 47): 22-MB slices, EPZS + 8x8 transform
+    ["InputFile=synthetic:4", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "SliceMode=1", "SliceArgument=22"],
 ]
 SEQ = dict(w=64, h=48, seed=21, frames=3, qp=28, search_range=16)
 
