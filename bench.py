@@ -198,15 +198,18 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
 
 
 def read_pmc_traffic():
-    """HBM bytes per macroblock of k_mb_analyse measured by rocprofv3 PMC passes
-    (tools/pmc_traffic.sh; the figure of the latest pass is kept in tools/pmc_traffic.json, which
-    travels to the GPU box, unlike profiles/), or None."""
+    """(HBM bytes per macroblock of k_mb_analyse, source description) from the rocprofv3 PMC passes
+    of tools/pmc_traffic.sh, or (None, None).  The figure of the latest pass is kept in
+    tools/pmc_traffic.json (it travels to the GPU box, unlike profiles/); it is a committed
+    measurement of an earlier run of the same kernel, not of this run."""
     p = os.path.join(ROOT, "tools", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f)["hbm_bytes_per_mb"]
+            j = json.load(f)
+        src = f"tools/pmc_traffic.json ({j.get('source', 'rocprofv3 PMC')}; {j.get('calibration', 'uncalibrated')})"
+        return j["hbm_bytes_per_mb"], src
     except (OSError, ValueError, KeyError, TypeError):
-        return None
+        return None, None
 
 
 # ------------------------------------------------------------------------------------------
@@ -248,6 +251,18 @@ def free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def pin_rank(local, nlocal):
+    """each stream's host work (launches, result copies) on cores of its own — pin the
+    rank to an equal share of the cores this process may use, before anything touches the GPU."""
+    cpus = sorted(os.sched_getaffinity(0))
+    share = len(cpus) // max(1, nlocal)
+    if share < 1:
+        return None
+    mine = set(cpus[local * share:(local + 1) * share])
+    os.sched_setaffinity(0, mine)
+    return sorted(mine)
 
 
 def launch(n):
@@ -300,6 +315,7 @@ def main():
         return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    pinned = pin_rank(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))) if world > 1 else None
     size = tuple(int(v) for v in args.size.split("x")) if args.size else None
     cfg = use_config(args.config, size)
     SLICE_MBS = max(0, args.slice_mbs)
@@ -331,17 +347,20 @@ def main():
         res, rec = enc.encode(*frames[1], jm.JMH_P_SLICE, QP, deblock=stream.deblock)
         np.savez(os.path.join(args.dump, f"rank{rank}.npz"), res=res, y=rec[0], u=rec[1], v=rec[2],
                  slots=np.array(stream.slots_used), device=device, warmup=stream.warmup_steps)
-    mine = {"rank": rank, "device": device, "dt": dt, "pictures_completed": tm.pictures_done}
+    mine = {"rank": rank, "device": device, "dt": dt, "pictures_completed": tm.pictures_done,
+            "cpus": None if pinned is None else f"{pinned[0]}-{pinned[-1]}" if pinned == list(range(pinned[0], pinned[-1] + 1))
+            else ",".join(map(str, pinned))}
     everyone = [mine]
     if dist is not None:
         everyone = [None] * world
         dist.all_gather_object(everyone, mine)
+    complete = all(e["pictures_completed"] == args.steps for e in everyone)
     if rank != 0:
         if dist is not None:
             dist.barrier()
         enc.sync()                                        # complete the pictures still in flight
         enc.close()
-        return 0
+        return 0 if complete else 4
 
     value = world * args.steps * DISP_W * DISP_H / 1e6 / dt
     pictures = max(1, tm.pictures)
@@ -354,7 +373,7 @@ def main():
     achieved_tads = ad_per_launch / (an_launch_ms * 1e-3) / 1e12
     peak_tads, peak_src = sad_peak()
     mb_ms_pic = tm.mb_ms / pictures
-    pmc = read_pmc_traffic() if args.config == 2 and search_mode == 0 else None   # PMC pass is for config 2
+    pmc, pmc_src = read_pmc_traffic() if args.config == 2 and search_mode == 0 else (None, None)   # config 2 pass
     sm_name = {0: "FFS SearchMode=0", -1: "full search SearchMode=-1", 3: "EPZS SearchMode=3"}[search_mode]
     ffs = search_mode == 0
     hbm = {
@@ -364,6 +383,7 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
         "traffic": round(pmc * mbs_per_launch) if pmc else None,
+        "traffic_source": pmc_src,
         "algorithmic_bytes_per_launch": round(bytes_per_launch),
     }
     launch_info = {
@@ -376,7 +396,7 @@ def main():
     if ffs:   # config 2: the FFS SAD table binds -> VALU roofline; HBM beside it
         roofline = dict(bound="valu", achieved=round(achieved_tads, 4), peak=round(peak_tads, 2),
                         unit="T abs-diff/s", frac=round(achieved_tads / peak_tads, 5),
-                        traffic=hbm["traffic"], peak_source=peak_src,
+                        traffic=hbm["traffic"], traffic_source=pmc_src, peak_source=peak_src,
                         algorithmic_ad_per_launch=round(ad_per_launch), **launch_info, hbm=hbm)
     else:     # EPZS: latency-bound; HBM is the roofline the north star names
         roofline = dict(hbm, **launch_info)
@@ -406,6 +426,8 @@ def main():
             "warmup_steps_run": stream.warmup_steps,
             "pictures_completed": [e["pictures_completed"] for e in everyone],
             "per_rank_s": [round(e["dt"], 5) for e in everyone],
+            "per_rank_mp_s": [round(args.steps * DISP_W * DISP_H / 1e6 / e["dt"], 3) for e in everyone],
+            "per_rank_cpus": [e["cpus"] for e in everyone],
             "note": "steady state: the pipeline is full at both ends (barrier + wait for the issued launches, "
                     "pictures in flight are not drained); exactly `steps` pictures complete inside",
         },
@@ -420,10 +442,10 @@ def main():
             "note": "jmh_frame_push/pop with host pictures: source H2D + results/recon/deblocked D2H, "
                     "steady state; latency = one picture on an empty pipeline (fill + drain)",
         },
-        "verified": None,
+        "verified": None if complete else False,
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and complete:
         with tempfile.TemporaryDirectory() as tmp:
             out["cpu_baseline"] = cpu_baseline(args.config, search_mode, tmp)
             out["verified"] = verify_against_oracle(jm, os.path.join(tmp, "oracle_seed0.npz"), search_mode, cfg["t8"],
@@ -436,6 +458,10 @@ def main():
     if out["verified"] is False:
         print("bench.py: GPU results differ from the oracle", file=sys.stderr)
         return 3
+    if not complete:
+        print("bench.py: a rank completed a different number of pictures than --steps in the timed region",
+              file=sys.stderr)
+        return 4
     return 0
 
 

@@ -9,7 +9,7 @@
  */
 #include <stdlib.h>
 #include <string.h>
-#include "jmhost.h"
+#include "bitstream_int.h"
 
 /* ---- bit writer ---------------------------------------------------------------------- */
 void jm_bits_init(jm_bits *b) { memset(b, 0, sizeof(*b)); }
@@ -39,6 +39,7 @@ void jm_trailing_bits(jm_bits *b) {
     while (b->nacc) jm_put(b, 0, 1);
 }
 void jm_bits_align_flush(jm_bits *b) { while (b->nacc) jm_put(b, 0, 1); }
+void jm_bits_append(jm_bits *b, const jm_bits *src) { for (long i = 0; i < src->len; i++) put_byte(b, src->buf[i]); }
 
 void jm_write_nal(jm_bits *out, int nal_ref_idc, int nal_type, const jm_bits *rbsp) {
     put_byte(out, 0); put_byte(out, 0); put_byte(out, 0); put_byte(out, 1);
@@ -89,7 +90,7 @@ void jm_write_sps(jm_bits *b, const jm_seq *s) {
 void jm_write_pps(jm_bits *b, const jm_seq *s) {
     jm_put_ue(b, 0);                         /* pic_parameter_set_id */
     jm_put_ue(b, 0);                         /* seq_parameter_set_id */
-    jm_put(b, 0, 1);                         /* entropy_coding_mode_flag (CAVLC) */
+    jm_put(b, s->entropy_coding ? 1 : 0, 1); /* entropy_coding_mode_flag (0 CAVLC, 1 CABAC) */
     jm_put(b, 0, 1);                         /* pic_order_present_flag */
     jm_put_ue(b, 0);                         /* num_slice_groups_minus1 */
     jm_put_ue(b, s->num_ref_frames - 1);     /* num_ref_idx_l0_active_minus1 */
@@ -222,20 +223,10 @@ static int write_residual_block(jm_bits *b, const int16_t *coeffs, int n, int nC
 }
 
 /* ---- slice ----------------------------------------------------------------------------- */
-typedef struct {
-    const jm_seq *s;
-    int16_t *mv;        /* per 4x4 [2] of the picture, final values (written MBs) */
-    int8_t *ref;        /* per 4x4, -1 intra / not yet written                      */
-    int8_t *ipm;        /* per 4x4 Intra4x4PredMode, -1: MB not I4x4               */
-    uint32_t *written;  /* per MB: the stamp of the slice that wrote it             */
-    uint32_t stamp;     /* the current slice's stamp (neighbours of other slices are not
-                           available, 6.4.8; the buffers serve every slice of a picture) */
-    uint8_t *tc;        /* per MB: 16 luma + 4 Cb + 4 Cr total_coeff               */
-} wctx;
-
-static int mb_ok(const wctx *w, int mx, int my) {
+int jm_w_mb_ok(const wctx *w, int mx, int my) {
     return mx >= 0 && my >= 0 && mx < w->s->mbw && my < w->s->mbh && w->written[my * w->s->mbw + mx] == w->stamp;
 }
+#define mb_ok jm_w_mb_ok
 /* neighbour 4x4 in luma pixels relative to MB (mx,my): returns availability + 4x4 index */
 static int nb(const wctx *w, int mx, int my, int xN, int yN, int *idx, int cur_ok) {
     int tx, ty;
@@ -252,7 +243,7 @@ static int nb(const wctx *w, int mx, int my, int xN, int yN, int *idx, int cur_o
 
 /* normative MVP (8.4.1.3) of the partition at (bx,by) size bw x bh (pixels, MB relative);
  * the current MB's mv/ref entries must already hold its final values. */
-static void mvp(const wctx *w, int mx, int my, int bx, int by, int bw, int bh, int *p) {
+void jm_w_mvp(const wctx *w, int mx, int my, int bx, int by, int bw, int bh, int *p) {
     int ia = 0, ib = 0, ic = 0, id = 0;
     int aa = nb(w, mx, my, bx - 1, by, &ia, 1), ab = nb(w, mx, my, bx, by - 1, &ib, 1);
     int ac = nb(w, mx, my, bx + bw, by - 1, &ic, 1), ad = nb(w, mx, my, bx - 1, by - 1, &id, 1);
@@ -282,7 +273,7 @@ static void mvp(const wctx *w, int mx, int my, int bx, int by, int bw, int bh, i
 
 static void put_mvd(jm_bits *b, const wctx *w, int mx, int my, const jmh_mb_result *r, int bx, int by, int bw, int bh) {
     int p[2];
-    mvp(w, mx, my, bx, by, bw, bh, p);
+    jm_w_mvp(w, mx, my, bx, by, bw, bh, p);
     int k = (by >> 2) * 4 + (bx >> 2);
     jm_put_se(b, r->mv[k][0] - p[0]);
     jm_put_se(b, r->mv[k][1] - p[1]);
@@ -302,12 +293,19 @@ static int calc_nc(const wctx *w, int mx, int my, int comp, int x4, int y4, cons
     return 0;
 }
 
-static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r, int slice_p) {
-    int mbt = r->mb_type, cbp = r->cbp, W4 = w->s->mbw * 4;
-    int is_i8 = mbt == JMH_I8MB, is_i4 = mbt == JMH_I4MB || is_i8, is_i16 = mbt == JMH_I16MB;
-    int is_intra = is_i4 || is_i16, t8 = r->transform_8x8;   /* is_i4: I_NxN (4x4 or 8x8) */
-    int cbpl = cbp & 15, cbpc = cbp >> 4;
-    /* mark the MB's final motion / intra data (needed by its own MVP / MPM derivations) */
+/* predIntra4x4PredMode / predIntra8x8PredMode (8.3.1.1 / 8.3.2.1): DC unless both the left and
+ * the upper neighbour exist; a neighbour that is not I_NxN counts as DC (2) */
+int jm_w_mpm(const wctx *w, int mx, int my, int x4, int y4) {
+    int ia = 0, ib = 0;
+    int aa = nb(w, mx, my, 4 * x4 - 1, 4 * y4, &ia, 1), ab = nb(w, mx, my, 4 * x4, 4 * y4 - 1, &ib, 1);
+    if (!aa || !ab) return 2;
+    int ma = w->ipm[ia] < 0 ? 2 : w->ipm[ia], mb = w->ipm[ib] < 0 ? 2 : w->ipm[ib];
+    return ma < mb ? ma : mb;
+}
+
+void jm_w_mark_mb(wctx *w, int mx, int my, const jmh_mb_result *r, int skip) {
+    int mbt = r->mb_type, W4 = w->s->mbw * 4;
+    int is_i4 = !skip && (mbt == JMH_I4MB || mbt == JMH_I8MB), is_intra = !skip && (is_i4 || mbt == JMH_I16MB);
     for (int k = 0; k < 16; k++) {
         int a = (my * 4 + (k >> 2)) * W4 + mx * 4 + (k & 3);
         w->mv[2 * a] = is_intra ? 0 : r->mv[k][0];
@@ -316,6 +314,15 @@ static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r,
         w->ipm[a] = is_i4 ? r->ipred[k] : -1;
     }
     w->written[my * w->s->mbw + mx] = w->stamp;
+}
+
+static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r, int slice_p) {
+    int mbt = r->mb_type, cbp = r->cbp;
+    int is_i8 = mbt == JMH_I8MB, is_i4 = mbt == JMH_I4MB || is_i8, is_i16 = mbt == JMH_I16MB;
+    int is_intra = is_i4 || is_i16, t8 = r->transform_8x8;   /* is_i4: I_NxN (4x4 or 8x8) */
+    int cbpl = cbp & 15, cbpc = cbp >> 4;
+    /* mark the MB's final motion / intra data (needed by its own MVP / MPM derivations) */
+    jm_w_mark_mb(w, mx, my, r, 0);
     int ue_type;
     if (is_i16) {
         int t = 1 + r->i16mode + 4 * cbpc + (cbpl ? 12 : 0);
@@ -327,31 +334,10 @@ static int write_mb(jm_bits *b, wctx *w, int mx, int my, const jmh_mb_result *r,
     if (mbt == JMH_P8x8)
         for (int i = 0; i < 4; i++) jm_put_ue(b, r->b8mode[i] - 4);
     if (is_i4 && w->s->transform_8x8_mode) jm_put(b, is_i8, 1);   /* transform_size_8x8_flag */
-    if (is_i8) {
-        for (int b8 = 0; b8 < 4; b8++) {           /* prev_intra8x8_pred_mode / rem (8.3.2.1) */
-            int x4 = (b8 & 1) * 2, y4 = (b8 >> 1) * 2, ia = 0, ib = 0;
-            int aa = nb(w, mx, my, 4 * x4 - 1, 4 * y4, &ia, 1), ab = nb(w, mx, my, 4 * x4, 4 * y4 - 1, &ib, 1);
-            int pred = 2;
-            if (aa && ab) {
-                int ma = w->ipm[ia] < 0 ? 2 : w->ipm[ia], mb = w->ipm[ib] < 0 ? 2 : w->ipm[ib];
-                pred = ma < mb ? ma : mb;
-            }
-            int m = r->ipred[y4 * 4 + x4];
-            if (m == pred) jm_put(b, 1, 1);
-            else { jm_put(b, 0, 1); jm_put(b, m < pred ? m : m - 1, 3); }
-        }
-    } else if (is_i4) {
-        for (int blk = 0; blk < 16; blk++) {
+    if (is_i4) {   /* prev_intra4x4_pred_mode_flag / rem (16 blocks), or the 8x8 ones (4 blocks) */
+        for (int blk = 0; blk < 16; blk += is_i8 ? 4 : 1) {
             int x4 = ((blk >> 2) & 1) * 2 + (blk & 1), y4 = (blk >> 3) * 2 + ((blk >> 1) & 1);
-            int ia = 0, ib = 0;
-            int aa = nb(w, mx, my, 4 * x4 - 1, 4 * y4, &ia, 1), ab = nb(w, mx, my, 4 * x4, 4 * y4 - 1, &ib, 1);
-            int pred;
-            if (!aa || !ab) pred = 2;
-            else {
-                int ma = w->ipm[ia] < 0 ? 2 : w->ipm[ia], mb = w->ipm[ib] < 0 ? 2 : w->ipm[ib];
-                pred = ma < mb ? ma : mb;
-            }
-            int m = r->ipred[y4 * 4 + x4];
+            int pred = jm_w_mpm(w, mx, my, x4, y4), m = r->ipred[y4 * 4 + x4];
             if (m == pred) jm_put(b, 1, 1);
             else { jm_put(b, 0, 1); jm_put(b, m < pred ? m : m - 1, 3); }
         }
@@ -410,6 +396,8 @@ struct jm_slice_writer {
     wctx w;
     int skip_run, slice_p;
     int open;                  /* header written and buffers allocated */
+    jm_cabac *cab;             /* SymbolMode 1: the CABAC coder (NULL: CAVLC)                 */
+    long bins;                 /* CABAC bins of the picture's slices                           */
 };
 
 /* slice_header (7.3.3) */
@@ -426,6 +414,8 @@ static void write_slice_header(jm_bits *b, const jm_seq *s, const jm_slice *sl) 
     }
     if (sl->idr) { jm_put(b, 0, 1); jm_put(b, 0, 1); } /* no_output_of_prior_pics, long_term */
     else jm_put(b, 0, 1);                             /* adaptive_ref_pic_marking_mode_flag */
+    if (s->entropy_coding && sl->slice_type != JMH_I_SLICE)
+        jm_put_ue(b, s->cabac_init_idc);              /* cabac_init_idc (FixedModelNumber) */
     jm_put_se(b, sl->qp - 26);                        /* slice_qp_delta */
     if (s->lf_params_flag) {
         jm_put_ue(b, s->lf_disable);
@@ -453,10 +443,15 @@ jm_slice_writer *jm_slice_begin(jm_bits *b, const jm_seq *s, const jm_slice *sl)
     w->stamp = 1;
     sw->slice_p = sl->slice_type == JMH_P_SLICE;
     sw->open = 1;
+    if (s->entropy_coding) {
+        if (!(sw->cab = jm_cabac_new(s))) { sw->open = 0; jm_slice_end(sw); return NULL; }
+        jm_cabac_slice_start(sw->cab, b, sl->slice_type, sl->qp);
+    }
     return sw;
 }
 
 static void close_slice_data(jm_slice_writer *sw) {
+    if (sw->cab) { sw->bins += jm_cabac_slice_end(sw->cab); return; }   /* ends with the stop bit */
     if (sw->slice_p && sw->skip_run) jm_put_ue(sw->b, sw->skip_run);
     sw->skip_run = 0;
     jm_trailing_bits(sw->b);
@@ -468,12 +463,14 @@ void jm_slice_restart(jm_slice_writer *sw, jm_bits *b, const jm_slice *sl) {
     sw->b = b;
     sw->w.stamp++;
     sw->slice_p = sl->slice_type == JMH_P_SLICE;
+    if (sw->cab) jm_cabac_slice_start(sw->cab, b, sl->slice_type, sl->qp);
 }
 
 void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
     wctx *w = &sw->w;
     const jm_seq *s = w->s;
     int mx = a % s->mbw, my = a / s->mbw, W4 = s->mbw * 4;
+    if (sw->cab) { jm_cabac_write_mb(sw->cab, w, mx, my, r, sw->slice_p); return; }
     if (sw->slice_p && r->mb_type == JMH_PSKIP) {
         for (int k = 0; k < 16; k++) {
             int i = (my * 4 + (k >> 2)) * W4 + mx * 4 + (k & 3);
@@ -489,11 +486,14 @@ void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
     write_mb(sw->b, w, mx, my, r, sw->slice_p);
 }
 
-void jm_slice_end(jm_slice_writer *sw) {
-    if (!sw) return;
+long jm_slice_end(jm_slice_writer *sw) {
+    if (!sw) return 0;
     if (sw->open) close_slice_data(sw);
+    const long bins = sw->bins;
+    jm_cabac_free(sw->cab);
     free(sw->w.mv); free(sw->w.ref); free(sw->w.ipm); free(sw->w.written); free(sw->w.tc);
     free(sw);
+    return bins;
 }
 
 int jm_write_slice(jm_bits *b, const jm_seq *s, const jm_slice *sl, const jmh_mb_result *const *res) {

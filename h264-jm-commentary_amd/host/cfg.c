@@ -51,6 +51,8 @@ static const map_entry Map[] = {
     {"Transform8x8Mode", 0, OFF(transform_8x8_mode), 0, 2},
     {"LevelIDC", 0, OFF(level_idc), 9, 62},
     {"SymbolMode", 0, OFF(symbol_mode), 0, 1},
+    {"ContextInitMethod", 0, OFF(context_init_method), 0, 1},
+    {"FixedModelNumber", 0, OFF(model_number), 0, 2},
     {"LoopFilterParametersFlag", 0, OFF(lf_params_flag), 0, 1},
     {"LoopFilterDisable", 0, OFF(lf_disable), 0, 1},
     {"LoopFilterAlphaC0Offset", 0, OFF(lf_alpha), -6, 6},
@@ -172,11 +174,13 @@ static int parse_file(jm_input *inp, const char *fn, char *err, int errlen) {
 
 int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->rdopt != 0) { snprintf(err, errlen, "RDOptimization=%d not supported (RDO-off path only)", inp->rdopt); return -1; }
-    if (inp->symbol_mode != 0) { snprintf(err, errlen, "SymbolMode=1 (CABAC) not supported in this build"); return -1; }
+    if (inp->symbol_mode && inp->profile_idc == 66) { snprintf(err, errlen, "SymbolMode=1 (CABAC) is not allowed in the Baseline profile (ProfileIDC=66)"); return -1; }
+    if (inp->symbol_mode && inp->context_init_method) { snprintf(err, errlen, "ContextInitMethod=1 (adaptive CABAC model selection) not supported (0: FixedModelNumber)"); return -1; }
+    if (inp->symbol_mode && inp->model_number) { snprintf(err, errlen, "FixedModelNumber=%d not supported (0: cabac_init_idc 0)", inp->model_number); return -1; }
     if (inp->search_mode != 0 && inp->search_mode != -1 && inp->search_mode != 3) { snprintf(err, errlen, "SearchMode=%d not supported (use -1, 0 or 3)", inp->search_mode); return -1; }
     if (inp->num_ref_frames != 1) { snprintf(err, errlen, "NumberReferenceFrames=%d not supported (1)", inp->num_ref_frames); return -1; }
     if (inp->constrained_intra) { snprintf(err, errlen, "UseConstrainedIntraPred=1 not supported"); return -1; }
-    if (inp->profile_idc != 66 && inp->profile_idc != 100) { snprintf(err, errlen, "ProfileIDC=%d not supported (66 or 100)", inp->profile_idc); return -1; }
+    if (inp->profile_idc != 66 && inp->profile_idc != 77 && inp->profile_idc != 100) { snprintf(err, errlen, "ProfileIDC=%d not supported (66, 77 or 100)", inp->profile_idc); return -1; }
     if (inp->transform_8x8_mode == 2) { snprintf(err, errlen, "Transform8x8Mode=2 not supported (0 or 1)"); return -1; }
     if (inp->transform_8x8_mode && inp->profile_idc < 100) { snprintf(err, errlen, "Transform8x8Mode=1 requires ProfileIDC=100 (High)"); return -1; }
     if ((inp->width & 1) || (inp->height & 1)) { snprintf(err, errlen, "Source size must be even"); return -1; }

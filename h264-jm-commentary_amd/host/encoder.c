@@ -61,10 +61,12 @@ static void encode_one_slice(const jm_seq *s, int first) {
 static int encode_picture_slices(jm86_img *im, const jm_seq *s, const jm_slice *sl0, const jmh_frame_params *fp,
                                  const jm_pic *cur, const jm_pic *ref, jm_bits *out) {
     const int nmb = s->mbw * s->mbh, step = s->slice_mbs > 0 ? s->slice_mbs : nmb;
+    const long len0 = out->len;
     jm_slice sl = *sl0;
     sl.first_mb = 0;
     jm_bits rbsp[2];             /* the slice being written and the next one (alternating) */
-    int k = 0;
+    int k = 0, nslices = 0;
+    long bins = 0;
     jm_bits_init(&rbsp[0]);
     jm_slice_writer *w = jm_slice_begin(&rbsp[0], s, &sl);
     if (!w) { jm_bits_free(&rbsp[0]); return JMH_E_OOM; }
@@ -73,7 +75,7 @@ static int encode_picture_slices(jm86_img *im, const jm_seq *s, const jm_slice *
     for (int first = 0; first < nmb; first += step) {
         encode_one_slice(s, first);
         if (first + step >= nmb) {
-            jm_slice_end(w);
+            bins = jm_slice_end(w);
         } else {
             jm_bits_init(&rbsp[k ^ 1]);
             sl.first_mb = first + step;
@@ -81,9 +83,22 @@ static int encode_picture_slices(jm86_img *im, const jm_seq *s, const jm_slice *
         }
         jm_write_nal(out, sl0->idr ? 3 : 2, sl0->idr ? 5 : 1, &rbsp[k]);
         jm_bits_free(&rbsp[k]);
+        nslices++;
         k ^= 1;
     }
     im->writer = NULL;
+    if (s->entropy_coding) {
+        /* cabac_zero_words (7.4.2.10, 9.3.4.6): BinCountsInNALunits <= 32/3 * NumBytesInVclNALunits
+           + RawMbBits * PicSizeInMbs / 32 (RawMbBits = 3072 at 8-bit 4:2:0); scaled by 3.  Each word
+           appended to the last slice is 0x000003 in the byte stream (emulation prevention). */
+        const long bytes = out->len - len0 - 4L * nslices;          /* NAL units, no start codes */
+        const long excess = 3 * bins - 288L * nmb - 32 * bytes;
+        for (long z = excess > 0 ? (excess + 95) / 96 : 0; z > 0; z--) {
+            static const uint8_t zw[3] = {0, 0, 3};
+            jm_bits t = {(uint8_t *)zw, 3, 3, 0, 0};
+            jm_bits_append(out, &t);
+        }
+    }
     return JMH_OK;
 }
 
@@ -169,6 +184,19 @@ static void pool_wait(wpool_t *P, int k) {
     pthread_mutex_unlock(&P->mu);
 }
 
+/* job state is shared with the writer threads: read and reset it under the pool lock only */
+static int job_busy(wpool_t *P, int k) {
+    pthread_mutex_lock(&P->mu);
+    const int st = P->jobs[k].state;
+    pthread_mutex_unlock(&P->mu);
+    return st != 0;
+}
+static void job_release(wpool_t *P, int k) {
+    pthread_mutex_lock(&P->mu);
+    P->jobs[k].state = 0;
+    pthread_mutex_unlock(&P->mu);
+}
+
 int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *log) {
     memset(st, 0, sizeof(*st));
     jmh_config cfg;
@@ -187,6 +215,8 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     s.lf_alpha = inp->lf_alpha; s.lf_beta = inp->lf_beta;
     s.constrained_intra = inp->constrained_intra;
     s.transform_8x8_mode = inp->transform_8x8_mode;
+    s.entropy_coding = inp->symbol_mode;
+    s.cabac_init_idc = inp->model_number;
 
     FILE *fin = NULL, *fout = NULL, *frec = NULL;
     uint64_t seed = 0;
@@ -209,38 +239,51 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     typedef struct { jm_pic cur; jmh_frame_params fp; int f, is_i, frame_num; } pend_t;
     pend_t *pend = (pend_t *)calloc(plen, sizeof(pend_t));
     jm_pic rec;
+    memset(&rec, 0, sizeof(rec));
     int alloc_fail = !pend || jm_pic_alloc(&rec, W, H);
     for (int k = 0; k < plen && !alloc_fail; k++) alloc_fail = jm_pic_alloc(&pend[k].cur, W, H);
-    if (alloc_fail) return JMH_E_OOM;
+    if (alloc_fail) {
+        if (pend) for (int k = 0; k < plen; k++) jm_pic_free(&pend[k].cur);
+        free(pend);
+        jm_pic_free(&rec);
+        if (fin) fclose(fin);
+        fclose(fout);
+        if (frec) fclose(frec);
+        return JMH_E_OOM;
+    }
     int nmb = s.mbw * s.mbh;
     const jmh_mb_result **res = (const jmh_mb_result **)malloc(sizeof(*res) * nmb);
     jm86_img im;
-    if (!res || jm86_init(&im, inp, be, W, H)) return JMH_E_OOM;
+    memset(&im, 0, sizeof(im));
     wpool_t pool;
     memset(&pool, 0, sizeof(pool));
-    if (nwr) {
-        pool.nj = nj; pool.s = &s; pool.inp = inp; pool.nth = nwr;
-        pool.jobs = (wjob_t *)calloc(nj, sizeof(wjob_t));
-        pool.queue = (int *)calloc(nj, sizeof(int));
-        pool.th = (pthread_t *)calloc(nwr, sizeof(pthread_t));
-        if (!pool.jobs || !pool.queue || !pool.th) return JMH_E_OOM;
-        for (int k = 0; k < nj; k++) {
-            if (jm86_init(&pool.jobs[k].im, inp, be, W, H) || jm_pic_alloc(&pool.jobs[k].rec, W, H)) return JMH_E_OOM;
-            pool.jobs[k].im.res = pool.jobs[k].im.mb_data;   /* results copied in at pop */
-            jm_bits_init(&pool.jobs[k].out);
-        }
-        img = &im;   /* jm86_init of the jobs set this thread's img */
-        pthread_mutex_init(&pool.mu, NULL);
-        pthread_cond_init(&pool.cv_work, NULL);
-        pthread_cond_init(&pool.cv_done, NULL);
-        for (int k = 0; k < nwr; k++)
-            if (pthread_create(&pool.th[k], NULL, writer_main, &pool)) return JMH_E_OOM;
-    }
+    int st_ret = 0, njobs_init = 0, nstarted = 0, pool_sync = 0;
     long jseq = 0, jflushed = 0;   /* jobs submitted / emitted (picture order) */
     double copy_ms = 0, write_ms = 0;
     double read_ms = 0, push_ms = 0, pop_ms = 0, flush_ms = 0;   /* main thread, for the summary */
     jm_bits out, rbsp;
     jm_bits_init(&out); jm_bits_init(&rbsp);
+    if (!res || jm86_init(&im, inp, be, W, H)) { st_ret = JMH_E_OOM; goto cleanup; }
+    if (nwr) {
+        pool.nj = nj; pool.s = &s; pool.inp = inp; pool.nth = nwr;
+        pool.jobs = (wjob_t *)calloc(nj, sizeof(wjob_t));
+        pool.queue = (int *)calloc(nj, sizeof(int));
+        pool.th = (pthread_t *)calloc(nwr, sizeof(pthread_t));
+        if (!pool.jobs || !pool.queue || !pool.th) { st_ret = JMH_E_OOM; goto cleanup; }
+        for (; njobs_init < nj; njobs_init++) {
+            wjob_t *j = &pool.jobs[njobs_init];
+            jm_bits_init(&j->out);
+            if (jm86_init(&j->im, inp, be, W, H) || jm_pic_alloc(&j->rec, W, H)) { njobs_init++; st_ret = JMH_E_OOM; goto cleanup; }
+            j->im.res = j->im.mb_data;   /* results copied in at pop */
+        }
+        img = &im;   /* jm86_init of the jobs set this thread's img */
+        pthread_mutex_init(&pool.mu, NULL);
+        pthread_cond_init(&pool.cv_work, NULL);
+        pthread_cond_init(&pool.cv_done, NULL);
+        pool_sync = 1;
+        for (; nstarted < nwr; nstarted++)
+            if (pthread_create(&pool.th[nstarted], NULL, writer_main, &pool)) { st_ret = JMH_E_OOM; goto cleanup; }
+    }
     jm_write_sps(&rbsp, &s); jm_write_nal(&out, 3, 7, &rbsp); jm_bits_free(&rbsp);
     jm_write_pps(&rbsp, &s); jm_write_nal(&out, 3, 8, &rbsp); jm_bits_free(&rbsp);
     long header_bits = out.len * 8;
@@ -254,7 +297,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         fprintf(log, " Frame  Bit/pic  QP   SnrY    SnrU    SnrV    Time(ms) MET(ms) Frm/Fld  I D\n");
     }
     double t_start = now_ms();
-    int st_ret = 0, frame_num = 0, head = 0, count = 0;
+    int frame_num = 0, head = 0, count = 0;
     /* the rest of encode_one_frame for a picture whose macroblock results are available:
        slice (CAVLC), deblocking / next reference, recon file, PSNR, report line */
     /* emit a finished job: NAL unit, recon, statistics, report line (picture order) */
@@ -275,7 +318,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
             fprintf(log, "%4d(%s) %8ld   %2d %7.4f %7.4f %7.4f %9.1f %7.1f    FRM\n", fj_->f,          \
                     fj_->is_i ? "IDR" : " P ", fj_->pic_bits, fj_->fp.qp, fj_->py, fj_->pu, fj_->pv,       \
                     fj_->write_ms + fj_->met, fj_->met);                                              \
-        fj_->state = 0;                                                                             \
+        job_release(&pool, (int)(fj_ - pool.jobs));                                                 \
         jflushed++;                                                                                \
         flush_ms += now_ms() - tf_;                                                                 \
     } while (0)
@@ -284,7 +327,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     do {                                                                                           \
         pend_t *p_ = (P);                                                                          \
         wjob_t *j_ = &pool.jobs[jseq % nj];                                                       \
-        if (j_->state) { FLUSH_JOB(j_); if (st_ret) break; }                                       \
+        if (job_busy(&pool, (int)(j_ - pool.jobs))) { FLUSH_JOB(j_); if (st_ret) break; }          \
         double t1 = now_ms();                                                                      \
         const jmh_mb_result *r0_ = be->mb_result(be->ctx, 0);                                      \
         if (nmb > 1 && be->mb_result(be->ctx, nmb - 1) != r0_ + (nmb - 1)) { st_ret = JMH_E_STATE; break; } \
@@ -309,7 +352,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         sl.idr = p_->f == 0; sl.slice_type = p_->fp.slice_type; sl.frame_num = p_->frame_num;      \
         sl.poc_lsb = 2 * p_->f; sl.idr_pic_id = 0; sl.qp = p_->fp.qp;                              \
         sl.first_mb = 0;                                                                           \
-        if (encode_picture_slices(&im, &s, &sl, &p_->fp, &p_->cur, &rec, &out)) { st_ret = JMH_E_OOM; break; } \
+        { int e_ = encode_picture_slices(&im, &s, &sl, &p_->fp, &p_->cur, &rec, &out); if (e_) { st_ret = e_; break; } } \
         double t2 = now_ms();                                                                      \
         st->entropy_ms += t2 - t1;                                                                 \
         long pic_bits = out.len * 8;                                                               \
@@ -395,20 +438,25 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     #undef EMIT
     #undef SUBMIT
     #undef FLUSH_JOB
-    if (nwr) {
+    st->total_ms = now_ms() - t_start;
+cleanup:
+    /* one teardown for every exit: stop and join the writer threads that started, free what
+       was allocated (also after a partial setup) */
+    if (nstarted) {
         pthread_mutex_lock(&pool.mu);
         pool.stop = 1;
         pthread_cond_broadcast(&pool.cv_work);
         pthread_mutex_unlock(&pool.mu);
-        for (int k = 0; k < nwr; k++) pthread_join(pool.th[k], NULL);
-        for (int k = 0; k < nj; k++) { jm86_free(&pool.jobs[k].im); jm_pic_free(&pool.jobs[k].rec); jm_bits_free(&pool.jobs[k].out); }
+        for (int k = 0; k < nstarted; k++) pthread_join(pool.th[k], NULL);
+    }
+    for (int k = 0; k < njobs_init; k++) { jm86_free(&pool.jobs[k].im); jm_pic_free(&pool.jobs[k].rec); jm_bits_free(&pool.jobs[k].out); }
+    if (pool_sync) {
         pthread_mutex_destroy(&pool.mu);
         pthread_cond_destroy(&pool.cv_work);
         pthread_cond_destroy(&pool.cv_done);
-        free(pool.jobs); free(pool.queue); free(pool.th);
-        img = &im;
     }
-    st->total_ms = now_ms() - t_start;
+    free(pool.jobs); free(pool.queue); free(pool.th);
+    img = &im;
     st->surface_checked = im.surface_checked;
     st->surface_searches = im.surface_searches;
     st->surface_mismatches = im.surface_mismatches;

@@ -49,7 +49,9 @@ typedef struct jm_input {
     int  epzs_subpel;          /* EPZSSubPelME (must be 0)                                     */
     int  offset_matrix_present;/* OffsetMatrixPresentFlag (must be 0: flat lists only)         */
     int  level_idc;            /* LevelIDC                                                    */
-    int  symbol_mode;          /* SymbolMode (0 = CAVLC)                                       */
+    int  symbol_mode;          /* SymbolMode (0 = CAVLC, 1 = CABAC)                            */
+    int  context_init_method;  /* ContextInitMethod (0: fixed; 1 adaptive is rejected)          */
+    int  model_number;         /* FixedModelNumber: cabac_init_idc of P slices (0)              */
     int  lf_params_flag;       /* LoopFilterParametersFlag                                    */
     int  lf_disable;           /* LoopFilterDisable                                           */
     int  lf_alpha, lf_beta;    /* LoopFilterAlphaC0Offset / LoopFilterBetaOffset              */
@@ -106,6 +108,7 @@ void jm_put_ue(jm_bits *b, uint32_t v);
 void jm_put_se(jm_bits *b, int32_t v);
 void jm_trailing_bits(jm_bits *b);
 void jm_bits_align_flush(jm_bits *b);
+void jm_bits_append(jm_bits *b, const jm_bits *src);   /* whole bytes of src (byte aligned b) */
 
 typedef struct jm_seq {
     int width, height;         /* coded */
@@ -119,6 +122,8 @@ typedef struct jm_seq {
     int constrained_intra;
     int transform_8x8_mode;    /* PPS transform_8x8_mode_flag (High profile)                   */
     int slice_mbs;             /* MBs per slice, raster order (SliceMode 1); 0: one slice      */
+    int entropy_coding;        /* PPS entropy_coding_mode_flag: 0 CAVLC, 1 CABAC (SymbolMode)  */
+    int cabac_init_idc;        /* cabac_init_idc of P slices (FixedModelNumber)                */
 } jm_seq;
 
 /* NAL unit (Annex B start code + emulation prevention) appended to out */
@@ -137,7 +142,8 @@ int  jm_write_slice(jm_bits *rbsp, const jm_seq *s, const jm_slice *sl,
 typedef struct jm_slice_writer jm_slice_writer;
 jm_slice_writer *jm_slice_begin(jm_bits *rbsp, const jm_seq *s, const jm_slice *sl);
 void jm_slice_write_mb(jm_slice_writer *w, int mb_addr, const jmh_mb_result *r);
-void jm_slice_end(jm_slice_writer *w);
+/* closes the last slice; returns the CABAC bins of the picture's slices (0 with CAVLC) */
+long jm_slice_end(jm_slice_writer *w);
 /* close the current slice's data in its rbsp and start the next slice (header into rbsp), keeping
    the picture's neighbour buffers (SliceMode 1: one writer per picture, one rbsp per slice) */
 void jm_slice_restart(jm_slice_writer *w, jm_bits *rbsp, const jm_slice *sl);

@@ -143,7 +143,15 @@ typedef struct {
     uint8_t tc[24];       /* total_coeff: 16 luma (raster 4x4), 4 cb, 4 cr               */
     int nzblk;            /* luma 4x4 blocks with non-zero coefficients (bit raster)      */
     int8_t ipm[16];
+    /* CABAC context selection state (9.3.3.1.1) */
+    int cbp;              /* coded_block_pattern (P_Skip 0)                                 */
+    int cmode;            /* intra_chroma_pred_mode                                          */
+    int cbf_dc;           /* coded_block_flag: bit 0 luma DC, 1 Cb DC, 2 Cr DC               */
+    int cbf4;             /* luma 4x4 blocks (raster)                                        */
+    int cbfc[2];          /* chroma AC blocks                                                */
 } mbinfo;
+
+typedef struct { br_t *b; uint32_t range, ofs; uint8_t st[460], mps[460]; } cabd_t;
 
 struct jmo_dec {
     char err[256];
@@ -160,13 +168,17 @@ struct jmo_dec {
     int dis_dbf, offA, offB;
     int slice_first;      /* first MB of the current slice: MBs before it are unavailable (6.4.8) */
     int mbs_done;         /* MBs of the current picture decoded so far (a picture may have many slices) */
+    int cabac;            /* PPS entropy_coding_mode_flag                                    */
+    int16_t *mvd;         /* per 4x4 [2]: mvd_l0 (CABAC contexts)                            */
+    cabd_t cab;
+    int prev_qpd;         /* the previous MB of the slice had mb_qp_delta != 0               */
 };
 
 int jmo_dec_create(jmo_dec **out) { *out = (jmo_dec *)calloc(1, sizeof(jmo_dec)); return *out ? 0 : JMH_E_OOM; }
 void jmo_dec_destroy(jmo_dec *d) {
     if (!d) return;
     for (int i = 0; i < 3; i++) { free(d->cur[i]); free(d->ref[i]); }
-    free(d->mi); free(d->mv); free(d->refi); free(d->dec4);
+    free(d->mi); free(d->mv); free(d->refi); free(d->dec4); free(d->mvd);
     free(d);
 }
 const char *jmo_dec_error(const jmo_dec *d) { return d->err; }
@@ -176,8 +188,9 @@ static void alloc_pics(jmo_dec *d) {
     size_t ls = (size_t)d->W * d->H;
     d->cur[0] = calloc(ls, 1); d->cur[1] = calloc(ls / 4, 1); d->cur[2] = calloc(ls / 4, 1);
     d->ref[0] = calloc(ls, 1); d->ref[1] = calloc(ls / 4, 1); d->ref[2] = calloc(ls / 4, 1);
-    free(d->mi); free(d->mv); free(d->refi); free(d->dec4);
+    free(d->mi); free(d->mv); free(d->refi); free(d->dec4); free(d->mvd);
     d->mi = calloc((size_t)d->mbw * d->mbh, sizeof(mbinfo));
+    d->mvd = calloc(ls / 16 * 2, sizeof(int16_t));
     d->mv = calloc(ls / 16 * 2, sizeof(int16_t));
     d->refi = calloc(ls / 16, 1);
     d->dec4 = calloc(ls / 16, 1);
@@ -213,7 +226,7 @@ static int parse_sps(jmo_dec *d, br_t *b) {
 }
 static int parse_pps(jmo_dec *d, br_t *b) {
     rue(b); rue(b);
-    if (rb(b)) { snprintf(d->err, sizeof d->err, "CABAC unsupported"); return -1; }
+    d->cabac = rb(b);                     /* entropy_coding_mode_flag */
     rb(b);
     if (rue(b)) { snprintf(d->err, sizeof d->err, "FMO unsupported"); return -1; }
     d->num_ref_l0 = rue(b) + 1;
@@ -585,134 +598,525 @@ static const int QPCt[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12,
 
 #define FAIL(...) do { snprintf(d->err, sizeof d->err, __VA_ARGS__); return -1; } while (0)
 
-static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_ue, int skip, int *qp) {
-    mbinfo *mi = &d->mi[my * d->mbw + mx];
-    memset(mi, 0, sizeof(*mi));
-    int W4 = d->W / 4;
-    for (int k = 0; k < 16; k++) { int i = (4 * my + (k >> 2)) * W4 + 4 * mx + (k & 3); d->dec4[i] = 0; d->refi[i] = -1; d->mv[2 * i] = d->mv[2 * i + 1] = 0; }
+/* ---- one macroblock's syntax, parsed by CAVLC (9.2) or CABAC (9.3), then reconstructed ---- */
+typedef struct {
+    int skip;              /* P_Skip                                                          */
+    int intra_type;        /* -1 inter (or P_Skip), 0 I_NxN, 1 I_16x16                         */
+    int i16mode, cmode, cbp;
+    int ipm[16];           /* Intra4x4 / Intra8x8 modes per 4x4 (raster)                       */
     int16_t mv16[16][2];
-    memset(mv16, 0, sizeof(mv16));
-    uint8_t pred[256], predu[64], predv[64];
-    int i16mode = 0, cbp = 0, intra_type = -1;    /* intra_type: -1 inter, 0 I_NxN, 1 I16 */
-    int no_sub8x8 = 0;
-    int ipm[16];
-    if (skip) {
-        mi->mbtype = 3;
-        int ia = 0, ib = 0;
-        int aa = nb4(d, mx, my, -1, 0, &ia), ab = nb4(d, mx, my, 0, -1, &ib);
-        int mvx = 0, mvy = 0;
-        if (aa && ab && !(d->refi[ia] == 0 && !d->mv[2 * ia] && !d->mv[2 * ia + 1]) && !(d->refi[ib] == 0 && !d->mv[2 * ib] && !d->mv[2 * ib + 1])) {
-            int p[2];
-            mvpred(d, mx, my, 0, 0, 16, 16, 0, p);
-            mvx = p[0]; mvy = p[1];
+    int dc16[16];          /* Intra16x16DCLevel (scan order)                                   */
+    int l4[16][16];        /* per 4x4 (raster): levels in zig-zag order (I16: AC at 1..15)      */
+    int l8[4][64];         /* per 8x8: 8x8 zig-zag order                                        */
+    int cdc[2][4];         /* chroma DC c0..c3                                                  */
+    int cac[2][4][16];     /* chroma AC (zig-zag, [0] unused)                                   */
+} mbsyn;
+
+/* reset the MB's partition / motion state before parsing it */
+static void mb_begin(jmo_dec *d, int mx, int my, mbsyn *s) {
+    memset(&d->mi[my * d->mbw + mx], 0, sizeof(mbinfo));
+    memset(s, 0, sizeof(*s));
+    int W4 = d->W / 4;
+    for (int k = 0; k < 16; k++) {
+        int i = (4 * my + (k >> 2)) * W4 + 4 * mx + (k & 3);
+        d->dec4[i] = 0; d->refi[i] = -1; d->mv[2 * i] = d->mv[2 * i + 1] = 0;
+        d->mvd[2 * i] = d->mvd[2 * i + 1] = 0;
+    }
+}
+
+/* P_Skip motion (8.4.1.1) */
+static void skip_motion(jmo_dec *d, int mx, int my, mbsyn *s) {
+    int ia = 0, ib = 0;
+    int aa = nb4(d, mx, my, -1, 0, &ia), ab = nb4(d, mx, my, 0, -1, &ib);
+    int mvx = 0, mvy = 0;
+    if (aa && ab && !(d->refi[ia] == 0 && !d->mv[2 * ia] && !d->mv[2 * ia + 1]) && !(d->refi[ib] == 0 && !d->mv[2 * ib] && !d->mv[2 * ib + 1])) {
+        int p[2];
+        mvpred(d, mx, my, 0, 0, 16, 16, 0, p);
+        mvx = p[0]; mvy = p[1];
+    }
+    set_part(d, mx, my, 0, 0, 16, 16, mvx, mvy, 0, s->mv16);
+    s->skip = 1;
+    s->intra_type = -1;
+    d->mi[my * d->mbw + mx].mbtype = 3;
+}
+
+/* predIntra4x4PredMode / predIntra8x8PredMode (8.3.1.1 / 8.3.2.1); ipm: this MB's modes so far */
+static int pred_ipm(const jmo_dec *d, int mx, int my, int x4, int y4, const int *ipm) {
+    int ma, mb;
+    if (x4 > 0) ma = ipm[y4 * 4 + x4 - 1];
+    else if (avail_mb(d, mx - 1, my, mx, my)) { const mbinfo *n = &d->mi[my * d->mbw + mx - 1]; ma = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[y4 * 4 + 3] : 2; }
+    else return 2;
+    if (y4 > 0) mb = ipm[(y4 - 1) * 4 + x4];
+    else if (avail_mb(d, mx, my - 1, mx, my)) { const mbinfo *n = &d->mi[(my - 1) * d->mbw + mx]; mb = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[12 + x4] : 2; }
+    else return 2;
+    return imin(ma, mb);
+}
+/* the intra mode of 4x4 block (x4, y4), 8x8 blocks fill their four 4x4 */
+static void set_ipm(mbsyn *s, int x4, int y4, int mode, int t8) {
+    if (!t8) { s->ipm[y4 * 4 + x4] = mode; return; }
+    for (int k = 0; k < 4; k++) s->ipm[(y4 + (k >> 1)) * 4 + x4 + (k & 1)] = mode;
+}
+
+static int parse_cavlc(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int t, mbsyn *s, int *qp) {
+    mbinfo *mi = &d->mi[my * d->mbw + mx];
+    int intra_type = -1, no_sub8x8 = 0, cbp = 0;
+    if (slice_p) { if (t >= 5) { t -= 5; intra_type = t == 0 ? 0 : 1; } }
+    else intra_type = t == 0 ? 0 : 1;
+    s->intra_type = intra_type;
+    if (intra_type == 1) {
+        if (t > 24) FAIL("I_PCM unsupported");
+        s->i16mode = (t - 1) % 4;
+        cbp = (((t - 1) / 4) % 3) << 4 | ((t >= 13) ? 15 : 0);
+    }
+    if (intra_type >= 0) {
+        mi->intra = 1;
+        mi->mbtype = intra_type == 0 ? 1 : 2;
+        if (intra_type == 0 && d->t8mode) mi->t8 = rb(b);
+        if (intra_type == 0) {
+            if (mi->t8) mi->mbtype = 4;
+            for (int blk = 0; blk < 16; blk += mi->t8 ? 4 : 1) {
+                int x4 = ((blk >> 2) & 1) * 2 + (blk & 1), y4 = (blk >> 3) * 2 + ((blk >> 1) & 1);
+                int flag = rb(b), rem = flag ? 0 : (int)rbits(b, 3);
+                int pm = pred_ipm(d, mx, my, x4, y4, s->ipm);
+                set_ipm(s, x4, y4, flag ? pm : (rem < pm ? rem : rem + 1), mi->t8);
+            }
+            for (int k = 0; k < 16; k++) mi->ipm[k] = (int8_t)s->ipm[k];
         }
-        set_part(d, mx, my, 0, 0, 16, 16, mvx, mvy, 0, mv16);
+        s->cmode = rue(b);
+        if (s->cmode > 3) FAIL("bad chroma mode");
     } else {
-        int t = mbt_ue;
-        if (slice_p) { if (t >= 5) { t -= 5; intra_type = t == 0 ? 0 : 1; } }
-        else intra_type = t == 0 ? 0 : 1;
-        if (intra_type == 1) {
-            if (t > 24) FAIL("I_PCM unsupported");
-            i16mode = (t - 1) % 4;
-            cbp = (((t - 1) / 4) % 3) << 4 | ((t >= 13) ? 15 : 0);
-        }
-        if (intra_type >= 0) {
-            mi->intra = 1;
-            mi->mbtype = intra_type == 0 ? 1 : 2;
-            if (intra_type == 0 && d->t8mode) mi->t8 = rb(b);
-            if (mi->t8) {                               /* Intra_8x8: predIntra8x8PredMode (8.3.2.1) */
-                mi->mbtype = 4;
-                int m8[4];
-                for (int b8 = 0; b8 < 4; b8++) {
-                    int x4 = (b8 & 1) * 2, y4 = (b8 >> 1) * 2;
-                    int flag = rb(b), rem = flag ? 0 : (int)rbits(b, 3);
-                    int ma = -1, mb = -1, dcp = 0;
-                    if (x4 > 0) ma = m8[b8 - 1];
-                    else if (avail_mb(d, mx - 1, my, mx, my)) { const mbinfo *n = &d->mi[my * d->mbw + mx - 1]; ma = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[y4 * 4 + 3] : 2; }
-                    else dcp = 1;
-                    if (y4 > 0) mb = m8[b8 - 2];
-                    else if (avail_mb(d, mx, my - 1, mx, my)) { const mbinfo *n = &d->mi[(my - 1) * d->mbw + mx]; mb = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[12 + x4] : 2; }
-                    else dcp = 1;
-                    int pm = dcp ? 2 : imin(ma, mb);
-                    m8[b8] = flag ? pm : (rem < pm ? rem : rem + 1);
-                }
-                for (int k = 0; k < 16; k++) { ipm[k] = m8[((k >> 3) << 1) + ((k & 3) >> 1)]; mi->ipm[k] = (int8_t)ipm[k]; }
-            } else if (intra_type == 0) {
-                for (int blk = 0; blk < 16; blk++) {
-                    int x4 = ((blk >> 2) & 1) * 2 + (blk & 1), y4 = (blk >> 3) * 2 + ((blk >> 1) & 1);
-                    int flag = rb(b), rem = flag ? 0 : (int)rbits(b, 3);
-                    /* predIntra4x4PredMode (8.3.1.1) */
-                    int ma = -1, mb = -1, dcp = 0;
-                    if (x4 > 0) ma = ipm[y4 * 4 + x4 - 1];
-                    else if (avail_mb(d, mx - 1, my, mx, my)) { const mbinfo *n = &d->mi[my * d->mbw + mx - 1]; ma = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[y4 * 4 + 3] : 2; }
-                    else dcp = 1;
-                    if (y4 > 0) mb = ipm[(y4 - 1) * 4 + x4];
-                    else if (avail_mb(d, mx, my - 1, mx, my)) { const mbinfo *n = &d->mi[(my - 1) * d->mbw + mx]; mb = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[12 + x4] : 2; }
-                    else dcp = 1;
-                    int pm = dcp ? 2 : imin(ma, mb);
-                    ipm[y4 * 4 + x4] = flag ? pm : (rem < pm ? rem : rem + 1);
-                }
-                memcpy(mi->ipm, (int8_t[16]){0}, 16);
-                for (int k = 0; k < 16; k++) mi->ipm[k] = (int8_t)ipm[k];
+        mi->mbtype = 0;
+        if (t > 4) FAIL("bad P mb_type %d", t);
+        if (d->num_ref_l0 > 1) FAIL("multiple refs unsupported");
+        no_sub8x8 = 1;
+        if (t == 3 || t == 4) {
+            int sub[4];
+            for (int i = 0; i < 4; i++) { sub[i] = rue(b); if (sub[i] > 3) FAIL("bad sub_mb_type"); if (sub[i]) no_sub8x8 = 0; }
+            for (int i = 0; i < 4; i++) {
+                int ox = (i & 1) * 8, oy = (i >> 1) * 8;
+                int sw = sub[i] == 0 || sub[i] == 1 ? 8 : 4, sh = sub[i] == 0 || sub[i] == 2 ? 8 : 4;
+                for (int y = 0; y < 8; y += sh)
+                    for (int x = 0; x < 8; x += sw) {
+                        int p[2];
+                        mvpred(d, mx, my, ox + x, oy + y, sw, sh, 0, p);
+                        int dx = rse(b), dy = rse(b);
+                        set_part(d, mx, my, ox + x, oy + y, sw, sh, p[0] + dx, p[1] + dy, 0, s->mv16);
+                    }
             }
-            int cmode = rue(b);
-            if (cmode > 3) FAIL("bad chroma mode");
-            if (predc(d, mx, my, 1, cmode, predu) || predc(d, mx, my, 2, cmode, predv)) FAIL("chroma pred mode %d unavailable at MB %d,%d", cmode, mx, my);
-            if (intra_type == 1 && pred16(d, mx, my, i16mode, pred)) FAIL("I16 mode %d unavailable at MB %d,%d", i16mode, mx, my);
         } else {
-            mi->mbtype = 0;
-            if (t > 4) FAIL("bad P mb_type %d", t);
-            no_sub8x8 = 1;
-            if (t == 3 || t == 4) {
-                int sub[4];
-                for (int i = 0; i < 4; i++) { sub[i] = rue(b); if (sub[i] > 3) FAIL("bad sub_mb_type"); if (sub[i]) no_sub8x8 = 0; }
-                if (d->num_ref_l0 > 1) FAIL("multiple refs unsupported");
-                for (int i = 0; i < 4; i++) {
-                    int ox = (i & 1) * 8, oy = (i >> 1) * 8;
-                    int sw = sub[i] == 0 || sub[i] == 1 ? 8 : 4, sh = sub[i] == 0 || sub[i] == 2 ? 8 : 4;
-                    for (int y = 0; y < 8; y += sh)
-                        for (int x = 0; x < 8; x += sw) {
-                            int p[2];
-                            mvpred(d, mx, my, ox + x, oy + y, sw, sh, 0, p);
-                            int dx = rse(b), dy = rse(b);
-                            set_part(d, mx, my, ox + x, oy + y, sw, sh, p[0] + dx, p[1] + dy, 0, mv16);
-                        }
-                }
-            } else {
-                if (d->num_ref_l0 > 1) FAIL("multiple refs unsupported");
-                int np = t == 0 ? 1 : 2, w = t == 2 ? 8 : 16, h = t == 1 ? 8 : 16;
-                for (int pi = 0; pi < np; pi++) {
-                    int x = t == 2 ? 8 * pi : 0, y = t == 1 ? 8 * pi : 0, p[2];
-                    mvpred(d, mx, my, x, y, w, h, 0, p);
-                    int dx = rse(b), dy = rse(b);
-                    set_part(d, mx, my, x, y, w, h, p[0] + dx, p[1] + dy, 0, mv16);
-                }
+            int np = t == 0 ? 1 : 2, w = t == 2 ? 8 : 16, h = t == 1 ? 8 : 16;
+            for (int pi = 0; pi < np; pi++) {
+                int x = t == 2 ? 8 * pi : 0, y = t == 1 ? 8 * pi : 0, p[2];
+                mvpred(d, mx, my, x, y, w, h, 0, p);
+                int dx = rse(b), dy = rse(b);
+                set_part(d, mx, my, x, y, w, h, p[0] + dx, p[1] + dy, 0, s->mv16);
             }
-        }
-        if (intra_type != 1) {
-            int code = rue(b);
-            if (code > 47) FAIL("bad cbp code");
-            cbp = intra_type == 0 ? cbp_intra[code] : cbp_inter[code];
-            if (intra_type < 0 && (cbp & 15) && d->t8mode && no_sub8x8) mi->t8 = rb(b);
-        }
-        if (cbp > 0 || intra_type == 1) {
-            int dq = rse(b);
-            *qp = (*qp + dq + 52) % 52;
         }
     }
-    mi->qp = *qp;
-    if (!mi->intra) inter_pred(d, mx, my, mv16, pred, predu, predv);
-    /* ---- residual + reconstruction ---- */
-    int qp_ = *qp, qpc = QPCt[iclip(0, 51, qp_ + d->cqp_off)];
+    if (intra_type != 1) {
+        int code = rue(b);
+        if (code > 47) FAIL("bad cbp code");
+        cbp = intra_type == 0 ? cbp_intra[code] : cbp_inter[code];
+        if (intra_type < 0 && (cbp & 15) && d->t8mode && no_sub8x8) mi->t8 = rb(b);
+    }
+    s->cbp = cbp;
+    if (cbp > 0 || intra_type == 1) {
+        int dq = rse(b);
+        *qp = (*qp + dq + 52) % 52;
+    }
+    /* residual (7.3.5.3, CAVLC): I16 DC, luma, chroma DC Cb Cr, chroma AC Cb Cr */
     int cbpl = cbp & 15, cbpc = cbp >> 4;
+    if (intra_type == 1 && read_block(b, calc_nc(d, mx, my, 0, 0, 0, mi->tc), 16, s->dc16) < 0) FAIL("I16 DC at %d,%d", mx, my);
+    for (int b8 = 0; b8 < 4; b8++)
+        for (int i4 = 0; i4 < 4; i4++) {
+            int x4 = (b8 & 1) * 2 + (i4 & 1), y4 = (b8 >> 1) * 2 + (i4 >> 1), c[16] = {0}, tc = 0;
+            if (cbpl & (1 << b8)) {
+                int nC = calc_nc(d, mx, my, 0, x4, y4, mi->tc);
+                if (intra_type == 1) { tc = read_block(b, nC, 15, c + 1); }
+                else tc = read_block(b, nC, 16, c);
+                if (tc < 0) FAIL("luma block %d at MB %d,%d", b8 * 4 + i4, mx, my);
+            }
+            mi->tc[y4 * 4 + x4] = (uint8_t)tc;
+            if (mi->t8) for (int k = 0; k < 16; k++) s->l8[b8][4 * k + i4] = c[k];   /* 4 interleaved blocks */
+            else for (int k = 0; k < 16; k++) s->l4[y4 * 4 + x4][k] = c[k];
+        }
+    if (cbpc)
+        for (int comp = 0; comp < 2; comp++) if (read_block(b, -1, 4, s->cdc[comp]) < 0) FAIL("chroma DC");
+    if (cbpc == 2)
+        for (int comp = 0; comp < 2; comp++)
+            for (int k = 0; k < 4; k++) {
+                int tc = read_block(b, calc_nc(d, mx, my, 1 + comp, k & 1, k >> 1, mi->tc), 15, s->cac[comp][k] + 1);
+                if (tc < 0) FAIL("chroma AC");
+                mi->tc[16 + 4 * comp + k] = (uint8_t)tc;
+            }
+    return b->err ? -1 : 0;
+}
+
+/* ---- CABAC parsing (9.3): arithmetic decoding engine, initialisation, binarisations ----- */
+/* Table 9-44 (own copy; the encoder's is in host/cabac.c) */
+static const uint8_t lps_range[64][4] = {
+    {128, 176, 208, 240}, {128, 167, 197, 227}, {128, 158, 187, 216}, {123, 150, 178, 205}, {116, 142, 169, 195}, {111, 135, 160, 185},
+    {105, 128, 152, 175}, {100, 122, 144, 166}, {95, 116, 137, 158},  {90, 110, 130, 150},  {85, 104, 123, 142},  {81, 99, 117, 135},
+    {77, 94, 111, 128},   {73, 89, 105, 122},   {69, 85, 100, 116},   {66, 80, 95, 110},    {62, 76, 90, 104},    {59, 72, 86, 99},
+    {56, 69, 81, 94},     {53, 65, 77, 89},     {51, 62, 73, 85},     {48, 59, 69, 80},     {46, 56, 66, 76},     {43, 53, 63, 72},
+    {41, 50, 59, 69},     {39, 48, 56, 65},     {37, 45, 54, 62},     {35, 43, 51, 59},     {33, 41, 48, 56},     {32, 39, 46, 53},
+    {30, 37, 43, 50},     {29, 35, 41, 48},     {27, 33, 39, 45},     {26, 31, 37, 43},     {24, 30, 35, 41},     {23, 28, 33, 39},
+    {22, 27, 32, 37},     {21, 26, 30, 35},     {20, 24, 29, 33},     {19, 23, 27, 31},     {18, 22, 26, 30},     {17, 21, 25, 28},
+    {16, 20, 23, 27},     {15, 19, 22, 25},     {14, 18, 21, 24},     {14, 17, 20, 23},     {13, 16, 19, 22},     {12, 15, 18, 21},
+    {12, 14, 17, 20},     {11, 14, 16, 19},     {11, 13, 15, 18},     {10, 12, 15, 17},     {10, 12, 14, 16},     {9, 11, 13, 15},
+    {9, 11, 12, 14},      {8, 10, 12, 14},      {8, 9, 11, 13},       {7, 9, 11, 12},       {7, 9, 10, 12},       {7, 8, 10, 11},
+    {6, 8, 9, 11},        {6, 7, 9, 10},        {6, 7, 8, 9},         {2, 2, 2, 2}};
+static const uint8_t lps_next[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12, 13, 13, 15, 15, 16, 16,
+                                     18, 18, 19, 19, 21, 21, 22, 22, 23, 24, 24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30,
+                                     31, 32, 32, 33, 33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
+/* Tables 9-12 .. 9-33 as runs of consecutive ctxIdx: {first ctxIdx, count} then (m, n) pairs;
+   I slices and cabac_init_idc 0 (own copy, typed per syntax element) */
+static const int16_t ctxinit_I[] = {
+    0, 11, 20, -15, 2, 54, 3, 74, 20, -15, 2, 54, 3, 74, -28, 127, -23, 104, -6, 53, -1, 54, 7, 51,
+    60, 4, 0, 41, 0, 63, 0, 63, 0, 63,                                               /* mb_qp_delta        */
+    64, 4, -9, 83, 4, 86, 0, 97, -7, 72,                                             /* intra chroma mode   */
+    68, 2, 13, 41, 3, 62,                                                            /* intra pred modes    */
+    73, 4, -17, 127, -13, 102, 0, 82, -7, 74,                                        /* cbp luma            */
+    77, 8, -21, 107, -27, 127, -31, 127, -24, 127, -18, 95, -27, 127, -21, 114, -30, 127,   /* cbp chroma */
+    85, 20, -17, 123, -12, 115, -16, 122, -11, 115, -12, 63, -2, 68, -15, 84, -13, 104, -3, 70, -8, 93,
+            -10, 90, -30, 127, -1, 74, -6, 97, -7, 91, -20, 127, -4, 56, -5, 82, -7, 76, -22, 125,   /* cbf */
+    105, 61, -7, 93, -11, 87, -3, 77, -5, 71, -4, 63, -4, 68, -12, 84, -7, 62, -7, 65, 8, 61, 5, 56, -2, 66, 1, 64,
+             0, 61, -2, 78, 1, 50, 7, 52, 10, 35, 0, 44, 11, 38, 1, 45, 0, 46, 5, 44, 31, 17, 1, 51, 7, 50, 28, 19,
+             16, 33, 14, 62, -13, 108, -15, 100, -13, 101, -13, 91, -12, 94, -10, 88, -16, 84, -10, 86, -7, 83,
+             -13, 87, -19, 94, 1, 70, 0, 72, -5, 74, 18, 59, -8, 102, -15, 100, 0, 95, -4, 75, 2, 72, -11, 75,
+             -3, 71, 15, 46, -13, 69, 0, 62, 0, 65, 21, 37, -15, 72, 9, 57, 16, 54, 0, 62, 12, 72,       /* sig */
+    166, 61, 24, 0, 15, 9, 8, 25, 13, 18, 15, 9, 13, 19, 10, 37, 12, 18, 6, 29, 20, 33, 15, 30, 4, 45, 1, 58,
+             0, 62, 7, 61, 12, 38, 11, 45, 15, 39, 11, 42, 13, 44, 16, 45, 12, 41, 10, 49, 30, 34, 18, 42, 10, 55,
+             17, 51, 17, 46, 0, 89, 26, -19, 22, -17, 26, -17, 30, -25, 28, -20, 33, -23, 37, -27, 33, -23,
+             40, -28, 38, -17, 33, -11, 40, -15, 41, -6, 38, 1, 41, 17, 30, -6, 27, 3, 26, 22, 37, -16, 35, -4,
+             38, -8, 38, -3, 37, 3, 38, 5, 42, 0, 35, 16, 39, 22, 14, 48, 27, 37, 21, 60, 12, 68, 2, 97, /* last */
+    227, 49, -3, 71, -6, 42, -5, 50, -3, 54, -2, 62, 0, 58, 1, 63, -2, 72, -1, 74, -9, 91, -5, 67, -5, 27,
+             -3, 39, -2, 44, 0, 46, -16, 64, -8, 68, -10, 78, -6, 77, -10, 86, -12, 92, -15, 55, -10, 60, -6, 62,
+             -4, 65, -12, 73, -8, 76, -7, 80, -9, 88, -17, 110, -11, 97, -20, 84, -11, 79, -6, 73, -4, 74,
+             -13, 86, -13, 96, -11, 97, -19, 117, -8, 78, -5, 33, -4, 48, -2, 53, -3, 62, -13, 71, -10, 79,
+             -12, 86, -13, 90, -14, 97,                                                            /* levels */
+    399, 3, 31, 21, 31, 31, 25, 50,                                                  /* transform_size_8x8  */
+    402, 15, -17, 120, -20, 112, -18, 114, -11, 85, -15, 92, -14, 89, -26, 71, -15, 81, -14, 80, 0, 68,
+             -14, 70, -24, 56, -23, 68, -24, 50, -11, 74,
+    417, 9, 23, -13, 26, -13, 40, -15, 49, -14, 44, 3, 45, 6, 44, 34, 33, 54, 19, 82,
+    426, 10, -3, 75, -1, 23, 1, 34, 1, 43, 0, 54, -2, 55, 0, 61, 1, 64, 0, 68, -9, 92,
+    -1};
+static const int16_t ctxinit_P0[] = {
+    0, 11, 20, -15, 2, 54, 3, 74, 20, -15, 2, 54, 3, 74, -28, 127, -23, 104, -6, 53, -1, 54, 7, 51,
+    11, 3, 23, 33, 23, 2, 21, 0,                                                     /* mb_skip_flag        */
+    14, 7, 1, 9, 0, 49, -37, 118, 5, 57, -13, 78, -11, 65, 1, 62,                    /* mb_type P           */
+    21, 3, 12, 49, -4, 73, 17, 50,                                                   /* sub_mb_type         */
+    40, 7, -3, 69, -6, 81, -11, 96, 6, 55, 7, 67, -5, 86, 2, 88,                     /* mvd x               */
+    47, 7, 0, 58, -3, 76, -10, 94, 5, 54, 4, 69, -3, 81, 0, 88,                      /* mvd y               */
+    54, 6, -7, 67, -5, 74, -4, 74, -5, 80, -7, 72, 1, 58,                            /* ref_idx             */
+    60, 4, 0, 41, 0, 63, 0, 63, 0, 63,
+    64, 4, -9, 83, 4, 86, 0, 97, -7, 72,
+    68, 2, 13, 41, 3, 62,
+    73, 4, -27, 126, -28, 98, -25, 101, -23, 67,
+    77, 8, -28, 82, -20, 94, -16, 83, -22, 110, -21, 91, -18, 102, -13, 93, -29, 127,
+    85, 20, -7, 92, -5, 89, -7, 96, -13, 108, -3, 46, -1, 65, -1, 57, -9, 93, -3, 74, -9, 92,
+            -8, 87, -23, 126, 5, 54, 6, 60, 6, 59, 6, 69, -1, 48, 0, 68, -4, 69, -8, 88,
+    105, 61, -2, 85, -6, 78, -1, 75, -7, 77, 2, 54, 5, 50, -3, 68, 1, 50, 6, 42, -4, 81, 1, 63, -4, 70, 0, 67,
+             2, 57, -2, 76, 11, 35, 4, 64, 1, 61, 11, 35, 18, 25, 12, 24, 13, 29, 13, 36, -10, 93, -7, 73,
+             -2, 73, 13, 46, 9, 49, -7, 100, 9, 53, 2, 53, 5, 53, -2, 61, 0, 56, 0, 56, -13, 63, -5, 60,
+             -1, 62, 4, 57, -6, 69, 4, 57, 14, 39, 4, 51, 13, 68, 3, 64, 1, 61, 9, 63, 7, 50, 16, 39, 5, 44,
+             4, 52, 11, 48, -5, 60, -1, 59, 0, 59, 22, 33, 5, 44, 14, 43, -1, 78, 0, 60, 9, 69,
+    166, 61, 11, 28, 2, 40, 3, 44, 0, 49, 0, 46, 2, 44, 2, 51, 0, 47, 4, 39, 2, 62, 6, 46, 0, 54, 3, 54,
+             2, 58, 4, 63, 6, 51, 6, 57, 7, 53, 6, 52, 6, 55, 11, 45, 14, 36, 8, 53, -1, 82, 7, 55, -3, 78,
+             15, 46, 22, 31, -1, 84, 25, 7, 30, -7, 28, 3, 28, 4, 32, 0, 34, -1, 30, 6, 30, 6, 32, 9, 31, 19,
+             26, 27, 26, 30, 37, 20, 28, 34, 17, 70, 1, 67, 5, 59, 9, 67, 16, 30, 18, 32, 18, 35, 22, 29,
+             24, 31, 23, 38, 18, 43, 20, 41, 11, 63, 9, 59, 9, 64, -1, 94, -2, 89, -9, 108,
+    227, 49, -6, 76, -2, 44, 0, 45, 0, 52, -3, 64, -2, 59, -4, 70, -4, 75, -8, 82, -17, 102, -9, 77, 3, 24,
+             0, 42, 0, 48, 0, 55, -6, 59, -7, 71, -12, 83, -11, 87, -30, 119, 1, 58, -3, 29, -1, 36, 1, 38,
+             2, 43, -6, 55, 0, 58, 0, 64, -3, 74, -10, 90, 0, 70, -4, 29, 5, 31, 7, 42, 1, 59, -2, 58,
+             -3, 72, -3, 81, -11, 97, 0, 58, 8, 5, 10, 14, 14, 18, 13, 27, 2, 40, 0, 58, -3, 70, -6, 79, -8, 85,
+    399, 3, 12, 40, 11, 51, 14, 59,
+    402, 15, -4, 79, -7, 71, -5, 69, -9, 70, -8, 66, -10, 68, -19, 73, -12, 69, -16, 70, -15, 67, -20, 62,
+             -19, 70, -16, 66, -22, 65, -20, 63,
+    417, 9, 9, -2, 26, -9, 33, -9, 39, -7, 41, -2, 45, 3, 49, 9, 45, 27, 36, 59,
+    426, 10, -6, 66, -7, 35, -7, 42, -8, 45, -5, 48, -12, 56, -6, 60, -5, 62, -8, 66, -8, 76,
+    -1};
+
+static void cabd_start(cabd_t *c, br_t *b, int slice_i, int qp) {
+    const int16_t *t = slice_i ? ctxinit_I : ctxinit_P0;
+    memset(c->st, 0, sizeof c->st);
+    memset(c->mps, 0, sizeof c->mps);
+    while (*t >= 0) {                               /* 9.3.1.1 */
+        int first = t[0], cnt = t[1];
+        t += 2;
+        for (int i = 0; i < cnt; i++, t += 2) {
+            int pre = iclip(1, 126, ((t[0] * iclip(0, 51, qp)) >> 4) + t[1]);
+            c->st[first + i] = (uint8_t)(pre <= 63 ? 63 - pre : pre - 64);
+            c->mps[first + i] = pre > 63;
+        }
+    }
+    c->b = b;
+    c->range = 510;                                 /* 9.3.1.2 */
+    c->ofs = rbits(b, 9);
+}
+static int cdec(cabd_t *c, int ctx) {               /* DecodeDecision (9.3.3.2.1) */
+    uint32_t lps = lps_range[c->st[ctx]][(c->range >> 6) & 3];
+    int bin;
+    c->range -= lps;
+    if (c->ofs >= c->range) {
+        bin = !c->mps[ctx];
+        c->ofs -= c->range;
+        c->range = lps;
+        if (!c->st[ctx]) c->mps[ctx] = !c->mps[ctx];
+        c->st[ctx] = lps_next[c->st[ctx]];
+    } else {
+        bin = c->mps[ctx];
+        if (c->st[ctx] < 62) c->st[ctx]++;
+    }
+    while (c->range < 256) { c->range <<= 1; c->ofs = (c->ofs << 1) | (uint32_t)rb(c->b); }
+    return bin;
+}
+static int cbypass(cabd_t *c) {
+    c->ofs = (c->ofs << 1) | (uint32_t)rb(c->b);
+    if (c->ofs >= c->range) { c->ofs -= c->range; return 1; }
+    return 0;
+}
+static int cterm(cabd_t *c) {
+    c->range -= 2;
+    if (c->ofs >= c->range) return 1;
+    while (c->range < 256) { c->range <<= 1; c->ofs = (c->ofs << 1) | (uint32_t)rb(c->b); }
+    return 0;
+}
+static unsigned ceg_bypass(cabd_t *c, int k) {       /* k-th order Exp-Golomb suffix (9.3.2.3) */
+    unsigned v = 0;
+    while (cbypass(c)) { v += 1u << k; if (++k > 24) return v; }
+    while (k--) v += (unsigned)cbypass(c) << k;
+    return v;
+}
+
+/* residual_block_cabac: coef[0..n) scan order; cbfctx < 0: coded_block_flag not coded (8x8) */
+static int cabac_block(cabd_t *c, int cat, int n, int cbfctx, int *coef) {
+    static const int so[5] = {0, 15, 29, 44, 47}, ao[5] = {0, 10, 20, 30, 39};
+    /* Table 9-43: 8x8 frame significant / last ctxIdxInc by scanning position */
+    static const uint8_t s8[63] = {0, 1, 2, 3, 4, 5, 5, 4, 4, 3, 3, 4, 4, 4, 5, 5, 4, 4, 4, 4, 3, 3, 6, 7, 7, 7, 8, 9, 10, 9, 8, 7,
+                                   7, 6, 11, 12, 13, 11, 6, 7, 8, 9, 14, 10, 9, 8, 6, 11, 12, 13, 11, 6, 9, 14, 10, 9, 11, 12, 13, 11, 14, 10, 12};
+    static const uint8_t l8[63] = {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
+                                   3, 3, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7, 8, 8, 8};
+    for (int i = 0; i < n; i++) coef[i] = 0;
+    if (cbfctx >= 0 && !cdec(c, cbfctx)) return 0;
+    int sbase = cat == 5 ? 402 : 105 + so[cat], lbase = cat == 5 ? 417 : 166 + so[cat], abase = cat == 5 ? 426 : 227 + ao[cat];
+    int sig[64] = {0}, lastpos = -1;
+    for (int i = 0; i < n - 1 && lastpos < 0; i++) {
+        int inc_s = cat == 5 ? s8[i] : cat == 3 ? imin(i, 2) : i, inc_l = cat == 5 ? l8[i] : cat == 3 ? imin(i, 2) : i;
+        if (cdec(c, sbase + inc_s)) { sig[i] = 1; if (cdec(c, lbase + inc_l)) lastpos = i; }
+    }
+    if (lastpos < 0) { lastpos = n - 1; sig[n - 1] = 1; }
+    int eq1 = 0, gt1 = 0;
+    for (int i = lastpos; i >= 0; i--) {
+        if (!sig[i]) continue;
+        int v = 0;
+        if (cdec(c, abase + (gt1 ? 0 : imin(4, 1 + eq1)))) {
+            int ctx = abase + 5 + imin(4 - (cat == 3), gt1);
+            v = 1;
+            while (v < 14 && cdec(c, ctx)) v++;
+            if (v == 14) v += (int)ceg_bypass(c, 0);
+        }
+        coef[i] = cbypass(c) ? -(v + 1) : v + 1;
+        if (v == 0) eq1++; else gt1++;
+    }
+    return 1;
+}
+
+/* mvd_l0 component: UEG3, signed, uCoff 9; bin 0 ctxIdxInc from absMvdComp(A) + absMvdComp(B) */
+static int cabac_mvd(cabd_t *c, int comp, int sum) {
+    int base = comp ? 47 : 40;
+    if (!cdec(c, base + (sum < 3 ? 0 : sum <= 32 ? 1 : 2))) return 0;
+    int a = 1;
+    while (a < 9 && cdec(c, base + imin(a + 2, 6))) a++;
+    if (a == 9) a += (int)ceg_bypass(c, 3);
+    return cbypass(c) ? -a : a;
+}
+/* absMvdComp of the neighbouring partition covering luma (xN, yN) relative to the MB (6.4.11.7) */
+static int mvd_abs_nb(const jmo_dec *d, int mx, int my, int xN, int yN, int comp) {
+    int tx = xN < 0 ? mx - 1 : mx, ty = yN < 0 ? my - 1 : my;
+    if ((tx != mx || ty != my) && !avail_mb(d, tx, ty, mx, my)) return 0;
+    int W4 = d->W / 4, i = ((16 * my + yN) >> 2) * W4 + ((16 * mx + xN) >> 2);
+    return iabs(d->mvd[2 * i + comp]);
+}
+static void cabac_part(jmo_dec *d, int mx, int my, int x, int y, int w, int h, mbsyn *s) {
+    int p[2], dm[2];
+    mvpred(d, mx, my, x, y, w, h, 0, p);
+    for (int comp = 0; comp < 2; comp++)
+        dm[comp] = cabac_mvd(&d->cab, comp, mvd_abs_nb(d, mx, my, x - 1, y, comp) + mvd_abs_nb(d, mx, my, x, y - 1, comp));
+    set_part(d, mx, my, x, y, w, h, p[0] + dm[0], p[1] + dm[1], 0, s->mv16);
+    int W4 = d->W / 4;
+    for (int yy = y; yy < y + h; yy += 4)
+        for (int xx = x; xx < x + w; xx += 4) {
+            int i = ((16 * my + yy) >> 2) * W4 + ((16 * mx + xx) >> 2);
+            d->mvd[2 * i] = (int16_t)dm[0]; d->mvd[2 * i + 1] = (int16_t)dm[1];
+        }
+}
+
+/* coded_block_flag condTermFlagN of a luma 4x4 block (x4, y4) of neighbour n (9.3.3.1.1.9) */
+static int cbf_luma_nb(const mbinfo *n, int x4, int y4, int cur_intra) {
+    if (!n) return cur_intra;
+    if (n->mbtype == 3) return 0;
+    if (!((n->cbp >> ((y4 >> 1) * 2 + (x4 >> 1))) & 1)) return 0;
+    if (n->t8) return 1;                             /* 8x8 block: flag inferred 1 */
+    return (n->cbf4 >> (y4 * 4 + x4)) & 1;
+}
+
+static int parse_cabac(jmo_dec *d, int mx, int my, int slice_p, mbsyn *s, int *qp) {
+    cabd_t *c = &d->cab;
+    mbinfo *mi = &d->mi[my * d->mbw + mx];
+    const mbinfo *A = avail_mb(d, mx - 1, my, mx, my) ? &d->mi[my * d->mbw + mx - 1] : NULL;
+    const mbinfo *B = avail_mb(d, mx, my - 1, mx, my) ? &d->mi[(my - 1) * d->mbw + mx] : NULL;
+    if (slice_p && cdec(c, 11 + (A && A->mbtype != 3) + (B && B->mbtype != 3))) {   /* mb_skip_flag */
+        skip_motion(d, mx, my, s);
+        d->prev_qpd = 0;
+        return 0;
+    }
+    /* mb_type */
+    int intra = 1, ptype = 0, i16 = 0, cbp = 0;
+    if (slice_p) intra = cdec(c, 14);
+    if (intra) {
+        int o = slice_p ? 17 : 3;
+        int inc = slice_p ? 0 : (A && A->mbtype != 1 && A->mbtype != 4) + (B && B->mbtype != 1 && B->mbtype != 4);
+        i16 = cdec(c, o + inc);
+        if (i16) {
+            if (cterm(c)) FAIL("I_PCM unsupported");
+            int luma = cdec(c, slice_p ? 18 : 6), chroma = cdec(c, slice_p ? 19 : 7);
+            if (chroma) chroma += cdec(c, slice_p ? 19 : 8);
+            int pm = cdec(c, slice_p ? 20 : 9) << 1;
+            pm |= cdec(c, slice_p ? 20 : 10);
+            s->i16mode = pm;
+            cbp = (chroma << 4) | (luma ? 15 : 0);
+        }
+    } else {
+        int b1 = cdec(c, 15), b2 = cdec(c, 16 + b1);
+        ptype = b1 ? (b2 ? 1 : 2) : (b2 ? 3 : 0);       /* 0 16x16, 1 16x8, 2 8x16, 3 8x8 */
+    }
+    int no_sub8x8 = 1;
+    if (intra) {
+        s->intra_type = i16 ? 1 : 0;
+        mi->intra = 1;
+        mi->mbtype = i16 ? 2 : 1;
+        if (!i16) {
+            if (d->t8mode) mi->t8 = cdec(c, 399 + (A && A->t8) + (B && B->t8));
+            if (mi->t8) mi->mbtype = 4;
+            for (int blk = 0; blk < 16; blk += mi->t8 ? 4 : 1) {
+                int x4 = ((blk >> 2) & 1) * 2 + (blk & 1), y4 = (blk >> 3) * 2 + ((blk >> 1) & 1);
+                int pm = pred_ipm(d, mx, my, x4, y4, s->ipm), mode = pm;
+                if (!cdec(c, 68)) {
+                    int rem = cdec(c, 69);
+                    rem |= cdec(c, 69) << 1;
+                    rem |= cdec(c, 69) << 2;
+                    mode = rem < pm ? rem : rem + 1;
+                }
+                set_ipm(s, x4, y4, mode, mi->t8);
+            }
+            for (int k = 0; k < 16; k++) mi->ipm[k] = (int8_t)s->ipm[k];
+        }
+        int ia = A && A->intra && A->cmode, ib = B && B->intra && B->cmode;
+        s->cmode = cdec(c, 64 + ia + ib);
+        if (s->cmode) { s->cmode += cdec(c, 67); if (s->cmode == 2) s->cmode += cdec(c, 67); }
+        mi->cmode = s->cmode;
+    } else {
+        s->intra_type = -1;
+        mi->mbtype = 0;
+        if (ptype == 3) {
+            int sub[4];                                  /* 0 8x8, 1 8x4, 2 4x8, 3 4x4 */
+            for (int i = 0; i < 4; i++) {
+                if (cdec(c, 21)) sub[i] = 0;
+                else if (!cdec(c, 22)) sub[i] = 1;
+                else sub[i] = cdec(c, 23) ? 2 : 3;
+                if (sub[i]) no_sub8x8 = 0;
+            }
+            for (int i = 0; i < 4; i++) {
+                int ox = (i & 1) * 8, oy = (i >> 1) * 8;
+                int sw = sub[i] <= 1 ? 8 : 4, sh = (sub[i] == 0 || sub[i] == 2) ? 8 : 4;
+                for (int y = 0; y < 8; y += sh)
+                    for (int x = 0; x < 8; x += sw) cabac_part(d, mx, my, ox + x, oy + y, sw, sh, s);
+            }
+        } else {
+            int np = ptype == 0 ? 1 : 2, w = ptype == 2 ? 8 : 16, h = ptype == 1 ? 8 : 16;
+            for (int pi = 0; pi < np; pi++) cabac_part(d, mx, my, ptype == 2 ? 8 * pi : 0, ptype == 1 ? 8 * pi : 0, w, h, s);
+        }
+    }
+    if (!i16) {                                           /* coded_block_pattern */
+        for (int b8 = 0; b8 < 4; b8++) {
+            int ta = (b8 & 1) ? !((cbp >> (b8 - 1)) & 1) : A ? !((A->cbp >> (b8 + 1)) & 1) : 0;
+            int tb = (b8 & 2) ? !((cbp >> (b8 - 2)) & 1) : B ? !((B->cbp >> (b8 + 2)) & 1) : 0;
+            cbp |= cdec(c, 73 + ta + 2 * tb) << b8;
+        }
+        int ca = A ? A->cbp >> 4 : 0, cb = B ? B->cbp >> 4 : 0;
+        if (cdec(c, 77 + (ca != 0) + 2 * (cb != 0))) cbp |= (1 + cdec(c, 81 + (ca == 2) + 2 * (cb == 2))) << 4;
+        if (!intra && (cbp & 15) && d->t8mode && no_sub8x8) mi->t8 = cdec(c, 399 + (A && A->t8) + (B && B->t8));
+    }
+    s->cbp = cbp;
+    mi->cbp = cbp;
+    if (!(cbp > 0 || i16)) { d->prev_qpd = 0; return 0; }
+    /* mb_qp_delta: U binarisation of the mapped value, ctxIdx 60..63 */
+    int k = 0;
+    if (cdec(c, 60 + d->prev_qpd)) { k = 1; while (cdec(c, k == 1 ? 62 : 63)) { if (++k > 104) FAIL("mb_qp_delta"); } }
+    int dq = (k & 1) ? (k + 1) / 2 : -(k / 2);
+    d->prev_qpd = dq != 0;
+    *qp = (*qp + dq + 52) % 52;
+    /* residual */
+    int cur_intra = intra, cbpl = cbp & 15, cbpc = cbp >> 4;
+    if (i16) {
+        int ta = A ? (A->mbtype == 2 ? A->cbf_dc & 1 : 0) : 1, tb = B ? (B->mbtype == 2 ? B->cbf_dc & 1 : 0) : 1;
+        mi->cbf_dc |= cabac_block(c, 0, 16, 85 + ta + 2 * tb, s->dc16);
+    }
+    for (int b8 = 0; b8 < 4; b8++) {
+        if (!((cbpl >> b8) & 1)) continue;
+        if (mi->t8) {
+            cabac_block(c, 5, 64, -1, s->l8[b8]);
+            continue;
+        }
+        for (int i4 = 0; i4 < 4; i4++) {
+            int x4 = (b8 & 1) * 2 + (i4 & 1), y4 = (b8 >> 1) * 2 + (i4 >> 1);
+            int ta = x4 ? (mi->cbf4 >> (y4 * 4 + x4 - 1)) & 1 : cbf_luma_nb(A, 3, y4, cur_intra);
+            int tb = y4 ? (mi->cbf4 >> ((y4 - 1) * 4 + x4)) & 1 : cbf_luma_nb(B, x4, 3, cur_intra);
+            int f = i16 ? cabac_block(c, 1, 15, 89 + ta + 2 * tb, s->l4[y4 * 4 + x4] + 1)
+                        : cabac_block(c, 2, 16, 93 + ta + 2 * tb, s->l4[y4 * 4 + x4]);
+            mi->cbf4 |= f << (y4 * 4 + x4);
+        }
+    }
+    if (cbpc)
+        for (int comp = 0; comp < 2; comp++) {
+            int ta = !A ? cur_intra : (A->mbtype == 3 || !(A->cbp >> 4)) ? 0 : (A->cbf_dc >> (1 + comp)) & 1;
+            int tb = !B ? cur_intra : (B->mbtype == 3 || !(B->cbp >> 4)) ? 0 : (B->cbf_dc >> (1 + comp)) & 1;
+            mi->cbf_dc |= cabac_block(c, 3, 4, 97 + ta + 2 * tb, s->cdc[comp]) << (1 + comp);
+        }
+    if (cbpc == 2)
+        for (int comp = 0; comp < 2; comp++)
+            for (int k4 = 0; k4 < 4; k4++) {
+                int ta = (k4 & 1) ? (mi->cbfc[comp] >> (k4 - 1)) & 1
+                         : !A ? cur_intra : (A->mbtype == 3 || (A->cbp >> 4) != 2) ? 0 : (A->cbfc[comp] >> (k4 + 1)) & 1;
+                int tb = (k4 & 2) ? (mi->cbfc[comp] >> (k4 - 2)) & 1
+                         : !B ? cur_intra : (B->mbtype == 3 || (B->cbp >> 4) != 2) ? 0 : (B->cbfc[comp] >> (k4 + 2)) & 1;
+                mi->cbfc[comp] |= cabac_block(c, 4, 15, 101 + ta + 2 * tb, s->cac[comp][k4] + 1) << k4;
+            }
+    return c->b->err ? -1 : 0;
+}
+
+/* prediction + residual reconstruction of a parsed macroblock (8.3, 8.4, 8.5) */
+static int recon_mb(jmo_dec *d, int mx, int my, const mbsyn *s, int qp_) {
+    mbinfo *mi = &d->mi[my * d->mbw + mx];
+    mi->qp = qp_;
+    mi->cbp = s->cbp;
+    uint8_t pred[256], predu[64], predv[64];
+    int intra_type = s->intra_type;
+    if (intra_type < 0) inter_pred(d, mx, my, s->mv16, pred, predu, predv);
+    else {
+        if (predc(d, mx, my, 1, s->cmode, predu) || predc(d, mx, my, 2, s->cmode, predv)) FAIL("chroma pred mode %d unavailable at MB %d,%d", s->cmode, mx, my);
+        if (intra_type == 1 && pred16(d, mx, my, s->i16mode, pred)) FAIL("I16 mode %d unavailable at MB %d,%d", s->i16mode, mx, my);
+    }
+    if (s->skip) mi->cbp = 0;
+    int qpc = QPCt[iclip(0, 51, qp_ + d->cqp_off)];
+    int cbpc = s->cbp >> 4;
     int32_t dcY[16] = {0};
     uint8_t *RY = d->cur[0];
     int W = d->W;
     if (intra_type == 1) {
-        int c[16];
-        if (read_block(b, calc_nc(d, mx, my, 0, 0, 0, mi->tc), 16, c) < 0) FAIL("I16 DC at %d,%d", mx, my);
         int32_t m[16], t2[16];
-        for (int k = 0; k < 16; k++) m[zz[k]] = c[k];
+        for (int k = 0; k < 16; k++) m[zz[k]] = s->dc16[k];
         for (int y = 0; y < 4; y++) {
             int32_t *r = m + 4 * y;
             int e0 = r[0] + r[1] + r[2] + r[3], e1 = r[0] + r[1] - r[2] - r[3], e2 = r[0] - r[1] - r[2] + r[3], e3 = r[0] - r[1] + r[2] - r[3];
@@ -723,43 +1127,26 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
             int f[4] = {a0 + a1 + a2 + a3, a0 + a1 - a2 - a3, a0 - a1 - a2 + a3, a0 - a1 + a2 - a3};
             for (int y = 0; y < 4; y++) {
                 int ls = lscale(qp_ % 6, 0);
-                int v = qp_ >= 36 ? f[y] * ls * (1 << (qp_ / 6 - 6)) : (f[y] * ls + (1 << (5 - qp_ / 6))) >> (6 - qp_ / 6);
-                dcY[4 * y + x] = v;
+                dcY[4 * y + x] = qp_ >= 36 ? f[y] * ls * (1 << (qp_ / 6 - 6)) : (f[y] * ls + (1 << (5 - qp_ / 6))) >> (6 - qp_ / 6);
             }
         }
     }
-    for (int b8 = 0; b8 < 4 && mi->t8; b8++) {       /* 8x8 transform: 4 interleaved CAVLC blocks */
-        int c64[64] = {0}, any = 0;
-        for (int i4 = 0; i4 < 4; i4++) {
-            int x4 = (b8 & 1) * 2 + (i4 & 1), y4 = (b8 >> 1) * 2 + (i4 >> 1), c[16] = {0}, tc = 0;
-            if (cbpl & (1 << b8)) {
-                tc = read_block(b, calc_nc(d, mx, my, 0, x4, y4, mi->tc), 16, c);
-                if (tc < 0) FAIL("luma 8x8 block %d at MB %d,%d", b8, mx, my);
-            }
-            mi->tc[y4 * 4 + x4] = (uint8_t)tc;
-            for (int k = 0; k < 16; k++) { c64[4 * k + i4] = c[k]; any |= c[k] != 0; }
-        }
+    for (int b8 = 0; b8 < 4 && mi->t8; b8++) {       /* 8x8 transform */
+        int any = 0;
+        for (int k = 0; k < 64; k++) any |= s->l8[b8][k] != 0;
         int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
         if (any) mi->nzblk |= 0x33 << ((by >> 2) * 4 + (bx >> 2));
         uint8_t *dst = RY + (16 * my + by) * W + 16 * mx + bx;
         if (intra_type == 0) {
             uint8_t p64[64];
-            if (pred8x8(d, mx, my, b8, ipm[(by >> 2) * 4 + (bx >> 2)], p64)) FAIL("I8 mode unavailable at MB %d,%d", mx, my);
-            recon8x8(c64, qp_, p64, 8, dst, W);
-        } else recon8x8(c64, qp_, pred + by * 16 + bx, 16, dst, W);
+            if (pred8x8(d, mx, my, b8, s->ipm[(by >> 2) * 4 + (bx >> 2)], p64)) FAIL("I8 mode unavailable at MB %d,%d", mx, my);
+            recon8x8(s->l8[b8], qp_, p64, 8, dst, W);
+        } else recon8x8(s->l8[b8], qp_, pred + by * 16 + bx, 16, dst, W);
     }
     for (int blk = 0; blk < 16 && !mi->t8; blk++) {
         int b8 = blk >> 2;
         int x4 = (b8 & 1) * 2 + (blk & 1), y4 = (b8 >> 1) * 2 + ((blk >> 1) & 1);
-        int c[16] = {0};
-        int tc = 0;
-        if (cbpl & (1 << b8)) {
-            int nC = calc_nc(d, mx, my, 0, x4, y4, mi->tc);
-            if (intra_type == 1) { int c15[15]; tc = read_block(b, nC, 15, c15); for (int k = 0; k < 15; k++) c[k + 1] = c15[k]; }
-            else tc = read_block(b, nC, 16, c);
-            if (tc < 0) FAIL("luma block %d at MB %d,%d", blk, mx, my);
-        }
-        mi->tc[y4 * 4 + x4] = (uint8_t)tc;
+        const int *c = s->l4[y4 * 4 + x4];
         int any = 0;
         for (int k = 0; k < 16; k++) any |= c[k] != 0;
         if (any) mi->nzblk |= 1 << (y4 * 4 + x4);
@@ -771,42 +1158,31 @@ static int decode_mb(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int mbt_u
         if (intra_type == 0) {
             uint8_t p4[16];
             int ok;
-            pred4x4(d, mx, my, 4 * x4, 4 * y4, blk, ipm[y4 * 4 + x4], p4, &ok);
-            if (!ok) FAIL("I4 mode %d unavailable at MB %d,%d blk %d", ipm[y4 * 4 + x4], mx, my, blk);
+            pred4x4(d, mx, my, 4 * x4, 4 * y4, blk, s->ipm[y4 * 4 + x4], p4, &ok);
+            if (!ok) FAIL("I4 mode %d unavailable at MB %d,%d blk %d", s->ipm[y4 * 4 + x4], mx, my, blk);
             recon4x4(m, p4, 4, dst, W);
         } else recon4x4(m, pred + 4 * y4 * 16 + 4 * x4, 16, dst, W);
     }
-    /* chroma */
     int dcc[2][4] = {{0}};
-    if (cbpc) {
+    if (cbpc)
         for (int comp = 0; comp < 2; comp++) {
-            int c[4];
-            if (read_block(b, -1, 4, c) < 0) FAIL("chroma DC");
+            const int *c = s->cdc[comp];
             int f[4] = {c[0] + c[1] + c[2] + c[3], c[0] - c[1] + c[2] - c[3], c[0] + c[1] - c[2] - c[3], c[0] - c[1] - c[2] + c[3]};
             for (int k = 0; k < 4; k++) dcc[comp][k] = (f[k] * lscale(qpc % 6, 0) * (1 << (qpc / 6))) >> 5;
         }
-    }
     for (int comp = 0; comp < 2; comp++) {
         uint8_t *R = d->cur[1 + comp];
         int Wc = d->W / 2;
         for (int k = 0; k < 4; k++) {
-            int c[16] = {0}, tc = 0;
-            if (cbpc == 2) {
-                int c15[15];
-                tc = read_block(b, calc_nc(d, mx, my, 1 + comp, k & 1, k >> 1, mi->tc), 15, c15);
-                if (tc < 0) FAIL("chroma AC");
-                for (int q = 0; q < 15; q++) c[q + 1] = c15[q];
-            }
-            mi->tc[16 + 4 * comp + k] = (uint8_t)tc;
             int32_t m[16];
-            for (int q = 0; q < 16; q++) m[zz[q]] = c[q];
+            for (int q = 0; q < 16; q++) m[zz[q]] = s->cac[comp][k][q];
             scale4x4(m, qpc, 1);
             m[0] = dcc[comp][k];
             int xo = (k & 1) * 4, yo = (k >> 1) * 4;
             recon4x4(m, (comp ? predv : predu) + yo * 8 + xo, 8, R + (8 * my + yo) * Wc + 8 * mx + xo, Wc);
         }
     }
-    return b->err ? -1 : 0;
+    return 0;
 }
 
 /* ---- deblocking (8.7), independent restatement ------------------------------------------ */
@@ -927,6 +1303,7 @@ static int decode_slice(jmo_dec *d, br_t *b, int nal_type, int nal_ref_idc, int 
         if (rb(b)) FAIL("reordering unsupported");
     }
     if (nal_ref_idc) { if (nal_type == 5) { rb(b); rb(b); } else if (rb(b)) FAIL("MMCO unsupported"); }
+    if (d->cabac && st == 0 && rue(b) != 0) FAIL("cabac_init_idc other than 0 unsupported");
     int qp = d->init_qp + rse(b);
     d->dis_dbf = 0; d->offA = d->offB = 0;
     if (d->dfc_present) {
@@ -937,19 +1314,37 @@ static int decode_slice(jmo_dec *d, br_t *b, int nal_type, int nal_ref_idc, int 
     if (first == 0) memset(d->dec4, 0, (size_t)d->W * d->H / 16);
     d->slice_first = first;
     int a = first, more = 1;
-    while (more && a < nmb) {
+    mbsyn syn;
+    if (d->cabac) {                            /* slice_data with CABAC (7.3.4) */
+        while (b->pos & 7) if (!rb(b)) FAIL("cabac_alignment_one_bit");
+        cabd_start(&d->cab, b, st == 2, qp);
+        d->prev_qpd = 0;
+        while (a < nmb) {
+            int mx = a % d->mbw, my = a / d->mbw;
+            mb_begin(d, mx, my, &syn);
+            if (parse_cabac(d, mx, my, st == 0, &syn, &qp) || recon_mb(d, mx, my, &syn, qp)) return -1;
+            a++;
+            if (b->err) FAIL("CABAC slice data overrun at MB %d", a);
+            if (cterm(&d->cab)) break;             /* end_of_slice_flag */
+        }
+    }
+    while (!d->cabac && more && a < nmb) {
         if (st == 0) {
             int run = rue(b);
             if (b->err) FAIL("skip run");
             for (int i = 0; i < run && a < nmb; i++, a++) {
-                if (decode_mb(d, b, a % d->mbw, a / d->mbw, 1, 0, 1, &qp)) return -1;
+                mb_begin(d, a % d->mbw, a / d->mbw, &syn);
+                skip_motion(d, a % d->mbw, a / d->mbw, &syn);
+                if (recon_mb(d, a % d->mbw, a / d->mbw, &syn, qp)) return -1;
             }
             if (run > 0) more = more_rbsp_data(b);
         }
         if (more && a < nmb) {
             int t = rue(b);
             if (b->err) FAIL("mb_type at MB %d", a);
-            if (decode_mb(d, b, a % d->mbw, a / d->mbw, st == 0, t, 0, &qp)) return -1;
+            int mx = a % d->mbw, my = a / d->mbw;
+            mb_begin(d, mx, my, &syn);
+            if (parse_cavlc(d, b, mx, my, st == 0, t, &syn, &qp) || recon_mb(d, mx, my, &syn, qp)) return -1;
             a++;
             more = more_rbsp_data(b);
         }

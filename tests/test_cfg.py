@@ -48,8 +48,25 @@ def test_jm86_spellings_accepted():
 def test_transform8x8_requires_high_profile():
     r = run("-p", "Transform8x8Mode=1")
     assert r.returncode != 0 and "ProfileIDC=100" in r.stderr
-    r = run("-p", "ProfileIDC=77")
+    r = run("-p", "ProfileIDC=88")
     assert r.returncode != 0 and "ProfileIDC" in r.stderr
+    r = run("-p", "ProfileIDC=77", "-p", "Transform8x8Mode=1")
+    assert r.returncode != 0 and "ProfileIDC=100" in r.stderr
+
+
+def test_cabac_keys():
+    """SymbolMode 1 (CABAC) needs Main / High; the adaptive context initialisation and
+    cabac_init_idc 1 / 2 are rejected loudly (docs/JM_SEMANTICS.md item 48)."""
+    r = run("-p", "SymbolMode=1")
+    assert r.returncode != 0 and "Baseline" in r.stderr
+    r = run("-p", "SymbolMode=1", "-p", "ProfileIDC=77", "-p", "ContextInitMethod=1")
+    assert r.returncode != 0 and "ContextInitMethod" in r.stderr
+    r = run("-p", "SymbolMode=1", "-p", "ProfileIDC=77", "-p", "FixedModelNumber=2")
+    assert r.returncode != 0 and "FixedModelNumber" in r.stderr
+    with tempfile.TemporaryDirectory() as d:
+        r = run("-p", "SymbolMode=1", "-p", "ProfileIDC=77", "-p", "FramesToBeEncoded=2", "-p", "SourceWidth=64",
+                "-p", "SourceHeight=48", "-p", "SearchRange=2", "-p", f"OutputFile={d}/o.264")
+        assert r.returncode == 0, r.stderr
 
 
 def test_slice_mode_keys():

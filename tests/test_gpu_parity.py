@@ -457,6 +457,13 @@ def run_lencod(binary, out_dir, extra):
      "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "SliceMode=1", "SliceArgument=40"],
     ["InputFile=synthetic:31", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=8",
      "SearchMode=-1", "SliceMode=1", "SliceArgument=1"],
+    # CABAC (SymbolMode 1, row f4): pipelined device backend + writer threads, Main and High
+    ["InputFile=synthetic:32", "FramesToBeEncoded=8", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=77", "SymbolMode=1", "IntraPeriod=4"],
+    ["InputFile=synthetic:33", "FramesToBeEncoded=6", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "SymbolMode=1", "SliceMode=1", "SliceArgument=22"],
+    ["InputFile=synthetic:34", "FramesToBeEncoded=4", "SourceWidth=176", "SourceHeight=144", "SearchRange=8",
+     "ProfileIDC=77", "SymbolMode=1", "SearchMode=-1", "QPFirstFrame=0", "QPRemainingFrame=2", "WriterThreads=0"],
 ])
 def test_lencod_bitstream_identical(extra):
     with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:

@@ -13,7 +13,7 @@ import tempfile
 import pytest
 
 from jmpaths import ORACLE
-from test_closed_loop import CONFIGS
+from test_closed_loop import CABAC, CONFIGS
 
 ASAN = os.path.join(ORACLE, "_build_asan")
 LENCOD_ASAN = os.path.join(ASAN, "lencod_cpu")
@@ -26,7 +26,8 @@ SAN_CASES = [CONFIGS[0], CONFIGS[1], CONFIGS[4], CONFIGS[6], CONFIGS[7], CONFIGS
              CONFIGS[6] + ["JMCallSurface=1"],
              CONFIGS[12] + ["WriterThreads=0", "JMCallSurface=1"],
              CONFIGS[19] + ["WriterThreads=4"],                # SliceMode 1 (several NAL units per picture)
-             CONFIGS[20] + ["JMCallSurface=1"]]
+             CONFIGS[20] + ["JMCallSurface=1"],
+             CABAC[0], CABAC[2], CABAC[5], CABAC[7] + ["WriterThreads=4"]]   # CABAC coder + parser
 
 ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=86",
            UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=87")

@@ -4,8 +4,9 @@
   python tools/make_golden.py          # rewrite tests/golden/*
 
 Fixtures (all data; no reference source text):
-  manifest.json   sha256 of lencod_cpu bitstreams + reconstructions for four encoder.cfg
-                  configurations (the first three as in the GPU bitstream test; one with slices), and of the
+  manifest.json   sha256 of lencod_cpu bitstreams + reconstructions for five encoder.cfg
+                  configurations (the first three as in the GPU bitstream test; one with slices, one
+                  CABAC), and of the
                   per-picture jmh_mb_result arrays + reconstructions of a 64x48 I-P-P sequence
   tq4x4.npz       dct_luma vectors: residual/prediction inputs and levels/recon/cost/nonzero
                   outputs at QP 0, 12, 28, 51, intra and inter rounding
@@ -40,6 +41,9 @@ LENCOD_CONFIGS = [
     # SliceMode 1 (docs/JM_SEMANTICS.md item 47): 22-MB slices, EPZS + 8x8 transform
     ["InputFile=synthetic:4", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
      "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "SliceMode=1", "SliceArgument=22"],
+    # CABAC (SymbolMode 1, docs/JM_SEMANTICS.md item 48): High, 8x8 transform, slices, an I picture every 3
+    ["InputFile=synthetic:5", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SymbolMode=1", "SliceMode=1", "SliceArgument=33", "IntraPeriod=3"],
 ]
 SEQ = dict(w=64, h=48, seed=21, frames=3, qp=28, search_range=16)
 
@@ -81,11 +85,15 @@ def main():
     ensure_built()
     os.makedirs(GOLD, exist_ok=True)
     rng = np.random.default_rng(20261015)
-    manifest = {"lencod": [], "sequence": {"spec": SEQ}}
+    manifest = {"provenance": "self-generated regression pins: outputs of this repository's oracle (lencod_cpu / "
+                              "liboracle), not of JM; JM parity is unpinned (no JM source, binary or vectors "
+                              "exist in the reference, DESIGN.md section 6)",
+                "lencod": [], "sequence": {"spec": SEQ}}
     for extra in LENCOD_CONFIGS:
         with tempfile.TemporaryDirectory() as d:
             bs, rec = run_lencod(LENCOD_CPU, extra, d)
-        manifest["lencod"].append({"params": extra, "bitstream_sha256": sha(bs), "bitstream_bytes": len(bs),
+        manifest["lencod"].append({"kind": "regression_pin", "params": extra, "bitstream_sha256": sha(bs),
+                                   "bitstream_bytes": len(bs),
                                    "recon_sha256": sha(rec), "bitstream_head_hex": bs[:48].hex()})
     manifest["sequence"]["pictures"] = oracle_sequence()
     with open(os.path.join(GOLD, "manifest.json"), "w") as f:
