@@ -50,6 +50,9 @@ struct DevParams {
     int t8;                     // Transform8x8Mode (High profile)
     int epzs_dual;              // EPZSDualRefinement (SearchMode 3)
     int slice_mbs;              // SliceMode 1: MBs per slice (the whole picture for one slice)
+    int maxv, qpbd;             // (1 << bit depth) - 1 (Clip1), QpBdOffsetY = QpBdOffsetC = 6 (bit depth - 8)
+    // plane pointers are byte addresses of uint8_t (bit depth 8) or uint16_t (9 / 10) samples:
+    // the kernels templated on the sample type cast them (PL<pel>)
     const uint8_t *orgY, *orgU, *orgV;
     const uint8_t *refY, *refU, *refV;
     uint8_t *recY, *recU, *recV;
@@ -112,6 +115,7 @@ struct TickArgs {
     int t8;                              // Transform8x8Mode: k_mb_intra8 ran, k_mb_final decides 4x4 / 8x8
     int epzs_dual;                       // EPZSDualRefinement (k_mb_epzs)
     int slice_mbs;                       // SliceMode 1: MBs per slice (>= 1; mbw * mbh for one slice)
+    int bd;                              // bit depth: 8 (uint8_t samples) or 9 / 10 (uint16_t, High 10)
     const uint32_t *ordtab;              // FFS order keys, [NPK / 2][NTA] packed pairs (jmh_create)
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
@@ -147,7 +151,8 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.t8 = t.t8;
     d.epzs_dual = t.epzs_dual;
     d.slice_mbs = t.slice_mbs;
-    const int ls = t.W * t.H, lc = ls >> 2;
+    d.maxv = (1 << t.bd) - 1; d.qpbd = 6 * (t.bd - 8);
+    const int ps = t.bd > 8 ? 2 : 1, ls = t.W * t.H * ps, lc = ls >> 2;
     d.orgY = q.org; d.orgU = q.org + ls; d.orgV = q.org + ls + lc;
     d.refY = q.ref; d.refU = q.ref + ls; d.refV = q.ref + ls + lc;
     d.recY = q.rec; d.recU = q.rec + ls; d.recV = q.rec + ls + lc;
@@ -160,3 +165,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.cqp_off = q.cqp_off; d.qsel = q.qsel; d.diag = q.diag; d.y_min = q.y_min;
     return d;
 }
+
+// sample-typed view of a DevParams plane pointer (bytes of uint8_t or uint16_t samples)
+template <class pel> __device__ __forceinline__ pel *PL(uint8_t *p) { return reinterpret_cast<pel *>(p); }
+template <class pel> __device__ __forceinline__ const pel *PL(const uint8_t *p) { return reinterpret_cast<const pel *>(p); }

@@ -138,6 +138,7 @@ struct jmh_ctx {
     uint8_t *d_scur, *d_sref;            // luma pictures of the per-block searches (jmh_search_pictures)
     uint32_t *d_ordtab;                  // FFS order keys of the analysis threads' strips (ordtab_fill)
     uint16_t *d_scur16, *d_sref16;       // 16-bit luma pictures of the High 10 seams (jmh_search_pictures_u16)
+    int bd, ps, maxv;                    // picture bit depth, bytes per sample (1, 2), (1 << bd) - 1
     int hbd_bits;                        //   and their bit depth
     int nslots;
     int depth, nring;
@@ -283,6 +284,10 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->jm_version < 0 || cfg->jm_version == 9 || cfg->jm_version > 99) return JMH_E_UNSUPPORTED_CFG;   // 0 / 8: JM 8.6, 10..: JM >= 10
     if (cfg->epzs_dual_refinement != 0 && cfg->epzs_dual_refinement != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->slice_mbs < 0) return JMH_E_INVALID_ARG;
+    if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
+    // High 10 pictures: the EPZS wavefront (k_mb_epzs / k_mb_intra / k_mb_final on 16-bit samples)
+    if (cfg->bit_depth > 8 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->bit_depth > 8) return JMH_E_UNSUPPORTED_CFG;   // TEMP: kernels not yet templated
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     int ndev = jmh_device_count();
@@ -296,7 +301,8 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     c->mbw = c->W / 16; c->mbh = c->H / 16;
     c->sr = cfg->search_range; c->side = 2 * c->sr + 1; c->npos = c->side * c->side;
     c->qstride = c->W + 2 * QPAD; c->qplane = c->qstride * (c->H + 2 * QPAD);
-    c->fsize = (size_t)c->W * c->H * 3 / 2;
+    c->bd = cfg->bit_depth > 8 ? cfg->bit_depth : 8; c->ps = c->bd > 8 ? 2 : 1; c->maxv = (1 << c->bd) - 1;
+    c->fsize = (size_t)c->W * c->H * 3 / 2 * c->ps;
     c->n4 = (size_t)c->W * c->H / 16; c->nmb = (size_t)c->mbw * c->mbh;
     c->nslots = cfg->num_frame_slots > 0 ? cfg->num_frame_slots : 1;
     c->nd = (c->mbw - 1) + 2 * (c->mbh - 1) + 1;
@@ -386,22 +392,40 @@ static void ordtab_fill(std::vector<uint32_t> &tab, int sr) {
     }
 }
 
-static void pack_planes(uint8_t *dst, int W, int H, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
-    for (int r = 0; r < H; r++) memcpy(dst + (size_t)r * W, y + (size_t)r * sy, W);
-    uint8_t *du = dst + (size_t)W * H, *dv = du + (size_t)W * H / 4;
+// planar 4:2:0 packing of ps-byte samples (strides in samples)
+static void pack_planes(uint8_t *dst, int W, int H, const void *yv, const void *uv, const void *vv, int sy, int sc, int ps) {
+    const uint8_t *y = (const uint8_t *)yv, *u = (const uint8_t *)uv, *v = (const uint8_t *)vv;
+    for (int r = 0; r < H; r++) memcpy(dst + (size_t)r * W * ps, y + (size_t)r * sy * ps, (size_t)W * ps);
+    uint8_t *du = dst + (size_t)W * H * ps, *dv = du + (size_t)W * H / 4 * ps;
     for (int r = 0; r < H / 2; r++) {
-        memcpy(du + (size_t)r * (W / 2), u + (size_t)r * sc, W / 2);
-        memcpy(dv + (size_t)r * (W / 2), v + (size_t)r * sc, W / 2);
+        memcpy(du + (size_t)r * (W / 2) * ps, u + (size_t)r * sc * ps, (size_t)(W / 2) * ps);
+        memcpy(dv + (size_t)r * (W / 2) * ps, v + (size_t)r * sc * ps, (size_t)(W / 2) * ps);
     }
 }
 
-static void unpack_planes(const uint8_t *src, int W, int H, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
-    size_t ls = (size_t)W * H;
-    for (int r = 0; r < H; r++) memcpy(y + (size_t)r * sy, src + (size_t)r * W, W);
+static void unpack_planes(const uint8_t *src, int W, int H, void *yv, void *uv, void *vv, int sy, int sc, int ps) {
+    uint8_t *y = (uint8_t *)yv, *u = (uint8_t *)uv, *v = (uint8_t *)vv;
+    size_t ls = (size_t)W * H * ps;
+    for (int r = 0; r < H; r++) memcpy(y + (size_t)r * sy * ps, src + (size_t)r * W * ps, (size_t)W * ps);
     for (int r = 0; r < H / 2; r++) {
-        memcpy(u + (size_t)r * sc, src + ls + (size_t)r * (W / 2), W / 2);
-        memcpy(v + (size_t)r * sc, src + ls + ls / 4 + (size_t)r * (W / 2), W / 2);
+        memcpy(u + (size_t)r * sc * ps, src + ls + (size_t)r * (W / 2) * ps, (size_t)(W / 2) * ps);
+        memcpy(v + (size_t)r * sc * ps, src + ls + ls / 4 + (size_t)r * (W / 2) * ps, (size_t)(W / 2) * ps);
     }
+}
+
+// a picture handed to a High 10 context: every sample within the bit depth (the kernels' cost keys
+// and transform headroom assume it), and the entry point's sample width matches the context
+static int check_pic(const jmh_ctx *c, const void *y, const void *u, const void *v, int sy, int sc, bool wide) {
+    if ((c->bd > 8) != wide) return JMH_E_UNSUPPORTED_CFG;
+    if (!wide) return JMH_OK;
+    const uint16_t *pl[3] = {(const uint16_t *)y, (const uint16_t *)u, (const uint16_t *)v};
+    for (int k = 0; k < 3; k++) {
+        const int w = k ? c->Wc : c->W, h = k ? c->Hc : c->H, s = k ? sc : sy;
+        for (int r = 0; r < h; r++)
+            for (int x = 0; x < w; x++)
+                if (pl[k][(size_t)r * s + x] > c->maxv) return JMH_E_INVALID_ARG;
+    }
+    return JMH_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -441,6 +465,7 @@ static int issue_tick(jmh_ctx *c) {
     t.t8 = c->cfg.transform_8x8_mode;
     t.epzs_dual = c->cfg.epzs_dual_refinement;
     t.slice_mbs = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : c->mbw * c->mbh;
+    t.bd = c->bd;
     t.ordtab = c->d_ordtab;
     int act[PMAX], nact = 0, nP = 0;
     const int nf = (int)c->fl.size();
@@ -614,17 +639,27 @@ static int claim_entry(jmh_ctx *c, int *out) {
 
 extern "C" {
 
-int jmh_set_reference(jmh_ctx *c, int list, int ref_idx, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
+}  // extern "C"
+static int set_reference_any(jmh_ctx *c, int list, int ref_idx, const void *y, const void *u, const void *v, int sy, int sc, bool wide) {
     if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
     if (list != 0 || ref_idx != 0) return JMH_E_UNSUPPORTED_CFG;
+    int r = check_pic(c, y, u, v, sy, sc, wide);
+    if (r) return r;
     HCHK(hipSetDevice(c->dev));
-    int r = drain(c);   // pictures in flight may read d_ref
+    r = drain(c);   // pictures in flight may read d_ref
     if (r) return r;
     HCHK(hipStreamSynchronize(c->st));   // staging buffer reuse
-    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc);
+    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc, c->ps);
     HCHK(hipMemcpyAsync(c->d_ref, c->h_stage_ref, c->fsize, hipMemcpyHostToDevice, c->st));
     c->ref_kind = REF_BUF; c->ref_entry = -1;
     return JMH_OK;
+}
+extern "C" {
+int jmh_set_reference(jmh_ctx *c, int list, int ref_idx, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
+    return set_reference_any(c, list, ref_idx, y, u, v, sy, sc, false);
+}
+int jmh_set_reference_u16(jmh_ctx *c, int list, int ref_idx, const uint16_t *y, const uint16_t *u, const uint16_t *v, int sy, int sc) {
+    return set_reference_any(c, list, ref_idx, y, u, v, sy, sc, true);
 }
 
 int jmh_set_reference_slot(jmh_ctx *c, int slot) {
@@ -643,10 +678,12 @@ int jmh_set_reference_slot(jmh_ctx *c, int slot) {
     return JMH_OK;
 }
 
-int jmh_frame_push(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc, const jmh_frame_params *fp) {
+}  // extern "C"
+static int frame_push_any(jmh_ctx *c, const void *y, const void *u, const void *v, int sy, int sc, const jmh_frame_params *fp, bool wide) {
     if (!c || !y || !u || !v || !fp || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
     int r = check_params(c, fp);
     if (r) return r;
+    if ((r = check_pic(c, y, u, v, sy, sc, wide))) return r;
     if ((int)c->popq.size() >= c->depth) return JMH_E_STATE;
     HCHK(hipSetDevice(c->dev));
     int e;
@@ -654,12 +691,19 @@ int jmh_frame_push(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t
     PicBuf &b = c->ring[e];
     if ((r = alloc_host(c, b))) return r;
     HCHK(hipEventSynchronize(b.ev_src));   // the previous H2D out of this staging buffer
-    pack_planes(b.h_src, c->W, c->H, y, u, v, sy, sc);
+    pack_planes(b.h_src, c->W, c->H, y, u, v, sy, sc, c->ps);
     HCHK(hipEventRecord(b.ev_t0, c->st));
     HCHK(hipMemcpyAsync(b.src, b.h_src, c->fsize, hipMemcpyHostToDevice, c->st));
     HCHK(hipEventRecord(b.ev_src, c->st));
     c->popq.push_back(e);
     return push_picture(c, b.src, e, fp, true);
+}
+extern "C" {
+int jmh_frame_push(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc, const jmh_frame_params *fp) {
+    return frame_push_any(c, y, u, v, sy, sc, fp, false);
+}
+int jmh_frame_push_u16(jmh_ctx *c, const uint16_t *y, const uint16_t *u, const uint16_t *v, int sy, int sc, const jmh_frame_params *fp) {
+    return frame_push_any(c, y, u, v, sy, sc, fp, true);
 }
 
 int jmh_frame_pop(jmh_ctx *c) {
@@ -690,6 +734,9 @@ int jmh_frame_pop(jmh_ctx *c) {
 int jmh_frame_submit(jmh_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc, const jmh_frame_params *fp) {
     return jmh_frame_push(c, y, u, v, sy, sc, fp);
 }
+int jmh_frame_submit_u16(jmh_ctx *c, const uint16_t *y, const uint16_t *u, const uint16_t *v, int sy, int sc, const jmh_frame_params *fp) {
+    return jmh_frame_push_u16(c, y, u, v, sy, sc, fp);
+}
 
 int jmh_frame_wait(jmh_ctx *c) { return jmh_frame_pop(c); }
 
@@ -698,30 +745,38 @@ const jmh_mb_result *jmh_get_mb_result(const jmh_ctx *c, int mb_addr) {
     return &c->ring[c->cur_entry].h_res[mb_addr];
 }
 
-int jmh_read_recon(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
+}  // extern "C"
+static int read_pic(jmh_ctx *c, void *y, void *u, void *v, int sy, int sc, bool wide, bool dbk) {
     if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
-    if (c->cur_entry < 0 || !c->ring[c->cur_entry].recon_read) return JMH_E_STATE;
-    unpack_planes(c->ring[c->cur_entry].h_rec, c->W, c->H, y, u, v, sy, sc);
+    if ((c->bd > 8) != wide) return JMH_E_UNSUPPORTED_CFG;
+    if (c->cur_entry < 0 || !(dbk ? c->ring[c->cur_entry].deblocked : c->ring[c->cur_entry].recon_read)) return JMH_E_STATE;
+    const PicBuf &b = c->ring[c->cur_entry];
+    unpack_planes(dbk ? b.h_dbk : b.h_rec, c->W, c->H, y, u, v, sy, sc, c->ps);
     return JMH_OK;
 }
-
-int jmh_read_deblocked(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) {
-    if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
-    if (c->cur_entry < 0 || !c->ring[c->cur_entry].deblocked) return JMH_E_STATE;
-    unpack_planes(c->ring[c->cur_entry].h_dbk, c->W, c->H, y, u, v, sy, sc);
-    return JMH_OK;
-}
-
-int jmh_load_frame(jmh_ctx *c, int slot, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
+static int load_frame_any(jmh_ctx *c, int slot, const void *y, const void *u, const void *v, int sy, int sc, bool wide) {
     if (!c || slot < 0 || slot >= c->nslots || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
+    int r = check_pic(c, y, u, v, sy, sc, wide);
+    if (r) return r;
     HCHK(hipSetDevice(c->dev));
-    int r = drain(c);   // pictures in flight may read the slot
+    r = drain(c);   // pictures in flight may read the slot
     if (r) return r;
     HCHK(hipStreamSynchronize(c->st));
-    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc);
+    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc, c->ps);
     HCHK(hipMemcpyAsync(c->d_slots + (size_t)slot * c->fsize, c->h_stage_ref, c->fsize, hipMemcpyHostToDevice, c->st));
     HCHK(hipStreamSynchronize(c->st));
     return JMH_OK;
+}
+extern "C" {
+int jmh_read_recon(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) { return read_pic(c, y, u, v, sy, sc, false, false); }
+int jmh_read_recon_u16(jmh_ctx *c, uint16_t *y, uint16_t *u, uint16_t *v, int sy, int sc) { return read_pic(c, y, u, v, sy, sc, true, false); }
+int jmh_read_deblocked(jmh_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int sy, int sc) { return read_pic(c, y, u, v, sy, sc, false, true); }
+int jmh_read_deblocked_u16(jmh_ctx *c, uint16_t *y, uint16_t *u, uint16_t *v, int sy, int sc) { return read_pic(c, y, u, v, sy, sc, true, true); }
+int jmh_load_frame(jmh_ctx *c, int slot, const uint8_t *y, const uint8_t *u, const uint8_t *v, int sy, int sc) {
+    return load_frame_any(c, slot, y, u, v, sy, sc, false);
+}
+int jmh_load_frame_u16(jmh_ctx *c, int slot, const uint16_t *y, const uint16_t *u, const uint16_t *v, int sy, int sc) {
+    return load_frame_any(c, slot, y, u, v, sy, sc, true);
 }
 
 int jmh_encode_slot(jmh_ctx *c, int slot, const jmh_frame_params *fp) {
@@ -820,6 +875,7 @@ int jmh_ffs_sad_table(jmh_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t 
     for (int i = 0; i < n_mb; i++)
         if (mb_xy[2 * i] < 0 || mb_xy[2 * i] >= c->mbw || mb_xy[2 * i + 1] < 0 || mb_xy[2 * i + 1] >= c->mbh) return JMH_E_INVALID_ARG;
     if (c->ref_kind == REF_NONE) return JMH_E_STATE;
+    if (c->bd > 8) return JMH_E_UNSUPPORTED_CFG;   // the 8-bit SAD-table seam (High 10: jmh_ffs_sad_table_u16)
     HCHK(hipSetDevice(c->dev));
     int r = drain(c);
     if (r) return r;
@@ -1029,6 +1085,7 @@ int jmh_tq8x8_batch_u16(jmh_ctx *c, int n, const int16_t *resid, const uint16_t 
 int jmh_read_qpel(jmh_ctx *c, uint8_t *out) {
     if (!c || !out) return JMH_E_INVALID_ARG;
     if (c->ref_kind == REF_NONE) return JMH_E_STATE;
+    if (c->bd > 8) return JMH_E_UNSUPPORTED_CFG;   // 8-bit phase planes
     HCHK(hipSetDevice(c->dev));
     int r = drain(c);
     if (r) return r;

@@ -59,10 +59,11 @@ void jm_write_sps(jm_bits *b, const jm_seq *s) {
     jm_put(b, 0, 8);                         /* constraint_set0..3 = 0, reserved_zero_4bits */
     jm_put(b, s->level_idc, 8);
     jm_put_ue(b, 0);                         /* seq_parameter_set_id */
-    if (s->profile_idc >= 100) {             /* High: 4:2:0, 8 bit, no scaling matrices */
+    if (s->profile_idc >= 100) {             /* High / High 10: 4:2:0, no scaling matrices */
+        const int bd = s->bit_depth > 8 ? s->bit_depth : 8;
         jm_put_ue(b, 1);                     /* chroma_format_idc */
-        jm_put_ue(b, 0);                     /* bit_depth_luma_minus8 */
-        jm_put_ue(b, 0);                     /* bit_depth_chroma_minus8 */
+        jm_put_ue(b, bd - 8);                /* bit_depth_luma_minus8 */
+        jm_put_ue(b, bd - 8);                /* bit_depth_chroma_minus8 */
         jm_put(b, 0, 1);                     /* qpprime_y_zero_transform_bypass_flag */
         jm_put(b, 0, 1);                     /* seq_scaling_matrix_present_flag */
     }

@@ -52,6 +52,8 @@ static const map_entry Map[] = {
     {"LevelIDC", 0, OFF(level_idc), 9, 62},
     {"SymbolMode", 0, OFF(symbol_mode), 0, 1},
     {"ContextInitMethod", 0, OFF(context_init_method), 0, 1},
+    {"SourceBitDepthLuma", 0, OFF(bit_depth_luma), 8, 14},
+    {"SourceBitDepthChroma", 0, OFF(bit_depth_chroma), 8, 14},
     {"FixedModelNumber", 0, OFF(model_number), 0, 2},
     {"LoopFilterParametersFlag", 0, OFF(lf_params_flag), 0, 1},
     {"LoopFilterDisable", 0, OFF(lf_disable), 0, 1},
@@ -97,6 +99,7 @@ void jm_input_defaults(jm_input *inp) {
     inp->jm_version = 8;
     inp->qoff_intra = inp->qoff_inter = -1;
     inp->slice_arg = 50;                       /* encoder.cfg SliceArgument default [J] */
+    inp->bit_depth_luma = inp->bit_depth_chroma = 8;
 }
 
 int jm_set_param(jm_input *inp, const char *key, const char *val, char *err, int errlen) {
@@ -180,7 +183,11 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->search_mode != 0 && inp->search_mode != -1 && inp->search_mode != 3) { snprintf(err, errlen, "SearchMode=%d not supported (use -1, 0 or 3)", inp->search_mode); return -1; }
     if (inp->num_ref_frames != 1) { snprintf(err, errlen, "NumberReferenceFrames=%d not supported (1)", inp->num_ref_frames); return -1; }
     if (inp->constrained_intra) { snprintf(err, errlen, "UseConstrainedIntraPred=1 not supported"); return -1; }
-    if (inp->profile_idc != 66 && inp->profile_idc != 77 && inp->profile_idc != 100) { snprintf(err, errlen, "ProfileIDC=%d not supported (66, 77 or 100)", inp->profile_idc); return -1; }
+    if (inp->profile_idc != 66 && inp->profile_idc != 77 && inp->profile_idc != 100 && inp->profile_idc != 110) { snprintf(err, errlen, "ProfileIDC=%d not supported (66, 77, 100 or 110)", inp->profile_idc); return -1; }
+    if (inp->bit_depth_luma > 10 || inp->bit_depth_chroma != inp->bit_depth_luma) { snprintf(err, errlen, "SourceBitDepthLuma=%d / SourceBitDepthChroma=%d not supported (equal, 8..10)", inp->bit_depth_luma, inp->bit_depth_chroma); return -1; }
+    if (inp->bit_depth_luma > 8 && inp->profile_idc != 110) { snprintf(err, errlen, "SourceBitDepthLuma=%d requires ProfileIDC=110 (High 10)", inp->bit_depth_luma); return -1; }
+    if (inp->bit_depth_luma > 8 && inp->search_mode != 3) { snprintf(err, errlen, "SourceBitDepthLuma > 8 supports SearchMode=3 (EPZS) only"); return -1; }
+    if (inp->bit_depth_luma > 8 && inp->jm_call_surface) { snprintf(err, errlen, "JMCallSurface=1 runs the 8-bit per-block seams (SourceBitDepthLuma 8)"); return -1; }
     if (inp->transform_8x8_mode == 2) { snprintf(err, errlen, "Transform8x8Mode=2 not supported (0 or 1)"); return -1; }
     if (inp->transform_8x8_mode && inp->profile_idc < 100) { snprintf(err, errlen, "Transform8x8Mode=1 requires ProfileIDC=100 (High)"); return -1; }
     if ((inp->width & 1) || (inp->height & 1)) { snprintf(err, errlen, "Source size must be even"); return -1; }
@@ -237,5 +244,6 @@ void jm_fill_config(const jm_input *inp, jmh_config *cfg) {
     cfg->jm_version = inp->jm_version;
     cfg->epzs_dual_refinement = inp->epzs_dual;
     cfg->slice_mbs = inp->slice_mode == 1 ? inp->slice_arg : 0;
+    cfg->bit_depth = inp->bit_depth_luma;
     if (inp->jm_version >= 10) { cfg->quant_offset[0] = inp->qoff_intra; cfg->quant_offset[1] = inp->qoff_inter; }
 }

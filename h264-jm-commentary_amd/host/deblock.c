@@ -43,52 +43,64 @@ static int strength(const jmh_mb_result *rp, int bp, const jmh_mb_result *rq, in
     return 0;
 }
 
-/* filter one line of samples across an edge; p[-k*step] = pk, p[k*step] = q_k (q0 at p[0]) */
-static void filter_line(uint8_t *q0p, int step, int bS, int alpha, int beta, int tc0, int chroma) {
-    int p0 = q0p[-step], p1 = q0p[-2 * step], q0 = q0p[0], q1 = q0p[step];
-    if (!(iabs_(p0 - q0) < alpha && iabs_(p1 - p0) < beta && iabs_(q1 - q0) < beta)) return;
-    if (chroma) {
-        if (bS < 4) {
-            int tc = tc0 + 1;
-            int d = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
-            q0p[-step] = (uint8_t)clip3(0, 255, p0 + d);
-            q0p[0] = (uint8_t)clip3(0, 255, q0 - d);
-        } else {
-            q0p[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
-            q0p[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
-        }
-        return;
+/* filter one line of samples across an edge; p[-k*step] = pk, p[k*step] = q_k (q0 at p[0]).
+ * alpha, beta, tc0 already scaled by 1 << (BitDepth - 8) (8.7.2.2 / 8.7.2.3), Clip1 to maxv. */
+#define FILTER_LINE(NAME, T)                                                                            \
+    static void NAME(T *q0p, int step, int bS, int alpha, int beta, int tc0, int chroma, int maxv) {    \
+        int p0 = q0p[-step], p1 = q0p[-2 * step], q0 = q0p[0], q1 = q0p[step];                        \
+        if (!(iabs_(p0 - q0) < alpha && iabs_(p1 - p0) < beta && iabs_(q1 - q0) < beta)) return;     \
+        if (chroma) {                                                                                  \
+            if (bS < 4) {                                                                              \
+                int tc = tc0 + 1;                                                                      \
+                int d = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);                          \
+                q0p[-step] = (T)clip3(0, maxv, p0 + d);                                                \
+                q0p[0] = (T)clip3(0, maxv, q0 - d);                                                    \
+            } else {                                                                                   \
+                q0p[-step] = (T)((2 * p1 + p0 + q1 + 2) >> 2);                                         \
+                q0p[0] = (T)((2 * q1 + q0 + p1 + 2) >> 2);                                             \
+            }                                                                                          \
+            return;                                                                                    \
+        }                                                                                              \
+        int p2 = q0p[-3 * step], q2 = q0p[2 * step];                                                   \
+        int ap = iabs_(p2 - p0), aq = iabs_(q2 - q0);                                                  \
+        if (bS < 4) {                                                                                  \
+            int tc = tc0 + (ap < beta) + (aq < beta);                                                  \
+            int d = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);                              \
+            q0p[-step] = (T)clip3(0, maxv, p0 + d);                                                    \
+            q0p[0] = (T)clip3(0, maxv, q0 - d);                                                        \
+            if (ap < beta) q0p[-2 * step] = (T)(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1)); \
+            if (aq < beta) q0p[step] = (T)(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));     \
+        } else {                                                                                       \
+            int p3 = q0p[-4 * step], q3 = q0p[3 * step];                                               \
+            int small = iabs_(p0 - q0) < ((alpha >> 2) + 2);                                           \
+            if (ap < beta && small) {                                                                  \
+                q0p[-step] = (T)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);                       \
+                q0p[-2 * step] = (T)((p2 + p1 + p0 + q0 + 2) >> 2);                                     \
+                q0p[-3 * step] = (T)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);                        \
+            } else q0p[-step] = (T)((2 * p1 + p0 + q1 + 2) >> 2);                                      \
+            if (aq < beta && small) {                                                                  \
+                q0p[0] = (T)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);                           \
+                q0p[step] = (T)((p0 + q0 + q1 + q2 + 2) >> 2);                                          \
+                q0p[2 * step] = (T)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);                         \
+            } else q0p[0] = (T)((2 * q1 + q0 + p1 + 2) >> 2);                                          \
+        }                                                                                              \
     }
-    int p2 = q0p[-3 * step], q2 = q0p[2 * step];
-    int ap = iabs_(p2 - p0), aq = iabs_(q2 - q0);
-    if (bS < 4) {
-        int tc = tc0 + (ap < beta) + (aq < beta);
-        int d = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
-        q0p[-step] = (uint8_t)clip3(0, 255, p0 + d);
-        q0p[0] = (uint8_t)clip3(0, 255, q0 - d);
-        if (ap < beta) q0p[-2 * step] = (uint8_t)(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
-        if (aq < beta) q0p[step] = (uint8_t)(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
-    } else {
-        int p3 = q0p[-4 * step], q3 = q0p[3 * step];
-        int small = iabs_(p0 - q0) < ((alpha >> 2) + 2);
-        if (ap < beta && small) {
-            q0p[-step] = (uint8_t)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-            q0p[-2 * step] = (uint8_t)((p2 + p1 + p0 + q0 + 2) >> 2);
-            q0p[-3 * step] = (uint8_t)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
-        } else q0p[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
-        if (aq < beta && small) {
-            q0p[0] = (uint8_t)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-            q0p[step] = (uint8_t)((p0 + q0 + q1 + q2 + 2) >> 2);
-            q0p[2 * step] = (uint8_t)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
-        } else q0p[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
-    }
+FILTER_LINE(filter_line8, uint8_t)
+FILTER_LINE(filter_line16, uint16_t)
+#undef FILTER_LINE
+
+/* QPc (Table 8-15) of qPI = QPY + chroma_qp_index_offset clipped to [-QpBdOffsetC, 51] */
+static int qpc_of(int qpi, int qpbd) {
+    qpi = clip3(-qpbd, 51, qpi);
+    return qpi < 0 ? qpi : QPC[qpi];
 }
 
 void jm_deblock_picture(jm_pic *p, const jm_seq *s, const jmh_mb_result *const *res, int qp) {
     if (s->lf_params_flag && s->lf_disable == 1) return;
     int offA = s->lf_params_flag ? 2 * s->lf_alpha : 0, offB = s->lf_params_flag ? 2 * s->lf_beta : 0;
     int W = p->w, Wc = p->w / 2;
-    int qpc = QPC[clip3(0, 51, qp + s->chroma_qp_offset)];
+    const int hbd = p->bd > 8, sc = hbd ? 1 << (p->bd - 8) : 1, maxv = hbd ? (1 << p->bd) - 1 : 255;
+    int qpc = qpc_of(qp + s->chroma_qp_offset, 6 * (p->bd - 8));     /* deblocking uses QPc, not QP'c */
     for (int my = 0; my < s->mbh; my++)
         for (int mx = 0; mx < s->mbw; mx++) {
             const jmh_mb_result *rq = res[my * s->mbw + mx];
@@ -111,25 +123,26 @@ void jm_deblock_picture(jm_pic *p, const jm_seq *s, const jmh_mb_result *const *
                     if (!bS[0] && !bS[1] && !bS[2] && !bS[3]) continue;
                     /* luma: qp of both MBs is the slice qp (no mb_qp_delta) */
                     int iA = clip3(0, 51, qp + offA), iB = clip3(0, 51, qp + offB);
-                    int alpha = ALPHA[iA], beta = BETA[iB];
+                    int alpha = ALPHA[iA] * sc, beta = BETA[iB] * sc;
                     for (int k = 0; k < 16; k++) {
                         int b = bS[k >> 2];
                         if (!b) continue;
-                        uint8_t *q0p = dir == 0 ? p->y + (size_t)(16 * my + k) * W + 16 * mx + 4 * e
-                                                : p->y + (size_t)(16 * my + 4 * e) * W + 16 * mx + k;
-                        filter_line(q0p, dir == 0 ? 1 : W, b, alpha, beta, b < 4 ? TC0[iA][b - 1] : 0, 0);
+                        const size_t o = dir == 0 ? (size_t)(16 * my + k) * W + 16 * mx + 4 * e : (size_t)(16 * my + 4 * e) * W + 16 * mx + k;
+                        const int tc0 = (b < 4 ? TC0[iA][b - 1] : 0) * sc;
+                        if (hbd) filter_line16(p->Y + o, dir == 0 ? 1 : W, b, alpha, beta, tc0, 0, maxv);
+                        else filter_line8(p->y + o, dir == 0 ? 1 : W, b, alpha, beta, tc0, 0, maxv);
                     }
                     if (e & 1) continue;                 /* chroma edges 0 and 2 (4:2:0) */
                     int cA = clip3(0, 51, qpc + offA), cB = clip3(0, 51, qpc + offB);
-                    int ca = ALPHA[cA], cb = BETA[cB];
+                    int ca = ALPHA[cA] * sc, cb = BETA[cB] * sc;
                     for (int pl = 0; pl < 2; pl++) {
-                        uint8_t *P = pl ? p->v : p->u;
                         for (int k = 0; k < 8; k++) {
                             int b = bS[k >> 1];
                             if (!b) continue;
-                            uint8_t *q0p = dir == 0 ? P + (size_t)(8 * my + k) * Wc + 8 * mx + 2 * e
-                                                    : P + (size_t)(8 * my + 2 * e) * Wc + 8 * mx + k;
-                            filter_line(q0p, dir == 0 ? 1 : Wc, b, ca, cb, b < 4 ? TC0[cA][b - 1] : 0, 1);
+                            const size_t o = dir == 0 ? (size_t)(8 * my + k) * Wc + 8 * mx + 2 * e : (size_t)(8 * my + 2 * e) * Wc + 8 * mx + k;
+                            const int tc0 = (b < 4 ? TC0[cA][b - 1] : 0) * sc;
+                            if (hbd) filter_line16((pl ? p->V : p->U) + o, dir == 0 ? 1 : Wc, b, ca, cb, tc0, 1, maxv);
+                            else filter_line8((pl ? p->v : p->u) + o, dir == 0 ? 1 : Wc, b, ca, cb, tc0, 1, maxv);
                         }
                     }
                 }

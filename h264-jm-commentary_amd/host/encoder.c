@@ -26,21 +26,29 @@ int jm_lambda_rdo_off(int qp) {
     return QP2QUANT[i < 0 ? 0 : i];
 }
 
-/* squared error summed in integers (per row in 32 bits: 65025 * w < 2^32 for w < 66051), so
-   the value equals JM's double accumulation of integer squares exactly */
-static double psnr(const uint8_t *a, int sa, const uint8_t *b, int sb, int w, int h) {
+/* squared error summed in integers (per row in 32 bits: 65025 * w < 2^32 for w < 66051; 64-bit
+   rows at High 10), so the value equals JM's double accumulation of integer squares exactly; the
+   peak is (1 << bit depth) - 1 (JM >= 10 img->max_imgpel_value [J]) */
+static double psnr_pl(const jm_pic *a, const jm_pic *b, int pl, int w, int h) {
     uint64_t se = 0;
+    const int st = pl ? a->w / 2 : a->w;
+    const size_t off = pl == 0 ? 0 : (size_t)a->w * a->h + (size_t)(pl - 1) * (a->w / 2) * (a->h / 2);
     for (int y = 0; y < h; y++) {
-        const uint8_t *pa = a + (size_t)y * sa, *pb = b + (size_t)y * sb;
-        uint32_t r = 0;
-        for (int x = 0; x < w; x++) {
-            const int d = pa[x] - pb[x];
-            r += (uint32_t)(d * d);
+        uint64_t r = 0;
+        if (a->bd > 8) {
+            const uint16_t *pa = a->Y + off + (size_t)y * st, *pb = b->Y + off + (size_t)y * st;
+            for (int x = 0; x < w; x++) { const int d = pa[x] - pb[x]; r += (uint64_t)(d * d); }
+        } else {
+            const uint8_t *pa = a->y + off + (size_t)y * st, *pb = b->y + off + (size_t)y * st;
+            uint32_t r32 = 0;
+            for (int x = 0; x < w; x++) { const int d = pa[x] - pb[x]; r32 += (uint32_t)(d * d); }
+            r = r32;
         }
         se += r;
     }
     if (se == 0) return 99.0;
-    return 10.0 * log10(255.0 * 255.0 * w * h / (double)se);
+    const double peak = a->bd > 8 ? (double)((1 << a->bd) - 1) : 255.0;
+    return 10.0 * log10(peak * peak * w * h / (double)se);
 }
 
 /* slice.c › encode_one_slice [J]: the macroblock loop of one slice through the JM 8.6 call
@@ -145,9 +153,10 @@ static void job_run(wpool_t *P, wjob_t *j) {
     j->out.len = 0;
     j->status = encode_picture_slices(&j->im, s, &j->sl, &j->fp, j->cur, &j->rec, &j->out);
     j->pic_bits = j->out.len * 8;
-    j->py = psnr(j->cur->y, W, j->rec.y, W, inp->width, inp->height);
-    j->pu = psnr(j->cur->u, W / 2, j->rec.u, W / 2, inp->width / 2, inp->height / 2);
-    j->pv = psnr(j->cur->v, W / 2, j->rec.v, W / 2, inp->width / 2, inp->height / 2);
+    j->py = psnr_pl(j->cur, &j->rec, 0, inp->width, inp->height);
+    j->pu = psnr_pl(j->cur, &j->rec, 1, inp->width / 2, inp->height / 2);
+    j->pv = psnr_pl(j->cur, &j->rec, 2, inp->width / 2, inp->height / 2);
+    (void)W;
     j->write_ms = now_ms() - t0;
 }
 
@@ -216,6 +225,8 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     s.constrained_intra = inp->constrained_intra;
     s.transform_8x8_mode = inp->transform_8x8_mode;
     s.entropy_coding = inp->symbol_mode;
+    s.bit_depth = inp->bit_depth_luma;
+    const int bd = inp->bit_depth_luma;
     s.cabac_init_idc = inp->model_number;
 
     FILE *fin = NULL, *fout = NULL, *frec = NULL;
@@ -240,8 +251,8 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     pend_t *pend = (pend_t *)calloc(plen, sizeof(pend_t));
     jm_pic rec;
     memset(&rec, 0, sizeof(rec));
-    int alloc_fail = !pend || jm_pic_alloc(&rec, W, H);
-    for (int k = 0; k < plen && !alloc_fail; k++) alloc_fail = jm_pic_alloc(&pend[k].cur, W, H);
+    int alloc_fail = !pend || jm_pic_alloc_bd(&rec, W, H, bd);
+    for (int k = 0; k < plen && !alloc_fail; k++) alloc_fail = jm_pic_alloc_bd(&pend[k].cur, W, H, bd);
     if (alloc_fail) {
         if (pend) for (int k = 0; k < plen; k++) jm_pic_free(&pend[k].cur);
         free(pend);
@@ -273,7 +284,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         for (; njobs_init < nj; njobs_init++) {
             wjob_t *j = &pool.jobs[njobs_init];
             jm_bits_init(&j->out);
-            if (jm86_init(&j->im, inp, be, W, H) || jm_pic_alloc(&j->rec, W, H)) { njobs_init++; st_ret = JMH_E_OOM; goto cleanup; }
+            if (jm86_init(&j->im, inp, be, W, H) || jm_pic_alloc_bd(&j->rec, W, H, bd)) { njobs_init++; st_ret = JMH_E_OOM; goto cleanup; }
             j->im.res = j->im.mb_data;   /* results copied in at pop */
         }
         img = &im;   /* jm86_init of the jobs set this thread's img */
@@ -369,9 +380,9 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         st->deblock_ms += t3 - t2;                                                                 \
         if (r_) { fprintf(stderr, "set_reference failed: %d\n", r_); st_ret = r_; break; }         \
         if (frec) jm_write_yuv_frame(frec, &rec, inp->width, inp->height);                         \
-        double py = psnr(p_->cur.y, W, rec.y, W, inp->width, inp->height);                         \
-        double pu = psnr(p_->cur.u, W / 2, rec.u, W / 2, inp->width / 2, inp->height / 2);         \
-        double pv = psnr(p_->cur.v, W / 2, rec.v, W / 2, inp->width / 2, inp->height / 2);         \
+        double py = psnr_pl(&p_->cur, &rec, 0, inp->width, inp->height);                           \
+        double pu = psnr_pl(&p_->cur, &rec, 1, inp->width / 2, inp->height / 2);                   \
+        double pv = psnr_pl(&p_->cur, &rec, 2, inp->width / 2, inp->height / 2);                   \
         st->psnr_y += py; st->psnr_u += pu; st->psnr_v += pv;                                      \
         st->bits += pic_bits;                                                                      \
         st->frames++;                                                                              \

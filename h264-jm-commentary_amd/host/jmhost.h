@@ -50,6 +50,8 @@ typedef struct jm_input {
     int  offset_matrix_present;/* OffsetMatrixPresentFlag (must be 0: flat lists only)         */
     int  level_idc;            /* LevelIDC                                                    */
     int  symbol_mode;          /* SymbolMode (0 = CAVLC, 1 = CABAC)                            */
+    int  bit_depth_luma;       /* SourceBitDepthLuma (JM >= 10 FRExt): 8, 9, 10                 */
+    int  bit_depth_chroma;     /* SourceBitDepthChroma: equal to the luma bit depth            */
     int  context_init_method;  /* ContextInitMethod (0: fixed; 1 adaptive is rejected)          */
     int  model_number;         /* FixedModelNumber: cabac_init_idc of P slices (0)              */
     int  lf_params_flag;       /* LoopFilterParametersFlag                                    */
@@ -80,15 +82,22 @@ int  jm_patch_input(jm_input *inp, char *err, int errlen);   /* PatchInp() */
 /* ---- pictures ---------------------------------------------------------------------------- */
 typedef struct jm_pic {
     int w, h;                  /* coded (multiple of 16) */
-    uint8_t *y, *u, *v;        /* contiguous planes, stride = w / w/2                            */
+    uint8_t *y, *u, *v;        /* contiguous planes, stride = w / w/2 (bit depth 8)              */
+    int bd;                    /* bit depth: 8 (y, u, v) or 9 / 10 (Y, U, V, 16-bit samples)     */
+    uint16_t *Y, *U, *V;       /* High 10 planes (JM >= 10 imgpel = unsigned short [J])          */
 } jm_pic;
 int  jm_pic_alloc(jm_pic *p, int w, int h);
+int  jm_pic_alloc_bd(jm_pic *p, int w, int h, int bd);
 void jm_pic_free(jm_pic *p);
 
 /* deterministic synthetic 4:2:0 source: integer-only texture, global
  * quarter-pel motion, moving rectangles, per-frame noise.  Writes the displayed w x h into the
  * coded picture and pads to the coded size by edge replication (JM PaddAutoCropBorders). */
 void jm_synth_frame(jm_pic *p, int disp_w, int disp_h, uint64_t seed, int frame);
+/* the same picture at bit depth bd (9 / 10) in 16-bit samples: each 8-bit sample v becomes
+   v << (bd - 8) plus (bd - 8) low bits of per-sample noise (10-bit texture range 64..943) */
+void jm_synth_frame_hbd(uint16_t *y, uint16_t *u, uint16_t *v, int w, int h, int disp_w, int disp_h, uint64_t seed,
+                        int frame, int bd);
 /* read frame `index` of a planar I420 file (displayed size) into the coded picture */
 int  jm_read_yuv_frame(FILE *f, jm_pic *p, int disp_w, int disp_h, int index);
 int  jm_write_yuv_frame(FILE *f, const jm_pic *p, int disp_w, int disp_h);
@@ -122,6 +131,7 @@ typedef struct jm_seq {
     int constrained_intra;
     int transform_8x8_mode;    /* PPS transform_8x8_mode_flag (High profile)                   */
     int slice_mbs;             /* MBs per slice, raster order (SliceMode 1); 0: one slice      */
+    int bit_depth;             /* BitDepthLuma = BitDepthChroma (High 10: 9 / 10)              */
     int entropy_coding;        /* PPS entropy_coding_mode_flag: 0 CAVLC, 1 CABAC (SymbolMode)  */
     int cabac_init_idc;        /* cabac_init_idc of P slices (FixedModelNumber)                */
 } jm_seq;

@@ -7,23 +7,29 @@
 #include <string.h>
 #include "jmhost.h"
 
+/* 8-bit pictures through the uint8_t entry points, High 10 ones through the _u16 ones */
 static int gpu_set_ref(void *ctx, const jm_pic *p) {
+    if (p->bd > 8) return jmh_set_reference_u16((jmh_ctx *)ctx, 0, 0, p->Y, p->U, p->V, p->w, p->w / 2);
     return jmh_set_reference((jmh_ctx *)ctx, 0, 0, p->y, p->u, p->v, p->w, p->w / 2);
 }
 static int gpu_encode(void *ctx, const jm_pic *cur, const jmh_frame_params *fp) {
-    int r = jmh_frame_submit((jmh_ctx *)ctx, cur->y, cur->u, cur->v, cur->w, cur->w / 2, fp);
+    int r = cur->bd > 8 ? jmh_frame_submit_u16((jmh_ctx *)ctx, cur->Y, cur->U, cur->V, cur->w, cur->w / 2, fp)
+                        : jmh_frame_submit((jmh_ctx *)ctx, cur->y, cur->u, cur->v, cur->w, cur->w / 2, fp);
     return r ? r : jmh_frame_wait((jmh_ctx *)ctx);
 }
 static const jmh_mb_result *gpu_res(void *ctx, int a) { return jmh_get_mb_result((const jmh_ctx *)ctx, a); }
 static int gpu_recon(void *ctx, jm_pic *p) {
+    if (p->bd > 8) return jmh_read_recon_u16((jmh_ctx *)ctx, p->Y, p->U, p->V, p->w, p->w / 2);
     return jmh_read_recon((jmh_ctx *)ctx, p->y, p->u, p->v, p->w, p->w / 2);
 }
 static void gpu_destroy(void *ctx) { jmh_destroy((jmh_ctx *)ctx); }
 static int gpu_deblocked(void *ctx, jm_pic *p) {
+    if (p->bd > 8) return jmh_read_deblocked_u16((jmh_ctx *)ctx, p->Y, p->U, p->V, p->w, p->w / 2);
     return jmh_read_deblocked((jmh_ctx *)ctx, p->y, p->u, p->v, p->w, p->w / 2);
 }
 static int gpu_ref_deblocked(void *ctx) { return jmh_set_reference_slot((jmh_ctx *)ctx, -2); }
 static int gpu_push(void *ctx, const jm_pic *cur, const jmh_frame_params *fp) {
+    if (cur->bd > 8) return jmh_frame_push_u16((jmh_ctx *)ctx, cur->Y, cur->U, cur->V, cur->w, cur->w / 2, fp);
     return jmh_frame_push((jmh_ctx *)ctx, cur->y, cur->u, cur->v, cur->w, cur->w / 2, fp);
 }
 static int gpu_pop(void *ctx) { return jmh_frame_pop((jmh_ctx *)ctx); }

@@ -12,33 +12,69 @@
 #include <string.h>
 #include "jmhost.h"
 
-int jm_pic_alloc(jm_pic *p, int w, int h) {
-    p->w = w; p->h = h;
+int jm_pic_alloc_bd(jm_pic *p, int w, int h, int bd) {
+    memset(p, 0, sizeof(*p));
+    p->w = w; p->h = h; p->bd = bd > 8 ? bd : 8;
     size_t ls = (size_t)w * h, cs = ls / 4;
+    if (p->bd > 8) {
+        p->Y = (uint16_t *)malloc((ls + 2 * cs) * sizeof(uint16_t));
+        if (!p->Y) return -1;
+        p->U = p->Y + ls;
+        p->V = p->U + cs;
+        return 0;
+    }
     p->y = (uint8_t *)malloc(ls + 2 * cs);
     if (!p->y) return -1;
     p->u = p->y + ls;
     p->v = p->u + cs;
     return 0;
 }
-void jm_pic_free(jm_pic *p) { free(p->y); p->y = p->u = p->v = NULL; }
+int jm_pic_alloc(jm_pic *p, int w, int h) { return jm_pic_alloc_bd(p, w, h, 8); }
+void jm_pic_free(jm_pic *p) {
+    free(p->y); p->y = p->u = p->v = NULL;
+    free(p->Y); p->Y = p->U = p->V = NULL;
+}
 
 /* PaddAutoCropBorders-style edge replication of the displayed area to the coded size */
+#define PAD_PLANES(T, Y, U, V)                                                                          \
+    do {                                                                                                \
+        int w = p->w, h = p->h;                                                                         \
+        for (int y = 0; y < dh; y++)                                                                    \
+            for (int x = dw; x < w; x++) Y[y * w + x] = Y[y * w + dw - 1];                              \
+        for (int y = dh; y < h; y++) memcpy(Y + (size_t)y * w, Y + (size_t)(dh - 1) * w, w * sizeof(T)); \
+        int cw = w / 2, ch = h / 2, cdw = dw / 2, cdh = dh / 2;                                         \
+        T *pl[2] = {U, V};                                                                              \
+        for (int k = 0; k < 2; k++) {                                                                   \
+            for (int y = 0; y < cdh; y++)                                                               \
+                for (int x = cdw; x < cw; x++) pl[k][y * cw + x] = pl[k][y * cw + cdw - 1];             \
+            for (int y = cdh; y < ch; y++)                                                              \
+                memcpy(pl[k] + (size_t)y * cw, pl[k] + (size_t)(cdh - 1) * cw, cw * sizeof(T));          \
+        }                                                                                               \
+    } while (0)
 void jm_pad_picture(jm_pic *p, int dw, int dh) {
-    int w = p->w, h = p->h;
+    if (p->bd > 8) PAD_PLANES(uint16_t, p->Y, p->U, p->V);
+    else PAD_PLANES(uint8_t, p->y, p->u, p->v);
+}
+
+/* High 10 files: 16-bit little-endian samples (JM >= 10 ReadOneFrame with symbol_size_in_bytes 2 [J]) */
+static int read_hbd(FILE *f, jm_pic *p, int dw, int dh, int index) {
+    long fs = (long)dw * dh * 3 / 2 * 2;
+    if (fseek(f, fs * index, SEEK_SET)) return -1;
     for (int y = 0; y < dh; y++)
-        for (int x = dw; x < w; x++) p->y[y * w + x] = p->y[y * w + dw - 1];
-    for (int y = dh; y < h; y++) memcpy(p->y + (size_t)y * w, p->y + (size_t)(dh - 1) * w, w);
-    int cw = w / 2, ch = h / 2, cdw = dw / 2, cdh = dh / 2;
-    uint8_t *pl[2] = {p->u, p->v};
-    for (int k = 0; k < 2; k++) {
-        for (int y = 0; y < cdh; y++)
-            for (int x = cdw; x < cw; x++) pl[k][y * cw + x] = pl[k][y * cw + cdw - 1];
-        for (int y = cdh; y < ch; y++) memcpy(pl[k] + (size_t)y * cw, pl[k] + (size_t)(cdh - 1) * cw, cw);
-    }
+        if (fread(p->Y + (size_t)y * p->w, 2, dw, f) != (size_t)dw) return -1;
+    for (int y = 0; y < dh / 2; y++)
+        if (fread(p->U + (size_t)y * (p->w / 2), 2, dw / 2, f) != (size_t)(dw / 2)) return -1;
+    for (int y = 0; y < dh / 2; y++)
+        if (fread(p->V + (size_t)y * (p->w / 2), 2, dw / 2, f) != (size_t)(dw / 2)) return -1;
+    const int maxv = (1 << p->bd) - 1;
+    for (size_t i = 0; i < (size_t)p->w * p->h * 3 / 2; i++)
+        if (p->Y[i] > maxv) p->Y[i] = (uint16_t)maxv;     /* samples beyond the bit depth: Clip1 */
+    jm_pad_picture(p, dw, dh);
+    return 0;
 }
 
 int jm_read_yuv_frame(FILE *f, jm_pic *p, int dw, int dh, int index) {
+    if (p->bd > 8) return read_hbd(f, p, dw, dh, index);
     long fs = (long)dw * dh * 3 / 2;
     if (fseek(f, fs * index, SEEK_SET)) return -1;
     if (p->w == dw) {   /* rows contiguous in the planes: one read per plane (no stdio buffering) */
@@ -58,6 +94,12 @@ int jm_read_yuv_frame(FILE *f, jm_pic *p, int dw, int dh, int index) {
 }
 
 int jm_write_yuv_frame(FILE *f, const jm_pic *p, int dw, int dh) {
+    if (p->bd > 8) {
+        for (int y = 0; y < dh; y++) fwrite(p->Y + (size_t)y * p->w, 2, dw, f);
+        for (int y = 0; y < dh / 2; y++) fwrite(p->U + (size_t)y * (p->w / 2), 2, dw / 2, f);
+        for (int y = 0; y < dh / 2; y++) fwrite(p->V + (size_t)y * (p->w / 2), 2, dw / 2, f);
+        return 0;
+    }
     for (int y = 0; y < dh; y++) fwrite(p->y + (size_t)y * p->w, 1, dw, f);
     for (int y = 0; y < dh / 2; y++) fwrite(p->u + (size_t)y * (p->w / 2), 1, dw / 2, f);
     for (int y = 0; y < dh / 2; y++) fwrite(p->v + (size_t)y * (p->w / 2), 1, dw / 2, f);
@@ -108,7 +150,35 @@ static int texture(uint64_t seed, int X, int Y, int plane) {
 
 typedef struct { int x, y, w, h, vx, vy; } rect_t;    /* pos/vel in quarter pels */
 
+static void synth8(jm_pic *p, int dw, int dh, uint64_t seed, int t);
 void jm_synth_frame(jm_pic *p, int dw, int dh, uint64_t seed, int t) {
+    if (p->bd <= 8) { synth8(p, dw, dh, seed, t); return; }
+    jm_synth_frame_hbd(p->Y, p->U, p->V, p->w, p->h, dw, dh, seed, t, p->bd);
+}
+
+void jm_synth_frame_hbd(uint16_t *Y, uint16_t *U, uint16_t *V, int w, int h, int dw, int dh, uint64_t seed, int t, int bd) {
+    jm_pic q;
+    if (jm_pic_alloc(&q, w, h)) return;
+    synth8(&q, dw, dh, seed, t);
+    const uint64_t s = 0x5EED0000ULL + seed + 77;
+    const int sh = bd - 8, lo = (1 << sh) - 1;
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++)
+            Y[(size_t)y * w + x] = (uint16_t)((q.y[(size_t)y * w + x] << sh) | (hash3(s, x, y, 2 * t) & lo));
+    for (int y = 0; y < dh / 2; y++)
+        for (int x = 0; x < dw / 2; x++) {
+            const size_t i = (size_t)y * (w / 2) + x;
+            U[i] = (uint16_t)((q.u[i] << sh) | (hash3(s, x, y, 2 * t + 1) & lo));
+            V[i] = (uint16_t)((q.v[i] << sh) | (hash3(s, y, x, 2 * t + 1) & lo));
+        }
+    jm_pic_free(&q);
+    jm_pic view;
+    memset(&view, 0, sizeof(view));
+    view.w = w; view.h = h; view.bd = bd; view.Y = Y; view.U = U; view.V = V;
+    jm_pad_picture(&view, dw, dh);
+}
+
+static void synth8(jm_pic *p, int dw, int dh, uint64_t seed, int t) {
     uint64_t s = 0x5EED0000ULL + seed;
     rect_t R[12];
     for (int k = 0; k < 12; k++) {

@@ -17,7 +17,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 10
+JMH_ABI_VERSION = 11
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -39,7 +39,7 @@ class JmhConfig(ctypes.Structure):
                 ("flags", ctypes.c_int32), ("pipeline_depth", ctypes.c_int32),
                 ("transform_8x8_mode", ctypes.c_int32), ("jm_version", ctypes.c_int32),
                 ("quant_offset", ctypes.c_int32 * 2), ("epzs_dual_refinement", ctypes.c_int32),
-                ("slice_mbs", ctypes.c_int32)]
+                ("slice_mbs", ctypes.c_int32), ("bit_depth", ctypes.c_int32)]
 
 
 class JmhFrameParams(ctypes.Structure):
@@ -107,6 +107,12 @@ _SIGS = {
     "jmh_tq4x4_batch": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "jmh_tq8x8_batch": (_I, [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P]),
     "jmh_read_qpel": (_I, [_P, _P]),
+    "jmh_set_reference_u16": (_I, [_P, _I, _I, _P, _P, _P, _I, _I]),
+    "jmh_frame_submit_u16": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(JmhFrameParams)]),
+    "jmh_frame_push_u16": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(JmhFrameParams)]),
+    "jmh_read_recon_u16": (_I, [_P, _P, _P, _P, _I, _I]),
+    "jmh_read_deblocked_u16": (_I, [_P, _P, _P, _P, _I, _I]),
+    "jmh_load_frame_u16": (_I, [_P, _I, _P, _P, _P, _I, _I]),
     "jmh_search_pictures": (_I, [_P, _P, _P, _I]),
     "jmh_block_motion_search": (_I, [_P, _I, _P, _P]),
     "jmh_search_pictures_u16": (_I, [_P, _P, _P, _I, _I]),
@@ -155,7 +161,8 @@ def _ptr(a):
 
 def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
                 restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False,
-                pipeline_depth=0, transform_8x8_mode=0, jm_version=8, quant_offset=(682, 342), epzs_dual_refinement=0, slice_mbs=0):
+                pipeline_depth=0, transform_8x8_mode=0, jm_version=8, quant_offset=(682, 342), epzs_dual_refinement=0, slice_mbs=0,
+                bit_depth=8):
     """jm_version >= 10 selects the JM >= 10 quantisation rounding with the flat OffsetMatrix
     entries quant_offset = (I slices, P slices) at OffsetBits 11 (docs/JM_SEMANTICS.md item 45)."""
     cfg = JmhConfig()
@@ -171,6 +178,7 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     cfg.jm_version = jm_version
     cfg.epzs_dual_refinement = epzs_dual_refinement
     cfg.slice_mbs = slice_mbs
+    cfg.bit_depth = bit_depth
     if jm_version >= 10:
         cfg.quant_offset[0], cfg.quant_offset[1] = quant_offset
     return cfg
@@ -205,6 +213,10 @@ class Encoder:
         self.w, self.h = width, height
         self.mbw, self.mbh = width // 16, height // 16
         self.cfg = make_config(width, height, **kw)
+        # High 10 contexts take 16-bit pictures through the *_u16 entry points
+        self.hbd = self.cfg.bit_depth > 8
+        self.sfx = "_u16" if self.hbd else ""
+        self.pdt = np.uint16 if self.hbd else np.uint8
         ctx = ctypes.c_void_p()
         _check(self.lib.jmh_create(ctypes.byref(self.cfg), device, ctypes.byref(ctx)), "jmh_create")
         self.ctx = ctx
@@ -220,22 +232,28 @@ class Encoder:
         except Exception:
             pass
 
+    def _planes(self, y, u, v):
+        return [np.ascontiguousarray(a, self.pdt) for a in (y, u, v)]
+
     def set_reference(self, y, u, v):
-        _check(self.lib.jmh_set_reference(self.ctx, 0, 0, _ptr(y), _ptr(u), _ptr(v),
-                                          self.w, self.w // 2), "jmh_set_reference")
+        y, u, v = self._planes(y, u, v)
+        fn = "jmh_set_reference" + self.sfx
+        _check(getattr(self.lib, fn)(self.ctx, 0, 0, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2), fn)
 
     def encode(self, y, u, v, slice_type, qp, chroma_qp_offset=0, deblock=None):
         fp = frame_params(slice_type, qp, chroma_qp_offset, deblock)
-        _check(self.lib.jmh_frame_submit(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2,
-                                         ctypes.byref(fp)), "jmh_frame_submit")
+        y, u, v = self._planes(y, u, v)
+        fn = "jmh_frame_submit" + self.sfx
+        _check(getattr(self.lib, fn)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2, ctypes.byref(fp)), fn)
         _check(self.lib.jmh_frame_wait(self.ctx), "jmh_frame_wait")
         return self.results(), self.recon()
 
     # ---- pipelined pictures (jmh_frame_push / jmh_frame_pop) ----
     def push(self, y, u, v, slice_type, qp, chroma_qp_offset=0, deblock=None):
         fp = frame_params(slice_type, qp, chroma_qp_offset, deblock)
-        _check(self.lib.jmh_frame_push(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2,
-                                       ctypes.byref(fp)), "jmh_frame_push")
+        y, u, v = self._planes(y, u, v)
+        fn = "jmh_frame_push" + self.sfx
+        _check(getattr(self.lib, fn)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2, ctypes.byref(fp)), fn)
 
     def pop(self):
         """Wait for the oldest pushed picture; returns (results, recon)."""
@@ -255,8 +273,9 @@ class Encoder:
         return np.frombuffer(bytes(buf), dtype=MB_RESULT_DTYPE).copy()
 
     def _read(self, fn):
-        y = np.empty((self.h, self.w), np.uint8)
-        u = np.empty((self.h // 2, self.w // 2), np.uint8)
+        fn += self.sfx
+        y = np.empty((self.h, self.w), self.pdt)
+        u = np.empty((self.h // 2, self.w // 2), self.pdt)
         v = np.empty_like(u)
         _check(getattr(self.lib, fn)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2), fn)
         return y, u, v
@@ -270,8 +289,9 @@ class Encoder:
 
     # ---- device-resident path (bench) ----
     def load_frame(self, slot, y, u, v):
-        _check(self.lib.jmh_load_frame(self.ctx, slot, _ptr(y), _ptr(u), _ptr(v), self.w,
-                                       self.w // 2), "jmh_load_frame")
+        y, u, v = self._planes(y, u, v)
+        fn = "jmh_load_frame" + self.sfx
+        _check(getattr(self.lib, fn)(self.ctx, slot, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2), fn)
 
     def set_reference_slot(self, slot):
         _check(self.lib.jmh_set_reference_slot(self.ctx, slot), "jmh_set_reference_slot")
@@ -397,16 +417,27 @@ def load_host(path=HOST_LIB_PATH):
 
 
 class _JmPic(ctypes.Structure):
-    _fields_ = [("w", ctypes.c_int), ("h", ctypes.c_int), ("y", _P), ("u", _P), ("v", _P)]
+    _fields_ = [("w", ctypes.c_int), ("h", ctypes.c_int), ("y", _P), ("u", _P), ("v", _P),
+                ("bd", ctypes.c_int), ("Y", _P), ("U", _P), ("V", _P)]
 
 
-def synth_frame(disp_w, disp_h, seed, index):
-    """Deterministic synthetic 4:2:0 picture (coded size = multiple of 16), as (y, u, v)."""
+def synth_frame(disp_w, disp_h, seed, index, bit_depth=8):
+    """Deterministic synthetic 4:2:0 picture (coded size = multiple of 16), as (y, u, v); bit_depth
+    9 / 10: 16-bit samples (jm_synth_frame_hbd)."""
     host = load_host()
+    if bit_depth > 8:
+        cw, ch = (disp_w + 15) // 16 * 16, (disp_h + 15) // 16 * 16
+        y = np.zeros((ch, cw), np.uint16)
+        u = np.zeros((ch // 2, cw // 2), np.uint16)
+        v = np.zeros_like(u)
+        host.jm_synth_frame_hbd.restype = None
+        host.jm_synth_frame_hbd.argtypes = [_P, _P, _P, _I, _I, _I, _I, ctypes.c_uint64, _I, _I]
+        host.jm_synth_frame_hbd(_ptr(y), _ptr(u), _ptr(v), cw, ch, disp_w, disp_h, seed, index, bit_depth)
+        return y, u, v
     cw, ch = (disp_w + 15) // 16 * 16, (disp_h + 15) // 16 * 16
     y = np.zeros((ch, cw), np.uint8)
     u = np.zeros((ch // 2, cw // 2), np.uint8)
     v = np.zeros_like(u)
-    pic = _JmPic(cw, ch, y.ctypes.data, u.ctypes.data, v.ctypes.data)
+    pic = _JmPic(cw, ch, y.ctypes.data, u.ctypes.data, v.ctypes.data, 8, None, None, None)
     host.jm_synth_frame(ctypes.byref(pic), disp_w, disp_h, seed, index)
     return y, u, v

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 10
+#define JMH_ABI_VERSION 11
 #define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
 #define JMH_QOFFSET_MAX 2047  /* jmh_config.quant_offset: OffsetBits 11 (1 << 11 = a whole step)    */
 
@@ -108,6 +108,12 @@ typedef struct jmh_config {
                                        prediction and the EPZS spatial memory see only neighbours of
                                        the same slice (H.264 6.4.8, docs/JM_SEMANTICS.md item 47);
                                        deblocking still crosses slice edges (idc 0)                 */
+    int32_t bit_depth;              /* BitDepthLuma = BitDepthChroma: 0 or 8 (8-bit pictures, the
+                                       uint8_t entry points), 9 or 10 (High 10: 16-bit samples through
+                                       the *_u16 picture entry points; SearchMode 3 or -1; quantisation
+                                       at QP + QpBdOffset, Clip1 to (1 << bit_depth) - 1, deblocking
+                                       thresholds scaled by 1 << (bit_depth - 8); docs/JM_SEMANTICS.md
+                                       items 49-52)                                                  */
 } jmh_config;
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */
@@ -307,6 +313,22 @@ int  jmh_tq4x4_batch_u16(jmh_ctx *ctx, int n, const int16_t *resid, const uint16
 int  jmh_tq8x8_batch_u16(jmh_ctx *ctx, int n, const int16_t *resid, const uint16_t *pred, int qp,
                          int intra, int bit_depth, int16_t *levels, uint16_t *recon,
                          int32_t *coeff_cost, int32_t *nonzero);
+
+/* ---- High 10 pictures (jmh_config.bit_depth 9 / 10): the picture entry points above on 16-bit
+ * samples 0 .. (1 << bit_depth) - 1, same semantics, strides in samples.  The whole wavefront
+ * (motion search, intra, mode decision, TQ + reconstruction, deblocking) runs on them.  A context
+ * with bit_depth 9 / 10 accepts only these for pictures (the uint8_t ones return
+ * JMH_E_UNSUPPORTED_CFG) and vice versa.                                                      */
+int  jmh_set_reference_u16(jmh_ctx *ctx, int list, int ref_idx, const uint16_t *y, const uint16_t *u,
+                           const uint16_t *v, int stride_y, int stride_c);
+int  jmh_frame_submit_u16(jmh_ctx *ctx, const uint16_t *y, const uint16_t *u, const uint16_t *v,
+                          int stride_y, int stride_c, const jmh_frame_params *fp);
+int  jmh_frame_push_u16(jmh_ctx *ctx, const uint16_t *y, const uint16_t *u, const uint16_t *v,
+                        int stride_y, int stride_c, const jmh_frame_params *fp);
+int  jmh_read_recon_u16(jmh_ctx *ctx, uint16_t *y, uint16_t *u, uint16_t *v, int stride_y, int stride_c);
+int  jmh_read_deblocked_u16(jmh_ctx *ctx, uint16_t *y, uint16_t *u, uint16_t *v, int stride_y, int stride_c);
+int  jmh_load_frame_u16(jmh_ctx *ctx, int slot, const uint16_t *y, const uint16_t *u, const uint16_t *v,
+                        int stride_y, int stride_c);
 
 /* jmh_read_qpel: the 16 quarter-pel phase planes of the current reference (test seam for
  *   UnifiedOneForthPix), out[16][H+8][W+8], phase = 4*yfrac + xfrac, 4-sample padding.      */

@@ -43,6 +43,7 @@ const int jmo_blc_size[8][2] = {{16, 16}, {16, 16}, {16, 8}, {8, 16},
 
 int jmo_qp2quant(int qp) { return jmo_qp2quant_tab[imax(0, qp - SHIFT_QP)]; }
 int jmo_qp_scale_cr(int qp) { return qp < 0 ? qp : jmo_qp_scale_cr_tab[iclip(0, 51, qp)]; }
+int jmo_qpc(int qpi, int qpbd) { qpi = iclip(-qpbd, 51, qpi); return qpi < 0 ? qpi : jmo_qp_scale_cr_tab[qpi]; }
 
 /* mvbits[v] [J] (Init_Motion_Search_Module): length of se(v) Exp-Golomb code, 9.1 */
 int jmo_mvbits(int v) {
@@ -80,57 +81,58 @@ void jmo_init_spiral(jmo_ctx *c) {
 }
 
 /* ---- luma quarter-pel interpolation, H.264 8.4.2.2.1 (normative) ----------------------- */
-static inline int px(const uint8_t *p, int w, int h, int s, int x, int y) {
-    return p[iclip(0, h - 1, y) * s + iclip(0, w - 1, x)];
-}
 static inline int tap6(int a, int b, int c, int d, int e, int f) {
     return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
 }
-/* b1: horizontal half-pel intermediate between (x,y) and (x+1,y) */
-static int hb1(const uint8_t *p, int w, int h, int s, int x, int y) {
-    return tap6(px(p, w, h, s, x - 2, y), px(p, w, h, s, x - 1, y), px(p, w, h, s, x, y),
-                px(p, w, h, s, x + 1, y), px(p, w, h, s, x + 2, y), px(p, w, h, s, x + 3, y));
-}
-/* h1: vertical half-pel intermediate between (x,y) and (x,y+1) */
-static int vh1(const uint8_t *p, int w, int h, int s, int x, int y) {
-    return tap6(px(p, w, h, s, x, y - 2), px(p, w, h, s, x, y - 1), px(p, w, h, s, x, y),
-                px(p, w, h, s, x, y + 1), px(p, w, h, s, x, y + 2), px(p, w, h, s, x, y + 3));
-}
-int jmo_luma_qpel_sample(const uint8_t *p, int w, int h, int s, int X, int Y) {
-    int x = X >> 2, y = Y >> 2, fx = X & 3, fy = Y & 3;
-    int G = px(p, w, h, s, x, y);
-    if (fx == 0 && fy == 0) return G;
-    int b = clip255((hb1(p, w, h, s, x, y) + 16) >> 5);
-    int hh = clip255((vh1(p, w, h, s, x, y) + 16) >> 5);
-    int jj = 0;
-    if ((fx == 2 && fy != 0) || (fy == 2 && fx != 0)) {
-        int j1 = tap6(vh1(p, w, h, s, x - 2, y), vh1(p, w, h, s, x - 1, y), vh1(p, w, h, s, x, y),
-                      vh1(p, w, h, s, x + 1, y), vh1(p, w, h, s, x + 2, y),
-                      vh1(p, w, h, s, x + 3, y));
-        jj = clip255((j1 + 512) >> 10);
-    }
-    int s_ = clip255((hb1(p, w, h, s, x, y + 1) + 16) >> 5);   /* b at row y+1   */
-    int m = clip255((vh1(p, w, h, s, x + 1, y) + 16) >> 5);    /* h at column x+1 */
-    int H_ = px(p, w, h, s, x + 1, y), M = px(p, w, h, s, x, y + 1);
-    switch (fy * 4 + fx) {
-    case 1: return (G + b + 1) >> 1;        /* a */
-    case 2: return b;                       /* b */
-    case 3: return (H_ + b + 1) >> 1;       /* c */
-    case 4: return (G + hh + 1) >> 1;       /* d */
-    case 5: return (b + hh + 1) >> 1;       /* e */
-    case 6: return (b + jj + 1) >> 1;       /* f */
-    case 7: return (b + m + 1) >> 1;        /* g */
-    case 8: return hh;                      /* h */
-    case 9: return (hh + jj + 1) >> 1;      /* i */
-    case 10: return jj;                     /* j */
-    case 11: return (jj + m + 1) >> 1;      /* k */
-    case 12: return (M + hh + 1) >> 1;      /* n */
-    case 13: return (hh + s_ + 1) >> 1;     /* p */
-    case 14: return (jj + s_ + 1) >> 1;     /* q */
-    case 15: return (m + s_ + 1) >> 1;      /* r */
-    }
+/* one sample at quarter-pel (X, Y) from integer samples PX(x, y) (clamped access), Clip1 = maxv */
+#define QPEL_BODY(PX)                                                                                   \
+    int x = X >> 2, y = Y >> 2, fx = X & 3, fy = Y & 3;                                                  \
+    int G = PX(x, y);                                                                                   \
+    if (fx == 0 && fy == 0) return G;                                                                   \
+    /* b1 / h1: horizontal / vertical half-pel intermediates between (x,y) and (x+1,y) / (x,y+1) */      \
+    int b = clipv(maxv, (HB1(PX, x, y) + 16) >> 5);                                                     \
+    int hh = clipv(maxv, (VH1(PX, x, y) + 16) >> 5);                                                    \
+    int jj = 0;                                                                                         \
+    if ((fx == 2 && fy != 0) || (fy == 2 && fx != 0)) {                                                 \
+        int j1 = tap6(VH1(PX, x - 2, y), VH1(PX, x - 1, y), VH1(PX, x, y), VH1(PX, x + 1, y),          \
+                      VH1(PX, x + 2, y), VH1(PX, x + 3, y));                                            \
+        jj = clipv(maxv, (j1 + 512) >> 10);                                                            \
+    }                                                                                                   \
+    int s_ = clipv(maxv, (HB1(PX, x, y + 1) + 16) >> 5);   /* b at row y+1   */                         \
+    int m = clipv(maxv, (VH1(PX, x + 1, y) + 16) >> 5);    /* h at column x+1 */                        \
+    int H_ = PX(x + 1, y), M = PX(x, y + 1);                                                             \
+    switch (fy * 4 + fx) {                                                                              \
+    case 1: return (G + b + 1) >> 1;        /* a */                                                     \
+    case 2: return b;                       /* b */                                                     \
+    case 3: return (H_ + b + 1) >> 1;       /* c */                                                     \
+    case 4: return (G + hh + 1) >> 1;       /* d */                                                     \
+    case 5: return (b + hh + 1) >> 1;       /* e */                                                     \
+    case 6: return (b + jj + 1) >> 1;       /* f */                                                     \
+    case 7: return (b + m + 1) >> 1;        /* g */                                                     \
+    case 8: return hh;                      /* h */                                                     \
+    case 9: return (hh + jj + 1) >> 1;      /* i */                                                     \
+    case 10: return jj;                     /* j */                                                     \
+    case 11: return (jj + m + 1) >> 1;      /* k */                                                     \
+    case 12: return (M + hh + 1) >> 1;      /* n */                                                     \
+    case 13: return (hh + s_ + 1) >> 1;     /* p */                                                     \
+    case 14: return (jj + s_ + 1) >> 1;     /* q */                                                     \
+    case 15: return (m + s_ + 1) >> 1;      /* r */                                                     \
+    }                                                                                                   \
     return G;
+#define HB1(PX, xx, yy) tap6(PX((xx) - 2, yy), PX((xx) - 1, yy), PX(xx, yy), PX((xx) + 1, yy), PX((xx) + 2, yy), PX((xx) + 3, yy))
+#define VH1(PX, xx, yy) tap6(PX(xx, (yy) - 2), PX(xx, (yy) - 1), PX(xx, yy), PX(xx, (yy) + 1), PX(xx, (yy) + 2), PX(xx, (yy) + 3))
+#define PX8(xx, yy) p[iclip(0, h - 1, yy) * s + iclip(0, w - 1, xx)]
+int jmo_luma_qpel_sample(const uint8_t *p, int w, int h, int s, int X, int Y) {
+    const int maxv = 255;
+    QPEL_BODY(PX8)
 }
+int jmo_qpel_px(const pel *p, int w, int h, int s, int X, int Y, int maxv) {
+    QPEL_BODY(PX8)
+}
+#undef PX8
+#undef HB1
+#undef VH1
+#undef QPEL_BODY
 
 /* UnifiedOneForthPix [J]: 16 phase planes of the reference, padded by JMO_PAD so that
  * clamping the integer position into [-PAD, W-1+PAD] (keeping the phase) equals the
@@ -139,11 +141,10 @@ void jmo_build_qpel(jmo_ctx *c) {
     int P = JMO_PAD, qs = c->qstride, qh = c->H + 2 * P;
     for (int ph = 0; ph < 16; ph++) {
         int fx = ph & 3, fy = ph >> 2;
-        uint8_t *pl = c->qpel + (size_t)ph * c->qplane;
+        pel *pl = c->qpel + (size_t)ph * c->qplane;
         for (int y = 0; y < qh; y++)
             for (int x = 0; x < qs; x++)
-                pl[y * qs + x] = (uint8_t)jmo_luma_qpel_sample(
-                    c->refY, c->W, c->H, c->W, 4 * (x - P) + fx, 4 * (y - P) + fy);
+                pl[y * qs + x] = (pel)jmo_qpel_px(c->refY, c->W, c->H, c->W, 4 * (x - P) + fx, 4 * (y - P) + fy, c->maxv);
     }
 }
 
@@ -214,14 +215,12 @@ static void inv4x4_core(const int32_t in[16], int32_t out[16]) {
 void jmo_inverse4x4(const int32_t *in, int32_t *out) { inv4x4_core(in, out); }
 
 /* inverse transform + reconstruction: clip((r + (pred<<6) + 32) >> 6) */
-void jmo_inv4x4_add(const int32_t m[16], const uint8_t *pred, int pstride, uint8_t *out,
-                    int ostride) {
+void jmo_inv4x4_add(const int32_t m[16], const pel *pred, int pstride, pel *out, int ostride, int maxv) {
     int32_t r[16];
     inv4x4_core(m, r);
     for (int y = 0; y < 4; y++)
         for (int x = 0; x < 4; x++)
-            out[y * ostride + x] =
-                (uint8_t)clip255((r[4 * y + x] + (pred[y * pstride + x] << DQ_BITS) + DQ_ROUND) >> DQ_BITS);
+            out[y * ostride + x] = (pel)clipv(maxv, (r[4 * y + x] + (pred[y * pstride + x] << DQ_BITS) + DQ_ROUND) >> DQ_BITS);
 }
 
 /* ======================================================================================== */
@@ -294,13 +293,12 @@ void jmo_inverse8x8(const int32_t *in, int32_t *out) {   /* rows first, then col
     for (int y = 0; y < 8; y++) inv8(in + 8 * y, 1, t + 8 * y, 1);
     for (int x = 0; x < 8; x++) inv8(t + x, 8, out + x, 8);
 }
-void jmo_inv8x8_add(const int32_t m[64], const uint8_t *pred, int pstride, uint8_t *out, int ostride) {
+void jmo_inv8x8_add(const int32_t m[64], const pel *pred, int pstride, pel *out, int ostride, int maxv) {
     int32_t r[64];
     jmo_inverse8x8(m, r);
     for (int y = 0; y < 8; y++)
         for (int x = 0; x < 8; x++)
-            out[y * ostride + x] =
-                (uint8_t)clip255((r[8 * y + x] + (pred[y * pstride + x] << DQ_BITS) + DQ_ROUND) >> DQ_BITS);
+            out[y * ostride + x] = (pel)clipv(maxv, (r[8 * y + x] + (pred[y * pstride + x] << DQ_BITS) + DQ_ROUND) >> DQ_BITS);
 }
 /* HadamardSAD8x8 [J]: (sum |H8 D H8| + 2) >> 2; SAD when use_hadamard == 0.  d[] raster. */
 int jmo_satd8x8(const int32_t d[64], int use_hadamard) {

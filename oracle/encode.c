@@ -28,8 +28,8 @@ typedef struct {
     int lambda;                /* lambda_mode == lambda_motion (RDO off, integer)        */
     int lf;                    /* LAMBDA_FACTOR(lambda) = 65536*lambda                     */
     int slice_p;
-    uint8_t org[256];          /* imgY_org of the MB                                       */
-    uint8_t orgc[2][64];
+    pel org[256];              /* imgY_org of the MB                                       */
+    pel orgc[2][64];
     /* FFS state (SetupFastFullPelSearch) */
     int setup_done, scx, scy, pos_00;
     int16_t all_mv[8][16][2];  /* img->all_mv[.][.][LIST_0][ref 0][blocktype]               */
@@ -439,10 +439,11 @@ static int block_motion_search(mbs *s, int blocktype, int bx4, int by4, int rang
  * arguments (MVP, centre, range, lambda_factor) on the pictures of jmo_search_pictures */
 int jmo_search_pictures(jmo_ctx *c, const uint8_t *cur_y, const uint8_t *ref_y, int stride) {
     if (!c || !cur_y || !ref_y || stride < c->W) return JMH_E_INVALID_ARG;
-    for (int y = 0; y < c->H; y++) {
-        memcpy(c->orgY + (size_t)y * c->W, cur_y + (size_t)y * stride, c->W);
-        memcpy(c->refY + (size_t)y * c->W, ref_y + (size_t)y * stride, c->W);
-    }
+    for (int y = 0; y < c->H; y++)
+        for (int x = 0; x < c->W; x++) {
+            c->orgY[(size_t)y * c->W + x] = cur_y[(size_t)y * stride + x];
+            c->refY[(size_t)y * c->W + x] = ref_y[(size_t)y * stride + x];
+        }
     jmo_build_qpel(c);
     c->have_ref = 1;
     return JMH_OK;
@@ -460,7 +461,7 @@ int jmo_block_motion_search(jmo_ctx *c, int n, const jmh_block_search *req, jmh_
         s->c = c; s->mbx = q->mb_x; s->mby = q->mb_y; s->pix_x = 16 * q->mb_x; s->pix_y = 16 * q->mb_y;
         s->lf = q->lambda_factor;
         s->slice_p = q->slice_p != 0;
-        for (int y = 0; y < 16; y++) memcpy(s->org + 16 * y, c->orgY + (s->pix_y + y) * c->W + s->pix_x, 16);
+        for (int y = 0; y < 16; y++) memcpy(s->org + 16 * y, c->orgY + (s->pix_y + y) * c->W + s->pix_x, 16 * sizeof(pel));
         int mvx = q->centre[0], mvy = q->centre[1], min_mcost;
         if (q->search_mode == 0) {
             ffs_setup_at(s, q->centre[0], q->centre[1]);
@@ -508,8 +509,8 @@ static void partition_motion_search(mbs *s, int blocktype, int block8x8) {
 /*  transform / quantisation                                                               */
 /* ====================================================================================== */
 /* dct_luma [J]: 4x4 forward, quant (deadzone qp_const), scan, dequant, inverse, recon */
-static int dct_luma4x4(const int32_t resid[16], const uint8_t *pred, int ps, int qp, int intra_round,
-                       int16_t levels[16], int *coeff_cost, uint8_t *rec, int rs) {
+static int dct_luma4x4(const int32_t resid[16], const pel *pred, int ps, int qp, int intra_round,
+                       int16_t levels[16], int *coeff_cost, pel *rec, int rs, int maxv) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS + qp_per;
     int qp_const = jmo_qround(intra_round, q_bits);
     int32_t m[16];
@@ -530,7 +531,7 @@ static int dct_luma4x4(const int32_t resid[16], const uint8_t *pred, int ps, int
         } else levels[k] = 0;
         m[pos] = isign(ilev, m[pos]);
     }
-    jmo_inv4x4_add(m, pred, ps, rec, rs);
+    jmo_inv4x4_add(m, pred, ps, rec, rs, maxv);
     return nonzero;
 }
 
@@ -540,8 +541,10 @@ int jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, in
     for (int i = 0; i < n; i++) {
         int32_t r[16];
         int cc = 0;
-        for (int k = 0; k < 16; k++) r[k] = resid[16 * i + k];
-        nonzero[i] = dct_luma4x4(r, pred + 16 * i, 4, qp, intra, levels + 16 * i, &cc, recon + 16 * i, 4);
+        pel p[16], o[16];
+        for (int k = 0; k < 16; k++) { r[k] = resid[16 * i + k]; p[k] = pred[16 * i + k]; }
+        nonzero[i] = dct_luma4x4(r, p, 4, qp, intra, levels + 16 * i, &cc, o, 4, 255);
+        for (int k = 0; k < 16; k++) recon[16 * i + k] = (pel)o[k];
         coeff_cost[i] = cc;
     }
     return JMH_OK;
@@ -552,8 +555,8 @@ int jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, in
  * for 4x4 (docs/JM_SEMANTICS.md item 1), 8x8 frame zig-zag, COEFF_COST8x8 on the 64-scan runs,
  * dequantisation by the normative 8.5.13.1 formula on the signed level (flat scaling lists),
  * reconstruction clip((r + (pred<<6) + 32) >> 6).  levels[64] in scan order. */
-static int dct_luma8x8(const int32_t resid[64], const uint8_t *pred, int ps, int qp, int intra_round,
-                       int16_t levels[64], int *coeff_cost, uint8_t *rec, int rs) {
+static int dct_luma8x8(const int32_t resid[64], const pel *pred, int ps, int qp, int intra_round,
+                       int16_t levels[64], int *coeff_cost, pel *rec, int rs, int maxv) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS_8 + qp_per;
     int qp_const = jmo_qround(intra_round, q_bits);
     int scan[64];
@@ -577,7 +580,7 @@ static int dct_luma8x8(const int32_t resid[64], const uint8_t *pred, int ps, int
         levels[k] = (int16_t)c;
         m[pos] = d;
     }
-    jmo_inv8x8_add(m, pred, ps, rec, rs);
+    jmo_inv8x8_add(m, pred, ps, rec, rs, maxv);
     return nonzero;
 }
 
@@ -587,8 +590,10 @@ int jmo_tq8x8_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, in
     for (int i = 0; i < n; i++) {
         int32_t r[64];
         int cc = 0;
-        for (int k = 0; k < 64; k++) r[k] = resid[64 * i + k];
-        nonzero[i] = dct_luma8x8(r, pred + 64 * i, 8, qp, intra, levels + 64 * i, &cc, recon + 64 * i, 8);
+        pel p[64], o[64];
+        for (int k = 0; k < 64; k++) { r[k] = resid[64 * i + k]; p[k] = pred[64 * i + k]; }
+        nonzero[i] = dct_luma8x8(r, p, 8, qp, intra, levels + 64 * i, &cc, o, 8, 255);
+        for (int k = 0; k < 64; k++) recon[64 * i + k] = (pel)o[k];
         coeff_cost[i] = cc;
     }
     return JMH_OK;
@@ -608,8 +613,8 @@ static void put_levels8(int16_t luma[16][16], int b8, const int16_t lev[64]) {
 
 /* dct_chroma [J] for one component: 4 4x4 AC blocks + 2x2 DC; returns updated cr_cbp.
  * resid/pred raster 8x8.  DC reconstruction follows H.264 8.5.11.2 exactly. */
-static int dct_chroma(const int32_t resid[64], const uint8_t pred[64], int qpc, int intra_round,
-                      int cr_cbp, int16_t dc_out[4], int16_t ac_out[4][16], uint8_t rec[64]) {
+static int dct_chroma(const int32_t resid[64], const pel pred[64], int qpc, int intra_round,
+                      int cr_cbp, int16_t dc_out[4], int16_t ac_out[4][16], pel rec[64], int maxv) {
     int qp_per = qpc / 6, qp_rem = qpc % 6, q_bits = Q_BITS + qp_per;
     int qp_const = jmo_qround(intra_round, q_bits);
     int32_t m[4][16];
@@ -660,14 +665,14 @@ static int dct_chroma(const int32_t resid[64], const uint8_t pred[64], int qpc, 
     for (int b = 0; b < 4; b++) {
         m[b][0] = (f[b] * 16 * v00 * (1 << qp_per)) >> 5;   /* (x << per) of the spec: x * 2^per (x may be < 0) */
         int ox = (b & 1) * 4, oy = (b >> 1) * 4;
-        jmo_inv4x4_add(m[b], pred + oy * 8 + ox, 8, rec + oy * 8 + ox, 8);
+        jmo_inv4x4_add(m[b], pred + oy * 8 + ox, 8, rec + oy * 8 + ox, 8, maxv);
     }
     return cr_cbp;
 }
 
 /* dct_luma_16x16 [J]: returns luma cbp (15 if any AC level, else 0) */
-static int dct_luma_16x16(const int32_t resid[256], const uint8_t pred[256], int qp, int rnd,
-                          int16_t dc_out[16], int16_t ac_out[16][16], int *cbp_blk, uint8_t rec[256]) {
+static int dct_luma_16x16(const int32_t resid[256], const pel pred[256], int qp, int rnd,
+                          int16_t dc_out[16], int16_t ac_out[16][16], int *cbp_blk, pel rec[256], int maxv) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS + qp_per;
     int qp_const = jmo_qround(rnd, q_bits), qp_const2 = qp_const << 1;   /* JM 8.6: always / 3 */
     int32_t m[16][16];                     /* [4x4 block raster][coef raster] */
@@ -725,7 +730,7 @@ static int dct_luma_16x16(const int32_t resid[256], const uint8_t pred[256], int
         if (nz) *cbp_blk |= 1 << b;
         m[b][0] = (f[b] * v00 * (1 << qp_per) + 2) >> 2;
         int ox = (b & 3) * 4, oy = (b >> 2) * 4;
-        jmo_inv4x4_add(m[b], pred + oy * 16 + ox, 16, rec + oy * 16 + ox, 16);
+        jmo_inv4x4_add(m[b], pred + oy * 16 + ox, 16, rec + oy * 16 + ox, 16, maxv);
     }
     return ac;
 }
@@ -749,9 +754,9 @@ static int luma_avail(const mbs *s, int x, int y) {
 
 /* intrapred_luma [J] / 8.3.1.2: the 9 Intra4x4 predictions of the 4x4 block at (bx,by)
  * (pixels, MB relative); pred[9][16]; avail[9] */
-static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int avail[9]) {
+static void intra4x4_pred(const mbs *s, int bx, int by, pel pred[9][16], int avail[9]) {
     const jmo_ctx *c = s->c;
-    const uint8_t *R = c->recY;
+    const pel *R = c->recY;
     int W = c->W, ax = s->pix_x + bx, ay = s->pix_y + by;
     int up = luma_avail(s, bx, by - 1), left = luma_avail(s, bx - 1, by);
     int ul = luma_avail(s, bx - 1, by - 1);
@@ -772,15 +777,15 @@ static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int
     for (int y = 0; y < 4; y++)
         for (int x = 0; x < 4; x++) {
             int k = 4 * y + x;
-            pred[0][k] = (uint8_t)PT(x);
-            pred[1][k] = (uint8_t)L[y];
+            pred[0][k] = (pel)PT(x);
+            pred[1][k] = (pel)L[y];
             /* DDL */
-            pred[3][k] = (uint8_t)((x == 3 && y == 3) ? (PT(6) + 3 * PT(7) + 2) >> 2
+            pred[3][k] = (pel)((x == 3 && y == 3) ? (PT(6) + 3 * PT(7) + 2) >> 2
                                                       : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2);
             /* DDR */
-            if (x > y) pred[4][k] = (uint8_t)((PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2);
-            else if (x < y) pred[4][k] = (uint8_t)((PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2);
-            else pred[4][k] = (uint8_t)((PT(0) + 2 * T[0] + PL(0) + 2) >> 2);
+            if (x > y) pred[4][k] = (pel)((PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2);
+            else if (x < y) pred[4][k] = (pel)((PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2);
+            else pred[4][k] = (pel)((PT(0) + 2 * T[0] + PL(0) + 2) >> 2);
             /* VR */
             {
                 int z = 2 * x - y, v;
@@ -788,7 +793,7 @@ static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int
                 else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
                 else if (z == -1) v = (PL(0) + 2 * T[0] + PT(0) + 2) >> 2;
                 else v = (PL(y - 1) + 2 * PL(y - 2) + PL(y - 3) + 2) >> 2;
-                pred[5][k] = (uint8_t)v;
+                pred[5][k] = (pel)v;
             }
             /* HD */
             {
@@ -797,11 +802,11 @@ static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int
                 else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
                 else if (z == -1) v = (PL(0) + 2 * T[0] + PT(0) + 2) >> 2;
                 else v = (PT(x - 1) + 2 * PT(x - 2) + PT(x - 3) + 2) >> 2;
-                pred[6][k] = (uint8_t)v;
+                pred[6][k] = (pel)v;
             }
             /* VL */
-            if (!(y & 1)) pred[7][k] = (uint8_t)((PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1);
-            else pred[7][k] = (uint8_t)((PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2);
+            if (!(y & 1)) pred[7][k] = (pel)((PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1);
+            else pred[7][k] = (pel)((PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2);
             /* HU */
             {
                 int z = x + 2 * y, v;
@@ -809,7 +814,7 @@ static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int
                 else if (z == 5) v = (L[2] + 3 * L[3] + 2) >> 2;
                 else if (!(z & 1)) v = (L[y + (x >> 1)] + L[y + (x >> 1) + 1] + 1) >> 1;
                 else v = (L[y + (x >> 1)] + 2 * L[y + (x >> 1) + 1] + L[y + (x >> 1) + 2] + 2) >> 2;
-                pred[8][k] = (uint8_t)v;
+                pred[8][k] = (pel)v;
             }
         }
     /* DC */
@@ -817,8 +822,8 @@ static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int
     if (up && left) dcv = (PT(0) + PT(1) + PT(2) + PT(3) + L[0] + L[1] + L[2] + L[3] + 4) >> 3;
     else if (left) dcv = (L[0] + L[1] + L[2] + L[3] + 2) >> 2;
     else if (up) dcv = (PT(0) + PT(1) + PT(2) + PT(3) + 2) >> 2;
-    else dcv = 128;
-    for (int k = 0; k < 16; k++) pred[2][k] = (uint8_t)dcv;
+    else dcv = (c->maxv + 1) >> 1;
+    for (int k = 0; k < 16; k++) pred[2][k] = (pel)dcv;
 #undef PT
 #undef PL
 }
@@ -826,6 +831,13 @@ static void intra4x4_pred(const mbs *s, int bx, int by, uint8_t pred[9][16], int
 /* Intra8x8 prediction (8.3.2.2, JM FRExt intrapred_luma8x8 [J]): reference sample filtering
  * (8.3.2.2.1) then the nine modes.  See jm_oracle.h for nb[] / avail. */
 int jmo_intra8x8_pred(const int32_t nb[25], int avail, uint8_t pred[9][64]) {
+    pel p[9][64];
+    int ok = jmo_intra8x8_pred_px(nb, avail, p, 128);
+    for (int m = 0; m < 9; m++)
+        for (int k = 0; k < 64; k++) pred[m][k] = (uint8_t)p[m][k];
+    return ok;
+}
+int jmo_intra8x8_pred_px(const int32_t nb[25], int avail, pel pred[9][64], int dc) {
     int left = avail & 1, up = (avail >> 1) & 1, ur = (avail >> 2) & 1, ul = (avail >> 3) & 1;
     int p[16], q[8], c = nb[0];                    /* raw top row (x = 0..15), left column, corner */
     for (int x = 0; x < 16; x++) p[x] = x < 8 || ur ? nb[1 + x] : nb[8];   /* substitution p[7,-1] */
@@ -848,7 +860,7 @@ int jmo_intra8x8_pred(const int32_t nb[25], int avail, uint8_t pred[9][64]) {
     }
 #define PT(i) ((i) < 0 ? Q : T[i])
 #define PL(j) ((j) < 0 ? Q : L[j])
-    int dcv = 128, st = 0, sl = 0;
+    int dcv = dc, st = 0, sl = 0;
     for (int i = 0; i < 8; i++) { st += up ? T[i] : 0; sl += left ? L[i] : 0; }
     if (up && left) dcv = (st + sl + 8) >> 4;
     else if (up) dcv = (st + 4) >> 3;
@@ -858,40 +870,40 @@ int jmo_intra8x8_pred(const int32_t nb[25], int avail, uint8_t pred[9][64]) {
     for (int y = 0; y < 8; y++)
         for (int x = 0; x < 8; x++) {
             int k = 8 * y + x, v;
-            pred[2][k] = (uint8_t)dcv;
+            pred[2][k] = (pel)dcv;
             if (up) {
-                pred[0][k] = (uint8_t)T[x];
-                pred[3][k] = (uint8_t)(x == 7 && y == 7 ? (T[14] + 3 * T[15] + 2) >> 2
+                pred[0][k] = (pel)T[x];
+                pred[3][k] = (pel)(x == 7 && y == 7 ? (T[14] + 3 * T[15] + 2) >> 2
                                                        : (T[x + y] + 2 * T[x + y + 1] + T[x + y + 2] + 2) >> 2);
-                pred[7][k] = (uint8_t)(!(y & 1) ? (T[x + (y >> 1)] + T[x + (y >> 1) + 1] + 1) >> 1
+                pred[7][k] = (pel)(!(y & 1) ? (T[x + (y >> 1)] + T[x + (y >> 1) + 1] + 1) >> 1
                                                 : (T[x + (y >> 1)] + 2 * T[x + (y >> 1) + 1] + T[x + (y >> 1) + 2] + 2) >> 2);
             }
             if (left) {
-                pred[1][k] = (uint8_t)L[y];
+                pred[1][k] = (pel)L[y];
                 int z = x + 2 * y;
                 if (z > 13) v = L[7];
                 else if (z == 13) v = (L[6] + 3 * L[7] + 2) >> 2;
                 else if (!(z & 1)) v = (L[y + (x >> 1)] + L[y + (x >> 1) + 1] + 1) >> 1;
                 else v = (L[y + (x >> 1)] + 2 * L[y + (x >> 1) + 1] + L[y + (x >> 1) + 2] + 2) >> 2;
-                pred[8][k] = (uint8_t)v;
+                pred[8][k] = (pel)v;
             }
             if (up && left && ul) {
                 if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
                 else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
                 else v = (PT(0) + 2 * Q + PL(0) + 2) >> 2;
-                pred[4][k] = (uint8_t)v;
+                pred[4][k] = (pel)v;
                 int z = 2 * x - y;
                 if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
                 else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
                 else if (z == -1) v = (PL(0) + 2 * Q + PT(0) + 2) >> 2;
                 else v = (PL(y - 2 * x - 1) + 2 * PL(y - 2 * x - 2) + PL(y - 2 * x - 3) + 2) >> 2;
-                pred[5][k] = (uint8_t)v;
+                pred[5][k] = (pel)v;
                 z = 2 * y - x;
                 if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
                 else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
                 else if (z == -1) v = (PL(0) + 2 * Q + PT(0) + 2) >> 2;
                 else v = (PT(x - 2 * y - 1) + 2 * PT(x - 2 * y - 2) + PT(x - 2 * y - 3) + 2) >> 2;
-                pred[6][k] = (uint8_t)v;
+                pred[6][k] = (pel)v;
             }
         }
 #undef PT
@@ -900,9 +912,9 @@ int jmo_intra8x8_pred(const int32_t nb[25], int avail, uint8_t pred[9][64]) {
 }
 
 /* intrapred_luma_16x16 [J] / 8.3.3 */
-static void intra16_pred(const mbs *s, uint8_t pred[4][256], int avail[4]) {
+static void intra16_pred(const mbs *s, pel pred[4][256], int avail[4]) {
     const jmo_ctx *c = s->c;
-    const uint8_t *R = c->recY;
+    const pel *R = c->recY;
     int W = c->W, ax = s->pix_x, ay = s->pix_y;
     int up = mb_avail(s, 0, -1), left = mb_avail(s, -1, 0), ul = mb_avail(s, -1, -1);
     int T[16], L[16], P = ul ? R[(ay - 1) * W + ax - 1] : 0;
@@ -913,7 +925,7 @@ static void intra16_pred(const mbs *s, uint8_t pred[4][256], int avail[4]) {
     avail[0] = up; avail[1] = left; avail[2] = 1; avail[3] = up && left && ul;
     int st = 0, sl = 0;
     for (int i = 0; i < 16; i++) { st += T[i]; sl += L[i]; }
-    int dcv = (up && left) ? (st + sl + 16) >> 5 : up ? (st + 8) >> 4 : left ? (sl + 8) >> 4 : 128;
+    int dcv = (up && left) ? (st + sl + 16) >> 5 : up ? (st + 8) >> 4 : left ? (sl + 8) >> 4 : (c->maxv + 1) >> 1;
     int ih = 0, iv = 0;
     for (int i = 1; i <= 8; i++) {
         ih += i * (T[7 + i] - (7 - i >= 0 ? T[7 - i] : P));
@@ -923,17 +935,18 @@ static void intra16_pred(const mbs *s, uint8_t pred[4][256], int avail[4]) {
     for (int y = 0; y < 16; y++)
         for (int x = 0; x < 16; x++) {
             int k = 16 * y + x;
-            pred[0][k] = (uint8_t)T[x];
-            pred[1][k] = (uint8_t)L[y];
-            pred[2][k] = (uint8_t)dcv;
-            pred[3][k] = (uint8_t)clip255((iaa + (x - 7) * ib + (y - 7) * ic + 16) >> 5);
+            pred[0][k] = (pel)T[x];
+            pred[1][k] = (pel)L[y];
+            pred[2][k] = (pel)dcv;
+            pred[3][k] = (pel)clipv(c->maxv, (iaa + (x - 7) * ib + (y - 7) * ic + 16) >> 5);
         }
 }
 
 /* IntraChromaPrediction8x8 [J] / 8.3.4 for one component; pred[4][64] */
-static void intra_chroma_pred(const mbs *s, int uv, uint8_t pred[4][64], int avail[4]) {
+static void intra_chroma_pred(const mbs *s, int uv, pel pred[4][64], int avail[4]) {
     const jmo_ctx *c = s->c;
-    const uint8_t *R = uv ? c->recV : c->recU;
+    const pel *R = uv ? c->recV : c->recU;
+    const int dc = (c->maxv + 1) >> 1;
     int W = c->Wc, ax = s->pix_x >> 1, ay = s->pix_y >> 1;
     int up = mb_avail(s, 0, -1), left = mb_avail(s, -1, 0), ul = mb_avail(s, -1, -1);
     int T[8], L[8], P = ul ? R[(ay - 1) * W + ax - 1] : 0;
@@ -944,14 +957,14 @@ static void intra_chroma_pred(const mbs *s, int uv, uint8_t pred[4][64], int ava
     avail[0] = 1; avail[1] = left; avail[2] = up; avail[3] = up && left && ul;
     for (int b = 0; b < 4; b++) {          /* DC per 4x4 chroma block (8.3.4.1-3) */
         int xo = (b & 1) * 4, yo = (b >> 1) * 4;
-        int s0 = 0, s1 = 0, s2 = 0, s3 = 0, sv = 128;
+        int s0 = 0, s1 = 0, s2 = 0, s3 = 0, sv = dc;
         for (int i = 0; i < 4; i++) { s0 += T[i]; s1 += T[4 + i]; s2 += L[i]; s3 += L[4 + i]; }
-        if (b == 0) sv = (up && left) ? (s0 + s2 + 4) >> 3 : up ? (s0 + 2) >> 2 : left ? (s2 + 2) >> 2 : 128;
-        else if (b == 1) sv = up ? (s1 + 2) >> 2 : left ? (s2 + 2) >> 2 : 128;
-        else if (b == 2) sv = left ? (s3 + 2) >> 2 : up ? (s0 + 2) >> 2 : 128;
-        else sv = (up && left) ? (s1 + s3 + 4) >> 3 : up ? (s1 + 2) >> 2 : left ? (s3 + 2) >> 2 : 128;
+        if (b == 0) sv = (up && left) ? (s0 + s2 + 4) >> 3 : up ? (s0 + 2) >> 2 : left ? (s2 + 2) >> 2 : dc;
+        else if (b == 1) sv = up ? (s1 + 2) >> 2 : left ? (s2 + 2) >> 2 : dc;
+        else if (b == 2) sv = left ? (s3 + 2) >> 2 : up ? (s0 + 2) >> 2 : dc;
+        else sv = (up && left) ? (s1 + s3 + 4) >> 3 : up ? (s1 + 2) >> 2 : left ? (s3 + 2) >> 2 : dc;
         for (int y = 0; y < 4; y++)
-            for (int x = 0; x < 4; x++) pred[0][(yo + y) * 8 + xo + x] = (uint8_t)sv;
+            for (int x = 0; x < 4; x++) pred[0][(yo + y) * 8 + xo + x] = (pel)sv;
     }
     int ih = 0, iv = 0;
     for (int i = 1; i <= 4; i++) {
@@ -961,14 +974,14 @@ static void intra_chroma_pred(const mbs *s, int uv, uint8_t pred[4][64], int ava
     int ib = (34 * ih + 32) >> 6, ic = (34 * iv + 32) >> 6, iaa = 16 * (L[7] + T[7]);
     for (int y = 0; y < 8; y++)
         for (int x = 0; x < 8; x++) {
-            pred[1][y * 8 + x] = (uint8_t)L[y];
-            pred[2][y * 8 + x] = (uint8_t)T[x];
-            pred[3][y * 8 + x] = (uint8_t)clip255((iaa + (x - 3) * ib + (y - 3) * ic + 16) >> 5);
+            pred[1][y * 8 + x] = (pel)L[y];
+            pred[2][y * 8 + x] = (pel)T[x];
+            pred[3][y * 8 + x] = (pel)clipv(c->maxv, (iaa + (x - 3) * ib + (y - 3) * ic + 16) >> 5);
         }
 }
 
 /* find_sad_16x16 [J]: Hadamard cost of the 4 Intra16x16 predictions */
-static int find_sad_16x16(const mbs *s, uint8_t pred[4][256], const int avail[4], int *mode) {
+static int find_sad_16x16(const mbs *s, pel pred[4][256], const int avail[4], int *mode) {
     int best = MAX_VALUE;
     *mode = 2;
     for (int k = 0; k < 4; k++) {
@@ -1010,17 +1023,17 @@ static int find_sad_16x16(const mbs *s, uint8_t pred[4][256], const int avail[4]
 /* ====================================================================================== */
 /*  motion compensation                                                                    */
 /* ====================================================================================== */
-static void luma_pred_4x4(const mbs *s, int bx4, int by4, int mvx, int mvy, uint8_t *out, int os) {
+static void luma_pred_4x4(const mbs *s, int bx4, int by4, int mvx, int mvy, pel *out, int os) {
     for (int y = 0; y < 4; y++)
         for (int x = 0; x < 4; x++)
-            out[y * os + x] = (uint8_t)jmo_qpel_at(s->c, 4 * (s->pix_x + 4 * bx4 + x) + mvx,
+            out[y * os + x] = (pel)jmo_qpel_at(s->c, 4 * (s->pix_x + 4 * bx4 + x) + mvx,
                                                   4 * (s->pix_y + 4 * by4 + y) + mvy);
 }
 /* OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2: pixel (i,j) uses the MV of luma 4x4 block
  * (i>>1, j>>1) */
-static void chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], uint8_t pred[64]) {
+static void chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], pel pred[64]) {
     const jmo_ctx *c = s->c;
-    const uint8_t *R = uv ? c->refV : c->refU;
+    const pel *R = uv ? c->refV : c->refU;
     int Wc = c->Wc, Hc = c->Hc;
     for (int j = 0; j < 8; j++)
         for (int i = 0; i < 8; i++) {
@@ -1029,7 +1042,7 @@ static void chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], uint8_
             int x0 = iclip(0, Wc - 1, ii >> 3), y0 = iclip(0, Hc - 1, jj >> 3);
             int x1 = iclip(0, Wc - 1, (ii + 7) >> 3), y1 = iclip(0, Hc - 1, (jj + 7) >> 3);
             int fx = ii & 7, fy = jj & 7;
-            pred[j * 8 + i] = (uint8_t)(((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] +
+            pred[j * 8 + i] = (pel)(((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] +
                                          (8 - fx) * fy * R[y1 * Wc + x0] + fx * fy * R[y1 * Wc + x1] + 32) >> 6);
         }
 }
@@ -1038,7 +1051,7 @@ static void chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], uint8_
 /*  Intra8x8 decision (High profile): JM FRExt rdopt.c › Mode_Decision_for_Intra8x8Macroblock /  */
 /*  Mode_Decision_for_new_8x8IntraBlocks, RDO off [J] (docs/JM_SEMANTICS.md items 26-28)      */
 /* ====================================================================================== */
-static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, uint8_t rec[256],
+static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, pel rec[256],
                              int16_t lev[4][64], int modes[4], int *cbp) {
     const jmo_ctx *c = s->c;
     int cost = 6 * lambda;                                 /* (int)floor(6*lambda+0.4999), once */
@@ -1054,8 +1067,8 @@ static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, uint8_
         for (int x = 0; x < 16; x++) if (up && (x < 8 || ur)) nb[1 + x] = SMP(bx + x, by - 1);
         for (int y = 0; y < 8; y++) if (left) nb[17 + y] = SMP(bx - 1, by + y);
 #undef SMP
-        uint8_t pred[9][64];
-        int ok = jmo_intra8x8_pred(nb, left | up << 1 | ur << 2 | ul << 3, pred);
+        pel pred[9][64];
+        int ok = jmo_intra8x8_pred_px(nb, left | up << 1 | ur << 2 | ul << 3, pred, (c->maxv + 1) >> 1);
         /* predIntra8x8PredMode (8.3.2.1): neighbour 4x4 modes (I4: that block, I8: repeated, else 2) */
         int ma = -1, mb = -1, ia = 0, ib = 0;
         if (bx) ma = modes[b8 - 1];
@@ -1077,7 +1090,7 @@ static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, uint8_
         for (int y = 0; y < 8; y++)
             for (int x = 0; x < 8; x++) r[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[best][8 * y + x];
         int dummy = 0;
-        if (dct_luma8x8(r, pred[best], 8, qp, intra_round, lev[b8], &dummy, rec + by * 16 + bx, 16)) *cbp |= 1 << b8;
+        if (dct_luma8x8(r, pred[best], 8, qp, intra_round, lev[b8], &dummy, rec + by * 16 + bx, 16, c->maxv)) *cbp |= 1 << b8;
         cost += bcost;
     }
     return cost;
@@ -1085,7 +1098,7 @@ static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, uint8_
 
 /* TransformDecision [J] (RDO off): over the final prediction of the MB, sum of the 16 4x4 SATDs
  * against the sum of the four 8x8 SATDs; 8x8 if strictly smaller (item 29) */
-static int transform_decision(const mbs *s, const uint8_t pred[256]) {
+static int transform_decision(const mbs *s, const pel pred[256]) {
     int had = s->c->cfg.use_hadamard, cost4 = 0, cost8 = 0;
     for (int b8 = 0; b8 < 4; b8++) {
         int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
@@ -1106,8 +1119,8 @@ static int transform_decision(const mbs *s, const uint8_t pred[256]) {
 /* ====================================================================================== */
 /*  encode_one_macroblock (RDO off)                                                         */
 /* ====================================================================================== */
-static void store_rec_luma(jmo_ctx *c, const mbs *s, const uint8_t rec[256]) {
-    for (int y = 0; y < 16; y++) memcpy(c->recY + (s->pix_y + y) * c->W + s->pix_x, rec + 16 * y, 16);
+static void store_rec_luma(jmo_ctx *c, const mbs *s, const pel rec[256]) {
+    for (int y = 0; y < 16; y++) memcpy(c->recY + (s->pix_y + y) * c->W + s->pix_x, rec + 16 * y, 16 * sizeof(pel));
 }
 
 void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
@@ -1119,17 +1132,18 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     s->lambda = c->fp.lambda_motion;
     s->lf = 65536 * s->lambda;
     s->slice_p = c->fp.slice_type == JMH_P_SLICE;
-    int qp = c->fp.qp, lambda = c->fp.lambda_mode;
+    /* quantisation at QP'Y = QPY + QpBdOffsetY (8.5.x; JM >= 10 bitdepth_luma_qp_scale [J]) */
+    const int qpy = c->fp.qp, qp = qpy + c->qpbd, lambda = c->fp.lambda_mode, maxv = c->maxv;
     /* JM 8.6: qp_const by slice type, Intra16x16 always / 3 [J]; JM >= 10: the slice's flat
      * OffsetMatrix entry for every block (items 1, 45) */
     const int jm10 = c->cfg.jm_version >= 10;
     int intra_round = jm10 ? JMO_RND_OFF(c->cfg.quant_offset[s->slice_p]) : !s->slice_p;
     int i16_round = jm10 ? intra_round : JMO_RND_I;
     int W = c->W, W4 = W >> 2;
-    for (int y = 0; y < 16; y++) memcpy(s->org + 16 * y, c->orgY + (s->pix_y + y) * W + s->pix_x, 16);
+    for (int y = 0; y < 16; y++) memcpy(s->org + 16 * y, c->orgY + (s->pix_y + y) * W + s->pix_x, 16 * sizeof(pel));
     for (int y = 0; y < 8; y++) {
-        memcpy(s->orgc[0] + 8 * y, c->orgU + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), 8);
-        memcpy(s->orgc[1] + 8 * y, c->orgV + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), 8);
+        memcpy(s->orgc[0] + 8 * y, c->orgU + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), 8 * sizeof(pel));
+        memcpy(s->orgc[1] + 8 * y, c->orgV + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), 8 * sizeof(pel));
     }
     jmh_mb_result *res = &c->res[s->mb_addr];
     memset(res, 0, sizeof(*res));
@@ -1178,7 +1192,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
 
     /* ===== Intra 8x8 decision (Transform8x8Mode; before Intra4x4, "<=") ===== */
     const int t8 = c->cfg.transform_8x8_mode;
-    uint8_t i8rec[256];
+    pel i8rec[256];
     int16_t i8lev[4][64];
     int i8modes[4] = {2, 2, 2, 2}, i8cbp = 0;
     if (t8) {
@@ -1186,7 +1200,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
         if (i8cost <= min_cost) { min_cost = i8cost; best_mode = JMH_I8MB; }
     }
     /* ===== Intra 4x4 decision (with TQ + recon of every 4x4 in coding order) ===== */
-    uint8_t i4rec[256];
+    pel i4rec[256];
     int16_t i4lev[16][16];
     int i4modes[16];
     int i4cbp = 0, i4cbpblk = 0, i4cost = 0;
@@ -1202,7 +1216,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                 int av_l = nb4(s, bx - 1, by, &ia), av_u = nb4(s, bx, by - 1, &ib);
                 int upMode = av_u ? c->ipred[ib] : -1, leftMode = av_l ? c->ipred[ia] : -1;
                 int mpm = (upMode < 0 || leftMode < 0) ? 2 : imin(upMode, leftMode);
-                uint8_t pred[9][16];
+                pel pred[9][16];
                 int avail[9];
                 intra4x4_pred(s, bx, by, pred, avail);
                 int best = 0, bcost = BIGCOST;
@@ -1223,8 +1237,8 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                     for (int x = 0; x < 4; x++)
                         r[4 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[best][4 * y + x];
                 int dummy = 0;
-                uint8_t *dst = c->recY + (s->pix_y + by) * c->W + s->pix_x + bx;
-                if (dct_luma4x4(r, pred[best], 4, qp, intra_round, i4lev[blk], &dummy, dst, c->W)) {
+                pel *dst = c->recY + (s->pix_y + by) * c->W + s->pix_x + bx;
+                if (dct_luma4x4(r, pred[best], 4, qp, intra_round, i4lev[blk], &dummy, dst, c->W, maxv)) {
                     i4cbp |= 1 << b8;
                     i4cbpblk |= 1 << blk;
                 }
@@ -1232,11 +1246,11 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
             }
             i4cost += cost8;
         }
-        for (int y = 0; y < 16; y++) memcpy(i4rec + 16 * y, c->recY + (s->pix_y + y) * c->W + s->pix_x, 16);
+        for (int y = 0; y < 16; y++) memcpy(i4rec + 16 * y, c->recY + (s->pix_y + y) * c->W + s->pix_x, 16 * sizeof(pel));
     }
     if (i4cost <= min_cost) { min_cost = i4cost; best_mode = JMH_I4MB; }
     /* ===== Intra 16x16 ===== */
-    uint8_t i16pred[4][256];
+    pel i16pred[4][256];
     int i16avail[4], i16mode = 2;
     intra16_pred(s, i16pred, i16avail);
     int i16cost = find_sad_16x16(s, i16pred, i16avail, &i16mode);
@@ -1258,10 +1272,10 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
             fmv[k][1] = s->all_mv[b8mode[b8]][k][1];
         }
     int cbp = 0, cbp_blk = 0, tr8 = 0;
-    uint8_t rec[256];
+    pel rec[256];
     if (best_mode == JMH_I8MB) {
         cbp = i8cbp; tr8 = 1;
-        memcpy(rec, i8rec, 256);
+        memcpy(rec, i8rec, sizeof(rec));
         for (int b8 = 0; b8 < 4; b8++) {
             put_levels8(res->luma, b8, i8lev[b8]);
             if ((cbp >> b8) & 1) cbp_blk |= 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2);
@@ -1269,16 +1283,16 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
         for (int k = 0; k < 16; k++) res->ipred[k] = (int8_t)i8modes[((k >> 3) << 1) + ((k & 3) >> 1)];
     } else if (best_mode == JMH_I4MB) {
         cbp = i4cbp; cbp_blk = i4cbpblk;
-        memcpy(rec, i4rec, 256);
+        memcpy(rec, i4rec, sizeof(rec));
         for (int k = 0; k < 16; k++) { res->ipred[k] = (int8_t)i4modes[k]; memcpy(res->luma[k], i4lev[k], 32); }
     } else if (best_mode == JMH_I16MB) {
         int32_t r[256];
         for (int k = 0; k < 256; k++) r[k] = s->org[k] - i16pred[i16mode][k];
-        cbp = dct_luma_16x16(r, i16pred[i16mode], qp, i16_round, res->luma_dc, res->luma, &cbp_blk, rec);
+        cbp = dct_luma_16x16(r, i16pred[i16mode], qp, i16_round, res->luma_dc, res->luma, &cbp_blk, rec, maxv);
         res->i16mode = (int8_t)i16mode;
     } else {
         /* LumaResidualCoding / LumaResidualCoding8x8 (also SetCoeffAndReconstruction8x8) */
-        uint8_t pred[256];
+        pel pred[256];
         int sum_cnt_nonz = 0;
         for (int k = 0; k < 16; k++) luma_pred_4x4(s, k & 3, k >> 2, fmv[k][0], fmv[k][1], pred + 4 * (k >> 2) * 16 + 4 * (k & 3), 16);
         if (t8 && (best_mode <= 3 || (b8mode[0] == 4 && b8mode[1] == 4 && b8mode[2] == 4 && b8mode[3] == 4)))
@@ -1291,7 +1305,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                 int16_t lv[64];
                 for (int y = 0; y < 8; y++)
                     for (int x = 0; x < 8; x++) r[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[(by + y) * 16 + bx + x];
-                if (dct_luma8x8(r, pred + by * 16 + bx, 16, qp, intra_round, lv, &coeff_cost, rec + by * 16 + bx, 16)) {
+                if (dct_luma8x8(r, pred + by * 16 + bx, 16, qp, intra_round, lv, &coeff_cost, rec + by * 16 + bx, 16, maxv)) {
                     cbp8 = 1;
                     blk8 = 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2);
                 }
@@ -1305,7 +1319,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                     for (int x = 0; x < 4; x++)
                         r[4 * y + x] = s->org[(4 * by4 + y) * 16 + 4 * bx4 + x] - pred[(4 * by4 + y) * 16 + 4 * bx4 + x];
                 if (dct_luma4x4(r, pred + 4 * by4 * 16 + 4 * bx4, 16, qp, intra_round, res->luma[k], &coeff_cost,
-                                rec + 4 * by4 * 16 + 4 * bx4, 16)) {
+                                rec + 4 * by4 * 16 + 4 * bx4, 16, maxv)) {
                     blk8 |= 1 << k;
                     cbp8 = 1;
                 }
@@ -1317,7 +1331,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                     int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1);
                     memset(res->luma[by4 * 4 + bx4], 0, 32);
                     for (int y = 0; y < 4; y++)
-                        memcpy(rec + (4 * by4 + y) * 16 + 4 * bx4, pred + (4 * by4 + y) * 16 + 4 * bx4, 4);
+                        memcpy(rec + (4 * by4 + y) * 16 + 4 * bx4, pred + (4 * by4 + y) * 16 + 4 * bx4, 4 * sizeof(pel));
                 }
             }
             if (cbp8) cbp |= 1 << b8;
@@ -1327,14 +1341,14 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
         if (sum_cnt_nonz <= LUMA_MB_COEFF_COST) {
             cbp = 0; cbp_blk = 0;
             memset(res->luma, 0, sizeof(res->luma));
-            memcpy(rec, pred, 256);
+            memcpy(rec, pred, sizeof(rec));
         }
     }
     store_rec_luma(c, s, rec);
 
     /* ===== chroma: IntraChromaPrediction8x8 (intra MBs) + ChromaResidualCoding ===== */
     int c_mode = 0;
-    uint8_t cpred[2][4][64];
+    pel cpred[2][4][64];
     if (is_intra) {
         int cav[4];
         intra_chroma_pred(s, 0, cpred[0], cav);
@@ -1355,17 +1369,18 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
             if (cost < min_c) { min_c = cost; c_mode = m; }
         }
     }
-    int qpc = jmo_qp_scale_cr(qp + c->fp.chroma_qp_offset);
+    /* QP'c = QPc(Clip3(-QpBdOffsetC, 51, QPY + chroma_qp_index_offset)) + QpBdOffsetC (8.5.8) */
+    int qpc = jmo_qpc(qpy + c->fp.chroma_qp_offset, c->qpbd) + c->qpbd;
     int cr_cbp = 0;
     for (int uv = 0; uv < 2; uv++) {
-        uint8_t pred[64], crec[64];
-        if (is_intra) memcpy(pred, cpred[uv][c_mode], 64);
+        pel pred[64], crec[64];
+        if (is_intra) memcpy(pred, cpred[uv][c_mode], sizeof(pred));
         else chroma_pred_mb(s, uv, fmv, pred);
         int32_t r[64];
         for (int k = 0; k < 64; k++) r[k] = s->orgc[uv][k] - pred[k];
-        cr_cbp = dct_chroma(r, pred, qpc, intra_round, cr_cbp, res->chroma_dc[uv], res->chroma_ac[uv], crec);
-        uint8_t *R = uv ? c->recV : c->recU;
-        for (int y = 0; y < 8; y++) memcpy(R + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), crec + 8 * y, 8);
+        cr_cbp = dct_chroma(r, pred, qpc, intra_round, cr_cbp, res->chroma_dc[uv], res->chroma_ac[uv], crec, maxv);
+        pel *R = uv ? c->recV : c->recU;
+        for (int y = 0; y < 8; y++) memcpy(R + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), crec + 8 * y, 8 * sizeof(pel));
     }
     cbp |= cr_cbp << 4;
 

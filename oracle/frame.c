@@ -19,6 +19,7 @@ static int cfg_ok(const jmh_config *cfg) {
     if (cfg->jm_version < 0 || cfg->jm_version == 9 || cfg->jm_version > 99) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->epzs_dual_refinement != 0 && cfg->epzs_dual_refinement != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->slice_mbs < 0) return JMH_E_INVALID_ARG;
+    if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     return JMH_OK;
@@ -32,16 +33,19 @@ int jmo_create(const jmh_config *cfg, jmo_ctx **out) {
     c->cfg = *cfg;
     c->W = cfg->width; c->H = cfg->height; c->Wc = c->W / 2; c->Hc = c->H / 2;
     c->mbw = c->W / 16; c->mbh = c->H / 16;
+    c->bd = cfg->bit_depth ? cfg->bit_depth : 8;
+    c->maxv = (1 << c->bd) - 1;
+    c->qpbd = 6 * (c->bd - 8);
     c->sr = cfg->search_range;
     c->npos = (2 * c->sr + 1) * (2 * c->sr + 1);
     jmo_init_spiral(c);
     size_t ls = (size_t)c->W * c->H, cs = (size_t)c->Wc * c->Hc, n4 = ls / 16;
-    c->orgY = malloc(ls); c->orgU = malloc(cs); c->orgV = malloc(cs);
-    c->refY = malloc(ls); c->refU = malloc(cs); c->refV = malloc(cs);
-    c->recY = calloc(ls, 1); c->recU = calloc(cs, 1); c->recV = calloc(cs, 1);
+    c->orgY = malloc(ls * sizeof(pel)); c->orgU = malloc(cs * sizeof(pel)); c->orgV = malloc(cs * sizeof(pel));
+    c->refY = malloc(ls * sizeof(pel)); c->refU = malloc(cs * sizeof(pel)); c->refV = malloc(cs * sizeof(pel));
+    c->recY = calloc(ls, sizeof(pel)); c->recU = calloc(cs, sizeof(pel)); c->recV = calloc(cs, sizeof(pel));
     c->qstride = c->W + 2 * JMO_PAD;
     c->qplane = c->qstride * (c->H + 2 * JMO_PAD);
-    c->qpel = malloc((size_t)16 * c->qplane);
+    c->qpel = malloc((size_t)16 * c->qplane * sizeof(pel));
     c->mv = calloc(2 * n4, sizeof(int16_t));
     c->refidx = calloc(n4, 1);
     c->ipred = calloc(n4, 1);
@@ -67,40 +71,56 @@ void jmo_destroy(jmo_ctx *c) {
     free(c);
 }
 
-static void copy_plane(uint8_t *dst, int dw, int dh, const uint8_t *src, int stride) {
-    for (int y = 0; y < dh; y++) memcpy(dst + (size_t)y * dw, src + (size_t)y * stride, dw);
+/* pictures enter as 8-bit (uint8_t entry points, bit depth 8) or 16-bit samples (the _u16 ones,
+ * High 10): stored as pel either way; a sample above (1 << bit depth) - 1 is an argument error */
+static int copy_plane(pel *dst, int dw, int dh, const void *src, int stride, int wide, int maxv) {
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            int v = wide ? ((const uint16_t *)src)[(size_t)y * stride + x] : ((const uint8_t *)src)[(size_t)y * stride + x];
+            if (v > maxv) return JMH_E_INVALID_ARG;
+            dst[(size_t)y * dw + x] = (pel)v;
+        }
+    return JMH_OK;
+}
+static int copy_pic(const jmo_ctx *c, pel *Y, pel *U, pel *V, const void *y, const void *u, const void *v, int sy, int sc,
+                    int wide) {
+    if ((c->bd > 8) != wide) return JMH_E_UNSUPPORTED_CFG;    /* 8-bit entry points <-> bit depth 8 */
+    int r = copy_plane(Y, c->W, c->H, y, sy, wide, c->maxv);
+    if (!r) r = copy_plane(U, c->Wc, c->Hc, u, sc, wide, c->maxv);
+    if (!r) r = copy_plane(V, c->Wc, c->Hc, v, sc, wide, c->maxv);
+    return r;
 }
 
-int jmo_set_reference(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
-                      int stride_y, int stride_c) {
+static int set_reference(jmo_ctx *c, const void *y, const void *u, const void *v, int stride_y, int stride_c, int wide) {
     if (!c || !y || !u || !v) return JMH_E_INVALID_ARG;
-    copy_plane(c->refY, c->W, c->H, y, stride_y);
-    copy_plane(c->refU, c->Wc, c->Hc, u, stride_c);
-    copy_plane(c->refV, c->Wc, c->Hc, v, stride_c);
+    int r = copy_pic(c, c->refY, c->refU, c->refV, y, u, v, stride_y, stride_c, wide);
+    if (r) return r;
     jmo_build_qpel(c);
     c->have_ref = 1;
     return JMH_OK;
+}
+int jmo_set_reference(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int stride_y, int stride_c) {
+    return set_reference(c, y, u, v, stride_y, stride_c, 0);
+}
+int jmo_set_reference_u16(jmo_ctx *c, const uint16_t *y, const uint16_t *u, const uint16_t *v, int stride_y, int stride_c) {
+    return set_reference(c, y, u, v, stride_y, stride_c, 1);
 }
 
 int jmo_load_current(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
                      int stride_y, int stride_c) {
     if (!c || !y || !u || !v) return JMH_E_INVALID_ARG;
-    copy_plane(c->orgY, c->W, c->H, y, stride_y);
-    copy_plane(c->orgU, c->Wc, c->Hc, u, stride_c);
-    copy_plane(c->orgV, c->Wc, c->Hc, v, stride_c);
-    return JMH_OK;
+    return copy_pic(c, c->orgY, c->orgU, c->orgV, y, u, v, stride_y, stride_c, 0);
 }
 
-int jmo_encode_frame(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
-                     int stride_y, int stride_c, const jmh_frame_params *fp) {
+static int encode_frame(jmo_ctx *c, const void *y, const void *u, const void *v, int stride_y, int stride_c,
+                        const jmh_frame_params *fp, int wide) {
     if (!c || !y || !u || !v || !fp) return JMH_E_INVALID_ARG;
     if (fp->slice_type != JMH_P_SLICE && fp->slice_type != JMH_I_SLICE) return JMH_E_UNSUPPORTED_CFG;
     if (fp->slice_type == JMH_P_SLICE && !c->have_ref) return JMH_E_STATE;
     if (fp->qp < 0 || fp->qp > 51) return JMH_E_INVALID_ARG;
+    int r = copy_pic(c, c->orgY, c->orgU, c->orgV, y, u, v, stride_y, stride_c, wide);
+    if (r) return r;
     c->fp = *fp;
-    copy_plane(c->orgY, c->W, c->H, y, stride_y);
-    copy_plane(c->orgU, c->Wc, c->Hc, u, stride_c);
-    copy_plane(c->orgV, c->Wc, c->Hc, v, stride_c);
     size_t n4 = (size_t)c->W * c->H / 16;
     memcpy(c->tmv, c->mv, 2 * n4 * sizeof(int16_t));     /* EPZS temporal predictors: the last */
     memcpy(c->tref, c->refidx, n4);                       /* encoded picture's motion field     */
@@ -111,25 +131,46 @@ int jmo_encode_frame(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8
         for (int mx = 0; mx < c->mbw; mx++) jmo_encode_mb(c, mx, my);
     return JMH_OK;
 }
+int jmo_encode_frame(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int stride_y, int stride_c,
+                     const jmh_frame_params *fp) {
+    return encode_frame(c, y, u, v, stride_y, stride_c, fp, 0);
+}
+int jmo_encode_frame_u16(jmo_ctx *c, const uint16_t *y, const uint16_t *u, const uint16_t *v, int stride_y,
+                         int stride_c, const jmh_frame_params *fp) {
+    return encode_frame(c, y, u, v, stride_y, stride_c, fp, 1);
+}
 
 const jmh_mb_result *jmo_mb_result(const jmo_ctx *c, int mb_addr) {
     if (!c || mb_addr < 0 || mb_addr >= c->mbw * c->mbh) return NULL;
     return &c->res[mb_addr];
 }
 
-int jmo_read_recon(const jmo_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y, int stride_c) {
+static void out_plane(void *dst, int stride, const pel *src, int w, int h, int wide) {
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            if (wide) ((uint16_t *)dst)[(size_t)y * stride + x] = src[(size_t)y * w + x];
+            else ((uint8_t *)dst)[(size_t)y * stride + x] = (uint8_t)src[(size_t)y * w + x];
+        }
+}
+static int read_recon(const jmo_ctx *c, void *y, void *u, void *v, int stride_y, int stride_c, int wide) {
     if (!c) return JMH_E_INVALID_ARG;
-    for (int r = 0; r < c->H; r++) memcpy(y + (size_t)r * stride_y, c->recY + (size_t)r * c->W, c->W);
-    for (int r = 0; r < c->Hc; r++) {
-        memcpy(u + (size_t)r * stride_c, c->recU + (size_t)r * c->Wc, c->Wc);
-        memcpy(v + (size_t)r * stride_c, c->recV + (size_t)r * c->Wc, c->Wc);
-    }
+    if ((c->bd > 8) != wide) return JMH_E_UNSUPPORTED_CFG;
+    out_plane(y, stride_y, c->recY, c->W, c->H, wide);
+    out_plane(u, stride_c, c->recU, c->Wc, c->Hc, wide);
+    out_plane(v, stride_c, c->recV, c->Wc, c->Hc, wide);
     return JMH_OK;
+}
+int jmo_read_recon(const jmo_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y, int stride_c) {
+    return read_recon(c, y, u, v, stride_y, stride_c, 0);
+}
+int jmo_read_recon_u16(const jmo_ctx *c, uint16_t *y, uint16_t *u, uint16_t *v, int stride_y, int stride_c) {
+    return read_recon(c, y, u, v, stride_y, stride_c, 1);
 }
 
 int jmo_read_qpel(const jmo_ctx *c, uint8_t *out) {
     if (!c || !c->have_ref) return JMH_E_STATE;
-    memcpy(out, c->qpel, (size_t)16 * c->qplane);
+    if (c->bd > 8) return JMH_E_UNSUPPORTED_CFG;
+    for (size_t i = 0; i < (size_t)16 * c->qplane; i++) out[i] = (uint8_t)c->qpel[i];
     return JMH_OK;
 }
 

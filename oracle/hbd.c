@@ -58,7 +58,7 @@ int jmo_hbd_pictures(jmo_hbd *h, const uint16_t *cur, const uint16_t *ref, int s
 
 static inline int rp(const jmo_hbd *h, int x, int y) { return h->ref[iclip(0, h->H - 1, y) * h->W + iclip(0, h->W - 1, x)]; }
 static inline int t6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
-static inline int clipv(const jmo_hbd *h, int v) { return iclip(0, h->maxv, v); }
+static inline int hclip(const jmo_hbd *h, int v) { return iclip(0, h->maxv, v); }
 static int hb1(const jmo_hbd *h, int x, int y) { return t6(rp(h, x - 2, y), rp(h, x - 1, y), rp(h, x, y), rp(h, x + 1, y), rp(h, x + 2, y), rp(h, x + 3, y)); }
 static int vh1(const jmo_hbd *h, int x, int y) { return t6(rp(h, x, y - 2), rp(h, x, y - 1), rp(h, x, y), rp(h, x, y + 1), rp(h, x, y + 2), rp(h, x, y + 3)); }
 
@@ -67,9 +67,9 @@ int jmo_hbd_qpel(const jmo_hbd *h, int X, int Y) {
     const int x = X >> 2, y = Y >> 2, fx = X & 3, fy = Y & 3;
     const int G = rp(h, x, y);
     if (!fx && !fy) return G;
-    const int b = clipv(h, (hb1(h, x, y) + 16) >> 5), hh = clipv(h, (vh1(h, x, y) + 16) >> 5);
-    const int s = clipv(h, (hb1(h, x, y + 1) + 16) >> 5), m = clipv(h, (vh1(h, x + 1, y) + 16) >> 5);
-    const int j = clipv(h, (t6(vh1(h, x - 2, y), vh1(h, x - 1, y), vh1(h, x, y), vh1(h, x + 1, y), vh1(h, x + 2, y), vh1(h, x + 3, y)) + 512) >> 10);
+    const int b = hclip(h, (hb1(h, x, y) + 16) >> 5), hh = hclip(h, (vh1(h, x, y) + 16) >> 5);
+    const int s = hclip(h, (hb1(h, x, y + 1) + 16) >> 5), m = hclip(h, (vh1(h, x + 1, y) + 16) >> 5);
+    const int j = hclip(h, (t6(vh1(h, x - 2, y), vh1(h, x - 1, y), vh1(h, x, y), vh1(h, x + 1, y), vh1(h, x + 2, y), vh1(h, x + 3, y)) + 512) >> 10);
     switch (fy * 4 + fx) {
     case 1: return (G + b + 1) >> 1;
     case 2: return b;

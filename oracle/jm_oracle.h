@@ -37,6 +37,12 @@ int  jmo_set_reference(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uin
 int  jmo_encode_frame(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v,
                       int stride_y, int stride_c, const jmh_frame_params *fp);
 const jmh_mb_result *jmo_mb_result(const jmo_ctx *c, int mb_addr);
+/* High 10 pictures (cfg.bit_depth 9 / 10): 16-bit samples; the uint8_t entry points serve bit depth 8 */
+int  jmo_set_reference_u16(jmo_ctx *c, const uint16_t *y, const uint16_t *u, const uint16_t *v, int stride_y,
+                           int stride_c);
+int  jmo_encode_frame_u16(jmo_ctx *c, const uint16_t *y, const uint16_t *u, const uint16_t *v, int stride_y,
+                          int stride_c, const jmh_frame_params *fp);
+int  jmo_read_recon_u16(const jmo_ctx *c, uint16_t *y, uint16_t *u, uint16_t *v, int stride_y, int stride_c);
 int  jmo_read_recon(const jmo_ctx *c, uint8_t *y, uint8_t *u, uint8_t *v, int stride_y,
                     int stride_c);
 /* copy the 16 quarter-pel phase planes: out[16][(H+2P)][(W+2P)], phase = 4*yfrac + xfrac  */

@@ -29,25 +29,31 @@ static inline int imin(int a, int b) { return a < b ? a : b; }
 static inline int imax(int a, int b) { return a > b ? a : b; }
 static inline int iclip(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 static inline int clip255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+/* samples: 16-bit storage for every bit depth (8: values 0..255; High 10: 0..1023, JM >= 10 imgpel
+ * = unsigned short [J]); Clip1 = clip to (1 << bit_depth) - 1 */
+typedef uint16_t pel;
+static inline int clipv(int maxv, int v) { return v < 0 ? 0 : (v > maxv ? maxv : v); }
 static inline int isign(int a, int b) { return b < 0 ? -iabs(a) : iabs(a); } /* JM sign(a,b) */
 
 /* ---- encoder state (replaces JM's img/enc_picture globals for the hot path) ------------ */
 struct jmo_ctx {
     jmh_config cfg;
     int W, H, Wc, Hc, mbw, mbh;
+    int bd, maxv, qpbd;              /* bit depth, (1 << bd) - 1, QpBdOffsetY = QpBdOffsetC = 6 (bd - 8) */
     int sr;                          /* max search range                                       */
     int npos;                        /* (2sr+1)^2                                              */
     int32_t *spiral_x, *spiral_y;    /* JM spiral_search_x/y [J]                               */
     int32_t *spiral_of;              /* window raster (dy+sr)*(2sr+1)+(dx+sr) -> spiral index   */
     /* current picture (coded size) */
-    uint8_t *orgY, *orgU, *orgV;
+    pel *orgY, *orgU, *orgV;
     /* reference: integer planes + 16 quarter-pel phase planes (padded by JMO_PAD) */
-    uint8_t *refY, *refU, *refV;
-    uint8_t *qpel;                   /* [16][H+2P][W+2P]                                        */
+    pel *refY, *refU, *refV;
+    pel *qpel;                       /* [16][H+2P][W+2P]                                        */
     int qstride, qplane;
     int have_ref;
     /* unfiltered reconstruction (enc_picture->imgY / imgUV) */
-    uint8_t *recY, *recU, *recV;
+    pel *recY, *recU, *recV;
     /* per-4x4 picture arrays (enc_picture->mv / ref_idx, img->ipredmode) */
     int16_t *mv;                     /* [(H/4)*(W/4)][2] */
     int8_t *refidx;                  /* [(H/4)*(W/4)]    */
@@ -77,8 +83,12 @@ void jmo_build_qpel(jmo_ctx *c);
 int  jmo_qpel_at(const jmo_ctx *c, int X, int Y);   /* from the phase planes (clamped)   */
 int  jmo_satd_block(const int32_t d[16], int use_hadamard);
 void jmo_fwd4x4(int32_t m[16]);                       /* in-place, raster                 */
-void jmo_inv4x4_add(const int32_t m[16], const uint8_t *pred, int pstride, uint8_t *out,
-                    int ostride);
+void jmo_inv4x4_add(const int32_t m[16], const pel *pred, int pstride, pel *out, int ostride, int maxv);
+/* spec luma sample at quarter-pel (X,Y) of a pel plane (8.4.2.2.1, Clip1 to maxv)            */
+int  jmo_qpel_px(const pel *p, int w, int h, int stride, int X, int Y, int maxv);
+/* QPc of a luma QP + chroma offset (8.5.8, Table 8-15), qPI clipped to [-qpbd, 51]: negative
+ * values map to themselves (high bit depth); add qpbd for QP'c                              */
+int  jmo_qpc(int qp_plus_offset, int qpbd);
 
 /* 8x8 transform (High profile) */
 #define Q_BITS_8 16               /* JM FRExt Q_BITS_8 [J]                                 */
@@ -101,7 +111,9 @@ int  jmo_coeff_cost8(int run);
 void jmo_scan8x8(int scan[64]);
 void jmo_fwd8x8(int32_t m[64]);
 void jmo_inverse8x8(const int32_t *in, int32_t *out);
-void jmo_inv8x8_add(const int32_t m[64], const uint8_t *pred, int pstride, uint8_t *out, int ostride);
+void jmo_inv8x8_add(const int32_t m[64], const pel *pred, int pstride, pel *out, int ostride, int maxv);
+/* Intra8x8 prediction on pel samples (jmo_intra8x8_pred's body); dc = 1 << (bd - 1)          */
+int  jmo_intra8x8_pred_px(const int32_t nb[25], int avail, pel pred[9][64], int dc);
 int  jmo_satd8x8(const int32_t d[64], int use_hadamard);
 
 /* encode.c */

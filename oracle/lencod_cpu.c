@@ -8,12 +8,19 @@
 #include "jm_oracle.h"
 #include "jmhost.h"
 
-static int o_set_ref(void *c, const jm_pic *p) { return jmo_set_reference((jmo_ctx *)c, p->y, p->u, p->v, p->w, p->w / 2); }
+static int o_set_ref(void *c, const jm_pic *p) {
+    if (p->bd > 8) return jmo_set_reference_u16((jmo_ctx *)c, p->Y, p->U, p->V, p->w, p->w / 2);
+    return jmo_set_reference((jmo_ctx *)c, p->y, p->u, p->v, p->w, p->w / 2);
+}
 static int o_encode(void *c, const jm_pic *p, const jmh_frame_params *fp) {
+    if (p->bd > 8) return jmo_encode_frame_u16((jmo_ctx *)c, p->Y, p->U, p->V, p->w, p->w / 2, fp);
     return jmo_encode_frame((jmo_ctx *)c, p->y, p->u, p->v, p->w, p->w / 2, fp);
 }
 static const jmh_mb_result *o_res(void *c, int a) { return jmo_mb_result((const jmo_ctx *)c, a); }
-static int o_recon(void *c, jm_pic *p) { return jmo_read_recon((const jmo_ctx *)c, p->y, p->u, p->v, p->w, p->w / 2); }
+static int o_recon(void *c, jm_pic *p) {
+    if (p->bd > 8) return jmo_read_recon_u16((const jmo_ctx *)c, p->Y, p->U, p->V, p->w, p->w / 2);
+    return jmo_read_recon((const jmo_ctx *)c, p->y, p->u, p->v, p->w, p->w / 2);
+}
 static void o_destroy(void *c) { jmo_destroy((jmo_ctx *)c); }
 /* the per-call seams of the JM call surface; jmo_search_pictures loads the same current and
  * reference luma the picture was encoded with (the oracle encodes one picture at a time) */

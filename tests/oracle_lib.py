@@ -22,6 +22,9 @@ def lib():
             "jmo_create": (_I, [ctypes.POINTER(jmhip.JmhConfig), ctypes.POINTER(_P)]),
             "jmo_destroy": (None, [_P]),
             "jmo_set_reference": (_I, [_P, _P, _P, _P, _I, _I]),
+            "jmo_set_reference_u16": (_I, [_P, _P, _P, _P, _I, _I]),
+            "jmo_encode_frame_u16": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(jmhip.JmhFrameParams)]),
+            "jmo_read_recon_u16": (_I, [_P, _P, _P, _P, _I, _I]),
             "jmo_encode_frame": (_I, [_P, _P, _P, _P, _I, _I, ctypes.POINTER(jmhip.JmhFrameParams)]),
             "jmo_mb_result": (_P, [_P, _I]),
             "jmo_read_recon": (_I, [_P, _P, _P, _P, _I, _I]),
@@ -75,6 +78,8 @@ class OracleEncoder:
         self.w, self.h = width, height
         self.mbw, self.mbh = width // 16, height // 16
         self.cfg = jmhip.make_config(width, height, **kw)
+        self.sfx = "_u16" if self.cfg.bit_depth > 8 else ""          # High 10: 16-bit pictures
+        self.pdt = np.uint16 if self.cfg.bit_depth > 8 else np.uint8
         c = ctypes.c_void_p()
         st = self.L.jmo_create(ctypes.byref(self.cfg), ctypes.byref(c))
         if st:
@@ -93,23 +98,26 @@ class OracleEncoder:
             pass
 
     def set_reference(self, y, u, v):
-        assert self.L.jmo_set_reference(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2) == 0
+        y, u, v = (np.ascontiguousarray(a, self.pdt) for a in (y, u, v))
+        assert getattr(self.L, "jmo_set_reference" + self.sfx)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2) == 0
 
     def load_current(self, y, u, v):
         assert self.L.jmo_load_current(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2) == 0
 
     def encode(self, y, u, v, slice_type, qp, chroma_qp_offset=0):
         fp = jmhip.frame_params(slice_type, qp, chroma_qp_offset)
-        st = self.L.jmo_encode_frame(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2, ctypes.byref(fp))
+        y, u, v = (np.ascontiguousarray(a, self.pdt) for a in (y, u, v))
+        st = getattr(self.L, "jmo_encode_frame" + self.sfx)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2,
+                                                           ctypes.byref(fp))
         assert st == 0, st
         n = self.mbw * self.mbh
         p = self.L.jmo_mb_result(self.ctx, 0)
         buf = (ctypes.c_char * (n * jmhip.MB_RESULT_DTYPE.itemsize)).from_address(p)
         res = np.frombuffer(bytes(buf), dtype=jmhip.MB_RESULT_DTYPE).copy()
-        ry = np.empty((self.h, self.w), np.uint8)
-        ru = np.empty((self.h // 2, self.w // 2), np.uint8)
+        ry = np.empty((self.h, self.w), self.pdt)
+        ru = np.empty((self.h // 2, self.w // 2), self.pdt)
         rv = np.empty_like(ru)
-        assert self.L.jmo_read_recon(self.ctx, _ptr(ry), _ptr(ru), _ptr(rv), self.w, self.w // 2) == 0
+        assert getattr(self.L, "jmo_read_recon" + self.sfx)(self.ctx, _ptr(ry), _ptr(ru), _ptr(rv), self.w, self.w // 2) == 0
         return res, (ry, ru, rv)
 
     def read_qpel(self):

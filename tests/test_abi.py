@@ -19,7 +19,7 @@ def test_library_exports_every_declared_symbol():
     ensure_built()
     lib = ctypes.CDLL(LIBJMHIP)
     names = declared()
-    assert len(names) == 31
+    assert len(names) == 37
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(jmhip.EXPORTED)
@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_strerror():
     lib = jmhip.load()
-    assert lib.jmh_abi_version() == jmhip.JMH_ABI_VERSION == 10
+    assert lib.jmh_abi_version() == jmhip.JMH_ABI_VERSION == 11
     for code, text in jmhip.STATUS.items():
         assert lib.jmh_strerror(code).decode() == text
 
