@@ -60,19 +60,22 @@ static __constant__ uint16_t c_i4tab[9][16] = {
     {0x0085, 0x00C9, 0x010D, 0x0151, 0x0C86, 0x10CA, 0x150E, 0x1952, 0x00C9, 0x010D, 0x0151, 0x0195, 0x10CA, 0x150E, 0x1952, 0x1D96},
     {0x02A5, 0x2EA6, 0x02E9, 0x32EA, 0x02E9, 0x32EA, 0x032D, 0x332E, 0x032D, 0x332E, 0x3332, 0x3332, 0x3332, 0x3332, 0x3332, 0x3332}};
 
-// intra neighbourhood of an MB in LDS (unfiltered reconstruction of the current picture)
+// intra neighbourhood of an MB in LDS (unfiltered reconstruction of the current picture);
+// pel = uint8_t (bit depth 8) or uint16_t (High 10, k_mb_intra only)
+template <class pel>
 struct IntraNb {
-    uint8_t orgc[2][64];
-    uint8_t rtop[24];                         // luma row y = -1, x = -1..19 -> [x + 1]
-    uint8_t rleft[16];
-    uint8_t ctop[2][12];                      // chroma rows y = -1, x = -1..7 -> [x + 1]
-    uint8_t cleft[2][8];
+    pel orgc[2][64];
+    pel rtop[24];                             // luma row y = -1, x = -1..19 -> [x + 1]
+    pel rleft[16];
+    pel ctop[2][12];                          // chroma rows y = -1, x = -1..7 -> [x + 1]
+    pel cleft[2][8];
 };
+template <class pel>
 struct IntraS {
-    uint8_t org[256];
-    uint8_t rec[256];
+    alignas(4) pel org[256];
+    alignas(4) pel rec[256];
     Border bd;
-    IntraNb nb;
+    IntraNb<pel> nb;
     int i4P[2][16];
     int8_t ipred_cur[16];
     int part[2][4];                           // per I4 wave: cost, cbp, blk mask
@@ -80,7 +83,7 @@ struct IntraS {
 struct MeS {
     uint8_t org[256];
     Border bd;
-    IntraNb nb;
+    IntraNb<uint8_t> nb;
     int16_t all_mv[8][16][2];
     int motion_cost[8][4];
     unsigned red[NTA / 64][MAXNS];            // per wave, per search of the stage: argmin keys
@@ -93,11 +96,11 @@ struct MeS {
     } hs;                                     //   [k][thread] (16x16 / 16x8 / 8x16 searches)
     unsigned long long *pst;                  // debug: per-stage stamps (thread 0), null when off
     int pn;
-    IntraS in;                                // the MB's intra decisions, run by waves 6 and 7
+    IntraS<uint8_t> in;                       // the MB's intra decisions, run by waves 6 and 7
 };
 union AnalyseS {
     MeS me;
-    IntraS in[4];
+    IntraS<uint8_t> in[4];
 };
 
 __device__ __forceinline__ void sstamp(MeS &s, int wave) {
@@ -105,29 +108,32 @@ __device__ __forceinline__ void sstamp(MeS &s, int wave) {
 }
 
 // prefetch of the intra neighbourhood by threads t in [0, 96)
-__device__ __forceinline__ void load_intra_nb(const DevParams &d, IntraNb &nb, int t, int mbx, int mby) {
+template <class pel>
+__device__ __forceinline__ void load_intra_nb(const DevParams &d, IntraNb<pel> &nb, int t, int mbx, int mby) {
+    const pel *recY = spl<pel>(d.recY), *recU = spl<pel>(d.recU), *recV = spl<pel>(d.recV);
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, Wc = d.Wc;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     if (t < 21) {                                  // luma row y = -1, x = -1..19
         const int x = t - 1;
         const bool av = x < 0 ? avTL : x < 16 ? avT : avTR;
-        nb.rtop[x + 1] = av ? d.recY[(pix_y - 1) * W + pix_x + x] : 0;
+        nb.rtop[x + 1] = av ? recY[(pix_y - 1) * W + pix_x + x] : 0;
     } else if (t < 37) {
         const int y = t - 21;
-        nb.rleft[y] = avL ? d.recY[(pix_y + y) * W + pix_x - 1] : 0;
+        nb.rleft[y] = avL ? recY[(pix_y + y) * W + pix_x - 1] : 0;
     } else if (t < 55) {                           // chroma rows y = -1, x = -1..7
         const int i = t - 37, uv = i / 9, x = i - 9 * uv - 1;
         const bool av = x < 0 ? avTL : avT;
-        nb.ctop[uv][x + 1] = av ? (uv ? d.recV : d.recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
+        nb.ctop[uv][x + 1] = av ? (uv ? recV : recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
     } else if (t < 71) {
         const int i = t - 55, uv = i >> 3, y = i & 7;
-        nb.cleft[uv][y] = avL ? (uv ? d.recV : d.recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
+        nb.cleft[uv][y] = avL ? (uv ? recV : recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
     }
 }
-__device__ __forceinline__ void load_orgc(const DevParams &d, IntraNb &nb, int t, int mbx, int mby) {   // t in [0, 128)
+template <class pel>
+__device__ __forceinline__ void load_orgc(const DevParams &d, IntraNb<pel> &nb, int t, int mbx, int mby) {   // t in [0, 128)
     const int uv = t >> 6, k = t & 63;
-    nb.orgc[uv][k] = (uv ? d.orgV : d.orgU)[((8 * mby) + (k >> 3)) * d.Wc + 8 * mbx + (k & 7)];
+    nb.orgc[uv][k] = spl<pel>(uv ? d.orgV : d.orgU)[((8 * mby) + (k >> 3)) * d.Wc + 8 * mbx + (k & 7)];
 }
 
 // ======================================================================================
@@ -660,14 +666,15 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
 //  intra decisions
 // ======================================================================================
 // intrapred_luma_16x16 + find_sad_16x16 on one wave: 4 modes x 16 blocks = 64 lanes
-__device__ __forceinline__ void i16_decision(const DevParams &d, const uint8_t *org, const IntraNb &nb, MbScratch *scr, int lane, bool avL, bool avT,
+template <class pel>
+__device__ __forceinline__ void i16_decision(const DevParams &d, const pel *org, const IntraNb<pel> &nb, MbScratch *scr, int lane, bool avL, bool avT,
                                              bool avTL) {
     const int m = lane >> 4, b = lane & 15, ox = (b & 3) * 4, oy = (b >> 2) * 4;
-    const uint8_t *T = nb.rtop + 1, *L = nb.rleft;
-    const I16Par par = i16_params(T, L, avT, avL);
+    const pel *T = nb.rtop + 1, *L = nb.rleft;
+    const I16Par par = i16_params(T, L, avT, avL, (d.maxv + 1) >> 1);
     int mm[16], t[16];
     for (int yy = 0; yy < 4; yy++)
-        for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy);
+        for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy, d.maxv);
     for (int yy = 0; yy < 4; yy++) {
         int *r = mm + 4 * yy;
         int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
@@ -692,15 +699,16 @@ __device__ __forceinline__ void i16_decision(const DevParams &d, const uint8_t *
 }
 
 // IntraChromaPrediction8x8 mode decision on one wave: 4 modes x 2 components x 4 blocks
-__device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraNb &nb, MbScratch *scr, int lane, bool avL, bool avT, bool avTL) {
+template <class pel>
+__device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraNb<pel> &nb, MbScratch *scr, int lane, bool avL, bool avT, bool avTL) {
     int sat = 0;
     if (lane < 32) {
         const int m = lane >> 3, uv = (lane >> 2) & 1, b = lane & 3, xo = (b & 1) * 4, yo = (b >> 1) * 4;
-        const uint8_t *T = nb.ctop[uv] + 1, *L = nb.cleft[uv];
+        const pel *T = nb.ctop[uv] + 1, *L = nb.cleft[uv];
         int df[16];
         for (int y = 0; y < 4; y++)
             for (int x = 0; x < 4; x++)
-                df[4 * y + x] = nb.orgc[uv][(yo + y) * 8 + xo + x] - chroma_pred_px(T, L, nb.ctop[uv][0], avT, avL, m, xo + x, yo + y);
+                df[4 * y + x] = nb.orgc[uv][(yo + y) * 8 + xo + x] - chroma_pred_px(T, L, nb.ctop[uv][0], avT, avL, m, xo + x, yo + y, d.maxv);
         sat = satd4x4(df, d.use_hadamard);
     }
     const bool cav[4] = {true, avL, avT, avT && avL && avTL};
@@ -718,7 +726,7 @@ __device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraN
 // ======================================================================================
 //  motion search of one P macroblock (all 41 searches)
 // ======================================================================================
-__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int mbx, int mby);
+__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int k, int w, int mbx, int mby);
 
 __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int mby) {
     const int tid = threadIdx.x;
@@ -907,19 +915,21 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
 // ======================================================================================
 //  role 0: Intra4x4 (Mode_Decision_for_Intra4x4Macroblock) in 10 diagonal steps
 // ======================================================================================
-__device__ __forceinline__ int lpix(const IntraS &s, int x, int y) {
+template <class pel>
+__device__ __forceinline__ int lpix(const IntraS<pel> &s, int x, int y) {
     if (y < 0) return s.nb.rtop[x + 1];
     if (x < 0) return s.nb.rleft[y];
     return s.rec[16 * y + x];
 }
 
 // one 4x4 block on one wave: 9 modes x 16 pixels in 3 passes, DPP SATD, then dct_luma on
-// lanes 0..15 of the chosen prediction
-__device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratch *scr, int w, int bx4, int by4, const int (&tab)[3],
+// lanes 0..15 of the chosen prediction (at QP'Y = QPY + QpBdOffsetY)
+template <class pel>
+__device__ __forceinline__ void i4_block(const DevParams &d, IntraS<pel> &s, MbScratch *scr, int w, int bx4, int by4, const int (&tab)[3],
                                          bool avL, bool avT, bool avTL, bool avTR, int qpk, int (&acc)[3]) {
     const int lane = threadIdx.x & 63, l = lane & 15, g = lane >> 4;
     const int bx = 4 * bx4, by = 4 * by4, blk = 4 * by4 + bx4;
-    const int lambda = d.lambda_mode, qp = d.qp, had = d.use_hadamard;
+    const int lambda = d.lambda_mode, qp = d.qp + d.qpbd, had = d.use_hadamard;
     const bool up = by > 0 || avT, left = bx > 0 || avL;
     const bool ul = (bx > 0 && by > 0) || (bx == 0 && by > 0 && avL) || (bx > 0 && by == 0 && avT) || (bx == 0 && by == 0 && avTL);
     bool ur = by == 0 ? (bx + 4 <= 15 ? avT : avTR) : (bx + 4 <= 15);
@@ -939,7 +949,7 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratc
     wave_lds_sync();
     const int org = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];
     const int st = P[1] + P[2] + P[3] + P[4], sl = P[9] + P[10] + P[11] + P[12];
-    const int dc = (up && left) ? (st + sl + 4) >> 3 : left ? (sl + 2) >> 2 : up ? (st + 2) >> 2 : 128;
+    const int dc = (up && left) ? (st + sl + 4) >> 3 : left ? (sl + 2) >> 2 : up ? (st + 2) >> 2 : (d.maxv + 1) >> 1;
     int pv[3], cst[3];
 #pragma unroll
     for (int it = 0; it < 3; it++) {
@@ -969,7 +979,7 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratc
         int lev, dq, cc;
         nz = lane_quant(c, l, qp, qpk, false, lev, dq, cc);
         scr->i4lev[blk][l] = (int16_t)lev;
-        s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (uint8_t)lane_inv4x4(dq, l, pp);
+        s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (pel)lane_inv4x4(dq, l, pp, d.maxv);
         if (l == 0) s.ipred_cur[blk] = (int8_t)best;
     }
     nz = __builtin_amdgcn_readlane(nz, 0);
@@ -979,7 +989,8 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS &s, MbScratc
 
 // one MB on 128 threads (tid = 0..127, waves 0 and 1 of the group); every thread of the
 // workgroup reaches the same barriers (act: the group has an MB)
-__device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mbx, int mby, int tid, bool act, bool i4) {
+template <class pel>
+__device__ __forceinline__ void intra_role(const DevParams &d, IntraS<pel> &s, int mbx, int mby, int tid, bool act, bool i4) {
     const int wave = tid >> 6, lane = tid & 63;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
     const MbAvail mav = mb_avail(d, mbx, mby);
@@ -987,14 +998,15 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
     const bool prof = act && prof_mb_here(d, mbx, mby);
     PSTAMP(12);
     if (act) {
-        s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-        s.org[tid + 128] = d.orgY[(pix_y + 8 + (tid >> 4)) * W + pix_x + (tid & 15)];
+        const pel *orgY = spl<pel>(d.orgY);
+        s.org[tid] = orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+        s.org[tid + 128] = orgY[(pix_y + 8 + (tid >> 4)) * W + pix_x + (tid & 15)];
         load_orgc(d, s.nb, tid, mbx, mby);
         if (tid < 10) load_border(d, s.bd, tid, mbx, mby);
         else if (tid >= 16 && tid < 16 + 71) load_intra_nb(d, s.nb, tid - 16, mbx, mby);
     }
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
-    const int q_bits = 15 + d.qp / 6;
+    const int q_bits = 15 + (d.qp + d.qpbd) / 6;
     const int qpk = q_round(d.qsel, q_bits);
     int tab[3];
 #pragma unroll
@@ -1019,7 +1031,7 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
         scr->i4blk = s.part[0][2] | s.part[1][2];
     }
     if (i4 && tid < 16) scr->ipred[tid] = s.ipred_cur[tid];
-    if (i4 && tid < 64) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
+    if (i4 && tid < (int)sizeof(s.rec) / 4) reinterpret_cast<uint32_t *>(scr->i4rec)[tid] = reinterpret_cast<const uint32_t *>(s.rec)[tid];
     PSTAMP(13);
     // Intra16x16 (wave 0) and intra chroma mode (wave 1) decisions
     if (wave == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
@@ -1030,7 +1042,7 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS &s, int mb
 // the Intra4x4 decision inside a motion-search workgroup, on its waves 6 and 7 (w = wave - 6)
 // while the sub-pel waves of a stage work; steps are separated by the stage barriers.  Slot
 // k = 0..9: diagonal k of the 4x4 grid; slot 10: the totals and results.
-__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS &s, MbScratch *scr, int k, int w, int mbx, int mby) {
+__device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int k, int w, int mbx, int mby) {
     const int lane = threadIdx.x & 63;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
@@ -1102,10 +1114,11 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
 // workgroup) in ONE launch of small workgroups -- instead of k_mb_analyse's 512-thread, 78 KB LDS
 // workgroups followed by k_mb_intra8 -- so the two independent decisions share the CUs (eight
 // workgroups per CU): blocks [0, nRg) the intra roles (longest, first), then the Intra8x8 blocks.
+template <class pel>
 __global__ __launch_bounds__(NT, 8) void k_mb_intra(const TickArgs t) {
     __shared__ union {
-        IntraS in[2];
-        I8S i8;
+        IntraS<pel> in[2];
+        I8S<pel> i8;
     } s;
     const int tot = t.pre[t.npic], nR = (tot + 1) / 2, nRg = xcd_grid(nR), b = blockIdx.x;
     if (b < nRg) {
@@ -1120,14 +1133,15 @@ __global__ __launch_bounds__(NT, 8) void k_mb_intra(const TickArgs t) {
     } else {
         const int mi = xcd_block(b - nRg, tot);
         if (mi >= tot) return;
-        intra8_mb(t, s.i8, mi);
+        intra8_mb<pel>(t, s.i8, mi);
     }
 }
 
 hipError_t jmh_launch_intra(const TickArgs &t, hipStream_t st) {
     const int tot = t.pre[t.npic];
     const int nblocks = xcd_grid((tot + 1) / 2) + (t.t8 ? xcd_grid(tot) : 0);
-    hipLaunchKernelGGL(k_mb_intra, dim3(nblocks), dim3(NT), 0, st, t);
+    if (t.bd > 8) hipLaunchKernelGGL(k_mb_intra<uint16_t>, dim3(nblocks), dim3(NT), 0, st, t);
+    else hipLaunchKernelGGL(k_mb_intra<uint8_t>, dim3(nblocks), dim3(NT), 0, st, t);
     return hipGetLastError();
 }
 

@@ -44,6 +44,7 @@ __device__ __forceinline__ int scan_of(int k) { return (int)((SCAN_PACKED >> (4 
 
 __device__ __forceinline__ int iclip(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ int clip255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+__device__ __forceinline__ int clipmx(int v, int maxv) { return v < 0 ? 0 : (v > maxv ? maxv : v); }   // Clip1
 __device__ __forceinline__ int isign(int a, int b) { return b < 0 ? -abs(a) : abs(a); }
 __device__ __forceinline__ int mvbits(int v) { return v == 0 ? 1 : 2 * (31 - __clz(abs(v))) + 3; }
 __device__ __forceinline__ int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
@@ -385,18 +386,20 @@ __device__ __forceinline__ int i4_pred_px(const int *P, int up, int left, int m,
 #undef PL
 }
 
-// chroma DC prediction of one 4x4 chroma block (8.3.4.1-3)
-__device__ __forceinline__ int chroma_dc(const uint8_t *T, const uint8_t *L, int up, int left, int b) {
+// chroma DC prediction of one 4x4 chroma block (8.3.4.1-3); dcd = 1 << (BitDepthC - 1)
+template <class pel>
+__device__ __forceinline__ int chroma_dc(const pel *T, const pel *L, int up, int left, int b, int dcd) {
     int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     for (int i = 0; i < 4; i++) { s0 += T[i]; s1 += T[4 + i]; s2 += L[i]; s3 += L[4 + i]; }
-    if (b == 0) return (up && left) ? (s0 + s2 + 4) >> 3 : up ? (s0 + 2) >> 2 : left ? (s2 + 2) >> 2 : 128;
-    if (b == 1) return up ? (s1 + 2) >> 2 : left ? (s2 + 2) >> 2 : 128;
-    if (b == 2) return left ? (s3 + 2) >> 2 : up ? (s0 + 2) >> 2 : 128;
-    return (up && left) ? (s1 + s3 + 4) >> 3 : up ? (s1 + 2) >> 2 : left ? (s3 + 2) >> 2 : 128;
+    if (b == 0) return (up && left) ? (s0 + s2 + 4) >> 3 : up ? (s0 + 2) >> 2 : left ? (s2 + 2) >> 2 : dcd;
+    if (b == 1) return up ? (s1 + 2) >> 2 : left ? (s2 + 2) >> 2 : dcd;
+    if (b == 2) return left ? (s3 + 2) >> 2 : up ? (s0 + 2) >> 2 : dcd;
+    return (up && left) ? (s1 + s3 + 4) >> 3 : up ? (s1 + 2) >> 2 : left ? (s3 + 2) >> 2 : dcd;
 }
-// chroma intra prediction (8.3.4) of mode m at pixel (x, y) of one component
-__device__ __forceinline__ int chroma_pred_px(const uint8_t *T, const uint8_t *L, int Pc, int up, int left, int m, int x, int y) {
-    if (m == 0) return chroma_dc(T, L, up, left, (y >> 2) * 2 + (x >> 2));
+// chroma intra prediction (8.3.4) of mode m at pixel (x, y) of one component (Clip1C to maxv)
+template <class pel>
+__device__ __forceinline__ int chroma_pred_px(const pel *T, const pel *L, int Pc, int up, int left, int m, int x, int y, int maxv = 255) {
+    if (m == 0) return chroma_dc(T, L, up, left, (y >> 2) * 2 + (x >> 2), (maxv + 1) >> 1);
     if (m == 1) return L[y];
     if (m == 2) return T[x];
     int ih = 0, iv = 0;
@@ -405,12 +408,13 @@ __device__ __forceinline__ int chroma_pred_px(const uint8_t *T, const uint8_t *L
         iv += i * (L[3 + i] - (3 - i >= 0 ? L[3 - i] : Pc));
     }
     int ib = (34 * ih + 32) >> 6, ic = (34 * iv + 32) >> 6, iaa = 16 * (L[7] + T[7]);
-    return clip255((iaa + (x - 3) * ib + (y - 3) * ic + 16) >> 5);
+    return clipmx((iaa + (x - 3) * ib + (y - 3) * ic + 16) >> 5, maxv);
 }
 // Intra16x16 prediction (8.3.3): mode-independent parameters, then per-pixel samples.
 // T = row y = -1 (T[-1] is the corner p[-1,-1]), L = column x = -1.
 struct I16Par { int dcv, ib, ic, iaa; };
-__device__ __forceinline__ I16Par i16_params(const uint8_t *T, const uint8_t *L, int up, int left) {
+template <class pel>
+__device__ __forceinline__ I16Par i16_params(const pel *T, const pel *L, int up, int left, int dcd = 128) {
     int st = 0, sl = 0, ih = 0, iv = 0;
     for (int i = 0; i < 16; i++) { st += T[i]; sl += L[i]; }
     for (int i = 1; i <= 8; i++) {
@@ -418,15 +422,16 @@ __device__ __forceinline__ I16Par i16_params(const uint8_t *T, const uint8_t *L,
         iv += i * (L[7 + i] - (7 - i >= 0 ? L[7 - i] : T[-1]));
     }
     I16Par p;
-    p.dcv = (up && left) ? (st + sl + 16) >> 5 : up ? (st + 8) >> 4 : left ? (sl + 8) >> 4 : 128;
+    p.dcv = (up && left) ? (st + sl + 16) >> 5 : up ? (st + 8) >> 4 : left ? (sl + 8) >> 4 : dcd;
     p.ib = (5 * ih + 32) >> 6; p.ic = (5 * iv + 32) >> 6; p.iaa = 16 * (L[15] + T[15]);
     return p;
 }
-__device__ __forceinline__ int i16_pred(const I16Par &p, const uint8_t *T, const uint8_t *L, int m, int x, int y) {
+template <class pel>
+__device__ __forceinline__ int i16_pred(const I16Par &p, const pel *T, const pel *L, int m, int x, int y, int maxv = 255) {
     if (m == 0) return T[x];
     if (m == 1) return L[y];
     if (m == 2) return p.dcv;
-    return clip255((p.iaa + (x - 7) * p.ib + (y - 7) * p.ic + 16) >> 5);
+    return clipmx((p.iaa + (x - 7) * p.ib + (y - 7) * p.ic + 16) >> 5, maxv);
 }
 
 // ======================================================================================

@@ -34,11 +34,11 @@ struct MbScratch {
     int32_t i16cost, i16mode, c_mode;
     int8_t ipred[16];
     int16_t i4lev[16][16];               // Intra4x4 levels in scan order
-    uint8_t i4rec[256];                  // Intra4x4 reconstruction of the MB
+    alignas(4) uint8_t i4rec[512];       // Intra4x4 reconstruction of the MB (256 samples of pel)
     // Intra8x8 decision (k_mb_intra8, Transform8x8Mode only)
     int32_t i8cost, i8cbp, i8modes;      // i8modes: 4 bits per 8x8 block
     int16_t i8lev[16][16];               // levels in the CAVLC interleave (jmh_mb_result.luma)
-    uint8_t i8rec[256];
+    alignas(4) uint8_t i8rec[512];
 };
 
 struct DevParams {
@@ -52,7 +52,7 @@ struct DevParams {
     int slice_mbs;              // SliceMode 1: MBs per slice (the whole picture for one slice)
     int maxv, qpbd;             // (1 << bit depth) - 1 (Clip1), QpBdOffsetY = QpBdOffsetC = 6 (bit depth - 8)
     // plane pointers are byte addresses of uint8_t (bit depth 8) or uint16_t (9 / 10) samples:
-    // the kernels templated on the sample type cast them (PL<pel>)
+    // the kernels templated on the sample type cast them (spl<pel>)
     const uint8_t *orgY, *orgU, *orgV;
     const uint8_t *refY, *refU, *refV;
     uint8_t *recY, *recU, *recV;
@@ -167,5 +167,5 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
 }
 
 // sample-typed view of a DevParams plane pointer (bytes of uint8_t or uint16_t samples)
-template <class pel> __device__ __forceinline__ pel *PL(uint8_t *p) { return reinterpret_cast<pel *>(p); }
-template <class pel> __device__ __forceinline__ const pel *PL(const uint8_t *p) { return reinterpret_cast<const pel *>(p); }
+template <class pel> __device__ __forceinline__ pel *spl(uint8_t *p) { return reinterpret_cast<pel *>(p); }
+template <class pel> __device__ __forceinline__ const pel *spl(const uint8_t *p) { return reinterpret_cast<const pel *>(p); }

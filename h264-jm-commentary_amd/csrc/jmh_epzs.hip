@@ -23,6 +23,9 @@
 // lane in the full-pel SADs, per search (into a small neighbourhood plane) for the sub-pel planes.
 // Results land in MbScratch exactly like the other search kernels (the intra workgroups and
 // k_mb_final are shared).
+// High 10 (pel = uint16_t): the same kernel on 16-bit samples -- two samples per dword, v_sad_u16
+// for the SADs, the packed-int16 Hadamard on 16-bit differences (|d| <= 1023 keeps every stage in
+// range), int32 horizontal taps, and the EPZS thresholds times 1 << (BitDepthY - 8).
 #include "jmh_common.h"
 
 #define NTE 64                                // one wave per macroblock
@@ -39,10 +42,13 @@
 #define GNS 36                                //   y in [-GNY, 4 h4 + 2 + GNY), stride GNS
 #define GNR (18 + 2 * GNY)
 
+template <class pel> struct EpzTap { typedef int16_t type; };   // unclipped 6-tap sums: |.| <= 42 * maxv
+template <> struct EpzTap<uint16_t> { typedef int32_t type; };
+template <class pel>
 struct EpzS {
-    uint8_t g[EW_MAX * EST];                  // the window
-    uint8_t gn[GNR * GNS + 8];                // a search's integer-sample neighbourhood read from global
-    uint8_t org[256];
+    alignas(4) pel g[EW_MAX * EST];           // the window
+    alignas(4) pel gn[GNR * GNS + 8];         // a search's integer-sample neighbourhood read from global
+    alignas(8) pel org[256];
     Border bd;
     int16_t all_mv[8][16][2];
     int motion_cost[8][4];
@@ -50,13 +56,14 @@ struct EpzS {
     int8_t tref[6][6];                        //   MB origin at [1][1]; -1: none)
     int16_t mem[7][16][2];                    // spatial memory: the left MB's searches (types 1..7)
     int memok;
-    uint8_t hp[3][HPL];                       // b, h, j of the block's [-1, w] x [-1, h] at its MV
-    int16_t b1[HPR + 5][HPR];                 // unclipped horizontal taps, rows -3 .. h + 1
+    alignas(4) pel hp[3][HPL];                // b, h, j of the block's [-1, w] x [-1, h] at its MV
+    typename EpzTap<pel>::type b1[HPR + 5][HPR];   // unclipped horizontal taps, rows -3 .. h + 1
 };
 
 // neighbour view of a search of block type bt in 8x8 block b8 (as NbMe in jmh_analyse.hip)
+template <class S>
 struct NbEpz {
-    const EpzS &s;
+    const S &s;
     int bt, b8, best8x8;
     __device__ __forceinline__ bool operator()(int xN, int yN, int &ref, int &mx, int &my) const {
         if (yN > 15 || (xN > 15 && yN >= 0)) return false;
@@ -73,20 +80,22 @@ struct NbEpz {
     }
 };
 
-__device__ __forceinline__ uint32_t eld_u32(const uint8_t *p) {   // 4 bytes at any LDS address
+__device__ __forceinline__ uint32_t eld_u32(const void *p) {   // 4 bytes at any LDS address
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 
 // the LDS window: picture position of its sample (0, 0) and window position of the MB origin
+template <class pel>
 struct EWin {
-    const uint8_t *ref;
+    const pel *ref;
     int W, H;
     int wx0, wy0, mx, my;
 };
 // reference sample at picture position (x, y), UMV-clamped (8.4.2.2.1), from global memory
-__device__ __forceinline__ uint32_t gref(const EWin &w, int x, int y) {
+template <class pel>
+__device__ __forceinline__ uint32_t gref(const EWin<pel> &w, int x, int y) {
     return w.ref[iclip(0, w.H - 1, y) * w.W + iclip(0, w.W - 1, x)];
 }
 
@@ -138,7 +147,8 @@ __device__ __forceinline__ void set_mvp_nb(const NB &nb, int bx4, int bby4, int 
 // spatial A / B / C (or D) (nb: the MVP's neighbour reads), 5-28 window rings R/4, R/2, R,
 // 29-33 temporal (co-located, left, right, up, down), 34 spatial memory (left MB), 35-40 earlier
 // block types.  False if not valid or outside the window around the centre.
-__device__ __forceinline__ bool epzs_cand(const DevParams &d, const EpzS &s, int i, int bt, int bx4, int by4, const MvpNb &nb,
+template <class S>
+__device__ __forceinline__ bool epzs_cand(const DevParams &d, const S &s, int i, int bt, int bx4, int by4, const MvpNb &nb,
                                           int range, int mvx0, int mvy0, int &x, int &y) {
     const int w4 = 1 << lw4_of(bt), h4 = 1 << lh4_of(bt), k0 = by4 * 4 + bx4;
     auto rnd = [](int v) { return (v + 2) >> 2; };
@@ -188,13 +198,39 @@ __device__ __forceinline__ void epzs_pat(bool sd, int e, int &px, int &py) {
 }
 
 // SAD of the whole block (4 w4 x 4 h4 at 4x4 position bx4, by4) at full-pel displacement (x, y)
-// on this lane: per row w4 + 1 aligned dwords, v_alignbyte, v_sad_u8
-template <int LW4, int LH4>
-__device__ __forceinline__ unsigned lane_block_sad(const EpzS &s, const EWin &wn, int bx4, int by4, int x, int y) {
+// on this lane: per row w4 + 1 aligned dwords, v_alignbyte, v_sad_u8 (16-bit samples: 2 w4 + 1
+// dwords, v_sad_u16)
+template <int LW4, int LH4, class pel>
+__device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWin<pel> &wn, int bx4, int by4, int x, int y) {
     constexpr int W4 = 1 << LW4, H = 4 << LH4;
     const int gx = wn.mx + 4 * bx4 + x, gy = wn.my + 4 * by4 + y;
     const uint32_t *org = reinterpret_cast<const uint32_t *>(s.org + (4 * by4) * 16 + 4 * bx4);
     uint32_t sad = 0;
+    if constexpr (sizeof(pel) == 2) {
+        constexpr int ND = 2 * W4;            // dwords of a block row
+        if (gx >= 0 && gx + 4 * W4 + 4 <= EST && gy >= 0 && gy + H <= EW_MAX) {
+            const int a = gy * EST + gx;
+            const uint32_t sel = (uint32_t)(a & 1) * 2;
+            const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~1));
+#pragma unroll
+            for (int r = 0; r < H; r++) {
+                uint32_t w[ND + 1];
+#pragma unroll
+                for (int q = 0; q <= ND; q++) w[q] = base[r * (EST / 2) + q];
+#pragma unroll
+                for (int q = 0; q < ND; q++) sad = __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), org[r * 8 + q], sad);
+            }
+        } else {
+            const int px = wn.wx0 + gx, py = wn.wy0 + gy;
+#pragma unroll 1
+            for (int r = 0; r < H; r++) {
+#pragma unroll
+                for (int q = 0; q < ND; q++)
+                    sad = __builtin_amdgcn_sad_u16(gref(wn, px + 2 * q, py + r) | gref(wn, px + 2 * q + 1, py + r) << 16, org[r * 8 + q], sad);
+            }
+        }
+        return sad;
+    }
     if (gx >= 0 && gx + 4 * W4 + 4 <= EST && gy >= 0 && gy + H <= EW_MAX) {   // inside the window
         const int a = gy * EST + gx;
         const uint32_t sel = (uint32_t)(a & 3);
@@ -227,10 +263,12 @@ typedef short e16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ e16x2 e_s2(uint32_t v) { return __builtin_bit_cast(e16x2, v); }
 __device__ __forceinline__ uint32_t e_u32(e16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ e16x2 e_abs2(e16x2 v) { return __builtin_elementwise_max(v, (e16x2)(0) - v); }
+__device__ __forceinline__ int had_packed(const e16x2 (&r)[4][2]);
 
 // row pointer and stride of half-grid plane pl (0 G = the window, 1 b, 2 h, 3 j) at block-
 // relative integer position (rx, ry) (b / h / j sample [y][x] = position (x - 1, y - 1))
-__device__ __forceinline__ const uint8_t *hp_row(const EpzS &s, int pl, const uint8_t *gb, int gs, int rx, int ry, int &stride) {
+template <class pel>
+__device__ __forceinline__ const pel *hp_row(const EpzS<pel> &s, int pl, const pel *gb, int gs, int rx, int ry, int &stride) {
     if (pl == 0) { stride = gs; return gb + ry * gs + rx; }
     stride = HPS;
     return s.hp[pl - 1] + (ry + 1) * HPS + rx + 1;
@@ -240,13 +278,43 @@ __device__ __forceinline__ const uint8_t *hp_row(const EpzS &s, int pl, const ui
 // MV (window position gx0, gy0 of the block origin): block-relative sub-block origin (sx, sy);
 // rows as dwords from the phase's two half-grid planes, their rounding average per byte, packed
 // int16 Hadamard (as subblock_satd)
-__device__ __forceinline__ int hp_satd(const EpzS &s, const uint8_t *gb, int gs, int sx, int sy, int obase, int ox, int oy, int had) {
+template <class pel>
+__device__ __forceinline__ int hp_satd(const EpzS<pel> &s, const pel *gb, int gs, int sx, int sy, int obase, int ox, int oy, int had) {
     const int off = qoff((oy & 3) * 4 + (ox & 3));
     const int xa = (off >> 12) & 15, ya = (off >> 8) & 15, xb = (off >> 4) & 15, yb = off & 15;
     const int rx = sx + (ox >> 2), ry = sy + (oy >> 2);
     int sa, sb;
-    const uint8_t *pA = hp_row(s, (xa & 1) + 2 * (ya & 1), gb, gs, rx + (xa >> 1), ry + (ya >> 1), sa);
-    const uint8_t *pB = hp_row(s, (xb & 1) + 2 * (yb & 1), gb, gs, rx + (xb >> 1), ry + (yb >> 1), sb);
+    const pel *pA = hp_row(s, (xa & 1) + 2 * (ya & 1), gb, gs, rx + (xa >> 1), ry + (ya >> 1), sa);
+    const pel *pB = hp_row(s, (xb & 1) + 2 * (yb & 1), gb, gs, rx + (xb >> 1), ry + (yb >> 1), sb);
+    if constexpr (sizeof(pel) == 2) {
+        // 16-bit samples: a row is two dwords; per sample (a + b + 1) >> 1, then the same packed
+        // int16 Hadamard (differences |d| <= 1023: every stage stays within int16)
+        uint32_t O[4][2], P[4][2];
+#pragma unroll
+        for (int yy = 0; yy < 4; yy++)
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const uint32_t A = eld_u32(pA + yy * sa + 2 * k), B = eld_u32(pB + yy * sb + 2 * k);
+                P[yy][k] = (A | B) - (((A ^ B) >> 1) & 0x7FFF7FFFu);
+                O[yy][k] = *reinterpret_cast<const uint32_t *>(s.org + obase + 16 * yy + 2 * k);
+            }
+        if (!had) {
+            uint32_t sad = 0;
+#pragma unroll
+            for (int yy = 0; yy < 4; yy++) {
+                sad = __builtin_amdgcn_sad_u16(O[yy][0], P[yy][0], sad);
+                sad = __builtin_amdgcn_sad_u16(O[yy][1], P[yy][1], sad);
+            }
+            return (int)sad;
+        }
+        e16x2 r[4][2];
+#pragma unroll
+        for (int yy = 0; yy < 4; yy++) {
+            r[yy][0] = e_s2(O[yy][0]) - e_s2(P[yy][0]);
+            r[yy][1] = e_s2(O[yy][1]) - e_s2(P[yy][1]);
+        }
+        return had_packed(r);
+    }
     uint32_t O[4], P[4];
 #pragma unroll
     for (int yy = 0; yy < 4; yy++) {
@@ -266,6 +334,13 @@ __device__ __forceinline__ int hp_satd(const EpzS &s, const uint8_t *gb, int gs,
         r[yy][0] = e_s2(__builtin_amdgcn_perm(0u, O[yy], 0x0c010c00u)) - e_s2(__builtin_amdgcn_perm(0u, P[yy], 0x0c010c00u));
         r[yy][1] = e_s2(__builtin_amdgcn_perm(0u, O[yy], 0x0c030c02u)) - e_s2(__builtin_amdgcn_perm(0u, P[yy], 0x0c030c02u));
     }
+    return had_packed(r);
+}
+
+// SATD() of a 4x4 difference block held as packed int16 pairs r[row][0] = (d0, d1), r[row][1] =
+// (d2, d3): vertical then horizontal butterflies, sum |.| via |a + b| + |a - b| = 2 max(|a|, |b|)
+// (the >> 1 of SATD folded in)
+__device__ __forceinline__ int had_packed(const e16x2 (&r)[4][2]) {
     e16x2 m[4][2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -287,8 +362,8 @@ __device__ __forceinline__ int hp_satd(const EpzS &s, const uint8_t *gb, int gs,
 }
 
 // BlockMotionSearch [J] of one block on the wave: EPZS full pel + SubPelBlockMotionSearch
-template <int BT>
-__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, const EWin &wn, int bx4, int by4, int mc, int b8, int best8x8, bool prof) {
+template <int BT, class pel>
+__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, const EWin<pel> &wn, int bx4, int by4, int mc, int b8, int best8x8, bool prof) {
     // debug (JMH_PHASE_PROF): steps of the MB's first 4x4 search into prof[41..46]
     const bool sp = prof && BT == 7 && bx4 == 0 && by4 == 0;
 #define SSTAMP(k) do { if (sp) d.prof[41 + (k)] = wall_clock64(); } while (0)
@@ -301,11 +376,11 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, const EW
     const int range = d.restrict_sr == 0 ? d.sr / min(2, BT) : d.sr;
     int pmx, pmy;
     MvpNb nb;
-    set_mvp_nb(NbEpz{s, BT, b8, best8x8}, bx4, by4, 4 * W4, 4 * H4, pmx, pmy, nb);
+    set_mvp_nb(NbEpz<EpzS<pel>>{s, BT, b8, best8x8}, bx4, by4, 4 * W4, 4 * H4, pmx, pmy, nb);
     pmx = __builtin_amdgcn_readfirstlane(pmx);
     pmy = __builtin_amdgcn_readfirstlane(pmy);
     const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
-    const int med = 16 * W4 * H4;
+    const int med = 16 * W4 * H4 * ((d.maxv + 1) >> 8);   // medthres x pel_error_me (High 10)
     SSTAMP(1);
     // ---- full pel: predictor `lane`, then pattern rounds
     int cx, cy;
@@ -378,14 +453,14 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, const EW
     const int gx0 = wn.mx + 4 * bx4 + fmx, gy0 = wn.my + 4 * by4 + fmy;   // window position of (0, 0)
     // integer samples around the block at its full-pel MV: the window, or when the reach
     // [-GNX, PW + GNX) x [-GNY, PH + GNY) leaves it, the neighbourhood plane read from global
-    const uint8_t *gb;
+    const pel *gb;
     int gs;
     if (gx0 - GNX >= 0 && gx0 + PW + GNX <= EST && gy0 - GNY >= 0 && gy0 + PH + GNY <= EW_MAX) {   // wave-uniform
         gb = s.g + gy0 * EST + gx0; gs = EST;
     } else {
         for (int i = lane; i < (PH + 2 * GNY) * GNS; i += NTE) {
             const int y = i / GNS, x = i - y * GNS;
-            s.gn[i] = (uint8_t)gref(wn, wn.wx0 + gx0 + x - GNX, wn.wy0 + gy0 + y - GNY);
+            s.gn[i] = (pel)gref(wn, wn.wx0 + gx0 + x - GNX, wn.wy0 + gy0 + y - GNY);
         }
         wave_lds_sync();
         gb = s.gn + GNY * GNS + GNX; gs = GNS;
@@ -394,18 +469,18 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, const EW
     for (int i = lane; i < PW * (PH + 5); i += NTE) {
         const int rr = i / PW, x = i - rr * PW, gx = x - 1, gy = rr - 3;
         const int h1 = tap6(G(gx - 2, gy), G(gx - 1, gy), G(gx, gy), G(gx + 1, gy), G(gx + 2, gy), G(gx + 3, gy));
-        s.b1[rr][x] = (int16_t)h1;
+        s.b1[rr][x] = (typename EpzTap<pel>::type)h1;
         if (rr >= 2 && rr < PH + 2) {
-            s.hp[0][(rr - 2) * HPS + x] = (uint8_t)clip255((h1 + 16) >> 5);
+            s.hp[0][(rr - 2) * HPS + x] = (pel)clipmx((h1 + 16) >> 5, d.maxv);
             s.hp[1][(rr - 2) * HPS + x] =
-                (uint8_t)clip255((tap6(G(gx, gy - 2), G(gx, gy - 1), G(gx, gy), G(gx, gy + 1), G(gx, gy + 2), G(gx, gy + 3)) + 16) >> 5);
+                (pel)clipmx((tap6(G(gx, gy - 2), G(gx, gy - 1), G(gx, gy), G(gx, gy + 1), G(gx, gy + 2), G(gx, gy + 3)) + 16) >> 5, d.maxv);
         }
     }
     wave_lds_sync();
     for (int i = lane; i < PW * PH; i += NTE) {
         const int y = i / PW, x = i - y * PW;
         s.hp[2][y * HPS + x] =
-            (uint8_t)clip255((tap6(s.b1[y][x], s.b1[y + 1][x], s.b1[y + 2][x], s.b1[y + 3][x], s.b1[y + 4][x], s.b1[y + 5][x]) + 512) >> 10);
+            (pel)clipmx((tap6(s.b1[y][x], s.b1[y + 1][x], s.b1[y + 2][x], s.b1[y + 3][x], s.b1[y + 4][x], s.b1[y + 5][x]) + 512) >> 10, d.maxv);
     }
     wave_lds_sync();
     SSTAMP(4);
@@ -508,8 +583,9 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS &s, const EW
 #undef SSTAMP
 }
 
+template <class pel>
 __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
-    __shared__ EpzS s;
+    __shared__ EpzS<pel> s;
     const int b = xcd_block(blockIdx.x, t.pre[t.nP]), lane = threadIdx.x;   // XCD-aware (jmh_device.h)
     if (b >= t.pre[t.nP]) return;
     const int e = tick_entry(t, b);
@@ -525,8 +601,12 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     // ---- inputs: the MB (one dword per lane), border cells, the temporal neighbourhood, the left
     //      MB's searches, the window (dword per task: two aligned global dwords + v_alignbyte
     //      inside the picture, clamped bytes at its edges: the spec's UMV access)
-    reinterpret_cast<uint32_t *>(s.org)[lane] =
-        *reinterpret_cast<const uint32_t *>(d.orgY + (pix_y + (lane >> 2)) * W + pix_x + 4 * (lane & 3));
+    const pel *orgY = spl<pel>(d.orgY), *refY = spl<pel>(d.refY);
+    if constexpr (sizeof(pel) == 1)
+        reinterpret_cast<uint32_t *>(s.org)[lane] = *reinterpret_cast<const uint32_t *>(orgY + (pix_y + (lane >> 2)) * W + pix_x + 4 * (lane & 3));
+    else
+        for (int i = lane; i < 128; i += NTE)
+            reinterpret_cast<uint32_t *>(s.org)[i] = *reinterpret_cast<const uint32_t *>(orgY + (pix_y + (i >> 3)) * W + pix_x + 2 * (i & 7));
     if (lane < 10) load_border(d, s.bd, lane, mbx, mby);
     if (lane < 32) s.motion_cost[lane >> 2][lane & 3] = 0;
     if (lane < 36) {
@@ -553,8 +633,44 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
         wcx = __builtin_amdgcn_readfirstlane(iclip(-sr, sr, pcx / 4) & ~3);
         wcy = __builtin_amdgcn_readfirstlane(iclip(-sr, sr, pcy / 4));
     }
-    const EWin wn{d.refY, W, d.H, pix_x + wcx - off, pix_y + wcy - off, off - wcx, off - wcy};
-    {
+    const EWin<pel> wn{refY, W, d.H, pix_x + wcx - off, pix_y + wcy - off, off - wcx, off - wcy};
+    if constexpr (sizeof(pel) == 2) {
+        // 16-bit samples: two per dword; with off % 4 == 0 a dword is aligned in the picture and
+        // wholly inside or outside it (as for bytes), else per-sample clamped reads
+        constexpr int ND2 = EST / 2, NB = 16;
+        const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND2;
+        if ((off & 3) == 0) {
+            for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
+                uint32_t v[NB];
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const int task = t0 + u * NTE + lane, y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
+                    const pel *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
+                    const int xs = x0 < 0 ? 0 : x0 >= W ? W - 2 : x0;
+                    v[u] = task < ntask ? *reinterpret_cast<const uint32_t *>(row + xs) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const int task = t0 + u * NTE + lane, y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
+                    if (task >= ntask) continue;
+                    uint32_t w = v[u];
+                    if (x0 < 0) w = (w & 0xFFFFu) * 0x10001u;
+                    else if (x0 >= W) w = (w >> 16) * 0x10001u;
+                    if (2 * j >= wdim) w = 0;
+                    *reinterpret_cast<uint32_t *>(s.g + y * EST + 2 * j) = w;
+                }
+            }
+        } else {
+            for (int task = lane; task < ntask; task += NTE) {
+                const int y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
+                const pel *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
+                uint32_t v = 0;
+                for (int q = 0; q < 2; q++)
+                    if (2 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (16 * q);
+                *reinterpret_cast<uint32_t *>(s.g + y * EST + 2 * j) = v;
+            }
+        }
+    } else {
         // with off % 4 == 0 the window's dwords are aligned in the picture (pix_x % 16 == 0, wcx %
         // 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an outside
         // dword is the replicated edge sample.  Two batches of 32 loads per lane in flight.
@@ -566,7 +682,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
 #pragma unroll
                 for (int u = 0; u < NB; u++) {
                     const int task = t0 + u * NTE + lane, y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
-                    const uint8_t *row = d.refY + iclip(0, d.H - 1, WY0 + y) * W;
+                    const uint8_t *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
                     const int xs = x0 < 0 ? 0 : x0 >= W ? W - 4 : x0;
                     v[u] = task < ntask ? *reinterpret_cast<const uint32_t *>(row + xs) : 0u;
                 }
@@ -584,7 +700,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
         } else {   // odd SearchRange: two aligned global dwords + v_alignbyte, clamped bytes at the edges
             for (int task = lane; task < ntask; task += NTE) {
                 const int y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
-                const uint8_t *row = d.refY + iclip(0, d.H - 1, WY0 + y) * W;
+                const uint8_t *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
                 uint32_t v;
                 if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
                     const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
@@ -659,6 +775,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
 
 hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st) {
     if (t.pre[t.nP] == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mb_epzs, dim3(xcd_grid(t.pre[t.nP])), dim3(NTE), 0, st, t);
+    if (t.bd > 8) hipLaunchKernelGGL(k_mb_epzs<uint16_t>, dim3(xcd_grid(t.pre[t.nP])), dim3(NTE), 0, st, t);
+    else hipLaunchKernelGGL(k_mb_epzs<uint8_t>, dim3(xcd_grid(t.pre[t.nP])), dim3(NTE), 0, st, t);
     return hipGetLastError();
 }

@@ -7,16 +7,18 @@
 #include "jmh_common.h"
 #include <cstdlib>
 
+// pel: uint8_t (bit depth 8) or uint16_t (High 10) samples
+template <class pel>
 struct FinS {
-    uint8_t org[256];
-    uint8_t orgc[2][64];
-    uint8_t rec[256];
-    uint8_t pred[256];                   // inter prediction (TransformDecision / 8x8 path)
+    pel org[256];
+    pel orgc[2][64];
+    pel rec[256];
+    pel pred[256];                       // inter prediction (TransformDecision / 8x8 path)
     int tdc[4][2];                       // per 8x8: sum of 4x4 SATDs, 8x8 SATD
-    uint8_t rtop[24];                    // luma row y = -1, x = -1..19 -> [x + 1]
-    uint8_t rleft[16];
-    uint8_t ctop[2][12];                 // chroma rows y = -1, x = -1..7 -> [x + 1]
-    uint8_t cleft[2][8];
+    pel rtop[24];                        // luma row y = -1, x = -1..19 -> [x + 1]
+    pel rleft[16];
+    pel ctop[2][12];                     // chroma rows y = -1, x = -1..7 -> [x + 1]
+    pel cleft[2][8];
     int16_t fmv[16][2];
     int16_t lev[16][16];
     int bcost[16];
@@ -32,10 +34,10 @@ struct FinS {
     int cbnz[2][4];
     int creset[2];
     int cdcnz[2];
-    uint8_t cfin[2][64];
+    pel cfin[2][64];
     // deblocking: the MB with 4 rows / columns of its (already filtered) top / left neighbours
-    uint8_t dy[20][20];                  // luma, rows / columns -4..15 -> [r + 4][c + 4]
-    uint8_t dc2[2][12][12];              // chroma, rows / columns -4..7
+    pel dy[20][20];                      // luma, rows / columns -4..15 -> [r + 4][c + 4]
+    pel dc2[2][12][12];                  // chroma, rows / columns -4..7
     int8_t bs[2][4][4];                  // boundary strength [dir][edge][segment]
 };
 
@@ -54,19 +56,21 @@ static __constant__ uint8_t c_tc0[52][3] = {
     {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11},
     {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
 
-// one line of samples across an edge (8.7.2.3 / 8.7.2.4): q0 at q[0], p_k at q[-(k+1)*step]
-__device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int alpha, int beta, int tc0, bool chroma) {
+// one line of samples across an edge (8.7.2.3 / 8.7.2.4): q0 at q[0], p_k at q[-(k+1)*step];
+// alpha / beta / tc0 already scaled by 1 << (BitDepth - 8), Clip1 to maxv
+template <class pel>
+__device__ __forceinline__ void filter_line(pel *q, int step, int bS, int alpha, int beta, int tc0, bool chroma, int maxv) {
     const int p0 = q[-step], p1 = q[-2 * step], q0 = q[0], q1 = q[step];
     if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
     if (chroma) {
         if (bS < 4) {
             const int tc = tc0 + 1;
             const int dl = iclip(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
-            q[-step] = (uint8_t)clip255(p0 + dl);
-            q[0] = (uint8_t)clip255(q0 - dl);
+            q[-step] = (pel)clipmx(p0 + dl, maxv);
+            q[0] = (pel)clipmx(q0 - dl, maxv);
         } else {
-            q[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
-            q[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+            q[-step] = (pel)((2 * p1 + p0 + q1 + 2) >> 2);
+            q[0] = (pel)((2 * q1 + q0 + p1 + 2) >> 2);
         }
         return;
     }
@@ -75,32 +79,32 @@ __device__ __forceinline__ void filter_line(uint8_t *q, int step, int bS, int al
     if (bS < 4) {
         const int tc = tc0 + (ap < beta) + (aq < beta);
         const int dl = iclip(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
-        q[-step] = (uint8_t)clip255(p0 + dl);
-        q[0] = (uint8_t)clip255(q0 - dl);
-        if (ap < beta) q[-2 * step] = (uint8_t)(p1 + iclip(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
-        if (aq < beta) q[step] = (uint8_t)(q1 + iclip(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
+        q[-step] = (pel)clipmx(p0 + dl, maxv);
+        q[0] = (pel)clipmx(q0 - dl, maxv);
+        if (ap < beta) q[-2 * step] = (pel)(p1 + iclip(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
+        if (aq < beta) q[step] = (pel)(q1 + iclip(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
     } else {
         const int p3 = q[-4 * step], q3 = q[3 * step];
         const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
         if (ap < beta && small) {
-            q[-step] = (uint8_t)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-            q[-2 * step] = (uint8_t)((p2 + p1 + p0 + q0 + 2) >> 2);
-            q[-3 * step] = (uint8_t)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
-        } else q[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
+            q[-step] = (pel)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+            q[-2 * step] = (pel)((p2 + p1 + p0 + q0 + 2) >> 2);
+            q[-3 * step] = (pel)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+        } else q[-step] = (pel)((2 * p1 + p0 + q1 + 2) >> 2);
         if (aq < beta && small) {
-            q[0] = (uint8_t)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-            q[step] = (uint8_t)((p0 + q0 + q1 + q2 + 2) >> 2);
-            q[2 * step] = (uint8_t)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
-        } else q[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+            q[0] = (pel)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+            q[step] = (pel)((p0 + q0 + q1 + q2 + 2) >> 2);
+            q[2 * step] = (pel)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+        } else q[0] = (pel)((2 * q1 + q0 + p1 + 2) >> 2);
     }
 }
 
 
 // OCC workgroups per CU: 8 (64 VGPRs, a few spilled) for ticks of more than 5 x 256 MBs (2160p,
 // one dispatch round), 5 (no spills, a shorter per-MB chain) for smaller ticks
-template <int OCC>
+template <int OCC, class pel>
 __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
-    __shared__ FinS s;
+    __shared__ FinS<pel> s;
     const int tid = threadIdx.x;
     const unsigned long long bt0 = t.bprof_fin ? wall_clock64() : 0;
     const int m = xcd_block(blockIdx.x, t.pre[t.npic]);       // XCD-aware (jmh_device.h)
@@ -111,7 +115,12 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
     const int W = d.W, Wc = d.Wc, W4 = d.W >> 2;
     const int slice_p = d.slice_type == JMH_P_SLICE;
-    const int qp = d.qp;
+    // QPY (deblocking) and QP'Y = QPY + QpBdOffsetY (quantisation); Clip1 to maxv
+    const int qpy = d.qp, qp = d.qp + d.qpbd, maxv = d.maxv;
+    const pel *orgY = spl<pel>(d.orgY), *orgU = spl<pel>(d.orgU), *orgV = spl<pel>(d.orgV);
+    const pel *refY = spl<pel>(d.refY), *refU = spl<pel>(d.refU), *refV = spl<pel>(d.refV);
+    pel *recY = spl<pel>(d.recY), *recU = spl<pel>(d.recU), *recV = spl<pel>(d.recV);
+    pel *dbkY = spl<pel>(d.dbkY), *dbkU = spl<pel>(d.dbkU), *dbkV = spl<pel>(d.dbkV);
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL;
     // deblocking filters across slice edges (disable_deblocking_filter_idc 0): picture edges only
@@ -121,24 +130,24 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     const MbScratch *sc = d.scr + mby * d.mbw + mbx;
 
     // ---- inputs into LDS
-    s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    s.org[tid] = orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     if (tid < 128) {
         const int uv = tid >> 6, k = tid & 63;
-        s.orgc[uv][k] = (uv ? d.orgV : d.orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
+        s.orgc[uv][k] = (uv ? orgV : orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
     } else if (tid >= 128 && tid < 149) {
         const int x = tid - 129;
         const bool av = x < 0 ? avTL : x < 16 ? avT : false;
-        s.rtop[x + 1] = av ? d.recY[(pix_y - 1) * W + pix_x + x] : 0;
+        s.rtop[x + 1] = av ? recY[(pix_y - 1) * W + pix_x + x] : 0;
     } else if (tid >= 160 && tid < 176) {
         const int y = tid - 160;
-        s.rleft[y] = avL ? d.recY[(pix_y + y) * W + pix_x - 1] : 0;
+        s.rleft[y] = avL ? recY[(pix_y + y) * W + pix_x - 1] : 0;
     } else if (tid >= 192 && tid < 210) {
         const int i = tid - 192, uv = i / 9, x = i - 9 * uv - 1;
         const bool av = x < 0 ? avTL : avT;
-        s.ctop[uv][x + 1] = av ? (uv ? d.recV : d.recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
+        s.ctop[uv][x + 1] = av ? (uv ? recV : recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
     } else if (tid >= 224 && tid < 240) {
         const int i = tid - 224, uv = i >> 3, y = i & 7;
-        s.cleft[uv][y] = avL ? (uv ? d.recV : d.recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
+        s.cleft[uv][y] = avL ? (uv ? recV : recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
     }
 
     // ---- mode decision (encode_one_macroblock, RDO off): costs from k_mb_analyse
@@ -182,18 +191,18 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
         for (int b = 0; b < 4; b++)
             if ((cbp >> b) & 1) cbp_blk |= 0x33 << ((b >> 1) * 8 + (b & 1) * 2);
         s.lev[blk][l] = sc->i8lev[blk][l];
-        s.rec[tid] = sc->i8rec[tid];
+        s.rec[tid] = spl<pel>(sc->i8rec)[tid];
     } else if (best_mode == JMH_I4MB) {
         cbp = sc->i4cbp; cbp_blk = sc->i4blk;
         s.lev[blk][l] = sc->i4lev[blk][l];
-        s.rec[tid] = sc->i4rec[tid];
+        s.rec[tid] = spl<pel>(sc->i4rec)[tid];
     } else if (best_mode == JMH_I16MB) {
         // dct_luma_16x16 [J]
         const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per;
         const int qp_const = q_round(q_sel16(d.qsel), q_bits), qp_const2 = qp_const << 1;
-        const uint8_t *T = s.rtop + 1, *L = s.rleft;
-        const I16Par par = i16_params(T, L, avT, avL);
-        const int p = i16_pred(par, T, L, i16mode, px4, py4);
+        const pel *T = s.rtop + 1, *L = s.rleft;
+        const I16Par par = i16_params(T, L, avT, avL, (maxv + 1) >> 1);
+        const int p = i16_pred(par, T, L, i16mode, px4, py4, maxv);
         const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
         if (l == 0) s.dc[blk] = c;
         __syncthreads();
@@ -233,16 +242,16 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
         unsigned nz = lane_quant(c, l, qp, qp_const, true, lev, dq, cc);
         s.lev[blk][l] = (int16_t)lev;
         if (l == 0) { dq = s.dcdq[blk]; s.bnz[blk] = nz != 0; }
-        s.rec[py4 * 16 + px4] = (uint8_t)lane_inv4x4(dq, l, p);
+        s.rec[py4 * 16 + px4] = (pel)lane_inv4x4(dq, l, p, maxv);
         __syncthreads();
         for (int b = 0; b < 16; b++)
             if (s.bnz[b]) { cbp = 15; cbp_blk |= 1 << b; }
     } else {
         // LumaResidualCoding / LumaResidualCoding8x8 (+ SetCoeffAndReconstruction8x8)
-        const int p = qpel_direct(d.refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1]);
+        const int p = qpel_direct(refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1], maxv);
         if (d.t8 && (best_mode <= 3 || best8x8 == 0x4444)) {
             // TransformDecision [J] (item 29): sum of 4x4 SATDs vs sum of 8x8 SATDs of the residual
-            s.pred[py4 * 16 + px4] = (uint8_t)p;
+            s.pred[py4 * 16 + px4] = (pel)p;
             __syncthreads();
             const int dv = s.org[qy * 16 + qx] - s.pred[qy * 16 + qx];
             const int c4 = wave_satd4x4s(dv, l8, d.use_hadamard), c8 = wave_satd8(dv, l8, d.use_hadamard);
@@ -257,7 +266,7 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
             const int c = wave_fwd8x8(s.org[qy * 16 + qx] - pv, l8);
             int lev, dq, cc;
             const unsigned long long nz = wave_quant8(c, l8, qp, q_round(d.qsel, q8), lev, dq, cc);
-            const int rv = wave_inv8x8(dq, l8, pv);
+            const int rv = wave_inv8x8(dq, l8, pv, maxv);
             if (l8 == 0) { s.bcost[w8] = cc; s.bnz[w8] = nz != 0; }
             __syncthreads();
             int sum_cnt = 0, keep8 = 0;
@@ -273,13 +282,13 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
             if (sum_cnt <= 5) { keep8 = 0; cbp = 0; cbp_blk = 0; }      // _LUMA_MB_COEFF_COST_
             const bool keep = (keep8 >> w8) & 1;
             s.lev[il_blk(w8, l8)][l8 >> 2] = keep ? (int16_t)lev : 0;
-            s.rec[qy * 16 + qx] = (uint8_t)(keep ? rv : pv);
+            s.rec[qy * 16 + qx] = (pel)(keep ? rv : pv);
         } else {
         const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
         int lev, dq, cc;
         const int q_bits = 15 + qp / 6;
         unsigned nz = lane_quant(c, l, qp, q_round(d.qsel, q_bits), false, lev, dq, cc);
-        const int rv = lane_inv4x4(dq, l, p);
+        const int rv = lane_inv4x4(dq, l, p, maxv);
         if (l == 0) { s.bcost[blk] = cc; s.bnz[blk] = nz != 0; }
         __syncthreads();
         int sum_cnt = 0, keep8 = 0;
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
         const int mb8 = ((blk >> 3) << 1) + ((blk & 3) >> 1);
         const bool keep = (keep8 >> mb8) & 1;
         s.lev[blk][l] = keep ? (int16_t)lev : 0;
-        s.rec[py4 * 16 + px4] = (uint8_t)(keep ? rv : p);
+        s.rec[py4 * 16 + px4] = (pel)(keep ? rv : p);
         }
     }
     const bool t8flag = tr8 && (best_mode == JMH_I8MB || (cbp & 15));   // transform_size_8x8_flag
@@ -310,7 +319,9 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
 
     // ======== chroma: prediction (intra mode from k_mb_analyse, or MC) + dct_chroma [J]
     const int c_mode = is_intra ? sc->c_mode : 0;
-    const int qpc = c_qpc[iclip(0, 51, qp + d.cqp_off)];
+    // QPc of qPI = Clip3(-QpBdOffsetC, 51, QPY + chroma_qp_index_offset) (8.5.8, Table 8-15:
+    // negative qPI map to themselves), quantised at QP'c = QPc + QpBdOffsetC
+    const int qpi = iclip(-d.qpbd, 51, qpy + d.cqp_off), qpcy = qpi < 0 ? qpi : c_qpc[qpi], qpc = qpcy + d.qpbd;
     const int cq_bits = 15 + qpc / 6;
     const int cqp_const = q_round(d.qsel, cq_bits);
     const int cuv = blk >> 2, cb = blk & 3;
@@ -318,10 +329,10 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     int cdq = 0, cpredv = 0;
     if (tid < 128) {
         if (is_intra) {
-            cpredv = chroma_pred_px(s.ctop[cuv] + 1, s.cleft[cuv], s.ctop[cuv][0], avT, avL, c_mode, cxo, cyo);
+            cpredv = chroma_pred_px(s.ctop[cuv] + 1, s.cleft[cuv], s.ctop[cuv][0], avT, avL, c_mode, cxo, cyo, maxv);
         } else {
             // OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2
-            const uint8_t *R = cuv ? d.refV : d.refU;
+            const pel *R = cuv ? refV : refU;
             const int vx = s.fmv[(cyo >> 1) * 4 + (cxo >> 1)][0], vy = s.fmv[(cyo >> 1) * 4 + (cxo >> 1)][1];
             const int ii = ((pix_x >> 1) + cxo) * 8 + vx, jj = ((pix_y >> 1) + cyo) * 8 + vy;
             const int x0 = iclip(0, Wc - 1, ii >> 3), y0 = iclip(0, d.Hc - 1, jj >> 3);
@@ -361,7 +372,7 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     if (tid < 128) {
         if (s.creset[cuv]) { cdq = 0; s.cac[cuv][cb][l] = 0; }
         if (l == 0) cdq = s.cdcq[cuv][cb];
-        s.cfin[cuv][cyo * 8 + cxo] = (uint8_t)lane_inv4x4(cdq, l, cpredv);
+        s.cfin[cuv][cyo * 8 + cxo] = (pel)lane_inv4x4(cdq, l, cpredv, maxv);
     }
     __syncthreads();
     PSTAMP(18);
@@ -408,9 +419,9 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
         const int uv = tid >> 6, b = (tid >> 4) & 3, q = tid & 15;
         res->chroma_ac[uv][b][q] = s.cac[uv][b][q];
         const int k = tid & 63;
-        (uv ? d.recV : d.recU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)] = s.cfin[uv][k];
+        (uv ? recV : recU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)] = s.cfin[uv][k];
     }
-    d.recY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)] = s.rec[tid];
+    recY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)] = s.rec[tid];
 
     // ======== DeblockMb [J] / 8.7 into the reference picture (d.dbkY..): this MB's edges, in
     // place on its already-filtered left / top neighbours. MBs of one diagonal touch disjoint
@@ -425,15 +436,15 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
                 const int r = i / 20 - 4, c = i % 20 - 4;
                 int v = 0;
                 if (r >= 0 && c >= 0) v = s.rec[16 * r + c];
-                else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL)) v = d.dbkY[(pix_y + r) * W + pix_x + c];
-                s.dy[r + 4][c + 4] = (uint8_t)v;
+                else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL)) v = dbkY[(pix_y + r) * W + pix_x + c];
+                s.dy[r + 4][c + 4] = (pel)v;
             } else {
                 const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
                 int v = 0;
                 if (r >= 0 && c >= 0) v = s.cfin[pl][8 * r + c];
                 else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL))
-                    v = (pl ? d.dbkV : d.dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c];
-                s.dc2[pl][r + 4][c + 4] = (uint8_t)v;
+                    v = (pl ? dbkV : dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c];
+                s.dc2[pl][r + 4][c + 4] = (pel)v;
             }
         }
         if (tid < 32) {                           // boundary strength (8.7.2.1), frame MBs, one slice
@@ -466,26 +477,27 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
         }
         __syncthreads();
         if (tid < 64 && filt) {                   // one wave: luma lines on lanes 0..15, chroma on 16..31
-            const int offA = d.lf_offA, offB = d.lf_offB;
-            const int iA = iclip(0, 51, qp + offA), iB = iclip(0, 51, qp + offB);
-            const int alpha = c_alpha[iA], beta = c_beta[iB];
-            const int t1 = c_tc0[iA][0], t2 = c_tc0[iA][1], t3 = c_tc0[iA][2];
-            const int cA = iclip(0, 51, qpc + offA), cB = iclip(0, 51, qpc + offB);
-            const int calpha = c_alpha[cA], cbeta = c_beta[cB];
-            const int u1 = c_tc0[cA][0], u2 = c_tc0[cA][1], u3 = c_tc0[cA][2];
+            // indices from QPY / QPc (8.7.2.2), thresholds times 1 << (BitDepth - 8) (8-457..8-470)
+            const int offA = d.lf_offA, offB = d.lf_offB, bsc = 1 << (d.qpbd / 6);
+            const int iA = iclip(0, 51, qpy + offA), iB = iclip(0, 51, qpy + offB);
+            const int alpha = bsc * c_alpha[iA], beta = bsc * c_beta[iB];
+            const int t1 = bsc * c_tc0[iA][0], t2 = bsc * c_tc0[iA][1], t3 = bsc * c_tc0[iA][2];
+            const int cA = iclip(0, 51, qpcy + offA), cB = iclip(0, 51, qpcy + offB);
+            const int calpha = bsc * c_alpha[cA], cbeta = bsc * c_beta[cB];
+            const int u1 = bsc * c_tc0[cA][0], u2 = bsc * c_tc0[cA][1], u3 = bsc * c_tc0[cA][2];
             for (int dir = 0; dir < 2; dir++)
                 for (int e = 0; e < 4; e++) {
                     if (tid < 16 && !((e & 1) && t8flag)) {             // 8x8 transform: no 4x4 luma edges
                         const int k = tid, b = s.bs[dir][e][k >> 2];
                         if (b) {
-                            uint8_t *q = dir == 0 ? &s.dy[k + 4][4 * e + 4] : &s.dy[4 * e + 4][k + 4];
-                            filter_line(q, dir == 0 ? 1 : 20, b, alpha, beta, b == 1 ? t1 : b == 2 ? t2 : t3, false);
+                            pel *q = dir == 0 ? &s.dy[k + 4][4 * e + 4] : &s.dy[4 * e + 4][k + 4];
+                            filter_line(q, dir == 0 ? 1 : 20, b, alpha, beta, b == 1 ? t1 : b == 2 ? t2 : t3, false, maxv);
                         }
                     } else if (tid < 32 && !(e & 1)) {
                         const int pl = (tid - 16) >> 3, k = tid & 7, b = s.bs[dir][e][k >> 1];
                         if (b) {
-                            uint8_t *q = dir == 0 ? &s.dc2[pl][k + 4][2 * e + 4] : &s.dc2[pl][2 * e + 4][k + 4];
-                            filter_line(q, dir == 0 ? 1 : 12, b, calpha, cbeta, b == 1 ? u1 : b == 2 ? u2 : u3, true);
+                            pel *q = dir == 0 ? &s.dc2[pl][k + 4][2 * e + 4] : &s.dc2[pl][2 * e + 4][k + 4];
+                            filter_line(q, dir == 0 ? 1 : 12, b, calpha, cbeta, b == 1 ? u1 : b == 2 ? u2 : u3, true, maxv);
                         }
                     }
                     wave_lds_sync();
@@ -496,11 +508,11 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
             if (i < 400) {
                 const int r = i / 20 - 4, c = i % 20 - 4;
                 if ((r >= 0 && c >= 0) || (r >= -3 && r < 0 && c >= 0 && dbT) || (c >= -3 && c < 0 && r >= 0 && dbL))
-                    d.dbkY[(pix_y + r) * W + pix_x + c] = s.dy[r + 4][c + 4];
+                    dbkY[(pix_y + r) * W + pix_x + c] = s.dy[r + 4][c + 4];
             } else {
                 const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
                 if ((r >= 0 && c >= 0) || (r == -1 && c >= 0 && c < 8 && dbT) || (c == -1 && r >= 0 && r < 8 && dbL))
-                    if (r < 8 && c < 8) (pl ? d.dbkV : d.dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c] = s.dc2[pl][r + 4][c + 4];
+                    if (r < 8 && c < 8) (pl ? dbkV : dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c] = s.dc2[pl][r + 4][c + 4];
             }
         }
         (void)Hc;
@@ -516,7 +528,8 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st) {
     static const bool occ8 = getenv("JMH_FINAL_OCC8") != nullptr;   // A/B: the 8-per-CU build always
     const int n = t.pre[t.npic];
-    if (occ8 || n > 5 * 256) hipLaunchKernelGGL(k_mb_final<8>, dim3(xcd_grid(n)), dim3(NT), 0, st, t);
-    else hipLaunchKernelGGL(k_mb_final<5>, dim3(xcd_grid(n)), dim3(NT), 0, st, t);
+    if (t.bd > 8) hipLaunchKernelGGL((k_mb_final<8, uint16_t>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
+    else if (occ8 || n > 5 * 256) hipLaunchKernelGGL((k_mb_final<8, uint8_t>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
+    else hipLaunchKernelGGL((k_mb_final<5, uint8_t>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
     return hipGetLastError();
 }

@@ -12,10 +12,10 @@
 #include "jmh_intra8.h"
 
 __global__ __launch_bounds__(NT, 8) void k_mb_intra8(const TickArgs t) {
-    __shared__ I8S s;
+    __shared__ I8S<uint8_t> s;   // bit depth 8 (FFS / full-search ticks)
     const int mi = xcd_block(blockIdx.x, t.pre[t.npic]);      // XCD-aware (jmh_device.h)
     if (mi >= t.pre[t.npic]) return;
-    intra8_mb(t, s, mi);
+    intra8_mb<uint8_t>(t, s, mi);
 }
 
 hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st) {

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "csrc", "libjmhip.so")
 HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
+JMH_E_INVALID_ARG, JMH_E_HIP, JMH_E_OOM, JMH_E_UNSUPPORTED_CFG, JMH_E_STATE, JMH_E_NO_DEVICE = -1, -2, -3, -4, -5, -6
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
 JMH_ABI_VERSION = 11
 JMH_FLAG_KERNEL_TIMING = 1

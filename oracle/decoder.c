@@ -159,7 +159,8 @@ struct jmo_dec {
     int mbw, mbh, W, H, crop_l, crop_r, crop_t, crop_b;
     int log2_fn, poc_type, log2_poc;
     int num_ref_l0, init_qp, cqp_off, dfc_present, cip, t8mode;
-    uint8_t *cur[3], *ref[3];
+    pel *cur[3], *ref[3];  /* 16-bit samples at every bit depth                               */
+    int bd, maxv, qpbd;   /* BitDepthY = BitDepthC, (1 << bd) - 1, QpBdOffset = 6 (bd - 8)   */
     int have_ref;
     mbinfo *mi;
     int16_t *mv;          /* per 4x4 [2] */
@@ -182,12 +183,13 @@ void jmo_dec_destroy(jmo_dec *d) {
     free(d);
 }
 const char *jmo_dec_error(const jmo_dec *d) { return d->err; }
+int jmo_dec_bit_depth(const jmo_dec *d) { return d->have_sps ? d->bd : 0; }
 
 static void alloc_pics(jmo_dec *d) {
     for (int i = 0; i < 3; i++) { free(d->cur[i]); free(d->ref[i]); }
     size_t ls = (size_t)d->W * d->H;
-    d->cur[0] = calloc(ls, 1); d->cur[1] = calloc(ls / 4, 1); d->cur[2] = calloc(ls / 4, 1);
-    d->ref[0] = calloc(ls, 1); d->ref[1] = calloc(ls / 4, 1); d->ref[2] = calloc(ls / 4, 1);
+    d->cur[0] = calloc(ls, sizeof(pel)); d->cur[1] = calloc(ls / 4, sizeof(pel)); d->cur[2] = calloc(ls / 4, sizeof(pel));
+    d->ref[0] = calloc(ls, sizeof(pel)); d->ref[1] = calloc(ls / 4, sizeof(pel)); d->ref[2] = calloc(ls / 4, sizeof(pel));
     free(d->mi); free(d->mv); free(d->refi); free(d->dec4); free(d->mvd);
     d->mi = calloc((size_t)d->mbw * d->mbh, sizeof(mbinfo));
     d->mvd = calloc(ls / 16 * 2, sizeof(int16_t));
@@ -201,12 +203,17 @@ static int parse_sps(jmo_dec *d, br_t *b) {
     int profile = rbits(b, 8);
     rbits(b, 16);
     rue(b);
-    if (profile == 100) {                 /* High: only 4:2:0 8-bit with flat scaling lists */
-        if (rue(b) != 1 || rue(b) != 0 || rue(b) != 0 || rb(b) || rb(b)) {
+    d->bd = 8;
+    if (profile == 100 || profile == 110) {   /* High / High 10: 4:2:0, BitDepthC = BitDepthY, flat scaling lists */
+        int cf = rue(b), bdl = rue(b) + 8, bdc = rue(b) + 8;
+        if (cf != 1 || bdl != bdc || bdl > (profile == 110 ? 10 : 8) || rb(b) || rb(b)) {
             snprintf(d->err, sizeof d->err, "High profile SPS options unsupported");
             return -1;
         }
+        d->bd = bdl;
     } else if (profile >= 100) { snprintf(d->err, sizeof d->err, "profile %d unsupported", profile); return -1; }
+    d->maxv = (1 << d->bd) - 1;
+    d->qpbd = 6 * (d->bd - 8);
     d->log2_fn = rue(b) + 4;
     d->poc_type = rue(b);
     if (d->poc_type != 0) { snprintf(d->err, sizeof d->err, "poc type"); return -1; }
@@ -265,8 +272,8 @@ static int lavail(const jmo_dec *d, int mx, int my, int x, int y, int blk_idx) {
     (void)blk_idx;
     return 1;
 }
-static void pred4x4(const jmo_dec *d, int mx, int my, int bx, int by, int blk_idx, int mode, uint8_t *pr, int *ok) {
-    const uint8_t *R = d->cur[0];
+static void pred4x4(const jmo_dec *d, int mx, int my, int bx, int by, int blk_idx, int mode, pel *pr, int *ok) {
+    const pel *R = d->cur[0];
     int W = d->W, X = 16 * mx + bx, Y = 16 * my + by;
     int up = lavail(d, mx, my, bx, by - 1, blk_idx), left = lavail(d, mx, my, bx - 1, by, blk_idx);
     int ul = lavail(d, mx, my, bx - 1, by - 1, blk_idx);
@@ -294,7 +301,7 @@ static void pred4x4(const jmo_dec *d, int mx, int my, int bx, int by, int blk_id
                 if (up && left) v = (T(0) + T(1) + T(2) + T(3) + L(0) + L(1) + L(2) + L(3) + 4) >> 3;
                 else if (left) v = (L(0) + L(1) + L(2) + L(3) + 2) >> 2;
                 else if (up) v = (T(0) + T(1) + T(2) + T(3) + 2) >> 2;
-                else v = 128;
+                else v = 1 << (d->bd - 1);
                 break;
             case 3: v = (x == 3 && y == 3) ? (T(6) + 3 * T(7) + 2) >> 2 : (T(x + y) + 2 * T(x + y + 1) + T(x + y + 2) + 2) >> 2; break;
             case 4:
@@ -331,13 +338,13 @@ static void pred4x4(const jmo_dec *d, int mx, int my, int bx, int by, int blk_id
                 break;
             }
             }
-            pr[4 * y + x] = (uint8_t)v;
+            pr[4 * y + x] = (pel)v;
         }
 #undef T
 #undef L
 }
-static int pred16(const jmo_dec *d, int mx, int my, int mode, uint8_t *pr) {
-    const uint8_t *R = d->cur[0];
+static int pred16(const jmo_dec *d, int mx, int my, int mode, pel *pr) {
+    const pel *R = d->cur[0];
     int W = d->W, X = 16 * mx, Y = 16 * my;
     int up = avail_mb(d, mx, my - 1, mx, my), left = avail_mb(d, mx - 1, my, mx, my), ul = avail_mb(d, mx - 1, my - 1, mx, my);
     int T[17], L[17];                   /* index 0 = corner */
@@ -348,19 +355,20 @@ static int pred16(const jmo_dec *d, int mx, int my, int mode, uint8_t *pr) {
     if (mode == 3 && !(up && left && ul)) return -1;
     int st = 0, sl = 0;
     for (int i = 1; i <= 16; i++) { st += T[i]; sl += L[i]; }
-    int dc = (up && left) ? (st + sl + 16) >> 5 : up ? (st + 8) >> 4 : left ? (sl + 8) >> 4 : 128;
+    int dc = (up && left) ? (st + sl + 16) >> 5 : up ? (st + 8) >> 4 : left ? (sl + 8) >> 4 : 1 << (d->bd - 1);
     int H = 0, V = 0;
     for (int xp = 0; xp < 8; xp++) { H += (xp + 1) * (T[1 + 8 + xp] - T[1 + 6 - xp]); V += (xp + 1) * (L[1 + 8 + xp] - L[1 + 6 - xp]); }
     int a = 16 * (L[16] + T[16]), bb = (5 * H + 32) >> 6, c = (5 * V + 32) >> 6;
     for (int y = 0; y < 16; y++)
         for (int x = 0; x < 16; x++) {
-            int v = mode == 0 ? T[1 + x] : mode == 1 ? L[1 + y] : mode == 2 ? dc : clip255((a + bb * (x - 7) + c * (y - 7) + 16) >> 5);
-            pr[16 * y + x] = (uint8_t)v;
+            int v = mode == 0 ? T[1 + x] : mode == 1 ? L[1 + y] : mode == 2 ? dc : iclip(0, d->maxv, (a + bb * (x - 7) + c * (y - 7) + 16) >> 5);
+            pr[16 * y + x] = (pel)v;
         }
     return 0;
 }
-static int predc(const jmo_dec *d, int mx, int my, int comp, int mode, uint8_t *pr) {
-    const uint8_t *R = d->cur[comp];
+static int predc(const jmo_dec *d, int mx, int my, int comp, int mode, pel *pr) {
+    const pel *R = d->cur[comp];
+    const int dcd = 1 << (d->bd - 1);
     int W = d->W / 2, X = 8 * mx, Y = 8 * my;
     int up = avail_mb(d, mx, my - 1, mx, my), left = avail_mb(d, mx - 1, my, mx, my), ul = avail_mb(d, mx - 1, my - 1, mx, my);
     int T[9], L[9];
@@ -374,9 +382,9 @@ static int predc(const jmo_dec *d, int mx, int my, int comp, int mode, uint8_t *
         if (mode == 0) {
             int su = 0, sv = 0;
             for (int i = 0; i < 4; i++) { su += T[1 + xo + i]; sv += L[1 + yo + i]; }
-            if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) v = (up && left) ? (su + sv + 4) >> 3 : left ? (sv + 2) >> 2 : up ? (su + 2) >> 2 : 128;
-            else if (xo > 0) v = up ? (su + 2) >> 2 : left ? (sv + 2) >> 2 : 128;
-            else v = left ? (sv + 2) >> 2 : up ? (su + 2) >> 2 : 128;
+            if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) v = (up && left) ? (su + sv + 4) >> 3 : left ? (sv + 2) >> 2 : up ? (su + 2) >> 2 : dcd;
+            else if (xo > 0) v = up ? (su + 2) >> 2 : left ? (sv + 2) >> 2 : dcd;
+            else v = left ? (sv + 2) >> 2 : up ? (su + 2) >> 2 : dcd;
         }
         for (int y = 0; y < 4; y++)
             for (int x = 0; x < 4; x++) {
@@ -387,9 +395,9 @@ static int predc(const jmo_dec *d, int mx, int my, int comp, int mode, uint8_t *
                     int H = 0, V = 0;
                     for (int xp = 0; xp < 4; xp++) { H += (xp + 1) * (T[1 + 4 + xp] - T[1 + 2 - xp]); V += (xp + 1) * (L[1 + 4 + xp] - L[1 + 2 - xp]); }
                     int a = 16 * (L[8] + T[8]), bb = (34 * H + 32) >> 6, c = (34 * V + 32) >> 6;
-                    w = clip255((a + bb * (xx - 3) + c * (yy - 3) + 16) >> 5);
+                    w = iclip(0, d->maxv, (a + bb * (xx - 3) + c * (yy - 3) + 16) >> 5);
                 }
-                pr[8 * yy + xx] = (uint8_t)w;
+                pr[8 * yy + xx] = (pel)w;
             }
     }
     return 0;
@@ -409,19 +417,19 @@ static void scale4x4(int32_t *c, int qp, int skip_dc) {
         else c[k] = (c[k] * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
     }
 }
-static void recon4x4(int32_t *c, const uint8_t *pred, int ps, uint8_t *out, int os) {
+static void recon4x4(int32_t *c, const pel *pred, int ps, pel *out, int os, int maxv) {
     int32_t r[16];
     jmo_inverse4x4(c, r);
     for (int y = 0; y < 4; y++)
-        for (int x = 0; x < 4; x++) out[y * os + x] = (uint8_t)clip255(pred[y * ps + x] + ((r[4 * y + x] + 32) >> 6));
+        for (int x = 0; x < 4; x++) out[y * os + x] = (pel)iclip(0, maxv, pred[y * ps + x] + ((r[4 * y + x] + 32) >> 6));
 }
 
 /* ---- Intra_8x8 (8.3.2.2): the 25 reference samples as one edge e[0..24] running from
  * p[-1,7] up to p[-1,0] (e[7-y]), the corner p[-1,-1] (e[8]) and along p[0..15,-1] (e[9+x]);
  * the 8.3.2.2.1 filter is a [1 2 1] tap along the edge whose missing outer neighbour is
  * replaced by the centre sample, and every directional mode reads that filtered edge. */
-static int pred8x8(const jmo_dec *d, int mx, int my, int b8, int mode, uint8_t *pr) {
-    const uint8_t *R = d->cur[0];
+static int pred8x8(const jmo_dec *d, int mx, int my, int b8, int mode, pel *pr) {
+    const pel *R = d->cur[0];
     int W = d->W, bx = 8 * (b8 & 1), by = 8 * (b8 >> 1), X = 16 * mx + bx, Y = 16 * my + by;
     int left = bx ? 1 : avail_mb(d, mx - 1, my, mx, my);
     int up = by ? 1 : avail_mb(d, mx, my - 1, mx, my);
@@ -444,7 +452,7 @@ static int pred8x8(const jmo_dec *d, int mx, int my, int b8, int mode, uint8_t *
     if (((mode == 0 || mode == 3 || mode == 7) && !up) || ((mode == 1 || mode == 8) && !left) ||
         ((mode == 4 || mode == 5 || mode == 6) && !(up && left && ul)))
         return -1;
-    int dc = 128, st = 0, sl = 0;
+    int dc = 1 << (d->bd - 1), st = 0, sl = 0;
     for (int i = 0; i < 8; i++) { st += up ? TT(i) : 0; sl += left ? LL(i) : 0; }
     if (up && left) dc = (st + sl + 8) >> 4;
     else if (up) dc = (st + 4) >> 3;
@@ -481,7 +489,7 @@ static int pred8x8(const jmo_dec *d, int mx, int my, int b8, int mode, uint8_t *
                 else v = (LL(y + (x >> 1)) + 2 * LL(y + (x >> 1) + 1) + LL(y + (x >> 1) + 2) + 2) >> 2;
                 break;
             }
-            pr[8 * y + x] = (uint8_t)v;
+            pr[8 * y + x] = (pel)v;
         }
 #undef TT
 #undef LL
@@ -504,7 +512,7 @@ static int lscale8(int qm, int i, int j) {
           : ((i % 4 == 0 && j % 4 == 2) || (i % 4 == 2 && j % 4 == 0)) ? 4 : 5;
     return 16 * v8[qm][k];
 }
-static void recon8x8(const int *c64, int qp, const uint8_t *pred, int ps, uint8_t *out, int os) {
+static void recon8x8(const int *c64, int qp, const pel *pred, int ps, pel *out, int os, int maxv) {
     int32_t m[64], r[64];
     for (int k = 0; k < 64; k++) {
         int x = zz8[k][0], y = zz8[k][1], ls = lscale8(qp % 6, y, x), c = c64[k];
@@ -512,15 +520,15 @@ static void recon8x8(const int *c64, int qp, const uint8_t *pred, int ps, uint8_
     }
     jmo_inverse8x8(m, r);
     for (int y = 0; y < 8; y++)
-        for (int x = 0; x < 8; x++) out[y * os + x] = (uint8_t)clip255(pred[y * ps + x] + ((r[8 * y + x] + 32) >> 6));
+        for (int x = 0; x < 8; x++) out[y * os + x] = (pel)iclip(0, maxv, pred[y * ps + x] + ((r[8 * y + x] + 32) >> 6));
 }
 
 /* ---- inter prediction (8.4.2.2) ------------------------------------------------------- */
-static void inter_pred(const jmo_dec *d, int mx, int my, const int16_t mv16[16][2], uint8_t *py, uint8_t *pu, uint8_t *pv) {
+static void inter_pred(const jmo_dec *d, int mx, int my, const int16_t mv16[16][2], pel *py, pel *pu, pel *pv) {
     for (int y = 0; y < 16; y++)
         for (int x = 0; x < 16; x++) {
             const int16_t *v = mv16[(y >> 2) * 4 + (x >> 2)];
-            py[16 * y + x] = (uint8_t)jmo_luma_qpel_sample(d->ref[0], d->W, d->H, d->W, 4 * (16 * mx + x) + v[0], 4 * (16 * my + y) + v[1]);
+            py[16 * y + x] = (pel)jmo_qpel_px(d->ref[0], d->W, d->H, d->W, 4 * (16 * mx + x) + v[0], 4 * (16 * my + y) + v[1], d->maxv);
         }
     int Wc = d->W / 2, Hc = d->H / 2;
     for (int c = 1; c <= 2; c++)
@@ -528,10 +536,10 @@ static void inter_pred(const jmo_dec *d, int mx, int my, const int16_t mv16[16][
             for (int x = 0; x < 8; x++) {
                 const int16_t *v = mv16[(y >> 1) * 4 + (x >> 1)];
                 int xi = 8 * mx + x + (v[0] >> 3), yi = 8 * my + y + (v[1] >> 3), fx = v[0] & 7, fy = v[1] & 7;
-                const uint8_t *R = d->ref[c];
+                const pel *R = d->ref[c];
                 int A = R[iclip(0, Hc - 1, yi) * Wc + iclip(0, Wc - 1, xi)], B = R[iclip(0, Hc - 1, yi) * Wc + iclip(0, Wc - 1, xi + 1)];
                 int C = R[iclip(0, Hc - 1, yi + 1) * Wc + iclip(0, Wc - 1, xi)], D = R[iclip(0, Hc - 1, yi + 1) * Wc + iclip(0, Wc - 1, xi + 1)];
-                (c == 1 ? pu : pv)[8 * y + x] = (uint8_t)(((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6);
+                (c == 1 ? pu : pv)[8 * y + x] = (pel)(((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6);
             }
 }
 
@@ -722,7 +730,7 @@ static int parse_cavlc(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int t, 
     s->cbp = cbp;
     if (cbp > 0 || intra_type == 1) {
         int dq = rse(b);
-        *qp = (*qp + dq + 52) % 52;
+        *qp = (*qp + dq + 52 + 2 * d->qpbd) % (52 + d->qpbd) - d->qpbd;   /* 7-37 */
     }
     /* residual (7.3.5.3, CAVLC): I16 DC, luma, chroma DC Cb Cr, chroma AC Cb Cr */
     int cbpl = cbp & 15, cbpc = cbp >> 4;
@@ -1056,7 +1064,7 @@ static int parse_cabac(jmo_dec *d, int mx, int my, int slice_p, mbsyn *s, int *q
     if (cdec(c, 60 + d->prev_qpd)) { k = 1; while (cdec(c, k == 1 ? 62 : 63)) { if (++k > 104) FAIL("mb_qp_delta"); } }
     int dq = (k & 1) ? (k + 1) / 2 : -(k / 2);
     d->prev_qpd = dq != 0;
-    *qp = (*qp + dq + 52) % 52;
+    *qp = (*qp + dq + 52 + 2 * d->qpbd) % (52 + d->qpbd) - d->qpbd;
     /* residual */
     int cur_intra = intra, cbpl = cbp & 15, cbpc = cbp >> 4;
     if (i16) {
@@ -1101,7 +1109,7 @@ static int recon_mb(jmo_dec *d, int mx, int my, const mbsyn *s, int qp_) {
     mbinfo *mi = &d->mi[my * d->mbw + mx];
     mi->qp = qp_;
     mi->cbp = s->cbp;
-    uint8_t pred[256], predu[64], predv[64];
+    pel pred[256], predu[64], predv[64];
     int intra_type = s->intra_type;
     if (intra_type < 0) inter_pred(d, mx, my, s->mv16, pred, predu, predv);
     else {
@@ -1109,10 +1117,13 @@ static int recon_mb(jmo_dec *d, int mx, int my, const mbsyn *s, int qp_) {
         if (intra_type == 1 && pred16(d, mx, my, s->i16mode, pred)) FAIL("I16 mode %d unavailable at MB %d,%d", s->i16mode, mx, my);
     }
     if (s->skip) mi->cbp = 0;
-    int qpc = QPCt[iclip(0, 51, qp_ + d->cqp_off)];
+    /* QPY of the MB is qp_; scaling at QP'Y = QPY + QpBdOffsetY and QP'C = QPC + QpBdOffsetC (8.5.8) */
+    const int qpi = iclip(-d->qpbd, 51, qp_ + d->cqp_off), maxv = d->maxv;
+    int qpc = (qpi < 0 ? qpi : QPCt[qpi]) + d->qpbd;
+    qp_ += d->qpbd;
     int cbpc = s->cbp >> 4;
     int32_t dcY[16] = {0};
-    uint8_t *RY = d->cur[0];
+    pel *RY = d->cur[0];
     int W = d->W;
     if (intra_type == 1) {
         int32_t m[16], t2[16];
@@ -1136,12 +1147,12 @@ static int recon_mb(jmo_dec *d, int mx, int my, const mbsyn *s, int qp_) {
         for (int k = 0; k < 64; k++) any |= s->l8[b8][k] != 0;
         int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
         if (any) mi->nzblk |= 0x33 << ((by >> 2) * 4 + (bx >> 2));
-        uint8_t *dst = RY + (16 * my + by) * W + 16 * mx + bx;
+        pel *dst = RY + (16 * my + by) * W + 16 * mx + bx;
         if (intra_type == 0) {
-            uint8_t p64[64];
+            pel p64[64];
             if (pred8x8(d, mx, my, b8, s->ipm[(by >> 2) * 4 + (bx >> 2)], p64)) FAIL("I8 mode unavailable at MB %d,%d", mx, my);
-            recon8x8(s->l8[b8], qp_, p64, 8, dst, W);
-        } else recon8x8(s->l8[b8], qp_, pred + by * 16 + bx, 16, dst, W);
+            recon8x8(s->l8[b8], qp_, p64, 8, dst, W, maxv);
+        } else recon8x8(s->l8[b8], qp_, pred + by * 16 + bx, 16, dst, W, maxv);
     }
     for (int blk = 0; blk < 16 && !mi->t8; blk++) {
         int b8 = blk >> 2;
@@ -1154,14 +1165,14 @@ static int recon_mb(jmo_dec *d, int mx, int my, const mbsyn *s, int qp_) {
         for (int k = 0; k < 16; k++) m[zz[k]] = c[k];
         scale4x4(m, qp_, intra_type == 1);
         if (intra_type == 1) m[0] = dcY[y4 * 4 + x4];
-        uint8_t *dst = RY + (16 * my + 4 * y4) * W + 16 * mx + 4 * x4;
+        pel *dst = RY + (16 * my + 4 * y4) * W + 16 * mx + 4 * x4;
         if (intra_type == 0) {
-            uint8_t p4[16];
+            pel p4[16];
             int ok;
             pred4x4(d, mx, my, 4 * x4, 4 * y4, blk, s->ipm[y4 * 4 + x4], p4, &ok);
             if (!ok) FAIL("I4 mode %d unavailable at MB %d,%d blk %d", s->ipm[y4 * 4 + x4], mx, my, blk);
-            recon4x4(m, p4, 4, dst, W);
-        } else recon4x4(m, pred + 4 * y4 * 16 + 4 * x4, 16, dst, W);
+            recon4x4(m, p4, 4, dst, W, maxv);
+        } else recon4x4(m, pred + 4 * y4 * 16 + 4 * x4, 16, dst, W, maxv);
     }
     int dcc[2][4] = {{0}};
     if (cbpc)
@@ -1171,7 +1182,7 @@ static int recon_mb(jmo_dec *d, int mx, int my, const mbsyn *s, int qp_) {
             for (int k = 0; k < 4; k++) dcc[comp][k] = (f[k] * lscale(qpc % 6, 0) * (1 << (qpc / 6))) >> 5;
         }
     for (int comp = 0; comp < 2; comp++) {
-        uint8_t *R = d->cur[1 + comp];
+        pel *R = d->cur[1 + comp];
         int Wc = d->W / 2;
         for (int k = 0; k < 4; k++) {
             int32_t m[16];
@@ -1179,7 +1190,7 @@ static int recon_mb(jmo_dec *d, int mx, int my, const mbsyn *s, int qp_) {
             scale4x4(m, qpc, 1);
             m[0] = dcc[comp][k];
             int xo = (k & 1) * 4, yo = (k >> 1) * 4;
-            recon4x4(m, (comp ? predv : predu) + yo * 8 + xo, 8, R + (8 * my + yo) * Wc + 8 * mx + xo, Wc);
+            recon4x4(m, (comp ? predv : predu) + yo * 8 + xo, 8, R + (8 * my + yo) * Wc + 8 * mx + xo, Wc, maxv);
         }
     }
     return 0;
@@ -1206,41 +1217,47 @@ static int bs_of(const jmo_dec *d, int xp, int yp, int xq, int yq, int mbedge) {
     if (iabs(d->mv[2 * ip] - d->mv[2 * iq]) >= 4 || iabs(d->mv[2 * ip + 1] - d->mv[2 * iq + 1]) >= 4) return 1;
     return 0;
 }
-static void edge_filter(uint8_t *s, int step, int bS, int qpav, int chroma, int offA, int offB) {
-    int iA = iclip(0, 51, qpav + offA), iB = iclip(0, 51, qpav + offB);
-    int a = Alpha[iA], bt = Beta[iB];
+/* alpha, beta, tC0 times 1 << (BitDepth - 8) (8-460, 8-461, 8-470); Clip1 to maxv */
+static void edge_filter(pel *s, int step, int bS, int qpav, int chroma, int offA, int offB, int bd) {
+    int iA = iclip(0, 51, qpav + offA), iB = iclip(0, 51, qpav + offB), sc = 1 << (bd - 8), maxv = (1 << bd) - 1;
+    int a = Alpha[iA] * sc, bt = Beta[iB] * sc;
     int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
     if (!(bS && iabs(p0 - q0) < a && iabs(p1 - p0) < bt && iabs(q1 - q0) < bt)) return;
     if (bS < 4) {
-        int tc0 = Tc0[iA][bS - 1], tc;
+        int tc0 = Tc0[iA][bS - 1] * sc, tc;
         if (chroma) tc = tc0 + 1;
         else {
             int p2 = s[-3 * step], q2 = s[2 * step];
             int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
             tc = tc0 + (ap < bt) + (aq < bt);
-            if (ap < bt) s[-2 * step] = (uint8_t)(p1 + iclip(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - 2 * p1) >> 1));
-            if (aq < bt) s[step] = (uint8_t)(q1 + iclip(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - 2 * q1) >> 1));
+            if (ap < bt) s[-2 * step] = (pel)(p1 + iclip(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - 2 * p1) >> 1));
+            if (aq < bt) s[step] = (pel)(q1 + iclip(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - 2 * q1) >> 1));
         }
         int dl = iclip(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
-        s[-step] = (uint8_t)clip255(p0 + dl);
-        s[0] = (uint8_t)clip255(q0 - dl);
+        s[-step] = (pel)iclip(0, maxv, p0 + dl);
+        s[0] = (pel)iclip(0, maxv, q0 - dl);
     } else if (chroma) {
-        s[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
-        s[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+        s[-step] = (pel)((2 * p1 + p0 + q1 + 2) >> 2);
+        s[0] = (pel)((2 * q1 + q0 + p1 + 2) >> 2);
     } else {
         int p2 = s[-3 * step], q2 = s[2 * step], p3 = s[-4 * step], q3 = s[3 * step];
         int ap = iabs(p2 - p0), aq = iabs(q2 - q0), sm = iabs(p0 - q0) < ((a >> 2) + 2);
         if (ap < bt && sm) {
-            s[-step] = (uint8_t)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-            s[-2 * step] = (uint8_t)((p2 + p1 + p0 + q0 + 2) >> 2);
-            s[-3 * step] = (uint8_t)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
-        } else s[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
+            s[-step] = (pel)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+            s[-2 * step] = (pel)((p2 + p1 + p0 + q0 + 2) >> 2);
+            s[-3 * step] = (pel)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+        } else s[-step] = (pel)((2 * p1 + p0 + q1 + 2) >> 2);
         if (aq < bt && sm) {
-            s[0] = (uint8_t)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-            s[step] = (uint8_t)((p0 + q0 + q1 + q2 + 2) >> 2);
-            s[2 * step] = (uint8_t)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
-        } else s[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+            s[0] = (pel)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+            s[step] = (pel)((p0 + q0 + q1 + q2 + 2) >> 2);
+            s[2 * step] = (pel)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+        } else s[0] = (pel)((2 * q1 + q0 + p1 + 2) >> 2);
     }
+}
+/* QPc of a macroblock's QPY (8.5.8, qPI clipped to [-QpBdOffsetC, 51]) for the chroma filter */
+static int qpc_of(const jmo_dec *d, int qpy) {
+    int qpi = iclip(-d->qpbd, 51, qpy + d->cqp_off);
+    return qpi < 0 ? qpi : QPCt[qpi];
 }
 static void deblock(jmo_dec *d) {
     if (d->dis_dbf == 1) return;
@@ -1254,15 +1271,15 @@ static void deblock(jmo_dec *d) {
                     if (e == 0 && ((vert && mx == 0) || (!vert && my == 0))) continue;
                     int qp_ = d->mi[vert ? my * d->mbw + mx - (e == 0) : (my - (e == 0)) * d->mbw + mx].qp;
                     int qav = (qp_ + qq + 1) >> 1;
-                    int qcav = (QPCt[iclip(0, 51, qp_ + d->cqp_off)] + QPCt[iclip(0, 51, qq + d->cqp_off)] + 1) >> 1;
+                    int qcav = (qpc_of(d, qp_) + qpc_of(d, qq) + 1) >> 1;
                     for (int k = 0; k < 16; k++) {
                         int xq = vert ? 16 * mx + e : 16 * mx + k, yq = vert ? 16 * my + k : 16 * my + e;
                         int bS = bs_of(d, vert ? xq - 1 : xq, vert ? yq : yq - 1, xq, yq, e == 0);
-                        edge_filter(d->cur[0] + yq * W + xq, vert ? 1 : W, bS, qav, 0, d->offA, d->offB);
+                        edge_filter(d->cur[0] + yq * W + xq, vert ? 1 : W, bS, qav, 0, d->offA, d->offB, d->bd);
                         if ((e & 7) == 0 && (k & 1) == 0) {
                             int cx = vert ? 8 * mx + e / 2 : 8 * mx + k / 2, cy = vert ? 8 * my + k / 2 : 8 * my + e / 2;
                             for (int c = 1; c <= 2; c++) {
-                                edge_filter(d->cur[c] + cy * Wc + cx, vert ? 1 : Wc, bS, qcav, 1, d->offA, d->offB);
+                                edge_filter(d->cur[c] + cy * Wc + cx, vert ? 1 : Wc, bS, qcav, 1, d->offA, d->offB, d->bd);
                             }
                         }
                     }
@@ -1382,18 +1399,25 @@ int jmo_decode_annexb(jmo_dec *d, const uint8_t *buf, long len, uint8_t *out, lo
             if (!r) r = decode_slice(d, &b, nal_type, nal_ref, &pic_done);
             if (!r && pic_done) {
                 int cw = d->W - 2 * (d->crop_l + d->crop_r), ch = d->H - 2 * (d->crop_t + d->crop_b);
-                long fs = (long)cw * ch * 3 / 2;
+                const int ps = d->bd > 8 ? 2 : 1;          /* output: bytes, or 16-bit LE samples (High 10) */
+                long fs = (long)cw * ch * 3 / 2 * ps;
                 if ((nframes + 1) * fs > out_cap) { snprintf(d->err, sizeof d->err, "output buffer too small"); r = -1; }
                 else {
                     uint8_t *o = out + nframes * fs;
-                    for (int y = 0; y < ch; y++) memcpy(o + (long)y * cw, d->cur[0] + (long)(y + 2 * d->crop_t) * d->W + 2 * d->crop_l, cw);
-                    for (int c = 1; c <= 2; c++)
-                        for (int y = 0; y < ch / 2; y++)
-                            memcpy(o + (long)cw * ch + (c - 1) * (long)(cw / 2) * (ch / 2) + (long)y * (cw / 2),
-                                   d->cur[c] + (long)(y + d->crop_t) * (d->W / 2) + d->crop_l, cw / 2);
+                    long k = 0;
+                    for (int c = 0; c < 3; c++) {
+                        const int pw = c ? cw / 2 : cw, ph = c ? ch / 2 : ch, st = c ? d->W / 2 : d->W;
+                        const int ox = c ? d->crop_l : 2 * d->crop_l, oy = c ? d->crop_t : 2 * d->crop_t;
+                        for (int y = 0; y < ph; y++)
+                            for (int x = 0; x < pw; x++, k++) {
+                                const pel v = d->cur[c][(long)(y + oy) * st + ox + x];
+                                if (ps == 1) o[k] = (uint8_t)v;
+                                else { o[2 * k] = (uint8_t)v; o[2 * k + 1] = (uint8_t)(v >> 8); }
+                            }
+                    }
                     nframes++;
                     *width = cw; *height = ch;
-                    for (int c = 0; c < 3; c++) { uint8_t *t = d->ref[c]; d->ref[c] = d->cur[c]; d->cur[c] = t; }
+                    for (int c = 0; c < 3; c++) { pel *t = d->ref[c]; d->ref[c] = d->cur[c]; d->cur[c] = t; }
                     d->have_ref = 1;
                 }
             }

@@ -338,7 +338,8 @@ static void epzs_refine(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, in
 
 static int epzs_search(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, int range, int *mvx, int *mvy) {
     int c0x = *mvx, c0y = *mvy;
-    int med = jmo_blc_size[bt][0] * jmo_blc_size[bt][1];  /* medthres: EPZSMedThresScale 1 */
+    /* medthres: EPZSMedThresScale 1, times pel_error_me = 1 << (bit depth - 8) (High 10) */
+    int med = jmo_blc_size[bt][0] * jmo_blc_size[bt][1] * ((s->c->maxv + 1) >> 8);
     int cand[41][2], ok[41];
     int n = epzs_predictors(s, bt, bx4, by4, range, c0x, c0y, cand, ok);
     int min_mcost = epzs_cost(s, bt, bx4, by4, c0x, c0y, pmvx, pmvy), bx = c0x, by = c0y;

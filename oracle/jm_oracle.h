@@ -111,6 +111,7 @@ void jmo_dec_destroy(jmo_dec *d);
 int  jmo_decode_annexb(jmo_dec *d, const uint8_t *buf, long len, uint8_t *out, long out_cap,
                        int *width, int *height);
 const char *jmo_dec_error(const jmo_dec *d);
+int jmo_dec_bit_depth(const jmo_dec *d);   /* of the last SPS (0: none yet); output samples are 16-bit LE above 8 */
 
 #ifdef __cplusplus
 }

@@ -23,9 +23,10 @@ int main(int argc, char **argv) {
     if (frames < 0) { fprintf(stderr, "decode error: %s\n", jmo_dec_error(d)); jmo_dec_destroy(d); free(out); return 2; }
     FILE *o = fopen(argv[2], "wb");
     if (!o) { perror(argv[2]); jmo_dec_destroy(d); free(out); return 1; }
-    fwrite(out, 1, (size_t)frames * w * h * 3 / 2, o);
+    const int bd = jmo_dec_bit_depth(d);
+    fwrite(out, 1, (size_t)frames * w * h * 3 / 2 * (bd > 8 ? 2 : 1), o);   /* 16-bit LE above 8 bits */
     fclose(o);
-    printf("decoded %d frames %dx%d\n", frames, w, h);
+    printf("decoded %d frames %dx%d bit depth %d\n", frames, w, h, bd);
     jmo_dec_destroy(d);
     free(out);
     return 0;

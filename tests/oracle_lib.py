@@ -60,6 +60,7 @@ def lib():
             "jmo_dec_destroy": (None, [_P]),
             "jmo_decode_annexb": (_I, [_P, _P, ctypes.c_long, _P, ctypes.c_long, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
             "jmo_dec_error": (ctypes.c_char_p, [_P]),
+            "jmo_dec_bit_depth": (_I, [_P]),
         }
         for n, (r, a) in sig.items():
             f = getattr(L, n)
@@ -175,15 +176,19 @@ def decode_annexb(data, max_frames=64, max_w=1920, max_h=1088):
     d = ctypes.c_void_p()
     L.jmo_dec_create(ctypes.byref(d))
     buf = np.frombuffer(data, np.uint8).copy()
-    cap = max_frames * max_w * max_h * 3 // 2
+    cap = max_frames * max_w * max_h * 3   # room for 16-bit samples (High 10)
     out = np.empty(cap, np.uint8)
     w, h = ctypes.c_int(), ctypes.c_int()
     n = L.jmo_decode_annexb(d, _ptr(buf), len(buf), _ptr(out), cap, ctypes.byref(w), ctypes.byref(h))
     err = L.jmo_dec_error(d).decode()
+    bd = L.jmo_dec_bit_depth(d)
     L.jmo_dec_destroy(d)
     if n < 0:
         raise RuntimeError("decode failed: " + err)
     fs = w.value * h.value * 3 // 2
+    if bd > 8:   # 16-bit LE samples
+        o16 = out[:n * fs * 2].view("<u2")
+        return [o16[i * fs:(i + 1) * fs] for i in range(n)], w.value, h.value
     return [out[i * fs:(i + 1) * fs] for i in range(n)], w.value, h.value
 
 

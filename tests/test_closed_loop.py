@@ -79,6 +79,27 @@ CABAC = [
      "LoopFilterAlphaC0Offset=3", "LoopFilterBetaOffset=-2", "QPFirstFrame=12", "QPRemainingFrame=20"],
 ]
 
+# High 10 (ProfileIDC 110): 9 / 10-bit samples through EPZS, I4 / I16 / I8, the 8x8
+# transform, QP'Y / QP'C = QP + 6 (bit depth - 8) (incl. negative QPc), scaled deblocking thresholds,
+# CAVLC and CABAC, slices, QP extremes
+HIGH10 = [
+    ["InputFile=synthetic:61", "FramesToBeEncoded=4", "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10",
+     "SearchMode=3", "SearchRange=16"],
+    ["InputFile=synthetic:62", "FramesToBeEncoded=4", "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10",
+     "SearchMode=3", "SearchRange=16", "Transform8x8Mode=1", "SourceWidth=352", "SourceHeight=288", "QPRemainingFrame=31"],
+    ["InputFile=synthetic:63", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=9", "SourceBitDepthChroma=9",
+     "SearchMode=3", "SearchRange=8", "Transform8x8Mode=1", "QPFirstFrame=0", "QPRemainingFrame=2", "ChromaQPOffset=-12"],
+    ["InputFile=synthetic:64", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10",
+     "SearchMode=3", "SearchRange=8", "QPFirstFrame=51", "QPRemainingFrame=51", "LoopFilterParametersFlag=1",
+     "LoopFilterAlphaC0Offset=6", "LoopFilterBetaOffset=6"],
+    ["InputFile=synthetic:65", "FramesToBeEncoded=4", "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10",
+     "SearchMode=3", "SearchRange=16", "Transform8x8Mode=1", "SymbolMode=1", "SliceMode=1", "SliceArgument=13",
+     "EPZSDualRefinement=1", "IntraPeriod=2"],
+    ["InputFile=synthetic:66", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10",
+     "SearchMode=3", "SearchRange=8", "SymbolMode=1", "QPFirstFrame=4", "QPRemainingFrame=6", "UseHadamard=0",
+     "SourceWidth=200", "SourceHeight=120"],
+]
+
 
 def encode(d, extra):
     args = [LENCOD_CPU, "-p", f"OutputFile={d}/a.264", "-p", f"ReconFile={d}/rec.yuv"]
@@ -104,6 +125,22 @@ def test_decoder_reproduces_recon_cabac(extra):
     """SymbolMode 1: the independent decoder's CABAC parser (own tables and context selection)
     reproduces the encoder's reconstruction."""
     test_decoder_reproduces_recon(extra)
+
+
+@pytest.mark.parametrize("extra", HIGH10, ids=[c[0].split(":")[1] for c in HIGH10])
+def test_decoder_reproduces_recon_high10(extra):
+    """High 10: the decoder's 16-bit path reproduces the encoder's 16-bit reconstruction."""
+    test_decoder_reproduces_recon(extra)
+
+
+def test_high10_recon_uses_the_range():
+    """10-bit reconstruction: 16-bit LE samples, some above 255 (not an 8-bit picture stored wide)."""
+    ensure_built()
+    import numpy as np
+    with tempfile.TemporaryDirectory() as d:
+        encode(d, HIGH10[0])
+        rec = np.fromfile(f"{d}/rec.yuv", "<u2")
+        assert rec.max() > 255 and rec.max() <= 1023
 
 
 def test_cabac_smaller_than_cavlc():

@@ -402,6 +402,104 @@ def test_pipelined_slots_equal_sequential():
         assert np.array_equal(x, y)
 
 
+# ---------------- High 10 (f5): the EPZS wavefront on 16-bit samples ----------------
+def hbd_seq(w, h, n, seed, bd, step=(29, -23)):
+    """moving_seq widened to bd bits: samples << (bd - 8) plus low-bit noise, full range used."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for y, u, v in moving_seq(w, h, n, seed, step):
+        sh = bd - 8
+        out.append(tuple(np.ascontiguousarray((p.astype(np.uint16) << sh) | rng.integers(0, 1 << sh, p.shape, dtype=np.uint16))
+                         for p in (y, u, v)))
+    return out
+
+
+@pytest.mark.parametrize("bd,kw,qp,cqp", [
+    (10, dict(search_range=16), 28, 0),
+    (10, dict(search_range=16, transform_8x8_mode=1), 28, 0),
+    (10, dict(search_range=32, transform_8x8_mode=1, restrict_search_range=0), 0, -12),   # QP'c < 12, QPc < 0
+    (10, dict(search_range=8), 51, 12),
+    (9, dict(search_range=16, transform_8x8_mode=1, use_hadamard=0), 20, 0),
+    (10, dict(search_range=16, transform_8x8_mode=1, slice_mbs=5), 30, 0),
+    (10, dict(search_range=16, epzs_dual_refinement=1, inter_search=(1, 0, 1, 1, 0, 1, 1)), 36, 3),
+])
+def test_high10_pictures(bd, kw, qp, cqp):
+    """f5: k_mb_epzs / k_mb_intra / k_mb_final on 16-bit samples == the oracle's 16-bit
+    restatement on every macroblock (QP'Y, QP'C incl. negative QPc, Clip1 to 2^bd - 1)."""
+    w, h = 176, 144
+    pics = hbd_seq(w, h, 4, seed=70 + qp, bd=bd)
+    g = jmhip.Encoder(w, h, search_mode=3, bit_depth=bd, **kw)
+    o = oracle_lib.OracleEncoder(w, h, search_mode=3, bit_depth=bd, **kw)
+    for i, pic in enumerate(pics):
+        st = jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE
+        gres, grec = g.encode(*pic, st, qp, chroma_qp_offset=cqp)
+        ores, orec = o.encode(*pic, st, qp, chroma_qp_offset=cqp)
+        assert_same(gres, grec, ores, orec, w // 16)
+        assert grec[0].dtype == np.uint16 and int(grec[0].max()) < (1 << bd)
+        g.set_reference(*orec)
+        o.set_reference(*orec)
+
+
+def test_high10_extremes():
+    """Saturated 10-bit content (0 / 1023 checkerboards): Clip1 at both ends, GPU == oracle."""
+    rng = np.random.default_rng(8)
+    w, h = 64, 48
+    pics = [tuple(np.ascontiguousarray((rng.integers(0, 2, s) * 1023).astype(np.uint16)) for s in ((h, w), (h // 2, w // 2), (h // 2, w // 2)))
+            for _ in range(3)]
+    for qp in (0, 18, 51):
+        g = jmhip.Encoder(w, h, search_range=8, search_mode=3, transform_8x8_mode=1, bit_depth=10)
+        o = oracle_lib.OracleEncoder(w, h, search_range=8, search_mode=3, transform_8x8_mode=1, bit_depth=10)
+        for i, pic in enumerate(pics):
+            st = jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE
+            gres, grec = g.encode(*pic, st, qp)
+            ores, orec = o.encode(*pic, st, qp)
+            assert_same(gres, grec, ores, orec, w // 16)
+            g.set_reference(*orec)
+            o.set_reference(*orec)
+
+
+def test_high10_config5_width_3840():
+    """Config 5's shape at its real width (3840, SliceArgument 240 = one MB row per slice), High 10
+    EPZS + 8x8 transform under large motion: GPU == oracle on every macroblock."""
+    w, h = 3840, 128
+    pics = hbd_seq(w, h, 3, seed=41, bd=10)
+    g = jmhip.Encoder(w, h, search_range=32, search_mode=3, transform_8x8_mode=1, slice_mbs=240, bit_depth=10)
+    o = oracle_lib.OracleEncoder(w, h, search_range=32, search_mode=3, transform_8x8_mode=1, slice_mbs=240, bit_depth=10)
+    for i, pic in enumerate(pics):
+        st = jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE
+        gres, grec = g.encode(*pic, st, 28)
+        ores, orec = o.encode(*pic, st, 28)
+        assert_same(gres, grec, ores, orec, w // 16)
+        g.set_reference(*orec)
+        o.set_reference(*orec)
+
+
+def test_high10_pipelined_chain_equals_sequential():
+    """16-bit pictures in flight together (device deblocking as the reference) == one at a time."""
+    w, h, n = 640, 480, 8
+    pics = hbd_seq(w, h, n, seed=3, bd=10, step=(-62, -61))
+    kw = dict(search_range=32, search_mode=3, transform_8x8_mode=1, bit_depth=10)
+    a = jmhip.Encoder(w, h, **kw)
+    b = jmhip.Encoder(w, h, pipeline_depth=1, **kw)
+    assert a.depth > 1
+    ra = run_chain(a, pics, 30, (0, 0, 0), True)
+    rb = run_chain(b, pics, 30, (0, 0, 0), False)
+    for (gres, grec, gdbk), (ores, orec, odbk) in zip(ra, rb):
+        assert_same(gres, grec, ores, orec, w // 16)
+        for x, y in zip(gdbk, odbk):
+            assert np.array_equal(x, y)
+
+
+def test_high10_rejects_other_search_modes_and_8bit_calls():
+    with pytest.raises(jmhip.JmhError):
+        jmhip.Encoder(64, 48, search_range=8, search_mode=0, bit_depth=10)
+    e = jmhip.Encoder(64, 48, search_range=8, search_mode=3, bit_depth=10)
+    y8 = np.zeros((48, 64), np.uint8), np.zeros((24, 32), np.uint8), np.zeros((24, 32), np.uint8)
+    assert e.lib.jmh_set_reference(e.ctx, 0, 0, y8[0].ctypes.data, y8[1].ctypes.data, y8[2].ctypes.data, 64, 32) == jmhip.JMH_E_UNSUPPORTED_CFG
+    big = [np.full(s, 1024, np.uint16) for s in ((48, 64), (24, 32), (24, 32))]   # out of range for 10 bits
+    assert e.lib.jmh_set_reference_u16(e.ctx, 0, 0, big[0].ctypes.data, big[1].ctypes.data, big[2].ctypes.data, 64, 32) == jmhip.JMH_E_INVALID_ARG
+
+
 # ---------------- end to end: lencod bitstream + recon, closed loop ----------------
 def run_lencod(binary, out_dir, extra):
     args = [binary, "-p", f"OutputFile={out_dir}/a.264", "-p", f"ReconFile={out_dir}/rec.yuv"]
@@ -464,6 +562,15 @@ def run_lencod(binary, out_dir, extra):
      "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "SymbolMode=1", "SliceMode=1", "SliceArgument=22"],
     ["InputFile=synthetic:34", "FramesToBeEncoded=4", "SourceWidth=176", "SourceHeight=144", "SearchRange=8",
      "ProfileIDC=77", "SymbolMode=1", "SearchMode=-1", "QPFirstFrame=0", "QPRemainingFrame=2", "WriterThreads=0"],
+    # High 10 (f5, ProfileIDC 110): the pipelined 16-bit wavefront, CAVLC and CABAC, slices
+    ["InputFile=synthetic:35", "FramesToBeEncoded=8", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchMode=3"],
+    ["InputFile=synthetic:36", "FramesToBeEncoded=6", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchMode=3",
+     "SymbolMode=1", "SliceMode=1", "SliceArgument=22", "IntraPeriod=3"],
+    ["InputFile=synthetic:37", "FramesToBeEncoded=4", "SourceWidth=200", "SourceHeight=120", "SearchRange=16",
+     "ProfileIDC=110", "SourceBitDepthLuma=9", "SourceBitDepthChroma=9", "SearchMode=3", "QPFirstFrame=2",
+     "QPRemainingFrame=4", "ChromaQPOffset=-10", "WriterThreads=0"],
 ])
 def test_lencod_bitstream_identical(extra):
     with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:

@@ -40,6 +40,9 @@ for s in "$@"; do
             cat gpurun_out/${TAG}_sad_peak.json ;;
     tests)  run tests 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread \
                 > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc ;;
+    hbd)    run hbd 600 python -u -m pytest tests -v -m gpu -k "high10 or lencod_bitstream" -p no:cacheprovider --timeout 300 \
+                --timeout-method thread > gpurun_out/${TAG}_hbd.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_hbd.log
+            [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     fast)   run fast 600 python -u -m pytest tests -x -v -m "gpu and not slow" -p no:cacheprovider --timeout 120 \
                 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_pytest.log
             [ $rc -eq 0 ] || exit $rc ;;
