@@ -27,6 +27,9 @@ k mod the device count); under torchrun WORLD_SIZE must equal --gpus.
 
 --config 3 runs BASELINE.json's config 3 instead (a variant line, not the headline metric):
 2160p synthetic, High profile, EPZS (SearchMode 3) + adaptive 8x8 transform (Transform8x8Mode 1).
+--config 5 runs config 5's hot path (a variant line): 2160p synthetic 10-bit (High 10, 16-bit samples
+in HBM), EPZS + 8x8 transform, SliceMode 1 with 240-MB slices (one MB row), RDO off -- CABAC is
+entropy coding (host, outside the ME+transform metric as for every config) and RDO-on is not built.
 
 Prints ONE JSON line (rank 0).
 """
@@ -55,6 +58,12 @@ CONFIGS = {
             workload="2160p synthetic YUV420, High profile (ProfileIDC 100), EPZS SearchMode=3 SearchRange=32, "
                      "Transform8x8Mode=1 (Intra8x8 + TransformDecision), UseHadamard=1, 7 inter block sizes, RDO off, "
                      "QP 28, IDR + {nf}-picture P sequence cycled (one independent stream per GPU)"),
+    5: dict(metric="ME+transform megapixels/sec @2160p High10 10-bit EPZS SR=32 + 8x8 transform, 240-MB slices, RDO off "
+                   "(config 5 variant)", disp=(3840, 2160), coded=(3840, 2160), search_mode=3, t8=1, bd=10, slice_mbs=240,
+            workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), EPZS SearchMode=3 "
+                     "SearchRange=32, Transform8x8Mode=1, UseHadamard=1, 7 inter block sizes, RDO off (RDOptimization=1 "
+                     "not built), CABAC on the host (entropy coding, outside the metric), QP 28, IDR + {nf}-picture P "
+                     "sequence cycled (one independent stream per GPU)"),
 }
 DISP_W, DISP_H = 1920, 1080
 W, H = 1920, 1088
@@ -63,7 +72,9 @@ SR, QP = 32, 28
 NMB = (W // 16) * (H // 16)
 # algorithmic HBM bytes per coded picture: current 1.5 B/px + reference 1.5 B/px
 # (each read once) + reconstruction 1.5 B/px and deblocked reconstruction 1.5 B/px written +
-# levels (int16 per sample) 3.0 B/px, plus per-MB side data (MVs, refs, modes, cbp) 80 B/MB
+# levels (int16 per sample) 3.0 B/px, plus per-MB side data (MVs, refs, modes, cbp) 80 B/MB; the
+# four picture terms double with 16-bit samples (bit depth > 8: 15 B/px)
+BD = 8
 BYTES_PER_PIXEL = 9.0
 SIDE_BYTES_PER_MB = 80
 BYTES_PER_FRAME = W * H * BYTES_PER_PIXEL + NMB * SIDE_BYTES_PER_MB
@@ -82,8 +93,10 @@ def load_module(name, path):
 
 def use_config(k, size=None):
     """switch the module-level workload constants to BASELINE.json config k (size: test override)"""
-    global DISP_W, DISP_H, W, H, NMB, BYTES_PER_FRAME, AD_PER_FRAME
+    global DISP_W, DISP_H, W, H, NMB, BYTES_PER_FRAME, AD_PER_FRAME, BD, BYTES_PER_PIXEL
     c = CONFIGS[k]
+    BD = c.get("bd", 8)
+    BYTES_PER_PIXEL = 6.0 * (2 if BD > 8 else 1) + 3.0
     (DISP_W, DISP_H), (W, H) = c["disp"], c["coded"]
     if size:
         DISP_W, DISP_H = size
@@ -116,9 +129,9 @@ def cpu_one_picture(seed, search_mode, t8=0, dump=None):
     import numpy as np
     import oracle_lib
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
-    frames = [jm.synth_frame(DISP_W, DISP_H, seed, i) for i in range(2)]
+    frames = [jm.synth_frame(DISP_W, DISP_H, seed, i, bit_depth=BD) for i in range(2)]
     o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
-                                 slice_mbs=SLICE_MBS)
+                                 slice_mbs=SLICE_MBS, bit_depth=BD)
     ires, irec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
     t0 = time.perf_counter()
     o.set_reference(*irec)
@@ -168,7 +181,8 @@ def cpu_baseline(config, search_mode, dump_dir):
     one = cpu_workers(1, config, search_mode, (DISP_W, DISP_H), dump_dir)[0]
     n = max(1, min(16, len(os.sched_getaffinity(0))))
     many = cpu_workers(n, config, search_mode, (DISP_W, DISP_H))
-    mode = {0: "FFS", -1: "full search", 3: "EPZS"}[search_mode] + (" + 8x8 transform" if CONFIGS[config]["t8"] else "")
+    mode = {0: "FFS", -1: "full search", 3: "EPZS"}[search_mode] + (" + 8x8 transform" if CONFIGS[config]["t8"] else "") \
+        + (f", {BD}-bit" if BD > 8 else "") + (f", {SLICE_MBS}-MB slices" if SLICE_MBS else "")
     return {"value": round(DISP_W * DISP_H / 1e6 / one, 4), "unit": "MP/s", "cores": 1, "kind": "port",
             "sample": f"one {DISP_W}x{DISP_H} P picture (coded {W}x{H}, {NMB} MBs, {mode} SR=32, QP {QP}) incl. "
                       f"quarter-pel interpolation, oracle/liboracle.so -O2 scalar, {one:.1f} s, on {cpu_model()}",
@@ -182,9 +196,9 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
     and the reconstructions with the oracle's (the dump of the cpu_baseline leg)."""
     import numpy as np
     d = np.load(dump)
-    frames = [jm.synth_frame(DISP_W, DISP_H, 0, i) for i in range(2)]
+    frames = [jm.synth_frame(DISP_W, DISP_H, 0, i, bit_depth=BD) for i in range(2)]
     g = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
-                   pipeline_depth=1, slice_mbs=SLICE_MBS)
+                   pipeline_depth=1, slice_mbs=SLICE_MBS, bit_depth=BD)
     try:
         ires, irec = g.encode(*frames[0], jm.JMH_I_SLICE, QP)
         g.set_reference(*irec)
@@ -294,12 +308,13 @@ def main():
     ap.add_argument("--frames", type=int, default=60, help="P pictures of the resident source sequence")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive / latency measurement")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
-                    help="BASELINE.json config: 2 = 1080p Baseline FFS (the headline), 3 = 2160p High EPZS + 8x8")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 5),
+                    help="BASELINE.json config: 2 = 1080p Baseline FFS (the headline), 3 = 2160p High EPZS + 8x8, "
+                         "5 = 2160p High 10 EPZS + 8x8 with 240-MB slices (RDO off)")
     ap.add_argument("--search-mode", type=int, default=None, choices=(0, -1, 3),
                     help="override the config's SearchMode (config 2 variants: -1 full search, 3 EPZS)")
-    ap.add_argument("--slice-mbs", type=int, default=0,
-                    help="SliceMode 1 with SliceArgument N macroblocks per slice (a variant line; 0: one slice)")
+    ap.add_argument("--slice-mbs", type=int, default=None,
+                    help="SliceMode 1 with SliceArgument N macroblocks per slice (0: one slice; default: the config's)")
     # test knobs (tests/test_multistream_gpu.py): a smaller picture, a final read-back picture
     ap.add_argument("--size", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--dump", default=None, help=argparse.SUPPRESS)
@@ -318,7 +333,7 @@ def main():
     pinned = pin_rank(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))) if world > 1 else None
     size = tuple(int(v) for v in args.size.split("x")) if args.size else None
     cfg = use_config(args.config, size)
-    SLICE_MBS = max(0, args.slice_mbs)
+    SLICE_MBS = max(0, cfg.get("slice_mbs", 0) if args.slice_mbs is None else args.slice_mbs)
     search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
     dist = None
     if world > 1:
@@ -331,9 +346,9 @@ def main():
     if ndev <= 0:
         raise SystemExit("bench.py: no HIP device")
     device = local % ndev
-    frames = [jm.synth_frame(DISP_W, DISP_H, rank, i) for i in range(args.frames + 1)]
+    frames = [jm.synth_frame(DISP_W, DISP_H, rank, i, bit_depth=BD) for i in range(args.frames + 1)]
     enc = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, slots=len(frames),
-                     kernel_timing=True, transform_8x8_mode=cfg["t8"], slice_mbs=SLICE_MBS)
+                     kernel_timing=True, transform_8x8_mode=cfg["t8"], slice_mbs=SLICE_MBS, bit_depth=BD)
     stream = streams.PStream(enc, frames, QP, deblock=None if args.no_deblock else (0, 0, 0))
     dt = streams.timed_run(stream, args.steps, args.warmup, dist, on_start=enc.timing)   # on_start resets the event sums
     tm = enc.timing()                                     # event sums of the timed steps only
@@ -388,7 +403,7 @@ def main():
     }
     launch_info = {
         "kernel": "k_mb_analyse" if ffs else
-                  "k_mb_me_full + k_mb_analyse" + (" + k_mb_intra8" if cfg["t8"] else "") + " (the tick's analysis launches)",
+                  ("k_mb_epzs" if search_mode == 3 else "k_mb_me_full") + " + k_mb_intra (the tick's analysis launches)",
         "avg_launch_ms": round(an_launch_ms, 5),
         "launches_per_picture": round(an_per_pic, 2),
         "mbs_per_launch": round(mbs_per_launch, 1),
@@ -411,7 +426,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8",
+        "dtype": "u16" if BD > 8 else "u8",
         "data": "synthetic",
         "config": {
             "workload": cfg["workload"].replace("{sm}", sm_name).replace("{nf}", str(args.frames))

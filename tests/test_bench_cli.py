@@ -1,0 +1,47 @@
+"""bench.py's host-side logic on CPU (no GPU): the config table, the algorithmic byte model and the
+CPU-baseline worker of every config (config 5: the 16-bit oracle path)."""
+import importlib.util
+import os
+import subprocess
+import sys
+
+import pytest
+
+from jmpaths import ensure_built
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load_bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_config_table():
+    b = load_bench()
+    c = b.use_config(2)
+    assert (b.W, b.H, b.BD, b.BYTES_PER_PIXEL, c["search_mode"]) == (1920, 1088, 8, 9.0, 0)
+    c = b.use_config(5)
+    assert (b.W, b.H, b.BD, c["slice_mbs"], c["t8"], c["search_mode"]) == (3840, 2160, 10, 240, 1, 3)
+    assert b.BYTES_PER_PIXEL == 15.0   # four 16-bit picture terms + int16 levels
+    c = b.use_config(3)
+    assert (b.BD, b.BYTES_PER_PIXEL) == (8, 9.0)
+
+
+@pytest.mark.parametrize("config,mode", [(2, 0), (3, 3), (5, 3)])
+def test_cpu_worker(config, mode, tmp_path):
+    """the cpu_baseline child on a small picture: prints its seconds; config 5 dumps 16-bit recon"""
+    ensure_built()
+    dump = tmp_path / "d.npz"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-worker", "0", str(config), str(mode), "64x48",
+                        str(dump)], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, JMH_BENCH_SLICE_MBS="4" if config == 5 else "0"))
+    assert r.returncode == 0, r.stderr
+    assert float(r.stdout.split()[-1]) > 0
+    import numpy as np
+    d = np.load(dump)
+    assert d["py"].dtype == (np.uint16 if config == 5 else np.uint8)
+    if config == 5:
+        assert int(d["py"].max()) > 255

@@ -56,11 +56,16 @@ for s in "$@"; do
             cat gpurun_out/${TAG}_benchf8.json ;;
     c3)     run c3 900 python bench.py --config 3 > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3_bench.err || exit $?
             cat gpurun_out/${TAG}_c3_bench.json ;;
+    c5)     run c5 900 python bench.py --config 5 > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5_bench.err || exit $?
+            cat gpurun_out/${TAG}_c5_bench.json ;;
     c3s)    run c3s 900 python bench.py --config 3 --slice-mbs 240 > gpurun_out/${TAG}_c3s_bench.json 2> gpurun_out/${TAG}_c3s_bench.err || exit $?
             cat gpurun_out/${TAG}_c3s_bench.json ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}" -o ${TAG} --output-format csv -- \
                 python3 "$R/bench.py" --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
             find gpurun_out/prof_${TAG} -name "*kernel_stats*" -exec cat {} \; ;;
+    profc5) run profc5 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c5" -o ${TAG}_c5 --output-format csv -- \
+                python3 "$R/bench.py" --config 5 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc5.log 2>&1 || exit $?
+            find gpurun_out/prof_${TAG}_c5 -name "*kernel_stats*" -exec cat {} \; ;;
     profc3) run profc3 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c3" -o ${TAG}_c3 --output-format csv -- \
                 python3 "$R/bench.py" --config 3 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc3.log 2>&1 || exit $?
             find gpurun_out/prof_${TAG}_c3 -name "*kernel_stats*" -exec cat {} \; ;;
