@@ -287,6 +287,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     // High 10 pictures: the EPZS wavefront (k_mb_epzs / k_mb_intra / k_mb_final on 16-bit samples)
     if (cfg->bit_depth > 8 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->rdo) return JMH_E_UNSUPPORTED_CFG;                              // RDOptimization 1: k_mb_rdo (not yet)
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     int ndev = jmh_device_count();

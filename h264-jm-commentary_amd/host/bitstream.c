@@ -399,6 +399,7 @@ struct jm_slice_writer {
     int open;                  /* header written and buffers allocated */
     jm_cabac *cab;             /* SymbolMode 1: the CABAC coder (NULL: CAVLC)                 */
     long bins;                 /* CABAC bins of the picture's slices                           */
+    long rate_checked, rate_bad;   /* RDOptimization 1: macroblocks whose RD rate was checked    */
 };
 
 /* slice_header (7.3.3) */
@@ -471,7 +472,14 @@ void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
     wctx *w = &sw->w;
     const jm_seq *s = w->s;
     int mx = a % s->mbw, my = a / s->mbw, W4 = s->mbw * 4;
-    if (sw->cab) { jm_cabac_write_mb(sw->cab, w, mx, my, r, sw->slice_p); return; }
+    if (sw->cab) {
+        jm_cabac_write_mb(sw->cab, w, mx, my, r, sw->slice_p);
+        if (s->rdo) {   /* the backend's RD rate of the chosen candidate == the bits written for it */
+            sw->rate_checked++;
+            sw->rate_bad += jm_cabac_mb_bits(sw->cab) != r->min_cost;
+        }
+        return;
+    }
     if (sw->slice_p && r->mb_type == JMH_PSKIP) {
         for (int k = 0; k < 16; k++) {
             int i = (my * 4 + (k >> 2)) * W4 + mx * 4 + (k & 3);
@@ -485,6 +493,11 @@ void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
     }
     if (sw->slice_p) { jm_put_ue(sw->b, sw->skip_run); sw->skip_run = 0; }
     write_mb(sw->b, w, mx, my, r, sw->slice_p);
+}
+
+void jm_slice_rate_check(const jm_slice_writer *sw, long *checked, long *bad) {
+    *checked = sw ? sw->rate_checked : 0;
+    *bad = sw ? sw->rate_bad : 0;
 }
 
 long jm_slice_end(jm_slice_writer *sw) {

@@ -39,6 +39,9 @@ void jm_cabac_slice_start(jm_cabac *c, jm_bits *b, int slice_type, int qp);
 /* one macroblock (mb_skip_flag in P slices, macroblock_layer), end_of_slice_flag of the
    previous one first */
 void jm_cabac_write_mb(jm_cabac *c, wctx *w, int mx, int my, const jmh_mb_result *r, int slice_p);
+/* bits of the last jm_cabac_write_mb (arienco_bits_written delta, no end_of_slice_flag): the RD rate
+   of that macroblock (RDOptimization 1 reports it in jmh_mb_result.min_cost) */
+long jm_cabac_mb_bits(const jm_cabac *c);
 /* end_of_slice_flag = 1 of the slice's last macroblock, flush (its last bit is the
    rbsp_stop_one_bit), alignment; returns the slice's bin count */
 long jm_cabac_slice_end(jm_cabac *c);

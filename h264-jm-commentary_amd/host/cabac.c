@@ -146,6 +146,8 @@ struct jm_cabac {
     uint32_t low, range;
     int outstanding, first;
     long bins, pic_bins;
+    long nbits;         /* arienco_bits_written: one per renormalisation step and bypass bin     */
+    long mb_bits;       /* of the last macroblock (mb_skip_flag .. residual, no end_of_slice_flag) */
     uint8_t state[NCTX], mps[NCTX];
     cmb *mb;
     int16_t *mvd;       /* per 4x4 of the picture [2]: mvd_l0 of the partition covering it      */
@@ -179,6 +181,7 @@ static void renorm(jm_cabac *c) {
         else { c->low -= 256; c->outstanding++; }
         c->range <<= 1;
         c->low <<= 1;
+        c->nbits++;
     }
 }
 static void enc(jm_cabac *c, int ctx, int bin) {
@@ -200,6 +203,7 @@ static void enc_bypass(jm_cabac *c, int bin) {
     else if (c->low < 512) put_bit(c, 0);
     else { c->low -= 512; c->outstanding++; }
     c->bins++;
+    c->nbits++;
 }
 static void enc_terminate(jm_cabac *c, int bin) {
     c->range -= 2;
@@ -358,11 +362,19 @@ static void level8x8(const jmh_mb_result *r, int b8, int16_t *out) {
     }
 }
 
+static void write_mb_body(jm_cabac *c, wctx *w, int mx, int my, const jmh_mb_result *r, int slice_p);
 void jm_cabac_write_mb(jm_cabac *c, wctx *w, int mx, int my, const jmh_mb_result *r, int slice_p) {
-    const jm_seq *s = w->s;
-    const int a = my * s->mbw + mx, W4 = s->mbw * 4;
     if (c->pending_eos) enc_terminate(c, 0);         /* end_of_slice_flag of the previous MB */
     c->pending_eos = 1;
+    const long nb0 = c->nbits;
+    write_mb_body(c, w, mx, my, r, slice_p);
+    c->mb_bits = c->nbits - nb0;
+}
+long jm_cabac_mb_bits(const jm_cabac *c) { return c->mb_bits; }
+
+static void write_mb_body(jm_cabac *c, wctx *w, int mx, int my, const jmh_mb_result *r, int slice_p) {
+    const jm_seq *s = w->s;
+    const int a = my * s->mbw + mx, W4 = s->mbw * 4;
     const int na = nb_mb(w, mx, my, 1), nbb = nb_mb(w, mx, my, 0);
     const cmb *A = na >= 0 ? &c->mb[na] : NULL, *B = nbb >= 0 ? &c->mb[nbb] : NULL;
     cmb *m = &c->mb[a];

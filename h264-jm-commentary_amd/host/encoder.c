@@ -26,6 +26,16 @@ int jm_lambda_rdo_off(int qp) {
     return QP2QUANT[i < 0 ? 0 : i];
 }
 
+/* RDOptimization 1 (rdopt.c encode_one_macroblock [J], no B pictures): lambda_mode = 0.85 *
+   2^((QP - SHIFT_QP) / 3) at QP + QpBdOffsetY (JM >= 13 init_lambda's bitdepth_luma_qp_scale),
+   lambda_motion = sqrt(lambda_mode), LAMBDA_FACTOR = (int)(65536 * lambda_motion + 0.5) */
+double jm_lambda_rdo_on(int qp, int bit_depth, int *lambda_factor) {
+    const int qpbd = bit_depth > 8 ? 6 * (bit_depth - 8) : 0;
+    const double lam = 0.85 * pow(2.0, (double)(qp + qpbd - 12) / 3.0);
+    if (lambda_factor) *lambda_factor = (int)(65536.0 * sqrt(lam) + 0.5);
+    return lam;
+}
+
 /* squared error summed in integers (per row in 32 bits: 65025 * w < 2^32 for w < 66051; 64-bit
    rows at High 10), so the value equals JM's double accumulation of integer squares exactly; the
    peak is (1 << bit depth) - 1 (JM >= 10 img->max_imgpel_value [J]) */
@@ -83,6 +93,10 @@ static int encode_picture_slices(jm86_img *im, const jm_seq *s, const jm_slice *
     for (int first = 0; first < nmb; first += step) {
         encode_one_slice(s, first);
         if (first + step >= nmb) {
+            long chk, bad;
+            jm_slice_rate_check(w, &chk, &bad);
+            im->rate_checked += chk;
+            im->rate_mismatches += bad;
             bins = jm_slice_end(w);
         } else {
             jm_bits_init(&rbsp[k ^ 1]);
@@ -228,6 +242,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
     s.bit_depth = inp->bit_depth_luma;
     const int bd = inp->bit_depth_luma;
     s.cabac_init_idc = inp->model_number;
+    s.rdo = inp->rdopt;
 
     FILE *fin = NULL, *fout = NULL, *frec = NULL;
     uint64_t seed = 0;
@@ -322,6 +337,8 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         if (frec) jm_write_yuv_frame(frec, &fj_->rec, inp->width, inp->height);                     \
         st->psnr_y += fj_->py; st->psnr_u += fj_->pu; st->psnr_v += fj_->pv;                          \
         st->bits += fj_->pic_bits;                                                                  \
+        im.rate_checked += fj_->im.rate_checked; im.rate_mismatches += fj_->im.rate_mismatches;     \
+        fj_->im.rate_checked = fj_->im.rate_mismatches = 0;                                         \
         st->frames++;                                                                              \
         st->entropy_ms += fj_->write_ms;                                                            \
         write_ms += fj_->write_ms;                                                                  \
@@ -417,6 +434,7 @@ int jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *
         fp->slice_type = p->is_i ? JMH_I_SLICE : JMH_P_SLICE;
         fp->qp = p->is_i ? inp->qp_i : inp->qp_p;
         fp->lambda_mode = fp->lambda_motion = jm_lambda_rdo_off(fp->qp);
+        if (inp->rdopt) fp->lambda_rd = jm_lambda_rdo_on(fp->qp, inp->bit_depth_luma, &fp->lambda_factor_rd);
         fp->chroma_qp_offset = inp->chroma_qp_offset;
         if (dev_dbk) {   /* same parameters jm_deblock_picture derives from the slice header */
             fp->deblock = 1;
@@ -476,6 +494,12 @@ cleanup:
                      "searches), %d inconsistent with the wavefront decision\n",
                 im.surface_checked, im.surface_searches, im.surface_mismatches);
     if (!st_ret && im.surface_mismatches) st_ret = JMH_E_STATE;
+    st->rate_checked = im.rate_checked;
+    st->rate_mismatches = im.rate_mismatches;
+    if (log && inp->rdopt)
+        fprintf(log, " RD rate check: %ld macroblocks, %ld whose RD rate differs from the CABAC bits written\n",
+                im.rate_checked, im.rate_mismatches);
+    if (!st_ret && im.rate_mismatches) st_ret = JMH_E_STATE;
     jm86_free(&im);
     if (st->frames) { st->psnr_y /= st->frames; st->psnr_u /= st->frames; st->psnr_v /= st->frames; }
     if (log && st->frames)

@@ -35,7 +35,7 @@ typedef struct jm_input {
     int  num_ref_frames;       /* NumberReferenceFrames                                       */
     int  restrict_search_range;/* RestrictSearchRange                                         */
     int  inter_search[8];      /* InterSearch16x16 .. InterSearch4x4 ([1..7])                 */
-    int  rdopt;                /* RDOptimization (must be 0)                                  */
+    int  rdopt;                /* RDOptimization: 0, or 1 with SymbolMode 1 (CABAC rate)       */
     int  profile_idc;          /* ProfileIDC (66 Baseline, 100 High)                          */
     int  transform_8x8_mode;   /* Transform8x8Mode (0, 1; needs ProfileIDC 100)               */
     int  jm_version;           /* JMVersion: 8 (JM 8.6 rules, default) or >= 10 (JM >= 10
@@ -134,6 +134,8 @@ typedef struct jm_seq {
     int bit_depth;             /* BitDepthLuma = BitDepthChroma (High 10: 9 / 10)              */
     int entropy_coding;        /* PPS entropy_coding_mode_flag: 0 CAVLC, 1 CABAC (SymbolMode)  */
     int cabac_init_idc;        /* cabac_init_idc of P slices (FixedModelNumber)                */
+    int rdo;                   /* RDOptimization 1: the writer checks each macroblock's RD rate
+                                  (jmh_mb_result.min_cost) against the CABAC bits it writes     */
 } jm_seq;
 
 /* NAL unit (Annex B start code + emulation prevention) appended to out */
@@ -154,6 +156,8 @@ jm_slice_writer *jm_slice_begin(jm_bits *rbsp, const jm_seq *s, const jm_slice *
 void jm_slice_write_mb(jm_slice_writer *w, int mb_addr, const jmh_mb_result *r);
 /* closes the last slice; returns the CABAC bins of the picture's slices (0 with CAVLC) */
 long jm_slice_end(jm_slice_writer *w);
+/* RDOptimization 1 + CABAC: macroblocks written so far and those whose RD rate differed */
+void jm_slice_rate_check(const jm_slice_writer *w, long *checked, long *bad);
 /* close the current slice's data in its rbsp and start the next slice (header into rbsp), keeping
    the picture's neighbour buffers (SliceMode 1: one writer per picture, one rbsp per slice) */
 void jm_slice_restart(jm_slice_writer *w, jm_bits *rbsp, const jm_slice *sl);
@@ -196,6 +200,7 @@ typedef struct jm_stats {
     long bits;
     double psnr_y, psnr_u, psnr_v;   /* averages                                              */
     int surface_checked, surface_searches, surface_mismatches;   /* JMCallSurface (jm86.c)      */
+    long rate_checked, rate_mismatches;                          /* RDOptimization 1 (writer)   */
 } jm_stats;
 
 /* ---- the JM 8.6 call surface (host/jm86.c) ------------------------------------------------
@@ -233,6 +238,7 @@ typedef struct jm86_img {
     uint8_t *enc_imgY;                /* enc_picture->imgY (dct_luma's reconstruction)          */
     int surface_searches;             /* BlockMotionSearch calls made (statistics)              */
     int surface_checked, surface_mismatches;   /* P MBs checked / found inconsistent            */
+    long rate_checked, rate_mismatches;        /* RDOptimization 1: MB rates checked by the writer */
     const jm_input *input;
     jm_backend *be;
     jm_slice_writer *writer;
@@ -256,6 +262,7 @@ int  dct_luma(int block_x, int block_y, int *coeff_cost, int old_intra_mode);
 
 void jm_fill_config(const jm_input *inp, jmh_config *cfg);
 int  jm_lambda_rdo_off(int qp);    /* QP2QUANT[max(0,qp-12)] */
+double jm_lambda_rdo_on(int qp, int bit_depth, int *lambda_factor);   /* 0.85*2^((qp+QpBdOffsetY-12)/3) */
 /* encode the whole sequence: returns 0 or a negative status */
 int  jm_encode_sequence(const jm_input *inp, jm_backend *be, jm_stats *st, FILE *log);
 

@@ -18,7 +18,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 JMH_OK = 0
 JMH_E_INVALID_ARG, JMH_E_HIP, JMH_E_OOM, JMH_E_UNSUPPORTED_CFG, JMH_E_STATE, JMH_E_NO_DEVICE = -1, -2, -3, -4, -5, -6
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 11
+JMH_ABI_VERSION = 12
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -31,6 +31,15 @@ def lambda_rdo_off(qp):
     return QP2QUANT[max(0, qp - 12)]
 
 
+def lambda_rdo_on(qp, bit_depth=8):
+    """RDOptimization 1 (host/encoder.c jm_lambda_rdo_on): (lambda_mode, LAMBDA_FACTOR(sqrt(lambda_mode)))
+    with lambda_mode = 0.85 * 2^((qp + QpBdOffsetY - 12) / 3) -- the same libm pow / sqrt as the C host."""
+    import math
+    qpbd = 6 * (bit_depth - 8) if bit_depth > 8 else 0
+    lam = 0.85 * math.pow(2.0, (qp + qpbd - 12) / 3.0)
+    return lam, int(65536.0 * math.sqrt(lam) + 0.5)
+
+
 class JmhConfig(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("search_range", ctypes.c_int32), ("search_mode", ctypes.c_int32),
@@ -40,7 +49,8 @@ class JmhConfig(ctypes.Structure):
                 ("flags", ctypes.c_int32), ("pipeline_depth", ctypes.c_int32),
                 ("transform_8x8_mode", ctypes.c_int32), ("jm_version", ctypes.c_int32),
                 ("quant_offset", ctypes.c_int32 * 2), ("epzs_dual_refinement", ctypes.c_int32),
-                ("slice_mbs", ctypes.c_int32), ("bit_depth", ctypes.c_int32)]
+                ("slice_mbs", ctypes.c_int32), ("bit_depth", ctypes.c_int32),
+                ("rdo", ctypes.c_int32), ("symbol_mode", ctypes.c_int32)]
 
 
 class JmhFrameParams(ctypes.Structure):
@@ -48,7 +58,8 @@ class JmhFrameParams(ctypes.Structure):
                 ("lambda_mode", ctypes.c_int32), ("lambda_motion", ctypes.c_int32),
                 ("chroma_qp_offset", ctypes.c_int32), ("deblock", ctypes.c_int32),
                 ("lf_disable", ctypes.c_int32), ("lf_alpha_div2", ctypes.c_int32),
-                ("lf_beta_div2", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("lf_beta_div2", ctypes.c_int32), ("lambda_factor_rd", ctypes.c_int32),
+                ("lambda_rd", ctypes.c_double)]
 
 
 class JmhTiming(ctypes.Structure):
@@ -163,7 +174,7 @@ def _ptr(a):
 def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
                 restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False,
                 pipeline_depth=0, transform_8x8_mode=0, jm_version=8, quant_offset=(682, 342), epzs_dual_refinement=0, slice_mbs=0,
-                bit_depth=8):
+                bit_depth=8, rdo=0, symbol_mode=None):
     """jm_version >= 10 selects the JM >= 10 quantisation rounding with the flat OffsetMatrix
     entries quant_offset = (I slices, P slices) at OffsetBits 11 (docs/JM_SEMANTICS.md item 45)."""
     cfg = JmhConfig()
@@ -180,16 +191,21 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     cfg.epzs_dual_refinement = epzs_dual_refinement
     cfg.slice_mbs = slice_mbs
     cfg.bit_depth = bit_depth
+    cfg.rdo = rdo
+    cfg.symbol_mode = (1 if rdo else 0) if symbol_mode is None else symbol_mode
     if jm_version >= 10:
         cfg.quant_offset[0], cfg.quant_offset[1] = quant_offset
     return cfg
 
 
-def frame_params(slice_type, qp, chroma_qp_offset=0, deblock=None):
-    """deblock: None (no device deblocking) or (disable_idc, alpha_div2, beta_div2)."""
+def frame_params(slice_type, qp, chroma_qp_offset=0, deblock=None, rdo=0, bit_depth=8):
+    """deblock: None (no device deblocking) or (disable_idc, alpha_div2, beta_div2); rdo: fill the
+    RDOptimization 1 lambdas."""
     fp = JmhFrameParams()
     fp.slice_type, fp.qp = slice_type, qp
     fp.lambda_mode = fp.lambda_motion = lambda_rdo_off(qp)
+    if rdo:
+        fp.lambda_rd, fp.lambda_factor_rd = lambda_rdo_on(qp, bit_depth)
     fp.chroma_qp_offset = chroma_qp_offset
     if deblock is not None:
         fp.deblock = 1
@@ -242,7 +258,7 @@ class Encoder:
         _check(getattr(self.lib, fn)(self.ctx, 0, 0, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2), fn)
 
     def encode(self, y, u, v, slice_type, qp, chroma_qp_offset=0, deblock=None):
-        fp = frame_params(slice_type, qp, chroma_qp_offset, deblock)
+        fp = frame_params(slice_type, qp, chroma_qp_offset, deblock, self.cfg.rdo, self.cfg.bit_depth)
         y, u, v = self._planes(y, u, v)
         fn = "jmh_frame_submit" + self.sfx
         _check(getattr(self.lib, fn)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2, ctypes.byref(fp)), fn)
@@ -251,7 +267,7 @@ class Encoder:
 
     # ---- pipelined pictures (jmh_frame_push / jmh_frame_pop) ----
     def push(self, y, u, v, slice_type, qp, chroma_qp_offset=0, deblock=None):
-        fp = frame_params(slice_type, qp, chroma_qp_offset, deblock)
+        fp = frame_params(slice_type, qp, chroma_qp_offset, deblock, self.cfg.rdo, self.cfg.bit_depth)
         y, u, v = self._planes(y, u, v)
         fn = "jmh_frame_push" + self.sfx
         _check(getattr(self.lib, fn)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2, ctypes.byref(fp)), fn)
@@ -298,7 +314,7 @@ class Encoder:
         _check(self.lib.jmh_set_reference_slot(self.ctx, slot), "jmh_set_reference_slot")
 
     def encode_slot(self, slot, slice_type, qp, deblock=None):
-        fp = frame_params(slice_type, qp, deblock=deblock)
+        fp = frame_params(slice_type, qp, deblock=deblock, rdo=self.cfg.rdo, bit_depth=self.cfg.bit_depth)
         _check(self.lib.jmh_encode_slot(self.ctx, slot, ctypes.byref(fp)), "jmh_encode_slot")
 
     def sync(self):

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 11
+#define JMH_ABI_VERSION 12
 #define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
 #define JMH_QOFFSET_MAX 2047  /* jmh_config.quant_offset: OffsetBits 11 (1 << 11 = a whole step)    */
 
@@ -114,6 +114,14 @@ typedef struct jmh_config {
                                        at QP + QpBdOffset, Clip1 to (1 << bit_depth) - 1, deblocking
                                        thresholds scaled by 1 << (bit_depth - 8); docs/JM_SEMANTICS.md
                                        items 49-52)                                                  */
+    int32_t rdo;                    /* RDOptimization: 0 off (the cost-based decision of rdopt.c's RDO-off
+                                       branch), 1 on: encode_one_macroblock's rate-distortion loop
+                                       (RDCost_for_macroblocks / RDCost_for_8x8blocks / RDCost_for_4x4
+                                       IntraBlocks [J]: SSD + lambda_rd * rate, the rate from the CABAC
+                                       coding state of the slice, csrc/jmh_cabac_rate.h); needs
+                                       symbol_mode 1, SearchMode 3 and transform_8x8_mode 0
+                                       (docs/JM_SEMANTICS.md items 53-60)                             */
+    int32_t symbol_mode;            /* SymbolMode: 0 CAVLC, 1 CABAC (the RD rate's entropy coder)     */
 } jmh_config;
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */
@@ -135,7 +143,10 @@ typedef struct jmh_frame_params {
     int32_t lf_disable;        /* disable_deblocking_filter_idc (1: copy, no filtering)          */
     int32_t lf_alpha_div2;     /* slice_alpha_c0_offset_div2                                     */
     int32_t lf_beta_div2;      /* slice_beta_offset_div2                                         */
-    int32_t reserved[3];
+    int32_t lambda_factor_rd;  /* RDO on: LAMBDA_FACTOR(lambda_motion) = (int)(65536 * sqrt(lambda_rd)
+                                  + 0.5), the motion searches' lambda (computed on the host, libm)   */
+    double  lambda_rd;         /* RDO on: lambda_mode = 0.85 * 2^((QP + QpBdOffsetY - 12) / 3) (P and
+                                  I slices, no B pictures), the J = D + lambda * R multiplier        */
 } jmh_frame_params;
 
 /* ---- per-macroblock result (what encode_one_macroblock leaves behind) ------------------- */

@@ -22,26 +22,12 @@
 #include <stdlib.h>
 #include "jmo_internal.h"
 
-typedef struct {
-    jmo_ctx *c;
-    int mbx, mby, pix_x, pix_y, mb_addr;
-    int lambda;                /* lambda_mode == lambda_motion (RDO off, integer)        */
-    int lf;                    /* LAMBDA_FACTOR(lambda) = 65536*lambda                     */
-    int slice_p;
-    pel org[256];              /* imgY_org of the MB                                       */
-    pel orgc[2][64];
-    /* FFS state (SetupFastFullPelSearch) */
-    int setup_done, scx, scy, pos_00;
-    int16_t all_mv[8][16][2];  /* img->all_mv[.][.][LIST_0][ref 0][blocktype]               */
-    int motion_cost[8][4];
-    int skip_mv[2];
-} mbs;
 
 /* ====================================================================================== */
 /*  neighbour access (getLuma4x4Neighbour / getNeighbour, H.264 6.4.11/6.4.12; neighbours
  *  outside the current slice are unavailable, 6.4.8 / JM_SEMANTICS item 47) */
 /* ====================================================================================== */
-static int nb4(const mbs *s, int xN, int yN, int *idx) {
+int jmo_nb4(const mbs *s, int xN, int yN, int *idx) {
     const jmo_ctx *c = s->c;
     int mx, my;
     if (yN > 15) return 0;
@@ -59,10 +45,10 @@ static void mvp_neighbours(const mbs *s, int block_x, int block_y, int bsx, int 
                            int *av_c, int *ia, int *ib, int *ic) {
     int mb_x = 4 * block_x, mb_y = 4 * block_y, id = 0;
     (void)bsy;
-    *av_a = nb4(s, mb_x - 1, mb_y, ia);
-    *av_b = nb4(s, mb_x, mb_y - 1, ib);
-    *av_c = nb4(s, mb_x + bsx, mb_y - 1, ic);
-    int av_d = nb4(s, mb_x - 1, mb_y - 1, &id);
+    *av_a = jmo_nb4(s, mb_x - 1, mb_y, ia);
+    *av_b = jmo_nb4(s, mb_x, mb_y - 1, ib);
+    *av_c = jmo_nb4(s, mb_x + bsx, mb_y - 1, ic);
+    int av_d = jmo_nb4(s, mb_x - 1, mb_y - 1, &id);
     if (mb_y > 0) {                       /* C inside the MB but later in decoding order */
         if (mb_x < 8) {
             if (mb_y == 8) { if (bsx == 16) *av_c = 0; }
@@ -73,7 +59,7 @@ static void mvp_neighbours(const mbs *s, int block_x, int block_y, int bsx, int 
 }
 
 /* SetMotionVectorPredictor [J] / H.264 8.4.1.3 (list 0). block_x/y in 4x4 units. */
-static void set_mvp(const mbs *s, int pmv[2], int ref, int block_x, int block_y, int bsx, int bsy) {
+void jmo_set_mvp(const mbs *s, int pmv[2], int ref, int block_x, int block_y, int bsx, int bsy) {
     const jmo_ctx *c = s->c;
     int ia = 0, ib = 0, ic = 0, av_a, av_b, av_c;
     mvp_neighbours(s, block_x, block_y, bsx, bsy, &av_a, &av_b, &av_c, &ia, &ib, &ic);
@@ -136,16 +122,16 @@ void jmo_mvp_median(int av_a, int rL, int ax, int ay, int av_b, int rU, int bx, 
 }
 
 /* FindSkipModeMotionVector [J] / H.264 8.4.1.1 */
-static void find_skip_mv(mbs *s) {
+void jmo_find_skip_mv(mbs *s) {
     const jmo_ctx *c = s->c;
     int ia = 0, ib = 0;
-    int av_a = nb4(s, -1, 0, &ia), av_b = nb4(s, 0, -1, &ib);
+    int av_a = jmo_nb4(s, -1, 0, &ia), av_b = jmo_nb4(s, 0, -1, &ib);
     int zl = !av_a ? 1 : (c->refidx[ia] == 0 && c->mv[2 * ia] == 0 && c->mv[2 * ia + 1] == 0);
     int za = !av_b ? 1 : (c->refidx[ib] == 0 && c->mv[2 * ib] == 0 && c->mv[2 * ib + 1] == 0);
     if (za || zl) { s->skip_mv[0] = s->skip_mv[1] = 0; }
     else {
         int pmv[2];
-        set_mvp(s, pmv, 0, 0, 0, 16, 16);
+        jmo_set_mvp(s, pmv, 0, 0, 0, 16, 16);
         s->skip_mv[0] = pmv[0]; s->skip_mv[1] = pmv[1];
     }
 }
@@ -193,7 +179,7 @@ static void ffs_setup_at(mbs *s, int scx, int scy) {
 }
 static void ffs_setup(mbs *s) {
     int sr = s->c->sr, pmv[2];
-    set_mvp(s, pmv, 0, 0, 0, 16, 16);
+    jmo_set_mvp(s, pmv, 0, 0, 0, 16, 16);
     ffs_setup_at(s, iclip(-sr, sr, pmv[0] / 4), iclip(-sr, sr, pmv[1] / 4));
 }
 
@@ -242,7 +228,7 @@ static int full_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int pm
     int max_pos = (2 * range + 1) * (2 * range + 1);
     int pic_x = s->pix_x + 4 * bx4, pic_y = s->pix_y + 4 * by4;
     int cxa = pic_x + *mvx, cya = pic_y + *mvy;
-    int check_00 = (blocktype == 1 && s->slice_p);
+    int check_00 = (blocktype == 1 && s->slice_p && !s->rdo);   /* !input->rdopt [J] */
     int min_mcost = BIGCOST, best_pos = 0;
     for (int pos = 0; pos < max_pos; pos++) {
         int cx = cxa + c->spiral_x[pos], cy = cya + c->spiral_y[pos];
@@ -390,7 +376,7 @@ static int subpel_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int 
     jmo_ctx *c = s->c;
     int had = c->cfg.use_hadamard;
     int w4 = jmo_blc_size[blocktype][0] >> 2, h4 = jmo_blc_size[blocktype][1] >> 2;
-    int check_position0 = (blocktype == 1 && *mvx == 0 && *mvy == 0 && had && s->slice_p);
+    int check_position0 = (blocktype == 1 && *mvx == 0 && *mvy == 0 && had && s->slice_p && !s->rdo);
     int min_pos2 = had ? 0 : 1, max_pos2 = 9;
     int mx = *mvx * 4, my = *mvy * 4, best_pos = 0;
     for (int pos = min_pos2; pos < max_pos2; pos++) {          /* half-pel */
@@ -420,7 +406,7 @@ static int block_motion_search(mbs *s, int blocktype, int bx4, int by4, int rang
     jmo_ctx *c = s->c;
     int bsx = jmo_blc_size[blocktype][0], bsy = jmo_blc_size[blocktype][1];
     int pmv[2];
-    set_mvp(s, pmv, 0, bx4, by4, bsx, bsy);
+    jmo_set_mvp(s, pmv, 0, bx4, by4, bsx, bsy);
     int mvx = iclip(-range, range, pmv[0] / 4), mvy = iclip(-range, range, pmv[1] / 4);
     int min_mcost;
     if (c->cfg.search_mode == 0) min_mcost = ffs_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
@@ -432,6 +418,8 @@ static int block_motion_search(mbs *s, int blocktype, int bx4, int by4, int rang
         for (int x = 0; x < (bsx >> 2); x++) {
             s->all_mv[blocktype][(by4 + y) * 4 + bx4 + x][0] = (int16_t)mvx;
             s->all_mv[blocktype][(by4 + y) * 4 + bx4 + x][1] = (int16_t)mvy;
+            s->pmv[blocktype][(by4 + y) * 4 + bx4 + x][0] = (int16_t)pmv[0];   /* for the RD rate's mvd */
+            s->pmv[blocktype][(by4 + y) * 4 + bx4 + x][1] = (int16_t)pmv[1];
         }
     return min_mcost;
 }
@@ -477,7 +465,7 @@ int jmo_block_motion_search(jmo_ctx *c, int n, const jmh_block_search *req, jmh_
     return JMH_OK;
 }
 
-static void write_enc_mv(mbs *s, int bx4, int by4, int w4, int h4, const int16_t (*mv)[2]) {
+void jmo_write_enc_mv(mbs *s, int bx4, int by4, int w4, int h4, const int16_t (*mv)[2]) {
     jmo_ctx *c = s->c;
     int W4 = c->W >> 2;
     for (int y = 0; y < h4; y++)
@@ -491,7 +479,7 @@ static void write_enc_mv(mbs *s, int bx4, int by4, int w4, int h4, const int16_t
 }
 
 /* PartitionMotionSearch [J] (list 0, single reference) */
-static void partition_motion_search(mbs *s, int blocktype, int block8x8) {
+void jmo_partition_motion_search(mbs *s, int blocktype, int block8x8) {
     static const int bx0[5][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 2, 0, 0}, {0, 2, 0, 2}};
     static const int by0[5][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 2, 0, 0}, {0, 0, 0, 0}, {0, 0, 2, 2}};
     int parttype = blocktype < 4 ? blocktype : 4;
@@ -502,7 +490,7 @@ static void partition_motion_search(mbs *s, int blocktype, int block8x8) {
     for (int v = by0[parttype][block8x8]; v < by0[parttype][block8x8] + step_v0; v += step_v)
         for (int h = bx0[parttype][block8x8]; h < bx0[parttype][block8x8] + step_h0; h += step_h) {
             s->motion_cost[blocktype][block8x8] += block_motion_search(s, blocktype, h, v, range);
-            write_enc_mv(s, h, v, step_h, step_v, s->all_mv[blocktype]);
+            jmo_write_enc_mv(s, h, v, step_h, step_v, s->all_mv[blocktype]);
         }
 }
 
@@ -510,7 +498,7 @@ static void partition_motion_search(mbs *s, int blocktype, int block8x8) {
 /*  transform / quantisation                                                               */
 /* ====================================================================================== */
 /* dct_luma [J]: 4x4 forward, quant (deadzone qp_const), scan, dequant, inverse, recon */
-static int dct_luma4x4(const int32_t resid[16], const pel *pred, int ps, int qp, int intra_round,
+int jmo_dct_luma4x4(const int32_t resid[16], const pel *pred, int ps, int qp, int intra_round,
                        int16_t levels[16], int *coeff_cost, pel *rec, int rs, int maxv) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS + qp_per;
     int qp_const = jmo_qround(intra_round, q_bits);
@@ -544,7 +532,7 @@ int jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, in
         int cc = 0;
         pel p[16], o[16];
         for (int k = 0; k < 16; k++) { r[k] = resid[16 * i + k]; p[k] = pred[16 * i + k]; }
-        nonzero[i] = dct_luma4x4(r, p, 4, qp, intra, levels + 16 * i, &cc, o, 4, 255);
+        nonzero[i] = jmo_dct_luma4x4(r, p, 4, qp, intra, levels + 16 * i, &cc, o, 4, 255);
         for (int k = 0; k < 16; k++) recon[16 * i + k] = (pel)o[k];
         coeff_cost[i] = cc;
     }
@@ -556,7 +544,7 @@ int jmo_tq4x4_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, in
  * for 4x4 (docs/JM_SEMANTICS.md item 1), 8x8 frame zig-zag, COEFF_COST8x8 on the 64-scan runs,
  * dequantisation by the normative 8.5.13.1 formula on the signed level (flat scaling lists),
  * reconstruction clip((r + (pred<<6) + 32) >> 6).  levels[64] in scan order. */
-static int dct_luma8x8(const int32_t resid[64], const pel *pred, int ps, int qp, int intra_round,
+int jmo_dct_luma8x8(const int32_t resid[64], const pel *pred, int ps, int qp, int intra_round,
                        int16_t levels[64], int *coeff_cost, pel *rec, int rs, int maxv) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS_8 + qp_per;
     int qp_const = jmo_qround(intra_round, q_bits);
@@ -593,7 +581,7 @@ int jmo_tq8x8_batch(int n, const int16_t *resid, const uint8_t *pred, int qp, in
         int cc = 0;
         pel p[64], o[64];
         for (int k = 0; k < 64; k++) { r[k] = resid[64 * i + k]; p[k] = pred[64 * i + k]; }
-        nonzero[i] = dct_luma8x8(r, p, 8, qp, intra, levels + 64 * i, &cc, o, 8, 255);
+        nonzero[i] = jmo_dct_luma8x8(r, p, 8, qp, intra, levels + 64 * i, &cc, o, 8, 255);
         for (int k = 0; k < 64; k++) recon[64 * i + k] = (pel)o[k];
         coeff_cost[i] = cc;
     }
@@ -605,7 +593,7 @@ void jmo_forward8x8(const int32_t *in, int32_t *out) {
 }
 
 /* store an 8x8 block's scan-order levels as CAVLC's four interleaved 4x4 blocks (7.3.5.3.2) */
-static void put_levels8(int16_t luma[16][16], int b8, const int16_t lev[64]) {
+void jmo_put_levels8(int16_t luma[16][16], int b8, const int16_t lev[64]) {
     for (int j = 0; j < 4; j++) {
         int blk = (2 * (b8 >> 1) + (j >> 1)) * 4 + 2 * (b8 & 1) + (j & 1);
         for (int k = 0; k < 16; k++) luma[blk][k] = lev[4 * k + j];
@@ -614,7 +602,7 @@ static void put_levels8(int16_t luma[16][16], int b8, const int16_t lev[64]) {
 
 /* dct_chroma [J] for one component: 4 4x4 AC blocks + 2x2 DC; returns updated cr_cbp.
  * resid/pred raster 8x8.  DC reconstruction follows H.264 8.5.11.2 exactly. */
-static int dct_chroma(const int32_t resid[64], const pel pred[64], int qpc, int intra_round,
+int jmo_dct_chroma(const int32_t resid[64], const pel pred[64], int qpc, int intra_round,
                       int cr_cbp, int16_t dc_out[4], int16_t ac_out[4][16], pel rec[64], int maxv) {
     int qp_per = qpc / 6, qp_rem = qpc % 6, q_bits = Q_BITS + qp_per;
     int qp_const = jmo_qround(intra_round, q_bits);
@@ -672,7 +660,7 @@ static int dct_chroma(const int32_t resid[64], const pel pred[64], int qpc, int 
 }
 
 /* dct_luma_16x16 [J]: returns luma cbp (15 if any AC level, else 0) */
-static int dct_luma_16x16(const int32_t resid[256], const pel pred[256], int qp, int rnd,
+int jmo_dct_luma_16x16(const int32_t resid[256], const pel pred[256], int qp, int rnd,
                           int16_t dc_out[16], int16_t ac_out[16][16], int *cbp_blk, pel rec[256], int maxv) {
     int qp_per = qp / 6, qp_rem = qp % 6, q_bits = Q_BITS + qp_per;
     int qp_const = jmo_qround(rnd, q_bits), qp_const2 = qp_const << 1;   /* JM 8.6: always / 3 */
@@ -739,7 +727,7 @@ static int dct_luma_16x16(const int32_t resid[256], const pel pred[256], int qp,
 /* ====================================================================================== */
 /*  intra prediction (H.264 8.3)                                                            */
 /* ====================================================================================== */
-static int mb_avail(const mbs *s, int dmx, int dmy) {
+int jmo_mb_avail(const mbs *s, int dmx, int dmy) {
     int mx = s->mbx + dmx, my = s->mby + dmy;
     return mx >= 0 && my >= 0 && mx < s->c->mbw && my < s->c->mbh &&
            (my < s->mby || (my == s->mby && mx < s->mbx)) &&
@@ -748,14 +736,14 @@ static int mb_avail(const mbs *s, int dmx, int dmy) {
 /* luma sample availability at MB-relative (x,y) for intra prediction */
 static int luma_avail(const mbs *s, int x, int y) {
     if (y > 15) return 0;
-    if (x < 0) return mb_avail(s, -1, y < 0 ? -1 : 0);
-    if (x <= 15) return y < 0 ? mb_avail(s, 0, -1) : 1;
-    return y < 0 ? mb_avail(s, 1, -1) : 0;
+    if (x < 0) return jmo_mb_avail(s, -1, y < 0 ? -1 : 0);
+    if (x <= 15) return y < 0 ? jmo_mb_avail(s, 0, -1) : 1;
+    return y < 0 ? jmo_mb_avail(s, 1, -1) : 0;
 }
 
 /* intrapred_luma [J] / 8.3.1.2: the 9 Intra4x4 predictions of the 4x4 block at (bx,by)
  * (pixels, MB relative); pred[9][16]; avail[9] */
-static void intra4x4_pred(const mbs *s, int bx, int by, pel pred[9][16], int avail[9]) {
+void jmo_intra4x4_pred(const mbs *s, int bx, int by, pel pred[9][16], int avail[9]) {
     const jmo_ctx *c = s->c;
     const pel *R = c->recY;
     int W = c->W, ax = s->pix_x + bx, ay = s->pix_y + by;
@@ -913,11 +901,11 @@ int jmo_intra8x8_pred_px(const int32_t nb[25], int avail, pel pred[9][64], int d
 }
 
 /* intrapred_luma_16x16 [J] / 8.3.3 */
-static void intra16_pred(const mbs *s, pel pred[4][256], int avail[4]) {
+void jmo_intra16_pred(const mbs *s, pel pred[4][256], int avail[4]) {
     const jmo_ctx *c = s->c;
     const pel *R = c->recY;
     int W = c->W, ax = s->pix_x, ay = s->pix_y;
-    int up = mb_avail(s, 0, -1), left = mb_avail(s, -1, 0), ul = mb_avail(s, -1, -1);
+    int up = jmo_mb_avail(s, 0, -1), left = jmo_mb_avail(s, -1, 0), ul = jmo_mb_avail(s, -1, -1);
     int T[16], L[16], P = ul ? R[(ay - 1) * W + ax - 1] : 0;
     for (int i = 0; i < 16; i++) {
         T[i] = up ? R[(ay - 1) * W + ax + i] : 0;
@@ -944,12 +932,12 @@ static void intra16_pred(const mbs *s, pel pred[4][256], int avail[4]) {
 }
 
 /* IntraChromaPrediction8x8 [J] / 8.3.4 for one component; pred[4][64] */
-static void intra_chroma_pred(const mbs *s, int uv, pel pred[4][64], int avail[4]) {
+void jmo_intra_chroma_pred(const mbs *s, int uv, pel pred[4][64], int avail[4]) {
     const jmo_ctx *c = s->c;
     const pel *R = uv ? c->recV : c->recU;
     const int dc = (c->maxv + 1) >> 1;
     int W = c->Wc, ax = s->pix_x >> 1, ay = s->pix_y >> 1;
-    int up = mb_avail(s, 0, -1), left = mb_avail(s, -1, 0), ul = mb_avail(s, -1, -1);
+    int up = jmo_mb_avail(s, 0, -1), left = jmo_mb_avail(s, -1, 0), ul = jmo_mb_avail(s, -1, -1);
     int T[8], L[8], P = ul ? R[(ay - 1) * W + ax - 1] : 0;
     for (int i = 0; i < 8; i++) {
         T[i] = up ? R[(ay - 1) * W + ax + i] : 0;
@@ -982,7 +970,7 @@ static void intra_chroma_pred(const mbs *s, int uv, pel pred[4][64], int avail[4
 }
 
 /* find_sad_16x16 [J]: Hadamard cost of the 4 Intra16x16 predictions */
-static int find_sad_16x16(const mbs *s, pel pred[4][256], const int avail[4], int *mode) {
+int jmo_find_sad_16x16(const mbs *s, pel pred[4][256], const int avail[4], int *mode) {
     int best = MAX_VALUE;
     *mode = 2;
     for (int k = 0; k < 4; k++) {
@@ -1024,7 +1012,7 @@ static int find_sad_16x16(const mbs *s, pel pred[4][256], const int avail[4], in
 /* ====================================================================================== */
 /*  motion compensation                                                                    */
 /* ====================================================================================== */
-static void luma_pred_4x4(const mbs *s, int bx4, int by4, int mvx, int mvy, pel *out, int os) {
+void jmo_luma_pred_4x4(const mbs *s, int bx4, int by4, int mvx, int mvy, pel *out, int os) {
     for (int y = 0; y < 4; y++)
         for (int x = 0; x < 4; x++)
             out[y * os + x] = (pel)jmo_qpel_at(s->c, 4 * (s->pix_x + 4 * bx4 + x) + mvx,
@@ -1032,7 +1020,7 @@ static void luma_pred_4x4(const mbs *s, int bx4, int by4, int mvx, int mvy, pel 
 }
 /* OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2: pixel (i,j) uses the MV of luma 4x4 block
  * (i>>1, j>>1) */
-static void chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], pel pred[64]) {
+void jmo_chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], pel pred[64]) {
     const jmo_ctx *c = s->c;
     const pel *R = uv ? c->refV : c->refU;
     int Wc = c->Wc, Hc = c->Hc;
@@ -1052,7 +1040,7 @@ static void chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], pel pr
 /*  Intra8x8 decision (High profile): JM FRExt rdopt.c › Mode_Decision_for_Intra8x8Macroblock /  */
 /*  Mode_Decision_for_new_8x8IntraBlocks, RDO off [J] (docs/JM_SEMANTICS.md items 26-28)      */
 /* ====================================================================================== */
-static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, pel rec[256],
+int jmo_intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, pel rec[256],
                              int16_t lev[4][64], int modes[4], int *cbp) {
     const jmo_ctx *c = s->c;
     int cost = 6 * lambda;                                 /* (int)floor(6*lambda+0.4999), once */
@@ -1073,9 +1061,9 @@ static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, pel re
         /* predIntra8x8PredMode (8.3.2.1): neighbour 4x4 modes (I4: that block, I8: repeated, else 2) */
         int ma = -1, mb = -1, ia = 0, ib = 0;
         if (bx) ma = modes[b8 - 1];
-        else if (nb4(s, -1, by, &ia)) ma = c->ipred[ia];
+        else if (jmo_nb4(s, -1, by, &ia)) ma = c->ipred[ia];
         if (by) mb = modes[b8 - 2];
-        else if (nb4(s, bx, -1, &ib)) mb = c->ipred[ib];
+        else if (jmo_nb4(s, bx, -1, &ib)) mb = c->ipred[ib];
         int mpm = (ma < 0 || mb < 0) ? 2 : imin(ma, mb);
         int best = 2, bcost = BIGCOST;
         for (int m = 0; m < 9; m++) {
@@ -1091,7 +1079,7 @@ static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, pel re
         for (int y = 0; y < 8; y++)
             for (int x = 0; x < 8; x++) r[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[best][8 * y + x];
         int dummy = 0;
-        if (dct_luma8x8(r, pred[best], 8, qp, intra_round, lev[b8], &dummy, rec + by * 16 + bx, 16, c->maxv)) *cbp |= 1 << b8;
+        if (jmo_dct_luma8x8(r, pred[best], 8, qp, intra_round, lev[b8], &dummy, rec + by * 16 + bx, 16, c->maxv)) *cbp |= 1 << b8;
         cost += bcost;
     }
     return cost;
@@ -1099,7 +1087,7 @@ static int intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, pel re
 
 /* TransformDecision [J] (RDO off): over the final prediction of the MB, sum of the 16 4x4 SATDs
  * against the sum of the four 8x8 SATDs; 8x8 if strictly smaller (item 29) */
-static int transform_decision(const mbs *s, const pel pred[256]) {
+int jmo_transform_decision(const mbs *s, const pel pred[256]) {
     int had = s->c->cfg.use_hadamard, cost4 = 0, cost8 = 0;
     for (int b8 = 0; b8 < 4; b8++) {
         int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
@@ -1120,7 +1108,7 @@ static int transform_decision(const mbs *s, const pel pred[256]) {
 /* ====================================================================================== */
 /*  encode_one_macroblock (RDO off)                                                         */
 /* ====================================================================================== */
-static void store_rec_luma(jmo_ctx *c, const mbs *s, const pel rec[256]) {
+void jmo_store_rec_luma(jmo_ctx *c, const mbs *s, const pel rec[256]) {
     for (int y = 0; y < 16; y++) memcpy(c->recY + (s->pix_y + y) * c->W + s->pix_x, rec + 16 * y, 16 * sizeof(pel));
 }
 
@@ -1164,7 +1152,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
             if (!valid[mode]) continue;
             int cost = 0;
             for (int block = 0; block < (mode == 1 ? 1 : 2); block++) {
-                partition_motion_search(s, mode, block);
+                jmo_partition_motion_search(s, mode, block);
                 cost += s->motion_cost[mode][block];   /* + (int)(2*lambda*min(ref,1)) == 0 */
             }
             if (cost < min_cost) { best_mode = mode; min_cost = cost; }
@@ -1176,18 +1164,18 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                 int min_cost8x8 = BIGCOST;
                 for (int mode = 4; mode <= 7; mode++) {
                     if (!valid[mode]) continue;
-                    partition_motion_search(s, mode, block);
+                    jmo_partition_motion_search(s, mode, block);
                     int cost = s->motion_cost[mode][block];
                     if (cost < min_cost8x8) { min_cost8x8 = cost; best8x8mode[block] = mode; }
                 }
                 cost8x8 += min_cost8x8;
                 /* reset stored motion vectors of this 8x8 to its best sub-mode */
                 int mode = best8x8mode[block];
-                if (mode > 0) write_enc_mv(s, (block & 1) * 2, (block >> 1) * 2, 2, 2, s->all_mv[mode]);
+                if (mode > 0) jmo_write_enc_mv(s, (block & 1) * 2, (block >> 1) * 2, 2, 2, s->all_mv[mode]);
             }
             if (cost8x8 < min_cost) { best_mode = JMH_P8x8; min_cost = cost8x8; }
         }
-        find_skip_mv(s);
+        jmo_find_skip_mv(s);
         memcpy(c->mem_mv, s->all_mv, sizeof(c->mem_mv));   /* EPZS spatial memory of the next MB */
     }
 
@@ -1197,7 +1185,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     int16_t i8lev[4][64];
     int i8modes[4] = {2, 2, 2, 2}, i8cbp = 0;
     if (t8) {
-        int i8cost = intra8x8_decision(s, qp, lambda, intra_round, i8rec, i8lev, i8modes, &i8cbp);
+        int i8cost = jmo_intra8x8_decision(s, qp, lambda, intra_round, i8rec, i8lev, i8modes, &i8cbp);
         if (i8cost <= min_cost) { min_cost = i8cost; best_mode = JMH_I8MB; }
     }
     /* ===== Intra 4x4 decision (with TQ + recon of every 4x4 in coding order) ===== */
@@ -1214,12 +1202,12 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                 int bx = 8 * (b8 & 1) + 4 * (b4 & 1), by = 8 * (b8 >> 1) + 4 * (b4 >> 1);
                 int blk = (by >> 2) * 4 + (bx >> 2);
                 int ia = 0, ib = 0;
-                int av_l = nb4(s, bx - 1, by, &ia), av_u = nb4(s, bx, by - 1, &ib);
+                int av_l = jmo_nb4(s, bx - 1, by, &ia), av_u = jmo_nb4(s, bx, by - 1, &ib);
                 int upMode = av_u ? c->ipred[ib] : -1, leftMode = av_l ? c->ipred[ia] : -1;
                 int mpm = (upMode < 0 || leftMode < 0) ? 2 : imin(upMode, leftMode);
                 pel pred[9][16];
                 int avail[9];
-                intra4x4_pred(s, bx, by, pred, avail);
+                jmo_intra4x4_pred(s, bx, by, pred, avail);
                 int best = 0, bcost = BIGCOST;
                 for (int m = 0; m < 9; m++) {
                     if (!avail[m]) continue;
@@ -1239,7 +1227,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                         r[4 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[best][4 * y + x];
                 int dummy = 0;
                 pel *dst = c->recY + (s->pix_y + by) * c->W + s->pix_x + bx;
-                if (dct_luma4x4(r, pred[best], 4, qp, intra_round, i4lev[blk], &dummy, dst, c->W, maxv)) {
+                if (jmo_dct_luma4x4(r, pred[best], 4, qp, intra_round, i4lev[blk], &dummy, dst, c->W, maxv)) {
                     i4cbp |= 1 << b8;
                     i4cbpblk |= 1 << blk;
                 }
@@ -1253,8 +1241,8 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     /* ===== Intra 16x16 ===== */
     pel i16pred[4][256];
     int i16avail[4], i16mode = 2;
-    intra16_pred(s, i16pred, i16avail);
-    int i16cost = find_sad_16x16(s, i16pred, i16avail, &i16mode);
+    jmo_intra16_pred(s, i16pred, i16avail);
+    int i16cost = jmo_find_sad_16x16(s, i16pred, i16avail, &i16mode);
     if (i16cost < min_cost) { min_cost = i16cost; best_mode = JMH_I16MB; }
 
     /* ===== final macroblock parameters ===== */
@@ -1278,7 +1266,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
         cbp = i8cbp; tr8 = 1;
         memcpy(rec, i8rec, sizeof(rec));
         for (int b8 = 0; b8 < 4; b8++) {
-            put_levels8(res->luma, b8, i8lev[b8]);
+            jmo_put_levels8(res->luma, b8, i8lev[b8]);
             if ((cbp >> b8) & 1) cbp_blk |= 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2);
         }
         for (int k = 0; k < 16; k++) res->ipred[k] = (int8_t)i8modes[((k >> 3) << 1) + ((k & 3) >> 1)];
@@ -1289,15 +1277,15 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     } else if (best_mode == JMH_I16MB) {
         int32_t r[256];
         for (int k = 0; k < 256; k++) r[k] = s->org[k] - i16pred[i16mode][k];
-        cbp = dct_luma_16x16(r, i16pred[i16mode], qp, i16_round, res->luma_dc, res->luma, &cbp_blk, rec, maxv);
+        cbp = jmo_dct_luma_16x16(r, i16pred[i16mode], qp, i16_round, res->luma_dc, res->luma, &cbp_blk, rec, maxv);
         res->i16mode = (int8_t)i16mode;
     } else {
         /* LumaResidualCoding / LumaResidualCoding8x8 (also SetCoeffAndReconstruction8x8) */
         pel pred[256];
         int sum_cnt_nonz = 0;
-        for (int k = 0; k < 16; k++) luma_pred_4x4(s, k & 3, k >> 2, fmv[k][0], fmv[k][1], pred + 4 * (k >> 2) * 16 + 4 * (k & 3), 16);
+        for (int k = 0; k < 16; k++) jmo_luma_pred_4x4(s, k & 3, k >> 2, fmv[k][0], fmv[k][1], pred + 4 * (k >> 2) * 16 + 4 * (k & 3), 16);
         if (t8 && (best_mode <= 3 || (b8mode[0] == 4 && b8mode[1] == 4 && b8mode[2] == 4 && b8mode[3] == 4)))
-            tr8 = transform_decision(s, pred);
+            tr8 = jmo_transform_decision(s, pred);
         for (int b8 = 0; b8 < 4; b8++) {
             int coeff_cost = 0, cbp8 = 0, blk8 = 0;
             if (tr8) {                                    /* dct_luma8x8 path */
@@ -1306,11 +1294,11 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                 int16_t lv[64];
                 for (int y = 0; y < 8; y++)
                     for (int x = 0; x < 8; x++) r[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[(by + y) * 16 + bx + x];
-                if (dct_luma8x8(r, pred + by * 16 + bx, 16, qp, intra_round, lv, &coeff_cost, rec + by * 16 + bx, 16, maxv)) {
+                if (jmo_dct_luma8x8(r, pred + by * 16 + bx, 16, qp, intra_round, lv, &coeff_cost, rec + by * 16 + bx, 16, maxv)) {
                     cbp8 = 1;
                     blk8 = 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2);
                 }
-                put_levels8(res->luma, b8, lv);
+                jmo_put_levels8(res->luma, b8, lv);
             }
             for (int b4 = 0; b4 < 4 && !tr8; b4++) {
                 int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1);
@@ -1319,7 +1307,7 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
                 for (int y = 0; y < 4; y++)
                     for (int x = 0; x < 4; x++)
                         r[4 * y + x] = s->org[(4 * by4 + y) * 16 + 4 * bx4 + x] - pred[(4 * by4 + y) * 16 + 4 * bx4 + x];
-                if (dct_luma4x4(r, pred + 4 * by4 * 16 + 4 * bx4, 16, qp, intra_round, res->luma[k], &coeff_cost,
+                if (jmo_dct_luma4x4(r, pred + 4 * by4 * 16 + 4 * bx4, 16, qp, intra_round, res->luma[k], &coeff_cost,
                                 rec + 4 * by4 * 16 + 4 * bx4, 16, maxv)) {
                     blk8 |= 1 << k;
                     cbp8 = 1;
@@ -1345,15 +1333,15 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
             memcpy(rec, pred, sizeof(rec));
         }
     }
-    store_rec_luma(c, s, rec);
+    jmo_store_rec_luma(c, s, rec);
 
     /* ===== chroma: IntraChromaPrediction8x8 (intra MBs) + ChromaResidualCoding ===== */
     int c_mode = 0;
     pel cpred[2][4][64];
     if (is_intra) {
         int cav[4];
-        intra_chroma_pred(s, 0, cpred[0], cav);
-        intra_chroma_pred(s, 1, cpred[1], cav);
+        jmo_intra_chroma_pred(s, 0, cpred[0], cav);
+        jmo_intra_chroma_pred(s, 1, cpred[1], cav);
         int min_c = BIGCOST;
         for (int m = 0; m < 4; m++) {                 /* DC, H, V, Plane */
             if (!cav[m]) continue;
@@ -1376,10 +1364,10 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
     for (int uv = 0; uv < 2; uv++) {
         pel pred[64], crec[64];
         if (is_intra) memcpy(pred, cpred[uv][c_mode], sizeof(pred));
-        else chroma_pred_mb(s, uv, fmv, pred);
+        else jmo_chroma_pred_mb(s, uv, fmv, pred);
         int32_t r[64];
         for (int k = 0; k < 64; k++) r[k] = s->orgc[uv][k] - pred[k];
-        cr_cbp = dct_chroma(r, pred, qpc, intra_round, cr_cbp, res->chroma_dc[uv], res->chroma_ac[uv], crec, maxv);
+        cr_cbp = jmo_dct_chroma(r, pred, qpc, intra_round, cr_cbp, res->chroma_dc[uv], res->chroma_ac[uv], crec, maxv);
         pel *R = uv ? c->recV : c->recU;
         for (int y = 0; y < 8; y++) memcpy(R + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), crec + 8 * y, 8 * sizeof(pel));
     }

@@ -20,6 +20,8 @@ static int cfg_ok(const jmh_config *cfg) {
     if (cfg->epzs_dual_refinement != 0 && cfg->epzs_dual_refinement != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->slice_mbs < 0) return JMH_E_INVALID_ARG;
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
+    /* RDOptimization 1: CABAC rate, 4x4 transform (docs/JM_SEMANTICS.md items 53-60) */
+    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode != 1 || cfg->transform_8x8_mode != 0)) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     return JMH_OK;
@@ -54,7 +56,8 @@ int jmo_create(const jmh_config *cfg, jmo_ctx **out) {
     c->mbintra = calloc((size_t)c->mbw * c->mbh, 1);
     c->res = calloc((size_t)c->mbw * c->mbh, sizeof(jmh_mb_result));
     c->blocksad = malloc(sizeof(uint16_t) * 16 * (size_t)c->npos);
-    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref) { jmo_destroy(c); return JMH_E_OOM; }
+    c->mbi = calloc((size_t)c->mbw * c->mbh, sizeof(jmr_mbinfo));
+    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref || !c->mbi) { jmo_destroy(c); return JMH_E_OOM; }
     memset(c->refidx, -1, n4);                             /* no previous picture: no motion */
     *out = c;
     return JMH_OK;
@@ -67,7 +70,7 @@ void jmo_destroy(jmo_ctx *c) {
     free(c->refY); free(c->refU); free(c->refV);
     free(c->recY); free(c->recU); free(c->recV);
     free(c->qpel); free(c->mv); free(c->refidx); free(c->ipred); free(c->mbintra);
-    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref);
+    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref); free(c->mbi);
     free(c);
 }
 
@@ -128,7 +131,10 @@ static int encode_frame(jmo_ctx *c, const void *y, const void *u, const void *v,
     memset(c->refidx, -1, n4);
     memset(c->ipred, 2, n4);
     for (int my = 0; my < c->mbh; my++)
-        for (int mx = 0; mx < c->mbw; mx++) jmo_encode_mb(c, mx, my);
+        for (int mx = 0; mx < c->mbw; mx++) {
+            if (c->cfg.rdo) jmo_encode_mb_rdo(c, mx, my);
+            else jmo_encode_mb(c, mx, my);
+        }
     return JMH_OK;
 }
 int jmo_encode_frame(jmo_ctx *c, const uint8_t *y, const uint8_t *u, const uint8_t *v, int stride_y, int stride_c,

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <string.h>
 #include "jm_oracle.h"
+#include "../h264-jm-commentary_amd/csrc/jmh_cabac_rate.h"
 
 #define MAX_VALUE 999999          /* JM 8.6 defines.h MAX_VALUE [J]                       */
 #define Q_BITS 15                 /* JM 8.6 defines.h Q_BITS [J]                          */
@@ -68,6 +69,11 @@ struct jmo_ctx {
     int16_t *tmv;                    /* [(H/4)*(W/4)][2], snapshot of mv at picture start        */
     int8_t *tref;                    /* [(H/4)*(W/4)], -1: intra / no previous picture          */
     int16_t mem_mv[8][16][2];        /* all_mv of the MB to the left (valid when mbx > 0)       */
+    /* RDOptimization = 1: the slice's CABAC coding state (contexts + codIRange, jmh_cabac_rate.h)
+       and what every coded macroblock leaves for its neighbours' context selection */
+    uint8_t cab_st[JMR_NCTX];
+    uint32_t cab_range;
+    jmr_mbinfo *mbi;
 };
 
 /* SliceMode 1 (SliceArgument MBs per slice, raster order): MB addresses a and n lie in one slice.
@@ -118,5 +124,49 @@ int  jmo_satd8x8(const int32_t d[64], int use_hadamard);
 
 /* encode.c */
 void jmo_encode_mb(jmo_ctx *c, int mbx, int mby);
+
+/* ---- encode.c internals shared with the RD mode decision (rdo.c) ------------------------ */
+typedef struct {
+    jmo_ctx *c;
+    int mbx, mby, pix_x, pix_y, mb_addr;
+    int lambda;                /* RDO off: lambda_mode == lambda_motion (integer)                  */
+    int lf;                    /* LAMBDA_FACTOR(lambda_motion): 65536*lambda (RDO off), RDO on the
+                                  host's (int)(65536 * sqrt(lambda_mode) + 0.5)                      */
+    int rdo;                   /* RDOptimization 1: no 16x16 zero-vector biases (!input->rdopt [J]) */
+    int slice_p;
+    pel org[256];              /* imgY_org of the MB                                       */
+    pel orgc[2][64];
+    /* FFS state (SetupFastFullPelSearch) */
+    int setup_done, scx, scy, pos_00;
+    int16_t all_mv[8][16][2];  /* img->all_mv[.][.][LIST_0][ref 0][blocktype]               */
+    int16_t pmv[8][16][2];     /* the MVP each search used (its partition's mvd = mv - pmv)   */
+    int motion_cost[8][4];
+    int skip_mv[2];
+} mbs;
+int  jmo_nb4(const mbs *s, int xN, int yN, int *idx);
+void jmo_set_mvp(const mbs *s, int pmv[2], int ref, int block_x, int block_y, int bsx, int bsy);
+void jmo_find_skip_mv(mbs *s);
+void jmo_write_enc_mv(mbs *s, int bx4, int by4, int w4, int h4, const int16_t (*mv)[2]);
+void jmo_partition_motion_search(mbs *s, int blocktype, int block8x8);
+int  jmo_dct_luma4x4(const int32_t resid[16], const pel *pred, int ps, int qp, int intra_round, int16_t levels[16],
+                     int *coeff_cost, pel *rec, int rs, int maxv);
+int  jmo_dct_luma8x8(const int32_t resid[64], const pel *pred, int ps, int qp, int intra_round, int16_t levels[64],
+                     int *coeff_cost, pel *rec, int rs, int maxv);
+void jmo_put_levels8(int16_t luma[16][16], int b8, const int16_t lev[64]);
+int  jmo_dct_chroma(const int32_t resid[64], const pel pred[64], int qpc, int intra_round, int cr_cbp, int16_t dc_out[4],
+                    int16_t ac_out[4][16], pel rec[64], int maxv);
+int  jmo_dct_luma_16x16(const int32_t resid[256], const pel pred[256], int qp, int rnd, int16_t dc_out[16],
+                        int16_t ac_out[16][16], int *cbp_blk, pel rec[256], int maxv);
+int  jmo_mb_avail(const mbs *s, int dmx, int dmy);
+void jmo_intra4x4_pred(const mbs *s, int bx, int by, pel pred[9][16], int avail[9]);
+void jmo_intra16_pred(const mbs *s, pel pred[4][256], int avail[4]);
+void jmo_intra_chroma_pred(const mbs *s, int uv, pel pred[4][64], int avail[4]);
+int  jmo_find_sad_16x16(const mbs *s, pel pred[4][256], const int avail[4], int *mode);
+void jmo_luma_pred_4x4(const mbs *s, int bx4, int by4, int mvx, int mvy, pel *out, int os);
+void jmo_chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], pel pred[64]);
+void jmo_store_rec_luma(jmo_ctx *c, const mbs *s, const pel rec[256]);
+
+/* rdo.c: encode_one_macroblock with RDOptimization = 1 (CABAC rate) */
+void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby);
 
 #endif

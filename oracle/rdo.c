@@ -1,0 +1,433 @@
+/*
+ * rdo.c — oracle restatement of JM lencod's encode_one_macroblock with RDOptimization = 1
+ * (TEST INFRASTRUCTURE ONLY; see jm_oracle.h for the parity status).
+ *
+ * Restated JM 8.6 functions [J] (no file:line exists: /root/reference holds README.md:1-4):
+ *   rdopt.c › encode_one_macroblock (the `input->rdopt` branches), RDCost_for_macroblocks,
+ *             RDCost_for_8x8blocks, RDCost_for_4x4IntraBlocks, Mode_Decision_for_4x4IntraBlocks,
+ *             SetCoeffAndReconstruction8x8, store_macroblock_parameters
+ *   rdopt_coding_state.c › store_coding_state / reset_coding_state (a copy of the context states
+ *             and codIRange: the only coding state a CABAC rate depends on, jmh_cabac_rate.h)
+ * with the entropy coder CABAC (SymbolMode 1) and the 4x4 transform (Transform8x8Mode 0).
+ * Every non-normative choice is an item of docs/JM_SEMANTICS.md (53-60):
+ *   - lambda_mode = fp.lambda_rd (0.85 * 2^((QP + QpBdOffsetY - 12) / 3), host libm), the searches'
+ *     LAMBDA_FACTOR(sqrt(lambda_mode)) = fp.lambda_factor_rd; rdcost = (double)D + lambda * rate;
+ *     candidates compared with strict '<' in JM's order;
+ *   - D = SSD of the reconstruction (luma 16x16 + both 8x8 chroma) for the macroblock loop, of the
+ *     8x8 / 4x4 luma block in the sub-decisions; rate = jmh_cabac_rate.h bits from the slice's
+ *     coding state at the start of the macroblock (the P8x8 loop: the running state after the
+ *     decided 8x8 blocks);
+ *   - the motion searches are the RDO-off ones (items 3-10, 33-40) at the RDO lambda without the
+ *     16x16 zero-vector biases (!input->rdopt) and with the RDO-off centre clamp kept (item 54).
+ */
+#include <stdlib.h>
+#include "jmo_internal.h"
+
+#define RD_HUGE 1e30
+
+typedef struct {               /* a luma candidate of the macroblock loop                          */
+    int mode;                  /* 0 (P_Skip), 1..3, JMH_P8x8, JMH_I16MB, JMH_I4MB                  */
+    pel rec[256];
+    int16_t luma[16][16], luma_dc[16];
+    int cbp, cbp_blk;          /* luma cbp bits, 4x4 coded bits                                    */
+    int16_t mv[16][2], mvd[16][2];
+    int8_t ipm[16], imode[16]; /* I4: rem codes (-1 = predicted mode), modes                       */
+    int i16mode, b8mode[4];
+    int dist;                  /* luma SSD                                                         */
+} lcand;
+typedef struct {               /* a chroma candidate (an inter candidate's MC or an intra mode)    */
+    pel rec[2][64];
+    int16_t dc[2][4], ac[2][4][16];
+    int cbpc, dist;
+} ccand;
+
+static int ssd(const pel *a, int as, const pel *b, int bs, int w, int h) {
+    int d = 0;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int e = a[y * as + x] - b[y * bs + x];
+            d += e * e;
+        }
+    return d;
+}
+
+/* LumaResidualCoding (RDO-off form, 4x4 transform): the prediction from the candidate's MVs, per
+   8x8 LumaResidualCoding8x8 with the _LUMA_COEFF_COST_ zeroing, then the MB-level one */
+static void luma_inter(const mbs *s, int qp, int rnd, lcand *L, pel pred[256]) {
+    const int maxv = s->c->maxv;
+    for (int k = 0; k < 16; k++) jmo_luma_pred_4x4(s, k & 3, k >> 2, L->mv[k][0], L->mv[k][1], pred + 4 * (k >> 2) * 16 + 4 * (k & 3), 16);
+    int sum = 0;
+    L->cbp = L->cbp_blk = 0;
+    memset(L->luma, 0, sizeof(L->luma));
+    for (int b8 = 0; b8 < 4; b8++) {
+        int cost = 0, cbp8 = 0, blk8 = 0;
+        for (int b4 = 0; b4 < 4; b4++) {
+            int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1), k = by4 * 4 + bx4;
+            int32_t r[16];
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++) r[4 * y + x] = s->org[(4 * by4 + y) * 16 + 4 * bx4 + x] - pred[(4 * by4 + y) * 16 + 4 * bx4 + x];
+            if (jmo_dct_luma4x4(r, pred + 4 * by4 * 16 + 4 * bx4, 16, qp, rnd, L->luma[k], &cost, L->rec + 4 * by4 * 16 + 4 * bx4, 16,
+                                maxv)) { blk8 |= 1 << k; cbp8 = 1; }
+        }
+        if (cost <= LUMA_COEFF_COST) {
+            cost = 0; cbp8 = 0; blk8 = 0;
+            for (int b4 = 0; b4 < 4; b4++) {
+                int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1);
+                memset(L->luma[by4 * 4 + bx4], 0, 32);
+                for (int y = 0; y < 4; y++) memcpy(L->rec + (4 * by4 + y) * 16 + 4 * bx4, pred + (4 * by4 + y) * 16 + 4 * bx4, 4 * sizeof(pel));
+            }
+        }
+        if (cbp8) L->cbp |= 1 << b8;
+        L->cbp_blk |= blk8;
+        sum += cost;
+    }
+    if (sum <= LUMA_MB_COEFF_COST) {
+        L->cbp = L->cbp_blk = 0;
+        memset(L->luma, 0, sizeof(L->luma));
+        memcpy(L->rec, pred, 256 * sizeof(pel));
+    }
+    L->dist = ssd(s->org, 16, L->rec, 16, 16, 16);
+}
+
+/* ChromaResidualCoding: prediction (intra mode cm, or MC with mv[]), dct_chroma unless skipped */
+static void chroma_code(const mbs *s, int qpc, int rnd, const pel (*ipred)[4][64], int cm, const int16_t (*mv)[2], int skipped,
+                        ccand *C) {
+    C->cbpc = 0;
+    C->dist = 0;
+    for (int uv = 0; uv < 2; uv++) {
+        pel pred[64];
+        if (ipred) memcpy(pred, ipred[uv][cm], sizeof(pred));
+        else jmo_chroma_pred_mb(s, uv, mv, pred);
+        if (skipped) {
+            memcpy(C->rec[uv], pred, sizeof(pred));
+            memset(C->dc[uv], 0, sizeof(C->dc[uv]));
+            memset(C->ac[uv], 0, sizeof(C->ac[uv]));
+        } else {
+            int32_t r[64];
+            for (int k = 0; k < 64; k++) r[k] = s->orgc[uv][k] - pred[k];
+            C->cbpc = jmo_dct_chroma(r, pred, qpc, rnd, C->cbpc, C->dc[uv], C->ac[uv], C->rec[uv], s->c->maxv);
+        }
+        C->dist += ssd(s->orgc[uv], 8, C->rec[uv], 8, 8, 8);
+    }
+}
+
+static void fill_cand(jmr_cand *r, const lcand *L, const ccand *C, int cm) {
+    memset(r, 0, sizeof(*r));
+    r->mb_type = L->mode;
+    r->cbp = L->cbp | C->cbpc << 4;
+    r->i16mode = L->i16mode;
+    r->cmode = cm;
+    for (int b = 0; b < 4; b++) r->b8mode[b] = L->b8mode[b];
+    r->ipm = L->ipm;
+    r->mvd = (const int16_t(*)[2])L->mvd;
+    r->luma = (const int16_t(*)[16])L->luma;
+    r->luma_dc = L->luma_dc;
+    r->cdc = (const int16_t(*)[4])C->dc;
+    r->cac = (const int16_t(*)[4][16])C->ac;
+}
+
+void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
+    mbs S;
+    mbs *s = &S;
+    memset(s, 0, sizeof(*s));
+    s->c = c; s->mbx = mbx; s->mby = mby; s->pix_x = 16 * mbx; s->pix_y = 16 * mby;
+    s->mb_addr = mby * c->mbw + mbx;
+    s->lf = c->fp.lambda_factor_rd;
+    s->lambda = c->fp.lambda_mode;
+    s->rdo = 1;
+    s->slice_p = c->fp.slice_type == JMH_P_SLICE;
+    const double lam = c->fp.lambda_rd;
+    const int qpy = c->fp.qp, qp = qpy + c->qpbd, maxv = c->maxv, W = c->W, W4 = W >> 2;
+    const int jm10 = c->cfg.jm_version >= 10;
+    const int rnd = jm10 ? JMO_RND_OFF(c->cfg.quant_offset[s->slice_p]) : !s->slice_p;
+    const int i16_rnd = jm10 ? rnd : JMO_RND_I;
+    const int qpc = jmo_qpc(qpy + c->fp.chroma_qp_offset, c->qpbd) + c->qpbd;
+    for (int y = 0; y < 16; y++) memcpy(s->org + 16 * y, c->orgY + (s->pix_y + y) * W + s->pix_x, 16 * sizeof(pel));
+    for (int y = 0; y < 8; y++) {
+        memcpy(s->orgc[0] + 8 * y, c->orgU + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), 8 * sizeof(pel));
+        memcpy(s->orgc[1] + 8 * y, c->orgV + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), 8 * sizeof(pel));
+    }
+    /* the slice's coding state: initialised at its first macroblock (9.3.1) */
+    const int a = s->mb_addr, nmb = c->mbw * c->mbh, k = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : nmb;
+    if (a % k == 0) { jmr_init_contexts(c->cab_st, !s->slice_p, qpy); c->cab_range = 510; }
+    const jmr_mbinfo *A = mbx > 0 && jmo_same_slice(c, a, a - 1) ? &c->mbi[a - 1] : NULL;
+    const jmr_mbinfo *B = mby > 0 && jmo_same_slice(c, a, a - c->mbw) ? &c->mbi[a - c->mbw] : NULL;
+    uint8_t st[JMR_NCTX];
+    jmr_eng e;
+#define RATE_BEGIN() (memcpy(st, c->cab_st, JMR_NCTX), e.st = st, e.range = c->cab_range, e.bits = 0)
+
+    const int *isr = c->cfg.inter_search;
+    int valid[9] = {0};
+    for (int m = 1; m <= 7; m++) valid[m] = s->slice_p && isr[m];
+    valid[8] = valid[4] || valid[5] || valid[6] || valid[7];
+
+    static lcand Lc[7];        /* 0 skip, 1..3, 4 P8x8, 5 I16, 6 I4 (one MB at a time) */
+    int have[7] = {0};
+    pel pred[256];
+    if (s->slice_p) {
+        /* ===== motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch) ===== */
+        for (int mode = 1; mode < 4; mode++)
+            if (valid[mode])
+                for (int block = 0; block < (mode == 1 ? 1 : 2); block++) jmo_partition_motion_search(s, mode, block);
+        /* ===== P8x8: per 8x8 block the sub-modes 4..7 by RDCost_for_8x8blocks ===== */
+        if (valid[8]) {
+            lcand *P = &Lc[4];
+            memset(P, 0, sizeof(*P));
+            P->mode = JMH_P8x8;
+            uint8_t st8[JMR_NCTX], stb[JMR_NCTX];
+            memcpy(st8, c->cab_st, JMR_NCTX);
+            uint32_t rg8 = c->cab_range, rgb = 0;
+            jmr_cur cur, curb;
+            memset(&cur, 0, sizeof(cur));
+            pel pred8[256], rec8[256];
+            int cnt_nonz = 0;
+            for (int block = 0; block < 4; block++) {
+                const int ox = 8 * (block & 1), oy = 8 * (block >> 1);
+                double best = RD_HUGE;
+                int bm = 0, bcost = 0, bcbp = 0, bblk = 0;
+                int16_t blev[4][16];
+                pel bpred[64], brec[64];
+                for (int mode = 4; mode <= 7; mode++) {
+                    if (!valid[mode]) continue;
+                    jmo_partition_motion_search(s, mode, block);
+                    /* LumaResidualCoding8x8 */
+                    pel p8[64], r8[64];
+                    int16_t lev[4][16];
+                    int cost = 0, cbpbit = 0, blk = 0;
+                    for (int b4 = 0; b4 < 4; b4++) {
+                        int bx4 = 2 * (block & 1) + (b4 & 1), by4 = 2 * (block >> 1) + (b4 >> 1), kk = by4 * 4 + bx4;
+                        int px = 4 * (b4 & 1), py = 4 * (b4 >> 1);
+                        jmo_luma_pred_4x4(s, bx4, by4, s->all_mv[mode][kk][0], s->all_mv[mode][kk][1], p8 + py * 8 + px, 8);
+                        int32_t r[16];
+                        for (int y = 0; y < 4; y++)
+                            for (int x = 0; x < 4; x++) r[4 * y + x] = s->org[(oy + py + y) * 16 + ox + px + x] - p8[(py + y) * 8 + px + x];
+                        if (jmo_dct_luma4x4(r, p8 + py * 8 + px, 8, qp, rnd, lev[b4], &cost, r8 + py * 8 + px, 8, maxv)) {
+                            cbpbit = 1; blk |= 1 << kk;
+                        }
+                    }
+                    if (cost <= LUMA_COEFF_COST) {
+                        cost = 0; cbpbit = 0; blk = 0;
+                        memset(lev, 0, sizeof(lev));
+                        memcpy(r8, p8, sizeof(r8));
+                    }
+                    int D = ssd(s->org + oy * 16 + ox, 16, r8, 8, 8, 8);
+                    /* rate: sub_mb_type, mvds, cbp bit, luma (RDCost_for_8x8blocks) */
+                    int16_t mvd[16][2], L16[16][16];
+                    memset(mvd, 0, sizeof(mvd));
+                    memset(L16, 0, sizeof(L16));
+                    for (int b4 = 0; b4 < 4; b4++) {
+                        int kk = (2 * (block >> 1) + (b4 >> 1)) * 4 + 2 * (block & 1) + (b4 & 1);
+                        mvd[kk][0] = (int16_t)(s->all_mv[mode][kk][0] - s->pmv[mode][kk][0]);
+                        mvd[kk][1] = (int16_t)(s->all_mv[mode][kk][1] - s->pmv[mode][kk][1]);
+                        memcpy(L16[kk], lev[b4], 32);
+                    }
+                    uint8_t stc[JMR_NCTX];
+                    memcpy(stc, st8, JMR_NCTX);
+                    jmr_eng eb = {stc, rg8, 0};
+                    jmr_cur cc = cur;
+                    jmr_b8(&eb, A, B, &cc, block, mode, (const int16_t(*)[2])mvd, cost > 0, (const int16_t(*)[16])L16);
+                    double rd = (double)D + lam * (double)eb.bits;
+                    if (rd < best) {
+                        best = rd; bm = mode; bcost = cost; bcbp = cbpbit; bblk = blk;
+                        memcpy(blev, lev, sizeof(blev)); memcpy(bpred, p8, sizeof(bpred)); memcpy(brec, r8, sizeof(brec));
+                        memcpy(stb, stc, JMR_NCTX); rgb = eb.range; curb = cc;
+                    }
+                }
+                /* the block's decision: coding state, SetRefAndMotionVectors, stored coefficients */
+                memcpy(st8, stb, JMR_NCTX); rg8 = rgb; cur = curb;
+                P->b8mode[block] = bm;
+                jmo_write_enc_mv(s, 2 * (block & 1), 2 * (block >> 1), 2, 2, s->all_mv[bm]);
+                for (int b4 = 0; b4 < 4; b4++) {
+                    int bx4 = 2 * (block & 1) + (b4 & 1), by4 = 2 * (block >> 1) + (b4 >> 1), kk = by4 * 4 + bx4;
+                    memcpy(P->luma[kk], blev[b4], 32);
+                    P->mv[kk][0] = s->all_mv[bm][kk][0]; P->mv[kk][1] = s->all_mv[bm][kk][1];
+                    P->mvd[kk][0] = (int16_t)(s->all_mv[bm][kk][0] - s->pmv[bm][kk][0]);
+                    P->mvd[kk][1] = (int16_t)(s->all_mv[bm][kk][1] - s->pmv[bm][kk][1]);
+                }
+                for (int y = 0; y < 8; y++) {
+                    memcpy(pred8 + (oy + y) * 16 + ox, bpred + 8 * y, 8 * sizeof(pel));
+                    memcpy(rec8 + (oy + y) * 16 + ox, brec + 8 * y, 8 * sizeof(pel));
+                }
+                if (bcost) { P->cbp |= bcbp << block; P->cbp_blk |= bblk; cnt_nonz += bcost; }
+            }
+            /* SetCoeffAndReconstruction8x8 */
+            if (cnt_nonz <= LUMA_MB_COEFF_COST) {
+                P->cbp = P->cbp_blk = 0;
+                memset(P->luma, 0, sizeof(P->luma));
+                memcpy(P->rec, pred8, sizeof(pred8));
+            } else memcpy(P->rec, rec8, sizeof(rec8));
+            P->dist = ssd(s->org, 16, P->rec, 16, 16, 16);
+            have[4] = 1;
+        }
+        jmo_find_skip_mv(s);
+        memcpy(c->mem_mv, s->all_mv, sizeof(c->mem_mv));   /* EPZS spatial memory of the next MB */
+        /* the inter candidates of the macroblock loop */
+        lcand *K = &Lc[0];
+        memset(K, 0, sizeof(*K));
+        K->mode = 0;
+        for (int q = 0; q < 16; q++) { K->mv[q][0] = (int16_t)s->skip_mv[0]; K->mv[q][1] = (int16_t)s->skip_mv[1]; }
+        for (int q = 0; q < 16; q++) jmo_luma_pred_4x4(s, q & 3, q >> 2, K->mv[q][0], K->mv[q][1], K->rec + 4 * (q >> 2) * 16 + 4 * (q & 3), 16);
+        K->dist = ssd(s->org, 16, K->rec, 16, 16, 16);
+        have[0] = 1;
+        for (int mode = 1; mode < 4; mode++) {
+            if (!valid[mode]) continue;
+            lcand *L = &Lc[mode];
+            memset(L, 0, sizeof(*L));
+            L->mode = mode;
+            for (int q = 0; q < 16; q++) {
+                L->mv[q][0] = s->all_mv[mode][q][0]; L->mv[q][1] = s->all_mv[mode][q][1];
+                L->mvd[q][0] = (int16_t)(s->all_mv[mode][q][0] - s->pmv[mode][q][0]);
+                L->mvd[q][1] = (int16_t)(s->all_mv[mode][q][1] - s->pmv[mode][q][1]);
+                L->b8mode[q & 3] = mode;
+            }
+            luma_inter(s, qp, rnd, L, pred);
+            have[mode] = 1;
+        }
+    }
+
+    /* ===== Intra16x16: the find_sad_16x16 mode, dct_luma_16x16 ===== */
+    {
+        lcand *L = &Lc[5];
+        memset(L, 0, sizeof(*L));
+        L->mode = JMH_I16MB;
+        pel ip[4][256];
+        int av[4], m = 2;
+        jmo_intra16_pred(s, ip, av);
+        jmo_find_sad_16x16(s, ip, av, &m);
+        int32_t r[256];
+        for (int q = 0; q < 256; q++) r[q] = s->org[q] - ip[m][q];
+        L->cbp = jmo_dct_luma_16x16(r, ip[m], qp, i16_rnd, L->luma_dc, L->luma, &L->cbp_blk, L->rec, maxv);
+        L->i16mode = m;
+        L->dist = ssd(s->org, 16, L->rec, 16, 16, 16);
+        have[5] = 1;
+    }
+    /* ===== Intra4x4: Mode_Decision_for_4x4IntraBlocks by RDCost_for_4x4IntraBlocks ===== */
+    {
+        lcand *L = &Lc[6];
+        memset(L, 0, sizeof(*L));
+        L->mode = JMH_I4MB;
+        for (int b8 = 0; b8 < 4; b8++)
+            for (int b4 = 0; b4 < 4; b4++) {
+                int bx = 8 * (b8 & 1) + 4 * (b4 & 1), by = 8 * (b8 >> 1) + 4 * (b4 >> 1), q = (by >> 2) * 4 + (bx >> 2);
+                int ia = 0, ib = 0;
+                int av_l = jmo_nb4(s, bx - 1, by, &ia), av_u = jmo_nb4(s, bx, by - 1, &ib);
+                int up = av_u ? c->ipred[ib] : -1, left = av_l ? c->ipred[ia] : -1;
+                int mpm = (up < 0 || left < 0) ? 2 : imin(up, left);
+                pel ip[9][16];
+                int av[9];
+                jmo_intra4x4_pred(s, bx, by, ip, av);
+                double best = RD_HUGE;
+                int bmode = 2, bnz = 0;
+                int16_t blev[16];
+                pel brec[16];
+                for (int m = 0; m < 9; m++) {
+                    if (!av[m]) continue;
+                    int32_t r[16];
+                    for (int y = 0; y < 4; y++)
+                        for (int x = 0; x < 4; x++) r[4 * y + x] = s->org[(by + y) * 16 + bx + x] - ip[m][4 * y + x];
+                    int16_t lev[16];
+                    pel rec4[16];
+                    int dummy = 0;
+                    int nz = jmo_dct_luma4x4(r, ip[m], 4, qp, rnd, lev, &dummy, rec4, 4, maxv);
+                    int D = ssd(s->org + by * 16 + bx, 16, rec4, 4, 4, 4);
+                    RATE_BEGIN();
+                    jmr_i4(&e, A, B, bx >> 2, by >> 2, m == mpm ? -1 : m < mpm ? m : m - 1, lev);
+                    double rd = (double)D + lam * (double)e.bits;
+                    if (rd < best) { best = rd; bmode = m; bnz = nz; memcpy(blev, lev, sizeof(blev)); memcpy(brec, rec4, sizeof(brec)); }
+                }
+                c->ipred[((s->pix_y + by) >> 2) * W4 + ((s->pix_x + bx) >> 2)] = (int8_t)bmode;
+                for (int y = 0; y < 4; y++) memcpy(c->recY + (s->pix_y + by + y) * W + s->pix_x + bx, brec + 4 * y, 4 * sizeof(pel));
+                memcpy(L->luma[q], blev, sizeof(blev));
+                L->imode[q] = (int8_t)bmode;
+                L->ipm[q] = (int8_t)(bmode == mpm ? -1 : bmode < mpm ? bmode : bmode - 1);
+                if (bnz) { L->cbp |= 1 << b8; L->cbp_blk |= 1 << q; }
+            }
+        for (int y = 0; y < 16; y++) memcpy(L->rec + 16 * y, c->recY + (s->pix_y + y) * W + s->pix_x, 16 * sizeof(pel));
+        L->dist = ssd(s->org, 16, L->rec, 16, 16, 16);
+        have[6] = 1;
+    }
+
+    /* ===== chroma candidates: each inter candidate's MC, the intra modes ===== */
+    static ccand Cc[7], Ci[4];
+    pel cip[2][4][64];
+    int cav[4];
+    jmo_intra_chroma_pred(s, 0, cip[0], cav);
+    jmo_intra_chroma_pred(s, 1, cip[1], cav);
+    for (int i = 0; i < 5; i++)
+        if (have[i]) chroma_code(s, qpc, rnd, NULL, 0, (const int16_t(*)[2])Lc[i].mv, i == 0, &Cc[i]);
+    for (int cm = 0; cm < 4; cm++)
+        if (cav[cm]) chroma_code(s, qpc, rnd, (const pel(*)[4][64])cip, cm, NULL, 0, &Ci[cm]);
+
+    /* ===== RDCost_for_macroblocks over c_ipred_mode (outer) and the modes (inner), JM order ===== */
+    static const int order[7] = {0, 1, 2, 3, 4, 5, 6};   /* 0, 1, 2, 3, P8x8, I16MB, I4MB */
+    double min_rd = RD_HUGE;
+    int bi = -1, bcm = 0, brate = 0;
+    for (int cm = 0; cm < 4; cm++) {
+        if (!cav[cm]) continue;
+        for (int oi = 0; oi < 7; oi++) {
+            int i = order[oi], intra = i >= 5;
+            if (!have[i] || (cm != 0 && !intra)) continue;
+            const ccand *C = intra ? &Ci[cm] : &Cc[i];
+            RATE_BEGIN();
+            if (i == 0) jmr_skip(&e, A, B, NULL);
+            else {
+                jmr_cand r;
+                fill_cand(&r, &Lc[i], C, intra ? cm : 0);
+                jmr_mb(&e, A, B, &r, s->slice_p, 0, NULL);
+            }
+            double rd = (double)(Lc[i].dist + C->dist) + lam * (double)e.bits;
+            if (rd < min_rd) { min_rd = rd; bi = i; bcm = intra ? cm : 0; brate = e.bits; }
+        }
+    }
+
+    /* ===== the chosen macroblock: results, reconstruction, picture arrays, coding state ===== */
+    const lcand *L = &Lc[bi];
+    const ccand *C = bi >= 5 ? &Ci[bcm] : &Cc[bi];
+    const int is_intra = bi >= 5;
+    jmh_mb_result *res = &c->res[a];
+    memset(res, 0, sizeof(*res));
+    int mb_type = L->mode == 0 ? JMH_PSKIP : L->mode;
+    res->mb_type = (int16_t)mb_type;
+    res->cbp = (int16_t)(L->cbp | C->cbpc << 4);
+    res->cbp_blk = L->cbp_blk;
+    for (int b = 0; b < 4; b++) {
+        res->b8mode[b] = (int8_t)(mb_type == JMH_PSKIP ? 0 : mb_type == JMH_P8x8 ? L->b8mode[b] : mb_type == JMH_I4MB ? JMH_IBLOCK
+                                                   : mb_type == JMH_I16MB ? 0 : mb_type);
+        res->ref_idx[b] = (int8_t)(is_intra ? -1 : 0);
+    }
+    res->i16mode = (int8_t)(mb_type == JMH_I16MB ? L->i16mode : 0);
+    res->c_ipred_mode = (int8_t)(is_intra ? bcm : 0);
+    res->min_cost = brate;                                /* the chosen candidate's rate (bits) */
+    memcpy(res->luma, L->luma, sizeof(res->luma));
+    memcpy(res->luma_dc, L->luma_dc, sizeof(res->luma_dc));
+    memcpy(res->chroma_dc, C->dc, sizeof(res->chroma_dc));
+    memcpy(res->chroma_ac, C->ac, sizeof(res->chroma_ac));
+    for (int q = 0; q < 16; q++) {
+        res->mv[q][0] = is_intra ? 0 : L->mv[q][0];
+        res->mv[q][1] = is_intra ? 0 : L->mv[q][1];
+        res->ipred[q] = (int8_t)(mb_type == JMH_I4MB ? L->imode[q] : 2);
+        int pa = ((s->pix_y >> 2) + (q >> 2)) * W4 + (s->pix_x >> 2) + (q & 3);
+        c->mv[2 * pa] = res->mv[q][0];
+        c->mv[2 * pa + 1] = res->mv[q][1];
+        c->refidx[pa] = (int8_t)(is_intra ? -1 : 0);
+        c->ipred[pa] = res->ipred[q];
+    }
+    c->mbintra[a] = (int8_t)is_intra;
+    jmo_store_rec_luma(c, s, L->rec);
+    for (int uv = 0; uv < 2; uv++) {
+        pel *R = uv ? c->recV : c->recU;
+        for (int y = 0; y < 8; y++) memcpy(R + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), C->rec[uv] + 8 * y, 8 * sizeof(pel));
+    }
+    /* write_one_macroblock: the coding state advances by the chosen macroblock, then the
+       end_of_slice_flag (0) unless the slice ends here */
+    e.st = c->cab_st; e.range = c->cab_range; e.bits = 0;
+    if (bi == 0) jmr_skip(&e, A, B, &c->mbi[a]);
+    else {
+        jmr_cand r;
+        fill_cand(&r, L, C, is_intra ? bcm : 0);
+        jmr_mb(&e, A, B, &r, s->slice_p, 0, &c->mbi[a]);
+    }
+    if ((a + 1) % k != 0 && a + 1 < nmb) jmr_end_of_mb(&e);
+    c->cab_range = e.range;
+#undef RATE_BEGIN
+}

@@ -106,7 +106,7 @@ class OracleEncoder:
         assert self.L.jmo_load_current(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2) == 0
 
     def encode(self, y, u, v, slice_type, qp, chroma_qp_offset=0):
-        fp = jmhip.frame_params(slice_type, qp, chroma_qp_offset)
+        fp = jmhip.frame_params(slice_type, qp, chroma_qp_offset, rdo=self.cfg.rdo, bit_depth=self.cfg.bit_depth)
         y, u, v = (np.ascontiguousarray(a, self.pdt) for a in (y, u, v))
         st = getattr(self.L, "jmo_encode_frame" + self.sfx)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2,
                                                            ctypes.byref(fp))

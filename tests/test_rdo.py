@@ -1,0 +1,110 @@
+"""RDOptimization = 1: encode_one_macroblock's rate-distortion loop
+(RDCost_for_macroblocks / RDCost_for_8x8blocks / RDCost_for_4x4IntraBlocks [J]) with the CABAC rate
+of csrc/jmh_cabac_rate.h, on the CPU oracle (oracle/rdo.c) through the product's host plumbing.
+
+Pinned here (CPU):
+  * the closed loop: the independent decoder reproduces the RD encoder's reconstruction;
+  * the rate: every committed macroblock's RD rate (jmh_mb_result.min_cost) equals the bits the
+    product's CABAC writer (host/cabac.c, an independent implementation checked by the decoder)
+    emits for it -- lencod prints "RD rate check" and fails on a mismatch;
+  * the configuration gate (PatchInp).
+JM parity of the RD choices is unpinned (no JM source here; docs/JM_SEMANTICS.md items 53-60)."""
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from jmpaths import JMDEC, LENCOD_CPU, ensure_built
+
+BASE = ["SymbolMode=1", "RDOptimization=1", "SearchMode=3"]
+RDO = [
+    ["InputFile=synthetic:71", "FramesToBeEncoded=4", "ProfileIDC=77", "SearchRange=16"],
+    ["InputFile=synthetic:72", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=8", "IntraPeriod=1"],
+    ["InputFile=synthetic:73", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=4", "QPFirstFrame=0",
+     "QPRemainingFrame=0"],
+    ["InputFile=synthetic:74", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=4", "QPFirstFrame=51",
+     "QPRemainingFrame=51"],
+    ["InputFile=synthetic:75", "FramesToBeEncoded=4", "ProfileIDC=77", "SearchRange=16", "SliceMode=1",
+     "SliceArgument=11", "ChromaQPOffset=-5", "QPRemainingFrame=36"],
+    ["InputFile=synthetic:76", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=8", "SliceMode=1",
+     "SliceArgument=1", "SourceWidth=200", "SourceHeight=120", "UseHadamard=0"],
+    ["InputFile=synthetic:77", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=8", "InterSearch16x16=0",
+     "InterSearch8x4=0", "RestrictSearchRange=0", "EPZSDualRefinement=1", "QPFirstFrame=12", "QPRemainingFrame=20"],
+    ["InputFile=synthetic:78", "FramesToBeEncoded=4", "ProfileIDC=77", "SearchRange=16", "SourceWidth=352",
+     "SourceHeight=288", "QPRemainingFrame=31", "JMVersion=10"],
+    # config 5's sample path: High 10, one MB row per slice
+    ["InputFile=synthetic:79", "FramesToBeEncoded=4", "ProfileIDC=110", "SourceBitDepthLuma=10",
+     "SourceBitDepthChroma=10", "SearchRange=16", "SliceMode=1", "SliceArgument=11", "IntraPeriod=3"],
+    ["InputFile=synthetic:80", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=9",
+     "SourceBitDepthChroma=9", "SearchRange=8", "QPFirstFrame=2", "QPRemainingFrame=4", "ChromaQPOffset=-12"],
+]
+
+
+def encode(d, extra, name="a"):
+    args = [LENCOD_CPU, "-p", f"OutputFile={d}/{name}.264", "-p", f"ReconFile={d}/{name}.yuv"]
+    for e in extra:
+        args += ["-p", e]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def rate_check(log):
+    m = re.search(r"RD rate check: (\d+) macroblocks, (\d+) whose", log)
+    assert m, log
+    return int(m.group(1)), int(m.group(2))
+
+
+@pytest.mark.parametrize("extra", RDO, ids=[c[0].split(":")[1] for c in RDO])
+def test_rdo_closed_loop_and_rate(extra):
+    ensure_built()
+    with tempfile.TemporaryDirectory() as d:
+        log = encode(d, BASE + extra)
+        n, bad = rate_check(log)
+        assert n > 0 and bad == 0, log
+        r = subprocess.run([JMDEC, f"{d}/a.264", f"{d}/dec.yuv"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/a.yuv", "rb").read()
+
+
+def test_rdo_changes_the_decisions():
+    """RDO on and off decide differently on the same input (and both decode)."""
+    ensure_built()
+    cfg = ["InputFile=synthetic:81", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=16", "SymbolMode=1",
+           "SearchMode=3"]
+    with tempfile.TemporaryDirectory() as d:
+        encode(d, cfg, "off")
+        encode(d, cfg + ["RDOptimization=1"], "on")
+        assert open(f"{d}/on.yuv", "rb").read() != open(f"{d}/off.yuv", "rb").read()
+
+
+def test_rdo_rate_distortion_tradeoff():
+    """Sanity of the Lagrangian: at the same QP the RD decisions cost fewer bits than RDO off on a
+    moving sequence (both at similar quality)."""
+    ensure_built()
+    cfg = ["InputFile=synthetic:82", "FramesToBeEncoded=5", "ProfileIDC=77", "SearchRange=16", "SymbolMode=1",
+           "SearchMode=3", "SourceWidth=352", "SourceHeight=288"]
+    with tempfile.TemporaryDirectory() as d:
+        off = encode(d, cfg, "off")
+        on = encode(d, cfg + ["RDOptimization=1"], "on")
+        bits = [int(re.search(r"bits (\d+)", x).group(1)) for x in (off, on)]
+        snr = [float(re.search(r"SNR Y\(dB\) ([\d.]+)", x).group(1)) for x in (off, on)]
+        assert bits[1] < bits[0], bits
+        assert snr[1] > snr[0] - 0.5, snr
+
+
+@pytest.mark.parametrize("bad,msg", [
+    (["SymbolMode=0", "ProfileIDC=77"], "needs SymbolMode=1"),
+    (["ProfileIDC=100", "Transform8x8Mode=1"], "Transform8x8Mode"),
+    (["SearchMode=0", "ProfileIDC=77"], "SearchMode=3"),
+    (["RDOptimization=2", "ProfileIDC=77"], "RDOptimization=2"),
+])
+def test_rdo_config_gate(bad, msg):
+    ensure_built()
+    with tempfile.TemporaryDirectory() as d:
+        args = [LENCOD_CPU, "-p", f"OutputFile={d}/a.264", "-p", "InputFile=synthetic:1", "-p", "FramesToBeEncoded=1"]
+        for e in ["SymbolMode=1", "RDOptimization=1", "SearchMode=3"] + bad:
+            args += ["-p", e]
+        r = subprocess.run(args, capture_output=True, text=True, timeout=60)
+        assert r.returncode != 0 and msg in (r.stdout + r.stderr), r.stdout + r.stderr
