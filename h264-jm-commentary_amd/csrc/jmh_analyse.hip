@@ -40,36 +40,13 @@
 #define JMH_EXP 0                             // tools/valu_split.sh builds variants without parts
 #endif
 #include "jmh_intra8.h"
+#include "jmh_intra.h"
 
 #define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
 #define MVB_LEN 1104
 #define PLS (WIN_DIM_MAX * WST + 32)          // stride between the G, b, h, j planes
 #define MAXNS 7                               // searches per stage (block 0 stage 0: 3 + 4)
 
-// Intra4x4 prediction (8.3.1.2) of mode m at pixel l as a formula over P[0..12]
-// (P[0] = p[-1,-1], P[1+i] = p[i,-1], P[9+j] = p[-1,j]): type | a << 2 | b << 6 | c << 10,
-// type 1: (Pa + Pb + 1) >> 1, 2: (Pa + 2 Pb + Pc + 2) >> 2 (a copy when a == b == c), 3: DC.
-static __constant__ uint16_t c_i4tab[9][16] = {
-    {0x0446, 0x088A, 0x0CCE, 0x1112, 0x0446, 0x088A, 0x0CCE, 0x1112, 0x0446, 0x088A, 0x0CCE, 0x1112, 0x0446, 0x088A, 0x0CCE, 0x1112},
-    {0x2666, 0x2666, 0x2666, 0x2666, 0x2AAA, 0x2AAA, 0x2AAA, 0x2AAA, 0x2EEE, 0x2EEE, 0x2EEE, 0x2EEE, 0x3332, 0x3332, 0x3332, 0x3332},
-    {0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003, 0x0003},
-    {0x0C86, 0x10CA, 0x150E, 0x1952, 0x10CA, 0x150E, 0x1952, 0x1D96, 0x150E, 0x1952, 0x1D96, 0x21DA, 0x1952, 0x1D96, 0x21DA, 0x221E},
-    {0x2406, 0x0842, 0x0C86, 0x10CA, 0x2A42, 0x2406, 0x0842, 0x0C86, 0x2EA6, 0x2A42, 0x2406, 0x0842, 0x32EA, 0x2EA6, 0x2A42, 0x2406},
-    {0x0041, 0x0085, 0x00C9, 0x010D, 0x0426, 0x0842, 0x0C86, 0x10CA, 0x026A, 0x0041, 0x0085, 0x00C9, 0x26AE, 0x0426, 0x0842, 0x0C86},
-    {0x0241, 0x0426, 0x004A, 0x048E, 0x02A5, 0x2A42, 0x0241, 0x0426, 0x02E9, 0x2EA6, 0x02A5, 0x2A42, 0x032D, 0x32EA, 0x02E9, 0x2EA6},
-    {0x0085, 0x00C9, 0x010D, 0x0151, 0x0C86, 0x10CA, 0x150E, 0x1952, 0x00C9, 0x010D, 0x0151, 0x0195, 0x10CA, 0x150E, 0x1952, 0x1D96},
-    {0x02A5, 0x2EA6, 0x02E9, 0x32EA, 0x02E9, 0x32EA, 0x032D, 0x332E, 0x032D, 0x332E, 0x3332, 0x3332, 0x3332, 0x3332, 0x3332, 0x3332}};
-
-// intra neighbourhood of an MB in LDS (unfiltered reconstruction of the current picture);
-// pel = uint8_t (bit depth 8) or uint16_t (High 10, k_mb_intra only)
-template <class pel>
-struct IntraNb {
-    pel orgc[2][64];
-    pel rtop[24];                             // luma row y = -1, x = -1..19 -> [x + 1]
-    pel rleft[16];
-    pel ctop[2][12];                          // chroma rows y = -1, x = -1..7 -> [x + 1]
-    pel cleft[2][8];
-};
 template <class pel>
 struct IntraS {
     alignas(4) pel org[256];
@@ -105,35 +82,6 @@ union AnalyseS {
 
 __device__ __forceinline__ void sstamp(MeS &s, int wave) {
     if (wave == 0 && __lane_id() == 0 && s.pst && s.pn < 44) s.pst[s.pn++] = wall_clock64();
-}
-
-// prefetch of the intra neighbourhood by threads t in [0, 96)
-template <class pel>
-__device__ __forceinline__ void load_intra_nb(const DevParams &d, IntraNb<pel> &nb, int t, int mbx, int mby) {
-    const pel *recY = spl<pel>(d.recY), *recU = spl<pel>(d.recU), *recV = spl<pel>(d.recV);
-    const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, Wc = d.Wc;
-    const MbAvail mav = mb_avail(d, mbx, mby);
-    const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
-    if (t < 21) {                                  // luma row y = -1, x = -1..19
-        const int x = t - 1;
-        const bool av = x < 0 ? avTL : x < 16 ? avT : avTR;
-        nb.rtop[x + 1] = av ? recY[(pix_y - 1) * W + pix_x + x] : 0;
-    } else if (t < 37) {
-        const int y = t - 21;
-        nb.rleft[y] = avL ? recY[(pix_y + y) * W + pix_x - 1] : 0;
-    } else if (t < 55) {                           // chroma rows y = -1, x = -1..7
-        const int i = t - 37, uv = i / 9, x = i - 9 * uv - 1;
-        const bool av = x < 0 ? avTL : avT;
-        nb.ctop[uv][x + 1] = av ? (uv ? recV : recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
-    } else if (t < 71) {
-        const int i = t - 55, uv = i >> 3, y = i & 7;
-        nb.cleft[uv][y] = avL ? (uv ? recV : recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
-    }
-}
-template <class pel>
-__device__ __forceinline__ void load_orgc(const DevParams &d, IntraNb<pel> &nb, int t, int mbx, int mby) {   // t in [0, 128)
-    const int uv = t >> 6, k = t & 63;
-    nb.orgc[uv][k] = spl<pel>(uv ? d.orgV : d.orgU)[((8 * mby) + (k >> 3)) * d.Wc + 8 * mbx + (k & 7)];
 }
 
 // ======================================================================================
@@ -665,37 +613,13 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
 // ======================================================================================
 //  intra decisions
 // ======================================================================================
-// intrapred_luma_16x16 + find_sad_16x16 on one wave: 4 modes x 16 blocks = 64 lanes
+// the Intra16x16 decision of the RDO-off wavefront (MbScratch i16cost / i16mode)
 template <class pel>
 __device__ __forceinline__ void i16_decision(const DevParams &d, const pel *org, const IntraNb<pel> &nb, MbScratch *scr, int lane, bool avL, bool avT,
                                              bool avTL) {
-    const int m = lane >> 4, b = lane & 15, ox = (b & 3) * 4, oy = (b >> 2) * 4;
-    const pel *T = nb.rtop + 1, *L = nb.rleft;
-    const I16Par par = i16_params(T, L, avT, avL, (d.maxv + 1) >> 1);
-    int mm[16], t[16];
-    for (int yy = 0; yy < 4; yy++)
-        for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy, d.maxv);
-    for (int yy = 0; yy < 4; yy++) {
-        int *r = mm + 4 * yy;
-        int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
-        t[4 * yy] = a0 + a1; t[4 * yy + 2] = a0 - a1; t[4 * yy + 1] = a2 + a3; t[4 * yy + 3] = a3 - a2;
-    }
-    int acs = 0, dcc = 0;
-    for (int xx = 0; xx < 4; xx++) {
-        int a0 = t[xx] + t[12 + xx], a1 = t[4 + xx] + t[8 + xx], a2 = t[4 + xx] - t[8 + xx], a3 = t[xx] - t[12 + xx];
-        int o0 = a0 + a1, o2 = a0 - a1, o1 = a2 + a3, o3 = a3 - a2;
-        if (xx == 0) dcc = o0; else acs += abs(o0);
-        acs += abs(o1) + abs(o2) + abs(o3);
-    }
-    const int cost = row16_sum(acs) + lane_had_abs(dcc / 4, b);
-    const bool av16[4] = {avT, avL, true, avT && avL && avTL};
-    int best = MAX_VALUE, i16mode = 2;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int c = __builtin_amdgcn_readlane(cost, 16 * k);
-        if (av16[k] && c < best) { best = c; i16mode = k; }
-    }
-    if (lane == 0) { scr->i16cost = best / 2; scr->i16mode = i16mode; }
+    int best, i16mode;
+    i16_pick(d, org, nb, lane, avL, avT, avTL, best, i16mode);
+    if (lane == 0) { scr->i16cost = best; scr->i16mode = i16mode; }
 }
 
 // IntraChromaPrediction8x8 mode decision on one wave: 4 modes x 2 components x 4 blocks

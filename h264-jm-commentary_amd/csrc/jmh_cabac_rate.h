@@ -71,15 +71,16 @@ typedef struct jmr_eng {
     int32_t bits;         /* arienco_bits_written delta (renormalisation steps + bypass bins)   */
 } jmr_eng;
 
-/* 9.3.1.1 with slice QP SliceQPY (cabac_init_idc 0 in P slices) */
-JMR_FN void jmr_init_contexts(uint8_t *st, int slice_i, int qp) {
+/* 9.3.1.1 with slice QP SliceQPY (cabac_init_idc 0 in P slices): context i, and all of them */
+JMR_FN uint8_t jmr_init_one(int i, int slice_i, int qp) {
     const int q = qp < 0 ? 0 : qp > 51 ? 51 : qp;
-    for (int i = 0; i < JMR_NCTX; i++) {
-        const int m = slice_i ? jmr_init_I[i][0] : jmr_init_P0[i][0], n = slice_i ? jmr_init_I[i][1] : jmr_init_P0[i][1];
-        int pre = ((m * q) >> 4) + n;
-        pre = pre < 1 ? 1 : pre > 126 ? 126 : pre;
-        st[i] = (uint8_t)(pre <= 63 ? (63 - pre) << 1 : ((pre - 64) << 1) | 1);
-    }
+    const int m = slice_i ? jmr_init_I[i][0] : jmr_init_P0[i][0], n = slice_i ? jmr_init_I[i][1] : jmr_init_P0[i][1];
+    int pre = ((m * q) >> 4) + n;
+    pre = pre < 1 ? 1 : pre > 126 ? 126 : pre;
+    return (uint8_t)(pre <= 63 ? (63 - pre) << 1 : ((pre - 64) << 1) | 1);
+}
+JMR_FN void jmr_init_contexts(uint8_t *st, int slice_i, int qp) {
+    for (int i = 0; i < JMR_NCTX; i++) st[i] = jmr_init_one(i, slice_i, qp);
 }
 
 JMR_FN int jmr_renorm_steps(uint32_t r) { return __builtin_clz(r) - 23; }   /* r in [2, 510] */
@@ -412,17 +413,18 @@ JMR_FN void jmr_i4(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, int x4,
 }
 
 /* RDCost_for_8x8blocks [J] (CABAC): the rate of sub-macroblock mode sm of 8x8 block b8 --
-   sub_mb_type, the mvds of its sub-partitions (mvd[] per 4x4), its coded_block_pattern bit and,
-   when it keeps coefficients (coded), the four luma 4x4 residuals -- on the running P8x8 state
-   (cur: the decided 8x8 blocks), which it advances as the write would (item 56) */
-JMR_FN void jmr_b8(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, jmr_cur *cur, int b8, int sm, const int16_t (*mvd)[2],
-                   int coded, const int16_t (*luma)[16]) {
+   sub_mb_type, the mvds of its sub-partitions, its coded_block_pattern bit and, when it keeps
+   coefficients (coded), the four luma 4x4 residuals -- on the running P8x8 state (cur: the
+   decided 8x8 blocks), which it advances as the write would (item 56).  mvd4 / lev4: the 8x8
+   block's four 4x4 in coding order (i4 = 2 * y + x) */
+JMR_FN void jmr_b8(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, jmr_cur *cur, int b8, int sm, const int16_t (*mvd4)[2],
+                   int coded, const int16_t (*lev4)[16]) {
     jmr_sub_mb_type(e, sm);
     const int w4 = (sm == 4 || sm == 5) ? 2 : 1, h4 = (sm == 4 || sm == 6) ? 2 : 1;
     for (int y = 0; y < 2; y += h4)
         for (int x = 0; x < 2; x += w4) {
             const int x4 = (b8 & 1) * 2 + x, y4 = (b8 >> 1) * 2 + y;
-            const int dx = mvd[y4 * 4 + x4][0], dy = mvd[y4 * 4 + x4][1];
+            const int dx = mvd4[2 * y + x][0], dy = mvd4[2 * y + x][1];
             jmr_mvd(e, A, B, (const int16_t(*)[2])cur->mvd, x4, y4, dx, dy);
             jmr_put_mvd(cur->mvd, x4, y4, w4, h4, dx, dy);
         }
@@ -433,7 +435,7 @@ JMR_FN void jmr_b8(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, jmr_cur
         const int x4 = (b8 & 1) * 2 + (i4 & 1), y4 = (b8 >> 1) * 2 + (i4 >> 1);
         const int ta = x4 ? (cur->cbf_l >> (y4 * 4 + x4 - 1)) & 1 : jmr_cbf_luma_term(A, 0, 3, y4);
         const int tb = y4 ? (cur->cbf_l >> ((y4 - 1) * 4 + x4)) & 1 : jmr_cbf_luma_term(B, 0, x4, 3);
-        const int f = jmr_residual(e, luma[y4 * 4 + x4], 16, 2, ta + 2 * tb);
+        const int f = jmr_residual(e, lev4[i4], 16, 2, ta + 2 * tb);
         cur->cbf_l |= (uint16_t)(f << (y4 * 4 + x4));
     }
 }

@@ -12,7 +12,8 @@
 #define NTA 512                          // threads per analysis workgroup (8 waves, 2 per SIMD)
 #define NPK 10                           // FFS search positions per analysis thread (a column strip)
 #define BIGCOST (1 << 20)
-#define PMAX 34                          // pictures per wavefront tick (pipelined pictures in flight)
+#define PMAX 33                          // pictures per wavefront tick (pipelined pictures in flight;
+                                         // 2160p needs 508 / PIPE_LAG + 1 = 33)
 // A picture's macroblock (x, y) reads its reference (the previous picture, deblocked) at pixel
 // offsets -68..+83 from the MB origin: window centre |MVP/4| <= SR, positions +-SR around it,
 // +-3/4 sub-pel, the 6-tap support and the LDS window margin (SR 32).  The farthest samples, rows
@@ -40,6 +41,23 @@ struct MbScratch {
     int16_t i8lev[16][16];               // levels in the CAVLC interleave (jmh_mb_result.luma)
     alignas(4) uint8_t i8rec[512];
 };
+
+// RDOptimization 1: the per-picture RD state, stored right after the picture's MbScratch array
+// (PicParams.scr + mbw * mbh) so that the kernel arguments stay within 4 KB: the lambdas from the
+// host, the slices' CABAC states (contexts + codIRange, jmh_cabac_rate.h) and what every coded
+// macroblock leaves for its neighbours' context selection
+struct jmr_mbinfo;
+struct RdoPic {
+    double lambda;                       // lambda_mode (jmh_frame_params.lambda_rd)
+    int32_t lf;                          // LAMBDA_FACTOR(sqrt(lambda_mode)) of the motion searches
+    int32_t pad;
+    uint8_t *cab;                        // [slice][JMR_NCTX] context states (state << 1 | valMPS)
+    uint32_t *range;                     // [slice] codIRange
+    jmr_mbinfo *mbi;                     // [MB]
+};
+
+// byte offset of the RdoPic in a picture's MbScratch allocation (16-aligned)
+__host__ __device__ __forceinline__ size_t rdo_pic_offset(size_t nmb) { return (nmb * sizeof(MbScratch) + 15) & ~(size_t)15; }
 
 struct DevParams {
     int W, H, Wc, Hc, mbw, mbh;
@@ -71,6 +89,12 @@ struct DevParams {
     int slice_type, qp, lambda_mode, lambda_motion, cqp_off;
     int qsel;                   // quantisation rounding selector of this slice (q_round, jmh_common.h)
     int diag, y_min;            // wavefront diagonal of this picture in the launch: mbx + 2*mby == diag
+                                //   (RDOptimization 1: diag = the stage of the RD schedule)
+    int rdo;                    // RDOptimization 1 (the RD kernels; no 16x16 zero-vector biases)
+    int lf;                     // LAMBDA_FACTOR of the motion searches: 65536 * lambda_motion (RDO
+                                //   off, integer lambda), the host's RDO one (RDOptimization 1)
+    double lambda_rd;           // RDOptimization 1: lambda_mode
+    const RdoPic *rp;           // RDOptimization 1: the picture's RD state
 };
 
 // Neighbour MB availability (6.4.8 / JM getNeighbour): inside the picture and in the current
@@ -116,6 +140,9 @@ struct TickArgs {
     int epzs_dual;                       // EPZSDualRefinement (k_mb_epzs)
     int slice_mbs;                       // SliceMode 1: MBs per slice (>= 1; mbw * mbh for one slice)
     int bd;                              // bit depth: 8 (uint8_t samples) or 9 / 10 (uint16_t, High 10)
+    int rdo;                             // RDOptimization 1: k_rdo_analyse + k_rdo_final on the stage
+    const int32_t *sched, *soff;         //   schedule: MB addresses in stage order, offsets per stage
+    void *rscr;                          //   the tick's candidate scratch (RdoScr per tick MB)
     const uint32_t *ordtab;              // FFS order keys, [NPK / 2][NTA] packed pairs (jmh_create)
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
@@ -163,7 +190,29 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.prof = e == 0 ? t.prof : nullptr; d.prof_mb = t.prof_mb;
     d.slice_type = q.slice_type; d.qp = q.qp; d.lambda_mode = q.lambda_mode; d.lambda_motion = q.lambda_motion;
     d.cqp_off = q.cqp_off; d.qsel = q.qsel; d.diag = q.diag; d.y_min = q.y_min;
+    d.rdo = t.rdo;
+    d.lf = q.lambda_motion << 16;
+    d.lambda_rd = 0;
+    d.rp = nullptr;
+    if (t.rdo) {
+        d.rp = reinterpret_cast<const RdoPic *>(reinterpret_cast<const uint8_t *>(q.scr) + rdo_pic_offset((size_t)t.mbw * t.mbh));
+        d.lf = d.rp->lf;
+        d.lambda_rd = d.rp->lambda;
+    }
     return d;
+}
+
+// the macroblock of tick MB index m (entry e): the diagonal mbx + 2 mby == diag of the RDO-off
+// wavefront, or the RD stage schedule's list (RDOptimization 1)
+__device__ __forceinline__ void tick_mb(const TickArgs &t, const DevParams &d, int e, int m, int &mbx, int &mby) {
+    if (t.rdo) {
+        const int a = t.sched[t.soff[d.diag] + (m - t.pre[e])];
+        mby = a / d.mbw;
+        mbx = a - mby * d.mbw;
+    } else {
+        mby = d.y_min + (m - t.pre[e]);
+        mbx = d.diag - 2 * mby;
+    }
 }
 
 // sample-typed view of a DevParams plane pointer (bytes of uint8_t or uint16_t samples)

@@ -4,8 +4,8 @@
 // 16-lane transform groups (LumaResidualCoding / dct_luma_16x16 / dct_chroma + reconstruction),
 // or, with Transform8x8Mode, TransformDecision and dct_luma8x8 on one wave per 8x8 block, and the
 // outputs the next diagonal depends on (reconstruction, MVs, reference indices, intra modes).
-#include "jmh_common.h"
-#include <cstdlib>
+#include "jmh_deblock.h"
+#include "jmh_intra.h"
 
 // pel: uint8_t (bit depth 8) or uint16_t (High 10) samples
 template <class pel>
@@ -35,70 +35,8 @@ struct FinS {
     int creset[2];
     int cdcnz[2];
     pel cfin[2][64];
-    // deblocking: the MB with 4 rows / columns of its (already filtered) top / left neighbours
-    pel dy[20][20];                      // luma, rows / columns -4..15 -> [r + 4][c + 4]
-    pel dc2[2][12][12];                  // chroma, rows / columns -4..7
-    int8_t bs[2][4][4];                  // boundary strength [dir][edge][segment]
+    DbkS<pel> db;                        // the fused deblocking (jmh_deblock.h)
 };
-
-// 8.7.2.2 thresholds (index = clip3(0, 51, qp + filter offset)) and tc0 (bS 1..3)
-static __constant__ uint8_t c_alpha[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   4,   4,
-                                           5,  6,  7,  8,  9,  10, 12, 13, 15, 17, 20, 22, 25,  28,  32,  36,  40,  45,
-                                           50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
-static __constant__ uint8_t c_beta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  2,  2,
-                                          2,  3,  3,  3,  3,  4,  4,  4,  6,  6,  7,  7,  8,  8,  9,  9,  10, 10,
-                                          11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
-static __constant__ uint8_t c_tc0[52][3] = {
-    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
-    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1},
-    {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1},
-    {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 2, 3}, {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4},
-    {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11},
-    {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
-
-// one line of samples across an edge (8.7.2.3 / 8.7.2.4): q0 at q[0], p_k at q[-(k+1)*step];
-// alpha / beta / tc0 already scaled by 1 << (BitDepth - 8), Clip1 to maxv
-template <class pel>
-__device__ __forceinline__ void filter_line(pel *q, int step, int bS, int alpha, int beta, int tc0, bool chroma, int maxv) {
-    const int p0 = q[-step], p1 = q[-2 * step], q0 = q[0], q1 = q[step];
-    if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-    if (chroma) {
-        if (bS < 4) {
-            const int tc = tc0 + 1;
-            const int dl = iclip(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
-            q[-step] = (pel)clipmx(p0 + dl, maxv);
-            q[0] = (pel)clipmx(q0 - dl, maxv);
-        } else {
-            q[-step] = (pel)((2 * p1 + p0 + q1 + 2) >> 2);
-            q[0] = (pel)((2 * q1 + q0 + p1 + 2) >> 2);
-        }
-        return;
-    }
-    const int p2 = q[-3 * step], q2 = q[2 * step];
-    const int ap = abs(p2 - p0), aq = abs(q2 - q0);
-    if (bS < 4) {
-        const int tc = tc0 + (ap < beta) + (aq < beta);
-        const int dl = iclip(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
-        q[-step] = (pel)clipmx(p0 + dl, maxv);
-        q[0] = (pel)clipmx(q0 - dl, maxv);
-        if (ap < beta) q[-2 * step] = (pel)(p1 + iclip(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
-        if (aq < beta) q[step] = (pel)(q1 + iclip(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
-    } else {
-        const int p3 = q[-4 * step], q3 = q[3 * step];
-        const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
-        if (ap < beta && small) {
-            q[-step] = (pel)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-            q[-2 * step] = (pel)((p2 + p1 + p0 + q0 + 2) >> 2);
-            q[-3 * step] = (pel)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
-        } else q[-step] = (pel)((2 * p1 + p0 + q1 + 2) >> 2);
-        if (aq < beta && small) {
-            q[0] = (pel)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-            q[step] = (pel)((p0 + q0 + q1 + q2 + 2) >> 2);
-            q[2 * step] = (pel)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
-        } else q[0] = (pel)((2 * q1 + q0 + p1 + 2) >> 2);
-    }
-}
-
 
 // OCC workgroups per CU: 8 (64 VGPRs, a few spilled) for ticks of more than 5 x 256 MBs (2160p,
 // one dispatch round), 5 (no spills, a shorter per-MB chain) for smaller ticks
@@ -120,11 +58,8 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     const pel *orgY = spl<pel>(d.orgY), *orgU = spl<pel>(d.orgU), *orgV = spl<pel>(d.orgV);
     const pel *refY = spl<pel>(d.refY), *refU = spl<pel>(d.refU), *refV = spl<pel>(d.refV);
     pel *recY = spl<pel>(d.recY), *recU = spl<pel>(d.recU), *recV = spl<pel>(d.recV);
-    pel *dbkY = spl<pel>(d.dbkY), *dbkU = spl<pel>(d.dbkU), *dbkV = spl<pel>(d.dbkV);
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL;
-    // deblocking filters across slice edges (disable_deblocking_filter_idc 0): picture edges only
-    const bool dbL = mbx > 0, dbT = mby > 0;
     const bool prof = prof_mb_here(d, mbx, mby);
     PSTAMP(16);
     const MbScratch *sc = d.scr + mby * d.mbw + mbx;
@@ -197,52 +132,14 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
         s.lev[blk][l] = sc->i4lev[blk][l];
         s.rec[tid] = spl<pel>(sc->i4rec)[tid];
     } else if (best_mode == JMH_I16MB) {
-        // dct_luma_16x16 [J]
-        const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per;
-        const int qp_const = q_round(q_sel16(d.qsel), q_bits), qp_const2 = qp_const << 1;
+        // dct_luma_16x16 [J] (jmh_intra.h i16_code)
         const pel *T = s.rtop + 1, *L = s.rleft;
         const I16Par par = i16_params(T, L, avT, avL, (maxv + 1) >> 1);
         const int p = i16_pred(par, T, L, i16mode, px4, py4, maxv);
-        const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
-        if (l == 0) s.dc[blk] = c;
-        __syncthreads();
-        if (tid == 0) {
-            int *dc = s.dc;
-            for (int yy = 0; yy < 4; yy++) {
-                int *r = dc + 4 * yy;
-                int a0 = r[0] + r[3], a3 = r[0] - r[3], a1 = r[1] + r[2], a2 = r[1] - r[2];
-                r[0] = a0 + a1; r[2] = a0 - a1; r[1] = a3 + a2; r[3] = a3 - a2;
-            }
-            for (int xx = 0; xx < 4; xx++) {
-                int a0 = dc[xx] + dc[12 + xx], a3 = dc[xx] - dc[12 + xx], a1 = dc[4 + xx] + dc[8 + xx], a2 = dc[4 + xx] - dc[8 + xx];
-                dc[xx] = (a0 + a1) >> 1; dc[8 + xx] = (a0 - a1) >> 1; dc[4 + xx] = (a3 + a2) >> 1; dc[12 + xx] = (a3 - a2) >> 1;
-            }
-            int lev[16];
-            for (int k = 0; k < 16; k++) {
-                int pos = scan_of(k);
-                int level = (abs(dc[pos]) * c_q3[qp_rem][0] + qp_const2) >> (q_bits + 1);
-                s.dclev[k] = (int16_t)isign(level, dc[pos]);
-                lev[pos] = s.dclev[k];
-            }
-            int t[16];
-            for (int yy = 0; yy < 4; yy++) {
-                const int *cc = lev + 4 * yy;
-                int e0 = cc[0] + cc[2], e1 = cc[0] - cc[2], e2 = cc[1] - cc[3], e3 = cc[1] + cc[3];
-                t[4 * yy] = e0 + e3; t[4 * yy + 3] = e0 - e3; t[4 * yy + 1] = e1 + e2; t[4 * yy + 2] = e1 - e2;
-            }
-            int v00 = c_dq3[qp_rem][0];
-            for (int xx = 0; xx < 4; xx++) {
-                int e0 = t[xx] + t[8 + xx], e1 = t[xx] - t[8 + xx], e2 = t[4 + xx] - t[12 + xx], e3 = t[4 + xx] + t[12 + xx];
-                int fv[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
-                for (int yy = 0; yy < 4; yy++) s.dcdq[4 * yy + xx] = (fv[yy] * v00 * (1 << qp_per) + 2) >> 2;
-            }
-        }
-        __syncthreads();
-        int lev, dq, cc;
-        unsigned nz = lane_quant(c, l, qp, qp_const, true, lev, dq, cc);
+        int lev, rv;
+        i16_code(p, (int)s.org[py4 * 16 + px4], qp, q_round(q_sel16(d.qsel), 15 + qp / 6), s.dc, s.dcdq, s.dclev, s.bnz, tid, maxv, lev, rv);
         s.lev[blk][l] = (int16_t)lev;
-        if (l == 0) { dq = s.dcdq[blk]; s.bnz[blk] = nz != 0; }
-        s.rec[py4 * 16 + px4] = (pel)lane_inv4x4(dq, l, p, maxv);
+        s.rec[py4 * 16 + px4] = (pel)rv;
         __syncthreads();
         for (int b = 0; b < 16; b++)
             if (s.bnz[b]) { cbp = 15; cbp_blk |= 1 << b; }
@@ -423,100 +320,8 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     }
     recY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)] = s.rec[tid];
 
-    // ======== DeblockMb [J] / 8.7 into the reference picture (d.dbkY..): this MB's edges, in
-    // place on its already-filtered left / top neighbours. MBs of one diagonal touch disjoint
-    // samples and every neighbour they read lies on an earlier diagonal, so the result equals
-    // JM's raster-order DeblockFrame.
-    if (d.dbkY) {
-        const int Hc = d.Hc;
-        const bool filt = d.lf_disable != 1;
-        __syncthreads();                          // s.rec, s.cfin final
-        for (int i = tid; i < 400 + 288; i += NT) {
-            if (i < 400) {
-                const int r = i / 20 - 4, c = i % 20 - 4;
-                int v = 0;
-                if (r >= 0 && c >= 0) v = s.rec[16 * r + c];
-                else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL)) v = dbkY[(pix_y + r) * W + pix_x + c];
-                s.dy[r + 4][c + 4] = (pel)v;
-            } else {
-                const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
-                int v = 0;
-                if (r >= 0 && c >= 0) v = s.cfin[pl][8 * r + c];
-                else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL))
-                    v = (pl ? dbkV : dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c];
-                s.dc2[pl][r + 4][c + 4] = (pel)v;
-            }
-        }
-        if (tid < 32) {                           // boundary strength (8.7.2.1), frame MBs, one slice
-            const int dir = tid >> 4, e = (tid >> 2) & 3, i = tid & 3;
-            const bool mb_edge = e == 0;
-            int bS = 0;
-            if (filt && !(mb_edge && (dir == 0 ? !dbL : !dbT))) {
-                const int bq = dir == 0 ? i * 4 + e : e * 4 + i;
-                const int bp = dir == 0 ? (mb_edge ? i * 4 + 3 : bq - 1) : (mb_edge ? 12 + i : bq - 4);
-                bool intra_p = is_intra, pcoef;
-                int pref, pmx, pmy;
-                const int qref = is_intra ? -1 : 0, qmx = s.fmv[bq][0], qmy = s.fmv[bq][1];
-                const bool qcoef = (cbp_blk >> bq) & 1;
-                if (mb_edge) {
-                    const int nx = dir == 0 ? mbx - 1 : mbx, ny = dir == 0 ? mby : mby - 1;
-                    const jmh_mb_result *rp = d.res + ny * d.mbw + nx;
-                    intra_p = rp->mb_type == JMH_I4MB || rp->mb_type == JMH_I16MB || rp->mb_type == JMH_I8MB;
-                    pcoef = (rp->cbp_blk >> bp) & 1;
-                    pref = intra_p ? -1 : 0;
-                    pmx = rp->mv[bp][0]; pmy = rp->mv[bp][1];
-                } else {
-                    pcoef = (cbp_blk >> bp) & 1;
-                    pref = qref; pmx = s.fmv[bp][0]; pmy = s.fmv[bp][1];
-                }
-                if (intra_p || is_intra) bS = mb_edge ? 4 : 3;
-                else if (pcoef || qcoef) bS = 2;
-                else if (pref != qref || abs(pmx - qmx) >= 4 || abs(pmy - qmy) >= 4) bS = 1;
-            }
-            s.bs[dir][e][i] = (int8_t)bS;
-        }
-        __syncthreads();
-        if (tid < 64 && filt) {                   // one wave: luma lines on lanes 0..15, chroma on 16..31
-            // indices from QPY / QPc (8.7.2.2), thresholds times 1 << (BitDepth - 8) (8-457..8-470)
-            const int offA = d.lf_offA, offB = d.lf_offB, bsc = 1 << (d.qpbd / 6);
-            const int iA = iclip(0, 51, qpy + offA), iB = iclip(0, 51, qpy + offB);
-            const int alpha = bsc * c_alpha[iA], beta = bsc * c_beta[iB];
-            const int t1 = bsc * c_tc0[iA][0], t2 = bsc * c_tc0[iA][1], t3 = bsc * c_tc0[iA][2];
-            const int cA = iclip(0, 51, qpcy + offA), cB = iclip(0, 51, qpcy + offB);
-            const int calpha = bsc * c_alpha[cA], cbeta = bsc * c_beta[cB];
-            const int u1 = bsc * c_tc0[cA][0], u2 = bsc * c_tc0[cA][1], u3 = bsc * c_tc0[cA][2];
-            for (int dir = 0; dir < 2; dir++)
-                for (int e = 0; e < 4; e++) {
-                    if (tid < 16 && !((e & 1) && t8flag)) {             // 8x8 transform: no 4x4 luma edges
-                        const int k = tid, b = s.bs[dir][e][k >> 2];
-                        if (b) {
-                            pel *q = dir == 0 ? &s.dy[k + 4][4 * e + 4] : &s.dy[4 * e + 4][k + 4];
-                            filter_line(q, dir == 0 ? 1 : 20, b, alpha, beta, b == 1 ? t1 : b == 2 ? t2 : t3, false, maxv);
-                        }
-                    } else if (tid < 32 && !(e & 1)) {
-                        const int pl = (tid - 16) >> 3, k = tid & 7, b = s.bs[dir][e][k >> 1];
-                        if (b) {
-                            pel *q = dir == 0 ? &s.dc2[pl][k + 4][2 * e + 4] : &s.dc2[pl][2 * e + 4][k + 4];
-                            filter_line(q, dir == 0 ? 1 : 12, b, calpha, cbeta, b == 1 ? u1 : b == 2 ? u2 : u3, true, maxv);
-                        }
-                    }
-                    wave_lds_sync();
-                }
-        }
-        __syncthreads();
-        for (int i = tid; i < 400 + 288; i += NT) {
-            if (i < 400) {
-                const int r = i / 20 - 4, c = i % 20 - 4;
-                if ((r >= 0 && c >= 0) || (r >= -3 && r < 0 && c >= 0 && dbT) || (c >= -3 && c < 0 && r >= 0 && dbL))
-                    dbkY[(pix_y + r) * W + pix_x + c] = s.dy[r + 4][c + 4];
-            } else {
-                const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
-                if ((r >= 0 && c >= 0) || (r == -1 && c >= 0 && c < 8 && dbT) || (c == -1 && r >= 0 && r < 8 && dbL))
-                    if (r < 8 && c < 8) (pl ? dbkV : dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c] = s.dc2[pl][r + 4][c + 4];
-            }
-        }
-        (void)Hc;
-    }
+    // ======== DeblockMb [J] / 8.7 into the reference picture (jmh_deblock.h)
+    if (d.dbkY) deblock_mb(d, s.db, s.rec, s.cfin, s.fmv, is_intra, cbp_blk, t8flag, qpy, qpcy, mbx, mby, tid);
     PSTAMP(19);
     if (t.bprof_fin && tid == 0) {
         t.bprof_fin[3 * blockIdx.x] = bt0;

@@ -20,6 +20,7 @@
 #include <vector>
 #include <algorithm>
 #include "jmh_device.h"
+#include "jmh_cabac_rate.h"
 
 hipError_t jmh_launch_interp(const uint8_t *ref, int W, int H, uint8_t *qpel, int qstride, int qplane, hipStream_t st);
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st);
@@ -28,6 +29,8 @@ hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st);
+size_t jmh_rdo_scratch_bytes();
 hipError_t jmh_launch_block_search_u16(int n, const jmh_block_search *reqs, jmh_block_result *out, const uint16_t *cur, const uint16_t *ref,
                                        int W, int H, int had, int bit_depth, hipStream_t st);
 hipError_t jmh_launch_sad_table_u16(const uint16_t *org, const uint16_t *ref, int W, int H, int sr, int n_mb, const int32_t *mb_xy,
@@ -111,6 +114,10 @@ struct PicBuf {
     uint8_t *h_src, *h_rec, *h_dbk;
     hipEvent_t ev_src, ev_t0, ev_done;   // staging reuse / push..done timing
     hipEvent_t ev_fin;                   // the picture's last tick (the copy stream's readback waits)
+    uint8_t *cab;                        // RDOptimization 1: the slices' context states,
+    uint32_t *range;                     //   codIRange, the MBs' context-selection records
+    jmr_mbinfo *mbi;
+    RdoPic *h_rp;                        //   pinned staging of the entry's RdoPic (after scr)
     int recon_read;                      // h_rec holds the occupant's reconstruction
     int unpopped;                        // readback picture not yet popped
     int deblocked;                       // the occupant was deblocked on the device (dbk valid)
@@ -158,6 +165,12 @@ struct jmh_ctx {
     jmh_timing timing;
     int ticks_total;
     std::vector<int> dcount, dymin;
+    int lag;                             // stages a picture trails its reference picture by
+    // RDOptimization 1: the RD stage schedule (MB addresses in stage order, offsets per stage),
+    // the tick's candidate scratch, slices per picture
+    int32_t *d_sched, *d_soff;
+    void *d_rscr;
+    int nslice;
 };
 
 #define HCHK(x)                                                                  \
@@ -195,9 +208,9 @@ int jmh_device_count(void) {
 }  // extern "C"
 
 static void free_entry(PicBuf &b) {
-    void *dev_bufs[] = {b.src, b.rec, b.dbk, b.mv, b.refidx, b.ipred, b.res, b.scr};
+    void *dev_bufs[] = {b.src, b.rec, b.dbk, b.mv, b.refidx, b.ipred, b.res, b.scr, b.cab, b.range, b.mbi};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
-    void *host_bufs[] = {b.h_res, b.h_src, b.h_rec, b.h_dbk};
+    void *host_bufs[] = {b.h_res, b.h_src, b.h_rec, b.h_dbk, b.h_rp};
     for (void *p : host_bufs) if (p) (void)hipHostFree(p);
     hipEvent_t evs[] = {b.ev_src, b.ev_t0, b.ev_done, b.ev_fin};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
@@ -209,7 +222,16 @@ static int alloc_entry(jmh_ctx *c, PicBuf &b) {
     ALLOC(b.src, c->fsize); ALLOC(b.rec, c->fsize); ALLOC(b.dbk, c->fsize);
     ALLOC(b.mv, c->n4 * 2 * sizeof(int16_t)); ALLOC(b.refidx, c->n4); ALLOC(b.ipred, c->n4);
     ALLOC(b.res, c->nmb * sizeof(jmh_mb_result));
-    ALLOC(b.scr, c->nmb * sizeof(MbScratch));
+    // RDOptimization 1: the picture's RdoPic sits right after its MbScratch array (jmh_device.h)
+    ALLOC(b.scr, c->cfg.rdo ? rdo_pic_offset(c->nmb) + sizeof(RdoPic) : c->nmb * sizeof(MbScratch));
+    if (c->cfg.rdo) {
+        ALLOC(b.cab, (size_t)c->nslice * JMR_NCTX);
+        ALLOC(b.range, (size_t)c->nslice * sizeof(uint32_t));
+        ALLOC(b.mbi, c->nmb * sizeof(jmr_mbinfo));
+        if (hipHostMalloc((void **)&b.h_rp, sizeof(RdoPic), hipHostMallocDefault) != hipSuccess) return JMH_E_OOM;
+        b.h_rp->lambda = 0; b.h_rp->lf = 0; b.h_rp->pad = 0;
+        b.h_rp->cab = b.cab; b.h_rp->range = b.range; b.h_rp->mbi = b.mbi;
+    }
 #undef ALLOC
     if (hipMemset(b.rec, 0, c->fsize) != hipSuccess || hipMemset(b.dbk, 0, c->fsize) != hipSuccess) return JMH_E_HIP;
     if (hipEventCreate(&b.ev_src) != hipSuccess || hipEventCreate(&b.ev_t0) != hipSuccess ||
@@ -249,6 +271,55 @@ struct DevTemps {
 
 static void ordtab_fill(std::vector<uint32_t> &tab, int sr);
 
+// RDOptimization 1: the RD stage schedule.  A macroblock's stage is one more than
+// the latest of its left, top and top-right neighbours (prediction, deblocking) and of its
+// predecessor in the slice (the CABAC coding state): with one MB row per slice the diagonals
+// x + 2y, with one slice per picture raster order.  A picture trails its reference picture by
+// lag = 1 + max over MBs of (latest stage in the MB's reference reach [0, x + 5] x [0, y + 5] -
+// its own stage) stages (PIPE_LAG's derivation, jmh_device.h).  Fills order (MB addresses by
+// stage, raster within a stage), off (stage offsets), c->dcount, c->nd, c->lag; non-zero when
+// the schedule's stages do not fit PicParams.diag (int16).
+static int rdo_schedule(jmh_ctx *c, std::vector<int> &order, std::vector<int> &off) {
+    const int mbw = c->mbw, mbh = c->mbh, n = mbw * mbh, k = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : n;
+    std::vector<int> stage(n);
+    int nd = 0;
+    for (int a = 0; a < n; a++) {
+        const int x = a % mbw, y = a / mbw;
+        int s = 0;
+        if (x > 0) s = std::max(s, stage[a - 1] + 1);
+        if (y > 0) s = std::max(s, stage[a - mbw] + 1);
+        if (y > 0 && x + 1 < mbw) s = std::max(s, stage[a - mbw + 1] + 1);
+        if (a % k != 0) s = std::max(s, stage[a - 1] + 1);
+        stage[a] = s;
+        nd = std::max(nd, s + 1);
+    }
+    if (nd > 32767) return -1;
+    c->nd = nd;
+    c->dcount.assign(nd, 0);
+    for (int a = 0; a < n; a++) c->dcount[stage[a]]++;
+    off.assign(nd + 1, 0);
+    for (int s = 0; s < nd; s++) off[s + 1] = off[s] + c->dcount[s];
+    order.assign(n, 0);
+    std::vector<int> fill(off.begin(), off.end() - 1);
+    for (int a = 0; a < n; a++) order[fill[stage[a]]++] = a;
+    std::vector<int> pm(n);                           // prefix maximum of the stages
+    for (int y = 0; y < mbh; y++)
+        for (int x = 0; x < mbw; x++) {
+            int v = stage[y * mbw + x];
+            if (x > 0) v = std::max(v, pm[y * mbw + x - 1]);
+            if (y > 0) v = std::max(v, pm[(y - 1) * mbw + x]);
+            pm[y * mbw + x] = v;
+        }
+    int lag = 1;
+    for (int y = 0; y < mbh; y++)
+        for (int x = 0; x < mbw; x++) {
+            const int X = std::min(x + 5, mbw - 1), Y = std::min(y + 5, mbh - 1);
+            lag = std::max(lag, pm[Y * mbw + X] - stage[y * mbw + x] + 1);
+        }
+    c->lag = lag;
+    return 0;
+}
+
 extern "C" {
 
 void jmh_destroy(jmh_ctx *c) {
@@ -258,7 +329,7 @@ void jmh_destroy(jmh_ctx *c) {
     if (c->cst) (void)hipStreamSynchronize(c->cst);
     for (PicBuf &b : c->ring) free_entry(b);
     void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab, c->d_scur16,
-                        c->d_sref16};
+                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     ring_free(c->ring_interp);
@@ -287,7 +358,9 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     // High 10 pictures: the EPZS wavefront (k_mb_epzs / k_mb_intra / k_mb_final on 16-bit samples)
     if (cfg->bit_depth > 8 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;
-    if (cfg->rdo) return JMH_E_UNSUPPORTED_CFG;                              // RDOptimization 1: k_mb_rdo (not yet)
+    // RDOptimization 1: the CABAC rate, EPZS searches, the 4x4 transform (k_rdo_analyse / k_rdo_final)
+    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode != 1 || cfg->search_mode != 3 || cfg->transform_8x8_mode != 0))
+        return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     int ndev = jmh_device_count();
@@ -306,8 +379,12 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     c->n4 = (size_t)c->W * c->H / 16; c->nmb = (size_t)c->mbw * c->mbh;
     c->nslots = cfg->num_frame_slots > 0 ? cfg->num_frame_slots : 1;
     c->nd = (c->mbw - 1) + 2 * (c->mbh - 1) + 1;
-    // enough pictures to cover the wavefront: one starts every PIPE_LAG diagonals
-    int auto_depth = (c->nd + PIPE_LAG - 1) / PIPE_LAG + 1;
+    c->lag = PIPE_LAG;
+    c->nslice = cfg->slice_mbs > 0 ? (int)((c->nmb + cfg->slice_mbs - 1) / cfg->slice_mbs) : 1;
+    std::vector<int> rd_order, rd_off;
+    if (cfg->rdo && rdo_schedule(c, rd_order, rd_off)) { delete c; return JMH_E_UNSUPPORTED_CFG; }
+    // enough pictures to cover the wavefront: one starts every lag stages
+    int auto_depth = (c->nd + c->lag - 1) / c->lag + 1;
     c->depth = cfg->pipeline_depth > 0 ? cfg->pipeline_depth : (auto_depth < PMAX ? auto_depth : PMAX);
     c->nring = c->depth + 2;
     c->next_id = 0; c->next_entry = 0; c->last_id = -1; c->last_entry = -1;
@@ -346,12 +423,23 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         if (hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         if (ring_init(c->ring_interp, 64) || ring_init(c->ring_mb, 64) ||
             ((cfg->flags & JMH_FLAG_KERNEL_TIMING) && (ring_init(c->ring_an, 2048) || ring_init(c->ring_fin, 2048)))) { st = JMH_E_HIP; goto fail; }
-        c->dcount.resize(c->nd); c->dymin.resize(c->nd);
-        for (int dg = 0; dg < c->nd; dg++) {
-            int ymin = dg - (c->mbw - 1) > 0 ? (dg - (c->mbw - 1) + 1) / 2 : 0;
-            int ymax = dg / 2 < c->mbh - 1 ? dg / 2 : c->mbh - 1;
-            c->dymin[dg] = ymin;
-            c->dcount[dg] = ymax >= ymin ? ymax - ymin + 1 : 0;
+        if (cfg->rdo) {   // the RD stage schedule (rdo_schedule), the tick's candidate scratch
+            c->dymin.assign(c->nd, 0);
+            int maxc = 0;
+            for (int sg = 0; sg < c->nd; sg++) maxc = std::max(maxc, c->dcount[sg]);
+            ALLOC(c->d_sched, rd_order.size() * sizeof(int32_t));
+            ALLOC(c->d_soff, rd_off.size() * sizeof(int32_t));
+            ALLOC(c->d_rscr, (size_t)PMAX * maxc * jmh_rdo_scratch_bytes());
+            if (hipMemcpy(c->d_sched, rd_order.data(), rd_order.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(c->d_soff, rd_off.data(), rd_off.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        } else {
+            c->dcount.resize(c->nd); c->dymin.resize(c->nd);
+            for (int dg = 0; dg < c->nd; dg++) {
+                int ymin = dg - (c->mbw - 1) > 0 ? (dg - (c->mbw - 1) + 1) / 2 : 0;
+                int ymax = dg / 2 < c->mbh - 1 ? dg / 2 : c->mbh - 1;
+                c->dymin[dg] = ymin;
+                c->dcount[dg] = ymax >= ymin ? ymax - ymin + 1 : 0;
+            }
         }
     }
 #undef ALLOC
@@ -467,6 +555,8 @@ static int issue_tick(jmh_ctx *c) {
     t.slice_mbs = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : c->mbw * c->mbh;
     t.bd = c->bd;
     t.ordtab = c->d_ordtab;
+    t.rdo = c->cfg.rdo;
+    t.sched = c->d_sched; t.soff = c->d_soff; t.rscr = c->d_rscr;
     int act[PMAX], nact = 0, nP = 0;
     const int nf = (int)c->fl.size();
     std::vector<int> before(nf);
@@ -475,7 +565,7 @@ static int issue_tick(jmh_ctx *c) {
         const Flight &f = c->fl[i];
         if (f.stage >= c->nd) continue;
         if (f.pred_id >= 0 && i > 0 && c->fl[i - 1].id == f.pred_id &&
-            before[i - 1] < c->nd && before[i - 1] - f.stage < PIPE_LAG) continue;
+            before[i - 1] < c->nd && before[i - 1] - f.stage < c->lag) continue;
         act[nact++] = i;
         nP += f.pp.slice_type == JMH_P_SLICE;
     }
@@ -504,7 +594,9 @@ static int issue_tick(jmh_ctx *c) {
     if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
         if (kt) HCHK(ring_begin(c->ring_an, c->st));
-        if (t.me_in_analyse) {                          // FFS: motion search + intra in k_mb_analyse
+        if (t.rdo) {                                    // RDOptimization 1: analyse + final
+            HCHK(jmh_launch_rdo(t, c->st));
+        } else if (t.me_in_analyse) {                   // FFS: motion search + intra in k_mb_analyse
             HCHK(jmh_launch_analyse(t, c->st));
             if (t.t8) HCHK(jmh_launch_intra8(t, c->st));   // Intra8x8 decision (High profile)
         } else {                                        // EPZS (one wave per MB) / SearchMode -1
@@ -513,7 +605,7 @@ static int issue_tick(jmh_ctx *c) {
             HCHK(jmh_launch_intra(t, c->st));           // all intra decisions incl. Intra8x8
         }
         if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
-        HCHK(jmh_launch_final(t, c->st));
+        if (!t.rdo) HCHK(jmh_launch_final(t, c->st));
         if (kt) HCHK(ring_end(c->ring_fin, c->st));
         c->ticks_total++;
         c->timing.ticks++;
@@ -596,6 +688,11 @@ static int push_picture(jmh_ctx *c, const uint8_t *src, int entry, const jmh_fra
     q.lf_disable = fp->lf_disable; q.lf_offA = 2 * fp->lf_alpha_div2; q.lf_offB = 2 * fp->lf_beta_div2;
     b.unpopped = readback;
     b.deblocked = fp->deblock != 0;
+    if (c->cfg.rdo) {   // the picture's lambdas into its RdoPic (stream order: before its ticks)
+        b.h_rp->lambda = fp->lambda_rd;
+        b.h_rp->lf = fp->lambda_factor_rd;
+        HCHK(hipMemcpyAsync(reinterpret_cast<uint8_t *>(b.scr) + rdo_pic_offset(c->nmb), b.h_rp, sizeof(RdoPic), hipMemcpyHostToDevice, c->st));
+    }
     c->fl.push_back(f);
     c->last_id = f.id;
     c->last_entry = entry;
@@ -616,6 +713,10 @@ static int check_params(const jmh_ctx *c, const jmh_frame_params *fp) {
     if (fp->deblock && (fp->lf_disable < 0 || fp->lf_disable > 2 || fp->lf_alpha_div2 < -6 || fp->lf_alpha_div2 > 6 ||
                         fp->lf_beta_div2 < -6 || fp->lf_beta_div2 > 6)) return JMH_E_INVALID_ARG;
     if (fp->slice_type == JMH_P_SLICE && c->ref_kind == REF_NONE) return JMH_E_STATE;
+    // RDOptimization 1: lambda_mode > 0 and its factor (at most 65536 * sqrt(0.85 * 2^21) ~ 8.4e7 at
+    // QP 51 + 12, kept below 2^31 / 64 so that factor * mvbits fits the searches' 32-bit costs)
+    if (c->cfg.rdo && !(fp->lambda_rd > 0 && fp->lambda_rd < 1e9 && fp->lambda_factor_rd > 0 && fp->lambda_factor_rd < (1 << 25)))
+        return JMH_E_INVALID_ARG;
     return JMH_OK;
 }
 

@@ -212,20 +212,17 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                     }
                     int D = ssd(s->org + oy * 16 + ox, 16, r8, 8, 8, 8);
                     /* rate: sub_mb_type, mvds, cbp bit, luma (RDCost_for_8x8blocks) */
-                    int16_t mvd[16][2], L16[16][16];
-                    memset(mvd, 0, sizeof(mvd));
-                    memset(L16, 0, sizeof(L16));
+                    int16_t mvd[4][2];
                     for (int b4 = 0; b4 < 4; b4++) {
                         int kk = (2 * (block >> 1) + (b4 >> 1)) * 4 + 2 * (block & 1) + (b4 & 1);
-                        mvd[kk][0] = (int16_t)(s->all_mv[mode][kk][0] - s->pmv[mode][kk][0]);
-                        mvd[kk][1] = (int16_t)(s->all_mv[mode][kk][1] - s->pmv[mode][kk][1]);
-                        memcpy(L16[kk], lev[b4], 32);
+                        mvd[b4][0] = (int16_t)(s->all_mv[mode][kk][0] - s->pmv[mode][kk][0]);
+                        mvd[b4][1] = (int16_t)(s->all_mv[mode][kk][1] - s->pmv[mode][kk][1]);
                     }
                     uint8_t stc[JMR_NCTX];
                     memcpy(stc, st8, JMR_NCTX);
                     jmr_eng eb = {stc, rg8, 0};
                     jmr_cur cc = cur;
-                    jmr_b8(&eb, A, B, &cc, block, mode, (const int16_t(*)[2])mvd, cost > 0, (const int16_t(*)[16])L16);
+                    jmr_b8(&eb, A, B, &cc, block, mode, (const int16_t(*)[2])mvd, cost > 0, (const int16_t(*)[16])lev);
                     double rd = (double)D + lam * (double)eb.bits;
                     if (rd < best) {
                         best = rd; bm = mode; bcost = cost; bcbp = cbpbit; bblk = blk;

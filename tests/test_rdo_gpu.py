@@ -1,0 +1,123 @@
+"""RDOptimization = 1 on the MI355X (row f4, config 5): k_rdo_analyse / k_rdo_final on the RD stage
+schedule must equal the CPU oracle (oracle/rdo.c) bit for bit -- every macroblock's result
+(mode, MVs, levels, the chosen candidate's rate in min_cost) and the reconstruction -- and the
+product lencod with the device RD loop must write the same bitstream as the CPU lencod, with the
+writer's RD rate check at 0 mismatches.  JM parity of the RD choices is unpinned
+(docs/JM_SEMANTICS.md items 53-60)."""
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from jmpaths import LENCOD, LENCOD_CPU, ensure_built, load_jmhip
+from test_gpu_parity import assert_same, hbd_seq, moving_seq, run_chain, run_lencod, synth_seq
+
+jmhip = load_jmhip()
+pytestmark = pytest.mark.gpu
+
+RDO = dict(rdo=1, symbol_mode=1, search_mode=3)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    ensure_built()
+    jmhip.load()
+
+
+def rdo_pair(w, h, pics, qp, cqp=0, bd=8, **kw):
+    g = jmhip.Encoder(w, h, bit_depth=bd, **RDO, **kw)
+    o = oracle_lib.OracleEncoder(w, h, bit_depth=bd, **RDO, **kw)
+    for i, pic in enumerate(pics):
+        st = jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE
+        gres, grec = g.encode(*pic, st, qp, chroma_qp_offset=cqp)
+        ores, orec = o.encode(*pic, st, qp, chroma_qp_offset=cqp)
+        assert_same(gres, grec, ores, orec, w // 16)
+        assert (gres["min_cost"] > 0).all()          # every MB reports its rate (bits)
+        g.set_reference(*orec)
+        o.set_reference(*orec)
+    return gres
+
+
+def test_rdo_qcif_ipp():
+    pics = synth_seq(176, 144, 4, 71)
+    res = rdo_pair(176, 144, pics, 28, search_range=16)
+    assert len(set(res["mb_type"].tolist())) > 2      # several modes actually compete
+
+
+@pytest.mark.parametrize("kw,qp,cqp", [
+    (dict(search_range=8), 0, 0),
+    (dict(search_range=8), 51, 0),
+    (dict(search_range=16, slice_mbs=11), 36, -5),
+    (dict(search_range=8, slice_mbs=1), 28, 0),
+    (dict(search_range=8, use_hadamard=0, restrict_search_range=0), 24, 0),
+    (dict(search_range=8, inter_search=(0, 1, 1, 1, 0, 1, 1), epzs_dual_refinement=1), 20, 3),
+    (dict(search_range=4, inter_search=(1, 0, 0, 0, 0, 0, 0)), 30, 0),
+    (dict(search_range=16, jm_version=10), 31, 0),
+])
+def test_rdo_configs(kw, qp, cqp):
+    pics = moving_seq(176, 144, 3, seed=80 + qp)
+    rdo_pair(176, 144, pics, qp, cqp, **kw)
+
+
+@pytest.mark.parametrize("bd,qp,cqp", [(10, 28, 0), (9, 4, -12), (10, 51, 12)])
+def test_rdo_high10(bd, qp, cqp):
+    pics = hbd_seq(176, 144, 3, seed=90 + qp, bd=bd)
+    rdo_pair(176, 144, pics, qp, cqp, bd=bd, search_range=16, slice_mbs=11)
+
+
+def test_rdo_config5_width_3840():
+    """Config 5's shape at its real width: High 10, one MB row per slice (SliceArgument 240), EPZS
+    SR 32, RDO on: the stage schedule is the diagonal wavefront, 240-MB CABAC chains per slice."""
+    w, h = 3840, 96
+    pics = hbd_seq(w, h, 3, seed=43, bd=10)
+    rdo_pair(w, h, pics, 28, bd=10, search_range=32, slice_mbs=240)
+
+
+@pytest.mark.parametrize("slice_mbs", [40, 0, 100])
+def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
+    """Pictures in flight on the RD stage schedule (one-row slices: diagonals, lag 16; one slice
+    per picture: raster order, lag 5 mbw + 6; 100-MB slices straddling rows) with the device-
+    deblocked reference == one picture at a time."""
+    w, h, n = 640, 320, 5
+    pics = moving_seq(w, h, n, seed=5, step=(-45, 38))
+    kw = dict(search_range=32, slice_mbs=slice_mbs, **RDO)
+    a = jmhip.Encoder(w, h, **kw)
+    b = jmhip.Encoder(w, h, pipeline_depth=1, **kw)
+    assert a.depth > 1
+    ra = run_chain(a, pics, 30, (0, 0, 0), True)
+    rb = run_chain(b, pics, 30, (0, 0, 0), False)
+    for (gres, grec, gdbk), (ores, orec, odbk) in zip(ra, rb):
+        assert_same(gres, grec, ores, orec, w // 16)
+        for x, y in zip(gdbk, odbk):
+            assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("extra", [
+    ["InputFile=synthetic:71", "FramesToBeEncoded=5", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "ProfileIDC=77"],
+    ["InputFile=synthetic:72", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=77", "SliceMode=1", "SliceArgument=22", "IntraPeriod=3", "QPRemainingFrame=33"],
+    ["InputFile=synthetic:73", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "SliceMode=1", "SliceArgument=22",
+     "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=2", "LoopFilterBetaOffset=-1"],
+])
+def test_rdo_lencod_bitstream_identical(extra):
+    """The product lencod (device RD loop, device deblocking, pipelined pictures, writer threads)
+    and the CPU lencod write identical bitstreams and reconstructions; both writers check every
+    macroblock's RD rate against the CABAC bits they emit."""
+    args = extra + ["SymbolMode=1", "RDOptimization=1", "SearchMode=3"]
+    with tempfile.TemporaryDirectory() as g, tempfile.TemporaryDirectory() as c:
+        lg = run_lencod(LENCOD, g, args)
+        lc = run_lencod(LENCOD_CPU, c, args)
+        for log in (lg, lc):
+            assert "RD rate check:" in log and ", 0 whose RD rate differs" in log, log
+        assert open(f"{g}/a.264", "rb").read() == open(f"{c}/a.264", "rb").read()
+        assert open(f"{g}/rec.yuv", "rb").read() == open(f"{c}/rec.yuv", "rb").read()
+
+
+def test_rdo_rejects_unsupported():
+    for kw in (dict(rdo=1, symbol_mode=0, search_mode=3), dict(rdo=1, symbol_mode=1, search_mode=0),
+               dict(rdo=1, symbol_mode=1, search_mode=3, transform_8x8_mode=1)):
+        with pytest.raises(jmhip.JmhError):
+            jmhip.Encoder(64, 48, search_range=8, **kw)

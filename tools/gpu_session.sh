@@ -7,6 +7,7 @@
 #   peak    tools/sad_peak_bin                       -> gpurun_out/TAG_sad_peak.json
 #   tests   pytest -m gpu (all)                      -> gpurun_out/TAG_pytest.log
 #   fast    pytest -m "gpu and not slow"             -> gpurun_out/TAG_pytest.log
+#   rdo     pytest tests/test_rdo_gpu.py (RDOptimization 1; failures reported, not fatal)
 #   smoke   __graft_entry__.smoke()                  -> gpurun_out/TAG_smoke.log
 #   bench   bench.py (defaults, with CPU baseline)   -> gpurun_out/TAG_bench.json
 #   bench20 bench.py --steps 20 --warmup 5 (the driver's invocation, no CPU baseline)
@@ -42,6 +43,9 @@ for s in "$@"; do
                 > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc ;;
     hbd)    run hbd 600 python -u -m pytest tests -v -m gpu -k "high10 or lencod_bitstream" -p no:cacheprovider --timeout 300 \
                 --timeout-method thread > gpurun_out/${TAG}_hbd.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_hbd.log
+            [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
+    rdo)    run rdo 900 python -u -m pytest tests/test_rdo_gpu.py -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+                > gpurun_out/${TAG}_rdo.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_rdo.log
             [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     fast)   run fast 600 python -u -m pytest tests -x -v -m "gpu and not slow" -p no:cacheprovider --timeout 120 \
                 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?; tail -5 gpurun_out/${TAG}_pytest.log
