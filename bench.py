@@ -27,9 +27,11 @@ k mod the device count); under torchrun WORLD_SIZE must equal --gpus.
 
 --config 3 runs BASELINE.json's config 3 instead (a variant line, not the headline metric):
 2160p synthetic, High profile, EPZS (SearchMode 3) + adaptive 8x8 transform (Transform8x8Mode 1).
---config 5 runs config 5's hot path (a variant line): 2160p synthetic 10-bit (High 10, 16-bit samples
-in HBM), EPZS + 8x8 transform, SliceMode 1 with 240-MB slices (one MB row), RDO off -- CABAC is
-entropy coding (host, outside the ME+transform metric as for every config) and RDO-on is not built.
+--config 5 runs config 5 (a variant line): 2160p synthetic 10-bit (High 10, 16-bit samples in HBM),
+EPZS, SliceMode 1 with 240-MB slices (one MB row), RDOptimization 1 -- the device RD loop with the
+CABAC rate of every candidate (k_rdo_analyse + k_rdo_final on the RD stage schedule; the bitstream
+itself is written on the host, outside the metric as for every config).  --rdo 0 runs the RDO-off
+variant of the same shape (EPZS + 8x8 transform).
 
 Prints ONE JSON line (rank 0).
 """
@@ -58,13 +60,20 @@ CONFIGS = {
             workload="2160p synthetic YUV420, High profile (ProfileIDC 100), EPZS SearchMode=3 SearchRange=32, "
                      "Transform8x8Mode=1 (Intra8x8 + TransformDecision), UseHadamard=1, 7 inter block sizes, RDO off, "
                      "QP 28, IDR + {nf}-picture P sequence cycled (one independent stream per GPU)"),
-    5: dict(metric="ME+transform megapixels/sec @2160p High10 10-bit EPZS SR=32 + 8x8 transform, 240-MB slices, RDO off "
-                   "(config 5 variant)", disp=(3840, 2160), coded=(3840, 2160), search_mode=3, t8=1, bd=10, slice_mbs=240,
+    5: dict(metric="ME+transform+RD megapixels/sec @2160p High10 10-bit EPZS SR=32, CABAC RDO on, 240-MB slices (config 5)",
+            disp=(3840, 2160), coded=(3840, 2160), search_mode=3, t8=0, bd=10, slice_mbs=240, rdo=1,
             workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), EPZS SearchMode=3 "
-                     "SearchRange=32, Transform8x8Mode=1, UseHadamard=1, 7 inter block sizes, RDO off (RDOptimization=1 "
-                     "not built), CABAC on the host (entropy coding, outside the metric), QP 28, IDR + {nf}-picture P "
-                     "sequence cycled (one independent stream per GPU)"),
+                     "SearchRange=32, UseHadamard=1, 7 inter block sizes, RDOptimization=1 with SymbolMode=1 (the CABAC "
+                     "rate of every candidate on the device), Transform8x8Mode=0, QP 28, IDR + {nf}-picture P sequence "
+                     "cycled (one independent stream per GPU)"),
 }
+# --config 5 --rdo 0: the RDO-off variant of config 5's shape (EPZS + 8x8 transform)
+CONFIG5_RDO_OFF = dict(metric="ME+transform megapixels/sec @2160p High10 10-bit EPZS SR=32 + 8x8 transform, 240-MB slices, "
+                              "RDO off (config 5 variant)", t8=1, rdo=0,
+                       workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), EPZS SearchMode=3 "
+                                "SearchRange=32, Transform8x8Mode=1, UseHadamard=1, 7 inter block sizes, RDO off, QP 28, "
+                                "IDR + {nf}-picture P sequence cycled (one independent stream per GPU)")
+RDO = 0              # RDOptimization of the run (the config's, or --rdo)
 DISP_W, DISP_H = 1920, 1080
 W, H = 1920, 1088
 SLICE_MBS = 0        # --slice-mbs: SliceMode 1 / SliceArgument (0: one slice per picture)
@@ -91,10 +100,14 @@ def load_module(name, path):
     return mod
 
 
-def use_config(k, size=None):
-    """switch the module-level workload constants to BASELINE.json config k (size: test override)"""
-    global DISP_W, DISP_H, W, H, NMB, BYTES_PER_FRAME, AD_PER_FRAME, BD, BYTES_PER_PIXEL
-    c = CONFIGS[k]
+def use_config(k, size=None, rdo=None):
+    """switch the module-level workload constants to BASELINE.json config k (size: test override;
+    rdo: override of the config's RDOptimization, config 5 only)"""
+    global DISP_W, DISP_H, W, H, NMB, BYTES_PER_FRAME, AD_PER_FRAME, BD, BYTES_PER_PIXEL, RDO
+    c = dict(CONFIGS[k])
+    if k == 5 and rdo == 0:
+        c.update(CONFIG5_RDO_OFF)
+    RDO = c.get("rdo", 0)
     BD = c.get("bd", 8)
     BYTES_PER_PIXEL = 6.0 * (2 if BD > 8 else 1) + 3.0
     (DISP_W, DISP_H), (W, H) = c["disp"], c["coded"]
@@ -131,7 +144,7 @@ def cpu_one_picture(seed, search_mode, t8=0, dump=None):
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
     frames = [jm.synth_frame(DISP_W, DISP_H, seed, i, bit_depth=BD) for i in range(2)]
     o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
-                                 slice_mbs=SLICE_MBS, bit_depth=BD)
+                                 slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO)
     ires, irec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
     t0 = time.perf_counter()
     o.set_reference(*irec)
@@ -152,7 +165,7 @@ def cpu_workers(n, config, search_mode, size, dump_dir=None):
         if dump_dir and k == 0:
             cmd.append(os.path.join(dump_dir, "oracle_seed0.npz"))
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
-                                      env=dict(os.environ, JMH_BENCH_SLICE_MBS=str(SLICE_MBS))))
+                                      env=dict(os.environ, JMH_BENCH_SLICE_MBS=str(SLICE_MBS), JMH_BENCH_RDO=str(RDO))))
     out = []
     for p in procs:
         s = p.communicate()[0]
@@ -173,7 +186,7 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(config, search_mode, dump_dir):
+def cpu_baseline(config, search_mode, dump_dir, T8):
     """The CPU path timed on this node's host cores: one process on one core (JM is
     single threaded; the reported baseline), and n processes on distinct streams at once
     (aggregate, n = min(16, cores available to this process)).  Worker 0 of the one-core run
@@ -181,8 +194,9 @@ def cpu_baseline(config, search_mode, dump_dir):
     one = cpu_workers(1, config, search_mode, (DISP_W, DISP_H), dump_dir)[0]
     n = max(1, min(16, len(os.sched_getaffinity(0))))
     many = cpu_workers(n, config, search_mode, (DISP_W, DISP_H))
-    mode = {0: "FFS", -1: "full search", 3: "EPZS"}[search_mode] + (" + 8x8 transform" if CONFIGS[config]["t8"] else "") \
-        + (f", {BD}-bit" if BD > 8 else "") + (f", {SLICE_MBS}-MB slices" if SLICE_MBS else "")
+    mode = {0: "FFS", -1: "full search", 3: "EPZS"}[search_mode] + (" + 8x8 transform" if T8 else "") \
+        + (f", {BD}-bit" if BD > 8 else "") + (f", {SLICE_MBS}-MB slices" if SLICE_MBS else "") \
+        + (", RDO on (CABAC rate)" if RDO else "")
     return {"value": round(DISP_W * DISP_H / 1e6 / one, 4), "unit": "MP/s", "cores": 1, "kind": "port",
             "sample": f"one {DISP_W}x{DISP_H} P picture (coded {W}x{H}, {NMB} MBs, {mode} SR=32, QP {QP}) incl. "
                       f"quarter-pel interpolation, oracle/liboracle.so -O2 scalar, {one:.1f} s, on {cpu_model()}",
@@ -198,7 +212,7 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
     d = np.load(dump)
     frames = [jm.synth_frame(DISP_W, DISP_H, 0, i, bit_depth=BD) for i in range(2)]
     g = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
-                   pipeline_depth=1, slice_mbs=SLICE_MBS, bit_depth=BD)
+                   pipeline_depth=1, slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO)
     try:
         ires, irec = g.encode(*frames[0], jm.JMH_I_SLICE, QP)
         g.set_reference(*irec)
@@ -297,7 +311,7 @@ def main():
     if len(sys.argv) in (6, 7) and sys.argv[1] == "--cpu-worker":    # child of cpu_baseline()
         SLICE_MBS = int(os.environ.get("JMH_BENCH_SLICE_MBS", "0"))
         w, h = (int(v) for v in sys.argv[5].split("x"))
-        c = use_config(int(sys.argv[3]), (w, h))
+        c = use_config(int(sys.argv[3]), (w, h), int(os.environ.get("JMH_BENCH_RDO", "0")))
         print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[4]), c["t8"], sys.argv[6] if len(sys.argv) == 7 else None),
               flush=True)
         return 0
@@ -310,7 +324,9 @@ def main():
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive / latency measurement")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 5),
                     help="BASELINE.json config: 2 = 1080p Baseline FFS (the headline), 3 = 2160p High EPZS + 8x8, "
-                         "5 = 2160p High 10 EPZS + 8x8 with 240-MB slices (RDO off)")
+                         "5 = 2160p High 10 EPZS, CABAC RDO on, 240-MB slices")
+    ap.add_argument("--rdo", type=int, default=None, choices=(0, 1),
+                    help="config 5: RDOptimization (default 1; 0 = the RDO-off variant with the 8x8 transform)")
     ap.add_argument("--search-mode", type=int, default=None, choices=(0, -1, 3),
                     help="override the config's SearchMode (config 2 variants: -1 full search, 3 EPZS)")
     ap.add_argument("--slice-mbs", type=int, default=None,
@@ -332,7 +348,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pinned = pin_rank(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))) if world > 1 else None
     size = tuple(int(v) for v in args.size.split("x")) if args.size else None
-    cfg = use_config(args.config, size)
+    if args.rdo is not None and args.config != 5:
+        ap.error("--rdo applies to --config 5")
+    cfg = use_config(args.config, size, args.rdo)
     SLICE_MBS = max(0, cfg.get("slice_mbs", 0) if args.slice_mbs is None else args.slice_mbs)
     search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
     dist = None
@@ -348,7 +366,7 @@ def main():
     device = local % ndev
     frames = [jm.synth_frame(DISP_W, DISP_H, rank, i, bit_depth=BD) for i in range(args.frames + 1)]
     enc = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, slots=len(frames),
-                     kernel_timing=True, transform_8x8_mode=cfg["t8"], slice_mbs=SLICE_MBS, bit_depth=BD)
+                     kernel_timing=True, transform_8x8_mode=cfg["t8"], slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO)
     stream = streams.PStream(enc, frames, QP, deblock=None if args.no_deblock else (0, 0, 0))
     dt = streams.timed_run(stream, args.steps, args.warmup, dist, on_start=enc.timing)   # on_start resets the event sums
     tm = enc.timing()                                     # event sums of the timed steps only
@@ -402,7 +420,7 @@ def main():
         "algorithmic_bytes_per_launch": round(bytes_per_launch),
     }
     launch_info = {
-        "kernel": "k_mb_analyse" if ffs else
+        "kernel": "k_rdo_analyse + k_rdo_final (the tick's RD launches)" if RDO else "k_mb_analyse" if ffs else
                   ("k_mb_epzs" if search_mode == 3 else "k_mb_me_full") + " + k_mb_intra (the tick's analysis launches)",
         "avg_launch_ms": round(an_launch_ms, 5),
         "launches_per_picture": round(an_per_pic, 2),
@@ -449,8 +467,8 @@ def main():
         "roofline": roofline,
         # per-launch averages (sampled every 8th diagonal) x launches per picture
         "kernel_ms_per_picture": {"wavefront": round(mb_ms_pic, 4),
-                                  "k_mb_analyse": round(an_launch_ms * an_per_pic, 4),
-                                  "k_mb_final": round(tm.final_ms / max(1, tm.final_launches) * an_per_pic, 4)},
+                                  ("k_rdo_analyse+k_rdo_final" if RDO else "k_mb_analyse"): round(an_launch_ms * an_per_pic, 4),
+                                  "k_mb_final": None if RDO else round(tm.final_ms / max(1, tm.final_launches) * an_per_pic, 4)},
         "host_path": None if host is None else {
             "pcie_inclusive_mp_s": round(host[0], 3),
             "single_picture_latency_ms": round(host[1], 3),
@@ -462,7 +480,7 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline and complete:
         with tempfile.TemporaryDirectory() as tmp:
-            out["cpu_baseline"] = cpu_baseline(args.config, search_mode, tmp)
+            out["cpu_baseline"] = cpu_baseline(args.config, search_mode, tmp, cfg["t8"])
             out["verified"] = verify_against_oracle(jm, os.path.join(tmp, "oracle_seed0.npz"), search_mode, cfg["t8"],
                                                     device)
     print(json.dumps(out), flush=True)

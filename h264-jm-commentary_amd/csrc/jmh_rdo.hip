@@ -603,7 +603,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
 }
 
 template <class pel>
-__global__ __launch_bounds__(NT) void k_rdo_analyse(const TickArgs t) {
+__global__ __launch_bounds__(NT, 2) void k_rdo_analyse(const TickArgs t) {
     __shared__ union {
         RdoInterS<pel> in;
         RdoIntraS<pel> ia;

@@ -24,20 +24,23 @@ def test_config_table():
     c = b.use_config(2)
     assert (b.W, b.H, b.BD, b.BYTES_PER_PIXEL, c["search_mode"]) == (1920, 1088, 8, 9.0, 0)
     c = b.use_config(5)
-    assert (b.W, b.H, b.BD, c["slice_mbs"], c["t8"], c["search_mode"]) == (3840, 2160, 10, 240, 1, 3)
+    assert (b.W, b.H, b.BD, c["slice_mbs"], c["t8"], c["search_mode"], b.RDO) == (3840, 2160, 10, 240, 0, 3, 1)
     assert b.BYTES_PER_PIXEL == 15.0   # four 16-bit picture terms + int16 levels
+    c = b.use_config(5, rdo=0)          # the RDO-off variant of config 5's shape
+    assert (c["t8"], b.RDO) == (1, 0) and "RDO off" in c["metric"]
     c = b.use_config(3)
     assert (b.BD, b.BYTES_PER_PIXEL) == (8, 9.0)
 
 
-@pytest.mark.parametrize("config,mode", [(2, 0), (3, 3), (5, 3)])
-def test_cpu_worker(config, mode, tmp_path):
-    """the cpu_baseline child on a small picture: prints its seconds; config 5 dumps 16-bit recon"""
+@pytest.mark.parametrize("config,mode,rdo", [(2, 0, 0), (3, 3, 0), (5, 3, 1), (5, 3, 0)])
+def test_cpu_worker(config, mode, rdo, tmp_path):
+    """the cpu_baseline child on a small picture: prints its seconds; config 5 dumps 16-bit recon
+    (RDO on: the oracle's RD loop; its MBs carry their CABAC rates in min_cost)"""
     ensure_built()
     dump = tmp_path / "d.npz"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-worker", "0", str(config), str(mode), "64x48",
                         str(dump)], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, JMH_BENCH_SLICE_MBS="4" if config == 5 else "0"))
+                       env=dict(os.environ, JMH_BENCH_SLICE_MBS="4" if config == 5 else "0", JMH_BENCH_RDO=str(rdo)))
     assert r.returncode == 0, r.stderr
     assert float(r.stdout.split()[-1]) > 0
     import numpy as np
@@ -45,3 +48,5 @@ def test_cpu_worker(config, mode, tmp_path):
     assert d["py"].dtype == (np.uint16 if config == 5 else np.uint8)
     if config == 5:
         assert int(d["py"].max()) > 255
+    if rdo:
+        assert d["pres"]["min_cost"].sum() > 0

@@ -14,6 +14,9 @@
 #   benchf8 bench20 with JMH_FINAL_OCC8=1 (k_mb_final's 8-per-CU build for every tick: A/B)
 #   c3      bench.py --config 3 (with CPU baseline)  -> gpurun_out/TAG_c3_bench.json
 #   c3s     config 3 with SliceMode 1, SliceArgument 240 (config 5's one-row slices, 8-bit, CAVLC)
+#   c5      bench.py --config 5 (High 10, RDO on, 240-MB slices; with CPU baseline)
+#   c5q     the same, 60 steps, no CPU baseline / host path (a quick GPU number)
+#   c5off   config 5's RDO-off variant (EPZS + 8x8 transform)
 #   lencodc5 lencodc3 with one slice and with SliceArgument 240 (135 one-row slices per picture)
 #   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
 #   profc3  the same for config 3
@@ -60,15 +63,21 @@ for s in "$@"; do
             cat gpurun_out/${TAG}_benchf8.json ;;
     c3)     run c3 900 python bench.py --config 3 > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3_bench.err || exit $?
             cat gpurun_out/${TAG}_c3_bench.json ;;
-    c5)     run c5 900 python bench.py --config 5 > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5_bench.err || exit $?
+    c5)     run c5 1100 python bench.py --config 5 > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5_bench.err || exit $?
             cat gpurun_out/${TAG}_c5_bench.json ;;
+    c5q)    run c5q 600 python bench.py --config 5 --steps 60 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_c5q_bench.json \
+                2> gpurun_out/${TAG}_c5q_bench.err || exit $?
+            cat gpurun_out/${TAG}_c5q_bench.json ;;
+    c5off)  run c5off 900 python bench.py --config 5 --rdo 0 --no-cpu-baseline > gpurun_out/${TAG}_c5off_bench.json \
+                2> gpurun_out/${TAG}_c5off_bench.err || exit $?
+            cat gpurun_out/${TAG}_c5off_bench.json ;;
     c3s)    run c3s 900 python bench.py --config 3 --slice-mbs 240 > gpurun_out/${TAG}_c3s_bench.json 2> gpurun_out/${TAG}_c3s_bench.err || exit $?
             cat gpurun_out/${TAG}_c3s_bench.json ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}" -o ${TAG} --output-format csv -- \
                 python3 "$R/bench.py" --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
             find gpurun_out/prof_${TAG} -name "*kernel_stats*" -exec cat {} \; ;;
     profc5) run profc5 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c5" -o ${TAG}_c5 --output-format csv -- \
-                python3 "$R/bench.py" --config 5 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc5.log 2>&1 || exit $?
+                python3 "$R/bench.py" --config 5 --steps 60 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc5.log 2>&1 || exit $?
             find gpurun_out/prof_${TAG}_c5 -name "*kernel_stats*" -exec cat {} \; ;;
     profc3) run profc3 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c3" -o ${TAG}_c3 --output-format csv -- \
                 python3 "$R/bench.py" --config 3 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc3.log 2>&1 || exit $?
