@@ -85,15 +85,23 @@ JMR_FN void jmr_init_contexts(uint8_t *st, int slice_i, int qp) {
 
 JMR_FN int jmr_renorm_steps(uint32_t r) { return __builtin_clz(r) - 23; }   /* r in [2, 510] */
 
+/* Table 9-44 lookups.  A kernel may define JMR_LPS / JMR_TLPS before including this header to
+   read LDS copies (a __constant__ array indexed per lane is a vector memory load, and a bin is a
+   dependent chain: context -> rangeTabLPS -> context) */
+#ifndef JMR_LPS
+#define JMR_LPS(s, q) jmr_lps[s][q]
+#define JMR_TLPS(s) jmr_trans_lps[s]
+#endif
+
 JMR_FN void jmr_bin(jmr_eng *e, int ctx, int bin) {   /* 9.3.4.2 */
     const uint32_t v = e->st[ctx];
     int s = (int)(v >> 1), mps = (int)(v & 1);
-    const uint32_t lps = jmr_lps[s][(e->range >> 6) & 3];
+    const uint32_t lps = JMR_LPS(s, (e->range >> 6) & 3);
     uint32_t r = e->range - lps;
     if (bin != mps) {
         r = lps;
         if (s == 0) mps ^= 1;
-        s = jmr_trans_lps[s];
+        s = JMR_TLPS(s);
     } else if (s < 62) s++;
     e->st[ctx] = (uint8_t)((s << 1) | mps);
     const int n = jmr_renorm_steps(r);
@@ -141,6 +149,7 @@ typedef struct jmr_cand {
     const int16_t *luma_dc;       /* [16] (I16)                                                   */
     const int16_t (*cdc)[4];      /* [2][4]                                                       */
     const int16_t (*cac)[4][16];  /* [2][4][16], [..][0] unused                                   */
+    int16_t (*mvw)[2];            /* [16] work: the mvds of the partitions written so far         */
 } jmr_cand;
 
 /* the current macroblock's partial coding state inside the P8x8 RD loop (what cs_b8 carries of
@@ -305,7 +314,7 @@ JMR_FN void jmr_mb(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, const j
             const int x4 = ((blk >> 2) & 1) * 2 + (blk & 1), y4 = (blk >> 3) * 2 + ((blk >> 1) & 1);
             jmr_ipred_mode(e, r->ipm[y4 * 4 + x4]);
         }
-    int16_t mv[16][2];                                 /* mvds of the partitions written so far */
+    int16_t (*mv)[2] = r->mvw;                         /* mvds of the partitions written so far */
     for (int k = 0; k < 16; k++) { mv[k][0] = 0; mv[k][1] = 0; }
     if (intra) {                                       /* intra_chroma_pred_mode: TU cMax 3 */
         const int cm = r->cmode;

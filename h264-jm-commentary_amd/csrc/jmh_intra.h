@@ -92,6 +92,40 @@ __device__ __forceinline__ void i16_pick(const DevParams &d, const pel *org, con
 }
 
 
+// the Intra16x16 DC path of dct_luma_16x16 [J] on one lane: dc[16] (the blocks' DC coefficients,
+// raster) -> the 4x4 Hadamard, the DC levels (scan order) in dclev and the dequantised DCs in dcdq
+__device__ __forceinline__ void i16_dc(int *dc, int16_t *dclev, int *dcdq, int qp, int qp_const) {
+    const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per, qp_const2 = qp_const << 1;
+    for (int yy = 0; yy < 4; yy++) {
+        int *r = dc + 4 * yy;
+        int a0 = r[0] + r[3], a3 = r[0] - r[3], a1 = r[1] + r[2], a2 = r[1] - r[2];
+        r[0] = a0 + a1; r[2] = a0 - a1; r[1] = a3 + a2; r[3] = a3 - a2;
+    }
+    for (int xx = 0; xx < 4; xx++) {
+        int a0 = dc[xx] + dc[12 + xx], a3 = dc[xx] - dc[12 + xx], a1 = dc[4 + xx] + dc[8 + xx], a2 = dc[4 + xx] - dc[8 + xx];
+        dc[xx] = (a0 + a1) >> 1; dc[8 + xx] = (a0 - a1) >> 1; dc[4 + xx] = (a3 + a2) >> 1; dc[12 + xx] = (a3 - a2) >> 1;
+    }
+    int lev[16];
+    for (int k = 0; k < 16; k++) {
+        int pos = scan_of(k);
+        int level = (abs(dc[pos]) * c_q3[qp_rem][0] + qp_const2) >> (q_bits + 1);
+        dclev[k] = (int16_t)isign(level, dc[pos]);
+        lev[pos] = dclev[k];
+    }
+    int t[16];
+    for (int yy = 0; yy < 4; yy++) {
+        const int *cc = lev + 4 * yy;
+        int e0 = cc[0] + cc[2], e1 = cc[0] - cc[2], e2 = cc[1] - cc[3], e3 = cc[1] + cc[3];
+        t[4 * yy] = e0 + e3; t[4 * yy + 3] = e0 - e3; t[4 * yy + 1] = e1 + e2; t[4 * yy + 2] = e1 - e2;
+    }
+    int v00 = c_dq3[qp_rem][0];
+    for (int xx = 0; xx < 4; xx++) {
+        int e0 = t[xx] + t[8 + xx], e1 = t[xx] - t[8 + xx], e2 = t[4 + xx] - t[12 + xx], e3 = t[4 + xx] + t[12 + xx];
+        int fv[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
+        for (int yy = 0; yy < 4; yy++) dcdq[4 * yy + xx] = (fv[yy] * v00 * (1 << qp_per) + 2) >> 2;
+    }
+}
+
 // dct_luma_16x16 [J] on 256 threads (tid = 16 * blk + l, blk = the 4x4 block in raster order, l =
 // the lane's raster position in it): p / org = the lane's prediction and source sample.  Returns
 // the lane's AC level (scan position l of block blk; 0 at l == 0) and reconstruction; the DC levels
@@ -100,40 +134,10 @@ __device__ __forceinline__ void i16_pick(const DevParams &d, const pel *org, con
 __device__ __forceinline__ void i16_code(int p, int org, int qp, int qp_const, int *dc, int *dcdq, int16_t *dclev, int *bnz, int tid,
                                          int maxv, int &lev_out, int &rec_out) {
     const int blk = tid >> 4, l = tid & 15;
-    const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per, qp_const2 = qp_const << 1;
     const int c = lane_fwd4x4(org - p, l);
     if (l == 0) dc[blk] = c;
     __syncthreads();
-    if (tid == 0) {
-        for (int yy = 0; yy < 4; yy++) {
-            int *r = dc + 4 * yy;
-            int a0 = r[0] + r[3], a3 = r[0] - r[3], a1 = r[1] + r[2], a2 = r[1] - r[2];
-            r[0] = a0 + a1; r[2] = a0 - a1; r[1] = a3 + a2; r[3] = a3 - a2;
-        }
-        for (int xx = 0; xx < 4; xx++) {
-            int a0 = dc[xx] + dc[12 + xx], a3 = dc[xx] - dc[12 + xx], a1 = dc[4 + xx] + dc[8 + xx], a2 = dc[4 + xx] - dc[8 + xx];
-            dc[xx] = (a0 + a1) >> 1; dc[8 + xx] = (a0 - a1) >> 1; dc[4 + xx] = (a3 + a2) >> 1; dc[12 + xx] = (a3 - a2) >> 1;
-        }
-        int lev[16];
-        for (int k = 0; k < 16; k++) {
-            int pos = scan_of(k);
-            int level = (abs(dc[pos]) * c_q3[qp_rem][0] + qp_const2) >> (q_bits + 1);
-            dclev[k] = (int16_t)isign(level, dc[pos]);
-            lev[pos] = dclev[k];
-        }
-        int t[16];
-        for (int yy = 0; yy < 4; yy++) {
-            const int *cc = lev + 4 * yy;
-            int e0 = cc[0] + cc[2], e1 = cc[0] - cc[2], e2 = cc[1] - cc[3], e3 = cc[1] + cc[3];
-            t[4 * yy] = e0 + e3; t[4 * yy + 3] = e0 - e3; t[4 * yy + 1] = e1 + e2; t[4 * yy + 2] = e1 - e2;
-        }
-        int v00 = c_dq3[qp_rem][0];
-        for (int xx = 0; xx < 4; xx++) {
-            int e0 = t[xx] + t[8 + xx], e1 = t[xx] - t[8 + xx], e2 = t[4 + xx] - t[12 + xx], e3 = t[4 + xx] + t[12 + xx];
-            int fv[4] = {e0 + e3, e1 + e2, e1 - e2, e0 - e3};
-            for (int yy = 0; yy < 4; yy++) dcdq[4 * yy + xx] = (fv[yy] * v00 * (1 << qp_per) + 2) >> 2;
-        }
-    }
+    if (tid == 0) i16_dc(dc, dclev, dcdq, qp, qp_const);
     __syncthreads();
     int lev, dq, cc;
     unsigned nz = lane_quant(c, l, qp, qp_const, true, lev, dq, cc);

@@ -16,7 +16,22 @@
 #include "jmh_epzs.h"
 #include "jmh_intra.h"
 #include "jmh_deblock.h"
+// Table 9-44 in LDS for every kernel of this file that codes bins (filled by jmr_lds_tables_load)
+__shared__ uint32_t g_jmr_lps[64];   // rangeTabLPS[s][0..3] packed per state
+__shared__ uint8_t g_jmr_tlps[64];   // transIdxLPS
+#if defined(__HIP_DEVICE_COMPILE__)
+#define JMR_LPS(s, q) ((g_jmr_lps[s] >> (8 * (q))) & 0xFF)
+#define JMR_TLPS(s) g_jmr_tlps[s]
+#endif
 #include "jmh_cabac_rate.h"
+
+// the LDS tables by threads [0, n); the caller synchronises before the first bin
+__device__ __forceinline__ void jmr_lds_tables_load(int t, int n) {
+    for (int i = t; i < 64 + 16; i += n) {
+        if (i < 64) g_jmr_lps[i] = reinterpret_cast<const uint32_t *>(jmr_lps)[i];
+        else reinterpret_cast<uint32_t *>(g_jmr_tlps)[i - 64] = reinterpret_cast<const uint32_t *>(jmr_trans_lps)[i - 64];
+    }
+}
 
 #define RD_NL 7       // luma candidates: 0 P_Skip, 1 16x16, 2 16x8, 3 8x16, 4 P8x8, 5 I16MB, 6 I4MB
 #define RD_NCAND 13   // macroblock-loop candidates: 5 inter + (I16, I4) x 4 chroma modes
@@ -25,6 +40,20 @@
 __device__ __forceinline__ double rd_cost(int dist, int bits, double lambda) {
 #pragma clang fp contract(off)
     return (double)dist + lambda * (double)bits;
+}
+
+// one luma sample at quarter-pel picture position (X, Y) of the MC of a candidate: from the
+// searches' LDS window when the whole wave's 6x6 neighbourhoods lie inside it (the window holds the
+// UMV-clamped reference, so the values are those of qpel_direct), else from the picture in HBM
+template <class pel>
+__device__ __forceinline__ int qpel_mb(const DevParams &d, const EpzS<pel> &e, const EWin<pel> &wn, int X, int Y) {
+    const int x = X >> 2, y = Y >> 2, wdim = 16 + 2 * min(2 * d.sr + 4, EOFF_L);
+    const bool in = x - 2 >= wn.wx0 && x + 3 < wn.wx0 + EST && y - 2 >= wn.wy0 && y + 3 < wn.wy0 + wdim;
+    if (__all(in)) {
+        const pel *g = e.g + (size_t)(0 - wn.wy0) * EST - wn.wx0;
+        return qpel_from([&](int xx, int yy) { return (int)g[yy * EST + xx]; }, X, Y, d.maxv);
+    }
+    return qpel_direct(spl<pel>(d.refY), d.W, d.H, X, Y, d.maxv);
 }
 
 template <class pel>
@@ -53,12 +82,6 @@ struct RdoScr {
 };
 size_t jmh_rdo_scratch_bytes() { return sizeof(RdoScr<uint16_t>); }
 
-// chroma-coding scratch of one candidate on 128 threads
-struct ChromaBuf {
-    int cdcin[2][4], cbcost[2][4], cbnz[2][4], cdcq[2][4], creset[2], cdcnz[2], red[2];
-    int16_t cdc[2][4];
-};
-
 // the coding state of the slice at the start of macroblock a into st (LDS, 4-aligned) by threads
 // [0, n): initialised (9.3.1.1) at the slice's first macroblock; returns codIRange
 __device__ __forceinline__ uint32_t rdo_state_load(const DevParams &d, int a, uint8_t *st, int t, int n) {
@@ -81,32 +104,22 @@ __device__ __forceinline__ void rdo_nb_load(const DevParams &d, int mbx, int mby
     }
     if (t == 0) { hasA = mav.L; hasB = mav.T; }
 }
-__device__ __forceinline__ void copy_ctx(uint8_t *dst, const uint8_t *src) {   // one lane, 72 dwords
-    for (int i = 0; i < JMR_NCTX / 4; i++) reinterpret_cast<uint32_t *>(dst)[i] = reinterpret_cast<const uint32_t *>(src)[i];
-}
-// sum over the 256 threads (every thread gets it); red: 4 ints of LDS
-__device__ __forceinline__ int block_sum(int v, int *red, int tid) {
-    v = wave_sum(v);
-    __syncthreads();
-    if ((tid & 63) == 0) red[tid >> 6] = v;
-    __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
-}
-
-// ChromaResidualCoding [J] of one candidate on 128 threads (t = 0..127): prediction = intra mode cm
-// (nb) or the MC of fmv; skipped (P_Skip): no residual.  act = false: the threads only take part
-// in the barriers.  Writes out (global) except its distortion, returned on every thread.
+// ChromaResidualCoding [J] of one candidate on ONE wave, a component per pass (lane = 4x4 block
+// cb4 x 16 + l): prediction = intra mode cm (nb) or the MC of fmv; skipped (P_Skip): no residual.
+// The 2x2 DC of a component reads its four blocks' DC lanes (wave-uniform).  Writes out (global)
+// except its distortion, returned (wave-uniform).
 template <class pel>
-__device__ __forceinline__ int chroma_cand(const DevParams &d, const pel (*orgc)[64], const IntraNb<pel> *nb, int cm, const int16_t (*fmv)[2],
-                                           bool skipped, bool act, ChromaBuf &cb, RdoChroma<pel> *out, int t, int mbx, int mby,
-                                           bool avT, bool avL) {
+__device__ __forceinline__ int chroma_cand_w(const DevParams &d, const pel (*orgc)[64], const IntraNb<pel> *nb, int cm, const int16_t (*fmv)[2],
+                                             bool skipped, RdoChroma<pel> *out, int lane, int mbx, int mby, bool avT, bool avL) {
     const int maxv = d.maxv, Wc = d.Wc, pix_x = 16 * mbx, pix_y = 16 * mby;
     const int qpi = iclip(-d.qpbd, 51, d.qp + d.cqp_off), qpcy = qpi < 0 ? qpi : c_qpc[qpi], qpc = qpcy + d.qpbd;
-    const int cq_bits = 15 + qpc / 6, cqp_const = q_round(d.qsel, cq_bits);
-    const int uv = t >> 6, cb4 = (t >> 4) & 3, l = t & 15;
+    const int cq_bits = 15 + qpc / 6, cqp_const = q_round(d.qsel, cq_bits), qp_per = qpc / 6, qp_rem = qpc % 6;
+    const int cb4 = lane >> 4, l = lane & 15;
     const int cxo = (cb4 & 1) * 4 + (l & 3), cyo = (cb4 >> 1) * 4 + (l >> 2);
-    int pv = 0, lev = 0, cdq = 0;
-    if (act) {
+    int e2 = 0, cr = 0;
+#pragma unroll 1
+    for (int uv = 0; uv < 2; uv++) {
+        int pv;
         if (nb) pv = chroma_pred_px(nb->ctop[uv] + 1, nb->cleft[uv], nb->ctop[uv][0], avT, avL, cm, cxo, cyo, maxv);
         else {   // OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2
             const pel *R = spl<pel>(uv ? d.refV : d.refU);
@@ -118,115 +131,116 @@ __device__ __forceinline__ int chroma_cand(const DevParams &d, const pel (*orgc)
             pv = ((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] + (8 - fx) * fy * R[y1 * Wc + x0] +
                   fx * fy * R[y1 * Wc + x1] + 32) >> 6;
         }
+        const int org = orgc[uv][cyo * 8 + cxo];
+        int rv = pv, lev = 0, dcl = 0;
         if (!skipped) {
-            const int c = lane_fwd4x4(orgc[uv][cyo * 8 + cxo] - pv, l);
-            if (l == 0) cb.cdcin[uv][cb4] = c;
-            int cc;
-            unsigned nz = lane_quant(c, l, qpc, cqp_const, true, lev, cdq, cc);
-            if (l == 0) { cb.cbcost[uv][cb4] = cc; cb.cbnz[uv][cb4] = nz != 0; }
-        }
-    }
-    __syncthreads();
-    if (act && !skipped && t < 2) {                    // the 2x2 DC of component t (dct_chroma)
-        const int qp_per = qpc / 6, qp_rem = qpc % 6;
-        const int *m = cb.cdcin[t];
-        const int m1[4] = {m[0] + m[1] + m[2] + m[3], m[0] - m[1] + m[2] - m[3], m[0] + m[1] - m[2] - m[3], m[0] - m[1] - m[2] + m[3]};
-        int dcnz = 0;
-        for (int k = 0; k < 4; k++) {
-            const int level = (abs(m1[k]) * c_q3[qp_rem][0] + 2 * cqp_const) >> (cq_bits + 1);
-            if (level) dcnz = 1;
-            cb.cdc[t][k] = (int16_t)isign(level, m1[k]);
-        }
-        const int c0 = cb.cdc[t][0], c1 = cb.cdc[t][1], c2 = cb.cdc[t][2], c3 = cb.cdc[t][3];
-        const int fv[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
-        const int v00 = c_dq3[qp_rem][0];
-        for (int k = 0; k < 4; k++) cb.cdcq[t][k] = (fv[k] * 16 * v00 * (1 << qp_per)) >> 5;   // 8.5.11.2
-        const int cost = cb.cbcost[t][0] + cb.cbcost[t][1] + cb.cbcost[t][2] + cb.cbcost[t][3];
-        const int acany = cb.cbnz[t][0] | cb.cbnz[t][1] | cb.cbnz[t][2] | cb.cbnz[t][3];
-        cb.creset[t] = cost < 4;                       // _CHROMA_COEFF_COST_
-        cb.cdcnz[t] = (dcnz ? 1 : 0) | (acany && cost >= 4 ? 2 : 0);
-    }
-    __syncthreads();
-    int e2 = 0;
-    if (act) {
-        int rv = pv;
-        if (!skipped) {
-            if (cb.creset[uv]) { cdq = 0; lev = 0; }
-            if (l == 0) cdq = cb.cdcq[uv][cb4];
+            const int c = lane_fwd4x4(org - pv, l);
+            int cdq, cc;
+            const unsigned nz = lane_quant(c, l, qpc, cqp_const, true, lev, cdq, cc);
+            int m[4], cost = 0, acany = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                m[q] = __builtin_amdgcn_readlane(c, 16 * q);
+                cost += __builtin_amdgcn_readlane(cc, 16 * q);
+                acany |= __builtin_amdgcn_readlane((int)nz, 16 * q);
+            }
+            // the 2x2 DC (dct_chroma), wave-uniform
+            const int m1[4] = {m[0] + m[1] + m[2] + m[3], m[0] - m[1] + m[2] - m[3], m[0] + m[1] - m[2] - m[3], m[0] - m[1] - m[2] + m[3]};
+            int dcnz = 0, cd[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int level = (abs(m1[k]) * c_q3[qp_rem][0] + 2 * cqp_const) >> (cq_bits + 1);
+                if (level) dcnz = 1;
+                cd[k] = isign(level, m1[k]);
+            }
+            const int fv[4] = {cd[0] + cd[1] + cd[2] + cd[3], cd[0] - cd[1] + cd[2] - cd[3], cd[0] + cd[1] - cd[2] - cd[3],
+                               cd[0] - cd[1] - cd[2] + cd[3]};
+            if (cost < 4) { cdq = 0; lev = 0; }            // _CHROMA_COEFF_COST_
+            if (l == 0) cdq = (fv[cb4] * 16 * c_dq3[qp_rem][0] * (1 << qp_per)) >> 5;   // 8.5.11.2
             rv = lane_inv4x4(cdq, l, pv, maxv);
+            dcl = cd[l & 3];
+            if (dcnz) cr = max(cr, 1);
+            if (acany && cost >= 4) cr = 2;
         }
-        out->ac[uv][cb4][l] = (int16_t)(skipped ? 0 : lev);
+        out->ac[uv][cb4][l] = (int16_t)lev;
         out->rec[uv][cyo * 8 + cxo] = (pel)rv;
-        const int e = orgc[uv][cyo * 8 + cxo] - rv;
-        e2 = e * e;
-        if (t < 8) out->dc[t >> 2][t & 3] = skipped ? 0 : cb.cdc[t >> 2][t & 3];
-        if (t == 0) {
-            int cr = 0;
-            if (!skipped)
-                for (int k = 0; k < 2; k++) {
-                    if (cb.cdcnz[k] & 1) cr = max(cr, 1);
-                    if (cb.cdcnz[k] & 2) cr = 2;
-                }
-            out->cbpc = cr;
-        }
+        if (lane < 4) out->dc[uv][lane] = (int16_t)dcl;
+        e2 += (org - rv) * (org - rv);
     }
-    e2 = wave_sum(e2);
-    if ((t & 63) == 0) cb.red[uv] = e2;
-    __syncthreads();
-    return cb.red[0] + cb.red[1];
+    if (lane == 0) out->cbpc = cr;
+    return wave_sum(e2);
 }
 
 // ======================================================================================
-//  role "inter": the searches, P8x8 by RDCost_for_8x8blocks, the inter candidates
+//  role "inter" (k_rdo_inter): ONE WAVE per P macroblock, wave-synchronous LDS (no workgroup
+//  barrier): the searches, P8x8 by RDCost_for_8x8blocks, the inter candidates
 // ======================================================================================
+// an 8x8 block's sub-mode candidates (P8x8 loop): live from the block's last search to its decision,
+// so for 16-bit samples they overlay the searches' sub-pel planes (hp, b1: four MBs per CU)
+struct RdoP8Tmp {
+    alignas(4) uint8_t stc[4][JMR_NCTX];   // per sub-mode rate lane
+    int16_t lev8[4][4][16];       // per sub-mode: the 8x8 block's four 4x4 levels (coding order)
+    int16_t mvd8[4][4][2];
+};
+template <class pel>
+struct RdoP8Px {
+    alignas(4) pel pred8[4][64], rec8[4][64];
+};
+template <class pel, bool OVERLAY = (sizeof(pel) == 2)>
+struct RdoP8Own {
+    RdoP8Tmp t;
+    RdoP8Px<pel> px;
+};
+template <class pel>
+struct RdoP8Own<pel, true> {};
 template <class pel>
 struct RdoInterS {
-    EpzS<pel> e;                  // the motion searches (wave 0)
+    EpzS<pel> e;                  // the motion searches
     alignas(4) pel orgc[2][64];
     alignas(4) uint8_t st0[JMR_NCTX];      // the slice's coding state at the MB start
     alignas(4) uint8_t strun[JMR_NCTX];    // the P8x8 running state (decided 8x8 blocks)
-    alignas(4) uint8_t stc[4][JMR_NCTX];   // per sub-mode rate lane
+    RdoP8Own<pel> own;
     jmr_mbinfo nbA, nbB;
-    int hasA, hasB;
     jmr_cur currun, curc[4];
-    int16_t lev8[4][4][16];       // per sub-mode: the 8x8 block's four 4x4 levels (coding order)
-    int16_t mvd8[4][4][2];
-    pel pred8[4][64], rec8[4][64];
-    int cost8[4], cbp8[4], blk8[4], dist8[4], bits8[4];
-    uint32_t rgc[4], rg0, rgrun;
-    int best8x8, sel;
+    int cost8[4], blk8[4], dist8[4], bits8[4];
+    uint32_t rgc[4];
     alignas(4) pel p8pred[256], p8rec[256];   // the P8x8 candidate, assembled block by block
     int16_t p8lev[16][16];
-    int p8cbp, p8blk, p8cnt;
-    int16_t fmv[2][16][2];        // MVs of the candidate(s) being coded
-    int bcost[16], bnz[16], red[4];
-    ChromaBuf cb[2];
-    int skipx, skipy;
+    int16_t fmv[16][2];           // MVs of the candidate being coded
+    int bcost[16], bnz[16];
 };
 
-// LumaResidualCoding [J] of an inter candidate (4x4 transform) on 256 threads: MC of s.fmv[0],
-// LumaResidualCoding8x8's _LUMA_COEFF_COST_ zeroing and the macroblock one; skipped: prediction only
+// LumaResidualCoding [J] of an inter candidate (4x4 transform) on one wave, a row of 4x4 blocks per
+// pass: MC of s.fmv, LumaResidualCoding8x8's _LUMA_COEFF_COST_ zeroing and the macroblock one;
+// skipped: prediction only
 template <class pel>
-__device__ __forceinline__ void luma_inter(const DevParams &d, RdoInterS<pel> &s, RdoLuma<pel> *L, bool skipped, int mbx, int mby, int tid) {
-    const int blk = tid >> 4, l = tid & 15, px4 = 4 * (blk & 3) + (l & 3), py4 = 4 * (blk >> 2) + (l >> 2);
-    const int qp = d.qp + d.qpbd, maxv = d.maxv;
-    const pel *refY = spl<pel>(d.refY);
-    const int p = qpel_direct(refY, d.W, d.H, 4 * (16 * mbx + px4) + s.fmv[0][blk][0], 4 * (16 * mby + py4) + s.fmv[0][blk][1], maxv);
-    const int org = s.e.org[py4 * 16 + px4];
-    int lev = 0, rv = p, cbp = 0, cbp_blk = 0;
+__device__ __forceinline__ void luma_inter(const DevParams &d, RdoInterS<pel> &s, const EWin<pel> &wn, RdoLuma<pel> *L, bool skipped, int mbx, int mby,
+                                           int lane) {
+    const int l = lane & 15, qp = d.qp + d.qpbd, maxv = d.maxv, rnd = q_round(d.qsel, 15 + qp / 6);
+    int lev[4], rv[4], pr[4], org[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int blk = 4 * i + (lane >> 4), px4 = 4 * (blk & 3) + (l & 3), py4 = 4 * i + (l >> 2);
+        pr[i] = qpel_mb(d, s.e, wn, 4 * (16 * mbx + px4) + s.fmv[blk][0], 4 * (16 * mby + py4) + s.fmv[blk][1]);
+        org[i] = s.e.org[py4 * 16 + px4];
+        lev[i] = 0; rv[i] = pr[i];
+        if (!skipped) {
+            const int c = lane_fwd4x4(org[i] - pr[i], l);
+            int dq, cc;
+            const unsigned nz = lane_quant(c, l, qp, rnd, false, lev[i], dq, cc);
+            rv[i] = lane_inv4x4(dq, l, pr[i], maxv);
+            if (l == 0) { s.bcost[blk] = cc; s.bnz[blk] = nz != 0; }
+        }
+    }
+    int cbp = 0, cbp_blk = 0;
     if (!skipped) {
-        const int c = lane_fwd4x4(org - p, l);
-        int dq, cc;
-        unsigned nz = lane_quant(c, l, qp, q_round(d.qsel, 15 + qp / 6), false, lev, dq, cc);
-        rv = lane_inv4x4(dq, l, p, maxv);
-        if (l == 0) { s.bcost[blk] = cc; s.bnz[blk] = nz != 0; }
-        __syncthreads();
+        wave_lds_sync();
         int sum_cnt = 0, keep8 = 0;
-        for (int b8 = 0; b8 < 4; b8++) {
+        for (int b8 = 0; b8 < 4; b8++) {                // wave-uniform
             const int base = (b8 >> 1) * 8 + (b8 & 1) * 2;
             int c8 = s.bcost[base] + s.bcost[base + 1] + s.bcost[base + 4] + s.bcost[base + 5];
             const int nz8 = s.bnz[base] | s.bnz[base + 1] | s.bnz[base + 4] | s.bnz[base + 5];
-            if (c8 <= 4) c8 = 0;                                   // _LUMA_COEFF_COST_
+            if (c8 <= 4) c8 = 0;                         // _LUMA_COEFF_COST_
             else {
                 keep8 |= 1 << b8;
                 if (nz8) cbp |= 1 << b8;
@@ -237,74 +251,94 @@ __device__ __forceinline__ void luma_inter(const DevParams &d, RdoInterS<pel> &s
             }
             sum_cnt += c8;
         }
-        if (sum_cnt <= 5) { keep8 = 0; cbp = 0; cbp_blk = 0; }      // _LUMA_MB_COEFF_COST_
-        const bool keep = (keep8 >> (((blk >> 3) << 1) + ((blk & 3) >> 1))) & 1;
-        if (!keep) { lev = 0; rv = p; }
+        if (sum_cnt <= 5) { keep8 = 0; cbp = 0; cbp_blk = 0; }   // _LUMA_MB_COEFF_COST_
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int blk = 4 * i + (lane >> 4);
+            if (!((keep8 >> (((blk >> 3) << 1) + ((blk & 3) >> 1))) & 1)) { lev[i] = 0; rv[i] = pr[i]; }
+        }
     }
-    L->luma[blk][l] = (int16_t)lev;
-    L->rec[py4 * 16 + px4] = (pel)rv;
-    const int e = org - rv;
-    const int dist = block_sum(e * e, s.red, tid);
-    if (tid == 0) { L->cbp = cbp; L->cbp_blk = cbp_blk; L->dist = dist; L->i16mode = 0; }
+    int e2 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int blk = 4 * i + (lane >> 4), px4 = 4 * (blk & 3) + (l & 3), py4 = 4 * i + (l >> 2);
+        L->luma[blk][l] = (int16_t)lev[i];
+        L->rec[py4 * 16 + px4] = (pel)rv[i];
+        e2 += (org[i] - rv[i]) * (org[i] - rv[i]);
+    }
+    const int dist = wave_sum(e2);
+    if (lane == 0) { L->cbp = cbp; L->cbp_blk = cbp_blk; L->dist = dist; L->i16mode = 0; }
 }
 
 template <class pel>
-__device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> &s, RdoScr<pel> *scr, int mbx, int mby, int tid) {
-    const int wave = tid >> 6, lane = tid & 63, a = mby * d.mbw + mbx;
-    const int pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
+__device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
+    const int a = mby * d.mbw + mbx, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
-    // ---- inputs: the searches' (wave 0), chroma, the coding state, the neighbours' records
-    EWin<pel> wn{};
-    if (wave == 0) wn = epzs_load_mb(d, s.e, mbx, mby, lane);
-    else if (wave == 1 || wave == 2) {
-        const int t = tid - 64, uv = t >> 6, k = t & 63;
-        s.orgc[uv][k] = spl<pel>(uv ? d.orgV : d.orgU)[(8 * mby + (k >> 3)) * d.Wc + 8 * mbx + (k & 7)];
+    RdoP8Tmp *tp;
+    RdoP8Px<pel> *px8;
+    if constexpr (sizeof(pel) == 2) {
+        static_assert(sizeof(RdoP8Tmp) <= sizeof(s.e.hp) && sizeof(RdoP8Px<pel>) <= sizeof(s.e.b1), "P8x8 overlay");
+        tp = reinterpret_cast<RdoP8Tmp *>(&s.e.hp[0][0]);
+        px8 = reinterpret_cast<RdoP8Px<pel> *>(&s.e.b1[0][0]);
     } else {
-        const uint32_t rg = rdo_state_load(d, a, s.st0, tid - 192, 64);
-        if (tid == 192) s.rg0 = rg;
-        rdo_nb_load(d, mbx, mby, s.nbA, s.nbB, s.hasA, s.hasB, tid - 192);
+        tp = &s.own.t;
+        px8 = &s.own.px;
     }
-    __syncthreads();
-    const jmr_mbinfo *A = s.hasA ? &s.nbA : nullptr, *B = s.hasB ? &s.nbB : nullptr;
-    // ---- motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch [J])
-    if (wave == 0) {
-        epzs_block<1>(d, s.e, wn, 0, 0, 0, 0, 0, false);
-        epzs_block<2>(d, s.e, wn, 0, 0, 0, 0, 0, false);
-        epzs_block<2>(d, s.e, wn, 0, 2, 1, 0, 0, false);
-        epzs_block<3>(d, s.e, wn, 0, 0, 0, 0, 0, false);
-        epzs_block<3>(d, s.e, wn, 2, 0, 1, 0, 0, false);
+    // ---- inputs: the searches' window, chroma, the coding state, the neighbours' records
+    const EWin<pel> wn = epzs_load_mb(d, s.e, mbx, mby, lane);
+    jmr_lds_tables_load(lane, 64);
+    for (int k = lane; k < 128; k += 64) {
+        const int uv = k >> 6, q = k & 63;
+        s.orgc[uv][q] = spl<pel>(uv ? d.orgV : d.orgU)[(8 * mby + (q >> 3)) * d.Wc + 8 * mbx + (q & 7)];
     }
-    const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
-    if (tid < JMR_NCTX / 4) reinterpret_cast<uint32_t *>(s.strun)[tid] = reinterpret_cast<const uint32_t *>(s.st0)[tid];
-    if (tid == 0) {
-        s.rgrun = s.rg0;
-        memset(&s.currun, 0, sizeof(s.currun));
-        s.best8x8 = 0; s.p8cbp = 0; s.p8blk = 0; s.p8cnt = 0;
-    }
-    __syncthreads();
-    // ---- P8x8: per 8x8 block the sub-modes' searches (wave 0), their LumaResidualCoding8x8 (wave
-    //      w = sub-mode 4 + w), their RDCost_for_8x8blocks rates (lane 0 of wave w), the decision
-    for (int b8 = 0; b8 < 4 && p8; b8++) {
-        const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1), best8x8 = s.best8x8;
-        if (wave == 0) {
-            epzs_block<4>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
-            epzs_block<5>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
-            epzs_block<5>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false);
-            epzs_block<6>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
-            epzs_block<6>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false);
-            epzs_block<7>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
-            epzs_block<7>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false);
-            epzs_block<7>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false);
-            epzs_block<7>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false);
+    int hasA = 0, hasB = 0;
+    const uint32_t rg0 = rdo_state_load(d, a, s.st0, lane, 64);
+    {
+        const int nw = (int)sizeof(jmr_mbinfo) / 4;
+        hasA = mav.L; hasB = mav.T;
+        if (lane < nw) {
+            if (hasA) reinterpret_cast<uint32_t *>(&s.nbA)[lane] = reinterpret_cast<const uint32_t *>(d.rp->mbi + a - 1)[lane];
+            if (hasB) reinterpret_cast<uint32_t *>(&s.nbB)[lane] = reinterpret_cast<const uint32_t *>(d.rp->mbi + a - d.mbw)[lane];
         }
-        __syncthreads();
-        const int sm = 4 + wave, b4 = lane >> 4, l = lane & 15;
+    }
+    wave_lds_sync();
+    const jmr_mbinfo *A = hasA ? &s.nbA : nullptr, *B = hasB ? &s.nbB : nullptr;
+    // ---- motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch [J])
+    epzs_block<1>(d, s.e, wn, 0, 0, 0, 0, 0, false);
+    epzs_block<2>(d, s.e, wn, 0, 0, 0, 0, 0, false);
+    epzs_block<2>(d, s.e, wn, 0, 2, 1, 0, 0, false);
+    epzs_block<3>(d, s.e, wn, 0, 0, 0, 0, 0, false);
+    epzs_block<3>(d, s.e, wn, 2, 0, 1, 0, 0, false);
+    const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
+    for (int i = lane; i < JMR_NCTX / 4; i += 64) reinterpret_cast<uint32_t *>(s.strun)[i] = reinterpret_cast<const uint32_t *>(s.st0)[i];
+    if (lane == 0) memset(&s.currun, 0, sizeof(s.currun));
+    uint32_t rgrun = rg0;
+    int best8x8 = 0, p8cbp = 0, p8blk = 0, p8cnt = 0;
+    wave_lds_sync();
+    // ---- P8x8: per 8x8 block the sub-modes' searches, their LumaResidualCoding8x8 (a pass per
+    //      sub-mode: four 4x4 blocks x 16 lanes), their RDCost_for_8x8blocks rates (lanes 0, 16,
+    //      32, 48 side by side), the decision
+    const int b4 = lane >> 4, l = lane & 15;
+#pragma unroll 1
+    for (int b8 = 0; b8 < 4 && p8; b8++) {
+        const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
+        epzs_block<4>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
+        epzs_block<5>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
+        epzs_block<5>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false);
+        epzs_block<6>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
+        epzs_block<6>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false);
+        epzs_block<7>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
+        epzs_block<7>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false);
+        epzs_block<7>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false);
+        epzs_block<7>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false);
         const int bx4 = X + (b4 & 1), by4 = Y + (b4 >> 1), k = by4 * 4 + bx4;
         const int px = 4 * bx4 + (l & 3), py = 4 * by4 + (l >> 2), q8 = (4 * (b4 >> 1) + (l >> 2)) * 8 + 4 * (b4 & 1) + (l & 3);
-        if (inter_on(d.isr, sm)) {                      // wave-uniform
-            const int p = qpel_direct(spl<pel>(d.refY), d.W, d.H, 4 * (pix_x + px) + s.e.all_mv[sm][k][0], 4 * (pix_y + py) + s.e.all_mv[sm][k][1],
-                                      maxv);
-            const int org = s.e.org[py * 16 + px];
+        const int org = s.e.org[py * 16 + px];
+#pragma unroll 1
+        for (int w = 0; w < 4; w++) {
+            const int sm = 4 + w;
+            if (!inter_on(d.isr, sm)) continue;         // wave-uniform
+            const int p = qpel_mb(d, s.e, wn, 4 * (pix_x + px) + s.e.all_mv[sm][k][0], 4 * (pix_y + py) + s.e.all_mv[sm][k][1]);
             const int c = lane_fwd4x4(org - p, l);
             int lev, dq, cc;
             const unsigned nz = lane_quant(c, l, qp, q_round(d.qsel, 15 + qp / 6), false, lev, dq, cc);
@@ -317,122 +351,117 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
                 if (__builtin_amdgcn_readlane((int)nz, 16 * q)) blk |= 1 << kq;
             }
             if (cost <= 4) { cost = 0; blk = 0; lev = 0; rv = p; }   // _LUMA_COEFF_COST_
-            s.lev8[wave][b4][l] = (int16_t)lev;
-            s.pred8[wave][q8] = (pel)p;
-            s.rec8[wave][q8] = (pel)rv;
-            const int e = org - rv;
-            const int dist = wave_sum(e * e);
-            if (lane == 0) { s.cost8[wave] = cost; s.cbp8[wave] = cost > 0; s.blk8[wave] = blk; s.dist8[wave] = dist; }
+            tp->lev8[w][b4][l] = (int16_t)lev;
+            px8->pred8[w][q8] = (pel)p;
+            px8->rec8[w][q8] = (pel)rv;
+            const int dist = wave_sum((org - rv) * (org - rv));
+            if (lane == 0) { s.cost8[w] = cost; s.blk8[w] = blk; s.dist8[w] = dist; }
             if (lane < 4) {
                 const int kk = (Y + (lane >> 1)) * 4 + X + (lane & 1);
-                s.mvd8[wave][lane][0] = (int16_t)(s.e.all_mv[sm][kk][0] - s.e.pmv[sm][kk][0]);
-                s.mvd8[wave][lane][1] = (int16_t)(s.e.all_mv[sm][kk][1] - s.e.pmv[sm][kk][1]);
+                tp->mvd8[w][lane][0] = (int16_t)(s.e.all_mv[sm][kk][0] - s.e.pmv[sm][kk][0]);
+                tp->mvd8[w][lane][1] = (int16_t)(s.e.all_mv[sm][kk][1] - s.e.pmv[sm][kk][1]);
             }
         }
-        __syncthreads();
-        if (lane == 0 && inter_on(d.isr, sm)) {         // RDCost_for_8x8blocks' rate
-            copy_ctx(s.stc[wave], s.strun);
-            jmr_eng e = {s.stc[wave], s.rgrun, 0};
-            s.curc[wave] = s.currun;
-            jmr_b8(&e, A, B, &s.curc[wave], b8, sm, (const int16_t(*)[2])s.mvd8[wave], s.cost8[wave] > 0, (const int16_t(*)[16])s.lev8[wave]);
-            s.bits8[wave] = e.bits;
-            s.rgc[wave] = e.range;
+        for (int i = lane; i < JMR_NCTX; i += 64) {     // each rate lane's copy of the running state
+            const int w = i / (JMR_NCTX / 4), j = i % (JMR_NCTX / 4);
+            reinterpret_cast<uint32_t *>(tp->stc[w])[j] = reinterpret_cast<const uint32_t *>(s.strun)[j];
         }
-        __syncthreads();
-        if (tid == 0) {
-            double best = 1e30;
-            int bm = 0;
-            for (int w = 0; w < 4; w++)
-                if (inter_on(d.isr, 4 + w)) {
-                    const double rd = rd_cost(s.dist8[w], s.bits8[w], d.lambda_rd);
-                    if (rd < best) { best = rd; bm = w; }
-                }
-            s.sel = bm;
-            s.best8x8 |= (4 + bm) << (4 * b8);
-            s.rgrun = s.rgc[bm];
-            s.currun = s.curc[bm];
-            if (s.cost8[bm]) { s.p8cbp |= s.cbp8[bm] << b8; s.p8blk |= s.blk8[bm]; s.p8cnt += s.cost8[bm]; }
+        wave_lds_sync();
+        if (l == 0 && inter_on(d.isr, 4 + b4)) {        // RDCost_for_8x8blocks' rate, sub-mode 4 + b4
+            const int w = b4;
+            jmr_eng e = {tp->stc[w], rgrun, 0};
+            s.curc[w] = s.currun;
+            jmr_b8(&e, A, B, &s.curc[w], b8, 4 + w, (const int16_t(*)[2])tp->mvd8[w], s.cost8[w] > 0, (const int16_t(*)[16])tp->lev8[w]);
+            s.bits8[w] = e.bits;
+            s.rgc[w] = e.range;
         }
-        __syncthreads();
-        const int sel = s.sel;
-        if (tid < JMR_NCTX / 4) reinterpret_cast<uint32_t *>(s.strun)[tid] = reinterpret_cast<const uint32_t *>(s.stc[sel])[tid];
-        if (tid < 64) {                                 // the decided block into the P8x8 candidate
-            const int yy = tid >> 3, xx = tid & 7;
-            s.p8pred[(8 * (b8 >> 1) + yy) * 16 + 8 * (b8 & 1) + xx] = s.pred8[sel][tid];
-            s.p8rec[(8 * (b8 >> 1) + yy) * 16 + 8 * (b8 & 1) + xx] = s.rec8[sel][tid];
-            const int qb = tid >> 4, kk = (Y + (qb >> 1)) * 4 + X + (qb & 1);
-            s.p8lev[kk][tid & 15] = s.lev8[sel][qb][tid & 15];
+        wave_lds_sync();
+        double best = 1e30;                             // wave-uniform decision
+        int bm = 0;
+        for (int w = 0; w < 4; w++)
+            if (inter_on(d.isr, 4 + w)) {
+                const double rd = rd_cost(s.dist8[w], s.bits8[w], d.lambda_rd);
+                if (rd < best) { best = rd; bm = w; }
+            }
+        best8x8 |= (4 + bm) << (4 * b8);
+        rgrun = s.rgc[bm];
+        if (s.cost8[bm]) { p8cbp |= 1 << b8; p8blk |= s.blk8[bm]; p8cnt += s.cost8[bm]; }
+        if (lane < JMR_NCTX / 4) reinterpret_cast<uint32_t *>(s.strun)[lane] = reinterpret_cast<const uint32_t *>(tp->stc[bm])[lane];
+        if (lane < (int)sizeof(jmr_cur) / 4) reinterpret_cast<uint32_t *>(&s.currun)[lane] = reinterpret_cast<const uint32_t *>(&s.curc[bm])[lane];
+        {                                               // the decided block into the P8x8 candidate
+            const int yy = lane >> 3, xx = lane & 7;
+            s.p8pred[(8 * (b8 >> 1) + yy) * 16 + 8 * (b8 & 1) + xx] = px8->pred8[bm][lane];
+            s.p8rec[(8 * (b8 >> 1) + yy) * 16 + 8 * (b8 & 1) + xx] = px8->rec8[bm][lane];
+            const int qb = lane >> 4, kk = (Y + (qb >> 1)) * 4 + X + (qb & 1);
+            s.p8lev[kk][lane & 15] = tp->lev8[bm][qb][lane & 15];
         }
-        __syncthreads();
+        wave_lds_sync();
     }
     RdoLuma<pel> *L = scr->L;
     if (p8) {                                           // SetCoeffAndReconstruction8x8
-        const bool zero = s.p8cnt <= 5;                 // _LUMA_MB_COEFF_COST_
-        const int blk = tid >> 4, l = tid & 15, b8 = ((blk >> 3) << 1) + ((blk & 3) >> 1), sm = (s.best8x8 >> (4 * b8)) & 15;
-        const pel rv = zero ? s.p8pred[tid] : s.p8rec[tid];
-        L[4].rec[tid] = rv;
-        L[4].luma[blk][l] = zero ? 0 : s.p8lev[blk][l];
-        if (tid < 32) {
-            const int kk = tid >> 1, c = tid & 1, smk = (s.best8x8 >> (4 * (((kk >> 3) << 1) + ((kk & 3) >> 1)))) & 15;
+        const bool zero = p8cnt <= 5;                   // _LUMA_MB_COEFF_COST_
+        int e2 = 0;
+        for (int i = lane; i < 256; i += 64) {
+            const pel rv = zero ? s.p8pred[i] : s.p8rec[i];
+            L[4].rec[i] = rv;
+            L[4].luma[i >> 4][i & 15] = zero ? 0 : s.p8lev[i >> 4][i & 15];
+            const int e = (int)s.e.org[i] - (int)rv;
+            e2 += e * e;
+        }
+        if (lane < 32) {
+            const int kk = lane >> 1, c = lane & 1, smk = (best8x8 >> (4 * (((kk >> 3) << 1) + ((kk & 3) >> 1)))) & 15;
             L[4].mv[kk][c] = s.e.all_mv[smk][kk][c];
             L[4].mvd[kk][c] = (int16_t)(s.e.all_mv[smk][kk][c] - s.e.pmv[smk][kk][c]);
         }
-        if (tid < 4) L[4].b8mode[tid] = (int8_t)((s.best8x8 >> (4 * tid)) & 15);
-        (void)sm;
-        const int e = (int)s.e.org[tid] - (int)rv;
-        const int dist = block_sum(e * e, s.red, tid);
-        if (tid == 0) { L[4].cbp = zero ? 0 : s.p8cbp; L[4].cbp_blk = zero ? 0 : s.p8blk; L[4].dist = dist; L[4].i16mode = 0; }
+        if (lane < 4) L[4].b8mode[lane] = (int8_t)((best8x8 >> (4 * lane)) & 15);
+        const int dist = wave_sum(e2);
+        if (lane == 0) { L[4].cbp = zero ? 0 : p8cbp; L[4].cbp_blk = zero ? 0 : p8blk; L[4].dist = dist; L[4].i16mode = 0; }
     }
-    // ---- FindSkipModeMotionVector [J], the spatial memory of the next MB (its EPZS predictor 34)
-    if (tid == 0) {
+    // ---- FindSkipModeMotionVector [J] (wave-uniform), the spatial memory of the next MB (its EPZS
+    //      predictor 34)
+    int skipx, skipy;
+    {
         int pcx, pcy;
         set_mvp(NbBorder{s.e.bd}, 0, 0, 16, 16, pcx, pcy);
         NbBorder nbv{s.e.bd};
         int ra = -1, ax = 0, ay = 0, rb = -1, bx = 0, by = 0;
         const bool aa = nbv(-1, 0, ra, ax, ay), ab = nbv(0, -1, rb, bx, by);
         const bool zl = !aa || (ra == 0 && ax == 0 && ay == 0), za = !ab || (rb == 0 && bx == 0 && by == 0);
-        s.skipx = (za || zl) ? 0 : pcx;
-        s.skipy = (za || zl) ? 0 : pcy;
+        skipx = (za || zl) ? 0 : pcx;
+        skipy = (za || zl) ? 0 : pcy;
     }
     MbScratch *ms = d.scr + a;
-    for (int i = tid; i < 7 * 32; i += NT) {
+    for (int i = lane; i < 7 * 32; i += 64) {
         const int m = 1 + i / 32, k = (i & 31) >> 1, c = i & 1;
         ms->all_mv[m][k][c] = s.e.all_mv[m][k][c];
     }
-    __syncthreads();
-    // ---- the skip / 16x16 / 16x8 / 8x16 candidates (LumaResidualCoding)
-    for (int c = 0; c < 4; c++) {
-        if (c > 0 && !inter_on(d.isr, c)) continue;     // uniform
-        if (tid < 32) {
-            const int k = tid >> 1, cc = tid & 1;
-            const int v = c == 0 ? (cc ? s.skipy : s.skipx) : s.e.all_mv[c][k][cc];
-            s.fmv[0][k][cc] = (int16_t)v;
-            L[c].mv[k][cc] = (int16_t)v;
-            L[c].mvd[k][cc] = (int16_t)(c == 0 ? 0 : v - s.e.pmv[c][k][cc]);
+    // ---- the skip / 16x16 / 16x8 / 8x16 candidates (LumaResidualCoding) and the chroma of all five
+    //      (ChromaResidualCoding [J], the MC of each candidate's MVs)
+#pragma unroll 1
+    for (int c = 0; c < 5; c++) {
+        if (c == 4 ? !p8 : c > 0 && !inter_on(d.isr, c)) continue;   // uniform
+        if (lane < 32) {
+            const int k = lane >> 1, cc = lane & 1;
+            const int smk = (best8x8 >> (4 * (((k >> 3) << 1) + ((k & 3) >> 1)))) & 15;
+            const int v = c == 0 ? (cc ? skipy : skipx) : s.e.all_mv[c == 4 ? smk : c][k][cc];
+            s.fmv[k][cc] = (int16_t)v;
+            if (c < 4) {
+                L[c].mv[k][cc] = (int16_t)v;
+                L[c].mvd[k][cc] = (int16_t)(c == 0 ? 0 : v - s.e.pmv[c][k][cc]);
+            }
         }
-        if (tid < 4) L[c].b8mode[tid] = (int8_t)c;
-        __syncthreads();
-        luma_inter(d, s, &L[c], c == 0, mbx, mby, tid);
-        __syncthreads();
-    }
-    // ---- their chroma (ChromaResidualCoding [J], the MC of each candidate's MVs), two at a time
-    for (int c0 = 0; c0 < 5; c0 += 2) {
-        const int half = tid >> 7, c = c0 + half;
-        const bool act = c < 5 && (c == 0 || (c == 4 ? p8 : inter_on(d.isr, c)));
-        if (act && (tid & 127) < 32) {
-            const int k = (tid & 127) >> 1, cc = tid & 1;
-            s.fmv[half][k][cc] = L[c].mv[k][cc];
-        }
-        __syncthreads();
-        const int dist = chroma_cand<pel>(d, s.orgc, nullptr, 0, s.fmv[half], c == 0, act, s.cb[half], act ? &scr->C[c] : nullptr, tid & 127,
-                                          mbx, mby, mav.T, mav.L);
-        if (act && (tid & 127) == 0) scr->C[c].dist = dist;
-        __syncthreads();
+        if (c < 4 && lane < 4) L[c].b8mode[lane] = (int8_t)c;
+        wave_lds_sync();
+        if (c < 4) luma_inter(d, s, wn, &L[c], c == 0, mbx, mby, lane);
+        const int dist = chroma_cand_w<pel>(d, s.orgc, nullptr, 0, s.fmv, c == 0, &scr->C[c], lane, mbx, mby, mav.T, mav.L);
+        if (lane == 0) scr->C[c].dist = dist;
+        wave_lds_sync();
     }
 }
 
 // ======================================================================================
-//  role "intra": Intra16x16, the chroma intra modes, Intra4x4 by RDCost_for_4x4IntraBlocks
+//  role "intra" (k_rdo_intra): ONE WAVE per macroblock, wave-synchronous: Intra16x16, the chroma
+//  intra modes, Intra4x4 by RDCost_for_4x4IntraBlocks
 // ======================================================================================
 template <class pel>
 struct RdoIntraS {
@@ -444,17 +473,12 @@ struct RdoIntraS {
     alignas(4) uint8_t st0[JMR_NCTX];
     alignas(4) uint8_t stc[9][JMR_NCTX];
     jmr_mbinfo nbA, nbB;
-    int hasA, hasB;
-    uint32_t rg0;
     int P[13];
     int16_t lev[9][16];
     pel r4[9][16];
     int dist[9], bits[9], nz[9];
-    int mpm, sel, i16mode, i16cost;
-    int i4cbp, i4blk;
-    int dc[16], dcdq[16], bnz[16], red[4];
+    int dc[16], dcdq[16];
     int16_t dclev[16];
-    ChromaBuf cb[2];
 };
 
 template <class pel>
@@ -465,94 +489,115 @@ __device__ __forceinline__ int i4_lpix(const RdoIntraS<pel> &s, int x, int y) {
 }
 
 template <class pel>
-__device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> &s, RdoScr<pel> *scr, int mbx, int mby, int tid) {
-    const int wave = tid >> 6, lane = tid & 63, a = mby * d.mbw + mbx;
-    const int W = d.W, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
+__device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
+    const int a = mby * d.mbw + mbx, W = d.W, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     const pel *orgY = spl<pel>(d.orgY);
-    s.org[tid] = orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    if (tid < 128) load_orgc(d, s.nb, tid, mbx, mby);
-    else if (tid < 128 + 71) load_intra_nb(d, s.nb, tid - 128, mbx, mby);
-    else if (tid >= 208 && tid < 218) load_border(d, s.bd, tid - 208, mbx, mby);
-    if (tid >= 192) {
-        const uint32_t rg = rdo_state_load(d, a, s.st0, tid - 192, 64);
-        if (tid == 192) s.rg0 = rg;
-        rdo_nb_load(d, mbx, mby, s.nbA, s.nbB, s.hasA, s.hasB, tid - 192);
+    for (int i = lane; i < 256; i += 64) s.org[i] = orgY[(pix_y + (i >> 4)) * W + pix_x + (i & 15)];
+    for (int i = lane; i < 128; i += 64) load_orgc(d, s.nb, i, mbx, mby);
+    for (int t = lane; t < 71; t += 64) load_intra_nb(d, s.nb, t, mbx, mby);
+    if (lane >= 54 && lane < 64) load_border(d, s.bd, lane - 54, mbx, mby);
+    const uint32_t rg0 = rdo_state_load(d, a, s.st0, lane, 64);
+    jmr_lds_tables_load(lane, 64);
+    {
+        const int nw = (int)sizeof(jmr_mbinfo) / 4;
+        if (lane < nw) {
+            if (avL) reinterpret_cast<uint32_t *>(&s.nbA)[lane] = reinterpret_cast<const uint32_t *>(d.rp->mbi + a - 1)[lane];
+            if (avT) reinterpret_cast<uint32_t *>(&s.nbB)[lane] = reinterpret_cast<const uint32_t *>(d.rp->mbi + a - d.mbw)[lane];
+        }
     }
-    __syncthreads();
-    const jmr_mbinfo *A = s.hasA ? &s.nbA : nullptr, *B = s.hasB ? &s.nbB : nullptr;
+    wave_lds_sync();
+    const jmr_mbinfo *A = avL ? &s.nbA : nullptr, *B = avT ? &s.nbB : nullptr;
     RdoLuma<pel> *L = scr->L;
-    // ---- Intra16x16: the find_sad_16x16 mode (wave 0), dct_luma_16x16 on every thread
-    if (wave == 0) {
+    const int b4 = lane >> 4, l = lane & 15;
+    // ---- Intra16x16: the find_sad_16x16 mode, dct_luma_16x16 a row of 4x4 blocks per pass (the DC
+    //      Hadamard on lane 0, i16_dc)
+    {
         int c16, m16;
         i16_pick(d, s.org, s.nb, lane, avL, avT, avTL, c16, m16);
-        if (lane == 0) { s.i16mode = m16; s.i16cost = c16; }
-    }
-    __syncthreads();
-    {
-        const int blk = tid >> 4, l = tid & 15, px4 = 4 * (blk & 3) + (l & 3), py4 = 4 * (blk >> 2) + (l >> 2);
         const pel *T = s.nb.rtop + 1, *Lf = s.nb.rleft;
         const I16Par par = i16_params(T, Lf, avT, avL, (maxv + 1) >> 1);
-        const int p = i16_pred(par, T, Lf, s.i16mode, px4, py4, maxv);
-        int lev, rv;
-        i16_code(p, (int)s.org[py4 * 16 + px4], qp, q_round(q_sel16(d.qsel), 15 + qp / 6), s.dc, s.dcdq, s.dclev, s.bnz, tid, maxv, lev, rv);
-        L[5].luma[blk][l] = (int16_t)lev;
-        L[5].rec[py4 * 16 + px4] = (pel)rv;
-        if (tid < 16) L[5].luma_dc[tid] = s.dclev[tid];
-        const int e = (int)s.org[py4 * 16 + px4] - rv;
-        const int dist = block_sum(e * e, s.red, tid);   // (synchronises: bnz final)
-        if (tid == 0) {
-            int cbp = 0, blkm = 0;
-            for (int b = 0; b < 16; b++)
-                if (s.bnz[b]) { cbp = 15; blkm |= 1 << b; }
-            L[5].cbp = cbp; L[5].cbp_blk = blkm; L[5].dist = dist; L[5].i16mode = s.i16mode;
+        const int rnd = q_round(q_sel16(d.qsel), 15 + qp / 6);
+        int c[4], pr[4], o[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int px4 = 4 * b4 + (l & 3), py4 = 4 * i + (l >> 2);
+            pr[i] = i16_pred(par, T, Lf, m16, px4, py4, maxv);
+            o[i] = s.org[py4 * 16 + px4];
+            c[i] = lane_fwd4x4(o[i] - pr[i], l);
+            if (l == 0) s.dc[4 * i + b4] = c[i];
         }
-        if (tid < 32) L[5].mv[tid >> 1][tid & 1] = 0;
+        wave_lds_sync();
+        if (lane == 0) i16_dc(s.dc, s.dclev, s.dcdq, qp, rnd);
+        wave_lds_sync();
+        int e2 = 0, cbp = 0, blkm = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int blk = 4 * i + b4, px4 = 4 * b4 + (l & 3), py4 = 4 * i + (l >> 2);
+            int lev, dq, cc;
+            const unsigned nz = lane_quant(c[i], l, qp, rnd, true, lev, dq, cc);
+            if (l == 0) dq = s.dcdq[blk];
+            const int rv = lane_inv4x4(dq, l, pr[i], maxv);
+            L[5].luma[blk][l] = (int16_t)lev;
+            L[5].rec[py4 * 16 + px4] = (pel)rv;
+            e2 += (o[i] - rv) * (o[i] - rv);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (__builtin_amdgcn_readlane((int)nz, 16 * q)) { cbp = 15; blkm |= 1 << (4 * i + q); }
+        }
+        if (lane < 16) L[5].luma_dc[lane] = s.dclev[lane];
+        if (lane < 32) L[5].mv[lane >> 1][lane & 1] = 0;
+        const int dist = wave_sum(e2);
+        if (lane == 0) { L[5].cbp = cbp; L[5].cbp_blk = blkm; L[5].dist = dist; L[5].i16mode = m16; }
     }
     // ---- the four chroma intra modes (ChromaResidualCoding of IntraChromaPrediction8x8 [J])
-    const bool cav[4] = {true, avL, avT, avT && avL && avTL};
-    for (int m0 = 0; m0 < 4; m0 += 2) {
-        const int half = tid >> 7, m = m0 + half;
-        const bool act = m == 0 || (m == 1 ? avL : m == 2 ? avT : cav[3]);
-        const int dist = chroma_cand<pel>(d, s.nb.orgc, &s.nb, m, nullptr, false, act, s.cb[half], act ? &scr->C[5 + m] : nullptr, tid & 127,
-                                          mbx, mby, avT, avL);
-        if (act && (tid & 127) == 0) scr->C[5 + m].dist = dist;
-        __syncthreads();
+#pragma unroll 1
+    for (int m = 0; m < 4; m++) {
+        const bool act = m == 0 || (m == 1 ? avL : m == 2 ? avT : avT && avL && avTL);
+        if (!act) continue;                             // uniform
+        const int dist = chroma_cand_w<pel>(d, s.nb.orgc, &s.nb, m, nullptr, false, &scr->C[5 + m], lane, mbx, mby, avT, avL);
+        if (lane == 0) scr->C[5 + m].dist = dist;
     }
     // ---- Intra4x4: Mode_Decision_for_4x4IntraBlocks [J] by RDCost_for_4x4IntraBlocks, 16 blocks in
-    //      coding order: 9 modes x 16 lanes code, lane 16 m rates mode m, thread 0 decides
-    if (tid == 0) { s.i4cbp = 0; s.i4blk = 0; }
+    //      coding order: 9 modes x 16 lanes code (three passes), lane m rates mode m, a wave-uniform
+    //      decision
+    int i4cbp = 0, i4blk = 0;
     const int rnd = q_round(d.qsel, 15 + qp / 6);
+#pragma unroll 1
     for (int i = 0; i < 16; i++) {
-        const int b8 = i >> 2, b4 = i & 3;
-        const int bx = 8 * (b8 & 1) + 4 * (b4 & 1), by = 8 * (b8 >> 1) + 4 * (b4 >> 1), bx4 = bx >> 2, by4 = by >> 2, blk = 4 * by4 + bx4;
+        const int b8 = i >> 2, bb = i & 3;
+        const int bx = 8 * (b8 & 1) + 4 * (bb & 1), by = 8 * (b8 >> 1) + 4 * (bb >> 1), bx4 = bx >> 2, by4 = by >> 2, blk = 4 * by4 + bx4;
         const bool up = by > 0 || avT, left = bx > 0 || avL;
         const bool ul = (bx > 0 && by > 0) || (bx == 0 && by > 0 && avL) || (bx > 0 && by == 0 && avT) || (bx == 0 && by == 0 && avTL);
         bool ur = by == 0 ? (bx + 4 <= 15 ? avT : avTR) : (bx + 4 <= 15);
         if ((bx == 4 || bx == 12) && (by == 4 || by == 12)) ur = false;
-        if (tid < 13) {
+        if (lane < 13) {
             int v;
-            if (tid == 0) v = ul ? i4_lpix(s, bx - 1, by - 1) : 0;
-            else if (tid <= 4) v = up ? i4_lpix(s, bx + tid - 1, by - 1) : 0;
-            else if (tid <= 8) v = up ? i4_lpix(s, ur ? bx + tid - 1 : bx + 3, by - 1) : 0;
-            else v = left ? i4_lpix(s, bx - 1, by + tid - 9) : 0;
-            s.P[tid] = v;
-        } else if (tid == 64) {
-            const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + bx4];
-            const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + by4];
-            s.mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
+            if (lane == 0) v = ul ? i4_lpix(s, bx - 1, by - 1) : 0;
+            else if (lane <= 4) v = up ? i4_lpix(s, bx + lane - 1, by - 1) : 0;
+            else if (lane <= 8) v = up ? i4_lpix(s, ur ? bx + lane - 1 : bx + 3, by - 1) : 0;
+            else v = left ? i4_lpix(s, bx - 1, by + lane - 9) : 0;
+            s.P[lane] = v;
         }
-        __syncthreads();
-        const int m = tid >> 4, l = tid & 15;
-        const bool avm = m < 9 && (m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul));
-        if (m < 9) {                                    // 144 threads: the nine modes' dct_luma
+        const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + bx4];
+        const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + by4];
+        const int mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
+        for (int k = lane; k < 9 * (JMR_NCTX / 4); k += 64) {   // each rate lane's copy of the MB-start state
+            const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
+            reinterpret_cast<uint32_t *>(s.stc[m])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
+        }
+        wave_lds_sync();
+        const int org = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];
+        const int st = s.P[1] + s.P[2] + s.P[3] + s.P[4], sl = s.P[9] + s.P[10] + s.P[11] + s.P[12];
+        const int dcp = (up && left) ? (st + sl + 4) >> 3 : left ? (sl + 2) >> 2 : up ? (st + 2) >> 2 : (maxv + 1) >> 1;
+#pragma unroll
+        for (int pass = 0; pass < 3; pass++) {          // the nine modes' dct_luma
+            const int m = 4 * pass + b4;
+            if (pass == 2 && b4 > 0) break;             // wave-uniform per 16-lane row; DPP stays inside rows
             const int e = c_i4tab[m][l], ty = e & 3;
             const int pa = s.P[(e >> 2) & 15], pb = s.P[(e >> 6) & 15], pc = s.P[(e >> 10) & 15];
-            const int st = s.P[1] + s.P[2] + s.P[3] + s.P[4], sl = s.P[9] + s.P[10] + s.P[11] + s.P[12];
-            const int dc = (up && left) ? (st + sl + 4) >> 3 : left ? (sl + 2) >> 2 : up ? (st + 2) >> 2 : (maxv + 1) >> 1;
-            const int p = ty == 1 ? (pa + pb + 1) >> 1 : ty == 2 ? (pa + 2 * pb + pc + 2) >> 2 : dc;
-            const int org = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];
+            const int p = ty == 1 ? (pa + pb + 1) >> 1 : ty == 2 ? (pa + 2 * pb + pc + 2) >> 2 : dcp;
             const int c = lane_fwd4x4(org - p, l);
             int lev, dq, cc;
             const unsigned nz = lane_quant(c, l, qp, rnd, false, lev, dq, cc);
@@ -562,78 +607,90 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
             const int dist = row16_sum((org - rv) * (org - rv));
             if (l == 0) { s.dist[m] = dist; s.nz[m] = nz != 0; }
         }
-        __syncthreads();
-        if (l == 0 && avm) {                            // lane 16 m: the block's rate in mode m
-            copy_ctx(s.stc[m], s.st0);
-            jmr_eng e = {s.stc[m], s.rg0, 0};
-            const int mpm = s.mpm;
-            jmr_i4(&e, A, B, bx4, by4, m == mpm ? -1 : m < mpm ? m : m - 1, s.lev[m]);
-            s.bits[m] = e.bits;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            double best = 1e30;
-            int bm = 2;
-            for (int mm = 0; mm < 9; mm++) {
-                const bool av = mm == 2 || ((mm == 0 || mm == 3 || mm == 7) && up) || ((mm == 1 || mm == 8) && left) || (up && left && ul);
-                if (!av) continue;
-                const double rd = rd_cost(s.dist[mm], s.bits[mm], d.lambda_rd);
-                if (rd < best) { best = rd; bm = mm; }
+        wave_lds_sync();
+        {                                               // lane m: the block's rate in mode m
+            const int m = lane;
+            const bool avm = m < 9 && (m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul));
+            if (avm) {
+                jmr_eng e = {s.stc[m], rg0, 0};
+                jmr_i4(&e, A, B, bx4, by4, m == mpm ? -1 : m < mpm ? m : m - 1, s.lev[m]);
+                s.bits[m] = e.bits;
             }
-            s.sel = bm;
+        }
+        wave_lds_sync();
+        double best = 1e30;                             // wave-uniform decision, strict '<'
+        int bm = 2;
+        for (int mm = 0; mm < 9; mm++) {
+            const bool av = mm == 2 || ((mm == 0 || mm == 3 || mm == 7) && up) || ((mm == 1 || mm == 8) && left) || (up && left && ul);
+            if (!av) continue;
+            const double rd = rd_cost(s.dist[mm], s.bits[mm], d.lambda_rd);
+            if (rd < best) { best = rd; bm = mm; }
+        }
+        if (lane == 0) {
             s.ipred_cur[blk] = (int8_t)bm;
-            const int mpm = s.mpm;
             L[6].imode[blk] = (int8_t)bm;
             L[6].ipm[blk] = (int8_t)(bm == mpm ? -1 : bm < mpm ? bm : bm - 1);
-            if (s.nz[bm]) { s.i4cbp |= 1 << b8; s.i4blk |= 1 << blk; }
         }
-        __syncthreads();
-        if (tid < 16) {
-            const int sel = s.sel;
-            s.rec[(by + (tid >> 2)) * 16 + bx + (tid & 3)] = s.r4[sel][tid];
-            L[6].luma[blk][tid] = s.lev[sel][tid];
+        if (s.nz[bm]) { i4cbp |= 1 << b8; i4blk |= 1 << blk; }
+        if (lane < 16) {
+            s.rec[(by + (lane >> 2)) * 16 + bx + (lane & 3)] = s.r4[bm][lane];
+            L[6].luma[blk][lane] = s.lev[bm][lane];
         }
-        __syncthreads();
+        wave_lds_sync();
     }
-    L[6].rec[tid] = s.rec[tid];
-    const int e = (int)s.org[tid] - (int)s.rec[tid];
-    const int dist = block_sum(e * e, s.red, tid);
-    if (tid == 0) { L[6].cbp = s.i4cbp; L[6].cbp_blk = s.i4blk; L[6].dist = dist; L[6].i16mode = 0; }
-    if (tid < 32) L[6].mv[tid >> 1][tid & 1] = 0;
+    int e2 = 0;
+    for (int i = lane; i < 256; i += 64) {
+        L[6].rec[i] = s.rec[i];
+        const int e = (int)s.org[i] - (int)s.rec[i];
+        e2 += e * e;
+    }
+    const int dist = wave_sum(e2);
+    if (lane == 0) { L[6].cbp = i4cbp; L[6].cbp_blk = i4blk; L[6].dist = dist; L[6].i16mode = 0; }
+    if (lane < 32) L[6].mv[lane >> 1][lane & 1] = 0;
 }
 
 template <class pel>
-__global__ __launch_bounds__(NT, 2) void k_rdo_analyse(const TickArgs t) {
-    __shared__ union {
-        RdoInterS<pel> in;
-        RdoIntraS<pel> ia;
-    } s;
-    const int tid = threadIdx.x, nP = t.pre[t.nP], nPg = xcd_grid(nP), tot = t.pre[t.npic], b = blockIdx.x;
-    RdoScr<pel> *base = reinterpret_cast<RdoScr<pel> *>(t.rscr);
-    if (b < nPg) {
-        const int m = xcd_block(b, nP);
-        if (m >= nP) return;                            // padding block (whole workgroup)
-        const int e = tick_entry(t, m);
-        const DevParams d = tick_params(t, e);
-        int mbx, mby;
-        tick_mb(t, d, e, m, mbx, mby);
-        rdo_inter_mb(d, s.in, base + m, mbx, mby, tid);
-    } else {
-        const int m = xcd_block(b - nPg, tot);
-        if (m >= tot) return;
-        const int e = tick_entry(t, m);
-        const DevParams d = tick_params(t, e);
-        int mbx, mby;
-        tick_mb(t, d, e, m, mbx, mby);
-        rdo_intra_mb(d, s.ia, base + m, mbx, mby, tid);
-    }
+__global__ __launch_bounds__(NTE) void k_rdo_inter(const TickArgs t) {
+    __shared__ RdoInterS<pel> s;
+    const int nP = t.pre[t.nP], m = xcd_block(blockIdx.x, nP);
+    if (m >= nP) return;                                // padding block (whole workgroup)
+    const int e = tick_entry(t, m);
+    const DevParams d = tick_params(t, e);
+    int mbx, mby;
+    tick_mb(t, d, e, m, mbx, mby);
+    rdo_inter_mb(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
+}
+template <class pel>
+__global__ __launch_bounds__(NTE) void k_rdo_intra(const TickArgs t) {
+    __shared__ RdoIntraS<pel> s;
+    const int tot = t.pre[t.npic], m = xcd_block(blockIdx.x, tot);
+    if (m >= tot) return;
+    const int e = tick_entry(t, m);
+    const DevParams d = tick_params(t, e);
+    int mbx, mby;
+    tick_mb(t, d, e, m, mbx, mby);
+    rdo_intra_mb(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
 }
 
 // ======================================================================================
 //  k_rdo_final: RDCost_for_macroblocks over the candidates, the decision, its outputs
 // ======================================================================================
+struct RdoFinL {                  // the syntax of a luma candidate the rate reads (RdoLuma's first 672 B + ipm)
+    int16_t luma[16][16];
+    int16_t luma_dc[16];
+    int16_t mv[16][2];
+    int16_t mvd[16][2];
+    int8_t ipm[16];
+};
+struct RdoFinC {                  // of a chroma candidate (RdoChroma's first 272 B)
+    int16_t dc[2][4];
+    int16_t ac[2][4][16];
+};
 template <class pel>
 struct RdoFinS {
+    RdoFinL fl[RD_NL];            // the candidates' syntax in LDS: the serial CABAC loops read it bin by bin
+    RdoFinC fc[9];
+    int16_t mvw[RD_NCAND][16][2];   // jmr_mb's work buffers
     alignas(4) uint8_t st0[JMR_NCTX];
     alignas(4) uint8_t stc[RD_NCAND][JMR_NCTX];
     jmr_mbinfo nbA, nbB, out[RD_NCAND];
@@ -666,6 +723,7 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         const uint32_t rg = rdo_state_load(d, a, s.st0, tid, 64);
         if (tid == 0) s.rg0 = rg;
     } else if (tid < 128) rdo_nb_load(d, mbx, mby, s.nbA, s.nbB, s.hasA, s.hasB, tid - 64);
+    else if (tid >= 160) jmr_lds_tables_load(tid - 160, 96);
     else if (tid == 128) {                              // the candidates in JM's order
         const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
         const bool cav[4] = {true, mav.L, mav.T, mav.T && mav.L && mav.TL};
@@ -682,14 +740,33 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     }
     __syncthreads();
     const jmr_mbinfo *A = s.hasA ? &s.nbA : nullptr, *B = s.hasB ? &s.nbB : nullptr;
-    // ---- one lane per candidate: its rate on its own copy of the coding state
-    if (tid < s.ncand) {
-        const int i = s.ci[tid], cm = s.ccm[tid];
+    // ---- one lane per candidate: its rate on its own copy of the coding state; candidate k on
+    //      lane k / 4 of wave k % 4, so the four SIMDs share the serial CABAC work
+    for (int i = tid; i < s.ncand * (JMR_NCTX / 4); i += NT) {
+        const int k = i / (JMR_NCTX / 4), j = i - k * (JMR_NCTX / 4);
+        reinterpret_cast<uint32_t *>(s.stc[k])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
+    }
+    {
+        constexpr int nl = 672 / 4, nc = (int)sizeof(RdoFinC) / 4;
+        static_assert(offsetof(RdoLuma<pel>, ipm) > 672 && offsetof(RdoFinL, ipm) == 672, "RdoFinL layout");
+        for (int i = tid; i < RD_NL * (nl + 4); i += NT) {
+            const int k = i / (nl + 4), j = i - k * (nl + 4);
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(&scr->L[k]);
+            reinterpret_cast<uint32_t *>(&s.fl[k])[j] = j < nl ? src[j] : reinterpret_cast<const uint32_t *>(scr->L[k].ipm)[j - nl];
+        }
+        for (int i = tid; i < 9 * nc; i += NT) {
+            const int k = i / nc, j = i - k * nc;
+            reinterpret_cast<uint32_t *>(&s.fc[k])[j] = reinterpret_cast<const uint32_t *>(&scr->C[k])[j];
+        }
+    }
+    __syncthreads();
+    const int kc = 4 * (tid & 63) + (tid >> 6);
+    if ((tid & 63) < 4 && kc < s.ncand) {
+        const int i = s.ci[kc], cm = s.ccm[kc];
         const RdoLuma<pel> &L = scr->L[i];
         const RdoChroma<pel> &C = scr->C[i >= 5 ? 5 + cm : i];
-        copy_ctx(s.stc[tid], s.st0);
-        jmr_eng en = {s.stc[tid], s.rg0, 0};
-        if (i == 0) jmr_skip(&en, A, B, &s.out[tid]);
+        jmr_eng en = {s.stc[kc], s.rg0, 0};
+        if (i == 0) jmr_skip(&en, A, B, &s.out[kc]);
         else {
             jmr_cand r;
             r.mb_type = i == 4 ? JMH_P8x8 : i == 5 ? JMH_I16MB : i == 6 ? JMH_I4MB : i;
@@ -698,17 +775,20 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
             r.cmode = i >= 5 ? cm : 0;
             r.t8 = 0;
             for (int q = 0; q < 4; q++) r.b8mode[q] = L.b8mode[q];
-            r.ipm = L.ipm;
-            r.mvd = L.mvd;
-            r.luma = L.luma;
-            r.luma_dc = L.luma_dc;
-            r.cdc = C.dc;
-            r.cac = C.ac;
-            jmr_mb(&en, A, B, &r, slice_p, 0, &s.out[tid]);
+            const RdoFinL &FL = s.fl[i];
+            const RdoFinC &FC = s.fc[i >= 5 ? 5 + cm : i];
+            r.ipm = FL.ipm;
+            r.mvd = FL.mvd;
+            r.luma = FL.luma;
+            r.luma_dc = FL.luma_dc;
+            r.cdc = FC.dc;
+            r.cac = FC.ac;
+            r.mvw = s.mvw[kc];
+            jmr_mb(&en, A, B, &r, slice_p, 0, &s.out[kc]);
         }
-        s.bits[tid] = en.bits;
-        s.rgo[tid] = en.range;
-        s.rd[tid] = rd_cost(L.dist + C.dist, en.bits, d.lambda_rd);
+        s.bits[kc] = en.bits;
+        s.rgo[kc] = en.range;
+        s.rd[kc] = rd_cost(L.dist + C.dist, en.bits, d.lambda_rd);
     }
     __syncthreads();
     if (tid == 0) {                                     // strict '<' in JM's order
@@ -794,9 +874,13 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
 hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st) {
     const int tot = t.pre[t.npic];
     if (!tot) return hipSuccess;
-    const int na = xcd_grid(t.pre[t.nP]) + xcd_grid(tot);
-    if (t.bd > 8) hipLaunchKernelGGL(k_rdo_analyse<uint16_t>, dim3(na), dim3(NT), 0, st, t);
-    else hipLaunchKernelGGL(k_rdo_analyse<uint8_t>, dim3(na), dim3(NT), 0, st, t);
+    const int nP = t.pre[t.nP];
+    if (nP) {
+        if (t.bd > 8) hipLaunchKernelGGL(k_rdo_inter<uint16_t>, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
+        else hipLaunchKernelGGL(k_rdo_inter<uint8_t>, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
+    }
+    if (t.bd > 8) hipLaunchKernelGGL(k_rdo_intra<uint16_t>, dim3(xcd_grid(tot)), dim3(NTE), 0, st, t);
+    else hipLaunchKernelGGL(k_rdo_intra<uint8_t>, dim3(xcd_grid(tot)), dim3(NTE), 0, st, t);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     if (t.bd > 8) hipLaunchKernelGGL(k_rdo_final<uint16_t>, dim3(xcd_grid(tot)), dim3(NT), 0, st, t);

@@ -369,7 +369,9 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
             if (i == 0) jmr_skip(&e, A, B, NULL);
             else {
                 jmr_cand r;
+                int16_t mvw[16][2];
                 fill_cand(&r, &Lc[i], C, intra ? cm : 0);
+                r.mvw = mvw;
                 jmr_mb(&e, A, B, &r, s->slice_p, 0, NULL);
             }
             double rd = (double)(Lc[i].dist + C->dist) + lam * (double)e.bits;
@@ -421,7 +423,9 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
     if (bi == 0) jmr_skip(&e, A, B, &c->mbi[a]);
     else {
         jmr_cand r;
+        int16_t mvw[16][2];
         fill_cand(&r, L, C, is_intra ? bcm : 0);
+        r.mvw = mvw;
         jmr_mb(&e, A, B, &r, s->slice_p, 0, &c->mbi[a]);
     }
     if ((a + 1) % k != 0 && a + 1 < nmb) jmr_end_of_mb(&e);
