@@ -274,6 +274,8 @@ template <class pel>
 __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
     const int a = mby * d.mbw + mbx, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
+    const bool prof = d.prof && lane == 0 && d.prof_mb == a;   // debug (JMH_PHASE_PROF): stamps 40..52
+    PSTAMP(40);
     RdoP8Tmp *tp;
     RdoP8Px<pel> *px8;
     if constexpr (sizeof(pel) == 2) {
@@ -302,6 +304,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         }
     }
     wave_lds_sync();
+    PSTAMP(41);
     const jmr_mbinfo *A = hasA ? &s.nbA : nullptr, *B = hasB ? &s.nbB : nullptr;
     // ---- motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch [J])
     epzs_block<1>(d, s.e, wn, 0, 0, 0, 0, 0, false);
@@ -309,6 +312,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     epzs_block<2>(d, s.e, wn, 0, 2, 1, 0, 0, false);
     epzs_block<3>(d, s.e, wn, 0, 0, 0, 0, 0, false);
     epzs_block<3>(d, s.e, wn, 2, 0, 1, 0, 0, false);
+    PSTAMP(42);
     const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
     for (int i = lane; i < JMR_NCTX / 4; i += 64) reinterpret_cast<uint32_t *>(s.strun)[i] = reinterpret_cast<const uint32_t *>(s.st0)[i];
     if (lane == 0) memset(&s.currun, 0, sizeof(s.currun));
@@ -331,6 +335,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         epzs_block<7>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false);
         epzs_block<7>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false);
         epzs_block<7>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false);
+        PSTAMP(43 + 2 * b8);
         const int bx4 = X + (b4 & 1), by4 = Y + (b4 >> 1), k = by4 * 4 + bx4;
         const int px = 4 * bx4 + (l & 3), py = 4 * by4 + (l >> 2), q8 = (4 * (b4 >> 1) + (l >> 2)) * 8 + 4 * (b4 & 1) + (l & 3);
         const int org = s.e.org[py * 16 + px];
@@ -396,6 +401,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
             s.p8lev[kk][lane & 15] = tp->lev8[bm][qb][lane & 15];
         }
         wave_lds_sync();
+        PSTAMP(44 + 2 * b8);
     }
     RdoLuma<pel> *L = scr->L;
     if (p8) {                                           // SetCoeffAndReconstruction8x8
@@ -457,6 +463,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         if (lane == 0) scr->C[c].dist = dist;
         wave_lds_sync();
     }
+    PSTAMP(52);
 }
 
 // ======================================================================================
@@ -493,6 +500,8 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
     const int a = mby * d.mbw + mbx, W = d.W, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
+    const bool prof = d.prof && lane == 0 && d.prof_mb == a;   // debug (JMH_PHASE_PROF): stamps 53..56
+    PSTAMP(53);
     const pel *orgY = spl<pel>(d.orgY);
     for (int i = lane; i < 256; i += 64) s.org[i] = orgY[(pix_y + (i >> 4)) * W + pix_x + (i & 15)];
     for (int i = lane; i < 128; i += 64) load_orgc(d, s.nb, i, mbx, mby);
@@ -551,6 +560,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
         const int dist = wave_sum(e2);
         if (lane == 0) { L[5].cbp = cbp; L[5].cbp_blk = blkm; L[5].dist = dist; L[5].i16mode = m16; }
     }
+    PSTAMP(54);
     // ---- the four chroma intra modes (ChromaResidualCoding of IntraChromaPrediction8x8 [J])
 #pragma unroll 1
     for (int m = 0; m < 4; m++) {
@@ -562,8 +572,12 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
     // ---- Intra4x4: Mode_Decision_for_4x4IntraBlocks [J] by RDCost_for_4x4IntraBlocks, 16 blocks in
     //      coding order: 9 modes x 16 lanes code (three passes), lane m rates mode m, a wave-uniform
     //      decision
+    PSTAMP(55);
     int i4cbp = 0, i4blk = 0;
     const int rnd = q_round(d.qsel, 15 + qp / 6);
+    int i4e[3];                                         // the lane's prediction formulas, once
+#pragma unroll
+    for (int pass = 0; pass < 3; pass++) i4e[pass] = 4 * pass + b4 < 9 ? c_i4tab[4 * pass + b4][l] : 0;
 #pragma unroll 1
     for (int i = 0; i < 16; i++) {
         const int b8 = i >> 2, bb = i & 3;
@@ -595,7 +609,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
         for (int pass = 0; pass < 3; pass++) {          // the nine modes' dct_luma
             const int m = 4 * pass + b4;
             if (pass == 2 && b4 > 0) break;             // wave-uniform per 16-lane row; DPP stays inside rows
-            const int e = c_i4tab[m][l], ty = e & 3;
+            const int e = i4e[pass], ty = e & 3;
             const int pa = s.P[(e >> 2) & 15], pb = s.P[(e >> 6) & 15], pc = s.P[(e >> 10) & 15];
             const int p = ty == 1 ? (pa + pb + 1) >> 1 : ty == 2 ? (pa + 2 * pb + pc + 2) >> 2 : dcp;
             const int c = lane_fwd4x4(org - p, l);
@@ -647,6 +661,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
     const int dist = wave_sum(e2);
     if (lane == 0) { L[6].cbp = i4cbp; L[6].cbp_blk = i4blk; L[6].dist = dist; L[6].i16mode = 0; }
     if (lane < 32) L[6].mv[lane >> 1][lane & 1] = 0;
+    PSTAMP(56);
 }
 
 template <class pel>
@@ -654,22 +669,35 @@ __global__ __launch_bounds__(NTE) void k_rdo_inter(const TickArgs t) {
     __shared__ RdoInterS<pel> s;
     const int nP = t.pre[t.nP], m = xcd_block(blockIdx.x, nP);
     if (m >= nP) return;                                // padding block (whole workgroup)
+    const unsigned long long bt0 = t.bprof ? wall_clock64() : 0;   // debug (JMH_BLOCK_PROF): role 4
     const int e = tick_entry(t, m);
     const DevParams d = tick_params(t, e);
     int mbx, mby;
     tick_mb(t, d, e, m, mbx, mby);
     rdo_inter_mb(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
+    if (t.bprof && threadIdx.x == 0) {
+        t.bprof[3 * blockIdx.x] = bt0;
+        t.bprof[3 * blockIdx.x + 1] = wall_clock64();
+        t.bprof[3 * blockIdx.x + 2] = 4;
+    }
 }
 template <class pel>
 __global__ __launch_bounds__(NTE) void k_rdo_intra(const TickArgs t) {
     __shared__ RdoIntraS<pel> s;
     const int tot = t.pre[t.npic], m = xcd_block(blockIdx.x, tot);
     if (m >= tot) return;
+    const unsigned long long bt0 = t.bprof ? wall_clock64() : 0;   // debug (JMH_BLOCK_PROF): role 1
     const int e = tick_entry(t, m);
     const DevParams d = tick_params(t, e);
     int mbx, mby;
     tick_mb(t, d, e, m, mbx, mby);
     rdo_intra_mb(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
+    if (t.bprof && threadIdx.x == 0) {
+        unsigned long long *bp = t.bprof + 3 * xcd_grid(t.pre[t.nP]);
+        bp[3 * blockIdx.x] = bt0;
+        bp[3 * blockIdx.x + 1] = wall_clock64();
+        bp[3 * blockIdx.x + 2] = 1;
+    }
 }
 
 // ======================================================================================
@@ -698,6 +726,7 @@ struct RdoFinS {
     uint32_t rg0, rgo[RD_NCAND];
     double rd[RD_NCAND];
     int bits[RD_NCAND], ci[RD_NCAND], ccm[RD_NCAND];
+    int8_t kof[4][4];             // the candidate on lane j < 4 of wave w (-1: none)
     int ncand, win;
     alignas(4) pel rec[256];
     pel cfin[2][64];
@@ -711,12 +740,15 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     const int tid = threadIdx.x, tot = t.pre[t.npic];
     const int m = xcd_block(blockIdx.x, tot);
     if (m >= tot) return;
+    const unsigned long long bt0 = t.bprof_fin ? wall_clock64() : 0;   // debug (JMH_BLOCK_PROF): role 3
     const int e = tick_entry(t, m);
     const DevParams d = tick_params(t, e);
     int mbx, mby;
     tick_mb(t, d, e, m, mbx, mby);
     const RdoScr<pel> *scr = reinterpret_cast<const RdoScr<pel> *>(t.rscr) + m;
     const int a = mby * d.mbw + mbx, W = d.W, Wc = d.Wc, W4 = d.W >> 2, pix_x = 16 * mbx, pix_y = 16 * mby;
+    const bool prof = d.prof && tid == 0 && d.prof_mb == a;   // debug (JMH_PHASE_PROF): stamps 57..60
+    PSTAMP(57);
     const bool slice_p = d.slice_type == JMH_P_SLICE;
     const MbAvail mav = mb_avail(d, mbx, mby);
     if (tid < 64) {
@@ -737,11 +769,19 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
             }
         }
         s.ncand = n;
+        // lanes of one wave run the same syntax (divergent lanes in different code cost the sum):
+        // wave 0 the Intra4x4 candidates, 1 the Intra16x16 ones, 2 skip / 16x16 / 16x8 / 8x16, 3 P8x8
+        int fill[4] = {0, 0, 0, 0};
+        for (int w = 0; w < 16; w++) s.kof[w >> 2][w & 3] = -1;
+        for (int k = 0; k < n; k++) {
+            const int i = s.ci[k], w = i == 6 ? 0 : i == 5 ? 1 : i == 4 ? 3 : 2;
+            s.kof[w][fill[w]++] = (int8_t)k;
+        }
     }
     __syncthreads();
     const jmr_mbinfo *A = s.hasA ? &s.nbA : nullptr, *B = s.hasB ? &s.nbB : nullptr;
-    // ---- one lane per candidate: its rate on its own copy of the coding state; candidate k on
-    //      lane k / 4 of wave k % 4, so the four SIMDs share the serial CABAC work
+    // ---- one lane per candidate: its rate on its own copy of the coding state (lanes 0..3 of the
+    //      four waves, grouped by macroblock type: kof)
     for (int i = tid; i < s.ncand * (JMR_NCTX / 4); i += NT) {
         const int k = i / (JMR_NCTX / 4), j = i - k * (JMR_NCTX / 4);
         reinterpret_cast<uint32_t *>(s.stc[k])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
@@ -760,8 +800,9 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         }
     }
     __syncthreads();
-    const int kc = 4 * (tid & 63) + (tid >> 6);
-    if ((tid & 63) < 4 && kc < s.ncand) {
+    PSTAMP(58);
+    const int kc = (tid & 63) < 4 ? s.kof[tid >> 6][tid & 3] : -1;
+    if (kc >= 0) {
         const int i = s.ci[kc], cm = s.ccm[kc];
         const RdoLuma<pel> &L = scr->L[i];
         const RdoChroma<pel> &C = scr->C[i >= 5 ? 5 + cm : i];
@@ -791,6 +832,7 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         s.rd[kc] = rd_cost(L.dist + C.dist, en.bits, d.lambda_rd);
     }
     __syncthreads();
+    PSTAMP(59);
     if (tid == 0) {                                     // strict '<' in JM's order
         double best = 1e30;
         int w = 0;
@@ -868,6 +910,12 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     if (d.dbkY) {
         const int qpi = iclip(-d.qpbd, 51, d.qp + d.cqp_off), qpcy = qpi < 0 ? qpi : c_qpc[qpi];
         deblock_mb(d, s.db, s.rec, s.cfin, s.fmv, is_intra, cbp_blk, false, d.qp, qpcy, mbx, mby, tid);
+    }
+    PSTAMP(60);
+    if (t.bprof_fin && tid == 0) {
+        t.bprof_fin[3 * blockIdx.x] = bt0;
+        t.bprof_fin[3 * blockIdx.x + 1] = wall_clock64();
+        t.bprof_fin[3 * blockIdx.x + 2] = 3;
     }
 }
 

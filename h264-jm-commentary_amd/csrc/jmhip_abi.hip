@@ -586,7 +586,9 @@ static int issue_tick(jmh_ctx *c) {
     if (c->d_bprof && c->ticks_total == c->bprof_tick) {
         t.bprof = c->d_bprof;
         // the analysis blocks: k_mb_analyse's (roles 0 / 2), or the separate search kernel's (role 4)
-        const int na = t.me_in_analyse ? xcd_grid(t.pre[nP]) + (t.pre[k] + 3) / 4 : xcd_grid(t.pre[nP]);
+        // RDO: k_rdo_inter's blocks (role 4), then k_rdo_intra's (role 1)
+        const int na = t.rdo ? xcd_grid(t.pre[nP]) + xcd_grid(t.pre[k])
+                             : t.me_in_analyse ? xcd_grid(t.pre[nP]) + (t.pre[k] + 3) / 4 : xcd_grid(t.pre[nP]);
         t.bprof_fin = c->d_bprof + 3 * na;
         HCHK(hipMemsetAsync(c->d_bprof, 0, ((size_t)3 * 3 * PMAX * c->mbh + 64) * sizeof(unsigned long long), c->st));
         c->bprof_blocks = na + xcd_grid(t.pre[k]);
@@ -906,12 +908,14 @@ int jmh_sync(jmh_ctx *c) {
         double sum[5] = {0, 0, 0, 0, 0}, mx[5] = {0, 0, 0, 0, 0};
         std::vector<double> durs[5];
         int n[5] = {0, 0, 0, 0, 0};
-        unsigned long long f0 = ~0ull, f1 = 0;
+        unsigned long long f0 = ~0ull, f1 = 0, r0[5], r1[5];
+        for (int r = 0; r < 5; r++) { r0[r] = ~0ull; r1[r] = 0; }
         for (int i = 0; i < c->bprof_blocks; i++) {
             unsigned long long a = h[3 * i], b = h[3 * i + 1];
             int role = (int)h[3 * i + 2];
             if (!a || role < 0 || role > 4 || b < a) continue;   // 0: padding block, not written
             if (role == 3) { f0 = a < f0 ? a : f0; f1 = b > f1 ? b : f1; }
+            r0[role] = a < r0[role] ? a : r0[role]; r1[role] = b > r1[role] ? b : r1[role];
             t0 = a < t0 ? a : t0; t1 = b > t1 ? b : t1;
             double dur = (double)(b - a) * us;
             sum[role] += dur; n[role]++; mx[role] = dur > mx[role] ? dur : mx[role];
@@ -921,8 +925,8 @@ int jmh_sync(jmh_ctx *c) {
         for (int r = 0; r < 5; r++)
             if (n[r]) {
                 std::sort(durs[r].begin(), durs[r].end());
-                fprintf(stderr, " role%d: n=%d mean=%.1fus p50=%.1f p90=%.1f max=%.1fus", r, n[r], sum[r] / n[r], durs[r][n[r] / 2],
-                        durs[r][(9 * n[r]) / 10], mx[r]);
+                fprintf(stderr, " role%d: n=%d mean=%.1fus p50=%.1f p90=%.1f max=%.1fus (from %.1f to %.1fus)", r, n[r], sum[r] / n[r],
+                        durs[r][n[r] / 2], durs[r][(9 * n[r]) / 10], mx[r], (double)(r0[r] - t0) * us, (double)(r1[r] - t0) * us);
             }
         if (f1) fprintf(stderr, " final: first start %.1fus after the analysis' first, span %.1fus", (double)(f0 - t0) * us, (double)(f1 - f0) * us);
         fprintf(stderr, "\n");
