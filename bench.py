@@ -29,7 +29,7 @@ k mod the device count); under torchrun WORLD_SIZE must equal --gpus.
 2160p synthetic, High profile, EPZS (SearchMode 3) + adaptive 8x8 transform (Transform8x8Mode 1).
 --config 5 runs config 5 (a variant line): 2160p synthetic 10-bit (High 10, 16-bit samples in HBM),
 EPZS, SliceMode 1 with 240-MB slices (one MB row), RDOptimization 1 -- the device RD loop with the
-CABAC rate of every candidate (k_rdo_analyse + k_rdo_final on the RD stage schedule; the bitstream
+CABAC rate of every candidate (k_rdo_inter + k_rdo_intra + k_rdo_final on the RD stage schedule; the bitstream
 itself is written on the host, outside the metric as for every config).  --rdo 0 runs the RDO-off
 variant of the same shape (EPZS + 8x8 transform).
 
@@ -244,32 +244,32 @@ def read_pmc_traffic():
 # the host-buffer path: PCIe-inclusive rate and single-picture latency (reported, not `value`)
 # ------------------------------------------------------------------------------------------
 def pcie_inclusive(jm, enc, frames, pictures):
-    """jmh_frame_push / jmh_frame_pop on host pictures (source H2D, results + recon + deblocked
-    D2H), steady state: `depth` pictures pushed untimed, then `pictures` push + pop pairs timed.
-    Returns (MP/s, single-picture latency ms on an empty pipeline)."""
+    """jmh_frame_push / jmh_frame_pop on host pictures as lencod drives them (source H2D; results
+    read in place, the deblocked picture into the caller's planes: D2H), steady state: `depth`
+    pictures pushed untimed, then exactly `pictures` pop + push pairs timed (the pipeline stays
+    full).  Returns (MP/s, single-picture latency ms on an empty pipeline)."""
+    import numpy as np
     enc.sync()
-    seq = frames[1:]
+    seq = [tuple(np.ascontiguousarray(p) for p in f) for f in frames[1:]]
+    out = (np.empty((enc.h, enc.w), enc.pdt), np.empty((enc.h // 2, enc.w // 2), enc.pdt),
+           np.empty((enc.h // 2, enc.w // 2), enc.pdt))
     dbk = (0, 0, 0)
     enc.set_reference_slot(-2)
     enc.push(*seq[0], jm.JMH_P_SLICE, QP, deblock=dbk)   # latency: one picture, empty pipeline
-    enc.pop()
+    enc.pop_into(*out)
     latency_ms = enc.timing().total_ms
-    pending = 0
     for i in range(enc.depth):
         enc.set_reference_slot(-2)
         enc.push(*seq[(1 + i) % len(seq)], jm.JMH_P_SLICE, QP, deblock=dbk)
-        pending += 1
     t0 = time.perf_counter()
     for i in range(pictures):
-        enc.pop()
+        enc.pop_into(*out)
         enc.set_reference_slot(-2)
         enc.push(*seq[(1 + enc.depth + i) % len(seq)], jm.JMH_P_SLICE, QP, deblock=dbk)
-    enc.pop()
     dt = time.perf_counter() - t0
-    pending -= 1
-    for _ in range(pending):
-        enc.pop()
-    return pictures * DISP_W * DISP_H / 1e6 / dt, latency_ms
+    for _ in range(enc.depth):
+        enc.pop_into(*out)
+    return pictures * DISP_W * DISP_H / 1e6 / dt, latency_ms, pictures
 
 
 # ------------------------------------------------------------------------------------------
@@ -373,7 +373,7 @@ def main():
 
     host = None
     if not args.no_host_path and size is None and not args.no_deblock:
-        host = pcie_inclusive(jm, enc, frames, min(args.steps, 3 * enc.depth))
+        host = pcie_inclusive(jm, enc, frames, max(120, 3 * enc.depth))
     if args.dump:                                         # test: one read-back picture after the chain
         import numpy as np
         enc.set_reference_slot(stream.ref_slot)
@@ -420,7 +420,7 @@ def main():
         "algorithmic_bytes_per_launch": round(bytes_per_launch),
     }
     launch_info = {
-        "kernel": "k_rdo_analyse + k_rdo_final (the tick's RD launches)" if RDO else "k_mb_analyse" if ffs else
+        "kernel": "k_rdo_inter + k_rdo_intra + k_rdo_final (the tick's RD launches)" if RDO else "k_mb_analyse" if ffs else
                   ("k_mb_epzs" if search_mode == 3 else "k_mb_me_full") + " + k_mb_intra (the tick's analysis launches)",
         "avg_launch_ms": round(an_launch_ms, 5),
         "launches_per_picture": round(an_per_pic, 2),
@@ -467,13 +467,17 @@ def main():
         "roofline": roofline,
         # per-launch averages (sampled every 8th diagonal) x launches per picture
         "kernel_ms_per_picture": {"wavefront": round(mb_ms_pic, 4),
-                                  ("k_rdo_analyse+k_rdo_final" if RDO else "k_mb_analyse"): round(an_launch_ms * an_per_pic, 4),
+                                  ("k_rdo_inter+k_rdo_intra+k_rdo_final" if RDO else "k_mb_analyse"): round(an_launch_ms * an_per_pic, 4),
                                   "k_mb_final": None if RDO else round(tm.final_ms / max(1, tm.final_launches) * an_per_pic, 4)},
         "host_path": None if host is None else {
             "pcie_inclusive_mp_s": round(host[0], 3),
             "single_picture_latency_ms": round(host[1], 3),
-            "note": "jmh_frame_push/pop with host pictures: source H2D + results/recon/deblocked D2H, "
-                    "steady state; latency = one picture on an empty pipeline (fill + drain)",
+            "note": "jmh_frame_push/pop with host pictures as lencod drives them: source H2D (packed into "
+                    "pinned staging), results/recon/deblocked D2H on the copy stream, the results read in "
+                    "place and the deblocked picture copied into the caller's planes; steady state, "
+                    "exactly `pictures` pop+push pairs timed; latency = one picture on an empty pipeline "
+                    "(fill + drain)",
+            "pictures": host[2],
         },
         "verified": None if complete else False,
         "cpu_baseline": None,

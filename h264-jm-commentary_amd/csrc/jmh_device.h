@@ -140,7 +140,7 @@ struct TickArgs {
     int epzs_dual;                       // EPZSDualRefinement (k_mb_epzs)
     int slice_mbs;                       // SliceMode 1: MBs per slice (>= 1; mbw * mbh for one slice)
     int bd;                              // bit depth: 8 (uint8_t samples) or 9 / 10 (uint16_t, High 10)
-    int rdo;                             // RDOptimization 1: k_rdo_analyse + k_rdo_final on the stage
+    int rdo;                             // RDOptimization 1: k_rdo_inter + k_rdo_intra + k_rdo_final on the stage
     const int32_t *sched, *soff;         //   schedule: MB addresses in stage order, offsets per stage
     void *rscr;                          //   the tick's candidate scratch (RdoScr per tick MB)
     const uint32_t *ordtab;              // FFS order keys, [NPK / 2][NTA] packed pairs (jmh_create)

@@ -3,15 +3,15 @@
 // RDCost_for_4x4IntraBlocks) with J = SSD + lambda * R and R the CABAC rate of the slice's coding
 // state (jmh_cabac_rate.h, shared with the CPU oracle oracle/rdo.c).  DESIGN.md §9 has the
 // schedule; one tick of the RD stage schedule runs
-//   k_rdo_analyse  role "inter" (P MBs): the EPZS searches (wave 0), P8x8 block by block with the
-//                  four sub-modes coded and rated on the four waves, the residual coding of the
-//                  skip / 16x16 / 16x8 / 8x16 / P8x8 candidates and their chroma;
-//                  role "intra" (all MBs): Intra16x16, the four chroma intra modes, Intra4x4 by
-//                  per-block RD (9 modes x 16 lanes code, 9 lanes rate);
-//   k_rdo_final    all MBs: one lane per macroblock candidate rates it on its own LDS copy of the
-//                  contexts, the strict-'<' minimum of D + lambda R in JM's order wins; results,
-//                  reconstruction, the slice's next coding state, the fused DeblockMb.
-// Candidates travel between the two launches through the tick's scratch (RdoScr, HBM).
+//   k_rdo_inter   P MBs, one wave each: the EPZS searches, P8x8 block by block (the sub-modes coded a
+//                 pass each, rated on four lanes side by side, a wave-uniform decision), the
+//                 residual coding of the skip / 16x16 / 16x8 / 8x16 / P8x8 candidates and their chroma;
+//   k_rdo_intra   all MBs, one wave each: Intra16x16, the four chroma intra modes, Intra4x4 by
+//                 per-block RD (9 modes x 16 lanes code in three passes, 9 lanes rate);
+//   k_rdo_final   all MBs: one lane per macroblock candidate rates it on its own LDS copy of the
+//                 contexts, the strict-'<' minimum of D + lambda R in JM's order wins; results,
+//                 reconstruction, the slice's next coding state, the fused DeblockMb.
+// Candidates travel to k_rdo_final through the tick's scratch (RdoScr, HBM).
 // docs/JM_SEMANTICS.md items 53-60 pin every RD choice.
 #include "jmh_epzs.h"
 #include "jmh_intra.h"

@@ -277,6 +277,23 @@ class Encoder:
         _check(self.lib.jmh_frame_pop(self.ctx), "jmh_frame_pop")
         return self.results(), self.recon()
 
+    def pop_into(self, y, u, v):
+        """What lencod does per picture: jmh_frame_pop, the results in place (a zero-copy view of the
+        library's host array, valid until the next pop) and the deblocked picture (the recon file /
+        PSNR input) into the caller's planes.  Returns the results view."""
+        _check(self.lib.jmh_frame_pop(self.ctx), "jmh_frame_pop")
+        fn = "jmh_read_deblocked" + self.sfx
+        _check(getattr(self.lib, fn)(self.ctx, _ptr(y), _ptr(u), _ptr(v), self.w, self.w // 2), fn)
+        return self.results_view()
+
+    def results_view(self):
+        n = self.mbw * self.mbh
+        p = self.lib.jmh_get_mb_result(self.ctx, 0)
+        if not p:
+            raise JmhError("no results")
+        buf = (ctypes.c_char * (n * MB_RESULT_DTYPE.itemsize)).from_address(p)
+        return np.frombuffer(buf, dtype=MB_RESULT_DTYPE)
+
     @property
     def depth(self):
         return self.lib.jmh_pipeline_depth(self.ctx)

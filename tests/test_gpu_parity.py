@@ -351,6 +351,33 @@ def run_chain(enc, pics, qp, dbk, pipelined):
     return out
 
 
+def test_pop_into_equals_pop():
+    """The lencod-style pop (results read in place, the deblocked picture into the caller's planes:
+    bench.py's host path) returns what pop() + deblocked() return."""
+    w, h = 320, 240
+    pics = moving_seq(w, h, 6, seed=3, step=(37, -29))
+    dbk = (0, 0, 0)
+    ref = run_chain(jmhip.Encoder(w, h, search_range=16), pics, 30, dbk, True)
+    enc = jmhip.Encoder(w, h, search_range=16)
+    planes = (np.empty((h, w), np.uint8), np.empty((h // 2, w // 2), np.uint8), np.empty((h // 2, w // 2), np.uint8))
+    got, pending = [], 0
+    for i, pic in enumerate(pics):
+        if i:
+            enc.set_reference_slot(-2)
+        if pending == enc.depth:
+            got.append((enc.pop_into(*planes).copy(), tuple(p.copy() for p in planes)))
+            pending -= 1
+        enc.push(*pic, jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE, 30, deblock=dbk)
+        pending += 1
+    for _ in range(pending):
+        got.append((enc.pop_into(*planes).copy(), tuple(p.copy() for p in planes)))
+    assert len(got) == len(ref)
+    for (gres, gdbk), (rres, _, rdbk) in zip(got, ref):
+        assert np.array_equal(gres, rres)
+        for x, y in zip(gdbk, rdbk):
+            assert np.array_equal(x, y)
+
+
 @pytest.mark.parametrize("w,h,sr,n,step,kw", [(176, 144, 16, 9, (37, -29), {}), (320, 240, 32, 8, (37, -29), {}),
                                               (1920, 1088, 32, 20, (37, -29), {}), (1920, 1088, 32, 12, (-62, -61), {}),
                                               (640, 480, 32, 10, (63, 62), {}),

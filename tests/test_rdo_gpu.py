@@ -1,4 +1,4 @@
-"""RDOptimization = 1 on the MI355X (row f4, config 5): k_rdo_analyse / k_rdo_final on the RD stage
+"""RDOptimization = 1 on the MI355X (row f4, config 5): k_rdo_inter / k_rdo_intra / k_rdo_final on the RD stage
 schedule must equal the CPU oracle (oracle/rdo.c) bit for bit -- every macroblock's result
 (mode, MVs, levels, the chosen candidate's rate in min_cost) and the reconstruction -- and the
 product lencod with the device RD loop must write the same bitstream as the CPU lencod, with the
