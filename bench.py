@@ -74,6 +74,8 @@ CONFIG5_RDO_OFF = dict(metric="ME+transform megapixels/sec @2160p High10 10-bit 
                                 "SearchRange=32, Transform8x8Mode=1, UseHadamard=1, 7 inter block sizes, RDO off, QP 28, "
                                 "IDR + {nf}-picture P sequence cycled (one independent stream per GPU)")
 RDO = 0              # RDOptimization of the run (the config's, or --rdo)
+EPZS_KW = {}         # --epzs-jm10: JM >= 10's EPZS options (docs/JM_SEMANTICS.md items 46, 61, 62)
+EPZS_JM10 = dict(epzs_subpel_me=1, epzs_subpel_thres_scale=2, epzs_min_thres_scale=0, epzs_max_thres_scale=2, epzs_dual_refinement=1)
 DISP_W, DISP_H = 1920, 1080
 W, H = 1920, 1088
 SLICE_MBS = 0        # --slice-mbs: SliceMode 1 / SliceArgument (0: one slice per picture)
@@ -144,7 +146,7 @@ def cpu_one_picture(seed, search_mode, t8=0, dump=None):
     jm = load_module("jmhip", os.path.join(PKG, "jmhip.py"))
     frames = [jm.synth_frame(DISP_W, DISP_H, seed, i, bit_depth=BD) for i in range(2)]
     o = oracle_lib.OracleEncoder(W, H, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
-                                 slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO)
+                                 slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO, **EPZS_KW)
     ires, irec = o.encode(*frames[0], jm.JMH_I_SLICE, QP)
     t0 = time.perf_counter()
     o.set_reference(*irec)
@@ -165,7 +167,8 @@ def cpu_workers(n, config, search_mode, size, dump_dir=None):
         if dump_dir and k == 0:
             cmd.append(os.path.join(dump_dir, "oracle_seed0.npz"))
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
-                                      env=dict(os.environ, JMH_BENCH_SLICE_MBS=str(SLICE_MBS), JMH_BENCH_RDO=str(RDO))))
+                                      env=dict(os.environ, JMH_BENCH_SLICE_MBS=str(SLICE_MBS), JMH_BENCH_RDO=str(RDO),
+                                               JMH_BENCH_EPZS10="1" if EPZS_KW else "0")))
     out = []
     for p in procs:
         s = p.communicate()[0]
@@ -212,7 +215,7 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
     d = np.load(dump)
     frames = [jm.synth_frame(DISP_W, DISP_H, 0, i, bit_depth=BD) for i in range(2)]
     g = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, transform_8x8_mode=t8,
-                   pipeline_depth=1, slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO)
+                   pipeline_depth=1, slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO, **EPZS_KW)
     try:
         ires, irec = g.encode(*frames[0], jm.JMH_I_SLICE, QP)
         g.set_reference(*irec)
@@ -312,6 +315,8 @@ def main():
         SLICE_MBS = int(os.environ.get("JMH_BENCH_SLICE_MBS", "0"))
         w, h = (int(v) for v in sys.argv[5].split("x"))
         c = use_config(int(sys.argv[3]), (w, h), int(os.environ.get("JMH_BENCH_RDO", "0")))
+        if os.environ.get("JMH_BENCH_EPZS10") == "1":
+            EPZS_KW.update(EPZS_JM10)
         print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[4]), c["t8"], sys.argv[6] if len(sys.argv) == 7 else None),
               flush=True)
         return 0
@@ -329,6 +334,9 @@ def main():
                     help="config 5: RDOptimization (default 1; 0 = the RDO-off variant with the 8x8 transform)")
     ap.add_argument("--search-mode", type=int, default=None, choices=(0, -1, 3),
                     help="override the config's SearchMode (config 2 variants: -1 full search, 3 EPZS)")
+    ap.add_argument("--epzs-jm10", action="store_true",
+                    help="EPZS configs: JM >= 10's EPZS options (EPZSSubPelME 1, EPZSSubPelThresScale 2, "
+                         "EPZSMin/MaxThresScale 0 / 2, EPZSDualRefinement 1)")
     ap.add_argument("--slice-mbs", type=int, default=None,
                     help="SliceMode 1 with SliceArgument N macroblocks per slice (0: one slice; default: the config's)")
     # test knobs (tests/test_multistream_gpu.py): a smaller picture, a final read-back picture
@@ -353,6 +361,10 @@ def main():
     cfg = use_config(args.config, size, args.rdo)
     SLICE_MBS = max(0, cfg.get("slice_mbs", 0) if args.slice_mbs is None else args.slice_mbs)
     search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
+    if args.epzs_jm10:
+        if search_mode != 3:
+            ap.error("--epzs-jm10 applies to EPZS (SearchMode 3)")
+        EPZS_KW.update(EPZS_JM10)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -366,7 +378,7 @@ def main():
     device = local % ndev
     frames = [jm.synth_frame(DISP_W, DISP_H, rank, i, bit_depth=BD) for i in range(args.frames + 1)]
     enc = jm.Encoder(W, H, device=device, search_range=SR, search_mode=search_mode, slots=len(frames),
-                     kernel_timing=True, transform_8x8_mode=cfg["t8"], slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO)
+                     kernel_timing=True, transform_8x8_mode=cfg["t8"], slice_mbs=SLICE_MBS, bit_depth=BD, rdo=RDO, **EPZS_KW)
     stream = streams.PStream(enc, frames, QP, deblock=None if args.no_deblock else (0, 0, 0))
     dt = streams.timed_run(stream, args.steps, args.warmup, dist, on_start=enc.timing)   # on_start resets the event sums
     tm = enc.timing()                                     # event sums of the timed steps only
@@ -449,7 +461,9 @@ def main():
         "config": {
             "workload": cfg["workload"].replace("{sm}", sm_name).replace("{nf}", str(args.frames))
                         + (f", SliceMode=1 SliceArgument={SLICE_MBS} ({-(-NMB // SLICE_MBS)} slices per picture)"
-                           if SLICE_MBS else ""),
+                           if SLICE_MBS else "")
+                        + (", JM >= 10 EPZS options: EPZSSubPelME=1 EPZSSubPelThresScale=2 EPZSMinThresScale=0 "
+                           "EPZSMaxThresScale=2 EPZSDualRefinement=1" if EPZS_KW else ""),
             "global_batch": world,
             "parallelism": f"streams{world}",
             "pipeline_depth": enc.depth,

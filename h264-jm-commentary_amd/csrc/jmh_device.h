@@ -27,6 +27,8 @@
 // workgroups) and consumed by k_mb_final on the same wavefront diagonal.
 struct MbScratch {
     int16_t all_mv[8][16][2];            // best MV per block type (1..7) and 4x4 block
+    uint16_t fpc[7][16];                 // EPZS: each search's full-pel cost per block type 1..7 and
+                                         //   4x4, saturated (the neighbours' distortion of item 61)
     int32_t motion_cost[8][4];           // per block type: partition cost (16x8/8x16 block, P8x8 b8)
     int32_t best8x8;                     // P8x8 sub-mode per b8, 4 bits each
     int32_t cost8x8;
@@ -67,6 +69,9 @@ struct DevParams {
                                 // indexed at run time would put the whole DevParams in scratch)
     int t8;                     // Transform8x8Mode (High profile)
     int epzs_dual;              // EPZSDualRefinement (SearchMode 3)
+    int epzs_subpel;            // EPZSSubPelME (item 62) and its EPZSSubPelThresScale
+    int epzs_spts;
+    int epzs_mints, epzs_maxts; // EPZSMinThresScale / EPZSMaxThresScale (item 61; maxts 0: off)
     int slice_mbs;              // SliceMode 1: MBs per slice (the whole picture for one slice)
     int maxv, qpbd;             // (1 << bit depth) - 1 (Clip1), QpBdOffsetY = QpBdOffsetC = 6 (bit depth - 8)
     // plane pointers are byte addresses of uint8_t (bit depth 8) or uint16_t (9 / 10) samples:
@@ -138,6 +143,8 @@ struct TickArgs {
                                          //   (full search, SearchMode -1, or EPZS, SearchMode 3)
     int t8;                              // Transform8x8Mode: k_mb_intra8 ran, k_mb_final decides 4x4 / 8x8
     int epzs_dual;                       // EPZSDualRefinement (k_mb_epzs)
+    int epzs_subpel, epzs_spts;          // EPZSSubPelME, EPZSSubPelThresScale
+    int epzs_mints, epzs_maxts;          // EPZSMinThresScale, EPZSMaxThresScale
     int slice_mbs;                       // SliceMode 1: MBs per slice (>= 1; mbw * mbh for one slice)
     int bd;                              // bit depth: 8 (uint8_t samples) or 9 / 10 (uint16_t, High 10)
     int rdo;                             // RDOptimization 1: k_rdo_inter + k_rdo_intra + k_rdo_final on the stage
@@ -177,6 +184,8 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     for (int i = 1; i < 8; i++) d.isr |= (t.inter_search[i] != 0) << i;
     d.t8 = t.t8;
     d.epzs_dual = t.epzs_dual;
+    d.epzs_subpel = t.epzs_subpel; d.epzs_spts = t.epzs_spts;
+    d.epzs_mints = t.epzs_mints; d.epzs_maxts = t.epzs_maxts;
     d.slice_mbs = t.slice_mbs;
     d.maxv = (1 << t.bd) - 1; d.qpbd = 6 * (t.bd - 8);
     const int ps = t.bd > 8 ? 2 : 1, ls = t.W * t.H * ps, lc = ls >> 2;

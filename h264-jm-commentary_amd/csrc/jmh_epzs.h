@@ -38,6 +38,8 @@ struct EpzS {
     int8_t tref[6][6];                        //   MB origin at [1][1]; -1: none)
     int16_t mem[7][16][2];                    // spatial memory: the left MB's searches (types 1..7)
     int memok;
+    uint16_t fpc[7][16];                      // item 61: this MB's full-pel costs per type and 4x4,
+    uint16_t fpb[7][10];                      //   the neighbour MBs' at the border cells (1..9)
     alignas(4) pel hp[3][HPL];                // b, h, j of the block's [-1, w] x [-1, h] at its MV
     typename EpzTap<pel>::type b1[HPR + 5][HPR];   // unclipped horizontal taps, rows -3 .. h + 1
 };
@@ -363,6 +365,33 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
     pmy = __builtin_amdgcn_readfirstlane(pmy);
     const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
     const int med = 16 * W4 * H4 * ((d.maxv + 1) >> 8);   // medthres x pel_error_me (High 10)
+    // the stop criterion after the predictors (wave-uniform): medthres, or EPZSDetermineStopCriterion
+    // (item 61) from the same block type's full-pel costs at A, B and C (no D substitution)
+    int stop = med;
+    if (d.epzs_maxts) {
+        const int pe = (d.maxv + 1) >> 8, npx = 16 * W4 * H4, mb_x = 4 * bx4, mb_y = 4 * by4, bsx = 4 * W4;
+        auto fpn = [&](int xN, int yN, int &v) -> bool {
+            if (yN > 15 || (xN > 15 && yN >= 0)) return false;
+            if (xN >= 0 && yN >= 0) { v = s.fpc[BT - 1][(yN >> 2) * 4 + (xN >> 2)]; return true; }
+            const int c = border_cell(xN, yN);
+            if (c < 0 || s.bd.ref[c] == -2) return false;
+            v = s.fpb[BT - 1][c];
+            return true;
+        };
+        int sad = 0x7FFFFFFF, v = 0;
+        if (fpn(mb_x - 1, mb_y, v)) sad = min(sad, v);
+        if (fpn(mb_x, mb_y - 1, v)) sad = min(sad, v);
+        bool cok = true;                                   // C inside the MB but later in decoding order
+        if (mb_y > 0) {
+            if (mb_x < 8) {
+                if (mb_y == 8) { if (bsx == 16) cok = false; }
+                else if (mb_x + bsx == 8) cok = false;
+            } else if (mb_x + bsx == 16) cok = false;
+        }
+        if (cok && fpn(mb_x + bsx, mb_y - 1, v)) sad = min(sad, v);
+        sad = min(max(sad, d.epzs_mints * npx * pe), d.epzs_maxts * npx * pe);
+        stop = __builtin_amdgcn_readfirstlane((9 * max(med, sad) + 2 * med) >> 3);
+    }
     SSTAMP(1);
     // ---- full pel: predictor `lane`, then pattern rounds
     int cx, cy;
@@ -378,12 +407,12 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
         min_mcost = (int)(m0 >> 6);
         bx = __builtin_amdgcn_readlane(cx, m0 & 63);
         by = __builtin_amdgcn_readlane(cy, m0 & 63);
-        if (min_mcost >= med) {                            // pattern refinement until it stops
+        if (min_mcost >= stop) {                           // pattern refinement until it stops
             // Rounds are resolved in batches: the cost of every position within |dx| + |dy| <= 4
             // of the batch centre (one per lane, 41 lanes), then up to 2 extended-diamond rounds
             // (each moves <= 2) or 4 small-diamond rounds (<= 1) on those costs, exactly as JM
             // scans them (pattern order, strict '<', window check); then a new batch.
-            const bool sd = min_mcost < med + ((3 * med) >> 1);
+            const bool sd = min_mcost < stop + ((3 * stop) >> 1);
             const int steps = sd ? 4 : 2;
             const int dia = lane < 41 ? (int)c_dia41[lane] : 0x44;
             const int ddx = (dia & 15) - 4, ddy = (dia >> 4) - 4;
@@ -427,6 +456,10 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
         }
     }
     const int fmx = bx, fmy = by;
+    if (lane < NSUB) {                                     // item 61: this search's full-pel cost
+        const int k = (by4 + (lane >> LW4)) * 4 + bx4 + (lane & (W4 - 1));
+        s.fpc[BT - 1][k] = (uint16_t)min(min_mcost, 65535);
+    }
     if (had) min_mcost = BIGCOST;
     SSTAMP(3);
     // ---- sub-pel neighbourhood of the block at (fmx, fmy): b, h, j planes, sample [y][x] =
@@ -469,7 +502,50 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
     // ---- half then quarter pel, JM order, strict '<'
     const bool check0 = BT == 1 && fmx == 0 && fmy == 0 && had && slice_p && !d.rdo;   // !input->rdopt [J]
     int qx = 0, qy = 0;
-    if constexpr (NSUB <= 4) {
+    if (d.epzs_subpel) {
+        // EPZSSubPelBlockMotionSearch (item 62): small-diamond rounds, half pel inside F +- 2, then
+        // quarter pel inside the half-pel result +- 1; a round = the 4 points x NSUB sub-blocks
+        // (<= 64 lane tasks), one wave minimum of (cost, point) keys = strict '<' in pattern order
+        auto round = [&](int cxq, int cyq, int step, int ox, int oy, bool centre) -> unsigned {
+            const int m = lane >> LNS, sub = lane & (NSUB - 1);
+            int px = cxq, py = cyq;
+            if (!centre) {
+                px += step * (m == 1 ? -1 : m == 2 ? 1 : 0);
+                py += step * (m == 0 ? -1 : m == 3 ? 1 : 0);
+            }
+            const bool val = m < (centre ? 1 : 4) && abs(px - ox) <= step && abs(py - oy) <= step;
+            int sat = 0;
+            if (val) {
+                const int sx = 4 * (sub & (W4 - 1)), sy = 4 * (sub >> LW4);
+                sat = hp_satd(s, gb, gs, sx, sy, 64 * by4 + 4 * bx4 + 16 * sy + sx, px, py, had);
+            }
+            if constexpr (NSUB >= 2) sat += dpp<0xB1>(sat);
+            if constexpr (NSUB >= 4) sat += dpp<0x4E>(sat);
+            if constexpr (NSUB >= 8) sat += dpp<0x141>(sat);
+            if constexpr (NSUB >= 16) sat += dpp<0x140>(sat);
+            unsigned key = 0xFFFFFFFFu;
+            if (val && sub == 0)
+                key = ((unsigned)(sat + wcost(d, mvbits(4 * fmx + px - pmx) + mvbits(4 * fmy + py - pmy)) + EKOFF) << 4) | (unsigned)m;
+            return wave_min_u32(key);
+        };
+        if (had) {                                         // the centre again, with SATD
+            const unsigned k = round(0, 0, 0, 0, 0, true);
+            if ((int)(k >> 4) - EKOFF < min_mcost) min_mcost = (int)(k >> 4) - EKOFF;
+        }
+        const int subthres = d.epzs_spts * 16 * NSUB * ((d.maxv + 1) >> 8);
+        for (int stage = 0; stage < 2; stage++) {
+            const int step = stage ? 1 : 2, ox = qx, oy = qy;
+            if (stage && min_mcost < subthres) break;
+            for (;;) {
+                const unsigned k = round(qx, qy, step, ox, oy, false);
+                if (k == 0xFFFFFFFFu || (int)(k >> 4) - EKOFF >= min_mcost) break;
+                min_mcost = (int)(k >> 4) - EKOFF;
+                const int m = k & 15;
+                qx += step * (m == 1 ? -1 : m == 2 ? 1 : 0);
+                qy += step * (m == 0 ? -1 : m == 3 ? 1 : 0);
+            }
+        }
+    } else if constexpr (NSUB <= 4) {
         // blocks of up to four 4x4: the SATD of every position of the 7x7 quarter-pel grid around
         // the full-pel MV in one batch (lane task = (position, 4x4 sub-block)), then the half-pel
         // pass over the 9 even positions and the quarter-pel pass around its winner on the costs
@@ -599,6 +675,18 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
         s.mem[m - 1][k][c] = left >= 0 ? d.scr[left].all_mv[m][k][c] : 0;
     }
     if (lane == 0) s.memok = left >= 0;
+    if (d.epzs_maxts && lane < 63) {              // item 61: the neighbours' full-pel costs, cells 1..9
+        const int bt = lane / 9, cell = 1 + lane % 9;
+        const MbAvail mav = mb_avail(d, mbx, mby);
+        const bool av = cell <= 4 ? mav.T : cell == 5 ? mav.TR : mav.L;
+        int v = 0;
+        if (av) {
+            const int a = cell <= 4 ? (mby - 1) * d.mbw + mbx : cell == 5 ? (mby - 1) * d.mbw + mbx + 1 : mby * d.mbw + mbx - 1;
+            const int k = cell <= 4 ? 12 + cell - 1 : cell == 5 ? 12 : 4 * (cell - 6) + 3;
+            v = d.scr[a].fpc[bt][k];
+        }
+        s.fpb[bt][cell] = (uint16_t)v;
+    }
     // the window: MB +- off, shifted to the MB's 16x16 MVP / 4 (clamped to +-SR; horizontally a
     // multiple of 4) when off < 2 SR + 4 -- the centre most searches search around
     int wcx = 0, wcy = 0;

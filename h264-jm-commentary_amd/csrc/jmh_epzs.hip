@@ -80,6 +80,8 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
         const int m = 1 + i / 32, k = (i & 31) >> 1, c = i & 1;
         scr->all_mv[m][k][c] = s.all_mv[m][k][c];
     }
+    if (d.epzs_maxts)                                   // item 61: the full-pel costs for the neighbours
+        for (int i = lane; i < 7 * 16; i += NTE) scr->fpc[i >> 4][i & 15] = s.fpc[i >> 4][i & 15];
     if (lane < 28) scr->motion_cost[1 + lane / 4][lane & 3] = s.motion_cost[1 + lane / 4][lane & 3];
     else if (lane == 32) { scr->best8x8 = best8x8; scr->cost8x8 = cost8x8; }
     else if (lane == 48) {

@@ -437,6 +437,8 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         skipy = (za || zl) ? 0 : pcy;
     }
     MbScratch *ms = d.scr + a;
+    if (d.epzs_maxts)                                   // item 61: the full-pel costs for the neighbours
+        for (int i = lane; i < 7 * 16; i += 64) ms->fpc[i >> 4][i & 15] = s.e.fpc[i >> 4][i & 15];
     for (int i = lane; i < 7 * 32; i += 64) {
         const int m = 1 + i / 32, k = (i & 31) >> 1, c = i & 1;
         ms->all_mv[m][k][c] = s.e.all_mv[m][k][c];

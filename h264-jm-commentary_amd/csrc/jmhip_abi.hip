@@ -354,6 +354,9 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version < 0 || cfg->jm_version == 9 || cfg->jm_version > 99) return JMH_E_UNSUPPORTED_CFG;   // 0 / 8: JM 8.6, 10..: JM >= 10
     if (cfg->epzs_dual_refinement != 0 && cfg->epzs_dual_refinement != 1) return JMH_E_UNSUPPORTED_CFG;
+    if ((cfg->epzs_subpel_me != 0 && cfg->epzs_subpel_me != 1) || cfg->epzs_subpel_thres_scale < 0 ||
+        cfg->epzs_subpel_thres_scale > JMH_EPZS_SCALE_MAX || cfg->epzs_min_thres_scale < 0 || cfg->epzs_min_thres_scale > JMH_EPZS_SCALE_MAX ||
+        cfg->epzs_max_thres_scale < 0 || cfg->epzs_max_thres_scale > JMH_EPZS_SCALE_MAX) return JMH_E_INVALID_ARG;
     if (cfg->slice_mbs < 0) return JMH_E_INVALID_ARG;
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     // High 10 pictures: the EPZS wavefront (k_mb_epzs / k_mb_intra / k_mb_final on 16-bit samples)
@@ -552,6 +555,8 @@ static int issue_tick(jmh_ctx *c) {
     t.me_in_analyse = c->cfg.search_mode == 0;
     t.t8 = c->cfg.transform_8x8_mode;
     t.epzs_dual = c->cfg.epzs_dual_refinement;
+    t.epzs_subpel = c->cfg.epzs_subpel_me; t.epzs_spts = c->cfg.epzs_subpel_thres_scale;
+    t.epzs_mints = c->cfg.epzs_min_thres_scale; t.epzs_maxts = c->cfg.epzs_max_thres_scale;
     t.slice_mbs = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : c->mbw * c->mbh;
     t.bd = c->bd;
     t.ordtab = c->d_ordtab;

@@ -75,6 +75,9 @@ static const map_entry Map[] = {
     {"SliceMode", 0, OFF(slice_mode), 0, 3},
     {"SliceArgument", 0, OFF(slice_arg), 1, 1 << 20},
     {"EPZSSubPelME", 0, OFF(epzs_subpel), 0, 1},
+    {"EPZSSubPelThresScale", 0, OFF(epzs_subpel_thres), 0, JMH_EPZS_SCALE_MAX},
+    {"EPZSMinThresScale", 0, OFF(epzs_min_thres), 0, JMH_EPZS_SCALE_MAX},
+    {"EPZSMaxThresScale", 0, OFF(epzs_max_thres), 0, JMH_EPZS_SCALE_MAX},
     {NULL, 0, 0, 0, 0}};
 #undef OFF
 
@@ -198,7 +201,6 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->jm_version == 9) { snprintf(err, errlen, "JMVersion=9 not supported (8 or >= 10)"); return -1; }
     if (inp->epzs_dual > 1) { snprintf(err, errlen, "EPZSDualRefinement=%d not supported (0 or 1)", inp->epzs_dual); return -1; }
     if (inp->slice_mode > 1) { snprintf(err, errlen, "SliceMode=%d not supported (0 or 1: SliceArgument macroblocks per slice)", inp->slice_mode); return -1; }
-    if (inp->epzs_subpel) { snprintf(err, errlen, "EPZSSubPelME=1 not supported (0: SubPelBlockMotionSearch)"); return -1; }
     if (inp->adaptive_rounding) { snprintf(err, errlen, "AdaptiveRounding=1 not supported (0)"); return -1; }
     if (inp->offset_matrix_present) { snprintf(err, errlen, "OffsetMatrixPresentFlag=1 not supported (flat lists: QOffsetIntra / QOffsetInter)"); return -1; }
     if (inp->jm_version < 10 && (inp->qoff_intra >= 0 || inp->qoff_inter >= 0)) { snprintf(err, errlen, "QOffsetIntra / QOffsetInter need JMVersion >= 10"); return -1; }
@@ -247,6 +249,10 @@ void jm_fill_config(const jm_input *inp, jmh_config *cfg) {
     cfg->transform_8x8_mode = inp->transform_8x8_mode;
     cfg->jm_version = inp->jm_version;
     cfg->epzs_dual_refinement = inp->epzs_dual;
+    cfg->epzs_subpel_me = inp->epzs_subpel;
+    cfg->epzs_subpel_thres_scale = inp->epzs_subpel_thres;
+    cfg->epzs_min_thres_scale = inp->epzs_min_thres;
+    cfg->epzs_max_thres_scale = inp->epzs_max_thres;
     cfg->slice_mbs = inp->slice_mode == 1 ? inp->slice_arg : 0;
     cfg->bit_depth = inp->bit_depth_luma;
     cfg->rdo = inp->rdopt;

@@ -46,7 +46,10 @@ typedef struct jm_input {
     int  epzs_dual;            /* EPZSDualRefinement (0, 1; SearchMode 3)                      */
     int  slice_mode;           /* SliceMode (0: one slice per picture, 1: SliceArgument MBs)   */
     int  slice_arg;            /* SliceArgument (MBs per slice with SliceMode 1)               */
-    int  epzs_subpel;          /* EPZSSubPelME (must be 0)                                     */
+    int  epzs_subpel;          /* EPZSSubPelME (0, 1; SearchMode 3; JM_SEMANTICS item 62)      */
+    int  epzs_subpel_thres;    /* EPZSSubPelThresScale (item 62)                               */
+    int  epzs_min_thres;       /* EPZSMinThresScale (item 61)                                  */
+    int  epzs_max_thres;       /* EPZSMaxThresScale (item 61; 0: the fixed medthres stop)      */
     int  offset_matrix_present;/* OffsetMatrixPresentFlag (must be 0: flat lists only)         */
     int  level_idc;            /* LevelIDC                                                    */
     int  symbol_mode;          /* SymbolMode (0 = CAVLC, 1 = CABAC)                            */

@@ -18,7 +18,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 JMH_OK = 0
 JMH_E_INVALID_ARG, JMH_E_HIP, JMH_E_OOM, JMH_E_UNSUPPORTED_CFG, JMH_E_STATE, JMH_E_NO_DEVICE = -1, -2, -3, -4, -5, -6
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 12
+JMH_ABI_VERSION = 13
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -50,7 +50,9 @@ class JmhConfig(ctypes.Structure):
                 ("transform_8x8_mode", ctypes.c_int32), ("jm_version", ctypes.c_int32),
                 ("quant_offset", ctypes.c_int32 * 2), ("epzs_dual_refinement", ctypes.c_int32),
                 ("slice_mbs", ctypes.c_int32), ("bit_depth", ctypes.c_int32),
-                ("rdo", ctypes.c_int32), ("symbol_mode", ctypes.c_int32)]
+                ("rdo", ctypes.c_int32), ("symbol_mode", ctypes.c_int32),
+                ("epzs_subpel_me", ctypes.c_int32), ("epzs_subpel_thres_scale", ctypes.c_int32),
+                ("epzs_min_thres_scale", ctypes.c_int32), ("epzs_max_thres_scale", ctypes.c_int32)]
 
 
 class JmhFrameParams(ctypes.Structure):
@@ -174,7 +176,8 @@ def _ptr(a):
 def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
                 restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False,
                 pipeline_depth=0, transform_8x8_mode=0, jm_version=8, quant_offset=(682, 342), epzs_dual_refinement=0, slice_mbs=0,
-                bit_depth=8, rdo=0, symbol_mode=None):
+                bit_depth=8, rdo=0, symbol_mode=None, epzs_subpel_me=0, epzs_subpel_thres_scale=0, epzs_min_thres_scale=0,
+                epzs_max_thres_scale=0):
     """jm_version >= 10 selects the JM >= 10 quantisation rounding with the flat OffsetMatrix
     entries quant_offset = (I slices, P slices) at OffsetBits 11 (docs/JM_SEMANTICS.md item 45)."""
     cfg = JmhConfig()
@@ -193,6 +196,8 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     cfg.bit_depth = bit_depth
     cfg.rdo = rdo
     cfg.symbol_mode = (1 if rdo else 0) if symbol_mode is None else symbol_mode
+    cfg.epzs_subpel_me, cfg.epzs_subpel_thres_scale = epzs_subpel_me, epzs_subpel_thres_scale
+    cfg.epzs_min_thres_scale, cfg.epzs_max_thres_scale = epzs_min_thres_scale, epzs_max_thres_scale
     if jm_version >= 10:
         cfg.quant_offset[0], cfg.quant_offset[1] = quant_offset
     return cfg

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 12
+#define JMH_ABI_VERSION 13
 #define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
 #define JMH_QOFFSET_MAX 2047  /* jmh_config.quant_offset: OffsetBits 11 (1 << 11 = a whole step)    */
 
@@ -122,7 +122,19 @@ typedef struct jmh_config {
                                        symbol_mode 1, SearchMode 3 and transform_8x8_mode 0
                                        (docs/JM_SEMANTICS.md items 53-60)                             */
     int32_t symbol_mode;            /* SymbolMode: 0 CAVLC, 1 CABAC (the RD rate's entropy coder)     */
+    /* JM >= 10 EPZS options (SearchMode 3; docs/JM_SEMANTICS.md items 61, 62); zero keeps items 36, 39 */
+    int32_t epzs_subpel_me;         /* EPZSSubPelME: 0 SubPelBlockMotionSearch, 1 the EPZS sub-pel
+                                       pattern search (small diamond at half, then quarter pel)      */
+    int32_t epzs_subpel_thres_scale;/* EPZSSubPelThresScale, 0..JMH_EPZS_SCALE_MAX: the quarter-pel
+                                       stage is skipped below scale x block pixels x pel_error (0:
+                                       never)                                                       */
+    int32_t epzs_min_thres_scale;   /* EPZSMinThresScale, 0..JMH_EPZS_SCALE_MAX                      */
+    int32_t epzs_max_thres_scale;   /* EPZSMaxThresScale, 0..JMH_EPZS_SCALE_MAX: 0 = the fixed medthres
+                                       stop after the predictors (item 36); >= 1 the stop criterion
+                                       from the neighbours' full-pel costs clamped to [min, max] x
+                                       block pixels x pel_error (EPZSDetermineStopCriterion, item 61) */
 } jmh_config;
+#define JMH_EPZS_SCALE_MAX 63       /* keeps every threshold below 2^16 at 10 bits */
 /* per-launch HIP-event timing of the two wavefront kernels on every 8th diagonal (jmh_timing
  * analyse_ms / final_ms and their launch counts: averages per launch, sampled uniformly)     */
 #define JMH_FLAG_KERNEL_TIMING 1

@@ -322,6 +322,32 @@ static void epzs_refine(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, in
     }
 }
 
+/* EPZSDetermineStopCriterion [J] restated (item 61): the stop criterion after the predictors from
+ * the full-pel costs of the same block type's searches at the neighbours A (left), B (above), C
+ * (above right, availability as SetMotionVectorPredictor's C but without the D substitution),
+ * clamped to [minthres, maxthres], then (9 max(medthres, s) + 2 medthres) >> 3 */
+static int epzs_stop_criterion(const mbs *s, int bt, int bx4, int by4, int w4, int h4, int med) {
+    const jmo_ctx *c = s->c;
+    const int pe = (c->maxv + 1) >> 8, npx = 16 * w4 * h4, mb_x = 4 * bx4, mb_y = 4 * by4, bsx = 4 * w4;
+    const int minthres = c->cfg.epzs_min_thres_scale * npx * pe, maxthres = c->cfg.epzs_max_thres_scale * npx * pe;
+    int ia = 0, ib = 0, ic = 0;
+    int va = jmo_nb4(s, mb_x - 1, mb_y, &ia), vb = jmo_nb4(s, mb_x, mb_y - 1, &ib), vc = jmo_nb4(s, mb_x + bsx, mb_y - 1, &ic);
+    if (mb_y > 0) {                       /* C inside the MB but later in decoding order */
+        if (mb_x < 8) {
+            if (mb_y == 8) { if (bsx == 16) vc = 0; }
+            else if (mb_x + bsx == 8) vc = 0;
+        } else if (mb_x + bsx == 16) vc = 0;
+    }
+    const uint16_t *fp = c->epzs_fp + (size_t)bt * (c->W >> 2) * (c->H >> 2);
+    int sad = 0x7FFFFFFF;
+    if (va && fp[ia] < sad) sad = fp[ia];
+    if (vb && fp[ib] < sad) sad = fp[ib];
+    if (vc && fp[ic] < sad) sad = fp[ic];
+    sad = sad < minthres ? minthres : sad;
+    sad = sad > maxthres ? maxthres : sad;
+    return (9 * (med > sad ? med : sad) + 2 * med) >> 3;
+}
+
 static int epzs_search(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, int range, int *mvx, int *mvy) {
     int c0x = *mvx, c0y = *mvy;
     /* medthres: EPZSMedThresScale 1, times pel_error_me = 1 << (bit depth - 8) (High 10) */
@@ -333,14 +359,18 @@ static int epzs_search(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, int
      * earliest first on ties -- what a scan keeping best and second best ends with */
     int m2 = 0x7FFFFFFF, x2 = 0, y2 = 0;
     if (min_mcost >= med) {
+        /* the stop criterion after the predictors: medthres, or the neighbour-adaptive one */
+        int stop = med;
+        if (s->c->cfg.epzs_max_thres_scale)
+            stop = epzs_stop_criterion(s, bt, bx4, by4, jmo_blc_size[bt][0] >> 2, jmo_blc_size[bt][1] >> 2, med);
         for (int i = 1; i < n; i++) {                       /* predictors in order, strict '<' */
             if (!ok[i] || iabs(cand[i][0] - c0x) > range || iabs(cand[i][1] - c0y) > range) continue;
             int mc = epzs_cost(s, bt, bx4, by4, cand[i][0], cand[i][1], pmvx, pmvy);
             if (mc < min_mcost) { m2 = min_mcost; x2 = bx; y2 = by; min_mcost = mc; bx = cand[i][0]; by = cand[i][1]; }
             else if (mc < m2) { m2 = mc; x2 = cand[i][0]; y2 = cand[i][1]; }
         }
-        if (min_mcost >= med) {                             /* pattern refinement          */
-            int sd = min_mcost < med + ((3 * med) >> 1);
+        if (min_mcost >= stop) {                            /* pattern refinement          */
+            int sd = min_mcost < stop + ((3 * stop) >> 1);
             int pbx = bx, pby = by;
             epzs_refine(s, bt, bx4, by4, pmvx, pmvy, range, c0x, c0y, sd, &bx, &by, &min_mcost);
             if (s->c->cfg.epzs_dual_refinement && m2 != 0x7FFFFFFF && (x2 != pbx || y2 != pby)) {
@@ -401,6 +431,43 @@ static int subpel_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int 
     return min_mcost;
 }
 
+/* EPZSSubPelBlockMotionSearch [J] restated (EPZSSubPelME = 1, item 62): from the full-pel MV F, a
+ * small diamond ((0,-1) (-1,0) (1,0) (0,1), strict '<' in that order, move to the best and repeat
+ * until nothing improves) at half-pel steps inside F +- 2, then -- unless the cost is already below
+ * EPZSSubPelThresScale x block pixels x pel_error -- at quarter-pel steps inside the half-pel
+ * result +- 1.  Costs as SubPelBlockMotionSearch (item 8): MV cost + SATD (or SAD); with
+ * UseHadamard the centre is first re-evaluated with SATD (the full-pel cost was SAD-based) */
+static int epzs_subpel_search(mbs *s, int bt, int bx4, int by4, int pmvx, int pmvy, int *mvx, int *mvy, int min_mcost) {
+    static const int dia[4][2] = {{0, -1}, {-1, 0}, {1, 0}, {0, 1}};
+    jmo_ctx *c = s->c;
+    const int w4 = jmo_blc_size[bt][0] >> 2, h4 = jmo_blc_size[bt][1] >> 2;
+    const int subthres = c->cfg.epzs_subpel_thres_scale * 16 * w4 * h4 * ((c->maxv + 1) >> 8);
+    int cx = *mvx * 4, cy = *mvy * 4;
+    if (c->cfg.use_hadamard) {
+        int m = mv_cost(s, 0, cx, cy, pmvx, pmvy) + subpel_satd(s, bx4, by4, w4, h4, cx, cy);
+        if (m < min_mcost) min_mcost = m;
+    }
+    for (int stage = 0; stage < 2; stage++) {
+        const int step = stage ? 1 : 2, ox = cx, oy = cy;
+        if (stage && min_mcost < subthres) break;
+        for (;;) {
+            int moved = 0, nbx = cx, nby = cy;
+            for (int k = 0; k < 4; k++) {
+                int nx = cx + step * dia[k][0], ny = cy + step * dia[k][1];
+                if (iabs(nx - ox) > step || iabs(ny - oy) > step) continue;   /* F +- 2, then +- 1 */
+                int m = mv_cost(s, 0, nx, ny, pmvx, pmvy);
+                if (m >= min_mcost) continue;
+                m += subpel_satd(s, bx4, by4, w4, h4, nx, ny);
+                if (m < min_mcost) { min_mcost = m; nbx = nx; nby = ny; moved = 1; }
+            }
+            if (!moved) break;
+            cx = nbx; cy = nby;
+        }
+    }
+    *mvx = cx; *mvy = cy;
+    return min_mcost;
+}
+
 /* BlockMotionSearch [J] (list 0, ref 0) */
 static int block_motion_search(mbs *s, int blocktype, int bx4, int by4, int range) {
     jmo_ctx *c = s->c;
@@ -412,8 +479,16 @@ static int block_motion_search(mbs *s, int blocktype, int bx4, int by4, int rang
     if (c->cfg.search_mode == 0) min_mcost = ffs_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
     else if (c->cfg.search_mode == 3) min_mcost = epzs_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
     else min_mcost = full_search(s, blocktype, bx4, by4, pmv[0], pmv[1], range, &mvx, &mvy);
+    if (c->cfg.search_mode == 3) {               /* the neighbours' distortion of item 61 */
+        uint16_t *fp = c->epzs_fp + (size_t)blocktype * (c->W >> 2) * (c->H >> 2);
+        for (int y = 0; y < (bsy >> 2); y++)
+            for (int x = 0; x < (bsx >> 2); x++)
+                fp[((s->pix_y >> 2) + by4 + y) * (c->W >> 2) + (s->pix_x >> 2) + bx4 + x] = (uint16_t)(min_mcost < 65535 ? min_mcost : 65535);
+    }
     if (c->cfg.use_hadamard) min_mcost = BIGCOST;
-    min_mcost = subpel_search(s, blocktype, bx4, by4, pmv[0], pmv[1], &mvx, &mvy, min_mcost);
+    if (c->cfg.search_mode == 3 && c->cfg.epzs_subpel_me)
+        min_mcost = epzs_subpel_search(s, blocktype, bx4, by4, pmv[0], pmv[1], &mvx, &mvy, min_mcost);
+    else min_mcost = subpel_search(s, blocktype, bx4, by4, pmv[0], pmv[1], &mvx, &mvy, min_mcost);
     for (int y = 0; y < (bsy >> 2); y++)
         for (int x = 0; x < (bsx >> 2); x++) {
             s->all_mv[blocktype][(by4 + y) * 4 + bx4 + x][0] = (int16_t)mvx;

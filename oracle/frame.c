@@ -19,6 +19,9 @@ static int cfg_ok(const jmh_config *cfg) {
     if (cfg->jm_version < 0 || cfg->jm_version == 9 || cfg->jm_version > 99) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->epzs_dual_refinement != 0 && cfg->epzs_dual_refinement != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->slice_mbs < 0) return JMH_E_INVALID_ARG;
+    if ((cfg->epzs_subpel_me != 0 && cfg->epzs_subpel_me != 1) || cfg->epzs_subpel_thres_scale < 0 ||
+        cfg->epzs_subpel_thres_scale > JMH_EPZS_SCALE_MAX || cfg->epzs_min_thres_scale < 0 || cfg->epzs_min_thres_scale > JMH_EPZS_SCALE_MAX ||
+        cfg->epzs_max_thres_scale < 0 || cfg->epzs_max_thres_scale > JMH_EPZS_SCALE_MAX) return JMH_E_INVALID_ARG;
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     /* RDOptimization 1: CABAC rate, 4x4 transform (docs/JM_SEMANTICS.md items 53-60) */
     if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode != 1 || cfg->transform_8x8_mode != 0)) return JMH_E_UNSUPPORTED_CFG;
@@ -57,7 +60,8 @@ int jmo_create(const jmh_config *cfg, jmo_ctx **out) {
     c->res = calloc((size_t)c->mbw * c->mbh, sizeof(jmh_mb_result));
     c->blocksad = malloc(sizeof(uint16_t) * 16 * (size_t)c->npos);
     c->mbi = calloc((size_t)c->mbw * c->mbh, sizeof(jmr_mbinfo));
-    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref || !c->mbi) { jmo_destroy(c); return JMH_E_OOM; }
+    c->epzs_fp = calloc(8 * n4, sizeof(uint16_t));
+    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref || !c->mbi || !c->epzs_fp) { jmo_destroy(c); return JMH_E_OOM; }
     memset(c->refidx, -1, n4);                             /* no previous picture: no motion */
     *out = c;
     return JMH_OK;
@@ -70,7 +74,7 @@ void jmo_destroy(jmo_ctx *c) {
     free(c->refY); free(c->refU); free(c->refV);
     free(c->recY); free(c->recU); free(c->recV);
     free(c->qpel); free(c->mv); free(c->refidx); free(c->ipred); free(c->mbintra);
-    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref); free(c->mbi);
+    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref); free(c->mbi); free(c->epzs_fp);
     free(c);
 }
 

@@ -69,6 +69,9 @@ struct jmo_ctx {
     int16_t *tmv;                    /* [(H/4)*(W/4)][2], snapshot of mv at picture start        */
     int8_t *tref;                    /* [(H/4)*(W/4)], -1: intra / no previous picture          */
     int16_t mem_mv[8][16][2];        /* all_mv of the MB to the left (valid when mbx > 0)       */
+    uint16_t *epzs_fp;               /* [8][(H/4)*(W/4)]: each search's full-pel cost (saturated at
+                                        65535) per block type and 4x4: the neighbours' distortion of
+                                        EPZSDetermineStopCriterion (item 61)                     */
     /* RDOptimization = 1: the slice's CABAC coding state (contexts + codIRange, jmh_cabac_rate.h)
        and what every coded macroblock leaves for its neighbours' context selection */
     uint8_t cab_st[JMR_NCTX];

@@ -179,7 +179,7 @@ def test_closed_loop_epzs_dual(extra):
 def test_epzs_knob_ranges():
     r = run("-p", "SearchMode=3", "-p", "EPZSDualRefinement=2")
     assert r.returncode != 0 and "EPZSDualRefinement" in r.stderr
-    r = run("-p", "SearchMode=3", "-p", "EPZSSubPelME=1")
+    r = run("-p", "SearchMode=3", "-p", "EPZSSubPelME=2")
     assert r.returncode != 0 and "EPZSSubPelME" in r.stderr
 
 
