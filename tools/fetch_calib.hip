@@ -17,12 +17,12 @@ __global__ void k_read(const uint8_t *__restrict__ p, size_t n, uint32_t *__rest
     for (size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * BYTES; i < n; i += stride) {
         if constexpr (BYTES == 16) {
             const uint4 v = *reinterpret_cast<const uint4 *>(p + i);
-            acc ^= v.x ^ v.y ^ v.z ^ v.w;
-        } else if constexpr (BYTES == 4) acc ^= *reinterpret_cast<const uint32_t *>(p + i);
-        else if constexpr (BYTES == 2) acc ^= *reinterpret_cast<const uint16_t *>(p + i);
-        else acc ^= p[i];
+            acc += v.x + v.y + v.z + v.w;
+        } else if constexpr (BYTES == 4) acc += *reinterpret_cast<const uint32_t *>(p + i);
+        else if constexpr (BYTES == 2) acc += *reinterpret_cast<const uint16_t *>(p + i);
+        else acc += p[i];
     }
-    if (acc == 0x9E3779B9u) out[0] = acc;   // keeps the loads; practically never taken
+    if (acc == 0x7FFFFFFEu) out[0] = acc;   // keeps the loads (a sum the data never gives)
 }
 __global__ void k_evict(uint32_t *__restrict__ p, size_t n) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = (uint32_t)i;
