@@ -94,16 +94,17 @@ JMR_FN int jmr_renorm_steps(uint32_t r) { return __builtin_clz(r) - 23; }   /* r
 #endif
 
 JMR_FN void jmr_bin(jmr_eng *e, int ctx, int bin) {   /* 9.3.4.2 */
+    /* branch-free: both table reads depend only on the state, the outcome selects (lanes of a
+       wave coding different bins stay converged) */
     const uint32_t v = e->st[ctx];
-    int s = (int)(v >> 1), mps = (int)(v & 1);
+    const int s = (int)(v >> 1), mps = (int)(v & 1);
     const uint32_t lps = JMR_LPS(s, (e->range >> 6) & 3);
-    uint32_t r = e->range - lps;
-    if (bin != mps) {
-        r = lps;
-        if (s == 0) mps ^= 1;
-        s = JMR_TLPS(s);
-    } else if (s < 62) s++;
-    e->st[ctx] = (uint8_t)((s << 1) | mps);
+    const int tl = JMR_TLPS(s);
+    const int lpsbin = bin != mps;
+    const uint32_t r = lpsbin ? lps : e->range - lps;
+    const int ns = lpsbin ? tl : (s < 62 ? s + 1 : s);
+    const int nm = mps ^ (lpsbin & (s == 0));
+    e->st[ctx] = (uint8_t)((ns << 1) | nm);
     const int n = jmr_renorm_steps(r);
     e->range = r << n;
     e->bits += n;
@@ -172,9 +173,11 @@ JMR_FN int jmr_cbf_luma_term(const jmr_mbinfo *n, int cur_intra, int x4, int y4)
 /* residual_block_cabac (7.3.5.3.3, 9.3.3.1.3): coef[0..n) in scan order, cat 0..4 (ctxBlockCat)
    or 5 (luma 8x8, no coded_block_flag: cbf_inc < 0); returns the coded_block_flag */
 JMR_FN int jmr_residual(jmr_eng *e, const int16_t *coef, int n, int cat, int cbf_inc) {
-    int last = -1;
+    /* the significance map as a bit mask first: the bins then read no coefficient but the levels */
+    uint64_t nzm = 0;
     for (int i = 0; i < n; i++)
-        if (coef[i]) last = i;
+        if (coef[i]) nzm |= (uint64_t)1 << i;
+    const int last = nzm ? 63 - __builtin_clzll(nzm) : -1;
     const int cbf = last >= 0;
     if (cbf_inc >= 0) jmr_bin(e, JMR_CTX(85) + 4 * cat + cbf_inc, cbf);
     if (!cbf) return 0;
@@ -185,16 +188,18 @@ JMR_FN int jmr_residual(jmr_eng *e, const int16_t *coef, int n, int cat, int cbf
     for (int i = 0; i < n - 1; i++) {                 /* significance map */
         const int si = cat == 5 ? jmr_sig8x8_inc[i] : cat == 3 ? (i < 2 ? i : 2) : i;
         const int li = cat == 5 ? jmr_last8x8_inc[i] : cat == 3 ? (i < 2 ? i : 2) : i;
-        jmr_bin(e, sig_base + si, coef[i] != 0);
-        if (coef[i]) {
+        const int sig = (int)((nzm >> i) & 1);
+        jmr_bin(e, sig_base + si, sig);
+        if (sig) {
             jmr_bin(e, last_base + li, i == last);
             if (i == last) break;
         }
     }
     int eq1 = 0, gt1 = 0;
     const int gmax = 4 - (cat == 3);
-    for (int i = last; i >= 0; i--) {                 /* levels, reverse scan order */
-        if (!coef[i]) continue;
+    for (uint64_t m = nzm; m;) {                      /* levels, reverse scan order */
+        const int i = 63 - __builtin_clzll(m);
+        m &= ~((uint64_t)1 << i);
         const int a = coef[i] < 0 ? -coef[i] : coef[i], v = a - 1;
         jmr_bin(e, abs_base + (gt1 ? 0 : (1 + eq1 < 4 ? 1 + eq1 : 4)), v > 0);
         if (v > 0) {
