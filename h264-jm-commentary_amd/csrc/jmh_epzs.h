@@ -11,8 +11,16 @@ __device__ __forceinline__ int wcost(const DevParams &d, int bits) {
 
 #define NTE 64                                // one wave per macroblock
 #define EOFF_L 52                             // LDS window margin around the MB (or 2 SR + 4 if less)
-#define EW_MAX (16 + 2 * EOFF_L)              // 120
-#define EST EW_MAX                            // window row stride
+#ifndef EOFF_L16
+#define EOFF_L16 40                           // ... for 16-bit samples: 30.4 KB k_rdo_inter, five MBs per CU (A/B: profiles/r5r_window_ab.txt)
+#endif
+// window geometry per sample type: margin, rows (= row stride) of the LDS window
+template <class pel>
+struct EGeo {
+    static constexpr int off = sizeof(pel) == 2 ? EOFF_L16 : EOFF_L;
+    static constexpr int ew = 16 + 2 * off;
+    static_assert(off % 2 == 0, "window rows must be whole dwords");
+};
 #define NPRED 41                              // EPZS predictor slots (oracle epzs_predictors)
 #define HPS 20                                // sub-pel plane stride (>= 18 + 2 alignment slack)
 #define HPR 18                                // sub-pel plane rows (block + 1 on each side)
@@ -27,7 +35,7 @@ template <class pel> struct EpzTap { typedef int16_t type; };   // unclipped 6-t
 template <> struct EpzTap<uint16_t> { typedef int32_t type; };
 template <class pel>
 struct EpzS {
-    alignas(4) pel g[EW_MAX * EST];           // the window
+    alignas(4) pel g[EGeo<pel>::ew * EGeo<pel>::ew];           // the window
     alignas(4) pel gn[GNR * GNS + 8];         // a search's integer-sample neighbourhood read from global
     alignas(8) pel org[256];
     Border bd;
@@ -192,15 +200,15 @@ __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWi
     uint32_t sad = 0;
     if constexpr (sizeof(pel) == 2) {
         constexpr int ND = 2 * W4;            // dwords of a block row
-        if (gx >= 0 && gx + 4 * W4 + 4 <= EST && gy >= 0 && gy + H <= EW_MAX) {
-            const int a = gy * EST + gx;
+        if (gx >= 0 && gx + 4 * W4 + 4 <= EGeo<pel>::ew && gy >= 0 && gy + H <= EGeo<pel>::ew) {
+            const int a = gy * EGeo<pel>::ew + gx;
             const uint32_t sel = (uint32_t)(a & 1) * 2;
             const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~1));
 #pragma unroll
             for (int r = 0; r < H; r++) {
                 uint32_t w[ND + 1];
 #pragma unroll
-                for (int q = 0; q <= ND; q++) w[q] = base[r * (EST / 2) + q];
+                for (int q = 0; q <= ND; q++) w[q] = base[r * (EGeo<pel>::ew / 2) + q];
 #pragma unroll
                 for (int q = 0; q < ND; q++) sad = __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), org[r * 8 + q], sad);
             }
@@ -215,15 +223,15 @@ __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWi
         }
         return sad;
     }
-    if (gx >= 0 && gx + 4 * W4 + 4 <= EST && gy >= 0 && gy + H <= EW_MAX) {   // inside the window
-        const int a = gy * EST + gx;
+    if (gx >= 0 && gx + 4 * W4 + 4 <= EGeo<pel>::ew && gy >= 0 && gy + H <= EGeo<pel>::ew) {   // inside the window
+        const int a = gy * EGeo<pel>::ew + gx;
         const uint32_t sel = (uint32_t)(a & 3);
         const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~3));
 #pragma unroll
         for (int r = 0; r < H; r++) {
             uint32_t w[W4 + 1];
 #pragma unroll
-            for (int q = 0; q <= W4; q++) w[q] = base[r * (EST / 4) + q];
+            for (int q = 0; q <= W4; q++) w[q] = base[r * (EGeo<pel>::ew / 4) + q];
 #pragma unroll
             for (int q = 0; q < W4; q++) sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), org[r * 4 + q], sad);
         }
@@ -470,8 +478,8 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
     // [-GNX, PW + GNX) x [-GNY, PH + GNY) leaves it, the neighbourhood plane read from global
     const pel *gb;
     int gs;
-    if (gx0 - GNX >= 0 && gx0 + PW + GNX <= EST && gy0 - GNY >= 0 && gy0 + PH + GNY <= EW_MAX) {   // wave-uniform
-        gb = s.g + gy0 * EST + gx0; gs = EST;
+    if (gx0 - GNX >= 0 && gx0 + PW + GNX <= EGeo<pel>::ew && gy0 - GNY >= 0 && gy0 + PH + GNY <= EGeo<pel>::ew) {   // wave-uniform
+        gb = s.g + gy0 * EGeo<pel>::ew + gx0; gs = EGeo<pel>::ew;
     } else {
         for (int i = lane; i < (PH + 2 * GNY) * GNS; i += NTE) {
             const int y = i / GNS, x = i - y * GNS;
@@ -651,7 +659,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
 template <class pel>
 __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> &s, int mbx, int mby, int lane) {
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, sr = d.sr;
-    const int off = min(2 * sr + 4, EOFF_L), wdim = 16 + 2 * off;
+    const int off = min(2 * sr + 4, EGeo<pel>::off), wdim = 16 + 2 * off;
     const int X0 = 4 * mbx, Y0 = 4 * mby, left = mb_avail(d, mbx, mby).L ? mby * d.mbw + mbx - 1 : -1;
     const pel *orgY = spl<pel>(d.orgY), *refY = spl<pel>(d.refY);
     if constexpr (sizeof(pel) == 1)
@@ -701,7 +709,7 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
     if constexpr (sizeof(pel) == 2) {
         // 16-bit samples: two per dword; with off % 4 == 0 a dword is aligned in the picture and
         // wholly inside or outside it (as for bytes), else per-sample clamped reads
-        constexpr int ND2 = EST / 2, NB = 16;
+        constexpr int ND2 = EGeo<pel>::ew / 2, NB = 16;
         const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND2;
         if ((off & 3) == 0) {
             for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
@@ -721,7 +729,7 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
                     if (x0 < 0) w = (w & 0xFFFFu) * 0x10001u;
                     else if (x0 >= W) w = (w >> 16) * 0x10001u;
                     if (2 * j >= wdim) w = 0;
-                    *reinterpret_cast<uint32_t *>(s.g + y * EST + 2 * j) = w;
+                    *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 2 * j) = w;
                 }
             }
         } else {
@@ -731,14 +739,14 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
                 uint32_t v = 0;
                 for (int q = 0; q < 2; q++)
                     if (2 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (16 * q);
-                *reinterpret_cast<uint32_t *>(s.g + y * EST + 2 * j) = v;
+                *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 2 * j) = v;
             }
         }
     } else {
         // with off % 4 == 0 the window's dwords are aligned in the picture (pix_x % 16 == 0, wcx %
         // 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an outside
         // dword is the replicated edge sample.  Two batches of 32 loads per lane in flight.
-        constexpr int ND4 = EST / 4, NB = 32;
+        constexpr int ND4 = EGeo<pel>::ew / 4, NB = 32;
         const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND4;
         if ((off & 3) == 0) {
             for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
@@ -758,7 +766,7 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
                     if (x0 < 0) w = (w & 0xFFu) * 0x01010101u;              // left of the picture
                     else if (x0 >= W) w = (w >> 24) * 0x01010101u;          // right of it
                     if (4 * j >= wdim) w = 0;
-                    *reinterpret_cast<uint32_t *>(s.g + y * EST + 4 * j) = w;
+                    *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 4 * j) = w;
                 }
             }
         } else {   // odd SearchRange: two aligned global dwords + v_alignbyte, clamped bytes at the edges
@@ -774,7 +782,7 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
                     for (int q = 0; q < 4; q++)
                         if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
                 }
-                *reinterpret_cast<uint32_t *>(s.g + y * EST + 4 * j) = v;
+                *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 4 * j) = v;
             }
         }
     }

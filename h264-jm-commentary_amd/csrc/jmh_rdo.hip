@@ -47,11 +47,11 @@ __device__ __forceinline__ double rd_cost(int dist, int bits, double lambda) {
 // UMV-clamped reference, so the values are those of qpel_direct), else from the picture in HBM
 template <class pel>
 __device__ __forceinline__ int qpel_mb(const DevParams &d, const EpzS<pel> &e, const EWin<pel> &wn, int X, int Y) {
-    const int x = X >> 2, y = Y >> 2, wdim = 16 + 2 * min(2 * d.sr + 4, EOFF_L);
-    const bool in = x - 2 >= wn.wx0 && x + 3 < wn.wx0 + EST && y - 2 >= wn.wy0 && y + 3 < wn.wy0 + wdim;
+    const int x = X >> 2, y = Y >> 2, wdim = 16 + 2 * min(2 * d.sr + 4, EGeo<pel>::off);
+    const bool in = x - 2 >= wn.wx0 && x + 3 < wn.wx0 + EGeo<pel>::ew && y - 2 >= wn.wy0 && y + 3 < wn.wy0 + wdim;
     if (__all(in)) {
-        const pel *g = e.g + (size_t)(0 - wn.wy0) * EST - wn.wx0;
-        return qpel_from([&](int xx, int yy) { return (int)g[yy * EST + xx]; }, X, Y, d.maxv);
+        const pel *g = e.g + (size_t)(0 - wn.wy0) * EGeo<pel>::ew - wn.wx0;
+        return qpel_from([&](int xx, int yy) { return (int)g[yy * EGeo<pel>::ew + xx]; }, X, Y, d.maxv);
     }
     return qpel_direct(spl<pel>(d.refY), d.W, d.H, X, Y, d.maxv);
 }
@@ -921,18 +921,27 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     }
 }
 
-hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st) {
+// one tick: k_rdo_inter and k_rdo_intra (on the side stream when given: fork / join events), then
+// k_rdo_final
+hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st, hipStream_t side, hipEvent_t fork, hipEvent_t join) {
     const int tot = t.pre[t.npic];
     if (!tot) return hipSuccess;
     const int nP = t.pre[t.nP];
+    hipError_t err;
+    hipStream_t ist = side ? side : st;
+    if (side && nP) {
+        if ((err = hipEventRecord(fork, st)) != hipSuccess || (err = hipStreamWaitEvent(side, fork, 0)) != hipSuccess) return err;
+    } else ist = st;
     if (nP) {
         if (t.bd > 8) hipLaunchKernelGGL(k_rdo_inter<uint16_t>, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
         else hipLaunchKernelGGL(k_rdo_inter<uint8_t>, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
     }
-    if (t.bd > 8) hipLaunchKernelGGL(k_rdo_intra<uint16_t>, dim3(xcd_grid(tot)), dim3(NTE), 0, st, t);
-    else hipLaunchKernelGGL(k_rdo_intra<uint8_t>, dim3(xcd_grid(tot)), dim3(NTE), 0, st, t);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return err;
+    if (t.bd > 8) hipLaunchKernelGGL(k_rdo_intra<uint16_t>, dim3(xcd_grid(tot)), dim3(NTE), 0, ist, t);
+    else hipLaunchKernelGGL(k_rdo_intra<uint8_t>, dim3(xcd_grid(tot)), dim3(NTE), 0, ist, t);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+    if (ist != st) {
+        if ((err = hipEventRecord(join, ist)) != hipSuccess || (err = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return err;
+    }
     if (t.bd > 8) hipLaunchKernelGGL(k_rdo_final<uint16_t>, dim3(xcd_grid(tot)), dim3(NT), 0, st, t);
     else hipLaunchKernelGGL(k_rdo_final<uint8_t>, dim3(xcd_grid(tot)), dim3(NT), 0, st, t);
     return hipGetLastError();

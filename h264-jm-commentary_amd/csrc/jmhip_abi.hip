@@ -29,7 +29,7 @@ hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st);
-hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st, hipStream_t side, hipEvent_t fork, hipEvent_t join);
 size_t jmh_rdo_scratch_bytes();
 hipError_t jmh_launch_block_search_u16(int n, const jmh_block_search *reqs, jmh_block_result *out, const uint16_t *cur, const uint16_t *ref,
                                        int W, int H, int had, int bit_depth, hipStream_t st);
@@ -139,6 +139,8 @@ struct jmh_ctx {
     int dev;
     hipStream_t st;                      // the wavefront ticks (and source uploads)
     hipStream_t cst;                     // readback of finished pictures, overlapping later ticks
+    hipStream_t sst = nullptr;           // RDO on: k_rdo_intra beside k_rdo_inter (JMH_RDO_SIDE=0: off)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int W, H, Wc, Hc, mbw, mbh, sr, side, npos, qstride, qplane, nd;
     size_t fsize, n4, nmb;               // bytes of one 4:2:0 picture (Y then U then V)
     uint8_t *d_ref, *d_qpel, *d_slots;   // explicit reference (set_reference), a1 seam, slots
@@ -327,6 +329,7 @@ void jmh_destroy(jmh_ctx *c) {
     (void)hipSetDevice(c->dev);
     if (c->st) (void)hipStreamSynchronize(c->st);
     if (c->cst) (void)hipStreamSynchronize(c->cst);
+    if (c->sst) (void)hipStreamSynchronize(c->sst);
     for (PicBuf &b : c->ring) free_entry(b);
     void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab, c->d_scur16,
                         c->d_sref16, c->d_sched, c->d_soff, c->d_rscr};
@@ -338,6 +341,9 @@ void jmh_destroy(jmh_ctx *c) {
     ring_free(c->ring_fin);
     if (c->st) (void)hipStreamDestroy(c->st);
     if (c->cst) (void)hipStreamDestroy(c->cst);
+    if (c->sst) (void)hipStreamDestroy(c->sst);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -398,6 +404,14 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     {
         if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        // RDO on: the intra role on a side stream, concurrent with the inter role (the inter
+        // workgroups' LDS leaves room for intra ones beside them); joined before k_rdo_final
+        const char *side = getenv("JMH_RDO_SIDE");
+        if (cfg->rdo && !(side && atoi(side) == 0)) {
+            if (hipStreamCreateWithFlags(&c->sst, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+        }
         ALLOC(c->d_ref, c->fsize);
         ALLOC(c->d_qpel, (size_t)16 * c->qplane);
         ALLOC(c->d_slots, c->fsize * c->nslots);
@@ -602,7 +616,7 @@ static int issue_tick(jmh_ctx *c) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
         if (kt) HCHK(ring_begin(c->ring_an, c->st));
         if (t.rdo) {                                    // RDOptimization 1: analyse + final
-            HCHK(jmh_launch_rdo(t, c->st));
+            HCHK(jmh_launch_rdo(t, c->st, c->sst, c->ev_fork, c->ev_join));
         } else if (t.me_in_analyse) {                   // FFS: motion search + intra in k_mb_analyse
             HCHK(jmh_launch_analyse(t, c->st));
             if (t.t8) HCHK(jmh_launch_intra8(t, c->st));   // Intra8x8 decision (High profile)

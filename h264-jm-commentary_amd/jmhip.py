@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "csrc", "libjmhip.so")
+LIB_PATH = os.environ.get("JMH_LIB_PATH") or os.path.join(HERE, "csrc", "libjmhip.so")   # override: A/B builds
 HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 
 JMH_OK = 0
