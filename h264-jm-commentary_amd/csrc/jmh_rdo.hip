@@ -75,10 +75,19 @@ struct RdoChroma {                // one chroma candidate (an inter candidate's 
     pel rec[2][64];
     int32_t cbpc, dist;
 };
+// the CABAC rate of an intra macroblock candidate, coded by k_rdo_intra (beside k_rdo_inter)
+struct RdoRate {
+    int32_t bits;
+    uint32_t range;               // codIRange after it
+    jmr_mbinfo out;               // what it leaves for the neighbours' context selection
+    int16_t mvw[16][2];           // jmr_mb's work buffer
+    alignas(4) uint8_t ctx[JMR_NCTX];   // the contexts after it
+};
 template <class pel>
 struct RdoScr {
     RdoLuma<pel> L[RD_NL];
     RdoChroma<pel> C[9];          // [0..4]: chroma of L[0..4]; [5 + m]: intra chroma mode m
+    RdoRate R[8];                 // [m]: I16MB with chroma mode m, [4 + m]: I4MB (available modes only)
 };
 size_t jmh_rdo_scratch_bytes() { return sizeof(RdoScr<uint16_t>); }
 
@@ -664,6 +673,48 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
     if (lane == 0) { L[6].cbp = i4cbp; L[6].cbp_blk = i4blk; L[6].dist = dist; L[6].i16mode = 0; }
     if (lane < 32) L[6].mv[lane >> 1][lane & 1] = 0;
     PSTAMP(56);
+    // ---- RDCost_for_macroblocks' rate of the eight intra candidates (I16MB / I4MB x the chroma
+    //      modes), here beside k_rdo_inter rather than on k_rdo_final's critical path: lane k < 8
+    //      codes candidate k on its own copy of the slice state (the Intra4x4 copies, free now),
+    //      reading the candidates this wave wrote to the tick scratch
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    for (int k = lane; k < 8 * (JMR_NCTX / 4); k += 64) {
+        const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
+        reinterpret_cast<uint32_t *>(s.stc[m])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
+    }
+    wave_lds_sync();
+    const int cm = lane & 3;
+    const bool cok = cm == 0 || (cm == 1 ? avL : cm == 2 ? avT : avT && avL && avTL);
+    if (lane < 8 && cok) {
+        const RdoLuma<pel> &Lc = L[lane < 4 ? 5 : 6];
+        const RdoChroma<pel> &C = scr->C[5 + cm];
+        RdoRate &R = scr->R[lane];
+        jmr_cand r;
+        r.mb_type = lane < 4 ? JMH_I16MB : JMH_I4MB;
+        r.cbp = Lc.cbp | C.cbpc << 4;
+        r.i16mode = Lc.i16mode;
+        r.cmode = cm;
+        r.t8 = 0;
+        for (int q = 0; q < 4; q++) r.b8mode[q] = 0;
+        r.ipm = Lc.ipm;
+        r.mvd = Lc.mvd;
+        r.luma = Lc.luma;
+        r.luma_dc = Lc.luma_dc;
+        r.cdc = C.dc;
+        r.cac = C.ac;
+        r.mvw = R.mvw;
+        jmr_eng en = {s.stc[lane], rg0, 0};
+        jmr_mb(&en, A, B, &r, d.slice_type == JMH_P_SLICE, 0, &R.out);
+        R.bits = en.bits;
+        R.range = en.range;
+    }
+    wave_lds_sync();
+    for (int k = lane; k < 8 * (JMR_NCTX / 4); k += 64) {
+        const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
+        reinterpret_cast<uint32_t *>(scr->R[m].ctx)[j] = reinterpret_cast<const uint32_t *>(s.stc[m])[j];
+    }
+    PSTAMP(61);
 }
 
 template <class pel>
@@ -671,6 +722,9 @@ __global__ __launch_bounds__(NTE) void k_rdo_inter(const TickArgs t) {
     __shared__ RdoInterS<pel> s;
     const int nP = t.pre[t.nP], m = xcd_block(blockIdx.x, nP);
     if (m >= nP) return;                                // padding block (whole workgroup)
+    // the inter role is the tick's long pole; the intra role's waves sharing its SIMDs (side
+    // stream) take the issue slots it leaves
+    __builtin_amdgcn_s_setprio(3);
     const unsigned long long bt0 = t.bprof ? wall_clock64() : 0;   // debug (JMH_BLOCK_PROF): role 4
     const int e = tick_entry(t, m);
     const DevParams d = tick_params(t, e);
@@ -718,8 +772,8 @@ struct RdoFinC {                  // of a chroma candidate (RdoChroma's first 27
 };
 template <class pel>
 struct RdoFinS {
-    RdoFinL fl[RD_NL];            // the candidates' syntax in LDS: the serial CABAC loops read it bin by bin
-    RdoFinC fc[9];
+    RdoFinL fl[5];                // the inter candidates' syntax in LDS: the serial CABAC loops read it bin by bin
+    RdoFinC fc[5];
     int16_t mvw[RD_NCAND][16][2];   // jmr_mb's work buffers
     alignas(4) uint8_t st0[JMR_NCTX];
     alignas(4) uint8_t stc[RD_NCAND][JMR_NCTX];
@@ -771,12 +825,15 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
             }
         }
         s.ncand = n;
-        // lanes of one wave run the same syntax (divergent lanes in different code cost the sum):
-        // wave 0 the Intra4x4 candidates, 1 the Intra16x16 ones, 2 skip / 16x16 / 16x8 / 8x16, 3 P8x8
+        // the inter candidates' rates, one per wave (lanes of a wave in different syntax would cost
+        // the sum of their paths): wave 0 16x16, 1 16x8, 2 8x16 and P_Skip, 3 P8x8; the intra
+        // candidates' rates come from k_rdo_intra (RdoScr.R)
         int fill[4] = {0, 0, 0, 0};
         for (int w = 0; w < 16; w++) s.kof[w >> 2][w & 3] = -1;
         for (int k = 0; k < n; k++) {
-            const int i = s.ci[k], w = i == 6 ? 0 : i == 5 ? 1 : i == 4 ? 3 : 2;
+            const int i = s.ci[k];
+            if (i >= 5) continue;
+            const int w = i == 1 ? 0 : i == 2 ? 1 : i == 4 ? 3 : 2;
             s.kof[w][fill[w]++] = (int8_t)k;
         }
     }
@@ -784,42 +841,55 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     const jmr_mbinfo *A = s.hasA ? &s.nbA : nullptr, *B = s.hasB ? &s.nbB : nullptr;
     // ---- one lane per candidate: its rate on its own copy of the coding state (lanes 0..3 of the
     //      four waves, grouped by macroblock type: kof)
-    for (int i = tid; i < s.ncand * (JMR_NCTX / 4); i += NT) {
+    for (int i = tid; i < s.ncand * (JMR_NCTX / 4); i += NT) {   // the inter candidates' state copies
         const int k = i / (JMR_NCTX / 4), j = i - k * (JMR_NCTX / 4);
-        reinterpret_cast<uint32_t *>(s.stc[k])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
+        if (s.ci[k] < 5) reinterpret_cast<uint32_t *>(s.stc[k])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
     }
     {
         constexpr int nl = 672 / 4, nc = (int)sizeof(RdoFinC) / 4;
         static_assert(offsetof(RdoLuma<pel>, ipm) > 672 && offsetof(RdoFinL, ipm) == 672, "RdoFinL layout");
-        for (int i = tid; i < RD_NL * (nl + 4); i += NT) {
+        for (int i = tid; i < 5 * (nl + 4); i += NT) {
             const int k = i / (nl + 4), j = i - k * (nl + 4);
             const uint32_t *src = reinterpret_cast<const uint32_t *>(&scr->L[k]);
             reinterpret_cast<uint32_t *>(&s.fl[k])[j] = j < nl ? src[j] : reinterpret_cast<const uint32_t *>(scr->L[k].ipm)[j - nl];
         }
-        for (int i = tid; i < 9 * nc; i += NT) {
+        for (int i = tid; i < 5 * nc; i += NT) {
             const int k = i / nc, j = i - k * nc;
             reinterpret_cast<uint32_t *>(&s.fc[k])[j] = reinterpret_cast<const uint32_t *>(&scr->C[k])[j];
+        }
+        // the intra candidates: their rates as k_rdo_intra coded them
+        const int nw = (int)sizeof(jmr_mbinfo) / 4;
+        for (int i = tid; i < s.ncand * (nw + 2); i += NT) {
+            const int k = i / (nw + 2), j = i - k * (nw + 2), ci = s.ci[k];
+            if (ci < 5) continue;
+            const RdoRate &R = scr->R[(ci == 5 ? 0 : 4) + s.ccm[k]];
+            if (j < nw) reinterpret_cast<uint32_t *>(&s.out[k])[j] = reinterpret_cast<const uint32_t *>(&R.out)[j];
+            else if (j == nw) s.rgo[k] = R.range;
+            else {
+                s.bits[k] = R.bits;
+                s.rd[k] = rd_cost(scr->L[ci].dist + scr->C[5 + s.ccm[k]].dist, R.bits, d.lambda_rd);
+            }
         }
     }
     __syncthreads();
     PSTAMP(58);
     const int kc = (tid & 63) < 4 ? s.kof[tid >> 6][tid & 3] : -1;
     if (kc >= 0) {
-        const int i = s.ci[kc], cm = s.ccm[kc];
+        const int i = s.ci[kc];
         const RdoLuma<pel> &L = scr->L[i];
-        const RdoChroma<pel> &C = scr->C[i >= 5 ? 5 + cm : i];
+        const RdoChroma<pel> &C = scr->C[i];
         jmr_eng en = {s.stc[kc], s.rg0, 0};
         if (i == 0) jmr_skip(&en, A, B, &s.out[kc]);
         else {
             jmr_cand r;
-            r.mb_type = i == 4 ? JMH_P8x8 : i == 5 ? JMH_I16MB : i == 6 ? JMH_I4MB : i;
+            r.mb_type = i == 4 ? JMH_P8x8 : i;
             r.cbp = L.cbp | C.cbpc << 4;
             r.i16mode = L.i16mode;
-            r.cmode = i >= 5 ? cm : 0;
+            r.cmode = 0;
             r.t8 = 0;
             for (int q = 0; q < 4; q++) r.b8mode[q] = L.b8mode[q];
             const RdoFinL &FL = s.fl[i];
-            const RdoFinC &FC = s.fc[i >= 5 ? 5 + cm : i];
+            const RdoFinC &FC = s.fc[i];
             r.ipm = FL.ipm;
             r.mvd = FL.mvd;
             r.luma = FL.luma;
@@ -898,7 +968,8 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     {
         const int slice = a / d.slice_mbs;
         uint32_t *dst = reinterpret_cast<uint32_t *>(d.rp->cab + (size_t)slice * JMR_NCTX);
-        if (tid < JMR_NCTX / 4) dst[tid] = reinterpret_cast<const uint32_t *>(s.stc[w])[tid];
+        const uint8_t *win_ctx = is_intra ? scr->R[(bi == 5 ? 0 : 4) + bcm].ctx : s.stc[w];
+        if (tid < JMR_NCTX / 4) dst[tid] = reinterpret_cast<const uint32_t *>(win_ctx)[tid];
         const int nw = (int)sizeof(jmr_mbinfo) / 4;
         if (tid >= 128 && tid < 128 + nw)
             reinterpret_cast<uint32_t *>(d.rp->mbi + a)[tid - 128] = reinterpret_cast<const uint32_t *>(&s.out[w])[tid - 128];
