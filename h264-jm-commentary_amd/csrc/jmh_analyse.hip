@@ -53,7 +53,6 @@ struct IntraS {
     alignas(4) pel rec[256];
     Border bd;
     IntraNb<pel> nb;
-    int i4P[2][16];
     int8_t ipred_cur[16];
     int part[2][4];                           // per I4 wave: cost, cbp, blk mask
 };
@@ -402,6 +401,14 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
 // waves through LDS; else lane j of every wave computes search j's, then readlane), the full-pel
 // argmin over all positions by every thread (EV fills bk[] from pmx/pmy), per-wave minima -> LDS
 // -> barrier, sub-pel search j on wave j (+ forwarded MVPs), barrier.
+// the wave of a stage's search j: waves 0, 1, 4, 5 (SIMDs 0 and 1) first, so that the Intra4x4
+// waves 6 and 7 (SIMDs 2 and 3) share their SIMDs with no sub-pel wave of the workgroup in stages
+// of up to four searches
+#ifndef JMH_SWMAP
+#define JMH_SWMAP 1
+#endif
+__device__ __forceinline__ constexpr int search_wave(int j) { return JMH_SWMAP ? (0x6325410 >> (4 * j)) & 15 : j; }
+
 template <int NS, bool FWD, class EV, class IDLE>
 __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &ps, const SDesc (&sd)[NS], int b8, int best8x8, EV ev,
                                          int islot, IDLE idle, int wave) {
@@ -419,7 +426,7 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
         // wave j computes search j's MVP (wave-uniform code for a constant block), then LDS
 #pragma unroll
         for (int j = 0; j < NS; j++)
-            if (wave == j) {
+            if (wave == search_wave(j)) {
                 int mx, my;
                 set_mvp(NbMe{s, sd[j].bt, b8, best8x8}, sd[j].bx4, sd[j].by4, 4 << lw4_of(sd[j].bt), 4 << lh4_of(sd[j].bt), mx, my);
                 if (lane == 0) { s.pmv[j][0] = mx; s.pmv[j][1] = my; }
@@ -441,8 +448,12 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
     sstamp(s, wave);
 #pragma unroll
     for (int j = 0; j < NS; j++)
-        if (wave == j) subpel_wave(d, s, j, sd[j], pmx[j], pmy[j], ps.scx, ps.scy, b8, best8x8);
-    if (islot >= 0 && wave >= 6) idle(islot, wave - 6);   // the MB's Intra4x4 on otherwise idle waves
+        if (wave == search_wave(j)) subpel_wave(d, s, j, sd[j], pmx[j], pmy[j], ps.scx, ps.scy, b8, best8x8);
+    if constexpr (NS <= 6) {
+        if (islot >= 0 && wave >= 6) idle(islot, wave - 6);   // the MB's Intra4x4 on otherwise idle waves
+    } else {
+        if (islot >= 0 && wave == 7) idle(islot, 0);          // one free wave: a one-block step
+    }
     __syncthreads();
     sstamp(s, wave);
 }
@@ -535,12 +546,15 @@ __device__ __forceinline__ void sad_strip(const MeS &s, PosState &ps) {
 // Every block leaves its 8x8 SAD (the sum of its 4x4 SADs) in the LDS 8x8 table, so block 3 also
 // runs the 16x16 / 16x8 / 8x16 searches, which are independent of P8x8: the first blocks of each
 // type in its stage 0, the second ones in its stage 1.  Intra4x4 slots 0..10 (waves 6, 7) run in
-// the stages of blocks 0..2 (block 3's stage 0 has no free waves).
+// the sub-pel phases of the stages listed below.
 template <int B8, class IDLE>
 __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState &ps, int &best8x8, int &cost8x8, IDLE idle, int wave, int tid) {
     constexpr int X = 2 * (B8 & 1), Y = 2 * (B8 >> 1);
-    constexpr int IS0 = B8 == 3 ? -1 : 4 * B8, IS1 = B8 == 3 ? -1 : 4 * B8 + 1;
-    constexpr int IS2 = B8 == 3 ? -1 : 4 * B8 + 2, IS3 = B8 >= 2 ? -1 : 4 * B8 + 3;
+    // Intra4x4 slots (diagonal steps 0..9, 10 = the results) in the stages whose sub-pel phase is
+    // long enough to hide a step: the multi-search stages 0 and 1 of every block (block 3's stage
+    // 0 has one free wave, so its step, 8, is a one-block step), two steps in single-search stages
+    constexpr int IS0 = 3 * B8 - (B8 == 3 ? 1 : 0), IS1 = IS0 + 1;
+    constexpr int IS2 = B8 <= 1 ? 3 * B8 + 2 : B8 == 3 ? 10 : -1, IS3 = -1;
     const int sr = d.sr;
     fence_state(ps);
     sad_strip<false, 4 * X, 4 * Y, 0, 0>(s, ps);        // the four 4x4 SADs of this 8x8 block
@@ -846,67 +860,100 @@ __device__ __forceinline__ int lpix(const IntraS<pel> &s, int x, int y) {
     return s.rec[16 * y + x];
 }
 
-// one 4x4 block on one wave: 9 modes x 16 pixels in 3 passes, DPP SATD, then dct_luma on
-// lanes 0..15 of the chosen prediction (at QP'Y = QPY + QpBdOffsetY)
+// the Intra4x4 prediction table entries of lane 4m + y (mode m < 9, block row y): c_i4tab of its
+// four samples, two 16-bit entries per dword (i4_block)
+__device__ __forceinline__ void i4_tabrow(int lane, int (&tabr)[2]) {
+    const int m = lane >> 2, y = lane & 3;
+    tabr[0] = m < 9 ? (int)(c_i4tab[m][4 * y] | (uint32_t)c_i4tab[m][4 * y + 1] << 16) : 0;
+    tabr[1] = m < 9 ? (int)(c_i4tab[m][4 * y + 2] | (uint32_t)c_i4tab[m][4 * y + 3] << 16) : 0;
+}
+
+// one 4x4 block on one wave.  Lane 4m + y (m < 9) predicts row y of mode m from the 13 neighbours
+// (held by lanes 0..12, fetched with ds_bpermute) and scores it: the horizontal Hadamard of the
+// row in registers, the vertical butterflies across the quad's rows by DPP.  One wave minimum of
+// (cost, mode) keys is JM's strict '<' scan in mode order; then dct_luma on lanes 0..15 of the
+// chosen prediction (at QP'Y = QPY + QpBdOffsetY)
 template <class pel>
-__device__ __forceinline__ void i4_block(const DevParams &d, IntraS<pel> &s, MbScratch *scr, int w, int bx4, int by4, const int (&tab)[3],
-                                         bool avL, bool avT, bool avTL, bool avTR, int qpk, int (&acc)[3]) {
-    const int lane = threadIdx.x & 63, l = lane & 15, g = lane >> 4;
+__device__ __forceinline__ void i4_block(const DevParams &d, IntraS<pel> &s, MbScratch *scr, int w, int bx4, int by4, const int (&tabr)[2],
+                                         bool avL, bool avT, bool avTL, bool avTR, int qpk, int (&acc)[3],
+                                         unsigned long long *pst = nullptr) {   // debug: sub-phase stamps [52..57]
+#define I4ST(k, v) do { if (pst) { asm volatile("" ::"v"(v)); if (__lane_id() == 0) pst[k] = wall_clock64(); } } while (0)
+    I4ST(52, bx4);
+    const int lane = threadIdx.x & 63, l = lane & 15;
     const int bx = 4 * bx4, by = 4 * by4, blk = 4 * by4 + bx4;
     const int lambda = d.lambda_mode, qp = d.qp + d.qpbd, had = d.use_hadamard;
     const bool up = by > 0 || avT, left = bx > 0 || avL;
     const bool ul = (bx > 0 && by > 0) || (bx == 0 && by > 0 && avL) || (bx > 0 && by == 0 && avT) || (bx == 0 && by == 0 && avTL);
     bool ur = by == 0 ? (bx + 4 <= 15 ? avT : avTR) : (bx + 4 <= 15);
     if ((bx == 4 || bx == 12) && (by == 4 || by == 12)) ur = false;
-    int *P = s.i4P[w];
+    (void)w;
+    int v = 0;                                // P[lane]: p[-1,-1], p[0..7,-1], p[-1,0..3]
     if (lane < 13) {
-        int v;
         if (lane == 0) v = ul ? lpix(s, bx - 1, by - 1) : 0;
         else if (lane <= 4) v = up ? lpix(s, bx + lane - 1, by - 1) : 0;
         else if (lane <= 8) v = up ? lpix(s, ur ? bx + lane - 1 : bx + 3, by - 1) : 0;
         else v = left ? lpix(s, bx - 1, by + lane - 9) : 0;
-        P[lane] = v;
     }
     const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + bx4];
     const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + by4];
     const int mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
-    wave_lds_sync();
-    const int org = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];
-    const int st = P[1] + P[2] + P[3] + P[4], sl = P[9] + P[10] + P[11] + P[12];
+    const int m = lane >> 2, y = lane & 3;
+    int o[4];
+#pragma unroll
+    for (int x = 0; x < 4; x++) o[x] = s.org[(by + y) * 16 + bx + x];
+    const int org = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];   // the TQ lanes' sample
+    int st = 0, sl = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { st += __builtin_amdgcn_readlane(v, 1 + i); sl += __builtin_amdgcn_readlane(v, 9 + i); }
     const int dc = (up && left) ? (st + sl + 4) >> 3 : left ? (sl + 2) >> 2 : up ? (st + 2) >> 2 : (d.maxv + 1) >> 1;
-    int pv[3], cst[3];
+    I4ST(53, mpm);
+    int pr[4], dd[4];
 #pragma unroll
-    for (int it = 0; it < 3; it++) {
-        const int m = 4 * it + g;
-        pv[it] = 0; cst[it] = BIGCOST + 1;
-        if (m < 9) {
-            const int e = tab[it], ty = e & 3;
-            const int a = P[(e >> 2) & 15], b = P[(e >> 6) & 15], c = P[(e >> 10) & 15];
-            const int p = ty == 1 ? (a + b + 1) >> 1 : ty == 2 ? (a + 2 * b + c + 2) >> 2 : dc;
-            const int sat = had ? row16_sum(abs(row16_had(org - p, l))) >> 1 : row16_sum(abs(org - p));
-            const bool avm = m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul);
-            pv[it] = p;
-            cst[it] = avm ? (m == mpm ? 0 : 4 * lambda) + sat : BIGCOST + 1;
-        }
+    for (int x = 0; x < 4; x++) {
+        const int e = (int)(((uint32_t)tabr[x >> 1] >> (16 * (x & 1))) & 0xFFFFu), ty = e & 3;
+        const int a = __shfl(v, (e >> 2) & 15, 64), b = __shfl(v, (e >> 6) & 15, 64), c = __shfl(v, (e >> 10) & 15, 64);
+        pr[x] = ty == 1 ? (a + b + 1) >> 1 : ty == 2 ? (a + 2 * b + c + 2) >> 2 : dc;
+        dd[x] = o[x] - pr[x];
     }
-    int best = 0, bc = BIGCOST;
+    int t;
+    if (had) {
+        const int h0 = dd[0] + dd[1], h1 = dd[0] - dd[1], h2 = dd[2] + dd[3], h3 = dd[2] - dd[3];
+        int g[4] = {h0 + h2, h1 + h3, h0 - h2, h1 - h3};
 #pragma unroll
-    for (int m = 0; m < 9; m++) {
-        const int c = __builtin_amdgcn_readlane(cst[m >> 2], 16 * (m & 3));
-        if (c < bc) { bc = c; best = m; }
+        for (int x = 0; x < 4; x++) { const int q = dpp<0xB1>(g[x]); g[x] = (y & 1) ? q - g[x] : g[x] + q; }
+#pragma unroll
+        for (int x = 0; x < 4; x++) { const int q = dpp<0x4E>(g[x]); g[x] = (y & 2) ? q - g[x] : g[x] + q; }
+        t = abs(g[0]) + abs(g[1]) + abs(g[2]) + abs(g[3]);
+    } else {
+        t = abs(dd[0]) + abs(dd[1]) + abs(dd[2]) + abs(dd[3]);
     }
-    const int src = (best >> 2) == 0 ? pv[0] : (best >> 2) == 1 ? pv[1] : pv[2];
-    const int pp = __shfl(src, 16 * (best & 3) + l, 64);
+    t += dpp<0xB1>(t);                        // the quad's rows
+    t += dpp<0x4E>(t);
+    const int sat = had ? t >> 1 : t;
+    const bool avm = m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul);
+    const int cst = (m < 9 && avm) ? (m == mpm ? 0 : 4 * lambda) + sat : BIGCOST;
+    const unsigned key = wave_min_u32((y == 0 && cst < BIGCOST) ? ((unsigned)cst << 4) | (unsigned)m : 0xFFFFFFFFu);
+    I4ST(54, key);
+    const int best = key == 0xFFFFFFFFu ? 0 : (int)(key & 15u), bc = key == 0xFFFFFFFFu ? BIGCOST : (int)(key >> 4);
+    // the winner's prediction at TQ lane l (raster 4y' + x'): register x' of lane 4 best + y'
+    const int srcl = 4 * best + (l >> 2);
+    const int q01 = __shfl((pr[0] & 0xFFFF) | (pr[1] << 16), srcl, 64), q23 = __shfl((pr[2] & 0xFFFF) | (pr[3] << 16), srcl, 64);
+    const int qx = (l & 2) ? q23 : q01;
+    const int pp = (l & 1) ? (int)((uint32_t)qx >> 16) : (qx & 0xFFFF);
+    I4ST(55, pp);
     unsigned nz = 0;
     if (lane < 16) {
         const int c = lane_fwd4x4(org - pp, l);
         int lev, dq, cc;
         nz = lane_quant(c, l, qp, qpk, false, lev, dq, cc);
+        I4ST(56, dq);
         scr->i4lev[blk][l] = (int16_t)lev;
         s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (pel)lane_inv4x4(dq, l, pp, d.maxv);
         if (l == 0) s.ipred_cur[blk] = (int8_t)best;
     }
     nz = __builtin_amdgcn_readlane(nz, 0);
+    I4ST(57, nz);
+#undef I4ST
     acc[0] += bc;
     if (nz) { acc[1] |= 1 << ((by4 >> 1) * 2 + (bx4 >> 1)); acc[2] |= 1 << blk; }
 }
@@ -932,18 +979,14 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS<pel> &s, i
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const int q_bits = 15 + (d.qp + d.qpbd) / 6;
     const int qpk = q_round(d.qsel, q_bits);
-    int tab[3];
-#pragma unroll
-    for (int it = 0; it < 3; it++) {
-        const int m = 4 * it + ((lane >> 4) & 3);
-        tab[it] = m < 9 ? c_i4tab[m][lane & 15] : 0;
-    }
+    int tabr[2];
+    i4_tabrow(lane, tabr);
     int acc[3] = {0, 0, 0};                   // cost, cbp (per b8), block mask
     __syncthreads();
     for (int dg = 0; dg < 10; dg++) {         // blocks with bx4 + 2*by4 == dg, by4 ascending
         const int by_lo = dg > 3 ? (dg - 2) >> 1 : 0;
         const int by4 = by_lo + wave, bx4 = dg - 2 * by4;
-        if (act && i4 && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+        if (act && i4 && by4 <= 3 && bx4 >= 0 && bx4 <= 3) i4_block(d, s, scr, wave, bx4, by4, tabr, avL, avT, avTL, avTR, qpk, acc);
         __syncthreads();
     }
     if (act && lane == 0) { s.part[wave][0] = acc[0]; s.part[wave][1] = acc[1]; s.part[wave][2] = acc[2]; }
@@ -963,8 +1006,9 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS<pel> &s, i
     PSTAMP(14);
 }
 
-// the Intra4x4 decision inside a motion-search workgroup, on its waves 6 and 7 (w = wave - 6)
-// while the sub-pel waves of a stage work; steps are separated by the stage barriers.  Slot
+// the Intra4x4 decision inside a motion-search workgroup, on its waves 6 and 7 (w = wave - 6; wave
+// 7 as w = 0 in block 3's first stage) while the sub-pel waves of a stage work; steps are separated
+// by the stage barriers.  Slot
 // k = 0..9: diagonal k of the 4x4 grid; slot 10: the totals and results.
 __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int k, int w, int mbx, int mby) {
     const int lane = threadIdx.x & 63;
@@ -973,17 +1017,14 @@ __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &
     if (k < 10) {
         const int q_bits = 15 + d.qp / 6;
         const int qpk = q_round(d.qsel, q_bits);
-        int tab[3];
-#pragma unroll
-        for (int it = 0; it < 3; it++) {
-            const int m = 4 * it + ((lane >> 4) & 3);
-            tab[it] = m < 9 ? c_i4tab[m][lane & 15] : 0;
-        }
+        int tabr[2];
+        i4_tabrow(lane, tabr);
         const int by_lo = k > 3 ? (k - 2) >> 1 : 0;
         const int by4 = by_lo + w, bx4 = k - 2 * by4;
         if (by4 <= 3 && bx4 >= 0 && bx4 <= 3) {   // the wave's running cost / cbp / block mask live in LDS
             int acc[3] = {s.part[w][0], s.part[w][1], s.part[w][2]};
-            i4_block(d, s, scr, w, bx4, by4, tab, avL, avT, avTL, avTR, qpk, acc);
+            unsigned long long *pst = (k == 4 && w == 0 && d.prof && d.prof_mb == mby * d.mbw + mbx) ? d.prof : nullptr;   // debug stamps
+            i4_block(d, s, scr, w, bx4, by4, tabr, avL, avT, avTL, avTR, qpk, acc, pst);
             if (lane == 0) { s.part[w][0] = acc[0]; s.part[w][1] = acc[1]; s.part[w][2] = acc[2]; }
         }
     } else if (w == 0) {
