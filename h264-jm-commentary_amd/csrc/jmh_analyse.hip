@@ -887,13 +887,13 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS<pel> &s, MbS
     bool ur = by == 0 ? (bx + 4 <= 15 ? avT : avTR) : (bx + 4 <= 15);
     if ((bx == 4 || bx == 12) && (by == 4 || by == 12)) ur = false;
     (void)w;
-    int v = 0;                                // P[lane]: p[-1,-1], p[0..7,-1], p[-1,0..3]
-    if (lane < 13) {
-        if (lane == 0) v = ul ? lpix(s, bx - 1, by - 1) : 0;
-        else if (lane <= 4) v = up ? lpix(s, bx + lane - 1, by - 1) : 0;
-        else if (lane <= 8) v = up ? lpix(s, ur ? bx + lane - 1 : bx + 3, by - 1) : 0;
-        else v = left ? lpix(s, bx - 1, by + lane - 9) : 0;
-    }
+    // P[lane]: p[-1,-1], p[0..7,-1], p[-1,0..3] -- one LDS read per lane from a selected address
+    // (the MB's reconstruction or its top / left neighbour samples), no divergent branches
+    const int px = lane == 0 || lane >= 9 ? bx - 1 : lane <= 4 || ur ? bx + lane - 1 : bx + 3;
+    const int py = lane >= 9 ? by + lane - 9 : by - 1;
+    const bool pav = lane < 13 && (lane == 0 ? ul : lane <= 8 ? up : left);
+    const pel *pp_ = !pav ? &s.rec[0] : py < 0 ? &s.nb.rtop[px + 1] : px < 0 ? &s.nb.rleft[py] : &s.rec[16 * py + px];
+    const int v = pav ? (int)*pp_ : 0;
     const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + bx4];
     const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + by4];
     const int mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
