@@ -860,6 +860,28 @@ __device__ __forceinline__ int lpix(const IntraS<pel> &s, int x, int y) {
     return s.rec[16 * y + x];
 }
 
+// lane_fwd4x4 / lane_inv4x4 with the row gathers as quad DPP broadcasts (the four samples of
+// row y of a 16-lane group are one quad); the column gathers stay ds_bpermute (whole quads active)
+__device__ __forceinline__ int quad_fwd4x4(int r, int l) {
+    const int y = l >> 2, x = l & 3;
+    const int v0 = dpp<0x00>(r), v1 = dpp<0x55>(r), v2 = dpp<0xAA>(r), v3 = dpp<0xFF>(r);
+    int p0 = v0 + v3, p3 = v0 - v3, p1 = v1 + v2, p2 = v1 - v2;
+    const int t = x == 0 ? p0 + p1 : x == 1 ? 2 * p3 + p2 : x == 2 ? p0 - p1 : p3 - 2 * p2;
+    const int u0 = g16(t, x), u1 = g16(t, 4 + x), u2 = g16(t, 8 + x), u3 = g16(t, 12 + x);
+    p0 = u0 + u3; p3 = u0 - u3; p1 = u1 + u2; p2 = u1 - u2;
+    return y == 0 ? p0 + p1 : y == 1 ? 2 * p3 + p2 : y == 2 ? p0 - p1 : p3 - 2 * p2;
+}
+__device__ __forceinline__ int quad_inv4x4(int dq, int l, int pred, int maxv) {
+    const int y = l >> 2, x = l & 3;
+    const int d0 = dpp<0x00>(dq), d1 = dpp<0x55>(dq), d2 = dpp<0xAA>(dq), d3 = dpp<0xFF>(dq);
+    int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+    const int t = x == 0 ? e0 + e3 : x == 1 ? e1 + e2 : x == 2 ? e1 - e2 : e0 - e3;
+    const int f0 = g16(t, x), f1 = g16(t, 4 + x), f2 = g16(t, 8 + x), f3 = g16(t, 12 + x);
+    e0 = f0 + f2; e1 = f0 - f2; e2 = (f1 >> 1) - f3; e3 = f1 + (f3 >> 1);
+    const int o = y == 0 ? e0 + e3 : y == 1 ? e1 + e2 : y == 2 ? e1 - e2 : e0 - e3;
+    return iclip(0, maxv, (o + (pred << 6) + 32) >> 6);
+}
+
 // the Intra4x4 prediction table entries of lane 4m + y (mode m < 9, block row y): c_i4tab of its
 // four samples, two 16-bit entries per dword (i4_block)
 __device__ __forceinline__ void i4_tabrow(int lane, int (&tabr)[2]) {
@@ -943,12 +965,12 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS<pel> &s, MbS
     I4ST(55, pp);
     unsigned nz = 0;
     if (lane < 16) {
-        const int c = lane_fwd4x4(org - pp, l);
+        const int c = quad_fwd4x4(org - pp, l);
         int lev, dq, cc;
         nz = lane_quant(c, l, qp, qpk, false, lev, dq, cc);
         I4ST(56, dq);
         scr->i4lev[blk][l] = (int16_t)lev;
-        s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (pel)lane_inv4x4(dq, l, pp, d.maxv);
+        s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (pel)quad_inv4x4(dq, l, pp, d.maxv);
         if (l == 0) s.ipred_cur[blk] = (int8_t)best;
     }
     nz = __builtin_amdgcn_readlane(nz, 0);
