@@ -28,13 +28,17 @@
 // range), int32 horizontal taps, and the EPZS thresholds times 1 << (BitDepthY - 8).
 #include "jmh_epzs.h"
 
-template <class pel>
+// JM10X: built with JM >= 10's EPZSSubPelME / adaptive-threshold paths (items 61, 62); the
+// instantiation without them (both knobs off, e.g. config 3's JM 8.6 EPZS) constant-folds those
+// branches away instead of testing them at run time (fewer VGPRs and instructions)
+template <class pel, bool JM10X>
 __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     __shared__ EpzS<pel> s;
     const int b = xcd_block(blockIdx.x, t.pre[t.nP]), lane = threadIdx.x;   // XCD-aware (jmh_device.h)
     if (b >= t.pre[t.nP]) return;
     const int e = tick_entry(t, b);
-    const DevParams d = tick_params(t, e);
+    DevParams d = tick_params(t, e);
+    if constexpr (!JM10X) { d.epzs_subpel = 0; d.epzs_maxts = 0; }
     const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const bool prof = d.prof && lane == 0 && d.prof_mb == mby * d.mbw + mbx;
@@ -104,7 +108,14 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
 
 hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st) {
     if (t.pre[t.nP] == 0) return hipSuccess;
-    if (t.bd > 8) hipLaunchKernelGGL(k_mb_epzs<uint16_t>, dim3(xcd_grid(t.pre[t.nP])), dim3(NTE), 0, st, t);
-    else hipLaunchKernelGGL(k_mb_epzs<uint8_t>, dim3(xcd_grid(t.pre[t.nP])), dim3(NTE), 0, st, t);
+    const dim3 g(xcd_grid(t.pre[t.nP]));
+    const bool x = t.epzs_subpel || t.epzs_maxts;
+    if (t.bd > 8) {
+        if (x) hipLaunchKernelGGL((k_mb_epzs<uint16_t, true>), g, dim3(NTE), 0, st, t);
+        else hipLaunchKernelGGL((k_mb_epzs<uint16_t, false>), g, dim3(NTE), 0, st, t);
+    } else {
+        if (x) hipLaunchKernelGGL((k_mb_epzs<uint8_t, true>), g, dim3(NTE), 0, st, t);
+        else hipLaunchKernelGGL((k_mb_epzs<uint8_t, false>), g, dim3(NTE), 0, st, t);
+    }
     return hipGetLastError();
 }
