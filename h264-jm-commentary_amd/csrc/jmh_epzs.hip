@@ -28,9 +28,9 @@
 // range), int32 horizontal taps, and the EPZS thresholds times 1 << (BitDepthY - 8).
 #include "jmh_epzs.h"
 
-// JM10X: built with JM >= 10's EPZSSubPelME / adaptive-threshold paths (items 61, 62); the
-// instantiation without them (both knobs off, e.g. config 3's JM 8.6 EPZS) constant-folds those
-// branches away instead of testing them at run time (fewer VGPRs and instructions)
+// JM10X: built with JM >= 10's EPZS options (EPZSDualRefinement, EPZSSubPelME, the adaptive
+// thresholds: items 46, 61, 62); the instantiation without them (all off, e.g. config 3's JM 8.6
+// EPZS) constant-folds those branches away instead of testing them at run time
 template <class pel, bool JM10X>
 __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     __shared__ EpzS<pel> s;
@@ -38,7 +38,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     if (b >= t.pre[t.nP]) return;
     const int e = tick_entry(t, b);
     DevParams d = tick_params(t, e);
-    if constexpr (!JM10X) { d.epzs_subpel = 0; d.epzs_maxts = 0; }
+    if constexpr (!JM10X) { d.epzs_dual = 0; d.epzs_subpel = 0; d.epzs_maxts = 0; }
     const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const bool prof = d.prof && lane == 0 && d.prof_mb == mby * d.mbw + mbx;
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
 hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st) {
     if (t.pre[t.nP] == 0) return hipSuccess;
     const dim3 g(xcd_grid(t.pre[t.nP]));
-    const bool x = t.epzs_subpel || t.epzs_maxts;
+    const bool x = t.epzs_dual || t.epzs_subpel || t.epzs_maxts;
     if (t.bd > 8) {
         if (x) hipLaunchKernelGGL((k_mb_epzs<uint16_t, true>), g, dim3(NTE), 0, st, t);
         else hipLaunchKernelGGL((k_mb_epzs<uint16_t, false>), g, dim3(NTE), 0, st, t);
