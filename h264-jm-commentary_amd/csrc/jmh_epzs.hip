@@ -39,6 +39,7 @@ __global__ __launch_bounds__(NTE) void k_mb_epzs(const TickArgs t) {
     const int e = tick_entry(t, b);
     DevParams d = tick_params(t, e);
     if constexpr (!JM10X) { d.epzs_dual = 0; d.epzs_subpel = 0; d.epzs_maxts = 0; }
+    if constexpr (sizeof(pel) == 1) { d.maxv = 255; d.qpbd = 0; }   // 8-bit samples: constants
     const int mby = d.y_min + (b - t.pre[e]), mbx = d.diag - 2 * mby;
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const bool prof = d.prof && lane == 0 && d.prof_mb == mby * d.mbw + mbx;

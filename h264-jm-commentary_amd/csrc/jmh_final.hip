@@ -40,7 +40,9 @@ struct FinS {
 
 // OCC workgroups per CU: 8 (64 VGPRs, a few spilled) for ticks of more than 5 x 256 MBs (2160p,
 // one dispatch round), 5 (no spills, a shorter per-MB chain) for smaller ticks
-template <int OCC, class pel>
+// T8: built with Transform8x8Mode's paths (I8MB, TransformDecision, dct_luma8x8); the
+// instantiation without them folds d.t8 = 0, and 8-bit samples fold Clip1 = 255, QpBdOffset = 0
+template <int OCC, class pel, bool T8>
 __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     __shared__ FinS<pel> s;
     const int tid = threadIdx.x;
@@ -48,7 +50,9 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
     const int m = xcd_block(blockIdx.x, t.pre[t.npic]);       // XCD-aware (jmh_device.h)
     if (m >= t.pre[t.npic]) return;                           // padding block (whole workgroup)
     const int e = tick_entry(t, m);
-    const DevParams d = tick_params(t, e);
+    DevParams d = tick_params(t, e);
+    if constexpr (!T8) d.t8 = 0;
+    if constexpr (sizeof(pel) == 1) { d.maxv = 255; d.qpbd = 0; }
     const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
     const int W = d.W, Wc = d.Wc, W4 = d.W >> 2;
@@ -333,8 +337,9 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
 hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st) {
     static const bool occ8 = getenv("JMH_FINAL_OCC8") != nullptr;   // A/B: the 8-per-CU build always
     const int n = t.pre[t.npic];
-    if (t.bd > 8) hipLaunchKernelGGL((k_mb_final<8, uint16_t>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
-    else if (occ8 || n > 5 * 256) hipLaunchKernelGGL((k_mb_final<8, uint8_t>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
-    else hipLaunchKernelGGL((k_mb_final<5, uint8_t>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
+    if (t.bd > 8) hipLaunchKernelGGL((k_mb_final<8, uint16_t, true>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
+    else if (occ8 || n > 5 * 256) hipLaunchKernelGGL((k_mb_final<8, uint8_t, true>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
+    else if (t.t8) hipLaunchKernelGGL((k_mb_final<5, uint8_t, true>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
+    else hipLaunchKernelGGL((k_mb_final<5, uint8_t, false>), dim3(xcd_grid(n)), dim3(NT), 0, st, t);
     return hipGetLastError();
 }
