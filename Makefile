@@ -1,15 +1,20 @@
-# Top-level build: the product (libjmhip.so + host plumbing + lencod) and the test-only oracle.
-.PHONY: all product oracle clean
-all: product oracle
+# Top-level build: the product (libjmhip.so + host plumbing + lencod), the test-only oracle and the
+# test harness binaries that combine the two (tests/harness).
+.PHONY: all product oracle harness clean
+all: product oracle harness
 
 product:
 	$(MAKE) -C h264-jm-commentary_amd/csrc libjmhip.so
 	$(MAKE) -C h264-jm-commentary_amd/host all
 
-oracle: product
+oracle:
 	$(MAKE) -C oracle all
+
+harness: product oracle
+	$(MAKE) -C tests/harness all
 
 clean:
 	$(MAKE) -C h264-jm-commentary_amd/csrc clean
 	$(MAKE) -C h264-jm-commentary_amd/host clean
 	$(MAKE) -C oracle clean
+	$(MAKE) -C tests/harness clean

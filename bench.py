@@ -228,16 +228,20 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
     return bool(ok)
 
 
-def read_pmc_traffic():
-    """(HBM bytes per macroblock of k_mb_analyse, source description) from the rocprofv3 PMC passes
-    of tools/pmc_traffic.sh, or (None, None).  The figure of the latest pass is kept in
-    tools/pmc_traffic.json (it travels to the GPU box, unlike profiles/); it is a committed
-    measurement of an earlier run of the same kernel, not of this run."""
+def read_pmc_traffic(config, search_mode):
+    """(HBM bytes per macroblock of the roofline's kernels, source description) from the rocprofv3
+    PMC passes of tools/pmc_traffic.sh for this config, or (None, None).  The latest pass per
+    config is kept in tools/pmc_traffic.json (it travels to the GPU box, unlike profiles/); it is
+    a committed measurement of an earlier run of the same kernels, not of this run."""
     p = os.path.join(ROOT, "tools", "pmc_traffic.json")
+    key = {(2, 0): "2", (3, 3): "3", (5, 3): "5"}.get((config, search_mode))
+    if key is None or (config == 5 and not RDO):
+        return None, None
     try:
         with open(p) as f:
-            j = json.load(f)
-        src = f"tools/pmc_traffic.json ({j.get('source', 'rocprofv3 PMC')}; {j.get('calibration', 'uncalibrated')})"
+            j = json.load(f)["configs"][key]
+        src = (f"tools/pmc_traffic.json config {key}: {j['kernel']} ({j.get('source', 'rocprofv3 PMC')}; "
+               f"{j.get('calibration', 'uncalibrated')})")
         return j["hbm_bytes_per_mb"], src
     except (OSError, ValueError, KeyError, TypeError):
         return None, None
@@ -409,18 +413,28 @@ def main():
 
     value = world * args.steps * DISP_W * DISP_H / 1e6 / dt
     pictures = max(1, tm.pictures)
-    an_launch_ms = tm.analyse_ms / max(1, tm.analyse_launches)
     an_per_pic = tm.ticks / pictures                     # one k_mb_analyse + one k_mb_final per tick
+    mb_ms_pic = tm.mb_ms / pictures
+    # the sampled launches' HIP events (every 8th tick) add a few us per launch; the wavefront
+    # brackets (one event pair per run of ticks) do not.  The per-launch figures are scaled so that
+    # the sampled launches of a tick sum to the bracketed wavefront time per tick (never above it):
+    # k_mb_analyse 93.8 us raw vs 90.0 us in rocprof's kernel trace (profiles/r6h_*)
+    an_raw_ms = tm.analyse_ms / max(1, tm.analyse_launches)
+    fin_raw_ms = 0.0 if RDO else tm.final_ms / max(1, tm.final_launches)
+    ev_scale = min(1.0, mb_ms_pic / an_per_pic / (an_raw_ms + fin_raw_ms)) if an_raw_ms + fin_raw_ms > 0 else 1.0
+    an_launch_ms, fin_launch_ms = an_raw_ms * ev_scale, fin_raw_ms * ev_scale
     mbs_per_launch = tm.tick_mbs / max(1, tm.ticks)      # MBs of all pictures in flight, per tick
     bytes_per_launch = BYTES_PER_FRAME / NMB * mbs_per_launch
     achieved_gbs = bytes_per_launch / (an_launch_ms * 1e-3) / 1e9
     ad_per_launch = AD_PER_FRAME / NMB * mbs_per_launch
     achieved_tads = ad_per_launch / (an_launch_ms * 1e-3) / 1e12
     peak_tads, peak_src = sad_peak()
-    mb_ms_pic = tm.mb_ms / pictures
-    pmc, pmc_src = read_pmc_traffic() if args.config == 2 and search_mode == 0 else (None, None)   # config 2 pass
+    pmc, pmc_src = read_pmc_traffic(args.config, search_mode)
     sm_name = {0: "FFS SearchMode=0", -1: "full search SearchMode=-1", 3: "EPZS SearchMode=3"}[search_mode]
     ffs = search_mode == 0
+    an_name = ("k_rdo_inter+k_rdo_intra+k_rdo_final" if RDO else
+               ("k_mb_analyse+k_mb_intra8" if cfg["t8"] else "k_mb_analyse") if ffs else
+               ("k_mb_epzs" if search_mode == 3 else "k_mb_me_full") + "+k_mb_intra")
     hbm = {
         "bound": "hbm",
         "achieved": round(achieved_gbs, 3),
@@ -432,9 +446,12 @@ def main():
         "algorithmic_bytes_per_launch": round(bytes_per_launch),
     }
     launch_info = {
-        "kernel": "k_rdo_inter + k_rdo_intra + k_rdo_final (the tick's RD launches)" if RDO else "k_mb_analyse" if ffs else
-                  ("k_mb_epzs" if search_mode == 3 else "k_mb_me_full") + " + k_mb_intra (the tick's analysis launches)",
+        "kernel": an_name.replace("+", " + ") + (" (the tick's RD launches: inter and intra on two streams, then final; "
+                                                  "the span of the three)" if RDO else
+                                                  "" if ffs and not cfg["t8"] else " (the tick's analysis launches)"),
         "avg_launch_ms": round(an_launch_ms, 5),
+        "avg_launch_ms_events_raw": round(an_raw_ms, 5),
+        "event_scale": round(ev_scale, 4),
         "launches_per_picture": round(an_per_pic, 2),
         "mbs_per_launch": round(mbs_per_launch, 1),
     }
@@ -479,10 +496,14 @@ def main():
                     "pictures in flight are not drained); exactly `steps` pictures complete inside",
         },
         "roofline": roofline,
-        # per-launch averages (sampled every 8th diagonal) x launches per picture
+        # per-launch averages (sampled every 8th tick, scaled to the bracketed wavefront time: see
+        # ev_scale) x launches per picture; RDO on: the span of a tick's three RD launches
         "kernel_ms_per_picture": {"wavefront": round(mb_ms_pic, 4),
-                                  ("k_rdo_inter+k_rdo_intra+k_rdo_final" if RDO else "k_mb_analyse"): round(an_launch_ms * an_per_pic, 4),
-                                  "k_mb_final": None if RDO else round(tm.final_ms / max(1, tm.final_launches) * an_per_pic, 4)},
+                                  an_name + (" (tick span)" if RDO else ""): round(an_launch_ms * an_per_pic, 4),
+                                  "k_mb_final": None if RDO else round(fin_launch_ms * an_per_pic, 4),
+                                  "note": "HIP events on the kernels' stream; the sampled per-launch averages are "
+                                          "scaled by event_scale so that a tick's launches sum to the bracketed "
+                                          "wavefront time per tick (the sampling events add a few us per launch)"},
         "host_path": None if host is None else {
             "pcie_inclusive_mp_s": round(host[0], 3),
             "single_picture_latency_ms": round(host[1], 3),

@@ -118,6 +118,7 @@ struct PicBuf {
     uint32_t *range;                     //   codIRange, the MBs' context-selection records
     jmr_mbinfo *mbi;
     RdoPic *h_rp;                        //   pinned staging of the entry's RdoPic (after scr)
+    hipEvent_t ev_rp;                    //   its H2D copy (h_rp is rewritten only after it completes)
     int recon_read;                      // h_rec holds the occupant's reconstruction
     int unpopped;                        // readback picture not yet popped
     int deblocked;                       // the occupant was deblocked on the device (dbk valid)
@@ -214,7 +215,7 @@ static void free_entry(PicBuf &b) {
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     void *host_bufs[] = {b.h_res, b.h_src, b.h_rec, b.h_dbk, b.h_rp};
     for (void *p : host_bufs) if (p) (void)hipHostFree(p);
-    hipEvent_t evs[] = {b.ev_src, b.ev_t0, b.ev_done, b.ev_fin};
+    hipEvent_t evs[] = {b.ev_src, b.ev_t0, b.ev_done, b.ev_fin, b.ev_rp};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
 }
 
@@ -233,6 +234,7 @@ static int alloc_entry(jmh_ctx *c, PicBuf &b) {
         if (hipHostMalloc((void **)&b.h_rp, sizeof(RdoPic), hipHostMallocDefault) != hipSuccess) return JMH_E_OOM;
         b.h_rp->lambda = 0; b.h_rp->lf = 0; b.h_rp->pad = 0;
         b.h_rp->cab = b.cab; b.h_rp->range = b.range; b.h_rp->mbi = b.mbi;
+        if (hipEventCreateWithFlags(&b.ev_rp, hipEventDisableTiming) != hipSuccess) return JMH_E_HIP;
     }
 #undef ALLOC
     if (hipMemset(b.rec, 0, c->fsize) != hipSuccess || hipMemset(b.dbk, 0, c->fsize) != hipSuccess) return JMH_E_HIP;
@@ -497,15 +499,34 @@ static void ordtab_fill(std::vector<uint32_t> &tab, int sr) {
     }
 }
 
-// planar 4:2:0 packing of ps-byte samples (strides in samples)
-static void pack_planes(uint8_t *dst, int W, int H, const void *yv, const void *uv, const void *vv, int sy, int sc, int ps) {
+// planar 4:2:0 packing of ps-byte samples (strides in samples).  16-bit samples are range-checked
+// on the way (the kernels' cost keys and transform headroom assume every sample <= maxv): false
+// when one exceeds maxv = (1 << bit depth) - 1, with dst then partially written.
+static inline uint16_t pack_row16(uint16_t *d, const uint16_t *s, int n) {
+    uint16_t acc = 0;
+    for (int x = 0; x < n; x++) { d[x] = s[x]; acc |= s[x]; }
+    return acc;
+}
+static bool pack_planes(uint8_t *dst, int W, int H, const void *yv, const void *uv, const void *vv, int sy, int sc, int ps,
+                        int maxv) {
     const uint8_t *y = (const uint8_t *)yv, *u = (const uint8_t *)uv, *v = (const uint8_t *)vv;
-    for (int r = 0; r < H; r++) memcpy(dst + (size_t)r * W * ps, y + (size_t)r * sy * ps, (size_t)W * ps);
     uint8_t *du = dst + (size_t)W * H * ps, *dv = du + (size_t)W * H / 4 * ps;
-    for (int r = 0; r < H / 2; r++) {
-        memcpy(du + (size_t)r * (W / 2) * ps, u + (size_t)r * sc * ps, (size_t)(W / 2) * ps);
-        memcpy(dv + (size_t)r * (W / 2) * ps, v + (size_t)r * sc * ps, (size_t)(W / 2) * ps);
+    if (ps == 1) {
+        for (int r = 0; r < H; r++) memcpy(dst + (size_t)r * W, y + (size_t)r * sy, (size_t)W);
+        for (int r = 0; r < H / 2; r++) {
+            memcpy(du + (size_t)r * (W / 2), u + (size_t)r * sc, (size_t)(W / 2));
+            memcpy(dv + (size_t)r * (W / 2), v + (size_t)r * sc, (size_t)(W / 2));
+        }
+        return true;
     }
+    const uint16_t *y16 = (const uint16_t *)y, *u16 = (const uint16_t *)u, *v16 = (const uint16_t *)v;
+    uint16_t acc = 0;
+    for (int r = 0; r < H; r++) acc |= pack_row16((uint16_t *)dst + (size_t)r * W, y16 + (size_t)r * sy, W);
+    for (int r = 0; r < H / 2; r++) {
+        acc |= pack_row16((uint16_t *)du + (size_t)r * (W / 2), u16 + (size_t)r * sc, W / 2);
+        acc |= pack_row16((uint16_t *)dv + (size_t)r * (W / 2), v16 + (size_t)r * sc, W / 2);
+    }
+    return (acc & ~maxv) == 0;   // maxv = 2^bd - 1: every sample <= maxv iff no bit above it is set
 }
 
 static void unpack_planes(const uint8_t *src, int W, int H, void *yv, void *uv, void *vv, int sy, int sc, int ps) {
@@ -518,19 +539,10 @@ static void unpack_planes(const uint8_t *src, int W, int H, void *yv, void *uv, 
     }
 }
 
-// a picture handed to a High 10 context: every sample within the bit depth (the kernels' cost keys
-// and transform headroom assume it), and the entry point's sample width matches the context
-static int check_pic(const jmh_ctx *c, const void *y, const void *u, const void *v, int sy, int sc, bool wide) {
-    if ((c->bd > 8) != wide) return JMH_E_UNSUPPORTED_CFG;
-    if (!wide) return JMH_OK;
-    const uint16_t *pl[3] = {(const uint16_t *)y, (const uint16_t *)u, (const uint16_t *)v};
-    for (int k = 0; k < 3; k++) {
-        const int w = k ? c->Wc : c->W, h = k ? c->Hc : c->H, s = k ? sc : sy;
-        for (int r = 0; r < h; r++)
-            for (int x = 0; x < w; x++)
-                if (pl[k][(size_t)r * s + x] > c->maxv) return JMH_E_INVALID_ARG;
-    }
-    return JMH_OK;
+// the entry point's sample width matches the context (the sample range of a 16-bit picture is
+// checked while it is packed into staging, pack_planes)
+static int check_pic(const jmh_ctx *c, bool wide) {
+    return (c->bd > 8) != wide ? JMH_E_UNSUPPORTED_CFG : JMH_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -710,9 +722,13 @@ static int push_picture(jmh_ctx *c, const uint8_t *src, int entry, const jmh_fra
     b.unpopped = readback;
     b.deblocked = fp->deblock != 0;
     if (c->cfg.rdo) {   // the picture's lambdas into its RdoPic (stream order: before its ticks)
+        // the entry's previous occupant may have been queued without any host wait since (the
+        // jmh_encode_slot path): its copy out of h_rp must have run before h_rp is rewritten
+        HCHK(hipEventSynchronize(b.ev_rp));
         b.h_rp->lambda = fp->lambda_rd;
         b.h_rp->lf = fp->lambda_factor_rd;
         HCHK(hipMemcpyAsync(reinterpret_cast<uint8_t *>(b.scr) + rdo_pic_offset(c->nmb), b.h_rp, sizeof(RdoPic), hipMemcpyHostToDevice, c->st));
+        HCHK(hipEventRecord(b.ev_rp, c->st));
     }
     c->fl.push_back(f);
     c->last_id = f.id;
@@ -734,8 +750,9 @@ static int check_params(const jmh_ctx *c, const jmh_frame_params *fp) {
     if (fp->deblock && (fp->lf_disable < 0 || fp->lf_disable > 2 || fp->lf_alpha_div2 < -6 || fp->lf_alpha_div2 > 6 ||
                         fp->lf_beta_div2 < -6 || fp->lf_beta_div2 > 6)) return JMH_E_INVALID_ARG;
     if (fp->slice_type == JMH_P_SLICE && c->ref_kind == REF_NONE) return JMH_E_STATE;
-    // RDOptimization 1: lambda_mode > 0 and its factor (at most 65536 * sqrt(0.85 * 2^21) ~ 8.4e7 at
-    // QP 51 + 12, kept below 2^31 / 64 so that factor * mvbits fits the searches' 32-bit costs)
+    // RDOptimization 1: lambda_mode > 0 and its factor (jm_lambda_rdo_on at QP 51 + QpBdOffset 12:
+    // lambda = 0.85 * 2^((63 - 12) / 3) = 0.85 * 2^17, factor = 65536 * sqrt(lambda) ~ 2.2e7 < 2^25,
+    // kept below 2^31 / 64 so that factor * mvbits fits the searches' 32-bit costs)
     if (c->cfg.rdo && !(fp->lambda_rd > 0 && fp->lambda_rd < 1e9 && fp->lambda_factor_rd > 0 && fp->lambda_factor_rd < (1 << 25)))
         return JMH_E_INVALID_ARG;
     return JMH_OK;
@@ -765,13 +782,13 @@ extern "C" {
 static int set_reference_any(jmh_ctx *c, int list, int ref_idx, const void *y, const void *u, const void *v, int sy, int sc, bool wide) {
     if (!c || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
     if (list != 0 || ref_idx != 0) return JMH_E_UNSUPPORTED_CFG;
-    int r = check_pic(c, y, u, v, sy, sc, wide);
+    int r = check_pic(c, wide);
     if (r) return r;
     HCHK(hipSetDevice(c->dev));
     r = drain(c);   // pictures in flight may read d_ref
     if (r) return r;
     HCHK(hipStreamSynchronize(c->st));   // staging buffer reuse
-    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc, c->ps);
+    if (!pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc, c->ps, c->maxv)) return JMH_E_INVALID_ARG;
     HCHK(hipMemcpyAsync(c->d_ref, c->h_stage_ref, c->fsize, hipMemcpyHostToDevice, c->st));
     c->ref_kind = REF_BUF; c->ref_entry = -1;
     return JMH_OK;
@@ -805,7 +822,7 @@ static int frame_push_any(jmh_ctx *c, const void *y, const void *u, const void *
     if (!c || !y || !u || !v || !fp || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
     int r = check_params(c, fp);
     if (r) return r;
-    if ((r = check_pic(c, y, u, v, sy, sc, wide))) return r;
+    if ((r = check_pic(c, wide))) return r;
     if ((int)c->popq.size() >= c->depth) return JMH_E_STATE;
     HCHK(hipSetDevice(c->dev));
     int e;
@@ -813,7 +830,9 @@ static int frame_push_any(jmh_ctx *c, const void *y, const void *u, const void *
     PicBuf &b = c->ring[e];
     if ((r = alloc_host(c, b))) return r;
     HCHK(hipEventSynchronize(b.ev_src));   // the previous H2D out of this staging buffer
-    pack_planes(b.h_src, c->W, c->H, y, u, v, sy, sc, c->ps);
+    // an out-of-range sample rejects the picture before anything is queued (the claimed entry
+    // stays free: nothing refers to it)
+    if (!pack_planes(b.h_src, c->W, c->H, y, u, v, sy, sc, c->ps, c->maxv)) return JMH_E_INVALID_ARG;
     HCHK(hipEventRecord(b.ev_t0, c->st));
     HCHK(hipMemcpyAsync(b.src, b.h_src, c->fsize, hipMemcpyHostToDevice, c->st));
     HCHK(hipEventRecord(b.ev_src, c->st));
@@ -878,13 +897,13 @@ static int read_pic(jmh_ctx *c, void *y, void *u, void *v, int sy, int sc, bool 
 }
 static int load_frame_any(jmh_ctx *c, int slot, const void *y, const void *u, const void *v, int sy, int sc, bool wide) {
     if (!c || slot < 0 || slot >= c->nslots || !y || !u || !v || sy < c->W || sc < c->Wc) return JMH_E_INVALID_ARG;
-    int r = check_pic(c, y, u, v, sy, sc, wide);
+    int r = check_pic(c, wide);
     if (r) return r;
     HCHK(hipSetDevice(c->dev));
     r = drain(c);   // pictures in flight may read the slot
     if (r) return r;
     HCHK(hipStreamSynchronize(c->st));
-    pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc, c->ps);
+    if (!pack_planes(c->h_stage_ref, c->W, c->H, y, u, v, sy, sc, c->ps, c->maxv)) return JMH_E_INVALID_ARG;
     HCHK(hipMemcpyAsync(c->d_slots + (size_t)slot * c->fsize, c->h_stage_ref, c->fsize, hipMemcpyHostToDevice, c->st));
     HCHK(hipStreamSynchronize(c->st));
     return JMH_OK;

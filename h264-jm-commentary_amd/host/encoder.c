@@ -111,10 +111,12 @@ static int encode_picture_slices(jm86_img *im, const jm_seq *s, const jm_slice *
     im->writer = NULL;
     if (s->entropy_coding) {
         /* cabac_zero_words (7.4.2.10, 9.3.4.6): BinCountsInNALunits <= 32/3 * NumBytesInVclNALunits
-           + RawMbBits * PicSizeInMbs / 32 (RawMbBits = 3072 at 8-bit 4:2:0); scaled by 3.  Each word
+           + RawMbBits * PicSizeInMbs / 32 (4:2:0: RawMbBits = 256 * BitDepthY + 128 * BitDepthC, 3072 at
+           8 bits, 3840 at High 10); scaled by 3, so 3 * RawMbBits / 32 = 36 * BitDepth per MB.  Each word
            appended to the last slice is 0x000003 in the byte stream (emulation prevention). */
         const long bytes = out->len - len0 - 4L * nslices;          /* NAL units, no start codes */
-        const long excess = 3 * bins - 288L * nmb - 32 * bytes;
+        const int bd = s->bit_depth > 8 ? s->bit_depth : 8;
+        const long excess = 3 * bins - 36L * bd * nmb - 32 * bytes;
         for (long z = excess > 0 ? (excess + 95) / 96 : 0; z > 0; z--) {
             static const uint8_t zw[3] = {0, 0, 3};
             jm_bits t = {(uint8_t *)zw, 3, 3, 0, 0};

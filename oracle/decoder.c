@@ -151,7 +151,7 @@ typedef struct {
     int cbfc[2];          /* chroma AC blocks                                                */
 } mbinfo;
 
-typedef struct { br_t *b; uint32_t range, ofs; uint8_t st[460], mps[460]; } cabd_t;
+typedef struct { br_t *b; uint32_t range, ofs; uint8_t st[JMO_NCTX], mps[JMO_NCTX]; } cabd_t;
 
 struct jmo_dec {
     char err[256];
@@ -761,8 +761,9 @@ static int parse_cavlc(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int t, 
 }
 
 /* ---- CABAC parsing (9.3): arithmetic decoding engine, initialisation, binarisations ----- */
-/* Table 9-44 (own copy; the encoder's is in host/cabac.c) */
-static const uint8_t lps_range[64][4] = {
+/* Table 9-44 (own copy; the encoder's is in host/cabac.c).  Shared with the oracle's RD-rate
+   encoder (cabac_enc.c), which has no other tie to this decoder */
+const uint8_t jmo_lps_range[64][4] = {
     {128, 176, 208, 240}, {128, 167, 197, 227}, {128, 158, 187, 216}, {123, 150, 178, 205}, {116, 142, 169, 195}, {111, 135, 160, 185},
     {105, 128, 152, 175}, {100, 122, 144, 166}, {95, 116, 137, 158},  {90, 110, 130, 150},  {85, 104, 123, 142},  {81, 99, 117, 135},
     {77, 94, 111, 128},   {73, 89, 105, 122},   {69, 85, 100, 116},   {66, 80, 95, 110},    {62, 76, 90, 104},    {59, 72, 86, 99},
@@ -774,7 +775,7 @@ static const uint8_t lps_range[64][4] = {
     {12, 14, 17, 20},     {11, 14, 16, 19},     {11, 13, 15, 18},     {10, 12, 15, 17},     {10, 12, 14, 16},     {9, 11, 13, 15},
     {9, 11, 12, 14},      {8, 10, 12, 14},      {8, 9, 11, 13},       {7, 9, 11, 12},       {7, 9, 10, 12},       {7, 8, 10, 11},
     {6, 8, 9, 11},        {6, 7, 9, 10},        {6, 7, 8, 9},         {2, 2, 2, 2}};
-static const uint8_t lps_next[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12, 13, 13, 15, 15, 16, 16,
+const uint8_t jmo_lps_next[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12, 13, 13, 15, 15, 16, 16,
                                      18, 18, 19, 19, 21, 21, 22, 22, 23, 24, 24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30,
                                      31, 32, 32, 33, 33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
 /* Tables 9-12 .. 9-33 as runs of consecutive ctxIdx: {first ctxIdx, count} then (m, n) pairs;
@@ -845,25 +846,30 @@ static const int16_t ctxinit_P0[] = {
     426, 10, -6, 66, -7, 35, -7, 42, -8, 45, -5, 48, -12, 56, -6, 60, -5, 62, -8, 66, -8, 76,
     -1};
 
-static void cabd_start(cabd_t *c, br_t *b, int slice_i, int qp) {
+/* 9.3.1.1: every context this codec uses (spec ctxIdx, < JMO_NCTX) for an I slice or cabac_init_idc 0 */
+void jmo_cabac_init_models(int slice_i, int qp, uint8_t *st, uint8_t *mps) {
     const int16_t *t = slice_i ? ctxinit_I : ctxinit_P0;
-    memset(c->st, 0, sizeof c->st);
-    memset(c->mps, 0, sizeof c->mps);
-    while (*t >= 0) {                               /* 9.3.1.1 */
+    memset(st, 0, JMO_NCTX);
+    memset(mps, 0, JMO_NCTX);
+    while (*t >= 0) {
         int first = t[0], cnt = t[1];
         t += 2;
         for (int i = 0; i < cnt; i++, t += 2) {
             int pre = iclip(1, 126, ((t[0] * iclip(0, 51, qp)) >> 4) + t[1]);
-            c->st[first + i] = (uint8_t)(pre <= 63 ? 63 - pre : pre - 64);
-            c->mps[first + i] = pre > 63;
+            st[first + i] = (uint8_t)(pre <= 63 ? 63 - pre : pre - 64);
+            mps[first + i] = pre > 63;
         }
     }
+}
+
+static void cabd_start(cabd_t *c, br_t *b, int slice_i, int qp) {
+    jmo_cabac_init_models(slice_i, qp, c->st, c->mps);
     c->b = b;
     c->range = 510;                                 /* 9.3.1.2 */
     c->ofs = rbits(b, 9);
 }
 static int cdec(cabd_t *c, int ctx) {               /* DecodeDecision (9.3.3.2.1) */
-    uint32_t lps = lps_range[c->st[ctx]][(c->range >> 6) & 3];
+    uint32_t lps = jmo_lps_range[c->st[ctx]][(c->range >> 6) & 3];
     int bin;
     c->range -= lps;
     if (c->ofs >= c->range) {
@@ -871,7 +877,7 @@ static int cdec(cabd_t *c, int ctx) {               /* DecodeDecision (9.3.3.2.1
         c->ofs -= c->range;
         c->range = lps;
         if (!c->st[ctx]) c->mps[ctx] = !c->mps[ctx];
-        c->st[ctx] = lps_next[c->st[ctx]];
+        c->st[ctx] = jmo_lps_next[c->st[ctx]];
     } else {
         bin = c->mps[ctx];
         if (c->st[ctx] < 62) c->st[ctx]++;
@@ -897,14 +903,16 @@ static unsigned ceg_bypass(cabd_t *c, int k) {       /* k-th order Exp-Golomb su
     return v;
 }
 
+/* Table 9-43: 8x8 frame significant / last ctxIdxInc by scanning position (shared with cabac_enc.c) */
+const uint8_t jmo_sig8x8_inc[63] = {0, 1, 2, 3, 4, 5, 5, 4, 4, 3, 3, 4, 4, 4, 5, 5, 4, 4, 4, 4, 3, 3, 6, 7, 7, 7, 8, 9, 10, 9, 8, 7,
+                                   7, 6, 11, 12, 13, 11, 6, 7, 8, 9, 14, 10, 9, 8, 6, 11, 12, 13, 11, 6, 9, 14, 10, 9, 11, 12, 13, 11, 14, 10, 12};
+const uint8_t jmo_last8x8_inc[63] = {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
+                                   3, 3, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7, 8, 8, 8};
+
 /* residual_block_cabac: coef[0..n) scan order; cbfctx < 0: coded_block_flag not coded (8x8) */
 static int cabac_block(cabd_t *c, int cat, int n, int cbfctx, int *coef) {
     static const int so[5] = {0, 15, 29, 44, 47}, ao[5] = {0, 10, 20, 30, 39};
-    /* Table 9-43: 8x8 frame significant / last ctxIdxInc by scanning position */
-    static const uint8_t s8[63] = {0, 1, 2, 3, 4, 5, 5, 4, 4, 3, 3, 4, 4, 4, 5, 5, 4, 4, 4, 4, 3, 3, 6, 7, 7, 7, 8, 9, 10, 9, 8, 7,
-                                   7, 6, 11, 12, 13, 11, 6, 7, 8, 9, 14, 10, 9, 8, 6, 11, 12, 13, 11, 6, 9, 14, 10, 9, 11, 12, 13, 11, 14, 10, 12};
-    static const uint8_t l8[63] = {0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
-                                   3, 3, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7, 8, 8, 8};
+    const uint8_t *s8 = jmo_sig8x8_inc, *l8 = jmo_last8x8_inc;
     for (int i = 0; i < n; i++) coef[i] = 0;
     if (cbfctx >= 0 && !cdec(c, cbfctx)) return 0;
     int sbase = cat == 5 ? 402 : 105 + so[cat], lbase = cat == 5 ? 417 : 166 + so[cat], abase = cat == 5 ? 426 : 227 + ao[cat];

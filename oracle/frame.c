@@ -59,9 +59,10 @@ int jmo_create(const jmh_config *cfg, jmo_ctx **out) {
     c->mbintra = calloc((size_t)c->mbw * c->mbh, 1);
     c->res = calloc((size_t)c->mbw * c->mbh, sizeof(jmh_mb_result));
     c->blocksad = malloc(sizeof(uint16_t) * 16 * (size_t)c->npos);
-    c->mbi = calloc((size_t)c->mbw * c->mbh, sizeof(jmr_mbinfo));
+    c->cabi = calloc((size_t)c->mbw * c->mbh, sizeof(jmo_cabmbi));
+    c->cab_mvd = calloc((size_t)(c->W / 4) * (c->H / 4) * 2, sizeof(int16_t));
     c->epzs_fp = calloc(8 * n4, sizeof(uint16_t));
-    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref || !c->mbi || !c->epzs_fp) { jmo_destroy(c); return JMH_E_OOM; }
+    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref || !c->cabi || !c->cab_mvd || !c->epzs_fp) { jmo_destroy(c); return JMH_E_OOM; }
     memset(c->refidx, -1, n4);                             /* no previous picture: no motion */
     *out = c;
     return JMH_OK;
@@ -74,7 +75,7 @@ void jmo_destroy(jmo_ctx *c) {
     free(c->refY); free(c->refU); free(c->refV);
     free(c->recY); free(c->recU); free(c->recV);
     free(c->qpel); free(c->mv); free(c->refidx); free(c->ipred); free(c->mbintra);
-    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref); free(c->mbi); free(c->epzs_fp);
+    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref); free(c->cabi); free(c->cab_mvd); free(c->epzs_fp);
     free(c);
 }
 

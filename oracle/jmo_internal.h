@@ -5,7 +5,6 @@
 #include <stdint.h>
 #include <string.h>
 #include "jm_oracle.h"
-#include "../h264-jm-commentary_amd/csrc/jmh_cabac_rate.h"
 
 #define MAX_VALUE 999999          /* JM 8.6 defines.h MAX_VALUE [J]                       */
 #define Q_BITS 15                 /* JM 8.6 defines.h Q_BITS [J]                          */
@@ -36,6 +35,75 @@ static inline int clip255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 typedef uint16_t pel;
 static inline int clipv(int maxv, int v) { return v < 0 ? 0 : (v > maxv ? maxv : v); }
 static inline int isign(int a, int b) { return b < 0 ? -iabs(a) : iabs(a); } /* JM sign(a,b) */
+
+/* ---- the oracle's CABAC coder for RD rates (cabac_enc.c; the tables are decoder.c's) ------- */
+#define JMO_NCTX 460                 /* spec ctxIdx 0..459 (frame coding, 4:2:0)                 */
+extern const uint8_t jmo_lps_range[64][4];   /* Table 9-44 rangeTabLPS                         */
+extern const uint8_t jmo_lps_next[64];       /*            transIdxLPS                         */
+extern const uint8_t jmo_sig8x8_inc[63], jmo_last8x8_inc[63];   /* Table 9-43 (frame)          */
+void jmo_cabac_init_models(int slice_i, int qp, uint8_t *st, uint8_t *mps);   /* 9.3.1.1        */
+typedef struct jmo_cab {
+    uint8_t st[JMO_NCTX], mps[JMO_NCTX];     /* pStateIdx, valMPS                               */
+    uint32_t low, range;                     /* codILow, codIRange                              */
+    int first, outstanding;                  /* firstBitFlag, bitsOutstanding                   */
+    long put;                                /* bits PutBit emitted (the first one included)    */
+} jmo_cab;
+typedef struct jmo_cabmbi {                  /* a coded macroblock, for its neighbours' ctxIdxInc */
+    uint8_t skip, intra, i16, nxn, t8;       /* P_Skip, intra, I_16x16, I_NxN, transform_size_8x8_flag */
+    uint8_t cbp, cmode, cbf_dc, cbfc[2];     /* cbp; intra_chroma_pred_mode; coded_block_flags: DC
+                                                (bit 0 luma, 1 Cb, 2 Cr), chroma AC (2x2 raster)  */
+    uint16_t cbf4;                           /* luma 4x4 coded_block_flags (raster; an 8x8-transform
+                                                block's inferred 1 on its four)                    */
+} jmo_cabmbi;
+typedef struct jmo_cabnb {                   /* the current macroblock's neighbours A, B          */
+    const jmo_cabmbi *A, *B;                 /* NULL: not available                              */
+    int16_t mvdA[4][2], mvdB[4][2];          /* mvd_l0 of A's right column, of B's bottom row     */
+} jmo_cabnb;
+typedef struct jmo_cabsyn {                  /* the syntax of a macroblock candidate               */
+    int mb_type, cbp, t8, i16mode, cmode;
+    int b8mode[4];
+    int ipm[16];                             /* I4MB raster / I8MB on each 8x8's top-left: -1 = the
+                                                predicted mode, else rem_intra_pred_mode           */
+    int16_t mvd[16][2];                      /* the mvd of the partition covering each 4x4 (raster) */
+    const int16_t (*luma)[16];               /* as jmh_mb_result.luma / luma_dc / chroma_*        */
+    const int16_t *luma_dc;
+    const int16_t (*cdc)[4];
+    const int16_t (*cac)[4][16];
+} jmo_cabsyn;
+typedef struct jmo_cabcur {                  /* the P8x8 RD loop's running macroblock state        */
+    int16_t mvd[16][2];
+    uint16_t cbf4;
+    uint8_t cbpl;
+} jmo_cabcur;
+void jmo_cab_start(jmo_cab *e, int slice_i, int qp);
+long jmo_cab_bits(const jmo_cab *e);         /* JM's arienco_bits_written                         */
+void jmo_cab_decision(jmo_cab *e, int ctx, int bin);
+void jmo_cab_bypass(jmo_cab *e, int bin);
+void jmo_cab_terminate(jmo_cab *e, int bin);
+void jmo_cab_skip(jmo_cab *e, const jmo_cabnb *nb);
+void jmo_cab_mb(jmo_cab *e, const jmo_cabnb *nb, const jmo_cabsyn *m, int slice_p, int t8mode, jmo_cabmbi *out,
+                int16_t mvd_out[16][2]);
+void jmo_cab_b8(jmo_cab *e, const jmo_cabnb *nb, jmo_cabcur *cur, int b8, int sm, const int16_t (*mvd4)[2], int coded,
+                const int16_t (*lev4)[16]);
+void jmo_cab_i4(jmo_cab *e, const jmo_cabnb *nb, int x4, int y4, int code, const int16_t *lev);
+
+/* Test hook (tests/csrc/rate_xcheck.c): every RD rate the oracle computes, with the coder state,
+ * neighbours and syntax it was computed from and the state after; NULL in normal use */
+enum { JMO_RATE_SKIP, JMO_RATE_MB, JMO_RATE_B8, JMO_RATE_I4 };
+typedef struct jmo_rate_event {
+    int kind, slice_p, t8mode;
+    const jmo_cab *before, *after;
+    const jmo_cabnb *nb;
+    const jmo_cabsyn *syn;                   /* JMO_RATE_MB                                       */
+    const jmo_cabcur *cur_before;            /* JMO_RATE_B8                                       */
+    int b8, sm, coded;
+    const int16_t (*mvd4)[2];
+    const int16_t (*lev4)[16];
+    int x4, y4, code;                        /* JMO_RATE_I4                                       */
+    const int16_t *lev;
+    long bits;                               /* the oracle's rate                                 */
+} jmo_rate_event;
+extern void (*jmo_rate_hook)(const jmo_rate_event *ev);
 
 /* ---- encoder state (replaces JM's img/enc_picture globals for the hot path) ------------ */
 struct jmo_ctx {
@@ -72,11 +140,11 @@ struct jmo_ctx {
     uint16_t *epzs_fp;               /* [8][(H/4)*(W/4)]: each search's full-pel cost (saturated at
                                         65535) per block type and 4x4: the neighbours' distortion of
                                         EPZSDetermineStopCriterion (item 61)                     */
-    /* RDOptimization = 1: the slice's CABAC coding state (contexts + codIRange, jmh_cabac_rate.h)
-       and what every coded macroblock leaves for its neighbours' context selection */
-    uint8_t cab_st[JMR_NCTX];
-    uint32_t cab_range;
-    jmr_mbinfo *mbi;
+    /* RDOptimization = 1: the slice's CABAC coder (cabac_enc.c), what every coded macroblock leaves
+       for its neighbours' context selection, and the mvd_l0 of every 4x4 block */
+    jmo_cab cab;
+    jmo_cabmbi *cabi;
+    int16_t *cab_mvd;                /* [(H/4)*(W/4)][2] */
 };
 
 /* SliceMode 1 (SliceArgument MBs per slice, raster order): MB addresses a and n lie in one slice.

@@ -6,17 +6,17 @@
  *   rdopt.c › encode_one_macroblock (the `input->rdopt` branches), RDCost_for_macroblocks,
  *             RDCost_for_8x8blocks, RDCost_for_4x4IntraBlocks, Mode_Decision_for_4x4IntraBlocks,
  *             SetCoeffAndReconstruction8x8, store_macroblock_parameters
- *   rdopt_coding_state.c › store_coding_state / reset_coding_state (a copy of the context states
- *             and codIRange: the only coding state a CABAC rate depends on, jmh_cabac_rate.h)
+ *   rdopt_coding_state.c › store_coding_state / reset_coding_state (a copy of the oracle's CABAC
+ *             coder, cabac_enc.c: contexts, codILow, codIRange, outstanding bits)
  * with the entropy coder CABAC (SymbolMode 1) and the 4x4 transform (Transform8x8Mode 0).
  * Every non-normative choice is an item of docs/JM_SEMANTICS.md (53-60):
  *   - lambda_mode = fp.lambda_rd (0.85 * 2^((QP + QpBdOffsetY - 12) / 3), host libm), the searches'
  *     LAMBDA_FACTOR(sqrt(lambda_mode)) = fp.lambda_factor_rd; rdcost = (double)D + lambda * rate;
  *     candidates compared with strict '<' in JM's order;
  *   - D = SSD of the reconstruction (luma 16x16 + both 8x8 chroma) for the macroblock loop, of the
- *     8x8 / 4x4 luma block in the sub-decisions; rate = jmh_cabac_rate.h bits from the slice's
- *     coding state at the start of the macroblock (the P8x8 loop: the running state after the
- *     decided 8x8 blocks);
+ *     8x8 / 4x4 luma block in the sub-decisions; rate = arienco_bits_written deltas of the oracle's
+ *     own CABAC coder (cabac_enc.c) from the slice's coding state at the start of the macroblock
+ *     (the P8x8 loop: the running state after the decided 8x8 blocks);
  *   - the motion searches are the RDO-off ones (items 3-10, 33-40) at the RDO lambda without the
  *     16x16 zero-vector biases (!input->rdopt) and with the RDO-off centre clamp kept (item 54).
  */
@@ -111,19 +111,27 @@ static void chroma_code(const mbs *s, int qpc, int rnd, const pel (*ipred)[4][64
     }
 }
 
-static void fill_cand(jmr_cand *r, const lcand *L, const ccand *C, int cm) {
+static void fill_syn(jmo_cabsyn *r, const lcand *L, const ccand *C, int cm) {
     memset(r, 0, sizeof(*r));
     r->mb_type = L->mode;
     r->cbp = L->cbp | C->cbpc << 4;
     r->i16mode = L->i16mode;
     r->cmode = cm;
     for (int b = 0; b < 4; b++) r->b8mode[b] = L->b8mode[b];
-    r->ipm = L->ipm;
-    r->mvd = (const int16_t(*)[2])L->mvd;
+    for (int q = 0; q < 16; q++) { r->ipm[q] = L->ipm[q]; r->mvd[q][0] = L->mvd[q][0]; r->mvd[q][1] = L->mvd[q][1]; }
     r->luma = (const int16_t(*)[16])L->luma;
     r->luma_dc = L->luma_dc;
     r->cdc = (const int16_t(*)[4])C->dc;
     r->cac = (const int16_t(*)[4][16])C->ac;
+}
+
+/* the rate of one RD candidate: the bits the coder emits from `before` (hooked for the tests) */
+static long rate_of(jmo_rate_event *ev, const jmo_cab *before, const jmo_cab *after) {
+    ev->before = before;
+    ev->after = after;
+    ev->bits = jmo_cab_bits(after) - jmo_cab_bits(before);
+    if (jmo_rate_hook) jmo_rate_hook(ev);
+    return ev->bits;
 }
 
 void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
@@ -149,12 +157,19 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
     }
     /* the slice's coding state: initialised at its first macroblock (9.3.1) */
     const int a = s->mb_addr, nmb = c->mbw * c->mbh, k = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : nmb;
-    if (a % k == 0) { jmr_init_contexts(c->cab_st, !s->slice_p, qpy); c->cab_range = 510; }
-    const jmr_mbinfo *A = mbx > 0 && jmo_same_slice(c, a, a - 1) ? &c->mbi[a - 1] : NULL;
-    const jmr_mbinfo *B = mby > 0 && jmo_same_slice(c, a, a - c->mbw) ? &c->mbi[a - c->mbw] : NULL;
-    uint8_t st[JMR_NCTX];
-    jmr_eng e;
-#define RATE_BEGIN() (memcpy(st, c->cab_st, JMR_NCTX), e.st = st, e.range = c->cab_range, e.bits = 0)
+    if (a % k == 0) jmo_cab_start(&c->cab, !s->slice_p, qpy);
+    jmo_cabnb nb;
+    memset(&nb, 0, sizeof(nb));
+    nb.A = mbx > 0 && jmo_same_slice(c, a, a - 1) ? &c->cabi[a - 1] : NULL;
+    nb.B = mby > 0 && jmo_same_slice(c, a, a - c->mbw) ? &c->cabi[a - c->mbw] : NULL;
+    for (int r = 0; r < 4; r++)
+        for (int comp = 0; comp < 2; comp++) {
+            if (nb.A) nb.mvdA[r][comp] = c->cab_mvd[2 * ((4 * mby + r) * W4 + 4 * mbx - 1) + comp];
+            if (nb.B) nb.mvdB[r][comp] = c->cab_mvd[2 * ((4 * mby - 1) * W4 + 4 * mbx + r) + comp];
+        }
+    jmo_cab e;
+    jmo_rate_event ev;
+#define RATE_BEGIN(kind_) (e = c->cab, memset(&ev, 0, sizeof(ev)), ev.kind = (kind_), ev.slice_p = s->slice_p, ev.nb = &nb)
 
     const int *isr = c->cfg.inter_search;
     int valid[9] = {0};
@@ -174,11 +189,11 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
             lcand *P = &Lc[4];
             memset(P, 0, sizeof(*P));
             P->mode = JMH_P8x8;
-            uint8_t st8[JMR_NCTX], stb[JMR_NCTX];
-            memcpy(st8, c->cab_st, JMR_NCTX);
-            uint32_t rg8 = c->cab_range, rgb = 0;
-            jmr_cur cur, curb;
+            static jmo_cab st8, stb, stc;
+            st8 = c->cab;
+            jmo_cabcur cur, curb;
             memset(&cur, 0, sizeof(cur));
+            curb = cur;
             pel pred8[256], rec8[256];
             int cnt_nonz = 0;
             for (int block = 0; block < 4; block++) {
@@ -218,20 +233,24 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                         mvd[b4][0] = (int16_t)(s->all_mv[mode][kk][0] - s->pmv[mode][kk][0]);
                         mvd[b4][1] = (int16_t)(s->all_mv[mode][kk][1] - s->pmv[mode][kk][1]);
                     }
-                    uint8_t stc[JMR_NCTX];
-                    memcpy(stc, st8, JMR_NCTX);
-                    jmr_eng eb = {stc, rg8, 0};
-                    jmr_cur cc = cur;
-                    jmr_b8(&eb, A, B, &cc, block, mode, (const int16_t(*)[2])mvd, cost > 0, (const int16_t(*)[16])lev);
-                    double rd = (double)D + lam * (double)eb.bits;
+                    stc = st8;
+                    jmo_cabcur cc = cur;
+                    jmo_cab_b8(&stc, &nb, &cc, block, mode, (const int16_t(*)[2])mvd, cost > 0, (const int16_t(*)[16])lev);
+                    jmo_rate_event eb;
+                    memset(&eb, 0, sizeof(eb));
+                    eb.kind = JMO_RATE_B8; eb.slice_p = 1; eb.nb = &nb; eb.cur_before = &cur;
+                    eb.b8 = block; eb.sm = mode; eb.coded = cost > 0;
+                    eb.mvd4 = (const int16_t(*)[2])mvd; eb.lev4 = (const int16_t(*)[16])lev;
+                    const long bits = rate_of(&eb, &st8, &stc);
+                    double rd = (double)D + lam * (double)bits;
                     if (rd < best) {
                         best = rd; bm = mode; bcost = cost; bcbp = cbpbit; bblk = blk;
                         memcpy(blev, lev, sizeof(blev)); memcpy(bpred, p8, sizeof(bpred)); memcpy(brec, r8, sizeof(brec));
-                        memcpy(stb, stc, JMR_NCTX); rgb = eb.range; curb = cc;
+                        stb = stc; curb = cc;
                     }
                 }
                 /* the block's decision: coding state, SetRefAndMotionVectors, stored coefficients */
-                memcpy(st8, stb, JMR_NCTX); rg8 = rgb; cur = curb;
+                st8 = stb; cur = curb;
                 P->b8mode[block] = bm;
                 jmo_write_enc_mv(s, 2 * (block & 1), 2 * (block >> 1), 2, 2, s->all_mv[bm]);
                 for (int b4 = 0; b4 < 4; b4++) {
@@ -327,9 +346,10 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                     int dummy = 0;
                     int nz = jmo_dct_luma4x4(r, ip[m], 4, qp, rnd, lev, &dummy, rec4, 4, maxv);
                     int D = ssd(s->org + by * 16 + bx, 16, rec4, 4, 4, 4);
-                    RATE_BEGIN();
-                    jmr_i4(&e, A, B, bx >> 2, by >> 2, m == mpm ? -1 : m < mpm ? m : m - 1, lev);
-                    double rd = (double)D + lam * (double)e.bits;
+                    RATE_BEGIN(JMO_RATE_I4);
+                    ev.x4 = bx >> 2; ev.y4 = by >> 2; ev.code = m == mpm ? -1 : m < mpm ? m : m - 1; ev.lev = lev;
+                    jmo_cab_i4(&e, &nb, ev.x4, ev.y4, ev.code, lev);
+                    double rd = (double)D + lam * (double)rate_of(&ev, &c->cab, &e);
                     if (rd < best) { best = rd; bmode = m; bnz = nz; memcpy(blev, lev, sizeof(blev)); memcpy(brec, rec4, sizeof(brec)); }
                 }
                 c->ipred[((s->pix_y + by) >> 2) * W4 + ((s->pix_x + bx) >> 2)] = (int8_t)bmode;
@@ -365,17 +385,19 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
             int i = order[oi], intra = i >= 5;
             if (!have[i] || (cm != 0 && !intra)) continue;
             const ccand *C = intra ? &Ci[cm] : &Cc[i];
-            RATE_BEGIN();
-            if (i == 0) jmr_skip(&e, A, B, NULL);
-            else {
-                jmr_cand r;
-                int16_t mvw[16][2];
-                fill_cand(&r, &Lc[i], C, intra ? cm : 0);
-                r.mvw = mvw;
-                jmr_mb(&e, A, B, &r, s->slice_p, 0, NULL);
+            jmo_cabsyn r;
+            if (i == 0) {
+                RATE_BEGIN(JMO_RATE_SKIP);
+                jmo_cab_skip(&e, &nb);
+            } else {
+                RATE_BEGIN(JMO_RATE_MB);
+                fill_syn(&r, &Lc[i], C, intra ? cm : 0);
+                ev.syn = &r;
+                jmo_cab_mb(&e, &nb, &r, s->slice_p, 0, NULL, NULL);
             }
-            double rd = (double)(Lc[i].dist + C->dist) + lam * (double)e.bits;
-            if (rd < min_rd) { min_rd = rd; bi = i; bcm = intra ? cm : 0; brate = e.bits; }
+            const long bits = rate_of(&ev, &c->cab, &e);
+            double rd = (double)(Lc[i].dist + C->dist) + lam * (double)bits;
+            if (rd < min_rd) { min_rd = rd; bi = i; bcm = intra ? cm : 0; brate = (int)bits; }
         }
     }
 
@@ -417,18 +439,25 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
         pel *R = uv ? c->recV : c->recU;
         for (int y = 0; y < 8; y++) memcpy(R + ((s->pix_y >> 1) + y) * c->Wc + (s->pix_x >> 1), C->rec[uv] + 8 * y, 8 * sizeof(pel));
     }
-    /* write_one_macroblock: the coding state advances by the chosen macroblock, then the
-       end_of_slice_flag (0) unless the slice ends here */
-    e.st = c->cab_st; e.range = c->cab_range; e.bits = 0;
-    if (bi == 0) jmr_skip(&e, A, B, &c->mbi[a]);
-    else {
-        jmr_cand r;
-        int16_t mvw[16][2];
-        fill_cand(&r, L, C, is_intra ? bcm : 0);
-        r.mvw = mvw;
-        jmr_mb(&e, A, B, &r, s->slice_p, 0, &c->mbi[a]);
+    /* write_one_macroblock: the coding state advances by the chosen macroblock (what it leaves for
+       its neighbours' contexts: jmo_cabmbi, the mvds of its 4x4 blocks), then the end_of_slice_flag
+       (0) unless the slice ends here */
+    int16_t mvd[16][2];
+    memset(mvd, 0, sizeof(mvd));
+    if (bi == 0) {
+        jmo_cab_skip(&c->cab, &nb);
+        memset(&c->cabi[a], 0, sizeof(c->cabi[a]));
+        c->cabi[a].skip = 1;
+    } else {
+        jmo_cabsyn r;
+        fill_syn(&r, L, C, is_intra ? bcm : 0);
+        jmo_cab_mb(&c->cab, &nb, &r, s->slice_p, 0, &c->cabi[a], mvd);
     }
-    if ((a + 1) % k != 0 && a + 1 < nmb) jmr_end_of_mb(&e);
-    c->cab_range = e.range;
+    for (int q = 0; q < 16; q++) {
+        const int pa = ((s->pix_y >> 2) + (q >> 2)) * W4 + (s->pix_x >> 2) + (q & 3);
+        c->cab_mvd[2 * pa] = mvd[q][0];
+        c->cab_mvd[2 * pa + 1] = mvd[q][1];
+    }
+    if ((a + 1) % k != 0 && a + 1 < nmb) jmo_cab_terminate(&c->cab, 0);
 #undef RATE_BEGIN
 }

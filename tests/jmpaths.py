@@ -11,16 +11,18 @@ LIBJMHIP = os.path.join(PKG, "csrc", "libjmhip.so")
 LIBJMHOST = os.path.join(PKG, "host", "build", "libjmhost.so")
 LENCOD = os.path.join(PKG, "host", "build", "lencod")
 LIBORACLE = os.path.join(ORACLE, "_build", "liboracle.so")
-LENCOD_CPU = os.path.join(ORACLE, "_build", "lencod_cpu")
+HARNESS = os.path.join(ROOT, "tests", "harness")
+LENCOD_CPU = os.path.join(HARNESS, "_build", "lencod_cpu")
+LENCOD_XCHECK = os.path.join(HARNESS, "_build", "lencod_xcheck")
 JMDEC = os.path.join(ORACLE, "_build", "jmdec")
-JM86_CHECK = os.path.join(ORACLE, "_build", "jm86_check")
+JM86_CHECK = os.path.join(HARNESS, "_build", "jm86_check")
 HEADER = os.path.join(ROOT, "include", "jmhip.h")
 
 
 def ensure_built():
-    need = [LIBJMHOST, LIBORACLE, LENCOD_CPU, JMDEC]
+    need = [LIBJMHOST, LIBORACLE, LENCOD_CPU, LENCOD_XCHECK, JMDEC]
     if not all(os.path.exists(p) for p in need):
-        subprocess.run(["make", "-s", "-C", ROOT, "oracle"], check=True)
+        subprocess.run(["make", "-s", "-C", ROOT, "harness"], check=True)
 
 
 def load_jmhip():

@@ -5,6 +5,7 @@ a3-a8 motion search (through whole-picture results), a9 mode decision, a10-a14 T
 and the lencod bitstream end to end.  Sizes are chosen so the oracle finishes in seconds;
 the 1080p cases use the size-independent closed-loop property (decoder output == recon).
 """
+import ctypes
 import os
 import subprocess
 import tempfile
@@ -525,6 +526,17 @@ def test_high10_rejects_other_search_modes_and_8bit_calls():
     assert e.lib.jmh_set_reference(e.ctx, 0, 0, y8[0].ctypes.data, y8[1].ctypes.data, y8[2].ctypes.data, 64, 32) == jmhip.JMH_E_UNSUPPORTED_CFG
     big = [np.full(s, 1024, np.uint16) for s in ((48, 64), (24, 32), (24, 32))]   # out of range for 10 bits
     assert e.lib.jmh_set_reference_u16(e.ctx, 0, 0, big[0].ctypes.data, big[1].ctypes.data, big[2].ctypes.data, 64, 32) == jmhip.JMH_E_INVALID_ARG
+    # one sample above 1023 (the last Cr sample) rejects a push / load (checked while packing) and
+    # leaves the context usable
+    ok = [np.full(s, 1023, np.uint16) for s in ((48, 64), (24, 32), (24, 32))]
+    one = [p.copy() for p in ok]
+    one[2][23, 31] = 1024
+    fp = jmhip.frame_params(jmhip.JMH_I_SLICE, 28, bit_depth=10)
+    ptrs = [p.ctypes.data for p in one]
+    assert e.lib.jmh_frame_push_u16(e.ctx, *ptrs, 64, 32, ctypes.byref(fp)) == jmhip.JMH_E_INVALID_ARG
+    assert e.lib.jmh_load_frame_u16(e.ctx, 0, *ptrs, 64, 32) == jmhip.JMH_E_INVALID_ARG
+    res, rec = e.encode(*ok, jmhip.JMH_I_SLICE, 28)
+    assert int(rec[0].max()) <= 1023
 
 
 # ---------------- end to end: lencod bitstream + recon, closed loop ----------------

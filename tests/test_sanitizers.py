@@ -1,7 +1,7 @@
 """AddressSanitizer + UndefinedBehaviorSanitizer runs of the host code: the CPU
-encoder (oracle/lencod_cpu.c driving the product's host plumbing — cfg, yuv, bitstream, deblock,
+encoder (tests/harness/lencod_cpu.c driving the product's host plumbing — cfg, yuv, bitstream, deblock,
 encoder loop with its writer threads, the JM 8.6 call surface) and the spec decoder, built by
-`make -C oracle sanitize` with -fsanitize=address,undefined -fno-sanitize-recover=undefined, on
+`make -C tests/harness sanitize` with -fsanitize=address,undefined -fno-sanitize-recover=undefined, on
 the closed-loop configurations.  Any report aborts the process, so a clean exit plus the
 closed-loop equality (decoder output == encoder reconstruction) is the check.  GPU-side ASan is
 not available on this pool; the device code is covered by the parity tests instead."""
@@ -12,10 +12,10 @@ import tempfile
 
 import pytest
 
-from jmpaths import ORACLE
+from jmpaths import HARNESS
 from test_closed_loop import CABAC, CONFIGS
 
-ASAN = os.path.join(ORACLE, "_build_asan")
+ASAN = os.path.join(HARNESS, "_build_asan")
 LENCOD_ASAN = os.path.join(ASAN, "lencod_cpu")
 JMDEC_ASAN = os.path.join(ASAN, "jmdec")
 
@@ -36,9 +36,9 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=86
 @pytest.fixture(scope="module")
 def sanitized():
     # one build at a time (pytest-xdist workers each run this fixture)
-    with open(os.path.join(ORACLE, ".sanitize.lock"), "w") as lk:
+    with open(os.path.join(HARNESS, ".sanitize.lock"), "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
-        r = subprocess.run(["make", "-s", "-C", ORACLE, "sanitize"], capture_output=True, text=True)
+        r = subprocess.run(["make", "-s", "-C", HARNESS, "sanitize"], capture_output=True, text=True)
     if r.returncode != 0:
         pytest.fail("sanitizer build failed:\n" + r.stdout + r.stderr)
     return LENCOD_ASAN, JMDEC_ASAN

@@ -20,7 +20,8 @@
 #   lencodc5 lencodc3 with one slice and with SliceArgument 240 (135 one-row slices per picture)
 #   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
 #   profc3  the same for config 3
-#   pmc     tools/pmc_traffic.sh (HBM bytes + SQ counters, separate passes)
+#   pmc     tools/pmc_traffic.sh (HBM bytes + SQ counters, separate passes), config 2
+#   pmc3 / pmc5  the same for config 3 / config 5 (RDO on)
 #   lencod  the product lencod end to end on an I420 file (tools/make_yuv.py), 1080p, 60 pictures
 #           (FFS SR 32), WriterThreads 0 / 4 / 8 -> gpurun_out/TAG_lencod1080_w*.log
 #   lencodc3 the same for the config-3 shape (2160p High, EPZS + 8x8), 30 pictures, 8 writers
@@ -104,6 +105,8 @@ for s in "$@"; do
               tail -3 gpurun_out/${TAG}_lencod2160_slices$sl.log
             done ;;
     pmc)    run pmc 900 bash tools/pmc_traffic.sh "$TAG" || exit $? ;;
+    pmc3)   run pmc3 900 bash tools/pmc_traffic.sh "${TAG}_c3" 30 3 || exit $? ;;
+    pmc5)   run pmc5 900 bash tools/pmc_traffic.sh "${TAG}_c5" 30 5 || exit $? ;;
     *)      echo "unknown step $s"; exit 2 ;;
   esac
 done

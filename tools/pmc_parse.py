@@ -14,9 +14,24 @@ import sys
 from collections import defaultdict
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r1"
-steps = int(sys.argv[2]) if len(sys.argv) > 2 else 30       # P pictures encoded in total (warmup + timed)
+config = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 root = os.path.join(os.environ.get("GRAFT_REPO_ROOT", os.getcwd()), "gpurun_out")
-NMB = 120 * 68
+NMB = 120 * 68 if config == 2 else 240 * 135
+# the kernels whose bytes the bench line's roofline prices (bench.py an_name)
+ROOFLINE = {2: ["k_mb_analyse"], 3: ["k_mb_epzs", "k_mb_intra"], 5: ["k_rdo_inter", "k_rdo_intra", "k_rdo_final"]}[config]
+
+
+def bench_line():
+    """the bench JSON line of the FETCH_SIZE pass (P pictures = the pipeline fill + the timed steps)"""
+    with open(os.path.join(root, f"pmc_{tag}_fetch_size.log")) as f:
+        for line in f:
+            if line.startswith("{"):
+                return json.loads(line)
+    raise SystemExit("no bench line in the FETCH_SIZE pass log")
+
+
+b = bench_line()
+steps = b["timed_region"]["warmup_steps_run"] + b["steps"]   # P pictures encoded in total
 
 
 def load(kind):
@@ -34,7 +49,7 @@ def load(kind):
     return {key: (sums[key], len(ids[key])) for key in sums}
 
 
-out = {"tag": tag, "pictures": {"idr": 1, "p": steps}, "kernels": {}}
+out = {"tag": tag, "config": config, "pictures": {"idr": 1, "p": steps}, "kernels": {}}
 for kind in ("fetch_size", "write_size", "sq_wave_cycles", "sq_insts_valu"):
     for (k, name), (s, n) in load(kind).items():
         out["kernels"].setdefault(k, {})[name] = {"total": s, "per_launch": s / max(1, n), "launches": n}
@@ -52,6 +67,15 @@ for k, cs in out["kernels"].items():
     if "SQ_INSTS_VALU" in cs:
         cs["insts_per_mb"] = {n: round(cs[n]["total"] / mbs, 1) for n in
                               ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU") if n in cs}
+def base_name(k):   # "void k_mb_epzs<unsigned char, false>" -> "k_mb_epzs"
+    k = k.split("(")[0].split("<")[0].strip()
+    return k[5:] if k.startswith("void ") else k
+
+
+roof = [k for k in out["kernels"] if base_name(k) in ROOFLINE]
+if roof and all("hbm_bytes_per_mb" in out["kernels"][k] for k in roof):
+    out["roofline_kernels"] = roof
+    out["roofline_hbm_bytes_per_mb"] = round(sum(out["kernels"][k]["hbm_bytes_per_mb"] for k in roof), 1)
 if hbm_total:
     out["hbm_bytes_per_mb"] = round(hbm_total / mbs, 1)
     out["note"] = ("all wavefront kernels; 2 x FETCH_SIZE + WRITE_SIZE over 1 IDR + %d P pictures, per MB; "
