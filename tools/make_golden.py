@@ -4,9 +4,10 @@
   python tools/make_golden.py          # rewrite tests/golden/*
 
 Fixtures (all data; no reference source text):
-  manifest.json   sha256 of lencod_cpu bitstreams + reconstructions for five encoder.cfg
+  manifest.json   sha256 of lencod_cpu bitstreams + reconstructions for eight encoder.cfg
                   configurations (the first three as in the GPU bitstream test; one with slices, one
-                  CABAC), and of the
+                  CABAC, two with RDOptimization 1 -- one of them High 10 -- and a High 10 RDO-off
+                  one), and of the
                   per-picture jmh_mb_result arrays + reconstructions of a 64x48 I-P-P sequence
   tq4x4.npz       dct_luma vectors: residual/prediction inputs and levels/recon/cost/nonzero
                   outputs at QP 0, 12, 28, 51, intra and inter rounding
@@ -44,6 +45,16 @@ LENCOD_CONFIGS = [
     # CABAC (SymbolMode 1, docs/JM_SEMANTICS.md item 48): High, 8x8 transform, slices, an I picture every 3
     ["InputFile=synthetic:5", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
      "ProfileIDC=100", "Transform8x8Mode=1", "SymbolMode=1", "SliceMode=1", "SliceArgument=33", "IntraPeriod=3"],
+    # RDOptimization 1 (items 53-60): CABAC RD loop, Main, EPZS, 11-MB slices
+    ["InputFile=synthetic:6", "FramesToBeEncoded=4", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "ProfileIDC=77", "SymbolMode=1", "RDOptimization=1", "SearchMode=3", "SliceMode=1", "SliceArgument=11"],
+    # config 5's shape: High 10 (ProfileIDC 110, 10-bit samples), CABAC RD loop, one-MB-row slices
+    ["InputFile=synthetic:7", "FramesToBeEncoded=3", "SourceWidth=352", "SourceHeight=96", "SearchRange=32",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "SymbolMode=1", "RDOptimization=1",
+     "SearchMode=3", "SliceMode=1", "SliceArgument=22", "QPRemainingFrame=30"],
+    # High 10 with RDO off: EPZS + 8x8 transform, CAVLC
+    ["InputFile=synthetic:8", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchMode=3"],
 ]
 SEQ = dict(w=64, h=48, seed=21, frames=3, qp=28, search_range=16)
 
