@@ -426,6 +426,14 @@ JMR_FN void jmr_i4(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, int x4,
     jmr_residual(e, lev, 16, 2, ta + 2 * tb);
 }
 
+/* RDCost_for_8x8IntraBlocks [J] (Transform8x8Mode): the rate of one Intra8x8 block candidate -- its
+   pred-mode syntax and its luma 8x8 residual (ctxBlockCat 5, no coded_block_flag) -- from the coding
+   state at the start of the macroblock (docs/JM_SEMANTICS.md item 63) */
+JMR_FN void jmr_i8(jmr_eng *e, int code, const int16_t *lev64) {
+    jmr_ipred_mode(e, code);
+    jmr_residual(e, lev64, 64, 5, -1);
+}
+
 /* RDCost_for_8x8blocks [J] (CABAC): the rate of sub-macroblock mode sm of 8x8 block b8 --
    sub_mb_type, the mvds of its sub-partitions, its coded_block_pattern bit and, when it keeps
    coefficients (coded), the four luma 4x4 residuals -- on the running P8x8 state (cur: the

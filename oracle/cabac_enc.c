@@ -384,3 +384,9 @@ void jmo_cab_i4(jmo_cab *e, const jmo_cabnb *nb, int x4, int y4, int code, const
     const int ta = x4 ? 0 : cbf_term_luma(nb->A, 1, 3, y4), tb = y4 ? 0 : cbf_term_luma(nb->B, 1, x4, 3);
     residual(e, lev, 16, 2, ta + 2 * tb);
 }
+/* RDCost_for_8x8IntraBlocks (item 63): the 8x8 block's pred-mode syntax and its luma 8x8 residual
+   (ctxBlockCat 5, 8x8 zig-zag order, no coded_block_flag) from the state at the macroblock start */
+void jmo_cab_i8(jmo_cab *e, int code, const int16_t *lev64) {
+    intra_pred_mode(e, code);
+    residual(e, lev64, 64, 5, 0);
+}

@@ -1115,6 +1115,36 @@ void jmo_chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], pel pred[
 /*  Intra8x8 decision (High profile): JM FRExt rdopt.c › Mode_Decision_for_Intra8x8Macroblock /  */
 /*  Mode_Decision_for_new_8x8IntraBlocks, RDO off [J] (docs/JM_SEMANTICS.md items 26-28)      */
 /* ====================================================================================== */
+/* the 25 neighbour samples of 8x8 block b8 (inside the MB from rec, the MB's reconstruction so
+ * far; outside from the picture) and their availability bits (1 left, 2 top, 4 top-right, 8
+ * top-left), as jmo_intra8x8_pred_px takes them */
+int jmo_i8_neighbours(const mbs *s, const pel rec[256], int b8, int32_t nb[25]) {
+    const jmo_ctx *c = s->c;
+    int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+#define SMP(x, y) (((x) >= 0 && (x) < 16 && (y) >= 0 && (y) < 16) ? rec[(y) * 16 + (x)] \
+                   : c->recY[(s->pix_y + (y)) * c->W + s->pix_x + (x)])
+    int left = luma_avail(s, bx - 1, by), up = luma_avail(s, bx, by - 1);
+    int ul = luma_avail(s, bx - 1, by - 1), ur = luma_avail(s, bx + 8, by - 1);
+    for (int i = 0; i < 25; i++) nb[i] = 0;
+    if (ul) nb[0] = SMP(bx - 1, by - 1);
+    for (int x = 0; x < 16; x++) if (up && (x < 8 || ur)) nb[1 + x] = SMP(bx + x, by - 1);
+    for (int y = 0; y < 8; y++) if (left) nb[17 + y] = SMP(bx - 1, by + y);
+#undef SMP
+    return left | up << 1 | ur << 2 | ul << 3;
+}
+/* predIntra8x8PredMode (8.3.2.1) of 8x8 block b8: neighbour 4x4 modes (I4: that block, I8:
+ * repeated, else 2), modes[] of the current MB's earlier 8x8 blocks */
+int jmo_i8_mpm(const mbs *s, int b8, const int modes[4]) {
+    const jmo_ctx *c = s->c;
+    int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+    int ma = -1, mb = -1, ia = 0, ib = 0;
+    if (bx) ma = modes[b8 - 1];
+    else if (jmo_nb4(s, -1, by, &ia)) ma = c->ipred[ia];
+    if (by) mb = modes[b8 - 2];
+    else if (jmo_nb4(s, bx, -1, &ib)) mb = c->ipred[ib];
+    return (ma < 0 || mb < 0) ? 2 : imin(ma, mb);
+}
+
 int jmo_intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, pel rec[256],
                              int16_t lev[4][64], int modes[4], int *cbp) {
     const jmo_ctx *c = s->c;
@@ -1122,24 +1152,11 @@ int jmo_intra8x8_decision(mbs *s, int qp, int lambda, int intra_round, pel rec[2
     *cbp = 0;
     for (int b8 = 0; b8 < 4; b8++) {
         int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
-#define SMP(x, y) (((x) >= 0 && (x) < 16 && (y) >= 0 && (y) < 16) ? rec[(y) * 16 + (x)] \
-                   : c->recY[(s->pix_y + (y)) * c->W + s->pix_x + (x)])
-        int left = luma_avail(s, bx - 1, by), up = luma_avail(s, bx, by - 1);
-        int ul = luma_avail(s, bx - 1, by - 1), ur = luma_avail(s, bx + 8, by - 1);
-        int32_t nb[25] = {0};
-        if (ul) nb[0] = SMP(bx - 1, by - 1);
-        for (int x = 0; x < 16; x++) if (up && (x < 8 || ur)) nb[1 + x] = SMP(bx + x, by - 1);
-        for (int y = 0; y < 8; y++) if (left) nb[17 + y] = SMP(bx - 1, by + y);
-#undef SMP
+        int32_t nb[25];
+        int av = jmo_i8_neighbours(s, rec, b8, nb);
         pel pred[9][64];
-        int ok = jmo_intra8x8_pred_px(nb, left | up << 1 | ur << 2 | ul << 3, pred, (c->maxv + 1) >> 1);
-        /* predIntra8x8PredMode (8.3.2.1): neighbour 4x4 modes (I4: that block, I8: repeated, else 2) */
-        int ma = -1, mb = -1, ia = 0, ib = 0;
-        if (bx) ma = modes[b8 - 1];
-        else if (jmo_nb4(s, -1, by, &ia)) ma = c->ipred[ia];
-        if (by) mb = modes[b8 - 2];
-        else if (jmo_nb4(s, bx, -1, &ib)) mb = c->ipred[ib];
-        int mpm = (ma < 0 || mb < 0) ? 2 : imin(ma, mb);
+        int ok = jmo_intra8x8_pred_px(nb, av, pred, (c->maxv + 1) >> 1);
+        int mpm = jmo_i8_mpm(s, b8, modes);
         int best = 2, bcost = BIGCOST;
         for (int m = 0; m < 9; m++) {
             if (!((ok >> m) & 1)) continue;

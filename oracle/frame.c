@@ -24,7 +24,7 @@ static int cfg_ok(const jmh_config *cfg) {
         cfg->epzs_max_thres_scale < 0 || cfg->epzs_max_thres_scale > JMH_EPZS_SCALE_MAX) return JMH_E_INVALID_ARG;
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     /* RDOptimization 1: CABAC rate, 4x4 transform (docs/JM_SEMANTICS.md items 53-60) */
-    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode != 1 || cfg->transform_8x8_mode != 0)) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode != 1)) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     return JMH_OK;

@@ -86,10 +86,11 @@ void jmo_cab_mb(jmo_cab *e, const jmo_cabnb *nb, const jmo_cabsyn *m, int slice_
 void jmo_cab_b8(jmo_cab *e, const jmo_cabnb *nb, jmo_cabcur *cur, int b8, int sm, const int16_t (*mvd4)[2], int coded,
                 const int16_t (*lev4)[16]);
 void jmo_cab_i4(jmo_cab *e, const jmo_cabnb *nb, int x4, int y4, int code, const int16_t *lev);
+void jmo_cab_i8(jmo_cab *e, int code, const int16_t *lev64);
 
 /* Test hook (tests/csrc/rate_xcheck.c): every RD rate the oracle computes, with the coder state,
  * neighbours and syntax it was computed from and the state after; NULL in normal use */
-enum { JMO_RATE_SKIP, JMO_RATE_MB, JMO_RATE_B8, JMO_RATE_I4 };
+enum { JMO_RATE_SKIP, JMO_RATE_MB, JMO_RATE_B8, JMO_RATE_I4, JMO_RATE_I8 };
 typedef struct jmo_rate_event {
     int kind, slice_p, t8mode;
     const jmo_cab *before, *after;
@@ -99,7 +100,7 @@ typedef struct jmo_rate_event {
     int b8, sm, coded;
     const int16_t (*mvd4)[2];
     const int16_t (*lev4)[16];
-    int x4, y4, code;                        /* JMO_RATE_I4                                       */
+    int x4, y4, code;                        /* JMO_RATE_I4 (JMO_RATE_I8: code, lev[64])          */
     const int16_t *lev;
     long bits;                               /* the oracle's rate                                 */
 } jmo_rate_event;
@@ -236,6 +237,8 @@ int  jmo_find_sad_16x16(const mbs *s, pel pred[4][256], const int avail[4], int 
 void jmo_luma_pred_4x4(const mbs *s, int bx4, int by4, int mvx, int mvy, pel *out, int os);
 void jmo_chroma_pred_mb(const mbs *s, int uv, const int16_t mv[16][2], pel pred[64]);
 void jmo_store_rec_luma(jmo_ctx *c, const mbs *s, const pel rec[256]);
+int  jmo_i8_neighbours(const mbs *s, const pel rec[256], int b8, int32_t nb[25]);
+int  jmo_i8_mpm(const mbs *s, int b8, const int modes[4]);
 
 /* rdo.c: encode_one_macroblock with RDOptimization = 1 (CABAC rate) */
 void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby);

@@ -8,7 +8,8 @@
  *             SetCoeffAndReconstruction8x8, store_macroblock_parameters
  *   rdopt_coding_state.c › store_coding_state / reset_coding_state (a copy of the oracle's CABAC
  *             coder, cabac_enc.c: contexts, codILow, codIRange, outstanding bits)
- * with the entropy coder CABAC (SymbolMode 1) and the 4x4 transform (Transform8x8Mode 0).
+ * with the entropy coder CABAC (SymbolMode 1), and with Transform8x8Mode 1 the JM FRExt additions
+ * [J]: RDCost_for_8x8IntraBlocks (I8MB) and transform_size_8x8_flag per inter candidate (item 63).
  * Every non-normative choice is an item of docs/JM_SEMANTICS.md (53-60):
  *   - lambda_mode = fp.lambda_rd (0.85 * 2^((QP + QpBdOffsetY - 12) / 3), host libm), the searches'
  *     LAMBDA_FACTOR(sqrt(lambda_mode)) = fp.lambda_factor_rd; rdcost = (double)D + lambda * rate;
@@ -26,12 +27,14 @@
 #define RD_HUGE 1e30
 
 typedef struct {               /* a luma candidate of the macroblock loop                          */
-    int mode;                  /* 0 (P_Skip), 1..3, JMH_P8x8, JMH_I16MB, JMH_I4MB                  */
+    int mode;                  /* 0 (P_Skip), 1..3, JMH_P8x8, JMH_I16MB, JMH_I4MB, JMH_I8MB        */
+    int t8;                    /* transform_size_8x8_flag of the candidate's luma                  */
     pel rec[256];
     int16_t luma[16][16], luma_dc[16];
     int cbp, cbp_blk;          /* luma cbp bits, 4x4 coded bits                                    */
     int16_t mv[16][2], mvd[16][2];
-    int8_t ipm[16], imode[16]; /* I4: rem codes (-1 = predicted mode), modes                       */
+    int8_t ipm[16], imode[16]; /* I4 / I8: rem codes (-1 = predicted mode; I8 at each 8x8's top-left
+                                  4x4), modes (I8: on the 8x8's four 4x4)                           */
     int i16mode, b8mode[4];
     int dist;                  /* luma SSD                                                         */
 } lcand;
@@ -51,8 +54,9 @@ static int ssd(const pel *a, int as, const pel *b, int bs, int w, int h) {
     return d;
 }
 
-/* LumaResidualCoding (RDO-off form, 4x4 transform): the prediction from the candidate's MVs, per
-   8x8 LumaResidualCoding8x8 with the _LUMA_COEFF_COST_ zeroing, then the MB-level one */
+/* LumaResidualCoding (RDO-off form): the prediction from the candidate's MVs, per 8x8
+   LumaResidualCoding8x8 -- four dct_luma, or with L->t8 one dct_luma8x8 (levels in the CAVLC
+   interleave of jmh_mb_result) -- with the _LUMA_COEFF_COST_ zeroing, then the MB-level one */
 static void luma_inter(const mbs *s, int qp, int rnd, lcand *L, pel pred[256]) {
     const int maxv = s->c->maxv;
     for (int k = 0; k < 16; k++) jmo_luma_pred_4x4(s, k & 3, k >> 2, L->mv[k][0], L->mv[k][1], pred + 4 * (k >> 2) * 16 + 4 * (k & 3), 16);
@@ -61,14 +65,26 @@ static void luma_inter(const mbs *s, int qp, int rnd, lcand *L, pel pred[256]) {
     memset(L->luma, 0, sizeof(L->luma));
     for (int b8 = 0; b8 < 4; b8++) {
         int cost = 0, cbp8 = 0, blk8 = 0;
-        for (int b4 = 0; b4 < 4; b4++) {
-            int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1), k = by4 * 4 + bx4;
-            int32_t r[16];
-            for (int y = 0; y < 4; y++)
-                for (int x = 0; x < 4; x++) r[4 * y + x] = s->org[(4 * by4 + y) * 16 + 4 * bx4 + x] - pred[(4 * by4 + y) * 16 + 4 * bx4 + x];
-            if (jmo_dct_luma4x4(r, pred + 4 * by4 * 16 + 4 * bx4, 16, qp, rnd, L->luma[k], &cost, L->rec + 4 * by4 * 16 + 4 * bx4, 16,
-                                maxv)) { blk8 |= 1 << k; cbp8 = 1; }
-        }
+        if (L->t8) {
+            const int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+            int32_t r[64];
+            int16_t lv[64];
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) r[8 * y + x] = s->org[(by + y) * 16 + bx + x] - pred[(by + y) * 16 + bx + x];
+            if (jmo_dct_luma8x8(r, pred + by * 16 + bx, 16, qp, rnd, lv, &cost, L->rec + by * 16 + bx, 16, maxv)) {
+                cbp8 = 1;
+                blk8 = 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2);
+            }
+            jmo_put_levels8(L->luma, b8, lv);
+        } else
+            for (int b4 = 0; b4 < 4; b4++) {
+                int bx4 = 2 * (b8 & 1) + (b4 & 1), by4 = 2 * (b8 >> 1) + (b4 >> 1), k = by4 * 4 + bx4;
+                int32_t r[16];
+                for (int y = 0; y < 4; y++)
+                    for (int x = 0; x < 4; x++) r[4 * y + x] = s->org[(4 * by4 + y) * 16 + 4 * bx4 + x] - pred[(4 * by4 + y) * 16 + 4 * bx4 + x];
+                if (jmo_dct_luma4x4(r, pred + 4 * by4 * 16 + 4 * bx4, 16, qp, rnd, L->luma[k], &cost, L->rec + 4 * by4 * 16 + 4 * bx4, 16,
+                                    maxv)) { blk8 |= 1 << k; cbp8 = 1; }
+            }
         if (cost <= LUMA_COEFF_COST) {
             cost = 0; cbp8 = 0; blk8 = 0;
             for (int b4 = 0; b4 < 4; b4++) {
@@ -114,6 +130,7 @@ static void chroma_code(const mbs *s, int qpc, int rnd, const pel (*ipred)[4][64
 static void fill_syn(jmo_cabsyn *r, const lcand *L, const ccand *C, int cm) {
     memset(r, 0, sizeof(*r));
     r->mb_type = L->mode;
+    r->t8 = L->t8;
     r->cbp = L->cbp | C->cbpc << 4;
     r->i16mode = L->i16mode;
     r->cmode = cm;
@@ -176,8 +193,12 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
     for (int m = 1; m <= 7; m++) valid[m] = s->slice_p && isr[m];
     valid[8] = valid[4] || valid[5] || valid[6] || valid[7];
 
-    static lcand Lc[7];        /* 0 skip, 1..3, 4 P8x8, 5 I16, 6 I4 (one MB at a time) */
-    int have[7] = {0};
+    /* candidates (one MB at a time): 0 skip, 1..3, 4 P8x8, 5 I16, 6 I4, 7 I8; Transform8x8Mode:
+       8..10 the 16x16 / 16x8 / 8x16 and 11 the P8x8 (all sub-modes 8x8) with the 8x8 transform */
+    enum { NC = 12 };
+    static lcand Lc[NC];
+    int have[NC] = {0};
+    const int t8m = c->cfg.transform_8x8_mode;
     pel pred[256];
     if (s->slice_p) {
         /* ===== motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch) ===== */
@@ -299,6 +320,16 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
             luma_inter(s, qp, rnd, L, pred);
             have[mode] = 1;
         }
+        /* Transform8x8Mode: the same motion with transform_size_8x8_flag 1 (item 63) */
+        for (int mode = 1; t8m && mode <= 4; mode++) {
+            if (!have[mode] || (mode == 4 && !(Lc[4].b8mode[0] == 4 && Lc[4].b8mode[1] == 4 && Lc[4].b8mode[2] == 4 &&
+                                               Lc[4].b8mode[3] == 4))) continue;
+            lcand *L = &Lc[mode + 7];
+            *L = Lc[mode];
+            L->t8 = 1;
+            luma_inter(s, qp, rnd, L, pred);
+            have[mode + 7] = 1;
+        }
     }
 
     /* ===== Intra16x16: the find_sad_16x16 mode, dct_luma_16x16 ===== */
@@ -363,9 +394,58 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
         L->dist = ssd(s->org, 16, L->rec, 16, 16, 16);
         have[6] = 1;
     }
+    /* ===== Intra8x8 (Transform8x8Mode): Mode_Decision_for_8x8IntraBlocks by RDCost_for_8x8IntraBlocks
+       per 8x8 block -- 8x8 TQ, D = SSD of the block, R = the pred-mode syntax + the 8x8 residual
+       from the state at the macroblock start; strict '<' over modes 0..8; the winner reconstructs
+       before the next block (item 63) ===== */
+    if (t8m) {
+        lcand *L = &Lc[7];
+        memset(L, 0, sizeof(*L));
+        L->mode = JMH_I8MB;
+        L->t8 = 1;
+        int modes[4] = {2, 2, 2, 2};
+        for (int b8 = 0; b8 < 4; b8++) {
+            const int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+            int32_t nbs[25];
+            const int avb = jmo_i8_neighbours(s, L->rec, b8, nbs);
+            pel ip[9][64];
+            const int ok = jmo_intra8x8_pred_px(nbs, avb, ip, (maxv + 1) >> 1);
+            const int mpm = jmo_i8_mpm(s, b8, modes);
+            double best = RD_HUGE;
+            int bmode = 2, bnz = 0;
+            int16_t blev[64];
+            pel brec[64];
+            for (int m = 0; m < 9; m++) {
+                if (!((ok >> m) & 1)) continue;
+                int32_t r[64];
+                for (int y = 0; y < 8; y++)
+                    for (int x = 0; x < 8; x++) r[8 * y + x] = s->org[(by + y) * 16 + bx + x] - ip[m][8 * y + x];
+                int16_t lev[64];
+                pel rec8[64];
+                int dummy = 0;
+                const int nz = jmo_dct_luma8x8(r, ip[m], 8, qp, rnd, lev, &dummy, rec8, 8, maxv);
+                const int D = ssd(s->org + by * 16 + bx, 16, rec8, 8, 8, 8);
+                RATE_BEGIN(JMO_RATE_I8);
+                ev.code = m == mpm ? -1 : m < mpm ? m : m - 1;
+                ev.lev = lev;
+                jmo_cab_i8(&e, ev.code, lev);
+                double rd = (double)D + lam * (double)rate_of(&ev, &c->cab, &e);
+                if (rd < best) { best = rd; bmode = m; bnz = nz; memcpy(blev, lev, sizeof(blev)); memcpy(brec, rec8, sizeof(brec)); }
+            }
+            modes[b8] = bmode;
+            for (int y = 0; y < 8; y++) memcpy(L->rec + (by + y) * 16 + bx, brec + 8 * y, 8 * sizeof(pel));
+            jmo_put_levels8(L->luma, b8, blev);
+            L->ipm[(b8 >> 1) * 8 + (b8 & 1) * 2] = (int8_t)(bmode == mpm ? -1 : bmode < mpm ? bmode : bmode - 1);
+            for (int q = 0; q < 16; q++)
+                if (((q >> 3) << 1) + ((q & 3) >> 1) == b8) L->imode[q] = (int8_t)bmode;
+            if (bnz) { L->cbp |= 1 << b8; L->cbp_blk |= 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2); }
+        }
+        L->dist = ssd(s->org, 16, L->rec, 16, 16, 16);
+        have[7] = 1;
+    }
 
     /* ===== chroma candidates: each inter candidate's MC, the intra modes ===== */
-    static ccand Cc[7], Ci[4];
+    static ccand Cc[5], Ci[4];
     pel cip[2][4][64];
     int cav[4];
     jmo_intra_chroma_pred(s, 0, cip[0], cav);
@@ -375,16 +455,18 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
     for (int cm = 0; cm < 4; cm++)
         if (cav[cm]) chroma_code(s, qpc, rnd, (const pel(*)[4][64])cip, cm, NULL, 0, &Ci[cm]);
 
-    /* ===== RDCost_for_macroblocks over c_ipred_mode (outer) and the modes (inner), JM order ===== */
-    static const int order[7] = {0, 1, 2, 3, 4, 5, 6};   /* 0, 1, 2, 3, P8x8, I16MB, I4MB */
+    /* ===== RDCost_for_macroblocks over c_ipred_mode (outer) and the modes (inner), JM order:
+       0, 1, 2, 3, P8x8 (each with the 4x4 then the 8x8 transform), I16MB, I4MB, I8MB ===== */
+    static const int order[NC] = {0, 1, 8, 2, 9, 3, 10, 4, 11, 5, 6, 7};
+#define CBASE(i) ((i) >= 8 ? (i) - 7 : (i))                  /* an inter candidate's chroma */
     double min_rd = RD_HUGE;
     int bi = -1, bcm = 0, brate = 0;
     for (int cm = 0; cm < 4; cm++) {
         if (!cav[cm]) continue;
-        for (int oi = 0; oi < 7; oi++) {
-            int i = order[oi], intra = i >= 5;
+        for (int oi = 0; oi < NC; oi++) {
+            int i = order[oi], intra = i >= 5 && i <= 7;
             if (!have[i] || (cm != 0 && !intra)) continue;
-            const ccand *C = intra ? &Ci[cm] : &Cc[i];
+            const ccand *C = intra ? &Ci[cm] : &Cc[CBASE(i)];
             jmo_cabsyn r;
             if (i == 0) {
                 RATE_BEGIN(JMO_RATE_SKIP);
@@ -393,7 +475,8 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                 RATE_BEGIN(JMO_RATE_MB);
                 fill_syn(&r, &Lc[i], C, intra ? cm : 0);
                 ev.syn = &r;
-                jmo_cab_mb(&e, &nb, &r, s->slice_p, 0, NULL, NULL);
+                ev.t8mode = t8m;
+                jmo_cab_mb(&e, &nb, &r, s->slice_p, t8m, NULL, NULL);
             }
             const long bits = rate_of(&ev, &c->cab, &e);
             double rd = (double)(Lc[i].dist + C->dist) + lam * (double)bits;
@@ -403,8 +486,9 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
 
     /* ===== the chosen macroblock: results, reconstruction, picture arrays, coding state ===== */
     const lcand *L = &Lc[bi];
-    const ccand *C = bi >= 5 ? &Ci[bcm] : &Cc[bi];
-    const int is_intra = bi >= 5;
+    const int is_intra = bi >= 5 && bi <= 7;
+    const ccand *C = is_intra ? &Ci[bcm] : &Cc[CBASE(bi)];
+#undef CBASE
     jmh_mb_result *res = &c->res[a];
     memset(res, 0, sizeof(*res));
     int mb_type = L->mode == 0 ? JMH_PSKIP : L->mode;
@@ -416,6 +500,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                                                    : mb_type == JMH_I16MB ? 0 : mb_type);
         res->ref_idx[b] = (int8_t)(is_intra ? -1 : 0);
     }
+    res->transform_8x8 = (int8_t)(L->t8 && (mb_type == JMH_I8MB || (L->cbp & 15)));
     res->i16mode = (int8_t)(mb_type == JMH_I16MB ? L->i16mode : 0);
     res->c_ipred_mode = (int8_t)(is_intra ? bcm : 0);
     res->min_cost = brate;                                /* the chosen candidate's rate (bits) */
@@ -426,7 +511,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
     for (int q = 0; q < 16; q++) {
         res->mv[q][0] = is_intra ? 0 : L->mv[q][0];
         res->mv[q][1] = is_intra ? 0 : L->mv[q][1];
-        res->ipred[q] = (int8_t)(mb_type == JMH_I4MB ? L->imode[q] : 2);
+        res->ipred[q] = (int8_t)(mb_type == JMH_I4MB || mb_type == JMH_I8MB ? L->imode[q] : 2);
         int pa = ((s->pix_y >> 2) + (q >> 2)) * W4 + (s->pix_x >> 2) + (q & 3);
         c->mv[2 * pa] = res->mv[q][0];
         c->mv[2 * pa + 1] = res->mv[q][1];
@@ -451,7 +536,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
     } else {
         jmo_cabsyn r;
         fill_syn(&r, L, C, is_intra ? bcm : 0);
-        jmo_cab_mb(&c->cab, &nb, &r, s->slice_p, 0, &c->cabi[a], mvd);
+        jmo_cab_mb(&c->cab, &nb, &r, s->slice_p, t8m, &c->cabi[a], mvd);
     }
     for (int q = 0; q < 16; q++) {
         const int pa = ((s->pix_y >> 2) + (q >> 2)) * W4 + (s->pix_x >> 2) + (q & 3);

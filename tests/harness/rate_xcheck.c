@@ -4,13 +4,14 @@
  * own CABAC coder (oracle/cabac_enc.c) on EVERY candidate the oracle's RD loop (oracle/rdo.c)
  * prices: P_Skip and whole-macroblock candidates of RDCost_for_macroblocks, the sub-modes of every
  * 8x8 block of RDCost_for_8x8blocks, the nine modes of every Intra4x4 block of
- * RDCost_for_4x4IntraBlocks — winners and losers alike.
+ * RDCost_for_4x4IntraBlocks, the nine modes of every Intra8x8 block of RDCost_for_8x8IntraBlocks
+ * (Transform8x8Mode) — winners and losers alike.
  *
  * Linked into lencod_xcheck (lencod_cpu + this file): a constructor installs jmo_rate_hook; each
  * event's coder state, neighbours and syntax are translated into the product's representation
  * (dense contexts JMR_CTX, jmr_mbinfo, jmr_cand, jmr_cur), the product engine codes the same
  * candidate, and its bit count, resulting context states and codIRange must equal the oracle's.
- * At exit one line:  "rate xcheck: N candidates (skip S, mb M, b8 B, i4 I), K mismatches"
+ * At exit one line:  "rate xcheck: N candidates (skip S, mb M, b8 B, i4 I, i8 J), K mismatches"
  * plus the first mismatches.  Exit status 5 when any mismatch (or no candidate) was seen.
  */
 #include <stdio.h>
@@ -20,7 +21,7 @@
 #include "../../oracle/jmo_internal.h"
 #include "../../h264-jm-commentary_amd/csrc/jmh_cabac_rate.h"
 
-static long n_ev[4], n_bad;
+static long n_ev[5], n_bad;
 static int n_printed;
 
 /* the spec contexts the product's dense space holds (JMR_CTX, tools/gen_cabac_tables.py): I/P
@@ -54,13 +55,14 @@ static void to_mbinfo(const jmo_cabmbi *m, const int16_t (*mvd_r)[2], const int1
 static void report(const jmo_rate_event *ev, long pbits, int ctx_bad, int range_bad) {
     n_bad++;
     if (n_printed++ >= 8) return;
-    static const char *kinds[] = {"skip", "mb", "b8", "i4"};
+    static const char *kinds[] = {"skip", "mb", "b8", "i4", "i8"};
     fprintf(stderr, "rate xcheck MISMATCH %s: oracle %ld bits, product %ld bits%s%s", kinds[ev->kind], ev->bits, pbits,
             ctx_bad >= 0 ? " (context state differs)" : "", range_bad ? " (codIRange differs)" : "");
     if (ctx_bad >= 0) fprintf(stderr, " first ctxIdx %d", ctx_bad);
     if (ev->kind == JMO_RATE_MB) fprintf(stderr, " mb_type %d cbp %d", ev->syn->mb_type, ev->syn->cbp);
     if (ev->kind == JMO_RATE_B8) fprintf(stderr, " b8 %d sub-mode %d coded %d", ev->b8, ev->sm, ev->coded);
     if (ev->kind == JMO_RATE_I4) fprintf(stderr, " block (%d,%d) code %d", ev->x4, ev->y4, ev->code);
+    if (ev->kind == JMO_RATE_I8) fprintf(stderr, " code %d", ev->code);
     fputc('\n', stderr);
 }
 
@@ -100,7 +102,8 @@ static void hook(const jmo_rate_event *ev) {
         jmr_b8(&e, pa, pb, &cur, ev->b8, ev->sm, ev->mvd4, ev->coded, ev->lev4);
         break;
     }
-    default: jmr_i4(&e, pa, pb, ev->x4, ev->y4, ev->code, ev->lev); break;
+    case JMO_RATE_I4: jmr_i4(&e, pa, pb, ev->x4, ev->y4, ev->code, ev->lev); break;
+    default: jmr_i8(&e, ev->code, ev->lev); break;
     }
     to_dense(ev->after, want);
     int ctx_bad = -1;
@@ -111,9 +114,9 @@ static void hook(const jmo_rate_event *ev) {
 }
 
 static void done(void) {
-    const long n = n_ev[0] + n_ev[1] + n_ev[2] + n_ev[3];
-    printf("rate xcheck: %ld candidates (skip %ld, mb %ld, b8 %ld, i4 %ld), %ld mismatches\n", n, n_ev[JMO_RATE_SKIP],
-           n_ev[JMO_RATE_MB], n_ev[JMO_RATE_B8], n_ev[JMO_RATE_I4], n_bad);
+    const long n = n_ev[0] + n_ev[1] + n_ev[2] + n_ev[3] + n_ev[4];
+    printf("rate xcheck: %ld candidates (skip %ld, mb %ld, b8 %ld, i4 %ld, i8 %ld), %ld mismatches\n", n, n_ev[JMO_RATE_SKIP],
+           n_ev[JMO_RATE_MB], n_ev[JMO_RATE_B8], n_ev[JMO_RATE_I4], n_ev[JMO_RATE_I8], n_bad);
     fflush(stdout);
     if (n_bad || !n) _exit(5);
 }

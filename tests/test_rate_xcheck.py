@@ -31,6 +31,13 @@ XCHECK = RDO + [
     # JM >= 10 EPZS options under RDO, low QP (long level codes: the UEG0 suffix of the rate)
     ["InputFile=synthetic:85", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=16", "EPZSSubPelME=1",
      "EPZSMaxThresScale=2", "QPFirstFrame=4", "QPRemainingFrame=6"],
+    # Transform8x8Mode 1 with RDO (item 63): I8MB by RDCost_for_8x8IntraBlocks, 8x8-transform inter candidates
+    ["InputFile=synthetic:86", "FramesToBeEncoded=4", "ProfileIDC=100", "Transform8x8Mode=1", "SearchRange=16"],
+    ["InputFile=synthetic:87", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=1", "SearchRange=8",
+     "QPFirstFrame=8", "QPRemainingFrame=10", "SliceMode=1", "SliceArgument=5"],
+    ["InputFile=synthetic:88", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=10",
+     "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SourceWidth=3840", "SourceHeight=48", "SearchRange=32",
+     "SliceMode=1", "SliceArgument=240"],
 ]
 
 
@@ -41,7 +48,8 @@ def run_xcheck(extra):
             args += ["-p", e]
         r = subprocess.run(args, capture_output=True, text=True, timeout=900)
     log = r.stdout + r.stderr
-    m = re.search(r"rate xcheck: (\d+) candidates \(skip (\d+), mb (\d+), b8 (\d+), i4 (\d+)\), (\d+) mismatches", log)
+    m = re.search(r"rate xcheck: (\d+) candidates \(skip (\d+), mb (\d+), b8 (\d+), i4 (\d+), i8 (\d+)\), (\d+) mismatches",
+                  log)
     assert m, log[-3000:]
     return r.returncode, [int(v) for v in m.groups()], log
 
@@ -49,8 +57,10 @@ def run_xcheck(extra):
 @pytest.mark.parametrize("extra", XCHECK, ids=[c[0].split(":")[1] for c in XCHECK])
 def test_rate_engine_equals_oracle_coder_on_every_candidate(extra):
     ensure_built()
-    rc, (n, skip, mb, b8, i4, bad), log = run_xcheck(extra)
+    rc, (n, skip, mb, b8, i4, i8, bad), log = run_xcheck(extra)
     assert rc == 0 and bad == 0, log[-3000:]
     assert n > 0 and mb > 0 and i4 > 0, log[-3000:]
     if "IntraPeriod=1" not in extra:                       # P pictures: skip and P8x8 candidates too
         assert skip > 0 and b8 > 0, log[-3000:]
+    if "Transform8x8Mode=1" in extra:                      # Intra8x8 candidates
+        assert i8 > 0, log[-3000:]

@@ -38,6 +38,13 @@ RDO = [
      "SourceBitDepthChroma=10", "SearchRange=16", "SliceMode=1", "SliceArgument=11", "IntraPeriod=3"],
     ["InputFile=synthetic:80", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=9",
      "SourceBitDepthChroma=9", "SearchRange=8", "QPFirstFrame=2", "QPRemainingFrame=4", "ChromaQPOffset=-12"],
+    # Transform8x8Mode 1 (item 63): I8MB by RDCost_for_8x8IntraBlocks, each inter candidate with the 8x8 transform
+    ["InputFile=synthetic:89", "FramesToBeEncoded=4", "ProfileIDC=100", "Transform8x8Mode=1", "SearchRange=16"],
+    ["InputFile=synthetic:90", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=1", "SearchRange=8",
+     "IntraPeriod=1", "QPFirstFrame=20"],
+    ["InputFile=synthetic:91", "FramesToBeEncoded=4", "ProfileIDC=110", "SourceBitDepthLuma=10",
+     "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchRange=16", "SliceMode=1", "SliceArgument=11",
+     "QPRemainingFrame=24", "JMVersion=10"],
 ]
 
 
@@ -96,7 +103,6 @@ def test_rdo_rate_distortion_tradeoff():
 
 @pytest.mark.parametrize("bad,msg", [
     (["SymbolMode=0", "ProfileIDC=77"], "needs SymbolMode=1"),
-    (["ProfileIDC=100", "Transform8x8Mode=1"], "Transform8x8Mode"),
     (["SearchMode=0", "ProfileIDC=77"], "SearchMode=3"),
     (["RDOptimization=2", "ProfileIDC=77"], "RDOptimization=2"),
 ])
