@@ -74,6 +74,7 @@ CONFIG5_RDO_OFF = dict(metric="ME+transform megapixels/sec @2160p High10 10-bit 
                                 "SearchRange=32, Transform8x8Mode=1, UseHadamard=1, 7 inter block sizes, RDO off, QP 28, "
                                 "IDR + {nf}-picture P sequence cycled (one independent stream per GPU)")
 RDO = 0              # RDOptimization of the run (the config's, or --rdo)
+T8_OVERRIDE = None   # --t8: Transform8x8Mode instead of the config's
 EPZS_KW = {}         # --epzs-jm10: JM >= 10's EPZS options (docs/JM_SEMANTICS.md items 46, 61, 62)
 EPZS_JM10 = dict(epzs_subpel_me=1, epzs_subpel_thres_scale=2, epzs_min_thres_scale=0, epzs_max_thres_scale=2, epzs_dual_refinement=1)
 DISP_W, DISP_H = 1920, 1080
@@ -168,7 +169,8 @@ def cpu_workers(n, config, search_mode, size, dump_dir=None):
             cmd.append(os.path.join(dump_dir, "oracle_seed0.npz"))
         procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
                                       env=dict(os.environ, JMH_BENCH_SLICE_MBS=str(SLICE_MBS), JMH_BENCH_RDO=str(RDO),
-                                               JMH_BENCH_EPZS10="1" if EPZS_KW else "0")))
+                                               JMH_BENCH_EPZS10="1" if EPZS_KW else "0", JMH_BENCH_T8=str(T8_OVERRIDE)
+                                               if T8_OVERRIDE is not None else "")))
     out = []
     for p in procs:
         s = p.communicate()[0]
@@ -314,11 +316,13 @@ def launch(n):
 
 
 def main():
-    global SLICE_MBS
+    global SLICE_MBS, T8_OVERRIDE
     if len(sys.argv) in (6, 7) and sys.argv[1] == "--cpu-worker":    # child of cpu_baseline()
         SLICE_MBS = int(os.environ.get("JMH_BENCH_SLICE_MBS", "0"))
         w, h = (int(v) for v in sys.argv[5].split("x"))
         c = use_config(int(sys.argv[3]), (w, h), int(os.environ.get("JMH_BENCH_RDO", "0")))
+        if os.environ.get("JMH_BENCH_T8", "") != "":
+            c["t8"] = int(os.environ["JMH_BENCH_T8"])
         if os.environ.get("JMH_BENCH_EPZS10") == "1":
             EPZS_KW.update(EPZS_JM10)
         print(cpu_one_picture(int(sys.argv[2]), int(sys.argv[4]), c["t8"], sys.argv[6] if len(sys.argv) == 7 else None),
@@ -336,6 +340,9 @@ def main():
                          "5 = 2160p High 10 EPZS, CABAC RDO on, 240-MB slices")
     ap.add_argument("--rdo", type=int, default=None, choices=(0, 1),
                     help="config 5: RDOptimization (default 1; 0 = the RDO-off variant with the 8x8 transform)")
+    ap.add_argument("--t8", type=int, default=None, choices=(0, 1),
+                    help="override the config's Transform8x8Mode (config 5 with RDO on: the 8x8-transform candidates "
+                         "and I8MB by RDCost_for_8x8IntraBlocks, docs/JM_SEMANTICS.md item 63)")
     ap.add_argument("--search-mode", type=int, default=None, choices=(0, -1, 3),
                     help="override the config's SearchMode (config 2 variants: -1 full search, 3 EPZS)")
     ap.add_argument("--epzs-jm10", action="store_true",
@@ -363,6 +370,14 @@ def main():
     if args.rdo is not None and args.config != 5:
         ap.error("--rdo applies to --config 5")
     cfg = use_config(args.config, size, args.rdo)
+    if args.t8 is not None:
+        if args.t8 and args.config == 2:
+            ap.error("--t8 1 needs a High profile config (3 or 5)")
+        T8_OVERRIDE = args.t8
+        if cfg["t8"] != args.t8:
+            cfg["workload"] = cfg["workload"].replace(f"Transform8x8Mode={cfg['t8']}", f"Transform8x8Mode={args.t8}")
+            cfg["metric"] = cfg["metric"] + (" + 8x8 transform" if args.t8 else " (4x4 transform)")
+        cfg["t8"] = args.t8
     SLICE_MBS = max(0, cfg.get("slice_mbs", 0) if args.slice_mbs is None else args.slice_mbs)
     search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
     if args.epzs_jm10:

@@ -62,8 +62,9 @@ __device__ __forceinline__ int vh1(const uint8_t *p, int w, int h, int x, int y)
 }
 // one luma sample at quarter-pel position (X, Y) (units of 1/4 pel) from integer samples px(x, y):
 // only the half-pel samples the phase needs (G, b, h, s, m, j of Figure 8-4), same values as
-// k_interp's 16 planes; maxv = (1 << BitDepthY) - 1 (Clip1Y)
-template <class PX>
+// k_interp's 16 planes; maxv = (1 << BitDepthY) - 1 (Clip1Y).  SERIAL_J: the centre sample j's six
+// columns one loop iteration at a time (six loads live instead of 36: no spills in a 64-VGPR kernel)
+template <class PX, bool SERIAL_J = false>
 __device__ __forceinline__ int qpel_from(PX px, int X, int Y, int maxv = 255) {
     const int x = X >> 2, y = Y >> 2, fx = X & 3, fy = Y & 3;
     auto hb1p = [&](int xx, int yy) { return tap6(px(xx - 2, yy), px(xx - 1, yy), px(xx, yy), px(xx + 1, yy), px(xx + 2, yy), px(xx + 3, yy)); };
@@ -82,17 +83,23 @@ __device__ __forceinline__ int qpel_from(PX px, int X, int Y, int maxv = 255) {
     }
     if ((fx & 1) && (fy & 1)) return (hb(x, fy == 1 ? y : y + 1) + vb(fx == 1 ? x : x + 1, y) + 1) >> 1;   // e g p r
     int j1 = 0;
+    if constexpr (SERIAL_J) {
+#pragma unroll 1
+        for (int k = 0; k < 6; k++) j1 += (k == 0 || k == 5 ? 1 : (k == 1 || k == 4 ? -5 : 20)) * vh1p(x - 2 + k, y);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 6; k++) j1 += (k == 0 || k == 5 ? 1 : (k == 1 || k == 4 ? -5 : 20)) * vh1p(x - 2 + k, y);
+        for (int k = 0; k < 6; k++) j1 += (k == 0 || k == 5 ? 1 : (k == 1 || k == 4 ? -5 : 20)) * vh1p(x - 2 + k, y);
+    }
     const int j = iclip(0, maxv, (j1 + 512) >> 10);
     if (fx == 2 && fy == 2) return j;
     const int o = fx == 2 ? hb(x, fy == 1 ? y : y + 1) : vb(fx == 1 ? x : x + 1, y);   // f q / i k
     return (j + o + 1) >> 1;
 }
 // ... straight from the reference picture in HBM, spec coordinate clamping (k_mb_final MC)
-template <class T>
+template <class T, bool SERIAL_J = false>
 __device__ __forceinline__ int qpel_direct(const T *ref, int W, int H, int X, int Y, int maxv = 255) {
-    return qpel_from([&](int x, int y) { return rpx(ref, W, H, x, y); }, X, Y, maxv);
+    auto px = [&](int x, int y) { return rpx(ref, W, H, x, y); };
+    return qpel_from<decltype(px), SERIAL_J>(px, X, Y, maxv);
 }
 
 __device__ __forceinline__ int spiral_index(int x, int y) {

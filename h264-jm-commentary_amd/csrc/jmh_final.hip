@@ -149,7 +149,12 @@ __global__ __launch_bounds__(NT, OCC) void k_mb_final(const TickArgs t) {
             if (s.bnz[b]) { cbp = 15; cbp_blk |= 1 << b; }
     } else {
         // LumaResidualCoding / LumaResidualCoding8x8 (+ SetCoeffAndReconstruction8x8)
-        const int p = qpel_direct(refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1], maxv);
+#ifdef JMH_AB_PLAIN_J   // A/B only: the earlier unrolled j (spills 56 B per lane at 64 VGPRs)
+        constexpr bool serial_j = false;
+#else
+        constexpr bool serial_j = OCC == 8;                 // no spills in the 64-VGPR build
+#endif
+        const int p = qpel_direct<pel, serial_j>(refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1], maxv);
         if (d.t8 && (best_mode <= 3 || best8x8 == 0x4444)) {
             // TransformDecision [J] (item 29): sum of 4x4 SATDs vs sum of 8x8 SATDs of the residual
             s.pred[py4 * 16 + px4] = (pel)p;

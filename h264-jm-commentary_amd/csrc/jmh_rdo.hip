@@ -1,18 +1,22 @@
 // jmh_rdo.hip — encode_one_macroblock with RDOptimization = 1 [J] on the device (row f4, config 5):
 // the rate-distortion loop of rdopt.c (RDCost_for_macroblocks, RDCost_for_8x8blocks,
-// RDCost_for_4x4IntraBlocks) with J = SSD + lambda * R and R the CABAC rate of the slice's coding
-// state (jmh_cabac_rate.h, shared with the CPU oracle oracle/rdo.c).  DESIGN.md §9 has the
+// RDCost_for_4x4IntraBlocks; with Transform8x8Mode RDCost_for_8x8IntraBlocks and the 8x8 transform per
+// inter candidate) with J = SSD + lambda * R and R the CABAC rate of the slice's coding state
+// (jmh_cabac_rate.h; the CPU oracle oracle/rdo.c prices the same candidates with its own 9.3.4.2
+// coder, and tests/test_rate_xcheck.py compares the two on every candidate).  DESIGN.md §9 has the
 // schedule; one tick of the RD stage schedule runs
 //   k_rdo_inter   P MBs, one wave each: the EPZS searches, P8x8 block by block (the sub-modes coded a
 //                 pass each, rated on four lanes side by side, a wave-uniform decision), the
-//                 residual coding of the skip / 16x16 / 16x8 / 8x16 / P8x8 candidates and their chroma;
+//                 residual coding of the skip / 16x16 / 16x8 / 8x16 / P8x8 candidates (Transform8x8Mode:
+//                 16x16 / 16x8 / 8x16 / all-8x8 P8x8 again with the 8x8 transform) and their chroma;
 //   k_rdo_intra   all MBs, one wave each: Intra16x16, the four chroma intra modes, Intra4x4 by
-//                 per-block RD (9 modes x 16 lanes code in three passes, 9 lanes rate);
+//                 per-block RD (9 modes x 16 lanes code in three passes, 9 lanes rate); Transform8x8Mode:
+//                 Intra8x8 by per-block RD (a pass per mode, lane = sample, 9 lanes rate);
 //   k_rdo_final   all MBs: one lane per macroblock candidate rates it on its own LDS copy of the
 //                 contexts, the strict-'<' minimum of D + lambda R in JM's order wins; results,
 //                 reconstruction, the slice's next coding state, the fused DeblockMb.
 // Candidates travel to k_rdo_final through the tick's scratch (RdoScr, HBM).
-// docs/JM_SEMANTICS.md items 53-60 pin every RD choice.
+// docs/JM_SEMANTICS.md items 53-60 and 63 pin every RD choice.
 #include "jmh_epzs.h"
 #include "jmh_intra.h"
 #include "jmh_deblock.h"
@@ -33,8 +37,12 @@ __device__ __forceinline__ void jmr_lds_tables_load(int t, int n) {
     }
 }
 
-#define RD_NL 7       // luma candidates: 0 P_Skip, 1 16x16, 2 16x8, 3 8x16, 4 P8x8, 5 I16MB, 6 I4MB
-#define RD_NCAND 13   // macroblock-loop candidates: 5 inter + (I16, I4) x 4 chroma modes
+// luma candidates: 0 P_Skip, 1 16x16, 2 16x8, 3 8x16, 4 P8x8, 5 I16MB, 6 I4MB, 7 I8MB; Transform8x8Mode:
+// 8..10 the 16x16 / 16x8 / 8x16 and 11 the (all sub-modes 8x8) P8x8 with the 8x8 transform
+#define RD_NL 12
+#define RD_NCAND 21   // macroblock-loop candidates: 9 inter + (I16, I4, I8) x 4 chroma modes
+__device__ __forceinline__ int rd_cbase(int i) { return i >= 8 ? i - 7 : i; }   // an inter candidate's base / chroma
+__device__ __forceinline__ bool rd_t8(int i) { return i >= 7; }                 // luma with the 8x8 transform
 
 // J = D + lambda * R in double, no contraction (the oracle's gcc x86-64 build has none either)
 __device__ __forceinline__ double rd_cost(int dist, int bits, double lambda) {
@@ -86,8 +94,8 @@ struct RdoRate {
 template <class pel>
 struct RdoScr {
     RdoLuma<pel> L[RD_NL];
-    RdoChroma<pel> C[9];          // [0..4]: chroma of L[0..4]; [5 + m]: intra chroma mode m
-    RdoRate R[8];                 // [m]: I16MB with chroma mode m, [4 + m]: I4MB (available modes only)
+    RdoChroma<pel> C[9];          // [0..4]: chroma of L[0..4] (and of L[8..11]); [5 + m]: intra chroma mode m
+    RdoRate R[12];                // [m]: I16MB with chroma mode m, [4 + m]: I4MB, [8 + m]: I8MB (available modes only)
 };
 size_t jmh_rdo_scratch_bytes() { return sizeof(RdoScr<uint16_t>); }
 
@@ -279,7 +287,51 @@ __device__ __forceinline__ void luma_inter(const DevParams &d, RdoInterS<pel> &s
     if (lane == 0) { L->cbp = cbp; L->cbp_blk = cbp_blk; L->dist = dist; L->i16mode = 0; }
 }
 
+// LumaResidualCoding [J] of an inter candidate with transform_size_8x8_flag 1 (Transform8x8Mode,
+// item 63) on one wave, an 8x8 block per pass (lane = sample): MC of s.fmv, dct_luma8x8 (levels in
+// jmh_mb_result's CAVLC interleave), the same _LUMA_COEFF_COST_ zeroing per 8x8 block and per
+// macroblock.  The P8x8 assembly buffers (p8pred / p8rec / p8lev, cost8 / blk8) are free by now.
 template <class pel>
+__device__ __forceinline__ void luma_inter8(const DevParams &d, RdoInterS<pel> &s, const EWin<pel> &wn, RdoLuma<pel> *L, int mbx, int mby,
+                                            int lane) {
+    const int qp = d.qp + d.qpbd, maxv = d.maxv, rnd = q_round(d.qsel, 16 + qp / 6), x = lane & 7, y = lane >> 3;
+#pragma unroll 1
+    for (int b8 = 0; b8 < 4; b8++) {
+        const int px = 8 * (b8 & 1) + x, py = 8 * (b8 >> 1) + y, k = (py >> 2) * 4 + (px >> 2);
+        const int p = qpel_mb(d, s.e, wn, 4 * (16 * mbx + px) + s.fmv[k][0], 4 * (16 * mby + py) + s.fmv[k][1]);
+        const int c = wave_fwd8x8((int)s.e.org[py * 16 + px] - p, lane);
+        int lev, dq, cost;
+        const unsigned long long nz = wave_quant8(c, lane, qp, rnd, lev, dq, cost);
+        s.p8pred[py * 16 + px] = (pel)p;
+        s.p8rec[py * 16 + px] = (pel)wave_inv8x8(dq, lane, p, maxv);
+        s.p8lev[il_blk(b8, lane)][lane >> 2] = (int16_t)lev;
+        if (lane == 0) { s.cost8[b8] = cost; s.blk8[b8] = nz != 0; }
+    }
+    wave_lds_sync();
+    int sum = 0, keep = 0, cbp = 0, cbp_blk = 0;        // wave-uniform
+    for (int b8 = 0; b8 < 4; b8++) {
+        const int c8 = s.cost8[b8] <= 4 ? 0 : s.cost8[b8];   // _LUMA_COEFF_COST_
+        if (c8) {
+            keep |= 1 << b8;
+            if (s.blk8[b8]) { cbp |= 1 << b8; cbp_blk |= 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2); }
+        }
+        sum += c8;
+    }
+    if (sum <= 5) keep = cbp = cbp_blk = 0;             // _LUMA_MB_COEFF_COST_
+    int e2 = 0;
+    for (int i = lane; i < 256; i += 64) {
+        const int b8 = ((i >> 7) << 1) + ((i & 15) >> 3), kb = (keep >> b8) & 1;
+        const pel rv = kb ? s.p8rec[i] : s.p8pred[i];
+        L->rec[i] = rv;
+        L->luma[i >> 4][i & 15] = ((keep >> (((i >> 7) << 1) + ((i >> 4 & 3) >> 1))) & 1) ? s.p8lev[i >> 4][i & 15] : 0;
+        const int e = (int)s.e.org[i] - (int)rv;
+        e2 += e * e;
+    }
+    const int dist = wave_sum(e2);
+    if (lane == 0) { L->cbp = cbp; L->cbp_blk = cbp_blk; L->dist = dist; L->i16mode = 0; }
+}
+
+template <class pel, bool T8>
 __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
     const int a = mby * d.mbw + mbx, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
@@ -474,6 +526,25 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         if (lane == 0) scr->C[c].dist = dist;
         wave_lds_sync();
     }
+    // ---- Transform8x8Mode (item 63): the same motion with the 8x8 transform: 16x16 / 16x8 / 8x16 and
+    //      the P8x8 whose four blocks chose the 8x8 sub-mode; the chroma is the base candidate's
+    if constexpr (T8) {
+#pragma unroll 1
+        for (int c = 1; c <= 4; c++) {
+            if (c == 4 ? !(p8 && best8x8 == 0x4444) : !inter_on(d.isr, c)) continue;   // uniform
+            if (lane < 32) {
+                const int k = lane >> 1, cc = lane & 1, sm = c == 4 ? 4 : c;
+                const int v = s.e.all_mv[sm][k][cc];
+                s.fmv[k][cc] = (int16_t)v;
+                L[c + 7].mv[k][cc] = (int16_t)v;
+                L[c + 7].mvd[k][cc] = (int16_t)(v - s.e.pmv[sm][k][cc]);
+            }
+            if (lane < 4) L[c + 7].b8mode[lane] = (int8_t)(c == 4 ? 4 : c);
+            wave_lds_sync();
+            luma_inter8(d, s, wn, &L[c + 7], mbx, mby, lane);
+            wave_lds_sync();
+        }
+    }
     PSTAMP(52);
 }
 
@@ -481,7 +552,18 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
 //  role "intra" (k_rdo_intra): ONE WAVE per macroblock, wave-synchronous: Intra16x16, the chroma
 //  intra modes, Intra4x4 by RDCost_for_4x4IntraBlocks
 // ======================================================================================
+// the Intra8x8 decision's state (Transform8x8Mode only: the RDO-off-transform build keeps k_rdo_intra's LDS)
+template <class pel, bool T8>
+struct RdoI8S {
+    alignas(4) pel rec8[256];     // the Intra8x8 reconstruction in progress
+    int raw[25], av[25], f[25];   // the reference edge: [7 - y] left, [8] corner, [9 + x] top (8.3.2.2.1)
+    int16_t lev8[9][64];          // per mode: levels in 8x8 zig-zag order
+    alignas(4) pel r8[9][64];     // per mode: the block's reconstruction (raster)
+    int m8[4];                    // the decided modes
+};
 template <class pel>
+struct RdoI8S<pel, false> {};
+template <class pel, bool T8>
 struct RdoIntraS {
     alignas(4) pel org[256];
     alignas(4) pel rec[256];      // the Intra4x4 reconstruction in progress
@@ -489,7 +571,8 @@ struct RdoIntraS {
     Border bd;
     int8_t ipred_cur[16];
     alignas(4) uint8_t st0[JMR_NCTX];
-    alignas(4) uint8_t stc[9][JMR_NCTX];
+    alignas(4) uint8_t stc[T8 ? 12 : 9][JMR_NCTX];
+    RdoI8S<pel, T8> i8;
     jmr_mbinfo nbA, nbB;
     int P[13];
     int16_t lev[9][16];
@@ -499,15 +582,119 @@ struct RdoIntraS {
     int16_t dclev[16];
 };
 
-template <class pel>
-__device__ __forceinline__ int i4_lpix(const RdoIntraS<pel> &s, int x, int y) {
+template <class pel, bool T8>
+__device__ __forceinline__ int i4_lpix(const RdoIntraS<pel, T8> &s, int x, int y) {
     if (y < 0) return s.nb.rtop[x + 1];
     if (x < 0) return s.nb.rleft[y];
     return s.rec[16 * y + x];
 }
 
+// Intra8x8 (Transform8x8Mode, item 63): Mode_Decision_for_8x8IntraBlocks [J] by RDCost_for_8x8IntraBlocks,
+// the four blocks in order on one wave: the filtered reference edge (8.3.2.2.1), a pass per mode
+// (lane = sample: prediction, dct_luma8x8, reconstruction, SSD), lane m rates mode m from the
+// macroblock-start state, a wave-uniform strict-'<' decision; the winner reconstructs
 template <class pel>
-__device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
+__device__ __forceinline__ void rdo_intra8(const DevParams &d, RdoIntraS<pel, true> &s, RdoLuma<pel> &L, const jmr_mbinfo *A, const jmr_mbinfo *B,
+                                           uint32_t rg0, const MbAvail &mav, int mbx, int mby, int lane) {
+    RdoI8S<pel, true> &q = s.i8;
+    const int qp = d.qp + d.qpbd, maxv = d.maxv, rnd = q_round(d.qsel, 16 + qp / 6), W = d.W, pix_x = 16 * mbx, pix_y = 16 * mby;
+    const int x = lane & 7, y = lane >> 3;
+    const pel *recY = spl<pel>(d.recY);
+    int cbp = 0, blkm = 0;
+#pragma unroll 1
+    for (int b8 = 0; b8 < 4; b8++) {
+        const int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
+        const bool left = bx ? true : mav.L, up = by ? true : mav.T;
+        const bool ul = bx && by ? true : bx ? mav.T : by ? mav.L : mav.TL;
+        const bool ur = b8 == 0 ? mav.T : b8 == 1 ? mav.TR : b8 == 2;
+        if (lane < 25) {
+            int xm, ym;
+            bool av;
+            if (lane < 8) { xm = bx - 1; ym = by + 7 - lane; av = left; }
+            else if (lane == 8) { xm = bx - 1; ym = by - 1; av = ul; }
+            else { const int xx = lane - 9; xm = bx + (xx < 8 || ur ? xx : 7); ym = by - 1; av = up; }
+            int v = 0;
+            if (av) v = (xm >= 0 && xm < 16 && ym >= 0) ? q.rec8[ym * 16 + xm] : recY[(pix_y + ym) * W + pix_x + xm];
+            q.raw[lane] = v;
+            q.av[lane] = av;
+        }
+        for (int k = lane; k < 9 * (JMR_NCTX / 4); k += 64) {   // each rate lane's copy of the MB-start state
+            const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
+            reinterpret_cast<uint32_t *>(s.stc[m])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
+        }
+        wave_lds_sync();
+        if (lane < 25 && q.av[lane]) {
+            const int c = q.raw[lane];
+            const int lo = lane > 0 && q.av[lane - 1] ? q.raw[lane - 1] : c, hi = lane < 24 && q.av[lane + 1] ? q.raw[lane + 1] : c;
+            q.f[lane] = (lo + 2 * c + hi + 2) >> 2;
+        }
+        // predIntra8x8PredMode (8.3.2.1): this MB's earlier blocks, else the neighbour's 4x4 mode
+        const int ma = bx ? q.m8[b8 - 1] : s.bd.ipm[6 + (by >> 2)], mb = by ? q.m8[b8 - 2] : s.bd.ipm[1 + (bx >> 2)];
+        const int mpm = (ma < 0 || mb < 0) ? 2 : min(ma, mb);
+        wave_lds_sync();
+        int st = 0, sl = 0;
+        for (int i = 0; i < 8; i++) { st += up ? q.f[9 + i] : 0; sl += left ? q.f[i] : 0; }
+        const int dcv = up && left ? (st + sl + 8) >> 4 : up ? (st + 4) >> 3 : left ? (sl + 4) >> 3 : (maxv + 1) >> 1;
+        const int ov = s.org[(by + y) * 16 + bx + x];
+#pragma unroll 1
+        for (int m = 0; m < 9; m++) {                   // the nine modes' dct_luma8x8 (wave-uniform skips)
+            const bool ok = m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) ||
+                            ((m == 4 || m == 5 || m == 6) && up && left && ul);
+            if (!ok) continue;
+            const int p = i8_pred_px(q.f, dcv, m, x, y);
+            const int c = wave_fwd8x8(ov - p, lane);
+            int lev, dq, cost;
+            const unsigned long long nz = wave_quant8(c, lane, qp, rnd, lev, dq, cost);
+            const int rv = wave_inv8x8(dq, lane, p, maxv);
+            q.lev8[m][lane] = (int16_t)lev;
+            q.r8[m][lane] = (pel)rv;
+            const int dist = wave_sum((ov - rv) * (ov - rv));
+            if (lane == 0) { s.dist[m] = dist; s.nz[m] = nz != 0; }
+        }
+        wave_lds_sync();
+        {                                               // lane m: the block's rate in mode m
+            const int m = lane;
+            const bool ok = m < 9 && (m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) ||
+                                      ((m == 4 || m == 5 || m == 6) && up && left && ul));
+            if (ok) {
+                jmr_eng e = {s.stc[m], rg0, 0};
+                jmr_i8(&e, m == mpm ? -1 : m < mpm ? m : m - 1, q.lev8[m]);
+                s.bits[m] = e.bits;
+            }
+        }
+        wave_lds_sync();
+        double best = 1e30;                             // wave-uniform decision, strict '<'
+        int bm = 2;
+        for (int mm = 0; mm < 9; mm++) {
+            const bool ok = mm == 2 || ((mm == 0 || mm == 3 || mm == 7) && up) || ((mm == 1 || mm == 8) && left) ||
+                            ((mm == 4 || mm == 5 || mm == 6) && up && left && ul);
+            if (!ok) continue;
+            const double rd = rd_cost(s.dist[mm], s.bits[mm], d.lambda_rd);
+            if (rd < best) { best = rd; bm = mm; }
+        }
+        q.rec8[(by + y) * 16 + bx + x] = q.r8[bm][lane];
+        L.luma[il_blk(b8, lane)][lane >> 2] = q.lev8[bm][lane];
+        if (lane == 0) {
+            q.m8[b8] = bm;
+            L.ipm[(b8 >> 1) * 8 + (b8 & 1) * 2] = (int8_t)(bm == mpm ? -1 : bm < mpm ? bm : bm - 1);
+        }
+        if (s.nz[bm]) { cbp |= 1 << b8; blkm |= 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2); }
+        wave_lds_sync();
+    }
+    int e2 = 0;
+    for (int i = lane; i < 256; i += 64) {
+        L.rec[i] = q.rec8[i];
+        const int e = (int)s.org[i] - (int)q.rec8[i];
+        e2 += e * e;
+    }
+    if (lane < 16) L.imode[lane] = (int8_t)q.m8[((lane >> 3) << 1) + ((lane & 3) >> 1)];
+    if (lane < 32) L.mv[lane >> 1][lane & 1] = 0;
+    const int dist = wave_sum(e2);
+    if (lane == 0) { L.cbp = cbp; L.cbp_blk = blkm; L.dist = dist; L.i16mode = 0; }
+}
+
+template <class pel, bool T8>
+__device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, T8> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
     const int a = mby * d.mbw + mbx, W = d.W, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
@@ -672,30 +859,35 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
     const int dist = wave_sum(e2);
     if (lane == 0) { L[6].cbp = i4cbp; L[6].cbp_blk = i4blk; L[6].dist = dist; L[6].i16mode = 0; }
     if (lane < 32) L[6].mv[lane >> 1][lane & 1] = 0;
+    if constexpr (T8) {
+        wave_lds_sync();
+        rdo_intra8(d, s, L[7], A, B, rg0, mav, mbx, mby, lane);
+    }
     PSTAMP(56);
     // ---- RDCost_for_macroblocks' rate of the eight intra candidates (I16MB / I4MB x the chroma
-    //      modes), here beside k_rdo_inter rather than on k_rdo_final's critical path: lane k < 8
-    //      codes candidate k on its own copy of the slice state (the Intra4x4 copies, free now),
-    //      reading the candidates this wave wrote to the tick scratch
+    //      modes; Transform8x8Mode: and I8MB), here beside k_rdo_inter rather than on k_rdo_final's
+    //      critical path: lane k < 8 (12) codes candidate k on its own copy of the slice state (the
+    //      Intra4x4 copies, free now), reading the candidates this wave wrote to the tick scratch
+    constexpr int NI = T8 ? 12 : 8;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (int k = lane; k < 8 * (JMR_NCTX / 4); k += 64) {
+    for (int k = lane; k < NI * (JMR_NCTX / 4); k += 64) {
         const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
         reinterpret_cast<uint32_t *>(s.stc[m])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
     }
     wave_lds_sync();
     const int cm = lane & 3;
     const bool cok = cm == 0 || (cm == 1 ? avL : cm == 2 ? avT : avT && avL && avTL);
-    if (lane < 8 && cok) {
-        const RdoLuma<pel> &Lc = L[lane < 4 ? 5 : 6];
+    if (lane < NI && cok) {
+        const RdoLuma<pel> &Lc = L[5 + (lane >> 2)];
         const RdoChroma<pel> &C = scr->C[5 + cm];
         RdoRate &R = scr->R[lane];
         jmr_cand r;
-        r.mb_type = lane < 4 ? JMH_I16MB : JMH_I4MB;
+        r.mb_type = lane < 4 ? JMH_I16MB : lane < 8 ? JMH_I4MB : JMH_I8MB;
         r.cbp = Lc.cbp | C.cbpc << 4;
         r.i16mode = Lc.i16mode;
         r.cmode = cm;
-        r.t8 = 0;
+        r.t8 = lane >= 8;
         for (int q = 0; q < 4; q++) r.b8mode[q] = 0;
         r.ipm = Lc.ipm;
         r.mvd = Lc.mvd;
@@ -705,19 +897,19 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel> 
         r.cac = C.ac;
         r.mvw = R.mvw;
         jmr_eng en = {s.stc[lane], rg0, 0};
-        jmr_mb(&en, A, B, &r, d.slice_type == JMH_P_SLICE, 0, &R.out);
+        jmr_mb(&en, A, B, &r, d.slice_type == JMH_P_SLICE, T8, &R.out);
         R.bits = en.bits;
         R.range = en.range;
     }
     wave_lds_sync();
-    for (int k = lane; k < 8 * (JMR_NCTX / 4); k += 64) {
+    for (int k = lane; k < NI * (JMR_NCTX / 4); k += 64) {
         const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
         reinterpret_cast<uint32_t *>(scr->R[m].ctx)[j] = reinterpret_cast<const uint32_t *>(s.stc[m])[j];
     }
     PSTAMP(61);
 }
 
-template <class pel>
+template <class pel, bool T8>
 __global__ __launch_bounds__(NTE) void k_rdo_inter(const TickArgs t) {
     __shared__ RdoInterS<pel> s;
     const int nP = t.pre[t.nP], m = xcd_block(blockIdx.x, nP);
@@ -730,16 +922,16 @@ __global__ __launch_bounds__(NTE) void k_rdo_inter(const TickArgs t) {
     const DevParams d = tick_params(t, e);
     int mbx, mby;
     tick_mb(t, d, e, m, mbx, mby);
-    rdo_inter_mb(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
+    rdo_inter_mb<pel, T8>(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
     if (t.bprof && threadIdx.x == 0) {
         t.bprof[3 * blockIdx.x] = bt0;
         t.bprof[3 * blockIdx.x + 1] = wall_clock64();
         t.bprof[3 * blockIdx.x + 2] = 4;
     }
 }
-template <class pel>
+template <class pel, bool T8>
 __global__ __launch_bounds__(NTE) void k_rdo_intra(const TickArgs t) {
-    __shared__ RdoIntraS<pel> s;
+    __shared__ RdoIntraS<pel, T8> s;
     const int tot = t.pre[t.npic], m = xcd_block(blockIdx.x, tot);
     if (m >= tot) return;
     const unsigned long long bt0 = t.bprof ? wall_clock64() : 0;   // debug (JMH_BLOCK_PROF): role 1
@@ -747,7 +939,7 @@ __global__ __launch_bounds__(NTE) void k_rdo_intra(const TickArgs t) {
     const DevParams d = tick_params(t, e);
     int mbx, mby;
     tick_mb(t, d, e, m, mbx, mby);
-    rdo_intra_mb(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
+    rdo_intra_mb<pel, T8>(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
     if (t.bprof && threadIdx.x == 0) {
         unsigned long long *bp = t.bprof + 3 * xcd_grid(t.pre[t.nP]);
         bp[3 * blockIdx.x] = bt0;
@@ -770,9 +962,11 @@ struct RdoFinC {                  // of a chroma candidate (RdoChroma's first 27
     int16_t dc[2][4];
     int16_t ac[2][4][16];
 };
+// the inter candidates' LDS syntax slot: 0..4 and (Transform8x8Mode) 8..11 -> 5..8
+__device__ __forceinline__ int rd_fslot(int i) { return i < 5 ? i : i - 3; }
 template <class pel>
 struct RdoFinS {
-    RdoFinL fl[5];                // the inter candidates' syntax in LDS: the serial CABAC loops read it bin by bin
+    RdoFinL fl[9];                // the inter candidates' syntax in LDS: the serial CABAC loops read it bin by bin
     RdoFinC fc[5];
     int16_t mvw[RD_NCAND][16][2];   // jmr_mb's work buffers
     alignas(4) uint8_t st0[JMR_NCTX];
@@ -790,7 +984,8 @@ struct RdoFinS {
     DbkS<pel> db;
 };
 
-template <class pel>
+// T8: Transform8x8Mode (the 8x8-transform and I8MB candidates; jmr_mb's 8x8 residual path)
+template <class pel, bool T8>
 __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     __shared__ RdoFinS<pel> s;
     const int tid = threadIdx.x, tot = t.pre[t.npic];
@@ -812,28 +1007,34 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         if (tid == 0) s.rg0 = rg;
     } else if (tid < 128) rdo_nb_load(d, mbx, mby, s.nbA, s.nbB, s.hasA, s.hasB, tid - 64);
     else if (tid >= 160) jmr_lds_tables_load(tid - 160, 96);
-    else if (tid == 128) {                              // the candidates in JM's order
+    else if (tid == 128) {                              // the candidates in JM's order (item 63 with Transform8x8Mode)
         const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
+        const bool p8t8 = T8 && p8 && scr->L[4].b8mode[0] == 4 && scr->L[4].b8mode[1] == 4 && scr->L[4].b8mode[2] == 4 &&
+                          scr->L[4].b8mode[3] == 4;
         const bool cav[4] = {true, mav.L, mav.T, mav.T && mav.L && mav.TL};
+        static constexpr int8_t order[RD_NL] = {0, 1, 8, 2, 9, 3, 10, 4, 11, 5, 6, 7};
         int n = 0;
         for (int cm = 0; cm < 4; cm++) {
             if (!cav[cm]) continue;
-            for (int i = 0; i < RD_NL; i++) {
-                const bool valid = i >= 5 || (slice_p && (i == 0 || (i == 4 ? p8 : inter_on(d.isr, i))));
-                if (!valid || (cm != 0 && i < 5)) continue;
+            for (int oi = 0; oi < RD_NL; oi++) {
+                const int i = order[oi], b = rd_cbase(i);
+                const bool intra = i >= 5 && i <= 7;
+                bool valid = intra ? (i < 7 || T8) : slice_p && (b == 0 || (b == 4 ? p8 : inter_on(d.isr, b)));
+                if (i >= 8) valid = valid && T8 && (i != 11 || p8t8);
+                if (!valid || (cm != 0 && !intra)) continue;
                 s.ci[n] = i; s.ccm[n] = cm; n++;
             }
         }
         s.ncand = n;
         // the inter candidates' rates, one per wave (lanes of a wave in different syntax would cost
-        // the sum of their paths): wave 0 16x16, 1 16x8, 2 8x16 and P_Skip, 3 P8x8; the intra
-        // candidates' rates come from k_rdo_intra (RdoScr.R)
+        // the sum of their paths): wave 0 16x16, 1 16x8, 2 8x16 and P_Skip, 3 P8x8, each with both
+        // transform sizes; the intra candidates' rates come from k_rdo_intra (RdoScr.R)
         int fill[4] = {0, 0, 0, 0};
         for (int w = 0; w < 16; w++) s.kof[w >> 2][w & 3] = -1;
         for (int k = 0; k < n; k++) {
-            const int i = s.ci[k];
-            if (i >= 5) continue;
-            const int w = i == 1 ? 0 : i == 2 ? 1 : i == 4 ? 3 : 2;
+            const int i = s.ci[k], b = rd_cbase(i);
+            if (i >= 5 && i <= 7) continue;
+            const int w = b == 1 ? 0 : b == 2 ? 1 : b == 4 ? 3 : 2;
             s.kof[w][fill[w]++] = (int8_t)k;
         }
     }
@@ -842,16 +1043,17 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     // ---- one lane per candidate: its rate on its own copy of the coding state (lanes 0..3 of the
     //      four waves, grouped by macroblock type: kof)
     for (int i = tid; i < s.ncand * (JMR_NCTX / 4); i += NT) {   // the inter candidates' state copies
-        const int k = i / (JMR_NCTX / 4), j = i - k * (JMR_NCTX / 4);
-        if (s.ci[k] < 5) reinterpret_cast<uint32_t *>(s.stc[k])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
+        const int k = i / (JMR_NCTX / 4), j = i - k * (JMR_NCTX / 4), ci = s.ci[k];
+        if (ci < 5 || ci >= 8) reinterpret_cast<uint32_t *>(s.stc[k])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
     }
     {
         constexpr int nl = 672 / 4, nc = (int)sizeof(RdoFinC) / 4;
         static_assert(offsetof(RdoLuma<pel>, ipm) > 672 && offsetof(RdoFinL, ipm) == 672, "RdoFinL layout");
-        for (int i = tid; i < 5 * (nl + 4); i += NT) {
-            const int k = i / (nl + 4), j = i - k * (nl + 4);
+        const int nfl = T8 ? 9 : 5;
+        for (int i = tid; i < nfl * (nl + 4); i += NT) {
+            const int f = i / (nl + 4), j = i - f * (nl + 4), k = f < 5 ? f : f + 3;
             const uint32_t *src = reinterpret_cast<const uint32_t *>(&scr->L[k]);
-            reinterpret_cast<uint32_t *>(&s.fl[k])[j] = j < nl ? src[j] : reinterpret_cast<const uint32_t *>(scr->L[k].ipm)[j - nl];
+            reinterpret_cast<uint32_t *>(&s.fl[f])[j] = j < nl ? src[j] : reinterpret_cast<const uint32_t *>(scr->L[k].ipm)[j - nl];
         }
         for (int i = tid; i < 5 * nc; i += NT) {
             const int k = i / nc, j = i - k * nc;
@@ -861,8 +1063,8 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         const int nw = (int)sizeof(jmr_mbinfo) / 4;
         for (int i = tid; i < s.ncand * (nw + 2); i += NT) {
             const int k = i / (nw + 2), j = i - k * (nw + 2), ci = s.ci[k];
-            if (ci < 5) continue;
-            const RdoRate &R = scr->R[(ci == 5 ? 0 : 4) + s.ccm[k]];
+            if (ci < 5 || ci > 7) continue;
+            const RdoRate &R = scr->R[4 * (ci - 5) + s.ccm[k]];
             if (j < nw) reinterpret_cast<uint32_t *>(&s.out[k])[j] = reinterpret_cast<const uint32_t *>(&R.out)[j];
             else if (j == nw) s.rgo[k] = R.range;
             else {
@@ -875,21 +1077,21 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     PSTAMP(58);
     const int kc = (tid & 63) < 4 ? s.kof[tid >> 6][tid & 3] : -1;
     if (kc >= 0) {
-        const int i = s.ci[kc];
+        const int i = s.ci[kc], b = rd_cbase(i);
         const RdoLuma<pel> &L = scr->L[i];
-        const RdoChroma<pel> &C = scr->C[i];
+        const RdoChroma<pel> &C = scr->C[b];
         jmr_eng en = {s.stc[kc], s.rg0, 0};
         if (i == 0) jmr_skip(&en, A, B, &s.out[kc]);
         else {
             jmr_cand r;
-            r.mb_type = i == 4 ? JMH_P8x8 : i;
+            r.mb_type = b == 4 ? JMH_P8x8 : b;
             r.cbp = L.cbp | C.cbpc << 4;
             r.i16mode = L.i16mode;
             r.cmode = 0;
-            r.t8 = 0;
+            r.t8 = T8 && i >= 8;
             for (int q = 0; q < 4; q++) r.b8mode[q] = L.b8mode[q];
-            const RdoFinL &FL = s.fl[i];
-            const RdoFinC &FC = s.fc[i];
+            const RdoFinL &FL = s.fl[rd_fslot(i)];
+            const RdoFinC &FC = s.fc[b];
             r.ipm = FL.ipm;
             r.mvd = FL.mvd;
             r.luma = FL.luma;
@@ -897,7 +1099,7 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
             r.cdc = FC.dc;
             r.cac = FC.ac;
             r.mvw = s.mvw[kc];
-            jmr_mb(&en, A, B, &r, slice_p, 0, &s.out[kc]);
+            jmr_mb(&en, A, B, &r, slice_p, T8, &s.out[kc]);
         }
         s.bits[kc] = en.bits;
         s.rgo[kc] = en.range;
@@ -914,12 +1116,13 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     }
     __syncthreads();
     // ---- the chosen macroblock: results, reconstruction, picture arrays, coding state
-    const int w = s.win, bi = s.ci[w], bcm = s.ccm[w];
+    const int w = s.win, bi = s.ci[w], bcm = s.ccm[w], bb = rd_cbase(bi);
     const RdoLuma<pel> &L = scr->L[bi];
-    const RdoChroma<pel> &C = scr->C[bi >= 5 ? 5 + bcm : bi];
-    const bool is_intra = bi >= 5;
-    const int mb_type = bi == 0 ? JMH_PSKIP : bi == 4 ? JMH_P8x8 : bi == 5 ? JMH_I16MB : bi == 6 ? JMH_I4MB : bi;
+    const bool is_intra = bi >= 5 && bi <= 7;
+    const RdoChroma<pel> &C = scr->C[is_intra ? 5 + bcm : bb];
+    const int mb_type = bi == 0 ? JMH_PSKIP : bb == 4 ? JMH_P8x8 : bi == 5 ? JMH_I16MB : bi == 6 ? JMH_I4MB : bi == 7 ? JMH_I8MB : bb;
     const int cbp = L.cbp | C.cbpc << 4, cbp_blk = L.cbp_blk;
+    const bool tr8 = T8 && rd_t8(bi) && (mb_type == JMH_I8MB || (cbp & 15));   // transform_size_8x8_flag
     jmh_mb_result *res = d.res + a;
     if (tid == 0) {
         res->mb_type = (int16_t)mb_type;
@@ -932,7 +1135,7 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         }
         res->i16mode = (int8_t)(mb_type == JMH_I16MB ? L.i16mode : 0);
         res->c_ipred_mode = (int8_t)(is_intra ? bcm : 0);
-        res->transform_8x8 = 0; res->pad0 = 0;
+        res->transform_8x8 = (int8_t)tr8; res->pad0 = 0;
         res->min_cost = s.bits[w];                      // the chosen candidate's rate (bits)
         res->reserved = 0;
     }
@@ -940,7 +1143,7 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     res->luma[blk][l] = L.luma[blk][l];
     if (tid < 16) {
         const int k = tid;
-        const int ip = mb_type == JMH_I4MB ? L.imode[k] : 2;
+        const int ip = mb_type == JMH_I4MB || mb_type == JMH_I8MB ? L.imode[k] : 2;
         const int mx = is_intra ? 0 : L.mv[k][0], my = is_intra ? 0 : L.mv[k][1];
         res->ipred[k] = (int8_t)ip;
         res->mv[k][0] = (int16_t)mx; res->mv[k][1] = (int16_t)my;
@@ -968,7 +1171,7 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     {
         const int slice = a / d.slice_mbs;
         uint32_t *dst = reinterpret_cast<uint32_t *>(d.rp->cab + (size_t)slice * JMR_NCTX);
-        const uint8_t *win_ctx = is_intra ? scr->R[(bi == 5 ? 0 : 4) + bcm].ctx : s.stc[w];
+        const uint8_t *win_ctx = is_intra ? scr->R[4 * (bi - 5) + bcm].ctx : s.stc[w];
         if (tid < JMR_NCTX / 4) dst[tid] = reinterpret_cast<const uint32_t *>(win_ctx)[tid];
         const int nw = (int)sizeof(jmr_mbinfo) / 4;
         if (tid >= 128 && tid < 128 + nw)
@@ -982,7 +1185,7 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     // ---- DeblockMb [J] (jmh_deblock.h)
     if (d.dbkY) {
         const int qpi = iclip(-d.qpbd, 51, d.qp + d.cqp_off), qpcy = qpi < 0 ? qpi : c_qpc[qpi];
-        deblock_mb(d, s.db, s.rec, s.cfin, s.fmv, is_intra, cbp_blk, false, d.qp, qpcy, mbx, mby, tid);
+        deblock_mb(d, s.db, s.rec, s.cfin, s.fmv, is_intra, cbp_blk, tr8, d.qp, qpcy, mbx, mby, tid);
     }
     PSTAMP(60);
     if (t.bprof_fin && tid == 0) {
@@ -1003,17 +1206,21 @@ hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st, hipStream_t side, h
     if (side && nP) {
         if ((err = hipEventRecord(fork, st)) != hipSuccess || (err = hipStreamWaitEvent(side, fork, 0)) != hipSuccess) return err;
     } else ist = st;
-    if (nP) {
-        if (t.bd > 8) hipLaunchKernelGGL(k_rdo_inter<uint16_t>, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
-        else hipLaunchKernelGGL(k_rdo_inter<uint8_t>, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
-    }
-    if (t.bd > 8) hipLaunchKernelGGL(k_rdo_intra<uint16_t>, dim3(xcd_grid(tot)), dim3(NTE), 0, ist, t);
-    else hipLaunchKernelGGL(k_rdo_intra<uint8_t>, dim3(xcd_grid(tot)), dim3(NTE), 0, ist, t);
+    // Transform8x8Mode: the instantiations with the 8x8-transform candidates (the others keep their
+    // registers and LDS)
+    typedef void (*Kern)(const TickArgs);
+    const Kern kin = t.bd > 8 ? (t.t8 ? k_rdo_inter<uint16_t, true> : k_rdo_inter<uint16_t, false>)
+                              : (t.t8 ? k_rdo_inter<uint8_t, true> : k_rdo_inter<uint8_t, false>);
+    const Kern kia = t.bd > 8 ? (t.t8 ? k_rdo_intra<uint16_t, true> : k_rdo_intra<uint16_t, false>)
+                              : (t.t8 ? k_rdo_intra<uint8_t, true> : k_rdo_intra<uint8_t, false>);
+    if (nP) hipLaunchKernelGGL(kin, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
+    hipLaunchKernelGGL(kia, dim3(xcd_grid(tot)), dim3(NTE), 0, ist, t);
     if ((err = hipGetLastError()) != hipSuccess) return err;
     if (ist != st) {
         if ((err = hipEventRecord(join, ist)) != hipSuccess || (err = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return err;
     }
-    if (t.bd > 8) hipLaunchKernelGGL(k_rdo_final<uint16_t>, dim3(xcd_grid(tot)), dim3(NT), 0, st, t);
-    else hipLaunchKernelGGL(k_rdo_final<uint8_t>, dim3(xcd_grid(tot)), dim3(NT), 0, st, t);
+    const Kern kfi = t.bd > 8 ? (t.t8 ? k_rdo_final<uint16_t, true> : k_rdo_final<uint16_t, false>)
+                              : (t.t8 ? k_rdo_final<uint8_t, true> : k_rdo_final<uint8_t, false>);
+    hipLaunchKernelGGL(kfi, dim3(xcd_grid(tot)), dim3(NT), 0, st, t);
     return hipGetLastError();
 }

@@ -3,7 +3,7 @@ schedule must equal the CPU oracle (oracle/rdo.c) bit for bit -- every macrobloc
 (mode, MVs, levels, the chosen candidate's rate in min_cost) and the reconstruction -- and the
 product lencod with the device RD loop must write the same bitstream as the CPU lencod, with the
 writer's RD rate check at 0 mismatches.  JM parity of the RD choices is unpinned
-(docs/JM_SEMANTICS.md items 53-60)."""
+(docs/JM_SEMANTICS.md items 53-60, 63)."""
 import tempfile
 
 import numpy as np
@@ -75,6 +75,36 @@ def test_rdo_config5_width_3840():
     rdo_pair(w, h, pics, 28, bd=10, search_range=32, slice_mbs=240)
 
 
+# ---- Transform8x8Mode 1 with RDO on (docs/JM_SEMANTICS.md item 63): I8MB by RDCost_for_8x8IntraBlocks,
+#      16x16 / 16x8 / 8x16 / all-8x8 P8x8 each also with transform_size_8x8_flag 1
+@pytest.mark.parametrize("kw,qp,cqp", [
+    (dict(search_range=16), 28, 0),
+    (dict(search_range=8), 8, 0),
+    (dict(search_range=8), 44, -3),
+    (dict(search_range=16, slice_mbs=11), 34, 2),
+    (dict(search_range=8, inter_search=(1, 1, 1, 1, 0, 0, 0), jm_version=10), 24, 0),   # P8x8 = all 8x8
+])
+def test_rdo_t8_configs(kw, qp, cqp):
+    pics = moving_seq(176, 144, 3, seed=60 + qp)
+    res = rdo_pair(176, 144, pics, qp, cqp, transform_8x8_mode=1, **kw)
+    assert res["transform_8x8"].any()
+
+
+@pytest.mark.parametrize("bd,qp", [(10, 28), (9, 6)])
+def test_rdo_t8_high10(bd, qp):
+    pics = hbd_seq(176, 144, 3, seed=95 + qp, bd=bd)
+    rdo_pair(176, 144, pics, qp, 0, bd=bd, search_range=16, slice_mbs=11, transform_8x8_mode=1)
+
+
+def test_rdo_t8_config5_width_3840():
+    """Config 5 with Transform8x8Mode 1 at its real width: High 10, one MB row per slice, EPZS SR 32,
+    RDO on with the 8x8-transform candidates and I8MB."""
+    w, h = 3840, 96
+    pics = hbd_seq(w, h, 3, seed=44, bd=10)
+    res = rdo_pair(w, h, pics, 28, bd=10, search_range=32, slice_mbs=240, transform_8x8_mode=1)
+    assert res["transform_8x8"].any()
+
+
 @pytest.mark.parametrize("slice_mbs", [40, 0, 100])
 def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
     """Pictures in flight on the RD stage schedule (one-row slices: diagonals, lag 16; one slice
@@ -102,6 +132,11 @@ def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
     ["InputFile=synthetic:73", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
      "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "SliceMode=1", "SliceArgument=22",
      "LoopFilterParametersFlag=1", "LoopFilterAlphaC0Offset=2", "LoopFilterBetaOffset=-1"],
+    ["InputFile=synthetic:74", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
+     "ProfileIDC=100", "Transform8x8Mode=1", "IntraPeriod=3"],
+    ["InputFile=synthetic:75", "FramesToBeEncoded=3", "SourceWidth=352", "SourceHeight=96", "SearchRange=32",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SliceMode=1",
+     "SliceArgument=22"],
 ])
 def test_rdo_lencod_bitstream_identical(extra):
     """The product lencod (device RD loop, device deblocking, pipelined pictures, writer threads)
@@ -118,7 +153,6 @@ def test_rdo_lencod_bitstream_identical(extra):
 
 
 def test_rdo_rejects_unsupported():
-    for kw in (dict(rdo=1, symbol_mode=0, search_mode=3), dict(rdo=1, symbol_mode=1, search_mode=0),
-               dict(rdo=1, symbol_mode=1, search_mode=3, transform_8x8_mode=1)):
+    for kw in (dict(rdo=1, symbol_mode=0, search_mode=3), dict(rdo=1, symbol_mode=1, search_mode=0)):
         with pytest.raises(jmhip.JmhError):
             jmhip.Encoder(64, 48, search_range=8, **kw)

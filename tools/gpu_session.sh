@@ -17,6 +17,7 @@
 #   c5      bench.py --config 5 (High 10, RDO on, 240-MB slices; with CPU baseline)
 #   c5q     the same, 60 steps, no CPU baseline / host path (a quick GPU number)
 #   c5off   config 5's RDO-off variant (EPZS + 8x8 transform)
+#   c5t8    config 5 with Transform8x8Mode 1 (RDO on: 8x8-transform candidates, I8MB; with CPU baseline)
 #   lencodc5 lencodc3 with one slice and with SliceArgument 240 (135 one-row slices per picture)
 #   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
 #   profc3  the same for config 3
@@ -66,6 +67,8 @@ for s in "$@"; do
             cat gpurun_out/${TAG}_c3_bench.json ;;
     c5)     run c5 1100 python bench.py --config 5 > gpurun_out/${TAG}_c5_bench.json 2> gpurun_out/${TAG}_c5_bench.err || exit $?
             cat gpurun_out/${TAG}_c5_bench.json ;;
+    c5t8)   run c5t8 1100 python bench.py --config 5 --t8 1 > gpurun_out/${TAG}_c5t8_bench.json 2> gpurun_out/${TAG}_c5t8_bench.err || exit $?
+            cat gpurun_out/${TAG}_c5t8_bench.json ;;
     c5q)    run c5q 600 python bench.py --config 5 --steps 60 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_c5q_bench.json \
                 2> gpurun_out/${TAG}_c5q_bench.err || exit $?
             cat gpurun_out/${TAG}_c5q_bench.json ;;
