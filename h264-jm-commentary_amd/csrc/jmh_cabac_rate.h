@@ -136,8 +136,16 @@ typedef struct jmr_mbinfo {
     uint8_t pad;
     uint16_t cbf_l;       /* luma 4x4 (raster); 8x8 transform: the 8x8 block's cbp bit on its four */
     uint16_t pad2;
-    int16_t mvd_r[4][2];  /* mvd_l0 of the right column (rows 0..3): A of the right neighbour   */
-    int16_t mvd_b[4][2];  /* of the bottom row (columns 0..3): B of the lower neighbour         */
+    union {               /* one entropy coder per slice: the record keeps the same size for both */
+        struct {
+            int16_t mvd_r[4][2];  /* CABAC: mvd_l0 of the right column (rows 0..3): A of the right neighbour */
+            int16_t mvd_b[4][2];  /*   of the bottom row (columns 0..3): B of the lower neighbour          */
+        };
+        struct {
+            uint8_t tcr[8], tcb[8];   /* SymbolMode 0 (jmh_cavlc_rate.h): TotalCoeff of the right column /
+                                         bottom row: luma 0..3, Cb 4..5, Cr 6..7 (zero for P_Skip)      */
+        };
+    };
 } jmr_mbinfo;
 
 /* a candidate of the macroblock-level RD loop (RDCost_for_macroblocks) */
@@ -159,6 +167,7 @@ typedef struct jmr_cur {
     int16_t mvd[16][2];
     uint16_t cbf_l;
     uint16_t cbp;
+    uint8_t tc[24];       /* SymbolMode 0: the decided blocks' TotalCoeff (jmh_cavlc_rate.h)      */
 } jmr_cur;
 
 /* coded_block_flag condTermFlagN (9.3.3.1.1.9) of luma 4x4 (x4, y4) of neighbour n (NULL: not

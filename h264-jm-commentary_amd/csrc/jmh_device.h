@@ -54,7 +54,7 @@ struct RdoPic {
     int32_t lf;                          // LAMBDA_FACTOR(sqrt(lambda_mode)) of the motion searches
     int32_t pad;
     uint8_t *cab;                        // [slice][JMR_NCTX] context states (state << 1 | valMPS)
-    uint32_t *range;                     // [slice] codIRange
+    uint32_t *range;                     // [slice] codIRange (CAVLC: the mb_skip_run so far)
     jmr_mbinfo *mbi;                     // [MB]
 };
 
@@ -99,6 +99,8 @@ struct DevParams {
     int lf;                     // LAMBDA_FACTOR of the motion searches: 65536 * lambda_motion (RDO
                                 //   off, integer lambda), the host's RDO one (RDOptimization 1)
     double lambda_rd;           // RDOptimization 1: lambda_mode
+    int cavlc;                  // RDOptimization 1 with SymbolMode 0: CAVLC rates (jmh_cavlc_rate.h, item 64);
+                                //   RdoPic.range[slice] then holds the slice's mb_skip_run so far
     const RdoPic *rp;           // RDOptimization 1: the picture's RD state
 };
 
@@ -148,6 +150,7 @@ struct TickArgs {
     int slice_mbs;                       // SliceMode 1: MBs per slice (>= 1; mbw * mbh for one slice)
     int bd;                              // bit depth: 8 (uint8_t samples) or 9 / 10 (uint16_t, High 10)
     int rdo;                             // RDOptimization 1: k_rdo_inter + k_rdo_intra + k_rdo_final on the stage
+                                         //   (1: CABAC rates, 2: CAVLC rates, SymbolMode 0)
     const int32_t *sched, *soff;         //   schedule: MB addresses in stage order, offsets per stage
     void *rscr;                          //   the tick's candidate scratch (RdoScr per tick MB)
     const uint32_t *ordtab;              // FFS order keys, [NPK / 2][NTA] packed pairs (jmh_create)
@@ -200,6 +203,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.slice_type = q.slice_type; d.qp = q.qp; d.lambda_mode = q.lambda_mode; d.lambda_motion = q.lambda_motion;
     d.cqp_off = q.cqp_off; d.qsel = q.qsel; d.diag = q.diag; d.y_min = q.y_min;
     d.rdo = t.rdo;
+    d.cavlc = t.rdo == 2;
     d.lf = q.lambda_motion << 16;
     d.lambda_rd = 0;
     d.rp = nullptr;

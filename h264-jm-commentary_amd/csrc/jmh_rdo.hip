@@ -15,8 +15,11 @@
 //   k_rdo_final   all MBs: one lane per macroblock candidate rates it on its own LDS copy of the
 //                 contexts, the strict-'<' minimum of D + lambda R in JM's order wins; results,
 //                 reconstruction, the slice's next coding state, the fused DeblockMb.
-// Candidates travel to k_rdo_final through the tick's scratch (RdoScr, HBM).
-// docs/JM_SEMANTICS.md items 53-60 and 63 pin every RD choice.
+// Candidates travel to k_rdo_final through the tick's scratch (RdoScr, HBM).  SymbolMode 0: the same
+// loop with R the CAVLC bit count (jmh_cavlc_rate.h: nC from the neighbours' and the decided blocks'
+// TotalCoeff, the slice's mb_skip_run in place of the coding state; oracle/cavlc_bits.c is its check).
+// docs/JM_SEMANTICS.md items 53-60, 63 and 64 pin every RD choice.
+#include <type_traits>
 #include "jmh_epzs.h"
 #include "jmh_intra.h"
 #include "jmh_deblock.h"
@@ -28,6 +31,7 @@ __shared__ uint8_t g_jmr_tlps[64];   // transIdxLPS
 #define JMR_TLPS(s) g_jmr_tlps[s]
 #endif
 #include "jmh_cabac_rate.h"
+#include "jmh_cavlc_rate.h"
 
 // the LDS tables by threads [0, n); the caller synchronises before the first bin
 __device__ __forceinline__ void jmr_lds_tables_load(int t, int n) {
@@ -100,9 +104,11 @@ struct RdoScr {
 size_t jmh_rdo_scratch_bytes() { return sizeof(RdoScr<uint16_t>); }
 
 // the coding state of the slice at the start of macroblock a into st (LDS, 4-aligned) by threads
-// [0, n): initialised (9.3.1.1) at the slice's first macroblock; returns codIRange
+// [0, n): initialised (9.3.1.1) at the slice's first macroblock; returns codIRange.  CAVLC (item 64):
+// no contexts; returns the slice's mb_skip_run before a
 __device__ __forceinline__ uint32_t rdo_state_load(const DevParams &d, int a, uint8_t *st, int t, int n) {
     const int slice = a / d.slice_mbs;
+    if (d.cavlc) return a % d.slice_mbs == 0 ? 0 : d.rp->range[slice];
     if (a % d.slice_mbs == 0) {
         for (int i = t; i < JMR_NCTX; i += n) st[i] = jmr_init_one(i, d.slice_type != JMH_P_SLICE, d.qp);
         return 510;
@@ -428,18 +434,24 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
                 tp->mvd8[w][lane][1] = (int16_t)(s.e.all_mv[sm][kk][1] - s.e.pmv[sm][kk][1]);
             }
         }
-        for (int i = lane; i < JMR_NCTX; i += 64) {     // each rate lane's copy of the running state
-            const int w = i / (JMR_NCTX / 4), j = i % (JMR_NCTX / 4);
-            reinterpret_cast<uint32_t *>(tp->stc[w])[j] = reinterpret_cast<const uint32_t *>(s.strun)[j];
-        }
+        if (!d.cavlc)
+            for (int i = lane; i < JMR_NCTX; i += 64) {   // each rate lane's copy of the running state
+                const int w = i / (JMR_NCTX / 4), j = i % (JMR_NCTX / 4);
+                reinterpret_cast<uint32_t *>(tp->stc[w])[j] = reinterpret_cast<const uint32_t *>(s.strun)[j];
+            }
         wave_lds_sync();
         if (l == 0 && inter_on(d.isr, 4 + b4)) {        // RDCost_for_8x8blocks' rate, sub-mode 4 + b4
             const int w = b4;
-            jmr_eng e = {tp->stc[w], rgrun, 0};
             s.curc[w] = s.currun;
-            jmr_b8(&e, A, B, &s.curc[w], b8, 4 + w, (const int16_t(*)[2])tp->mvd8[w], s.cost8[w] > 0, (const int16_t(*)[16])tp->lev8[w]);
-            s.bits8[w] = e.bits;
-            s.rgc[w] = e.range;
+            if (d.cavlc)                                // the decided blocks' TotalCoeff (nC)
+                s.bits8[w] = jmv_b8(A, B, &s.curc[w], b8, 4 + w, (const int16_t(*)[2])tp->mvd8[w], s.cost8[w] > 0,
+                                    (const int16_t(*)[16])tp->lev8[w]);
+            else {
+                jmr_eng e = {tp->stc[w], rgrun, 0};
+                jmr_b8(&e, A, B, &s.curc[w], b8, 4 + w, (const int16_t(*)[2])tp->mvd8[w], s.cost8[w] > 0, (const int16_t(*)[16])tp->lev8[w]);
+                s.bits8[w] = e.bits;
+                s.rgc[w] = e.range;
+            }
         }
         wave_lds_sync();
         double best = 1e30;                             // wave-uniform decision
@@ -450,9 +462,9 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
                 if (rd < best) { best = rd; bm = w; }
             }
         best8x8 |= (4 + bm) << (4 * b8);
-        rgrun = s.rgc[bm];
+        if (!d.cavlc) rgrun = s.rgc[bm];
         if (s.cost8[bm]) { p8cbp |= 1 << b8; p8blk |= s.blk8[bm]; p8cnt += s.cost8[bm]; }
-        if (lane < JMR_NCTX / 4) reinterpret_cast<uint32_t *>(s.strun)[lane] = reinterpret_cast<const uint32_t *>(tp->stc[bm])[lane];
+        if (!d.cavlc && lane < JMR_NCTX / 4) reinterpret_cast<uint32_t *>(s.strun)[lane] = reinterpret_cast<const uint32_t *>(tp->stc[bm])[lane];
         if (lane < (int)sizeof(jmr_cur) / 4) reinterpret_cast<uint32_t *>(&s.currun)[lane] = reinterpret_cast<const uint32_t *>(&s.curc[bm])[lane];
         {                                               // the decided block into the P8x8 candidate
             const int yy = lane >> 3, xx = lane & 7;
@@ -574,6 +586,8 @@ struct RdoIntraS {
     alignas(4) uint8_t stc[T8 ? 12 : 9][JMR_NCTX];
     RdoI8S<pel, T8> i8;
     jmr_mbinfo nbA, nbB;
+    uint8_t tcd[24];              // CAVLC: the TotalCoeff of the blocks decided so far (nC, item 64)
+    uint8_t tcm[9][4];            //   ... of each mode's block (Intra4x4: [m][0]; Intra8x8: its four 4x4)
     int P[13];
     int16_t lev[9][16];
     pel r4[9][16];
@@ -593,7 +607,7 @@ __device__ __forceinline__ int i4_lpix(const RdoIntraS<pel, T8> &s, int x, int y
 // the four blocks in order on one wave: the filtered reference edge (8.3.2.2.1), a pass per mode
 // (lane = sample: prediction, dct_luma8x8, reconstruction, SSD), lane m rates mode m from the
 // macroblock-start state, a wave-uniform strict-'<' decision; the winner reconstructs
-template <class pel>
+template <class pel, bool CAV>
 __device__ __forceinline__ void rdo_intra8(const DevParams &d, RdoIntraS<pel, true> &s, RdoLuma<pel> &L, const jmr_mbinfo *A, const jmr_mbinfo *B,
                                            uint32_t rg0, const MbAvail &mav, int mbx, int mby, int lane) {
     RdoI8S<pel, true> &q = s.i8;
@@ -618,7 +632,7 @@ __device__ __forceinline__ void rdo_intra8(const DevParams &d, RdoIntraS<pel, tr
             q.raw[lane] = v;
             q.av[lane] = av;
         }
-        for (int k = lane; k < 9 * (JMR_NCTX / 4); k += 64) {   // each rate lane's copy of the MB-start state
+        for (int k = lane; k < 9 * (JMR_NCTX / 4) && !CAV; k += 64) {   // each rate lane's copy of the MB-start state
             const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
             reinterpret_cast<uint32_t *>(s.stc[m])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
         }
@@ -656,7 +670,8 @@ __device__ __forceinline__ void rdo_intra8(const DevParams &d, RdoIntraS<pel, tr
             const int m = lane;
             const bool ok = m < 9 && (m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) ||
                                       ((m == 4 || m == 5 || m == 6) && up && left && ul));
-            if (ok) {
+            if (ok && CAV) s.bits[m] = jmv_i8(A, B, s.tcd, b8, m == mpm ? -1 : m < mpm ? m : m - 1, q.lev8[m], s.tcm[m]);
+            else if (ok) {
                 jmr_eng e = {s.stc[m], rg0, 0};
                 jmr_i8(&e, m == mpm ? -1 : m < mpm ? m : m - 1, q.lev8[m]);
                 s.bits[m] = e.bits;
@@ -678,6 +693,7 @@ __device__ __forceinline__ void rdo_intra8(const DevParams &d, RdoIntraS<pel, tr
             q.m8[b8] = bm;
             L.ipm[(b8 >> 1) * 8 + (b8 & 1) * 2] = (int8_t)(bm == mpm ? -1 : bm < mpm ? bm : bm - 1);
         }
+        if (lane < 4) s.tcd[((b8 >> 1) * 2 + (lane >> 1)) * 4 + (b8 & 1) * 2 + (lane & 1)] = s.tcm[bm][lane];
         if (s.nz[bm]) { cbp |= 1 << b8; blkm |= 0x33 << ((b8 >> 1) * 8 + (b8 & 1) * 2); }
         wave_lds_sync();
     }
@@ -693,7 +709,7 @@ __device__ __forceinline__ void rdo_intra8(const DevParams &d, RdoIntraS<pel, tr
     if (lane == 0) { L.cbp = cbp; L.cbp_blk = blkm; L.dist = dist; L.i16mode = 0; }
 }
 
-template <class pel, bool T8>
+template <class pel, bool T8, bool CAV>
 __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, T8> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
     const int a = mby * d.mbw + mbx, W = d.W, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
@@ -773,6 +789,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
     PSTAMP(55);
     int i4cbp = 0, i4blk = 0;
     const int rnd = q_round(d.qsel, 15 + qp / 6);
+    if (lane < 24) s.tcd[lane] = 0;
     int i4e[3];                                         // the lane's prediction formulas, once
 #pragma unroll
     for (int pass = 0; pass < 3; pass++) i4e[pass] = 4 * pass + b4 < 9 ? c_i4tab[4 * pass + b4][l] : 0;
@@ -795,7 +812,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
         const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + bx4];
         const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + by4];
         const int mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
-        for (int k = lane; k < 9 * (JMR_NCTX / 4); k += 64) {   // each rate lane's copy of the MB-start state
+        for (int k = lane; k < 9 * (JMR_NCTX / 4) && !CAV; k += 64) {   // each rate lane's copy of the MB-start state
             const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
             reinterpret_cast<uint32_t *>(s.stc[m])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
         }
@@ -823,7 +840,11 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
         {                                               // lane m: the block's rate in mode m
             const int m = lane;
             const bool avm = m < 9 && (m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul));
-            if (avm) {
+            if (avm && CAV) {
+                int tc;
+                s.bits[m] = jmv_i4(A, B, s.tcd, bx4, by4, m == mpm ? -1 : m < mpm ? m : m - 1, s.lev[m], &tc);
+                s.tcm[m][0] = (uint8_t)tc;
+            } else if (avm) {
                 jmr_eng e = {s.stc[m], rg0, 0};
                 jmr_i4(&e, A, B, bx4, by4, m == mpm ? -1 : m < mpm ? m : m - 1, s.lev[m]);
                 s.bits[m] = e.bits;
@@ -839,6 +860,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
             if (rd < best) { best = rd; bm = mm; }
         }
         if (lane == 0) {
+            s.tcd[blk] = s.tcm[bm][0];
             s.ipred_cur[blk] = (int8_t)bm;
             L[6].imode[blk] = (int8_t)bm;
             L[6].ipm[blk] = (int8_t)(bm == mpm ? -1 : bm < mpm ? bm : bm - 1);
@@ -860,8 +882,9 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
     if (lane == 0) { L[6].cbp = i4cbp; L[6].cbp_blk = i4blk; L[6].dist = dist; L[6].i16mode = 0; }
     if (lane < 32) L[6].mv[lane >> 1][lane & 1] = 0;
     if constexpr (T8) {
+        if (lane < 24) s.tcd[lane] = 0;
         wave_lds_sync();
-        rdo_intra8(d, s, L[7], A, B, rg0, mav, mbx, mby, lane);
+        rdo_intra8<pel, CAV>(d, s, L[7], A, B, rg0, mav, mbx, mby, lane);
     }
     PSTAMP(56);
     // ---- RDCost_for_macroblocks' rate of the eight intra candidates (I16MB / I4MB x the chroma
@@ -871,7 +894,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
     constexpr int NI = T8 ? 12 : 8;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    for (int k = lane; k < NI * (JMR_NCTX / 4); k += 64) {
+    for (int k = lane; k < NI * (JMR_NCTX / 4) && !CAV; k += 64) {
         const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
         reinterpret_cast<uint32_t *>(s.stc[m])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
     }
@@ -896,13 +919,18 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
         r.cdc = C.dc;
         r.cac = C.ac;
         r.mvw = R.mvw;
-        jmr_eng en = {s.stc[lane], rg0, 0};
-        jmr_mb(&en, A, B, &r, d.slice_type == JMH_P_SLICE, T8, &R.out);
-        R.bits = en.bits;
-        R.range = en.range;
+        if (CAV) {                                  // rg0: the mb_skip_run before this macroblock
+            R.bits = jmv_mb(A, B, &r, d.slice_type == JMH_P_SLICE, T8, (int)rg0, reinterpret_cast<uint8_t *>(R.mvw), &R.out);
+            R.range = 0;
+        } else {
+            jmr_eng en = {s.stc[lane], rg0, 0};
+            jmr_mb(&en, A, B, &r, d.slice_type == JMH_P_SLICE, T8, &R.out);
+            R.bits = en.bits;
+            R.range = en.range;
+        }
     }
     wave_lds_sync();
-    for (int k = lane; k < NI * (JMR_NCTX / 4); k += 64) {
+    for (int k = lane; k < NI * (JMR_NCTX / 4) && !CAV; k += 64) {
         const int m = k / (JMR_NCTX / 4), j = k - m * (JMR_NCTX / 4);
         reinterpret_cast<uint32_t *>(scr->R[m].ctx)[j] = reinterpret_cast<const uint32_t *>(s.stc[m])[j];
     }
@@ -929,7 +957,8 @@ __global__ __launch_bounds__(NTE) void k_rdo_inter(const TickArgs t) {
         t.bprof[3 * blockIdx.x + 2] = 4;
     }
 }
-template <class pel, bool T8>
+// CAV: SymbolMode 0 (the CAVLC rates; the CABAC build keeps its registers)
+template <class pel, bool T8, bool CAV>
 __global__ __launch_bounds__(NTE) void k_rdo_intra(const TickArgs t) {
     __shared__ RdoIntraS<pel, T8> s;
     const int tot = t.pre[t.npic], m = xcd_block(blockIdx.x, tot);
@@ -939,7 +968,7 @@ __global__ __launch_bounds__(NTE) void k_rdo_intra(const TickArgs t) {
     const DevParams d = tick_params(t, e);
     int mbx, mby;
     tick_mb(t, d, e, m, mbx, mby);
-    rdo_intra_mb<pel, T8>(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
+    rdo_intra_mb<pel, T8, CAV>(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
     if (t.bprof && threadIdx.x == 0) {
         unsigned long long *bp = t.bprof + 3 * xcd_grid(t.pre[t.nP]);
         bp[3 * blockIdx.x] = bt0;
@@ -984,8 +1013,9 @@ struct RdoFinS {
     DbkS<pel> db;
 };
 
-// T8: Transform8x8Mode (the 8x8-transform and I8MB candidates; jmr_mb's 8x8 residual path)
-template <class pel, bool T8>
+// T8: Transform8x8Mode (the 8x8-transform and I8MB candidates; jmr_mb's 8x8 residual path); CAV:
+// SymbolMode 0 (jmv_mb rates, the slice's mb_skip_run)
+template <class pel, bool T8, bool CAV>
 __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     __shared__ RdoFinS<pel> s;
     const int tid = threadIdx.x, tot = t.pre[t.npic];
@@ -1042,7 +1072,7 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     const jmr_mbinfo *A = s.hasA ? &s.nbA : nullptr, *B = s.hasB ? &s.nbB : nullptr;
     // ---- one lane per candidate: its rate on its own copy of the coding state (lanes 0..3 of the
     //      four waves, grouped by macroblock type: kof)
-    for (int i = tid; i < s.ncand * (JMR_NCTX / 4); i += NT) {   // the inter candidates' state copies
+    for (int i = tid; i < s.ncand * (JMR_NCTX / 4) && !CAV; i += NT) {   // the inter candidates' state copies
         const int k = i / (JMR_NCTX / 4), j = i - k * (JMR_NCTX / 4), ci = s.ci[k];
         if (ci < 5 || ci >= 8) reinterpret_cast<uint32_t *>(s.stc[k])[j] = reinterpret_cast<const uint32_t *>(s.st0)[j];
     }
@@ -1081,8 +1111,10 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         const RdoLuma<pel> &L = scr->L[i];
         const RdoChroma<pel> &C = scr->C[b];
         jmr_eng en = {s.stc[kc], s.rg0, 0};
-        if (i == 0) jmr_skip(&en, A, B, &s.out[kc]);
-        else {
+        if (i == 0) {
+            if (CAV) s.out[kc] = jmr_mbinfo{};     // P_Skip: rate 0, its run is written with the next coded MB
+            else jmr_skip(&en, A, B, &s.out[kc]);
+        } else {
             jmr_cand r;
             r.mb_type = b == 4 ? JMH_P8x8 : b;
             r.cbp = L.cbp | C.cbpc << 4;
@@ -1099,7 +1131,8 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
             r.cdc = FC.dc;
             r.cac = FC.ac;
             r.mvw = s.mvw[kc];
-            jmr_mb(&en, A, B, &r, slice_p, T8, &s.out[kc]);
+            if (CAV) en.bits = jmv_mb(A, B, &r, slice_p, T8, (int)s.rg0, reinterpret_cast<uint8_t *>(s.mvw[kc]), &s.out[kc]);
+            else jmr_mb(&en, A, B, &r, slice_p, T8, &s.out[kc]);
         }
         s.bits[kc] = en.bits;
         s.rgo[kc] = en.range;
@@ -1172,11 +1205,12 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         const int slice = a / d.slice_mbs;
         uint32_t *dst = reinterpret_cast<uint32_t *>(d.rp->cab + (size_t)slice * JMR_NCTX);
         const uint8_t *win_ctx = is_intra ? scr->R[4 * (bi - 5) + bcm].ctx : s.stc[w];
-        if (tid < JMR_NCTX / 4) dst[tid] = reinterpret_cast<const uint32_t *>(win_ctx)[tid];
+        if (tid < JMR_NCTX / 4 && !CAV) dst[tid] = reinterpret_cast<const uint32_t *>(win_ctx)[tid];
         const int nw = (int)sizeof(jmr_mbinfo) / 4;
         if (tid >= 128 && tid < 128 + nw)
             reinterpret_cast<uint32_t *>(d.rp->mbi + a)[tid - 128] = reinterpret_cast<const uint32_t *>(&s.out[w])[tid - 128];
-        if (tid == 192) {
+        if (tid == 192 && CAV) d.rp->range[slice] = bi == 0 ? s.rg0 + 1 : 0;   // mb_skip_run
+        else if (tid == 192) {
             jmr_eng en = {nullptr, s.rgo[w], 0};
             if ((a + 1) % d.slice_mbs != 0 && a + 1 < d.mbw * d.mbh) jmr_end_of_mb(&en);
             d.rp->range[slice] = en.range;
@@ -1195,6 +1229,19 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
     }
 }
 
+// the instantiation of k_rdo_intra / k_rdo_final for the sample type, Transform8x8Mode and SymbolMode
+typedef void (*RdoKern)(const TickArgs);
+template <bool W, bool T8>
+static RdoKern rdo_pick(bool fin, bool cav) {
+    typedef typename std::conditional<W, uint16_t, uint8_t>::type pel;
+    if (fin) return cav ? k_rdo_final<pel, T8, true> : k_rdo_final<pel, T8, false>;
+    return cav ? k_rdo_intra<pel, T8, true> : k_rdo_intra<pel, T8, false>;
+}
+static RdoKern rdo_pick(bool wide, bool t8, bool fin, bool cav) {
+    return wide ? (t8 ? rdo_pick<true, true>(fin, cav) : rdo_pick<true, false>(fin, cav))
+                : (t8 ? rdo_pick<false, true>(fin, cav) : rdo_pick<false, false>(fin, cav));
+}
+
 // one tick: k_rdo_inter and k_rdo_intra (on the side stream when given: fork / join events), then
 // k_rdo_final
 hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st, hipStream_t side, hipEvent_t fork, hipEvent_t join) {
@@ -1206,21 +1253,20 @@ hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st, hipStream_t side, h
     if (side && nP) {
         if ((err = hipEventRecord(fork, st)) != hipSuccess || (err = hipStreamWaitEvent(side, fork, 0)) != hipSuccess) return err;
     } else ist = st;
-    // Transform8x8Mode: the instantiations with the 8x8-transform candidates (the others keep their
-    // registers and LDS)
+    // Transform8x8Mode / SymbolMode 0: the instantiations with the 8x8-transform candidates / the
+    // CAVLC rates (the others keep their registers and LDS)
     typedef void (*Kern)(const TickArgs);
     const Kern kin = t.bd > 8 ? (t.t8 ? k_rdo_inter<uint16_t, true> : k_rdo_inter<uint16_t, false>)
                               : (t.t8 ? k_rdo_inter<uint8_t, true> : k_rdo_inter<uint8_t, false>);
-    const Kern kia = t.bd > 8 ? (t.t8 ? k_rdo_intra<uint16_t, true> : k_rdo_intra<uint16_t, false>)
-                              : (t.t8 ? k_rdo_intra<uint8_t, true> : k_rdo_intra<uint8_t, false>);
+    const bool cav = t.rdo == 2;
+    const Kern kia = rdo_pick(t.bd > 8, t.t8 != 0, false, cav);
     if (nP) hipLaunchKernelGGL(kin, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
     hipLaunchKernelGGL(kia, dim3(xcd_grid(tot)), dim3(NTE), 0, ist, t);
     if ((err = hipGetLastError()) != hipSuccess) return err;
     if (ist != st) {
         if ((err = hipEventRecord(join, ist)) != hipSuccess || (err = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return err;
     }
-    const Kern kfi = t.bd > 8 ? (t.t8 ? k_rdo_final<uint16_t, true> : k_rdo_final<uint16_t, false>)
-                              : (t.t8 ? k_rdo_final<uint8_t, true> : k_rdo_final<uint8_t, false>);
+    const Kern kfi = rdo_pick(t.bd > 8, t.t8 != 0, true, cav);
     hipLaunchKernelGGL(kfi, dim3(xcd_grid(tot)), dim3(NT), 0, st, t);
     return hipGetLastError();
 }

@@ -174,6 +174,10 @@ struct jmh_ctx {
     int32_t *d_sched, *d_soff;
     void *d_rscr;
     int nslice;
+    // macroblocks per tick at most (0: every ready diagonal).  RD ticks: one dispatch round of
+    // k_rdo_inter (its LDS fits five MBs per CU), so that a tick is never one full round plus a
+    // partial one; the pictures beyond the cap wait for the next tick (oldest pictures first)
+    int tick_cap;
 };
 
 #define HCHK(x)                                                                  \
@@ -370,7 +374,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     // High 10 pictures: the EPZS wavefront (k_mb_epzs / k_mb_intra / k_mb_final on 16-bit samples)
     if (cfg->bit_depth > 8 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;
     // RDOptimization 1: the CABAC rate, EPZS searches, either transform mode (k_rdo_inter / k_rdo_intra / k_rdo_final)
-    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode != 1 || cfg->search_mode != 3))
+    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode < 0 || cfg->symbol_mode > 1 || cfg->search_mode != 3))
         return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
@@ -401,6 +405,13 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     c->next_id = 0; c->next_entry = 0; c->last_id = -1; c->last_entry = -1;
     c->ref_kind = REF_NONE; c->ref_entry = -1; c->cur_entry = -1;
     c->prof_mb = -1;
+    c->tick_cap = 0;
+    if (cfg->rdo) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess || cus <= 0) cus = 256;
+        c->tick_cap = 5 * cus;
+    }
+    if (const char *e = getenv("JMH_TICK_CAP")) c->tick_cap = atoi(e);   // A/B (0: no cap)
     int st = JMH_OK;
 #define ALLOC(p, n) do { if (hipMalloc((void **)&(p), (n)) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
     {
@@ -586,17 +597,20 @@ static int issue_tick(jmh_ctx *c) {
     t.slice_mbs = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : c->mbw * c->mbh;
     t.bd = c->bd;
     t.ordtab = c->d_ordtab;
-    t.rdo = c->cfg.rdo;
+    t.rdo = c->cfg.rdo ? (c->cfg.symbol_mode ? 1 : 2) : 0;   // 2: CAVLC rates
     t.sched = c->d_sched; t.soff = c->d_soff; t.rscr = c->d_rscr;
     int act[PMAX], nact = 0, nP = 0;
     const int nf = (int)c->fl.size();
     std::vector<int> before(nf);
     for (int i = 0; i < nf; i++) before[i] = c->fl[i].stage = skip_empty(c, c->fl[i].stage);
+    int capped = 0;
     for (int i = 0; i < nf && nact < PMAX; i++) {
         const Flight &f = c->fl[i];
         if (f.stage >= c->nd) continue;
         if (f.pred_id >= 0 && i > 0 && c->fl[i - 1].id == f.pred_id &&
             before[i - 1] < c->nd && before[i - 1] - f.stage < c->lag) continue;
+        if (c->tick_cap > 0 && nact > 0 && capped + c->dcount[f.stage] > c->tick_cap) break;   // younger pictures wait
+        capped += c->dcount[f.stage];
         act[nact++] = i;
         nP += f.pp.slice_type == JMH_P_SLICE;
     }

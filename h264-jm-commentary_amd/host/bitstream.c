@@ -196,13 +196,13 @@ static int write_residual_block(jm_bits *b, const int16_t *coeffs, int n, int nC
         int v = lev[i];
         int code = v > 0 ? 2 * v - 2 : -2 * v - 1;
         if (i == t1 && t1 < 3) code -= 2;
-        if (sl == 0) {
-            if (code < 14) jm_put(b, 1, code + 1);
-            else if (code < 30) { jm_put(b, 1, 15); jm_put(b, code - 14, 4); }
-            else { jm_put(b, 1, 16); jm_put(b, code - 30, 12); }
-        } else {
-            if (code < (15 << sl)) { jm_put(b, 1, (code >> sl) + 1); jm_put(b, code & ((1 << sl) - 1), sl); }
-            else { jm_put(b, 1, 16); jm_put(b, code - (15 << sl), 12); }
+        if (sl == 0 && code < 14) jm_put(b, 1, code + 1);
+        else if (sl == 0 && code < 30) { jm_put(b, 1, 15); jm_put(b, code - 14, 4); }
+        else if (sl > 0 && code < (15 << sl)) { jm_put(b, 1, (code >> sl) + 1); jm_put(b, code & ((1 << sl) - 1), sl); }
+        else {   /* level_prefix >= 15 (9.2.2.1): prefix 15 takes 12 suffix bits, each further one 1 more */
+            int rest = code - (sl == 0 ? 30 : 15 << sl), prefix = 15;
+            while (rest >= (1 << (prefix - 3))) { rest -= 1 << (prefix - 3); prefix++; }
+            jm_put(b, 0, prefix); jm_put(b, 1, 1); jm_put(b, (uint32_t)rest, prefix - 3);
         }
         if (sl == 0) sl = 1;
         int a = v < 0 ? -v : v;
@@ -489,10 +489,16 @@ void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
         w->written[a] = w->stamp;
         memset(w->tc + (size_t)a * 24, 0, 24);
         sw->skip_run++;
+        if (s->rdo) { sw->rate_checked++; sw->rate_bad += r->min_cost != 0; }   /* nothing written yet */
         return;
     }
+    const long bit0 = 8 * sw->b->len + sw->b->nacc;
     if (sw->slice_p) { jm_put_ue(sw->b, sw->skip_run); sw->skip_run = 0; }
     write_mb(sw->b, w, mx, my, r, sw->slice_p);
+    if (s->rdo) {   /* the backend's CAVLC RD rate of the chosen candidate == the bits written for it */
+        sw->rate_checked++;
+        sw->rate_bad += 8 * sw->b->len + sw->b->nacc - bit0 != r->min_cost;
+    }
 }
 
 void jm_slice_rate_check(const jm_slice_writer *sw, long *checked, long *bad) {

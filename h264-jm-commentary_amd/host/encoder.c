@@ -499,7 +499,7 @@ cleanup:
     st->rate_checked = im.rate_checked;
     st->rate_mismatches = im.rate_mismatches;
     if (log && inp->rdopt)
-        fprintf(log, " RD rate check: %ld macroblocks, %ld whose RD rate differs from the CABAC bits written\n",
+        fprintf(log, " RD rate check: %ld macroblocks, %ld whose RD rate differs from the bits written (CABAC or CAVLC)\n",
                 im.rate_checked, im.rate_mismatches);
     if (!st_ret && im.rate_mismatches) st_ret = JMH_E_STATE;
     jm86_free(&im);

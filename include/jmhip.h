@@ -117,10 +117,11 @@ typedef struct jmh_config {
     int32_t rdo;                    /* RDOptimization: 0 off (the cost-based decision of rdopt.c's RDO-off
                                        branch), 1 on: encode_one_macroblock's rate-distortion loop
                                        (RDCost_for_macroblocks / RDCost_for_8x8blocks / RDCost_for_4x4
-                                       IntraBlocks [J]: SSD + lambda_rd * rate, the rate from the CABAC
-                                       coding state of the slice, csrc/jmh_cabac_rate.h); needs
-                                       symbol_mode 1, SearchMode 3 and transform_8x8_mode 0
-                                       (docs/JM_SEMANTICS.md items 53-60)                             */
+                                       IntraBlocks / RDCost_for_8x8IntraBlocks [J]: SSD + lambda_rd *
+                                       rate, the rate from the CABAC coding state of the slice,
+                                       csrc/jmh_cabac_rate.h, or with symbol_mode 0 the CAVLC bit count,
+                                       csrc/jmh_cavlc_rate.h); needs SearchMode 3
+                                       (docs/JM_SEMANTICS.md items 53-60, 63, 64)                     */
     int32_t symbol_mode;            /* SymbolMode: 0 CAVLC, 1 CABAC (the RD rate's entropy coder)     */
     /* JM >= 10 EPZS options (SearchMode 3; docs/JM_SEMANTICS.md items 61, 62); zero keeps items 36, 39 */
     int32_t epzs_subpel_me;         /* EPZSSubPelME: 0 SubPelBlockMotionSearch, 1 the EPZS sub-pel

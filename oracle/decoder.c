@@ -30,8 +30,9 @@ static uint32_t rue(br_t *b) {
 }
 static int32_t rse(br_t *b) { uint32_t k = rue(b); return (k & 1) ? (int32_t)((k + 1) / 2) : -(int32_t)(k / 2); }
 
-/* ---- CAVLC tables (same normative tables, decoded by prefix match) -------------------- */
-static const uint8_t ct_len[3][4][17] = {
+/* ---- CAVLC tables (same normative tables, decoded by prefix match).  The code lengths and the
+   coded_block_pattern mapping are shared with the oracle's RD-rate counter (cavlc_bits.c) ---- */
+const uint8_t jmo_ct_len[3][4][17] = {
     {{1, 6, 8, 9, 10, 11, 13, 13, 13, 14, 14, 15, 15, 16, 16, 16, 16}, {0, 2, 6, 8, 9, 10, 11, 13, 13, 14, 14, 15, 15, 15, 16, 16, 16},
      {0, 0, 3, 7, 8, 9, 10, 11, 13, 13, 14, 14, 15, 15, 16, 16, 16}, {0, 0, 0, 5, 6, 7, 8, 9, 10, 11, 13, 14, 14, 15, 15, 16, 16}},
     {{2, 6, 6, 7, 8, 8, 9, 11, 11, 12, 12, 12, 13, 13, 13, 14, 14}, {0, 2, 5, 6, 6, 7, 8, 9, 11, 11, 12, 12, 13, 13, 14, 14, 14},
@@ -45,9 +46,9 @@ static const uint8_t ct_code[3][4][17] = {
      {0, 0, 3, 9, 5, 5, 5, 5, 13, 9, 13, 9, 13, 9, 6, 10, 5}, {0, 0, 0, 5, 4, 6, 8, 4, 4, 4, 12, 8, 12, 12, 8, 1, 4}},
     {{15, 15, 11, 8, 15, 11, 9, 8, 15, 11, 15, 11, 8, 13, 9, 5, 1}, {0, 14, 15, 12, 10, 8, 14, 10, 14, 14, 10, 14, 10, 7, 12, 8, 4},
      {0, 0, 13, 14, 11, 9, 13, 9, 13, 10, 13, 9, 13, 9, 11, 7, 3}, {0, 0, 0, 12, 11, 10, 9, 8, 13, 12, 12, 12, 8, 12, 10, 6, 2}}};
-static const uint8_t ctdc_len[4][5] = {{2, 6, 6, 6, 6}, {0, 1, 6, 7, 8}, {0, 0, 3, 7, 8}, {0, 0, 0, 6, 7}};
+const uint8_t jmo_ctdc_len[4][5] = {{2, 6, 6, 6, 6}, {0, 1, 6, 7, 8}, {0, 0, 3, 7, 8}, {0, 0, 0, 6, 7}};
 static const uint8_t ctdc_code[4][5] = {{1, 7, 4, 3, 2}, {0, 1, 6, 3, 3}, {0, 0, 1, 2, 2}, {0, 0, 0, 5, 0}};
-static const uint8_t tz_len[15][16] = {
+const uint8_t jmo_tz_len[15][16] = {
     {1, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 9}, {3, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 6, 6, 6, 6}, {4, 3, 3, 3, 4, 4, 3, 3, 4, 5, 5, 6, 5, 6},
     {5, 3, 4, 4, 3, 3, 3, 4, 3, 4, 5, 5, 5}, {4, 4, 4, 3, 3, 3, 3, 3, 4, 5, 4, 5}, {6, 5, 3, 3, 3, 3, 3, 3, 4, 3, 6},
     {6, 5, 3, 3, 3, 2, 3, 4, 3, 6}, {6, 4, 5, 3, 2, 2, 3, 3, 6}, {6, 6, 4, 2, 2, 3, 2, 5}, {5, 5, 3, 2, 2, 2, 4}, {4, 4, 3, 3, 1, 3},
@@ -57,16 +58,16 @@ static const uint8_t tz_code[15][16] = {
     {3, 7, 5, 4, 6, 5, 4, 3, 3, 2, 2, 1, 0}, {5, 4, 3, 7, 6, 5, 4, 3, 2, 1, 1, 0}, {1, 1, 7, 6, 5, 4, 3, 2, 1, 1, 0},
     {1, 1, 5, 4, 3, 3, 2, 1, 1, 0}, {1, 1, 1, 3, 3, 2, 2, 1, 0}, {1, 0, 1, 3, 2, 1, 1, 1}, {1, 0, 1, 3, 2, 1, 1}, {0, 1, 1, 2, 1, 3},
     {0, 1, 1, 1, 1}, {0, 1, 1, 1}, {0, 1, 1}, {0, 1}};
-static const uint8_t tzdc_len[3][4] = {{1, 2, 3, 3}, {1, 2, 2, 0}, {1, 1, 0, 0}};
+const uint8_t jmo_tzdc_len[3][4] = {{1, 2, 3, 3}, {1, 2, 2, 0}, {1, 1, 0, 0}};
 static const uint8_t tzdc_code[3][4] = {{1, 1, 1, 0}, {1, 1, 0, 0}, {1, 0, 0, 0}};
-static const uint8_t rb_len[7][15] = {{1, 1}, {1, 2, 2}, {2, 2, 2, 2}, {2, 2, 2, 3, 3}, {2, 2, 3, 3, 3, 3}, {2, 3, 3, 3, 3, 3, 3},
+const uint8_t jmo_rb_len[7][15] = {{1, 1}, {1, 2, 2}, {2, 2, 2, 2}, {2, 2, 2, 3, 3}, {2, 2, 3, 3, 3, 3}, {2, 3, 3, 3, 3, 3, 3},
                                       {3, 3, 3, 3, 3, 3, 3, 4, 5, 6, 7, 8, 9, 10, 11}};
 static const uint8_t rb_code[7][15] = {{1, 0}, {1, 1, 0}, {3, 2, 1, 0}, {3, 2, 1, 1, 0}, {3, 2, 3, 2, 1, 0}, {3, 0, 1, 3, 2, 5, 4},
                                        {7, 6, 5, 4, 3, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1}};
 /* Table 9-4: codeNum -> coded_block_pattern (ChromaArrayType 1) */
-static const uint8_t cbp_intra[48] = {47, 31, 15, 0, 23, 27, 29, 30, 7, 11, 13, 14, 39, 43, 45, 46, 16, 3, 5, 10, 12, 19, 21, 26,
+const uint8_t jmo_cbp_intra[48] = {47, 31, 15, 0, 23, 27, 29, 30, 7, 11, 13, 14, 39, 43, 45, 46, 16, 3, 5, 10, 12, 19, 21, 26,
                                       28, 35, 37, 42, 44, 1, 2, 4, 8, 17, 18, 20, 24, 6, 9, 22, 25, 32, 33, 34, 36, 40, 38, 41};
-static const uint8_t cbp_inter[48] = {0, 16, 1, 2, 4, 8, 32, 3, 5, 10, 12, 15, 47, 7, 11, 13, 14, 6, 9, 31, 35, 37, 42, 44,
+const uint8_t jmo_cbp_inter[48] = {0, 16, 1, 2, 4, 8, 32, 3, 5, 10, 12, 15, 47, 7, 11, 13, 14, 6, 9, 31, 35, 37, 42, 44,
                                       33, 34, 36, 40, 39, 43, 45, 46, 17, 18, 20, 24, 19, 21, 26, 28, 23, 27, 29, 30, 22, 25, 38, 41};
 
 static int match(br_t *b, int code, int len) {
@@ -81,14 +82,14 @@ static int read_block(br_t *b, int nC, int maxn, int *coef) {
     int tc = -1, t1 = -1;
     if (nC == -1) {
         for (int a = 0; a < 4 && tc < 0; a++)
-            for (int c = a; c < 5; c++) if (match(b, ctdc_code[a][c], ctdc_len[a][c])) { t1 = a; tc = c; break; }
+            for (int c = a; c < 5; c++) if (match(b, ctdc_code[a][c], jmo_ctdc_len[a][c])) { t1 = a; tc = c; break; }
     } else if (nC >= 8) {
         int v = rbits(b, 6);
         if (v == 3) { tc = 0; t1 = 0; } else { tc = (v >> 2) + 1; t1 = v & 3; }
     } else {
         int t = nC < 2 ? 0 : nC < 4 ? 1 : 2;
         for (int a = 0; a < 4 && tc < 0; a++)
-            for (int c = a; c < 17; c++) if (c > 0 || a == 0) if (match(b, ct_code[t][a][c], ct_len[t][a][c])) { t1 = a; tc = c; break; }
+            for (int c = a; c < 17; c++) if (c > 0 || a == 0) if (match(b, ct_code[t][a][c], jmo_ct_len[t][a][c])) { t1 = a; tc = c; break; }
     }
     if (tc < 0 || tc > maxn || t1 > tc) return -1;
     if (!tc) return 0;
@@ -97,10 +98,11 @@ static int read_block(br_t *b, int nC, int maxn, int *coef) {
     for (int i = 0; i < tc; i++) {
         if (i < t1) { lev[i] = rb(b) ? -1 : 1; continue; }
         int prefix = 0;
-        while (!rb(b)) { if (++prefix > 15 || b->err) return -1; }
+        while (!rb(b)) { if (++prefix > 28 || b->err) return -1; }
         int size = (prefix == 14 && sl == 0) ? 4 : (prefix >= 15 ? prefix - 3 : sl);
         int code = (imin(15, prefix) << sl) + (size ? (int)rbits(b, size) : 0);
         if (prefix >= 15 && sl == 0) code += 15;
+        if (prefix >= 16) code += (1 << (prefix - 3)) - 4096;   /* 9.2.2.1 */
         if (i == t1 && t1 < 3) code += 2;
         lev[i] = (code & 1) ? (-code - 1) >> 1 : (code + 2) >> 1;
         if (sl == 0) sl = 1;
@@ -109,8 +111,8 @@ static int read_block(br_t *b, int nC, int maxn, int *coef) {
     int tz = 0;
     if (tc < maxn) {
         tz = -1;
-        if (nC == -1) { for (int z = 0; z <= 4 - tc; z++) if (match(b, tzdc_code[tc - 1][z], tzdc_len[tc - 1][z])) { tz = z; break; } }
-        else { for (int z = 0; z <= 16 - tc; z++) if (match(b, tz_code[tc - 1][z], tz_len[tc - 1][z])) { tz = z; break; } }
+        if (nC == -1) { for (int z = 0; z <= 4 - tc; z++) if (match(b, tzdc_code[tc - 1][z], jmo_tzdc_len[tc - 1][z])) { tz = z; break; } }
+        else { for (int z = 0; z <= 16 - tc; z++) if (match(b, tz_code[tc - 1][z], jmo_tz_len[tc - 1][z])) { tz = z; break; } }
         if (tz < 0) return -1;
     }
     int zl = tz, run[16];
@@ -118,7 +120,7 @@ static int read_block(br_t *b, int nC, int maxn, int *coef) {
         run[i] = 0;
         if (zl > 0) {
             int t = zl > 6 ? 6 : zl - 1, got = -1;
-            for (int r = 0; r <= imin(zl, 14); r++) if (match(b, rb_code[t][r], rb_len[t][r])) { got = r; break; }
+            for (int r = 0; r <= imin(zl, 14); r++) if (match(b, rb_code[t][r], jmo_rb_len[t][r])) { got = r; break; }
             if (got < 0) return -1;
             run[i] = got;
         }
@@ -724,7 +726,7 @@ static int parse_cavlc(jmo_dec *d, br_t *b, int mx, int my, int slice_p, int t, 
     if (intra_type != 1) {
         int code = rue(b);
         if (code > 47) FAIL("bad cbp code");
-        cbp = intra_type == 0 ? cbp_intra[code] : cbp_inter[code];
+        cbp = intra_type == 0 ? jmo_cbp_intra[code] : jmo_cbp_inter[code];
         if (intra_type < 0 && (cbp & 15) && d->t8mode && no_sub8x8) mi->t8 = rb(b);
     }
     s->cbp = cbp;

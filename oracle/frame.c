@@ -24,7 +24,7 @@ static int cfg_ok(const jmh_config *cfg) {
         cfg->epzs_max_thres_scale < 0 || cfg->epzs_max_thres_scale > JMH_EPZS_SCALE_MAX) return JMH_E_INVALID_ARG;
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     /* RDOptimization 1: CABAC rate, 4x4 transform (docs/JM_SEMANTICS.md items 53-60) */
-    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode != 1)) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->rdo != 0 && cfg->rdo != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;
     return JMH_OK;
@@ -61,8 +61,9 @@ int jmo_create(const jmh_config *cfg, jmo_ctx **out) {
     c->blocksad = malloc(sizeof(uint16_t) * 16 * (size_t)c->npos);
     c->cabi = calloc((size_t)c->mbw * c->mbh, sizeof(jmo_cabmbi));
     c->cab_mvd = calloc((size_t)(c->W / 4) * (c->H / 4) * 2, sizeof(int16_t));
+    c->cav_tc = calloc((size_t)c->mbw * c->mbh, 24);
     c->epzs_fp = calloc(8 * n4, sizeof(uint16_t));
-    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref || !c->cabi || !c->cab_mvd || !c->epzs_fp) { jmo_destroy(c); return JMH_E_OOM; }
+    if (!c->orgY || !c->qpel || !c->res || !c->blocksad || !c->tmv || !c->tref || !c->cabi || !c->cab_mvd || !c->cav_tc || !c->epzs_fp) { jmo_destroy(c); return JMH_E_OOM; }
     memset(c->refidx, -1, n4);                             /* no previous picture: no motion */
     *out = c;
     return JMH_OK;
@@ -75,7 +76,7 @@ void jmo_destroy(jmo_ctx *c) {
     free(c->refY); free(c->refU); free(c->refV);
     free(c->recY); free(c->recU); free(c->recV);
     free(c->qpel); free(c->mv); free(c->refidx); free(c->ipred); free(c->mbintra);
-    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref); free(c->cabi); free(c->cab_mvd); free(c->epzs_fp);
+    free(c->res); free(c->blocksad); free(c->tmv); free(c->tref); free(c->cabi); free(c->cab_mvd); free(c->cav_tc); free(c->epzs_fp);
     free(c);
 }
 

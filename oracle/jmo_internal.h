@@ -88,7 +88,21 @@ void jmo_cab_b8(jmo_cab *e, const jmo_cabnb *nb, jmo_cabcur *cur, int b8, int sm
 void jmo_cab_i4(jmo_cab *e, const jmo_cabnb *nb, int x4, int y4, int code, const int16_t *lev);
 void jmo_cab_i8(jmo_cab *e, int code, const int16_t *lev64);
 
-/* Test hook (tests/csrc/rate_xcheck.c): every RD rate the oracle computes, with the coder state,
+/* ---- the oracle's CAVLC bit count for RD rates (cavlc_bits.c; the tables are decoder.c's) --- */
+extern const uint8_t jmo_ct_len[3][4][17], jmo_ctdc_len[4][5], jmo_tz_len[15][16], jmo_tzdc_len[3][4], jmo_rb_len[7][15];
+extern const uint8_t jmo_cbp_intra[48], jmo_cbp_inter[48];   /* Table 9-4: codeNum -> cbp       */
+typedef struct jmo_cavnb {                   /* TotalCoeff of the neighbours A, B (NULL: not available):
+                                                16 luma (4x4 raster), 4 Cb, 4 Cr (2x2 raster)     */
+    const uint8_t *A, *B;
+} jmo_cavnb;
+int jmo_cavlc_block_bits(const int16_t *coef, int n, int nC, int *total_coeff);
+int jmo_cavlc_mb_bits(const jmo_cavnb *nb, const jmo_cabsyn *m, int slice_p, int t8mode, int skip_run, uint8_t tc_out[24]);
+int jmo_cavlc_b8_bits(const jmo_cavnb *nb, uint8_t cur_tc[24], int b8, int sm, const int16_t (*mvd4)[2], int coded,
+                      const int16_t (*lev4)[16]);
+int jmo_cavlc_i4_bits(const jmo_cavnb *nb, uint8_t cur_tc[24], int x4, int y4, int code, const int16_t *lev);
+int jmo_cavlc_i8_bits(const jmo_cavnb *nb, uint8_t cur_tc[24], int b8, int code, const int16_t *lev64);
+
+/* Test hook (tests/harness/rate_xcheck.c): every RD rate the oracle computes, with the coder state,
  * neighbours and syntax it was computed from and the state after; NULL in normal use */
 enum { JMO_RATE_SKIP, JMO_RATE_MB, JMO_RATE_B8, JMO_RATE_I4, JMO_RATE_I8 };
 typedef struct jmo_rate_event {
@@ -103,6 +117,11 @@ typedef struct jmo_rate_event {
     int x4, y4, code;                        /* JMO_RATE_I4 (JMO_RATE_I8: code, lev[64])          */
     const int16_t *lev;
     long bits;                               /* the oracle's rate                                 */
+    /* SymbolMode 0 (CAVLC): no coder state; the neighbours' TotalCoeff, the current MB's so far (B8,
+       I4, I8) and the slice's pending mb_skip_run (MB) */
+    int cavlc, skip_run, b8i;                /* b8i: JMO_RATE_I8's 8x8 block                       */
+    const jmo_cavnb *cnb;
+    const uint8_t *tc_before;
 } jmo_rate_event;
 extern void (*jmo_rate_hook)(const jmo_rate_event *ev);
 
@@ -146,6 +165,9 @@ struct jmo_ctx {
     jmo_cab cab;
     jmo_cabmbi *cabi;
     int16_t *cab_mvd;                /* [(H/4)*(W/4)][2] */
+    /* ... with SymbolMode 0: the slice's pending mb_skip_run and every MB's 24 TotalCoeff */
+    int cav_run;
+    uint8_t *cav_tc;                 /* [mbw*mbh][24] */
 };
 
 /* SliceMode 1 (SliceArgument MBs per slice, raster order): MB addresses a and n lie in one slice.

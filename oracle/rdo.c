@@ -150,6 +150,16 @@ static long rate_of(jmo_rate_event *ev, const jmo_cab *before, const jmo_cab *af
     if (jmo_rate_hook) jmo_rate_hook(ev);
     return ev->bits;
 }
+/* ... with SymbolMode 0: the CAVLC bit count (cavlc_bits.c), tc_before the current MB's TotalCoeff
+   the candidate was counted from */
+static long rate_cav(jmo_rate_event *ev, const jmo_cavnb *cnb, const uint8_t *tc_before, long bits) {
+    ev->cavlc = 1;
+    ev->cnb = cnb;
+    ev->tc_before = tc_before;
+    ev->bits = bits;
+    if (jmo_rate_hook) jmo_rate_hook(ev);
+    return bits;
+}
 
 void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
     mbs S;
@@ -174,7 +184,11 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
     }
     /* the slice's coding state: initialised at its first macroblock (9.3.1) */
     const int a = s->mb_addr, nmb = c->mbw * c->mbh, k = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : nmb;
-    if (a % k == 0) jmo_cab_start(&c->cab, !s->slice_p, qpy);
+    const int cavlc = c->cfg.symbol_mode == 0;              /* SymbolMode 0: CAVLC rates (item 64) */
+    if (a % k == 0) {
+        if (cavlc) c->cav_run = 0;
+        else jmo_cab_start(&c->cab, !s->slice_p, qpy);
+    }
     jmo_cabnb nb;
     memset(&nb, 0, sizeof(nb));
     nb.A = mbx > 0 && jmo_same_slice(c, a, a - 1) ? &c->cabi[a - 1] : NULL;
@@ -186,6 +200,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
         }
     jmo_cab e;
     jmo_rate_event ev;
+    jmo_cavnb cnb = {nb.A ? c->cav_tc + (size_t)(a - 1) * 24 : NULL, nb.B ? c->cav_tc + (size_t)(a - c->mbw) * 24 : NULL};
 #define RATE_BEGIN(kind_) (e = c->cab, memset(&ev, 0, sizeof(ev)), ev.kind = (kind_), ev.slice_p = s->slice_p, ev.nb = &nb)
 
     const int *isr = c->cfg.inter_search;
@@ -215,6 +230,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
             jmo_cabcur cur, curb;
             memset(&cur, 0, sizeof(cur));
             curb = cur;
+            uint8_t ctc[24] = {0}, ctcb[24] = {0};        /* CAVLC: the decided blocks' TotalCoeff */
             pel pred8[256], rec8[256];
             int cnt_nonz = 0;
             for (int block = 0; block < 4; block++) {
@@ -254,24 +270,34 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                         mvd[b4][0] = (int16_t)(s->all_mv[mode][kk][0] - s->pmv[mode][kk][0]);
                         mvd[b4][1] = (int16_t)(s->all_mv[mode][kk][1] - s->pmv[mode][kk][1]);
                     }
-                    stc = st8;
-                    jmo_cabcur cc = cur;
-                    jmo_cab_b8(&stc, &nb, &cc, block, mode, (const int16_t(*)[2])mvd, cost > 0, (const int16_t(*)[16])lev);
                     jmo_rate_event eb;
                     memset(&eb, 0, sizeof(eb));
                     eb.kind = JMO_RATE_B8; eb.slice_p = 1; eb.nb = &nb; eb.cur_before = &cur;
                     eb.b8 = block; eb.sm = mode; eb.coded = cost > 0;
                     eb.mvd4 = (const int16_t(*)[2])mvd; eb.lev4 = (const int16_t(*)[16])lev;
-                    const long bits = rate_of(&eb, &st8, &stc);
+                    jmo_cabcur cc = cur;
+                    uint8_t tcc[24];
+                    long bits;
+                    if (cavlc) {
+                        memcpy(tcc, ctc, 24);
+                        bits = rate_cav(&eb, &cnb, ctc, jmo_cavlc_b8_bits(&cnb, tcc, block, mode, (const int16_t(*)[2])mvd, cost > 0,
+                                                                        (const int16_t(*)[16])lev));
+                    } else {
+                        stc = st8;
+                        jmo_cab_b8(&stc, &nb, &cc, block, mode, (const int16_t(*)[2])mvd, cost > 0, (const int16_t(*)[16])lev);
+                        bits = rate_of(&eb, &st8, &stc);
+                    }
                     double rd = (double)D + lam * (double)bits;
                     if (rd < best) {
                         best = rd; bm = mode; bcost = cost; bcbp = cbpbit; bblk = blk;
                         memcpy(blev, lev, sizeof(blev)); memcpy(bpred, p8, sizeof(bpred)); memcpy(brec, r8, sizeof(brec));
-                        stb = stc; curb = cc;
+                        if (cavlc) memcpy(ctcb, tcc, 24);
+                        else { stb = stc; curb = cc; }
                     }
                 }
                 /* the block's decision: coding state, SetRefAndMotionVectors, stored coefficients */
-                st8 = stb; cur = curb;
+                if (cavlc) memcpy(ctc, ctcb, 24);
+                else { st8 = stb; cur = curb; }
                 P->b8mode[block] = bm;
                 jmo_write_enc_mv(s, 2 * (block & 1), 2 * (block >> 1), 2, 2, s->all_mv[bm]);
                 for (int b4 = 0; b4 < 4; b4++) {
@@ -353,6 +379,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
         lcand *L = &Lc[6];
         memset(L, 0, sizeof(*L));
         L->mode = JMH_I4MB;
+        uint8_t i4tc[24] = {0};                         /* CAVLC: the decided blocks' TotalCoeff */
         for (int b8 = 0; b8 < 4; b8++)
             for (int b4 = 0; b4 < 4; b4++) {
                 int bx = 8 * (b8 & 1) + 4 * (b4 & 1), by = 8 * (b8 >> 1) + 4 * (b4 >> 1), q = (by >> 2) * 4 + (bx >> 2);
@@ -367,6 +394,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                 int bmode = 2, bnz = 0;
                 int16_t blev[16];
                 pel brec[16];
+                uint8_t btc[24];
                 for (int m = 0; m < 9; m++) {
                     if (!av[m]) continue;
                     int32_t r[16];
@@ -379,10 +407,22 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                     int D = ssd(s->org + by * 16 + bx, 16, rec4, 4, 4, 4);
                     RATE_BEGIN(JMO_RATE_I4);
                     ev.x4 = bx >> 2; ev.y4 = by >> 2; ev.code = m == mpm ? -1 : m < mpm ? m : m - 1; ev.lev = lev;
-                    jmo_cab_i4(&e, &nb, ev.x4, ev.y4, ev.code, lev);
-                    double rd = (double)D + lam * (double)rate_of(&ev, &c->cab, &e);
-                    if (rd < best) { best = rd; bmode = m; bnz = nz; memcpy(blev, lev, sizeof(blev)); memcpy(brec, rec4, sizeof(brec)); }
+                    uint8_t tcc[24];
+                    long bits;
+                    if (cavlc) {
+                        memcpy(tcc, i4tc, 24);
+                        bits = rate_cav(&ev, &cnb, i4tc, jmo_cavlc_i4_bits(&cnb, tcc, ev.x4, ev.y4, ev.code, lev));
+                    } else {
+                        jmo_cab_i4(&e, &nb, ev.x4, ev.y4, ev.code, lev);
+                        bits = rate_of(&ev, &c->cab, &e);
+                    }
+                    double rd = (double)D + lam * (double)bits;
+                    if (rd < best) {
+                        best = rd; bmode = m; bnz = nz; memcpy(blev, lev, sizeof(blev)); memcpy(brec, rec4, sizeof(brec));
+                        if (cavlc) memcpy(btc, tcc, 24);
+                    }
                 }
+                if (cavlc) memcpy(i4tc, btc, 24);
                 c->ipred[((s->pix_y + by) >> 2) * W4 + ((s->pix_x + bx) >> 2)] = (int8_t)bmode;
                 for (int y = 0; y < 4; y++) memcpy(c->recY + (s->pix_y + by + y) * W + s->pix_x + bx, brec + 4 * y, 4 * sizeof(pel));
                 memcpy(L->luma[q], blev, sizeof(blev));
@@ -404,6 +444,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
         L->mode = JMH_I8MB;
         L->t8 = 1;
         int modes[4] = {2, 2, 2, 2};
+        uint8_t i8tc[24] = {0};                         /* CAVLC: the decided blocks' TotalCoeff */
         for (int b8 = 0; b8 < 4; b8++) {
             const int bx = 8 * (b8 & 1), by = 8 * (b8 >> 1);
             int32_t nbs[25];
@@ -415,6 +456,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
             int bmode = 2, bnz = 0;
             int16_t blev[64];
             pel brec[64];
+            uint8_t btc[24];
             for (int m = 0; m < 9; m++) {
                 if (!((ok >> m) & 1)) continue;
                 int32_t r[64];
@@ -428,10 +470,23 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
                 RATE_BEGIN(JMO_RATE_I8);
                 ev.code = m == mpm ? -1 : m < mpm ? m : m - 1;
                 ev.lev = lev;
-                jmo_cab_i8(&e, ev.code, lev);
-                double rd = (double)D + lam * (double)rate_of(&ev, &c->cab, &e);
-                if (rd < best) { best = rd; bmode = m; bnz = nz; memcpy(blev, lev, sizeof(blev)); memcpy(brec, rec8, sizeof(brec)); }
+                ev.b8i = b8;
+                uint8_t tcc[24];
+                long bits;
+                if (cavlc) {
+                    memcpy(tcc, i8tc, 24);
+                    bits = rate_cav(&ev, &cnb, i8tc, jmo_cavlc_i8_bits(&cnb, tcc, b8, ev.code, lev));
+                } else {
+                    jmo_cab_i8(&e, ev.code, lev);
+                    bits = rate_of(&ev, &c->cab, &e);
+                }
+                double rd = (double)D + lam * (double)bits;
+                if (rd < best) {
+                    best = rd; bmode = m; bnz = nz; memcpy(blev, lev, sizeof(blev)); memcpy(brec, rec8, sizeof(brec));
+                    if (cavlc) memcpy(btc, tcc, 24);
+                }
             }
+            if (cavlc) memcpy(i8tc, btc, 24);
             modes[b8] = bmode;
             for (int y = 0; y < 8; y++) memcpy(L->rec + (by + y) * 16 + bx, brec + 8 * y, 8 * sizeof(pel));
             jmo_put_levels8(L->luma, b8, blev);
@@ -468,17 +523,27 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
             if (!have[i] || (cm != 0 && !intra)) continue;
             const ccand *C = intra ? &Ci[cm] : &Cc[CBASE(i)];
             jmo_cabsyn r;
+            long bits;
             if (i == 0) {
                 RATE_BEGIN(JMO_RATE_SKIP);
-                jmo_cab_skip(&e, &nb);
+                if (cavlc) bits = rate_cav(&ev, &cnb, NULL, 0);   /* the run is written with the next coded MB */
+                else {
+                    jmo_cab_skip(&e, &nb);
+                    bits = rate_of(&ev, &c->cab, &e);
+                }
             } else {
                 RATE_BEGIN(JMO_RATE_MB);
                 fill_syn(&r, &Lc[i], C, intra ? cm : 0);
                 ev.syn = &r;
                 ev.t8mode = t8m;
-                jmo_cab_mb(&e, &nb, &r, s->slice_p, t8m, NULL, NULL);
+                if (cavlc) {
+                    ev.skip_run = c->cav_run;
+                    bits = rate_cav(&ev, &cnb, NULL, jmo_cavlc_mb_bits(&cnb, &r, s->slice_p, t8m, c->cav_run, NULL));
+                } else {
+                    jmo_cab_mb(&e, &nb, &r, s->slice_p, t8m, NULL, NULL);
+                    bits = rate_of(&ev, &c->cab, &e);
+                }
             }
-            const long bits = rate_of(&ev, &c->cab, &e);
             double rd = (double)(Lc[i].dist + C->dist) + lam * (double)bits;
             if (rd < min_rd) { min_rd = rd; bi = i; bcm = intra ? cm : 0; brate = (int)bits; }
         }
@@ -529,7 +594,16 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
        (0) unless the slice ends here */
     int16_t mvd[16][2];
     memset(mvd, 0, sizeof(mvd));
-    if (bi == 0) {
+    if (cavlc) {                                          /* CAVLC: the skip run, the TotalCoeff */
+        uint8_t *tco = c->cav_tc + (size_t)a * 24;
+        if (bi == 0) { c->cav_run++; memset(tco, 0, 24); }
+        else {
+            jmo_cabsyn r;
+            fill_syn(&r, L, C, is_intra ? bcm : 0);
+            jmo_cavlc_mb_bits(&cnb, &r, s->slice_p, t8m, c->cav_run, tco);
+            c->cav_run = 0;
+        }
+    } else if (bi == 0) {
         jmo_cab_skip(&c->cab, &nb);
         memset(&c->cabi[a], 0, sizeof(c->cabi[a]));
         c->cabi[a].skip = 1;
@@ -543,6 +617,6 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
         c->cab_mvd[2 * pa] = mvd[q][0];
         c->cab_mvd[2 * pa + 1] = mvd[q][1];
     }
-    if ((a + 1) % k != 0 && a + 1 < nmb) jmo_cab_terminate(&c->cab, 0);
+    if (!cavlc && (a + 1) % k != 0 && a + 1 < nmb) jmo_cab_terminate(&c->cab, 0);
 #undef RATE_BEGIN
 }

@@ -1,5 +1,5 @@
-"""The product's CABAC rate engine against an independent coder, candidate by candidate (row f4,
-parity of the RD decision).
+"""The product's CABAC and CAVLC rate engines against independent counts, candidate by candidate
+(row f4, parity of the RD decision).
 
 csrc/jmh_cabac_rate.h is the text the RD kernels (k_rdo_inter / k_rdo_intra / k_rdo_final) compile:
 it counts renormalisation steps over a dense context space.  The oracle prices RD candidates with its
@@ -19,7 +19,7 @@ import tempfile
 import pytest
 
 from jmpaths import LENCOD_XCHECK, ensure_built
-from test_rdo import BASE, RDO
+from test_rdo import BASE, CAVLC, RDO
 
 XCHECK = RDO + [
     # config 5's slice structure at its real width: 240-MB (one row) slices, High 10 and 8-bit
@@ -41,10 +41,10 @@ XCHECK = RDO + [
 ]
 
 
-def run_xcheck(extra):
+def run_xcheck(extra, base=BASE):
     with tempfile.TemporaryDirectory() as d:
         args = [LENCOD_XCHECK, "-p", f"OutputFile={d}/a.264"]
-        for e in BASE + extra:
+        for e in base + extra:
             args += ["-p", e]
         r = subprocess.run(args, capture_output=True, text=True, timeout=900)
     log = r.stdout + r.stderr
@@ -64,3 +64,12 @@ def test_rate_engine_equals_oracle_coder_on_every_candidate(extra):
         assert skip > 0 and b8 > 0, log[-3000:]
     if "Transform8x8Mode=1" in extra:                      # Intra8x8 candidates
         assert i8 > 0, log[-3000:]
+
+
+@pytest.mark.parametrize("extra", CAVLC, ids=[c[0].split(":")[1] for c in CAVLC])
+def test_cavlc_rate_engine_equals_oracle_count_on_every_candidate(extra):
+    """SymbolMode 0 (item 64): csrc/jmh_cavlc_rate.h against oracle/cavlc_bits.c, every candidate."""
+    ensure_built()
+    rc, (n, skip, mb, b8, i4, i8, bad), log = run_xcheck(extra, ["SymbolMode=0", "RDOptimization=1", "SearchMode=3"])
+    assert rc == 0 and bad == 0, log[-3000:]
+    assert n > 0 and mb > 0 and i4 > 0, log[-3000:]

@@ -75,6 +75,36 @@ def test_rdo_closed_loop_and_rate(extra):
         assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/a.yuv", "rb").read()
 
 
+# SymbolMode 0 (docs/JM_SEMANTICS.md item 64): the RD loop with CAVLC rates -- JM's default encoder.cfg
+# shape (RDOptimization 1, CAVLC), Baseline / Main / High / High 10
+CAVLC = [
+    ["InputFile=synthetic:92", "FramesToBeEncoded=4", "ProfileIDC=66", "SearchRange=16"],
+    ["InputFile=synthetic:93", "FramesToBeEncoded=3", "ProfileIDC=66", "SearchRange=8", "QPFirstFrame=0", "QPRemainingFrame=2"],
+    ["InputFile=synthetic:94", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=8", "QPFirstFrame=51",
+     "QPRemainingFrame=48", "SliceMode=1", "SliceArgument=1"],
+    ["InputFile=synthetic:95", "FramesToBeEncoded=4", "ProfileIDC=100", "Transform8x8Mode=1", "SearchRange=16",
+     "SliceMode=1", "SliceArgument=11", "ChromaQPOffset=4"],
+    ["InputFile=synthetic:96", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=1", "SearchRange=8",
+     "QPFirstFrame=0", "QPRemainingFrame=0", "IntraPeriod=2"],          # large 8x8 levels: level_prefix > 15
+    ["InputFile=synthetic:97", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=10",
+     "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchRange=16", "QPRemainingFrame=20", "JMVersion=10"],
+    ["InputFile=synthetic:98", "FramesToBeEncoded=3", "ProfileIDC=66", "SearchRange=8", "SourceWidth=200",
+     "SourceHeight=120", "InterSearch8x4=0", "InterSearch4x8=0", "UseHadamard=0"],
+]
+
+
+@pytest.mark.parametrize("extra", CAVLC, ids=[c[0].split(":")[1] for c in CAVLC])
+def test_rdo_cavlc_closed_loop_and_rate(extra):
+    ensure_built()
+    with tempfile.TemporaryDirectory() as d:
+        log = encode(d, ["SymbolMode=0", "RDOptimization=1", "SearchMode=3"] + extra)
+        n, bad = rate_check(log)
+        assert n > 0 and bad == 0, log
+        r = subprocess.run([JMDEC, f"{d}/a.264", f"{d}/dec.yuv"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/a.yuv", "rb").read()
+
+
 def test_rdo_changes_the_decisions():
     """RDO on and off decide differently on the same input (and both decode)."""
     ensure_built()
@@ -102,7 +132,6 @@ def test_rdo_rate_distortion_tradeoff():
 
 
 @pytest.mark.parametrize("bad,msg", [
-    (["SymbolMode=0", "ProfileIDC=77"], "needs SymbolMode=1"),
     (["SearchMode=0", "ProfileIDC=77"], "SearchMode=3"),
     (["RDOptimization=2", "ProfileIDC=77"], "RDOptimization=2"),
 ])

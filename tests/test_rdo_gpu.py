@@ -3,7 +3,7 @@ schedule must equal the CPU oracle (oracle/rdo.c) bit for bit -- every macrobloc
 (mode, MVs, levels, the chosen candidate's rate in min_cost) and the reconstruction -- and the
 product lencod with the device RD loop must write the same bitstream as the CPU lencod, with the
 writer's RD rate check at 0 mismatches.  JM parity of the RD choices is unpinned
-(docs/JM_SEMANTICS.md items 53-60, 63)."""
+(docs/JM_SEMANTICS.md items 53-60, 63; SymbolMode 0, the CAVLC rates: item 64)."""
 import tempfile
 
 import numpy as np
@@ -25,9 +25,10 @@ def built():
     jmhip.load()
 
 
-def rdo_pair(w, h, pics, qp, cqp=0, bd=8, **kw):
-    g = jmhip.Encoder(w, h, bit_depth=bd, **RDO, **kw)
-    o = oracle_lib.OracleEncoder(w, h, bit_depth=bd, **RDO, **kw)
+def rdo_pair(w, h, pics, qp, cqp=0, bd=8, symbol_mode=1, **kw):
+    kw = dict(RDO, **kw, symbol_mode=symbol_mode)
+    g = jmhip.Encoder(w, h, bit_depth=bd, **kw)
+    o = oracle_lib.OracleEncoder(w, h, bit_depth=bd, **kw)
     for i, pic in enumerate(pics):
         st = jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE
         gres, grec = g.encode(*pic, st, qp, chroma_qp_offset=cqp)
@@ -105,6 +106,35 @@ def test_rdo_t8_config5_width_3840():
     assert res["transform_8x8"].any()
 
 
+# ---- SymbolMode 0 (docs/JM_SEMANTICS.md item 64): the RD rate is the CAVLC bit count (nC from the
+#      neighbours' and the decided blocks' TotalCoeff, the slice's mb_skip_run before a coded MB)
+@pytest.mark.parametrize("kw,qp,cqp", [
+    (dict(search_range=16), 28, 0),
+    (dict(search_range=8), 0, 0),                                   # long level codes (escapes)
+    (dict(search_range=8, slice_mbs=1), 48, 0),                     # runs reset at every slice
+    (dict(search_range=16, slice_mbs=11), 34, 4),
+    (dict(search_range=8, inter_search=(0, 1, 1, 1, 0, 1, 1), use_hadamard=0), 24, 0),
+    (dict(search_range=16, transform_8x8_mode=1), 30, 0),
+    (dict(search_range=8, transform_8x8_mode=1, jm_version=10), 4, -2),
+])
+def test_rdo_cavlc_configs(kw, qp, cqp):
+    pics = moving_seq(176, 144, 3, seed=30 + qp)
+    rdo_pair(176, 144, pics, qp, cqp, symbol_mode=0, **kw)
+
+
+@pytest.mark.parametrize("bd,t8", [(10, 0), (10, 1), (9, 0)])
+def test_rdo_cavlc_high10(bd, t8):
+    pics = hbd_seq(176, 144, 3, seed=33 + bd, bd=bd)
+    rdo_pair(176, 144, pics, 26, 0, bd=bd, symbol_mode=0, search_range=16, slice_mbs=11, transform_8x8_mode=t8)
+
+
+def test_rdo_cavlc_config5_width_3840():
+    """Config 5's shape with SymbolMode 0: High 10, one MB row per slice, EPZS SR 32, CAVLC rates."""
+    w, h = 3840, 96
+    pics = hbd_seq(w, h, 3, seed=45, bd=10)
+    rdo_pair(w, h, pics, 28, bd=10, symbol_mode=0, search_range=32, slice_mbs=240)
+
+
 @pytest.mark.parametrize("slice_mbs", [40, 0, 100])
 def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
     """Pictures in flight on the RD stage schedule (one-row slices: diagonals, lag 16; one slice
@@ -137,12 +167,18 @@ def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
     ["InputFile=synthetic:75", "FramesToBeEncoded=3", "SourceWidth=352", "SourceHeight=96", "SearchRange=32",
      "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SliceMode=1",
      "SliceArgument=22"],
+    # SymbolMode 0 (item 64)
+    ["InputFile=synthetic:76", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
+     "ProfileIDC=66", "SymbolMode=0"],
+    ["InputFile=synthetic:77", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=96", "SearchRange=32",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SliceMode=1",
+     "SliceArgument=22", "SymbolMode=0", "QPRemainingFrame=40"],
 ])
 def test_rdo_lencod_bitstream_identical(extra):
     """The product lencod (device RD loop, device deblocking, pipelined pictures, writer threads)
     and the CPU lencod write identical bitstreams and reconstructions; both writers check every
-    macroblock's RD rate against the CABAC bits they emit."""
-    args = extra + ["SymbolMode=1", "RDOptimization=1", "SearchMode=3"]
+    macroblock's RD rate against the CABAC / CAVLC bits they emit."""
+    args = (["SymbolMode=1"] if "SymbolMode=0" not in extra else []) + extra + ["RDOptimization=1", "SearchMode=3"]
     with tempfile.TemporaryDirectory() as g, tempfile.TemporaryDirectory() as c:
         lg = run_lencod(LENCOD, g, args)
         lc = run_lencod(LENCOD_CPU, c, args)
@@ -153,6 +189,7 @@ def test_rdo_lencod_bitstream_identical(extra):
 
 
 def test_rdo_rejects_unsupported():
-    for kw in (dict(rdo=1, symbol_mode=0, search_mode=3), dict(rdo=1, symbol_mode=1, search_mode=0)):
+    for kw in (dict(rdo=1, symbol_mode=2, search_mode=3), dict(rdo=1, symbol_mode=1, search_mode=0),
+               dict(rdo=1, symbol_mode=0, search_mode=-1)):
         with pytest.raises(jmhip.JmhError):
             jmhip.Encoder(64, 48, search_range=8, **kw)
