@@ -292,6 +292,9 @@ JMR_FN void jmr_mb(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, const j
     const int mbt = r->mb_type;
     const int is_i8 = mbt == JMH_I8MB, is_nxn = mbt == JMH_I4MB || is_i8, is_i16 = mbt == JMH_I16MB;
     const int intra = is_nxn || is_i16, cbp = r->cbp, cbpl = cbp & 15, cbpc = cbp >> 4;
+    /* the sub-macroblock types packed 4 bits each: the candidate (a private struct on the device) is
+       read at constant offsets only, so it stays in registers */
+    const int b8m = r->b8mode[0] | r->b8mode[1] << 4 | r->b8mode[2] << 8 | r->b8mode[3] << 12;
     jmr_mbinfo m = {0};
     m.kind = (uint8_t)(is_i16 ? JMR_K_I16 : is_nxn ? JMR_K_INXN : JMR_K_INTER);
     m.cbp = (uint8_t)cbp;
@@ -318,7 +321,7 @@ JMR_FN void jmr_mb(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, const j
         jmr_bin(e, JMR_CTX(16) + b1, b2);
     }
     if (mbt == JMH_P8x8)
-        for (int i = 0; i < 4; i++) jmr_sub_mb_type(e, r->b8mode[i]);
+        for (int i = 0; i < 4; i++) jmr_sub_mb_type(e, (b8m >> (4 * i)) & 15);
     if (is_nxn && t8mode) {
         jmr_bin(e, JMR_CTX(399) + (A && A->t8) + (B && B->t8), is_i8);
         m.t8 = (uint8_t)is_i8;
@@ -351,7 +354,7 @@ JMR_FN void jmr_mb(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, const j
                 jmr_put_mvd(mv, x4, y4, w4, h4, dx, dy);
                 continue;
             }
-            const int sm = r->b8mode[p], w4 = (sm == 4 || sm == 5) ? 2 : 1, h4 = (sm == 4 || sm == 6) ? 2 : 1;
+            const int sm = (b8m >> (4 * p)) & 15, w4 = (sm == 4 || sm == 5) ? 2 : 1, h4 = (sm == 4 || sm == 6) ? 2 : 1;
             for (int y = 0; y < 2; y += h4)
                 for (int x = 0; x < 2; x += w4) {
                     const int x4 = (p & 1) * 2 + x, y4 = (p >> 1) * 2 + y;
@@ -368,7 +371,7 @@ JMR_FN void jmr_mb(jmr_eng *e, const jmr_mbinfo *A, const jmr_mbinfo *B, const j
         if (cbpc) jmr_bin(e, JMR_CTX(81) + (ca == 2) + 2 * (cb == 2), cbpc == 2);
     }
     if (!intra && cbpl && t8mode &&
-        (mbt != JMH_P8x8 || (r->b8mode[0] == 4 && r->b8mode[1] == 4 && r->b8mode[2] == 4 && r->b8mode[3] == 4))) {
+        (mbt != JMH_P8x8 || b8m == 0x4444)) {
         jmr_bin(e, JMR_CTX(399) + (A && A->t8) + (B && B->t8), r->t8 != 0);
         m.t8 = (uint8_t)(r->t8 != 0);
     }
