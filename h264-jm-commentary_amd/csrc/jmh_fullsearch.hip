@@ -13,6 +13,14 @@
 // The searches run in JM's order (16x16, 16x8, 8x16, then per 8x8 block the sub-modes 4..7),
 // which is dependency-exact by construction.  The results land in MbScratch exactly like
 // k_mb_analyse's FFS search, so the intra workgroups and k_mb_final are shared.
+//
+// Templated on the sample type and the search: pel = uint16_t is High 10 (two samples per dword,
+// v_sad_u16, Clip1 to (1 << BitDepth) - 1 in the half-pel planes; a 16x16 SAD < 2^18, so the
+// `cost << 13` keys still fit 32 bits), and FFS = true is SearchMode 0 for those pictures
+// (FastFullPelBlockMotionSearch [J]: every search of the MB on the window centred on the 16x16
+// MVP / 4 clamped to +-SR, the (0,0) vector checked first -- order key 0, the spiral positions
+// 1.. -- and no 16x16 zero-vector bias in full pel).  8-bit FFS keeps k_mb_analyse's shared 4x4
+// SAD table; here each search sums its block directly (7x the SAD work, on the 10-bit path only).
 #include "jmh_common.h"
 
 #define NTF 256                               // threads per full-search workgroup
@@ -22,29 +30,33 @@
 #define FKOFF 4096                            // cost offset in keys (16x16 zero-vector bias)
 
 
+template <class pel>
 struct FullS {
-    uint8_t g[FW_MAX * FST + 16];
-    uint8_t org[256];
+    pel g[FW_MAX * FST + 16];
+    pel org[256];
     Border bd;
     int16_t all_mv[8][16][2];
     int motion_cost[8][4];
     unsigned red[2][NTF / 64];
     int ccost[2][9];
     int cost0;
-    uint8_t hp[3][18][20];                     // half-pel b / h / j around the block at its full-pel MV
+    pel hp[3][18][20];                         // half-pel b / h / j around the block at its full-pel MV
+    int scx, scy;                              // FFS: the window centre (16x16 MVP / 4, clamped)
 };
 
 // half-grid sample (hx, hy) relative to the block origin at its full-pel MV (window (gx0, gy0)):
 // even / even = integer sample, odd x = b, odd y = h, both odd = j (8.4.2.2.1)
-__device__ __forceinline__ int hg_at(const FullS &s, int gx0, int gy0, int hx, int hy) {
+template <class pel>
+__device__ __forceinline__ int hg_at(const FullS<pel> &s, int gx0, int gy0, int hx, int hy) {
     if (!((hx | hy) & 1)) return s.g[(gy0 + (hy >> 1)) * FST + gx0 + (hx >> 1)];
     const int pl = (hx & hy & 1) ? 2 : (hx & 1) ? 0 : 1;
     return s.hp[pl][(hy >> 1) + 1][(hx >> 1) + 1];
 }
 
 // neighbour view of a search of block type bt in 8x8 block b8 (as NbMe in jmh_analyse.hip)
+template <class pel>
 struct NbFull {
-    const FullS &s;
+    const FullS<pel> &s;
     int bt, b8, best8x8;
     __device__ __forceinline__ bool operator()(int xN, int yN, int &ref, int &mx, int &my) const {
         if (yN > 15 || (xN > 15 && yN >= 0)) return false;
@@ -61,7 +73,7 @@ struct NbFull {
     }
 };
 
-__device__ __forceinline__ uint32_t lds_u32(const uint8_t *p) {   // 4 bytes at any LDS address
+__device__ __forceinline__ uint32_t lds_u32(const void *p) {   // 4 bytes at any LDS address
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
@@ -69,7 +81,8 @@ __device__ __forceinline__ uint32_t lds_u32(const uint8_t *p) {   // 4 bytes at 
 
 // workgroup minimum of per-thread keys (double-buffered slot: consecutive calls need no second
 // barrier); every thread returns the minimum
-__device__ __forceinline__ unsigned wg_min(FullS &s, unsigned k, int &slot) {
+template <class pel>
+__device__ __forceinline__ unsigned wg_min(FullS<pel> &s, unsigned k, int &slot) {
     k = wave_min_u32(k);
     if ((threadIdx.x & 63) == 0) s.red[slot][threadIdx.x >> 6] = k;
     __syncthreads();
@@ -80,8 +93,10 @@ __device__ __forceinline__ unsigned wg_min(FullS &s, unsigned k, int &slot) {
     return m;
 }
 
-// BlockMotionSearch [J] for one block: full-pel full search + SubPelBlockMotionSearch
-__device__ __forceinline__ void full_block_search(const DevParams &d, FullS &s, int off, int bt, int bx4, int by4, int mc, int b8,
+// BlockMotionSearch [J] for one block: full-pel full search (FFS: on the MB's common window) +
+// SubPelBlockMotionSearch
+template <class pel, bool FFS>
+__device__ __forceinline__ void full_block_search(const DevParams &d, FullS<pel> &s, int off, int bt, int bx4, int by4, int mc, int b8,
                                                            int best8x8, int X0, int Y0, int pslot) {
     const int tid = threadIdx.x;
     const bool prof = pslot >= 0 && pslot < 28 && d.prof && tid == 0 && d.prof_mb == (Y0 >> 2) * d.mbw + (X0 >> 2);
@@ -90,32 +105,46 @@ __device__ __forceinline__ void full_block_search(const DevParams &d, FullS &s, 
     const int range = d.restrict_sr == 0 ? d.sr / min(2, bt) : d.sr;
     const int lw4 = lw4_of(bt), lh4 = lh4_of(bt), w4 = 1 << lw4, h4 = 1 << lh4, lns = lw4 + lh4, nsub = 1 << lns;
     int pmx, pmy;
-    set_mvp(NbFull{s, bt, b8, best8x8}, bx4, by4, 4 * w4, 4 * h4, pmx, pmy);
-    const int mvx0 = iclip(-range, range, pmx / 4), mvy0 = iclip(-range, range, pmy / 4);
+    set_mvp(NbFull<pel>{s, bt, b8, best8x8}, bx4, by4, 4 * w4, 4 * h4, pmx, pmy);
+    if (FFS && bt == 1) {                              // SetupFastFullPelSearch: the MB's window centre
+        if (tid == 0) { s.scx = iclip(-d.sr, d.sr, pmx / 4); s.scy = iclip(-d.sr, d.sr, pmy / 4); }
+        __syncthreads();
+    }
+    const int mvx0 = FFS ? s.scx : iclip(-range, range, pmx / 4), mvy0 = FFS ? s.scy : iclip(-range, range, pmy / 4);
     int fmx, fmy, min_mcost;
     {
-    // ---- full pel: every thread a stride of positions, SADs by dword v_sad_u8
+    // ---- full pel: every thread a stride of positions, SADs by dword v_sad_u8 / v_sad_u16
+    constexpr int PD = 4 / (int)sizeof(pel);           // samples per dword
     const int side = 2 * range + 1, npos = side * side;
-    unsigned kb = 0xFFFFFFFFu;
-    for (int p = tid; p < npos; p += NTF) {
-        const int dy = p / side - range, dx = p - (dy + range) * side - range;
-        const int cx = mvx0 + dx, cy = mvy0 + dy;
+    // the block's SAD + MV cost at MV (cx, cy) (window position = MB origin + block + MV)
+    auto cost_at = [&](int cx, int cy) {
         int cost = lam * (mvbits(4 * cx - pmx) + mvbits(4 * cy - pmy));
-        if (bt == 1 && slice_p && cx == 0 && cy == 0) cost -= 16 * lam;
+        if (!FFS && bt == 1 && slice_p && cx == 0 && cy == 0) cost -= 16 * lam;
         const int wx = off + 4 * bx4 + cx, wy = off + 4 * by4 + cy;
         uint32_t sad = 0;
         for (int r = 0; r < 4 * h4; r++) {
-            const uint8_t *row = s.g + (wy + r) * FST + wx;
+            const pel *row = s.g + (wy + r) * FST + wx;
             const uint32_t *org = reinterpret_cast<const uint32_t *>(s.org + (4 * by4 + r) * 16 + 4 * bx4);
-            for (int q = 0; q < w4; q++) sad = __builtin_amdgcn_sad_u8(lds_u32(row + 4 * q), org[q], sad);
+            for (int q = 0; q < 4 * w4 / PD; q++) {
+                if constexpr (sizeof(pel) == 1) sad = __builtin_amdgcn_sad_u8(lds_u32(row + PD * q), org[q], sad);
+                else sad = __builtin_amdgcn_sad_u16(lds_u32(row + PD * q), org[q], sad);
+            }
         }
-        cost += (int)sad;
-        kb = min(kb, ((unsigned)(cost + FKOFF) << 13) | (unsigned)spiral_index(dx, dy));
+        return cost + (int)sad;
+    };
+    // key = cost << 13 | JM order: full search the spiral index; FFS 0 for its (0,0) pre-check,
+    // spiral index + 1 for the positions
+    unsigned kb = 0xFFFFFFFFu;
+    for (int p = tid; p < npos; p += NTF) {
+        const int dy = p / side - range, dx = p - (dy + range) * side - range;
+        kb = min(kb, ((unsigned)(cost_at(mvx0 + dx, mvy0 + dy) + FKOFF) << 13) | (unsigned)(spiral_index(dx, dy) + FFS));
     }
+    if (FFS && tid == NTF - 1) kb = min(kb, (unsigned)(cost_at(0, 0) + FKOFF) << 13);
     int slot = 0;
     const unsigned best = wg_min(s, kb, slot);
     int rx, ry;
-    spiral_pos((int)(best & 8191u), rx, ry);
+    if (FFS && (best & 8191u) == 0) { rx = -mvx0; ry = -mvy0; }
+    else spiral_pos((int)(best & 8191u) - FFS, rx, ry);
     fmx = mvx0 + rx; fmy = mvy0 + ry;
     min_mcost = had ? BIGCOST : (int)(best >> 13) - FKOFF;
     }
@@ -124,20 +153,21 @@ __device__ __forceinline__ void full_block_search(const DevParams &d, FullS &s, 
     // sample is the average of two half-grid samples; one 16-lane group per (candidate, 4x4)
     const bool check0 = bt == 1 && fmx == 0 && fmy == 0 && had && slice_p;
     auto px = [&](int x, int y) { return (int)s.g[y * FST + x]; };
+    const int maxv = d.maxv;
     const int gx0 = off + 4 * bx4 + fmx, gy0 = off + 4 * by4 + fmy;
     {
         const int PW = 4 * w4 + 2, PH = 4 * h4 + 2;
         for (int i = tid; i < PW * PH; i += NTF) {
             const int y = i / PW, x = i - y * PW, gx = gx0 + x - 1, gy = gy0 + y - 1;
-            s.hp[0][y][x] = (uint8_t)clip255((tap6(px(gx - 2, gy), px(gx - 1, gy), px(gx, gy), px(gx + 1, gy), px(gx + 2, gy), px(gx + 3, gy)) + 16) >> 5);
-            s.hp[1][y][x] = (uint8_t)clip255((tap6(px(gx, gy - 2), px(gx, gy - 1), px(gx, gy), px(gx, gy + 1), px(gx, gy + 2), px(gx, gy + 3)) + 16) >> 5);
+            s.hp[0][y][x] = (pel)iclip(0, maxv, (tap6(px(gx - 2, gy), px(gx - 1, gy), px(gx, gy), px(gx + 1, gy), px(gx + 2, gy), px(gx + 3, gy)) + 16) >> 5);
+            s.hp[1][y][x] = (pel)iclip(0, maxv, (tap6(px(gx, gy - 2), px(gx, gy - 1), px(gx, gy), px(gx, gy + 1), px(gx, gy + 2), px(gx, gy + 3)) + 16) >> 5);
             int v[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) {
                 const int xx = gx - 2 + k;
                 v[k] = tap6(px(xx, gy - 2), px(xx, gy - 1), px(xx, gy), px(xx, gy + 1), px(xx, gy + 2), px(xx, gy + 3));
             }
-            s.hp[2][y][x] = (uint8_t)clip255((tap6(v[0], v[1], v[2], v[3], v[4], v[5]) + 512) >> 10);
+            s.hp[2][y][x] = (pel)iclip(0, maxv, (tap6(v[0], v[1], v[2], v[3], v[4], v[5]) + 512) >> 10);
         }
     }
     const int grp = tid >> 4, l = tid & 15;
@@ -180,8 +210,9 @@ __device__ __forceinline__ void full_block_search(const DevParams &d, FullS &s, 
     if (prof) d.prof[35 + pslot] = wall_clock64();
 }
 
+template <class pel, bool FFS>
 __global__ __launch_bounds__(NTF, 6) void k_mb_me_full(const TickArgs t) {
-    __shared__ FullS s;
+    __shared__ FullS<pel> s;
     const int b = xcd_block(blockIdx.x, t.pre[t.nP]), tid = threadIdx.x;   // XCD-aware (jmh_device.h)
     if (b >= t.pre[t.nP]) return;
     const int e = tick_entry(t, b);
@@ -192,25 +223,29 @@ __global__ __launch_bounds__(NTF, 6) void k_mb_me_full(const TickArgs t) {
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     const int X0 = 4 * mbx, Y0 = 4 * mby;
     if (d.prof && tid == 0 && d.prof_mb == mby * d.mbw + mbx) d.prof[32] = wall_clock64();
-    s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    s.org[tid] = spl<pel>(d.orgY)[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
     if (tid < 10) load_border(d, s.bd, tid, mbx, mby);
     else if (tid >= 32 && tid < 64) s.motion_cost[(tid - 32) >> 2][tid & 3] = 0;
     {   // window: MB pixel (0,0) at (off, off); per-coordinate clamping is the spec's UMV access
-        constexpr int ND4 = FST / 4;
+        constexpr int PD = 4 / (int)sizeof(pel), ND4 = FST / PD, SB = 8 * (int)sizeof(pel);
         const int X0 = pix_x - off, Y0 = pix_y - off;
         for (int task = tid; task < wdim * ND4; task += NTF) {
-            const int y = task / ND4, j = task - y * ND4, x0 = X0 + 4 * j;
-            const uint8_t *row = d.refY + iclip(0, d.H - 1, Y0 + y) * W;
+            const int y = task / ND4, j = task - y * ND4, x0 = X0 + PD * j;
+            const pel *row = spl<pel>(d.refY) + iclip(0, d.H - 1, Y0 + y) * W;
             uint32_t v;
-            if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
-                const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
-                v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
+            if (PD * j + PD - 1 < wdim && x0 >= 0 && x0 + PD - 1 < W) {
+                if constexpr (sizeof(pel) == 1) {
+                    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
+                    v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
+                } else {
+                    v = *reinterpret_cast<const uint32_t *>(row + x0);   // x0 even: pix_x - 2 SR - 4 + 2 j
+                }
             } else {
                 v = 0;
-                for (int q = 0; q < 4; q++)
-                    if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
+                for (int q = 0; q < PD; q++)
+                    if (PD * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (SB * q);
             }
-            *reinterpret_cast<uint32_t *>(s.g + y * FST + 4 * j) = v;
+            *reinterpret_cast<uint32_t *>(s.g + y * FST + PD * j) = v;
         }
     }
     __syncthreads();
@@ -232,7 +267,7 @@ __global__ __launch_bounds__(NTF, 6) void k_mb_me_full(const TickArgs t) {
             const int sx = j == 4 || j == 6 || j == 8 ? 1 : 0, sy = j == 2 || j == 7 || j == 8 ? 1 : 0;
             bx4 = 2 * (b8 & 1) + sx; by4 = 2 * (b8 >> 1) + sy;
         }
-        full_block_search(d, s, off, bt, bx4, by4, mc, b8, i < 5 ? 0 : best8x8, X0, Y0, i < 14 ? 2 * i : -1);
+        full_block_search<pel, FFS>(d, s, off, bt, bx4, by4, mc, b8, i < 5 ? 0 : best8x8, X0, Y0, i < 14 ? 2 * i : -1);
         if (i >= 5 && (i - 5) % 9 == 8) {
             int mc8 = BIGCOST, bm = 0;
             for (int mode = 4; mode <= 7; mode++) {
@@ -265,6 +300,9 @@ __global__ __launch_bounds__(NTF, 6) void k_mb_me_full(const TickArgs t) {
 
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st) {
     if (t.pre[t.nP] == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mb_me_full, dim3(xcd_grid(t.pre[t.nP])), dim3(NTF), 0, st, t);
+    typedef void (*Kern)(const TickArgs);
+    const bool ffs = t.search_mode == 0;   // 8-bit FFS runs in k_mb_analyse
+    const Kern k = t.bd > 8 ? (ffs ? k_mb_me_full<uint16_t, true> : k_mb_me_full<uint16_t, false>) : k_mb_me_full<uint8_t, false>;
+    hipLaunchKernelGGL(k, dim3(xcd_grid(t.pre[t.nP])), dim3(NTF), 0, st, t);
     return hipGetLastError();
 }

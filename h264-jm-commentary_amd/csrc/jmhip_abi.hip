@@ -372,7 +372,6 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->slice_mbs < 0) return JMH_E_INVALID_ARG;
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     // High 10 pictures: the EPZS wavefront (k_mb_epzs / k_mb_intra / k_mb_final on 16-bit samples)
-    if (cfg->bit_depth > 8 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;
     // RDOptimization 1: the CABAC rate, EPZS searches, either transform mode (k_rdo_inter / k_rdo_intra / k_rdo_final)
     if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode < 0 || cfg->symbol_mode > 1 || cfg->search_mode != 3))
         return JMH_E_UNSUPPORTED_CFG;
@@ -589,7 +588,7 @@ static int issue_tick(jmh_ctx *c) {
     t.search_mode = c->cfg.search_mode; t.use_hadamard = c->cfg.use_hadamard; t.restrict_sr = c->cfg.restrict_search_range;
     for (int i = 0; i < 8; i++) t.inter_search[i] = c->cfg.inter_search[i];
     t.prof = c->d_prof; t.prof_mb = c->prof_mb;
-    t.me_in_analyse = c->cfg.search_mode == 0;
+    t.me_in_analyse = c->cfg.search_mode == 0 && c->bd == 8;   // High 10 FFS: k_mb_me_full<uint16_t, true>
     t.t8 = c->cfg.transform_8x8_mode;
     t.epzs_dual = c->cfg.epzs_dual_refinement;
     t.epzs_subpel = c->cfg.epzs_subpel_me; t.epzs_spts = c->cfg.epzs_subpel_thres_scale;
@@ -646,7 +645,7 @@ static int issue_tick(jmh_ctx *c) {
         } else if (t.me_in_analyse) {                   // FFS: motion search + intra in k_mb_analyse
             HCHK(jmh_launch_analyse(t, c->st));
             if (t.t8) HCHK(jmh_launch_intra8(t, c->st));   // Intra8x8 decision (High profile)
-        } else {                                        // EPZS (one wave per MB) / SearchMode -1
+        } else {                                        // EPZS (one wave per MB) / SearchMode -1 / High 10 FFS
             if (t.search_mode == 3) HCHK(jmh_launch_epzs(t, c->st));
             else HCHK(jmh_launch_me_full(t, c->st));
             HCHK(jmh_launch_intra(t, c->st));           // all intra decisions incl. Intra8x8

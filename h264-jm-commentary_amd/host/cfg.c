@@ -191,7 +191,6 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->profile_idc != 66 && inp->profile_idc != 77 && inp->profile_idc != 100 && inp->profile_idc != 110) { snprintf(err, errlen, "ProfileIDC=%d not supported (66, 77, 100 or 110)", inp->profile_idc); return -1; }
     if (inp->bit_depth_luma > 10 || inp->bit_depth_chroma != inp->bit_depth_luma) { snprintf(err, errlen, "SourceBitDepthLuma=%d / SourceBitDepthChroma=%d not supported (equal, 8..10)", inp->bit_depth_luma, inp->bit_depth_chroma); return -1; }
     if (inp->bit_depth_luma > 8 && inp->profile_idc != 110) { snprintf(err, errlen, "SourceBitDepthLuma=%d requires ProfileIDC=110 (High 10)", inp->bit_depth_luma); return -1; }
-    if (inp->bit_depth_luma > 8 && inp->search_mode != 3) { snprintf(err, errlen, "SourceBitDepthLuma > 8 supports SearchMode=3 (EPZS) only"); return -1; }
     if (inp->bit_depth_luma > 8 && inp->jm_call_surface) { snprintf(err, errlen, "JMCallSurface=1 runs the 8-bit per-block seams (SourceBitDepthLuma 8)"); return -1; }
     if (inp->transform_8x8_mode == 2) { snprintf(err, errlen, "Transform8x8Mode=2 not supported (0 or 1)"); return -1; }
     if (inp->transform_8x8_mode && inp->profile_idc < 100) { snprintf(err, errlen, "Transform8x8Mode=1 requires ProfileIDC=100 (High)"); return -1; }

@@ -110,7 +110,7 @@ typedef struct jmh_config {
                                        deblocking still crosses slice edges (idc 0)                 */
     int32_t bit_depth;              /* BitDepthLuma = BitDepthChroma: 0 or 8 (8-bit pictures, the
                                        uint8_t entry points), 9 or 10 (High 10: 16-bit samples through
-                                       the *_u16 picture entry points; SearchMode 3 only; quantisation
+                                       the *_u16 picture entry points; SearchMode 0, -1 or 3; quantisation
                                        at QP + QpBdOffset, Clip1 to (1 << bit_depth) - 1, deblocking
                                        thresholds scaled by 1 << (bit_depth - 8); docs/JM_SEMANTICS.md
                                        items 49-52)                                                  */

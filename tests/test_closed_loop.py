@@ -98,6 +98,11 @@ HIGH10 = [
     ["InputFile=synthetic:66", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10",
      "SearchMode=3", "SearchRange=8", "SymbolMode=1", "QPFirstFrame=4", "QPRemainingFrame=6", "UseHadamard=0",
      "SourceWidth=200", "SourceHeight=120"],
+    # FFS and full search on 16-bit samples
+    ["InputFile=synthetic:67", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10",
+     "SearchMode=0", "SearchRange=16", "Transform8x8Mode=1"],
+    ["InputFile=synthetic:68", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=9", "SourceBitDepthChroma=9",
+     "SearchMode=-1", "SearchRange=8", "RestrictSearchRange=0", "SymbolMode=1", "QPFirstFrame=10", "QPRemainingFrame=12"],
 ]
 
 

@@ -518,9 +518,66 @@ def test_high10_pipelined_chain_equals_sequential():
             assert np.array_equal(x, y)
 
 
-def test_high10_rejects_other_search_modes_and_8bit_calls():
+@pytest.mark.parametrize("sm,bd,kw,qp", [
+    (0, 10, dict(search_range=16), 28),
+    (0, 10, dict(search_range=32, restrict_search_range=0, transform_8x8_mode=1), 20),
+    (0, 9, dict(search_range=8, use_hadamard=0, restrict_search_range=1), 40),
+    (0, 10, dict(search_range=16, slice_mbs=7, inter_search=(1, 0, 1, 1, 0, 1, 1)), 4),
+    (-1, 10, dict(search_range=16), 28),
+    (-1, 10, dict(search_range=8, restrict_search_range=0, transform_8x8_mode=1), 51),
+    (-1, 9, dict(search_range=16, use_hadamard=0, slice_mbs=11), 12),
+])
+def test_high10_ffs_and_full_search(sm, bd, kw, qp):
+    """16-bit samples through k_mb_me_full<uint16_t, FFS> (SearchMode 0: FastFullPelBlockMotionSearch on the
+    MB's common window, SearchMode -1: FullPelBlockMotionSearch) == the oracle on every macroblock
+    (VERDICT r3 item 7)."""
+    w, h = 176, 144
+    pics = hbd_seq(w, h, 4, seed=110 + qp + sm, bd=bd, step=(5, -3))
+    g = jmhip.Encoder(w, h, search_mode=sm, bit_depth=bd, **kw)
+    o = oracle_lib.OracleEncoder(w, h, search_mode=sm, bit_depth=bd, **kw)
+    for i, pic in enumerate(pics):
+        st = jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE
+        gres, grec = g.encode(*pic, st, qp)
+        ores, orec = o.encode(*pic, st, qp)
+        assert_same(gres, grec, ores, orec, w // 16)
+        g.set_reference(*orec)
+        o.set_reference(*orec)
+
+
+@pytest.mark.parametrize("sm", [0, -1])
+def test_high10_ffs_full_width_3840(sm):
+    """10-bit FFS / full search at 3840 wide, SR 32, large motion: GPU == oracle."""
+    w, h = 3840, 64
+    pics = hbd_seq(w, h, 3, seed=47 - sm, bd=10)
+    g = jmhip.Encoder(w, h, search_range=32, search_mode=sm, bit_depth=10)
+    o = oracle_lib.OracleEncoder(w, h, search_range=32, search_mode=sm, bit_depth=10)
+    for i, pic in enumerate(pics):
+        st = jmhip.JMH_I_SLICE if i == 0 else jmhip.JMH_P_SLICE
+        gres, grec = g.encode(*pic, st, 30)
+        ores, orec = o.encode(*pic, st, 30)
+        assert_same(gres, grec, ores, orec, w // 16)
+        g.set_reference(*orec)
+        o.set_reference(*orec)
+
+
+def test_high10_ffs_pipelined_chain_equals_sequential():
+    w, h, n = 640, 320, 5
+    pics = hbd_seq(w, h, n, seed=4, bd=10, step=(-45, 38))
+    kw = dict(search_range=32, search_mode=0, bit_depth=10)
+    a = jmhip.Encoder(w, h, **kw)
+    b = jmhip.Encoder(w, h, pipeline_depth=1, **kw)
+    assert a.depth > 1
+    ra = run_chain(a, pics, 30, (0, 0, 0), True)
+    rb = run_chain(b, pics, 30, (0, 0, 0), False)
+    for (gres, grec, gdbk), (ores, orec, odbk) in zip(ra, rb):
+        assert_same(gres, grec, ores, orec, w // 16)
+        for x, y in zip(gdbk, odbk):
+            assert np.array_equal(x, y)
+
+
+def test_high10_rejects_other_bit_depths_and_8bit_calls():
     with pytest.raises(jmhip.JmhError):
-        jmhip.Encoder(64, 48, search_range=8, search_mode=0, bit_depth=10)
+        jmhip.Encoder(64, 48, search_range=8, search_mode=0, bit_depth=12)
     e = jmhip.Encoder(64, 48, search_range=8, search_mode=3, bit_depth=10)
     y8 = np.zeros((48, 64), np.uint8), np.zeros((24, 32), np.uint8), np.zeros((24, 32), np.uint8)
     assert e.lib.jmh_set_reference(e.ctx, 0, 0, y8[0].ctypes.data, y8[1].ctypes.data, y8[2].ctypes.data, 64, 32) == jmhip.JMH_E_UNSUPPORTED_CFG
@@ -610,6 +667,12 @@ def run_lencod(binary, out_dir, extra):
     ["InputFile=synthetic:37", "FramesToBeEncoded=4", "SourceWidth=200", "SourceHeight=120", "SearchRange=16",
      "ProfileIDC=110", "SourceBitDepthLuma=9", "SourceBitDepthChroma=9", "SearchMode=3", "QPFirstFrame=2",
      "QPRemainingFrame=4", "ChromaQPOffset=-10", "WriterThreads=0"],
+    # High 10 with FFS / full search
+    ["InputFile=synthetic:38", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=32",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchMode=0"],
+    ["InputFile=synthetic:39", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "SearchMode=-1", "SymbolMode=1",
+     "SliceMode=1", "SliceArgument=22"],
 ])
 def test_lencod_bitstream_identical(extra):
     with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:
