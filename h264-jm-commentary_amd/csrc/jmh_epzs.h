@@ -46,6 +46,7 @@ struct EpzS {
     int8_t tref[6][6];                        //   MB origin at [1][1]; -1: none)
     int16_t mem[7][16][2];                    // spatial memory: the left MB's searches (types 1..7)
     int memok;
+    int scx, scy;                             // RDO with FFS (item 65): the MB's window centre
     uint16_t fpc[7][16];                      // item 61: this MB's full-pel costs per type and 4x4,
     uint16_t fpb[7][10];                      //   the neighbour MBs' at the border cells (1..9)
     alignas(4) pel hp[3][HPL];                // b, h, j of the block's [-1, w] x [-1, h] at its MV
@@ -401,6 +402,33 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
         stop = __builtin_amdgcn_readfirstlane((9 * max(med, sad) + 2 * med) >> 3);
     }
     SSTAMP(1);
+    int bx = mvx0, by = mvy0, min_mcost;
+    if (d.search_mode != 3) {
+        // RDOptimization 1 with SearchMode 0 / -1 (k_rdo_inter, item 65): FastFullPelBlockMotionSearch
+        // on the MB's window centred on the 16x16 MVP / 4 (clamped), or FullPelBlockMotionSearch on
+        // the block's own centre; every position of +-range on a lane stride (SAD from the LDS window
+        // or, outside it, from the reference picture), key = cost << 13 | spiral index (cost < 2^19:
+        // 16x16 SAD < 2^18, no negative bias under RDO), one wave minimum; no (0,0) pre-check and no
+        // zero-vector bias (!input->rdopt [J])
+        if (BT == 1 && d.search_mode == 0) {
+            if (lane == 0) { s.scx = iclip(-d.sr, d.sr, pmx / 4); s.scy = iclip(-d.sr, d.sr, pmy / 4); }
+            wave_lds_sync();
+        }
+        const int ccx = d.search_mode == 0 ? s.scx : mvx0, ccy = d.search_mode == 0 ? s.scy : mvy0;
+        const int side = 2 * range + 1, npos = side * side;
+        unsigned kb = 0xFFFFFFFFu;
+#pragma unroll 1
+        for (int p = lane; p < npos; p += NTE) {
+            const int dy = p / side - range, dx = p - (dy + range) * side - range, x = ccx + dx, y = ccy + dy;
+            const int c = (int)lane_block_sad<LW4, LH4>(s, wn, bx4, by4, x, y) + wcost(d, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+            kb = min(kb, ((unsigned)c << 13) | (unsigned)spiral_index(dx, dy));
+        }
+        kb = wave_min_u32(kb);
+        int rx, ry;
+        spiral_pos((int)(kb & 8191u), rx, ry);
+        bx = ccx + rx; by = ccy + ry;
+        min_mcost = (int)(kb >> 13);
+    } else {
     // ---- full pel: predictor `lane`, then pattern rounds
     int cx, cy;
     const bool cv = epzs_cand(d, s, lane, BT, bx4, by4, nb, range, mvx0, mvy0, cx, cy);
@@ -409,7 +437,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
                    wcost(d, mvbits(4 * cx - pmx) + mvbits(4 * cy - pmy));
     const int cost0 = __builtin_amdgcn_readfirstlane(c0);   // predictor 0: the centre, always valid
     SSTAMP(2);
-    int bx = mvx0, by = mvy0, min_mcost = cost0;
+    min_mcost = cost0;
     if (cost0 >= med) {                                    // else: stop at the centre
         const unsigned m0 = wave_min_u32(cv ? ((unsigned)c0 << 6) | (unsigned)lane : 0xFFFFFFFFu);
         min_mcost = (int)(m0 >> 6);
@@ -462,6 +490,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
                 }
             }
         }
+    }
     }
     const int fmx = bx, fmy = by;
     if (lane < NSUB) {                                     // item 61: this search's full-pel cost

@@ -211,7 +211,7 @@ __device__ __forceinline__ void full_block_search(const DevParams &d, FullS<pel>
 }
 
 template <class pel, bool FFS>
-__global__ __launch_bounds__(NTF, 6) void k_mb_me_full(const TickArgs t) {
+__global__ __launch_bounds__(NTF, sizeof(pel) == 1 ? 6 : 3) void k_mb_me_full(const TickArgs t) {   // 16-bit: LDS allows 3 per CU
     __shared__ FullS<pel> s;
     const int b = xcd_block(blockIdx.x, t.pre[t.nP]), tid = threadIdx.x;   // XCD-aware (jmh_device.h)
     if (b >= t.pre[t.nP]) return;

@@ -373,7 +373,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->bit_depth != 0 && (cfg->bit_depth < 8 || cfg->bit_depth > 10)) return JMH_E_UNSUPPORTED_CFG;
     // High 10 pictures: the EPZS wavefront (k_mb_epzs / k_mb_intra / k_mb_final on 16-bit samples)
     // RDOptimization 1: the CABAC rate, EPZS searches, either transform mode (k_rdo_inter / k_rdo_intra / k_rdo_final)
-    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode < 0 || cfg->symbol_mode > 1 || cfg->search_mode != 3))
+    if (cfg->rdo != 0 && (cfg->rdo != 1 || cfg->symbol_mode < 0 || cfg->symbol_mode > 1))
         return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version >= 10 && (cfg->quant_offset[0] < 0 || cfg->quant_offset[0] > JMH_QOFFSET_MAX || cfg->quant_offset[1] < 0 ||
                                   cfg->quant_offset[1] > JMH_QOFFSET_MAX)) return JMH_E_INVALID_ARG;

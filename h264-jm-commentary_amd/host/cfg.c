@@ -180,7 +180,6 @@ static int parse_file(jm_input *inp, const char *fn, char *err, int errlen) {
 
 int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->rdopt > 1) { snprintf(err, errlen, "RDOptimization=%d not supported (0 or 1)", inp->rdopt); return -1; }
-    if (inp->rdopt && inp->search_mode != 3) { snprintf(err, errlen, "RDOptimization=1 supports SearchMode=3 (EPZS) only"); return -1; }
     if (inp->rdopt && inp->jm_call_surface) { snprintf(err, errlen, "JMCallSurface=1 checks the RDO-off decision (RDOptimization=0)"); return -1; }
     if (inp->symbol_mode && inp->profile_idc == 66) { snprintf(err, errlen, "SymbolMode=1 (CABAC) is not allowed in the Baseline profile (ProfileIDC=66)"); return -1; }
     if (inp->symbol_mode && inp->context_init_method) { snprintf(err, errlen, "ContextInitMethod=1 (adaptive CABAC model selection) not supported (0: FixedModelNumber)"); return -1; }

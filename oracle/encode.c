@@ -202,7 +202,7 @@ static int ffs_search(mbs *s, int blocktype, int bx4, int by4, int pmvx, int pmv
     int max_pos = (2 * range + 1) * (2 * range + 1);
     int min_mcost = BIGCOST, best_pos = 0;
     if (!s->setup_done) ffs_setup(s);
-    {   /* cost for (0,0)-vector first (RDO off) */
+    if (!s->rdo) {   /* cost for (0,0)-vector first: RDO off only (!input->rdopt [J], item 65) */
         int r = (-s->scy + sr) * side + (-s->scx + sr);
         int mcost = block_sad_at(s, bx4, by4, w4, h4, r) + mv_cost(s, 2, 0, 0, pmvx, pmvy);
         if (mcost < min_mcost) { min_mcost = mcost; best_pos = s->pos_00; }

@@ -45,6 +45,14 @@ RDO = [
     ["InputFile=synthetic:91", "FramesToBeEncoded=4", "ProfileIDC=110", "SourceBitDepthLuma=10",
      "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchRange=16", "SliceMode=1", "SliceArgument=11",
      "QPRemainingFrame=24", "JMVersion=10"],
+    # SearchMode 0 (FFS) and -1 (full search) under RDO (item 65): no (0,0) pre-check, no zero bias
+    ["InputFile=synthetic:99", "FramesToBeEncoded=4", "ProfileIDC=77", "SearchRange=16", "SearchMode=0"],
+    ["InputFile=synthetic:100", "FramesToBeEncoded=3", "ProfileIDC=77", "SearchRange=8", "SearchMode=-1",
+     "SliceMode=1", "SliceArgument=11", "RestrictSearchRange=0"],
+    ["InputFile=synthetic:101", "FramesToBeEncoded=3", "ProfileIDC=110", "SourceBitDepthLuma=10",
+     "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchRange=16", "SearchMode=0", "UseHadamard=0"],
+    ["InputFile=synthetic:102", "FramesToBeEncoded=3", "ProfileIDC=100", "Transform8x8Mode=1", "SearchRange=8",
+     "SearchMode=-1", "QPFirstFrame=40", "QPRemainingFrame=44"],
 ]
 
 
@@ -132,7 +140,7 @@ def test_rdo_rate_distortion_tradeoff():
 
 
 @pytest.mark.parametrize("bad,msg", [
-    (["SearchMode=0", "ProfileIDC=77"], "SearchMode=3"),
+    (["SearchMode=2", "ProfileIDC=77"], "SearchMode=2"),
     (["RDOptimization=2", "ProfileIDC=77"], "RDOptimization=2"),
 ])
 def test_rdo_config_gate(bad, msg):

@@ -135,6 +135,29 @@ def test_rdo_cavlc_config5_width_3840():
     rdo_pair(w, h, pics, 28, bd=10, symbol_mode=0, search_range=32, slice_mbs=240)
 
 
+# ---- SearchMode 0 (FFS) / -1 (full search) under RDO (item 65): k_rdo_inter's searches scan every
+#      position of the window on a lane stride; no (0,0) pre-check, no zero-vector bias
+@pytest.mark.parametrize("sm,bd,kw,qp", [
+    (0, 8, dict(search_range=16), 28),
+    (0, 8, dict(search_range=8, slice_mbs=11, transform_8x8_mode=1), 36),
+    (-1, 8, dict(search_range=8, restrict_search_range=0), 20),
+    (0, 10, dict(search_range=16, symbol_mode=0), 30),
+    (-1, 10, dict(search_range=8, transform_8x8_mode=1), 26),
+])
+def test_rdo_ffs_full_search(sm, bd, kw, qp):
+    pics = (hbd_seq(176, 144, 3, seed=120 + qp, bd=bd) if bd > 8 else moving_seq(176, 144, 3, seed=120 + qp))
+    kw = dict(kw)
+    symbol_mode = kw.pop("symbol_mode", 1)
+    rdo_pair(176, 144, pics, qp, 0, bd=bd, symbol_mode=symbol_mode, search_mode=sm, **kw)
+
+
+def test_rdo_ffs_width_3840():
+    """RDO + FFS at 3840 wide with one-row slices, SR 32 (many positions outside k_rdo_inter's window)."""
+    w, h = 3840, 64
+    pics = hbd_seq(w, h, 3, seed=48, bd=10)
+    rdo_pair(w, h, pics, 28, bd=10, search_range=32, slice_mbs=240, search_mode=0)
+
+
 @pytest.mark.parametrize("slice_mbs", [40, 0, 100])
 def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
     """Pictures in flight on the RD stage schedule (one-row slices: diagonals, lag 16; one slice
@@ -167,6 +190,11 @@ def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
     ["InputFile=synthetic:75", "FramesToBeEncoded=3", "SourceWidth=352", "SourceHeight=96", "SearchRange=32",
      "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SliceMode=1",
      "SliceArgument=22"],
+    # SearchMode 0 / -1 under RDO (item 65)
+    ["InputFile=synthetic:78", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
+     "ProfileIDC=77", "SearchMode=0"],
+    ["InputFile=synthetic:79", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=8",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=-1", "SymbolMode=0"],
     # SymbolMode 0 (item 64)
     ["InputFile=synthetic:76", "FramesToBeEncoded=5", "SourceWidth=352", "SourceHeight=288", "SearchRange=16",
      "ProfileIDC=66", "SymbolMode=0"],
@@ -178,7 +206,7 @@ def test_rdo_lencod_bitstream_identical(extra):
     """The product lencod (device RD loop, device deblocking, pipelined pictures, writer threads)
     and the CPU lencod write identical bitstreams and reconstructions; both writers check every
     macroblock's RD rate against the CABAC / CAVLC bits they emit."""
-    args = (["SymbolMode=1"] if "SymbolMode=0" not in extra else []) + extra + ["RDOptimization=1", "SearchMode=3"]
+    args = ["SymbolMode=1", "SearchMode=3"] + extra + ["RDOptimization=1"]   # later entries win
     with tempfile.TemporaryDirectory() as g, tempfile.TemporaryDirectory() as c:
         lg = run_lencod(LENCOD, g, args)
         lc = run_lencod(LENCOD_CPU, c, args)
@@ -189,7 +217,7 @@ def test_rdo_lencod_bitstream_identical(extra):
 
 
 def test_rdo_rejects_unsupported():
-    for kw in (dict(rdo=1, symbol_mode=2, search_mode=3), dict(rdo=1, symbol_mode=1, search_mode=0),
-               dict(rdo=1, symbol_mode=0, search_mode=-1)):
+    for kw in (dict(rdo=1, symbol_mode=2, search_mode=3), dict(rdo=2, symbol_mode=1, search_mode=3),
+               dict(rdo=1, symbol_mode=0, search_mode=2)):
         with pytest.raises(jmhip.JmhError):
             jmhip.Encoder(64, 48, search_range=8, **kw)
