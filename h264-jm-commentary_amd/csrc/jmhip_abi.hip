@@ -404,13 +404,11 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     c->next_id = 0; c->next_entry = 0; c->last_id = -1; c->last_entry = -1;
     c->ref_kind = REF_NONE; c->ref_entry = -1; c->cur_entry = -1;
     c->prof_mb = -1;
+    // A/B knob only: at most this many MBs per tick (younger pictures wait).  Capping config 5's RD
+    // ticks at one dispatch round (5 x 256 CUs) measured 333 MP/s against 474 uncapped
+    // (profiles/r7a_tick_cap_ab.txt): the longer ticks of the full pipeline win, so no cap by default.
     c->tick_cap = 0;
-    if (cfg->rdo) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) != hipSuccess || cus <= 0) cus = 256;
-        c->tick_cap = 5 * cus;
-    }
-    if (const char *e = getenv("JMH_TICK_CAP")) c->tick_cap = atoi(e);   // A/B (0: no cap)
+    if (const char *e = getenv("JMH_TICK_CAP")) c->tick_cap = atoi(e);
     int st = JMH_OK;
 #define ALLOC(p, n) do { if (hipMalloc((void **)&(p), (n)) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
     {
