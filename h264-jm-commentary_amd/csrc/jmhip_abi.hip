@@ -415,9 +415,13 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
             hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         // RDO on: the intra role on a side stream, concurrent with the inter role (the inter
-        // workgroups' LDS leaves room for intra ones beside them); joined before k_rdo_final
-        const char *side = getenv("JMH_RDO_SIDE");
-        if (cfg->rdo && !(side && atoi(side) == 0)) {
+        // workgroups' LDS leaves room for intra ones beside them); joined before k_rdo_final.
+        // RDO off with a separate search kernel (EPZS, full search, High 10 FFS): k_mb_intra on the
+        // side stream beside k_mb_epzs / k_mb_me_full, joined before k_mb_final (A/B knobs:
+        // JMH_RDO_SIDE=0, JMH_INTRA_SIDE=0)
+        const char *side = getenv(cfg->rdo ? "JMH_RDO_SIDE" : "JMH_INTRA_SIDE");
+        const bool sep_search = cfg->rdo || cfg->search_mode != 0 || (cfg->bit_depth > 8);
+        if (sep_search && !(side && atoi(side) == 0)) {
             if (hipStreamCreateWithFlags(&c->sst, hipStreamNonBlocking) != hipSuccess ||
                 hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) { st = JMH_E_HIP; goto fail; }
@@ -644,9 +648,14 @@ static int issue_tick(jmh_ctx *c) {
             HCHK(jmh_launch_analyse(t, c->st));
             if (t.t8) HCHK(jmh_launch_intra8(t, c->st));   // Intra8x8 decision (High profile)
         } else {                                        // EPZS (one wave per MB) / SearchMode -1 / High 10 FFS
+            // the intra decisions (independent of the searches) on the side stream: its workgroups
+            // take the CUs the search workgroups leave as they finish; joined before k_mb_final
+            const bool side = c->sst && nP > 0;
+            if (side) { HCHK(hipEventRecord(c->ev_fork, c->st)); HCHK(hipStreamWaitEvent(c->sst, c->ev_fork, 0)); }
             if (t.search_mode == 3) HCHK(jmh_launch_epzs(t, c->st));
             else HCHK(jmh_launch_me_full(t, c->st));
-            HCHK(jmh_launch_intra(t, c->st));           // all intra decisions incl. Intra8x8
+            HCHK(jmh_launch_intra(t, side ? c->sst : c->st));   // all intra decisions incl. Intra8x8
+            if (side) { HCHK(hipEventRecord(c->ev_join, c->sst)); HCHK(hipStreamWaitEvent(c->st, c->ev_join, 0)); }
         }
         if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
         if (!t.rdo) HCHK(jmh_launch_final(t, c->st));
