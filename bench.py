@@ -230,7 +230,7 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
     return bool(ok)
 
 
-def read_pmc_traffic(config, search_mode):
+def read_pmc_traffic(config, search_mode, t8=None, slice_mbs=None):
     """(HBM bytes per macroblock of the roofline's kernels, source description) from the rocprofv3
     PMC passes of tools/pmc_traffic.sh for this config, or (None, None).  The latest pass per
     config is kept in tools/pmc_traffic.json (it travels to the GPU box, unlike profiles/); it is
@@ -242,6 +242,10 @@ def read_pmc_traffic(config, search_mode):
     try:
         with open(p) as f:
             j = json.load(f)["configs"][key]
+        # only the configuration the pass measured (Transform8x8Mode, slices)
+        if ("t8" in j and t8 is not None and j["t8"] != t8) or \
+           ("slice_mbs" in j and slice_mbs is not None and j["slice_mbs"] != slice_mbs):
+            return None, None
         src = (f"tools/pmc_traffic.json config {key}: {j['kernel']} ({j.get('source', 'rocprofv3 PMC')}; "
                f"{j.get('calibration', 'uncalibrated')})")
         return j["hbm_bytes_per_mb"], src
@@ -444,7 +448,7 @@ def main():
     ad_per_launch = AD_PER_FRAME / NMB * mbs_per_launch
     achieved_tads = ad_per_launch / (an_launch_ms * 1e-3) / 1e12
     peak_tads, peak_src = sad_peak()
-    pmc, pmc_src = read_pmc_traffic(args.config, search_mode)
+    pmc, pmc_src = read_pmc_traffic(args.config, search_mode, cfg["t8"], SLICE_MBS)
     sm_name = {0: "FFS SearchMode=0", -1: "full search SearchMode=-1", 3: "EPZS SearchMode=3"}[search_mode]
     ffs = search_mode == 0
     an_name = ("k_rdo_inter+k_rdo_intra+k_rdo_final" if RDO else
