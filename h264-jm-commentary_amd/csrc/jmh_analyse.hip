@@ -1070,12 +1070,14 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
     const bool first_thread = threadIdx.x == 0;   // a lane mask: threadIdx itself dies early
     const int role = b < nPg ? 2 : 0;
+    int tag = role;                                           // debug (JMH_BLOCK_PROF): role | MB << 4 | entry << 20
     if (role == 2) {
         const int m = xcd_block(b, nPm);                      // XCD-aware: neighbouring MBs share an L2
         if (m >= nPm) return;                                 // padding block (whole workgroup)
         const int e = tick_entry(t, m);
         const DevParams d = tick_params(t, e);
         const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
+        tag = 2 | (mby * d.mbw + mbx) << 4 | e << 20;
         me_mb(d, s.me, mbx, mby);
     } else {
         const int q = __builtin_amdgcn_readfirstlane(4 * (b - nPg) + (int)(threadIdx.x >> 7));
@@ -1090,7 +1092,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
         if (first_thread) {
             t.bprof[3 * b] = t0;
             t.bprof[3 * b + 1] = wall_clock64();
-            t.bprof[3 * b + 2] = role;
+            t.bprof[3 * b + 2] = (unsigned)tag;
         }
     }
 }

@@ -965,13 +965,15 @@ int jmh_sync(jmh_ctx *c) {
         unsigned long long t0 = ~0ull, t1 = 0;
         double sum[5] = {0, 0, 0, 0, 0}, mx[5] = {0, 0, 0, 0, 0};
         std::vector<double> durs[5];
+        std::vector<std::pair<double, unsigned long long>> slow;   // role-2 blocks: (duration, i)
         int n[5] = {0, 0, 0, 0, 0};
         unsigned long long f0 = ~0ull, f1 = 0, r0[5], r1[5];
         for (int r = 0; r < 5; r++) { r0[r] = ~0ull; r1[r] = 0; }
         for (int i = 0; i < c->bprof_blocks; i++) {
             unsigned long long a = h[3 * i], b = h[3 * i + 1];
-            int role = (int)h[3 * i + 2];
+            int role = (int)(h[3 * i + 2] & 15);                   // k_mb_analyse: | MB << 4 | entry << 20
             if (!a || role < 0 || role > 4 || b < a) continue;   // 0: padding block, not written
+            if (role == 2) slow.push_back({(double)(b - a) * us, (unsigned long long)i});
             if (role == 3) { f0 = a < f0 ? a : f0; f1 = b > f1 ? b : f1; }
             r0[role] = a < r0[role] ? a : r0[role]; r1[role] = b > r1[role] ? b : r1[role];
             t0 = a < t0 ? a : t0; t1 = b > t1 ? b : t1;
@@ -988,6 +990,27 @@ int jmh_sync(jmh_ctx *c) {
             }
         if (f1) fprintf(stderr, " final: first start %.1fus after the analysis' first, span %.1fus", (double)(f0 - t0) * us, (double)(f1 - f0) * us);
         fprintf(stderr, "\n");
+        if (!slow.empty()) {                                    // the slowest motion-search blocks: which MBs
+            std::sort(slow.begin(), slow.end());
+            fprintf(stderr, "jmh_blocks slowest role2 (mbx,mby,entry start+dur us):");
+            for (size_t k = slow.size() > 12 ? slow.size() - 12 : 0; k < slow.size(); k++) {
+                const unsigned long long i = slow[k].second, tg = h[3 * i + 2];
+                const int mb = (int)((tg >> 4) & 0xFFFF), en = (int)(tg >> 20);
+                fprintf(stderr, " (%d,%d,%d %.1f+%.1f)", mb % c->mbw, mb / c->mbw, en, (double)(h[3 * i] - t0) * us, slow[k].first);
+            }
+            double xs[8] = {0}, xm[8] = {0};                     // per XCD (hardware block % 8)
+            int xn[8] = {0};
+            for (auto &q : slow) { const int x = (int)(q.second % 8); xs[x] += q.first; xn[x]++; xm[x] = q.first > xm[x] ? q.first : xm[x]; }
+            fprintf(stderr, " per XCD mean/max:");
+            for (int x = 0; x < 8; x++) if (xn[x]) fprintf(stderr, " %d:%.1f/%.1f", x, xs[x] / xn[x], xm[x]);
+            fprintf(stderr, " fastest:");
+            for (size_t k = 0; k < slow.size() && k < 6; k++) {
+                const unsigned long long i = slow[k].second, tg = h[3 * i + 2];
+                const int mb = (int)((tg >> 4) & 0xFFFF), en = (int)(tg >> 20);
+                fprintf(stderr, " (%d,%d,%d %.1f+%.1f)", mb % c->mbw, mb / c->mbw, en, (double)(h[3 * i] - t0) * us, slow[k].first);
+            }
+            fprintf(stderr, "\n");
+        }
         c->bprof_blocks = 0;
     }
     if (c->d_prof) {   // debug: phase timestamps of MB prof_mb (first picture of a tick)

@@ -4,10 +4,11 @@
   python tools/make_golden.py          # rewrite tests/golden/*
 
 Fixtures (all data; no reference source text):
-  manifest.json   sha256 of lencod_cpu bitstreams + reconstructions for eight encoder.cfg
+  manifest.json   sha256 of lencod_cpu bitstreams + reconstructions for eleven encoder.cfg
                   configurations (the first three as in the GPU bitstream test; one with slices, one
                   CABAC, two with RDOptimization 1 -- one of them High 10 -- and a High 10 RDO-off
-                  one), and of the
+                  one; round 4: RDO with CAVLC + FFS, RDO with the 8x8 transform at 10 bits, 10-bit
+                  FFS), and of the
                   per-picture jmh_mb_result arrays + reconstructions of a 64x48 I-P-P sequence
   tq4x4.npz       dct_luma vectors: residual/prediction inputs and levels/recon/cost/nonzero
                   outputs at QP 0, 12, 28, 51, intra and inter rounding
@@ -55,6 +56,16 @@ LENCOD_CONFIGS = [
     # High 10 with RDO off: EPZS + 8x8 transform, CAVLC
     ["InputFile=synthetic:8", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
      "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SearchMode=3"],
+    # round 4: JM's default encoder.cfg shape -- RDOptimization 1 with CAVLC rates and FFS (items 64, 65)
+    ["InputFile=synthetic:9", "FramesToBeEncoded=4", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "ProfileIDC=66", "RDOptimization=1", "SymbolMode=0", "SearchMode=0"],
+    # RDOptimization 1 with the 8x8 transform at 10 bits (item 63): I8MB, 8x8-transform inter candidates
+    ["InputFile=synthetic:10", "FramesToBeEncoded=3", "SourceWidth=352", "SourceHeight=96", "SearchRange=32",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "Transform8x8Mode=1", "SymbolMode=1",
+     "RDOptimization=1", "SearchMode=3", "SliceMode=1", "SliceArgument=22"],
+    # FFS on 10-bit samples, RDO off (item 66)
+    ["InputFile=synthetic:11", "FramesToBeEncoded=3", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
+     "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "SearchMode=0"],
 ]
 SEQ = dict(w=64, h=48, seed=21, frames=3, qp=28, search_range=16)
 
