@@ -10,7 +10,10 @@ __device__ __forceinline__ int wcost(const DevParams &d, int bits) {
 }
 
 #define NTE 64                                // one wave per macroblock
-#define EOFF_L 52                             // LDS window margin around the MB (or 2 SR + 4 if less)
+#ifndef EOFF_L                                // (-DEOFF_L=...: A/B builds)
+#define EOFF_L 48                             // LDS window margin around the MB (or 2 SR + 4 if less;
+                                              //   A/B on config 3: profiles/r7j_window_ab.txt)
+#endif
 #ifndef EOFF_L16
 #define EOFF_L16 40                           // ... for 16-bit samples: 30.4 KB k_rdo_inter, five MBs per CU (A/B: profiles/r5r_window_ab.txt)
 #endif
@@ -40,7 +43,6 @@ struct EpzS {
     alignas(8) pel org[256];
     Border bd;
     int16_t all_mv[8][16][2];
-    int16_t pmv[8][16][2];                    // the MVP each search used
     int motion_cost[8][4];
     int16_t tmv[6][6][2];                     // previous picture's MVs around the MB (4x4 units,
     int8_t tref[6][6];                        //   MB origin at [1][1]; -1: none)
@@ -354,12 +356,15 @@ __device__ __forceinline__ int had_packed(const e16x2 (&r)[4][2]) {
     return (int)((t & 0xFFFFu) + (t >> 16));
 }
 
-// BlockMotionSearch [J] of one block on the wave: EPZS full pel + SubPelBlockMotionSearch
+// BlockMotionSearch [J] of one block on the wave: EPZS full pel + SubPelBlockMotionSearch;
+// pmvo (k_rdo_inter; null in k_mb_epzs): receives the MVP each search used (the RD rate's mvd)
 template <int BT, class pel>
-__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, const EWin<pel> &wn, int bx4, int by4, int mc, int b8, int best8x8, bool prof) {
-    // debug (JMH_PHASE_PROF): steps of the MB's first 4x4 search into prof[41..46]
-    const bool sp = prof && BT == 7 && bx4 == 0 && by4 == 0;
-#define SSTAMP(k) do { if (sp) d.prof[41 + (k)] = wall_clock64(); } while (0)
+__device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, const EWin<pel> &wn, int bx4, int by4, int mc, int b8, int best8x8, bool prof,
+                                           int16_t (*pmvo)[16][2] = nullptr) {
+    // debug (JMH_PHASE_PROF): steps of the MB's first 4x4 search into prof[41..46], of its 16x16
+    // search into prof[47..52] (k_mb_epzs only)
+    const bool sp = prof && ((BT == 7 && bx4 == 0 && by4 == 0) || BT == 1);
+#define SSTAMP(k) do { if (sp) d.prof[(BT == 1 ? 47 : 41) + (k)] = wall_clock64(); } while (0)
     SSTAMP(0);
     constexpr int LW4 = BT <= 2 ? 2 : (BT <= 5 ? 1 : 0), LH4 = (BT == 1 || BT == 3) ? 2 : (BT == 2 || BT == 4 || BT == 6) ? 1 : 0;
     constexpr int W4 = 1 << LW4, H4 = 1 << LH4, LNS = LW4 + LH4, NSUB = 1 << LNS;
@@ -671,8 +676,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
         const int k = (by4 + (lane >> LW4)) * 4 + bx4 + (lane & (W4 - 1));
         s.all_mv[BT][k][0] = (int16_t)(4 * fmx + qx);
         s.all_mv[BT][k][1] = (int16_t)(4 * fmy + qy);
-        s.pmv[BT][k][0] = (int16_t)pmx;           // the MVP of the search: the RD rate's mvd
-        s.pmv[BT][k][1] = (int16_t)pmy;
+        if (pmvo) { pmvo[BT][k][0] = (int16_t)pmx; pmvo[BT][k][1] = (int16_t)pmy; }
     }
     if (lane == 0) s.motion_cost[BT][mc] += min_mcost;
     wave_lds_sync();

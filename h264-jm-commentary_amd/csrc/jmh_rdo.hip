@@ -219,6 +219,7 @@ struct RdoP8Own<pel, true> {};
 template <class pel>
 struct RdoInterS {
     EpzS<pel> e;                  // the motion searches
+    int16_t pmv[8][16][2];        // the MVP each search used (the candidates' mvds)
     alignas(4) pel orgc[2][64];
     alignas(4) uint8_t st0[JMR_NCTX];      // the slice's coding state at the MB start
     alignas(4) uint8_t strun[JMR_NCTX];    // the P8x8 running state (decided 8x8 blocks)
@@ -374,11 +375,11 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     PSTAMP(41);
     const jmr_mbinfo *A = hasA ? &s.nbA : nullptr, *B = hasB ? &s.nbB : nullptr;
     // ---- motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch [J])
-    epzs_block<1>(d, s.e, wn, 0, 0, 0, 0, 0, false);
-    epzs_block<2>(d, s.e, wn, 0, 0, 0, 0, 0, false);
-    epzs_block<2>(d, s.e, wn, 0, 2, 1, 0, 0, false);
-    epzs_block<3>(d, s.e, wn, 0, 0, 0, 0, 0, false);
-    epzs_block<3>(d, s.e, wn, 2, 0, 1, 0, 0, false);
+    epzs_block<1>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
+    epzs_block<2>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
+    epzs_block<2>(d, s.e, wn, 0, 2, 1, 0, 0, false, s.pmv);
+    epzs_block<3>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
+    epzs_block<3>(d, s.e, wn, 2, 0, 1, 0, 0, false, s.pmv);
     PSTAMP(42);
     const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
     for (int i = lane; i < JMR_NCTX / 4; i += 64) reinterpret_cast<uint32_t *>(s.strun)[i] = reinterpret_cast<const uint32_t *>(s.st0)[i];
@@ -393,15 +394,15 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
 #pragma unroll 1
     for (int b8 = 0; b8 < 4 && p8; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        epzs_block<4>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
-        epzs_block<5>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
-        epzs_block<5>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false);
-        epzs_block<6>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
-        epzs_block<6>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false);
-        epzs_block<7>(d, s.e, wn, X, Y, b8, b8, best8x8, false);
-        epzs_block<7>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false);
-        epzs_block<7>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false);
-        epzs_block<7>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false);
+        epzs_block<4>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<5>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<5>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv);
+        epzs_block<6>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<6>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<7>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<7>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<7>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv);
+        epzs_block<7>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false, s.pmv);
         PSTAMP(43 + 2 * b8);
         const int bx4 = X + (b4 & 1), by4 = Y + (b4 >> 1), k = by4 * 4 + bx4;
         const int px = 4 * bx4 + (l & 3), py = 4 * by4 + (l >> 2), q8 = (4 * (b4 >> 1) + (l >> 2)) * 8 + 4 * (b4 & 1) + (l & 3);
@@ -430,8 +431,8 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
             if (lane == 0) { s.cost8[w] = cost; s.blk8[w] = blk; s.dist8[w] = dist; }
             if (lane < 4) {
                 const int kk = (Y + (lane >> 1)) * 4 + X + (lane & 1);
-                tp->mvd8[w][lane][0] = (int16_t)(s.e.all_mv[sm][kk][0] - s.e.pmv[sm][kk][0]);
-                tp->mvd8[w][lane][1] = (int16_t)(s.e.all_mv[sm][kk][1] - s.e.pmv[sm][kk][1]);
+                tp->mvd8[w][lane][0] = (int16_t)(s.e.all_mv[sm][kk][0] - s.pmv[sm][kk][0]);
+                tp->mvd8[w][lane][1] = (int16_t)(s.e.all_mv[sm][kk][1] - s.pmv[sm][kk][1]);
             }
         }
         if (!d.cavlc)
@@ -490,7 +491,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         if (lane < 32) {
             const int kk = lane >> 1, c = lane & 1, smk = (best8x8 >> (4 * (((kk >> 3) << 1) + ((kk & 3) >> 1)))) & 15;
             L[4].mv[kk][c] = s.e.all_mv[smk][kk][c];
-            L[4].mvd[kk][c] = (int16_t)(s.e.all_mv[smk][kk][c] - s.e.pmv[smk][kk][c]);
+            L[4].mvd[kk][c] = (int16_t)(s.e.all_mv[smk][kk][c] - s.pmv[smk][kk][c]);
         }
         if (lane < 4) L[4].b8mode[lane] = (int8_t)((best8x8 >> (4 * lane)) & 15);
         const int dist = wave_sum(e2);
@@ -528,7 +529,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
             s.fmv[k][cc] = (int16_t)v;
             if (c < 4) {
                 L[c].mv[k][cc] = (int16_t)v;
-                L[c].mvd[k][cc] = (int16_t)(c == 0 ? 0 : v - s.e.pmv[c][k][cc]);
+                L[c].mvd[k][cc] = (int16_t)(c == 0 ? 0 : v - s.pmv[c][k][cc]);
             }
         }
         if (c < 4 && lane < 4) L[c].b8mode[lane] = (int8_t)c;
@@ -549,7 +550,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
                 const int v = s.e.all_mv[sm][k][cc];
                 s.fmv[k][cc] = (int16_t)v;
                 L[c + 7].mv[k][cc] = (int16_t)v;
-                L[c + 7].mvd[k][cc] = (int16_t)(v - s.e.pmv[sm][k][cc]);
+                L[c + 7].mvd[k][cc] = (int16_t)(v - s.pmv[sm][k][cc]);
             }
             if (lane < 4) L[c + 7].b8mode[lane] = (int8_t)(c == 4 ? 4 : c);
             wave_lds_sync();
