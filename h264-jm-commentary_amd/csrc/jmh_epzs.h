@@ -14,6 +14,13 @@ __device__ __forceinline__ int wcost(const DevParams &d, int bits) {
 #define EOFF_L 48                             // LDS window margin around the MB (or 2 SR + 4 if less;
                                               //   A/B on config 3: profiles/r7j_window_ab.txt)
 #endif
+// window loads in flight per lane (one batch of global loads per round trip)
+#ifndef EPZS_NB8
+#define EPZS_NB8 32
+#endif
+#ifndef EPZS_NB16
+#define EPZS_NB16 16
+#endif
 #ifndef EOFF_L16
 #define EOFF_L16 40                           // ... for 16-bit samples: 30.4 KB k_rdo_inter, five MBs per CU (A/B: profiles/r5r_window_ab.txt)
 #endif
@@ -742,7 +749,7 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
     if constexpr (sizeof(pel) == 2) {
         // 16-bit samples: two per dword; with off % 4 == 0 a dword is aligned in the picture and
         // wholly inside or outside it (as for bytes), else per-sample clamped reads
-        constexpr int ND2 = EGeo<pel>::ew / 2, NB = 16;
+        constexpr int ND2 = EGeo<pel>::ew / 2, NB = EPZS_NB16;
         const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND2;
         if ((off & 3) == 0) {
             for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
@@ -779,7 +786,7 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
         // with off % 4 == 0 the window's dwords are aligned in the picture (pix_x % 16 == 0, wcx %
         // 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an outside
         // dword is the replicated edge sample.  Two batches of 32 loads per lane in flight.
-        constexpr int ND4 = EGeo<pel>::ew / 4, NB = 32;
+        constexpr int ND4 = EGeo<pel>::ew / 4, NB = EPZS_NB8;
         const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND4;
         if ((off & 3) == 0) {
             for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
