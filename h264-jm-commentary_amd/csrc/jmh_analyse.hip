@@ -41,7 +41,6 @@
 #endif
 #include "jmh_intra8.h"
 #include "jmh_intra.h"
-#include "jmh_final.h"
 
 #define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
 #define MVB_LEN 1104
@@ -78,22 +77,7 @@ struct MeS {
 union AnalyseS {
     MeS me;
     IntraS<uint8_t> in[4];
-    FinS<uint8_t> fin;                        // the fused final role (TickArgs.fused)
 };
-
-// fused final: a producer's "this MB's part is written" (agent-scope release: visible to every
-// XCD), and the consumer's bounded wait for it (tens of ms at most: a wrong result, never a hang)
-__device__ __forceinline__ void done_release(int32_t *f, int v) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool done_wait(const int32_t *f, int v) {
-    for (int i = 0; i < (1 << 16); i++) {
-        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v) return true;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    return false;
-}
 
 __device__ __forceinline__ void sstamp(MeS &s, int wave) {
     if (wave == 0 && __lane_id() == 0 && s.pst && s.pn < 44) s.pst[s.pn++] = wall_clock64();
@@ -997,11 +981,9 @@ __device__ __forceinline__ void i4_block(const DevParams &d, IntraS<pel> &s, MbS
 }
 
 // one MB on 128 threads (tid = 0..127, waves 0 and 1 of the group); every thread of the
-// workgroup reaches the same barriers (act: the group has an MB).
-// fseq (fused final): > 0 stores the tick's sequence number into MbScratch.done_i0 / done_i1 once
-// wave 0 / 1 has written its part of the MB
+// workgroup reaches the same barriers (act: the group has an MB)
 template <class pel>
-__device__ __forceinline__ void intra_role(const DevParams &d, IntraS<pel> &s, int mbx, int mby, int tid, bool act, bool i4, int fseq = 0) {
+__device__ __forceinline__ void intra_role(const DevParams &d, IntraS<pel> &s, int mbx, int mby, int tid, bool act, bool i4) {
     const int wave = tid >> 6, lane = tid & 63;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
     const MbAvail mav = mb_avail(d, mbx, mby);
@@ -1043,7 +1025,6 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS<pel> &s, i
     // Intra16x16 (wave 0) and intra chroma mode (wave 1) decisions
     if (wave == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
     else chroma_decision(d, s.nb, scr, lane, avL, avT, avTL);
-    if (fseq && lane == 0) done_release(wave ? &scr->done_i1 : &scr->done_i0, fseq);
     PSTAMP(14);
 }
 
@@ -1085,32 +1066,9 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     // dispatched first), then intra workgroups over every MB, four MBs (128 threads each) per
     // workgroup: Intra16x16 + chroma decisions, and Intra4x4 for MBs without a motion-search
     // workgroup (I pictures; SearchMode -1, where k_mb_me_full searched)
-    // fused final (TickArgs.fused): then one workgroup per MB runs k_mb_final's work on its first
-    // 256 threads once the MB's producers have signalled (MbScratch.done_*).  Workgroups are
-    // dispatched in block order on every XCD, so when a final workgroup waits, every producer it
-    // waits for has been dispatched (on its own XCD, before that XCD's final workgroups) and runs
-    // to completion: no deadlock; the wait is bounded anyway.
     const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0, nPg = xcd_grid(nPm), tot = t.pre[t.npic], b = blockIdx.x;
-    const int nIg = (tot + 3) / 4;                            // the intra workgroups
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
     const bool first_thread = threadIdx.x == 0;   // a lane mask: threadIdx itself dies early
-    if (t.fused && b >= nPg + nIg) {
-        const int m = xcd_block(b - nPg - nIg, tot);
-        if (m >= tot || threadIdx.x >= NT) return;            // padding block; the upper half idles
-        const int e = tick_entry(t, m);
-        const DevParams d = tick_params(t, e);
-        const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
-        const MbScratch *sc = d.scr + mby * d.mbw + mbx;
-        if (threadIdx.x == 0) {
-            bool ok = done_wait(&sc->done_i0, t.seq) && done_wait(&sc->done_i1, t.seq);
-            if (m < nPm) ok = ok && done_wait(&sc->done_s, t.seq);
-            (void)ok;
-        }
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // the producers' MbScratch writes
-        final_mb<5, uint8_t, false>(t, s.fin, m, threadIdx.x, b, t0);
-        return;
-    }
     const int role = b < nPg ? 2 : 0;
     int tag = role;                                           // debug (JMH_BLOCK_PROF): role | MB << 4 | entry << 20
     if (role == 2) {
@@ -1121,18 +1079,13 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
         const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
         tag = 2 | (mby * d.mbw + mbx) << 4 | e << 20;
         me_mb(d, s.me, mbx, mby);
-        if (t.fused) {                                        // the MB's search + Intra4x4 results are written
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // every wave's stores, then one flag
-            __syncthreads();
-            if (threadIdx.x == 0) done_release(&d.scr[mby * d.mbw + mbx].done_s, t.seq);
-        }
     } else {
         const int q = __builtin_amdgcn_readfirstlane(4 * (b - nPg) + (int)(threadIdx.x >> 7));
         const bool act = q < tot;
         const int e = tick_entry(t, act ? q : 0);
         const DevParams d = tick_params(t, e);
         const int mby = d.y_min + ((act ? q : t.pre[e]) - t.pre[e]), mbx = d.diag - 2 * mby;
-        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act, q >= nPm, t.fused ? t.seq : 0);
+        intra_role(d, s.in[threadIdx.x >> 7], mbx, mby, threadIdx.x & 127, act, q >= nPm);
     }
     if (t.bprof) {
         __syncthreads();
@@ -1150,8 +1103,11 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
 // workgroup) in ONE launch of small workgroups -- instead of k_mb_analyse's 512-thread, 78 KB LDS
 // workgroups followed by k_mb_intra8 -- so the two independent decisions share the CUs (eight
 // workgroups per CU): blocks [0, nRg) the intra roles (longest, first), then the Intra8x8 blocks.
+#ifndef JMH_INTRA_OCC
+#define JMH_INTRA_OCC 8                       // waves per SIMD the register budget targets (A/B: -D)
+#endif
 template <class pel>
-__global__ __launch_bounds__(NT, 8) void k_mb_intra(const TickArgs t) {
+__global__ __launch_bounds__(NT, JMH_INTRA_OCC) void k_mb_intra(const TickArgs t) {
     __shared__ union {
         IntraS<pel> in[2];
         I8S<pel> i8;
@@ -1182,7 +1138,7 @@ hipError_t jmh_launch_intra(const TickArgs &t, hipStream_t st) {
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
-    const int nblocks = xcd_grid(t.me_in_analyse ? t.pre[t.nP] : 0) + (t.pre[t.npic] + 3) / 4 + (t.fused ? xcd_grid(t.pre[t.npic]) : 0);
+    const int nblocks = xcd_grid(t.me_in_analyse ? t.pre[t.nP] : 0) + (t.pre[t.npic] + 3) / 4;
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }

@@ -42,10 +42,6 @@ struct MbScratch {
     int32_t i8cost, i8cbp, i8modes;      // i8modes: 4 bits per 8x8 block
     int16_t i8lev[16][16];               // levels in the CAVLC interleave (jmh_mb_result.luma)
     alignas(4) uint8_t i8rec[512];
-    // fused final (FFS ticks, TickArgs.fused): the tick sequence number each producer stores, with
-    // release, once its part of this MB is written -- the search workgroup, and waves 0 / 1 of the
-    // intra group (zeroed at allocation; sequence numbers start at 1)
-    int32_t done_s, done_i0, done_i1;
 };
 
 // RDOptimization 1: the per-picture RD state, stored right after the picture's MbScratch array
@@ -153,8 +149,6 @@ struct TickArgs {
     int epzs_mints, epzs_maxts;          // EPZSMinThresScale, EPZSMaxThresScale
     int slice_mbs;                       // SliceMode 1: MBs per slice (>= 1; mbw * mbh for one slice)
     int bd;                              // bit depth: 8 (uint8_t samples) or 9 / 10 (uint16_t, High 10)
-    int fused;                           // FFS ticks: k_mb_final's work as k_mb_analyse's last role (spin on
-    int seq;                             //   MbScratch.done_*; seq = this tick's number, >= 1)
     int rdo;                             // RDOptimization 1: k_rdo_inter + k_rdo_intra + k_rdo_final on the stage
                                          //   (1: CABAC rates, 2: CAVLC rates, SymbolMode 0)
     const int32_t *sched, *soff;         //   schedule: MB addresses in stage order, offsets per stage

@@ -3,8 +3,9 @@
 // with 16-lane transform groups (LumaResidualCoding / dct_luma_16x16 / dct_chroma +
 // reconstruction), or, with Transform8x8Mode, TransformDecision and dct_luma8x8 on one wave per
 // 8x8 block, the outputs the next diagonal depends on (reconstruction, MVs, reference indices,
-// intra modes) and the fused DeblockMb.  Run by k_mb_final (jmh_final.hip) and, for FFS ticks
-// with the fused final, by k_mb_analyse's final role (jmh_analyse.hip).
+// intra modes) and the fused DeblockMb, run by k_mb_final (jmh_final.hip).  (Round 4 also ran it
+// as a last role of k_mb_analyse, waiting on per-MB flags: 1159 -> 792 MP/s on config 2,
+// profiles/r7m_fused_final_ab.txt, not kept.)
 #ifndef JMH_FINAL_H
 #define JMH_FINAL_H
 #include "jmh_deblock.h"

@@ -178,7 +178,6 @@ struct jmh_ctx {
     // k_rdo_inter (its LDS fits five MBs per CU), so that a tick is never one full round plus a
     // partial one; the pictures beyond the cap wait for the next tick (oldest pictures first)
     int tick_cap;
-    bool fused_final;                    // FFS ticks: k_mb_final's work inside k_mb_analyse (JMH_FUSED_FINAL)
 };
 
 #define HCHK(x)                                                                  \
@@ -232,7 +231,6 @@ static int alloc_entry(jmh_ctx *c, PicBuf &b) {
     ALLOC(b.res, c->nmb * sizeof(jmh_mb_result));
     // RDOptimization 1: the picture's RdoPic sits right after its MbScratch array (jmh_device.h)
     ALLOC(b.scr, c->cfg.rdo ? rdo_pic_offset(c->nmb) + sizeof(RdoPic) : c->nmb * sizeof(MbScratch));
-    if (hipMemset(b.scr, 0, c->nmb * sizeof(MbScratch)) != hipSuccess) return JMH_E_HIP;   // done_* = 0
     if (c->cfg.rdo) {
         ALLOC(b.cab, (size_t)c->nslice * JMR_NCTX);
         ALLOC(b.range, (size_t)c->nslice * sizeof(uint32_t));
@@ -411,10 +409,6 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     // (profiles/r7a_tick_cap_ab.txt): the longer ticks of the full pipeline win, so no cap by default.
     c->tick_cap = 0;
     if (const char *e = getenv("JMH_TICK_CAP")) c->tick_cap = atoi(e);
-    {   // the fused final (FFS, 8-bit, 4x4 transform, RDO off): A/B knob JMH_FUSED_FINAL
-        const char *e = getenv("JMH_FUSED_FINAL");
-        c->fused_final = e && atoi(e) != 0 && cfg->search_mode == 0 && c->bd == 8 && !cfg->transform_8x8_mode && !cfg->rdo;
-    }
     int st = JMH_OK;
 #define ALLOC(p, n) do { if (hipMalloc((void **)&(p), (n)) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
     {
@@ -597,8 +591,6 @@ static int issue_tick(jmh_ctx *c) {
     for (int i = 0; i < 8; i++) t.inter_search[i] = c->cfg.inter_search[i];
     t.prof = c->d_prof; t.prof_mb = c->prof_mb;
     t.me_in_analyse = c->cfg.search_mode == 0 && c->bd == 8;   // High 10 FFS: k_mb_me_full<uint16_t, true>
-    t.fused = c->fused_final && t.me_in_analyse;
-    t.seq = c->ticks_total + 1;                         // >= 1: MbScratch.done_* start at 0
     t.t8 = c->cfg.transform_8x8_mode;
     t.epzs_dual = c->cfg.epzs_dual_refinement;
     t.epzs_subpel = c->cfg.epzs_subpel_me; t.epzs_spts = c->cfg.epzs_subpel_thres_scale;
@@ -643,7 +635,7 @@ static int issue_tick(jmh_ctx *c) {
         // RDO: k_rdo_inter's blocks (role 4), then k_rdo_intra's (role 1)
         const int na = t.rdo ? xcd_grid(t.pre[nP]) + xcd_grid(t.pre[k])
                              : t.me_in_analyse ? xcd_grid(t.pre[nP]) + (t.pre[k] + 3) / 4 : xcd_grid(t.pre[nP]);
-        t.bprof_fin = t.fused ? c->d_bprof : c->d_bprof + 3 * na;   // fused: the final blocks follow in one grid
+        t.bprof_fin = c->d_bprof + 3 * na;
         HCHK(hipMemsetAsync(c->d_bprof, 0, ((size_t)3 * 3 * PMAX * c->mbh + 64) * sizeof(unsigned long long), c->st));
         c->bprof_blocks = na + xcd_grid(t.pre[k]);
     }
@@ -666,7 +658,7 @@ static int issue_tick(jmh_ctx *c) {
             if (side) { HCHK(hipEventRecord(c->ev_join, c->sst)); HCHK(hipStreamWaitEvent(c->st, c->ev_join, 0)); }
         }
         if (kt) { HCHK(ring_end(c->ring_an, c->st)); HCHK(ring_begin(c->ring_fin, c->st)); }
-        if (!t.rdo && !t.fused) HCHK(jmh_launch_final(t, c->st));
+        if (!t.rdo) HCHK(jmh_launch_final(t, c->st));
         if (kt) HCHK(ring_end(c->ring_fin, c->st));
         c->ticks_total++;
         c->timing.ticks++;
