@@ -164,10 +164,14 @@ typedef struct jmr_cand {
 /* the current macroblock's partial coding state inside the P8x8 RD loop (what cs_b8 carries of
    currMB: mvd, the coded_block_flag bits and the luma cbp of the decided 8x8 blocks) */
 typedef struct jmr_cur {
-    int16_t mvd[16][2];
-    uint16_t cbf_l;
-    uint16_t cbp;
-    uint8_t tc[24];       /* SymbolMode 0: the decided blocks' TotalCoeff (jmh_cavlc_rate.h)      */
+    union {               /* one entropy coder per slice */
+        struct {
+            int16_t mvd[16][2];
+            uint16_t cbf_l;
+            uint16_t cbp;
+        };
+        uint8_t tc[24];   /* SymbolMode 0: the decided blocks' TotalCoeff (jmh_cavlc_rate.h)      */
+    };
 } jmr_cur;
 
 /* coded_block_flag condTermFlagN (9.3.3.1.1.9) of luma 4x4 (x4, y4) of neighbour n (NULL: not

@@ -132,7 +132,7 @@ __device__ __forceinline__ void rdo_nb_load(const DevParams &d, int mbx, int mby
 // The 2x2 DC of a component reads its four blocks' DC lanes (wave-uniform).  Writes out (global)
 // except its distortion, returned (wave-uniform).
 template <class pel>
-__device__ __forceinline__ int chroma_cand_w(const DevParams &d, const pel (*orgc)[64], const IntraNb<pel> *nb, int cm, const int16_t (*fmv)[2],
+__device__ __forceinline__ int chroma_cand_w(const DevParams &d, const pel *oc0, const pel *oc1, int ostr, const IntraNb<pel> *nb, int cm, const int16_t (*fmv)[2],
                                              bool skipped, RdoChroma<pel> *out, int lane, int mbx, int mby, bool avT, bool avL) {
     const int maxv = d.maxv, Wc = d.Wc, pix_x = 16 * mbx, pix_y = 16 * mby;
     const int qpi = iclip(-d.qpbd, 51, d.qp + d.cqp_off), qpcy = qpi < 0 ? qpi : c_qpc[qpi], qpc = qpcy + d.qpbd;
@@ -154,7 +154,7 @@ __device__ __forceinline__ int chroma_cand_w(const DevParams &d, const pel (*org
             pv = ((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] + (8 - fx) * fy * R[y1 * Wc + x0] +
                   fx * fy * R[y1 * Wc + x1] + 32) >> 6;
         }
-        const int org = orgc[uv][cyo * 8 + cxo];
+        const int org = (uv ? oc1 : oc0)[cyo * ostr + cxo];
         int rv = pv, lev = 0, dcl = 0;
         if (!skipped) {
             const int c = lane_fwd4x4(org - pv, l);
@@ -220,7 +220,9 @@ template <class pel>
 struct RdoInterS {
     EpzS<pel> e;                  // the motion searches
     int16_t pmv[8][16][2];        // the MVP each search used (the candidates' mvds)
+#ifndef RDO_ORGC_GLOBAL
     alignas(4) pel orgc[2][64];
+#endif
     alignas(4) uint8_t st0[JMR_NCTX];      // the slice's coding state at the MB start
     alignas(4) uint8_t strun[JMR_NCTX];    // the P8x8 running state (decided 8x8 blocks)
     RdoP8Own<pel> own;
@@ -231,7 +233,8 @@ struct RdoInterS {
     alignas(4) pel p8pred[256], p8rec[256];   // the P8x8 candidate, assembled block by block
     int16_t p8lev[16][16];
     int16_t fmv[16][2];           // MVs of the candidate being coded
-    int bcost[16], bnz[16];
+    int16_t bcost[16];            // per 4x4: coefficient cost (saturated at 32767: MAX_VALUE for a level > 1), non-zero levels
+    uint8_t bnz[16];
 };
 
 // LumaResidualCoding [J] of an inter candidate (4x4 transform) on one wave, a row of 4x4 blocks per
@@ -253,7 +256,7 @@ __device__ __forceinline__ void luma_inter(const DevParams &d, RdoInterS<pel> &s
             int dq, cc;
             const unsigned nz = lane_quant(c, l, qp, rnd, false, lev[i], dq, cc);
             rv[i] = lane_inv4x4(dq, l, pr[i], maxv);
-            if (l == 0) { s.bcost[blk] = cc; s.bnz[blk] = nz != 0; }
+            if (l == 0) { s.bcost[blk] = (int16_t)min(cc, 32767); s.bnz[blk] = nz != 0; }   // saturated: only its sums are compared (with 4 and 5)
         }
     }
     int cbp = 0, cbp_blk = 0;
@@ -357,10 +360,12 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     // ---- inputs: the searches' window, chroma, the coding state, the neighbours' records
     const EWin<pel> wn = epzs_load_mb(d, s.e, mbx, mby, lane);
     jmr_lds_tables_load(lane, 64);
+#ifndef RDO_ORGC_GLOBAL
     for (int k = lane; k < 128; k += 64) {
         const int uv = k >> 6, q = k & 63;
         s.orgc[uv][q] = spl<pel>(uv ? d.orgV : d.orgU)[(8 * mby + (q >> 3)) * d.Wc + 8 * mbx + (q & 7)];
     }
+#endif
     int hasA = 0, hasB = 0;
     const uint32_t rg0 = rdo_state_load(d, a, s.st0, lane, 64);
     {
@@ -535,7 +540,14 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         if (c < 4 && lane < 4) L[c].b8mode[lane] = (int8_t)c;
         wave_lds_sync();
         if (c < 4) luma_inter(d, s, wn, &L[c], c == 0, mbx, mby, lane);
-        const int dist = chroma_cand_w<pel>(d, s.orgc, nullptr, 0, s.fmv, c == 0, &scr->C[c], lane, mbx, mby, mav.T, mav.L);
+#ifndef RDO_ORGC_GLOBAL
+        const pel *oc0 = s.orgc[0], *oc1 = s.orgc[1];
+        constexpr int ostr = 8;
+#else   // A/B: the MB's chroma source from the picture (256 B less LDS)
+        const int ostr = d.Wc;
+        const pel *oc0 = spl<pel>(d.orgU) + 8 * mby * ostr + 8 * mbx, *oc1 = spl<pel>(d.orgV) + 8 * mby * ostr + 8 * mbx;
+#endif
+        const int dist = chroma_cand_w<pel>(d, oc0, oc1, ostr, nullptr, 0, s.fmv, c == 0, &scr->C[c], lane, mbx, mby, mav.T, mav.L);
         if (lane == 0) scr->C[c].dist = dist;
         wave_lds_sync();
     }
@@ -781,7 +793,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
     for (int m = 0; m < 4; m++) {
         const bool act = m == 0 || (m == 1 ? avL : m == 2 ? avT : avT && avL && avTL);
         if (!act) continue;                             // uniform
-        const int dist = chroma_cand_w<pel>(d, s.nb.orgc, &s.nb, m, nullptr, false, &scr->C[5 + m], lane, mbx, mby, avT, avL);
+        const int dist = chroma_cand_w<pel>(d, s.nb.orgc[0], s.nb.orgc[1], 8, &s.nb, m, nullptr, false, &scr->C[5 + m], lane, mbx, mby, avT, avL);
         if (lane == 0) scr->C[5 + m].dist = dist;
     }
     // ---- Intra4x4: Mode_Decision_for_4x4IntraBlocks [J] by RDCost_for_4x4IntraBlocks, 16 blocks in

@@ -183,6 +183,36 @@ def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
             assert np.array_equal(x, y)
 
 
+def test_rdo_slot_chain_varying_qp():
+    """an encode_slot chain with RDO on, a different QP (so different lambdas) per
+    picture and more pictures than the context's ring (depth + 2 entries): every picture's lambdas
+    are staged through its ring entry's pinned buffer while earlier pictures are still in flight.
+    Pipelined == one picture at a time, checked through the reference the chain leaves for a
+    final read-back picture, for CABAC and CAVLC rates."""
+    w, h = 352, 96
+    pics = moving_seq(w, h, 4, seed=7, step=(-9, 5))
+    qps = [22, 34, 27, 40, 25]
+    for symbol_mode in (1, 0):
+        res = []
+        for depth in (0, 1):
+            e = jmhip.Encoder(w, h, search_range=16, slots=3, pipeline_depth=depth, slice_mbs=22,
+                              **dict(RDO, symbol_mode=symbol_mode))
+            if depth == 0:
+                assert e.depth > 1
+            for i in range(3):
+                e.load_frame(i, *pics[i])
+            e.encode_slot(0, jmhip.JMH_I_SLICE, 26, deblock=(0, 0, 0))
+            for k in range(13):
+                e.set_reference_slot(-2)
+                e.encode_slot(1 + k % 2, jmhip.JMH_P_SLICE, qps[k % len(qps)], deblock=(0, 0, 0))
+            e.set_reference_slot(-2)
+            res.append(e.encode(*pics[3], jmhip.JMH_P_SLICE, 30, deblock=(0, 0, 0)) + (e.deblocked(),))
+        (gres, grec, gd), (ores, orec, od) = res
+        assert_same(gres, grec, ores, orec, w // 16)
+        for x, y in zip(gd, od):
+            assert np.array_equal(x, y)
+
+
 @pytest.mark.parametrize("extra", [
     ["InputFile=synthetic:71", "FramesToBeEncoded=5", "SourceWidth=176", "SourceHeight=144", "SearchRange=16",
      "ProfileIDC=77"],
