@@ -220,9 +220,6 @@ template <class pel>
 struct RdoInterS {
     EpzS<pel> e;                  // the motion searches
     int16_t pmv[8][16][2];        // the MVP each search used (the candidates' mvds)
-#ifndef RDO_ORGC_GLOBAL
-    alignas(4) pel orgc[2][64];
-#endif
     alignas(4) uint8_t st0[JMR_NCTX];      // the slice's coding state at the MB start
     alignas(4) uint8_t strun[JMR_NCTX];    // the P8x8 running state (decided 8x8 blocks)
     RdoP8Own<pel> own;
@@ -360,12 +357,6 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     // ---- inputs: the searches' window, chroma, the coding state, the neighbours' records
     const EWin<pel> wn = epzs_load_mb(d, s.e, mbx, mby, lane);
     jmr_lds_tables_load(lane, 64);
-#ifndef RDO_ORGC_GLOBAL
-    for (int k = lane; k < 128; k += 64) {
-        const int uv = k >> 6, q = k & 63;
-        s.orgc[uv][q] = spl<pel>(uv ? d.orgV : d.orgU)[(8 * mby + (q >> 3)) * d.Wc + 8 * mbx + (q & 7)];
-    }
-#endif
     int hasA = 0, hasB = 0;
     const uint32_t rg0 = rdo_state_load(d, a, s.st0, lane, 64);
     {
@@ -540,13 +531,11 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         if (c < 4 && lane < 4) L[c].b8mode[lane] = (int8_t)c;
         wave_lds_sync();
         if (c < 4) luma_inter(d, s, wn, &L[c], c == 0, mbx, mby, lane);
-#ifndef RDO_ORGC_GLOBAL
-        const pel *oc0 = s.orgc[0], *oc1 = s.orgc[1];
-        constexpr int ostr = 8;
-#else   // A/B: the MB's chroma source from the picture (256 B less LDS)
+        // the MB's chroma source straight from the picture (each sample read once per candidate):
+        // its LDS copy would keep k_rdo_inter<u16> at six MBs per CU instead of seven
+        // (profiles/r7n_rdo_lds_ab.txt)
         const int ostr = d.Wc;
         const pel *oc0 = spl<pel>(d.orgU) + 8 * mby * ostr + 8 * mbx, *oc1 = spl<pel>(d.orgV) + 8 * mby * ostr + 8 * mbx;
-#endif
         const int dist = chroma_cand_w<pel>(d, oc0, oc1, ostr, nullptr, 0, s.fmv, c == 0, &scr->C[c], lane, mbx, mby, mav.T, mav.L);
         if (lane == 0) scr->C[c].dist = dist;
         wave_lds_sync();
