@@ -531,9 +531,8 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         if (c < 4 && lane < 4) L[c].b8mode[lane] = (int8_t)c;
         wave_lds_sync();
         if (c < 4) luma_inter(d, s, wn, &L[c], c == 0, mbx, mby, lane);
-        // the MB's chroma source straight from the picture (each sample read once per candidate):
-        // its LDS copy would keep k_rdo_inter<u16> at six MBs per CU instead of seven
-        // (profiles/r7n_rdo_lds_ab.txt)
+        // the MB's chroma source straight from the picture (each sample read once per candidate;
+        // 128-256 B less LDS, profiles/r7n_rdo_lds_ab.txt)
         const int ostr = d.Wc;
         const pel *oc0 = spl<pel>(d.orgU) + 8 * mby * ostr + 8 * mbx, *oc1 = spl<pel>(d.orgV) + 8 * mby * ostr + 8 * mbx;
         const int dist = chroma_cand_w<pel>(d, oc0, oc1, ostr, nullptr, 0, s.fmv, c == 0, &scr->C[c], lane, mbx, mby, mav.T, mav.L);
