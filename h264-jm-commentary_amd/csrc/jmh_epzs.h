@@ -594,8 +594,8 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
                 qy += step * (m == 0 ? -1 : m == 3 ? 1 : 0);
             }
         }
-    } else if constexpr (NSUB <= 4) {
-        // blocks of up to four 4x4: the SATD of every position of the 7x7 quarter-pel grid around
+    } else if constexpr (NSUB <= 2) {
+        // blocks of one or two 4x4: the SATD of every position of the 7x7 quarter-pel grid around
         // the full-pel MV in one batch (lane task = (position, 4x4 sub-block)), then the half-pel
         // pass over the 9 even positions and the quarter-pel pass around its winner on the costs
         constexpr int NIT = (49 * NSUB + NTE - 1) / NTE;
@@ -645,15 +645,20 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
             qx += sp9x(kb & 15); qy += sp9y(kb & 15);
         }
     } else {
-        // larger blocks: half pass, then the quarter pass around its winner (9 x NSUB tasks each)
+        // 8x8 and larger blocks: the half pass, then the quarter pass around its winner; a pass's
+        // tasks are (candidate min_pos..8) x NSUB sub-blocks, NSUB consecutive lanes per candidate,
+        // so the quarter pass (8 candidates) is one round for 8x8, 16x8 and 8x16, two for 16x16
+        // (8x8 in the 7x7 batch above took four)
 #pragma unroll
         for (int pass = 0; pass < 2; pass++) {
             const int step = pass == 0 ? 2 : 1, min_pos = pass == 0 ? (had ? 0 : 1) : 1;
+            const int ntask = (9 - min_pos) << LNS;
             unsigned kb = 0xFFFFFFFFu;
 #pragma unroll
             for (int t0 = 0; t0 < (9 << LNS); t0 += NTE) {
-                const int task = t0 + lane, c = task >> LNS, sub = task & (NSUB - 1);
-                const bool val = c < 9 && c >= min_pos;
+                if (t0 >= ntask) break;                    // wave-uniform
+                const int task = t0 + lane, c = min_pos + (task >> LNS), sub = task & (NSUB - 1);
+                const bool val = c < 9;
                 const int ox = qx + step * sp9x(c), oy = qy + step * sp9y(c);
                 int sat = 0;
                 if (val) {
@@ -662,7 +667,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
                 }
                 sat += dpp<0xB1>(sat);
                 sat += dpp<0x4E>(sat);
-                sat += dpp<0x141>(sat);
+                if constexpr (NSUB >= 8) sat += dpp<0x141>(sat);
                 if constexpr (NSUB >= 16) sat += dpp<0x140>(sat);
                 if (val && sub == 0) {
                     int cost = sat + wcost(d, mvbits(4 * fmx + ox - pmx) + mvbits(4 * fmy + oy - pmy));
