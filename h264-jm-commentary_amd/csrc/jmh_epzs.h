@@ -530,58 +530,21 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
         gb = s.gn + GNY * GNS + GNX; gs = GNS;
     }
     auto G = [&](int x, int y) { return (int)gb[y * gs + x]; };
-    // four outputs per lane task from nine loaded samples: the horizontal taps (b1, b) over runs of
-    // four columns, the vertical ones (h) over runs of four rows, then j from b1 the same way
-    // (2.4x fewer LDS reads and half the passes of one output per task).  Runs past PW / PH read
-    // at most 3 columns / rows beyond the original reach (inside the window margin or the GN*
-    // neighbourhood) and store nothing.
-    constexpr int NCG = (PW + 3) / 4, NRG = (PH + 3) / 4;
-#pragma unroll
-    for (int i0 = 0; i0 < (PH + 5) * NCG; i0 += NTE) {   // b1 rows -3 .. PH + 1, b rows -1 .. PH - 2
-        const int i = i0 + lane;
-        if (i < (PH + 5) * NCG) {
-            const int rr = i / NCG, x0 = 4 * (i - rr * NCG), gy = rr - 3;
-            int g[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++) g[k] = G(x0 - 3 + k, gy);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int x = x0 + q, h1 = tap6(g[q], g[q + 1], g[q + 2], g[q + 3], g[q + 4], g[q + 5]);
-                if (x < PW) {
-                    s.b1[rr][x] = (typename EpzTap<pel>::type)h1;
-                    if (rr >= 2 && rr < PH + 2) s.hp[0][(rr - 2) * HPS + x] = (pel)clipmx((h1 + 16) >> 5, d.maxv);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int i0 = 0; i0 < PW * NRG; i0 += NTE) {         // h rows -1 .. PH - 2
-        const int i = i0 + lane;
-        if (i < PW * NRG) {
-            const int rg = i / PW, x = i - rg * PW, gx = x - 1, r0 = 4 * rg;
-            int g[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++) g[k] = G(gx, r0 - 3 + k);
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (r0 + q < PH)
-                    s.hp[1][(r0 + q) * HPS + x] = (pel)clipmx((tap6(g[q], g[q + 1], g[q + 2], g[q + 3], g[q + 4], g[q + 5]) + 16) >> 5, d.maxv);
+    for (int i = lane; i < PW * (PH + 5); i += NTE) {
+        const int rr = i / PW, x = i - rr * PW, gx = x - 1, gy = rr - 3;
+        const int h1 = tap6(G(gx - 2, gy), G(gx - 1, gy), G(gx, gy), G(gx + 1, gy), G(gx + 2, gy), G(gx + 3, gy));
+        s.b1[rr][x] = (typename EpzTap<pel>::type)h1;
+        if (rr >= 2 && rr < PH + 2) {
+            s.hp[0][(rr - 2) * HPS + x] = (pel)clipmx((h1 + 16) >> 5, d.maxv);
+            s.hp[1][(rr - 2) * HPS + x] =
+                (pel)clipmx((tap6(G(gx, gy - 2), G(gx, gy - 1), G(gx, gy), G(gx, gy + 1), G(gx, gy + 2), G(gx, gy + 3)) + 16) >> 5, d.maxv);
         }
     }
     wave_lds_sync();
-#pragma unroll
-    for (int i0 = 0; i0 < PW * NRG; i0 += NTE) {         // j from the b1 column
-        const int i = i0 + lane;
-        if (i < PW * NRG) {
-            const int rg = i / PW, x = i - rg * PW, r0 = 4 * rg;
-            int v[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++) v[k] = s.b1[min(r0 + k, PH + 4)][x];
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (r0 + q < PH)
-                    s.hp[2][(r0 + q) * HPS + x] = (pel)clipmx((tap6(v[q], v[q + 1], v[q + 2], v[q + 3], v[q + 4], v[q + 5]) + 512) >> 10, d.maxv);
-        }
+    for (int i = lane; i < PW * PH; i += NTE) {
+        const int y = i / PW, x = i - y * PW;
+        s.hp[2][y * HPS + x] =
+            (pel)clipmx((tap6(s.b1[y][x], s.b1[y + 1][x], s.b1[y + 2][x], s.b1[y + 3][x], s.b1[y + 4][x], s.b1[y + 5][x]) + 512) >> 10, d.maxv);
     }
     wave_lds_sync();
     SSTAMP(4);
