@@ -241,7 +241,11 @@ def read_pmc_traffic(config, search_mode, t8=None, slice_mbs=None):
         return None, None
     try:
         with open(p) as f:
-            j = json.load(f)["configs"][key]
+            confs = json.load(f)["configs"]
+        # a separate pass per Transform8x8Mode where one exists ("5t8": config 5 with 8x8 transform)
+        if t8 and key + "t8" in confs:
+            key += "t8"
+        j = confs[key]
         # only the configuration the pass measured (Transform8x8Mode, slices)
         if ("t8" in j and t8 is not None and j["t8"] != t8) or \
            ("slice_mbs" in j and slice_mbs is not None and j["slice_mbs"] != slice_mbs):

@@ -22,7 +22,7 @@
 #   prof    rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG/
 #   profc3  the same for config 3
 #   pmc     tools/pmc_traffic.sh (HBM bytes + SQ counters, separate passes), config 2
-#   pmc3 / pmc5  the same for config 3 / config 5 (RDO on)
+#   pmc3 / pmc5  the same for config 3 / config 5 (RDO on); pmc5t8 config 5 with Transform8x8Mode 1
 #   lencod  the product lencod end to end on an I420 file (tools/make_yuv.py), 1080p, 60 pictures
 #           (FFS SR 32), WriterThreads 0 / 4 / 8 -> gpurun_out/TAG_lencod1080_w*.log
 #   lencodc3 the same for the config-3 shape (2160p High, EPZS + 8x8), 30 pictures, 8 writers
@@ -83,6 +83,9 @@ for s in "$@"; do
     profc5) run profc5 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c5" -o ${TAG}_c5 --output-format csv -- \
                 python3 "$R/bench.py" --config 5 --steps 60 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc5.log 2>&1 || exit $?
             find gpurun_out/prof_${TAG}_c5 -name "*kernel_stats*" -exec cat {} \; ;;
+    profc5t8) run profc5t8 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c5t8" -o ${TAG}_c5t8 --output-format csv -- \
+                python3 "$R/bench.py" --config 5 --t8 1 --steps 60 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc5t8.log 2>&1 || exit $?
+            find gpurun_out/prof_${TAG}_c5t8 -name "*kernel_stats*" -exec cat {} \; ;;
     profc3) run profc3 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_c3" -o ${TAG}_c3 --output-format csv -- \
                 python3 "$R/bench.py" --config 3 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_profc3.log 2>&1 || exit $?
             find gpurun_out/prof_${TAG}_c3 -name "*kernel_stats*" -exec cat {} \; ;;
@@ -110,6 +113,7 @@ for s in "$@"; do
     pmc)    run pmc 900 bash tools/pmc_traffic.sh "$TAG" || exit $? ;;
     pmc3)   run pmc3 900 bash tools/pmc_traffic.sh "${TAG}_c3" 30 3 || exit $? ;;
     pmc5)   run pmc5 900 bash tools/pmc_traffic.sh "${TAG}_c5" 30 5 || exit $? ;;
+    pmc5t8) run pmc5t8 900 bash tools/pmc_traffic.sh "${TAG}_c5t8" 30 5 "--t8 1" || exit $? ;;
     *)      echo "unknown step $s"; exit 2 ;;
   esac
 done
