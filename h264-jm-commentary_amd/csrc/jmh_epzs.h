@@ -21,6 +21,9 @@ __device__ __forceinline__ int wcost(const DevParams &d, int bits) {
 #ifndef EPZS_NB16
 #define EPZS_NB16 16
 #endif
+#ifndef EPZS_FB_ROWS
+#define EPZS_FB_ROWS 4                        // k_rdo_inter: block rows per batch of global loads when a SAD
+#endif                                        //   leaves the window (k_mb_epzs: 1; A/B profiles/r7x_fallback_ab.txt)
 #ifndef EOFF_L16
 #define EOFF_L16 40                           // ... for 16-bit samples: 30.4 KB k_rdo_inter, five MBs per CU (A/B: profiles/r5r_window_ab.txt)
 #endif
@@ -202,9 +205,10 @@ __device__ __forceinline__ void epzs_pat(bool sd, int e, int &px, int &py) {
 // SAD of the whole block (4 w4 x 4 h4 at 4x4 position bx4, by4) at full-pel displacement (x, y)
 // on this lane: per row w4 + 1 aligned dwords, v_alignbyte, v_sad_u8 (16-bit samples: 2 w4 + 1
 // dwords, v_sad_u16)
-template <int LW4, int LH4, class pel>
+template <int LW4, int LH4, class pel, int FBR = 1>
 __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWin<pel> &wn, int bx4, int by4, int x, int y) {
     constexpr int W4 = 1 << LW4, H = 4 << LH4;
+    static_assert(H % FBR == 0, "fallback row batches must tile the block");
     const int gx = wn.mx + 4 * bx4 + x, gy = wn.my + 4 * by4 + y;
     const uint32_t *org = reinterpret_cast<const uint32_t *>(s.org + (4 * by4) * 16 + 4 * bx4);
     uint32_t sad = 0;
@@ -222,13 +226,19 @@ __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWi
 #pragma unroll
                 for (int q = 0; q < ND; q++) sad = __builtin_amdgcn_sad_u16(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), org[r * 8 + q], sad);
             }
-        } else {
+        } else {   // outside: the reference picture in global memory, clamped, FBR rows per round trip
             const int px = wn.wx0 + gx, py = wn.wy0 + gy;
 #pragma unroll 1
-            for (int r = 0; r < H; r++) {
+            for (int r0 = 0; r0 < H; r0 += FBR) {
+                uint32_t v[FBR][ND];
 #pragma unroll
-                for (int q = 0; q < ND; q++)
-                    sad = __builtin_amdgcn_sad_u16(gref(wn, px + 2 * q, py + r) | gref(wn, px + 2 * q + 1, py + r) << 16, org[r * 8 + q], sad);
+                for (int r = 0; r < FBR; r++)
+#pragma unroll
+                    for (int q = 0; q < ND; q++) v[r][q] = gref(wn, px + 2 * q, py + r0 + r) | gref(wn, px + 2 * q + 1, py + r0 + r) << 16;
+#pragma unroll
+                for (int r = 0; r < FBR; r++)
+#pragma unroll
+                    for (int q = 0; q < ND; q++) sad = __builtin_amdgcn_sad_u16(v[r][q], org[(r0 + r) * 8 + q], sad);
             }
         }
         return sad;
@@ -245,17 +255,23 @@ __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWi
 #pragma unroll
             for (int q = 0; q < W4; q++) sad = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), org[r * 4 + q], sad);
         }
-    } else {   // outside: the reference picture in global memory, clamped (rare: far predictors)
+    } else {   // outside: the reference picture in global memory, clamped (far predictors), as above
         const int px = wn.wx0 + gx, py = wn.wy0 + gy;
 #pragma unroll 1
-        for (int r = 0; r < H; r++) {
+        for (int r0 = 0; r0 < H; r0 += FBR) {
+            uint32_t v[FBR][W4];
 #pragma unroll
-            for (int q = 0; q < W4; q++) {
-                uint32_t v = 0;
+            for (int r = 0; r < FBR; r++)
 #pragma unroll
-                for (int b = 0; b < 4; b++) v |= gref(wn, px + 4 * q + b, py + r) << (8 * b);
-                sad = __builtin_amdgcn_sad_u8(v, org[r * 4 + q], sad);
-            }
+                for (int q = 0; q < W4; q++) {
+                    v[r][q] = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++) v[r][q] |= gref(wn, px + 4 * q + b, py + r0 + r) << (8 * b);
+                }
+#pragma unroll
+            for (int r = 0; r < FBR; r++)
+#pragma unroll
+                for (int q = 0; q < W4; q++) sad = __builtin_amdgcn_sad_u8(v[r][q], org[(r0 + r) * 4 + q], sad);
         }
     }
     return sad;
@@ -365,7 +381,7 @@ __device__ __forceinline__ int had_packed(const e16x2 (&r)[4][2]) {
 
 // BlockMotionSearch [J] of one block on the wave: EPZS full pel + SubPelBlockMotionSearch;
 // pmvo (k_rdo_inter; null in k_mb_epzs): receives the MVP each search used (the RD rate's mvd)
-template <int BT, class pel>
+template <int BT, class pel, int FBR = 1>
 __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, const EWin<pel> &wn, int bx4, int by4, int mc, int b8, int best8x8, bool prof,
                                            int16_t (*pmvo)[16][2] = nullptr) {
     // debug (JMH_PHASE_PROF): steps of the MB's first 4x4 search into prof[41..46], of its 16x16
@@ -432,7 +448,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
 #pragma unroll 1
         for (int p = lane; p < npos; p += NTE) {
             const int dy = p / side - range, dx = p - (dy + range) * side - range, x = ccx + dx, y = ccy + dy;
-            const int c = (int)lane_block_sad<LW4, LH4>(s, wn, bx4, by4, x, y) + wcost(d, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+            const int c = (int)lane_block_sad<LW4, LH4, pel, FBR>(s, wn, bx4, by4, x, y) + wcost(d, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
             kb = min(kb, ((unsigned)c << 13) | (unsigned)spiral_index(dx, dy));
         }
         kb = wave_min_u32(kb);
@@ -445,7 +461,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
     int cx, cy;
     const bool cv = epzs_cand(d, s, lane, BT, bx4, by4, nb, range, mvx0, mvy0, cx, cy);
     if (!cv) { cx = mvx0; cy = mvy0; }   // any valid position for the SAD (key discarded)
-    const int c0 = (int)lane_block_sad<LW4, LH4>(s, wn, bx4, by4, cx, cy) +
+    const int c0 = (int)lane_block_sad<LW4, LH4, pel, FBR>(s, wn, bx4, by4, cx, cy) +
                    wcost(d, mvbits(4 * cx - pmx) + mvbits(4 * cy - pmy));
     const int cost0 = __builtin_amdgcn_readfirstlane(c0);   // predictor 0: the centre, always valid
     SSTAMP(2);
@@ -469,7 +485,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
                     const int x = rbx + ddx, y = rby + ddy;
                     const bool inw = lane < 41 && abs(x - mvx0) <= range && abs(y - mvy0) <= range;
                     int c = 0;
-                    if (inw) c = (int)lane_block_sad<LW4, LH4>(s, wn, bx4, by4, x, y) + wcost(d, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
+                    if (inw) c = (int)lane_block_sad<LW4, LH4, pel, FBR>(s, wn, bx4, by4, x, y) + wcost(d, mvbits(4 * x - pmx) + mvbits(4 * y - pmy));
                     for (int k = 0; k < steps; k++) {
                         const int rx = x - rbx, ry = y - rby;   // this lane's position relative to the current best
                         int e = 15;
@@ -522,9 +538,18 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
     if (gx0 - GNX >= 0 && gx0 + PW + GNX <= EGeo<pel>::ew && gy0 - GNY >= 0 && gy0 + PH + GNY <= EGeo<pel>::ew) {   // wave-uniform
         gb = s.g + gy0 * EGeo<pel>::ew + gx0; gs = EGeo<pel>::ew;
     } else {
-        for (int i = lane; i < (PH + 2 * GNY) * GNS; i += NTE) {
-            const int y = i / GNS, x = i - y * GNS;
-            s.gn[i] = (pel)gref(wn, wn.wx0 + gx0 + x - GNX, wn.wy0 + gy0 + y - GNY);
+        constexpr int NGN = (PH + 2 * GNY) * GNS;
+#pragma unroll 1
+        for (int i0 = 0; i0 < NGN; i0 += FBR * NTE) {   // FBR loads per lane in flight
+            pel v[FBR];
+#pragma unroll
+            for (int k = 0; k < FBR; k++) {
+                const int i = min(i0 + k * NTE + lane, NGN - 1), y = i / GNS, x = i - y * GNS;
+                v[k] = (pel)gref(wn, wn.wx0 + gx0 + x - GNX, wn.wy0 + gy0 + y - GNY);
+            }
+#pragma unroll
+            for (int k = 0; k < FBR; k++)
+                if (i0 + k * NTE + lane < NGN) s.gn[i0 + k * NTE + lane] = v[k];
         }
         wave_lds_sync();
         gb = s.gn + GNY * GNS + GNX; gs = GNS;

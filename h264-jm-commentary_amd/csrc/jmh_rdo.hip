@@ -371,11 +371,11 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     PSTAMP(41);
     const jmr_mbinfo *A = hasA ? &s.nbA : nullptr, *B = hasB ? &s.nbB : nullptr;
     // ---- motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch [J])
-    epzs_block<1>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
-    epzs_block<2>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
-    epzs_block<2>(d, s.e, wn, 0, 2, 1, 0, 0, false, s.pmv);
-    epzs_block<3>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
-    epzs_block<3>(d, s.e, wn, 2, 0, 1, 0, 0, false, s.pmv);
+    epzs_block<1, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
+    epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
+    epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 2, 1, 0, 0, false, s.pmv);
+    epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
+    epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 2, 0, 1, 0, 0, false, s.pmv);
     PSTAMP(42);
     const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
     for (int i = lane; i < JMR_NCTX / 4; i += 64) reinterpret_cast<uint32_t *>(s.strun)[i] = reinterpret_cast<const uint32_t *>(s.st0)[i];
@@ -390,15 +390,15 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
 #pragma unroll 1
     for (int b8 = 0; b8 < 4 && p8; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        epzs_block<4>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<5>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<5>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv);
-        epzs_block<6>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<6>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<7>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<7>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<7>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv);
-        epzs_block<7>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false, s.pmv);
+        epzs_block<4, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv);
+        epzs_block<6, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<6, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false, s.pmv);
         PSTAMP(43 + 2 * b8);
         const int bx4 = X + (b4 & 1), by4 = Y + (b4 >> 1), k = by4 * 4 + bx4;
         const int px = 4 * bx4 + (l & 3), py = 4 * by4 + (l >> 2), q8 = (4 * (b4 >> 1) + (l >> 2)) * 8 + 4 * (b4 & 1) + (l & 3);
@@ -938,8 +938,11 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
     PSTAMP(61);
 }
 
+#ifndef JMH_RDO_INTER_WPE
+#define JMH_RDO_INTER_WPE 1                   // waves per SIMD the register budget must allow (2: five per CU
+#endif                                        //   at 16 bits, 32 B of scratch, 10 % slower: profiles/r7x_fallback_ab.txt)
 template <class pel, bool T8>
-__global__ __launch_bounds__(NTE) void k_rdo_inter(const TickArgs t) {
+__global__ __launch_bounds__(NTE, JMH_RDO_INTER_WPE) void k_rdo_inter(const TickArgs t) {
     __shared__ RdoInterS<pel> s;
     const int nP = t.pre[t.nP], m = xcd_block(blockIdx.x, nP);
     if (m >= nP) return;                                // padding block (whole workgroup)
