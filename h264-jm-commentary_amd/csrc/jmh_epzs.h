@@ -24,6 +24,10 @@ __device__ __forceinline__ int wcost(const DevParams &d, int bits) {
 #ifndef EPZS_FB_ROWS
 #define EPZS_FB_ROWS 4                        // k_rdo_inter: block rows per batch of global loads when a SAD
 #endif                                        //   leaves the window (k_mb_epzs: 1; A/B profiles/r7x_fallback_ab.txt)
+#ifndef EPZS_EDGE
+#define EPZS_EDGE 0                           // samples a window SAD needs right of its block: none -- the extra
+#endif                                        //   dword a row reads for v_alignbyte only feeds unused bytes, and
+                                              //   past the window's last row it stays inside EpzS (gn follows g)
 #ifndef EOFF_L16
 #define EOFF_L16 40                           // ... for 16-bit samples: 30.4 KB k_rdo_inter, five MBs per CU (A/B: profiles/r5r_window_ab.txt)
 #endif
@@ -214,7 +218,7 @@ __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWi
     uint32_t sad = 0;
     if constexpr (sizeof(pel) == 2) {
         constexpr int ND = 2 * W4;            // dwords of a block row
-        if (gx >= 0 && gx + 4 * W4 + 4 <= EGeo<pel>::ew && gy >= 0 && gy + H <= EGeo<pel>::ew) {
+        if (gx >= 0 && gx + 4 * W4 + EPZS_EDGE <= EGeo<pel>::ew && gy >= 0 && gy + H <= EGeo<pel>::ew) {
             const int a = gy * EGeo<pel>::ew + gx;
             const uint32_t sel = (uint32_t)(a & 1) * 2;
             const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~1));
@@ -243,7 +247,7 @@ __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWi
         }
         return sad;
     }
-    if (gx >= 0 && gx + 4 * W4 + 4 <= EGeo<pel>::ew && gy >= 0 && gy + H <= EGeo<pel>::ew) {   // inside the window
+    if (gx >= 0 && gx + 4 * W4 + EPZS_EDGE <= EGeo<pel>::ew && gy >= 0 && gy + H <= EGeo<pel>::ew) {   // inside the window
         const int a = gy * EGeo<pel>::ew + gx;
         const uint32_t sel = (uint32_t)(a & 3);
         const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~3));
