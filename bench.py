@@ -48,19 +48,24 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "h264-jm-commentary_amd")
 
-METRIC = "ME+transform megapixels/sec @1080p FullSearch SR=32; bit-exact vs the in-repo JM restatement (oracle)"
+# `value` times the device-resident path: inputs already in HBM, no H2D / D2H inside the timed
+# region.  SURVEY §8d's submit-to-host-visible timer (incl. PCIe) is host_path.pcie_inclusive_mp_s.
+TIMER = "device-resident (inputs in HBM, no H2D/D2H in the timed region)"
+METRIC = ("ME+transform megapixels/sec @1080p FullSearch SR=32; bit-exact vs the in-repo JM restatement (oracle); "
+          + TIMER)
 # BASELINE.json configs measured here: 2 (the headline) and 3 (variant)
 CONFIGS = {
     2: dict(metric=METRIC, disp=(1920, 1080), coded=(1920, 1088), search_mode=0, t8=0,
             workload="1080p synthetic YUV420 (coded 1920x1088), Baseline, {sm} SearchRange=32, RestrictSearchRange=2, "
                      "UseHadamard=1, 7 inter block sizes, RDO off, QP 28, IDR + {nf}-picture P sequence cycled "
                      "(one independent stream per GPU)"),
-    3: dict(metric="ME+transform megapixels/sec @2160p High EPZS SR=32 + 8x8 transform (config 3)", disp=(3840, 2160),
+    3: dict(metric="ME+transform megapixels/sec @2160p High EPZS SR=32 + 8x8 transform (config 3); " + TIMER, disp=(3840, 2160),
             coded=(3840, 2160), search_mode=3, t8=1,
             workload="2160p synthetic YUV420, High profile (ProfileIDC 100), EPZS SearchMode=3 SearchRange=32, "
                      "Transform8x8Mode=1 (Intra8x8 + TransformDecision), UseHadamard=1, 7 inter block sizes, RDO off, "
                      "QP 28, IDR + {nf}-picture P sequence cycled (one independent stream per GPU)"),
-    5: dict(metric="ME+transform+RD megapixels/sec @2160p High10 10-bit EPZS SR=32, CABAC RDO on, 240-MB slices (config 5)",
+    5: dict(metric="ME+transform+RD megapixels/sec @2160p High10 10-bit EPZS SR=32, CABAC RDO on, 240-MB slices (config 5); "
+                   + TIMER,
             disp=(3840, 2160), coded=(3840, 2160), search_mode=3, t8=0, bd=10, slice_mbs=240, rdo=1,
             workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), EPZS SearchMode=3 "
                      "SearchRange=32, UseHadamard=1, 7 inter block sizes, RDOptimization=1 with SymbolMode=1 (the CABAC "
@@ -69,7 +74,7 @@ CONFIGS = {
 }
 # --config 5 --rdo 0: the RDO-off variant of config 5's shape (EPZS + 8x8 transform)
 CONFIG5_RDO_OFF = dict(metric="ME+transform megapixels/sec @2160p High10 10-bit EPZS SR=32 + 8x8 transform, 240-MB slices, "
-                              "RDO off (config 5 variant)", t8=1, rdo=0,
+                              "RDO off (config 5 variant); " + TIMER, t8=1, rdo=0,
                        workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), EPZS SearchMode=3 "
                                 "SearchRange=32, Transform8x8Mode=1, UseHadamard=1, 7 inter block sizes, RDO off, QP 28, "
                                 "IDR + {nf}-picture P sequence cycled (one independent stream per GPU)")
@@ -132,6 +137,22 @@ VALU_SAD_MEASURED_TADS = 152.90
 def sad_peak():
     """(T AD/s, source) of v_sad_u8 on this chip (measured, tools/sad_peak.hip)."""
     return VALU_SAD_MEASURED_TADS, "measured: v_sad_u8 62.2 lane-ops/CU/clk (tools/sad_peak.hip, profiles/r2_sad_peak.json), at 2.4 GHz"
+
+
+# VALU issue peak: a wave64 vector instruction issues over 2 cycles on a SIMD-32 (MI355X guide,
+# "A wave (64 lanes) ... issues each VALU instruction over 2 cycles"), 4 SIMDs x 256 CUs at 2.4 GHz
+VALU_ISSUE_PEAK_TWIS = 256 * 4 * 2.4e9 / 2 / 1e12      # 1.2288 T wave-instructions/s
+
+
+def exit_status(verified, complete):
+    """(exit code, stderr message) of a finished run: 3 when the GPU results differ from the oracle
+    (`verified` False), 4 when a rank completed a different number of pictures than --steps in the
+    timed region (`complete` False: the timing, not the results, is off), else 0."""
+    if verified is False:
+        return 3, "bench.py: GPU results differ from the oracle"
+    if not complete:
+        return 4, "bench.py: a rank completed a different number of pictures than --steps in the timed region"
+    return 0, None
 
 
 # ------------------------------------------------------------------------------------------
@@ -231,8 +252,9 @@ def verify_against_oracle(jm, dump, search_mode, t8, device):
 
 
 def read_pmc_traffic(config, search_mode, t8=None, slice_mbs=None):
-    """(HBM bytes per macroblock of the roofline's kernels, source description) from the rocprofv3
-    PMC passes of tools/pmc_traffic.sh for this config, or (None, None).  The latest pass per
+    """(the pass's record: hbm_bytes_per_mb and, where counted, valu_insts_per_mb of the roofline's
+    kernels; source description) from the rocprofv3 PMC passes of tools/pmc_traffic.sh for this
+    config, or (None, None).  The latest pass per
     config is kept in tools/pmc_traffic.json (it travels to the GPU box, unlike profiles/); it is
     a committed measurement of an earlier run of the same kernels, not of this run."""
     p = os.path.join(ROOT, "tools", "pmc_traffic.json")
@@ -252,7 +274,7 @@ def read_pmc_traffic(config, search_mode, t8=None, slice_mbs=None):
             return None, None
         src = (f"tools/pmc_traffic.json config {key}: {j['kernel']} ({j.get('source', 'rocprofv3 PMC')}; "
                f"{j.get('calibration', 'uncalibrated')})")
-        return j["hbm_bytes_per_mb"], src
+        return j, src
     except (OSError, ValueError, KeyError, TypeError):
         return None, None
 
@@ -452,7 +474,9 @@ def main():
     ad_per_launch = AD_PER_FRAME / NMB * mbs_per_launch
     achieved_tads = ad_per_launch / (an_launch_ms * 1e-3) / 1e12
     peak_tads, peak_src = sad_peak()
-    pmc, pmc_src = read_pmc_traffic(args.config, search_mode, cfg["t8"], SLICE_MBS)
+    pmc_rec, pmc_src = read_pmc_traffic(args.config, search_mode, cfg["t8"], SLICE_MBS)
+    pmc = pmc_rec["hbm_bytes_per_mb"] if pmc_rec else None
+    valu_mb = pmc_rec.get("valu_insts_per_mb") if pmc_rec else None
     sm_name = {0: "FFS SearchMode=0", -1: "full search SearchMode=-1", 3: "EPZS SearchMode=3"}[search_mode]
     ffs = search_mode == 0
     an_name = ("k_rdo_inter+k_rdo_intra+k_rdo_final" if RDO else
@@ -478,15 +502,33 @@ def main():
         "launches_per_picture": round(an_per_pic, 2),
         "mbs_per_launch": round(mbs_per_launch, 1),
     }
+    # the issue view: the kernels' VALU wave-instructions per MB (the committed PMC pass) x the MBs
+    # of a launch / the launch time, against the chip's VALU issue rate
+    issue = None
+    if valu_mb:
+        achieved_twis = valu_mb * mbs_per_launch / (an_launch_ms * 1e-3) / 1e12
+        issue = dict(bound="valu-issue", achieved=round(achieved_twis, 4), peak=round(VALU_ISSUE_PEAK_TWIS, 4),
+                     unit="T VALU wave-instructions/s", frac=round(achieved_twis / VALU_ISSUE_PEAK_TWIS, 4),
+                     valu_insts_per_mb=valu_mb, valu_insts_per_mb_kernels=pmc_rec.get("valu_kernels"),
+                     sad_floor_insts_per_mb=round((2 * SR + 1) ** 2 * 256 / 4 / 64) if ffs else None,
+                     traffic=hbm["traffic"], traffic_source=pmc_src,
+                     traffic_over_algorithmic=round(hbm["traffic"] / bytes_per_launch, 2) if hbm["traffic"] else None,
+                     peak_source="MI355X guide: a wave64 VALU instruction issues over 2 cycles on a SIMD-32; "
+                                 "256 CUs x 4 SIMDs x 2.4 GHz / 2",
+                     note="VALU wave-instructions per MB from the committed PMC pass (SQ_INSTS_VALU, " + str(pmc_src)
+                          + ") x the MBs of a launch / this run's launch time")
     if ffs:   # config 2: the FFS SAD table binds -> VALU roofline; HBM beside it
         roofline = dict(bound="valu", achieved=round(achieved_tads, 4), peak=round(peak_tads, 2),
                         unit="T abs-diff/s", frac=round(achieved_tads / peak_tads, 5),
                         traffic=hbm["traffic"], traffic_source=pmc_src, peak_source=peak_src,
-                        algorithmic_ad_per_launch=round(ad_per_launch), **launch_info, hbm=hbm)
-    else:     # EPZS: latency-bound; HBM is the roofline the north star names
+                        algorithmic_ad_per_launch=round(ad_per_launch), **launch_info, hbm=hbm, issue=issue)
+    elif issue:   # EPZS / RD searches: bound by instruction issue along dependent chains, not HBM
+        roofline = dict(issue, **launch_info, hbm=hbm)
+    else:
         roofline = dict(hbm, **launch_info)
     out = {
         "metric": cfg["metric"],
+        "timer": TIMER + "; SURVEY §8d's submit-to-host-visible timer: host_path.pcie_inclusive_mp_s",
         "value": round(value, 3),
         "unit": "MP/s",
         "n_gpus": world,
@@ -537,10 +579,11 @@ def main():
                     "(fill + drain)",
             "pictures": host[2],
         },
-        "verified": None if complete else False,
+        "complete": complete,                             # exactly --steps pictures inside the timed region
+        "verified": None,                                 # the oracle comparison (cpu_baseline leg)
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline and complete:
+    if world == 1 and not args.no_cpu_baseline:
         with tempfile.TemporaryDirectory() as tmp:
             out["cpu_baseline"] = cpu_baseline(args.config, search_mode, tmp, cfg["t8"])
             out["verified"] = verify_against_oracle(jm, os.path.join(tmp, "oracle_seed0.npz"), search_mode, cfg["t8"],
@@ -550,14 +593,10 @@ def main():
         dist.barrier()
     enc.sync()                                            # complete the pictures still in flight
     enc.close()
-    if out["verified"] is False:
-        print("bench.py: GPU results differ from the oracle", file=sys.stderr)
-        return 3
-    if not complete:
-        print("bench.py: a rank completed a different number of pictures than --steps in the timed region",
-              file=sys.stderr)
-        return 4
-    return 0
+    rc, msg = exit_status(out["verified"], complete)
+    if msg:
+        print(msg, file=sys.stderr)
+    return rc
 
 
 if __name__ == "__main__":

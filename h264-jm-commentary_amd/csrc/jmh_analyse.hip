@@ -62,16 +62,17 @@ struct MeS {
     IntraNb<uint8_t> nb;
     int16_t all_mv[8][16][2];
     int motion_cost[8][4];
-    unsigned red[NTA / 64][MAXNS];            // per wave, per search of the stage: argmin keys
+    unsigned red[NTS / 64][MAXNS];            // per search wave, per search of the stage: argmin keys
     int pmv[MAXNS][2];                        // MVPs of the next stage's searches (forwarded)
     uint16_t mvc[MVB_LEN];                    // lambda * mvbits(v) at [v + MVB_OFF] (|v| <= 4*2*SR + 259)
     uint8_t planes[4 * PLS];                  // G (the window), b, h, j
     union {
         int16_t h1[WIN_DIM_MAX * WST];        // unclipped vertical 6-tap intermediates (planes only)
-        uint2 sad8[NPK * NTA];                // then: the 8x8 SADs of every thread's positions,
+        uint2 sad8[NPK * NTS];                // then: the 8x8 SADs of every thread's positions,
     } hs;                                     //   [k][thread] (16x16 / 16x8 / 8x16 searches)
     unsigned long long *pst;                  // debug: per-stage stamps (thread 0), null when off
     int pn;
+    unsigned bar;                             // JMH_I4WAVE: arrivals at the search waves' barriers (search_sync)
     IntraS<uint8_t> in;                       // the MB's intra decisions, run by waves 6 and 7
 };
 union AnalyseS {
@@ -123,10 +124,11 @@ __device__ __forceinline__ unsigned psum(const uint32_t (&r)[2]) {
 // per-thread search state: SADs of the thread's NPK positions and their JM order keys
 struct PosState {
     uint32_t sadp[NPK][2];
-    uint32_t ordk2[NPK / 2]; // JM order of positions 2i (low half) and 2i+1 (high half): 0 = (0,0)
+    uint32_t ordk2[NPK2];    // JM order of positions 2i (low half) and 2i+1 (high half): 0 = (0,0)
                              // pre-check, else spiral index + 1; 0xFFFF for slots outside the table
     int dx, dy0;
     int scx, scy;            // window centre (full pel, relative to the MB)
+    unsigned bgen;           // JMH_I4WAVE: arrivals search_sync waits for (wave-uniform)
 };
 
 // optimisation fence on the register-resident search state, once per stage: keeps the compiler
@@ -138,7 +140,7 @@ __device__ __forceinline__ void fence_state(PosState &ps) {
         for (int q = 0; q < 2; q++) asm volatile("" : "+v"(ps.sadp[k][q]));
     }
 #pragma unroll
-    for (int k = 0; k < NPK / 2; k++) asm volatile("" : "+v"(ps.ordk2[k]));
+    for (int k = 0; k < NPK2; k++) asm volatile("" : "+v"(ps.ordk2[k]));
     asm volatile("" : "+v"(ps.dx), "+v"(ps.dy0));   // nor position arithmetic (RestrictSearchRange 0)
 }
 
@@ -315,7 +317,7 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
     const int sr = d.sr, lam = d.lambda_motion, had = d.use_hadamard;
     unsigned best = s.red[0][j];
 #pragma unroll
-    for (int w = 1; w < NTA / 64; w++) best = min(best, s.red[w][j]);
+    for (int w = 1; w < NTS / 64; w++) best = min(best, s.red[w][j]);
     const unsigned order = best & 8191u;
     int rx, ry;
     if (order == 0) { rx = -scx; ry = -scy; }
@@ -409,6 +411,24 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
 #endif
 __device__ __forceinline__ constexpr int search_wave(int j) { return JMH_SWMAP ? (0x6325410 >> (4 * j)) & 15 : j; }
 
+// barrier of the search waves.  JMH_I4WAVE: the seven search waves count their arrivals in LDS
+// (one monotonic counter, the release / acquire fences order the stage's LDS writes and reads
+// around it) -- an s_barrier would also wait for the intra wave 7, which runs its own chain.  Every
+// search wave reaches every barrier, so the poll always ends.
+__device__ __forceinline__ void search_sync(MeS &s, PosState &ps) {
+#if JMH_I4WAVE
+    ps.bgen += NTS / 64;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (__lane_id() == 0) __hip_atomic_fetch_add(&s.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < ps.bgen)
+        __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+    (void)s; (void)ps;
+    __syncthreads();
+#endif
+}
+
 template <int NS, bool FWD, class EV, class IDLE>
 __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &ps, const SDesc (&sd)[NS], int b8, int best8x8, EV ev,
                                          int islot, IDLE idle, int wave) {
@@ -431,7 +451,7 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
                 set_mvp(NbMe{s, sd[j].bt, b8, best8x8}, sd[j].bx4, sd[j].by4, 4 << lw4_of(sd[j].bt), 4 << lh4_of(sd[j].bt), mx, my);
                 if (lane == 0) { s.pmv[j][0] = mx; s.pmv[j][1] = my; }
             }
-        __syncthreads();
+        search_sync(s, ps);
 #pragma unroll
         for (int j = 0; j < NS; j++) {   // uniform: SGPRs
             pmx[j] = __builtin_amdgcn_readfirstlane(s.pmv[j][0]);
@@ -444,17 +464,21 @@ __device__ __forceinline__ void me_stage(const DevParams &d, MeS &s, PosState &p
         const unsigned v = wave_min_u32(bk[j]);
         if (lane == 0) s.red[wave][j] = v;
     }
-    __syncthreads();
+    search_sync(s, ps);
     sstamp(s, wave);
 #pragma unroll
     for (int j = 0; j < NS; j++)
         if (wave == search_wave(j)) subpel_wave(d, s, j, sd[j], pmx[j], pmy[j], ps.scx, ps.scy, b8, best8x8);
+#if !JMH_I4WAVE
     if constexpr (NS <= 6) {
         if (islot >= 0 && wave >= 6) idle(islot, wave - 6);   // the MB's Intra4x4 on otherwise idle waves
     } else {
         if (islot >= 0 && wave == 7) idle(islot, 0);          // one free wave: a one-block step
     }
-    __syncthreads();
+#else
+    (void)islot; (void)idle;
+#endif
+    search_sync(s, ps);
     sstamp(s, wave);
 }
 
@@ -480,7 +504,7 @@ __device__ __forceinline__ void eval_sad8(const MeS &s, const PosState &ps, int 
         const int rx = abs(ps.dx - sr);
 #pragma unroll
         for (int k = 0; k < NPK; k++) {
-            const uint2 v = s.hs.sad8[k * NTA + tid];
+            const uint2 v = s.hs.sad8[k * NTS + tid];
             const uint32_t r[2] = {v.x, v.y};
             const uint32_t o = ordk_of(ps, k);
             unsigned c[3];
@@ -563,7 +587,7 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
 #pragma unroll
     for (int k = 0; k < NPK; k++) {
         const uint32_t a = ps.sadp[k][0], b = ps.sadp[k][1];
-        reinterpret_cast<uint16_t *>(&s.hs.sad8[k * NTA + tid])[B8] = (uint16_t)((a & 0xFFFFu) + (a >> 16) + (b & 0xFFFFu) + (b >> 16));
+        reinterpret_cast<uint16_t *>(&s.hs.sad8[k * NTS + tid])[B8] = (uint16_t)((a & 0xFFFFu) + (a >> 16) + (b & 0xFFFFu) + (b >> 16));
     }
     if constexpr (B8 == 3) {
         // stage 0: 8x8, 8x4 upper, 4x8 left, 4x4 top-left + 16x16, 16x8 upper, 8x16 left
@@ -665,6 +689,7 @@ __device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraN
 //  motion search of one P macroblock (all 41 searches)
 // ======================================================================================
 __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int k, int w, int mbx, int mby);
+__device__ __forceinline__ void intra_wave(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int mbx, int mby);
 
 __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int mby) {
     const int tid = threadIdx.x;
@@ -674,8 +699,11 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     const bool prof = prof_mb_here(d, mbx, mby);
     PSTAMP(0);
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
-    if (tid == 0) { s.pst = prof ? d.prof + 20 : nullptr; s.pn = 0; }
+    if (tid == 0) { s.pst = prof ? d.prof + 20 : nullptr; s.pn = 0; s.bar = 0; }
     if (tid < 256) s.in.org[tid] = s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+#if JMH_I4WAVE
+    else if (tid < 384) load_orgc(d, s.in.nb, tid - 256, mbx, mby);   // the intra wave's chroma decision
+#endif
     else if (tid >= 384 && tid < 394) { load_border(d, s.bd, tid - 384, mbx, mby); load_border(d, s.in.bd, tid - 384, mbx, mby); }
     else if (tid >= 472 && tid < 478) s.in.part[(tid - 472) / 3][(tid - 472) % 3] = 0;
     else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
@@ -686,6 +714,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
 #else
     auto idle = [&](int k, int w) { intra_slot(d, s.in, scr, k, w, mbx, mby); };
 #endif
+    (void)scr;
     for (int i = tid; i < MVB_LEN; i += NTA) s.mvc[i] = (uint16_t)__umul24(d.lambda_motion, mvbits(i - MVB_OFF));
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
@@ -742,6 +771,7 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         ps.dx = sact ? tid % side : 0;
         ps.dy0 = sact ? (tid / side) * NPK : 0;
         ps.scx = scx; ps.scy = scy;
+        ps.bgen = 0;
         // (the 8x8 SADs of the 16x16 / 16x8 / 8x16 searches come from each 8x8 block's 4x4 SADs,
         // p8x8_block)
         PSTAMP(8);
@@ -749,12 +779,12 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         // the loads overlap the half-pel planes); the (0,0) pre-check position, order 0, depends on
         // the MB's window centre
 #pragma unroll
-        for (int k2 = 0; k2 < NPK / 2; k2++) ps.ordk2[k2] = d.ordtab[k2 * NTA + tid];
+        for (int k2 = 0; k2 < NPK2; k2++) ps.ordk2[k2] = d.ordtab[k2 * NTA + tid];
         {
             const int k0 = sr - scy - ps.dy0;   // strip slot of the pre-check position
             const bool mine = sact && ps.dx == sr - scx;
 #pragma unroll
-            for (int k2 = 0; k2 < NPK / 2; k2++)
+            for (int k2 = 0; k2 < NPK2; k2++)
                 if (mine && (k0 >> 1) == k2) ps.ordk2[k2] &= (k0 & 1) ? 0x0000FFFFu : 0xFFFF0000u;
         }
         PSTAMP(9);
@@ -819,6 +849,14 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
         }
         __syncthreads();   // h1 is dead: its LDS holds the 8x8 SADs from here on
         PSTAMP(2);
+#if JMH_I4WAVE
+        if (wave == NTS / 64) {   // the last s_barrier this wave meets: the intra decisions from here on
+#if !(JMH_EXP & 2)
+            intra_wave(d, s.in, scr, mbx, mby);
+#endif
+            return;
+        }
+#endif
         {   // ---- P8x8 (4 x 4 stages), the 16x16 / 16x8 / 8x16 searches inside block 3's stages 0, 1
             int best8x8 = 0, cost8x8 = 0;
             p8x8_block<0>(d, s, ps, best8x8, cost8x8, idle, wave, tid);
@@ -1060,6 +1098,33 @@ __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &
     }
 }
 
+// JMH_I4WAVE: the intra decisions of a P macroblock on wave 7 of its motion-search workgroup, on
+// a schedule of their own (the search waves synchronise among themselves, search_sync): Intra4x4
+// over the 16 blocks in JM's decoding order on one wave (each block's neighbours are earlier in
+// it; the LDS writes of one wave are seen by its later reads), then the Intra16x16 and chroma
+// intra-mode decisions, so that no intra workgroup runs for a P picture's MBs
+__device__ __forceinline__ void intra_wave(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int mbx, int mby) {
+    const int lane = __lane_id();
+    const MbAvail mav = mb_avail(d, mbx, mby);
+    const int qpk = q_round(d.qsel, 15 + d.qp / 6);
+    int tabr[2];
+    i4_tabrow(lane, tabr);
+    int acc[3] = {0, 0, 0};                   // cost, cbp (per b8), block mask
+    for (int blk = 0; blk < 16; blk++) {
+        const int bx4 = 2 * ((blk >> 2) & 1) + (blk & 1), by4 = 2 * (blk >> 3) + ((blk >> 1) & 1);
+        i4_block(d, s, scr, 0, bx4, by4, tabr, mav.L, mav.T, mav.TL, mav.TR, qpk, acc);
+    }
+    if (lane == 0) {
+        scr->i4cost = 24 * d.lambda_mode + acc[0];   // 4 x (int)floor(6*lambda+0.4999)
+        scr->i4cbp = acc[1];
+        scr->i4blk = acc[2];
+    }
+    if (lane < 16) scr->ipred[lane] = s.ipred_cur[lane];
+    reinterpret_cast<uint32_t *>(scr->i4rec)[lane] = reinterpret_cast<const uint32_t *>(s.rec)[lane];
+    i16_decision(d, s.org, s.nb, scr, lane, mav.L, mav.T, mav.TL);
+    chroma_decision(d, s.nb, scr, lane, mav.L, mav.T, mav.TL);
+}
+
 __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     __shared__ AnalyseS s;
     // blocks: [0, nPm) the motion search of each P picture MB with its Intra4x4 decision (longest,
@@ -1070,17 +1135,17 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     const unsigned long long t0 = t.bprof ? wall_clock64() : 0;
     const bool first_thread = threadIdx.x == 0;   // a lane mask: threadIdx itself dies early
     const int role = b < nPg ? 2 : 0;
-    int tag = role;                                           // debug (JMH_BLOCK_PROF): role | MB << 4 | entry << 20
+    unsigned long long tag = role;                            // debug (JMH_BLOCK_PROF): role | MB << 4 | entry << 32
     if (role == 2) {
         const int m = xcd_block(b, nPm);                      // XCD-aware: neighbouring MBs share an L2
         if (m >= nPm) return;                                 // padding block (whole workgroup)
         const int e = tick_entry(t, m);
         const DevParams d = tick_params(t, e);
         const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
-        tag = 2 | (mby * d.mbw + mbx) << 4 | e << 20;
+        tag = 2u | (unsigned long long)(mby * d.mbw + mbx) << 4 | (unsigned long long)e << 32;
         me_mb(d, s.me, mbx, mby);
     } else {
-        const int q = __builtin_amdgcn_readfirstlane(4 * (b - nPg) + (int)(threadIdx.x >> 7));
+        const int q = __builtin_amdgcn_readfirstlane((JMH_I4WAVE ? nPm : 0) + 4 * (b - nPg) + (int)(threadIdx.x >> 7));
         const bool act = q < tot;
         const int e = tick_entry(t, act ? q : 0);
         const DevParams d = tick_params(t, e);
@@ -1092,7 +1157,7 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
         if (first_thread) {
             t.bprof[3 * b] = t0;
             t.bprof[3 * b + 1] = wall_clock64();
-            t.bprof[3 * b + 2] = (unsigned)tag;
+            t.bprof[3 * b + 2] = tag;
         }
     }
 }
@@ -1138,7 +1203,9 @@ hipError_t jmh_launch_intra(const TickArgs &t, hipStream_t st) {
 }
 
 hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
-    const int nblocks = xcd_grid(t.me_in_analyse ? t.pre[t.nP] : 0) + (t.pre[t.npic] + 3) / 4;
+    const int nPm = t.me_in_analyse ? t.pre[t.nP] : 0;   // JMH_I4WAVE: their intra decisions ran on wave 7
+    const int nblocks = xcd_grid(nPm) + (t.pre[t.npic] - (JMH_I4WAVE ? nPm : 0) + 3) / 4;
+    if (nblocks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }

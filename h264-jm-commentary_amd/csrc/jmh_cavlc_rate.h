@@ -57,6 +57,9 @@ JMV_TABLE uint8_t jmv_cbp_p[48] = {0,  2,  3,  7,  4,  8,  17, 13, 5,  18, 9,  1
                                    35, 45, 38, 41, 39, 42, 43, 19, 6,  24, 25, 20, 26, 21, 46, 28, 27, 47, 22, 29, 23, 30, 31, 12};
 
 JMV_FN int jmv_ue(unsigned v) { return 127 - 2 * __builtin_clzll((unsigned long long)v + 1ull); }   /* 2 floor(log2(v+1)) + 1 */
+/* P_Skip: 0 bits (the run goes out with the next coded macroblock) except at the picture's last
+   macroblock, where JM's writeMBLayer writes the pending run, this macroblock included (item 64(a)) */
+JMV_FN int jmv_skip(int skip_run, int last_in_picture) { return last_in_picture ? jmv_ue((unsigned)skip_run + 1u) : 0; }
 JMV_FN int jmv_se(int v) { return jmv_ue(v > 0 ? (unsigned)(2 * v - 1) : (unsigned)(-2 * v)); }
 
 /* residual_block_cavlc: coef[st * i] for i in [0, n) in scan order (st 4: a CAVLC-interleaved 4x4

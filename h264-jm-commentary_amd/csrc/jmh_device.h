@@ -10,7 +10,17 @@
 #define QPAD 4                           // quarter-pel plane padding (== oracle JMO_PAD)
 #define NT 256                           // threads per finalize / unit workgroup
 #define NTA 512                          // threads per analysis workgroup (8 waves, 2 per SIMD)
-#define NPK 10                           // FFS search positions per analysis thread (a column strip)
+// JMH_I4WAVE 1: a P macroblock's intra decisions run on wave 7 of its motion-search workgroup on
+// their own schedule (the seven search waves meet at LDS-counter barriers, never at s_barrier, which
+// would wait for wave 7), so the Intra4x4 chain is off the search's stage chain; 0: the Intra4x4
+// steps ride in the stages' sub-pel phases on waves 6 and 7 (A/B: -DJMH_I4WAVE=0)
+#ifndef JMH_I4WAVE
+#define JMH_I4WAVE 0
+#endif
+#define NTS (JMH_I4WAVE ? 448 : NTA)     // threads of the FFS position strips (the search waves)
+#define NPK (JMH_I4WAVE ? 11 : 10)       // FFS search positions per search thread (a column strip):
+                                         //   65 x ceil(65 / NPK) strips <= NTS
+#define NPK2 ((NPK + 1) / 2)             // packed order-key pairs per thread
 #define BIGCOST (1 << 20)
 #define PMAX 33                          // pictures per wavefront tick (pipelined pictures in flight;
                                          // 2160p needs 508 / PIPE_LAG + 1 = 33)
@@ -153,7 +163,7 @@ struct TickArgs {
                                          //   (1: CABAC rates, 2: CAVLC rates, SymbolMode 0)
     const int32_t *sched, *soff;         //   schedule: MB addresses in stage order, offsets per stage
     void *rscr;                          //   the tick's candidate scratch (RdoScr per tick MB)
-    const uint32_t *ordtab;              // FFS order keys, [NPK / 2][NTA] packed pairs (jmh_create)
+    const uint32_t *ordtab;              // FFS order keys, [NPK2][NTA] packed pairs (jmh_create)
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
     PicParams p[PMAX];

@@ -1116,7 +1116,10 @@ __global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
         const RdoChroma<pel> &C = scr->C[b];
         jmr_eng en = {s.stc[kc], s.rg0, 0};
         if (i == 0) {
-            if (CAV) s.out[kc] = jmr_mbinfo{};     // P_Skip: rate 0, its run is written with the next coded MB
+            if (CAV) {                          // P_Skip: its run is written with the next coded MB (rate 0), or
+                s.out[kc] = jmr_mbinfo{};       //   by this MB when it is the picture's last (item 64(a))
+                en.bits = jmv_skip((int)s.rg0, a == d.mbw * d.mbh - 1);
+            }
             else jmr_skip(&en, A, B, &s.out[kc]);
         } else {
             jmr_cand r;

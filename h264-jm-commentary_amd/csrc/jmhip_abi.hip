@@ -174,10 +174,6 @@ struct jmh_ctx {
     int32_t *d_sched, *d_soff;
     void *d_rscr;
     int nslice;
-    // macroblocks per tick at most (0: every ready diagonal).  RD ticks: one dispatch round of
-    // k_rdo_inter (its LDS fits five MBs per CU), so that a tick is never one full round plus a
-    // partial one; the pictures beyond the cap wait for the next tick (oldest pictures first)
-    int tick_cap;
 };
 
 #define HCHK(x)                                                                  \
@@ -404,11 +400,6 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     c->next_id = 0; c->next_entry = 0; c->last_id = -1; c->last_entry = -1;
     c->ref_kind = REF_NONE; c->ref_entry = -1; c->cur_entry = -1;
     c->prof_mb = -1;
-    // A/B knob only: at most this many MBs per tick (younger pictures wait).  Capping config 5's RD
-    // ticks at one dispatch round (5 x 256 CUs) measured 333 MP/s against 474 uncapped
-    // (profiles/r7a_tick_cap_ab.txt): the longer ticks of the full pipeline win, so no cap by default.
-    c->tick_cap = 0;
-    if (const char *e = getenv("JMH_TICK_CAP")) c->tick_cap = atoi(e);
     int st = JMH_OK;
 #define ALLOC(p, n) do { if (hipMalloc((void **)&(p), (n)) != hipSuccess) { st = JMH_E_OOM; goto fail; } } while (0)
     {
@@ -496,12 +487,14 @@ static int host_spiral_index(int x, int y) {
 
 // order keys of the FFS analysis threads (k_mb_analyse): thread t owns window column t % side,
 // rows (t / side) * NPK .. + NPK - 1; key = spiral index + 1 (0 is the (0,0) pre-check, set per
-// MB in the kernel), 0xFFFF outside the window.  [NPK / 2][NTA] packed pairs (low = even slot).
+// MB in the kernel), 0xFFFF outside the window.  [NPK2][NTA] packed pairs (low = even slot); only
+// the NTS search threads own strips.
 static void ordtab_fill(std::vector<uint32_t> &tab, int sr) {
     const int side = 2 * sr + 1, nstrips = (side + NPK - 1) / NPK;
-    tab.assign((size_t)(NPK / 2) * NTA, 0);
+    static_assert(SIDE_MAX * ((SIDE_MAX + NPK - 1) / NPK) <= NTS, "the search threads cover every FFS position");
+    tab.assign((size_t)NPK2 * NTA, 0);
     for (int t = 0; t < NTA; t++) {
-        const bool sact = t < side * nstrips;
+        const bool sact = t < side * nstrips && t < NTS;
         const int dx = sact ? t % side : 0, dy0 = sact ? (t / side) * NPK : 0;
         for (int k = 0; k < NPK; k++) {
             const int dy = dy0 + k;
@@ -604,14 +597,11 @@ static int issue_tick(jmh_ctx *c) {
     const int nf = (int)c->fl.size();
     std::vector<int> before(nf);
     for (int i = 0; i < nf; i++) before[i] = c->fl[i].stage = skip_empty(c, c->fl[i].stage);
-    int capped = 0;
     for (int i = 0; i < nf && nact < PMAX; i++) {
         const Flight &f = c->fl[i];
         if (f.stage >= c->nd) continue;
         if (f.pred_id >= 0 && i > 0 && c->fl[i - 1].id == f.pred_id &&
             before[i - 1] < c->nd && before[i - 1] - f.stage < c->lag) continue;
-        if (c->tick_cap > 0 && nact > 0 && capped + c->dcount[f.stage] > c->tick_cap) break;   // younger pictures wait
-        capped += c->dcount[f.stage];
         act[nact++] = i;
         nP += f.pp.slice_type == JMH_P_SLICE;
     }
@@ -850,8 +840,9 @@ static int frame_push_any(jmh_ctx *c, const void *y, const void *u, const void *
     PicBuf &b = c->ring[e];
     if ((r = alloc_host(c, b))) return r;
     HCHK(hipEventSynchronize(b.ev_src));   // the previous H2D out of this staging buffer
-    // an out-of-range sample rejects the picture before anything is queued (the claimed entry
-    // stays free: nothing refers to it)
+    // an out-of-range sample rejects the picture before its own copy or ticks are queued: the
+    // claimed entry stays free (nothing refers to it).  Not side-effect free: claiming the entry
+    // may already have issued ticks of earlier pictures (legal progress of their wavefronts)
     if (!pack_planes(b.h_src, c->W, c->H, y, u, v, sy, sc, c->ps, c->maxv)) return JMH_E_INVALID_ARG;
     HCHK(hipEventRecord(b.ev_t0, c->st));
     HCHK(hipMemcpyAsync(b.src, b.h_src, c->fsize, hipMemcpyHostToDevice, c->st));
@@ -971,7 +962,7 @@ int jmh_sync(jmh_ctx *c) {
         for (int r = 0; r < 5; r++) { r0[r] = ~0ull; r1[r] = 0; }
         for (int i = 0; i < c->bprof_blocks; i++) {
             unsigned long long a = h[3 * i], b = h[3 * i + 1];
-            int role = (int)(h[3 * i + 2] & 15);                   // k_mb_analyse: | MB << 4 | entry << 20
+            int role = (int)(h[3 * i + 2] & 15);                   // k_mb_analyse: | MB << 4 | entry << 32
             if (!a || role < 0 || role > 4 || b < a) continue;   // 0: padding block, not written
             if (role == 2) slow.push_back({(double)(b - a) * us, (unsigned long long)i});
             if (role == 3) { f0 = a < f0 ? a : f0; f1 = b > f1 ? b : f1; }
@@ -995,7 +986,7 @@ int jmh_sync(jmh_ctx *c) {
             fprintf(stderr, "jmh_blocks slowest role2 (mbx,mby,entry start+dur us):");
             for (size_t k = slow.size() > 12 ? slow.size() - 12 : 0; k < slow.size(); k++) {
                 const unsigned long long i = slow[k].second, tg = h[3 * i + 2];
-                const int mb = (int)((tg >> 4) & 0xFFFF), en = (int)(tg >> 20);
+                const int mb = (int)((tg >> 4) & 0xFFFFFFFu), en = (int)(tg >> 32);
                 fprintf(stderr, " (%d,%d,%d %.1f+%.1f)", mb % c->mbw, mb / c->mbw, en, (double)(h[3 * i] - t0) * us, slow[k].first);
             }
             double xs[8] = {0}, xm[8] = {0};                     // per XCD (hardware block % 8)
@@ -1006,7 +997,7 @@ int jmh_sync(jmh_ctx *c) {
             fprintf(stderr, " fastest:");
             for (size_t k = 0; k < slow.size() && k < 6; k++) {
                 const unsigned long long i = slow[k].second, tg = h[3 * i + 2];
-                const int mb = (int)((tg >> 4) & 0xFFFF), en = (int)(tg >> 20);
+                const int mb = (int)((tg >> 4) & 0xFFFFFFFu), en = (int)(tg >> 32);
                 fprintf(stderr, " (%d,%d,%d %.1f+%.1f)", mb % c->mbw, mb / c->mbw, en, (double)(h[3 * i] - t0) * us, slow[k].first);
             }
             fprintf(stderr, "\n");

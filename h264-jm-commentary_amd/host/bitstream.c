@@ -489,7 +489,13 @@ void jm_slice_write_mb(jm_slice_writer *sw, int a, const jmh_mb_result *r) {
         w->written[a] = w->stamp;
         memset(w->tc + (size_t)a * 24, 0, 24);
         sw->skip_run++;
-        if (s->rdo) { sw->rate_checked++; sw->rate_bad += r->min_cost != 0; }   /* nothing written yet */
+        if (s->rdo) {   /* nothing written yet -- except the run itself at the picture's last MB (item 64(a)) */
+            long expect = 0;
+            if (a == s->mbw * s->mbh - 1) for (unsigned v = (unsigned)sw->skip_run + 1u; v; v >>= 1) expect += 2;   /* ue */
+            if (expect) expect--;
+            sw->rate_checked++;
+            sw->rate_bad += r->min_cost != expect;
+        }
         return;
     }
     const long bit0 = 8 * sw->b->len + sw->b->nacc;

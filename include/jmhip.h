@@ -120,8 +120,8 @@ typedef struct jmh_config {
                                        IntraBlocks / RDCost_for_8x8IntraBlocks [J]: SSD + lambda_rd *
                                        rate, the rate from the CABAC coding state of the slice,
                                        csrc/jmh_cabac_rate.h, or with symbol_mode 0 the CAVLC bit count,
-                                       csrc/jmh_cavlc_rate.h); needs SearchMode 3
-                                       (docs/JM_SEMANTICS.md items 53-60, 63, 64)                     */
+                                       csrc/jmh_cavlc_rate.h); with SearchMode 3, 0 or -1
+                                       (docs/JM_SEMANTICS.md items 53-60, 63, 64, 65)                 */
     int32_t symbol_mode;            /* SymbolMode: 0 CAVLC, 1 CABAC (the RD rate's entropy coder)     */
     /* JM >= 10 EPZS options (SearchMode 3; docs/JM_SEMANTICS.md items 61, 62); zero keeps items 36, 39 */
     int32_t epzs_subpel_me;         /* EPZSSubPelME: 0 SubPelBlockMotionSearch, 1 the EPZS sub-pel

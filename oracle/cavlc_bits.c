@@ -101,6 +101,14 @@ static int luma8_bits(const jmo_cavnb *nb, uint8_t *cur, int b8, const int16_t (
     return bits;
 }
 
+/* a P_Skip candidate: nothing is written for it (its run goes out with the next coded macroblock of
+   the slice), except at the picture's last macroblock, where writeMBLayer finds no next macroblock
+   (FmoGetNextMBNr -1) and writes the run, this macroblock included: ue(skip_run + 1)
+   (docs/JM_SEMANTICS.md item 64(a)) */
+int jmo_cavlc_skip_bits(int skip_run, int last_in_picture) {
+    return last_in_picture ? ue_len((unsigned)skip_run + 1u) : 0;
+}
+
 /* a whole macroblock candidate: the mb_skip_run before it (P slices), macroblock_layer (7.3.5) as
    writeMBLayer writes it; tc_out (may be NULL): its 24 TotalCoeff for the neighbours' nC */
 int jmo_cavlc_mb_bits(const jmo_cavnb *nb, const jmo_cabsyn *m, int slice_p, int t8mode, int skip_run, uint8_t tc_out[24]) {

@@ -99,6 +99,7 @@ int jmo_cavlc_block_bits(const int16_t *coef, int n, int nC, int *total_coeff);
 int jmo_cavlc_mb_bits(const jmo_cavnb *nb, const jmo_cabsyn *m, int slice_p, int t8mode, int skip_run, uint8_t tc_out[24]);
 int jmo_cavlc_b8_bits(const jmo_cavnb *nb, uint8_t cur_tc[24], int b8, int sm, const int16_t (*mvd4)[2], int coded,
                       const int16_t (*lev4)[16]);
+int jmo_cavlc_skip_bits(int skip_run, int last_in_picture);
 int jmo_cavlc_i4_bits(const jmo_cavnb *nb, uint8_t cur_tc[24], int x4, int y4, int code, const int16_t *lev);
 int jmo_cavlc_i8_bits(const jmo_cavnb *nb, uint8_t cur_tc[24], int b8, int code, const int16_t *lev64);
 
@@ -120,6 +121,7 @@ typedef struct jmo_rate_event {
     /* SymbolMode 0 (CAVLC): no coder state; the neighbours' TotalCoeff, the current MB's so far (B8,
        I4, I8) and the slice's pending mb_skip_run (MB) */
     int cavlc, skip_run, b8i;                /* b8i: JMO_RATE_I8's 8x8 block                       */
+    int last_mb;                             /* JMO_RATE_SKIP: the last MB of the picture          */
     const jmo_cavnb *cnb;
     const uint8_t *tc_before;
 } jmo_rate_event;

@@ -526,7 +526,11 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
             long bits;
             if (i == 0) {
                 RATE_BEGIN(JMO_RATE_SKIP);
-                if (cavlc) bits = rate_cav(&ev, &cnb, NULL, 0);   /* the run is written with the next coded MB */
+                if (cavlc) {   /* the run is written with the next coded MB, or here at the picture's last MB */
+                    ev.skip_run = c->cav_run;
+                    ev.last_mb = a == nmb - 1;
+                    bits = rate_cav(&ev, &cnb, NULL, jmo_cavlc_skip_bits(c->cav_run, a == nmb - 1));
+                }
                 else {
                     jmo_cab_skip(&e, &nb);
                     bits = rate_of(&ev, &c->cab, &e);

@@ -86,7 +86,7 @@ static void hook_cavlc(const jmo_rate_event *ev) {
     if (ev->tc_before) memcpy(tc, ev->tc_before, 24);
     long bits = 0;
     switch (ev->kind) {
-    case JMO_RATE_SKIP: bits = 0; break;
+    case JMO_RATE_SKIP: bits = jmv_skip(ev->skip_run, ev->last_mb); break;
     case JMO_RATE_MB: {
         const jmo_cabsyn *m = ev->syn;
         int8_t ipm[16];

@@ -50,3 +50,39 @@ def test_cpu_worker(config, mode, rdo, tmp_path):
         assert int(d["py"].max()) > 255
     if rdo:
         assert d["pres"]["min_cost"].sum() > 0
+
+
+def test_exit_status():
+    """an incomplete timed region is its own failure (4), never reported as an oracle mismatch (3);
+    `verified` None (no oracle leg) with a complete region is success"""
+    b = load_bench()
+    assert b.exit_status(True, True) == (0, None)
+    assert b.exit_status(None, True) == (0, None)
+    rc, msg = b.exit_status(None, False)
+    assert rc == 4 and "oracle" not in msg and "--steps" in msg
+    rc, msg = b.exit_status(True, False)
+    assert rc == 4 and "oracle" not in msg
+    rc, msg = b.exit_status(False, True)
+    assert rc == 3 and "differ from the oracle" in msg
+    assert b.exit_status(False, False)[0] == 3
+
+
+def test_metric_names_timer():
+    """every bench metric says which timer `value` uses (device-resident; the PCIe-inclusive rate
+    is host_path.pcie_inclusive_mp_s)"""
+    b = load_bench()
+    for k in (2, 3, 5):
+        assert "device-resident" in b.use_config(k)["metric"]
+    assert "device-resident" in b.use_config(5, rdo=0)["metric"]
+
+
+def test_pmc_records_issue_roofline():
+    """tools/pmc_traffic.json carries the VALU instructions per MB the issue roofline of every
+    config prices (configs 3 and 5 report bound "valu-issue")"""
+    b = load_bench()
+    b.use_config(3)
+    for config, mode, t8, sl in ((2, 0, 0, 0), (3, 3, 1, 0), (5, 3, 0, 240), (5, 3, 1, 240)):
+        b.RDO = 1 if config == 5 else 0
+        rec, src = b.read_pmc_traffic(config, mode, t8, sl)
+        assert rec and rec["valu_insts_per_mb"] > 4225 and rec["hbm_bytes_per_mb"] > 0, (config, src)
+        assert abs(sum(rec["valu_kernels"].values()) - rec["valu_insts_per_mb"]) < 1

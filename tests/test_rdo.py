@@ -151,3 +151,59 @@ def test_rdo_config_gate(bad, msg):
             args += ["-p", e]
         r = subprocess.run(args, capture_output=True, text=True, timeout=60)
         assert r.returncode != 0 and msg in (r.stdout + r.stderr), r.stdout + r.stderr
+
+
+def ue_bits(v):
+    """length of ue(v) (9.1)"""
+    return 2 * (v + 1).bit_length() - 1
+
+
+@pytest.mark.parametrize("slice_mbs", [0, 11, 99])
+def test_rdo_cavlc_last_mb_skip_run(slice_mbs):
+    """docs/JM_SEMANTICS.md item 64(a): with CAVLC rates a P_Skip costs 0 bits (its mb_skip_run goes
+    out with the next coded macroblock) except at the picture's last macroblock, where JM's
+    writeMBLayer finds no next macroblock (FmoGetNextMBNr -1) and writes the pending run, this MB
+    included: the skip candidate's rate is ue(run + 1).  A P picture whose source is the I
+    picture's reconstruction: every macroblock is skipped."""
+    import numpy as np
+    import oracle_lib
+    from jmpaths import load_jmhip
+    ensure_built()
+    jm = load_jmhip()
+    w, h = 176, 144
+    nmb = (w // 16) * (h // 16)
+    rng = np.random.default_rng(5)
+    y = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    u = rng.integers(0, 256, (h // 2, w // 2), dtype=np.uint8)
+    v = rng.integers(0, 256, (h // 2, w // 2), dtype=np.uint8)
+    o = oracle_lib.OracleEncoder(w, h, rdo=1, symbol_mode=0, search_mode=3, search_range=8, slice_mbs=slice_mbs)
+    try:
+        _, rec = o.encode(y, u, v, jm.JMH_I_SLICE, 28)
+        o.set_reference(*rec)
+        res, _ = o.encode(*rec, jm.JMH_P_SLICE, 28)       # P: its source is the reference itself
+    finally:
+        o.close()
+    mt, mc = res["mb_type"].tolist(), res["min_cost"].tolist()
+    assert mt.count(0) == nmb                              # all P_Skip
+    k = slice_mbs or nmb
+    run = (nmb - 1) % k                                    # skipped MBs before the last one in its slice
+    assert mc[-1] == ue_bits(run + 1)
+    assert all(c == 0 for c in mc[:-1])
+
+
+def test_rdo_cavlc_last_mb_skip_writer():
+    """the same rule through the product writer: a flat picture (its I reconstruction is exact, so
+    every P macroblock is skipped, the last one included); the writer's RD rate check (the run
+    written at the slice end == the last skip's rate) and the closed loop"""
+    ensure_built()
+    w, h, n = 96, 64, 3
+    with tempfile.TemporaryDirectory() as d:
+        with open(f"{d}/flat.yuv", "wb") as f:
+            f.write(bytes([128]) * (w * h * 3 // 2) * n)
+        log = encode(d, ["SymbolMode=0", "RDOptimization=1", "SearchMode=3", "ProfileIDC=66", "SearchRange=8",
+                         f"InputFile={d}/flat.yuv", f"FramesToBeEncoded={n}", f"SourceWidth={w}", f"SourceHeight={h}"])
+        nchk, bad = rate_check(log)
+        assert nchk == 3 * (w // 16) * (h // 16) and bad == 0, log
+        r = subprocess.run([JMDEC, f"{d}/a.264", f"{d}/dec.yuv"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/a.yuv", "rb").read()

@@ -257,3 +257,19 @@ def test_rdo_rejects_unsupported():
                dict(rdo=1, symbol_mode=0, search_mode=2)):
         with pytest.raises(jmhip.JmhError):
             jmhip.Encoder(64, 48, search_range=8, **kw)
+
+
+@pytest.mark.parametrize("slice_mbs,bd", [(0, 8), (11, 8), (0, 10)])
+def test_rdo_cavlc_last_mb_skip(slice_mbs, bd):
+    """docs/JM_SEMANTICS.md item 64(a) on the device: flat pictures (every P macroblock skipped); the
+    last macroblock's skip carries ue(mb_skip_run + 1), every other skip 0 bits -- GPU == oracle"""
+    w, h = 176, 144
+    nmb = (w // 16) * (h // 16)
+    dt = np.uint16 if bd > 8 else np.uint8
+    mid = 1 << (bd - 1)
+    pic = (np.full((h, w), mid, dt), np.full((h // 2, w // 2), mid, dt), np.full((h // 2, w // 2), mid, dt))
+    res = rdo_pair(w, h, [pic] * 3, 28, bd=bd, symbol_mode=0, search_range=8, slice_mbs=slice_mbs)
+    mt, mc = res["mb_type"].tolist(), res["min_cost"].tolist()
+    assert mt.count(0) == nmb
+    run = (nmb - 1) % (slice_mbs or nmb)
+    assert mc[-1] == 2 * (run + 2).bit_length() - 1 and not any(mc[:-1])

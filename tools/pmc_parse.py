@@ -76,6 +76,8 @@ roof = [k for k in out["kernels"] if base_name(k) in ROOFLINE]
 if roof and all("hbm_bytes_per_mb" in out["kernels"][k] for k in roof):
     out["roofline_kernels"] = roof
     out["roofline_hbm_bytes_per_mb"] = round(sum(out["kernels"][k]["hbm_bytes_per_mb"] for k in roof), 1)
+    if all("insts_per_mb" in out["kernels"][k] for k in roof):   # bench.py's issue roofline
+        out["roofline_valu_insts_per_mb"] = round(sum(out["kernels"][k]["insts_per_mb"]["SQ_INSTS_VALU"] for k in roof), 1)
 if hbm_total:
     out["hbm_bytes_per_mb"] = round(hbm_total / mbs, 1)
     out["note"] = ("all wavefront kernels; 2 x FETCH_SIZE + WRITE_SIZE over 1 IDR + %d P pictures, per MB; "
