@@ -41,21 +41,13 @@
 #endif
 #include "jmh_intra8.h"
 #include "jmh_intra.h"
+#include "jmh_i4.h"
 
 #define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
 #define MVB_LEN 1104
 #define PLS (WIN_DIM_MAX * WST + 32)          // stride between the G, b, h, j planes
 #define MAXNS 7                               // searches per stage (block 0 stage 0: 3 + 4)
 
-template <class pel>
-struct IntraS {
-    alignas(4) pel org[256];
-    alignas(4) pel rec[256];
-    Border bd;
-    IntraNb<pel> nb;
-    int8_t ipred_cur[16];
-    int part[2][4];                           // per I4 wave: cost, cbp, blk mask
-};
 struct MeS {
     uint8_t org[256];
     Border bd;
@@ -888,136 +880,6 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     }
 }
 
-// ======================================================================================
-//  role 0: Intra4x4 (Mode_Decision_for_Intra4x4Macroblock) in 10 diagonal steps
-// ======================================================================================
-template <class pel>
-__device__ __forceinline__ int lpix(const IntraS<pel> &s, int x, int y) {
-    if (y < 0) return s.nb.rtop[x + 1];
-    if (x < 0) return s.nb.rleft[y];
-    return s.rec[16 * y + x];
-}
-
-// lane_fwd4x4 / lane_inv4x4 with the row gathers as quad DPP broadcasts (the four samples of
-// row y of a 16-lane group are one quad); the column gathers stay ds_bpermute (whole quads active)
-__device__ __forceinline__ int quad_fwd4x4(int r, int l) {
-    const int y = l >> 2, x = l & 3;
-    const int v0 = dpp<0x00>(r), v1 = dpp<0x55>(r), v2 = dpp<0xAA>(r), v3 = dpp<0xFF>(r);
-    int p0 = v0 + v3, p3 = v0 - v3, p1 = v1 + v2, p2 = v1 - v2;
-    const int t = x == 0 ? p0 + p1 : x == 1 ? 2 * p3 + p2 : x == 2 ? p0 - p1 : p3 - 2 * p2;
-    const int u0 = g16(t, x), u1 = g16(t, 4 + x), u2 = g16(t, 8 + x), u3 = g16(t, 12 + x);
-    p0 = u0 + u3; p3 = u0 - u3; p1 = u1 + u2; p2 = u1 - u2;
-    return y == 0 ? p0 + p1 : y == 1 ? 2 * p3 + p2 : y == 2 ? p0 - p1 : p3 - 2 * p2;
-}
-__device__ __forceinline__ int quad_inv4x4(int dq, int l, int pred, int maxv) {
-    const int y = l >> 2, x = l & 3;
-    const int d0 = dpp<0x00>(dq), d1 = dpp<0x55>(dq), d2 = dpp<0xAA>(dq), d3 = dpp<0xFF>(dq);
-    int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
-    const int t = x == 0 ? e0 + e3 : x == 1 ? e1 + e2 : x == 2 ? e1 - e2 : e0 - e3;
-    const int f0 = g16(t, x), f1 = g16(t, 4 + x), f2 = g16(t, 8 + x), f3 = g16(t, 12 + x);
-    e0 = f0 + f2; e1 = f0 - f2; e2 = (f1 >> 1) - f3; e3 = f1 + (f3 >> 1);
-    const int o = y == 0 ? e0 + e3 : y == 1 ? e1 + e2 : y == 2 ? e1 - e2 : e0 - e3;
-    return iclip(0, maxv, (o + (pred << 6) + 32) >> 6);
-}
-
-// the Intra4x4 prediction table entries of lane 4m + y (mode m < 9, block row y): c_i4tab of its
-// four samples, two 16-bit entries per dword (i4_block)
-__device__ __forceinline__ void i4_tabrow(int lane, int (&tabr)[2]) {
-    const int m = lane >> 2, y = lane & 3;
-    tabr[0] = m < 9 ? (int)(c_i4tab[m][4 * y] | (uint32_t)c_i4tab[m][4 * y + 1] << 16) : 0;
-    tabr[1] = m < 9 ? (int)(c_i4tab[m][4 * y + 2] | (uint32_t)c_i4tab[m][4 * y + 3] << 16) : 0;
-}
-
-// one 4x4 block on one wave.  Lane 4m + y (m < 9) predicts row y of mode m from the 13 neighbours
-// (held by lanes 0..12, fetched with ds_bpermute) and scores it: the horizontal Hadamard of the
-// row in registers, the vertical butterflies across the quad's rows by DPP.  One wave minimum of
-// (cost, mode) keys is JM's strict '<' scan in mode order; then dct_luma on lanes 0..15 of the
-// chosen prediction (at QP'Y = QPY + QpBdOffsetY)
-template <class pel>
-__device__ __forceinline__ void i4_block(const DevParams &d, IntraS<pel> &s, MbScratch *scr, int w, int bx4, int by4, const int (&tabr)[2],
-                                         bool avL, bool avT, bool avTL, bool avTR, int qpk, int (&acc)[3],
-                                         unsigned long long *pst = nullptr) {   // debug: sub-phase stamps [52..57]
-#define I4ST(k, v) do { if (pst) { asm volatile("" ::"v"(v)); if (__lane_id() == 0) pst[k] = wall_clock64(); } } while (0)
-    I4ST(52, bx4);
-    const int lane = threadIdx.x & 63, l = lane & 15;
-    const int bx = 4 * bx4, by = 4 * by4, blk = 4 * by4 + bx4;
-    const int lambda = d.lambda_mode, qp = d.qp + d.qpbd, had = d.use_hadamard;
-    const bool up = by > 0 || avT, left = bx > 0 || avL;
-    const bool ul = (bx > 0 && by > 0) || (bx == 0 && by > 0 && avL) || (bx > 0 && by == 0 && avT) || (bx == 0 && by == 0 && avTL);
-    bool ur = by == 0 ? (bx + 4 <= 15 ? avT : avTR) : (bx + 4 <= 15);
-    if ((bx == 4 || bx == 12) && (by == 4 || by == 12)) ur = false;
-    (void)w;
-    // P[lane]: p[-1,-1], p[0..7,-1], p[-1,0..3] -- one LDS read per lane from a selected address
-    // (the MB's reconstruction or its top / left neighbour samples), no divergent branches
-    const int px = lane == 0 || lane >= 9 ? bx - 1 : lane <= 4 || ur ? bx + lane - 1 : bx + 3;
-    const int py = lane >= 9 ? by + lane - 9 : by - 1;
-    const bool pav = lane < 13 && (lane == 0 ? ul : lane <= 8 ? up : left);
-    const pel *pp_ = !pav ? &s.rec[0] : py < 0 ? &s.nb.rtop[px + 1] : px < 0 ? &s.nb.rleft[py] : &s.rec[16 * py + px];
-    const int v = pav ? (int)*pp_ : 0;
-    const int upM = by > 0 ? s.ipred_cur[blk - 4] : s.bd.ipm[1 + bx4];
-    const int leftM = bx > 0 ? s.ipred_cur[blk - 1] : s.bd.ipm[6 + by4];
-    const int mpm = (upM < 0 || leftM < 0) ? 2 : min(upM, leftM);
-    const int m = lane >> 2, y = lane & 3;
-    int o[4];
-#pragma unroll
-    for (int x = 0; x < 4; x++) o[x] = s.org[(by + y) * 16 + bx + x];
-    const int org = s.org[(by + (l >> 2)) * 16 + bx + (l & 3)];   // the TQ lanes' sample
-    int st = 0, sl = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) { st += __builtin_amdgcn_readlane(v, 1 + i); sl += __builtin_amdgcn_readlane(v, 9 + i); }
-    const int dc = (up && left) ? (st + sl + 4) >> 3 : left ? (sl + 2) >> 2 : up ? (st + 2) >> 2 : (d.maxv + 1) >> 1;
-    I4ST(53, mpm);
-    int pr[4], dd[4];
-#pragma unroll
-    for (int x = 0; x < 4; x++) {
-        const int e = (int)(((uint32_t)tabr[x >> 1] >> (16 * (x & 1))) & 0xFFFFu), ty = e & 3;
-        const int a = __shfl(v, (e >> 2) & 15, 64), b = __shfl(v, (e >> 6) & 15, 64), c = __shfl(v, (e >> 10) & 15, 64);
-        pr[x] = ty == 1 ? (a + b + 1) >> 1 : ty == 2 ? (a + 2 * b + c + 2) >> 2 : dc;
-        dd[x] = o[x] - pr[x];
-    }
-    int t;
-    if (had) {
-        const int h0 = dd[0] + dd[1], h1 = dd[0] - dd[1], h2 = dd[2] + dd[3], h3 = dd[2] - dd[3];
-        int g[4] = {h0 + h2, h1 + h3, h0 - h2, h1 - h3};
-#pragma unroll
-        for (int x = 0; x < 4; x++) { const int q = dpp<0xB1>(g[x]); g[x] = (y & 1) ? q - g[x] : g[x] + q; }
-#pragma unroll
-        for (int x = 0; x < 4; x++) { const int q = dpp<0x4E>(g[x]); g[x] = (y & 2) ? q - g[x] : g[x] + q; }
-        t = abs(g[0]) + abs(g[1]) + abs(g[2]) + abs(g[3]);
-    } else {
-        t = abs(dd[0]) + abs(dd[1]) + abs(dd[2]) + abs(dd[3]);
-    }
-    t += dpp<0xB1>(t);                        // the quad's rows
-    t += dpp<0x4E>(t);
-    const int sat = had ? t >> 1 : t;
-    const bool avm = m == 2 || ((m == 0 || m == 3 || m == 7) && up) || ((m == 1 || m == 8) && left) || (up && left && ul);
-    const int cst = (m < 9 && avm) ? (m == mpm ? 0 : 4 * lambda) + sat : BIGCOST;
-    const unsigned key = wave_min_u32((y == 0 && cst < BIGCOST) ? ((unsigned)cst << 4) | (unsigned)m : 0xFFFFFFFFu);
-    I4ST(54, key);
-    const int best = key == 0xFFFFFFFFu ? 0 : (int)(key & 15u), bc = key == 0xFFFFFFFFu ? BIGCOST : (int)(key >> 4);
-    // the winner's prediction at TQ lane l (raster 4y' + x'): register x' of lane 4 best + y'
-    const int srcl = 4 * best + (l >> 2);
-    const int q01 = __shfl((pr[0] & 0xFFFF) | (pr[1] << 16), srcl, 64), q23 = __shfl((pr[2] & 0xFFFF) | (pr[3] << 16), srcl, 64);
-    const int qx = (l & 2) ? q23 : q01;
-    const int pp = (l & 1) ? (int)((uint32_t)qx >> 16) : (qx & 0xFFFF);
-    I4ST(55, pp);
-    unsigned nz = 0;
-    if (lane < 16) {
-        const int c = quad_fwd4x4(org - pp, l);
-        int lev, dq, cc;
-        nz = lane_quant(c, l, qp, qpk, false, lev, dq, cc);
-        I4ST(56, dq);
-        scr->i4lev[blk][l] = (int16_t)lev;
-        s.rec[(by + (l >> 2)) * 16 + bx + (l & 3)] = (pel)quad_inv4x4(dq, l, pp, d.maxv);
-        if (l == 0) s.ipred_cur[blk] = (int8_t)best;
-    }
-    nz = __builtin_amdgcn_readlane(nz, 0);
-    I4ST(57, nz);
-#undef I4ST
-    acc[0] += bc;
-    if (nz) { acc[1] |= 1 << ((by4 >> 1) * 2 + (bx4 >> 1)); acc[2] |= 1 << blk; }
-}
-
 // one MB on 128 threads (tid = 0..127, waves 0 and 1 of the group); every thread of the
 // workgroup reaches the same barriers (act: the group has an MB)
 template <class pel>
@@ -1105,6 +967,8 @@ __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &
 // intra-mode decisions, so that no intra workgroup runs for a P picture's MBs
 __device__ __forceinline__ void intra_wave(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int mbx, int mby) {
     const int lane = __lane_id();
+    const bool prof = prof_mb_here(d, mbx, mby, NTS / 64);   // debug (JMH_PHASE_PROF): stamps 60..62
+    PSTAMP(60);
     const MbAvail mav = mb_avail(d, mbx, mby);
     const int qpk = q_round(d.qsel, 15 + d.qp / 6);
     int tabr[2];
@@ -1121,8 +985,10 @@ __device__ __forceinline__ void intra_wave(const DevParams &d, IntraS<uint8_t> &
     }
     if (lane < 16) scr->ipred[lane] = s.ipred_cur[lane];
     reinterpret_cast<uint32_t *>(scr->i4rec)[lane] = reinterpret_cast<const uint32_t *>(s.rec)[lane];
+    PSTAMP(61);
     i16_decision(d, s.org, s.nb, scr, lane, mav.L, mav.T, mav.TL);
     chroma_decision(d, s.nb, scr, lane, mav.L, mav.T, mav.TL);
+    PSTAMP(62);
 }
 
 __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {

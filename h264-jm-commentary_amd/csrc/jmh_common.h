@@ -170,25 +170,56 @@ __device__ __forceinline__ void wave_lds_sync() {
 // ======================================================================================
 __device__ __forceinline__ int g16(int v, int src) { return __shfl(v, (int)(threadIdx.x & 48) + src, 64); }
 
+// The output of a 4x4 butterfly stage at position k (a lane's x or y) is one expression with per-lane coefficients: a ?: chain
+// over four different sums compiles to divergent branches.
+//   forward, position k of (p0, p1, p2, p3) = (v0 + v3, v1 + v2, v1 - v2, v0 - v3):
+//     k 0: p0 + p1, 1: 2 p3 + p2, 2: p0 - p1, 3: p3 - 2 p2  =  ca * (k odd ? p3 : p0) + cb * (k odd ? p2 : p1)
+__device__ __forceinline__ int fwd_tap(int p0, int p1, int p2, int p3, int k) {
+    const int a = (k & 1) ? p3 : p0, b = (k & 1) ? p2 : p1;
+    const int ca = k == 1 ? 2 : 1, cb = k < 2 ? 1 : k == 2 ? -1 : -2;
+    return ca * a + cb * b;
+}
+//   inverse, (e0, e1, e2, e3) = (d0 + d2, d0 - d2, (d1 >> 1) - d3, d1 + (d3 >> 1)):
+//     k 0: e0 + e3, 1: e1 + e2, 2: e1 - e2, 3: e0 - e3  =  (k 0/3 ? e0 : e1) +- (k 0/3 ? e3 : e2)
+__device__ __forceinline__ int inv_tap(int e0, int e1, int e2, int e3, int k) {
+    const bool outer = k == 0 || k == 3;
+    const int a = outer ? e0 : e1, b = outer ? e3 : e2;
+    return k < 2 ? a + b : a - b;
+}
+#ifndef JMH_LANE_TAPS
+#define JMH_LANE_TAPS 1                       // A/B: 0 = the ?: chains in lane_fwd4x4 / lane_inv4x4
+#endif
 // forward 4x4 core transform (dct_luma [J]): rows then columns
 __device__ __forceinline__ int lane_fwd4x4(int r, int l) {
     int y = l >> 2, x = l & 3;
     int v0 = g16(r, 4 * y), v1 = g16(r, 4 * y + 1), v2 = g16(r, 4 * y + 2), v3 = g16(r, 4 * y + 3);
     int p0 = v0 + v3, p3 = v0 - v3, p1 = v1 + v2, p2 = v1 - v2;
+#if JMH_LANE_TAPS
+    const int t = fwd_tap(p0, p1, p2, p3, x);
+    const int u0 = g16(t, x), u1 = g16(t, 4 + x), u2 = g16(t, 8 + x), u3 = g16(t, 12 + x);
+    return fwd_tap(u0 + u3, u1 + u2, u1 - u2, u0 - u3, y);
+#else
     int t = x == 0 ? p0 + p1 : x == 1 ? 2 * p3 + p2 : x == 2 ? p0 - p1 : p3 - 2 * p2;
     int u0 = g16(t, x), u1 = g16(t, 4 + x), u2 = g16(t, 8 + x), u3 = g16(t, 12 + x);
     p0 = u0 + u3; p3 = u0 - u3; p1 = u1 + u2; p2 = u1 - u2;
     return y == 0 ? p0 + p1 : y == 1 ? 2 * p3 + p2 : y == 2 ? p0 - p1 : p3 - 2 * p2;
+#endif
 }
 // inverse 4x4 (8.5.12.2, rows first) + reconstruction clip((x + (pred << 6) + 32) >> 6) to maxv
 __device__ __forceinline__ int lane_inv4x4(int dq, int l, int pred, int maxv = 255) {
     int y = l >> 2, x = l & 3;
     int d0 = g16(dq, 4 * y), d1 = g16(dq, 4 * y + 1), d2 = g16(dq, 4 * y + 2), d3 = g16(dq, 4 * y + 3);
     int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+#if JMH_LANE_TAPS
+    const int t = inv_tap(e0, e1, e2, e3, x);
+    const int f0 = g16(t, x), f1 = g16(t, 4 + x), f2 = g16(t, 8 + x), f3 = g16(t, 12 + x);
+    const int o = inv_tap(f0 + f2, f0 - f2, (f1 >> 1) - f3, f1 + (f3 >> 1), y);
+#else
     int t = x == 0 ? e0 + e3 : x == 1 ? e1 + e2 : x == 2 ? e1 - e2 : e0 - e3;
     int f0 = g16(t, x), f1 = g16(t, 4 + x), f2 = g16(t, 8 + x), f3 = g16(t, 12 + x);
     e0 = f0 + f2; e1 = f0 - f2; e2 = (f1 >> 1) - f3; e3 = f1 + (f3 >> 1);
     int o = y == 0 ? e0 + e3 : y == 1 ? e1 + e2 : y == 2 ? e1 - e2 : e0 - e3;
+#endif
     return iclip(0, maxv, (o + (pred << 6) + 32) >> 6);
 }
 // quantisation rounding offset at q_bits (docs/JM_SEMANTICS.md items 1 and 45; oracle jmo_qround):
@@ -206,11 +237,19 @@ __device__ __forceinline__ unsigned lane_quant(int c, int l, int qp, int qp_cons
     const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 15 + qp_per;
     const int x = l & 3, y = l >> 2;
     const int cls = ((x | y) & 1) == 0 ? 0 : ((x & y) & 1) ? 1 : 2;
-    const int qc = cls == 0 ? c_q3[qp_rem][0] : cls == 1 ? c_q3[qp_rem][1] : c_q3[qp_rem][2];
-    const int dqc = cls == 0 ? c_dq3[qp_rem][0] : cls == 1 ? c_dq3[qp_rem][1] : c_dq3[qp_rem][2];
+    // the three scalings of qp_rem as wave-uniform values (scalar loads), then a per-lane select:
+    // without the readfirstlane the compiler folds the select into a per-lane indexed load, a
+    // vector memory round trip inside every block's dependent chain
+    const int q0 = __builtin_amdgcn_readfirstlane(c_q3[qp_rem][0]), q1 = __builtin_amdgcn_readfirstlane(c_q3[qp_rem][1]);
+    const int q2 = __builtin_amdgcn_readfirstlane(c_q3[qp_rem][2]);
+    const int d0 = __builtin_amdgcn_readfirstlane(c_dq3[qp_rem][0]), d1 = __builtin_amdgcn_readfirstlane(c_dq3[qp_rem][1]);
+    const int d2 = __builtin_amdgcn_readfirstlane(c_dq3[qp_rem][2]);
+    const int qc = cls == 0 ? q0 : cls == 1 ? q1 : q2;
+    const int dqc = cls == 0 ? d0 : cls == 1 ? d1 : d2;
     int level = (abs(c) * qc + qp_const) >> q_bits;
     if (ac_only && l == 0) level = 0;
-    dq = level ? isign(level * dqc << qp_per, c) : 0;
+    const int dqm = level * dqc << qp_per;    // |level| x scale: the sign of c, 0 for a zero level
+    dq = c < 0 ? -dqm : dqm;
     const int sr = scan_of(l);
     const int lvs = g16(level, sr), cs = g16(c, sr);
     const unsigned long long bal = __ballot(lvs != 0);

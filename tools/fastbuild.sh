@@ -8,7 +8,7 @@ DEFS=${DEFS:-}
 OUT=${OUT:-libjmhip.so}
 OBJ=.obj/$(echo "$DEFS" | tr -c 'A-Za-z0-9_=\n' '_' )
 mkdir -p "$OBJ"
-HDRS="jmh_device.h jmh_common.h jmh_epzs.h jmh_intra.h jmh_deblock.h jmh_intra8.h jmh_cabac_rate.h jmh_cavlc_rate.h jmh_final.h jmh_cabac_tables.h ../../include/jmhip.h"
+HDRS="jmh_device.h jmh_common.h jmh_epzs.h jmh_intra.h jmh_i4.h jmh_deblock.h jmh_intra8.h jmh_cabac_rate.h jmh_cavlc_rate.h jmh_final.h jmh_cabac_tables.h ../../include/jmhip.h"
 pids=()
 for f in jmh_kernels jmh_analyse jmh_fullsearch jmh_epzs jmh_intra8 jmh_final jmh_block jmh_hbd jmh_rdo jmhip_abi; do
   o=$OBJ/$f.o
