@@ -124,8 +124,31 @@ __device__ __forceinline__ int coeff_cost_run(int run) { return run == 0 ? 3 : r
 // ---- cross-lane helpers ----------------------------------------------------------------
 // DPP lane moves: quad_perm [1,0,3,2] (0xB1), [2,3,0,1] (0x4E), [3,2,1,0] (0x1B),
 // row_half_mirror (0x141), row_mirror (0x140), row_ror:8 (0x128) — all within a 16-lane row
+// A disabled source lane reads 0 (bound_ctrl): with that (or an identity old value, dpp_umin)
+// the compiler folds the move into the consuming v_add / v_sub / v_min as a DPP operand, one
+// instruction instead of a copy, a v_mov_dpp and the operation.  Every caller runs its rows fully
+// active (a lane's result is used only where every lane its reduction reads was active).
+#ifndef JMH_DPP_FOLD
+#define JMH_DPP_FOLD 1                        // A/B: 0 = the earlier update_dpp(v, v) moves
+#endif
 template <int CTRL>
-__device__ __forceinline__ int dpp(int v) { return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp(int v) {
+#if JMH_DPP_FOLD
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+#else
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false);
+#endif
+}
+// min(v, v of the DPP source lane) with 0xFFFFFFFF as the old value: folds into v_min_u32_dpp, and
+// a disabled source lane leaves v unchanged
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_umin(unsigned v) {
+#if JMH_DPP_FOLD
+    return min(v, (unsigned)__builtin_amdgcn_update_dpp(-1, (int)v, CTRL, 0xF, 0xF, false));
+#else
+    return min(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false));
+#endif
+}
 // sum over each aligned 16-lane row (all 16 lanes must be active); every lane gets the sum
 __device__ __forceinline__ int row16_sum(int v) {
     v += dpp<0xB1>(v);
@@ -150,10 +173,10 @@ __device__ __forceinline__ int row16_had(int v, int l) {
 }
 // minimum over the whole (fully active) wave, wave-uniform result
 __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
-    v = min(v, (unsigned)dpp<0xB1>((int)v));
-    v = min(v, (unsigned)dpp<0x4E>((int)v));
-    v = min(v, (unsigned)dpp<0x141>((int)v));
-    v = min(v, (unsigned)dpp<0x140>((int)v));
+    v = dpp_umin<0xB1>(v);
+    v = dpp_umin<0x4E>(v);
+    v = dpp_umin<0x141>(v);
+    v = dpp_umin<0x140>(v);
     unsigned a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
     unsigned c = __builtin_amdgcn_readlane(v, 32), e = __builtin_amdgcn_readlane(v, 48);
     return min(min(a, b), min(c, e));
