@@ -185,11 +185,7 @@ struct SDesc {
 // from the full-pel position; wbase = window offset of the sub-block's top-left sample there.
 // One lane does the whole block: rows of 4 samples as dwords (two aligned LDS reads +
 // v_alignbyte per plane), the rounding average of the two planes per byte.
-__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t *p) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
-}
+__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t *p) { return lds_u32_any(p); }
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s16x2 as_s2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -313,7 +309,11 @@ __device__ __forceinline__ void subpel_wave(const DevParams &d, MeS &s, int j, c
     const unsigned order = best & 8191u;
     int rx, ry;
     if (order == 0) { rx = -scx; ry = -scy; }
-    else spiral_pos((int)order - 1, rx, ry);
+    else {   // spiral index -> position from the context's table (a scalar load, no sqrt)
+        const uint32_t e = d.ordtab[ORDTAB_SPOS + order - 1];
+        rx = (int)(int16_t)(e & 0xFFFFu);
+        ry = (int)e >> 16;
+    }
     const int fmx = scx + rx, fmy = scy + ry;
     int min_mcost = had ? BIGCOST : (int)(best >> 13);
     const int lw4 = lw4_of(q.bt), lns = lw4 + lh4_of(q.bt), nsub = 1 << lns;
@@ -1075,3 +1075,16 @@ hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }
+
+#ifdef JMH_ISA_PROBE
+// ISA inspection only (hipcc -DJMH_ISA_PROBE -S): one sub-pel search of a 4x4 and of an 8x8 block
+__global__ __launch_bounds__(NTA, 4) void k_probe_subpel(const TickArgs t, int j) {
+    __shared__ MeS s;
+    const DevParams d = tick_params(t, 0);
+    const SDesc q4 = {7, 1, 0, 0, 7, 0, 1, 0}, q8 = {4, 0, 0, 0, 0, 0, 0, 0};
+    if (j) subpel_wave(d, s, 0, q4, t.W, t.H, 3, -2, 0, 0);
+    else subpel_wave(d, s, 0, q8, t.W, t.H, 3, -2, 0, 0);
+    __syncthreads();
+    if (threadIdx.x < 64) d.mv[threadIdx.x] = s.all_mv[j ? 7 : 4][threadIdx.x & 15][threadIdx.x >> 4 & 1] + s.motion_cost[4][0] + s.pmv[0][0];
+}
+#endif

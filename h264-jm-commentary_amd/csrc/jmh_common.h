@@ -121,6 +121,18 @@ __device__ __forceinline__ void spiral_pos(int k, int &x, int &y) {
 // COEFF_COST [J] of a |level| == 1 coefficient by preceding zero run
 __device__ __forceinline__ int coeff_cost_run(int run) { return run == 0 ? 3 : run <= 2 ? 2 : run <= 5 ? 1 : 0; }
 
+// 4 bytes at any byte address of LDS: two aligned LDS dwords + v_alignbyte.  The pointer is cast
+// to the LDS address space before its low bits are taken: through a generic integer the reads
+// become flat loads (the vector memory path, waited on with vmcnt) instead of one ds_read2_b32.
+// Every caller passes an LDS address.
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+__device__ __forceinline__ uint32_t lds_u32_any(const void *p) {
+    const uint32_t a = (uint32_t)(uintptr_t)(lds_cu8 *)p;
+    lds_cu32 *q = (lds_cu32 *)(uintptr_t)(a & ~3u);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], a & 3);
+}
+
 // ---- cross-lane helpers ----------------------------------------------------------------
 // DPP lane moves: quad_perm [1,0,3,2] (0xB1), [2,3,0,1] (0x4E), [3,2,1,0] (0x1B),
 // row_half_mirror (0x141), row_mirror (0x140), row_ror:8 (0x128) — all within a 16-lane row

@@ -21,6 +21,7 @@
 #define NPK (JMH_I4WAVE ? 11 : 10)       // FFS search positions per search thread (a column strip):
                                          //   65 x ceil(65 / NPK) strips <= NTS
 #define NPK2 ((NPK + 1) / 2)             // packed order-key pairs per thread
+#define ORDTAB_SPOS (NPK2 * NTA)         // ordtab: the spiral-index -> position table after the keys
 #define BIGCOST (1 << 20)
 #define PMAX 33                          // pictures per wavefront tick (pipelined pictures in flight;
                                          // 2160p needs 508 / PIPE_LAG + 1 = 33)

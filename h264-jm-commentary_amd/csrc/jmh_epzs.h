@@ -89,11 +89,7 @@ struct NbEpz {
     }
 };
 
-__device__ __forceinline__ uint32_t eld_u32(const void *p) {   // 4 bytes at any LDS address
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
-}
+__device__ __forceinline__ uint32_t eld_u32(const void *p) { return lds_u32_any(p); }   // 4 bytes at any LDS address
 
 // the LDS window: picture position of its sample (0, 0) and window position of the MB origin
 template <class pel>

@@ -73,11 +73,7 @@ struct NbFull {
     }
 };
 
-__device__ __forceinline__ uint32_t lds_u32(const void *p) {   // 4 bytes at any LDS address
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
-}
+__device__ __forceinline__ uint32_t lds_u32(const void *p) { return lds_u32_any(p); }   // 4 bytes at any LDS address
 
 // workgroup minimum of per-thread keys (double-buffered slot: consecutive calls need no second
 // barrier); every thread returns the minimum

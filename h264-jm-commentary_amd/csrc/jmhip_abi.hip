@@ -488,11 +488,15 @@ static int host_spiral_index(int x, int y) {
 // order keys of the FFS analysis threads (k_mb_analyse): thread t owns window column t % side,
 // rows (t / side) * NPK .. + NPK - 1; key = spiral index + 1 (0 is the (0,0) pre-check, set per
 // MB in the kernel), 0xFFFF outside the window.  [NPK2][NTA] packed pairs (low = even slot); only
-// the NTS search threads own strips.
+// the NTS search threads own strips.  Then the inverse, ORDTAB_SPOS: spiral index -> position
+// (x & 0xFFFF | y << 16), read with one scalar load where a search's winner is decoded.
 static void ordtab_fill(std::vector<uint32_t> &tab, int sr) {
     const int side = 2 * sr + 1, nstrips = (side + NPK - 1) / NPK;
     static_assert(SIDE_MAX * ((SIDE_MAX + NPK - 1) / NPK) <= NTS, "the search threads cover every FFS position");
-    tab.assign((size_t)NPK2 * NTA, 0);
+    tab.assign((size_t)ORDTAB_SPOS + (size_t)side * side, 0);
+    for (int y = -sr; y <= sr; y++)
+        for (int x = -sr; x <= sr; x++)
+            tab[(size_t)ORDTAB_SPOS + host_spiral_index(x, y)] = ((uint32_t)x & 0xFFFFu) | (uint32_t)y << 16;
     for (int t = 0; t < NTA; t++) {
         const bool sact = t < side * nstrips && t < NTS;
         const int dx = sact ? t % side : 0, dy0 = sact ? (t / side) * NPK : 0;
