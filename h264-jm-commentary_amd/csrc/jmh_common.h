@@ -538,6 +538,20 @@ static __constant__ uint8_t c_scan8[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 2
                                            12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
                                            35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                            58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+// the same as immediates (no memory access: the index varies across lanes), eight per qword
+__device__ __forceinline__ int scan8_of(int l) {
+    const int g = l >> 3;
+    const uint64_t q = g < 4 ? (g < 2 ? (g == 0 ? 0x0a03020910080100ull : 0x05040b1219201811ull) : (g == 2 ? 0x22293028211a130cull : 0x1c150e07060d141bull))
+                             : (g < 6 ? (g == 4 ? 0x242b323938312a23ull : 0x332c251e170f161dull) : (g == 6 ? 0x2e271f262d343b3aull : 0x3f3e372f363d3c35ull));
+    return (int)((q >> (8 * (l & 7))) & 63);
+}
+// one of six per-class values of a wave-uniform table row (scalar loads + a per-lane select)
+__device__ __forceinline__ int pick6(const int *row, int cls) {
+    const int a0 = __builtin_amdgcn_readfirstlane(row[0]), a1 = __builtin_amdgcn_readfirstlane(row[1]);
+    const int a2 = __builtin_amdgcn_readfirstlane(row[2]), a3 = __builtin_amdgcn_readfirstlane(row[3]);
+    const int a4 = __builtin_amdgcn_readfirstlane(row[4]), a5 = __builtin_amdgcn_readfirstlane(row[5]);
+    return cls < 3 ? (cls == 0 ? a0 : cls == 1 ? a1 : a2) : (cls == 3 ? a3 : cls == 4 ? a4 : a5);
+}
 // COEFF_COST8x8 [J] of a |level| == 1 coefficient by preceding zero run (64-scan)
 __device__ __forceinline__ int coeff_cost8_run(int run) { return run < 4 ? 3 : run < 12 ? 2 : run < 24 ? 1 : 0; }
 
@@ -608,11 +622,11 @@ __device__ __forceinline__ int wave_inv8x8(int dq, int l, int pred, int maxv = 2
 __device__ __forceinline__ unsigned long long wave_quant8(int c, int l, int qp, int qp_const, int &lev_scan, int &dq, int &cost) {
     const int qp_per = qp / 6, qp_rem = qp % 6, q_bits = 16 + qp_per;
     const int cls = class8(l & 7, l >> 3);
-    const int level = (abs(c) * c_q8[qp_rem][cls] + qp_const) >> q_bits;
+    const int level = (abs(c) * pick6(c_q8[qp_rem], cls) + qp_const) >> q_bits;
     const int sl = c < 0 ? -level : level;
-    const int ls = 16 * c_dq8[qp_rem][cls];
+    const int ls = 16 * pick6(c_dq8[qp_rem], cls);
     dq = !level ? 0 : qp >= 36 ? sl * ls * (1 << (qp_per - 6)) : (sl * ls + (1 << (5 - qp_per))) >> (6 - qp_per);
-    const int lvs = w64(sl, c_scan8[l]);
+    const int lvs = w64(sl, scan8_of(l));
     const unsigned long long m = __ballot(lvs != 0);
     int k = 0;
     if (lvs) {

@@ -191,8 +191,15 @@ __device__ __forceinline__ bool epzs_cand(const DevParams &d, const S &s, int i,
 }
 
 // offsets (dx + 4) | (dy + 4) << 4 of the 41 positions with |dx| + |dy| <= 4 (refinement batches)
-static __constant__ uint8_t c_dia41[41] = {4,  19, 20, 21, 34, 35, 36, 37, 38, 49, 50, 51, 52, 53, 54, 55, 64, 65, 66, 67, 68,
-                                           69, 70, 71, 72, 81, 82, 83, 84, 85, 86, 87, 98, 99, 100, 101, 102, 115, 116, 117, 132};
+// the 41 points with |dx| + |dy| <= 4 in raster order, (dy + 4) << 4 | (dx + 4), from the lane
+// index by arithmetic (a per-lane table read is a vector memory round trip in every batch): row r
+// (dy = r - 4) of the diamond starts after 0, 1, 4, 9, 16, 25, 32, 37, 40 points and its centre
+// (dx = 0) is point 0, 2, 6, 12, 20, 28, 34, 38, 40 (6 bits each below)
+__device__ __forceinline__ int dia41(int L) {
+    const int r = (L >= 1) + (L >= 4) + (L >= 9) + (L >= 16) + (L >= 25) + (L >= 32) + (L >= 37) + (L >= 40);
+    const int dx = L - (int)((0x289a2714306080ull >> (6 * r)) & 63);
+    return r << 4 | (dx + 4);
+}
 
 // refinement pattern point e: small diamond (0,-1) (-1,0) (1,0) (0,1); extended diamond (0,-2)
 // (-1,-1) (1,-1) (-2,0) (2,0) (-1,1) (1,1) (0,2) then the small diamond
@@ -478,7 +485,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
             // scans them (pattern order, strict '<', window check); then a new batch.
             const bool sd = min_mcost < stop + ((3 * stop) >> 1);
             const int steps = sd ? 4 : 2;
-            const int dia = lane < 41 ? (int)c_dia41[lane] : 0x44;
+            const int dia = lane < 41 ? dia41(lane) : 0x44;
             const int ddx = (dia & 15) - 4, ddy = (dia >> 4) - 4;
             auto refine = [&](int &rbx, int &rby, int &rcost) {
                 for (bool done = false; !done;) {
