@@ -460,7 +460,7 @@ def main():
     pictures = max(1, tm.pictures)
     an_per_pic = tm.ticks / pictures                     # one k_mb_analyse + one k_mb_final per tick
     mb_ms_pic = tm.mb_ms / pictures
-    # the sampled launches' HIP events (every 8th tick) add a few us per launch; the wavefront
+    # the sampled launches' HIP events (every 32nd tick) add a few us per launch; the wavefront
     # brackets (one event pair per run of ticks) do not.  The per-launch figures are scaled so that
     # the sampled launches of a tick sum to the bracketed wavefront time per tick (never above it):
     # k_mb_analyse 93.8 us raw vs 90.0 us in rocprof's kernel trace (profiles/r6h_*)
@@ -561,7 +561,7 @@ def main():
                     "pictures in flight are not drained); exactly `steps` pictures complete inside",
         },
         "roofline": roofline,
-        # per-launch averages (sampled every 8th tick, scaled to the bracketed wavefront time: see
+        # per-launch averages (sampled every 32nd tick, scaled to the bracketed wavefront time: see
         # ev_scale) x launches per picture; RDO on: the span of a tick's three RD launches
         "kernel_ms_per_picture": {"wavefront": round(mb_ms_pic, 4),
                                   an_name + (" (tick span)" if RDO else ""): round(an_launch_ms * an_per_pic, 4),

@@ -56,7 +56,7 @@ static int q_selector(const jmh_config &cfg, bool i_slice) {
 
 // JMH_FLAG_KERNEL_TIMING brackets every KT_STRIDE-th tick's two launches with events: the
 // averages are sampled uniformly while the event packets stay off most launches
-#define KT_STRIDE 8
+#define KT_STRIDE 32                      // an event pair between two launches costs ~7 us on that tick
 // ring of begin/end event pairs; completed pairs are folded into `sum` (ms)
 struct EvRing {
     std::vector<hipEvent_t> a, b;
