@@ -1,0 +1,27 @@
+#!/usr/bin/env python3
+"""Fold a PMC pass summary (tools/pmc_parse.py output, committed under profiles/) into
+tools/pmc_traffic.json, the record bench.py prices its roofline traffic and VALU issue with.
+    python tools/pmc_update.py KEY profiles/TAG_pmc.json "bench args of the pass"
+KEY: "2", "3", "5" or "5t8"."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+key, path, args = sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else ""
+p = json.load(open(path))
+t = json.load(open(os.path.join(ROOT, "tools", "pmc_traffic.json")))
+c = t["configs"][key]
+roof = p["roofline_kernels"]
+c["tag"] = p["tag"]
+c["kernel"] = " + ".join(k.replace("void ", "").split("<")[0] for k in roof)
+c["source"] = (f"{os.path.relpath(path, ROOT)} (tools/pmc_traffic.sh {p['tag']}{' ' + args if args else ''}: rocprofv3 --pmc "
+               f"FETCH_SIZE and WRITE_SIZE in separate passes over bench.py, 1 IDR + {p['pictures']['p']} P pictures, "
+               f"FETCH_SIZE doubled per the MI355X guide's gfx950 correction)")
+c["hbm_bytes_per_mb"] = p["roofline_hbm_bytes_per_mb"]
+if len(roof) > 1:
+    c["per_kernel_hbm_bytes_per_mb"] = {k: p["kernels"][k]["hbm_bytes_per_mb"] for k in roof}
+c["valu_insts_per_mb"] = p["roofline_valu_insts_per_mb"]
+c["valu_kernels"] = {k: p["kernels"][k]["insts_per_mb"]["SQ_INSTS_VALU"] for k in roof}
+json.dump(t, open(os.path.join(ROOT, "tools", "pmc_traffic.json"), "w"), indent=1)
+print(key, c["hbm_bytes_per_mb"], c["valu_insts_per_mb"])
