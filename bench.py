@@ -61,13 +61,13 @@ CONFIGS = {
                      "(one independent stream per GPU)"),
     3: dict(metric="ME+transform megapixels/sec @2160p High EPZS SR=32 + 8x8 transform (config 3); " + TIMER, disp=(3840, 2160),
             coded=(3840, 2160), search_mode=3, t8=1,
-            workload="2160p synthetic YUV420, High profile (ProfileIDC 100), EPZS SearchMode=3 SearchRange=32, "
+            workload="2160p synthetic YUV420, High profile (ProfileIDC 100), {sm} SearchRange=32, "
                      "Transform8x8Mode=1 (Intra8x8 + TransformDecision), UseHadamard=1, 7 inter block sizes, RDO off, "
                      "QP 28, IDR + {nf}-picture P sequence cycled (one independent stream per GPU)"),
     5: dict(metric="ME+transform+RD megapixels/sec @2160p High10 10-bit EPZS SR=32, CABAC RDO on, 240-MB slices (config 5); "
                    + TIMER,
             disp=(3840, 2160), coded=(3840, 2160), search_mode=3, t8=0, bd=10, slice_mbs=240, rdo=1,
-            workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), EPZS SearchMode=3 "
+            workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), {sm} "
                      "SearchRange=32, UseHadamard=1, 7 inter block sizes, RDOptimization=1 with SymbolMode=1 (the CABAC "
                      "rate of every candidate on the device), Transform8x8Mode=0, QP 28, IDR + {nf}-picture P sequence "
                      "cycled (one independent stream per GPU)"),
@@ -75,7 +75,7 @@ CONFIGS = {
 # --config 5 --rdo 0: the RDO-off variant of config 5's shape (EPZS + 8x8 transform)
 CONFIG5_RDO_OFF = dict(metric="ME+transform megapixels/sec @2160p High10 10-bit EPZS SR=32 + 8x8 transform, 240-MB slices, "
                               "RDO off (config 5 variant); " + TIMER, t8=1, rdo=0,
-                       workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), EPZS SearchMode=3 "
+                       workload="2160p synthetic YUV420 10-bit (16-bit samples), High 10 (ProfileIDC 110), {sm} "
                                 "SearchRange=32, Transform8x8Mode=1, UseHadamard=1, 7 inter block sizes, RDO off, QP 28, "
                                 "IDR + {nf}-picture P sequence cycled (one independent stream per GPU)")
 RDO = 0              # RDOptimization of the run (the config's, or --rdo)
@@ -410,6 +410,9 @@ def main():
         cfg["t8"] = args.t8
     SLICE_MBS = max(0, cfg.get("slice_mbs", 0) if args.slice_mbs is None else args.slice_mbs)
     search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
+    if search_mode != cfg["search_mode"]:   # the metric names the search the line measured
+        sm_label = {0: "FFS", -1: "FullSearch", 3: "EPZS"}
+        cfg["metric"] = cfg["metric"].replace(sm_label[cfg["search_mode"]], sm_label[search_mode], 1)
     if args.epzs_jm10:
         if search_mode != 3:
             ap.error("--epzs-jm10 applies to EPZS (SearchMode 3)")
