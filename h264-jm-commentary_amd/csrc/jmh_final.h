@@ -119,6 +119,28 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
     }
     __syncthreads();
 
+    // ======== chroma prediction, ahead of the luma (JMH_FINAL_CPRED_EARLY): the inter prediction's
+    // reference reads then travel with the luma MC's instead of one round trip after them
+    const int c_mode = is_intra ? sc->c_mode : 0;
+    const int cuv = (tid >> 4) >> 2, cb = (tid >> 4) & 3;
+    const int cxo = (cb & 1) * 4 + (tid & 3), cyo = (cb >> 1) * 4 + ((tid & 15) >> 2);
+    int cpredv = 0;
+    if (tid < 128) {
+        if (is_intra) {
+            cpredv = chroma_pred_px(s.ctop[cuv] + 1, s.cleft[cuv], s.ctop[cuv][0], avT, avL, c_mode, cxo, cyo, maxv);
+        } else {
+            // OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2
+            const pel *R = cuv ? refV : refU;
+            const int vx = s.fmv[(cyo >> 1) * 4 + (cxo >> 1)][0], vy = s.fmv[(cyo >> 1) * 4 + (cxo >> 1)][1];
+            const int ii = ((pix_x >> 1) + cxo) * 8 + vx, jj = ((pix_y >> 1) + cyo) * 8 + vy;
+            const int x0 = iclip(0, Wc - 1, ii >> 3), y0 = iclip(0, d.Hc - 1, jj >> 3);
+            const int x1 = iclip(0, Wc - 1, (ii + 7) >> 3), y1 = iclip(0, d.Hc - 1, (jj + 7) >> 3);
+            const int fx = ii & 7, fy = jj & 7;
+            cpredv = ((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] + (8 - fx) * fy * R[y1 * Wc + x0] +
+                      fx * fy * R[y1 * Wc + x1] + 32) >> 6;
+        }
+    }
+
     // ======== luma residual coding: 16 blocks x 16 lanes
     int cbp = 0, cbp_blk = 0;
     bool tr8 = false;                                                 // 8x8 transform
@@ -223,29 +245,13 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
     PSTAMP(17);
 
     // ======== chroma: prediction (intra mode from k_mb_analyse, or MC) + dct_chroma [J]
-    const int c_mode = is_intra ? sc->c_mode : 0;
     // QPc of qPI = Clip3(-QpBdOffsetC, 51, QPY + chroma_qp_index_offset) (8.5.8, Table 8-15:
     // negative qPI map to themselves), quantised at QP'c = QPc + QpBdOffsetC
     const int qpi = iclip(-d.qpbd, 51, qpy + d.cqp_off), qpcy = qpi < 0 ? qpi : c_qpc[qpi], qpc = qpcy + d.qpbd;
     const int cq_bits = 15 + qpc / 6;
     const int cqp_const = q_round(d.qsel, cq_bits);
-    const int cuv = blk >> 2, cb = blk & 3;
-    const int cxo = (cb & 1) * 4 + lx, cyo = (cb >> 1) * 4 + ly;
-    int cdq = 0, cpredv = 0;
+    int cdq = 0;
     if (tid < 128) {
-        if (is_intra) {
-            cpredv = chroma_pred_px(s.ctop[cuv] + 1, s.cleft[cuv], s.ctop[cuv][0], avT, avL, c_mode, cxo, cyo, maxv);
-        } else {
-            // OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2
-            const pel *R = cuv ? refV : refU;
-            const int vx = s.fmv[(cyo >> 1) * 4 + (cxo >> 1)][0], vy = s.fmv[(cyo >> 1) * 4 + (cxo >> 1)][1];
-            const int ii = ((pix_x >> 1) + cxo) * 8 + vx, jj = ((pix_y >> 1) + cyo) * 8 + vy;
-            const int x0 = iclip(0, Wc - 1, ii >> 3), y0 = iclip(0, d.Hc - 1, jj >> 3);
-            const int x1 = iclip(0, Wc - 1, (ii + 7) >> 3), y1 = iclip(0, d.Hc - 1, (jj + 7) >> 3);
-            const int fx = ii & 7, fy = jj & 7;
-            cpredv = ((8 - fx) * (8 - fy) * R[y0 * Wc + x0] + fx * (8 - fy) * R[y0 * Wc + x1] + (8 - fx) * fy * R[y1 * Wc + x0] +
-                      fx * fy * R[y1 * Wc + x1] + 32) >> 6;
-        }
         const int c = lane_fwd4x4(s.orgc[cuv][cyo * 8 + cxo] - cpredv, l);
         if (l == 0) s.cdcin[cuv][cb] = c;
         int lev, cc;
