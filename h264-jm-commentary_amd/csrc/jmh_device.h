@@ -164,11 +164,18 @@ struct TickArgs {
                                          //   (1: CABAC rates, 2: CAVLC rates, SymbolMode 0)
     const int32_t *sched, *soff;         //   schedule: MB addresses in stage order, offsets per stage
     void *rscr;                          //   the tick's candidate scratch (RdoScr per tick MB)
+    void *ffs;                           //   SearchMode 0: the tick MBs' SAD tables (null: the searches scan)
+    unsigned long long ffs_slot;         //   ... bytes per tick MB (ffs_slot_bytes)
     const uint32_t *ordtab;              // FFS order keys, [NPK2][NTA] packed pairs (jmh_create)
     int npic, nP;
     int pre[PMAX + 1];                   // MB prefix sums over the entries
     PicParams p[PMAX];
 };
+// RDOptimization 1 + SearchMode 0: bytes of one tick MB's SAD table (jmh_epzs.h ffs_table_build)
+__host__ __device__ __forceinline__ size_t ffs_slot_bytes(int sr) {
+    const size_t np = (size_t)(2 * sr + 1) * (2 * sr + 1);
+    return np * (5 * 4 + 36 * 2);
+}
 static_assert(sizeof(TickArgs) <= 4096, "TickArgs is passed by value in the kernel argument segment");
 
 // XCD-aware block order.  Workgroups are dispatched round-robin over the 8 XCDs (hardware block b

@@ -284,6 +284,168 @@ __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWi
     return sad;
 }
 
+// ---- RDOptimization 1 with SearchMode 0 (item 65): SetupFastFullPelSearch's SAD table [J], shared
+//      by the MB's 41 searches.  One table per tick MB in global memory (ffs_slot_bytes), raster over
+//      the (2 SR + 1)^2 full-pel positions around the MB's FFS centre (the 16x16 MVP / 4, clamped):
+//      u32 [5][NP] for 16x16; 16x8 top, bottom; 8x16 left, right, then u16 [4][9][NP] per 8x8 block
+//      for 8x8; 8x4 top, bottom; 4x8 left, right; its four 4x4 (an 8x8 SAD <= 64 x 1023 < 2^16).
+//      The raster -> spiral-index map (the searches' tie order) follows the spiral table in ordtab.
+// table of the search of block type bt at 4x4 position (bx4, by4): 0..4 u32, 5 + b8 * 9 + j u16
+__device__ __forceinline__ int ffs_tab_index(int bt, int bx4, int by4) {
+    const int b8 = (by4 >> 1) * 2 + (bx4 >> 1);
+    switch (bt) {
+    case 1: return 0;
+    case 2: return 1 + (by4 >> 1);
+    case 3: return 3 + (bx4 >> 1);
+    case 4: return 5 + b8 * 9;
+    case 5: return 5 + b8 * 9 + 1 + (by4 & 1);
+    case 6: return 5 + b8 * 9 + 3 + (bx4 & 1);
+    default: return 5 + b8 * 9 + 5 + (by4 & 1) * 2 + (bx4 & 1);
+    }
+}
+// the tables of one MB on its wave, centre (ccx, ccy), built just before the searches that read
+// them (so they are still in the caches): BIG the 16x16 / 16x8 / 8x16 tables from the four 8x8
+// SADs, else those of 8x8 block b8 from its four 4x4 SADs.  Every position lies inside the LDS
+// window (shifted to the same MVP, margin >= SR + 3).  Lane = column of positions; the window
+// rows slide past the block: each reference row is read once and its SADs against all H block
+// rows go to the H positions (rows) in flight, a position completing every row.  A column past 64
+// (SR 32) per position.  The caller fences before the searches read the tables.
+template <class pel, bool BIG>
+__device__ __forceinline__ void ffs_build_phase(const DevParams &d, const EpzS<pel> &s, const EWin<pel> &wn, uint8_t *tab, int ccx, int ccy, int b8,
+                                                int lane) {
+    constexpr int EW = EGeo<pel>::ew, PPD = 4 / sizeof(pel);   // samples per dword
+    constexpr int H = BIG ? 16 : 8, ND = H / PPD, OD = 16 / PPD;   // block rows (and columns), dwords per block / MB row
+    const int R = d.sr, side = 2 * R + 1, np = side * side;
+    const int ox = BIG ? 0 : 8 * (b8 & 1), oy = BIG ? 0 : 8 * (b8 >> 1);
+    uint32_t *big = reinterpret_cast<uint32_t *>(tab);
+    uint16_t *sml = reinterpret_cast<uint16_t *>(tab + (size_t)20 * np) + (size_t)(BIG ? 0 : b8) * 9 * np;
+    uint32_t o[H][ND];                                   // the block's rows (wave-uniform)
+#pragma unroll
+    for (int r = 0; r < H; r++)
+#pragma unroll
+        for (int q = 0; q < ND; q++) o[r][q] = reinterpret_cast<const uint32_t *>(s.org)[(oy + r) * OD + ox / PPD + q];
+    // accumulator of block row k, dword q: BIG the 8x8, else the 4x4 (raster in the block)
+    auto ai = [](int k, int q) { return (BIG ? (k >> 3) : (k >> 2)) * 2 + q / (ND / 2); };
+    auto sad = [](uint32_t r, uint32_t o, uint32_t c) {
+        if constexpr (sizeof(pel) == 2) return __builtin_amdgcn_sad_u16(r, o, c);
+        else return __builtin_amdgcn_sad_u8(r, o, c);
+    };
+    auto store = [&](int p, const uint32_t (&a)[4]) {
+        if constexpr (BIG) {
+            big[p] = a[0] + a[1] + a[2] + a[3];
+            big[np + p] = a[0] + a[1]; big[2 * np + p] = a[2] + a[3];
+            big[3 * np + p] = a[0] + a[2]; big[4 * np + p] = a[1] + a[3];
+        } else {
+            uint16_t *t = sml + p;
+            t[0] = (uint16_t)(a[0] + a[1] + a[2] + a[3]);
+            t[1 * np] = (uint16_t)(a[0] + a[1]); t[2 * np] = (uint16_t)(a[2] + a[3]);
+            t[3 * np] = (uint16_t)(a[0] + a[2]); t[4 * np] = (uint16_t)(a[1] + a[3]);
+            t[5 * np] = (uint16_t)a[0]; t[6 * np] = (uint16_t)a[1]; t[7 * np] = (uint16_t)a[2]; t[8 * np] = (uint16_t)a[3];
+        }
+    };
+    const int wy0 = wn.my + ccy - R + oy, wx0 = wn.mx + ccx - R + ox;   // window position of position (0, 0)
+    const int nc = min(side, NTE), c = min(lane, nc - 1), nrow = side + H - 1;
+    {
+        const int a0 = wy0 * EW + wx0 + c;
+        const uint32_t sel = (uint32_t)(a0 & (PPD - 1)) * sizeof(pel);
+        const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a0 & ~(PPD - 1)));
+        uint32_t acc[H][4];
+#pragma unroll 1
+        for (int Y0 = 0; Y0 < nrow; Y0 += H) {
+#pragma unroll
+            for (int j = 0; j < H; j++) {
+                const int Y = Y0 + j;                    // the window row read (position rows Y - H + 1 .. Y)
+                if (Y >= nrow) break;                    // wave-uniform
+#pragma unroll
+                for (int i = 0; i < 4; i++) acc[j][i] = 0;   // position row Y starts
+                uint32_t w[ND + 1], rf[ND];
+#pragma unroll
+                for (int q = 0; q <= ND; q++) w[q] = base[Y * (EW / PPD) + q];
+#pragma unroll
+                for (int q = 0; q < ND; q++) rf[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sel);
+#pragma unroll
+                for (int k = 0; k < H; k++)             // block row k <-> position row Y - k
+#pragma unroll
+                    for (int q = 0; q < ND; q++) acc[(j - k) & (H - 1)][ai(k, q)] = sad(rf[q], o[k][q], acc[(j - k) & (H - 1)][ai(k, q)]);
+                const int y = Y - (H - 1);               // complete
+                if (y >= 0 && y < side && lane < nc) store(y * side + c, acc[(j + 1) & (H - 1)]);
+            }
+        }
+    }
+#pragma unroll 1
+    for (int cc = NTE; cc < side; cc++)                  // SR 32: column 64, a lane per row
+        for (int y0 = 0; y0 < side; y0 += NTE) {
+            const int y = min(y0 + lane, side - 1), a = (wy0 + y) * EW + wx0 + cc;
+            const uint32_t sel = (uint32_t)(a & (PPD - 1)) * sizeof(pel);
+            const uint32_t *base = reinterpret_cast<const uint32_t *>(s.g + (a & ~(PPD - 1)));
+            uint32_t a4[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < H; k++) {
+                uint32_t w[ND + 1];
+#pragma unroll
+                for (int q = 0; q <= ND; q++) w[q] = base[k * (EW / PPD) + q];
+#pragma unroll
+                for (int q = 0; q < ND; q++) a4[ai(k, q)] = sad(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sel), o[k][q], a4[ai(k, q)]);
+            }
+            if (y0 + lane < side) store(y * side + cc, a4);
+        }
+}
+template <class pel>
+__device__ __forceinline__ void ffs_table_build(const DevParams &d, const EpzS<pel> &s, const EWin<pel> &wn, uint8_t *tab, int ccx, int ccy, int b8,
+                                                int lane) {
+    if (b8 < 0) ffs_build_phase<pel, true>(d, s, wn, tab, ccx, ccy, 0, lane);
+    else ffs_build_phase<pel, false>(d, s, wn, tab, ccx, ccy, b8, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// the full-pel search of one block from the table: every position of +-range around the centre,
+// key = cost << 13 | spiral index (JM's scan order, strict '<'), one wave minimum.  Lanes take the
+// columns of a row (the row's MV-cost bits uniform; lanes past the last column repeat it), FFS_RB
+// rows' loads in flight per round trip; columns past 64 a lane per row.
+#ifndef FFS_RB
+#define FFS_RB 16
+#endif
+template <class T>
+__device__ __forceinline__ unsigned ffs_table_min_t(const DevParams &d, const T *tab, int range, int ccx, int ccy, int pmx, int pmy, int lane) {
+    const int R = d.sr, side = 2 * R + 1, np = side * side, n = 2 * range + 1, c0 = R - range;
+    const uint32_t *spr = d.ordtab + ORDTAB_SPOS + np;
+    unsigned kb = 0xFFFFFFFFu;
+    const int lc = min(lane, n - 1);
+    // WEIGHTED_COST under RDO, (lf x (bits_x + bits_y)) >> 16, as lf bits_x + lf bits_y (the row's
+    // term uniform): no per-position multiply (products < 2^32 as in wcost)
+    const unsigned lf = d.lf, lfx = lf * (unsigned)mvbits(4 * (ccx + lc - range) - pmx);
+#pragma unroll 1
+    for (int r0 = 0; r0 < n; r0 += FFS_RB) {
+        uint32_t sv[FFS_RB], pv[FFS_RB];
+#pragma unroll
+        for (int j = 0; j < FFS_RB; j++) {
+            const int p = (min(r0 + j, n - 1) + c0) * side + c0 + lc;
+            sv[j] = tab[p];
+            pv[j] = spr[p];
+        }
+#pragma unroll
+        for (int j = 0; j < FFS_RB; j++) {
+            const unsigned lfy = lf * (unsigned)mvbits(4 * (ccy + min(r0 + j, n - 1) - range) - pmy);   // uniform
+            kb = min(kb, ((sv[j] + ((lfx + lfy) >> 16)) << 13) | pv[j]);
+        }
+    }
+#pragma unroll 1
+    for (int cc = NTE; cc < n; cc++) {                   // n = 65 (SR 32): one column
+        const unsigned lfc = lf * (unsigned)mvbits(4 * (ccx + cc - range) - pmx);
+        for (int rr = 0; rr < n; rr += NTE) {
+            const int row = min(rr + lane, n - 1), p = (row + c0) * side + c0 + cc;
+            const unsigned lfr = lf * (unsigned)mvbits(4 * (ccy + row - range) - pmy);
+            kb = min(kb, (((unsigned)tab[p] + ((lfc + lfr) >> 16)) << 13) | spr[p]);
+        }
+    }
+    return wave_min_u32(kb);
+}
+__device__ __forceinline__ unsigned ffs_table_min(const DevParams &d, const uint8_t *tab, int ti, int range, int ccx, int ccy, int pmx, int pmy, int lane) {
+    const size_t np = (size_t)(2 * d.sr + 1) * (2 * d.sr + 1);
+    if (ti < 5) return ffs_table_min_t(d, reinterpret_cast<const uint32_t *>(tab) + (size_t)ti * np, range, ccx, ccy, pmx, pmy, lane);
+    return ffs_table_min_t(d, reinterpret_cast<const uint16_t *>(tab + 20 * np) + (size_t)(ti - 5) * np, range, ccx, ccy, pmx, pmy, lane);
+}
+
 typedef short e16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ e16x2 e_s2(uint32_t v) { return __builtin_bit_cast(e16x2, v); }
 __device__ __forceinline__ uint32_t e_u32(e16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -390,7 +552,7 @@ __device__ __forceinline__ int had_packed(const e16x2 (&r)[4][2]) {
 // pmvo (k_rdo_inter; null in k_mb_epzs): receives the MVP each search used (the RD rate's mvd)
 template <int BT, class pel, int FBR = 1>
 __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, const EWin<pel> &wn, int bx4, int by4, int mc, int b8, int best8x8, bool prof,
-                                           int16_t (*pmvo)[16][2] = nullptr) {
+                                           int16_t (*pmvo)[16][2] = nullptr, const uint8_t *ftab = nullptr) {
     // debug (JMH_PHASE_PROF): steps of the MB's first 4x4 search into prof[41..46], of its 16x16
     // search into prof[47..52] (k_mb_epzs only)
     const bool sp = prof && ((BT == 7 && bx4 == 0 && by4 == 0) || BT == 1);
@@ -452,6 +614,9 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
         const int ccx = d.search_mode == 0 ? s.scx : mvx0, ccy = d.search_mode == 0 ? s.scy : mvy0;
         const int side = 2 * range + 1, npos = side * side;
         unsigned kb = 0xFFFFFFFFu;
+        if (ftab && d.search_mode == 0) {               // the MB's shared SAD table (ffs_table_build)
+            kb = ffs_table_min(d, ftab, ffs_tab_index(BT, bx4, by4), range, ccx, ccy, pmx, pmy, lane);
+        } else {
 #pragma unroll 1
         for (int p = lane; p < npos; p += NTE) {
             const int dy = p / side - range, dx = p - (dy + range) * side - range, x = ccx + dx, y = ccy + dy;
@@ -459,6 +624,7 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
             kb = min(kb, ((unsigned)c << 13) | (unsigned)spiral_index(dx, dy));
         }
         kb = wave_min_u32(kb);
+        }
         int rx, ry;
         spiral_pos((int)(kb & 8191u), rx, ry);
         bx = ccx + rx; by = ccy + ry;

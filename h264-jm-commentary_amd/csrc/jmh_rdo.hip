@@ -339,7 +339,7 @@ __device__ __forceinline__ void luma_inter8(const DevParams &d, RdoInterS<pel> &
 }
 
 template <class pel, bool T8>
-__device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
+__device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> &s, RdoScr<pel> *scr, uint8_t *ftab, int mbx, int mby, int lane) {
     const int a = mby * d.mbw + mbx, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool prof = d.prof && lane == 0 && d.prof_mb == a;   // debug (JMH_PHASE_PROF): stamps 40..52
@@ -370,12 +370,24 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     wave_lds_sync();
     PSTAMP(41);
     const jmr_mbinfo *A = hasA ? &s.nbA : nullptr, *B = hasB ? &s.nbB : nullptr;
+    // SearchMode 0: the SAD tables of the searches (SetupFastFullPelSearch [J]) around the FFS centre,
+    // the 16x16 / 16x8 / 8x16 ones here, each 8x8 block's before its searches
+    int fcx = 0, fcy = 0;
+    if (ftab) {
+        int pmx, pmy;
+        MvpNb nb;
+        set_mvp_nb(NbEpz<EpzS<pel>>{s.e, 1, 0, 0}, 0, 0, 16, 16, pmx, pmy, nb);
+        fcx = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmx / 4));
+        fcy = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmy / 4));
+        ffs_table_build(d, s.e, wn, ftab, fcx, fcy, -1, lane);
+        PSTAMP(20);
+    }
     // ---- motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch [J])
-    epzs_block<1, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
-    epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
-    epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 2, 1, 0, 0, false, s.pmv);
-    epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv);
-    epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 2, 0, 1, 0, 0, false, s.pmv);
+    epzs_block<1, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
+    epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
+    epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 2, 1, 0, 0, false, s.pmv, ftab);
+    epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
+    epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 2, 0, 1, 0, 0, false, s.pmv, ftab);
     PSTAMP(42);
     const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
     for (int i = lane; i < JMR_NCTX / 4; i += 64) reinterpret_cast<uint32_t *>(s.strun)[i] = reinterpret_cast<const uint32_t *>(s.st0)[i];
@@ -390,15 +402,19 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
 #pragma unroll 1
     for (int b8 = 0; b8 < 4 && p8; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        epzs_block<4, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv);
-        epzs_block<6, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<6, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv);
-        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv);
-        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false, s.pmv);
+        if (ftab) {
+            ffs_table_build(d, s.e, wn, ftab, fcx, fcy, b8, lane);
+            PSTAMP(21 + b8);                            // debug: stamps 20..24 after the SAD tables
+        }
+        epzs_block<4, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<6, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<6, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
         PSTAMP(43 + 2 * b8);
         const int bx4 = X + (b4 & 1), by4 = Y + (b4 >> 1), k = by4 * 4 + bx4;
         const int px = 4 * bx4 + (l & 3), py = 4 * by4 + (l >> 2), q8 = (4 * (b4 >> 1) + (l >> 2)) * 8 + 4 * (b4 & 1) + (l & 3);
@@ -954,7 +970,9 @@ __global__ __launch_bounds__(NTE, JMH_RDO_INTER_WPE) void k_rdo_inter(const Tick
     const DevParams d = tick_params(t, e);
     int mbx, mby;
     tick_mb(t, d, e, m, mbx, mby);
-    rdo_inter_mb<pel, T8>(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, mbx, mby, threadIdx.x);
+    // SearchMode 0: the MB's SAD table in the tick slot's (ffs_slot_bytes; null: every search scans)
+    uint8_t *ftab = t.ffs ? reinterpret_cast<uint8_t *>(t.ffs) + (size_t)m * t.ffs_slot : nullptr;
+    rdo_inter_mb<pel, T8>(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, ftab, mbx, mby, threadIdx.x);
     if (t.bprof && threadIdx.x == 0) {
         t.bprof[3 * blockIdx.x] = bt0;
         t.bprof[3 * blockIdx.x + 1] = wall_clock64();

@@ -173,6 +173,7 @@ struct jmh_ctx {
     // the tick's candidate scratch, slices per picture
     int32_t *d_sched, *d_soff;
     void *d_rscr;
+    void *d_ffs;                         // RDO + SearchMode 0: the tick MBs' SAD tables (k_rdo_inter)
     int nslice;
 };
 
@@ -334,7 +335,7 @@ void jmh_destroy(jmh_ctx *c) {
     if (c->sst) (void)hipStreamSynchronize(c->sst);
     for (PicBuf &b : c->ring) free_entry(b);
     void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab, c->d_scur16,
-                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr};
+                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr, c->d_ffs};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     ring_free(c->ring_interp);
@@ -452,6 +453,9 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
             ALLOC(c->d_sched, rd_order.size() * sizeof(int32_t));
             ALLOC(c->d_soff, rd_off.size() * sizeof(int32_t));
             ALLOC(c->d_rscr, (size_t)PMAX * maxc * jmh_rdo_scratch_bytes());
+            // SearchMode 0: one SAD table per tick MB (JMH_RDO_FFS_TABLE=0: every search scans, A/B)
+            const char *ft = getenv("JMH_RDO_FFS_TABLE");
+            if (cfg->search_mode == 0 && !(ft && atoi(ft) == 0)) ALLOC(c->d_ffs, (size_t)PMAX * maxc * ffs_slot_bytes(c->sr));
             if (hipMemcpy(c->d_sched, rd_order.data(), rd_order.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
                 hipMemcpy(c->d_soff, rd_off.data(), rd_off.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         } else {
@@ -493,10 +497,14 @@ static int host_spiral_index(int x, int y) {
 static void ordtab_fill(std::vector<uint32_t> &tab, int sr) {
     const int side = 2 * sr + 1, nstrips = (side + NPK - 1) / NPK;
     static_assert(SIDE_MAX * ((SIDE_MAX + NPK - 1) / NPK) <= NTS, "the search threads cover every FFS position");
-    tab.assign((size_t)ORDTAB_SPOS + (size_t)side * side, 0);
+    // after the keys: spiral index -> position, then raster position -> spiral index (the RDO FFS
+    // table's tie order, jmh_epzs.h ffs_table_min)
+    tab.assign((size_t)ORDTAB_SPOS + (size_t)2 * side * side, 0);
     for (int y = -sr; y <= sr; y++)
-        for (int x = -sr; x <= sr; x++)
+        for (int x = -sr; x <= sr; x++) {
             tab[(size_t)ORDTAB_SPOS + host_spiral_index(x, y)] = ((uint32_t)x & 0xFFFFu) | (uint32_t)y << 16;
+            tab[(size_t)ORDTAB_SPOS + (size_t)side * side + (size_t)(y + sr) * side + x + sr] = (uint32_t)host_spiral_index(x, y);
+        }
     for (int t = 0; t < NTA; t++) {
         const bool sact = t < side * nstrips && t < NTS;
         const int dx = sact ? t % side : 0, dy0 = sact ? (t / side) * NPK : 0;
@@ -597,6 +605,7 @@ static int issue_tick(jmh_ctx *c) {
     t.ordtab = c->d_ordtab;
     t.rdo = c->cfg.rdo ? (c->cfg.symbol_mode ? 1 : 2) : 0;   // 2: CAVLC rates
     t.sched = c->d_sched; t.soff = c->d_soff; t.rscr = c->d_rscr;
+    t.ffs = c->d_ffs; t.ffs_slot = ffs_slot_bytes(c->sr);
     int act[PMAX], nact = 0, nP = 0;
     const int nf = (int)c->fl.size();
     std::vector<int> before(nf);

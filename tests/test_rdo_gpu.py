@@ -141,14 +141,18 @@ def test_rdo_cavlc_config5_width_3840():
     rdo_pair(w, h, pics, 28, bd=10, symbol_mode=0, search_range=32, slice_mbs=240)
 
 
-# ---- SearchMode 0 (FFS) / -1 (full search) under RDO (item 65): k_rdo_inter's searches scan every
-#      position of the window on a lane stride; no (0,0) pre-check, no zero-vector bias
+# ---- SearchMode 0 (FFS) / -1 (full search) under RDO (item 65): FFS from the MB's shared SAD table
+#      (SetupFastFullPelSearch), full search scanning every position of the window on a lane stride;
+#      no (0,0) pre-check, no zero-vector bias
 @pytest.mark.parametrize("sm,bd,kw,qp", [
     (0, 8, dict(search_range=16), 28),
     (0, 8, dict(search_range=8, slice_mbs=11, transform_8x8_mode=1), 36),
     (-1, 8, dict(search_range=8, restrict_search_range=0), 20),
     (0, 10, dict(search_range=16, symbol_mode=0), 30),
     (-1, 10, dict(search_range=8, transform_8x8_mode=1), 26),
+    # SR 32: the SAD table's full 65 x 65 grid (a column past the 64 lanes), MB centres near the edges
+    (0, 8, dict(search_range=32), 28),
+    (0, 10, dict(search_range=32, restrict_search_range=0, slice_mbs=33), 32),
 ])
 def test_rdo_ffs_full_search(sm, bd, kw, qp):
     pics = (hbd_seq(176, 144, 3, seed=120 + qp, bd=bd) if bd > 8 else moving_seq(176, 144, 3, seed=120 + qp))

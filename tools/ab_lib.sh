@@ -10,7 +10,7 @@ for r in $(seq 1 $ROUNDS); do
   for v in $VARS; do
     if [ $v = default ]; then L=""; else L="$R/h264-jm-commentary_amd/csrc/ab/libjmhip_$v.so"; fi
     o=gpurun_out/${TAG}_c${CONFIG}_${v}_$r
-    JMH_LIB_PATH=$L timeout -k 10 300 python bench.py --config $CONFIG --steps 60 --no-cpu-baseline --no-host-path > $o.json 2> $o.err
+    JMH_LIB_PATH=$L timeout -k 10 300 python bench.py --config $CONFIG --steps 60 --no-cpu-baseline --no-host-path ${BENCH_EXTRA:-} > $o.json 2> $o.err
     echo "c$CONFIG $v round $r: $(grep -o '"value": [0-9.]*' $o.json)"
   done
 done
