@@ -338,8 +338,11 @@ __device__ __forceinline__ void luma_inter8(const DevParams &d, RdoInterS<pel> &
     if (lane == 0) { L->cbp = cbp; L->cbp_blk = cbp_blk; L->dist = dist; L->i16mode = 0; }
 }
 
-template <class pel, bool T8>
-__device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> &s, RdoScr<pel> *scr, uint8_t *ftab, int mbx, int mby, int lane) {
+// FFS: SearchMode 0 with the MB's SAD tables in ftab (its own instantiation: the table build's
+// registers stay out of the EPZS kernel's allocation)
+template <class pel, bool T8, bool FFS>
+__device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> &s, RdoScr<pel> *scr, uint8_t *ftab_, int mbx, int mby, int lane) {
+    uint8_t *const ftab = FFS ? ftab_ : nullptr;
     const int a = mby * d.mbw + mbx, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool prof = d.prof && lane == 0 && d.prof_mb == a;   // debug (JMH_PHASE_PROF): stamps 40..52
@@ -957,7 +960,7 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
 #ifndef JMH_RDO_INTER_WPE
 #define JMH_RDO_INTER_WPE 1                   // waves per SIMD the register budget must allow (2: five per CU
 #endif                                        //   at 16 bits, 32 B of scratch, 10 % slower: profiles/r7x_fallback_ab.txt)
-template <class pel, bool T8>
+template <class pel, bool T8, bool FFS>
 __global__ __launch_bounds__(NTE, JMH_RDO_INTER_WPE) void k_rdo_inter(const TickArgs t) {
     __shared__ RdoInterS<pel> s;
     const int nP = t.pre[t.nP], m = xcd_block(blockIdx.x, nP);
@@ -972,7 +975,7 @@ __global__ __launch_bounds__(NTE, JMH_RDO_INTER_WPE) void k_rdo_inter(const Tick
     tick_mb(t, d, e, m, mbx, mby);
     // SearchMode 0: the MB's SAD table in the tick slot's (ffs_slot_bytes; null: every search scans)
     uint8_t *ftab = t.ffs ? reinterpret_cast<uint8_t *>(t.ffs) + (size_t)m * t.ffs_slot : nullptr;
-    rdo_inter_mb<pel, T8>(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, ftab, mbx, mby, threadIdx.x);
+    rdo_inter_mb<pel, T8, FFS>(d, s, reinterpret_cast<RdoScr<pel> *>(t.rscr) + m, ftab, mbx, mby, threadIdx.x);
     if (t.bprof && threadIdx.x == 0) {
         t.bprof[3 * blockIdx.x] = bt0;
         t.bprof[3 * blockIdx.x + 1] = wall_clock64();
@@ -1281,8 +1284,10 @@ hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st, hipStream_t side, h
     // Transform8x8Mode / SymbolMode 0: the instantiations with the 8x8-transform candidates / the
     // CAVLC rates (the others keep their registers and LDS)
     typedef void (*Kern)(const TickArgs);
-    const Kern kin = t.bd > 8 ? (t.t8 ? k_rdo_inter<uint16_t, true> : k_rdo_inter<uint16_t, false>)
-                              : (t.t8 ? k_rdo_inter<uint8_t, true> : k_rdo_inter<uint8_t, false>);
+    const Kern kin = t.ffs ? (t.bd > 8 ? (t.t8 ? k_rdo_inter<uint16_t, true, true> : k_rdo_inter<uint16_t, false, true>)
+                                       : (t.t8 ? k_rdo_inter<uint8_t, true, true> : k_rdo_inter<uint8_t, false, true>))
+                           : (t.bd > 8 ? (t.t8 ? k_rdo_inter<uint16_t, true, false> : k_rdo_inter<uint16_t, false, false>)
+                                       : (t.t8 ? k_rdo_inter<uint8_t, true, false> : k_rdo_inter<uint8_t, false, false>));
     const bool cav = t.rdo == 2;
     const Kern kia = rdo_pick(t.bd > 8, t.t8 != 0, false, cav);
     if (nP) hipLaunchKernelGGL(kin, dim3(xcd_grid(nP)), dim3(NTE), 0, st, t);
