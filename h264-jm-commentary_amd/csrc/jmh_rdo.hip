@@ -1040,8 +1040,11 @@ struct RdoFinS {
 
 // T8: Transform8x8Mode (the 8x8-transform and I8MB candidates; jmr_mb's 8x8 residual path); CAV:
 // SymbolMode 0 (jmv_mb rates, the slice's mb_skip_run)
+#ifndef JMH_RDO_FINAL_WPE
+#define JMH_RDO_FINAL_WPE 5                   // Transform8x8Mode: waves per SIMD the register budget must allow
+#endif                                        //   (the 8x8 CABAC residual path would take 146 VGPRs: three)
 template <class pel, bool T8, bool CAV>
-__global__ __launch_bounds__(NT) void k_rdo_final(const TickArgs t) {
+__global__ __launch_bounds__(NT, T8 ? JMH_RDO_FINAL_WPE : 1) void k_rdo_final(const TickArgs t) {
     __shared__ RdoFinS<pel> s;
     const int tid = threadIdx.x, tot = t.pre[t.npic];
     const int m = xcd_block(blockIdx.x, tot);
