@@ -80,8 +80,9 @@ struct DbkS {
 // the MB's deblocking on NT threads (tid), after its reconstruction rec (LDS, 16x16) / cfin (LDS,
 // 2 x 8x8) is final.  fmv: the MB's MVs per 4x4, cbp_blk: its coded 4x4 blocks, t8flag: 8x8
 // transform (no 4x4 luma edges), qpy / qpcy: QPY and QPc (thresholds).  Every thread of the
-// workgroup must call it (it synchronises).
-template <class pel>
+// workgroup must call it (it synchronises).  NTH: threads of the workgroup (256, or 512 in the
+// 512-thread final bodies: the sample loads / stores stride over all of them)
+template <class pel, int NTH = NT>
 __device__ __forceinline__ void deblock_mb(const DevParams &d, DbkS<pel> &s, const pel *rec, const pel (*cfin)[64], const int16_t (*fmv)[2],
                                            bool is_intra, int cbp_blk, bool t8flag, int qpy, int qpcy, int mbx, int mby, int tid) {
     pel *dbkY = spl<pel>(d.dbkY), *dbkU = spl<pel>(d.dbkU), *dbkV = spl<pel>(d.dbkV);
@@ -91,7 +92,7 @@ __device__ __forceinline__ void deblock_mb(const DevParams &d, DbkS<pel> &s, con
     {
         const bool filt = d.lf_disable != 1;
         __syncthreads();                          // rec, cfin final
-        for (int i = tid; i < 400 + 288; i += NT) {
+        for (int i = tid; i < 400 + 288; i += NTH) {
             if (i < 400) {
                 const int r = i / 20 - 4, c = i % 20 - 4;
                 int v = 0;
@@ -164,7 +165,7 @@ __device__ __forceinline__ void deblock_mb(const DevParams &d, DbkS<pel> &s, con
                 }
         }
         __syncthreads();
-        for (int i = tid; i < 400 + 288; i += NT) {
+        for (int i = tid; i < 400 + 288; i += NTH) {
             if (i < 400) {
                 const int r = i / 20 - 4, c = i % 20 - 4;
                 if ((r >= 0 && c >= 0) || (r >= -3 && r < 0 && c >= 0 && dbT) || (c >= -3 && c < 0 && r >= 0 && dbL))

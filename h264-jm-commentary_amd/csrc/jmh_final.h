@@ -46,15 +46,19 @@ struct FinS {
 // one dispatch round), 5 (no spills, a shorter per-MB chain) for smaller ticks
 // T8: built with Transform8x8Mode's paths (I8MB, TransformDecision, dct_luma8x8); the
 // instantiation without them folds d.t8 = 0, and 8-bit samples fold Clip1 = 255, QpBdOffset = 0
-// tick MB index m on threads tid = 0..255 of the workgroup (hwb: the hardware block, for the block
-// profile; bt0 its start stamp)
-template <int OCC, class pel, bool T8>
-__device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m, int tid, int hwb, unsigned long long bt0) {
-    const int e = tick_entry(t, m);
-    DevParams d = tick_params(t, e);
+// NTH: threads of the workgroup.  256: the luma coding on all of them, the chroma coding after it on
+// threads 0..127.  512 (k_mb_final512, k_mb_flow): luma on threads 0..255 while waves 4 and 5 run the
+// chroma prediction, transform and quantisation (dct_chroma's first half) beside it; only the
+// chroma DC and the inverse transform follow the luma.  Every thread of the workgroup calls it.
+template <int OCC, class pel, bool T8, int NTH>
+__device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, int mby, int tid) {
+    constexpr bool W2 = NTH == 512;
+    static_assert(NTH == 256 || NTH == 512, "final_core runs on 256 or 512 threads");
     if constexpr (!T8) d.t8 = 0;
     if constexpr (sizeof(pel) == 1) { d.maxv = 255; d.qpbd = 0; }
-    const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
+    const bool lu = !W2 || tid < 256;                    // luma threads (wave-uniform)
+    const int ct = W2 ? tid - 256 : tid;                 // chroma thread index (valid in [0, 128))
+    const bool chv = ct >= 0 && ct < 128;
     const int pix_x = 16 * mbx, pix_y = 16 * mby;
     const int W = d.W, Wc = d.Wc, W4 = d.W >> 2;
     const int slice_p = d.slice_type == JMH_P_SLICE;
@@ -70,24 +74,27 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
     const MbScratch *sc = d.scr + mby * d.mbw + mbx;
 
     // ---- inputs into LDS
-    s.org[tid] = orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    if (tid < 128) {
-        const int uv = tid >> 6, k = tid & 63;
-        s.orgc[uv][k] = (uv ? orgV : orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
-    } else if (tid >= 128 && tid < 149) {
-        const int x = tid - 129;
-        const bool av = x < 0 ? avTL : x < 16 ? avT : false;
-        s.rtop[x + 1] = av ? recY[(pix_y - 1) * W + pix_x + x] : 0;
-    } else if (tid >= 160 && tid < 176) {
-        const int y = tid - 160;
-        s.rleft[y] = avL ? recY[(pix_y + y) * W + pix_x - 1] : 0;
-    } else if (tid >= 192 && tid < 210) {
-        const int i = tid - 192, uv = i / 9, x = i - 9 * uv - 1;
-        const bool av = x < 0 ? avTL : avT;
-        s.ctop[uv][x + 1] = av ? (uv ? recV : recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
-    } else if (tid >= 224 && tid < 240) {
-        const int i = tid - 224, uv = i >> 3, y = i & 7;
-        s.cleft[uv][y] = avL ? (uv ? recV : recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
+    if (lu) s.org[tid] = orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    if (!W2 || tid >= 256) {
+        const int u = ct;
+        if (u < 128) {
+            const int uv = u >> 6, k = u & 63;
+            s.orgc[uv][k] = (uv ? orgV : orgU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)];
+        } else if (u >= 128 && u < 149) {
+            const int x = u - 129;
+            const bool av = x < 0 ? avTL : x < 16 ? avT : false;
+            s.rtop[x + 1] = av ? recY[(pix_y - 1) * W + pix_x + x] : 0;
+        } else if (u >= 160 && u < 176) {
+            const int y = u - 160;
+            s.rleft[y] = avL ? recY[(pix_y + y) * W + pix_x - 1] : 0;
+        } else if (u >= 192 && u < 210) {
+            const int i = u - 192, uv = i / 9, x = i - 9 * uv - 1;
+            const bool av = x < 0 ? avTL : avT;
+            s.ctop[uv][x + 1] = av ? (uv ? recV : recU)[((pix_y >> 1) - 1) * Wc + (pix_x >> 1) + x] : 0;
+        } else if (u >= 224 && u < 240) {
+            const int i = u - 224, uv = i >> 3, y = i & 7;
+            s.cleft[uv][y] = avL ? (uv ? recV : recU)[((pix_y >> 1) + y) * Wc + (pix_x >> 1) - 1] : 0;
+        }
     }
 
     // ---- mode decision (encode_one_macroblock, RDO off): costs from k_mb_analyse
@@ -119,13 +126,14 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
     }
     __syncthreads();
 
-    // ======== chroma prediction, ahead of the luma (JMH_FINAL_CPRED_EARLY): the inter prediction's
-    // reference reads then travel with the luma MC's instead of one round trip after them
+    // ======== chroma prediction, ahead of the luma: the inter prediction's reference reads then
+    // travel with the luma MC's instead of one round trip after them
     const int c_mode = is_intra ? sc->c_mode : 0;
-    const int cuv = (tid >> 4) >> 2, cb = (tid >> 4) & 3;
-    const int cxo = (cb & 1) * 4 + (tid & 3), cyo = (cb >> 1) * 4 + ((tid & 15) >> 2);
+    const int l = tid & 15;
+    const int cuv = (ct >> 4) >> 2, cb = (ct >> 4) & 3;
+    const int cxo = (cb & 1) * 4 + (ct & 3), cyo = (cb >> 1) * 4 + ((ct & 15) >> 2);
     int cpredv = 0;
-    if (tid < 128) {
+    if (chv) {
         if (is_intra) {
             cpredv = chroma_pred_px(s.ctop[cuv] + 1, s.cleft[cuv], s.ctop[cuv][0], avT, avL, c_mode, cxo, cyo, maxv);
         } else {
@@ -140,11 +148,58 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
                       fx * fy * R[y1 * Wc + x1] + 32) >> 6;
         }
     }
+    // dct_chroma [J] in three parts: (A) forward transform + AC quantisation per 4x4, (B) the 2x2 DC
+    // on two threads, (C) inverse transform + reconstruction.  QPc of qPI = Clip3(-QpBdOffsetC, 51,
+    // QPY + chroma_qp_index_offset) (8.5.8, Table 8-15: negative qPI map to themselves), quantised
+    // at QP'c = QPc + QpBdOffsetC
+    const int qpi = iclip(-d.qpbd, 51, qpy + d.cqp_off), qpcy = qpi < 0 ? qpi : c_qpc[qpi], qpc = qpcy + d.qpbd;
+    const int cq_bits = 15 + qpc / 6;
+    const int cqp_const = q_round(d.qsel, cq_bits);
+    int cdq = 0;
+    auto chroma_a = [&]() {
+        if (chv) {
+            const int c = lane_fwd4x4(s.orgc[cuv][cyo * 8 + cxo] - cpredv, l);
+            if (l == 0) s.cdcin[cuv][cb] = c;
+            int lev, cc;
+            unsigned nz = lane_quant(c, l, qpc, cqp_const, true, lev, cdq, cc);
+            s.cac[cuv][cb][l] = (int16_t)lev;
+            if (l == 0) { s.cbcost[cuv][cb] = cc; s.cbnz[cuv][cb] = nz != 0; }
+        }
+    };
+    auto chroma_b = [&]() {
+        if (ct >= 0 && ct < 2) {
+            const int uv = ct, qp_per = qpc / 6, qp_rem = qpc % 6;
+            const int *m = s.cdcin[uv];
+            int m1[4] = {m[0] + m[1] + m[2] + m[3], m[0] - m[1] + m[2] - m[3], m[0] + m[1] - m[2] - m[3], m[0] - m[1] - m[2] + m[3]};
+            int dcnz = 0;
+            for (int k = 0; k < 4; k++) {
+                int level = (abs(m1[k]) * c_q3[qp_rem][0] + 2 * cqp_const) >> (cq_bits + 1);
+                if (level) dcnz = 1;
+                s.cdc[uv][k] = (int16_t)isign(level, m1[k]);
+            }
+            int c0 = s.cdc[uv][0], c1 = s.cdc[uv][1], c2 = s.cdc[uv][2], c3 = s.cdc[uv][3];
+            int fv[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+            int v00 = c_dq3[qp_rem][0];
+            for (int k = 0; k < 4; k++) s.cdcq[uv][k] = (fv[k] * 16 * v00 * (1 << qp_per)) >> 5;   // 8.5.11.2
+            int cost = s.cbcost[uv][0] + s.cbcost[uv][1] + s.cbcost[uv][2] + s.cbcost[uv][3];
+            int acany = s.cbnz[uv][0] | s.cbnz[uv][1] | s.cbnz[uv][2] | s.cbnz[uv][3];
+            s.creset[uv] = cost < 4;                                  // _CHROMA_COEFF_COST_
+            s.cdcnz[uv] = (dcnz ? 1 : 0) | (acany && cost >= 4 ? 2 : 0);
+        }
+    };
+    auto chroma_c = [&]() {
+        if (chv) {
+            if (s.creset[cuv]) { cdq = 0; s.cac[cuv][cb][l] = 0; }
+            if (l == 0) cdq = s.cdcq[cuv][cb];
+            s.cfin[cuv][cyo * 8 + cxo] = (pel)lane_inv4x4(cdq, l, cpredv, maxv);
+        }
+    };
+    if constexpr (W2) chroma_a();                                      // beside the luma coding
 
-    // ======== luma residual coding: 16 blocks x 16 lanes
+    // ======== luma residual coding: 16 blocks x 16 lanes (threads 0..255)
     int cbp = 0, cbp_blk = 0;
     bool tr8 = false;                                                 // 8x8 transform
-    const int blk = tid >> 4, l = tid & 15, lx = l & 3, ly = l >> 2;
+    const int blk = tid >> 4, lx = l & 3, ly = l >> 2;
     const int px4 = 4 * (blk & 3) + lx, py4 = 4 * (blk >> 2) + ly;   // MB pixel of this lane
     const int w8 = tid >> 6, l8 = tid & 63;                           // 8x8 layout: wave = 8x8 block
     const int qx = 8 * (w8 & 1) + (l8 & 7), qy = 8 * (w8 >> 1) + (l8 >> 3);
@@ -152,21 +207,31 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
         cbp = sc->i8cbp; tr8 = true;
         for (int b = 0; b < 4; b++)
             if ((cbp >> b) & 1) cbp_blk |= 0x33 << ((b >> 1) * 8 + (b & 1) * 2);
-        s.lev[blk][l] = sc->i8lev[blk][l];
-        s.rec[tid] = spl<pel>(sc->i8rec)[tid];
+        if (lu) {
+            s.lev[blk][l] = sc->i8lev[blk][l];
+            s.rec[tid] = spl<pel>(sc->i8rec)[tid];
+        }
     } else if (best_mode == JMH_I4MB) {
         cbp = sc->i4cbp; cbp_blk = sc->i4blk;
-        s.lev[blk][l] = sc->i4lev[blk][l];
-        s.rec[tid] = spl<pel>(sc->i4rec)[tid];
+        if (lu) {
+            s.lev[blk][l] = sc->i4lev[blk][l];
+            s.rec[tid] = spl<pel>(sc->i4rec)[tid];
+        }
     } else if (best_mode == JMH_I16MB) {
         // dct_luma_16x16 [J] (jmh_intra.h i16_code)
-        const pel *T = s.rtop + 1, *L = s.rleft;
-        const I16Par par = i16_params(T, L, avT, avL, (maxv + 1) >> 1);
-        const int p = i16_pred(par, T, L, i16mode, px4, py4, maxv);
+        int p = 0, org = 0;
+        if (lu) {
+            const pel *T = s.rtop + 1, *L = s.rleft;
+            const I16Par par = i16_params(T, L, avT, avL, (maxv + 1) >> 1);
+            p = i16_pred(par, T, L, i16mode, px4, py4, maxv);
+            org = (int)s.org[py4 * 16 + px4];
+        }
         int lev, rv;
-        i16_code(p, (int)s.org[py4 * 16 + px4], qp, q_round(q_sel16(d.qsel), 15 + qp / 6), s.dc, s.dcdq, s.dclev, s.bnz, tid, maxv, lev, rv);
-        s.lev[blk][l] = (int16_t)lev;
-        s.rec[py4 * 16 + px4] = (pel)rv;
+        i16_code(p, org, qp, q_round(q_sel16(d.qsel), 15 + qp / 6), s.dc, s.dcdq, s.dclev, s.bnz, tid, maxv, lev, rv, lu);
+        if (lu) {
+            s.lev[blk][l] = (int16_t)lev;
+            s.rec[py4 * 16 + px4] = (pel)rv;
+        }
         __syncthreads();
         for (int b = 0; b < 16; b++)
             if (s.bnz[b]) { cbp = 15; cbp_blk |= 1 << b; }
@@ -175,26 +240,31 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
         // the 64-VGPR build samples the 6-tap's centre column by column: no spills (the unrolled
         // form spilled 56 B per lane and measured 0.9 % faster, profiles/r7b_c3_serialj_ab.txt)
         constexpr bool serial_j = OCC == 8;
-        const int p = qpel_direct<pel, serial_j>(refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1], maxv);
+        const int p = lu ? qpel_direct<pel, serial_j>(refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1], maxv) : 0;
         if (d.t8 && (best_mode <= 3 || best8x8 == 0x4444)) {
             // TransformDecision [J] (item 29): sum of 4x4 SATDs vs sum of 8x8 SATDs of the residual
-            s.pred[py4 * 16 + px4] = (pel)p;
+            if (lu) s.pred[py4 * 16 + px4] = (pel)p;
             __syncthreads();
-            const int dv = s.org[qy * 16 + qx] - s.pred[qy * 16 + qx];
-            const int c4 = wave_satd4x4s(dv, l8, d.use_hadamard), c8 = wave_satd8(dv, l8, d.use_hadamard);
-            if (l8 == 0) { s.tdc[w8][0] = c4; s.tdc[w8][1] = c8; }
+            if (lu) {
+                const int dv = s.org[qy * 16 + qx] - s.pred[qy * 16 + qx];
+                const int c4 = wave_satd4x4s(dv, l8, d.use_hadamard), c8 = wave_satd8(dv, l8, d.use_hadamard);
+                if (l8 == 0) { s.tdc[w8][0] = c4; s.tdc[w8][1] = c8; }
+            }
             __syncthreads();
             tr8 = s.tdc[0][1] + s.tdc[1][1] + s.tdc[2][1] + s.tdc[3][1] < s.tdc[0][0] + s.tdc[1][0] + s.tdc[2][0] + s.tdc[3][0];
         }
         if (tr8) {
             // dct_luma8x8 [J] on one wave per 8x8 block, COEFF_COST8x8 thresholds as for 4x4
-            const int pv = s.pred[qy * 16 + qx];
-            const int q8 = 16 + qp / 6;
-            const int c = wave_fwd8x8(s.org[qy * 16 + qx] - pv, l8);
-            int lev, dq, cc;
-            const unsigned long long nz = wave_quant8(c, l8, qp, q_round(d.qsel, q8), lev, dq, cc);
-            const int rv = wave_inv8x8(dq, l8, pv, maxv);
-            if (l8 == 0) { s.bcost[w8] = cc; s.bnz[w8] = nz != 0; }
+            int lev = 0, rv = 0, pv = 0;
+            if (lu) {
+                pv = s.pred[qy * 16 + qx];
+                const int q8 = 16 + qp / 6;
+                const int c = wave_fwd8x8(s.org[qy * 16 + qx] - pv, l8);
+                int dq, cc;
+                const unsigned long long nz = wave_quant8(c, l8, qp, q_round(d.qsel, q8), lev, dq, cc);
+                rv = wave_inv8x8(dq, l8, pv, maxv);
+                if (l8 == 0) { s.bcost[w8] = cc; s.bnz[w8] = nz != 0; }
+            }
             __syncthreads();
             int sum_cnt = 0, keep8 = 0;
             for (int b8 = 0; b8 < 4; b8++) {
@@ -207,16 +277,21 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
                 sum_cnt += c8;
             }
             if (sum_cnt <= 5) { keep8 = 0; cbp = 0; cbp_blk = 0; }      // _LUMA_MB_COEFF_COST_
-            const bool keep = (keep8 >> w8) & 1;
-            s.lev[il_blk(w8, l8)][l8 >> 2] = keep ? (int16_t)lev : 0;
-            s.rec[qy * 16 + qx] = (pel)(keep ? rv : pv);
+            if (lu) {
+                const bool keep = (keep8 >> w8) & 1;
+                s.lev[il_blk(w8, l8)][l8 >> 2] = keep ? (int16_t)lev : 0;
+                s.rec[qy * 16 + qx] = (pel)(keep ? rv : pv);
+            }
         } else {
-        const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
-        int lev, dq, cc;
-        const int q_bits = 15 + qp / 6;
-        unsigned nz = lane_quant(c, l, qp, q_round(d.qsel, q_bits), false, lev, dq, cc);
-        const int rv = lane_inv4x4(dq, l, p, maxv);
-        if (l == 0) { s.bcost[blk] = cc; s.bnz[blk] = nz != 0; }
+        int lev = 0, rv = 0;
+        if (lu) {
+            const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
+            int dq, cc;
+            const int q_bits = 15 + qp / 6;
+            unsigned nz = lane_quant(c, l, qp, q_round(d.qsel, q_bits), false, lev, dq, cc);
+            rv = lane_inv4x4(dq, l, p, maxv);
+            if (l == 0) { s.bcost[blk] = cc; s.bnz[blk] = nz != 0; }
+        }
         __syncthreads();
         int sum_cnt = 0, keep8 = 0;
         for (int b8 = 0; b8 < 4; b8++) {
@@ -235,56 +310,23 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
             sum_cnt += c8;
         }
         if (sum_cnt <= 5) { keep8 = 0; cbp = 0; cbp_blk = 0; }      // _LUMA_MB_COEFF_COST_
-        const int mb8 = ((blk >> 3) << 1) + ((blk & 3) >> 1);
-        const bool keep = (keep8 >> mb8) & 1;
-        s.lev[blk][l] = keep ? (int16_t)lev : 0;
-        s.rec[py4 * 16 + px4] = (pel)(keep ? rv : p);
+        if (lu) {
+            const int mb8 = ((blk >> 3) << 1) + ((blk & 3) >> 1);
+            const bool keep = (keep8 >> mb8) & 1;
+            s.lev[blk][l] = keep ? (int16_t)lev : 0;
+            s.rec[py4 * 16 + px4] = (pel)(keep ? rv : p);
+        }
         }
     }
     const bool t8flag = tr8 && (best_mode == JMH_I8MB || (cbp & 15));   // transform_size_8x8_flag
     PSTAMP(17);
 
-    // ======== chroma: prediction (intra mode from k_mb_analyse, or MC) + dct_chroma [J]
-    // QPc of qPI = Clip3(-QpBdOffsetC, 51, QPY + chroma_qp_index_offset) (8.5.8, Table 8-15:
-    // negative qPI map to themselves), quantised at QP'c = QPc + QpBdOffsetC
-    const int qpi = iclip(-d.qpbd, 51, qpy + d.cqp_off), qpcy = qpi < 0 ? qpi : c_qpc[qpi], qpc = qpcy + d.qpbd;
-    const int cq_bits = 15 + qpc / 6;
-    const int cqp_const = q_round(d.qsel, cq_bits);
-    int cdq = 0;
-    if (tid < 128) {
-        const int c = lane_fwd4x4(s.orgc[cuv][cyo * 8 + cxo] - cpredv, l);
-        if (l == 0) s.cdcin[cuv][cb] = c;
-        int lev, cc;
-        unsigned nz = lane_quant(c, l, qpc, cqp_const, true, lev, cdq, cc);
-        s.cac[cuv][cb][l] = (int16_t)lev;
-        if (l == 0) { s.cbcost[cuv][cb] = cc; s.cbnz[cuv][cb] = nz != 0; }
-    }
+    // ======== chroma: the rest of dct_chroma [J]
+    if constexpr (!W2) chroma_a();
     __syncthreads();
-    if (tid < 2) {
-        const int uv = tid, qp_per = qpc / 6, qp_rem = qpc % 6;
-        const int *m = s.cdcin[uv];
-        int m1[4] = {m[0] + m[1] + m[2] + m[3], m[0] - m[1] + m[2] - m[3], m[0] + m[1] - m[2] - m[3], m[0] - m[1] - m[2] + m[3]};
-        int dcnz = 0;
-        for (int k = 0; k < 4; k++) {
-            int level = (abs(m1[k]) * c_q3[qp_rem][0] + 2 * cqp_const) >> (cq_bits + 1);
-            if (level) dcnz = 1;
-            s.cdc[uv][k] = (int16_t)isign(level, m1[k]);
-        }
-        int c0 = s.cdc[uv][0], c1 = s.cdc[uv][1], c2 = s.cdc[uv][2], c3 = s.cdc[uv][3];
-        int fv[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
-        int v00 = c_dq3[qp_rem][0];
-        for (int k = 0; k < 4; k++) s.cdcq[uv][k] = (fv[k] * 16 * v00 * (1 << qp_per)) >> 5;   // 8.5.11.2
-        int cost = s.cbcost[uv][0] + s.cbcost[uv][1] + s.cbcost[uv][2] + s.cbcost[uv][3];
-        int acany = s.cbnz[uv][0] | s.cbnz[uv][1] | s.cbnz[uv][2] | s.cbnz[uv][3];
-        s.creset[uv] = cost < 4;                                  // _CHROMA_COEFF_COST_
-        s.cdcnz[uv] = (dcnz ? 1 : 0) | (acany && cost >= 4 ? 2 : 0);
-    }
+    chroma_b();
     __syncthreads();
-    if (tid < 128) {
-        if (s.creset[cuv]) { cdq = 0; s.cac[cuv][cb][l] = 0; }
-        if (l == 0) cdq = s.cdcq[cuv][cb];
-        s.cfin[cuv][cyo * 8 + cxo] = (pel)lane_inv4x4(cdq, l, cpredv, maxv);
-    }
+    chroma_c();
     __syncthreads();
     PSTAMP(18);
     int cr = 0;
@@ -312,7 +354,7 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
         res->min_cost = min_cost;
         res->reserved = 0;
     }
-    res->luma[blk][l] = s.lev[blk][l];
+    if (lu) res->luma[blk][l] = s.lev[blk][l];
     if (tid < 16) {
         const int k = tid;
         const int ip = best_mode == JMH_I4MB ? sc->ipred[k]
@@ -326,17 +368,27 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
         d.ipred[a] = (int8_t)ip;
     }
     if (tid < 8) { const int uv = tid >> 2, k = tid & 3; res->chroma_dc[uv][k] = s.cdc[uv][k]; }
-    if (tid < 128) {
-        const int uv = tid >> 6, b = (tid >> 4) & 3, q = tid & 15;
+    if (chv) {
+        const int uv = ct >> 6, b = (ct >> 4) & 3, q = ct & 15;
         res->chroma_ac[uv][b][q] = s.cac[uv][b][q];
-        const int k = tid & 63;
+        const int k = ct & 63;
         (uv ? recV : recU)[((pix_y >> 1) + (k >> 3)) * Wc + (pix_x >> 1) + (k & 7)] = s.cfin[uv][k];
     }
-    recY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)] = s.rec[tid];
+    if (lu) recY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)] = s.rec[tid];
 
     // ======== DeblockMb [J] / 8.7 into the reference picture (jmh_deblock.h)
-    if (d.dbkY) deblock_mb(d, s.db, s.rec, s.cfin, s.fmv, is_intra, cbp_blk, t8flag, qpy, qpcy, mbx, mby, tid);
+    if (d.dbkY) deblock_mb<pel, NTH>(d, s.db, s.rec, s.cfin, s.fmv, is_intra, cbp_blk, t8flag, qpy, qpcy, mbx, mby, tid);
     PSTAMP(19);
+}
+
+// tick MB index m on threads tid = 0..NTH-1 of the workgroup (hwb: the hardware block, for the
+// block profile; bt0 its start stamp)
+template <int OCC, class pel, bool T8, int NTH = NT>
+__device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m, int tid, int hwb, unsigned long long bt0) {
+    const int e = tick_entry(t, m);
+    const DevParams d = tick_params(t, e);
+    const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
+    final_core<OCC, pel, T8, NTH>(d, s, mbx, mby, tid);
     if (t.bprof_fin && tid == 0) {
         t.bprof_fin[3 * hwb] = bt0;
         t.bprof_fin[3 * hwb + 1] = wall_clock64();

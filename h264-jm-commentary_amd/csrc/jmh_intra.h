@@ -131,8 +131,10 @@ __device__ __forceinline__ void i16_dc(int *dc, int16_t *dclev, int *dcdq, int q
 // the lane's AC level (scan position l of block blk; 0 at l == 0) and reconstruction; the DC levels
 // (scan order) land in dclev and the per-block AC non-zero flags in bnz (LDS).  dc / dcdq: LDS
 // scratch.  Every thread of the workgroup must call it (two barriers).
+// act false (wave-uniform: the chroma / idle waves of a 512-thread final): only the barriers.
 __device__ __forceinline__ void i16_code(int p, int org, int qp, int qp_const, int *dc, int *dcdq, int16_t *dclev, int *bnz, int tid,
-                                         int maxv, int &lev_out, int &rec_out) {
+                                         int maxv, int &lev_out, int &rec_out, bool act = true) {
+    if (!act) { __syncthreads(); __syncthreads(); lev_out = rec_out = 0; return; }
     const int blk = tid >> 4, l = tid & 15;
     const int c = lane_fwd4x4(org - p, l);
     if (l == 0) dc[blk] = c;
