@@ -461,17 +461,19 @@ def main():
 
     value = world * args.steps * DISP_W * DISP_H / 1e6 / dt
     pictures = max(1, tm.pictures)
-    an_per_pic = tm.ticks / pictures                     # one k_mb_analyse + one k_mb_final per tick
+    FLOW = tm.flow_launches > 0                          # dataflow: one k_mb_flow launch per segment of ticks
+    an_per_pic = (tm.flow_launches if FLOW else tm.ticks) / pictures   # tick model: one k_mb_analyse + one k_mb_final per tick
     mb_ms_pic = tm.mb_ms / pictures
     # the sampled launches' HIP events (every 32nd tick) add a few us per launch; the wavefront
     # brackets (one event pair per run of ticks) do not.  The per-launch figures are scaled so that
     # the sampled launches of a tick sum to the bracketed wavefront time per tick (never above it):
     # k_mb_analyse 93.8 us raw vs 90.0 us in rocprof's kernel trace (profiles/r6h_*)
     an_raw_ms = tm.analyse_ms / max(1, tm.analyse_launches)
-    fin_raw_ms = 0.0 if RDO else tm.final_ms / max(1, tm.final_launches)
+    fin_raw_ms = 0.0 if RDO or FLOW else tm.final_ms / max(1, tm.final_launches)
     ev_scale = min(1.0, mb_ms_pic / an_per_pic / (an_raw_ms + fin_raw_ms)) if an_raw_ms + fin_raw_ms > 0 else 1.0
     an_launch_ms, fin_launch_ms = an_raw_ms * ev_scale, fin_raw_ms * ev_scale
-    mbs_per_launch = tm.tick_mbs / max(1, tm.ticks)      # MBs of all pictures in flight, per tick
+    # MBs of all pictures in flight per tick, or per dataflow segment
+    mbs_per_launch = tm.flow_mbs / tm.flow_launches if FLOW else tm.tick_mbs / max(1, tm.ticks)
     bytes_per_launch = BYTES_PER_FRAME / NMB * mbs_per_launch
     achieved_gbs = bytes_per_launch / (an_launch_ms * 1e-3) / 1e9
     ad_per_launch = AD_PER_FRAME / NMB * mbs_per_launch
@@ -482,7 +484,7 @@ def main():
     valu_mb = pmc_rec.get("valu_insts_per_mb") if pmc_rec else None
     sm_name = {0: "FFS SearchMode=0", -1: "full search SearchMode=-1", 3: "EPZS SearchMode=3"}[search_mode]
     ffs = search_mode == 0
-    an_name = ("k_rdo_inter+k_rdo_intra+k_rdo_final" if RDO else
+    an_name = ("k_mb_flow" if FLOW else "k_rdo_inter+k_rdo_intra+k_rdo_final" if RDO else
                ("k_mb_analyse+k_mb_intra8" if cfg["t8"] else "k_mb_analyse") if ffs else
                ("k_mb_epzs" if search_mode == 3 else "k_mb_me_full") + "+k_mb_intra")
     hbm = {
@@ -496,7 +498,9 @@ def main():
         "algorithmic_bytes_per_launch": round(bytes_per_launch),
     }
     launch_info = {
-        "kernel": an_name.replace("+", " + ") + (" (the tick's RD launches: inter and intra on two streams, then final; "
+        "kernel": an_name.replace("+", " + ") + (" (the dataflow wavefront: one launch per segment of ticks, one workgroup "
+                                                  "per macroblock running its search, intra decisions and final)" if FLOW else
+                                                  " (the tick's RD launches: inter and intra on two streams, then final; "
                                                   "the span of the three)" if RDO else
                                                   "" if ffs and not cfg["t8"] else " (the tick's analysis launches)"),
         "avg_launch_ms": round(an_launch_ms, 5),

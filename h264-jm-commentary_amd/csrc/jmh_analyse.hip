@@ -42,6 +42,9 @@
 #include "jmh_intra8.h"
 #include "jmh_intra.h"
 #include "jmh_i4.h"
+#ifdef JMH_FLOW_TU
+#include "jmh_final.h"          // k_mb_flow (jmh_flow.hip compiles this file with JMH_FLOW_TU)
+#endif
 
 #define MVB_OFF 544                           // mvbits LUT: |4*(centre+offset) - pmv| <= 256 + 259
 #define MVB_LEN 1104
@@ -991,6 +994,7 @@ __device__ __forceinline__ void intra_wave(const DevParams &d, IntraS<uint8_t> &
     PSTAMP(62);
 }
 
+#ifndef JMH_FLOW_TU   // the tick kernels (jmh_flow.hip builds k_mb_flow from the same device functions)
 __global__ __launch_bounds__(NTA, 4) void k_mb_analyse(const TickArgs t) {
     __shared__ AnalyseS s;
     // blocks: [0, nPm) the motion search of each P picture MB with its Intra4x4 decision (longest,
@@ -1075,6 +1079,137 @@ hipError_t jmh_launch_analyse(const TickArgs &t, hipStream_t st) {
     hipLaunchKernelGGL(k_mb_analyse, dim3(nblocks), dim3(NTA), 0, st, t);
     return hipGetLastError();
 }
+#endif
+
+#ifdef JMH_FLOW_TU
+// ======================================================================================
+//  k_mb_flow: the dataflow wavefront (jmh_device.h FlowArgs)
+// ======================================================================================
+__device__ __forceinline__ DevParams flow_params(const FlowArgs &f, const PicParams &q) {
+    DevParams d;
+    d.W = f.W; d.H = f.H; d.Wc = f.W >> 1; d.Hc = f.H >> 1; d.mbw = f.mbw; d.mbh = f.mbh;
+    d.sr = f.sr; d.side = 2 * f.sr + 1; d.npos = d.side * d.side;
+    d.search_mode = f.search_mode; d.use_hadamard = f.use_hadamard; d.restrict_sr = f.restrict_sr;
+    d.isr = f.isr;
+    d.t8 = 0;
+    d.epzs_dual = 0; d.epzs_subpel = 0; d.epzs_spts = 0; d.epzs_mints = 0; d.epzs_maxts = 0;
+    d.slice_mbs = f.slice_mbs;
+    d.maxv = 255; d.qpbd = 0;
+    const int ls = f.W * f.H, lc = ls >> 2;
+    d.orgY = q.org; d.orgU = q.org + ls; d.orgV = q.org + ls + lc;
+    d.refY = q.ref; d.refU = q.ref + ls; d.refV = q.ref + ls + lc;
+    d.recY = q.rec; d.recU = q.rec + ls; d.recV = q.rec + ls + lc;
+    d.dbkY = q.dbk; d.dbkU = q.dbk ? q.dbk + ls : nullptr; d.dbkV = q.dbk ? q.dbk + ls + lc : nullptr;
+    d.lf_disable = q.lf_disable; d.lf_offA = q.lf_offA; d.lf_offB = q.lf_offB;
+    d.mv = q.mv; d.refidx = q.refidx; d.ipred = q.ipred; d.res = q.res; d.scr = q.scr;
+    d.tmv = nullptr; d.tref = nullptr; d.ordtab = f.ordtab;
+    d.prof = f.prof; d.prof_mb = f.prof_mb;
+    d.slice_type = q.slice_type; d.qp = q.qp; d.lambda_mode = q.lambda_mode; d.lambda_motion = q.lambda_motion;
+    d.cqp_off = q.cqp_off; d.qsel = q.qsel; d.diag = q.diag; d.y_min = q.y_min;
+    d.rdo = 0; d.cavlc = 0;
+    d.lf = q.lambda_motion << 16;
+    d.lambda_rd = 0;
+    d.rp = nullptr;
+    return d;
+}
+
+#define FLOW_SPIN_MAX (1 << 17)               // polls before a dependency wait gives up (~0.1 s; a wait
+                                              // lasts a few macroblocks, ~0.2 ms, at most)
+__device__ __forceinline__ bool flow_done(const FlowArgs &f, int e, int mb, uint32_t gen) {
+    return __hip_atomic_load(f.flags + (size_t)e * f.nmb + mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gen;
+}
+
+// Persistent: every workgroup claims tickets until the segment is exhausted.  Per macroblock: its
+// left and top-right (top at the right edge) neighbours and the reference picture's MB (x+5, y+5)
+// (PIPE_LAG's reach, clamped) must be done -- the rest of the wavefront's dependencies follow from
+// theirs; then the P macroblock's me_mb (41 searches + Intra4x4), its Intra16x16 / chroma
+// decisions on waves 0 / 1 (or an I macroblock's intra_role), and final_core on all 512 threads.
+// Publication: every wave's stores drained, the workgroup barrier, one agent-scope release, the
+// flag; a waiter polls relaxed, then one agent-scope acquire before the workgroup reads
+// (MI355X_MICROARCH.md, inter-workgroup visibility).
+// One workgroup per macroblock of the segment (grid = the segment's MB count), which claims its
+// macroblock by an atomic ticket when it starts, so the MBs run in tick order as the hardware
+// dispatches workgroups into freed slots.  Per macroblock: its left and top-right (top at the
+// right edge) neighbours and the reference picture's MB (x+5, y+5) (PIPE_LAG's reach, clamped) must
+// be done -- the rest of the wavefront's dependencies follow from theirs; a claimed ticket belongs
+// to a running workgroup and waits only on smaller tickets, so every wait ends.  Then the P
+// macroblock's me_mb (41 searches + Intra4x4), its Intra16x16 / chroma decisions on waves 0 / 1 (an
+// I macroblock: intra_role), and final_core on all 512 threads.  Publication: every wave's stores
+// drained, the workgroup barrier, one agent-scope release, the flag; a waiter polls relaxed, then
+// one agent-scope acquire before the workgroup reads (MI355X_MICROARCH.md, inter-workgroup
+// visibility).
+__global__ __launch_bounds__(NTA, 4) void k_mb_flow(const FlowArgs f) {
+    __shared__ union {
+        AnalyseS a;
+        FinS<uint8_t> fin;
+    } s;
+    __shared__ int s_item;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        const unsigned n = atomicAdd(f.head, 1u) - f.base;   // < nitems: one ticket per workgroup
+        const int item = (int)f.items[n];
+        const int e = item >> 24, mby = (item >> 12) & 0xFFF, mbx = item & 0xFFF;
+        const FlowPic &P = f.pics[e];
+        const uint32_t g = P.gen;
+        const int mb = mby * f.mbw + mbx;
+        const int re = P.pp.slice_type == JMH_P_SLICE ? P.ref_entry : -1;
+        const int rmb = min(mby + 5, f.mbh - 1) * f.mbw + min(mbx + 5, f.mbw - 1);
+        const int tmb = mby > 0 ? (mbx + 1 < f.mbw ? mb - f.mbw + 1 : mb - f.mbw) : -1;
+        // bounded: after FLOW_SPIN_MAX polls (or once any wait of the launch has timed out) the
+        // workgroup goes on and the host reports the launch as failed
+        int spin = 0;
+        while (!((mbx == 0 || flow_done(f, e, mb - 1, g)) && (tmb < 0 || flow_done(f, e, tmb, g)) &&
+                 (re < 0 || flow_done(f, re, rmb, P.ref_gen)))) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spin > FLOW_SPIN_MAX) { __hip_atomic_store(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); break; }
+            if ((spin & 63) == 0 && __hip_atomic_load(f.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_item = item;
+    }
+    __syncthreads();
+    const int item = __builtin_amdgcn_readfirstlane(s_item);   // uniform: the parameters stay scalar loads
+    const int e = item >> 24, mby = (item >> 12) & 0xFFF, mbx = item & 0xFFF;
+    const bool pslice = f.pics[e].pp.slice_type == JMH_P_SLICE;
+    {   // the analysis (DevParams scoped per phase: one set live across me_mb spills)
+        const DevParams d = flow_params(f, f.pics[e].pp);
+        if (pslice) {
+            if (tid >= 256 && tid < 384) load_orgc(d, s.a.me.in.nb, tid - 256, mbx, mby);   // the chroma decision's source
+            me_mb(d, s.a.me, mbx, mby);
+        } else {
+            intra_role(d, s.a.in[tid >> 7], mbx, mby, tid & 127, tid < 128, true);
+        }
+    }
+    asm volatile("" ::: "memory");                            // re-read the parameters below
+    {
+        const DevParams d = flow_params(f, f.pics[e].pp);
+        const int wave = tid >> 6, lane = tid & 63;
+        if (pslice) {
+            __syncthreads();
+            MbScratch *scr = d.scr + mby * d.mbw + mbx;
+            const MbAvail mav = mb_avail(d, mbx, mby);
+            if (wave == 0) i16_decision(d, s.a.me.in.org, s.a.me.in.nb, scr, lane, mav.L, mav.T, mav.TL);
+            else if (wave == 1) chroma_decision(d, s.a.me.in.nb, scr, lane, mav.L, mav.T, mav.TL);
+        }
+        __syncthreads();                                      // MbScratch complete, the analysis LDS dead
+        final_core<5, uint8_t, false, NTA>(d, s.fin, mbx, mby, tid);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(f.flags + (size_t)e * f.nmb + mby * f.mbw + mbx, f.pics[e].gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+hipError_t jmh_launch_flow(const FlowArgs &f, hipStream_t st) {
+    if (f.nitems <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mb_flow, dim3(f.nitems), dim3(NTA), 0, st, f);
+    return hipGetLastError();
+}
+#endif
 
 #ifdef JMH_ISA_PROBE
 // ISA inspection only (hipcc -DJMH_ISA_PROBE -S): one sub-pel search of a 4x4 and of an 8x8 block

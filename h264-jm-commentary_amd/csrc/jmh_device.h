@@ -178,6 +178,42 @@ __host__ __device__ __forceinline__ size_t ffs_slot_bytes(int sr) {
 }
 static_assert(sizeof(TickArgs) <= 4096, "TickArgs is passed by value in the kernel argument segment");
 
+// ---------------------------------------------------------------------------------------------
+//  Dataflow wavefront (k_mb_flow, SearchMode 0 with 8-bit samples, RDO off): one persistent launch
+//  per segment of ticks.  The host flattens the segment's ticks into a list of macroblocks in tick
+//  order; a workgroup claims the next one with an atomic ticket, waits until the macroblocks it
+//  depends on are done (per-MB flags), and runs its whole encode_one_macroblock -- motion search,
+//  intra decisions, the final -- before publishing its own flag.  Every dependency precedes the
+//  MB in tick order, and every claimed ticket belongs to a resident workgroup, so the wait always
+//  ends.
+// ---------------------------------------------------------------------------------------------
+// per ring entry, copied to the device with each segment: the picture's parameters and the flag
+// generations that mark its macroblocks (and its reference picture's) done
+struct FlowPic {
+    PicParams pp;
+    uint32_t gen;                        // flags[entry][mb] >= gen: MB done (the entry's use count)
+    int32_t ref_entry;                   // ring entry of the reference picture (-1: none / explicit buffer)
+    uint32_t ref_gen;
+    int32_t pad;
+};
+struct FlowArgs {
+    int W, H, mbw, mbh, sr, search_mode, use_hadamard, restrict_sr;
+    int isr;                             // InterSearch bits 1..7
+    int slice_mbs;
+    const uint32_t *ordtab;
+    unsigned long long *prof;
+    int prof_mb;
+    const FlowPic *pics;                 // [nring]
+    const uint32_t *items;               // the segment's MBs in tick order: entry << 24 | mby << 12 | mbx
+    int nitems;
+    int nmb;
+    unsigned *head;                      // ticket counter (monotonic over launches)
+    unsigned base;                       // its value at this launch's first ticket
+    uint32_t *flags;                     // [nring][nmb] generations
+    unsigned *err;                       // host-visible: set when a dependency wait timed out
+};
+#define FLOW_ITEM(e, x, y) (((uint32_t)(e) << 24) | ((uint32_t)(y) << 12) | (uint32_t)(x))
+
 // XCD-aware block order.  Workgroups are dispatched round-robin over the 8 XCDs (hardware block b
 // runs on XCD b % 8), each with its own L2.  A launch of n logical blocks uses 8 * ceil(n / 8)
 // hardware blocks and gives every XCD one contiguous run of the logical list, whose consecutive

@@ -29,6 +29,7 @@ hipError_t jmh_launch_final(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_intra8(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_me_full(const TickArgs &t, hipStream_t st);
 hipError_t jmh_launch_epzs(const TickArgs &t, hipStream_t st);
+hipError_t jmh_launch_flow(const FlowArgs &f, hipStream_t st);
 hipError_t jmh_launch_rdo(const TickArgs &t, hipStream_t st, hipStream_t side, hipEvent_t fork, hipEvent_t join);
 size_t jmh_rdo_scratch_bytes();
 hipError_t jmh_launch_block_search_u16(int n, const jmh_block_search *reqs, jmh_block_result *out, const uint16_t *cur, const uint16_t *ref,
@@ -122,6 +123,7 @@ struct PicBuf {
     int recon_read;                      // h_rec holds the occupant's reconstruction
     int unpopped;                        // readback picture not yet popped
     int deblocked;                       // the occupant was deblocked on the device (dbk valid)
+    uint32_t gen;                        // dataflow: occupants so far (the flag value of its MBs)
 };
 
 // a picture in flight (not yet fully issued)
@@ -175,6 +177,23 @@ struct jmh_ctx {
     void *d_rscr;
     void *d_ffs;                         // RDO + SearchMode 0: the tick MBs' SAD tables (k_rdo_inter)
     int nslice;
+    // dataflow wavefront (k_mb_flow): ticks are not launched one by one but
+    // collected into a segment of macroblocks in tick order, launched as one grid on a flush
+    bool flow = false;
+    int seg_max = 0;                     // ticks per segment before a flush (JMH_FLOW_SEG)
+    std::vector<FlowPic> fpic;           // per ring entry: parameters + flag generations
+    std::vector<uint32_t> seg;           // the pending segment's macroblocks (FLOW_ITEM)
+    unsigned long long seg_mask = 0;     // ring entries the pending segment reads or writes
+    int seg_ticks = 0;
+    size_t seg_cap = 0;                  // items the device / staging buffers hold
+    uint8_t *d_seg = nullptr;            // device: FlowPic[nring], then the items
+    uint8_t *h_seg[2] = {nullptr, nullptr};   // pinned staging, alternating
+    hipEvent_t ev_seg[2] = {nullptr, nullptr};
+    int seg_slot = 0;
+    uint32_t *d_flags = nullptr;         // [nring][nmb] generations of the finished MBs
+    unsigned *d_head = nullptr;          // ticket counter
+    unsigned head_base = 0;
+    unsigned *h_err = nullptr;           // pinned, device-written: a dependency wait timed out
 };
 
 #define HCHK(x)                                                                  \
@@ -335,9 +354,14 @@ void jmh_destroy(jmh_ctx *c) {
     if (c->sst) (void)hipStreamSynchronize(c->sst);
     for (PicBuf &b : c->ring) free_entry(b);
     void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab, c->d_scur16,
-                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr, c->d_ffs};
+                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr, c->d_ffs, c->d_seg, c->d_flags, c->d_head};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
+    for (int i = 0; i < 2; i++) {
+        if (c->h_seg[i]) (void)hipHostFree(c->h_seg[i]);
+        if (c->ev_seg[i]) (void)hipEventDestroy(c->ev_seg[i]);
+    }
+    if (c->h_err) (void)hipHostFree(c->h_err);
     ring_free(c->ring_interp);
     ring_free(c->ring_mb);
     ring_free(c->ring_an);
@@ -397,7 +421,18 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     // enough pictures to cover the wavefront: one starts every lag stages
     int auto_depth = (c->nd + c->lag - 1) / c->lag + 1;
     c->depth = cfg->pipeline_depth > 0 ? cfg->pipeline_depth : (auto_depth < PMAX ? auto_depth : PMAX);
-    c->nring = c->depth + 2;
+    // dataflow wavefront: FFS on 8-bit samples, RDO off, no 8x8 transform (k_mb_analyse's search +
+    // k_mb_final); JMH_FLOW=0 keeps the tick launches, as does the per-tick block profile
+    {
+        const char *fe = getenv("JMH_FLOW");
+        c->flow = cfg->search_mode == 0 && c->bd == 8 && !cfg->rdo && !cfg->transform_8x8_mode && !(fe && atoi(fe) == 0) &&
+                  !getenv("JMH_BLOCK_PROF") && c->mbw < 4096 && c->mbh < 4096;
+        const char *sg = getenv("JMH_FLOW_SEG");
+        c->seg_max = sg && atoi(sg) > 0 ? atoi(sg) : 64;
+    }
+    // (dataflow: four more entries, so that an entry's next occupant rarely falls into the segment
+    // that still finishes its previous one, which would force a flush)
+    c->nring = c->depth + 2 + (c->flow ? 4 : 0);
     c->next_id = 0; c->next_entry = 0; c->last_id = -1; c->last_entry = -1;
     c->ref_kind = REF_NONE; c->ref_entry = -1; c->cur_entry = -1;
     c->prof_mb = -1;
@@ -443,6 +478,23 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
             if (hipMemset(c->d_prof, 0, 64 * sizeof(unsigned long long)) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         }
         if (hipHostMalloc((void **)&c->h_stage_ref, c->fsize, hipHostMallocDefault) != hipSuccess) { st = JMH_E_OOM; goto fail; }
+        if (c->flow) {
+            // segment buffers: seg_max ticks of at most PMAX diagonals each
+            c->seg_cap = (size_t)c->seg_max * PMAX * (size_t)std::min(c->mbh, (c->mbw + 1) / 2 + 1) + 1;
+            const size_t sb = (size_t)c->nring * sizeof(FlowPic) + c->seg_cap * sizeof(uint32_t);
+            ALLOC(c->d_seg, sb);
+            ALLOC(c->d_flags, (size_t)c->nring * c->nmb * sizeof(uint32_t));
+            ALLOC(c->d_head, sizeof(unsigned));
+            for (int i = 0; i < 2; i++)
+                if (hipHostMalloc((void **)&c->h_seg[i], sb, hipHostMallocDefault) != hipSuccess ||
+                    hipEventCreateWithFlags(&c->ev_seg[i], hipEventDisableTiming) != hipSuccess) { st = JMH_E_OOM; goto fail; }
+            if (hipHostMalloc((void **)&c->h_err, sizeof(unsigned), hipHostMallocCoherent) != hipSuccess) { st = JMH_E_OOM; goto fail; }
+            *c->h_err = 0;
+            if (hipMemset(c->d_flags, 0, (size_t)c->nring * c->nmb * sizeof(uint32_t)) != hipSuccess ||
+                hipMemset(c->d_head, 0, sizeof(unsigned)) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+            c->fpic.assign(c->nring, FlowPic{});
+            c->seg.reserve(c->seg_cap);
+        }
         if (hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         if (ring_init(c->ring_interp, 64) || ring_init(c->ring_mb, 64) ||
             ((cfg->flags & JMH_FLAG_KERNEL_TIMING) && (ring_init(c->ring_an, 2048) || ring_init(c->ring_fin, 2048)))) { st = JMH_E_HIP; goto fail; }
@@ -570,12 +622,67 @@ static int skip_empty(const jmh_ctx *c, int stage) {
     return stage;
 }
 
+// dataflow: launch the pending segment -- the FlowPic table and the items into the device
+// buffer (pinned staging, alternating; a staging buffer is rewritten only after its copy ran), then
+// one k_mb_flow grid of one workgroup per macroblock.  Stream order covers everything before and
+// after the segment; inside it the per-MB flags do.
+static int flow_flush(jmh_ctx *c) {
+    if (!c->flow || c->seg.empty()) return JMH_OK;
+    const int sl = c->seg_slot;
+    c->seg_slot ^= 1;
+    HCHK(hipEventSynchronize(c->ev_seg[sl]));
+    const size_t pb = (size_t)c->nring * sizeof(FlowPic), ib = c->seg.size() * sizeof(uint32_t);
+    memcpy(c->h_seg[sl], c->fpic.data(), pb);
+    memcpy(c->h_seg[sl] + pb, c->seg.data(), ib);
+    HCHK(hipMemcpyAsync(c->d_seg, c->h_seg[sl], pb + ib, hipMemcpyHostToDevice, c->st));
+    HCHK(hipEventRecord(c->ev_seg[sl], c->st));
+    FlowArgs f;
+    memset(&f, 0, sizeof(f));
+    f.W = c->W; f.H = c->H; f.mbw = c->mbw; f.mbh = c->mbh; f.sr = c->sr;
+    f.search_mode = c->cfg.search_mode; f.use_hadamard = c->cfg.use_hadamard; f.restrict_sr = c->cfg.restrict_search_range;
+    for (int i = 1; i < 8; i++) f.isr |= (c->cfg.inter_search[i] != 0) << i;
+    f.slice_mbs = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : c->mbw * c->mbh;
+    f.ordtab = c->d_ordtab;
+    f.prof = c->d_prof; f.prof_mb = c->prof_mb;
+    f.pics = reinterpret_cast<const FlowPic *>(c->d_seg);
+    f.items = reinterpret_cast<const uint32_t *>(c->d_seg + pb);
+    f.nitems = (int)c->seg.size();
+    f.nmb = (int)c->nmb;
+    f.head = c->d_head; f.base = c->head_base;
+    f.flags = c->d_flags;
+    f.err = c->h_err;
+    const bool kt = c->ring_an.cap > 0;
+    HCHK(ring_begin(c->ring_mb, c->st));
+    if (kt) HCHK(ring_begin(c->ring_an, c->st));
+    HCHK(jmh_launch_flow(f, c->st));
+    if (kt) HCHK(ring_end(c->ring_an, c->st));
+    HCHK(ring_end(c->ring_mb, c->st));
+    c->head_base += (unsigned)c->seg.size();
+    c->timing.flow_launches++;
+    c->timing.flow_mbs += (int)c->seg.size();
+    c->seg.clear();
+    c->seg_mask = 0;
+    c->seg_ticks = 0;
+    return JMH_OK;
+}
+
+// a dependency wait of k_mb_flow that timed out (never expected: every wait ends by construction)
+static int flow_check(jmh_ctx *c) {
+    if (c->flow && c->h_err && __atomic_load_n(c->h_err, __ATOMIC_ACQUIRE)) {
+        fprintf(stderr, "jmhip: k_mb_flow dependency wait timed out (results invalid)\n");
+        return JMH_E_HIP;
+    }
+    return JMH_OK;
+}
+
 // after a picture's last tick: its readback on the copy stream (the D2H overlaps the ticks of
 // the pictures still in flight; the entry's device buffers are not written again before the host
 // has popped the picture, which waits for ev_done), then the done event
 static int finish_picture(jmh_ctx *c, const Flight &f) {
     c->timing.pictures_done++;
     if (!f.readback) return JMH_OK;
+    int r = flow_flush(c);                // the picture's last MBs before its events
+    if (r) return r;
     PicBuf &b = c->ring[f.entry];
     HCHK(hipEventRecord(b.ev_fin, c->st));
     HCHK(hipStreamWaitEvent(c->cst, b.ev_fin, 0));
@@ -642,7 +749,24 @@ static int issue_tick(jmh_ctx *c) {
         HCHK(hipMemsetAsync(c->d_bprof, 0, ((size_t)3 * 3 * PMAX * c->mbh + 64) * sizeof(unsigned long long), c->st));
         c->bprof_blocks = na + xcd_grid(t.pre[k]);
     }
-    if (nact) {
+    if (nact && c->flow) {
+        // dataflow: the tick's macroblocks join the pending segment in tick order (P pictures
+        // first, diagonal MBs top to bottom, as the tick kernels' block order)
+        for (int pass = 0; pass < 2; pass++)
+            for (int a = 0; a < nact; a++) {
+                const Flight &f = c->fl[act[a]];
+                if ((f.pp.slice_type == JMH_P_SLICE) != (pass == 0)) continue;
+                const int y0 = c->dymin[f.stage], n = c->dcount[f.stage];
+                for (int i = 0; i < n; i++) c->seg.push_back(FLOW_ITEM(f.entry, f.stage - 2 * (y0 + i), y0 + i));
+                c->seg_mask |= 1ull << f.entry;
+                if (f.ref_entry >= 0) c->seg_mask |= 1ull << f.ref_entry;
+            }
+        c->seg_ticks++;
+        c->ticks_total++;
+        c->timing.ticks++;
+        c->timing.tick_mbs += mbs;
+        c->timing.mb_launches += 1;
+    } else if (nact) {
         const bool kt = c->ring_an.cap > 0 && c->ticks_total % KT_STRIDE == 0;   // sampled per-launch timing
         if (kt) HCHK(ring_begin(c->ring_an, c->st));
         if (t.rdo) {                                    // RDOptimization 1: analyse + final
@@ -678,6 +802,7 @@ static int issue_tick(jmh_ctx *c) {
         c->fl.pop_front();
         if (r) return r;
     }
+    if (c->flow && c->seg_ticks >= c->seg_max) return flow_flush(c);
     return JMH_OK;
 }
 
@@ -691,6 +816,14 @@ static bool entry_busy(const jmh_ctx *c, int e) {
 template <class Cond>
 static int issue_while(jmh_ctx *c, Cond cond) {
     if (!cond()) return JMH_OK;
+    if (c->flow) {   // the launches happen at flushes (flow_flush brackets them with ring_mb)
+        int r = JMH_OK;
+        while (!r && cond()) {
+            if (c->fl.empty()) return JMH_E_STATE;
+            r = issue_tick(c);
+        }
+        return r;
+    }
     HCHK(ring_begin(c->ring_mb, c->st));
     int r = JMH_OK;
     while (!r && cond()) {
@@ -701,7 +834,10 @@ static int issue_while(jmh_ctx *c, Cond cond) {
     return r;
 }
 
-static int drain(jmh_ctx *c) { return issue_while(c, [c] { return !c->fl.empty(); }); }
+static int drain(jmh_ctx *c) {
+    int r = issue_while(c, [c] { return !c->fl.empty(); });
+    return r ? r : flow_flush(c);
+}
 
 static const uint8_t *ref_ptr(const jmh_ctx *c) {
     if (c->ref_kind == REF_REC) return c->ring[c->ref_entry].rec;
@@ -753,6 +889,13 @@ static int push_picture(jmh_ctx *c, const uint8_t *src, int entry, const jmh_fra
         HCHK(hipMemcpyAsync(reinterpret_cast<uint8_t *>(b.scr) + rdo_pic_offset(c->nmb), b.h_rp, sizeof(RdoPic), hipMemcpyHostToDevice, c->st));
         HCHK(hipEventRecord(b.ev_rp, c->st));
     }
+    if (c->flow) {
+        FlowPic &fp2 = c->fpic[entry];
+        fp2.pp = q;
+        fp2.gen = ++b.gen;
+        fp2.ref_entry = f.ref_entry;
+        fp2.ref_gen = f.ref_entry >= 0 ? c->ring[f.ref_entry].gen : 0;
+    }
     c->fl.push_back(f);
     c->last_id = f.id;
     c->last_entry = entry;
@@ -788,6 +931,7 @@ static int claim_entry(jmh_ctx *c, int *out) {
     if (c->ring[e].unpopped) return JMH_E_STATE;
     int r = issue_while(c, [c, e] { return entry_busy(c, e); });
     if (r) return r;
+    if (c->flow && ((c->seg_mask >> e) & 1) && (r = flow_flush(c))) return r;   // its last readers before its rewrite
     if ((c->ref_kind == REF_REC || c->ref_kind == REF_DBK) && c->ref_entry == e) {
         if ((r = drain(c))) return r;   // pictures in flight may still read d_ref
         HCHK(hipMemcpyAsync(c->d_ref, ref_ptr(c), c->fsize, hipMemcpyDeviceToDevice, c->st));
@@ -888,6 +1032,7 @@ int jmh_frame_pop(jmh_ctx *c) {
     int ahead = PIPE_LAG;
     if ((r = issue_while(c, [c, &ahead] { return ahead-- > 0 && !c->fl.empty(); }))) return r;
     HCHK(hipEventSynchronize(c->ring[e].ev_done));
+    if ((r = flow_check(c))) return r;
     c->popq.pop_front();
     c->ring[e].unpopped = 0;
     c->cur_entry = e;
@@ -960,6 +1105,7 @@ int jmh_sync(jmh_ctx *c) {
     int r = drain(c);
     if (r) return r;
     HCHK(hipStreamSynchronize(c->st));
+    if ((r = flow_check(c))) return r;
     if (c->d_bprof && c->bprof_blocks) {   // debug: block durations of one tick, per role
         std::vector<unsigned long long> h(3 * c->bprof_blocks);
         HCHK(hipMemcpy(h.data(), c->d_bprof, h.size() * 8, hipMemcpyDeviceToHost));
@@ -1038,13 +1184,17 @@ int jmh_sync(jmh_ctx *c) {
 int jmh_wait_issued(jmh_ctx *c) {
     if (!c) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
+    int r = flow_flush(c);
+    if (r) return r;
     HCHK(hipStreamSynchronize(c->st));
-    return JMH_OK;
+    return flow_check(c);
 }
 
 int jmh_get_timing(jmh_ctx *c, jmh_timing *t) {
     if (!c || !t) return JMH_E_INVALID_ARG;
     HCHK(hipSetDevice(c->dev));
+    int r = flow_flush(c);
+    if (r) return r;
     HCHK(hipStreamSynchronize(c->st));   // the issued launches only: pictures in flight stay
     int npic = 0;
     ring_drain(c->ring_interp, c->timing.interp_ms, c->timing.interps);
@@ -1057,7 +1207,8 @@ int jmh_get_timing(jmh_ctx *c, jmh_timing *t) {
     // counters restart (total_ms stays: the last popped picture)
     c->timing.pictures = 0; c->timing.mb_launches = 0; c->timing.ticks = 0; c->timing.tick_mbs = 0;
     c->timing.pictures_done = 0;
-    return JMH_OK;
+    c->timing.flow_launches = 0; c->timing.flow_mbs = 0;
+    return flow_check(c);
 }
 
 int jmh_ffs_sad_table(jmh_ctx *c, int n_mb, const int32_t *mb_xy, const int32_t *centres, uint16_t *out) {

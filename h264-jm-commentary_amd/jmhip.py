@@ -18,7 +18,7 @@ HOST_LIB_PATH = os.path.join(HERE, "host", "build", "libjmhost.so")
 JMH_OK = 0
 JMH_E_INVALID_ARG, JMH_E_HIP, JMH_E_OOM, JMH_E_UNSUPPORTED_CFG, JMH_E_STATE, JMH_E_NO_DEVICE = -1, -2, -3, -4, -5, -6
 JMH_P_SLICE, JMH_I_SLICE = 0, 2
-JMH_ABI_VERSION = 13
+JMH_ABI_VERSION = 14
 JMH_FLAG_KERNEL_TIMING = 1
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "unsupported configuration", -5: "invalid call order", -6: "no HIP device"}
@@ -71,7 +71,8 @@ class JmhTiming(ctypes.Structure):
                 ("analyse_ms", ctypes.c_float), ("analyse_launches", ctypes.c_int32),
                 ("final_ms", ctypes.c_float), ("final_launches", ctypes.c_int32),
                 ("ticks", ctypes.c_int32), ("tick_mbs", ctypes.c_int32),
-                ("pictures_done", ctypes.c_int32)]
+                ("pictures_done", ctypes.c_int32),
+                ("flow_launches", ctypes.c_int32), ("flow_mbs", ctypes.c_int32)]
 
 
 class JmhBlockSearch(ctypes.Structure):

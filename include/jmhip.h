@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JMH_ABI_VERSION 13
+#define JMH_ABI_VERSION 14
 #define JMH_LAMBDA_MAX 1023   /* jmh_frame_params lambdas: lambda * mvbits fits the u16 cost tables */
 #define JMH_QOFFSET_MAX 2047  /* jmh_config.quant_offset: OffsetBits 11 (1 << 11 = a whole step)    */
 
@@ -208,6 +208,10 @@ typedef struct jmh_timing {
     int32_t tick_mbs;          /* macroblocks processed by those ticks                          */
     int32_t pictures_done;     /* pictures whose last tick was issued (completed once the
                                   issued work has drained: jmh_wait_issued)                      */
+    int32_t flow_launches;     /* ABI 14: dataflow launches (k_mb_flow: one per segment of ticks,
+                                  SearchMode 0 at 8 bits, RDO off); analyse_ms / analyse_launches
+                                  then time those launches                                        */
+    int32_t flow_mbs;          /*   ... and the macroblocks they processed                        */
 } jmh_timing;
 
 typedef struct jmh_ctx jmh_ctx;

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_strerror():
     lib = jmhip.load()
-    assert lib.jmh_abi_version() == jmhip.JMH_ABI_VERSION == 13
+    assert lib.jmh_abi_version() == jmhip.JMH_ABI_VERSION == 14
     for code, text in jmhip.STATUS.items():
         assert lib.jmh_strerror(code).decode() == text
 

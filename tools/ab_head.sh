@@ -7,7 +7,7 @@ T=$(mktemp -d)
 git -C "$R" archive HEAD h264-jm-commentary_amd/csrc include | tar -x -C "$T"
 cd "$T/h264-jm-commentary_amd/csrc"
 pids=()
-for f in jmh_kernels jmh_analyse jmh_fullsearch jmh_epzs jmh_intra8 jmh_final jmh_block jmh_hbd jmh_rdo jmhip_abi; do
+for f in jmh_kernels jmh_analyse jmh_flow jmh_fullsearch jmh_epzs jmh_intra8 jmh_final jmh_block jmh_hbd jmh_rdo jmhip_abi; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -c $f.hip -o "$T/$f.o" &
   pids+=($!)
 done
