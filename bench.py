@@ -55,7 +55,9 @@ METRIC = ("ME+transform megapixels/sec @1080p FullSearch SR=32; bit-exact vs the
           + TIMER)
 # BASELINE.json configs measured here: 2 (the headline) and 3 (variant)
 CONFIGS = {
-    2: dict(metric=METRIC, disp=(1920, 1080), coded=(1920, 1088), search_mode=0, t8=0,
+    # metric_sm: how the metric names the config's own search (BASELINE.json: "FullSearch" for FFS,
+    # JM's exact fast full search), replaced when --search-mode measures another one
+    2: dict(metric=METRIC, metric_sm="FullSearch", disp=(1920, 1080), coded=(1920, 1088), search_mode=0, t8=0,
             workload="1080p synthetic YUV420 (coded 1920x1088), Baseline, {sm} SearchRange=32, RestrictSearchRange=2, "
                      "UseHadamard=1, 7 inter block sizes, RDO off, QP 28, IDR + {nf}-picture P sequence cycled "
                      "(one independent stream per GPU)"),
@@ -212,13 +214,38 @@ def cpu_model():
     return "unknown"
 
 
+def available_cores():
+    """(n, affinity, quota, online): the CPUs this process may use -- its affinity mask, capped by
+    the cgroup's CPU quota (cgroup v2 cpu.max or v1 cfs_quota_us / cfs_period_us) where one is set,
+    which on a shared box is far below the CPUs it can see -- and the machine's online count."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, aff, quota, os.cpu_count()
+
+
 def cpu_baseline(config, search_mode, dump_dir, T8):
     """The CPU path timed on this node's host cores: one process on one core (JM is
     single threaded; the reported baseline), and n processes on distinct streams at once
-    (aggregate, n = min(16, cores available to this process)).  Worker 0 of the one-core run
-    dumps its I + P results for the GPU check."""
+    (aggregate, n = every core available to this process: available_cores).  Worker 0 of the
+    one-core run dumps its I + P results for the GPU check."""
     one = cpu_workers(1, config, search_mode, (DISP_W, DISP_H), dump_dir)[0]
-    n = max(1, min(16, len(os.sched_getaffinity(0))))
+    n, aff, quota, online = available_cores()
     many = cpu_workers(n, config, search_mode, (DISP_W, DISP_H))
     mode = {0: "FFS", -1: "full search", 3: "EPZS"}[search_mode] + (" + 8x8 transform" if T8 else "") \
         + (f", {BD}-bit" if BD > 8 else "") + (f", {SLICE_MBS}-MB slices" if SLICE_MBS else "") \
@@ -227,8 +254,10 @@ def cpu_baseline(config, search_mode, dump_dir, T8):
             "sample": f"one {DISP_W}x{DISP_H} P picture (coded {W}x{H}, {NMB} MBs, {mode} SR=32, QP {QP}) incl. "
                       f"quarter-pel interpolation, oracle/liboracle.so -O2 scalar, {one:.1f} s, on {cpu_model()}",
             "all_cores": {"value": round(n * DISP_W * DISP_H / 1e6 / max(many), 4), "unit": "MP/s", "cores": n,
-                          "sample": f"{n} processes, one P picture each on distinct streams, concurrently, "
-                                    f"{max(many):.1f} s wall"}}
+                          "cores_available": {"affinity": aff, "cgroup_quota": quota, "online": online},
+                          "sample": f"{n} processes (every core available to this process: affinity {aff}, cgroup "
+                                    f"quota {'none' if quota is None else f'{quota:g}'}; {online} online), one P picture "
+                                    f"each on distinct streams, concurrently, {max(many):.1f} s wall"}}
 
 
 def verify_against_oracle(jm, dump, search_mode, t8, device):
@@ -411,8 +440,8 @@ def main():
     SLICE_MBS = max(0, cfg.get("slice_mbs", 0) if args.slice_mbs is None else args.slice_mbs)
     search_mode = cfg["search_mode"] if args.search_mode is None else args.search_mode
     if search_mode != cfg["search_mode"]:   # the metric names the search the line measured
-        sm_label = {0: "FFS", -1: "FullSearch", 3: "EPZS"}
-        cfg["metric"] = cfg["metric"].replace(sm_label[cfg["search_mode"]], sm_label[search_mode], 1)
+        own = cfg.get("metric_sm", {0: "FFS", -1: "FullSearch", 3: "EPZS"}[cfg["search_mode"]])
+        cfg["metric"] = cfg["metric"].replace(own, {0: "FFS", -1: "FullSearch SearchMode=-1", 3: "EPZS"}[search_mode], 1)
     if args.epzs_jm10:
         if search_mode != 3:
             ap.error("--epzs-jm10 applies to EPZS (SearchMode 3)")

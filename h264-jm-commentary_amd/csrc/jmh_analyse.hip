@@ -573,7 +573,8 @@ __device__ __forceinline__ void p8x8_block(const DevParams &d, MeS &s, PosState 
     // long enough to hide a step: the multi-search stages 0 and 1 of every block (block 3's stage
     // 0 has one free wave, so its step, 8, is a one-block step), two steps in single-search stages
     constexpr int IS0 = 3 * B8 - (B8 == 3 ? 1 : 0), IS1 = IS0 + 1;
-    constexpr int IS2 = B8 <= 1 ? 3 * B8 + 2 : B8 == 3 ? 10 : -1, IS3 = -1;
+    // (k_mb_flow: block 2's stage 2, slot 11, the Intra16x16 and chroma intra-mode decisions)
+    constexpr int IS2 = B8 <= 1 ? 3 * B8 + 2 : B8 == 3 ? 10 : 11, IS3 = -1;
     const int sr = d.sr;
     fence_state(ps);
     sad_strip<false, 4 * X, 4 * Y, 0, 0>(s, ps);        // the four 4x4 SADs of this 8x8 block
@@ -655,17 +656,34 @@ __device__ __forceinline__ void i16_decision(const DevParams &d, const pel *org,
     if (lane == 0) { scr->i16cost = best; scr->i16mode = i16mode; }
 }
 
-// IntraChromaPrediction8x8 mode decision on one wave: 4 modes x 2 components x 4 blocks
+// IntraChromaPrediction8x8 mode decision on one wave: 4 modes x 2 components x 4 blocks.  A lane's
+// DC and plane parameters once, then each sample selected without branching (a per-lane mode
+// switch ran all four paths, the plane's parameters per sample)
 template <class pel>
 __device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraNb<pel> &nb, MbScratch *scr, int lane, bool avL, bool avT, bool avTL) {
     int sat = 0;
     if (lane < 32) {
         const int m = lane >> 3, uv = (lane >> 2) & 1, b = lane & 3, xo = (b & 1) * 4, yo = (b >> 1) * 4;
         const pel *T = nb.ctop[uv] + 1, *L = nb.cleft[uv];
+        const int Pc = nb.ctop[uv][0];
+        const int dcv = chroma_dc(T, L, avT, avL, b, (d.maxv + 1) >> 1);
+        int ih = 0, iv = 0;
+#pragma unroll
+        for (int i = 1; i <= 4; i++) {
+            ih += i * (T[3 + i] - (3 - i >= 0 ? T[3 - i] : Pc));
+            iv += i * (L[3 + i] - (3 - i >= 0 ? L[3 - i] : Pc));
+        }
+        const int ib = (34 * ih + 32) >> 6, ic = (34 * iv + 32) >> 6, iaa = 16 * (L[7] + T[7]);
         int df[16];
+#pragma unroll
         for (int y = 0; y < 4; y++)
-            for (int x = 0; x < 4; x++)
-                df[4 * y + x] = nb.orgc[uv][(yo + y) * 8 + xo + x] - chroma_pred_px(T, L, nb.ctop[uv][0], avT, avL, m, xo + x, yo + y, d.maxv);
+#pragma unroll
+            for (int x = 0; x < 4; x++) {
+                const int px = xo + x, py = yo + y;
+                const int pl = clipmx((iaa + (px - 3) * ib + (py - 3) * ic + 16) >> 5, d.maxv);
+                const int p = m == 0 ? dcv : m == 1 ? (int)L[py] : m == 2 ? (int)T[px] : pl;
+                df[4 * y + x] = nb.orgc[uv][py * 8 + px] - p;
+            }
         sat = satd4x4(df, d.use_hadamard);
     }
     const bool cav[4] = {true, avL, avT, avT && avL && avTL};
@@ -939,7 +957,12 @@ __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &
     const int lane = threadIdx.x & 63;
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
-    if (k < 10) {
+    if (k == 11) {                                       // k_mb_flow: Intra16x16 (wave 6), chroma (wave 7)
+        if (d.i16c) {
+            if (w == 0) i16_decision(d, s.org, s.nb, scr, lane, avL, avT, avTL);
+            else chroma_decision(d, s.nb, scr, lane, avL, avT, avTL);
+        }
+    } else if (k < 10) {
         const int q_bits = 15 + d.qp / 6;
         const int qpk = q_round(d.qsel, q_bits);
         int tabr[2];
@@ -1107,11 +1130,43 @@ __device__ __forceinline__ DevParams flow_params(const FlowArgs &f, const PicPar
     d.slice_type = q.slice_type; d.qp = q.qp; d.lambda_mode = q.lambda_mode; d.lambda_motion = q.lambda_motion;
     d.cqp_off = q.cqp_off; d.qsel = q.qsel; d.diag = q.diag; d.y_min = q.y_min;
     d.rdo = 0; d.cavlc = 0;
+    d.i16c = 1;
     d.lf = q.lambda_motion << 16;
     d.lambda_rd = 0;
     d.rp = nullptr;
     return d;
 }
+
+// k_mb_flow's luma MC: the quarter-pel sample at (X, Y) from the P macroblock's search window
+// planes still in LDS (G, b, h, j at window coordinates; ox / oy: the window origin in the
+// picture), the same values as qpel_direct (the window is the clamped reference and the planes
+// its 6-tap half samples).  The final's MVs are the searches' results, within +-(SR + 3/4) of the
+// window centre, so every sample lies in the planes' rows / columns [3, 2 SR + 21).
+struct PlaneMC {
+    uint32_t g;                                // LDS byte address of the G plane
+    int ox, oy;
+    __device__ __forceinline__ int at(int plane, int x, int y) const {
+        return ((lds_cu8 *)(uintptr_t)(g + plane * PLS + y * WST + x))[0];
+    }
+    __device__ __forceinline__ int operator()(int X, int Y) const {
+        const int x = (X >> 2) - ox, y = (Y >> 2) - oy, fx = X & 3, fy = Y & 3;
+        if (fy == 0) {
+            const int G = at(0, x, y);
+            if (fx == 0) return G;
+            const int b = at(1, x, y);
+            return fx == 2 ? b : ((fx == 1 ? G : at(0, x + 1, y)) + b + 1) >> 1;
+        }
+        if (fx == 0) {
+            const int h = at(2, x, y);
+            return fy == 2 ? h : ((fy == 1 ? at(0, x, y) : at(0, x, y + 1)) + h + 1) >> 1;
+        }
+        if ((fx & 1) && (fy & 1)) return (at(1, x, fy == 1 ? y : y + 1) + at(2, fx == 1 ? x : x + 1, y) + 1) >> 1;   // e g p r
+        const int j = at(3, x, y);
+        if (fx == 2 && fy == 2) return j;
+        const int o = fx == 2 ? at(1, x, fy == 1 ? y : y + 1) : at(2, fx == 1 ? x : x + 1, y);   // f q / i k
+        return (j + o + 1) >> 1;
+    }
+};
 
 #define FLOW_SPIN_MAX (1 << 17)               // polls before a dependency wait gives up (~0.1 s; a wait
                                               // lasts a few macroblocks, ~0.2 ms, at most)
@@ -1139,39 +1194,62 @@ __device__ __forceinline__ bool flow_done(const FlowArgs &f, int e, int mb, uint
 // one agent-scope acquire before the workgroup reads (MI355X_MICROARCH.md, inter-workgroup
 // visibility).
 __global__ __launch_bounds__(NTA, 4) void k_mb_flow(const FlowArgs f) {
-    __shared__ union {
-        AnalyseS a;
+    // the final's LDS beside the analysis' (81.1 KB: still two workgroups per CU), so that it reads
+    // the MB's source, intra neighbourhood and search window planes where the analysis left them
+    __shared__ struct {
         FinS<uint8_t> fin;
+        AnalyseS a;
     } s;
     __shared__ int s_item;
+    __shared__ unsigned s_tk;
     const int tid = threadIdx.x;
+    const unsigned long long t0 = f.fprof ? wall_clock64() : 0;
     if (tid == 0) {
         const unsigned n = atomicAdd(f.head, 1u) - f.base;   // < nitems: one ticket per workgroup
-        const int item = (int)f.items[n];
-        const int e = item >> 24, mby = (item >> 12) & 0xFFF, mbx = item & 0xFFF;
-        const FlowPic &P = f.pics[e];
-        const uint32_t g = P.gen;
-        const int mb = mby * f.mbw + mbx;
-        const int re = P.pp.slice_type == JMH_P_SLICE ? P.ref_entry : -1;
-        const int rmb = min(mby + 5, f.mbh - 1) * f.mbw + min(mbx + 5, f.mbw - 1);
-        const int tmb = mby > 0 ? (mbx + 1 < f.mbw ? mb - f.mbw + 1 : mb - f.mbw) : -1;
-        // bounded: after FLOW_SPIN_MAX polls (or once any wait of the launch has timed out) the
-        // workgroup goes on and the host reports the launch as failed
-        int spin = 0;
-        while (!((mbx == 0 || flow_done(f, e, mb - 1, g)) && (tmb < 0 || flow_done(f, e, tmb, g)) &&
-                 (re < 0 || flow_done(f, re, rmb, P.ref_gen)))) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spin > FLOW_SPIN_MAX) { __hip_atomic_store(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); break; }
-            if ((spin & 63) == 0 && __hip_atomic_load(f.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        s_tk = n;
+        int item = n < (unsigned)f.nitems ? (int)f.items[n] : -1;
+        // (never expected) a ticket or item out of range: reported, the workgroup does nothing
+        if (item < 0 || (item >> 24) >= f.nring || ((item >> 12) & 0xFFF) >= f.mbh || (item & 0xFFF) >= f.mbw) {
+            __hip_atomic_store(f.err + 1, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(f.err + 2, (unsigned)item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(f.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            item = -1;
+        } else {
+            const int e = item >> 24, mby = (item >> 12) & 0xFFF, mbx = item & 0xFFF;
+            const FlowPic &P = f.pics[e];
+            const uint32_t g = P.gen;
+            const int mb = mby * f.mbw + mbx;
+            const int re = P.pp.slice_type == JMH_P_SLICE ? P.ref_entry : -1;
+            const int rmb = min(mby + 5, f.mbh - 1) * f.mbw + min(mbx + 5, f.mbw - 1);
+            const int tmb = mby > 0 ? (mbx + 1 < f.mbw ? mb - f.mbw + 1 : mb - f.mbw) : -1;
+            // bounded: after FLOW_SPIN_MAX polls (or once any wait of the launch has timed out) the
+            // workgroup goes on and the host reports the launch as failed
+            int spin = 0;
+            while (!((mbx == 0 || flow_done(f, e, mb - 1, g)) && (tmb < 0 || flow_done(f, e, tmb, g)) &&
+                     (re < 0 || flow_done(f, re, rmb, P.ref_gen)))) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spin > FLOW_SPIN_MAX) { __hip_atomic_store(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); break; }
+                if ((spin & 63) == 0 && __hip_atomic_load(f.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         s_item = item;
     }
     __syncthreads();
     const int item = __builtin_amdgcn_readfirstlane(s_item);   // uniform: the parameters stay scalar loads
+    if (item < 0) return;
     const int e = item >> 24, mby = (item >> 12) & 0xFFF, mbx = item & 0xFFF;
     const bool pslice = f.pics[e].pp.slice_type == JMH_P_SLICE;
+    // debug stamps (JMH_FLOW_PROF): the slot is re-derived at each use, nothing stays live across me_mb
+#define FLOW_FP (f.fprof ? f.fprof + 6 * (size_t)__builtin_amdgcn_readfirstlane(s_tk) : nullptr)
+    if (unsigned long long *fp = FLOW_FP; fp && tid == 0) {
+        fp[0] = t0;
+        fp[1] = wall_clock64();
+        const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (15 << 11));    // HW_ID bits 0..15
+        const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));   // XCC_ID bits 0..3
+        fp[5] = (unsigned long long)(hw | xcc << 16) << 32 | (unsigned)item;
+    }
     {   // the analysis (DevParams scoped per phase: one set live across me_mb spills)
         const DevParams d = flow_params(f, f.pics[e].pp);
         if (pslice) {
@@ -1181,27 +1259,32 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_flow(const FlowArgs f) {
             intra_role(d, s.a.in[tid >> 7], mbx, mby, tid & 127, tid < 128, true);
         }
     }
+    if (unsigned long long *fp = FLOW_FP; fp && tid == 0) fp[2] = wall_clock64();
     asm volatile("" ::: "memory");                            // re-read the parameters below
     {
         const DevParams d = flow_params(f, f.pics[e].pp);
-        const int wave = tid >> 6, lane = tid & 63;
-        if (pslice) {
-            __syncthreads();
-            MbScratch *scr = d.scr + mby * d.mbw + mbx;
-            const MbAvail mav = mb_avail(d, mbx, mby);
-            if (wave == 0) i16_decision(d, s.a.me.in.org, s.a.me.in.nb, scr, lane, mav.L, mav.T, mav.TL);
-            else if (wave == 1) chroma_decision(d, s.a.me.in.nb, scr, lane, mav.L, mav.T, mav.TL);
-        }
-        __syncthreads();                                      // MbScratch complete, the analysis LDS dead
-        final_core<5, uint8_t, false, NTA>(d, s.fin, mbx, mby, tid);
+        const bool prof = prof_mb_here(d, mbx, mby);
+        PSTAMP(56);
+        __syncthreads();                                      // MbScratch complete
+        PSTAMP(58);
+        int pcx = 0, pcy = 0;                                 // me_mb's window origin (SetupFastFullPelSearch centre)
+        if (pslice) set_mvp(NbBorder{s.a.me.bd}, 0, 0, 16, 16, pcx, pcy);
+        const int scx = iclip(-d.sr, d.sr, pcx / 4), scy = iclip(-d.sr, d.sr, pcy / 4);
+        const PlaneMC mc{(uint32_t)(uintptr_t)(lds_cu8 *)s.a.me.planes, 16 * mbx + scx - d.sr - WM, 16 * mby + scy - d.sr - WM};
+        IntraS<uint8_t> &in = pslice ? s.a.me.in : s.a.in[0];  // (I macroblocks: no MC)
+        final_core<5, uint8_t, false, NTA>(d, s.fin, mbx, mby, tid, mc, in.org, &in.nb);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+        unsigned long long *fp = FLOW_FP;
+        if (fp) fp[3] = wall_clock64();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(f.flags + (size_t)e * f.nmb + mby * f.mbw + mbx, f.pics[e].gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fp) fp[4] = wall_clock64();
     }
+#undef FLOW_FP
 }
 
 hipError_t jmh_launch_flow(const FlowArgs &f, hipStream_t st) {

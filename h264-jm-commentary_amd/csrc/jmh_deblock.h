@@ -75,14 +75,57 @@ struct DbkS {
     pel dy[20][20];                      // luma, rows / columns -4..15 -> [r + 4][c + 4]
     pel dc2[2][12][12];                  // chroma, rows / columns -4..7
     int8_t bs[2][4][4];                  // boundary strength [dir][edge][segment]
+    int16_t nmv[2][4][2];                // deblock_prefetch: the left / top neighbour's MV of each
+    int32_t nbits[2];                    //   edge segment's 4x4 block, its cbp_blk bits and intra flag
+    int8_t nintra[2];
 };
+
+// DeblockMb's inputs from outside the macroblock -- the left and top neighbours' filtered samples
+// (4 rows / columns, luma and chroma) and the mb_type / cbp_blk / MVs its boundary strengths read
+// -- into LDS, NTH threads.  Final from the moment the MB's dependencies are done: only the MB
+// itself, its left / top neighbours and the top-right one (done before it) write those samples, so
+// the caller issues these loads early (final_core: with its own inputs) and deblock_mb<PRE> uses them.
+template <class pel, int NTH>
+__device__ __forceinline__ void deblock_prefetch(const DevParams &d, DbkS<pel> &s, int mbx, int mby, int tid) {
+    const pel *dbkY = spl<pel>(d.dbkY), *dbkU = spl<pel>(d.dbkU), *dbkV = spl<pel>(d.dbkV);
+    const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, Wc = d.Wc;
+    const bool dbL = mbx > 0, dbT = mby > 0;
+    for (int i = tid; i < 256 + 16; i += NTH) {
+        if (i < 128) {                                   // luma: rows -4..-1 (i < 64), columns -4..-1
+            const bool top = i < 64;
+            const int a = i & 63, r = top ? (a >> 4) - 4 : a >> 2, c = top ? a & 15 : (a & 3) - 4;
+            s.dy[r + 4][c + 4] = (top ? dbT : dbL) ? dbkY[(pix_y + r) * W + pix_x + c] : (pel)0;
+        } else if (i < 256) {                            // chroma: per plane rows -4..-1, columns -4..-1
+            const int j = i - 128, pl = j >> 6, a = j & 63;
+            const bool top = a < 32;
+            const int b = a & 31, r = top ? (b >> 3) - 4 : b >> 2, c = top ? b & 7 : (b & 3) - 4;
+            s.dc2[pl][r + 4][c + 4] = (top ? dbT : dbL) ? (pl ? dbkV : dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c] : (pel)0;
+        } else {                                         // the neighbours' results (bS, 8.7.2.1)
+            const int j = i - 256, dir = j >> 3, k = j & 7;
+            const bool av = dir == 0 ? dbL : dbT;
+            if (av) {
+                const jmh_mb_result *rp = d.res + (dir == 0 ? mby * d.mbw + mbx - 1 : (mby - 1) * d.mbw + mbx);
+                if (k < 4) {
+                    const int bp = dir == 0 ? k * 4 + 3 : 12 + k;
+                    s.nmv[dir][k][0] = rp->mv[bp][0];
+                    s.nmv[dir][k][1] = rp->mv[bp][1];
+                } else if (k == 4) {
+                    s.nbits[dir] = rp->cbp_blk;
+                } else if (k == 5) {
+                    const int t = rp->mb_type;
+                    s.nintra[dir] = t == JMH_I4MB || t == JMH_I16MB || t == JMH_I8MB;
+                }
+            }
+        }
+    }
+}
 
 // the MB's deblocking on NT threads (tid), after its reconstruction rec (LDS, 16x16) / cfin (LDS,
 // 2 x 8x8) is final.  fmv: the MB's MVs per 4x4, cbp_blk: its coded 4x4 blocks, t8flag: 8x8
 // transform (no 4x4 luma edges), qpy / qpcy: QPY and QPc (thresholds).  Every thread of the
 // workgroup must call it (it synchronises).  NTH: threads of the workgroup (256, or 512 in the
 // 512-thread final bodies: the sample loads / stores stride over all of them)
-template <class pel, int NTH = NT>
+template <class pel, int NTH = NT, bool PRE = false>
 __device__ __forceinline__ void deblock_mb(const DevParams &d, DbkS<pel> &s, const pel *rec, const pel (*cfin)[64], const int16_t (*fmv)[2],
                                            bool is_intra, int cbp_blk, bool t8flag, int qpy, int qpcy, int mbx, int mby, int tid) {
     pel *dbkY = spl<pel>(d.dbkY), *dbkU = spl<pel>(d.dbkU), *dbkV = spl<pel>(d.dbkV);
@@ -97,14 +140,19 @@ __device__ __forceinline__ void deblock_mb(const DevParams &d, DbkS<pel> &s, con
                 const int r = i / 20 - 4, c = i % 20 - 4;
                 int v = 0;
                 if (r >= 0 && c >= 0) v = rec[16 * r + c];
-                else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL)) v = dbkY[(pix_y + r) * W + pix_x + c];
+                else if ((r < 0) != (c < 0)) {
+                    if (PRE) continue;                   // deblock_prefetch loaded the borders
+                    if ((r < 0 && dbT) || (c < 0 && dbL)) v = dbkY[(pix_y + r) * W + pix_x + c];
+                }
                 s.dy[r + 4][c + 4] = (pel)v;
             } else {
                 const int j = i - 400, pl = j / 144, r = (j % 144) / 12 - 4, c = j % 12 - 4;
                 int v = 0;
                 if (r >= 0 && c >= 0) v = cfin[pl][8 * r + c];
-                else if ((r < 0 && c >= 0 && dbT) || (c < 0 && r >= 0 && dbL))
-                    v = (pl ? dbkV : dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c];
+                else if ((r < 0) != (c < 0)) {
+                    if (PRE) continue;
+                    if ((r < 0 && dbT) || (c < 0 && dbL)) v = (pl ? dbkV : dbkU)[((pix_y >> 1) + r) * Wc + (pix_x >> 1) + c];
+                }
                 s.dc2[pl][r + 4][c + 4] = (pel)v;
             }
         }
@@ -119,7 +167,12 @@ __device__ __forceinline__ void deblock_mb(const DevParams &d, DbkS<pel> &s, con
                 int pref, pmx, pmy;
                 const int qref = is_intra ? -1 : 0, qmx = fmv[bq][0], qmy = fmv[bq][1];
                 const bool qcoef = (cbp_blk >> bq) & 1;
-                if (mb_edge) {
+                if (mb_edge && PRE) {
+                    intra_p = s.nintra[dir];
+                    pcoef = (s.nbits[dir] >> bp) & 1;
+                    pref = intra_p ? -1 : 0;
+                    pmx = s.nmv[dir][i][0]; pmy = s.nmv[dir][i][1];
+                } else if (mb_edge) {
                     const int nx = dir == 0 ? mbx - 1 : mbx, ny = dir == 0 ? mby : mby - 1;
                     const jmh_mb_result *rp = d.res + ny * d.mbw + nx;
                     intra_p = rp->mb_type == JMH_I4MB || rp->mb_type == JMH_I16MB || rp->mb_type == JMH_I8MB;

@@ -13,9 +13,15 @@
 // JMH_I4WAVE 1: a P macroblock's intra decisions run on wave 7 of its motion-search workgroup on
 // their own schedule (the seven search waves meet at LDS-counter barriers, never at s_barrier, which
 // would wait for wave 7), so the Intra4x4 chain is off the search's stage chain; 0: the Intra4x4
-// steps ride in the stages' sub-pel phases on waves 6 and 7 (A/B: -DJMH_I4WAVE=0)
+// steps ride in the stages' sub-pel phases on waves 6 and 7 (A/B: -DJMH_I4WAVE=0).  The variant
+// measured slower (1143 vs 1168 MP/s, profiles/r8a_i4wave_ab.txt) and is kept for A/B only: it is
+// correct only while intra_wave and every search stage after the split are free of __syncthreads
+// (an s_barrier would pair arrivals of unrelated program points), and no test builds it.
 #ifndef JMH_I4WAVE
 #define JMH_I4WAVE 0
+#endif
+#if JMH_I4WAVE && !defined(JMH_I4WAVE_AB)
+#error "JMH_I4WAVE is an A/B-only variant: define JMH_I4WAVE_AB to build it (see the comment above)"
 #endif
 #define NTS (JMH_I4WAVE ? 448 : NTA)     // threads of the FFS position strips (the search waves)
 #define NPK (JMH_I4WAVE ? 11 : 10)       // FFS search positions per search thread (a column strip):
@@ -113,6 +119,8 @@ struct DevParams {
     int cavlc;                  // RDOptimization 1 with SymbolMode 0: CAVLC rates (jmh_cavlc_rate.h, item 64);
                                 //   RdoPic.range[slice] then holds the slice's mb_skip_run so far
     const RdoPic *rp;           // RDOptimization 1: the picture's RD state
+    int i16c;                   // k_mb_flow: the P macroblock's Intra16x16 / chroma decisions run on
+                                //   me_mb's idle waves (intra slot 11); 0: k_mb_analyse's intra roles do them
 };
 
 // Neighbour MB availability (6.4.8 / JM getNeighbour): inside the picture and in the current
@@ -206,11 +214,15 @@ struct FlowArgs {
     const FlowPic *pics;                 // [nring]
     const uint32_t *items;               // the segment's MBs in tick order: entry << 24 | mby << 12 | mbx
     int nitems;
-    int nmb;
+    int nmb, nring;
     unsigned *head;                      // ticket counter (monotonic over launches)
     unsigned base;                       // its value at this launch's first ticket
     uint32_t *flags;                     // [nring][nmb] generations
-    unsigned *err;                       // host-visible: set when a dependency wait timed out
+    unsigned *err;                       // host-visible: [0] 1 = a dependency wait timed out, 2 = a ticket /
+                                         //   item out of range ([1] ticket, [2] item)
+    unsigned long long *fprof;           // debug (JMH_FLOW_PROF=<launch>): per ticket 6 words -- start,
+                                         //   dependencies met, analysis done, final done, flag stored,
+                                         //   hardware id << 32 | item (null: off)
 };
 #define FLOW_ITEM(e, x, y) (((uint32_t)(e) << 24) | ((uint32_t)(y) << 12) | (uint32_t)(x))
 
@@ -258,6 +270,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.cqp_off = q.cqp_off; d.qsel = q.qsel; d.diag = q.diag; d.y_min = q.y_min;
     d.rdo = t.rdo;
     d.cavlc = t.rdo == 2;
+    d.i16c = 0;
     d.lf = q.lambda_motion << 16;
     d.lambda_rd = 0;
     d.rp = nullptr;

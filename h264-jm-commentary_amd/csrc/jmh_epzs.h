@@ -37,6 +37,9 @@ struct EGeo {
     static constexpr int off = sizeof(pel) == 2 ? EOFF_L16 : EOFF_L;
     static constexpr int ew = 16 + 2 * off;
     static_assert(off % 2 == 0, "window rows must be whole dwords");
+    // ffs_build_phase reads every table position straight from the window, with no global
+    // fallback: the margin must cover SRMAX + 3 (the 6-tap reach) around the FFS centre
+    static_assert(off >= SRMAX + 3, "the FFS SAD table (RDO + SearchMode 0) needs a window margin >= SRMAX + 3");
 };
 #define NPRED 41                              // EPZS predictor slots (oracle epzs_predictors)
 #define HPS 20                                // sub-pel plane stride (>= 18 + 2 alignment slack)

@@ -50,8 +50,13 @@ struct FinS {
 // threads 0..127.  512 (k_mb_final512, k_mb_flow): luma on threads 0..255 while waves 4 and 5 run the
 // chroma prediction, transform and quantisation (dct_chroma's first half) beside it; only the
 // chroma DC and the inverse transform follow the luma.  Every thread of the workgroup calls it.
-template <int OCC, class pel, bool T8, int NTH>
-__device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, int mby, int tid) {
+// mc(X, Y): the luma sample at quarter-pel position (X, Y) of the reference (qpel_direct from HBM in
+// the tick kernels; k_mb_flow reads its search window's G / b / h / j planes in LDS).  porg / pnb:
+// the MB's source and intra neighbourhood already in LDS (k_mb_flow's analysis state), or null:
+// loaded here.
+template <int OCC, class pel, bool T8, int NTH, class MC>
+__device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, int mby, int tid, MC mc, const pel *porg = nullptr,
+                                           const IntraNb<pel> *pnb = nullptr) {
     constexpr bool W2 = NTH == 512;
     static_assert(NTH == 256 || NTH == 512, "final_core runs on 256 or 512 threads");
     if constexpr (!T8) d.t8 = 0;
@@ -65,7 +70,7 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
     // QPY (deblocking) and QP'Y = QPY + QpBdOffsetY (quantisation); Clip1 to maxv
     const int qpy = d.qp, qp = d.qp + d.qpbd, maxv = d.maxv;
     const pel *orgY = spl<pel>(d.orgY), *orgU = spl<pel>(d.orgU), *orgV = spl<pel>(d.orgV);
-    const pel *refY = spl<pel>(d.refY), *refU = spl<pel>(d.refU), *refV = spl<pel>(d.refV);
+    const pel *refU = spl<pel>(d.refU), *refV = spl<pel>(d.refV);
     pel *recY = spl<pel>(d.recY), *recU = spl<pel>(d.recU), *recV = spl<pel>(d.recV);
     const MbAvail mav = mb_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL;
@@ -73,9 +78,15 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
     PSTAMP(16);
     const MbScratch *sc = d.scr + mby * d.mbw + mbx;
 
-    // ---- inputs into LDS
-    if (lu) s.org[tid] = orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
-    if (!W2 || tid >= 256) {
+    // ---- inputs into LDS (unless the caller's LDS holds them)
+    const pel *S_org = porg ? porg : s.org;
+    const pel(*S_orgc)[64] = pnb ? pnb->orgc : s.orgc;
+    const pel *S_rtop = pnb ? pnb->rtop : s.rtop, *S_rleft = pnb ? pnb->rleft : s.rleft;
+    const pel(*S_ctop)[12] = pnb ? pnb->ctop : s.ctop;
+    const pel(*S_cleft)[8] = pnb ? pnb->cleft : s.cleft;
+    if (lu && !porg) s.org[tid] = orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    if (d.dbkY) deblock_prefetch<pel, NTH>(d, s.db, mbx, mby, tid);   // its latency under the decision and the luma
+    if (!pnb && (!W2 || tid >= 256)) {
         const int u = ct;
         if (u < 128) {
             const int uv = u >> 6, k = u & 63;
@@ -135,7 +146,7 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
     int cpredv = 0;
     if (chv) {
         if (is_intra) {
-            cpredv = chroma_pred_px(s.ctop[cuv] + 1, s.cleft[cuv], s.ctop[cuv][0], avT, avL, c_mode, cxo, cyo, maxv);
+            cpredv = chroma_pred_px(S_ctop[cuv] + 1, S_cleft[cuv], S_ctop[cuv][0], avT, avL, c_mode, cxo, cyo, maxv);
         } else {
             // OneComponentChromaPrediction4x4 [J] / 8.4.2.2.2
             const pel *R = cuv ? refV : refU;
@@ -158,7 +169,7 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
     int cdq = 0;
     auto chroma_a = [&]() {
         if (chv) {
-            const int c = lane_fwd4x4(s.orgc[cuv][cyo * 8 + cxo] - cpredv, l);
+            const int c = lane_fwd4x4(S_orgc[cuv][cyo * 8 + cxo] - cpredv, l);
             if (l == 0) s.cdcin[cuv][cb] = c;
             int lev, cc;
             unsigned nz = lane_quant(c, l, qpc, cqp_const, true, lev, cdq, cc);
@@ -221,10 +232,10 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
         // dct_luma_16x16 [J] (jmh_intra.h i16_code)
         int p = 0, org = 0;
         if (lu) {
-            const pel *T = s.rtop + 1, *L = s.rleft;
+            const pel *T = S_rtop + 1, *L = S_rleft;
             const I16Par par = i16_params(T, L, avT, avL, (maxv + 1) >> 1);
             p = i16_pred(par, T, L, i16mode, px4, py4, maxv);
-            org = (int)s.org[py4 * 16 + px4];
+            org = (int)S_org[py4 * 16 + px4];
         }
         int lev, rv;
         i16_code(p, org, qp, q_round(q_sel16(d.qsel), 15 + qp / 6), s.dc, s.dcdq, s.dclev, s.bnz, tid, maxv, lev, rv, lu);
@@ -237,16 +248,13 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
             if (s.bnz[b]) { cbp = 15; cbp_blk |= 1 << b; }
     } else {
         // LumaResidualCoding / LumaResidualCoding8x8 (+ SetCoeffAndReconstruction8x8)
-        // the 64-VGPR build samples the 6-tap's centre column by column: no spills (the unrolled
-        // form spilled 56 B per lane and measured 0.9 % faster, profiles/r7b_c3_serialj_ab.txt)
-        constexpr bool serial_j = OCC == 8;
-        const int p = lu ? qpel_direct<pel, serial_j>(refY, d.W, d.H, 4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1], maxv) : 0;
+        const int p = lu ? mc(4 * (pix_x + px4) + s.fmv[blk][0], 4 * (pix_y + py4) + s.fmv[blk][1]) : 0;
         if (d.t8 && (best_mode <= 3 || best8x8 == 0x4444)) {
             // TransformDecision [J] (item 29): sum of 4x4 SATDs vs sum of 8x8 SATDs of the residual
             if (lu) s.pred[py4 * 16 + px4] = (pel)p;
             __syncthreads();
             if (lu) {
-                const int dv = s.org[qy * 16 + qx] - s.pred[qy * 16 + qx];
+                const int dv = S_org[qy * 16 + qx] - s.pred[qy * 16 + qx];
                 const int c4 = wave_satd4x4s(dv, l8, d.use_hadamard), c8 = wave_satd8(dv, l8, d.use_hadamard);
                 if (l8 == 0) { s.tdc[w8][0] = c4; s.tdc[w8][1] = c8; }
             }
@@ -259,7 +267,7 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
             if (lu) {
                 pv = s.pred[qy * 16 + qx];
                 const int q8 = 16 + qp / 6;
-                const int c = wave_fwd8x8(s.org[qy * 16 + qx] - pv, l8);
+                const int c = wave_fwd8x8(S_org[qy * 16 + qx] - pv, l8);
                 int dq, cc;
                 const unsigned long long nz = wave_quant8(c, l8, qp, q_round(d.qsel, q8), lev, dq, cc);
                 rv = wave_inv8x8(dq, l8, pv, maxv);
@@ -285,7 +293,7 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
         } else {
         int lev = 0, rv = 0;
         if (lu) {
-            const int c = lane_fwd4x4(s.org[py4 * 16 + px4] - p, l);
+            const int c = lane_fwd4x4(S_org[py4 * 16 + px4] - p, l);
             int dq, cc;
             const int q_bits = 15 + qp / 6;
             unsigned nz = lane_quant(c, l, qp, q_round(d.qsel, q_bits), false, lev, dq, cc);
@@ -377,7 +385,7 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
     if (lu) recY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)] = s.rec[tid];
 
     // ======== DeblockMb [J] / 8.7 into the reference picture (jmh_deblock.h)
-    if (d.dbkY) deblock_mb<pel, NTH>(d, s.db, s.rec, s.cfin, s.fmv, is_intra, cbp_blk, t8flag, qpy, qpcy, mbx, mby, tid);
+    if (d.dbkY) deblock_mb<pel, NTH, true>(d, s.db, s.rec, s.cfin, s.fmv, is_intra, cbp_blk, t8flag, qpy, qpcy, mbx, mby, tid);
     PSTAMP(19);
 }
 
@@ -388,7 +396,12 @@ __device__ __forceinline__ void final_mb(const TickArgs &t, FinS<pel> &s, int m,
     const int e = tick_entry(t, m);
     const DevParams d = tick_params(t, e);
     const int mby = d.y_min + (m - t.pre[e]), mbx = d.diag - 2 * mby;
-    final_core<OCC, pel, T8, NTH>(d, s, mbx, mby, tid);
+    // the 64-VGPR build samples the 6-tap's centre column by column: no spills (the unrolled form
+    // spilled 56 B per lane and measured 0.9 % faster, profiles/r7b_c3_serialj_ab.txt)
+    const pel *refY = spl<pel>(d.refY);
+    const int W = d.W, H = d.H, maxv = sizeof(pel) == 1 ? 255 : d.maxv;
+    auto mc = [=](int X, int Y) { return qpel_direct<pel, OCC == 8>(refY, W, H, X, Y, maxv); };
+    final_core<OCC, pel, T8, NTH>(d, s, mbx, mby, tid, mc);
     if (t.bprof_fin && tid == 0) {
         t.bprof_fin[3 * hwb] = bt0;
         t.bprof_fin[3 * hwb + 1] = wall_clock64();

@@ -57,16 +57,45 @@ __device__ __forceinline__ void load_orgc(const DevParams &d, IntraNb<pel> &nb, 
 }
 
 // intrapred_luma_16x16 + find_sad_16x16 on one wave (4 modes x 16 blocks = 64 lanes): the
-// find_sad_16x16 cost and mode, wave-uniform
+// find_sad_16x16 cost and mode, wave-uniform.  The prediction's parameters (8.3.3: the DC sums and
+// the plane's H / V) come from lane reductions -- lanes 0..15 hold p[k, -1], 16..31 p[-1, k]:
+// H = sum (k - 7) p[k, -1] - 8 p[-1, -1], V likewise -- and every lane selects its mode's sample
+// without branching (a per-lane mode switch ran all four paths on every lane).  The whole wave
+// must be active.
 template <class pel>
 __device__ __forceinline__ void i16_pick(const DevParams &d, const pel *org, const IntraNb<pel> &nb, int lane, bool avL, bool avT, bool avTL,
                                          int &cost16, int &mode16) {
     const int m = lane >> 4, b = lane & 15, ox = (b & 3) * 4, oy = (b >> 2) * 4;
     const pel *T = nb.rtop + 1, *L = nb.rleft;
-    const I16Par par = i16_params(T, L, avT, avL, (d.maxv + 1) >> 1);
+    const int k = lane & 15, nv = lane < 16 ? (int)T[k] : (int)L[k];
+    const int s1 = row16_sum(nv), s2 = row16_sum((k - 7) * nv);
+    const int st = __builtin_amdgcn_readlane(s1, 0), sl = __builtin_amdgcn_readlane(s1, 16);
+    const int corner = T[-1];
+    const int ih = __builtin_amdgcn_readlane(s2, 0) - 8 * corner, iv = __builtin_amdgcn_readlane(s2, 16) - 8 * corner;
+    const int dcv = (avT && avL) ? (st + sl + 16) >> 5 : avT ? (st + 8) >> 4 : avL ? (sl + 8) >> 4 : (d.maxv + 1) >> 1;
+    const int ib = (5 * ih + 32) >> 6, ic = (5 * iv + 32) >> 6, iaa = 16 * (L[15] + T[15]);
+    int tx[4], ly[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { tx[i] = T[ox + i]; ly[i] = L[oy + i]; }
     int mm[16], t[16];
-    for (int yy = 0; yy < 4; yy++)
-        for (int xx = 0; xx < 4; xx++) mm[4 * yy + xx] = org[(oy + yy) * 16 + ox + xx] - i16_pred(par, T, L, m, ox + xx, oy + yy, d.maxv);
+#pragma unroll
+    for (int yy = 0; yy < 4; yy++) {
+        int o[4];
+        if constexpr (sizeof(pel) == 1) {
+            const uint32_t w = *reinterpret_cast<const uint32_t *>(org + (oy + yy) * 16 + ox);
+#pragma unroll
+            for (int xx = 0; xx < 4; xx++) o[xx] = (int)((w >> (8 * xx)) & 255u);
+        } else {
+#pragma unroll
+            for (int xx = 0; xx < 4; xx++) o[xx] = org[(oy + yy) * 16 + ox + xx];
+        }
+#pragma unroll
+        for (int xx = 0; xx < 4; xx++) {
+            const int pl = clipmx((iaa + (ox + xx - 7) * ib + (oy + yy - 7) * ic + 16) >> 5, d.maxv);
+            const int p = m == 0 ? tx[xx] : m == 1 ? ly[yy] : m == 2 ? dcv : pl;
+            mm[4 * yy + xx] = o[xx] - p;
+        }
+    }
     for (int yy = 0; yy < 4; yy++) {
         int *r = mm + 4 * yy;
         int a0 = r[0] + r[3], a1 = r[1] + r[2], a2 = r[1] - r[2], a3 = r[0] - r[3];
@@ -83,9 +112,9 @@ __device__ __forceinline__ void i16_pick(const DevParams &d, const pel *org, con
     const bool av16[4] = {avT, avL, true, avT && avL && avTL};
     int best = MAX_VALUE, i16mode = 2;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int c = __builtin_amdgcn_readlane(cost, 16 * k);
-        if (av16[k] && c < best) { best = c; i16mode = k; }
+    for (int k2 = 0; k2 < 4; k2++) {
+        const int c = __builtin_amdgcn_readlane(cost, 16 * k2);
+        if (av16[k2] && c < best) { best = c; i16mode = k2; }
     }
     cost16 = best / 2;
     mode16 = i16mode;

@@ -194,6 +194,10 @@ struct jmh_ctx {
     unsigned *d_head = nullptr;          // ticket counter
     unsigned head_base = 0;
     unsigned *h_err = nullptr;           // pinned, device-written: a dependency wait timed out
+    int fprof_launch = -1, flow_count = 0;   // debug: JMH_FLOW_PROF=<launch> -> JMH_FLOW_PROF_OUT (raw u64)
+    unsigned long long *d_fprof = nullptr;
+    size_t fprof_n = 0;
+    std::vector<uint32_t> fprof_items;
 };
 
 #define HCHK(x)                                                                  \
@@ -354,7 +358,7 @@ void jmh_destroy(jmh_ctx *c) {
     if (c->sst) (void)hipStreamSynchronize(c->sst);
     for (PicBuf &b : c->ring) free_entry(b);
     void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab, c->d_scur16,
-                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr, c->d_ffs, c->d_seg, c->d_flags, c->d_head};
+                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr, c->d_ffs, c->d_seg, c->d_flags, c->d_head, c->d_fprof};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     for (int i = 0; i < 2; i++) {
@@ -488,12 +492,19 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
             for (int i = 0; i < 2; i++)
                 if (hipHostMalloc((void **)&c->h_seg[i], sb, hipHostMallocDefault) != hipSuccess ||
                     hipEventCreateWithFlags(&c->ev_seg[i], hipEventDisableTiming) != hipSuccess) { st = JMH_E_OOM; goto fail; }
-            if (hipHostMalloc((void **)&c->h_err, sizeof(unsigned), hipHostMallocCoherent) != hipSuccess) { st = JMH_E_OOM; goto fail; }
-            *c->h_err = 0;
-            if (hipMemset(c->d_flags, 0, (size_t)c->nring * c->nmb * sizeof(uint32_t)) != hipSuccess ||
-                hipMemset(c->d_head, 0, sizeof(unsigned)) != hipSuccess) { st = JMH_E_HIP; goto fail; }
+            if (hipHostMalloc((void **)&c->h_err, 4 * sizeof(unsigned), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) { st = JMH_E_OOM; goto fail; }
+            memset(c->h_err, 0, 4 * sizeof(unsigned));
+            // on the context's stream: a plain hipMemset of device memory may still be pending on the
+            // null stream, which the non-blocking stream does not wait for, when the first segment
+            // claims its tickets (seen with two processes on one GPU)
+            if (hipMemsetAsync(c->d_flags, 0, (size_t)c->nring * c->nmb * sizeof(uint32_t), c->st) != hipSuccess ||
+                hipMemsetAsync(c->d_head, 0, sizeof(unsigned), c->st) != hipSuccess) { st = JMH_E_HIP; goto fail; }
             c->fpic.assign(c->nring, FlowPic{});
             c->seg.reserve(c->seg_cap);
+            if (const char *e = getenv("JMH_FLOW_PROF")) {
+                c->fprof_launch = atoi(e);
+                ALLOC(c->d_fprof, c->seg_cap * 6 * sizeof(unsigned long long));
+            }
         }
         if (hipMemset(c->d_ref, 0, c->fsize) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         if (ring_init(c->ring_interp, 64) || ring_init(c->ring_mb, 64) ||
@@ -507,7 +518,12 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
             ALLOC(c->d_rscr, (size_t)PMAX * maxc * jmh_rdo_scratch_bytes());
             // SearchMode 0: one SAD table per tick MB (JMH_RDO_FFS_TABLE=0: every search scans, A/B)
             const char *ft = getenv("JMH_RDO_FFS_TABLE");
-            if (cfg->search_mode == 0 && !(ft && atoi(ft) == 0)) ALLOC(c->d_ffs, (size_t)PMAX * maxc * ffs_slot_bytes(c->sr));
+            // (a failed allocation leaves d_ffs null: the searches then scan, with identical results)
+            if (cfg->search_mode == 0 && !(ft && atoi(ft) == 0) &&
+                hipMalloc(&c->d_ffs, (size_t)PMAX * maxc * ffs_slot_bytes(c->sr)) != hipSuccess) {
+                c->d_ffs = nullptr;
+                (void)hipGetLastError();
+            }
             if (hipMemcpy(c->d_sched, rd_order.data(), rd_order.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
                 hipMemcpy(c->d_soff, rd_off.data(), rd_off.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess) { st = JMH_E_HIP; goto fail; }
         } else {
@@ -521,6 +537,9 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         }
     }
 #undef ALLOC
+    // every initialising memset (null stream, possibly still pending: hipMemset of device memory
+    // returns before it completes) done before the context's non-blocking streams run
+    if (hipDeviceSynchronize() != hipSuccess) { st = JMH_E_HIP; goto fail; }
     *out = c;
     return JMH_OK;
 fail:
@@ -632,6 +651,11 @@ static int flow_flush(jmh_ctx *c) {
     c->seg_slot ^= 1;
     HCHK(hipEventSynchronize(c->ev_seg[sl]));
     const size_t pb = (size_t)c->nring * sizeof(FlowPic), ib = c->seg.size() * sizeof(uint32_t);
+    if (c->seg.size() > c->seg_cap) return JMH_E_STATE;   // (never expected: seg_max ticks of <= PMAX diagonals)
+    for (uint32_t it : c->seg) {
+        const int e = (int)(it >> 24);
+        if (e >= c->nring || c->fpic[e].gen == 0) { fprintf(stderr, "jmhip: flow segment item 0x%08x without a picture\n", it); return JMH_E_STATE; }
+    }
     memcpy(c->h_seg[sl], c->fpic.data(), pb);
     memcpy(c->h_seg[sl] + pb, c->seg.data(), ib);
     HCHK(hipMemcpyAsync(c->d_seg, c->h_seg[sl], pb + ib, hipMemcpyHostToDevice, c->st));
@@ -647,10 +671,16 @@ static int flow_flush(jmh_ctx *c) {
     f.pics = reinterpret_cast<const FlowPic *>(c->d_seg);
     f.items = reinterpret_cast<const uint32_t *>(c->d_seg + pb);
     f.nitems = (int)c->seg.size();
-    f.nmb = (int)c->nmb;
+    f.nmb = (int)c->nmb; f.nring = c->nring;
     f.head = c->d_head; f.base = c->head_base;
     f.flags = c->d_flags;
     f.err = c->h_err;
+    if (c->d_fprof && c->flow_count == c->fprof_launch) {
+        f.fprof = c->d_fprof;
+        c->fprof_n = c->seg.size();
+        c->fprof_items = c->seg;
+    }
+    c->flow_count++;
     const bool kt = c->ring_an.cap > 0;
     HCHK(ring_begin(c->ring_mb, c->st));
     if (kt) HCHK(ring_begin(c->ring_an, c->st));
@@ -666,10 +696,29 @@ static int flow_flush(jmh_ctx *c) {
     return JMH_OK;
 }
 
-// a dependency wait of k_mb_flow that timed out (never expected: every wait ends by construction)
+// a dependency wait of k_mb_flow that timed out (never expected: every wait ends by construction);
+// debug: the profiled launch's stamps to JMH_FLOW_PROF_OUT once it has run
 static int flow_check(jmh_ctx *c) {
+    if (c->fprof_n && c->flow_count > c->fprof_launch) {
+        std::vector<unsigned long long> h(6 * c->fprof_n);
+        HCHK(hipStreamSynchronize(c->st));
+        HCHK(hipMemcpy(h.data(), c->d_fprof, h.size() * 8, hipMemcpyDeviceToHost));
+        int rate_khz = 0;
+        HCHK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->dev));
+        const char *path = getenv("JMH_FLOW_PROF_OUT");
+        if (FILE *fo = fopen(path ? path : "flow_prof.bin", "wb")) {
+            const unsigned long long hdr[4] = {(unsigned long long)c->fprof_n, (unsigned long long)rate_khz, (unsigned long long)c->mbw,
+                                               (unsigned long long)c->mbh};
+            fwrite(hdr, 8, 4, fo);
+            fwrite(h.data(), 8, h.size(), fo);
+            fwrite(c->fprof_items.data(), 4, c->fprof_items.size(), fo);
+            fclose(fo);
+        }
+        c->fprof_n = 0;
+    }
     if (c->flow && c->h_err && __atomic_load_n(c->h_err, __ATOMIC_ACQUIRE)) {
-        fprintf(stderr, "jmhip: k_mb_flow dependency wait timed out (results invalid)\n");
+        if (c->h_err[0] == 2) fprintf(stderr, "jmhip: k_mb_flow ticket %u item 0x%08x out of range (results invalid)\n", c->h_err[1], c->h_err[2]);
+        else fprintf(stderr, "jmhip: k_mb_flow dependency wait timed out (results invalid)\n");
         return JMH_E_HIP;
     }
     return JMH_OK;
