@@ -704,7 +704,18 @@ __device__ __forceinline__ void chroma_decision(const DevParams &d, const IntraN
 __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int k, int w, int mbx, int mby);
 __device__ __forceinline__ void intra_wave(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int mbx, int mby);
 
-__device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int mby) {
+// the part of me_mb's setup that reads no other workgroup's output (the source block, the lambda *
+// mvbits table, zeroed accumulators): k_mb_flow runs it while its dependencies finish (pre = true
+// then skips it in me_mb)
+__device__ __forceinline__ void me_prologue(const DevParams &d, MeS &s, int mbx, int mby) {
+    const int tid = threadIdx.x;
+    if (tid < 256) s.in.org[tid] = s.org[tid] = d.orgY[(16 * mby + (tid >> 4)) * d.W + 16 * mbx + (tid & 15)];
+    else if (tid >= 472 && tid < 478) s.in.part[(tid - 472) / 3][(tid - 472) % 3] = 0;
+    else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
+    for (int i = tid; i < MVB_LEN; i += NTA) s.mvc[i] = (uint16_t)__umul24(d.lambda_motion, mvbits(i - MVB_OFF));
+}
+
+__device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int mby, bool pre = false) {
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // an SGPR: tid itself dies after the setup
     const int W = d.W, sr = d.sr, side = d.side;
@@ -713,13 +724,13 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     PSTAMP(0);
     MbScratch *scr = d.scr + mby * d.mbw + mbx;
     if (tid == 0) { s.pst = prof ? d.prof + 20 : nullptr; s.pn = 0; s.bar = 0; }
-    if (tid < 256) s.in.org[tid] = s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)];
+    if (tid < 256) { if (!pre) s.in.org[tid] = s.org[tid] = d.orgY[(pix_y + (tid >> 4)) * W + pix_x + (tid & 15)]; }
 #if JMH_I4WAVE
     else if (tid < 384) load_orgc(d, s.in.nb, tid - 256, mbx, mby);   // the intra wave's chroma decision
 #endif
     else if (tid >= 384 && tid < 394) { load_border(d, s.bd, tid - 384, mbx, mby); load_border(d, s.in.bd, tid - 384, mbx, mby); }
-    else if (tid >= 472 && tid < 478) s.in.part[(tid - 472) / 3][(tid - 472) % 3] = 0;
-    else if (tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
+    else if (!pre && tid >= 472 && tid < 478) s.in.part[(tid - 472) / 3][(tid - 472) % 3] = 0;
+    else if (!pre && tid >= 480 && tid < 512) s.motion_cost[(tid - 480) >> 2][tid & 3] = 0;
     // the MB's Intra4x4 decision (10 diagonal steps, then the results) runs on waves 6 and 7
     // while the motion search's sub-pel waves work: slots 0..10 (intra_slot)
 #if JMH_EXP & 2   // instruction-count experiment: no Intra4x4 in the search workgroup
@@ -728,7 +739,8 @@ __device__ __forceinline__ void me_mb(const DevParams &d, MeS &s, int mbx, int m
     auto idle = [&](int k, int w) { intra_slot(d, s.in, scr, k, w, mbx, mby); };
 #endif
     (void)scr;
-    for (int i = tid; i < MVB_LEN; i += NTA) s.mvc[i] = (uint16_t)__umul24(d.lambda_motion, mvbits(i - MVB_OFF));
+    if (!pre)
+        for (int i = tid; i < MVB_LEN; i += NTA) s.mvc[i] = (uint16_t)__umul24(d.lambda_motion, mvbits(i - MVB_OFF));
     int pcx = 0, pcy = 0, scx = 0, scy = 0;
     uint8_t *G = s.planes;
     const int wdim = 2 * sr + 16 + 2 * WM;
@@ -1214,25 +1226,6 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_flow(const FlowArgs f) {
             __hip_atomic_store(f.err + 2, (unsigned)item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(f.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             item = -1;
-        } else {
-            const int e = item >> 24, mby = (item >> 12) & 0xFFF, mbx = item & 0xFFF;
-            const FlowPic &P = f.pics[e];
-            const uint32_t g = P.gen;
-            const int mb = mby * f.mbw + mbx;
-            const int re = P.pp.slice_type == JMH_P_SLICE ? P.ref_entry : -1;
-            const int rmb = min(mby + 5, f.mbh - 1) * f.mbw + min(mbx + 5, f.mbw - 1);
-            const int tmb = mby > 0 ? (mbx + 1 < f.mbw ? mb - f.mbw + 1 : mb - f.mbw) : -1;
-            // bounded: after FLOW_SPIN_MAX polls (or once any wait of the launch has timed out) the
-            // workgroup goes on and the host reports the launch as failed
-            int spin = 0;
-            while (!((mbx == 0 || flow_done(f, e, mb - 1, g)) && (tmb < 0 || flow_done(f, e, tmb, g)) &&
-                     (re < 0 || flow_done(f, re, rmb, P.ref_gen)))) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spin > FLOW_SPIN_MAX) { __hip_atomic_store(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); break; }
-                if ((spin & 63) == 0 && __hip_atomic_load(f.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         s_item = item;
     }
@@ -1241,6 +1234,31 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_flow(const FlowArgs f) {
     if (item < 0) return;
     const int e = item >> 24, mby = (item >> 12) & 0xFFF, mbx = item & 0xFFF;
     const bool pslice = f.pics[e].pp.slice_type == JMH_P_SLICE;
+    if (pslice) {   // what reads no other workgroup's output, while the dependencies finish
+        const DevParams d = flow_params(f, f.pics[e].pp);
+        me_prologue(d, s.a.me, mbx, mby);
+        if (tid >= 256 && tid < 384) load_orgc(d, s.a.me.in.nb, tid - 256, mbx, mby);   // the chroma decision's source
+    }
+    if (tid == 0) {
+        const FlowPic &P = f.pics[e];
+        const uint32_t g = P.gen;
+        const int mb = mby * f.mbw + mbx;
+        const int re = pslice ? P.ref_entry : -1;
+        const int rmb = min(mby + 5, f.mbh - 1) * f.mbw + min(mbx + 5, f.mbw - 1);
+        const int tmb = mby > 0 ? (mbx + 1 < f.mbw ? mb - f.mbw + 1 : mb - f.mbw) : -1;
+        // bounded: after FLOW_SPIN_MAX polls (or once any wait of the launch has timed out) the
+        // workgroup goes on and the host reports the launch as failed
+        int spin = 0;
+        while (!((mbx == 0 || flow_done(f, e, mb - 1, g)) && (tmb < 0 || flow_done(f, e, tmb, g)) &&
+                 (re < 0 || flow_done(f, re, rmb, P.ref_gen)))) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spin > FLOW_SPIN_MAX) { __hip_atomic_store(f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); break; }
+            if ((spin & 63) == 0 && __hip_atomic_load(f.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
     // debug stamps (JMH_FLOW_PROF): the slot is re-derived at each use, nothing stays live across me_mb
 #define FLOW_FP (f.fprof ? f.fprof + 6 * (size_t)__builtin_amdgcn_readfirstlane(s_tk) : nullptr)
     if (unsigned long long *fp = FLOW_FP; fp && tid == 0) {
@@ -1252,12 +1270,8 @@ __global__ __launch_bounds__(NTA, 4) void k_mb_flow(const FlowArgs f) {
     }
     {   // the analysis (DevParams scoped per phase: one set live across me_mb spills)
         const DevParams d = flow_params(f, f.pics[e].pp);
-        if (pslice) {
-            if (tid >= 256 && tid < 384) load_orgc(d, s.a.me.in.nb, tid - 256, mbx, mby);   // the chroma decision's source
-            me_mb(d, s.a.me, mbx, mby);
-        } else {
-            intra_role(d, s.a.in[tid >> 7], mbx, mby, tid & 127, tid < 128, true);
-        }
+        if (pslice) me_mb(d, s.a.me, mbx, mby, true);
+        else intra_role(d, s.a.in[tid >> 7], mbx, mby, tid & 127, tid < 128, true);
     }
     if (unsigned long long *fp = FLOW_FP; fp && tid == 0) fp[2] = wall_clock64();
     asm volatile("" ::: "memory");                            // re-read the parameters below

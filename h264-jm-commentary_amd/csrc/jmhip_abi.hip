@@ -181,6 +181,8 @@ struct jmh_ctx {
     // collected into a segment of macroblocks in tick order, launched as one grid on a flush
     bool flow = false;
     int seg_max = 0;                     // ticks per segment before a flush (JMH_FLOW_SEG)
+    int seg_lim = 0;                     // the current limit: 8 ticks after a wait, doubling up to seg_max,
+                                         //   so that the device starts soon after the host resumes issuing
     std::vector<FlowPic> fpic;           // per ring entry: parameters + flag generations
     std::vector<uint32_t> seg;           // the pending segment's macroblocks (FLOW_ITEM)
     unsigned long long seg_mask = 0;     // ring entries the pending segment reads or writes
@@ -432,7 +434,8 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         c->flow = cfg->search_mode == 0 && c->bd == 8 && !cfg->rdo && !cfg->transform_8x8_mode && !(fe && atoi(fe) == 0) &&
                   !getenv("JMH_BLOCK_PROF") && c->mbw < 4096 && c->mbh < 4096;
         const char *sg = getenv("JMH_FLOW_SEG");
-        c->seg_max = sg && atoi(sg) > 0 ? atoi(sg) : 64;
+        c->seg_max = sg && atoi(sg) > 0 ? atoi(sg) : 128;   // A/B 64 / 128 / 256: 1392.6 / 1402.4 / 1401.4 MP/s (profiles/r10g_flow_seg_ab.txt)
+        c->seg_lim = std::min(8, c->seg_max);
     }
     // (dataflow: four more entries, so that an entry's next occupant rarely falls into the segment
     // that still finishes its previous one, which would force a flush)
@@ -851,7 +854,10 @@ static int issue_tick(jmh_ctx *c) {
         c->fl.pop_front();
         if (r) return r;
     }
-    if (c->flow && c->seg_ticks >= c->seg_max) return flow_flush(c);
+    if (c->flow && c->seg_ticks >= c->seg_lim) {
+        c->seg_lim = std::min(2 * c->seg_lim, c->seg_max);
+        return flow_flush(c);
+    }
     return JMH_OK;
 }
 
@@ -1153,6 +1159,7 @@ int jmh_sync(jmh_ctx *c) {
     HCHK(hipSetDevice(c->dev));
     int r = drain(c);
     if (r) return r;
+    c->seg_lim = std::min(8, c->seg_max);
     HCHK(hipStreamSynchronize(c->st));
     if ((r = flow_check(c))) return r;
     if (c->d_bprof && c->bprof_blocks) {   // debug: block durations of one tick, per role
@@ -1235,6 +1242,7 @@ int jmh_wait_issued(jmh_ctx *c) {
     HCHK(hipSetDevice(c->dev));
     int r = flow_flush(c);
     if (r) return r;
+    c->seg_lim = std::min(8, c->seg_max);
     HCHK(hipStreamSynchronize(c->st));
     return flow_check(c);
 }

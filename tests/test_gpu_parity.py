@@ -709,3 +709,14 @@ def test_1080p_p_frame_parity():
     gres, grec = g.encode(*pics[1], jmhip.JMH_P_SLICE, 28)
     ores, orec = o.encode(*pics[1], jmhip.JMH_P_SLICE, 28)
     assert_same(gres, grec, ores, orec, w // 16)
+
+
+@pytest.mark.slow
+def test_config3_2160p_parity():
+    """BASELINE config 3 at its full size: 3840x2160 High profile, EPZS SR 32 +
+    Transform8x8Mode 1, the bench's synthetic stream 0 (IDR + P): GPU == oracle on every macroblock
+    and every reconstructed sample (the oracle takes ~10 s per picture)."""
+    w, h = 3840, 2160
+    pics = [jmhip.synth_frame(w, h, 0, i) for i in range(2)]
+    encode_pair(w, h, pics, [jmhip.JMH_I_SLICE, jmhip.JMH_P_SLICE], 28, search_range=32, search_mode=3,
+                transform_8x8_mode=1)

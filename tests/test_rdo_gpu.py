@@ -277,3 +277,13 @@ def test_rdo_cavlc_last_mb_skip(slice_mbs, bd):
     assert mt.count(0) == nmb
     run = (nmb - 1) % (slice_mbs or nmb)
     assert mc[-1] == 2 * (run + 2).bit_length() - 1 and not any(mc[:-1])
+
+
+@pytest.mark.slow
+def test_rdo_config5_2160p_parity():
+    """BASELINE config 5 at its full size: 3840x2160 High 10, EPZS SR 32, CABAC
+    RDOptimization 1, 240-MB (one-row) slices, the bench's synthetic 10-bit stream 0 (IDR + P):
+    GPU == oracle on every macroblock, rate and reconstructed sample."""
+    w, h = 3840, 2160
+    pics = [jmhip.synth_frame(w, h, 0, i, bit_depth=10) for i in range(2)]
+    rdo_pair(w, h, pics, 28, bd=10, search_range=32, slice_mbs=240)
