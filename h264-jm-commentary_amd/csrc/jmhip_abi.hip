@@ -181,16 +181,21 @@ struct jmh_ctx {
     // collected into a segment of macroblocks in tick order, launched as one grid on a flush
     bool flow = false;
     int seg_max = 0;                     // ticks per segment before a flush (JMH_FLOW_SEG)
-    int seg_lim = 0;                     // the current limit: 8 ticks after a wait, doubling up to seg_max,
-                                         //   so that the device starts soon after the host resumes issuing
+    int seg_min = 0;                     // ... or, once the device is idle, this many (JMH_FLOW_SEG_MIN)
+    hipEvent_t ev_flow = nullptr;        // the last segment launch's end: a segment of >= seg_min ticks
+                                         //   is flushed as soon as the device has run out of work
     std::vector<FlowPic> fpic;           // per ring entry: parameters + flag generations
     std::vector<uint32_t> seg;           // the pending segment's macroblocks (FLOW_ITEM)
     unsigned long long seg_mask = 0;     // ring entries the pending segment reads or writes
     int seg_ticks = 0;
     size_t seg_cap = 0;                  // items the device / staging buffers hold
-    uint8_t *d_seg = nullptr;            // device: FlowPic[nring], then the items
-    uint8_t *h_seg[2] = {nullptr, nullptr};   // pinned staging, alternating
-    hipEvent_t ev_seg[2] = {nullptr, nullptr};
+    // segment buffers, alternating: pinned staging -> device on the upload stream, beside the
+    // previous segment's launch (a buffer is rewritten once the launch that read it has ended)
+    uint8_t *d_seg[2] = {nullptr, nullptr};   // device: FlowPic[nring], then the items
+    uint8_t *h_seg[2] = {nullptr, nullptr};   // pinned staging
+    hipEvent_t ev_seg[2] = {nullptr, nullptr};   // the upload out of h_seg[i] / into d_seg[i] done
+    hipEvent_t ev_kseg[2] = {nullptr, nullptr};  // the launch that read d_seg[i] done
+    hipStream_t ust = nullptr;           // the segment uploads
     int seg_slot = 0;
     uint32_t *d_flags = nullptr;         // [nring][nmb] generations of the finished MBs
     unsigned *d_head = nullptr;          // ticket counter
@@ -360,14 +365,18 @@ void jmh_destroy(jmh_ctx *c) {
     if (c->sst) (void)hipStreamSynchronize(c->sst);
     for (PicBuf &b : c->ring) free_entry(b);
     void *dev_bufs[] = {c->d_ref, c->d_qpel, c->d_slots, c->d_prof, c->d_bprof, c->d_scur, c->d_sref, c->d_ordtab, c->d_scur16,
-                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr, c->d_ffs, c->d_seg, c->d_flags, c->d_head, c->d_fprof};
+                        c->d_sref16, c->d_sched, c->d_soff, c->d_rscr, c->d_ffs, c->d_seg[0], c->d_seg[1], c->d_flags, c->d_head,
+                        c->d_fprof};
     for (void *p : dev_bufs) if (p) (void)hipFree(p);
     if (c->h_stage_ref) (void)hipHostFree(c->h_stage_ref);
     for (int i = 0; i < 2; i++) {
         if (c->h_seg[i]) (void)hipHostFree(c->h_seg[i]);
         if (c->ev_seg[i]) (void)hipEventDestroy(c->ev_seg[i]);
+        if (c->ev_kseg[i]) (void)hipEventDestroy(c->ev_kseg[i]);
     }
+    if (c->ust) { (void)hipStreamSynchronize(c->ust); (void)hipStreamDestroy(c->ust); }
     if (c->h_err) (void)hipHostFree(c->h_err);
+    if (c->ev_flow) (void)hipEventDestroy(c->ev_flow);
     ring_free(c->ring_interp);
     ring_free(c->ring_mb);
     ring_free(c->ring_an);
@@ -434,12 +443,14 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
         c->flow = cfg->search_mode == 0 && c->bd == 8 && !cfg->rdo && !cfg->transform_8x8_mode && !(fe && atoi(fe) == 0) &&
                   !getenv("JMH_BLOCK_PROF") && c->mbw < 4096 && c->mbh < 4096;
         const char *sg = getenv("JMH_FLOW_SEG");
-        c->seg_max = sg && atoi(sg) > 0 ? atoi(sg) : 128;   // A/B 64 / 128 / 256: 1392.6 / 1402.4 / 1401.4 MP/s (profiles/r10g_flow_seg_ab.txt)
-        c->seg_lim = std::min(8, c->seg_max);
+        const char *sm = getenv("JMH_FLOW_SEG_MIN");
+        c->seg_min = sm && atoi(sm) > 0 ? atoi(sm) : 8;
+        c->seg_max = sg && atoi(sg) > 0 ? std::min(atoi(sg), 256) : 128;   // (<= 256: nring stays < 64, seg_mask's bits)   // A/B 64 / 128 / 256: 1392.6 / 1402.4 / 1401.4 MP/s (profiles/r10g_flow_seg_ab.txt)
     }
-    // (dataflow: four more entries, so that an entry's next occupant rarely falls into the segment
-    // that still finishes its previous one, which would force a flush)
-    c->nring = c->depth + 2 + (c->flow ? 4 : 0);
+    // (dataflow: enough more entries that an entry's next occupant never falls into a segment that
+    // still finishes its previous one, which would force a flush: a segment of seg_max ticks spans
+    // seg_max / lag pictures)
+    c->nring = c->depth + 2 + (c->flow ? (c->seg_max + c->lag - 1) / c->lag + 2 : 0);
     c->next_id = 0; c->next_entry = 0; c->last_id = -1; c->last_entry = -1;
     c->ref_kind = REF_NONE; c->ref_entry = -1; c->cur_entry = -1;
     c->prof_mb = -1;
@@ -489,13 +500,17 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
             // segment buffers: seg_max ticks of at most PMAX diagonals each
             c->seg_cap = (size_t)c->seg_max * PMAX * (size_t)std::min(c->mbh, (c->mbw + 1) / 2 + 1) + 1;
             const size_t sb = (size_t)c->nring * sizeof(FlowPic) + c->seg_cap * sizeof(uint32_t);
-            ALLOC(c->d_seg, sb);
+            ALLOC(c->d_seg[0], sb);
+            ALLOC(c->d_seg[1], sb);
+            if (hipStreamCreateWithFlags(&c->ust, hipStreamNonBlocking) != hipSuccess) { st = JMH_E_HIP; goto fail; }
             ALLOC(c->d_flags, (size_t)c->nring * c->nmb * sizeof(uint32_t));
             ALLOC(c->d_head, sizeof(unsigned));
             for (int i = 0; i < 2; i++)
                 if (hipHostMalloc((void **)&c->h_seg[i], sb, hipHostMallocDefault) != hipSuccess ||
-                    hipEventCreateWithFlags(&c->ev_seg[i], hipEventDisableTiming) != hipSuccess) { st = JMH_E_OOM; goto fail; }
+                    hipEventCreateWithFlags(&c->ev_seg[i], hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&c->ev_kseg[i], hipEventDisableTiming) != hipSuccess) { st = JMH_E_OOM; goto fail; }
             if (hipHostMalloc((void **)&c->h_err, 4 * sizeof(unsigned), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) { st = JMH_E_OOM; goto fail; }
+            if (hipEventCreateWithFlags(&c->ev_flow, hipEventDisableTiming) != hipSuccess) { st = JMH_E_HIP; goto fail; }
             memset(c->h_err, 0, 4 * sizeof(unsigned));
             // on the context's stream: a plain hipMemset of device memory may still be pending on the
             // null stream, which the non-blocking stream does not wait for, when the first segment
@@ -661,8 +676,10 @@ static int flow_flush(jmh_ctx *c) {
     }
     memcpy(c->h_seg[sl], c->fpic.data(), pb);
     memcpy(c->h_seg[sl] + pb, c->seg.data(), ib);
-    HCHK(hipMemcpyAsync(c->d_seg, c->h_seg[sl], pb + ib, hipMemcpyHostToDevice, c->st));
-    HCHK(hipEventRecord(c->ev_seg[sl], c->st));
+    HCHK(hipStreamWaitEvent(c->ust, c->ev_kseg[sl], 0));   // the launch two segments back read d_seg[sl]
+    HCHK(hipMemcpyAsync(c->d_seg[sl], c->h_seg[sl], pb + ib, hipMemcpyHostToDevice, c->ust));
+    HCHK(hipEventRecord(c->ev_seg[sl], c->ust));
+    HCHK(hipStreamWaitEvent(c->st, c->ev_seg[sl], 0));
     FlowArgs f;
     memset(&f, 0, sizeof(f));
     f.W = c->W; f.H = c->H; f.mbw = c->mbw; f.mbh = c->mbh; f.sr = c->sr;
@@ -671,8 +688,8 @@ static int flow_flush(jmh_ctx *c) {
     f.slice_mbs = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : c->mbw * c->mbh;
     f.ordtab = c->d_ordtab;
     f.prof = c->d_prof; f.prof_mb = c->prof_mb;
-    f.pics = reinterpret_cast<const FlowPic *>(c->d_seg);
-    f.items = reinterpret_cast<const uint32_t *>(c->d_seg + pb);
+    f.pics = reinterpret_cast<const FlowPic *>(c->d_seg[sl]);
+    f.items = reinterpret_cast<const uint32_t *>(c->d_seg[sl] + pb);
     f.nitems = (int)c->seg.size();
     f.nmb = (int)c->nmb; f.nring = c->nring;
     f.head = c->d_head; f.base = c->head_base;
@@ -690,6 +707,8 @@ static int flow_flush(jmh_ctx *c) {
     HCHK(jmh_launch_flow(f, c->st));
     if (kt) HCHK(ring_end(c->ring_an, c->st));
     HCHK(ring_end(c->ring_mb, c->st));
+    HCHK(hipEventRecord(c->ev_flow, c->st));
+    HCHK(hipEventRecord(c->ev_kseg[sl], c->st));
     c->head_base += (unsigned)c->seg.size();
     c->timing.flow_launches++;
     c->timing.flow_mbs += (int)c->seg.size();
@@ -854,10 +873,11 @@ static int issue_tick(jmh_ctx *c) {
         c->fl.pop_front();
         if (r) return r;
     }
-    if (c->flow && c->seg_ticks >= c->seg_lim) {
-        c->seg_lim = std::min(2 * c->seg_lim, c->seg_max);
+    // flush at seg_max ticks, or earlier once the device has finished every launched segment (so
+    // that it starts soon after the host resumes issuing and segments stay as long as the host's
+    // lead allows: each launch boundary drains the device)
+    if (c->flow && (c->seg_ticks >= c->seg_max || (c->seg_ticks >= c->seg_min && hipEventQuery(c->ev_flow) == hipSuccess)))
         return flow_flush(c);
-    }
     return JMH_OK;
 }
 
@@ -1159,7 +1179,6 @@ int jmh_sync(jmh_ctx *c) {
     HCHK(hipSetDevice(c->dev));
     int r = drain(c);
     if (r) return r;
-    c->seg_lim = std::min(8, c->seg_max);
     HCHK(hipStreamSynchronize(c->st));
     if ((r = flow_check(c))) return r;
     if (c->d_bprof && c->bprof_blocks) {   // debug: block durations of one tick, per role
@@ -1242,7 +1261,6 @@ int jmh_wait_issued(jmh_ctx *c) {
     HCHK(hipSetDevice(c->dev));
     int r = flow_flush(c);
     if (r) return r;
-    c->seg_lim = std::min(8, c->seg_max);
     HCHK(hipStreamSynchronize(c->st));
     return flow_check(c);
 }
