@@ -18,7 +18,8 @@ config = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 root = os.path.join(os.environ.get("GRAFT_REPO_ROOT", os.getcwd()), "gpurun_out")
 NMB = 120 * 68 if config == 2 else 240 * 135
 # the kernels whose bytes the bench line's roofline prices (bench.py an_name)
-ROOFLINE = {2: ["k_mb_analyse"], 3: ["k_mb_epzs", "k_mb_intra"], 5: ["k_rdo_inter", "k_rdo_intra", "k_rdo_final"]}[config]
+# (config 2: k_mb_flow, the dataflow wavefront, or with JMH_FLOW=0 the tick kernels' k_mb_analyse)
+ROOFLINE = {2: ["k_mb_flow", "k_mb_analyse"], 3: ["k_mb_epzs", "k_mb_intra"], 5: ["k_rdo_inter", "k_rdo_intra", "k_rdo_final"]}[config]
 
 
 def bench_line():
@@ -73,6 +74,8 @@ def base_name(k):   # "void k_mb_epzs<unsigned char, false>" -> "k_mb_epzs"
 
 
 roof = [k for k in out["kernels"] if base_name(k) in ROOFLINE]
+if config == 2 and any(base_name(k) == "k_mb_flow" for k in roof):   # the dataflow run: its one kernel
+    roof = [k for k in roof if base_name(k) == "k_mb_flow"]
 if roof and all("hbm_bytes_per_mb" in out["kernels"][k] for k in roof):
     out["roofline_kernels"] = roof
     out["roofline_hbm_bytes_per_mb"] = round(sum(out["kernels"][k]["hbm_bytes_per_mb"] for k in roof), 1)

@@ -2,7 +2,8 @@
 """Fold a PMC pass summary (tools/pmc_parse.py output, committed under profiles/) into
 tools/pmc_traffic.json, the record bench.py prices its roofline traffic and VALU issue with.
     python tools/pmc_update.py KEY profiles/TAG_pmc.json "bench args of the pass"
-KEY: "2", "3", "5" or "5t8"."""
+KEY: "2" (config 2, the dataflow kernel k_mb_flow), "2t" (config 2 with JMH_FLOW=0: the tick kernels),
+"3", "5" or "5t8"."""
 import json
 import os
 import sys
@@ -11,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 key, path, args = sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else ""
 p = json.load(open(path))
 t = json.load(open(os.path.join(ROOT, "tools", "pmc_traffic.json")))
-c = t["configs"][key]
+c = t["configs"].setdefault(key, {})
 roof = p["roofline_kernels"]
 c["tag"] = p["tag"]
 c["kernel"] = " + ".join(k.replace("void ", "").split("<")[0] for k in roof)
