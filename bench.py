@@ -287,7 +287,8 @@ def read_pmc_traffic(config, search_mode, t8=None, slice_mbs=None):
     config is kept in tools/pmc_traffic.json (it travels to the GPU box, unlike profiles/); it is
     a committed measurement of an earlier run of the same kernels, not of this run."""
     p = os.path.join(ROOT, "tools", "pmc_traffic.json")
-    key = {(2, 0): "2" if os.environ.get("JMH_FLOW", "1") != "0" else "2t", (3, 3): "3", (5, 3): "5"}.get((config, search_mode))
+    key = {(2, 0): "2" if os.environ.get("JMH_FLOW", "1") != "0" else "2t", (3, 3): "3", (5, 3): "5",
+           (5, 0): "5ffs"}.get((config, search_mode))
     if key is None or (config == 5 and not RDO):
         return None, None
     try:

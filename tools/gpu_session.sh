@@ -114,6 +114,13 @@ for s in "$@"; do
     pmc3)   run pmc3 900 bash tools/pmc_traffic.sh "${TAG}_c3" 30 3 || exit $? ;;
     pmc5)   run pmc5 900 bash tools/pmc_traffic.sh "${TAG}_c5" 30 5 || exit $? ;;
     pmc5t8) run pmc5t8 900 bash tools/pmc_traffic.sh "${TAG}_c5t8" 30 5 "--t8 1" || exit $? ;;
+    pmc5ffs) run pmc5ffs 900 bash tools/pmc_traffic.sh "${TAG}_c5ffs" 30 5 "--search-mode 0" || exit $? ;;
+    proft)  JMH_FLOW=0 run proft 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_tick" -o ${TAG}_tick --output-format csv -- \
+                python3 "$R/bench.py" --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_proft.log 2>&1 || exit $?
+            find gpurun_out/prof_${TAG}_tick -name "*kernel_stats*" -exec cat {} \; ;;
+    c5ffs)  run c5ffs 900 python bench.py --config 5 --search-mode 0 --steps 60 --no-cpu-baseline --no-host-path > gpurun_out/${TAG}_c5ffs_bench.json \
+                2> gpurun_out/${TAG}_c5ffs_bench.err || exit $?
+            cat gpurun_out/${TAG}_c5ffs_bench.json ;;
     *)      echo "unknown step $s"; exit 2 ;;
   esac
 done
