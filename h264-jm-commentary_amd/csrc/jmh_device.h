@@ -182,7 +182,7 @@ struct TickArgs {
 // RDOptimization 1 + SearchMode 0: bytes of one tick MB's SAD table (jmh_epzs.h ffs_table_build)
 __host__ __device__ __forceinline__ size_t ffs_slot_bytes(int sr) {
     const size_t np = (size_t)(2 * sr + 1) * (2 * sr + 1);
-    return np * (5 * 4 + 36 * 2);
+    return np * 5 * 8;                   // five phases of four u16 SADs per position
 }
 static_assert(sizeof(TickArgs) <= 4096, "TickArgs is passed by value in the kernel argument segment");
 

@@ -289,62 +289,58 @@ __device__ __forceinline__ unsigned lane_block_sad(const EpzS<pel> &s, const EWi
 
 // ---- RDOptimization 1 with SearchMode 0 (item 65): SetupFastFullPelSearch's SAD table [J], shared
 //      by the MB's 41 searches.  One table per tick MB in global memory (ffs_slot_bytes), raster over
-//      the (2 SR + 1)^2 full-pel positions around the MB's FFS centre (the 16x16 MVP / 4, clamped):
-//      u32 [5][NP] for 16x16; 16x8 top, bottom; 8x16 left, right, then u16 [4][9][NP] per 8x8 block
-//      for 8x8; 8x4 top, bottom; 4x8 left, right; its four 4x4 (an 8x8 SAD <= 64 x 1023 < 2^16).
-//      The raster -> spiral-index map (the searches' tie order) follows the spiral table in ordtab.
-// table of the search of block type bt at 4x4 position (bx4, by4): 0..4 u32, 5 + b8 * 9 + j u16
+//      the (2 SR + 1)^2 full-pel positions around the MB's FFS centre (the 16x16 MVP / 4, clamped),
+//      five phases of one 8-byte entry per position: phase 0 the four 8x8 SADs, phase 1 + b8 the
+//      four 4x4 SADs of 8x8 block b8, as u16 (an 8x8 SAD <= 64 x 1023 < 2^16) in raster order.  A
+//      search sums the one, two or four it needs at read time (two v_perm + two v_sad_u16 against
+//      zero): one dwordx2 store per position and phase instead of a store per block type, 169 KB
+//      per MB at SR 32 (JM's nine-plus-five tables were 389 KB), and the nine searches of an 8x8
+//      block read the same 34 KB.  The raster -> spiral-index map (the searches' tie order) follows
+//      the spiral table in ordtab.
+// entry of the search of block type bt at 4x4 position (bx4, by4): phase << 4 | selector (0: all
+// four halves, 1: low dword, 2: high dword, 3: halves 0 + 2, 4: halves 1 + 3, 5 + k: half k)
 __device__ __forceinline__ int ffs_tab_index(int bt, int bx4, int by4) {
     const int b8 = (by4 >> 1) * 2 + (bx4 >> 1);
     switch (bt) {
     case 1: return 0;
     case 2: return 1 + (by4 >> 1);
     case 3: return 3 + (bx4 >> 1);
-    case 4: return 5 + b8 * 9;
-    case 5: return 5 + b8 * 9 + 1 + (by4 & 1);
-    case 6: return 5 + b8 * 9 + 3 + (bx4 & 1);
-    default: return 5 + b8 * 9 + 5 + (by4 & 1) * 2 + (bx4 & 1);
+    case 4: return (1 + b8) << 4;
+    case 5: return (1 + b8) << 4 | (1 + (by4 & 1));
+    case 6: return (1 + b8) << 4 | (3 + (bx4 & 1));
+    default: return (1 + b8) << 4 | (5 + (by4 & 1) * 2 + (bx4 & 1));
     }
 }
-// the tables of one MB on its wave, centre (ccx, ccy), built just before the searches that read
-// them (so they are still in the caches): BIG the 16x16 / 16x8 / 8x16 tables from the four 8x8
-// SADs, else those of 8x8 block b8 from its four 4x4 SADs.  Every position lies inside the LDS
-// window (shifted to the same MVP, margin >= SR + 3).  Lane = column of positions; the window
-// rows slide past the block: each reference row is read once and its SADs against all H block
-// rows go to the H positions (rows) in flight, a position completing every row.  A column past 64
-// (SR 32) per position.  The caller fences before the searches read the tables.
-template <class pel, bool BIG>
+// the tables of one MB on its wave, centre (ccx, ccy), built before its first search: per 8x8 block
+// b8 the four 4x4 SADs (phase 1 + b8), and their sum, the 8x8 SAD, into half b8 of phase 0 (the
+// four 8x8 SADs: the 16x16 / 16x8 / 8x16 searches need no pass of their own).  Every position lies
+// inside the LDS window (shifted to the same MVP, margin >= SR + 3).  Lane = column of positions;
+// the window rows slide past the block: each reference row is read once and its SADs against the 8
+// block rows go to the 8 positions (rows) in flight, a position completing every row.  A column
+// past 64 (SR 32) a lane per position.
+template <class pel>
 __device__ __forceinline__ void ffs_build_phase(const DevParams &d, const EpzS<pel> &s, const EWin<pel> &wn, uint8_t *tab, int ccx, int ccy, int b8,
                                                 int lane) {
     constexpr int EW = EGeo<pel>::ew, PPD = 4 / sizeof(pel);   // samples per dword
-    constexpr int H = BIG ? 16 : 8, ND = H / PPD, OD = 16 / PPD;   // block rows (and columns), dwords per block / MB row
+    constexpr int H = 8, ND = H / PPD, OD = 16 / PPD;    // block rows (and columns), dwords per block / MB row
     const int R = d.sr, side = 2 * R + 1, np = side * side;
-    const int ox = BIG ? 0 : 8 * (b8 & 1), oy = BIG ? 0 : 8 * (b8 >> 1);
-    uint32_t *big = reinterpret_cast<uint32_t *>(tab);
-    uint16_t *sml = reinterpret_cast<uint16_t *>(tab + (size_t)20 * np) + (size_t)(BIG ? 0 : b8) * 9 * np;
+    const int ox = 8 * (b8 & 1), oy = 8 * (b8 >> 1);
+    uint2 *tb = reinterpret_cast<uint2 *>(tab) + (size_t)(1 + b8) * np;
+    uint16_t *t0 = reinterpret_cast<uint16_t *>(tab) + b8;
     uint32_t o[H][ND];                                   // the block's rows (wave-uniform)
 #pragma unroll
     for (int r = 0; r < H; r++)
 #pragma unroll
         for (int q = 0; q < ND; q++) o[r][q] = reinterpret_cast<const uint32_t *>(s.org)[(oy + r) * OD + ox / PPD + q];
-    // accumulator of block row k, dword q: BIG the 8x8, else the 4x4 (raster in the block)
-    auto ai = [](int k, int q) { return (BIG ? (k >> 3) : (k >> 2)) * 2 + q / (ND / 2); };
+    // accumulator of block row k, dword q: the 4x4 (raster in the block)
+    auto ai = [](int k, int q) { return (k >> 2) * 2 + q / (ND / 2); };
     auto sad = [](uint32_t r, uint32_t o, uint32_t c) {
         if constexpr (sizeof(pel) == 2) return __builtin_amdgcn_sad_u16(r, o, c);
         else return __builtin_amdgcn_sad_u8(r, o, c);
     };
     auto store = [&](int p, const uint32_t (&a)[4]) {
-        if constexpr (BIG) {
-            big[p] = a[0] + a[1] + a[2] + a[3];
-            big[np + p] = a[0] + a[1]; big[2 * np + p] = a[2] + a[3];
-            big[3 * np + p] = a[0] + a[2]; big[4 * np + p] = a[1] + a[3];
-        } else {
-            uint16_t *t = sml + p;
-            t[0] = (uint16_t)(a[0] + a[1] + a[2] + a[3]);
-            t[1 * np] = (uint16_t)(a[0] + a[1]); t[2 * np] = (uint16_t)(a[2] + a[3]);
-            t[3 * np] = (uint16_t)(a[0] + a[2]); t[4 * np] = (uint16_t)(a[1] + a[3]);
-            t[5 * np] = (uint16_t)a[0]; t[6 * np] = (uint16_t)a[1]; t[7 * np] = (uint16_t)a[2]; t[8 * np] = (uint16_t)a[3];
-        }
+        tb[p] = make_uint2(a[0] | a[1] << 16, a[2] | a[3] << 16);
+        t0[4 * p] = (uint16_t)(a[0] + a[1] + a[2] + a[3]);
     };
     const int wy0 = wn.my + ccy - R + oy, wx0 = wn.mx + ccx - R + ox;   // window position of position (0, 0)
     const int nc = min(side, NTE), c = min(lane, nc - 1), nrow = side + H - 1;
@@ -394,59 +390,83 @@ __device__ __forceinline__ void ffs_build_phase(const DevParams &d, const EpzS<p
         }
 }
 template <class pel>
-__device__ __forceinline__ void ffs_table_build(const DevParams &d, const EpzS<pel> &s, const EWin<pel> &wn, uint8_t *tab, int ccx, int ccy, int b8,
-                                                int lane) {
-    if (b8 < 0) ffs_build_phase<pel, true>(d, s, wn, tab, ccx, ccy, 0, lane);
-    else ffs_build_phase<pel, false>(d, s, wn, tab, ccx, ccy, b8, lane);
+__device__ __forceinline__ void ffs_table_build(const DevParams &d, const EpzS<pel> &s, const EWin<pel> &wn, uint8_t *tab, int ccx, int ccy, int lane) {
+#pragma unroll 1
+    for (int b8 = 0; b8 < 4; b8++) ffs_build_phase<pel>(d, s, wn, tab, ccx, ccy, b8, lane);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 // the full-pel search of one block from the table: every position of +-range around the centre,
-// key = cost << 13 | spiral index (JM's scan order, strict '<'), one wave minimum.  Lanes take the
-// columns of a row (the row's MV-cost bits uniform; lanes past the last column repeat it), FFS_RB
-// rows' loads in flight per round trip; columns past 64 a lane per row.
+// key = cost << 13 | spiral index (JM's scan order, strict '<'; the raster -> spiral map in ordtab),
+// one wave minimum.  Lanes take the columns of a row (the row's MV-cost bits uniform; lanes past the
+// last column repeat it), FFS_RB rows' loads in flight per round trip, and with them the column past
+// 64 (SR 32) of those rows on lanes 0 .. FFS_RB - 1.  The entry's halves summed per selector class
+// M (uniform): 0 all four (uint2, two v_sad_u16), 1 one dword's pair (u32, one v_sad_u16), 2 halves
+// 0 + 2 or 1 + 3 (uint2, v_perm + v_sad_u16), 3 one half (u32, one shift or mask).
 #ifndef FFS_RB
-#define FFS_RB 16
+#define FFS_RB 16                                     // rows per round trip, 8-byte entries (M 0, 2)
 #endif
-template <class T>
-__device__ __forceinline__ unsigned ffs_table_min_t(const DevParams &d, const T *tab, int range, int ccx, int ccy, int pmx, int pmy, int lane) {
+#ifndef FFS_RB4
+#define FFS_RB4 16                                    // ... 4-byte reads (M 1, 3)
+#endif
+template <int M>
+__device__ __forceinline__ unsigned ffs_min_m(const DevParams &d, const uint8_t *tab_, int ph, int sel, int range, int ccx, int ccy, int pmx, int pmy, int lane) {
     const int R = d.sr, side = 2 * R + 1, np = side * side, n = 2 * range + 1, c0 = R - range;
+    typedef typename std::conditional<M == 0 || M == 2, uint2, uint32_t>::type E;
+    // the dword (M 1, 3) or the whole entry (M 0, 2)
+    const E *tab = reinterpret_cast<const E *>(reinterpret_cast<const uint2 *>(tab_) + (size_t)ph * np) + ((M == 1 || M == 3) ? (sel >> 1) : 0);
+    constexpr int ES = (M == 1 || M == 3) ? 2 : 1;       // entry stride in E
+    const uint32_t pm = (sel & 1) ? 0x07060302u : 0x05040100u;   // M 2: halves 1 + 3 / 0 + 2
+    const int sh = 16 * (sel & 1);                       // M 3: the half in its dword
+    auto val = [&](E v) -> unsigned {
+        if constexpr (M == 0) return __builtin_amdgcn_sad_u16(v.y, 0u, __builtin_amdgcn_sad_u16(v.x, 0u, 0u));
+        else if constexpr (M == 1) return __builtin_amdgcn_sad_u16(v, 0u, 0u);
+        else if constexpr (M == 2) return __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(v.y, v.x, pm), 0u, 0u);
+        else return (v >> sh) & 0xFFFFu;
+    };
     const uint32_t *spr = d.ordtab + ORDTAB_SPOS + np;
+    constexpr int RB = (M == 0 || M == 2) ? FFS_RB : FFS_RB4;
     unsigned kb = 0xFFFFFFFFu;
     const int lc = min(lane, n - 1);
     // WEIGHTED_COST under RDO, (lf x (bits_x + bits_y)) >> 16, as lf bits_x + lf bits_y (the row's
     // term uniform): no per-position multiply (products < 2^32 as in wcost)
     const unsigned lf = d.lf, lfx = lf * (unsigned)mvbits(4 * (ccx + lc - range) - pmx);
+    const bool xc = n > NTE;                             // the column past 64 (wave-uniform)
+    const unsigned lfc = lf * (unsigned)mvbits(4 * (ccx + NTE - range) - pmx);
 #pragma unroll 1
-    for (int r0 = 0; r0 < n; r0 += FFS_RB) {
-        uint32_t sv[FFS_RB], pv[FFS_RB];
+    for (int r0 = 0; r0 < n; r0 += RB) {
+        E sv[RB], xv{};
+        uint32_t pv[RB], xp = 0;
+        const int xr = min(r0 + lane, n - 1);
 #pragma unroll
-        for (int j = 0; j < FFS_RB; j++) {
+        for (int j = 0; j < RB; j++) {
             const int p = (min(r0 + j, n - 1) + c0) * side + c0 + lc;
-            sv[j] = tab[p];
+            sv[j] = tab[(size_t)ES * p];
             pv[j] = spr[p];
         }
-#pragma unroll
-        for (int j = 0; j < FFS_RB; j++) {
-            const unsigned lfy = lf * (unsigned)mvbits(4 * (ccy + min(r0 + j, n - 1) - range) - pmy);   // uniform
-            kb = min(kb, ((sv[j] + ((lfx + lfy) >> 16)) << 13) | pv[j]);
+        if (xc) {
+            const int p = (xr + c0) * side + c0 + NTE;
+            xv = tab[(size_t)ES * p];
+            xp = spr[p];
         }
-    }
-#pragma unroll 1
-    for (int cc = NTE; cc < n; cc++) {                   // n = 65 (SR 32): one column
-        const unsigned lfc = lf * (unsigned)mvbits(4 * (ccx + cc - range) - pmx);
-        for (int rr = 0; rr < n; rr += NTE) {
-            const int row = min(rr + lane, n - 1), p = (row + c0) * side + c0 + cc;
-            const unsigned lfr = lf * (unsigned)mvbits(4 * (ccy + row - range) - pmy);
-            kb = min(kb, (((unsigned)tab[p] + ((lfc + lfr) >> 16)) << 13) | spr[p]);
+#pragma unroll
+        for (int j = 0; j < RB; j++) {
+            const unsigned lfy = lf * (unsigned)mvbits(4 * (ccy + min(r0 + j, n - 1) - range) - pmy);   // uniform
+            kb = min(kb, ((val(sv[j]) + ((lfx + lfy) >> 16)) << 13) | pv[j]);
+        }
+        if (xc && lane < RB) {
+            const unsigned lfr = lf * (unsigned)mvbits(4 * (ccy + xr - range) - pmy);
+            kb = min(kb, ((val(xv) + ((lfc + lfr) >> 16)) << 13) | xp);
         }
     }
     return wave_min_u32(kb);
 }
 __device__ __forceinline__ unsigned ffs_table_min(const DevParams &d, const uint8_t *tab, int ti, int range, int ccx, int ccy, int pmx, int pmy, int lane) {
-    const size_t np = (size_t)(2 * d.sr + 1) * (2 * d.sr + 1);
-    if (ti < 5) return ffs_table_min_t(d, reinterpret_cast<const uint32_t *>(tab) + (size_t)ti * np, range, ccx, ccy, pmx, pmy, lane);
-    return ffs_table_min_t(d, reinterpret_cast<const uint16_t *>(tab + 20 * np) + (size_t)(ti - 5) * np, range, ccx, ccy, pmx, pmy, lane);
+    const int ph = ti >> 4, sel = ti & 15;
+    if (sel == 0) return ffs_min_m<0>(d, tab, ph, 0, range, ccx, ccy, pmx, pmy, lane);
+    if (sel <= 2) return ffs_min_m<1>(d, tab, ph, 2 * (sel - 1), range, ccx, ccy, pmx, pmy, lane);
+    if (sel <= 4) return ffs_min_m<2>(d, tab, ph, sel - 3, range, ccx, ccy, pmx, pmy, lane);
+    return ffs_min_m<3>(d, tab, ph, sel - 5, range, ccx, ccy, pmx, pmy, lane);
 }
 
 typedef short e16x2 __attribute__((ext_vector_type(2)));

@@ -373,8 +373,8 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     wave_lds_sync();
     PSTAMP(41);
     const jmr_mbinfo *A = hasA ? &s.nbA : nullptr, *B = hasB ? &s.nbB : nullptr;
-    // SearchMode 0: the SAD tables of the searches (SetupFastFullPelSearch [J]) around the FFS centre,
-    // the 16x16 / 16x8 / 8x16 ones here, each 8x8 block's before its searches
+    // SearchMode 0: the SAD tables of the 41 searches (SetupFastFullPelSearch [J]) around the FFS
+    // centre, before the first
     int fcx = 0, fcy = 0;
     if (ftab) {
         int pmx, pmy;
@@ -382,7 +382,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         set_mvp_nb(NbEpz<EpzS<pel>>{s.e, 1, 0, 0}, 0, 0, 16, 16, pmx, pmy, nb);
         fcx = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmx / 4));
         fcy = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmy / 4));
-        ffs_table_build(d, s.e, wn, ftab, fcx, fcy, -1, lane);
+        ffs_table_build(d, s.e, wn, ftab, fcx, fcy, lane);
         PSTAMP(20);
     }
     // ---- motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch [J])
@@ -405,10 +405,6 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
 #pragma unroll 1
     for (int b8 = 0; b8 < 4 && p8; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
-        if (ftab) {
-            ffs_table_build(d, s.e, wn, ftab, fcx, fcy, b8, lane);
-            PSTAMP(21 + b8);                            // debug: stamps 20..24 after the SAD tables
-        }
         epzs_block<4, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab);
         epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab);
         epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
