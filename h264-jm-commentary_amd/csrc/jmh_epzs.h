@@ -404,10 +404,10 @@ __device__ __forceinline__ void ffs_table_build(const DevParams &d, const EpzS<p
 // M (uniform): 0 all four (uint2, two v_sad_u16), 1 one dword's pair (u32, one v_sad_u16), 2 halves
 // 0 + 2 or 1 + 3 (uint2, v_perm + v_sad_u16), 3 one half (u32, one shift or mask).
 #ifndef FFS_RB
-#define FFS_RB 16                                     // rows per round trip, 8-byte entries (M 0, 2)
+#define FFS_RB 22                                     // rows per round trip, 8-byte entries (M 0, 2)
 #endif
 #ifndef FFS_RB4
-#define FFS_RB4 16                                    // ... 4-byte reads (M 1, 3)
+#define FFS_RB4 22                                    // ... 4-byte reads (M 1, 3)
 #endif
 template <int M>
 __device__ __forceinline__ unsigned ffs_min_m(const DevParams &d, const uint8_t *tab_, int ph, int sel, int range, int ccx, int ccy, int pmx, int pmy, int lane) {
@@ -418,11 +418,12 @@ __device__ __forceinline__ unsigned ffs_min_m(const DevParams &d, const uint8_t 
     constexpr int ES = (M == 1 || M == 3) ? 2 : 1;       // entry stride in E
     const uint32_t pm = (sel & 1) ? 0x07060302u : 0x05040100u;   // M 2: halves 1 + 3 / 0 + 2
     const int sh = 16 * (sel & 1);                       // M 3: the half in its dword
-    auto val = [&](E v) -> unsigned {
-        if constexpr (M == 0) return __builtin_amdgcn_sad_u16(v.y, 0u, __builtin_amdgcn_sad_u16(v.x, 0u, 0u));
-        else if constexpr (M == 1) return __builtin_amdgcn_sad_u16(v, 0u, 0u);
-        else if constexpr (M == 2) return __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(v.y, v.x, pm), 0u, 0u);
-        else return (v >> sh) & 0xFFFFu;
+    // the SAD plus t (the MV cost), v_sad_u16 against zero accumulating it
+    auto val = [&](E v, unsigned t) -> unsigned {
+        if constexpr (M == 0) return __builtin_amdgcn_sad_u16(v.y, 0u, __builtin_amdgcn_sad_u16(v.x, 0u, t));
+        else if constexpr (M == 1) return __builtin_amdgcn_sad_u16(v, 0u, t);
+        else if constexpr (M == 2) return __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(v.y, v.x, pm), 0u, t);
+        else return ((v >> sh) & 0xFFFFu) + t;
     };
     const uint32_t *spr = d.ordtab + ORDTAB_SPOS + np;
     constexpr int RB = (M == 0 || M == 2) ? FFS_RB : FFS_RB4;
@@ -452,11 +453,11 @@ __device__ __forceinline__ unsigned ffs_min_m(const DevParams &d, const uint8_t 
 #pragma unroll
         for (int j = 0; j < RB; j++) {
             const unsigned lfy = lf * (unsigned)mvbits(4 * (ccy + min(r0 + j, n - 1) - range) - pmy);   // uniform
-            kb = min(kb, ((val(sv[j]) + ((lfx + lfy) >> 16)) << 13) | pv[j]);
+            kb = min(kb, (val(sv[j], (lfx + lfy) >> 16) << 13) | pv[j]);
         }
         if (xc && lane < RB) {
             const unsigned lfr = lf * (unsigned)mvbits(4 * (ccy + xr - range) - pmy);
-            kb = min(kb, ((val(xv) + ((lfc + lfr) >> 16)) << 13) | xp);
+            kb = min(kb, (val(xv, (lfc + lfr) >> 16) << 13) | xp);
         }
     }
     return wave_min_u32(kb);
@@ -918,6 +919,109 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
 }
 
 
+// the LDS window of a macroblock's searches: MB +- off, shifted to the MB's 16x16 MVP / 4 (clamped
+// to +-SR; horizontally a multiple of 4) when off < 2 SR + 4 -- the centre most searches search
+// around (the border cells in s.bd, synced)
+template <class pel>
+__device__ __forceinline__ EWin<pel> epzs_place(const DevParams &d, const EpzS<pel> &s, int mbx, int mby) {
+    const int sr = d.sr, off = min(2 * sr + 4, EGeo<pel>::off);
+    int wcx = 0, wcy = 0;
+    if (off < 2 * sr + 4) {
+        int pcx, pcy;
+        set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
+        wcx = __builtin_amdgcn_readfirstlane(iclip(-sr, sr, pcx / 4) & ~3);
+        wcy = __builtin_amdgcn_readfirstlane(iclip(-sr, sr, pcy / 4));
+    }
+    return EWin<pel>{spl<pel>(d.refY), d.W, d.H, 16 * mbx + wcx - off, 16 * mby + wcy - off, off - wcx, off - wcy};
+}
+// ... its samples, NTH threads (dword per task: two aligned global dwords + v_alignbyte inside the
+// picture, clamped samples at its edges: the spec's UMV access)
+template <class pel, int NTH>
+__device__ __forceinline__ void epzs_load_window(const DevParams &d, EpzS<pel> &s, const EWin<pel> &wn, int lane) {
+    const int W = d.W, off = min(2 * d.sr + 4, EGeo<pel>::off), wdim = 16 + 2 * off;
+    const pel *refY = wn.ref;
+    if constexpr (sizeof(pel) == 2) {
+        // 16-bit samples: two per dword; with off % 4 == 0 a dword is aligned in the picture and
+        // wholly inside or outside it (as for bytes), else per-sample clamped reads
+        constexpr int ND2 = EGeo<pel>::ew / 2, NB = EPZS_NB16;
+        const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND2;
+        if ((off & 3) == 0) {
+            for (int t0 = 0; t0 < ntask; t0 += NB * NTH) {
+                uint32_t v[NB];
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const int task = t0 + u * NTH + lane, y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
+                    const pel *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
+                    const int xs = x0 < 0 ? 0 : x0 >= W ? W - 2 : x0;
+                    v[u] = task < ntask ? *reinterpret_cast<const uint32_t *>(row + xs) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const int task = t0 + u * NTH + lane, y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
+                    if (task >= ntask) continue;
+                    uint32_t w = v[u];
+                    if (x0 < 0) w = (w & 0xFFFFu) * 0x10001u;
+                    else if (x0 >= W) w = (w >> 16) * 0x10001u;
+                    if (2 * j >= wdim) w = 0;
+                    *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 2 * j) = w;
+                }
+            }
+        } else {
+            for (int task = lane; task < ntask; task += NTH) {
+                const int y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
+                const pel *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
+                uint32_t v = 0;
+                for (int q = 0; q < 2; q++)
+                    if (2 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (16 * q);
+                *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 2 * j) = v;
+            }
+        }
+    } else {
+        // with off % 4 == 0 the window's dwords are aligned in the picture (pix_x % 16 == 0, wcx %
+        // 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an outside
+        // dword is the replicated edge sample.  Two batches of 32 loads per lane in flight.
+        constexpr int ND4 = EGeo<pel>::ew / 4, NB = EPZS_NB8;
+        const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND4;
+        if ((off & 3) == 0) {
+            for (int t0 = 0; t0 < ntask; t0 += NB * NTH) {
+                uint32_t v[NB];
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const int task = t0 + u * NTH + lane, y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
+                    const uint8_t *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
+                    const int xs = x0 < 0 ? 0 : x0 >= W ? W - 4 : x0;
+                    v[u] = task < ntask ? *reinterpret_cast<const uint32_t *>(row + xs) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < NB; u++) {
+                    const int task = t0 + u * NTH + lane, y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
+                    if (task >= ntask) continue;
+                    uint32_t w = v[u];
+                    if (x0 < 0) w = (w & 0xFFu) * 0x01010101u;              // left of the picture
+                    else if (x0 >= W) w = (w >> 24) * 0x01010101u;          // right of it
+                    if (4 * j >= wdim) w = 0;
+                    *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 4 * j) = w;
+                }
+            }
+        } else {   // odd SearchRange: two aligned global dwords + v_alignbyte, clamped bytes at the edges
+            for (int task = lane; task < ntask; task += NTH) {
+                const int y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
+                const uint8_t *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
+                uint32_t v;
+                if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
+                    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
+                    v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
+                } else {
+                    v = 0;
+                    for (int q = 0; q < 4; q++)
+                        if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
+                }
+                *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 4 * j) = v;
+            }
+        }
+    }
+}
+
 // the inputs of one macroblock's searches on one wave (lane = 0..63): the MB (one dword per lane),
 // border cells, the temporal neighbourhood, the left MB's searches, the window (dword per task: two
 // aligned global dwords + v_alignbyte inside the picture, clamped bytes at its edges: the spec's
@@ -925,9 +1029,9 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
 template <class pel>
 __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> &s, int mbx, int mby, int lane) {
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, sr = d.sr;
-    const int off = min(2 * sr + 4, EGeo<pel>::off), wdim = 16 + 2 * off;
+    const int off = min(2 * sr + 4, EGeo<pel>::off);
     const int X0 = 4 * mbx, Y0 = 4 * mby, left = mb_avail(d, mbx, mby).L ? mby * d.mbw + mbx - 1 : -1;
-    const pel *orgY = spl<pel>(d.orgY), *refY = spl<pel>(d.refY);
+    const pel *orgY = spl<pel>(d.orgY);
     if constexpr (sizeof(pel) == 1)
         reinterpret_cast<uint32_t *>(s.org)[lane] = *reinterpret_cast<const uint32_t *>(orgY + (pix_y + (lane >> 2)) * W + pix_x + 4 * (lane & 3));
     else
@@ -961,96 +1065,8 @@ __device__ __forceinline__ EWin<pel> epzs_load_mb(const DevParams &d, EpzS<pel> 
         }
         s.fpb[bt][cell] = (uint16_t)v;
     }
-    // the window: MB +- off, shifted to the MB's 16x16 MVP / 4 (clamped to +-SR; horizontally a
-    // multiple of 4) when off < 2 SR + 4 -- the centre most searches search around
-    int wcx = 0, wcy = 0;
-    if (off < 2 * sr + 4) {
-        wave_lds_sync();   // the border cells
-        int pcx, pcy;
-        set_mvp(NbBorder{s.bd}, 0, 0, 16, 16, pcx, pcy);
-        wcx = __builtin_amdgcn_readfirstlane(iclip(-sr, sr, pcx / 4) & ~3);
-        wcy = __builtin_amdgcn_readfirstlane(iclip(-sr, sr, pcy / 4));
-    }
-    const EWin<pel> wn{refY, W, d.H, pix_x + wcx - off, pix_y + wcy - off, off - wcx, off - wcy};
-    if constexpr (sizeof(pel) == 2) {
-        // 16-bit samples: two per dword; with off % 4 == 0 a dword is aligned in the picture and
-        // wholly inside or outside it (as for bytes), else per-sample clamped reads
-        constexpr int ND2 = EGeo<pel>::ew / 2, NB = EPZS_NB16;
-        const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND2;
-        if ((off & 3) == 0) {
-            for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
-                uint32_t v[NB];
-#pragma unroll
-                for (int u = 0; u < NB; u++) {
-                    const int task = t0 + u * NTE + lane, y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
-                    const pel *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
-                    const int xs = x0 < 0 ? 0 : x0 >= W ? W - 2 : x0;
-                    v[u] = task < ntask ? *reinterpret_cast<const uint32_t *>(row + xs) : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < NB; u++) {
-                    const int task = t0 + u * NTE + lane, y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
-                    if (task >= ntask) continue;
-                    uint32_t w = v[u];
-                    if (x0 < 0) w = (w & 0xFFFFu) * 0x10001u;
-                    else if (x0 >= W) w = (w >> 16) * 0x10001u;
-                    if (2 * j >= wdim) w = 0;
-                    *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 2 * j) = w;
-                }
-            }
-        } else {
-            for (int task = lane; task < ntask; task += NTE) {
-                const int y = task / ND2, j = task - y * ND2, x0 = WX0 + 2 * j;
-                const pel *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
-                uint32_t v = 0;
-                for (int q = 0; q < 2; q++)
-                    if (2 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (16 * q);
-                *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 2 * j) = v;
-            }
-        }
-    } else {
-        // with off % 4 == 0 the window's dwords are aligned in the picture (pix_x % 16 == 0, wcx %
-        // 4 == 0) and lie wholly inside or wholly left / right of it (W % 16 == 0): an outside
-        // dword is the replicated edge sample.  Two batches of 32 loads per lane in flight.
-        constexpr int ND4 = EGeo<pel>::ew / 4, NB = EPZS_NB8;
-        const int WX0 = wn.wx0, WY0 = wn.wy0, ntask = wdim * ND4;
-        if ((off & 3) == 0) {
-            for (int t0 = 0; t0 < ntask; t0 += NB * NTE) {
-                uint32_t v[NB];
-#pragma unroll
-                for (int u = 0; u < NB; u++) {
-                    const int task = t0 + u * NTE + lane, y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
-                    const uint8_t *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
-                    const int xs = x0 < 0 ? 0 : x0 >= W ? W - 4 : x0;
-                    v[u] = task < ntask ? *reinterpret_cast<const uint32_t *>(row + xs) : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < NB; u++) {
-                    const int task = t0 + u * NTE + lane, y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
-                    if (task >= ntask) continue;
-                    uint32_t w = v[u];
-                    if (x0 < 0) w = (w & 0xFFu) * 0x01010101u;              // left of the picture
-                    else if (x0 >= W) w = (w >> 24) * 0x01010101u;          // right of it
-                    if (4 * j >= wdim) w = 0;
-                    *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 4 * j) = w;
-                }
-            }
-        } else {   // odd SearchRange: two aligned global dwords + v_alignbyte, clamped bytes at the edges
-            for (int task = lane; task < ntask; task += NTE) {
-                const int y = task / ND4, j = task - y * ND4, x0 = WX0 + 4 * j;
-                const uint8_t *row = refY + iclip(0, d.H - 1, WY0 + y) * W;
-                uint32_t v;
-                if (4 * j + 3 < wdim && x0 >= 0 && x0 + 3 < W) {
-                    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (x0 & ~3));
-                    v = __builtin_amdgcn_alignbyte((x0 & 3) ? p[1] : 0u, p[0], x0 & 3);
-                } else {
-                    v = 0;
-                    for (int q = 0; q < 4; q++)
-                        if (4 * j + q < wdim) v |= (uint32_t)row[iclip(0, W - 1, x0 + q)] << (8 * q);
-                }
-                *reinterpret_cast<uint32_t *>(s.g + y * EGeo<pel>::ew + 4 * j) = v;
-            }
-        }
-    }
+    if (off < 2 * sr + 4) wave_lds_sync();   // the border cells
+    const EWin<pel> wn = epzs_place(d, s, mbx, mby);
+    epzs_load_window<pel, NTE>(d, s, wn, lane);
     return wn;
 }

@@ -375,13 +375,12 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     const jmr_mbinfo *A = hasA ? &s.nbA : nullptr, *B = hasB ? &s.nbB : nullptr;
     // SearchMode 0: the SAD tables of the 41 searches (SetupFastFullPelSearch [J]) around the FFS
     // centre, before the first
-    int fcx = 0, fcy = 0;
     if (ftab) {
         int pmx, pmy;
         MvpNb nb;
         set_mvp_nb(NbEpz<EpzS<pel>>{s.e, 1, 0, 0}, 0, 0, 16, 16, pmx, pmy, nb);
-        fcx = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmx / 4));
-        fcy = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmy / 4));
+        const int fcx = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmx / 4));
+        const int fcy = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmy / 4));
         ffs_table_build(d, s.e, wn, ftab, fcx, fcy, lane);
         PSTAMP(20);
     }
