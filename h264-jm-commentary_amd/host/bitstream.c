@@ -295,11 +295,13 @@ static int calc_nc(const wctx *w, int mx, int my, int comp, int x4, int y4, cons
 }
 
 /* predIntra4x4PredMode / predIntra8x8PredMode (8.3.1.1 / 8.3.2.1): DC unless both the left and
- * the upper neighbour exist; a neighbour that is not I_NxN counts as DC (2) */
+ * the upper neighbour exist (and, with constrained_intra_pred_flag, are intra); a neighbour that
+ * is not I_NxN counts as DC (2) */
 int jm_w_mpm(const wctx *w, int mx, int my, int x4, int y4) {
     int ia = 0, ib = 0;
     int aa = nb(w, mx, my, 4 * x4 - 1, 4 * y4, &ia, 1), ab = nb(w, mx, my, 4 * x4, 4 * y4 - 1, &ib, 1);
     if (!aa || !ab) return 2;
+    if (w->s->constrained_intra && (w->ref[ia] >= 0 || w->ref[ib] >= 0)) return 2;
     int ma = w->ipm[ia] < 0 ? 2 : w->ipm[ia], mb = w->ipm[ib] < 0 ? 2 : w->ipm[ib];
     return ma < mb ? ma : mb;
 }

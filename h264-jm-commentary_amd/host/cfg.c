@@ -186,7 +186,6 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->symbol_mode && inp->model_number) { snprintf(err, errlen, "FixedModelNumber=%d not supported (0: cabac_init_idc 0)", inp->model_number); return -1; }
     if (inp->search_mode != 0 && inp->search_mode != -1 && inp->search_mode != 3) { snprintf(err, errlen, "SearchMode=%d not supported (use -1, 0 or 3)", inp->search_mode); return -1; }
     if (inp->num_ref_frames != 1) { snprintf(err, errlen, "NumberReferenceFrames=%d not supported (1)", inp->num_ref_frames); return -1; }
-    if (inp->constrained_intra) { snprintf(err, errlen, "UseConstrainedIntraPred=1 not supported"); return -1; }
     if (inp->profile_idc != 66 && inp->profile_idc != 77 && inp->profile_idc != 100 && inp->profile_idc != 110) { snprintf(err, errlen, "ProfileIDC=%d not supported (66, 77, 100 or 110)", inp->profile_idc); return -1; }
     if (inp->bit_depth_luma > 10 || inp->bit_depth_chroma != inp->bit_depth_luma) { snprintf(err, errlen, "SourceBitDepthLuma=%d / SourceBitDepthChroma=%d not supported (equal, 8..10)", inp->bit_depth_luma, inp->bit_depth_chroma); return -1; }
     if (inp->bit_depth_luma > 8 && inp->profile_idc != 110) { snprintf(err, errlen, "SourceBitDepthLuma=%d requires ProfileIDC=110 (High 10)", inp->bit_depth_luma); return -1; }

@@ -265,12 +265,19 @@ static int avail_mb(const jmo_dec *d, int mx, int my, int cmx, int cmy) {
     if (mx < 0 || my < 0 || mx >= d->mbw || my >= d->mbh || my * d->mbw + mx < d->slice_first) return 0;
     return my < cmy || (my == cmy && mx < cmx);
 }
+/* ... for Intra prediction: with constrained_intra_pred_flag an inter (or skipped) neighbour's
+ * samples are not available (8.3.1.2, 8.3.2.2, 8.3.3, 8.3.4) */
+static int iavail_mb(const jmo_dec *d, int mx, int my, int cmx, int cmy) {
+    if (!avail_mb(d, mx, my, cmx, cmy)) return 0;
+    const int t = d->mi[my * d->mbw + mx].mbtype;
+    return !d->cip || t == 1 || t == 2 || t == 4;
+}
 /* availability of luma sample at MB-relative (x,y) for intra 4x4 block at (bx,by) */
 static int lavail(const jmo_dec *d, int mx, int my, int x, int y, int blk_idx) {
-    if (x > 15 || y > 15) { if (x > 15 && y < 0) return avail_mb(d, mx + 1, my - 1, mx, my); return 0; }
-    if (x < 0 && y < 0) return avail_mb(d, mx - 1, my - 1, mx, my);
-    if (x < 0) return avail_mb(d, mx - 1, my, mx, my);
-    if (y < 0) return avail_mb(d, mx, my - 1, mx, my);
+    if (x > 15 || y > 15) { if (x > 15 && y < 0) return iavail_mb(d, mx + 1, my - 1, mx, my); return 0; }
+    if (x < 0 && y < 0) return iavail_mb(d, mx - 1, my - 1, mx, my);
+    if (x < 0) return iavail_mb(d, mx - 1, my, mx, my);
+    if (y < 0) return iavail_mb(d, mx, my - 1, mx, my);
     (void)blk_idx;
     return 1;
 }
@@ -281,7 +288,7 @@ static void pred4x4(const jmo_dec *d, int mx, int my, int bx, int by, int blk_id
     int ul = lavail(d, mx, my, bx - 1, by - 1, blk_idx);
     int ur = lavail(d, mx, my, bx + 4, by - 1, blk_idx);
     if (blk_idx == 3 || blk_idx == 11 || blk_idx == 7 || blk_idx == 13 || blk_idx == 15) ur = 0;
-    if ((blk_idx == 5) && !avail_mb(d, mx + 1, my - 1, mx, my)) ur = 0;
+    if ((blk_idx == 5) && !iavail_mb(d, mx + 1, my - 1, mx, my)) ur = 0;
     int p[13];                           /* p[0] = (-1,-1), p[1..8] = (0..7,-1), p[9..12] = (-1,0..3) */
     p[0] = ul ? R[(Y - 1) * W + X - 1] : 0;
     for (int i = 0; i < 4; i++) p[1 + i] = up ? R[(Y - 1) * W + X + i] : 0;
@@ -348,7 +355,7 @@ static void pred4x4(const jmo_dec *d, int mx, int my, int bx, int by, int blk_id
 static int pred16(const jmo_dec *d, int mx, int my, int mode, pel *pr) {
     const pel *R = d->cur[0];
     int W = d->W, X = 16 * mx, Y = 16 * my;
-    int up = avail_mb(d, mx, my - 1, mx, my), left = avail_mb(d, mx - 1, my, mx, my), ul = avail_mb(d, mx - 1, my - 1, mx, my);
+    int up = iavail_mb(d, mx, my - 1, mx, my), left = iavail_mb(d, mx - 1, my, mx, my), ul = iavail_mb(d, mx - 1, my - 1, mx, my);
     int T[17], L[17];                   /* index 0 = corner */
     T[0] = L[0] = ul ? R[(Y - 1) * W + X - 1] : 0;
     for (int i = 0; i < 16; i++) { T[1 + i] = up ? R[(Y - 1) * W + X + i] : 0; L[1 + i] = left ? R[(Y + i) * W + X - 1] : 0; }
@@ -372,7 +379,7 @@ static int predc(const jmo_dec *d, int mx, int my, int comp, int mode, pel *pr) 
     const pel *R = d->cur[comp];
     const int dcd = 1 << (d->bd - 1);
     int W = d->W / 2, X = 8 * mx, Y = 8 * my;
-    int up = avail_mb(d, mx, my - 1, mx, my), left = avail_mb(d, mx - 1, my, mx, my), ul = avail_mb(d, mx - 1, my - 1, mx, my);
+    int up = iavail_mb(d, mx, my - 1, mx, my), left = iavail_mb(d, mx - 1, my, mx, my), ul = iavail_mb(d, mx - 1, my - 1, mx, my);
     int T[9], L[9];
     T[0] = L[0] = ul ? R[(Y - 1) * W + X - 1] : 0;
     for (int i = 0; i < 8; i++) { T[1 + i] = up ? R[(Y - 1) * W + X + i] : 0; L[1 + i] = left ? R[(Y + i) * W + X - 1] : 0; }
@@ -433,10 +440,10 @@ static void recon4x4(int32_t *c, const pel *pred, int ps, pel *out, int os, int 
 static int pred8x8(const jmo_dec *d, int mx, int my, int b8, int mode, pel *pr) {
     const pel *R = d->cur[0];
     int W = d->W, bx = 8 * (b8 & 1), by = 8 * (b8 >> 1), X = 16 * mx + bx, Y = 16 * my + by;
-    int left = bx ? 1 : avail_mb(d, mx - 1, my, mx, my);
-    int up = by ? 1 : avail_mb(d, mx, my - 1, mx, my);
-    int ul = bx && by ? 1 : bx ? avail_mb(d, mx, my - 1, mx, my) : by ? avail_mb(d, mx - 1, my, mx, my) : avail_mb(d, mx - 1, my - 1, mx, my);
-    int ur = b8 == 0 ? avail_mb(d, mx, my - 1, mx, my) : b8 == 1 ? avail_mb(d, mx + 1, my - 1, mx, my) : b8 == 2;
+    int left = bx ? 1 : iavail_mb(d, mx - 1, my, mx, my);
+    int up = by ? 1 : iavail_mb(d, mx, my - 1, mx, my);
+    int ul = bx && by ? 1 : bx ? iavail_mb(d, mx, my - 1, mx, my) : by ? iavail_mb(d, mx - 1, my, mx, my) : iavail_mb(d, mx - 1, my - 1, mx, my);
+    int ur = b8 == 0 ? iavail_mb(d, mx, my - 1, mx, my) : b8 == 1 ? iavail_mb(d, mx + 1, my - 1, mx, my) : b8 == 2;
     int e[25], av[25], f[25];
     for (int i = 0; i < 25; i++) { e[i] = 0; av[i] = 0; }
     for (int y = 0; y < 8; y++) if (left) { e[7 - y] = R[(Y + y) * W + X - 1]; av[7 - y] = 1; }
@@ -653,11 +660,12 @@ static void skip_motion(jmo_dec *d, int mx, int my, mbsyn *s) {
 /* predIntra4x4PredMode / predIntra8x8PredMode (8.3.1.1 / 8.3.2.1); ipm: this MB's modes so far */
 static int pred_ipm(const jmo_dec *d, int mx, int my, int x4, int y4, const int *ipm) {
     int ma, mb;
+    /* dcPredModePredictedFlag: a neighbour not available, or inter under constrained_intra_pred */
     if (x4 > 0) ma = ipm[y4 * 4 + x4 - 1];
-    else if (avail_mb(d, mx - 1, my, mx, my)) { const mbinfo *n = &d->mi[my * d->mbw + mx - 1]; ma = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[y4 * 4 + 3] : 2; }
+    else if (iavail_mb(d, mx - 1, my, mx, my)) { const mbinfo *n = &d->mi[my * d->mbw + mx - 1]; ma = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[y4 * 4 + 3] : 2; }
     else return 2;
     if (y4 > 0) mb = ipm[(y4 - 1) * 4 + x4];
-    else if (avail_mb(d, mx, my - 1, mx, my)) { const mbinfo *n = &d->mi[(my - 1) * d->mbw + mx]; mb = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[12 + x4] : 2; }
+    else if (iavail_mb(d, mx, my - 1, mx, my)) { const mbinfo *n = &d->mi[(my - 1) * d->mbw + mx]; mb = (n->mbtype == 1 || n->mbtype == 4) ? n->ipm[12 + x4] : 2; }
     else return 2;
     return imin(ma, mb);
 }

@@ -808,12 +808,18 @@ int jmo_mb_avail(const mbs *s, int dmx, int dmy) {
            (my < s->mby || (my == s->mby && mx < s->mbx)) &&
            jmo_same_slice(s->c, s->mby * s->c->mbw + s->mbx, my * s->c->mbw + mx);
 }
+/* availability of a neighbour MB's samples for intra prediction: with UseConstrainedIntraPred
+ * (constrained_intra_pred_flag, 8.3.1.2 / 8.3.2.2 / 8.3.3 / 8.3.4) an inter-coded neighbour's
+ * samples are "not available for Intra prediction" */
+static int intra_avail(const mbs *s, int dmx, int dmy) {
+    return jmo_mb_avail(s, dmx, dmy) && (!s->c->cfg.constrained_intra_pred || s->c->mbintra[(s->mby + dmy) * s->c->mbw + s->mbx + dmx]);
+}
 /* luma sample availability at MB-relative (x,y) for intra prediction */
 static int luma_avail(const mbs *s, int x, int y) {
     if (y > 15) return 0;
-    if (x < 0) return jmo_mb_avail(s, -1, y < 0 ? -1 : 0);
-    if (x <= 15) return y < 0 ? jmo_mb_avail(s, 0, -1) : 1;
-    return y < 0 ? jmo_mb_avail(s, 1, -1) : 0;
+    if (x < 0) return intra_avail(s, -1, y < 0 ? -1 : 0);
+    if (x <= 15) return y < 0 ? intra_avail(s, 0, -1) : 1;
+    return y < 0 ? intra_avail(s, 1, -1) : 0;
 }
 
 /* intrapred_luma [J] / 8.3.1.2: the 9 Intra4x4 predictions of the 4x4 block at (bx,by)
@@ -980,7 +986,7 @@ void jmo_intra16_pred(const mbs *s, pel pred[4][256], int avail[4]) {
     const jmo_ctx *c = s->c;
     const pel *R = c->recY;
     int W = c->W, ax = s->pix_x, ay = s->pix_y;
-    int up = jmo_mb_avail(s, 0, -1), left = jmo_mb_avail(s, -1, 0), ul = jmo_mb_avail(s, -1, -1);
+    int up = intra_avail(s, 0, -1), left = intra_avail(s, -1, 0), ul = intra_avail(s, -1, -1);
     int T[16], L[16], P = ul ? R[(ay - 1) * W + ax - 1] : 0;
     for (int i = 0; i < 16; i++) {
         T[i] = up ? R[(ay - 1) * W + ax + i] : 0;
@@ -1012,7 +1018,7 @@ void jmo_intra_chroma_pred(const mbs *s, int uv, pel pred[4][64], int avail[4]) 
     const pel *R = uv ? c->recV : c->recU;
     const int dc = (c->maxv + 1) >> 1;
     int W = c->Wc, ax = s->pix_x >> 1, ay = s->pix_y >> 1;
-    int up = jmo_mb_avail(s, 0, -1), left = jmo_mb_avail(s, -1, 0), ul = jmo_mb_avail(s, -1, -1);
+    int up = intra_avail(s, 0, -1), left = intra_avail(s, -1, 0), ul = intra_avail(s, -1, -1);
     int T[8], L[8], P = ul ? R[(ay - 1) * W + ax - 1] : 0;
     for (int i = 0; i < 8; i++) {
         T[i] = up ? R[(ay - 1) * W + ax + i] : 0;
@@ -1486,7 +1492,12 @@ void jmo_encode_mb(jmo_ctx *c, int mbx, int mby) {
         c->mv[2 * a + 1] = fmv[k][1];
         c->refidx[a] = (int8_t)(is_intra ? -1 : 0);
         if (best_mode == JMH_I8MB) c->ipred[a] = res->ipred[k];
-        else if (best_mode != JMH_I4MB) { c->ipred[a] = 2; res->ipred[k] = 2; }
+        else if (best_mode != JMH_I4MB) {
+            res->ipred[k] = 2;
+            /* predIntraNxNPredMode (8.3.1.1): an inter neighbour under constrained_intra_pred sets
+             * dcPredModePredictedFlag, as an unavailable one (-1 here) */
+            c->ipred[a] = (int8_t)(!is_intra && c->cfg.constrained_intra_pred ? -1 : 2);
+        }
     }
     c->mbintra[s->mb_addr] = (int8_t)is_intra;
 }

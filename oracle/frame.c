@@ -13,7 +13,8 @@ static int cfg_ok(const jmh_config *cfg) {
         return JMH_E_INVALID_ARG;
     if (cfg->search_range < 1 || cfg->search_range > JMO_MAX_SR) return JMH_E_INVALID_ARG;
     if (cfg->search_mode != 0 && cfg->search_mode != -1 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;
-    if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred != 0) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->num_ref_frames != 1) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->constrained_intra_pred != 0 && cfg->constrained_intra_pred != 1) return JMH_E_INVALID_ARG;
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
     if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->jm_version < 0 || cfg->jm_version == 9 || cfg->jm_version > 99) return JMH_E_UNSUPPORTED_CFG;

@@ -585,7 +585,7 @@ void jmo_encode_mb_rdo(jmo_ctx *c, int mbx, int mby) {
         c->mv[2 * pa] = res->mv[q][0];
         c->mv[2 * pa + 1] = res->mv[q][1];
         c->refidx[pa] = (int8_t)(is_intra ? -1 : 0);
-        c->ipred[pa] = res->ipred[q];
+        c->ipred[pa] = (int8_t)(!is_intra && c->cfg.constrained_intra_pred ? -1 : res->ipred[q]);   /* (8.3.1.1, as encode.c) */
     }
     c->mbintra[a] = (int8_t)is_intra;
     jmo_store_rec_luma(c, s, L->rec);

@@ -105,6 +105,21 @@ HIGH10 = [
      "SearchMode=-1", "SearchRange=8", "RestrictSearchRange=0", "SymbolMode=1", "QPFirstFrame=10", "QPRemainingFrame=12"],
 ]
 
+# UseConstrainedIntraPred 1 (constrained_intra_pred_flag): intra MBs of P pictures predict only
+# from intra neighbours (inter neighbours' samples "not available for Intra prediction", 8.3), and
+# an inter neighbour sets dcPredModePredictedFlag (8.3.1.1); CAVLC / CABAC, I4 / I8 / I16, slices, RDO
+CIP = [
+    ["InputFile=synthetic:81", "FramesToBeEncoded=5", "SearchRange=2", "QPRemainingFrame=20", "UseConstrainedIntraPred=1"],
+    ["InputFile=synthetic:82", "FramesToBeEncoded=4", "UseConstrainedIntraPred=1", "SymbolMode=1", "ProfileIDC=77",
+     "QPRemainingFrame=40", "SearchRange=8"],
+    ["InputFile=synthetic:83", "FramesToBeEncoded=4", "UseConstrainedIntraPred=1", "ProfileIDC=100", "Transform8x8Mode=1",
+     "SearchMode=3", "SearchRange=4", "SliceMode=1", "SliceArgument=13", "QPRemainingFrame=24"],
+    ["InputFile=synthetic:84", "FramesToBeEncoded=3", "UseConstrainedIntraPred=1", "RDOptimization=1", "SymbolMode=1",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "SearchRange=8", "QPRemainingFrame=30"],
+    ["InputFile=synthetic:85", "FramesToBeEncoded=3", "UseConstrainedIntraPred=1", "ProfileIDC=110", "SourceBitDepthLuma=10",
+     "SourceBitDepthChroma=10", "SearchMode=3", "SearchRange=8", "RDOptimization=1", "QPRemainingFrame=44"],
+]
+
 
 def encode(d, extra):
     args = [LENCOD_CPU, "-p", f"OutputFile={d}/a.264", "-p", f"ReconFile={d}/rec.yuv"]
@@ -224,3 +239,14 @@ def test_slices_of_skipped_macroblocks(arg):
         assert r.returncode == 0, r.stderr
         assert open(f"{d}/dec.yuv", "rb").read() == open(f"{d}/rec.yuv", "rb").read()
         assert len(nal_types(open(f"{d}/a.264", "rb").read())) == 2 + 3 * -(-99 // arg)
+
+
+@pytest.mark.parametrize("extra", CIP, ids=[c[0].split(":")[1] for c in CIP])
+def test_decoder_reproduces_recon_constrained_intra(extra):
+    """UseConstrainedIntraPred 1: the decoder's constrained intra availability and mode prediction
+    reproduce the encoder's reconstruction -- and the flag changes it (intra MBs next to inter ones)."""
+    test_decoder_reproduces_recon(extra)
+    with tempfile.TemporaryDirectory() as d, tempfile.TemporaryDirectory() as d0:
+        encode(d, extra)
+        encode(d0, [e for e in extra if not e.startswith("UseConstrainedIntraPred")])
+        assert open(f"{d}/rec.yuv", "rb").read() != open(f"{d0}/rec.yuv", "rb").read()
