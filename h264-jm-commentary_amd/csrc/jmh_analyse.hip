@@ -919,7 +919,7 @@ template <class pel>
 __device__ __forceinline__ void intra_role(const DevParams &d, IntraS<pel> &s, int mbx, int mby, int tid, bool act, bool i4) {
     const int wave = tid >> 6, lane = tid & 63;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W;
-    const MbAvail mav = mb_avail(d, mbx, mby);
+    const MbAvail mav = intra_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     const bool prof = act && prof_mb_here(d, mbx, mby);
     PSTAMP(12);
@@ -967,7 +967,7 @@ __device__ __forceinline__ void intra_role(const DevParams &d, IntraS<pel> &s, i
 // k = 0..9: diagonal k of the 4x4 grid; slot 10: the totals and results.
 __device__ __forceinline__ void intra_slot(const DevParams &d, IntraS<uint8_t> &s, MbScratch *scr, int k, int w, int mbx, int mby) {
     const int lane = threadIdx.x & 63;
-    const MbAvail mav = mb_avail(d, mbx, mby);
+    const MbAvail mav = intra_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     if (k == 11) {                                       // k_mb_flow: Intra16x16 (wave 6), chroma (wave 7)
         if (d.i16c) {
@@ -1007,7 +1007,7 @@ __device__ __forceinline__ void intra_wave(const DevParams &d, IntraS<uint8_t> &
     const int lane = __lane_id();
     const bool prof = prof_mb_here(d, mbx, mby, NTS / 64);   // debug (JMH_PHASE_PROF): stamps 60..62
     PSTAMP(60);
-    const MbAvail mav = mb_avail(d, mbx, mby);
+    const MbAvail mav = intra_avail(d, mbx, mby);
     const int qpk = q_round(d.qsel, 15 + d.qp / 6);
     int tabr[2];
     i4_tabrow(lane, tabr);
@@ -1143,6 +1143,7 @@ __device__ __forceinline__ DevParams flow_params(const FlowArgs &f, const PicPar
     d.cqp_off = q.cqp_off; d.qsel = q.qsel; d.diag = q.diag; d.y_min = q.y_min;
     d.rdo = 0; d.cavlc = 0;
     d.i16c = 1;
+    d.cip = 0;                                           // (the dataflow path runs without UseConstrainedIntraPred)
     d.lf = q.lambda_motion << 16;
     d.lambda_rd = 0;
     d.rp = nullptr;

@@ -405,6 +405,7 @@ __device__ __forceinline__ void load_border(const DevParams &d, Border &b, int t
     if (av) {
         int a = (4 * mby + by4) * W4 + 4 * mbx + bx4;
         ref = d.refidx[a]; mx = d.mv[2 * a]; my = d.mv[2 * a + 1]; ipm = d.ipred[a];
+        if (d.cip && ref >= 0) ipm = -1;   // UseConstrainedIntraPred: an inter neighbour sets dcPredModePredictedFlag
     }
     b.ref[t] = (int8_t)ref; b.mv[t][0] = (int16_t)mx; b.mv[t][1] = (int16_t)my; b.ipm[t] = (int8_t)ipm;
 }

@@ -119,6 +119,7 @@ struct DevParams {
     int cavlc;                  // RDOptimization 1 with SymbolMode 0: CAVLC rates (jmh_cavlc_rate.h, item 64);
                                 //   RdoPic.range[slice] then holds the slice's mb_skip_run so far
     const RdoPic *rp;           // RDOptimization 1: the picture's RD state
+    int cip;                    // UseConstrainedIntraPred: intra prediction from intra neighbours only (intra_avail)
     int i16c;                   // k_mb_flow: the P macroblock's Intra16x16 / chroma decisions run on
                                 //   me_mb's idle waves (intra slot 11); 0: k_mb_analyse's intra roles do them
 };
@@ -134,6 +135,21 @@ __device__ __forceinline__ MbAvail mb_avail(const DevParams &d, int mbx, int mby
     v.T = mby > 0 && a - d.mbw >= first;
     v.TL = mbx > 0 && mby > 0 && a - d.mbw - 1 >= first;
     v.TR = mby > 0 && mbx + 1 < d.mbw && a - d.mbw + 1 >= first;
+    return v;
+}
+// ... for intra prediction (samples and the Intra4x4 / 8x8 mode prediction): with
+// UseConstrainedIntraPred an inter (or skipped) neighbour is "not available for Intra prediction"
+// (8.3.1.1 dcPredModePredictedFlag, 8.3.1.2, 8.3.2, 8.3.3, 8.3.4); its refidx (-1: intra) is final
+// by the time the MB's intra analysis runs
+__device__ __forceinline__ MbAvail intra_avail(const DevParams &d, int mbx, int mby) {
+    MbAvail v = mb_avail(d, mbx, mby);
+    if (d.cip && d.slice_type == JMH_P_SLICE) {
+        const int W4 = d.W >> 2, a = 4 * mby * W4 + 4 * mbx;   // the MB's top-left 4x4
+        v.L = v.L && d.refidx[a - 1] < 0;
+        v.T = v.T && d.refidx[a - W4] < 0;
+        v.TL = v.TL && d.refidx[a - W4 - 1] < 0;
+        v.TR = v.TR && d.refidx[a - W4 + 4] < 0;
+    }
     return v;
 }
 
@@ -167,6 +183,7 @@ struct TickArgs {
     int epzs_subpel, epzs_spts;          // EPZSSubPelME, EPZSSubPelThresScale
     int epzs_mints, epzs_maxts;          // EPZSMinThresScale, EPZSMaxThresScale
     int slice_mbs;                       // SliceMode 1: MBs per slice (>= 1; mbw * mbh for one slice)
+    int cip;                             // UseConstrainedIntraPred
     int bd;                              // bit depth: 8 (uint8_t samples) or 9 / 10 (uint16_t, High 10)
     int rdo;                             // RDOptimization 1: k_rdo_inter + k_rdo_intra + k_rdo_final on the stage
                                          //   (1: CABAC rates, 2: CAVLC rates, SymbolMode 0)
@@ -271,6 +288,7 @@ __device__ __forceinline__ DevParams tick_params(const TickArgs &t, int e) {
     d.rdo = t.rdo;
     d.cavlc = t.rdo == 2;
     d.i16c = 0;
+    d.cip = t.cip;
     d.lf = q.lambda_motion << 16;
     d.lambda_rd = 0;
     d.rp = nullptr;

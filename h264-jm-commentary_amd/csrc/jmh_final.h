@@ -72,7 +72,7 @@ __device__ __forceinline__ void final_core(DevParams d, FinS<pel> &s, int mbx, i
     const pel *orgY = spl<pel>(d.orgY), *orgU = spl<pel>(d.orgU), *orgV = spl<pel>(d.orgV);
     const pel *refU = spl<pel>(d.refU), *refV = spl<pel>(d.refV);
     pel *recY = spl<pel>(d.recY), *recU = spl<pel>(d.recU), *recV = spl<pel>(d.recV);
-    const MbAvail mav = mb_avail(d, mbx, mby);
+    const MbAvail mav = intra_avail(d, mbx, mby);   // (the intra prediction's neighbours)
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL;
     const bool prof = prof_mb_here(d, mbx, mby);
     PSTAMP(16);

@@ -32,7 +32,7 @@ template <class pel>
 __device__ __forceinline__ void load_intra_nb(const DevParams &d, IntraNb<pel> &nb, int t, int mbx, int mby) {
     const pel *recY = spl<pel>(d.recY), *recU = spl<pel>(d.recU), *recV = spl<pel>(d.recV);
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, Wc = d.Wc;
-    const MbAvail mav = mb_avail(d, mbx, mby);
+    const MbAvail mav = intra_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     if (t < 21) {                                  // luma row y = -1, x = -1..19
         const int x = t - 1;

@@ -22,7 +22,7 @@ __device__ __forceinline__ void intra8_mb(const TickArgs &t, I8S<pel> &s, int mi
     const DevParams d = tick_params(t, e);
     const int mby = d.y_min + (mi - t.pre[e]), mbx = d.diag - 2 * mby;
     const int pix_x = 16 * mbx, pix_y = 16 * mby, W = d.W, W4 = d.W >> 2;
-    const MbAvail mav = mb_avail(d, mbx, mby);
+    const MbAvail mav = intra_avail(d, mbx, mby);
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     const int lambda = d.lambda_mode, qp = d.qp + d.qpbd, had = d.use_hadamard;
     const pel *orgY = spl<pel>(d.orgY), *recY = spl<pel>(d.recY);

@@ -727,7 +727,7 @@ __device__ __forceinline__ void rdo_intra8(const DevParams &d, RdoIntraS<pel, tr
 template <class pel, bool T8, bool CAV>
 __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, T8> &s, RdoScr<pel> *scr, int mbx, int mby, int lane) {
     const int a = mby * d.mbw + mbx, W = d.W, pix_x = 16 * mbx, pix_y = 16 * mby, qp = d.qp + d.qpbd, maxv = d.maxv;
-    const MbAvail mav = mb_avail(d, mbx, mby);
+    const MbAvail mav0 = mb_avail(d, mbx, mby), mav = intra_avail(d, mbx, mby);   // context neighbours / intra prediction
     const bool avL = mav.L, avT = mav.T, avTL = mav.TL, avTR = mav.TR;
     const bool prof = d.prof && lane == 0 && d.prof_mb == a;   // debug (JMH_PHASE_PROF): stamps 53..56
     PSTAMP(53);
@@ -741,12 +741,12 @@ __device__ __forceinline__ void rdo_intra_mb(const DevParams &d, RdoIntraS<pel, 
     {
         const int nw = (int)sizeof(jmr_mbinfo) / 4;
         if (lane < nw) {
-            if (avL) reinterpret_cast<uint32_t *>(&s.nbA)[lane] = reinterpret_cast<const uint32_t *>(d.rp->mbi + a - 1)[lane];
-            if (avT) reinterpret_cast<uint32_t *>(&s.nbB)[lane] = reinterpret_cast<const uint32_t *>(d.rp->mbi + a - d.mbw)[lane];
+            if (mav0.L) reinterpret_cast<uint32_t *>(&s.nbA)[lane] = reinterpret_cast<const uint32_t *>(d.rp->mbi + a - 1)[lane];
+            if (mav0.T) reinterpret_cast<uint32_t *>(&s.nbB)[lane] = reinterpret_cast<const uint32_t *>(d.rp->mbi + a - d.mbw)[lane];
         }
     }
     wave_lds_sync();
-    const jmr_mbinfo *A = avL ? &s.nbA : nullptr, *B = avT ? &s.nbB : nullptr;
+    const jmr_mbinfo *A = mav0.L ? &s.nbA : nullptr, *B = mav0.T ? &s.nbB : nullptr;
     RdoLuma<pel> *L = scr->L;
     const int b4 = lane >> 4, l = lane & 15;
     // ---- Intra16x16: the find_sad_16x16 mode, dct_luma_16x16 a row of 4x4 blocks per pass (the DC
@@ -1054,7 +1054,7 @@ __global__ __launch_bounds__(NT, T8 ? JMH_RDO_FINAL_WPE : 1) void k_rdo_final(co
     const bool prof = d.prof && tid == 0 && d.prof_mb == a;   // debug (JMH_PHASE_PROF): stamps 57..60
     PSTAMP(57);
     const bool slice_p = d.slice_type == JMH_P_SLICE;
-    const MbAvail mav = mb_avail(d, mbx, mby);
+    const MbAvail mav = intra_avail(d, mbx, mby);       // (the chroma modes' availability)
     if (tid < 64) {
         const uint32_t rg = rdo_state_load(d, a, s.st0, tid, 64);
         if (tid == 0) s.rg0 = rg;

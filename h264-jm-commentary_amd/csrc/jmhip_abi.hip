@@ -396,7 +396,8 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     if (cfg->search_range < 1 || cfg->search_range > 64) return JMH_E_INVALID_ARG;
     if (cfg->search_range > SRMAX) return JMH_E_UNSUPPORTED_CFG;            // LDS-resident window
     if (cfg->search_mode != 0 && cfg->search_mode != -1 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;   // FFS / full / EPZS
-    if (cfg->num_ref_frames != 1 || cfg->constrained_intra_pred) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->num_ref_frames != 1) return JMH_E_UNSUPPORTED_CFG;
+    if (cfg->constrained_intra_pred != 0 && cfg->constrained_intra_pred != 1) return JMH_E_INVALID_ARG;
     if (cfg->restrict_search_range < 0 || cfg->restrict_search_range > 2) return JMH_E_INVALID_ARG;
     if (cfg->pipeline_depth < 0 || cfg->pipeline_depth > PMAX) return JMH_E_INVALID_ARG;
     if (cfg->transform_8x8_mode != 0 && cfg->transform_8x8_mode != 1) return JMH_E_UNSUPPORTED_CFG;
@@ -440,7 +441,8 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     // k_mb_final); JMH_FLOW=0 keeps the tick launches, as does the per-tick block profile
     {
         const char *fe = getenv("JMH_FLOW");
-        c->flow = cfg->search_mode == 0 && c->bd == 8 && !cfg->rdo && !cfg->transform_8x8_mode && !(fe && atoi(fe) == 0) &&
+        c->flow = cfg->search_mode == 0 && c->bd == 8 && !cfg->rdo && !cfg->transform_8x8_mode && !cfg->constrained_intra_pred &&
+                  !(fe && atoi(fe) == 0) &&
                   !getenv("JMH_BLOCK_PROF") && c->mbw < 4096 && c->mbh < 4096;
         const char *sg = getenv("JMH_FLOW_SEG");
         const char *sm = getenv("JMH_FLOW_SEG_MIN");
@@ -779,6 +781,7 @@ static int issue_tick(jmh_ctx *c) {
     t.epzs_subpel = c->cfg.epzs_subpel_me; t.epzs_spts = c->cfg.epzs_subpel_thres_scale;
     t.epzs_mints = c->cfg.epzs_min_thres_scale; t.epzs_maxts = c->cfg.epzs_max_thres_scale;
     t.slice_mbs = c->cfg.slice_mbs > 0 ? c->cfg.slice_mbs : c->mbw * c->mbh;
+    t.cip = c->cfg.constrained_intra_pred;
     t.bd = c->bd;
     t.ordtab = c->d_ordtab;
     t.rdo = c->cfg.rdo ? (c->cfg.symbol_mode ? 1 : 2) : 0;   // 2: CAVLC rates

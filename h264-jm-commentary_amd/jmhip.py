@@ -178,7 +178,7 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
                 restrict_search_range=2, inter_search=(1, 1, 1, 1, 1, 1, 1), slots=2, kernel_timing=False,
                 pipeline_depth=0, transform_8x8_mode=0, jm_version=8, quant_offset=(682, 342), epzs_dual_refinement=0, slice_mbs=0,
                 bit_depth=8, rdo=0, symbol_mode=None, epzs_subpel_me=0, epzs_subpel_thres_scale=0, epzs_min_thres_scale=0,
-                epzs_max_thres_scale=0):
+                epzs_max_thres_scale=0, constrained_intra_pred=0):
     """jm_version >= 10 selects the JM >= 10 quantisation rounding with the flat OffsetMatrix
     entries quant_offset = (I slices, P slices) at OffsetBits 11 (docs/JM_SEMANTICS.md item 45)."""
     cfg = JmhConfig()
@@ -187,7 +187,7 @@ def make_config(width, height, search_range=32, search_mode=0, use_hadamard=1,
     cfg.use_hadamard, cfg.restrict_search_range = use_hadamard, restrict_search_range
     for i, v in enumerate(inter_search):
         cfg.inter_search[i + 1] = v
-    cfg.num_ref_frames, cfg.constrained_intra_pred, cfg.num_frame_slots = 1, 0, slots
+    cfg.num_ref_frames, cfg.constrained_intra_pred, cfg.num_frame_slots = 1, constrained_intra_pred, slots
     cfg.flags = JMH_FLAG_KERNEL_TIMING if kernel_timing else 0
     cfg.pipeline_depth = pipeline_depth
     cfg.transform_8x8_mode = transform_8x8_mode

@@ -87,7 +87,7 @@ typedef struct jmh_config {
     int32_t restrict_search_range;  /* RestrictSearchRange 0 / 1 / 2                              */
     int32_t inter_search[8];        /* [1..7] = InterSearch16x16 .. InterSearch4x4 ([0] unused)   */
     int32_t num_ref_frames;         /* NumberReferenceFrames (this build: 1)                      */
-    int32_t constrained_intra_pred; /* UseConstrainedIntraPred (this build: 0)                    */
+    int32_t constrained_intra_pred; /* UseConstrainedIntraPred 0 / 1 (constrained_intra_pred_flag) */
     int32_t num_frame_slots;        /* device-resident input frame slots (bench / pipelining)     */
     int32_t flags;                  /* JMH_FLAG_* (0 for the defaults)                            */
     int32_t pipeline_depth;         /* pictures in flight at once (0: enough to fill the device,  */

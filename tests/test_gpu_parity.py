@@ -686,6 +686,35 @@ def test_lencod_bitstream_identical(extra):
         assert open(f"{a}/dec.yuv", "rb").read() == open(f"{a}/rec.yuv", "rb").read()
 
 
+# UseConstrainedIntraPred 1 (constrained_intra_pred_flag): the device's intra availability
+# (intra_avail: inter neighbours not available for intra prediction, their 4x4 modes not for the mode
+# prediction) == the oracle's, through the whole lencod (tick FFS path, full search, EPZS + High +
+# slices, CABAC, RDO 8 / 10 bit); each case also differs from its UseConstrainedIntraPred 0 encoding
+@pytest.mark.parametrize("extra", [
+    ["InputFile=synthetic:81", "FramesToBeEncoded=5", "SourceWidth=176", "SourceHeight=144", "SearchRange=2",
+     "QPRemainingFrame=20"],
+    ["InputFile=synthetic:82", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=8",
+     "ProfileIDC=77", "SymbolMode=1", "QPRemainingFrame=40"],
+    ["InputFile=synthetic:83", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=4",
+     "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "SliceMode=1", "SliceArgument=22", "QPRemainingFrame=24"],
+    ["InputFile=synthetic:86", "FramesToBeEncoded=4", "SourceWidth=352", "SourceHeight=288", "SearchRange=8",
+     "ProfileIDC=100", "Transform8x8Mode=1", "QPRemainingFrame=26"],
+    ["InputFile=synthetic:87", "FramesToBeEncoded=4", "SourceWidth=176", "SourceHeight=144", "SearchRange=4",
+     "SearchMode=-1", "QPRemainingFrame=30"],
+    ["InputFile=synthetic:84", "FramesToBeEncoded=3", "SourceWidth=352", "SourceHeight=288", "SearchRange=8",
+     "RDOptimization=1", "SymbolMode=1", "ProfileIDC=100", "Transform8x8Mode=1", "SearchMode=3", "QPRemainingFrame=30"],
+    ["InputFile=synthetic:85", "FramesToBeEncoded=3", "SourceWidth=352", "SourceHeight=288", "SearchRange=8",
+     "RDOptimization=1", "ProfileIDC=110", "SourceBitDepthLuma=10", "SourceBitDepthChroma=10", "SearchMode=3",
+     "QPRemainingFrame=44"],
+], ids=["ffs", "cabac", "high_epzs_slices", "high_ffs", "full", "rdo_t8", "rdo_high10"])
+def test_lencod_constrained_intra(extra):
+    test_lencod_bitstream_identical(extra + ["UseConstrainedIntraPred=1"])
+    with tempfile.TemporaryDirectory() as a, tempfile.TemporaryDirectory() as b:
+        run_lencod(LENCOD_CPU, a, extra + ["UseConstrainedIntraPred=1"])
+        run_lencod(LENCOD_CPU, b, extra)
+        assert open(f"{a}/rec.yuv", "rb").read() != open(f"{b}/rec.yuv", "rb").read()
+
+
 @pytest.mark.slow
 def test_1080p_closed_loop_gpu():
     """Full config-2 size: GPU bitstream decodes to exactly the GPU reconstruction."""
