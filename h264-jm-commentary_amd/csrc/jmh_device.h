@@ -39,6 +39,11 @@
 // may run diagonal d once picture q-1 has completed diagonal (x+5) + 2(y+5) = d + 15: a lag of
 // PIPE_LAG diagonals (tests/test_gpu_parity.py checks pipelined == sequential at the window edge).
 #define PIPE_LAG 16
+// SearchRange > 32 (EPZS only, up to 64): the same argument with the reach 16 + 2 SR + 3 pixels, i.e.
+// MB (x + R, y + R), R = (19 + 2 SR) / 16 (5 at SR 32, 9 at SR 64): a lag of 3 R + 1 diagonals (the
+// RD stage schedule's lag follows the same reach, jmhip_abi.hip rdo_schedule)
+__host__ __device__ __forceinline__ int ref_reach(int sr) { return sr <= SRMAX ? 5 : (19 + 2 * sr) / 16; }
+__host__ __device__ __forceinline__ int pipe_lag(int sr) { return sr <= SRMAX ? PIPE_LAG : 3 * ref_reach(sr) + 1; }
 
 // Per-macroblock analysis results, written by k_mb_analyse (three roles on separate
 // workgroups) and consumed by k_mb_final on the same wavefront diagonal.

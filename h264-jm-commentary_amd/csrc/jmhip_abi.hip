@@ -310,7 +310,7 @@ static void ordtab_fill(std::vector<uint32_t> &tab, int sr);
 // the latest of its left, top and top-right neighbours (prediction, deblocking) and of its
 // predecessor in the slice (the CABAC coding state): with one MB row per slice the diagonals
 // x + 2y, with one slice per picture raster order.  A picture trails its reference picture by
-// lag = 1 + max over MBs of (latest stage in the MB's reference reach [0, x + 5] x [0, y + 5] -
+// lag = 1 + max over MBs of (latest stage in the MB's reference reach [0, x + R] x [0, y + R] (R = ref_reach: 5 up to SR 32) -
 // its own stage) stages (PIPE_LAG's derivation, jmh_device.h).  Fills order (MB addresses by
 // stage, raster within a stage), off (stage offsets), c->dcount, c->nd, c->lag; non-zero when
 // the schedule's stages do not fit PicParams.diag (int16).
@@ -346,9 +346,10 @@ static int rdo_schedule(jmh_ctx *c, std::vector<int> &order, std::vector<int> &o
             pm[y * mbw + x] = v;
         }
     int lag = 1;
+    const int R = ref_reach(c->sr);
     for (int y = 0; y < mbh; y++)
         for (int x = 0; x < mbw; x++) {
-            const int X = std::min(x + 5, mbw - 1), Y = std::min(y + 5, mbh - 1);
+            const int X = std::min(x + R, mbw - 1), Y = std::min(y + R, mbh - 1);
             lag = std::max(lag, pm[Y * mbw + X] - stage[y * mbw + x] + 1);
         }
     c->lag = lag;
@@ -394,7 +395,9 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     *out = nullptr;
     if (cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 15) || (cfg->height & 15)) return JMH_E_INVALID_ARG;
     if (cfg->search_range < 1 || cfg->search_range > 64) return JMH_E_INVALID_ARG;
-    if (cfg->search_range > SRMAX) return JMH_E_UNSUPPORTED_CFG;            // LDS-resident window
+    // SearchRange > 32: EPZS only (its window falls back to the reference in global memory; the FFS
+    // and full-search windows are LDS-resident at SRMAX)
+    if (cfg->search_range > SRMAX && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->search_mode != 0 && cfg->search_mode != -1 && cfg->search_mode != 3) return JMH_E_UNSUPPORTED_CFG;   // FFS / full / EPZS
     if (cfg->num_ref_frames != 1) return JMH_E_UNSUPPORTED_CFG;
     if (cfg->constrained_intra_pred != 0 && cfg->constrained_intra_pred != 1) return JMH_E_INVALID_ARG;
@@ -430,7 +433,7 @@ int jmh_create(const jmh_config *cfg, int hip_device, jmh_ctx **out) {
     c->n4 = (size_t)c->W * c->H / 16; c->nmb = (size_t)c->mbw * c->mbh;
     c->nslots = cfg->num_frame_slots > 0 ? cfg->num_frame_slots : 1;
     c->nd = (c->mbw - 1) + 2 * (c->mbh - 1) + 1;
-    c->lag = PIPE_LAG;
+    c->lag = pipe_lag(c->sr);
     c->nslice = cfg->slice_mbs > 0 ? (int)((c->nmb + cfg->slice_mbs - 1) / cfg->slice_mbs) : 1;
     std::vector<int> rd_order, rd_off;
     if (cfg->rdo && rdo_schedule(c, rd_order, rd_off)) { delete c; return JMH_E_UNSUPPORTED_CFG; }
@@ -1379,6 +1382,7 @@ static int check_block_requests(const jmh_ctx *c, int n, const jmh_block_search 
         static const int bw4[8] = {4, 4, 4, 2, 2, 2, 1, 1}, bh4[8] = {4, 4, 2, 4, 2, 1, 2, 1};
         if (q.block_x < 0 || q.block_y < 0 || q.block_x + bw4[q.blocktype] > 4 || q.block_y + bh4[q.blocktype] > 4) return JMH_E_INVALID_ARG;
         if (q.search_range < 0 || q.search_range > c->sr) return JMH_E_INVALID_ARG;
+        if (q.search_range > SRMAX) return JMH_E_UNSUPPORTED_CFG;   // 13-bit spiral order keys: (2 SR + 1)^2 < 8192
         if (q.lambda_factor < 0 || q.lambda_factor > (1 << 24)) return JMH_E_INVALID_ARG;
         if (q.search_mode != 0 && q.search_mode != -1) return JMH_E_UNSUPPORTED_CFG;
         if (abs(q.centre[0]) > 2048 || abs(q.centre[1]) > 2048 || abs(q.pred_mv[0]) > 8192 || abs(q.pred_mv[1]) > 8192) return JMH_E_INVALID_ARG;

@@ -185,6 +185,7 @@ int jm_patch_input(jm_input *inp, char *err, int errlen) {
     if (inp->symbol_mode && inp->context_init_method) { snprintf(err, errlen, "ContextInitMethod=1 (adaptive CABAC model selection) not supported (0: FixedModelNumber)"); return -1; }
     if (inp->symbol_mode && inp->model_number) { snprintf(err, errlen, "FixedModelNumber=%d not supported (0: cabac_init_idc 0)", inp->model_number); return -1; }
     if (inp->search_mode != 0 && inp->search_mode != -1 && inp->search_mode != 3) { snprintf(err, errlen, "SearchMode=%d not supported (use -1, 0 or 3)", inp->search_mode); return -1; }
+    if (inp->search_range > 32 && inp->search_mode != 3) { snprintf(err, errlen, "SearchRange=%d > 32 needs SearchMode=3 (the FFS / full-search windows are LDS-resident at 32)", inp->search_range); return -1; }
     if (inp->num_ref_frames != 1) { snprintf(err, errlen, "NumberReferenceFrames=%d not supported (1)", inp->num_ref_frames); return -1; }
     if (inp->profile_idc != 66 && inp->profile_idc != 77 && inp->profile_idc != 100 && inp->profile_idc != 110) { snprintf(err, errlen, "ProfileIDC=%d not supported (66, 77, 100 or 110)", inp->profile_idc); return -1; }
     if (inp->bit_depth_luma > 10 || inp->bit_depth_chroma != inp->bit_depth_luma) { snprintf(err, errlen, "SourceBitDepthLuma=%d / SourceBitDepthChroma=%d not supported (equal, 8..10)", inp->bit_depth_luma, inp->bit_depth_chroma); return -1; }

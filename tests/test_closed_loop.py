@@ -52,6 +52,9 @@ CONFIGS = [
      "SearchRange=16", "ProfileIDC=100", "Transform8x8Mode=1", "SourceWidth=352", "SourceHeight=288"],
     ["InputFile=synthetic:36", "FramesToBeEncoded=3", "SliceMode=1", "SliceArgument=13", "ProfileIDC=100",
      "Transform8x8Mode=1", "SearchMode=3", "EPZSDualRefinement=1", "QPRemainingFrame=36"],
+    # SearchRange 64 (EPZS only above 32)
+    ["InputFile=synthetic:37", "FramesToBeEncoded=4", "SearchMode=3", "SearchRange=64", "SourceWidth=352",
+     "SourceHeight=288"],
 ]
 # CABAC (SymbolMode 1, row f4; Main / High profile, cabac_init_idc 0): I16 / I4 / I8, P8x8 sub-partitions,
 # the 8x8 transform, slices, QP extremes (levels beyond the UEG0 prefix, mvd beyond the UEG3 prefix)

@@ -187,6 +187,24 @@ def test_rdo_pipelined_chain_equals_sequential(slice_mbs):
             assert np.array_equal(x, y)
 
 
+def test_rdo_search_range_64():
+    """RDOptimization 1 with EPZS at SearchRange 64: GPU == oracle, and the RD stage schedule's
+    lag from the reach (9 MBs) keeps pictures in flight == one at a time."""
+    w, h = 320, 240
+    pics = moving_seq(w, h, 4, seed=64, step=(97, -83))
+    rdo_pair(w, h, pics, 30, search_range=64, search_mode=3, slice_mbs=20)
+    kw = dict(search_range=64, slice_mbs=20, **RDO)
+    a = jmhip.Encoder(w, h, **kw)
+    b = jmhip.Encoder(w, h, pipeline_depth=1, **kw)
+    assert a.depth > 1
+    ra = run_chain(a, pics, 30, (0, 0, 0), True)
+    rb = run_chain(b, pics, 30, (0, 0, 0), False)
+    for (gres, grec, gdbk), (ores, orec, odbk) in zip(ra, rb):
+        assert_same(gres, grec, ores, orec, w // 16)
+        for x, y in zip(gdbk, odbk):
+            assert np.array_equal(x, y)
+
+
 def test_rdo_slot_chain_varying_qp():
     """an encode_slot chain with RDO on, a different QP (so different lambdas) per
     picture and more pictures than the context's ring (depth + 2 entries): every picture's lambdas
