@@ -470,6 +470,77 @@ __device__ __forceinline__ unsigned ffs_table_min(const DevParams &d, const uint
     return ffs_min_m<3>(d, tab, ph, sel - 5, range, ccx, ccy, pmx, pmy, lane);
 }
 
+// the full-pel argmins of NS searches over one table phase in one pass: searches whose MVPs need no
+// other search of the group (SET 0: 16x16, 16x8 top, 8x16 left on phase 0; 8x8, 8x4 top, 4x8 left,
+// 4x4 #0 on phase 1 + b8; SET 1, once those are done: 16x8 bottom, 8x16 right; 8x4 bottom, 4x8
+// right, 4x4 #1), equal ranges (RestrictSearchRange != 0).  Search k of SET 0 sums all four halves,
+// the low dword's pair, halves 0 + 2, half 0; of SET 1 the high dword's pair, halves 1 + 3, half 1.
+// Keys as ffs_table_min (the argmin is bound by its round trips: one pass serves NS searches)
+template <int NS, int SET = 0>
+__device__ __forceinline__ void ffs_group_min(const DevParams &d, const uint8_t *tab_, int ph, int range, int ccx, int ccy, const int (&pmx)[4],
+                                              const int (&pmy)[4], int lane, unsigned (&kb)[4]) {
+    const int R = d.sr, side = 2 * R + 1, np = side * side, n = 2 * range + 1, c0 = R - range;
+    const uint2 *tab = reinterpret_cast<const uint2 *>(tab_) + (size_t)ph * np;
+    const uint32_t *spr = d.ordtab + ORDTAB_SPOS + np;
+    constexpr int RB = FFS_RB;
+    const int lc = min(lane, n - 1);
+    const unsigned lf = d.lf;
+    const bool xc = n > NTE;
+    unsigned lfx[NS], lfc[NS];
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+        kb[k] = 0xFFFFFFFFu;
+        lfx[k] = lf * (unsigned)mvbits(4 * (ccx + lc - range) - pmx[k]);
+        lfc[k] = lf * (unsigned)mvbits(4 * (ccx + NTE - range) - pmx[k]);
+    }
+    auto val = [](int k, uint2 v, unsigned t) -> unsigned {
+        if (SET == 1) {
+            if (k == 0) return __builtin_amdgcn_sad_u16(v.y, 0u, t);
+            if (k == 1) return __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(v.y, v.x, 0x07060302u), 0u, t);
+            return (v.x >> 16) + t;
+        }
+        if (k == 0) return __builtin_amdgcn_sad_u16(v.y, 0u, __builtin_amdgcn_sad_u16(v.x, 0u, t));
+        if (k == 1) return __builtin_amdgcn_sad_u16(v.x, 0u, t);
+        if (k == 2) return __builtin_amdgcn_sad_u16(__builtin_amdgcn_perm(v.y, v.x, 0x05040100u), 0u, t);
+        return (v.x & 0xFFFFu) + t;
+    };
+#pragma unroll 1
+    for (int r0 = 0; r0 < n; r0 += RB) {
+        uint2 sv[RB], xv = make_uint2(0, 0);
+        uint32_t pv[RB], xp = 0;
+        const int xr = min(r0 + lane, n - 1);
+#pragma unroll
+        for (int j = 0; j < RB; j++) {
+            const int p = (min(r0 + j, n - 1) + c0) * side + c0 + lc;
+            sv[j] = tab[p];
+            pv[j] = spr[p];
+        }
+        if (xc) {
+            const int p = (xr + c0) * side + c0 + NTE;
+            xv = tab[p];
+            xp = spr[p];
+        }
+#pragma unroll
+        for (int j = 0; j < RB; j++) {
+            const int y = ccy + min(r0 + j, n - 1) - range;
+#pragma unroll
+            for (int k = 0; k < NS; k++) {
+                const unsigned lfy = lf * (unsigned)mvbits(4 * y - pmy[k]);   // uniform
+                kb[k] = min(kb[k], (val(k, sv[j], (lfx[k] + lfy) >> 16) << 13) | pv[j]);
+            }
+        }
+        if (xc && lane < RB) {
+#pragma unroll
+            for (int k = 0; k < NS; k++) {
+                const unsigned lfr = lf * (unsigned)mvbits(4 * (ccy + xr - range) - pmy[k]);
+                kb[k] = min(kb[k], (val(k, xv, (lfc[k] + lfr) >> 16) << 13) | xp);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NS; k++) kb[k] = wave_min_u32(kb[k]);
+}
+
 typedef short e16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ e16x2 e_s2(uint32_t v) { return __builtin_bit_cast(e16x2, v); }
 __device__ __forceinline__ uint32_t e_u32(e16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -576,7 +647,7 @@ __device__ __forceinline__ int had_packed(const e16x2 (&r)[4][2]) {
 // pmvo (k_rdo_inter; null in k_mb_epzs): receives the MVP each search used (the RD rate's mvd)
 template <int BT, class pel, int FBR = 1>
 __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, const EWin<pel> &wn, int bx4, int by4, int mc, int b8, int best8x8, bool prof,
-                                           int16_t (*pmvo)[16][2] = nullptr, const uint8_t *ftab = nullptr) {
+                                           int16_t (*pmvo)[16][2] = nullptr, const uint8_t *ftab = nullptr, unsigned fkb = 0xFFFFFFFFu) {
     // debug (JMH_PHASE_PROF): steps of the MB's first 4x4 search into prof[41..46], of its 16x16
     // search into prof[47..52] (k_mb_epzs only)
     const bool sp = prof && ((BT == 7 && bx4 == 0 && by4 == 0) || BT == 1);
@@ -639,7 +710,8 @@ __device__ __forceinline__ void epzs_block(const DevParams &d, EpzS<pel> &s, con
         const int side = 2 * range + 1, npos = side * side;
         unsigned kb = 0xFFFFFFFFu;
         if (ftab && d.search_mode == 0) {               // the MB's shared SAD table (ffs_table_build)
-            kb = ffs_table_min(d, ftab, ffs_tab_index(BT, bx4, by4), range, ccx, ccy, pmx, pmy, lane);
+            // fkb: this search's key from a grouped pass (ffs_group_min), else its own argmin
+            kb = fkb != 0xFFFFFFFFu ? fkb : ffs_table_min(d, ftab, ffs_tab_index(BT, bx4, by4), range, ccx, ccy, pmx, pmy, lane);
         } else {
 #pragma unroll 1
         for (int p = lane; p < npos; p += NTE) {

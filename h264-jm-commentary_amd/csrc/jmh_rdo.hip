@@ -375,21 +375,55 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
     const jmr_mbinfo *A = hasA ? &s.nbA : nullptr, *B = hasB ? &s.nbB : nullptr;
     // SearchMode 0: the SAD tables of the 41 searches (SetupFastFullPelSearch [J]) around the FFS
     // centre, before the first
+    int fcx = 0, fcy = 0;
     if (ftab) {
         int pmx, pmy;
         MvpNb nb;
         set_mvp_nb(NbEpz<EpzS<pel>>{s.e, 1, 0, 0}, 0, 0, 16, 16, pmx, pmy, nb);
-        const int fcx = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmx / 4));
-        const int fcy = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmy / 4));
+        fcx = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmx / 4));
+        fcy = __builtin_amdgcn_readfirstlane(iclip(-d.sr, d.sr, pmy / 4));
         ffs_table_build(d, s.e, wn, ftab, fcx, fcy, lane);
         PSTAMP(20);
     }
+    // SearchMode 0 with equal ranges: the full-pel argmins of the searches whose MVPs need no other
+    // search of their group in one pass over the table phase (ffs_group_min)
+    const bool grp = ftab && d.restrict_sr != 0;
+    auto mvp = [&](int bt, int bx4, int by4, int bsx, int bsy, int b8, int b88, int &px, int &py) {
+        MvpNb nb;
+        set_mvp_nb(NbEpz<EpzS<pel>>{s.e, bt, b8, b88}, bx4, by4, bsx, bsy, px, py, nb);
+        px = __builtin_amdgcn_readfirstlane(px);
+        py = __builtin_amdgcn_readfirstlane(py);
+    };
+    unsigned gk[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (grp) {
+        int px[4] = {0, 0, 0, 0}, py[4] = {0, 0, 0, 0};
+        mvp(1, 0, 0, 16, 16, 0, 0, px[0], py[0]);
+        mvp(2, 0, 0, 16, 8, 0, 0, px[1], py[1]);
+        mvp(3, 0, 0, 8, 16, 0, 0, px[2], py[2]);
+        ffs_group_min<3>(d, ftab, 0, d.sr, fcx, fcy, px, py, lane, gk);
+    }
     // ---- motion estimation for 16x16, 16x8, 8x16 (PartitionMotionSearch [J])
-    epzs_block<1, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
-    epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
-    epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 2, 1, 0, 0, false, s.pmv, ftab);
-    epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
-    epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 2, 0, 1, 0, 0, false, s.pmv, ftab);
+    if constexpr (FFS) {
+        // the partitions' first searches, then their second ones (a full search's MVP reads only its
+        // own type's earlier results, so the order across types changes nothing)
+        epzs_block<1, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab, gk[0]);
+        epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab, gk[1]);
+        epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab, gk[2]);
+        if (grp) {
+            int px[4] = {0, 0, 0, 0}, py[4] = {0, 0, 0, 0};
+            mvp(2, 0, 2, 16, 8, 0, 0, px[0], py[0]);
+            mvp(3, 2, 0, 8, 16, 0, 0, px[1], py[1]);
+            ffs_group_min<2, 1>(d, ftab, 0, d.sr, fcx, fcy, px, py, lane, gk);
+        }
+        epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 2, 1, 0, 0, false, s.pmv, ftab, gk[0]);
+        epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 2, 0, 1, 0, 0, false, s.pmv, ftab, gk[1]);
+    } else {
+        epzs_block<1, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
+        epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
+        epzs_block<2, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 2, 1, 0, 0, false, s.pmv, ftab);
+        epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 0, 0, 0, 0, 0, false, s.pmv, ftab);
+        epzs_block<3, pel, EPZS_FB_ROWS>(d, s.e, wn, 2, 0, 1, 0, 0, false, s.pmv, ftab);
+    }
     PSTAMP(42);
     const bool p8 = inter_on(d.isr, 4) || inter_on(d.isr, 5) || inter_on(d.isr, 6) || inter_on(d.isr, 7);
     for (int i = lane; i < JMR_NCTX / 4; i += 64) reinterpret_cast<uint32_t *>(s.strun)[i] = reinterpret_cast<const uint32_t *>(s.st0)[i];
@@ -404,6 +438,33 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
 #pragma unroll 1
     for (int b8 = 0; b8 < 4 && p8; b8++) {
         const int X = 2 * (b8 & 1), Y = 2 * (b8 >> 1);
+        if constexpr (FFS) {
+        unsigned bk[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        if (grp) {                                      // 8x8, 8x4 top, 4x8 left, 4x4 #0
+            int px[4], py[4];
+            mvp(4, X, Y, 8, 8, b8, best8x8, px[0], py[0]);
+            mvp(5, X, Y, 8, 4, b8, best8x8, px[1], py[1]);
+            mvp(6, X, Y, 4, 8, b8, best8x8, px[2], py[2]);
+            mvp(7, X, Y, 4, 4, b8, best8x8, px[3], py[3]);
+            ffs_group_min<4>(d, ftab, 1 + b8, d.sr, fcx, fcy, px, py, lane, bk);
+        }
+        epzs_block<4, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab, bk[0]);
+        epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab, bk[1]);
+        epzs_block<6, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab, bk[2]);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab, bk[3]);
+        if (grp) {                                      // 8x4 bottom, 4x8 right, 4x4 #1
+            int px[4] = {0, 0, 0, 0}, py[4] = {0, 0, 0, 0};
+            mvp(5, X, Y + 1, 8, 4, b8, best8x8, px[0], py[0]);
+            mvp(6, X + 1, Y, 4, 8, b8, best8x8, px[1], py[1]);
+            mvp(7, X + 1, Y, 4, 4, b8, best8x8, px[2], py[2]);
+            ffs_group_min<3, 1>(d, ftab, 1 + b8, d.sr, fcx, fcy, px, py, lane, bk);
+        }
+        epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv, ftab, bk[0]);
+        epzs_block<6, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv, ftab, bk[1]);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv, ftab, bk[2]);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
+        epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
+        } else {
         epzs_block<4, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab);
         epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y, b8, b8, best8x8, false, s.pmv, ftab);
         epzs_block<5, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
@@ -413,6 +474,7 @@ __device__ __forceinline__ void rdo_inter_mb(const DevParams &d, RdoInterS<pel> 
         epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y, b8, b8, best8x8, false, s.pmv, ftab);
         epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
         epzs_block<7, pel, EPZS_FB_ROWS>(d, s.e, wn, X + 1, Y + 1, b8, b8, best8x8, false, s.pmv, ftab);
+        }
         PSTAMP(43 + 2 * b8);
         const int bx4 = X + (b4 & 1), by4 = Y + (b4 >> 1), k = by4 * 4 + bx4;
         const int px = 4 * bx4 + (l & 3), py = 4 * by4 + (l >> 2), q8 = (4 * (b4 >> 1) + (l >> 2)) * 8 + 4 * (b4 & 1) + (l & 3);
