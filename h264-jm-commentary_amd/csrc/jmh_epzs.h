@@ -476,13 +476,16 @@ __device__ __forceinline__ unsigned ffs_table_min(const DevParams &d, const uint
 // right, 4x4 #1), equal ranges (RestrictSearchRange != 0).  Search k of SET 0 sums all four halves,
 // the low dword's pair, halves 0 + 2, half 0; of SET 1 the high dword's pair, halves 1 + 3, half 1.
 // Keys as ffs_table_min (the argmin is bound by its round trips: one pass serves NS searches)
+#ifndef FFS_GRB
+#define FFS_GRB 13                                   // rows per round trip of a grouped pass (5 at SR 32: fewer
+#endif                                               //   live registers beat fewer trips, profiles/r11a)
 template <int NS, int SET = 0>
 __device__ __forceinline__ void ffs_group_min(const DevParams &d, const uint8_t *tab_, int ph, int range, int ccx, int ccy, const int (&pmx)[4],
                                               const int (&pmy)[4], int lane, unsigned (&kb)[4]) {
     const int R = d.sr, side = 2 * R + 1, np = side * side, n = 2 * range + 1, c0 = R - range;
     const uint2 *tab = reinterpret_cast<const uint2 *>(tab_) + (size_t)ph * np;
     const uint32_t *spr = d.ordtab + ORDTAB_SPOS + np;
-    constexpr int RB = FFS_RB;
+    constexpr int RB = FFS_GRB;
     const int lc = min(lane, n - 1);
     const unsigned lf = d.lf;
     const bool xc = n > NTE;
